@@ -1,0 +1,189 @@
+"""GAT-stack edges/sec (fwd+bwd) on the synthetic 1k-camera / 200k-point scene (BASELINE config 4).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+A step = one forward + backward of the full GraphAttnSfMNet (12 blocks, learning
+conf widths, fp32) over the whole scene, loss = a fixed linear functional of
+Ps_norm and pts3D.  Inputs (scene graph, features, weights)
+are resident in HBM before timing.  value = E * K / (max over ranks of the
+timed wall time).  With N > 1 the scene's points are sharded over the ranks
+(gasfm_amd.distributed) — strong scaling: the scene is fixed.
+
+Also reported, on the same line:
+  roofline      the fused edge-softmax + aggregation forward of the point direction
+                (attn_fwd_kernel<32,8>, the north-star kernel), timed live with HIP
+                events on its launch stream over the timed region; achieved =
+                BASELINE.md's algorithmic bytes / mean duration; peak 8.0 TB/s.
+  cpu_baseline  the oracle's torch-CPU restatement of the reference + PyG op sequence
+                (oracle.gasfm_ref with PYG_FAITHFUL) on a bounded sample scene,
+                rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def attn_fwd_bytes(E, N, H, HC, perm):
+    """BASELINE.md algorithmic bytes of one fused edge-softmax + aggregation forward."""
+    return E * 4 * HC + E * 4 * int(perm) + N * 4 * HC + N * 4 * HC + N * 8 * H + (N + 1) * 4
+
+
+def cpu_baseline(sample_scale, threads):
+    """Oracle (reference + PyG op sequence, torch CPU fp32) fwd+bwd edges/s on a sample scene."""
+    import gasfm_amd
+    from gasfm_amd import synthetic
+    from oracle import gasfm_ref, scenes
+    torch.set_num_threads(threads)
+    sc = synthetic.scaled_config4(sample_scale, seed=4)
+    g = scenes.graph_from_edges(sc.cam, sc.pt, sc.m, sc.n)
+    vals = torch.from_numpy(sc.normalized_values())
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf())
+    sd = {k: v.detach().clone().requires_grad_(True) for k, v in net.state_dict().items()}
+    gasfm_ref.PYG_FAITHFUL = True
+    times = []
+    for it in range(4):  # 1 warm-up + median of 3
+        t0 = time.perf_counter()
+        out = gasfm_ref.forward(sd, vals, g, dtype=torch.float32)
+        (out["Ps_norm"].sum() + out["pts3D"].sum()).backward()
+        times.append(time.perf_counter() - t0)
+        for v in sd.values():
+            v.grad = None
+    gasfm_ref.PYG_FAITHFUL = False
+    t = float(np.median(times[1:]))
+    return {"value": sc.num_edges / t, "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": f"scaled config 4 (m={sc.m}, n={sc.n}, E={sc.num_edges}), 12 blocks, fp32, fwd+bwd, "
+                      f"median of 3 after 1 warm-up, {t:.2f} s/step, "
+                      f"torch {torch.__version__} CPU threads={threads}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--m", type=int, default=1000)
+    ap.add_argument("--n", type=int, default=200_000)
+    ap.add_argument("--layers", type=int, default=12)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-scale", type=float, default=0.05)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        torch.distributed.init_process_group("nccl", device_id=dev)
+
+    import gasfm_amd
+    from gasfm_amd import attention, synthetic
+
+    t0 = time.time()
+    sc = synthetic.windowed_scene(args.m, args.n, seed=4)
+    E = sc.num_edges
+    conf = gasfm_amd.learning_conf(num_layers=args.layers)
+    torch.manual_seed(0)
+    net = gasfm_amd.GraphAttnSfMNet(conf)
+    if world > 1:
+        from gasfm_amd import distributed as gdist
+        data = gdist.shard_scene(sc, rank, world).to(dev)
+        model = gdist.ShardedGraphAttnSfMNet(net.to(dev))
+    else:
+        data = gasfm_amd.SceneData.from_synthetic(sc).to(dev)
+        model = net.to(dev)
+    gen = torch.Generator().manual_seed(123)
+    cP = torch.randn((sc.m, 3, 4), generator=gen).to(dev)
+    cX = torch.randn((4, sc.n), generator=gen).to(dev)
+    log(f"[rank {rank}] scene m={sc.m} n={sc.n} E={E} built+moved in {time.time() - t0:.1f}s")
+
+    def step():
+        pred = model(data)
+        ps, pts = pred["Ps_norm"], pred["pts3D"]
+        cx = cX if pts.shape[1] == sc.n else cX[:, data.point_slice]
+        loss = (ps * cP).sum() / world + (pts * cx).sum()
+        loss.backward()
+        for p in model.parameters():
+            p.grad = None
+
+    for _ in range(args.warmup):
+        step()
+    timer = attention.KernelTimer(lambda tag, HC: tag == "proj2scenepoint" and HC == 32)
+    attention.KERNEL_TIMER = timer
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    timer.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    timer.enabled = False
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    kern_ms = timer.mean_ms()
+    plan = data.graph_wrappers["proj2scenepoint"].plan
+    e_local = plan.num_edges
+    n_local = plan.num_targets
+    bytes_per_launch = attn_fwd_bytes(e_local, n_local, 4, 32, plan.perm is not None)
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9 if kern_ms else None
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            aff = len(os.sched_getaffinity(0))
+            cpu = cpu_baseline(args.cpu_sample_scale, max(1, min(aff, 16)))
+        res = {
+            "metric": "GAT-stack edges/sec (fwd+bwd) on cam/point scene graph; 1/2/4/8 MI355X",
+            "value": E * args.steps / dt,
+            "unit": "edges/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * dt / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (config 4 generator: SfM-like windowed visibility, default_rng(4)); random-init "
+                    "weights of the learning_euc GASFM architecture",
+            "config": {"workload": f"config 4: m={sc.m} cameras, n={sc.n} points, E={E} projections, "
+                                   f"{args.layers}-block GraphAttnSfMNet (learning_euc widths) fwd+bwd",
+                       "cameras": sc.m, "points": sc.n, "edges": E, "blocks": args.layers,
+                       "parallelism": f"point-sharded x{world}" if world > 1 else "single GPU"},
+            "roofline": {"kernel": "attn_fwd_kernel<32,8> point direction (proj2scenepoint), per launch",
+                         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                         "algorithmic_bytes": bytes_per_launch, "mean_us": kern_ms * 1e3 if kern_ms else None,
+                         "launches_timed": len(timer.events)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

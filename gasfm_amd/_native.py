@@ -1,0 +1,159 @@
+"""ctypes binding of the gasfm C ABI (include/gasfm.h).
+
+The HIP library is REQUIRED: if ``libgasfm.so`` is missing or fails to load,
+importing the compute entry points raises — there is no CPU or PyTorch
+fallback for the attention path.  Host-only entry points (graph
+preprocessing) work without a GPU, so DataLoader workers can use them.
+"""
+import ctypes
+import os
+
+import numpy as np
+import torch
+
+from .build import LIB
+
+GASFM_OK, GASFM_ERR_INVALID, GASFM_ERR_OOM, GASFM_ERR_HIP, GASFM_ERR_UNSUPPORTED = range(5)
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+
+# name -> (restype, argtypes); mirrors include/gasfm.h
+_SIGS = {
+    "gasfm_last_error": (ctypes.c_char_p, []),
+    "gasfm_version": (_i32, []),
+    "gasfm_build_csr": (_i32, [_vp, _i64, _i32, _vp, _vp]),
+    "gasfm_plan_work": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_gat_attn_fwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _f32, _i32,
+                                  _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_gat_attn_combine": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp,
+                                      _vp]),
+    "gasfm_gat_attn_bwd_waves": (_i32, [_i32]),
+    "gasfm_gat_attn_bwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _f32, _vp,
+                                  _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp]),
+    "gasfm_gat_attn_bwd_combine": (_i32, [_vp, _i32, _i32, _vp, _vp, _i64, _vp]),
+    "gasfm_colsum_ws_floats": (_i64, [_i64, _i32]),
+    "gasfm_colsum": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _vp]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libgasfm.so (raising loudly if absent)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise ImportError(
+                f"gasfm native library not built: {LIB} missing. Run `python -m gasfm_amd.build` "
+                "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        L = ctypes.CDLL(LIB)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def check(status, what):
+    if status == GASFM_OK:
+        return
+    msg = lib().gasfm_last_error().decode(errors="replace")
+    if status == GASFM_ERR_OOM:
+        raise torch.OutOfMemoryError(f"{what}: {msg}")
+    raise RuntimeError(f"{what} failed (status {status}): {msg}")
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+# ---------------------------------------------------------------- host graph preprocessing
+def build_csr(key, n):
+    """Stable counting sort of int32 keys in [0, n): returns (ptr[n+1], perm[E]) numpy int32."""
+    key = np.ascontiguousarray(key, dtype=np.int32)
+    E = key.shape[0]
+    ptr = np.empty(n + 1, dtype=np.int32)
+    perm = np.empty(max(E, 1), dtype=np.int32)
+    st = lib().gasfm_build_csr(key.ctypes.data_as(_vp), E, n, ptr.ctypes.data_as(_vp),
+                               perm.ctypes.data_as(_vp))
+    check(st, "gasfm_build_csr")
+    return ptr, perm[:E]
+
+
+def plan_work(seg_ptr, max_piece, all_partial=False):
+    """Split segments into work items; returns (items[n,4], combine[k,4], n_slots) numpy int32."""
+    seg_ptr = np.ascontiguousarray(seg_ptr, dtype=np.int32)
+    N = seg_ptr.shape[0] - 1
+    ni, nc, ns = _i32(0), _i32(0), _i32(0)
+    L = lib()
+    L.gasfm_plan_work(seg_ptr.ctypes.data_as(_vp), N, max_piece, int(all_partial), None,
+                      ctypes.byref(ni), None, ctypes.byref(nc), ctypes.byref(ns))
+    items = np.empty((max(ni.value, 1), 4), dtype=np.int32)
+    comb = np.empty((max(nc.value, 1), 4), dtype=np.int32)
+    ni2, nc2 = _i32(ni.value), _i32(nc.value)
+    st = L.gasfm_plan_work(seg_ptr.ctypes.data_as(_vp), N, max_piece, int(all_partial),
+                           items.ctypes.data_as(_vp), ctypes.byref(ni2), comb.ctypes.data_as(_vp),
+                           ctypes.byref(nc2), ctypes.byref(ns))
+    check(st, "gasfm_plan_work")
+    return items[:ni2.value], comb[:nc2.value], ns.value
+
+
+# ---------------------------------------------------------------- device kernels
+def attn_fwd(XL, XR, att, bias, perm, items, n_items, H, C, slope, finalize, out, seg_max, seg_sum,
+             part_acc=None, part_max=None, part_sum=None):
+    st = lib().gasfm_gat_attn_fwd(
+        _p(XL), XL.stride(0), _p(XR), XR.stride(0), _p(att), _p(bias), _p(perm), _p(items), n_items, H, C,
+        slope, int(finalize), _p(out), out.stride(0), _p(seg_max), _p(seg_sum), _p(part_acc), _p(part_max),
+        _p(part_sum), _stream(out))
+    check(st, "gasfm_gat_attn_fwd")
+
+
+def attn_combine(combine, n_combine, H, C, part_acc, part_max, part_sum, bias, finalize, out, seg_max,
+                 seg_sum):
+    st = lib().gasfm_gat_attn_combine(
+        _p(combine), n_combine, H, C, _p(part_acc), _p(part_max), _p(part_sum), _p(bias), int(finalize),
+        _p(out), out.stride(0), _p(seg_max), _p(seg_sum), _stream(out))
+    check(st, "gasfm_gat_attn_combine")
+
+
+def attn_bwd_waves(n_items):
+    return lib().gasfm_gat_attn_bwd_waves(n_items)
+
+
+def attn_bwd(XL, XR, att, bias, perm, items, n_items, H, C, slope, out, seg_max, seg_sum, gout, dXL, dXR,
+             part_dxr, datt_part):
+    st = lib().gasfm_gat_attn_bwd(
+        _p(XL), XL.stride(0), _p(XR), XR.stride(0), _p(att), _p(bias), _p(perm), _p(items), n_items, H, C,
+        slope, _p(out), out.stride(0), _p(seg_max), _p(seg_sum), _p(gout), gout.stride(0), _p(dXL),
+        dXL.stride(0), _p(dXR), dXR.stride(0), _p(part_dxr), _p(datt_part), _stream(dXL))
+    check(st, "gasfm_gat_attn_bwd")
+
+
+def attn_bwd_combine(combine, n_combine, HC, part_dxr, dXR):
+    st = lib().gasfm_gat_attn_bwd_combine(_p(combine), n_combine, HC, _p(part_dxr), _p(dXR), dXR.stride(0),
+                                          _stream(dXR))
+    check(st, "gasfm_gat_attn_bwd_combine")
+
+
+def colsum(A, out=None):
+    """Deterministic column sum of a 2-D fp32 CUDA tensor (row stride may exceed cols)."""
+    assert A.dim() == 2 and A.stride(1) == 1 and A.dtype == torch.float32
+    rows, cols = A.shape
+    if out is None:
+        out = torch.empty(cols, dtype=torch.float32, device=A.device)
+    ws = torch.empty(int(lib().gasfm_colsum_ws_floats(rows, cols)), dtype=torch.float32, device=A.device)
+    st = lib().gasfm_colsum(_p(A), rows, cols, max(A.stride(0), cols), _p(ws), _p(out), _stream(out))
+    check(st, "gasfm_colsum")
+    return out

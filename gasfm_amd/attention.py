@@ -1,0 +1,216 @@
+"""Destination-grouped attention plans and the autograd wrapper of the HIP kernels.
+
+An ``AttnPlan`` is the MI355X-side form of one of the reference's star graphs
+(``AxialAggregationGraphWrapper.edge_index``, utils/dataset_utils.py:511-537):
+instead of an edge_index over E+N concatenated nodes it stores, per
+destination segment, the range of its edges in destination order plus (for
+the unsorted point direction) the permutation into edge order, and the split
+of long segments into balanced work items.  Plans are built once per scene on
+the CPU (DataLoader-worker safe) and moved to the device with ``.to``.
+
+``gat_attention`` is the differentiable fused edge-softmax + aggregation:
+forward and backward are the HIP kernels of gasfm_amd/csrc/gat_attn.hip; no
+PyTorch or CPU fallback exists (a missing library raises).
+"""
+import copy
+
+import numpy as np
+import torch
+
+from . import _native
+
+DEFAULT_MAX_PIECE = 256
+
+# Optional live kernel timer (bench.py): callable(tag, HC) -> bool selecting which
+# attention launches to bracket with HIP events on the launch stream.
+KERNEL_TIMER = None
+
+
+class KernelTimer:
+    """Records (start, end) torch.cuda.Events around selected kernel launches."""
+
+    def __init__(self, select):
+        self.select = select
+        self.events = []
+        self.enabled = False
+
+    def __call__(self, tag, HC):
+        return self.enabled and self.select(tag, HC)
+
+    def mean_ms(self):
+        torch.cuda.synchronize()
+        if not self.events:
+            return None
+        return sum(a.elapsed_time(b) for a, b in self.events) / len(self.events)
+
+
+class AttnPlan:
+    """Edges grouped by destination segment (CSR), with balanced work items.
+
+    seg_ptr  int32 [N+1]   edge range of each destination segment
+    perm     int32 [E]     source row of the k-th edge in segment order, or None
+                           when segment order == source row order (identity)
+    items    int32 [I, 4]  (seg, begin, end, slot) work items (see gasfm.h)
+    combine  int32 [K, 4]  (seg, slot_begin, slot_count, slot_stride)
+    """
+
+    def __init__(self, seg_ptr, perm, items, combine, n_slots, num_targets, num_edges, src_rows,
+                 all_partial=False, max_piece=DEFAULT_MAX_PIECE):
+        self.seg_ptr = seg_ptr
+        self.perm = perm
+        self.items = items
+        self.combine = combine
+        self.n_slots = int(n_slots)
+        self.num_targets = int(num_targets)
+        self.num_edges = int(num_edges)
+        self.src_rows = int(src_rows)  # number of source rows the perm may reference
+        self.all_partial = bool(all_partial)
+        self.max_piece = int(max_piece)
+        self.n_items = int(items.shape[0])
+        self.n_combine = int(combine.shape[0])
+        self.bwd_waves = _native.attn_bwd_waves(self.n_items) if self.n_items else 0
+        self.tag = None  # graph name (proj2view, proj2scenepoint, ...) for timing / logs
+
+    # ------------------------------------------------------------------ construction
+    @classmethod
+    def from_targets(cls, dst, num_targets, src=None, src_rows=None, max_piece=DEFAULT_MAX_PIECE,
+                     all_partial=False):
+        """Plan for edges e -> dst[e] (source row src[e], default e).
+
+        ``dst``/``src`` are 1-D integer arrays (numpy or CPU tensors).  Sources must be
+        unique (each source row has exactly one out-edge), which holds for every GASFM
+        star graph; ``GATv2Conv.forward`` handles general graphs by gathering first.
+        """
+        dst = np.ascontiguousarray(torch.as_tensor(dst).cpu().numpy(), dtype=np.int32)
+        E = int(dst.shape[0])
+        if src is not None:
+            src = np.ascontiguousarray(torch.as_tensor(src).cpu().numpy(), dtype=np.int32)
+            assert src.shape == dst.shape
+        if src_rows is None:
+            src_rows = E if src is None else (int(src.max()) + 1 if E else 0)
+        if E and (dst.min() < 0 or dst.max() >= num_targets):
+            raise ValueError("destination index out of range")
+        if E and np.all(dst[1:] >= dst[:-1]):
+            seg_ptr = np.zeros(num_targets + 1, dtype=np.int32)
+            np.cumsum(np.bincount(dst, minlength=num_targets), out=seg_ptr[1:])
+            perm = None if src is None or np.array_equal(src, np.arange(E, dtype=np.int32)) else src.copy()
+        else:
+            seg_ptr, order = _native.build_csr(dst, num_targets)
+            perm = order if src is None else src[order]
+        items, comb, n_slots = _native.plan_work(seg_ptr, max_piece, all_partial)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a))
+        return cls(t(seg_ptr), None if perm is None else t(perm), t(items), t(comb), n_slots, num_targets, E,
+                   src_rows, all_partial, max_piece)
+
+    def to(self, device, **kwargs):
+        ret = copy.copy(self)
+        for k in ("seg_ptr", "perm", "items", "combine"):
+            v = getattr(self, k)
+            if v is not None:
+                setattr(ret, k, v.to(device, **kwargs))
+        return ret
+
+    @property
+    def device(self):
+        return self.items.device
+
+    def segment_lengths(self):
+        return (self.seg_ptr[1:] - self.seg_ptr[:-1]).cpu().numpy()
+
+
+def _check(t, name, rows=None, cols=None):
+    if not t.is_cuda or t.dtype != torch.float32:
+        raise TypeError(f"{name}: expected a float32 CUDA tensor (no CPU fallback), got {t.dtype} on {t.device}")
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"{name}: expected 2-D tensor with unit column stride")
+    if rows is not None and t.shape[0] < rows:
+        raise ValueError(f"{name}: has {t.shape[0]} rows, plan needs {rows}")
+    if cols is not None and t.shape[1] != cols:
+        raise ValueError(f"{name}: has {t.shape[1]} columns, expected {cols}")
+
+
+def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True):
+    """Launch the forward kernels; returns (out, seg_max, seg_sum) for all plan targets."""
+    HC = att.numel()
+    C = HC // heads
+    N = plan.num_targets
+    dev = XL.device
+    _check(XL, "XL", plan.src_rows, HC)
+    _check(XR, "XR", N if XR.stride(0) else 1, HC)
+    out = torch.empty((N, HC), dtype=torch.float32, device=dev)
+    smax = torch.empty((N, heads), dtype=torch.float32, device=dev)
+    ssum = torch.empty((N, heads), dtype=torch.float32, device=dev)
+    pa = pm = ps = None
+    if plan.n_slots:
+        pa = torch.empty((plan.n_slots, HC), dtype=torch.float32, device=dev)
+        pm = torch.empty((plan.n_slots, heads), dtype=torch.float32, device=dev)
+        ps = torch.empty((plan.n_slots, heads), dtype=torch.float32, device=dev)
+    attf = att.reshape(-1).contiguous()
+    timed = KERNEL_TIMER is not None and KERNEL_TIMER(plan.tag, HC)
+    if timed:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+    _native.attn_fwd(XL, XR, attf, bias, plan.perm, plan.items, plan.n_items, heads, C, slope, finalize, out,
+                     smax, ssum, pa, pm, ps)
+    if timed:
+        ev[1].record()
+        KERNEL_TIMER.events.append(ev)
+    if plan.n_combine:
+        _native.attn_combine(plan.combine, plan.n_combine, heads, C, pa, pm, ps, bias, finalize, out, smax, ssum)
+    return out, smax, ssum
+
+
+def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, gout, dXL=None):
+    """Launch the backward kernels; returns (dXL, dXR, datt[HC])."""
+    HC = att.numel()
+    C = HC // heads
+    dev = XL.device
+    gout = gout if (gout.stride(1) == 1 and gout.stride(0) >= HC) else gout.contiguous()
+    if dXL is None:
+        # every source row is written exactly once when the plan's edges cover all rows
+        full = plan.num_edges == XL.shape[0] == plan.src_rows
+        dXL = (torch.empty if full else torch.zeros)((XL.shape[0], HC), dtype=torch.float32, device=dev)
+    dXR = torch.empty((plan.num_targets, HC), dtype=torch.float32, device=dev)
+    part = torch.empty((plan.n_slots, HC), dtype=torch.float32, device=dev) if plan.n_slots else None
+    datt_part = torch.empty((max(plan.bwd_waves, 1), HC), dtype=torch.float32, device=dev)
+    attf = att.reshape(-1).contiguous()
+    if plan.n_items:
+        _native.attn_bwd(XL, XR, attf, bias, plan.perm, plan.items, plan.n_items, heads, C, slope, out, smax,
+                         ssum, gout, dXL, dXR, part, datt_part)
+        if plan.n_combine:
+            _native.attn_bwd_combine(plan.combine, plan.n_combine, HC, part, dXR)
+        datt = _native.colsum(datt_part)
+    else:
+        dXR.zero_()
+        datt = torch.zeros(HC, dtype=torch.float32, device=dev)
+    return dXL, dXR, datt
+
+
+class GatAttentionFn(torch.autograd.Function):
+    """out[i] = sum_{j->i} softmax_j(att . leaky_relu(XL[j] + XR[i])) XL[j] + bias."""
+
+    @staticmethod
+    def forward(ctx, XL, XR, att, bias, plan, heads, slope):
+        out, smax, ssum = attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True)
+        ctx.plan, ctx.heads, ctx.slope = plan, heads, slope
+        ctx.save_for_backward(XL, XR, att, bias, out, smax, ssum)
+        ctx.mark_non_differentiable(smax, ssum)
+        return out, smax, ssum
+
+    @staticmethod
+    def backward(ctx, gout, _gm, _gs):
+        XL, XR, att, bias, out, smax, ssum = ctx.saved_tensors
+        if gout is None:
+            return None, None, None, None, None, None, None
+        dXL, dXR, datt = attn_backward_raw(XL, XR, att, bias, ctx.plan, ctx.heads, ctx.slope, out, smax, ssum,
+                                           gout)
+        dbias = _native.colsum(gout if gout.stride(1) == 1 else gout.contiguous())
+        return dXL, dXR, datt.view_as(att), dbias, None, None, None
+
+
+def gat_attention(XL, XR, att, bias, plan, heads, negative_slope=0.2):
+    """Fused GATv2 attention over ``plan``; returns out [num_targets, H*C]."""
+    if plan.device != XL.device:
+        raise ValueError(f"plan on {plan.device}, features on {XL.device}: call plan.to(device) first")
+    out, _, _ = GatAttentionFn.apply(XL, XR, att, bias, plan, heads, negative_slope)
+    return out

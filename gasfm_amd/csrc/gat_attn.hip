@@ -1,0 +1,758 @@
+// Fused GATv2 edge-softmax + aggregation, forward and backward, for gfx950.
+//
+// Replaces PyG GATv2Conv's message()/utils.softmax/scatter-'add' sequence as
+// used by the reference (code/models/layers.py:329-335, 426-432, 550-556,
+// 566-572): instead of materialising [E,H,C] intermediates and running
+// scatter-max / scatter-sum / scatter-add with float atomics, one wavefront
+// streams the edges of one destination segment (or of one piece of a long
+// segment) once, computes the GATv2 logits in registers, keeps an online
+// (max, sum, acc) softmax state per head and writes the destination row.
+//
+// Wave layout (64 lanes): every edge row of HC = H*C floats is spread over
+// LPE = HC/VEC lanes holding VEC consecutive floats (16-byte loads); a wave
+// holds EPR = 64/LPE edge rows side by side and U such row-groups in flight
+// per step.  Per-head logits need a reduction over LPH = C/VEC lanes (or none
+// when a lane holds several whole heads); the EPR row states are merged with
+// xor-shuffles at the end of the item.
+//
+//   HC=32 (C=8, the 12/9 main blocks):    VEC 4, LPE 8,  EPR 8,  U 4 -> 32 edges/step
+//   HC=4  (C=1, block 0):                 VEC 4, LPE 1,  EPR 64, U 2
+//   HC=64 (C=16, scenepoint->global):     VEC 4, LPE 16, EPR 4,  U 4
+//   HC=1024 (C=256, view->global):        VEC 16, LPE 64, EPR 1, U 2
+// Other (H, C) combinations run the generic kernel at the bottom (still HIP).
+//
+// Determinism: no atomics; split segments go through ordered combine passes.
+#include <hip/hip_runtime.h>
+#include <cmath>
+
+#include "common.hpp"
+
+namespace gasfm {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ float leaky(float z, float slope) { return z > 0.f ? z : z * slope; }
+
+template <int HC_, int C_>
+struct Geom {
+  static constexpr int HC = HC_;
+  static constexpr int C = C_;
+  static constexpr int H = HC / C;
+  static constexpr int VEC = (HC / kWave > 4) ? HC / kWave : 4;
+  static constexpr int LPE = HC / VEC;
+  static constexpr int EPR = kWave / LPE;
+  static constexpr int HPL = (C >= VEC) ? 1 : VEC / C;  // heads held by one lane
+  static constexpr int LPH = (C >= VEC) ? C / VEC : 1;  // lanes sharing one head
+  static constexpr int CPH = (C >= VEC) ? VEC : C;      // lane floats per held head
+  static constexpr int U = (VEC == 4) ? ((EPR >= 64) ? 2 : 4) : (VEC == 8 ? 2 : 1);
+  static_assert(HC % VEC == 0 && kWave % LPE == 0, "bad geometry");
+  static_assert(LPE * EPR == kWave, "bad geometry");
+};
+
+template <int N>
+__device__ __forceinline__ void load_vec(float (&d)[N], const float* p) {
+#pragma unroll
+  for (int k = 0; k < N / 4; ++k) {
+    const float4 v = *reinterpret_cast<const float4*>(p + 4 * k);
+    d[4 * k + 0] = v.x;
+    d[4 * k + 1] = v.y;
+    d[4 * k + 2] = v.z;
+    d[4 * k + 3] = v.w;
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void store_vec(float* p, const float (&d)[N]) {
+#pragma unroll
+  for (int k = 0; k < N / 4; ++k)
+    *reinterpret_cast<float4*>(p + 4 * k) = make_float4(d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]);
+}
+
+// Sum over the LPH lanes that share a head (lanes are contiguous within an edge row).
+template <int LPH>
+__device__ __forceinline__ float head_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < LPH; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ float safe_scale(float m_old, float m_new) {
+  // exp(m_old - m_new) with the empty-state convention (both -inf -> 0).
+  return (m_new == -INFINITY) ? 0.f : __expf(m_old - m_new);
+}
+
+// Merge partner state (m2, s2, a2) into (m, s, a) for the HPL heads of a lane.
+template <class G>
+__device__ __forceinline__ void merge_state(float (&m)[G::HPL], float (&s)[G::HPL], float (&a)[G::VEC],
+                                            const float (&m2)[G::HPL], const float (&s2)[G::HPL],
+                                            const float (&a2)[G::VEC]) {
+#pragma unroll
+  for (int hh = 0; hh < G::HPL; ++hh) {
+    const float mn = fmaxf(m[hh], m2[hh]);
+    const float f1 = safe_scale(m[hh], mn), f2 = safe_scale(m2[hh], mn);
+    s[hh] = s[hh] * f1 + s2[hh] * f2;
+#pragma unroll
+    for (int c = 0; c < G::CPH; ++c) a[hh * G::CPH + c] = a[hh * G::CPH + c] * f1 + a2[hh * G::CPH + c] * f2;
+    m[hh] = mn;
+  }
+}
+
+// Combine the EPR row states of a wave (xor over the row bits of the lane id).
+template <class G>
+__device__ __forceinline__ void reduce_rows(float (&m)[G::HPL], float (&s)[G::HPL], float (&a)[G::VEC]) {
+#pragma unroll
+  for (int o = G::LPE; o < kWave; o <<= 1) {
+    float m2[G::HPL], s2[G::HPL], a2[G::VEC];
+#pragma unroll
+    for (int hh = 0; hh < G::HPL; ++hh) {
+      m2[hh] = __shfl_xor(m[hh], o);
+      s2[hh] = __shfl_xor(s[hh], o);
+    }
+#pragma unroll
+    for (int v = 0; v < G::VEC; ++v) a2[v] = __shfl_xor(a[v], o);
+    merge_state<G>(m, s, a, m2, s2, a2);
+  }
+}
+
+__device__ __forceinline__ int wave_id_uniform() {
+  return __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) / kWave);
+}
+
+// ------------------------------------------------------------------------------------------
+// forward
+// ------------------------------------------------------------------------------------------
+template <class G>
+__global__ __launch_bounds__(kBlock) void attn_fwd_kernel(
+    const float* __restrict__ XL, int64_t ldXL, const float* __restrict__ XR, int64_t ldXR,
+    const float* __restrict__ att, const float* __restrict__ bias, const int32_t* __restrict__ perm,
+    const gasfm_work_item* __restrict__ items, int n_items, float slope, int finalize,
+    float* __restrict__ out, int64_t ldOut, float* __restrict__ seg_max, float* __restrict__ seg_sum,
+    float* __restrict__ part_acc, float* __restrict__ part_max, float* __restrict__ part_sum) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int row = lane / G::LPE;
+  const int li = lane % G::LPE;
+  const int f0 = li * G::VEC;
+  const int nwaves = gridDim.x * (blockDim.x / kWave);
+
+  float attv[G::VEC];
+  load_vec<G::VEC>(attv, att + f0);
+
+  for (int it = wave_id_uniform(); it < n_items; it += nwaves) {
+    const gasfm_work_item w = items[it];
+    float xr[G::VEC];
+    load_vec<G::VEC>(xr, XR + int64_t(w.seg) * ldXR + f0);
+
+    float m[G::HPL], s[G::HPL], acc[G::VEC];
+#pragma unroll
+    for (int hh = 0; hh < G::HPL; ++hh) {
+      m[hh] = -INFINITY;
+      s[hh] = 0.f;
+    }
+#pragma unroll
+    for (int v = 0; v < G::VEC; ++v) acc[v] = 0.f;
+
+    for (int e0 = w.begin; e0 < w.end; e0 += G::EPR * G::U) {
+      float xl[G::U][G::VEC];
+      bool valid[G::U];
+#pragma unroll
+      for (int u = 0; u < G::U; ++u) {
+        const int e = e0 + u * G::EPR + row;
+        valid[u] = e < w.end;
+        if (valid[u]) {
+          const int64_t src = perm ? int64_t(perm[e]) : int64_t(e);
+          load_vec<G::VEC>(xl[u], XL + src * ldXL + f0);
+        } else {
+#pragma unroll
+          for (int v = 0; v < G::VEC; ++v) xl[u][v] = 0.f;
+        }
+      }
+      // logits for the U rows, per held head
+      float lg[G::U][G::HPL];
+#pragma unroll
+      for (int u = 0; u < G::U; ++u) {
+#pragma unroll
+        for (int hh = 0; hh < G::HPL; ++hh) {
+          float p = 0.f;
+#pragma unroll
+          for (int c = 0; c < G::CPH; ++c) {
+            const int v = hh * G::CPH + c;
+            p = fmaf(leaky(xl[u][v] + xr[v], slope), attv[v], p);
+          }
+          p = head_sum<G::LPH>(p);
+          lg[u][hh] = valid[u] ? p : -INFINITY;
+        }
+      }
+      // online softmax update with one rescale per step
+#pragma unroll
+      for (int hh = 0; hh < G::HPL; ++hh) {
+        float cm = lg[0][hh];
+#pragma unroll
+        for (int u = 1; u < G::U; ++u) cm = fmaxf(cm, lg[u][hh]);
+        const float mn = fmaxf(m[hh], cm);
+        const float f = safe_scale(m[hh], mn);
+        float ssum = s[hh] * f;
+        float a[G::CPH];
+#pragma unroll
+        for (int c = 0; c < G::CPH; ++c) a[c] = acc[hh * G::CPH + c] * f;
+#pragma unroll
+        for (int u = 0; u < G::U; ++u) {
+          const float p = (lg[u][hh] == -INFINITY) ? 0.f : __expf(lg[u][hh] - mn);
+          ssum += p;
+#pragma unroll
+          for (int c = 0; c < G::CPH; ++c) a[c] = fmaf(p, xl[u][hh * G::CPH + c], a[c]);
+        }
+        s[hh] = ssum;
+#pragma unroll
+        for (int c = 0; c < G::CPH; ++c) acc[hh * G::CPH + c] = a[c];
+        m[hh] = mn;
+      }
+    }
+    reduce_rows<G>(m, s, acc);
+
+    if (row == 0) {
+      const bool head_leader = (li % G::LPH) == 0;
+      const int h0 = (f0 / G::C);  // first head held by this lane
+      if (w.slot < 0) {
+        float o[G::VEC];
+#pragma unroll
+        for (int hh = 0; hh < G::HPL; ++hh) {
+          const float inv = 1.f / (s[hh] + 1e-16f);
+#pragma unroll
+          for (int c = 0; c < G::CPH; ++c) {
+            const int v = hh * G::CPH + c;
+            o[v] = finalize ? fmaf(acc[v], inv, bias[f0 + v]) : acc[v];
+          }
+        }
+        store_vec<G::VEC>(out + int64_t(w.seg) * ldOut + f0, o);
+        if (head_leader) {
+#pragma unroll
+          for (int hh = 0; hh < G::HPL; ++hh) {
+            seg_max[int64_t(w.seg) * G::H + h0 + hh] = m[hh];
+            seg_sum[int64_t(w.seg) * G::H + h0 + hh] = s[hh];
+          }
+        }
+      } else {
+        store_vec<G::VEC>(part_acc + int64_t(w.slot) * G::HC + f0, acc);
+        if (head_leader) {
+#pragma unroll
+          for (int hh = 0; hh < G::HPL; ++hh) {
+            part_max[int64_t(w.slot) * G::H + h0 + hh] = m[hh];
+            part_sum[int64_t(w.slot) * G::H + h0 + hh] = s[hh];
+          }
+        }
+      }
+    }
+  }
+}
+
+// Ordered merge of partial states.  One workgroup per combine entry; rows of
+// the workgroup take slots k = row, row + R, ... in order and the row states
+// are merged in row order (first within a wave, then across waves via LDS),
+// so the summation order is fixed for a given launch geometry.
+template <class G>
+__global__ __launch_bounds__(1024) void attn_combine_kernel(
+    const gasfm_combine_item* __restrict__ comb, const float* __restrict__ part_acc,
+    const float* __restrict__ part_max, const float* __restrict__ part_sum,
+    const float* __restrict__ bias, int finalize, float* __restrict__ out, int64_t ldOut,
+    float* __restrict__ seg_max, float* __restrict__ seg_sum) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const gasfm_combine_item ci = comb[blockIdx.x];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wv = threadIdx.x / kWave;
+  const int nw = blockDim.x / kWave;
+  const int li = lane % G::LPE;
+  const int f0 = li * G::VEC;
+  const int grow = threadIdx.x / G::LPE;  // global row id in the workgroup
+  const int R = blockDim.x / G::LPE;
+  const int h0 = f0 / G::C;
+
+  float m[G::HPL], s[G::HPL], a[G::VEC];
+#pragma unroll
+  for (int hh = 0; hh < G::HPL; ++hh) {
+    m[hh] = -INFINITY;
+    s[hh] = 0.f;
+  }
+#pragma unroll
+  for (int v = 0; v < G::VEC; ++v) a[v] = 0.f;
+
+  for (int k = grow; k < ci.slot_count; k += R) {
+    const int64_t slot = int64_t(ci.slot_begin) + int64_t(k) * ci.slot_stride;
+    float m2[G::HPL], s2[G::HPL], a2[G::VEC];
+#pragma unroll
+    for (int hh = 0; hh < G::HPL; ++hh) {
+      m2[hh] = part_max[slot * G::H + h0 + hh];
+      s2[hh] = part_sum[slot * G::H + h0 + hh];
+    }
+    load_vec<G::VEC>(a2, part_acc + slot * G::HC + f0);
+    merge_state<G>(m, s, a, m2, s2, a2);
+  }
+  reduce_rows<G>(m, s, a);
+  // cross-wave merge through LDS: wave w's row-0 lanes publish their state
+  constexpr int ST = G::VEC + 2 * G::HPL;
+  const int row_in_wave = lane / G::LPE;
+  if (row_in_wave == 0) {
+    float* p = lds + (wv * G::LPE + li) * ST;
+#pragma unroll
+    for (int v = 0; v < G::VEC; ++v) p[v] = a[v];
+#pragma unroll
+    for (int hh = 0; hh < G::HPL; ++hh) {
+      p[G::VEC + hh] = m[hh];
+      p[G::VEC + G::HPL + hh] = s[hh];
+    }
+  }
+  __syncthreads();
+  if (wv == 0 && row_in_wave == 0) {
+    for (int w2 = 1; w2 < nw; ++w2) {
+      const float* p = lds + (w2 * G::LPE + li) * ST;
+      float m2[G::HPL], s2[G::HPL], a2[G::VEC];
+#pragma unroll
+      for (int v = 0; v < G::VEC; ++v) a2[v] = p[v];
+#pragma unroll
+      for (int hh = 0; hh < G::HPL; ++hh) {
+        m2[hh] = p[G::VEC + hh];
+        s2[hh] = p[G::VEC + G::HPL + hh];
+      }
+      merge_state<G>(m, s, a, m2, s2, a2);
+    }
+    float o[G::VEC];
+#pragma unroll
+    for (int hh = 0; hh < G::HPL; ++hh) {
+      const float inv = 1.f / (s[hh] + 1e-16f);
+#pragma unroll
+      for (int c = 0; c < G::CPH; ++c) {
+        const int v = hh * G::CPH + c;
+        o[v] = finalize ? fmaf(a[v], inv, bias[f0 + v]) : a[v];
+      }
+    }
+    store_vec<G::VEC>(out + int64_t(ci.seg) * ldOut + f0, o);
+    if ((li % G::LPH) == 0) {
+#pragma unroll
+      for (int hh = 0; hh < G::HPL; ++hh) {
+        seg_max[int64_t(ci.seg) * G::H + h0 + hh] = m[hh];
+        seg_sum[int64_t(ci.seg) * G::H + h0 + hh] = s[hh];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward
+//   alpha_j = exp(e_j - M) / (S + 1e-16)          (M, S: the forward's final stats)
+//   delta   = sum_c g_c (out - bias)_c             (= sum_j alpha_j * dalpha_j)
+//   dalpha_j = sum_c g_c XL_jc ;  de_j = alpha_j (dalpha_j - delta)
+//   dz_j = de_j * att * leaky'(z_j) ;  dXL_j = alpha_j g + dz_j ;  dXR = sum_j dz_j
+//   datt += de_j * leaky(z_j)
+// ------------------------------------------------------------------------------------------
+template <class G>
+__global__ __launch_bounds__(kBlock) void attn_bwd_kernel(
+    const float* __restrict__ XL, int64_t ldXL, const float* __restrict__ XR, int64_t ldXR,
+    const float* __restrict__ att, const float* __restrict__ bias, const int32_t* __restrict__ perm,
+    const gasfm_work_item* __restrict__ items, int n_items, float slope, const float* __restrict__ out,
+    int64_t ldOut, const float* __restrict__ seg_max, const float* __restrict__ seg_sum,
+    const float* __restrict__ gout, int64_t ldG, float* __restrict__ dXL, int64_t ldDXL,
+    float* __restrict__ dXR, int64_t ldDXR, float* __restrict__ part_dxr, float* __restrict__ datt_part) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int row = lane / G::LPE;
+  const int li = lane % G::LPE;
+  const int f0 = li * G::VEC;
+  const int h0 = f0 / G::C;
+  const int wave = wave_id_uniform();
+  const int nwaves = gridDim.x * (blockDim.x / kWave);
+
+  float attv[G::VEC], bv[G::VEC], datt[G::VEC];
+  load_vec<G::VEC>(attv, att + f0);
+  load_vec<G::VEC>(bv, bias + f0);
+#pragma unroll
+  for (int v = 0; v < G::VEC; ++v) datt[v] = 0.f;
+
+  for (int it = wave; it < n_items; it += nwaves) {
+    const gasfm_work_item w = items[it];
+    const int64_t sg = w.seg;
+    float xr[G::VEC], g[G::VEC], o[G::VEC];
+    load_vec<G::VEC>(xr, XR + sg * ldXR + f0);
+    load_vec<G::VEC>(g, gout + sg * ldG + f0);
+    load_vec<G::VEC>(o, out + sg * ldOut + f0);
+    float M[G::HPL], inv[G::HPL], delta[G::HPL];
+#pragma unroll
+    for (int hh = 0; hh < G::HPL; ++hh) {
+      M[hh] = seg_max[sg * G::H + h0 + hh];
+      inv[hh] = 1.f / (seg_sum[sg * G::H + h0 + hh] + 1e-16f);
+      float d = 0.f;
+#pragma unroll
+      for (int c = 0; c < G::CPH; ++c) {
+        const int v = hh * G::CPH + c;
+        d = fmaf(g[v], o[v] - bv[v], d);
+      }
+      delta[hh] = head_sum<G::LPH>(d);
+    }
+    float dxr[G::VEC];
+#pragma unroll
+    for (int v = 0; v < G::VEC; ++v) dxr[v] = 0.f;
+
+    for (int e0 = w.begin; e0 < w.end; e0 += G::EPR * G::U) {
+      float xl[G::U][G::VEC];
+      int64_t src[G::U];
+      bool valid[G::U];
+#pragma unroll
+      for (int u = 0; u < G::U; ++u) {
+        const int e = e0 + u * G::EPR + row;
+        valid[u] = e < w.end;
+        src[u] = 0;
+        if (valid[u]) {
+          src[u] = perm ? int64_t(perm[e]) : int64_t(e);
+          load_vec<G::VEC>(xl[u], XL + src[u] * ldXL + f0);
+        } else {
+#pragma unroll
+          for (int v = 0; v < G::VEC; ++v) xl[u][v] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < G::U; ++u) {
+        float z[G::VEC];
+        float dx[G::VEC];
+#pragma unroll
+        for (int hh = 0; hh < G::HPL; ++hh) {
+          float p = 0.f, da = 0.f;
+#pragma unroll
+          for (int c = 0; c < G::CPH; ++c) {
+            const int v = hh * G::CPH + c;
+            z[v] = xl[u][v] + xr[v];
+            p = fmaf(leaky(z[v], slope), attv[v], p);
+            da = fmaf(g[v], xl[u][v], da);
+          }
+          p = head_sum<G::LPH>(p);
+          da = head_sum<G::LPH>(da);
+          const float alpha = valid[u] ? __expf(p - M[hh]) * inv[hh] : 0.f;
+          const float de = alpha * (da - delta[hh]);
+#pragma unroll
+          for (int c = 0; c < G::CPH; ++c) {
+            const int v = hh * G::CPH + c;
+            const float dz = de * attv[v] * (z[v] > 0.f ? 1.f : slope);
+            dx[v] = fmaf(alpha, g[v], dz);
+            dxr[v] += dz;
+            datt[v] = fmaf(de, leaky(z[v], slope), datt[v]);
+          }
+        }
+        if (valid[u]) store_vec<G::VEC>(dXL + src[u] * ldDXL + f0, dx);
+      }
+    }
+#pragma unroll
+    for (int o2 = G::LPE; o2 < kWave; o2 <<= 1) {
+#pragma unroll
+      for (int v = 0; v < G::VEC; ++v) dxr[v] += __shfl_xor(dxr[v], o2);
+    }
+    if (row == 0) {
+      if (w.slot < 0)
+        store_vec<G::VEC>(dXR + sg * ldDXR + f0, dxr);
+      else
+        store_vec<G::VEC>(part_dxr + int64_t(w.slot) * G::HC + f0, dxr);
+    }
+  }
+#pragma unroll
+  for (int o2 = G::LPE; o2 < kWave; o2 <<= 1) {
+#pragma unroll
+    for (int v = 0; v < G::VEC; ++v) datt[v] += __shfl_xor(datt[v], o2);
+  }
+  if (row == 0) store_vec<G::VEC>(datt_part + int64_t(wave) * G::HC + f0, datt);
+}
+
+// dXR[seg] = ordered sum of its partial slots.  One wave per entry, lanes over features.
+__global__ __launch_bounds__(kBlock) void attn_bwd_combine_kernel(const gasfm_combine_item* __restrict__ comb,
+                                                             int n_comb, int HC,
+                                                             const float* __restrict__ part,
+                                                             float* __restrict__ dXR, int64_t ld) {
+  const int wave = wave_id_uniform();
+  const int lane = threadIdx.x & (kWave - 1);
+  if (wave >= n_comb) return;
+  const gasfm_combine_item ci = comb[wave];
+  for (int f = lane; f < HC; f += kWave) {
+    float acc = 0.f;
+    for (int k = 0; k < ci.slot_count; ++k)
+      acc += part[(int64_t(ci.slot_begin) + int64_t(k) * ci.slot_stride) * HC + f];
+    dXR[int64_t(ci.seg) * ld + f] = acc;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// generic (any H, C) fallback: one wave per item, lanes over the HC features, edges serial.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void attn_fwd_generic(
+    const float* __restrict__ XL, int64_t ldXL, const float* __restrict__ XR, int64_t ldXR,
+    const float* __restrict__ att, const float* __restrict__ bias, const int32_t* __restrict__ perm,
+    const gasfm_work_item* __restrict__ items, int n_items, int H, int C, float slope, int finalize,
+    float* __restrict__ out, int64_t ldOut, float* __restrict__ seg_max, float* __restrict__ seg_sum,
+    float* __restrict__ part_acc, float* __restrict__ part_max, float* __restrict__ part_sum) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wib = threadIdx.x / kWave;
+  float* lg = lds + wib * 2 * H;  // [H] logits scratch + [H] running max
+  const int HC = H * C;
+  const int nwaves = gridDim.x * (blockDim.x / kWave);
+  for (int it = wave_id_uniform(); it < n_items; it += nwaves) {
+    const gasfm_work_item w = items[it];
+    // Two passes per item: max, then exp/sum/acc (simple and exact).
+    for (int h = lane; h < H; h += kWave) lg[H + h] = -INFINITY;
+    __builtin_amdgcn_wave_barrier();
+    for (int e = w.begin; e < w.end; ++e) {
+      const int64_t src = perm ? perm[e] : e;
+      for (int h = lane; h < H; h += kWave) {
+        float p = 0.f;
+        for (int c = 0; c < C; ++c) {
+          const int f = h * C + c;
+          p = fmaf(leaky(XL[src * ldXL + f] + XR[int64_t(w.seg) * ldXR + f], slope), att[f], p);
+        }
+        lg[H + h] = fmaxf(lg[H + h], p);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int f = lane; f < HC; f += kWave) {
+      const int h = f / C;
+      const float M = lg[H + h];
+      float s = 0.f, a = 0.f;
+      for (int e = w.begin; e < w.end; ++e) {
+        const int64_t src = perm ? perm[e] : e;
+        float p = 0.f;
+        for (int c = 0; c < C; ++c) {
+          const int ff = h * C + c;
+          p = fmaf(leaky(XL[src * ldXL + ff] + XR[int64_t(w.seg) * ldXR + ff], slope), att[ff], p);
+        }
+        const float ex = __expf(p - M);
+        s += ex;
+        a = fmaf(ex, XL[src * ldXL + f], a);
+      }
+      if (w.slot < 0) {
+        out[int64_t(w.seg) * ldOut + f] = finalize ? a / (s + 1e-16f) + bias[f] : a;
+        if (f % C == 0) {
+          seg_max[int64_t(w.seg) * H + h] = M;
+          seg_sum[int64_t(w.seg) * H + h] = s;
+        }
+      } else {
+        part_acc[int64_t(w.slot) * HC + f] = a;
+        if (f % C == 0) {
+          part_max[int64_t(w.slot) * H + h] = M;
+          part_sum[int64_t(w.slot) * H + h] = s;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void attn_combine_generic(
+    const gasfm_combine_item* __restrict__ comb, int n_comb, int H, int C, const float* __restrict__ part_acc,
+    const float* __restrict__ part_max, const float* __restrict__ part_sum, const float* __restrict__ bias,
+    int finalize, float* __restrict__ out, int64_t ldOut, float* __restrict__ seg_max,
+    float* __restrict__ seg_sum) {
+  const int wave = wave_id_uniform();
+  const int lane = threadIdx.x & (kWave - 1);
+  if (wave >= n_comb) return;
+  const gasfm_combine_item ci = comb[wave];
+  const int HC = H * C;
+  for (int f = lane; f < HC; f += kWave) {
+    const int h = f / C;
+    float m = -INFINITY, s = 0.f, a = 0.f;
+    for (int k = 0; k < ci.slot_count; ++k) {
+      const int64_t slot = int64_t(ci.slot_begin) + int64_t(k) * ci.slot_stride;
+      const float m2 = part_max[slot * H + h], s2 = part_sum[slot * H + h], a2 = part_acc[slot * HC + f];
+      const float mn = fmaxf(m, m2);
+      const float f1 = safe_scale(m, mn), f2 = safe_scale(m2, mn);
+      s = s * f1 + s2 * f2;
+      a = a * f1 + a2 * f2;
+      m = mn;
+    }
+    out[int64_t(ci.seg) * ldOut + f] = finalize ? a / (s + 1e-16f) + bias[f] : a;
+    if (f % C == 0) {
+      seg_max[int64_t(ci.seg) * H + h] = m;
+      seg_sum[int64_t(ci.seg) * H + h] = s;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void attn_bwd_generic(
+    const float* __restrict__ XL, int64_t ldXL, const float* __restrict__ XR, int64_t ldXR,
+    const float* __restrict__ att, const float* __restrict__ bias, const int32_t* __restrict__ perm,
+    const gasfm_work_item* __restrict__ items, int n_items, int H, int C, float slope,
+    const float* __restrict__ out, int64_t ldOut, const float* __restrict__ seg_max,
+    const float* __restrict__ seg_sum, const float* __restrict__ gout, int64_t ldG, float* __restrict__ dXL,
+    int64_t ldDXL, float* __restrict__ dXR, int64_t ldDXR, float* __restrict__ part_dxr,
+    float* __restrict__ datt_part) {
+  // one lane per feature f; per-head scalars recomputed per lane (serial over C) — slow but general.
+  const int wave = wave_id_uniform();
+  const int lane = threadIdx.x & (kWave - 1);
+  const int nwaves = gridDim.x * (blockDim.x / kWave);
+  const int HC = H * C;
+  for (int f = lane; f < HC; f += kWave) datt_part[int64_t(wave) * HC + f] = 0.f;
+  for (int it = wave; it < n_items; it += nwaves) {
+    const gasfm_work_item w = items[it];
+    const int64_t sg = w.seg;
+    for (int f = lane; f < HC; f += kWave) {
+      const int h = f / C;
+      const float M = seg_max[sg * H + h];
+      const float inv = 1.f / (seg_sum[sg * H + h] + 1e-16f);
+      float delta = 0.f;
+      for (int c = 0; c < C; ++c) {
+        const int ff = h * C + c;
+        delta = fmaf(gout[sg * ldG + ff], out[sg * ldOut + ff] - bias[ff], delta);
+      }
+      float dxr = 0.f, dat = 0.f;
+      for (int e = w.begin; e < w.end; ++e) {
+        const int64_t src = perm ? perm[e] : e;
+        float p = 0.f, da = 0.f;
+        for (int c = 0; c < C; ++c) {
+          const int ff = h * C + c;
+          const float x = XL[src * ldXL + ff];
+          p = fmaf(leaky(x + XR[sg * ldXR + ff], slope), att[ff], p);
+          da = fmaf(gout[sg * ldG + ff], x, da);
+        }
+        const float alpha = __expf(p - M) * inv;
+        const float de = alpha * (da - delta);
+        const float z = XL[src * ldXL + f] + XR[sg * ldXR + f];
+        const float dz = de * att[f] * (z > 0.f ? 1.f : slope);
+        dXL[src * ldDXL + f] = fmaf(alpha, gout[sg * ldG + f], dz);
+        dxr += dz;
+        dat = fmaf(de, leaky(z, slope), dat);
+      }
+      if (w.slot < 0)
+        dXR[sg * ldDXR + f] = dxr;
+      else
+        part_dxr[int64_t(w.slot) * HC + f] = dxr;
+      datt_part[int64_t(wave) * HC + f] += dat;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// dispatch
+// ------------------------------------------------------------------------------------------
+static int grid_for(int n_items) {
+  // up to 8 resident waves/SIMD * 4 SIMD * 256 CU = 8192 waves; grid-stride beyond that.
+  const int waves = n_items < 8192 ? (n_items > 0 ? n_items : 1) : 8192;
+  return (waves + (kBlock / kWave) - 1) / (kBlock / kWave);
+}
+
+template <class F>
+static bool dispatch_shape(int H, int C, F&& f) {
+  const int HC = H * C;
+  if (HC == 32 && C == 8) return f(Geom<32, 8>{}), true;
+  if (HC == 4 && C == 1) return f(Geom<4, 1>{}), true;
+  if (HC == 64 && C == 16) return f(Geom<64, 16>{}), true;
+  if (HC == 1024 && C == 256) return f(Geom<1024, 256>{}), true;
+  if (HC == 32 && C == 32) return f(Geom<32, 32>{}), true;
+  if (HC == 64 && C == 64) return f(Geom<64, 64>{}), true;
+  if (HC == 128 && C == 32) return f(Geom<128, 32>{}), true;
+  if (HC == 256 && C == 64) return f(Geom<256, 64>{}), true;
+  return false;
+}
+
+}  // namespace gasfm
+
+using namespace gasfm;
+
+extern "C" int gasfm_gat_attn_fwd(const float* XL, int64_t ldXL, const float* XR, int64_t ldXR,
+                                  const float* att, const float* bias, const int32_t* perm,
+                                  const gasfm_work_item* items, int32_t n_items, int32_t H, int32_t C,
+                                  float slope, int32_t finalize, float* out, int64_t ldOut,
+                                  float* seg_max, float* seg_sum, float* part_acc, float* part_max,
+                                  float* part_sum, void* stream) {
+  GASFM_REQUIRE(H > 0 && C > 0 && n_items >= 0, "gasfm_gat_attn_fwd: H=%d C=%d n_items=%d", H, C, n_items);
+  if (n_items == 0) return GASFM_OK;
+  GASFM_REQUIRE(XL && XR && att && bias && items && out && seg_max && seg_sum,
+                "gasfm_gat_attn_fwd: null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int grid = grid_for(n_items);
+  const bool vec_ok = (H * C) % 4 == 0 && ldXL % 4 == 0 && ldXR % 4 == 0 && ldOut % 4 == 0 &&
+                      aligned16(XL) && aligned16(XR) && aligned16(out) && aligned16(att) &&
+                      aligned16(bias) && (!part_acc || aligned16(part_acc));
+  bool done = false;
+  if (vec_ok) {
+    done = dispatch_shape(H, C, [&](auto g) {
+      using G = decltype(g);
+      hipLaunchKernelGGL((attn_fwd_kernel<G>), dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att,
+                         bias, perm, items, n_items, slope, finalize, out, ldOut, seg_max, seg_sum, part_acc,
+                         part_max, part_sum);
+    });
+  }
+  if (!done) {
+    hipLaunchKernelGGL(attn_fwd_generic, dim3(grid), dim3(kBlock), (kBlock / kWave) * 2 * H * sizeof(float), st,
+                       XL, ldXL, XR, ldXR, att, bias, perm, items, n_items, H, C, slope, finalize, out, ldOut,
+                       seg_max, seg_sum, part_acc, part_max, part_sum);
+  }
+  return launch_status("gasfm_gat_attn_fwd");
+}
+
+extern "C" int gasfm_gat_attn_combine(const gasfm_combine_item* combine, int32_t n_combine, int32_t H,
+                                      int32_t C, const float* part_acc, const float* part_max,
+                                      const float* part_sum, const float* bias, int32_t finalize, float* out,
+                                      int64_t ldOut, float* seg_max, float* seg_sum, void* stream) {
+  GASFM_REQUIRE(H > 0 && C > 0 && n_combine >= 0, "gasfm_gat_attn_combine: bad args");
+  if (n_combine == 0) return GASFM_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const bool vec_ok = (H * C) % 4 == 0 && ldOut % 4 == 0 && aligned16(out) && aligned16(part_acc) &&
+                      aligned16(bias);
+  bool done = false;
+  if (vec_ok) {
+    done = dispatch_shape(H, C, [&](auto g) {
+      using G = decltype(g);
+      const int threads = 1024;
+      const size_t lds = size_t(threads / kWave) * G::LPE * (G::VEC + 2 * G::HPL) * sizeof(float);
+      hipLaunchKernelGGL((attn_combine_kernel<G>), dim3(n_combine), dim3(threads), lds, st, combine, part_acc,
+                         part_max, part_sum, bias, finalize, out, ldOut, seg_max, seg_sum);
+    });
+  }
+  if (!done) {
+    const int grid = (n_combine + (kBlock / kWave) - 1) / (kBlock / kWave);
+    hipLaunchKernelGGL(attn_combine_generic, dim3(grid), dim3(kBlock), 0, st, combine, n_combine, H, C, part_acc,
+                       part_max, part_sum, bias, finalize, out, ldOut, seg_max, seg_sum);
+  }
+  return launch_status("gasfm_gat_attn_combine");
+}
+
+extern "C" int gasfm_gat_attn_bwd_waves(int32_t n_items) {
+  return grid_for(n_items) * (kBlock / kWave);
+}
+
+extern "C" int gasfm_gat_attn_bwd(const float* XL, int64_t ldXL, const float* XR, int64_t ldXR,
+                                  const float* att, const float* bias, const int32_t* perm,
+                                  const gasfm_work_item* items, int32_t n_items, int32_t H, int32_t C,
+                                  float slope, const float* out, int64_t ldOut, const float* seg_max,
+                                  const float* seg_sum, const float* gout, int64_t ldG, float* dXL,
+                                  int64_t ldDXL, float* dXR, int64_t ldDXR, float* part_dxr,
+                                  float* datt_part, void* stream) {
+  GASFM_REQUIRE(H > 0 && C > 0 && n_items >= 0, "gasfm_gat_attn_bwd: bad args");
+  if (n_items == 0) return GASFM_OK;
+  GASFM_REQUIRE(XL && XR && att && bias && items && out && seg_max && seg_sum && gout && dXL && dXR && datt_part,
+                "gasfm_gat_attn_bwd: null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int grid = grid_for(n_items);
+  const bool vec_ok = (H * C) % 4 == 0 && ldXL % 4 == 0 && ldXR % 4 == 0 && ldOut % 4 == 0 && ldG % 4 == 0 &&
+                      ldDXL % 4 == 0 && ldDXR % 4 == 0 && aligned16(XL) && aligned16(XR) && aligned16(out) &&
+                      aligned16(gout) && aligned16(dXL) && aligned16(dXR) && aligned16(att) &&
+                      aligned16(bias) && aligned16(datt_part) && (!part_dxr || aligned16(part_dxr));
+  bool done = false;
+  if (vec_ok) {
+    done = dispatch_shape(H, C, [&](auto g) {
+      using G = decltype(g);
+      hipLaunchKernelGGL((attn_bwd_kernel<G>), dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att, bias,
+                         perm, items, n_items, slope, out, ldOut, seg_max, seg_sum, gout, ldG, dXL, ldDXL, dXR,
+                         ldDXR, part_dxr, datt_part);
+    });
+  }
+  if (!done) {
+    hipLaunchKernelGGL(attn_bwd_generic, dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att, bias, perm,
+                       items, n_items, H, C, slope, out, ldOut, seg_max, seg_sum, gout, ldG, dXL, ldDXL, dXR,
+                       ldDXR, part_dxr, datt_part);
+  }
+  return launch_status("gasfm_gat_attn_bwd");
+}
+
+extern "C" int gasfm_gat_attn_bwd_combine(const gasfm_combine_item* combine, int32_t n_combine, int32_t HC,
+                                          const float* part_dxr, float* dXR, int64_t ldDXR, void* stream) {
+  GASFM_REQUIRE(HC > 0 && n_combine >= 0, "gasfm_gat_attn_bwd_combine: bad args");
+  if (n_combine == 0) return GASFM_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int grid = (n_combine + (kBlock / kWave) - 1) / (kBlock / kWave);
+  hipLaunchKernelGGL(attn_bwd_combine_kernel, dim3(grid), dim3(kBlock), 0, st, combine, n_combine, HC, part_dxr,
+                     dXR, ldDXR);
+  return launch_status("gasfm_gat_attn_bwd_combine");
+}

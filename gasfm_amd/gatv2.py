@@ -1,0 +1,129 @@
+"""``GATv2Conv`` for MI355X: PyG-compatible parameters, fused HIP attention.
+
+Drop-in for ``torch_geometric.nn.GATv2Conv`` as the reference constructs it
+(code/models/layers.py:304-309, 401-406, 506-511, 521-526: concat=True,
+negative_slope=0.2, dropout=0, bias=True, share_weights=False, no edge_dim,
+add_self_loops=False).  Parameter names/shapes match PyG exactly
+(``lin_l.{weight,bias}`` [H*C, F_in], ``lin_r.*``, ``att`` [1, H, C],
+``bias`` [H*C]) so reference state_dicts load unchanged.
+
+Two call forms:
+  forward(x, edge_index)   the PyG call used by the reference layer code
+                           (generic graphs; plan cached per edge_index tensor)
+  attend(x_src, x_tgt, plan)  the MI355X fast path used by gasfm_amd.model:
+                           lin_l on source rows only, lin_r on target rows only
+                           (PyG computes both on all E+N rows), then the fused
+                           edge-softmax + aggregation kernel.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .attention import AttnPlan, gat_attention
+
+
+def _glorot_(t):
+    a = math.sqrt(6.0 / (t.size(-2) + t.size(-1)))
+    with torch.no_grad():
+        t.uniform_(-a, a)
+
+
+class GATv2Conv(torch.nn.Module):
+    def __init__(self, in_channels, out_channels, heads=1, concat=True, negative_slope=0.2, dropout=0.0,
+                 add_self_loops=True, edge_dim=None, fill_value="mean", bias=True, share_weights=False,
+                 **kwargs):
+        super().__init__()
+        if add_self_loops:
+            raise NotImplementedError("GATv2Conv(add_self_loops=True): GASFM builds its star graphs without "
+                                      "self loops (layers.py:308); not supported by the MI355X kernel")
+        if not concat or dropout != 0.0 or edge_dim is not None or share_weights:
+            raise NotImplementedError("only concat=True, dropout=0, edge_dim=None, share_weights=False")
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.heads = heads
+        self.negative_slope = float(negative_slope)
+        self.lin_l = torch.nn.Linear(in_channels, heads * out_channels, bias=bias)
+        self.lin_r = torch.nn.Linear(in_channels, heads * out_channels, bias=bias)
+        self.att = torch.nn.Parameter(torch.empty(1, heads, out_channels))
+        if bias:
+            self.bias = torch.nn.Parameter(torch.empty(heads * out_channels))
+        else:
+            self.register_parameter("bias", None)
+        self._plan_cache = {}
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        # PyG: glorot weights, zero biases, glorot att, zero bias
+        _glorot_(self.lin_l.weight)
+        _glorot_(self.lin_r.weight)
+        for lin in (self.lin_l, self.lin_r):
+            if lin.bias is not None:
+                torch.nn.init.zeros_(lin.bias)
+        _glorot_(self.att)
+        if self.bias is not None:
+            torch.nn.init.zeros_(self.bias)
+
+    def __deepcopy__(self, memo):
+        # plans hold device tensors keyed by data_ptr: never carry them across copies
+        cls = self.__class__
+        new = cls.__new__(cls)
+        memo[id(self)] = new
+        import copy
+        for k, v in self.__dict__.items():
+            setattr(new, k, {} if k == "_plan_cache" else copy.deepcopy(v, memo))
+        return new
+
+    def _bias(self, ref):
+        if self.bias is not None:
+            return self.bias
+        return torch.zeros(self.heads * self.out_channels, dtype=ref.dtype, device=ref.device)
+
+    # ------------------------------------------------------------------ fast path
+    def attend(self, x_src, x_tgt, plan):
+        """Attention of plan's destinations over source rows.
+
+        x_src [S, F_in]: source node features (rows addressed by plan.perm or edge order)
+        x_tgt [N, F_in] target node features, or None for the reference's zero target
+              features (dataset_utils.py:569-571), where lin_r(0) == lin_r.bias.
+        """
+        XL = self.lin_l(x_src)
+        if x_tgt is None:
+            # one zero row through lin_r (== its bias) broadcast over the targets: lin_r.weight
+            # still receives its (zero) gradient, as in the reference, so train.py:137's
+            # torch.cat over every p.grad keeps working.
+            zero = torch.zeros((1, self.in_channels), dtype=x_src.dtype, device=x_src.device)
+            XR = self.lin_r(zero).expand(plan.num_targets, -1)
+        else:
+            XR = self.lin_r(x_tgt)
+        return gat_attention(XL, XR, self.att, self._bias(XL), plan, self.heads, self.negative_slope)
+
+    # ------------------------------------------------------------------ PyG call form
+    def _plan_for(self, edge_index, num_nodes):
+        key = (edge_index.data_ptr(), edge_index.shape[1], edge_index._version, num_nodes, str(edge_index.device))
+        plan = self._plan_cache.get(key)
+        if plan is None:
+            src, dst = edge_index[0].cpu(), edge_index[1].cpu()
+            unique_src = src.numel() == 0 or int(torch.bincount(src).max()) <= 1
+            if unique_src:
+                plan = AttnPlan.from_targets(dst, num_nodes, src=src, src_rows=num_nodes)
+            else:
+                # repeated sources: gather per-edge source rows first (edge order == plan order)
+                plan = AttnPlan.from_targets(dst, num_nodes)
+                plan.gather_src = src.to(edge_index.device)
+            plan = plan.to(edge_index.device)
+            if not unique_src:
+                plan.gather_src = src.to(edge_index.device)
+            self._plan_cache.clear()
+            self._plan_cache[key] = plan
+        return plan
+
+    def forward(self, x, edge_index):
+        N = x.shape[0]
+        plan = self._plan_for(edge_index, N)
+        XL = self.lin_l(x)
+        XR = self.lin_r(x)
+        gs = getattr(plan, "gather_src", None)
+        if gs is not None:
+            XL = XL.index_select(0, gs)
+        return gat_attention(XL, XR, self.att, self._bias(XL), plan, self.heads, self.negative_slope)

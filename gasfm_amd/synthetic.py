@@ -1,0 +1,122 @@
+"""Synthetic camera/point scenes for the BASELINE configs (no datasets ship offline).
+
+config 1 (BASELINE.json configs[0]): m=10, n=200, every point in
+    3 distinct random cameras, numpy default_rng(0), pixels U(1,1000),
+    K = [[800,0,500],[0,800,500],[0,0,1]], Ps_gt = [I|0].
+config 4 (configs[3]): m=1000, n=200,000, point j visible in
+    k_j = clip(2 + Poisson(18), 2, m) distinct cameras drawn from a contiguous
+    window of 2*k_j cameras around a random centre (SfM-like locality),
+    default_rng(4); every camera keeps >= 8 points (constants.py:6).  E ~ 4.0M.
+
+A scene is returned in sparse form (cam, pt, pixel xy) so that config 4 never
+materialises the dense 2m x n measurement matrix; ``dense_M`` builds it for
+small scenes (the reference's SceneData input, Euclidean.py:22-39).
+"""
+from dataclasses import dataclass
+
+import numpy as np
+
+K_DEFAULT = np.array([[800.0, 0.0, 500.0], [0.0, 800.0, 500.0], [0.0, 0.0, 1.0]])
+
+
+@dataclass
+class SyntheticScene:
+    m: int
+    n: int
+    cam: np.ndarray   # [E] int64, cam-major sorted (then point)
+    pt: np.ndarray    # [E] int64
+    xy: np.ndarray    # [E, 2] float32 pixel coordinates
+    K: np.ndarray     # [3, 3]
+
+    @property
+    def num_edges(self):
+        return int(self.cam.shape[0])
+
+    def normalized_values(self):
+        """(N @ [x, y, 1])[:2] with N = K^-1 (Euclidean.py:30-32, geo_utils.normalize_M)."""
+        N = np.linalg.inv(self.K)
+        h = np.concatenate([self.xy.astype(np.float64), np.ones((self.num_edges, 1))], axis=1)
+        v = h @ N.T
+        return v[:, :2].astype(np.float32)
+
+    def dense_M(self):
+        M = np.zeros((2 * self.m, self.n), dtype=np.float32)
+        M[2 * self.cam, self.pt] = self.xy[:, 0]
+        M[2 * self.cam + 1, self.pt] = self.xy[:, 1]
+        return M
+
+    def Ns(self):
+        return np.repeat(np.linalg.inv(self.K)[None].astype(np.float32), self.m, axis=0)
+
+    def Ps_gt(self):
+        P = np.zeros((self.m, 3, 4), dtype=np.float32)
+        P[:, :3, :3] = np.eye(3, dtype=np.float32)
+        return P
+
+
+def _sorted(m, n, cam, pt, rng):
+    order = np.lexsort((pt, cam))
+    cam, pt = cam[order].astype(np.int64), pt[order].astype(np.int64)
+    xy = rng.uniform(1.0, 1000.0, size=(cam.shape[0], 2)).astype(np.float32)
+    return SyntheticScene(m, n, cam, pt, xy, K_DEFAULT.copy())
+
+
+def random_scene(m, n, views_per_point, seed, window=None):
+    """Each point in `views_per_point` distinct cameras (uniform, or inside a window)."""
+    rng = np.random.default_rng(seed)
+    cams = np.empty((n, views_per_point), dtype=np.int64)
+    for j in range(n):
+        cams[j] = rng.choice(m, size=views_per_point, replace=False)
+    pt = np.repeat(np.arange(n, dtype=np.int64), views_per_point)
+    return _sorted(m, n, cams.reshape(-1), pt, rng)
+
+
+def config1():
+    return random_scene(10, 200, 3, seed=0)
+
+
+def windowed_scene(m, n, mean_extra=18, seed=4, min_pts_per_cam=8):
+    """config-4 generator (vectorised over points grouped by their view count)."""
+    rng = np.random.default_rng(seed)
+    k = np.clip(2 + rng.poisson(mean_extra, size=n), 2, m).astype(np.int64)
+    centre = rng.integers(0, m, size=n)
+    cam_parts, pt_parts = [], []
+    for kv in np.unique(k):
+        idx = np.nonzero(k == kv)[0]
+        w = min(2 * int(kv), m)
+        # kv distinct offsets out of a window of w cameras: argsort of random keys
+        keys = rng.random((idx.shape[0], w))
+        offs = np.argsort(keys, axis=1)[:, :kv] - w // 2
+        cams = (centre[idx, None] + offs) % m
+        cam_parts.append(cams.reshape(-1))
+        pt_parts.append(np.repeat(idx, kv))
+    cam = np.concatenate(cam_parts)
+    pt = np.concatenate(pt_parts)
+    counts = np.bincount(cam, minlength=m)
+    if counts.min() < min_pts_per_cam:
+        # top up starving cameras with extra observations of random points not yet seen
+        extra_c, extra_p = [], []
+        seen = set(zip(cam.tolist(), pt.tolist())) if cam.shape[0] < 5_000_000 else None
+        for c in np.nonzero(counts < min_pts_per_cam)[0]:
+            need = min_pts_per_cam - counts[c]
+            while need > 0:
+                p = int(rng.integers(0, n))
+                if seen is not None and (int(c), p) in seen:
+                    continue
+                extra_c.append(c)
+                extra_p.append(p)
+                if seen is not None:
+                    seen.add((int(c), p))
+                need -= 1
+        cam = np.concatenate([cam, np.asarray(extra_c, dtype=np.int64)])
+        pt = np.concatenate([pt, np.asarray(extra_p, dtype=np.int64)])
+    return _sorted(m, n, cam, pt, rng)
+
+
+def config4(m=1000, n=200_000, seed=4):
+    return windowed_scene(m, n, seed=seed)
+
+
+def scaled_config4(scale, seed=4):
+    """config 4 with m and n scaled by `scale` (parity tests at oracle-friendly sizes)."""
+    return windowed_scene(max(16, int(1000 * scale)), max(64, int(200_000 * scale)), seed=seed)

@@ -1,0 +1,151 @@
+/*
+ * gasfm.h — C ABI of the MI355X (gfx950) GASFM graph-attention hot path.
+ *
+ * The reference has no native boundary for this path: the arithmetic sits in
+ * PyG's GATv2Conv (third party, called at code/models/layers.py:329-335,
+ * 426-432, 550-556, 566-572) and in aten ops inside
+ * GraphAttnSfMLayer / GraphAttnSfMProjectionFeatureUpdate
+ * (layers.py:222-263, 911-956).  Each entry point below names the reference
+ * computation it replaces.  The Python host side (gasfm_amd/) binds these
+ * through ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Plain pointers and sizes; no torch types.  All device buffers are
+ *    caller-allocated (the library never allocates device memory), fp32
+ *    features, int32 indices, row-major with explicit leading dimensions
+ *    (in elements; feature row starts must be 16-byte aligned).
+ *  - `stream` is a hipStream_t passed as void* (the caller's current stream).
+ *  - Every function returns a status code (GASFM_OK == 0) and never aborts;
+ *    gasfm_last_error() returns a thread-local message for the last failure.
+ *    GASFM_ERR_OOM corresponds to hipErrorOutOfMemory (host maps it to
+ *    torch.OutOfMemoryError, which train.py:225-241 catches).
+ *  - Reductions are deterministic: no float atomics anywhere; segment sums
+ *    are done by one wave per segment piece plus ordered combine passes.
+ */
+#ifndef GASFM_H
+#define GASFM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  GASFM_OK = 0,
+  GASFM_ERR_INVALID = 1,     /* bad argument / shape / alignment */
+  GASFM_ERR_OOM = 2,         /* hipErrorOutOfMemory */
+  GASFM_ERR_HIP = 3,         /* any other HIP runtime error */
+  GASFM_ERR_UNSUPPORTED = 4  /* (H, C) combination without a kernel */
+};
+
+/* One unit of attention work: edges [begin, end) (positions in the segment's
+ * edge order, i.e. indices into `perm` when perm != NULL) of segment `seg`.
+ * slot < 0: the item covers the whole segment and writes the segment's
+ * result directly; slot >= 0: it writes an un-normalised partial
+ * (max, sum, acc) into partial slot `slot`. */
+typedef struct gasfm_work_item {
+  int32_t seg, begin, end, slot;
+} gasfm_work_item;
+
+/* Ordered combine of partial slots: slots slot_begin + k*slot_stride,
+ * k = 0..slot_count-1, are merged (in k order) into segment `seg`. */
+typedef struct gasfm_combine_item {
+  int32_t seg, slot_begin, slot_count, slot_stride;
+} gasfm_combine_item;
+
+const char* gasfm_last_error(void);
+int gasfm_version(void);
+
+/* ---- graph preprocessing (host, CPU; usable in DataLoader workers) ------ */
+
+/* Counting-sort CSR build: ptr[n+1] = segment offsets of `key` (values in
+ * [0, n)), perm[E] = edge ids grouped by key, stable (ascending edge id inside
+ * a segment).  Replaces the implicit grouping PyG's scatter does over
+ * edge_index[1] (dataset_utils.py:531-535) for the unsorted point direction.
+ * Reference-side caller: SceneData.create_axial_aggregation_graphs
+ * (SceneData.py:153-239). */
+int gasfm_build_csr(const int32_t* key, int64_t E, int32_t n,
+                    int32_t* ptr, int32_t* perm);
+
+/* Split segments longer than max_piece edges into pieces.  Writes at most
+ * *n_items items (capacity in, count out) and *n_combine combine entries;
+ * returns GASFM_ERR_INVALID if a capacity is too small (counts then hold the
+ * required sizes).  all_partial != 0 makes every segment write a partial
+ * (multi-GPU camera direction), with slot == seg for unsplit segments. */
+int gasfm_plan_work(const int32_t* seg_ptr, int32_t N, int32_t max_piece,
+                    int32_t all_partial,
+                    gasfm_work_item* items, int32_t* n_items,
+                    gasfm_combine_item* combine, int32_t* n_combine,
+                    int32_t* n_slots);
+
+/* ---- fused GATv2 edge-softmax + aggregation (device) ------------------- */
+
+/* Forward of PyG GATv2Conv's message/softmax/aggregate on pre-projected
+ * rows (replaces gatv2_conv.py message() + utils.softmax + scatter 'add',
+ * called at layers.py:329-335 etc.):
+ *   e_j[h]   = sum_c att[h,c] * leaky_relu(XL[src_j,h,c] + XR[seg,h,c], slope)
+ *   out[seg] = sum_j softmax_j(e)[h] * XL[src_j,h,:] + bias      (finalize)
+ * src_j = perm[j] if perm != NULL else j.  Complete items write
+ * out[seg] (finalized if finalize != 0, otherwise the raw acc) plus
+ * seg_max[seg,h], seg_sum[seg,h] (sum of exp(e - max), no epsilon).  Split
+ * items write raw partials to part_{acc,max,sum}[slot].  Segments with no
+ * edges give out = bias, max = -inf, sum = 0. */
+int gasfm_gat_attn_fwd(const float* XL, int64_t ldXL,
+                       const float* XR, int64_t ldXR,
+                       const float* att, const float* bias,
+                       const int32_t* perm,
+                       const gasfm_work_item* items, int32_t n_items,
+                       int32_t H, int32_t C, float negative_slope,
+                       int32_t finalize,
+                       float* out, int64_t ldOut, float* seg_max, float* seg_sum,
+                       float* part_acc, float* part_max, float* part_sum,
+                       void* stream);
+
+/* Ordered merge of partials (split pieces, or one partial per rank after an
+ * all-gather).  Writes out/seg_max/seg_sum at index seg (finalized with bias
+ * when finalize != 0, else raw partial form). */
+int gasfm_gat_attn_combine(const gasfm_combine_item* combine, int32_t n_combine,
+                           int32_t H, int32_t C,
+                           const float* part_acc, const float* part_max,
+                           const float* part_sum,
+                           const float* bias, int32_t finalize,
+                           float* out, int64_t ldOut, float* seg_max, float* seg_sum,
+                           void* stream);
+
+/* Backward of the above given dOut (gout), the forward's finalized out and
+ * per-segment stats.  Writes dXL[src_j] for every edge (each row exactly
+ * once), dXR[seg] for complete items (partials to part_dxr[slot] for split
+ * items; merge with gasfm_gat_attn_bwd_combine) and one datt partial row per
+ * wave into datt_part[n_waves, H*C] (n_waves from
+ * gasfm_gat_attn_bwd_waves(); reduce with gasfm_colsum). */
+int gasfm_gat_attn_bwd_waves(int32_t n_items);
+int gasfm_gat_attn_bwd(const float* XL, int64_t ldXL,
+                       const float* XR, int64_t ldXR,
+                       const float* att, const float* bias,
+                       const int32_t* perm,
+                       const gasfm_work_item* items, int32_t n_items,
+                       int32_t H, int32_t C, float negative_slope,
+                       const float* out, int64_t ldOut,
+                       const float* seg_max, const float* seg_sum,
+                       const float* gout, int64_t ldG,
+                       float* dXL, int64_t ldDXL,
+                       float* dXR, int64_t ldDXR,
+                       float* part_dxr, float* datt_part,
+                       void* stream);
+
+/* dXR[seg] = sum_k part_dxr[slot_begin + k*slot_stride]  (ordered). */
+int gasfm_gat_attn_bwd_combine(const gasfm_combine_item* combine, int32_t n_combine,
+                               int32_t HC, const float* part_dxr,
+                               float* dXR, int64_t ldDXR, void* stream);
+
+/* out[c] = sum_r A[r*ld + c] for c < cols (two-pass, deterministic).
+ * ws must hold gasfm_colsum_ws_floats(rows, cols) floats. */
+int64_t gasfm_colsum_ws_floats(int64_t rows, int32_t cols);
+int gasfm_colsum(const float* A, int64_t rows, int32_t cols, int64_t ld,
+                 float* ws, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GASFM_H */

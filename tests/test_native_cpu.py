@@ -1,0 +1,122 @@
+"""C-ABI library checks that need no GPU: load, exported symbols, host graph preprocessing."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import gasfm_amd
+from conftest import REPO, golden
+from gasfm_amd import _native
+
+
+def header_functions():
+    text = open(os.path.join(REPO, "include", "gasfm.h")).read()
+    return sorted(set(re.findall(r"\b(gasfm_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _native.lib()
+    declared = header_functions()
+    assert len(declared) >= 10
+    for name in declared:
+        assert hasattr(lib, name), f"{name} declared in include/gasfm.h but not exported"
+    assert set(declared) == set(_native.exported_symbols())
+    assert lib.gasfm_version() >= 1
+
+
+def test_build_csr_matches_numpy_stable_sort():
+    rng = np.random.default_rng(0)
+    for n, E in ((1, 0), (1, 5), (50, 1000), (7, 3)):
+        key = rng.integers(0, n, size=E).astype(np.int32)
+        ptr, perm = _native.build_csr(key, n)
+        ref_perm = np.argsort(key, kind="stable")
+        np.testing.assert_array_equal(perm, ref_perm)
+        np.testing.assert_array_equal(ptr, np.concatenate([[0], np.cumsum(np.bincount(key, minlength=n))]))
+
+
+def test_build_csr_rejects_bad_keys():
+    with pytest.raises(RuntimeError, match="outside"):
+        _native.build_csr(np.array([0, 3], dtype=np.int32), 3)
+
+
+def test_plan_work_splits_and_covers():
+    rng = np.random.default_rng(1)
+    lens = rng.integers(0, 40, size=100)
+    lens[[3, 50]] = [1000, 257]
+    ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    items, comb, n_slots = _native.plan_work(ptr, 32)
+    covered = np.zeros(ptr[-1], dtype=np.int32)
+    for s, b, e, slot in items:
+        assert ptr[s] <= b <= e <= ptr[s + 1]
+        assert e - b <= 32
+        covered[b:e] += 1
+        assert (slot >= 0) == (lens[s] > 32)
+    assert (covered == 1).all()
+    assert len(items) >= 100 and set(comb[:, 0]) == {i for i in range(100) if lens[i] > 32}
+    assert comb[:, 2].sum() == n_slots
+    # every segment, empty ones included, has exactly one item or one combine entry
+    whole = {int(s) for s, b, e, slot in items if slot < 0}
+    assert whole | set(comb[:, 0].tolist()) == set(range(100))
+
+
+def test_plan_work_all_partial_slots():
+    ptr = np.array([0, 3, 3, 10], dtype=np.int32)
+    items, comb, n_slots = _native.plan_work(ptr, 4, all_partial=True)
+    assert n_slots == 3 + 2  # one slot per segment + pieces of the split segment
+    assert {int(i[3]) for i in items if i[0] != 2} == {0, 1}
+    assert comb.tolist() == [[2, 3, 2, 1]]
+
+
+def test_attn_plan_point_direction():
+    s = golden("scene_config1.npz")
+    idx = s["indices"]
+    plan = gasfm_amd.AttnPlan.from_targets(idx[1], 200)
+    assert plan.perm is not None
+    perm = plan.perm.numpy()
+    np.testing.assert_array_equal(idx[1][perm], np.sort(idx[1], kind="stable"))
+    plan_c = gasfm_amd.AttnPlan.from_targets(idx[0], 10)
+    assert plan_c.perm is None  # cam-major edges are already CSR
+
+
+def test_state_dict_layout_matches_reference():
+    f = golden("net_small.npz")
+    ref_keys = {k[3:]: f[k].shape for k in f.files if k.startswith("sd/")}
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.conf.small_conf(2))
+    ours = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    assert ours == {k: tuple(v) for k, v in ref_keys.items()}
+    full = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf()).state_dict()
+    assert len(full) == 886 and sum(v.numel() for v in full.values()) == 145_165_560
+    assert sum(v.numel() for v in gasfm_amd.GraphAttnSfMNet(gasfm_amd.optim_conf()).state_dict().values()) \
+        == 109_108_632
+
+
+def test_compute_path_refuses_cpu_tensors():
+    plan = gasfm_amd.AttnPlan.from_targets(np.array([0, 0, 1]), 2)
+    XL = torch.randn(3, 32)
+    with pytest.raises(TypeError, match="CUDA"):
+        gasfm_amd.gat_attention(XL, torch.randn(2, 32), torch.randn(4, 8), torch.randn(32), plan, 4)
+
+
+def test_conf_parser_roundtrip():
+    text = """
+    dataset { calibrated = true
+      test_set = ["A" "B"] }
+    model {
+      type = "graph_attn_sfm.GraphAttnSfMNet"
+      n_heads = 4
+      view_head { enabled = true
+        rot_representation = "quat" }
+      depth_head.enabled = false
+    }
+    train.lr = 0.0001
+    """
+    c = gasfm_amd.Conf.parse_string(text)
+    assert c.get_int("model.n_heads") == 4
+    assert c.get_bool("model.view_head.enabled") is True
+    assert c.get_bool("model.depth_head.enabled") is False
+    assert c.get_string("model.view_head.rot_representation") == "quat"
+    assert c.get("dataset.test_set") == ["A", "B"]
+    assert abs(c.get_float("train.lr") - 1e-4) < 1e-12
+    assert c.get_int("model.missing", default=None) is None
