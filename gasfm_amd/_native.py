@@ -35,6 +35,15 @@ _SIGS = {
                                   _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp]),
     "gasfm_gat_attn_bwd_combine": (_i32, [_vp, _i32, _i32, _vp, _vp, _i64, _vp]),
     "gasfm_colsum_ws_floats": (_i64, [_i64, _i32]),
+    "gasfm_edge_part_floats": (_i32, [_i32, _i64, _i32]),
+    "gasfm_edge_prologue_fwd": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _i64, _vp]),
+    "gasfm_edge_epilogue_fwd": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _i32, _vp, _vp, _vp, _vp,
+                                       _f32, _vp, _vp]),
+    "gasfm_edge_epilogue_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _i32, _f32, _vp, _vp, _vp,
+                                       _vp, _vp]),
+    "gasfm_edge_prologue_bwd": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _vp, _i32, _f32, _vp, _vp,
+                                       _vp]),
+    "gasfm_segment_rowsum": (_i32, [_vp, _i32, _vp, _vp, _i64, _f32, _vp, _vp, _vp]),
     "gasfm_colsum": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _vp]),
 }
 
@@ -157,3 +166,52 @@ def colsum(A, out=None):
     st = lib().gasfm_colsum(_p(A), rows, cols, max(A.stride(0), cols), _p(ws), _p(out), _stream(out))
     check(st, "gasfm_colsum")
     return out
+
+
+# ---------------------------------------------------------------- fused per-edge block kernels
+def _req(t, name, cols=None):
+    if not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous():
+        raise TypeError(f"{name}: expected a contiguous float32 CUDA tensor (no CPU fallback)")
+    if cols is not None and t.shape[-1] != cols:
+        raise ValueError(f"{name}: expected {cols} columns, got {tuple(t.shape)}")
+
+
+def edge_part_floats(which, E, n_items=0):
+    return lib().gasfm_edge_part_floats(which, E, n_items)
+
+
+def edge_prologue_fwd(P, ln_w, ln_b, eps, W, b, Y):
+    _req(P, "P", 32)
+    st = lib().gasfm_edge_prologue_fwd(_p(P), P.shape[0], _p(ln_w), _p(ln_b), eps, _p(W), _p(b), _p(Y), Y.stride(0),
+                                       _stream(P))
+    check(st, "gasfm_edge_prologue_fwd")
+
+
+def edge_epilogue_fwd(P, P0, cam, pt, ln_w, ln_b, eps, Wp, bp, Sp, Sv, Sg, scale, out):
+    _req(P, "P", 32)
+    for t, n in ((Sp, "Sp"), (Sv, "Sv"), (Sg, "Sg"), (Wp, "Wp")):
+        _req(t, n)
+    st = lib().gasfm_edge_epilogue_fwd(_p(P), _p(P0), _p(cam), _p(pt), P.shape[0], _p(ln_w), _p(ln_b), eps, _p(Wp),
+                                       Wp.shape[1], _p(bp), _p(Sp), _p(Sv), _p(Sg), scale, _p(out), _stream(P))
+    check(st, "gasfm_edge_epilogue_fwd")
+
+
+def edge_epilogue_bwd(items, n_items, dPo, P, P0, ln_w, ln_b, eps, Wp, scale, dSv, part_dsv, dP0, part_w):
+    _req(dPo, "dP'", 32)
+    st = lib().gasfm_edge_epilogue_bwd(_p(items), n_items, _p(dPo), _p(P), _p(P0), _p(ln_w), _p(ln_b), eps, _p(Wp),
+                                       Wp.shape[1], scale, _p(dSv), _p(part_dsv), _p(dP0), _p(part_w), _stream(dPo))
+    check(st, "gasfm_edge_epilogue_bwd")
+
+
+def edge_prologue_bwd(dXL, P, dRes, ln_w, ln_b, eps, W, Wp, scale, dP, part):
+    _req(P, "P", 32)
+    st = lib().gasfm_edge_prologue_bwd(_p(dXL), dXL.stride(0), _p(P), _p(dRes), P.shape[0], _p(ln_w), _p(ln_b), eps,
+                                       _p(W), _p(Wp), Wp.shape[1] if Wp is not None else 0, scale, _p(dP), _p(part),
+                                       _stream(P))
+    check(st, "gasfm_edge_prologue_bwd")
+
+
+def segment_rowsum(items, n_items, perm, X, scale, out, part):
+    st = lib().gasfm_segment_rowsum(_p(items), n_items, _p(perm), _p(X), X.stride(0), scale, _p(out), _p(part),
+                                    _stream(X))
+    check(st, "gasfm_segment_rowsum")

@@ -457,20 +457,33 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_kernel(
   if (row == 0) store_vec<G::VEC>(datt_part + int64_t(wave) * G::HC + f0, datt);
 }
 
-// dXR[seg] = ordered sum of its partial slots.  One wave per entry, lanes over features.
+// dXR[seg] = ordered sum of its partial slots.  One workgroup per entry: thread t owns
+// column t % HC and slot group t / HC (R = 256/HC groups, or 1 with column loops for
+// HC > 256); the group sums are added in group order, so the result is deterministic.
 __global__ __launch_bounds__(kBlock) void attn_bwd_combine_kernel(const gasfm_combine_item* __restrict__ comb,
                                                              int n_comb, int HC,
                                                              const float* __restrict__ part,
                                                              float* __restrict__ dXR, int64_t ld) {
-  const int wave = wave_id_uniform();
-  const int lane = threadIdx.x & (kWave - 1);
-  if (wave >= n_comb) return;
-  const gasfm_combine_item ci = comb[wave];
-  for (int f = lane; f < HC; f += kWave) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  const gasfm_combine_item ci = comb[blockIdx.x];
+  const int R = HC <= kBlock ? kBlock / HC : 1;
+  const int grp = threadIdx.x / (HC <= kBlock ? HC : kBlock);
+  for (int f0 = 0; f0 < HC; f0 += kBlock) {
+    const int f = f0 + (HC <= kBlock ? int(threadIdx.x % HC) : int(threadIdx.x));
     float acc = 0.f;
-    for (int k = 0; k < ci.slot_count; ++k)
-      acc += part[(int64_t(ci.slot_begin) + int64_t(k) * ci.slot_stride) * HC + f];
-    dXR[int64_t(ci.seg) * ld + f] = acc;
+    if (grp < R && f < HC) {
+#pragma unroll 4
+      for (int k = grp; k < ci.slot_count; k += R)
+        acc += part[(int64_t(ci.slot_begin) + int64_t(k) * ci.slot_stride) * HC + f];
+    }
+    __syncthreads();
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    if (grp == 0 && f < HC) {
+      float t = 0.f;
+      for (int g = 0; g < R; ++g) t += sh[g * (HC <= kBlock ? HC : kBlock) + threadIdx.x];
+      dXR[int64_t(ci.seg) * ld + f] = t;
+    }
   }
 }
 
@@ -751,8 +764,7 @@ extern "C" int gasfm_gat_attn_bwd_combine(const gasfm_combine_item* combine, int
   GASFM_REQUIRE(HC > 0 && n_combine >= 0, "gasfm_gat_attn_bwd_combine: bad args");
   if (n_combine == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int grid = (n_combine + (kBlock / kWave) - 1) / (kBlock / kWave);
-  hipLaunchKernelGGL(attn_bwd_combine_kernel, dim3(grid), dim3(kBlock), 0, st, combine, n_combine, HC, part_dxr,
-                     dXR, ldDXR);
+  hipLaunchKernelGGL(attn_bwd_combine_kernel, dim3(n_combine), dim3(kBlock), kBlock * sizeof(float), st, combine,
+                     n_combine, HC, part_dxr, dXR, ldDXR);
   return launch_status("gasfm_gat_attn_bwd_combine");
 }

@@ -1,0 +1,139 @@
+"""Autograd wrappers of the fused per-edge block kernels (gasfm_amd/csrc/edge_block.hip).
+
+A GASFM block (layers.py:222-263) on its E projection rows is expressed with
+three differentiable ops whose forward AND backward are HIP kernels:
+
+  EdgePrologueFn   P -> (XL = [Wl_pt; Wl_cam] relu(LN(P)) + b,  token)
+  DualAttentionFn  XL -> (point aggregates, camera aggregates)   (fused GATv2 kernels)
+  EdgeEpilogueFn   (P, P0, token, Sp, Sv, Sg) -> P' = P + (Wp [P_hat|P0] + bp + Sp[pt] + Sv[cam] + Sg)/4
+
+P_hat = relu(LN(P)) is never materialised: both kernels recompute it from P.
+The `token` output of the prologue is a zero-stride placeholder whose gradient
+the epilogue's backward sets to dP' (the block-output gradient), so that the
+prologue's backward kernel can do the whole P-side backward in one pass:
+  dP = LN_bwd(mask * (Wl^T dXL + Wp^T dP'/4)) + dP'      (identity residual, layers.py:254-261)
+Node-level work between them (per-point / per-camera / global MLPs) stays in
+torch and runs on MFMA through hipBLASLt.
+"""
+import torch
+
+from . import _native
+from .attention import attn_backward_raw, attn_forward_raw
+
+PROJ_SCALE = 0.25  # the "/ 4" of layers.py:945
+
+
+def _colsum_parts(part, rows):
+    return _native.colsum(part.view(rows, -1))
+
+
+class EdgePrologueFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, P, ln_w, ln_b, W, b, Wp, eps):
+        E = P.shape[0]
+        XL = torch.empty((E, W.shape[0]), dtype=torch.float32, device=P.device)
+        _native.edge_prologue_fwd(P, ln_w, ln_b, eps, W.contiguous(), b.contiguous(), XL)
+        ctx.eps = eps
+        ctx.has_ln = ln_w is not None
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(P, ln_w, ln_b, W, Wp)
+        token = P.new_zeros((1, 1)).expand(E, P.shape[1])
+        return XL, token
+
+    @staticmethod
+    def backward(ctx, dXL, dtoken):
+        P, ln_w, ln_b, W, Wp = ctx.saved_tensors
+        E = P.shape[0]
+        if dXL is None:
+            dXL = torch.zeros((E, W.shape[0]), dtype=torch.float32, device=P.device)
+        dXL = dXL.contiguous()
+        dRes = None
+        if dtoken is not None and dtoken.stride(0) != 0:
+            dRes = dtoken.contiguous()
+        dP = torch.empty_like(P)
+        rows = _native.edge_part_floats(0, E) // (64 * 32 + 64 + 64)
+        part = torch.empty((rows, 64 * 32 + 64 + 64), dtype=torch.float32, device=P.device)
+        _native.edge_prologue_bwd(dXL, P, dRes, ln_w, ln_b, ctx.eps, W.contiguous(),
+                                  Wp.contiguous() if dRes is not None else None, PROJ_SCALE, dP, part)
+        tot = _colsum_parts(part, rows)
+        dW = tot[:64 * 32].view(64, 32)
+        db = tot[64 * 32:64 * 32 + 64]
+        dgam = tot[64 * 32 + 64:64 * 32 + 96] if ctx.has_ln else None
+        dbet = tot[64 * 32 + 96:] if ctx.has_ln else None
+        return dP, dgam, dbet, dW, db, None, None
+
+
+class DualAttentionFn(torch.autograd.Function):
+    """Point- and camera-direction GATv2 attention over the two halves of XL [E, 64]."""
+
+    @staticmethod
+    def forward(ctx, XL, XR_pt, XR_cam, att_pt, att_cam, bias_pt, bias_cam, plan_pt, plan_cam, heads, slope):
+        h = XL.shape[1] // 2
+        XLp, XLc = XL[:, :h], XL[:, h:]
+        out_p, mp, sp = attn_forward_raw(XLp, XR_pt, att_pt, bias_pt, plan_pt, heads, slope)
+        out_c, mc, sc = attn_forward_raw(XLc, XR_cam, att_cam, bias_cam, plan_cam, heads, slope)
+        ctx.plans = (plan_pt, plan_cam)
+        ctx.heads, ctx.slope = heads, slope
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(XL, XR_pt, XR_cam, att_pt, att_cam, bias_pt, bias_cam, out_p, mp, sp, out_c, mc, sc)
+        return out_p, out_c
+
+    @staticmethod
+    def backward(ctx, g_p, g_c):
+        XL, XR_pt, XR_cam, att_pt, att_cam, bias_pt, bias_cam, out_p, mp, sp, out_c, mc, sc = ctx.saved_tensors
+        plan_pt, plan_cam = ctx.plans
+        h = XL.shape[1] // 2
+        if g_p is None:
+            g_p = torch.zeros_like(out_p)
+        if g_c is None:
+            g_c = torch.zeros_like(out_c)
+        dXL = torch.empty_like(XL)
+        _, dXRp, dattp = attn_backward_raw(XL[:, :h], XR_pt, att_pt, bias_pt, plan_pt, ctx.heads, ctx.slope, out_p, mp,
+                                           sp, g_p, dXL=dXL[:, :h])
+        _, dXRc, dattc = attn_backward_raw(XL[:, h:], XR_cam, att_cam, bias_cam, plan_cam, ctx.heads, ctx.slope, out_c,
+                                           mc, sc, g_c, dXL=dXL[:, h:])
+        dbp = _native.colsum(g_p.contiguous())
+        dbc = _native.colsum(g_c.contiguous())
+        return (dXL, dXRp, dXRc, dattp.view_as(att_pt), dattc.view_as(att_cam), dbp, dbc, None, None, None, None)
+
+
+class EdgeEpilogueFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, P, P0, token, Sp, Sv, Sg, Wp, bp, ln_w, ln_b, eps, edges):
+        out = torch.empty_like(P)
+        Wp_c = Wp.contiguous()
+        _native.edge_epilogue_fwd(P, P0, edges.cam, edges.pt, ln_w, ln_b, eps, Wp_c, bp.contiguous(),
+                                  Sp.contiguous(), Sv.contiguous(), Sg.reshape(-1).contiguous(), PROJ_SCALE, out)
+        ctx.eps = eps
+        ctx.edges = edges
+        ctx.sg_shape = Sg.shape
+        ctx.save_for_backward(P, P0, Wp_c, ln_w, ln_b)
+        return out
+
+    @staticmethod
+    def backward(ctx, dPo):
+        P, P0, Wp, ln_w, ln_b = ctx.saved_tensors
+        edges = ctx.edges
+        dPo = dPo.contiguous()
+        dev = P.device
+        pc = edges.plans["proj2view"]
+        pp = edges.plans["proj2scenepoint"]
+        # camera side: dSv (+ dWp, dP0) in one pass over the camera work items
+        dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
+        part_dsv = torch.empty((max(pc.n_slots, 1), 32), dtype=torch.float32, device=dev)
+        dP0 = torch.empty((P.shape[0], 2), dtype=torch.float32, device=dev) if P0 is not None else None
+        wg = _native.edge_part_floats(1, P.shape[0], pc.n_items) // (32 * 34)
+        part_w = torch.empty((wg, 32 * Wp.shape[1]), dtype=torch.float32, device=dev)
+        _native.edge_epilogue_bwd(pc.items, pc.n_items, dPo, P, P0, ln_w, ln_b, ctx.eps, Wp, PROJ_SCALE, dSv,
+                                  part_dsv, dP0, part_w)
+        if pc.n_combine:
+            _native.attn_bwd_combine(pc.combine, pc.n_combine, 32, part_dsv, dSv)
+        dWp = _native.colsum(part_w).view(32, Wp.shape[1])
+        dSg = _native.colsum(dSv)          # == d bias_proj: every edge belongs to one camera
+        # point side: dSp = per-point sum of dP'/4 through the point permutation
+        dSp = torch.empty((edges.n, 32), dtype=torch.float32, device=dev)
+        part_dsp = torch.empty((max(pp.n_slots, 1), 32), dtype=torch.float32, device=dev)
+        _native.segment_rowsum(pp.items, pp.n_items, pp.perm, dPo, PROJ_SCALE, dSp, part_dsp)
+        if pp.n_combine:
+            _native.attn_bwd_combine(pp.combine, pp.n_combine, 32, part_dsp, dSp)
+        return (None, dP0, dPo, dSp, dSv, dSg.view(ctx.sg_shape), dWp, dSg.clone(), None, None, None, None)

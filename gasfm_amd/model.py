@@ -25,6 +25,7 @@ from torch.nn import Identity, LayerNorm, Linear, Module, ModuleList, ReLU, Sequ
 
 from . import edge_ops
 from .attention import AttnPlan
+from .edge_block import DualAttentionFn, EdgeEpilogueFn, EdgePrologueFn
 from .gatv2 import GATv2Conv
 
 GRAPH_NAMES = ("proj2view", "proj2scenepoint", "view2global", "scenepoint2global")
@@ -88,7 +89,18 @@ class _NodeAggregation(Module):
         """proj_feats [E, F_in] (edge order) -> node features [N, n_feat_out]."""
         assert self.stateful == (prev is not None)
         x_agg = getattr(self, self._state_key)(prev) if prev is not None else None
-        x = self.graph_conv.attend(proj_feats, x_agg, plan)
+        return self.tail(self.graph_conv.attend(proj_feats, x_agg, plan), prev)
+
+    def target_rows(self, prev, num_targets):
+        """XR = lin_r(x_agg) of the destination nodes (lin_r(0) broadcast when stateless)."""
+        conv = self.graph_conv
+        if prev is None:
+            zero = torch.zeros((1, conv.in_channels), device=conv.lin_r.weight.device)
+            return conv.lin_r(zero).expand(num_targets, -1)
+        return conv.lin_r(getattr(self, self._state_key)(prev))
+
+    def tail(self, x, prev):
+        """Everything after the GATv2 aggregation: proj, state skip, LN+ReLU, MLP, skip."""
         if self.n_feat_agg != self.n_feat_out:
             x = getattr(self, self._proj_key)(x)
         if prev is not None:
@@ -234,9 +246,38 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
             self.global2scenepoint = Global2ScenePoint(n_feat_global_out, n_feat_scenepoint_out,
                                                        n_hidden_layers_scenepoint_update)
 
+    def fusable(self):
+        """Edge side expressible with the fused 32-wide kernels (every GASFM conf, blocks >= 1)."""
+        ok = True
+        for m in (self.proj2scenepoint, self.proj2view):
+            c = m.graph_conv
+            ok &= c.in_channels == 32 and c.heads * c.out_channels == 32 and c.lin_l.bias is not None
+            ok &= c.bias is not None
+        return bool(ok)
+
+    def lin_l_stack(self):
+        a, b = self.proj2scenepoint.graph_conv.lin_l, self.proj2view.graph_conv.lin_l
+        return torch.cat([a.weight, b.weight], 0), torch.cat([a.bias, b.bias], 0)
+
+    def forward_fused(self, XL, plans, prev_pt=None, prev_view=None, prev_glob=None):
+        """Node side of the update given XL = [lin_l_point(P_hat) | lin_l_camera(P_hat)] [E, 64]."""
+        sp, sv = self.proj2scenepoint, self.proj2view
+        pp, pc = plans["proj2scenepoint"], plans["proj2view"]
+        XRp = sp.target_rows(prev_pt, pp.num_targets)
+        XRc = sv.target_rows(prev_view, pc.num_targets)
+        cp, cc = sp.graph_conv, sv.graph_conv
+        agg_p, agg_c = DualAttentionFn.apply(XL, XRp, XRc, cp.att, cc.att, cp.bias, cc.bias, pp, pc, cp.heads,
+                                             cp.negative_slope)
+        pts = sp.tail(agg_p, prev_pt)
+        view = sv.tail(agg_c, prev_view)
+        return self._finish(pts, view, plans, prev_glob)
+
     def forward_plan(self, P_hat, plans, prev_pt=None, prev_view=None, prev_glob=None):
         pts = self.proj2scenepoint.forward_plan(P_hat, plans["proj2scenepoint"], prev_pt)
         view = self.proj2view.forward_plan(P_hat, plans["proj2view"], prev_view)
+        return self._finish(pts, view, plans, prev_glob)
+
+    def _finish(self, pts, view, plans, prev_glob):
         glob = None
         if self.output_global or self.global2view_and_global2scenepoint_enabled:
             glob = self.view_and_scenepoint2global.forward_plan(view, pts, plans["view2global"],
@@ -312,8 +353,33 @@ class GraphAttnSfMLayer(Module):
                 self.residual_skipconn_proj_norm_layer = LayerNorm(n_feat_proj_in)
             self.skip_projection = ProjLayer(n_feat_proj_in, n_feat_proj_out)
 
+    def fusable(self):
+        pfu = self.projection_feature_update
+        w = pfu.lin_proj.weight
+        return (self.use_norm_proj_update and self.add_residual_skipconn_proj_update and self.skip_projection is None
+                and pfu.n_hidden_layers_proj_update == 0 and pfu.normalize_global_features
+                and w.shape[0] == 32 and w.shape[1] in (32, 34)
+                and (w.shape[1] == 34) == self.add_skipconn_from_init_projfeat
+                and self.prev_projfeat_norm_layer.normalized_shape == (32,)
+                and self.global_feature_update.fusable())
+
+    def forward_fused(self, P, plans, edges, prev_pt, prev_view, prev_glob, P0):
+        """Blocks >= 1 with the fused HIP edge kernels (see gasfm_amd/edge_block.py)."""
+        ln = self.prev_projfeat_norm_layer
+        gfu = self.global_feature_update
+        pfu = self.projection_feature_update
+        W, b = gfu.lin_l_stack()
+        XL, token = EdgePrologueFn.apply(P, ln.weight, ln.bias, W, b, pfu.lin_proj.weight, ln.eps)
+        pts, view, glob = gfu.forward_fused(XL, plans, prev_pt, prev_view, prev_glob)
+        sp, sv, sg = pfu.node_terms(pts, view, glob)
+        P_new = EdgeEpilogueFn.apply(P, P0 if self.add_skipconn_from_init_projfeat else None, token, sp, sv, sg,
+                                     pfu.lin_proj.weight, pfu.lin_proj.bias, ln.weight, ln.bias, ln.eps, edges)
+        return P_new, pts, view, glob
+
     def forward_plan(self, P, plans, edges, prev_pt=None, prev_view=None, prev_glob=None, P0=None):
         """P [E, F_in] edge features (cam-major) -> (P' [E, F_out], pts, view, glob)."""
+        if P.is_cuda and self.fusable():
+            return self.forward_fused(P, plans, edges, prev_pt, prev_view, prev_glob, P0)
         if self.use_norm_proj_update:
             P_hat = edge_ops.layer_norm_relu(P, self.prev_projfeat_norm_layer)
         else:
@@ -496,8 +562,15 @@ class GraphAttnSfMNet(Module):
             P, pts, view, glob = blk.forward_plan(P, plans, edges, pts if sf else None, view if sf else None,
                                                   glob if sf else None, P0=P0)
         if self.view_head_enabled or self.scenepoint_head_enabled:
-            pts, view, _ = self.final_global_update.forward_plan(P, plans, pts if sf else None,
-                                                                 view if sf else None, glob if sf else None)
+            fgu = self.final_global_update
+            args = (pts if sf else None, view if sf else None, glob if sf else None)
+            if P.is_cuda and P.shape[1] == 32 and fgu.fusable():
+                # raw (un-normalised) projection features (graph_attn_sfm.py:141-148): no LN prologue
+                W, b = fgu.lin_l_stack()
+                XL, _ = EdgePrologueFn.apply(P.contiguous(), None, None, W, b, None, 1e-5)
+                pts, view, _ = fgu.forward_fused(XL, plans, *args)
+            else:
+                pts, view, _ = fgu.forward_plan(P, plans, *args)
         return P, pts, view
 
     def forward(self, data):

