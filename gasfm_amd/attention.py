@@ -161,7 +161,7 @@ def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True):
 
 
 def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, gout, dXL=None):
-    """Launch the backward kernels; returns (dXL, dXR, datt[HC])."""
+    """Launch the backward kernels; returns (dXL, dXR, datt[HC], dbias[HC])."""
     HC = att.numel()
     C = HC // heads
     dev = XL.device
@@ -172,18 +172,20 @@ def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, go
         dXL = (torch.empty if full else torch.zeros)((XL.shape[0], HC), dtype=torch.float32, device=dev)
     dXR = torch.empty((plan.num_targets, HC), dtype=torch.float32, device=dev)
     part = torch.empty((plan.n_slots, HC), dtype=torch.float32, device=dev) if plan.n_slots else None
-    datt_part = torch.empty((max(plan.bwd_waves, 1), HC), dtype=torch.float32, device=dev)
+    datt_part = torch.empty((max(plan.bwd_waves, 1), 2 * HC), dtype=torch.float32, device=dev)
     attf = att.reshape(-1).contiguous()
     if plan.n_items:
         _native.attn_bwd(XL, XR, attf, bias, plan.perm, plan.items, plan.n_items, heads, C, slope, out, smax,
                          ssum, gout, dXL, dXR, part, datt_part)
         if plan.n_combine:
             _native.attn_bwd_combine(plan.combine, plan.n_combine, HC, part, dXR)
-        datt = _native.colsum(datt_part)
+        tot = _native.colsum(datt_part)
+        datt, dbias = tot[:HC], tot[HC:]
     else:
         dXR.zero_()
         datt = torch.zeros(HC, dtype=torch.float32, device=dev)
-    return dXL, dXR, datt
+        dbias = torch.zeros(HC, dtype=torch.float32, device=dev)
+    return dXL, dXR, datt, dbias
 
 
 class GatAttentionFn(torch.autograd.Function):
@@ -202,9 +204,8 @@ class GatAttentionFn(torch.autograd.Function):
         XL, XR, att, bias, out, smax, ssum = ctx.saved_tensors
         if gout is None:
             return None, None, None, None, None, None, None
-        dXL, dXR, datt = attn_backward_raw(XL, XR, att, bias, ctx.plan, ctx.heads, ctx.slope, out, smax, ssum,
-                                           gout)
-        dbias = _native.colsum(gout if gout.stride(1) == 1 else gout.contiguous())
+        dXL, dXR, datt, dbias = attn_backward_raw(XL, XR, att, bias, ctx.plan, ctx.heads, ctx.slope, out, smax,
+                                                  ssum, gout)
         return dXL, dXR, datt.view_as(att), dbias, None, None, None
 
 

@@ -360,11 +360,11 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_kernel(
   const int wave = wave_id_uniform();
   const int nwaves = gridDim.x * (blockDim.x / kWave);
 
-  float attv[G::VEC], bv[G::VEC], datt[G::VEC];
+  float attv[G::VEC], bv[G::VEC], datt[G::VEC], dbias[G::VEC];
   load_vec<G::VEC>(attv, att + f0);
   load_vec<G::VEC>(bv, bias + f0);
 #pragma unroll
-  for (int v = 0; v < G::VEC; ++v) datt[v] = 0.f;
+  for (int v = 0; v < G::VEC; ++v) datt[v] = dbias[v] = 0.f;
 
   for (int it = wave; it < n_items; it += nwaves) {
     const gasfm_work_item w = items[it];
@@ -373,6 +373,11 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_kernel(
     load_vec<G::VEC>(xr, XR + sg * ldXR + f0);
     load_vec<G::VEC>(g, gout + sg * ldG + f0);
     load_vec<G::VEC>(o, out + sg * ldOut + f0);
+    // d bias = sum of gout over segments: count each segment once (its first item) on row 0
+    if (row == 0 && (it == 0 || items[it - 1].seg != w.seg)) {
+#pragma unroll
+      for (int v = 0; v < G::VEC; ++v) dbias[v] += g[v];
+    }
     float M[G::HPL], inv[G::HPL], delta[G::HPL];
 #pragma unroll
     for (int hh = 0; hh < G::HPL; ++hh) {
@@ -454,7 +459,10 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_kernel(
 #pragma unroll
     for (int v = 0; v < G::VEC; ++v) datt[v] += __shfl_xor(datt[v], o2);
   }
-  if (row == 0) store_vec<G::VEC>(datt_part + int64_t(wave) * G::HC + f0, datt);
+  if (row == 0) {
+    store_vec<G::VEC>(datt_part + int64_t(wave) * 2 * G::HC + f0, datt);
+    store_vec<G::VEC>(datt_part + int64_t(wave) * 2 * G::HC + G::HC + f0, dbias);
+  }
 }
 
 // dXR[seg] = ordered sum of its partial slots.  One workgroup per entry: thread t owns
@@ -595,11 +603,13 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_generic(
   const int lane = threadIdx.x & (kWave - 1);
   const int nwaves = gridDim.x * (blockDim.x / kWave);
   const int HC = H * C;
-  for (int f = lane; f < HC; f += kWave) datt_part[int64_t(wave) * HC + f] = 0.f;
+  for (int f = lane; f < 2 * HC; f += kWave) datt_part[int64_t(wave) * 2 * HC + f] = 0.f;
   for (int it = wave; it < n_items; it += nwaves) {
     const gasfm_work_item w = items[it];
     const int64_t sg = w.seg;
+    const bool first = it == 0 || items[it - 1].seg != w.seg;
     for (int f = lane; f < HC; f += kWave) {
+      if (first) datt_part[int64_t(wave) * 2 * HC + HC + f] += gout[sg * ldG + f];
       const int h = f / C;
       const float M = seg_max[sg * H + h];
       const float inv = 1.f / (seg_sum[sg * H + h] + 1e-16f);
@@ -630,7 +640,7 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_generic(
         dXR[sg * ldDXR + f] = dxr;
       else
         part_dxr[int64_t(w.slot) * HC + f] = dxr;
-      datt_part[int64_t(wave) * HC + f] += dat;
+      datt_part[int64_t(wave) * 2 * HC + f] += dat;
     }
   }
 }

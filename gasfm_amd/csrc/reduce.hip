@@ -5,37 +5,68 @@
 // GATv2Conv.att (PyG, layers.py:304-309 etc.) and LayerNorm/Linear biases.
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
+
 #include "common.hpp"
 
 namespace gasfm {
 
 constexpr int kColBlock = 256;
-constexpr int kMaxColBlocks = 512;
+constexpr int kMaxColBlocks = 1024;
 
 static int colsum_blocks(int64_t rows) {
-  const int64_t b = (rows + 255) / 256;
+  const int64_t b = (rows + 127) / 128;
   return int(b < 1 ? 1 : (b > kMaxColBlocks ? kMaxColBlocks : b));
 }
 
-// Threads of a block cover (row lane, column) pairs: with cols <= 256 the block
-// walks RPB = 256/cols rows at a time so that short rows still coalesce.
+// Pass 1.  cols % 4 == 0 and 16-byte aligned rows: each thread owns a float4 column
+// group (c4) and a row lane (rl); RL = 256 / (cols/4) row lanes stride the block's row
+// range with 4 independent loads in flight, then the row lanes are summed through LDS
+// in lane order.  Other shapes: thread per column, rows serial.
 __global__ __launch_bounds__(kColBlock) void colsum_pass1(const float* __restrict__ A, int64_t rows, int cols,
                                                        int64_t ld, float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
   const int nb = gridDim.x;
   const int64_t r0 = rows * blockIdx.x / nb, r1 = rows * (blockIdx.x + 1) / nb;
-  if (cols <= kColBlock) {
-    const int rpb = kColBlock / cols;
-    const int c = threadIdx.x % cols, rr = threadIdx.x / cols;
-    float acc = 0.f;
-    if (rr < rpb)
-      for (int64_t r = r0 + rr; r < r1; r += rpb) acc += A[r * ld + c];
-    sh[threadIdx.x] = acc;
+  const int C4 = cols / 4;
+  if ((cols & 3) == 0 && (ld & 3) == 0 && C4 <= kColBlock && (reinterpret_cast<uintptr_t>(A) & 15) == 0) {
+    const int RL = kColBlock / C4;
+    const int c4 = threadIdx.x % C4, rl = threadIdx.x / C4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (rl < RL) {
+      int64_t r = r0 + rl;
+      for (; r + 3 * RL < r1; r += 4 * RL) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(A + (r + u * RL) * ld + 4 * c4);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          acc.x += v[u].x;
+          acc.y += v[u].y;
+          acc.z += v[u].z;
+          acc.w += v[u].w;
+        }
+      }
+      for (; r < r1; r += RL) {
+        const float4 v = *reinterpret_cast<const float4*>(A + r * ld + 4 * c4);
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+      }
+    }
+    reinterpret_cast<float4*>(sh)[threadIdx.x] = acc;
     __syncthreads();
-    if (threadIdx.x < cols) {
-      float t = 0.f;
-      for (int k = 0; k < rpb; ++k) t += sh[k * cols + threadIdx.x];
-      ws[int64_t(blockIdx.x) * cols + threadIdx.x] = t;
+    if (threadIdx.x < C4) {
+      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int k = 0; k < RL; ++k) {
+        const float4 v = reinterpret_cast<const float4*>(sh)[k * C4 + threadIdx.x];
+        t.x += v.x;
+        t.y += v.y;
+        t.z += v.z;
+        t.w += v.w;
+      }
+      reinterpret_cast<float4*>(ws + int64_t(blockIdx.x) * cols)[threadIdx.x] = t;
     }
   } else {
     for (int c = threadIdx.x; c < cols; c += kColBlock) {
@@ -46,13 +77,20 @@ __global__ __launch_bounds__(kColBlock) void colsum_pass1(const float* __restric
   }
 }
 
+// Pass 2: block handles 64 columns; 4 row lanes sum blocks b = rl, rl+4, ... then
+// the lanes are added in order (deterministic for a given launch geometry).
 __global__ __launch_bounds__(kColBlock) void colsum_pass2(const float* __restrict__ ws, int nb, int cols,
                                                        float* __restrict__ out) {
-  for (int c = blockIdx.x * kColBlock + threadIdx.x; c < cols; c += gridDim.x * kColBlock) {
-    float acc = 0.f;
-    for (int b = 0; b < nb; ++b) acc += ws[int64_t(b) * cols + c];
-    out[c] = acc;
+  __shared__ float sh[kColBlock];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rl = threadIdx.x >> 6;
+  float acc = 0.f;
+  if (c < cols) {
+#pragma unroll 4
+    for (int b = rl; b < nb; b += 4) acc += ws[int64_t(b) * cols + c];
   }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  if (rl == 0 && c < cols) out[c] = ((sh[threadIdx.x] + sh[threadIdx.x + 64]) + sh[threadIdx.x + 128]) + sh[threadIdx.x + 192];
 }
 
 }  // namespace gasfm
@@ -70,10 +108,11 @@ extern "C" int gasfm_colsum(const float* A, int64_t rows, int32_t cols, int64_t 
   GASFM_REQUIRE(ws && out && (rows == 0 || A), "gasfm_colsum: null pointer");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int nb = colsum_blocks(rows);
-  hipLaunchKernelGGL(colsum_pass1, dim3(nb), dim3(kColBlock), kColBlock * sizeof(float), st, A, rows, cols, ld, ws);
+  hipLaunchKernelGGL(colsum_pass1, dim3(nb), dim3(kColBlock), 4 * kColBlock * sizeof(float), st, A, rows, cols, ld,
+                     ws);
   int rc = launch_status("gasfm_colsum/pass1");
   if (rc) return rc;
-  const int g2 = (cols + kColBlock - 1) / kColBlock;
+  const int g2 = (cols + 63) / 64;
   hipLaunchKernelGGL(colsum_pass2, dim3(g2), dim3(kColBlock), 0, st, ws, nb, cols, out);
   return launch_status("gasfm_colsum/pass2");
 }

@@ -88,12 +88,10 @@ class DualAttentionFn(torch.autograd.Function):
         if g_c is None:
             g_c = torch.zeros_like(out_c)
         dXL = torch.empty_like(XL)
-        _, dXRp, dattp = attn_backward_raw(XL[:, :h], XR_pt, att_pt, bias_pt, plan_pt, ctx.heads, ctx.slope, out_p, mp,
-                                           sp, g_p, dXL=dXL[:, :h])
-        _, dXRc, dattc = attn_backward_raw(XL[:, h:], XR_cam, att_cam, bias_cam, plan_cam, ctx.heads, ctx.slope, out_c,
-                                           mc, sc, g_c, dXL=dXL[:, h:])
-        dbp = _native.colsum(g_p.contiguous())
-        dbc = _native.colsum(g_c.contiguous())
+        _, dXRp, dattp, dbp = attn_backward_raw(XL[:, :h], XR_pt, att_pt, bias_pt, plan_pt, ctx.heads, ctx.slope,
+                                                out_p, mp, sp, g_p, dXL=dXL[:, :h])
+        _, dXRc, dattc, dbc = attn_backward_raw(XL[:, h:], XR_cam, att_cam, bias_cam, plan_cam, ctx.heads, ctx.slope,
+                                                out_c, mc, sc, g_c, dXL=dXL[:, h:])
         return (dXL, dXRp, dXRc, dattp.view_as(att_pt), dattc.view_as(att_cam), dbp, dbc, None, None, None, None)
 
 

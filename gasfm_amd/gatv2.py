@@ -20,6 +20,7 @@ import math
 import torch
 import torch.nn.functional as F
 
+from . import dense
 from .attention import AttnPlan, gat_attention
 
 
@@ -87,7 +88,7 @@ class GATv2Conv(torch.nn.Module):
         x_tgt [N, F_in] target node features, or None for the reference's zero target
               features (dataset_utils.py:569-571), where lin_r(0) == lin_r.bias.
         """
-        XL = self.lin_l(x_src)
+        XL = dense.linear(x_src, self.lin_l)
         if x_tgt is None:
             # one zero row through lin_r (== its bias) broadcast over the targets: lin_r.weight
             # still receives its (zero) gradient, as in the reference, so train.py:137's
@@ -95,7 +96,7 @@ class GATv2Conv(torch.nn.Module):
             zero = torch.zeros((1, self.in_channels), dtype=x_src.dtype, device=x_src.device)
             XR = self.lin_r(zero).expand(plan.num_targets, -1)
         else:
-            XR = self.lin_r(x_tgt)
+            XR = dense.linear(x_tgt, self.lin_r)
         return gat_attention(XL, XR, self.att, self._bias(XL), plan, self.heads, self.negative_slope)
 
     # ------------------------------------------------------------------ PyG call form
@@ -106,13 +107,11 @@ class GATv2Conv(torch.nn.Module):
             src, dst = edge_index[0].cpu(), edge_index[1].cpu()
             unique_src = src.numel() == 0 or int(torch.bincount(src).max()) <= 1
             if unique_src:
-                plan = AttnPlan.from_targets(dst, num_nodes, src=src, src_rows=num_nodes)
+                plan = AttnPlan.from_targets(dst, num_nodes, src=src, src_rows=num_nodes).to(edge_index.device)
+                plan.gather_src = None
             else:
                 # repeated sources: gather per-edge source rows first (edge order == plan order)
-                plan = AttnPlan.from_targets(dst, num_nodes)
-                plan.gather_src = src.to(edge_index.device)
-            plan = plan.to(edge_index.device)
-            if not unique_src:
+                plan = AttnPlan.from_targets(dst, num_nodes).to(edge_index.device)
                 plan.gather_src = src.to(edge_index.device)
             self._plan_cache.clear()
             self._plan_cache[key] = plan
@@ -123,7 +122,6 @@ class GATv2Conv(torch.nn.Module):
         plan = self._plan_for(edge_index, N)
         XL = self.lin_l(x)
         XR = self.lin_r(x)
-        gs = getattr(plan, "gather_src", None)
-        if gs is not None:
-            XL = XL.index_select(0, gs)
+        if plan.gather_src is not None:
+            XL = XL.index_select(0, plan.gather_src)
         return gat_attention(XL, XR, self.att, self._bias(XL), plan, self.heads, self.negative_slope)

@@ -23,7 +23,7 @@ import torch
 import torch.nn.functional as F
 from torch.nn import Identity, LayerNorm, Linear, Module, ModuleList, ReLU, Sequential
 
-from . import edge_ops
+from . import dense, edge_ops
 from .attention import AttnPlan
 from .edge_block import DualAttentionFn, EdgeEpilogueFn, EdgePrologueFn
 from .gatv2 import GATv2Conv
@@ -88,7 +88,7 @@ class _NodeAggregation(Module):
     def forward_plan(self, proj_feats, plan, prev):
         """proj_feats [E, F_in] (edge order) -> node features [N, n_feat_out]."""
         assert self.stateful == (prev is not None)
-        x_agg = getattr(self, self._state_key)(prev) if prev is not None else None
+        x_agg = dense.sequential(getattr(self, self._state_key), prev) if prev is not None else None
         return self.tail(self.graph_conv.attend(proj_feats, x_agg, plan), prev)
 
     def target_rows(self, prev, num_targets):
@@ -97,18 +97,18 @@ class _NodeAggregation(Module):
         if prev is None:
             zero = torch.zeros((1, conv.in_channels), device=conv.lin_r.weight.device)
             return conv.lin_r(zero).expand(num_targets, -1)
-        return conv.lin_r(getattr(self, self._state_key)(prev))
+        return dense.linear(dense.sequential(getattr(self, self._state_key), prev), conv.lin_r)
 
     def tail(self, x, prev):
         """Everything after the GATv2 aggregation: proj, state skip, LN+ReLU, MLP, skip."""
         if self.n_feat_agg != self.n_feat_out:
-            x = getattr(self, self._proj_key)(x)
+            x = dense.linear(x, getattr(self, self._proj_key))
         if prev is not None:
             x = prev + x
         skip = x
         if self.use_norm_pre_mlp:
-            x = F.relu(self.norm_pre_mlp(x))
-        return skip + self.mlp(x)
+            x = F.relu(dense.layer_norm(x, self.norm_pre_mlp))
+        return skip + dense.sequential(self.mlp, x)
 
 
 class Proj2View(_NodeAggregation):
@@ -159,8 +159,8 @@ class ViewAndScenePoint2Global(Module):
 
     def forward_plan(self, view, pts, plan_v2g, plan_s2g, prev):
         assert self.stateful == (prev is not None)
-        xv = self.norm_and_proj_global2view(prev) if prev is not None else None
-        xp = self.norm_and_proj_global2scenepoint(prev) if prev is not None else None
+        xv = dense.sequential(self.norm_and_proj_global2view, prev) if prev is not None else None
+        xp = dense.sequential(self.norm_and_proj_global2scenepoint, prev) if prev is not None else None
         v2g = self.graph_conv_view2global.attend(view, xv, plan_v2g)
         s2g = self.graph_conv_scenepoint2global.attend(pts, xp, plan_s2g)
         x = torch.cat([v2g, s2g], dim=1)
@@ -311,10 +311,11 @@ class GraphAttnSfMProjectionFeatureUpdate(Module):
 
     def node_terms(self, pts, view, glob):
         if self.normalize_global_features:
-            pts = F.relu(self.scenepoint_norm_layer(pts))
-            view = F.relu(self.view_norm_layer(view))
-            glob = F.relu(self.global_norm_layer(glob))
-        return self.lin_scenepoint(pts), self.lin_view(view), self.lin_global(glob)
+            pts = F.relu(dense.layer_norm(pts, self.scenepoint_norm_layer))
+            view = F.relu(dense.layer_norm(view, self.view_norm_layer))
+            glob = F.relu(dense.layer_norm(glob, self.global_norm_layer))
+        return dense.linear(pts, self.lin_scenepoint), dense.linear(view, self.lin_view), \
+            dense.linear(glob, self.lin_global)
 
 
 class ProjLayer(Module):
@@ -587,7 +588,7 @@ class GraphAttnSfMNet(Module):
         if self.view_head_enabled:
             pred.update(self.extract_view_outputs(self.view_head(F.relu(view))))
         if self.scenepoint_head_enabled:
-            n_out = self.scenepoint_head(F.relu(pts)).T
+            n_out = dense.sequential(self.scenepoint_head, F.relu(pts)).T
             pred["pts3D"] = torch.cat([n_out, torch.ones(1, n_out.shape[1], dtype=n_out.dtype, device=device)])
         return pred
 

@@ -116,8 +116,8 @@ int gasfm_gat_attn_combine(const gasfm_combine_item* combine, int32_t n_combine,
 /* Backward of the above given dOut (gout), the forward's finalized out and
  * per-segment stats.  Writes dXL[src_j] for every edge (each row exactly
  * once), dXR[seg] for complete items (partials to part_dxr[slot] for split
- * items; merge with gasfm_gat_attn_bwd_combine) and one datt partial row per
- * wave into datt_part[n_waves, H*C] (n_waves from
+ * items; merge with gasfm_gat_attn_bwd_combine) and one partial row per
+ * wave into datt_part[n_waves, 2*H*C] = [d att | d bias] (n_waves from
  * gasfm_gat_attn_bwd_waves(); reduce with gasfm_colsum). */
 int gasfm_gat_attn_bwd_waves(int32_t n_items);
 int gasfm_gat_attn_bwd(const float* XL, int64_t ldXL,
