@@ -92,6 +92,7 @@ def main():
     dev = torch.device("cuda", local_rank)
     if world > 1:
         torch.distributed.init_process_group("nccl", device_id=dev)
+        log(f"[rank {rank}] process group up (world {world})")
 
     import gasfm_amd
     from gasfm_amd import attention, synthetic
@@ -117,9 +118,12 @@ def main():
     def step():
         pred = model(data)
         ps, pts = pred["Ps_norm"], pred["pts3D"]
-        cx = cX if pts.shape[1] == sc.n else cX[:, data.point_slice]
-        loss = (ps * cP).sum() / world + (pts * cx).sum()
+        cx = cX if world == 1 else cX[:, data.point_slice]
+        # replicated outputs enter every rank's loss in full, local points once (distributed.py)
+        loss = (ps * cP).sum() + (pts * cx).sum()
         loss.backward()
+        if world > 1:
+            model.sync_grads()
         for p in model.parameters():
             p.grad = None
 

@@ -27,9 +27,8 @@ _SIGS = {
     "gasfm_build_csr": (_i32, [_vp, _i64, _i32, _vp, _vp]),
     "gasfm_plan_work": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_gat_attn_fwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _f32, _i32,
-                                  _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "gasfm_gat_attn_combine": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp,
-                                      _vp]),
+                                  _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
+    "gasfm_gat_attn_combine": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _i64, _vp]),
     "gasfm_gat_attn_bwd_waves": (_i32, [_i32]),
     "gasfm_gat_attn_bwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _f32, _vp,
                                   _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp]),
@@ -120,20 +119,23 @@ def plan_work(seg_ptr, max_piece, all_partial=False):
 
 
 # ---------------------------------------------------------------- device kernels
-def attn_fwd(XL, XR, att, bias, perm, items, n_items, H, C, slope, finalize, out, seg_max, seg_sum,
-             part_acc=None, part_max=None, part_sum=None):
+def attn_fwd(XL, XR, att, bias, perm, items, n_items, H, C, slope, finalize, out, seg_max, seg_sum, part=None,
+             ldStat=None):
+    """part: packed partial rows [slots, H*C + 2H] (acc | max | sum) or None."""
+    ldStat = H if ldStat is None else ldStat
     st = lib().gasfm_gat_attn_fwd(
         _p(XL), XL.stride(0), _p(XR), XR.stride(0), _p(att), _p(bias), _p(perm), _p(items), n_items, H, C,
-        slope, int(finalize), _p(out), out.stride(0), _p(seg_max), _p(seg_sum), _p(part_acc), _p(part_max),
-        _p(part_sum), _stream(out))
+        slope, int(finalize), _p(out), out.stride(0) if out is not None else 0, _p(seg_max), _p(seg_sum), ldStat,
+        _p(part), _stream(XL))
     check(st, "gasfm_gat_attn_fwd")
 
 
-def attn_combine(combine, n_combine, H, C, part_acc, part_max, part_sum, bias, finalize, out, seg_max,
-                 seg_sum):
-    st = lib().gasfm_gat_attn_combine(
-        _p(combine), n_combine, H, C, _p(part_acc), _p(part_max), _p(part_sum), _p(bias), int(finalize),
-        _p(out), out.stride(0), _p(seg_max), _p(seg_sum), _stream(out))
+def attn_combine(combine, n_combine, H, C, part, bias, finalize, out, seg_max, seg_sum, ldOut=None, ldStat=None):
+    """Merge packed partial rows; out/seg_max/seg_sum may be views into a packed buffer (raw mode)."""
+    ldOut = out.stride(0) if ldOut is None else ldOut
+    ldStat = H if ldStat is None else ldStat
+    st = lib().gasfm_gat_attn_combine(_p(combine), n_combine, H, C, _p(part), _p(bias), int(finalize), _p(out),
+                                      ldOut, _p(seg_max), _p(seg_sum), ldStat, _stream(part))
     check(st, "gasfm_gat_attn_combine")
 
 

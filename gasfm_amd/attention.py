@@ -131,6 +131,8 @@ def _check(t, name, rows=None, cols=None):
 
 def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True):
     """Launch the forward kernels; returns (out, seg_max, seg_sum) for all plan targets."""
+    if plan.all_partial:
+        raise ValueError("all-partial plans go through attn_forward_partial")
     HC = att.numel()
     C = HC // heads
     N = plan.num_targets
@@ -140,23 +142,53 @@ def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True):
     out = torch.empty((N, HC), dtype=torch.float32, device=dev)
     smax = torch.empty((N, heads), dtype=torch.float32, device=dev)
     ssum = torch.empty((N, heads), dtype=torch.float32, device=dev)
-    pa = pm = ps = None
-    if plan.n_slots:
-        pa = torch.empty((plan.n_slots, HC), dtype=torch.float32, device=dev)
-        pm = torch.empty((plan.n_slots, heads), dtype=torch.float32, device=dev)
-        ps = torch.empty((plan.n_slots, heads), dtype=torch.float32, device=dev)
+    part = torch.empty((plan.n_slots, HC + 2 * heads), dtype=torch.float32, device=dev) if plan.n_slots else None
     attf = att.reshape(-1).contiguous()
     timed = KERNEL_TIMER is not None and KERNEL_TIMER(plan.tag, HC)
     if timed:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
     _native.attn_fwd(XL, XR, attf, bias, plan.perm, plan.items, plan.n_items, heads, C, slope, finalize, out,
-                     smax, ssum, pa, pm, ps)
+                     smax, ssum, part)
     if timed:
         ev[1].record()
         KERNEL_TIMER.events.append(ev)
     if plan.n_combine:
-        _native.attn_combine(plan.combine, plan.n_combine, heads, C, pa, pm, ps, bias, finalize, out, smax, ssum)
+        _native.attn_combine(plan.combine, plan.n_combine, heads, C, part, bias, finalize, out, smax, ssum)
+    return out, smax, ssum
+
+
+def attn_forward_partial(XL, XR, att, plan, heads, slope):
+    """Un-normalised per-segment partials of an all-partial plan.
+
+    Returns a packed [N, H*C + 2H] buffer (acc | max | sum) per destination segment —
+    what one rank contributes before the cross-rank combine.
+    """
+    assert plan.all_partial
+    HC = att.numel()
+    C = HC // heads
+    N = plan.num_targets
+    _check(XL, "XL", plan.src_rows, HC)
+    _check(XR, "XR", N if XR.stride(0) else 1, HC)
+    LDP = HC + 2 * heads
+    part = torch.empty((max(plan.n_slots, N), LDP), dtype=torch.float32, device=XL.device)
+    attf = att.reshape(-1).contiguous()
+    _native.attn_fwd(XL, XR, attf, None, plan.perm, plan.items, plan.n_items, heads, C, slope, False, None, None,
+                     None, part)
+    if plan.n_combine:  # merge split pieces (slots >= N) into rows [0, N), raw
+        _native.attn_combine(plan.combine, plan.n_combine, heads, C, part, None, False, part, part[:, HC:],
+                             part[:, HC + heads:], ldOut=LDP, ldStat=LDP)
+    return part[:N]
+
+
+def combine_partials(gathered, world, N, heads, bias, combine_items):
+    """Finalize W stacked packed partial blocks [W*N, LDP] -> (out [N,HC], seg_max, seg_sum)."""
+    HC = bias.numel()
+    C = HC // heads
+    out = torch.empty((N, HC), dtype=torch.float32, device=gathered.device)
+    smax = torch.empty((N, heads), dtype=torch.float32, device=gathered.device)
+    ssum = torch.empty((N, heads), dtype=torch.float32, device=gathered.device)
+    _native.attn_combine(combine_items, N, heads, C, gathered, bias, True, out, smax, ssum)
     return out, smax, ssum
 
 

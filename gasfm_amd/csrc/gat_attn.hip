@@ -127,8 +127,9 @@ __global__ __launch_bounds__(kBlock) void attn_fwd_kernel(
     const float* __restrict__ XL, int64_t ldXL, const float* __restrict__ XR, int64_t ldXR,
     const float* __restrict__ att, const float* __restrict__ bias, const int32_t* __restrict__ perm,
     const gasfm_work_item* __restrict__ items, int n_items, float slope, int finalize,
-    float* __restrict__ out, int64_t ldOut, float* __restrict__ seg_max, float* __restrict__ seg_sum,
-    float* __restrict__ part_acc, float* __restrict__ part_max, float* __restrict__ part_sum) {
+    float* __restrict__ out, int64_t ldOut, float* __restrict__ seg_max, float* __restrict__ seg_sum, int64_t ldStat,
+    float* __restrict__ part) {
+  constexpr int LDP = G::HC + 2 * G::H;  // packed partial row: [acc HC | max H | sum H]
   const int lane = threadIdx.x & (kWave - 1);
   const int row = lane / G::LPE;
   const int li = lane % G::LPE;
@@ -228,17 +229,18 @@ __global__ __launch_bounds__(kBlock) void attn_fwd_kernel(
         if (head_leader) {
 #pragma unroll
           for (int hh = 0; hh < G::HPL; ++hh) {
-            seg_max[int64_t(w.seg) * G::H + h0 + hh] = m[hh];
-            seg_sum[int64_t(w.seg) * G::H + h0 + hh] = s[hh];
+            seg_max[int64_t(w.seg) * ldStat + h0 + hh] = m[hh];
+            seg_sum[int64_t(w.seg) * ldStat + h0 + hh] = s[hh];
           }
         }
       } else {
-        store_vec<G::VEC>(part_acc + int64_t(w.slot) * G::HC + f0, acc);
+        float* pr = part + int64_t(w.slot) * LDP;
+        store_vec<G::VEC>(pr + f0, acc);
         if (head_leader) {
 #pragma unroll
           for (int hh = 0; hh < G::HPL; ++hh) {
-            part_max[int64_t(w.slot) * G::H + h0 + hh] = m[hh];
-            part_sum[int64_t(w.slot) * G::H + h0 + hh] = s[hh];
+            pr[G::HC + h0 + hh] = m[hh];
+            pr[G::HC + G::H + h0 + hh] = s[hh];
           }
         }
       }
@@ -252,11 +254,11 @@ __global__ __launch_bounds__(kBlock) void attn_fwd_kernel(
 // so the summation order is fixed for a given launch geometry.
 template <class G>
 __global__ __launch_bounds__(1024) void attn_combine_kernel(
-    const gasfm_combine_item* __restrict__ comb, const float* __restrict__ part_acc,
-    const float* __restrict__ part_max, const float* __restrict__ part_sum,
+    const gasfm_combine_item* __restrict__ comb, const float* __restrict__ part,
     const float* __restrict__ bias, int finalize, float* __restrict__ out, int64_t ldOut,
-    float* __restrict__ seg_max, float* __restrict__ seg_sum) {
+    float* __restrict__ seg_max, float* __restrict__ seg_sum, int64_t ldStat) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int LDP = G::HC + 2 * G::H;
   const gasfm_combine_item ci = comb[blockIdx.x];
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = threadIdx.x / kWave;
@@ -281,10 +283,10 @@ __global__ __launch_bounds__(1024) void attn_combine_kernel(
     float m2[G::HPL], s2[G::HPL], a2[G::VEC];
 #pragma unroll
     for (int hh = 0; hh < G::HPL; ++hh) {
-      m2[hh] = part_max[slot * G::H + h0 + hh];
-      s2[hh] = part_sum[slot * G::H + h0 + hh];
+      m2[hh] = part[slot * LDP + G::HC + h0 + hh];
+      s2[hh] = part[slot * LDP + G::HC + G::H + h0 + hh];
     }
-    load_vec<G::VEC>(a2, part_acc + slot * G::HC + f0);
+    load_vec<G::VEC>(a2, part + slot * LDP + f0);
     merge_state<G>(m, s, a, m2, s2, a2);
   }
   reduce_rows<G>(m, s, a);
@@ -329,8 +331,8 @@ __global__ __launch_bounds__(1024) void attn_combine_kernel(
     if ((li % G::LPH) == 0) {
 #pragma unroll
       for (int hh = 0; hh < G::HPL; ++hh) {
-        seg_max[int64_t(ci.seg) * G::H + h0 + hh] = m[hh];
-        seg_sum[int64_t(ci.seg) * G::H + h0 + hh] = s[hh];
+        seg_max[int64_t(ci.seg) * ldStat + h0 + hh] = m[hh];
+        seg_sum[int64_t(ci.seg) * ldStat + h0 + hh] = s[hh];
       }
     }
   }
@@ -502,9 +504,10 @@ __global__ __launch_bounds__(kBlock) void attn_fwd_generic(
     const float* __restrict__ XL, int64_t ldXL, const float* __restrict__ XR, int64_t ldXR,
     const float* __restrict__ att, const float* __restrict__ bias, const int32_t* __restrict__ perm,
     const gasfm_work_item* __restrict__ items, int n_items, int H, int C, float slope, int finalize,
-    float* __restrict__ out, int64_t ldOut, float* __restrict__ seg_max, float* __restrict__ seg_sum,
-    float* __restrict__ part_acc, float* __restrict__ part_max, float* __restrict__ part_sum) {
+    float* __restrict__ out, int64_t ldOut, float* __restrict__ seg_max, float* __restrict__ seg_sum, int64_t ldStat,
+    float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int LDP = H * C + 2 * H;
   const int lane = threadIdx.x & (kWave - 1);
   const int wib = threadIdx.x / kWave;
   float* lg = lds + wib * 2 * H;  // [H] logits scratch + [H] running max
@@ -545,14 +548,14 @@ __global__ __launch_bounds__(kBlock) void attn_fwd_generic(
       if (w.slot < 0) {
         out[int64_t(w.seg) * ldOut + f] = finalize ? a / (s + 1e-16f) + bias[f] : a;
         if (f % C == 0) {
-          seg_max[int64_t(w.seg) * H + h] = M;
-          seg_sum[int64_t(w.seg) * H + h] = s;
+          seg_max[int64_t(w.seg) * ldStat + h] = M;
+          seg_sum[int64_t(w.seg) * ldStat + h] = s;
         }
       } else {
-        part_acc[int64_t(w.slot) * HC + f] = a;
+        part[int64_t(w.slot) * LDP + f] = a;
         if (f % C == 0) {
-          part_max[int64_t(w.slot) * H + h] = M;
-          part_sum[int64_t(w.slot) * H + h] = s;
+          part[int64_t(w.slot) * LDP + HC + h] = M;
+          part[int64_t(w.slot) * LDP + HC + H + h] = s;
         }
       }
     }
@@ -561,10 +564,9 @@ __global__ __launch_bounds__(kBlock) void attn_fwd_generic(
 }
 
 __global__ __launch_bounds__(kBlock) void attn_combine_generic(
-    const gasfm_combine_item* __restrict__ comb, int n_comb, int H, int C, const float* __restrict__ part_acc,
-    const float* __restrict__ part_max, const float* __restrict__ part_sum, const float* __restrict__ bias,
-    int finalize, float* __restrict__ out, int64_t ldOut, float* __restrict__ seg_max,
-    float* __restrict__ seg_sum) {
+    const gasfm_combine_item* __restrict__ comb, int n_comb, int H, int C, const float* __restrict__ part,
+    const float* __restrict__ bias, int finalize, float* __restrict__ out, int64_t ldOut, float* __restrict__ seg_max,
+    float* __restrict__ seg_sum, int64_t ldStat) {
   const int wave = wave_id_uniform();
   const int lane = threadIdx.x & (kWave - 1);
   if (wave >= n_comb) return;
@@ -575,7 +577,8 @@ __global__ __launch_bounds__(kBlock) void attn_combine_generic(
     float m = -INFINITY, s = 0.f, a = 0.f;
     for (int k = 0; k < ci.slot_count; ++k) {
       const int64_t slot = int64_t(ci.slot_begin) + int64_t(k) * ci.slot_stride;
-      const float m2 = part_max[slot * H + h], s2 = part_sum[slot * H + h], a2 = part_acc[slot * HC + f];
+      const int64_t LDP = HC + 2 * H;
+      const float m2 = part[slot * LDP + HC + h], s2 = part[slot * LDP + HC + H + h], a2 = part[slot * LDP + f];
       const float mn = fmaxf(m, m2);
       const float f1 = safe_scale(m, mn), f2 = safe_scale(m2, mn);
       s = s * f1 + s2 * f2;
@@ -584,8 +587,8 @@ __global__ __launch_bounds__(kBlock) void attn_combine_generic(
     }
     out[int64_t(ci.seg) * ldOut + f] = finalize ? a / (s + 1e-16f) + bias[f] : a;
     if (f % C == 0) {
-      seg_max[int64_t(ci.seg) * H + h] = m;
-      seg_sum[int64_t(ci.seg) * H + h] = s;
+      seg_max[int64_t(ci.seg) * ldStat + h] = m;
+      seg_sum[int64_t(ci.seg) * ldStat + h] = s;
     }
   }
 }
@@ -676,57 +679,54 @@ extern "C" int gasfm_gat_attn_fwd(const float* XL, int64_t ldXL, const float* XR
                                   const float* att, const float* bias, const int32_t* perm,
                                   const gasfm_work_item* items, int32_t n_items, int32_t H, int32_t C,
                                   float slope, int32_t finalize, float* out, int64_t ldOut,
-                                  float* seg_max, float* seg_sum, float* part_acc, float* part_max,
-                                  float* part_sum, void* stream) {
+                                  float* seg_max, float* seg_sum, int64_t ldStat, float* part, void* stream) {
   GASFM_REQUIRE(H > 0 && C > 0 && n_items >= 0, "gasfm_gat_attn_fwd: H=%d C=%d n_items=%d", H, C, n_items);
   if (n_items == 0) return GASFM_OK;
-  GASFM_REQUIRE(XL && XR && att && bias && items && out && seg_max && seg_sum,
+  GASFM_REQUIRE(XL && XR && att && items && ((out && seg_max && seg_sum && bias) || part),
                 "gasfm_gat_attn_fwd: null pointer");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int grid = grid_for(n_items);
   const bool vec_ok = (H * C) % 4 == 0 && ldXL % 4 == 0 && ldXR % 4 == 0 && ldOut % 4 == 0 &&
                       aligned16(XL) && aligned16(XR) && aligned16(out) && aligned16(att) &&
-                      aligned16(bias) && (!part_acc || aligned16(part_acc));
+                      aligned16(bias) && (!part || aligned16(part)) && ((H * C + 2 * H) % 4 == 0);
   bool done = false;
   if (vec_ok) {
     done = dispatch_shape(H, C, [&](auto g) {
       using G = decltype(g);
       hipLaunchKernelGGL((attn_fwd_kernel<G>), dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att,
-                         bias, perm, items, n_items, slope, finalize, out, ldOut, seg_max, seg_sum, part_acc,
-                         part_max, part_sum);
+                         bias, perm, items, n_items, slope, finalize, out, ldOut, seg_max, seg_sum, ldStat, part);
     });
   }
   if (!done) {
     hipLaunchKernelGGL(attn_fwd_generic, dim3(grid), dim3(kBlock), (kBlock / kWave) * 2 * H * sizeof(float), st,
                        XL, ldXL, XR, ldXR, att, bias, perm, items, n_items, H, C, slope, finalize, out, ldOut,
-                       seg_max, seg_sum, part_acc, part_max, part_sum);
+                       seg_max, seg_sum, ldStat, part);
   }
   return launch_status("gasfm_gat_attn_fwd");
 }
 
 extern "C" int gasfm_gat_attn_combine(const gasfm_combine_item* combine, int32_t n_combine, int32_t H,
-                                      int32_t C, const float* part_acc, const float* part_max,
-                                      const float* part_sum, const float* bias, int32_t finalize, float* out,
-                                      int64_t ldOut, float* seg_max, float* seg_sum, void* stream) {
+                                      int32_t C, const float* part, const float* bias, int32_t finalize, float* out,
+                                      int64_t ldOut, float* seg_max, float* seg_sum, int64_t ldStat, void* stream) {
   GASFM_REQUIRE(H > 0 && C > 0 && n_combine >= 0, "gasfm_gat_attn_combine: bad args");
   if (n_combine == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const bool vec_ok = (H * C) % 4 == 0 && ldOut % 4 == 0 && aligned16(out) && aligned16(part_acc) &&
-                      aligned16(bias);
+  const bool vec_ok = (H * C) % 4 == 0 && ldOut % 4 == 0 && aligned16(out) && aligned16(part) &&
+                      aligned16(bias) && ((H * C + 2 * H) % 4 == 0);
   bool done = false;
   if (vec_ok) {
     done = dispatch_shape(H, C, [&](auto g) {
       using G = decltype(g);
       const int threads = 1024;
       const size_t lds = size_t(threads / kWave) * G::LPE * (G::VEC + 2 * G::HPL) * sizeof(float);
-      hipLaunchKernelGGL((attn_combine_kernel<G>), dim3(n_combine), dim3(threads), lds, st, combine, part_acc,
-                         part_max, part_sum, bias, finalize, out, ldOut, seg_max, seg_sum);
+      hipLaunchKernelGGL((attn_combine_kernel<G>), dim3(n_combine), dim3(threads), lds, st, combine, part, bias,
+                         finalize, out, ldOut, seg_max, seg_sum, ldStat);
     });
   }
   if (!done) {
     const int grid = (n_combine + (kBlock / kWave) - 1) / (kBlock / kWave);
-    hipLaunchKernelGGL(attn_combine_generic, dim3(grid), dim3(kBlock), 0, st, combine, n_combine, H, C, part_acc,
-                       part_max, part_sum, bias, finalize, out, ldOut, seg_max, seg_sum);
+    hipLaunchKernelGGL(attn_combine_generic, dim3(grid), dim3(kBlock), 0, st, combine, n_combine, H, C, part, bias,
+                       finalize, out, ldOut, seg_max, seg_sum, ldStat);
   }
   return launch_status("gasfm_gat_attn_combine");
 }

@@ -1,0 +1,223 @@
+"""Point-sharded multi-GPU GASFM: one process per GPU, RCCL (torch.distributed "nccl") over xGMI.
+
+The reference runs one scene on one device (main.py:77-78); this module splits a
+scene's 3D points into contiguous ranges balanced by edge count:
+
+  local       every edge of a rank's points, the point-direction attention, all
+              point MLPs, the per-edge block body (LN, projection update,
+              residual), the point head.
+  replicated  camera (view) and global node computations and the view head:
+              identical on every rank, from identical inputs.
+  exchange    the camera-direction attention and the points->global attention
+              produce per-rank partial softmax states (max, sum, acc) for their
+              destinations; ONE all-gather of the packed partial rows
+              (m x (HC + 2H) floats) per half-layer, then every rank merges
+              the W partials in rank order with gasfm_gat_attn_combine, so all
+              ranks hold bitwise-identical camera / global aggregates.
+Backward: a replicated tensor consumed by local computation (camera XR, Sv, Sg,
+global XR) receives a partial gradient from each rank -> ``AllReduceGrad`` sums
+it (one all-reduce, m x 32 floats) before the replicated backward continues, so
+replicated parameters get identical full gradients without any collective.
+Parameters used by local computation get partial gradients, summed by one
+bucketed all-reduce in ``sync_grads`` (~1.3 MB for 12 blocks).  No DDP
+all-reduce of the 145 M replicated parameters.
+
+Loss convention: each rank's loss must contain the replicated outputs'
+(Ps_norm) term in full and its own points' (pts3D[:, point_slice]) term.
+"""
+import copy
+import fnmatch
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _native
+from .attention import AttnPlan, attn_backward_raw, attn_forward_partial, combine_partials
+from .scene import MIN_N_POINTS_PER_VIEW, MIN_N_VIEWS_PER_POINT, SceneData, build_graph_wrappers
+
+# parameters whose gradient comes from rank-local computation (edges / points); everything
+# else is computed identically on all ranks from all-reduced boundary gradients
+LOCAL_PARAM_PATTERNS = (
+    "embed.*",
+    "equivariant_blocks.*.prev_projfeat_norm_layer.*",
+    "*proj2scenepoint.*",
+    "*proj2view.graph_conv.lin_l.*",
+    "*proj2view.graph_conv.att",
+    "*graph_conv_scenepoint2global.lin_l.*",
+    "*graph_conv_scenepoint2global.att",
+    "*projection_feature_update.lin_proj.*",
+    "*projection_feature_update.scenepoint_norm_layer.*",
+    "*projection_feature_update.lin_scenepoint.*",
+    "*residual_skipconn_proj_norm_layer.*",
+    "*skip_projection.*",
+    "scenepoint_head.*",
+    "depth_head.*",
+)
+
+
+def is_local_param(name):
+    return any(fnmatch.fnmatchcase(name, p) for p in LOCAL_PARAM_PATTERNS)
+
+
+class ShardContext:
+    def __init__(self, rank, world, group=None):
+        self.rank, self.world, self.group = rank, world, group
+        self._combine_cache = {}
+
+    def combine_items(self, N, device):
+        key = (N, str(device))
+        if key not in self._combine_cache:
+            s = torch.arange(N, dtype=torch.int32)
+            items = torch.stack([s, s, torch.full_like(s, self.world), torch.full_like(s, N)], 1)
+            self._combine_cache[key] = items.contiguous().to(device)
+        return self._combine_cache[key]
+
+    # collectives: RCCL for GPU tensors on the nccl backend; gloo stages through the host
+    def _staged(self, t):
+        return dist.get_backend(self.group) == "gloo" and t.is_cuda
+
+    def all_gather(self, t):
+        t = t.contiguous()
+        if self._staged(t):
+            parts = [torch.empty_like(t, device="cpu") for _ in range(self.world)]
+            dist.all_gather(parts, t.cpu(), group=self.group)
+            return torch.cat(parts, 0).to(t.device)
+        out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t, group=self.group)
+        return out
+
+    def all_reduce_(self, t):
+        if self._staged(t):
+            c = t.cpu()
+            dist.all_reduce(c, group=self.group)
+            t.copy_(c)
+        else:
+            dist.all_reduce(t, group=self.group)
+        return t
+
+
+class AllReduceGrad(torch.autograd.Function):
+    """Identity forward; sums the gradient over ranks (replicated -> local boundary)."""
+
+    @staticmethod
+    def forward(ctx, x, shard):
+        ctx.shard = shard
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ctx.shard.all_reduce_(g.contiguous().clone()), None
+
+
+def replicated_to_local(x, shard):
+    return x if shard is None else AllReduceGrad.apply(x, shard)
+
+
+class ShardedAttentionFn(torch.autograd.Function):
+    """GATv2 attention whose destinations are replicated but whose edges are sharded.
+
+    forward: local partial -> all-gather -> ordered combine (identical on all ranks)
+    backward: local edges against the global max/sum/out -> dXL (local), dXR and datt
+              (partial: summed by AllReduceGrad / sync_grads), dbias (already full).
+    """
+
+    @staticmethod
+    def forward(ctx, XL, XR, att, bias, plan, plan_partial, heads, slope, shard):
+        part = attn_forward_partial(XL, XR, att, plan_partial, heads, slope)
+        gathered = shard.all_gather(part)
+        N = plan.num_targets
+        out, smax, ssum = combine_partials(gathered, shard.world, N, heads, bias, shard.combine_items(N, XL.device))
+        ctx.plan, ctx.heads, ctx.slope = plan, heads, slope
+        ctx.save_for_backward(XL, XR, att, bias, out, smax, ssum)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        XL, XR, att, bias, out, smax, ssum = ctx.saved_tensors
+        dXL, dXR, datt, dbias = attn_backward_raw(XL, XR, att, bias, ctx.plan, ctx.heads, ctx.slope, out, smax,
+                                                  ssum, g)
+        return dXL, dXR, datt.view_as(att), dbias, None, None, None, None, None
+
+
+def partition_points(pt, n, world):
+    """Contiguous point ranges with ~equal edge counts: returns boundaries [world+1]."""
+    counts = np.bincount(np.asarray(pt), minlength=n)
+    csum = np.concatenate([[0], np.cumsum(counts)])
+    E = csum[-1]
+    bounds = [0]
+    for r in range(1, world):
+        bounds.append(int(np.searchsorted(csum, E * r / world, side="left")))
+    bounds.append(n)
+    return np.maximum.accumulate(np.asarray(bounds))
+
+
+def shard_scene(scene, rank, world, max_piece=None):
+    """Rank-local SceneData of a synthetic (or any cam-major) scene.
+
+    scene: object with m, n, cam, pt (cam-major sorted) and normalized_values().
+    """
+    cam = np.asarray(scene.cam)
+    pt = np.asarray(scene.pt)
+    m, n = scene.m, scene.n
+    bounds = partition_points(pt, n, world)
+    p0, p1 = int(bounds[rank]), int(bounds[rank + 1])
+    sel = (pt >= p0) & (pt < p1)
+    vals = scene.normalized_values()[sel]
+    lcam, lpt = cam[sel], pt[sel] - p0
+    data = SceneData.from_sparse(lcam, lpt, vals, m, p1 - p0, scene_name=f"shard{rank}", max_piece=max_piece)
+    gw = data.graph_wrappers
+    # view validity is a GLOBAL property (>= 8 points over all ranks): replicated view2global plan
+    pts_per_cam = np.bincount(cam, minlength=m)
+    vv = torch.from_numpy(np.nonzero(pts_per_cam >= MIN_N_POINTS_PER_VIEW)[0].astype(np.int64))
+    gw["view2global"].valid_indices = torch.stack([vv, torch.zeros_like(vv)])
+    gw["view2global"].plan = AttnPlan.from_targets(torch.zeros_like(vv), 1, src=vv, src_rows=m, max_piece=8)
+    gw["view2global"].plan.tag = "view2global"
+    # partial (exchange) plans for the camera direction and the points -> global graph
+    kw = {} if max_piece is None else {"max_piece": max_piece}
+    data.partial_plans = {
+        "proj2view": AttnPlan.from_targets(lcam, m, all_partial=True, **kw),
+        "scenepoint2global": AttnPlan.from_targets(
+            torch.zeros(gw["scenepoint2global"].plan.num_edges, dtype=torch.int64), 1,
+            src=gw["scenepoint2global"].valid_indices[1], src_rows=p1 - p0, all_partial=True,
+            max_piece=gw["scenepoint2global"].plan.max_piece),
+    }
+    for k, p in data.partial_plans.items():
+        p.tag = k + "_partial"
+    data.point_slice = slice(p0, p1)
+    data.n_global = n
+    data.shard = ShardContext(rank, world)
+    return data
+
+
+class ShardedGraphAttnSfMNet(torch.nn.Module):
+    """Wraps a GraphAttnSfMNet for point-sharded execution on this rank.
+
+    forward(data) with data from ``shard_scene``: returns Ps_norm (replicated, all
+    cameras) and pts3D for this rank's points only.  Call ``sync_grads()`` after
+    backward (sums the gradients of rank-local parameters over the ranks).
+    """
+
+    def __init__(self, net, group=None):
+        super().__init__()
+        self.net = net
+        self.group = group
+        self.local_names = [k for k, _ in net.named_parameters() if is_local_param(k)]
+
+    def forward(self, data):
+        shard = data.shard
+        shard.group = self.group
+        return self.net.forward(data, shard=shard, partial_plans=data.partial_plans)
+
+    def sync_grads(self):
+        params = dict(self.net.named_parameters())
+        grads = [params[k].grad for k in self.local_names if params[k].grad is not None]
+        if not grads or dist.get_world_size(self.group) == 1:
+            return
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        shard = ShardContext(dist.get_rank(self.group), dist.get_world_size(self.group), self.group)
+        shard.all_reduce_(flat)
+        off = 0
+        for g in grads:
+            g.copy_(flat[off:off + g.numel()].view_as(g))
+            off += g.numel()

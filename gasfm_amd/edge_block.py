@@ -18,7 +18,7 @@ torch and runs on MFMA through hipBLASLt.
 import torch
 
 from . import _native
-from .attention import attn_backward_raw, attn_forward_raw
+from .attention import attn_backward_raw, attn_forward_partial, attn_forward_raw, combine_partials
 
 PROJ_SCALE = 0.25  # the "/ 4" of layers.py:945
 
@@ -67,11 +67,19 @@ class DualAttentionFn(torch.autograd.Function):
     """Point- and camera-direction GATv2 attention over the two halves of XL [E, 64]."""
 
     @staticmethod
-    def forward(ctx, XL, XR_pt, XR_cam, att_pt, att_cam, bias_pt, bias_cam, plan_pt, plan_cam, heads, slope):
+    def forward(ctx, XL, XR_pt, XR_cam, att_pt, att_cam, bias_pt, bias_cam, plan_pt, plan_cam, heads, slope,
+                plan_cam_partial=None, shard=None):
         h = XL.shape[1] // 2
         XLp, XLc = XL[:, :h], XL[:, h:]
         out_p, mp, sp = attn_forward_raw(XLp, XR_pt, att_pt, bias_pt, plan_pt, heads, slope)
-        out_c, mc, sc = attn_forward_raw(XLc, XR_cam, att_cam, bias_cam, plan_cam, heads, slope)
+        if shard is None:
+            out_c, mc, sc = attn_forward_raw(XLc, XR_cam, att_cam, bias_cam, plan_cam, heads, slope)
+        else:  # camera segments span ranks: local partials -> all-gather -> ordered combine
+            part = attn_forward_partial(XLc, XR_cam, att_cam, plan_cam_partial, heads, slope)
+            gathered = shard.all_gather(part)
+            N = plan_cam.num_targets
+            out_c, mc, sc = combine_partials(gathered, shard.world, N, heads, bias_cam,
+                                             shard.combine_items(N, XL.device))
         ctx.plans = (plan_pt, plan_cam)
         ctx.heads, ctx.slope = heads, slope
         ctx.set_materialize_grads(False)
@@ -92,7 +100,8 @@ class DualAttentionFn(torch.autograd.Function):
                                                 out_p, mp, sp, g_p, dXL=dXL[:, :h])
         _, dXRc, dattc, dbc = attn_backward_raw(XL[:, h:], XR_cam, att_cam, bias_cam, plan_cam, ctx.heads, ctx.slope,
                                                 out_c, mc, sc, g_c, dXL=dXL[:, h:])
-        return (dXL, dXRp, dXRc, dattp.view_as(att_pt), dattc.view_as(att_cam), dbp, dbc, None, None, None, None)
+        return (dXL, dXRp, dXRc, dattp.view_as(att_pt), dattc.view_as(att_cam), dbp, dbc, None, None, None, None,
+                None, None)
 
 
 class EdgeEpilogueFn(torch.autograd.Function):

@@ -19,6 +19,8 @@ reference's concatenate-then-PyG sequence:
 Dense per-node projections (view 1024 / global 2048 widths) run on MFMA through
 torch (hipBLASLt).
 """
+import copy
+
 import torch
 import torch.nn.functional as F
 from torch.nn import Identity, LayerNorm, Linear, Module, ModuleList, ReLU, Sequential
@@ -27,6 +29,25 @@ from . import dense, edge_ops
 from .attention import AttnPlan
 from .edge_block import DualAttentionFn, EdgeEpilogueFn, EdgePrologueFn
 from .gatv2 import GATv2Conv
+
+
+def replicated_to_local(x, shard):
+    if shard is None:
+        return x
+    from .distributed import AllReduceGrad
+    return AllReduceGrad.apply(x, shard)
+
+
+class _LazySharded:
+    """ShardedAttentionFn, imported on first use (keeps torch.distributed out of the 1-GPU import path)."""
+
+    @staticmethod
+    def apply(*args):
+        from .distributed import ShardedAttentionFn as F_
+        return F_.apply(*args)
+
+
+ShardedAttentionFn = _LazySharded
 
 GRAPH_NAMES = ("proj2view", "proj2scenepoint", "view2global", "scenepoint2global")
 
@@ -85,9 +106,15 @@ class _NodeAggregation(Module):
             self.norm_pre_mlp = LayerNorm(n_feat_out)
         self.mlp = get_linear_layers((2 + n_hidden_layers) * [n_feat_out], norm=False)
 
-    def forward_plan(self, proj_feats, plan, prev):
+    def forward_plan(self, proj_feats, plan, prev, plan_partial=None, shard=None):
         """proj_feats [E, F_in] (edge order) -> node features [N, n_feat_out]."""
         assert self.stateful == (prev is not None)
+        if shard is not None and plan_partial is not None:
+            XR = replicated_to_local(self.target_rows(prev, plan.num_targets), shard)
+            XL = dense.linear(proj_feats, self.graph_conv.lin_l)
+            c = self.graph_conv
+            x = ShardedAttentionFn.apply(XL, XR, c.att, c.bias, plan, plan_partial, c.heads, c.negative_slope, shard)
+            return self.tail(x, prev)
         x_agg = dense.sequential(getattr(self, self._state_key), prev) if prev is not None else None
         return self.tail(self.graph_conv.attend(proj_feats, x_agg, plan), prev)
 
@@ -157,12 +184,23 @@ class ViewAndScenePoint2Global(Module):
             self.norm_pre_mlp = LayerNorm(n_feat_global_out)
         self.mlp = get_linear_layers((2 + n_hidden_layers_global_update) * [n_feat_global_out], norm=False)
 
-    def forward_plan(self, view, pts, plan_v2g, plan_s2g, prev):
+    def forward_plan(self, view, pts, plan_v2g, plan_s2g, prev, plan_s2g_partial=None, shard=None):
         assert self.stateful == (prev is not None)
         xv = dense.sequential(self.norm_and_proj_global2view, prev) if prev is not None else None
         xp = dense.sequential(self.norm_and_proj_global2scenepoint, prev) if prev is not None else None
         v2g = self.graph_conv_view2global.attend(view, xv, plan_v2g)
-        s2g = self.graph_conv_scenepoint2global.attend(pts, xp, plan_s2g)
+        c = self.graph_conv_scenepoint2global
+        if shard is None:
+            s2g = c.attend(pts, xp, plan_s2g)
+        else:  # points are sharded, the global target is replicated
+            if xp is None:
+                zero = torch.zeros((1, c.in_channels), device=pts.device)
+                XR = c.lin_r(zero).expand(1, -1)
+            else:
+                XR = dense.linear(xp, c.lin_r)
+            XR = replicated_to_local(XR, shard)
+            s2g = ShardedAttentionFn.apply(dense.linear(pts, c.lin_l), XR, c.att, c.bias, plan_s2g,
+                                           plan_s2g_partial, c.heads, c.negative_slope, shard)
         x = torch.cat([v2g, s2g], dim=1)
         if hasattr(self, "proj_view_and_scenepoint2global"):
             x = self.proj_view_and_scenepoint2global(x)
@@ -263,25 +301,29 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         """Node side of the update given XL = [lin_l_point(P_hat) | lin_l_camera(P_hat)] [E, 64]."""
         sp, sv = self.proj2scenepoint, self.proj2view
         pp, pc = plans["proj2scenepoint"], plans["proj2view"]
+        shard = plans.get("_shard")
         XRp = sp.target_rows(prev_pt, pp.num_targets)
-        XRc = sv.target_rows(prev_view, pc.num_targets)
+        XRc = replicated_to_local(sv.target_rows(prev_view, pc.num_targets), shard)
         cp, cc = sp.graph_conv, sv.graph_conv
         agg_p, agg_c = DualAttentionFn.apply(XL, XRp, XRc, cp.att, cc.att, cp.bias, cc.bias, pp, pc, cp.heads,
-                                             cp.negative_slope)
+                                             cp.negative_slope, plans.get("_partial", {}).get("proj2view"), shard)
         pts = sp.tail(agg_p, prev_pt)
         view = sv.tail(agg_c, prev_view)
         return self._finish(pts, view, plans, prev_glob)
 
     def forward_plan(self, P_hat, plans, prev_pt=None, prev_view=None, prev_glob=None):
+        shard = plans.get("_shard")
         pts = self.proj2scenepoint.forward_plan(P_hat, plans["proj2scenepoint"], prev_pt)
-        view = self.proj2view.forward_plan(P_hat, plans["proj2view"], prev_view)
+        view = self.proj2view.forward_plan(P_hat, plans["proj2view"], prev_view,
+                                           plans.get("_partial", {}).get("proj2view"), shard)
         return self._finish(pts, view, plans, prev_glob)
 
     def _finish(self, pts, view, plans, prev_glob):
         glob = None
         if self.output_global or self.global2view_and_global2scenepoint_enabled:
-            glob = self.view_and_scenepoint2global.forward_plan(view, pts, plans["view2global"],
-                                                                plans["scenepoint2global"], prev_glob)
+            glob = self.view_and_scenepoint2global.forward_plan(
+                view, pts, plans["view2global"], plans["scenepoint2global"], prev_glob,
+                plans.get("_partial", {}).get("scenepoint2global"), plans.get("_shard"))
         if self.global2view_and_global2scenepoint_enabled:
             pts = self.global2scenepoint(glob, pts)
             view = self.global2view(glob, view)
@@ -373,6 +415,8 @@ class GraphAttnSfMLayer(Module):
         XL, token = EdgePrologueFn.apply(P, ln.weight, ln.bias, W, b, pfu.lin_proj.weight, ln.eps)
         pts, view, glob = gfu.forward_fused(XL, plans, prev_pt, prev_view, prev_glob)
         sp, sv, sg = pfu.node_terms(pts, view, glob)
+        shard = plans.get("_shard")
+        sv, sg = replicated_to_local(sv, shard), replicated_to_local(sg, shard)
         P_new = EdgeEpilogueFn.apply(P, P0 if self.add_skipconn_from_init_projfeat else None, token, sp, sv, sg,
                                      pfu.lin_proj.weight, pfu.lin_proj.bias, ln.weight, ln.bias, ln.eps, edges)
         return P_new, pts, view, glob
@@ -389,6 +433,8 @@ class GraphAttnSfMLayer(Module):
         pfu = self.projection_feature_update
         x_cat = torch.cat([P_hat, P0], dim=1) if self.add_skipconn_from_init_projfeat else P_hat
         sp, sv, sg = pfu.node_terms(pts, view, glob)
+        shard = plans.get("_shard")
+        sv, sg = replicated_to_local(sv, shard), replicated_to_local(sg, shard)
         delta = edge_ops.projection_update(x_cat, pfu.lin_proj, sp, sv, sg, edges)
         if pfu.n_hidden_layers_proj_update > 0:
             delta = pfu.mlp(F.relu(delta))
@@ -574,10 +620,13 @@ class GraphAttnSfMNet(Module):
                 pts, view, _ = fgu.forward_plan(P, plans, *args)
         return P, pts, view
 
-    def forward(self, data):
+    def forward(self, data, shard=None, partial_plans=None):
         values = data.x.values
         device = values.device
         edges = self.edge_index_for(data, device)
+        if shard is not None:
+            edges = copy.copy(edges)
+            edges.plans = dict(edges.plans, _shard=shard, _partial=partial_plans)
         P, pts, view = self.forward_features(values, edges)
         pred = {}
         if self.depth_head_enabled:

@@ -86,11 +86,13 @@ int gasfm_plan_work(const int32_t* seg_ptr, int32_t N, int32_t max_piece,
  * called at layers.py:329-335 etc.):
  *   e_j[h]   = sum_c att[h,c] * leaky_relu(XL[src_j,h,c] + XR[seg,h,c], slope)
  *   out[seg] = sum_j softmax_j(e)[h] * XL[src_j,h,:] + bias      (finalize)
- * src_j = perm[j] if perm != NULL else j.  Complete items write
+ * src_j = perm[j] if perm != NULL else j.  Complete items (slot < 0) write
  * out[seg] (finalized if finalize != 0, otherwise the raw acc) plus
- * seg_max[seg,h], seg_sum[seg,h] (sum of exp(e - max), no epsilon).  Split
- * items write raw partials to part_{acc,max,sum}[slot].  Segments with no
- * edges give out = bias, max = -inf, sum = 0. */
+ * seg_max[seg*ldStat + h], seg_sum[seg*ldStat + h] (sum of exp(e - max), no
+ * epsilon).  Items with slot >= 0 write a raw partial into the PACKED partial
+ * row part[slot*(HC+2H) ..] = [acc (HC) | max (H) | sum (H)] — the unit one
+ * rank contributes to the multi-GPU all-gather.  Segments with no edges give
+ * out = bias, max = -inf, sum = 0. */
 int gasfm_gat_attn_fwd(const float* XL, int64_t ldXL,
                        const float* XR, int64_t ldXR,
                        const float* att, const float* bias,
@@ -98,20 +100,18 @@ int gasfm_gat_attn_fwd(const float* XL, int64_t ldXL,
                        const gasfm_work_item* items, int32_t n_items,
                        int32_t H, int32_t C, float negative_slope,
                        int32_t finalize,
-                       float* out, int64_t ldOut, float* seg_max, float* seg_sum,
-                       float* part_acc, float* part_max, float* part_sum,
-                       void* stream);
+                       float* out, int64_t ldOut, float* seg_max, float* seg_sum, int64_t ldStat,
+                       float* part, void* stream);
 
-/* Ordered merge of partials (split pieces, or one partial per rank after an
- * all-gather).  Writes out/seg_max/seg_sum at index seg (finalized with bias
- * when finalize != 0, else raw partial form). */
+/* Ordered merge of packed partial rows (split pieces, or one row per rank
+ * after an all-gather).  Writes out/seg_max/seg_sum at index seg: finalized
+ * with bias when finalize != 0, else raw (pass out = a packed partial buffer,
+ * ldOut = ldStat = HC+2H, seg_max = out+HC, seg_sum = out+HC+H). */
 int gasfm_gat_attn_combine(const gasfm_combine_item* combine, int32_t n_combine,
-                           int32_t H, int32_t C,
-                           const float* part_acc, const float* part_max,
-                           const float* part_sum,
+                           int32_t H, int32_t C, const float* part,
                            const float* bias, int32_t finalize,
                            float* out, int64_t ldOut, float* seg_max, float* seg_sum,
-                           void* stream);
+                           int64_t ldStat, void* stream);
 
 /* Backward of the above given dOut (gout), the forward's finalized out and
  * per-segment stats.  Writes dXL[src_j] for every edge (each row exactly
