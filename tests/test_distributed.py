@@ -149,8 +149,10 @@ def _worker_sharded_model(rank, world, port, q):
         loss = (pred["Ps_norm"] * cP).sum() + (pred["pts3D"] * cX[:, data.point_slice]).sum()
         loss.backward()
         model.sync_grads()
-        grads = {k: p.grad.detach().cpu() for k, p in net.named_parameters()}
-        q.put((rank, pred["Ps_norm"].detach().cpu(), pred["pts3D"].detach().cpu(), data.point_slice, grads))
+        # numpy (pickled by value): tensors would travel as shared-memory fds owned by this process
+        grads = {k: p.grad.detach().cpu().numpy() for k, p in net.named_parameters()}
+        q.put((rank, pred["Ps_norm"].detach().cpu().numpy(), pred["pts3D"].detach().cpu().numpy(),
+               (data.point_slice.start, data.point_slice.stop), grads))
     finally:
         dist.destroy_process_group()
 
@@ -182,12 +184,13 @@ def test_sharded_model_matches_single_gpu(device):
         p.join(timeout=120)
         assert p.exitcode == 0
     res.sort(key=lambda t: t[0])
-    for rank, ps, pts, sl, grads in res:
-        np.testing.assert_allclose(ps.numpy(), pred["Ps_norm"].detach().cpu().numpy(), atol=1e-5, rtol=1e-4)
-        np.testing.assert_allclose(pts.numpy(), pred["pts3D"][:, sl].detach().cpu().numpy(), atol=1e-5, rtol=1e-4)
+    for rank, ps, pts, (a, b), grads in res:
+        np.testing.assert_allclose(ps, pred["Ps_norm"].detach().cpu().numpy(), atol=1e-5, rtol=1e-4)
+        np.testing.assert_allclose(pts, pred["pts3D"][:, a:b].detach().cpu().numpy(), atol=1e-5, rtol=1e-4)
         for k, r in ref_grads.items():
-            d = float((grads[k] - r).norm())
-            assert d <= 1e-3 * float(r.norm()) + 1e-6, f"rank {rank} {k}: {d:.3e} vs {float(r.norm()):.3e}"
-    # replicated parameters end bitwise identical on both ranks
+            r = r.numpy()
+            d = float(np.linalg.norm(grads[k] - r))
+            assert d <= 1e-3 * float(np.linalg.norm(r)) + 1e-6, f"rank {rank} {k}: {d:.3e} vs {np.linalg.norm(r):.3e}"
+    # every parameter gradient ends bitwise identical on both ranks (replicated optimizer steps stay in sync)
     for k in ref_grads:
-        assert torch.equal(res[0][4][k], res[1][4][k]), k
+        assert np.array_equal(res[0][4][k], res[1][4][k]), k
