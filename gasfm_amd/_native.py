@@ -44,6 +44,13 @@ _SIGS = {
                                        _vp]),
     "gasfm_segment_rowsum": (_i32, [_vp, _i32, _vp, _vp, _i64, _f32, _vp, _vp, _vp]),
     "gasfm_colsum": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _vp]),
+    "gasfm_edge0_part_rows": (_i32, [_i32, _i64, _i32]),
+    "gasfm_edge0_prologue_fwd": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
+    "gasfm_edge0_epilogue_fwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp,
+                                        _vp, _vp, _f32, _vp, _vp]),
+    "gasfm_edge0_epilogue_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _f32, _vp, _vp,
+                                        _vp, _vp, _vp]),
+    "gasfm_edge0_prologue_bwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
 }
 
 _lib = None
@@ -217,3 +224,41 @@ def segment_rowsum(items, n_items, perm, X, scale, out, part):
     st = lib().gasfm_segment_rowsum(_p(items), n_items, _p(perm), _p(X), X.stride(0), scale, _p(out), _p(part),
                                     _stream(X))
     check(st, "gasfm_segment_rowsum")
+
+
+# ---------------------------------------------------------------- block 0 (2-wide) edge kernels
+def edge0_part_rows(which, E, n_items=0):
+    return lib().gasfm_edge0_part_rows(which, E, n_items)
+
+
+def edge0_prologue_fwd(P, ln_w, ln_b, eps, W0, b0, XL):
+    _req(P, "P", 2)
+    st = lib().gasfm_edge0_prologue_fwd(_p(P), P.shape[0], _p(ln_w), _p(ln_b), eps, _p(W0), _p(b0), _p(XL),
+                                        _stream(P))
+    check(st, "gasfm_edge0_prologue_fwd")
+
+
+def edge0_epilogue_fwd(P, cam, pt, lna_w, lna_b, lnb_w, lnb_b, eps, Wp, bp, Wsk, bsk, Sp, Sv, Sg, scale, out):
+    _req(P, "P", 2)
+    for t, n in ((Sp, "Sp"), (Sv, "Sv"), (Sg, "Sg")):
+        _req(t, n)
+    st = lib().gasfm_edge0_epilogue_fwd(_p(P), _p(cam), _p(pt), P.shape[0], _p(lna_w), _p(lna_b), _p(lnb_w),
+                                        _p(lnb_b), eps, _p(Wp), _p(bp), _p(Wsk), _p(bsk), _p(Sp), _p(Sv), _p(Sg),
+                                        scale, _p(out), _stream(P))
+    check(st, "gasfm_edge0_epilogue_fwd")
+
+
+def edge0_epilogue_bwd(items, n_items, dPo, P, lna_w, lna_b, lnb_w, lnb_b, eps, Wp, Wsk, scale, dSv, part_dsv, aux,
+                       part):
+    _req(dPo, "dP'", 32)
+    st = lib().gasfm_edge0_epilogue_bwd(_p(items), n_items, _p(dPo), _p(P), _p(lna_w), _p(lna_b), _p(lnb_w),
+                                        _p(lnb_b), eps, _p(Wp), _p(Wsk), scale, _p(dSv), _p(part_dsv), _p(aux),
+                                        _p(part), _stream(dPo))
+    check(st, "gasfm_edge0_epilogue_bwd")
+
+
+def edge0_prologue_bwd(dXL, P, aux, ln_w, ln_b, eps, W0, dP, part):
+    _req(dXL, "dXL0", 8)
+    st = lib().gasfm_edge0_prologue_bwd(_p(dXL), _p(P), _p(aux), P.shape[0], _p(ln_w), _p(ln_b), eps, _p(W0),
+                                        _p(dP), _p(part), _stream(P))
+    check(st, "gasfm_edge0_prologue_bwd")

@@ -28,8 +28,13 @@ __global__ __launch_bounds__(kColBlock) void colsum_pass1(const float* __restric
   extern __shared__ __attribute__((aligned(16))) float sh[];
   const int nb = gridDim.x;
   const int64_t r0 = rows * blockIdx.x / nb, r1 = rows * (blockIdx.x + 1) / nb;
-  const int C4 = cols / 4;
-  if ((cols & 3) == 0 && (ld & 3) == 0 && C4 <= kColBlock && (reinterpret_cast<uintptr_t>(A) & 15) == 0) {
+  // blockIdx.y selects a chunk of up to 4*256 columns (wide partial matrices)
+  const int cbase = blockIdx.y * 4 * kColBlock;
+  A += cbase;
+  ws += cbase;
+  const int ccols = (cols - cbase) < 4 * kColBlock ? (cols - cbase) : 4 * kColBlock;
+  const int C4 = ccols / 4;
+  if ((cols & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0) {
     const int RL = kColBlock / C4;
     const int c4 = threadIdx.x % C4, rl = threadIdx.x / C4;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -69,7 +74,7 @@ __global__ __launch_bounds__(kColBlock) void colsum_pass1(const float* __restric
       reinterpret_cast<float4*>(ws + int64_t(blockIdx.x) * cols)[threadIdx.x] = t;
     }
   } else {
-    for (int c = threadIdx.x; c < cols; c += kColBlock) {
+    for (int c = threadIdx.x; c < ccols; c += kColBlock) {
       float acc = 0.f;
       for (int64_t r = r0; r < r1; ++r) acc += A[r * ld + c];
       ws[int64_t(blockIdx.x) * cols + c] = acc;
@@ -108,8 +113,9 @@ extern "C" int gasfm_colsum(const float* A, int64_t rows, int32_t cols, int64_t 
   GASFM_REQUIRE(ws && out && (rows == 0 || A), "gasfm_colsum: null pointer");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int nb = colsum_blocks(rows);
-  hipLaunchKernelGGL(colsum_pass1, dim3(nb), dim3(kColBlock), 4 * kColBlock * sizeof(float), st, A, rows, cols, ld,
-                     ws);
+  const int nchunk = (cols + 4 * kColBlock - 1) / (4 * kColBlock);
+  hipLaunchKernelGGL(colsum_pass1, dim3(nb, nchunk), dim3(kColBlock), 4 * kColBlock * sizeof(float), st, A, rows,
+                     cols, ld, ws);
   int rc = launch_status("gasfm_colsum/pass1");
   if (rc) return rc;
   const int g2 = (cols + 63) / 64;

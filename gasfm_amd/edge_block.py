@@ -144,3 +144,71 @@ class EdgeEpilogueFn(torch.autograd.Function):
         if pp.n_combine:
             _native.attn_bwd_combine(pp.combine, pp.n_combine, 32, part_dsp, dSp)
         return (None, dP0, dPo, dSp, dSv, dSg.view(ctx.sg_shape), dWp, dSg.clone(), None, None, None, None)
+
+
+class Block0PrologueFn(torch.autograd.Function):
+    """Block 0: XL0 = [Wl_pt; Wl_cam] relu(LN_a(P)) + b for 2-wide P (layers.py:232-234, 329, 426)."""
+
+    @staticmethod
+    def forward(ctx, P, ln_w, ln_b, W0, b0, eps):
+        E = P.shape[0]
+        XL = torch.empty((E, 8), dtype=torch.float32, device=P.device)
+        _native.edge0_prologue_fwd(P, ln_w, ln_b, eps, W0.contiguous(), b0.contiguous(), XL)
+        ctx.eps = eps
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(P, ln_w, ln_b, W0)
+        return XL, P.new_zeros((1, 1)).expand(E, 4)
+
+    @staticmethod
+    def backward(ctx, dXL, daux):
+        P, ln_w, ln_b, W0 = ctx.saved_tensors
+        E = P.shape[0]
+        dXL = torch.zeros((E, 8), dtype=torch.float32, device=P.device) if dXL is None else dXL.contiguous()
+        aux = daux.contiguous() if daux is not None and daux.stride(0) != 0 else None
+        dP = torch.empty_like(P)
+        rows = _native.edge0_part_rows(0, E)
+        part = torch.empty((rows, 28), dtype=torch.float32, device=P.device)
+        _native.edge0_prologue_bwd(dXL, P, aux, ln_w, ln_b, ctx.eps, W0.contiguous(), dP, part)
+        tot = _native.colsum(part)
+        return dP, tot[24:26], tot[26:28], tot[:16].view(8, 2), tot[16:24], None
+
+
+class Block0EpilogueFn(torch.autograd.Function):
+    """Block 0: P' = Wsk relu(LN_b(P)) + bsk + (Wp relu(LN_a(P)) + bp + Sp[pt] + Sv[cam] + Sg) / 4."""
+
+    @staticmethod
+    def forward(ctx, P, token, Sp, Sv, Sg, Wp, bp, lna_w, lna_b, lnb_w, lnb_b, Wsk, bsk, eps, edges):
+        out = torch.empty((P.shape[0], Wp.shape[0]), dtype=torch.float32, device=P.device)
+        _native.edge0_epilogue_fwd(P, edges.cam, edges.pt, lna_w, lna_b, lnb_w, lnb_b, eps, Wp.contiguous(),
+                                   bp.contiguous(), Wsk.contiguous(), bsk.contiguous(), Sp.contiguous(),
+                                   Sv.contiguous(), Sg.reshape(-1).contiguous(), PROJ_SCALE, out)
+        ctx.eps, ctx.edges, ctx.sg_shape = eps, edges, Sg.shape
+        ctx.save_for_backward(P, lna_w, lna_b, lnb_w, lnb_b, Wp, Wsk)
+        return out
+
+    @staticmethod
+    def backward(ctx, dPo):
+        P, lna_w, lna_b, lnb_w, lnb_b, Wp, Wsk = ctx.saved_tensors
+        edges = ctx.edges
+        dPo = dPo.contiguous()
+        dev = P.device
+        E = P.shape[0]
+        pc, pp = edges.plans["proj2view"], edges.plans["proj2scenepoint"]
+        dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
+        part_dsv = torch.empty((max(pc.n_slots, 1), 32), dtype=torch.float32, device=dev)
+        aux = torch.empty((E, 4), dtype=torch.float32, device=dev)
+        rows = _native.edge0_part_rows(1, E, pc.n_items)
+        part = torch.empty((rows, 164), dtype=torch.float32, device=dev)
+        _native.edge0_epilogue_bwd(pc.items, pc.n_items, dPo, P, lna_w, lna_b, lnb_w, lnb_b, ctx.eps,
+                                   Wp.contiguous(), Wsk.contiguous(), PROJ_SCALE, dSv, part_dsv, aux, part)
+        if pc.n_combine:
+            _native.attn_bwd_combine(pc.combine, pc.n_combine, 32, part_dsv, dSv)
+        tot = _native.colsum(part)
+        dSg = _native.colsum(dSv)
+        dSp = torch.empty((edges.n, 32), dtype=torch.float32, device=dev)
+        part_dsp = torch.empty((max(pp.n_slots, 1), 32), dtype=torch.float32, device=dev)
+        _native.segment_rowsum(pp.items, pp.n_items, pp.perm, dPo, PROJ_SCALE, dSp, part_dsp)
+        if pp.n_combine:
+            _native.attn_bwd_combine(pp.combine, pp.n_combine, 32, part_dsp, dSp)
+        return (None, aux, dSp, dSv, dSg.view(ctx.sg_shape), tot[:64].view(32, 2), dSg.clone(), None, None,
+                tot[160:162], tot[162:164], tot[64:128].view(32, 2), tot[128:160], None, None)

@@ -27,7 +27,7 @@ from torch.nn import Identity, LayerNorm, Linear, Module, ModuleList, ReLU, Sequ
 
 from . import dense, edge_ops
 from .attention import AttnPlan
-from .edge_block import DualAttentionFn, EdgeEpilogueFn, EdgePrologueFn
+from .edge_block import Block0EpilogueFn, Block0PrologueFn, DualAttentionFn, EdgeEpilogueFn, EdgePrologueFn
 from .gatv2 import GATv2Conv
 
 
@@ -293,6 +293,15 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
             ok &= c.bias is not None
         return bool(ok)
 
+    def fusable0(self):
+        """Block-0 shape: 2-wide inputs, H*C = 4 per direction (every GASFM conf)."""
+        ok = True
+        for m in (self.proj2scenepoint, self.proj2view):
+            c = m.graph_conv
+            ok &= c.in_channels == 2 and c.heads * c.out_channels == 4 and c.lin_l.bias is not None
+            ok &= c.bias is not None
+        return bool(ok)
+
     def lin_l_stack(self):
         a, b = self.proj2scenepoint.graph_conv.lin_l, self.proj2view.graph_conv.lin_l
         return torch.cat([a.weight, b.weight], 0), torch.cat([a.bias, b.bias], 0)
@@ -406,6 +415,32 @@ class GraphAttnSfMLayer(Module):
                 and self.prev_projfeat_norm_layer.normalized_shape == (32,)
                 and self.global_feature_update.fusable())
 
+    def fusable0(self):
+        pfu = self.projection_feature_update
+        w = pfu.lin_proj.weight
+        return (self.use_norm_proj_update and self.add_residual_skipconn_proj_update
+                and self.skip_projection is not None and not self.add_skipconn_from_init_projfeat
+                and pfu.n_hidden_layers_proj_update == 0 and pfu.normalize_global_features
+                and tuple(w.shape) == (32, 2) and tuple(self.skip_projection.lin_proj.weight.shape) == (32, 2)
+                and self.prev_projfeat_norm_layer.normalized_shape == (2,)
+                and self.global_feature_update.fusable0())
+
+    def forward_fused0(self, P, plans, edges):
+        """Block 0 (2-wide inputs, projected residual) with the block-0 HIP edge kernels."""
+        la, lb = self.prev_projfeat_norm_layer, self.residual_skipconn_proj_norm_layer
+        gfu = self.global_feature_update
+        pfu = self.projection_feature_update
+        W, b = gfu.lin_l_stack()
+        XL, token = Block0PrologueFn.apply(P.contiguous(), la.weight, la.bias, W, b, la.eps)
+        pts, view, glob = gfu.forward_fused(XL, plans, None, None, None)
+        sp, sv, sg = pfu.node_terms(pts, view, glob)
+        shard = plans.get("_shard")
+        sv, sg = replicated_to_local(sv, shard), replicated_to_local(sg, shard)
+        sk = self.skip_projection.lin_proj
+        P_new = Block0EpilogueFn.apply(P.contiguous(), token, sp, sv, sg, pfu.lin_proj.weight, pfu.lin_proj.bias,
+                                       la.weight, la.bias, lb.weight, lb.bias, sk.weight, sk.bias, la.eps, edges)
+        return P_new, pts, view, glob
+
     def forward_fused(self, P, plans, edges, prev_pt, prev_view, prev_glob, P0):
         """Blocks >= 1 with the fused HIP edge kernels (see gasfm_amd/edge_block.py)."""
         ln = self.prev_projfeat_norm_layer
@@ -425,6 +460,8 @@ class GraphAttnSfMLayer(Module):
         """P [E, F_in] edge features (cam-major) -> (P' [E, F_out], pts, view, glob)."""
         if P.is_cuda and self.fusable():
             return self.forward_fused(P, plans, edges, prev_pt, prev_view, prev_glob, P0)
+        if P.is_cuda and prev_pt is None and prev_view is None and prev_glob is None and self.fusable0():
+            return self.forward_fused0(P, plans, edges)
         if self.use_norm_proj_update:
             P_hat = edge_ops.layer_norm_relu(P, self.prev_projfeat_norm_layer)
         else:
@@ -601,7 +638,8 @@ class GraphAttnSfMNet(Module):
     def forward_features(self, values, edges):
         """Block stack + final update on raw tensors; returns (P, pts, view) after the final update."""
         plans = edges.plans
-        P = self.embed(values)
+        lin = self.embed.post_embed_lin
+        P = dense.linear(values, lin) if lin is not None else self.embed(values)
         P0 = P if self.add_skipconn_from_init_projfeat else None
         pts = view = glob = None
         sf = self.stateful_global_features

@@ -188,6 +188,36 @@ int gasfm_segment_rowsum(const gasfm_work_item* items, int32_t n_items, const in
                          const float* X, int64_t ldX, float scale, float* out, float* part,
                          void* stream);
 
+/* ---- block 0 per-edge body (2-wide embedded projections; layers.py:148-263 with F_in = 2) ---- */
+
+/* Partial rows per workgroup: which = 0 -> edge0_prologue_bwd ([dW0 16 | db0 8 | dgamma_a 2 |
+ * dbeta_a 2]), 1 -> edge0_epilogue_bwd ([dWp 64 | dWsk 64 | dbsk 32 | dgamma_b 2 | dbeta_b 2]). */
+int gasfm_edge0_part_rows(int32_t which, int64_t E, int32_t n_items);
+
+/* XL0[e] (8 floats) = W0 relu(LN_a(P[e])) + b0, W0 = [Wl_point; Wl_camera] [8 x 2]. */
+int gasfm_edge0_prologue_fwd(const float* P, int64_t E, const float* ln_w, const float* ln_b, float eps,
+                             const float* W0, const float* b0, float* XL, void* stream);
+
+/* P'[e] = Wsk relu(LN_b(P[e])) + bsk + scale*(Wp relu(LN_a(P[e])) + bp + Sp[pt] + Sv[cam] + Sg). */
+int gasfm_edge0_epilogue_fwd(const float* P, const int32_t* cam, const int32_t* pt, int64_t E,
+                             const float* ln_a_w, const float* ln_a_b, const float* ln_b_w,
+                             const float* ln_b_b, float eps, const float* Wp, const float* bp,
+                             const float* Wsk, const float* bsk, const float* Sp, const float* Sv,
+                             const float* Sg, float scale, float* Pout, void* stream);
+
+/* Camera work items: dSv (+ partial slots), aux[e] = (dP_hat_a (2), dP from the skip branch (2)),
+ * per-workgroup partials of dWp, dWsk, dbsk, dgamma_b, dbeta_b. */
+int gasfm_edge0_epilogue_bwd(const gasfm_work_item* items, int32_t n_items, const float* dPo,
+                             const float* P, const float* ln_a_w, const float* ln_a_b,
+                             const float* ln_b_w, const float* ln_b_b, float eps, const float* Wp,
+                             const float* Wsk, float scale, float* dSv, float* part_dsv, float* aux,
+                             float* part, void* stream);
+
+/* dP = LN_a_bwd(mask (W0^T dXL0 + aux.xy)) + aux.zw and partials of dW0, db0, dgamma_a, dbeta_a. */
+int gasfm_edge0_prologue_bwd(const float* dXL, const float* P, const float* aux, int64_t E,
+                             const float* ln_w, const float* ln_b, float eps, const float* W0, float* dP,
+                             float* part, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

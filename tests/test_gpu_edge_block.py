@@ -108,3 +108,39 @@ def test_segment_rowsum_matches_index_add(device):
         _native.attn_bwd_combine(plan.combine, plan.n_combine, 32, part, out)
     ref = torch.zeros(n, 32, dtype=torch.float64).index_add(0, dst, X.double().cpu()) * 0.25
     np.testing.assert_allclose(out.cpu().numpy(), ref.numpy(), atol=1e-5, rtol=1e-4)
+
+
+def test_block0_edge_body_fwd_bwd(device):
+    """Block 0: 2-wide LN, lin_l 2->4 per direction, projected residual (layers.py:214-220, 256-261)."""
+    from gasfm_amd.edge_block import Block0EpilogueFn, Block0PrologueFn
+    from gasfm_amd.model import EdgeIndex
+    sc, data = _graph(30, 2000, 5, seed=9)
+    data = data.to(device)
+    E, m, n = sc.num_edges, sc.m, sc.n
+    plans = {k: w.plan for k, w in data.graph_wrappers.items()}
+    idx = data.x.indices
+    edges = EdgeIndex(idx[0].int().contiguous(), idx[1].int().contiguous(), m, n, plans)
+    g = torch.Generator().manual_seed(3)
+    r = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64)
+    leaves = dict(P=r(E, 2), law=1 + 0.1 * r(2), lab=0.1 * r(2), lbw=1 + 0.1 * r(2), lbb=0.1 * r(2),
+                  W0=r(8, 2), b0=0.1 * r(8), Wp=r(32, 2), bp=0.1 * r(32), Wsk=r(32, 2), bsk=0.1 * r(32),
+                  Sp=r(n, 32), Sv=r(m, 32), Sg=r(1, 32))
+    G1, G2 = r(E, 8), r(E, 32)
+    ref = {k: v.clone().requires_grad_(True) for k, v in leaves.items()}
+    cam, pt = idx[0].cpu(), idx[1].cpu()
+    Pa = F.relu(F.layer_norm(ref["P"], (2,), ref["law"], ref["lab"], 1e-5))
+    Pb = F.relu(F.layer_norm(ref["P"], (2,), ref["lbw"], ref["lbb"], 1e-5))
+    XL_ref = Pa @ ref["W0"].T + ref["b0"]
+    Pn_ref = Pb @ ref["Wsk"].T + ref["bsk"] + (Pa @ ref["Wp"].T + ref["bp"] + ref["Sp"][pt] + ref["Sv"][cam]
+                                                + ref["Sg"]) / 4
+    ((XL_ref * G1).sum() + (Pn_ref * G2).sum()).backward()
+    dev = {k: v.float().to(device).requires_grad_(True) for k, v in leaves.items()}
+    XL, tok = Block0PrologueFn.apply(dev["P"], dev["law"], dev["lab"], dev["W0"], dev["b0"], 1e-5)
+    Pn = Block0EpilogueFn.apply(dev["P"], tok, dev["Sp"], dev["Sv"], dev["Sg"], dev["Wp"], dev["bp"], dev["law"],
+                                dev["lab"], dev["lbw"], dev["lbb"], dev["Wsk"], dev["bsk"], 1e-5, edges)
+    ((XL * G1.float().to(device)).sum() + (Pn * G2.float().to(device)).sum()).backward()
+    np.testing.assert_allclose(XL.detach().cpu().numpy(), XL_ref.detach().numpy(), atol=1e-5, rtol=1e-4)
+    np.testing.assert_allclose(Pn.detach().cpu().numpy(), Pn_ref.detach().numpy(), atol=1e-5, rtol=1e-4)
+    np.testing.assert_allclose(dev["P"].grad.cpu().numpy(), ref["P"].grad.numpy(), atol=1e-4, rtol=1e-4)
+    for k in ("law", "lab", "lbw", "lbb", "W0", "b0", "Wp", "bp", "Wsk", "bsk", "Sp", "Sv", "Sg"):
+        normwise(dev[k].grad, ref[k].grad, msg=k)
