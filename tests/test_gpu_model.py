@@ -12,26 +12,13 @@ import pytest
 import torch
 
 import gasfm_amd
-from conftest import golden
+from conftest import check_grad, golden
 from oracle import gasfm_ref, scenes
 from oracle.weights import deterministic_state_dict
 
 pytestmark = pytest.mark.gpu
 
 OUT_ATOL, OUT_RTOL = 1e-4, 1e-3
-
-
-def check_grad(got, ref, name, ref32=None):
-    """Normwise 1e-3 relative; where the fp32 oracle itself is worse than that (cancellation in
-    tiny gradients, e.g. the view->global att), within 10x of the fp32 oracle's own error."""
-    got = got.detach().double().cpu().numpy()
-    ref = np.asarray(ref, dtype=np.float64)
-    nr = np.linalg.norm(ref)
-    bound = 1e-3 * nr + 1e-9
-    if ref32 is not None:
-        bound = max(bound, 10 * np.linalg.norm(np.asarray(ref32, dtype=np.float64) - ref))
-    err = np.linalg.norm(got - ref)
-    assert err <= bound, f"{name}: normwise {err:.3e} vs |ref| {nr:.3e} (bound {bound:.3e})"
 
 
 def scene_from_fixture(device):
