@@ -139,8 +139,29 @@ def test_block0_edge_body_fwd_bwd(device):
     Pn = Block0EpilogueFn.apply(dev["P"], tok, dev["Sp"], dev["Sv"], dev["Sg"], dev["Wp"], dev["bp"], dev["law"],
                                 dev["lab"], dev["lbw"], dev["lbb"], dev["Wsk"], dev["bsk"], 1e-5, edges)
     ((XL * G1.float().to(device)).sum() + (Pn * G2.float().to(device)).sum()).backward()
-    np.testing.assert_allclose(XL.detach().cpu().numpy(), XL_ref.detach().numpy(), atol=1e-5, rtol=1e-4)
-    np.testing.assert_allclose(Pn.detach().cpu().numpy(), Pn_ref.detach().numpy(), atol=1e-5, rtol=1e-4)
-    np.testing.assert_allclose(dev["P"].grad.cpu().numpy(), ref["P"].grad.numpy(), atol=1e-4, rtol=1e-4)
+    # A 2-wide LayerNorm is ill-conditioned where x0 ~ x1 (rstd -> 1/sqrt(eps)): fp32 rounding of
+    # x0 - x1 is amplified ~300x there, in the reference's fp32 path as much as here.  Elementwise
+    # bound: the fp32 torch evaluation's own error (x4) on top of 1e-5 + 1e-4|ref|.
+    r32 = {k: v.float().requires_grad_(True) for k, v in leaves.items()}
+    Pa32 = F.relu(F.layer_norm(r32["P"], (2,), r32["law"], r32["lab"], 1e-5))
+    Pb32 = F.relu(F.layer_norm(r32["P"], (2,), r32["lbw"], r32["lbb"], 1e-5))
+    XL32 = Pa32 @ r32["W0"].T + r32["b0"]
+    Pn32 = Pb32 @ r32["Wsk"].T + r32["bsk"] + (Pa32 @ r32["Wp"].T + r32["bp"] + r32["Sp"][pt] + r32["Sv"][cam]
+                                               + r32["Sg"]) / 4
+    ((XL32 * G1.float()).sum() + (Pn32 * G2.float()).sum()).backward()
+
+    def close32(got, r64, r32_, atol=1e-5):
+        got, r64, r32_ = (np.asarray(t.detach().double().cpu()) for t in (got, r64, r32_))
+        bound = atol + 1e-4 * np.abs(r64) + 4 * np.abs(r32_ - r64)
+        assert np.all(np.abs(got - r64) <= bound), float(np.max(np.abs(got - r64) - bound))
+
+    close32(XL, XL_ref, XL32)
+    close32(Pn, Pn_ref, Pn32)
+    # dP: normwise (rows with x0 ~ x1 have rstd ~ 1/sqrt(eps) and large, equally-amplified errors)
+    e_got = float((dev["P"].grad.double().cpu() - ref["P"].grad).norm())
+    e_32 = float((r32["P"].grad.double() - ref["P"].grad).norm())
+    assert e_got <= 4 * e_32 + 1e-5 * float(ref["P"].grad.norm()), (e_got, e_32)
     for k in ("law", "lab", "lbw", "lbb", "W0", "b0", "Wp", "bp", "Wsk", "bsk", "Sp", "Sv", "Sg"):
-        normwise(dev[k].grad, ref[k].grad, msg=k)
+        err32 = float((r32[k].grad.double() - ref[k].grad).norm())
+        got = float((dev[k].grad.double().cpu() - ref[k].grad).norm())
+        assert got <= max(1e-5 * float(ref[k].grad.norm()) + 1e-6, 4 * err32), (k, got, err32)
