@@ -14,16 +14,19 @@
 //   edge_prologue_bwd   dP = LN_bwd(mask * (Wl^T dXL + Wp^T dP'/4)) + dP', dWl, dbl, dgamma, dbeta
 // plus segment_rowsum (dSp = per-point sum of dP'/4 through the point permutation).
 //
-// Layout: every kernel works on 32-edge tiles held by ONE wavefront.  The
-// tile is staged row-major in the wave's private LDS slice (row stride 33 /
-// 65 floats: conflict-free for both the "row per lane" and the "column per
-// lane" reads below), and the GEMM-shaped parts run on the f32 MFMA
-// v_mfma_f32_32x32x2_f32 (exact fp32, K split as lane halves h = lane>>5):
-//   tile x W     A[i][k] = T[i][2s+h],  B[k][n] = W(...)     -> C: col = lane&31,
-//                                                               row = (r&3)+8(r>>2)+4h
-//   T1^T x T2    A[m][k] = T1[2s+h][m], B[k][n] = T2[2s+h][n]  (reduction over edges)
-// Weight-gradient partials are reduced across the workgroup's waves in LDS
-// and written once per workgroup; gasfm_colsum finishes them (deterministic).
+// Layout: each wavefront owns 16-edge tiles.  A tile is staged row-major in the
+// wave's LDS slice (row strides 34 / 66 floats: the "row per lane" reads of the
+// MFMA A operand hit 32 distinct banks), the workgroup's weights are staged once
+// in LDS with row stride 48 (the two k-rows one B read touches fall 16 banks
+// apart), and the GEMM-shaped parts run on the exact-fp32 MFMA
+// v_mfma_f32_16x16x4_f32 (lane l: A[i = l&15][k = l>>4], B[k = l>>4][j = l&15],
+// C: col = l&15, row = 4(l>>4) + r):
+//   tile x W     A[i][k] = T[i][4s+g]                      -> per-edge outputs
+//   T1^T x T2    A[m][k] = T1[4s+g][m], B[k][n] = T2[4s+g][n] -> reduction over edges
+// Per-row reductions (LayerNorm backward) stay in registers: a row's 32 columns
+// live on 16 lanes x 2 column tiles and are summed with 4 xor-shuffles.
+// Weight-gradient partials are reduced over the workgroup's waves in LDS and
+// written once per workgroup; gasfm_colsum finishes them (deterministic).
 #include <hip/hip_runtime.h>
 
 #include "common.hpp"
@@ -31,57 +34,71 @@
 namespace gasfm {
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kW = 64;           // wave
 constexpr int kWaves = 4;        // waves per workgroup
 constexpr int kThreads = kW * kWaves;
 constexpr int F = 32;            // projection feature width (n_feat_proj)
 constexpr int NX = 64;           // XL width: 32 (point conv) + 32 (camera conv)
-constexpr int LD33 = F + 1;
-constexpr int LD65 = NX + 1;
-constexpr int kMaxGrid = 1024;   // workgroups (x4 waves) for the grid-stride kernels
+constexpr int TR = 16;           // edges per tile
+constexpr int LD34 = 34;         // LDS row stride of 32-wide tiles
+constexpr int LD66 = 66;         // LDS row stride of 64-wide tiles
+constexpr int LDW = 48;          // LDS row stride of staged weights (<= 32 columns)
+constexpr int LDW64 = 80;        // LDS row stride of staged 64-column weights
+constexpr int kMaxGrid = 2048;   // workgroups for the grid-stride kernels
 
-__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
-__device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
-__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
-__device__ __forceinline__ f32x16 zero16() {
-  f32x16 z;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) z[r] = 0.f;
-  return z;
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// Sum over the 16 lanes of a lane group (same l>>4): xor 1,2,4,8.
+__device__ __forceinline__ float sum16(float v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 8);
+  return v;
+}
+// Sum over the 4 lane groups (l>>4): xor 16, 32.
+__device__ __forceinline__ float sum_groups(float v) {
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
 }
 
-// Load a 32 x 32 fp32 tile (rows row0.., stride 32 in global) and, per row,
-// LayerNorm + ReLU it.  Writes x_hat (normalised, pre-affine) to Xh and the
-// activated relu(x_hat*g + b) to Ph (either may be null), raw values to Raw,
-// and rstd per row to Rs.  Rows >= nrows are zero (x_hat = 0).
-// Row r of the tile is held by the 8 lanes 8k..8k+7 (k = r%8) in step u = r/8.
+// Load a 16 x 32 tile of P (rows row0.., global stride 32): the 8 lanes 8k..8k+7 hold row
+// k + 8u (u = 0, 1).  Per row LayerNorm statistics by 3 xor-shuffles.  Writes x_hat
+// (pre-affine; identity when !LN) to Xh, relu(x_hat*g+b) (x when !LN) to Ph, raw values
+// to Raw (each optional, stride 34) and rstd to Rs.  Rows >= nrows are zeros.
 template <bool LN>
 __device__ __forceinline__ void load_norm_tile(const float* __restrict__ P, int64_t row0, int nrows,
                                                const float* __restrict__ gam, const float* __restrict__ bet,
                                                float eps, float* Xh, float* Ph, float* Raw, float* Rs, int lane) {
   const int c = (lane & 7) * 4;
   float4 g4 = make_float4(1.f, 1.f, 1.f, 1.f), b4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (LN) {
+  if (LN && Ph) {
     g4 = *reinterpret_cast<const float4*>(gam + c);
     b4 = *reinterpret_cast<const float4*>(bet + c);
   }
-  float4 v[4];
+  float4 v[2];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < 2; ++u) {
     const int r = (lane >> 3) + 8 * u;
     v[u] = (r < nrows) ? *reinterpret_cast<const float4*>(P + (row0 + r) * F + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < 2; ++u) {
     const int r = (lane >> 3) + 8 * u;
-    float x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+    const float x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
     if (Raw) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) Raw[r * LD33 + c + k] = x[k];
+      for (int k = 0; k < 4; ++k) Raw[r * LD34 + c + k] = x[k];
     }
     float mean = 0.f, rstd = 1.f;
     if (LN) {
@@ -102,34 +119,39 @@ __device__ __forceinline__ void load_norm_tile(const float* __restrict__ P, int6
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float xh = LN ? (x[k] - mean) * rstd : x[k];
-      if (Xh) Xh[r * LD33 + c + k] = (r < nrows) ? xh : 0.f;
-      if (Ph) Ph[r * LD33 + c + k] = (r < nrows) ? (LN ? fmaxf(fmaf(xh, gg[k], bb[k]), 0.f) : xh) : 0.f;
+      if (Xh) Xh[r * LD34 + c + k] = (r < nrows) ? xh : 0.f;
+      if (Ph) Ph[r * LD34 + c + k] = (r < nrows) ? (LN ? fmaxf(fmaf(xh, gg[k], bb[k]), 0.f) : xh) : 0.f;
     }
     if (Rs && (lane & 7) == 0) Rs[r] = rstd;
   }
 }
 
-// Row-major [32 x W] tile from global (stride ld) into LDS (stride W+1); rows >= nrows zero.
-template <int W>
+// Row-major [16 x W] tile from global (stride ld) into LDS (stride LDT); rows >= nrows zero.
+template <int W, int LDT>
 __device__ __forceinline__ void load_tile(const float* __restrict__ X, int64_t ld, int64_t row0, int nrows,
                                           float* T, int lane) {
   constexpr int V = W / 4;            // float4 per row
-  constexpr int STEPS = 32 * V / kW;  // float4 per lane
+  constexpr int STEPS = TR * V / kW;  // float4 per lane
+  float4 v[STEPS];
 #pragma unroll
   for (int u = 0; u < STEPS; ++u) {
     const int q = lane + kW * u;
     const int r = q / V, c = (q % V) * 4;
-    const float4 v = (r < nrows) ? *reinterpret_cast<const float4*>(X + (row0 + r) * ld + c)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-    float* d = T + r * (W + 1) + c;
-    d[0] = v.x;
-    d[1] = v.y;
-    d[2] = v.z;
-    d[3] = v.w;
+    v[u] = (r < nrows) ? *reinterpret_cast<const float4*>(X + (row0 + r) * ld + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int u = 0; u < STEPS; ++u) {
+    const int q = lane + kW * u;
+    const int r = q / V, c = (q % V) * 4;
+    float* d = T + r * LDT + c;
+    d[0] = v[u].x;
+    d[1] = v[u].y;
+    d[2] = v[u].z;
+    d[3] = v[u].w;
   }
 }
 
-// Sum `n` floats per lane across the workgroup's waves (LDS scratch >= kWaves*kW*n),
+// Sum `N` floats per lane across the workgroup's waves (LDS scratch >= kWaves*N*kW floats);
 // wave 0 returns the totals in v.
 template <int N>
 __device__ __forceinline__ void wg_reduce(float (&v)[N], float* scratch, int wave, int lane) {
@@ -157,37 +179,37 @@ __global__ __launch_bounds__(kThreads) void edge_prologue_fwd_kernel(const float
                                                                     const float* __restrict__ W,
                                                                     const float* __restrict__ b,
                                                                     float* __restrict__ Y, int64_t ldY) {
-  __shared__ float lds[kWaves][32 * LD33];
+  __shared__ float Wt[F * LDW64];            // W^T: Wt[k][n] = W[n][k]
+  __shared__ float tiles[kWaves][TR * LD34];
+  for (int q = threadIdx.x; q < NX * F; q += kThreads) Wt[(q % F) * LDW64 + q / F] = W[q];
+  __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
-  const int i = lane & 31, h = lane >> 5;
-  float* T = lds[wave];
-  float wB[2][16];
+  const int c = lane & 15, g = lane >> 4;
+  float* T = tiles[wave];
+  float bias[4];
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-    for (int s = 0; s < 16; ++s) wB[nt][s] = W[(nt * 32 + i) * F + 2 * s + h];
-  const float bias0 = b[i], bias1 = b[32 + i];
-  const int64_t ntiles = (E + 31) / 32;
+  for (int nt = 0; nt < 4; ++nt) bias[nt] = b[nt * 16 + c];
+  const int64_t ntiles = (E + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWaves + wave, nw = int64_t(gridDim.x) * kWaves;
   for (int64_t t = gw; t < ntiles; t += nw) {
-    const int64_t row0 = t * 32;
-    const int nrows = int(E - row0 < 32 ? E - row0 : 32);
+    const int64_t row0 = t * TR;
+    const int nrows = int(E - row0 < TR ? E - row0 : TR);
     load_norm_tile<LN>(P, row0, nrows, gam, bet, eps, nullptr, T, nullptr, nullptr, lane);
     wave_sync();
-    f32x16 acc0 = zero16(), acc1 = zero16();
+    f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const float a = T[i * LD33 + 2 * s + h];
-      acc0 = mfma(a, wB[0][s], acc0);
-      acc1 = mfma(a, wB[1][s], acc1);
+    for (int s = 0; s < F / 4; ++s) {
+      const float a = T[c * LD34 + 4 * s + g];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma16(a, Wt[(4 * s + g) * LDW64 + nt * 16 + c], acc[nt]);
     }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = crow(r, h);
-      if (row < nrows) {
-        float* y = Y + (row0 + row) * ldY;
-        y[i] = acc0[r] + bias0;
-        y[32 + i] = acc1[r] + bias1;
+    for (int r = 0; r < 4; ++r) {
+      const int e = 4 * g + r;
+      if (e < nrows) {
+        float* y = Y + (row0 + e) * ldY;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) y[nt * 16 + c] = acc[nt][r] + bias[nt];
       }
     }
     wave_sync();
@@ -195,7 +217,7 @@ __global__ __launch_bounds__(kThreads) void edge_prologue_fwd_kernel(const float
 }
 
 // =====================================================================================
-// edge_epilogue_fwd: P'[e] = P[e] + (Wp [relu(LN(P[e])) | P0[e]] + bp + Sp[pt] + Sv[cam] + Sg) / 4
+// edge_epilogue_fwd: P'[e] = P[e] + scale (Wp [relu(LN(P[e])) | P0[e]] + bp + Sp[pt] + Sv[cam] + Sg)
 // Wp: [32 x ldWp] (ldWp = 34 with the init-feature skip, 32 without: P0 == null)
 // =====================================================================================
 __global__ __launch_bounds__(kThreads) void edge_epilogue_fwd_kernel(
@@ -203,39 +225,57 @@ __global__ __launch_bounds__(kThreads) void edge_epilogue_fwd_kernel(
     const int32_t* __restrict__ pt, int64_t E, const float* __restrict__ gam, const float* __restrict__ bet,
     float eps, const float* __restrict__ Wp, int ldWp, const float* __restrict__ bp, const float* __restrict__ Sp,
     const float* __restrict__ Sv, const float* __restrict__ Sg, float scale, float* __restrict__ Pout) {
-  __shared__ float lds[kWaves][2 * 32 * LD33 + 64];
-  __shared__ int32_t idx[kWaves][64];
+  __shared__ float Wt[F * LDW];              // Wt[k][n] = Wp[n][k], k < 32
+  __shared__ float tiles[kWaves][2 * TR * LD34 + 2 * TR];
+  __shared__ int32_t idx[kWaves][2 * TR];
+  for (int q = threadIdx.x; q < F * F; q += kThreads) Wt[(q % F) * LDW + q / F] = Wp[(q / F) * ldWp + q % F];
+  __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
-  const int i = lane & 31, h = lane >> 5;
-  float* Ph = lds[wave];
-  float* Raw = Ph + 32 * LD33;
-  float* Q0 = Raw + 32 * LD33;
+  const int c = lane & 15, g = lane >> 4;
+  float* Ph = tiles[wave];
+  float* Raw = Ph + TR * LD34;
+  float* Q0 = Raw + TR * LD34;
   int32_t* ix = idx[wave];
-  float wB[16];
+  float w32[2], w33[2], cst[2];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) wB[s] = Wp[i * ldWp + 2 * s + h];
-  const float w32 = P0 ? Wp[i * ldWp + 32] : 0.f, w33 = P0 ? Wp[i * ldWp + 33] : 0.f;
-  const float cst = bp[i] + Sg[i];
-  const int64_t ntiles = (E + 31) / 32;
+  for (int nt = 0; nt < 2; ++nt) {
+    const int j = nt * 16 + c;
+    w32[nt] = P0 ? Wp[j * ldWp + 32] : 0.f;
+    w33[nt] = P0 ? Wp[j * ldWp + 33] : 0.f;
+    cst[nt] = bp[j] + Sg[j];
+  }
+  const int64_t ntiles = (E + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWaves + wave, nw = int64_t(gridDim.x) * kWaves;
   for (int64_t t = gw; t < ntiles; t += nw) {
-    const int64_t row0 = t * 32;
-    const int nrows = int(E - row0 < 32 ? E - row0 : 32);
+    const int64_t row0 = t * TR;
+    const int nrows = int(E - row0 < TR ? E - row0 : TR);
     load_norm_tile<true>(P, row0, nrows, gam, bet, eps, nullptr, Ph, Raw, nullptr, lane);
-    if (P0) Q0[lane] = (lane < 2 * nrows) ? P0[row0 * 2 + lane] : 0.f;
-    ix[lane] = (i < nrows) ? (h ? pt[row0 + i] : cam[row0 + i]) : 0;
+    if (P0 && lane < 2 * TR) Q0[lane] = (lane < 2 * nrows) ? P0[row0 * 2 + lane] : 0.f;
+    if (lane < 2 * TR) {
+      const int e = lane & 15;
+      ix[lane] = (e < nrows) ? (lane < TR ? cam[row0 + e] : pt[row0 + e]) : 0;
+    }
     wave_sync();
-    f32x16 acc = zero16();
+    f32x4 acc[2] = {zero4(), zero4()};
 #pragma unroll
-    for (int s = 0; s < 16; ++s) acc = mfma(Ph[i * LD33 + 2 * s + h], wB[s], acc);
+    for (int s = 0; s < F / 4; ++s) {
+      const float a = Ph[c * LD34 + 4 * s + g];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = crow(r, h);
-      if (row < nrows) {
-        float y = acc[r] + cst;
-        if (P0) y = fmaf(w32, Q0[2 * row], fmaf(w33, Q0[2 * row + 1], y));
-        y += Sp[int64_t(ix[32 + row]) * F + i] + Sv[int64_t(ix[row]) * F + i];
-        Pout[(row0 + row) * F + i] = fmaf(y, scale, Raw[row * LD33 + i]);
+      for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma16(a, Wt[(4 * s + g) * LDW + nt * 16 + c], acc[nt]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = 4 * g + r;
+      if (e < nrows) {
+        const int64_t vr = int64_t(ix[e]) * F, pr = int64_t(ix[TR + e]) * F;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int j = nt * 16 + c;
+          float y = acc[nt][r] + cst[nt];
+          if (P0) y = fmaf(w32[nt], Q0[2 * e], fmaf(w33[nt], Q0[2 * e + 1], y));
+          y += Sp[pr + j] + Sv[vr + j];
+          Pout[(row0 + e) * F + j] = fmaf(y, scale, Raw[e * LD34 + j]);
+        }
       }
     }
     wave_sync();
@@ -252,221 +292,256 @@ __global__ __launch_bounds__(kThreads) void edge_epilogue_bwd_kernel(
     const float* __restrict__ P, const float* __restrict__ P0, const float* __restrict__ gam,
     const float* __restrict__ bet, float eps, const float* __restrict__ Wp, int ldWp, float scale,
     float* __restrict__ dSv, float* __restrict__ part_dsv, float* __restrict__ dP0, float* __restrict__ part_w) {
-  __shared__ float lds[kWaves][2 * 32 * LD33 + 64];
-  __shared__ float red[kWaves * 18 * kW];
+  __shared__ float lds[kWaves * 20 * kW > kWaves * (2 * TR * LD34 + 2 * TR) ? kWaves * 20 * kW
+                                                                              : kWaves * (2 * TR * LD34 + 2 * TR)];
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
-  const int i = lane & 31, h = lane >> 5;
-  float* D = lds[wave];
-  float* Ph = D + 32 * LD33;
-  float* Q0 = Ph + 32 * LD33;
-  // Wp[:, 32:34] for dP0: lane (i,h) needs Wp[j][32+c] for j in its half -> registers
-  float w2[16][2];
+  const int c = lane & 15, g = lane >> 4;
+  float* D = lds + wave * (2 * TR * LD34 + 2 * TR);
+  float* Ph = D + TR * LD34;
+  float* Q0 = Ph + TR * LD34;
+  // dP0[e][c'] = sum_j d[e][j] Wp[j][32+c']: lane (e = c, group g) sums j in [8g, 8g+8)
+  float w2[8][2];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int j = 16 * h + k;
+  for (int k = 0; k < 8; ++k) {
+    const int j = 8 * g + k;
     w2[k][0] = P0 ? Wp[j * ldWp + 32] * scale : 0.f;
     w2[k][1] = P0 ? Wp[j * ldWp + 33] * scale : 0.f;
   }
-  f32x16 accW = zero16();
-  float accP0[2] = {0.f, 0.f};
+  f32x4 accW[2][2] = {{zero4(), zero4()}, {zero4(), zero4()}};
+  float accP0[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
   const int gw = blockIdx.x * kWaves + wave, nw = gridDim.x * kWaves;
   for (int it = gw; it < n_items; it += nw) {
     const gasfm_work_item w = items[it];
-    float dsv = 0.f;
-    for (int64_t row0 = w.begin; row0 < w.end; row0 += 32) {
-      const int nrows = int(w.end - row0 < 32 ? w.end - row0 : 32);
-      load_tile<F>(dPo, F, row0, nrows, D, lane);
+    float dsv[2] = {0.f, 0.f};
+    for (int64_t row0 = w.begin; row0 < w.end; row0 += TR) {
+      const int nrows = int(w.end - row0 < TR ? w.end - row0 : TR);
+      load_tile<F, LD34>(dPo, F, row0, nrows, D, lane);
       load_norm_tile<true>(P, row0, nrows, gam, bet, eps, nullptr, Ph, nullptr, nullptr, lane);
-      if (P0) Q0[lane] = (lane < 2 * nrows) ? P0[row0 * 2 + lane] : 0.f;
+      if (P0 && lane < 2 * TR) Q0[lane] = (lane < 2 * nrows) ? P0[row0 * 2 + lane] : 0.f;
       wave_sync();
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int row = 2 * s + h;
-        const float a = D[row * LD33 + i] * scale;
-        accW = mfma(a, Ph[row * LD33 + i], accW);
-        dsv += a;
-        if (P0) {
-          accP0[0] = fmaf(a, Q0[2 * row], accP0[0]);
-          accP0[1] = fmaf(a, Q0[2 * row + 1], accP0[1]);
+      for (int s = 0; s < TR / 4; ++s) {
+        const int row = 4 * s + g;
+        float a[2], bb[2];
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2) {
+          a[t2] = D[row * LD34 + t2 * 16 + c] * scale;
+          bb[t2] = Ph[row * LD34 + t2 * 16 + c];
+          dsv[t2] += a[t2];
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) accW[mt][nt] = mfma16(a[mt], bb[nt], accW[mt][nt]);
+          if (P0) {
+            accP0[mt][0] = fmaf(a[mt], Q0[2 * row], accP0[mt][0]);
+            accP0[mt][1] = fmaf(a[mt], Q0[2 * row + 1], accP0[mt][1]);
+          }
         }
       }
-      if (P0) {  // dP0[row i] = sum_j d[i][j] * Wp[j][32:34]; lane half h takes j in [16h, 16h+16)
+      if (P0) {
         float q0 = 0.f, q1 = 0.f;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const float d = D[i * LD33 + 16 * h + k];
+        for (int k = 0; k < 8; ++k) {
+          const float d = D[c * LD34 + 8 * g + k];
           q0 = fmaf(d, w2[k][0], q0);
           q1 = fmaf(d, w2[k][1], q1);
         }
-        q0 += __shfl_xor(q0, 32);
-        q1 += __shfl_xor(q1, 32);
-        if (i < nrows) dP0[(row0 + i) * 2 + h] = h ? q1 : q0;
+        q0 = sum_groups(q0);
+        q1 = sum_groups(q1);
+        if (g < 2 && c < nrows) dP0[(row0 + c) * 2 + g] = g ? q1 : q0;
       }
       wave_sync();
     }
-    dsv += __shfl_xor(dsv, 32);
-    if (h == 0) {
-      if (w.slot < 0)
-        dSv[int64_t(w.seg) * F + i] = dsv;
-      else
-        part_dsv[int64_t(w.slot) * F + i] = dsv;
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) dsv[t2] = sum_groups(dsv[t2]);
+    if (g == 0) {
+      float* dst = (w.slot < 0) ? dSv + int64_t(w.seg) * F : part_dsv + int64_t(w.slot) * F;
+      dst[c] = dsv[0];
+      dst[16 + c] = dsv[1];
     }
   }
-  // workgroup reduction of dWp: accW (C layout: row = out j = crow(r,h), col = feature i),
-  // accP0[c]: out j = i, summed over the lane halves
-  float v[18];
+  float v[20];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = accW[r];
-  v[16] = accP0[0];
-  v[17] = accP0[1];
-  wg_reduce<18>(v, red, wave, lane);
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[(mt * 2 + nt) * 4 + r] = accW[mt][nt][r];
+  v[16] = accP0[0][0];
+  v[17] = accP0[0][1];
+  v[18] = accP0[1][0];
+  v[19] = accP0[1][1];
+  wg_reduce<20>(v, lds, wave, lane);
   if (wave == 0) {
     float* out = part_w + int64_t(blockIdx.x) * 32 * ldWp;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) out[crow(r, h) * ldWp + i] = v[r];
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[(mt * 16 + 4 * g + r) * ldWp + nt * 16 + c] = v[(mt * 2 + nt) * 4 + r];
     if (P0) {
-      const float p0 = v[16] + __shfl_xor(v[16], 32), p1 = v[17] + __shfl_xor(v[17], 32);
-      if (h == 0) {
-        out[i * ldWp + 32] = p0;
-        out[i * ldWp + 33] = p1;
+      float p[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) p[k] = sum_groups(v[16 + k]);
+      if (g == 0) {
+        out[c * ldWp + 32] = p[0];
+        out[c * ldWp + 33] = p[1];
+        out[(16 + c) * ldWp + 32] = p[2];
+        out[(16 + c) * ldWp + 33] = p[3];
       }
     }
   }
 }
 
 // =====================================================================================
-// edge_prologue_bwd: dP = LN_bwd(mask * (W^T dXL + Wp[:, :32]^T dRes*scale)) + dRes
+// edge_prologue_bwd: dP = LN_bwd(mask * (W^T dXL + scale Wp[:, :32]^T dRes)) + dRes
 // part layout per workgroup: [64*32 dW][64 db][32 dgamma][32 dbeta]
 // =====================================================================================
+constexpr int PB_WAVE = TR * LD66 + 2 * TR * LD34 + TR;  // dXL, x_hat, dRes tiles + rstd
+constexpr int PB_W = NX * LDW + F * LDW;                  // W [64 x 32], scale*Wp [32 x 32]
 template <bool LN, bool RES>
 __global__ __launch_bounds__(kThreads) void edge_prologue_bwd_kernel(
     const float* __restrict__ dXL, int64_t ldX, const float* __restrict__ P, const float* __restrict__ dRes,
     int64_t E, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
     const float* __restrict__ W, const float* __restrict__ Wp, int ldWp, float scale, float* __restrict__ dP,
     float* __restrict__ part) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int PER_WAVE = 32 * LD65 + 2 * 32 * LD33 + 96;
+  __shared__ float lds[PB_W + kWaves * PB_WAVE];
+  float* Wl = lds;                  // B[k][j] = W[k][j]     (k < 64)
+  float* Wq = lds + NX * LDW;       // B[k][j] = scale Wp[k][j] (k < 32)
+  for (int q = threadIdx.x; q < NX * F; q += kThreads) Wl[(q / F) * LDW + q % F] = W[q];
+  if (RES)
+    for (int q = threadIdx.x; q < F * F; q += kThreads) Wq[(q / F) * LDW + q % F] = scale * Wp[(q / F) * ldWp + q % F];
+  __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
-  const int i = lane & 31, h = lane >> 5;
-  float* T1 = lds + wave * PER_WAVE;  // dXL tile   32 x 65
-  float* T2 = T1 + 32 * LD65;         // x_hat      32 x 33
-  float* T3 = T2 + 32 * LD33;         // dRes, then G = dy*gamma
-  float* Rs = T3 + 32 * LD33;         // rstd[32], S1[32], S2[32]
-  float wB1[32], wB2[16];
+  const int c = lane & 15, g = lane >> 4;
+  float* T1 = lds + PB_W + wave * PB_WAVE;  // dXL     16 x 66
+  float* T2 = T1 + TR * LD66;               // x_hat   16 x 34
+  float* T3 = T2 + TR * LD34;               // dRes    16 x 34
+  float* Rs = T3 + TR * LD34;               // rstd    16
+  float gi[2], bi[2];
 #pragma unroll
-  for (int s = 0; s < 32; ++s) wB1[s] = W[(2 * s + h) * F + i];  // B[k][j] = W[k][j]
+  for (int nt = 0; nt < 2; ++nt) {
+    gi[nt] = LN ? gam[nt * 16 + c] : 1.f;
+    bi[nt] = LN ? bet[nt * 16 + c] : 0.f;
+  }
+  f32x4 accW[4][2];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) wB2[s] = RES ? Wp[(2 * s + h) * ldWp + i] * scale : 0.f;
-  const float gi = LN ? gam[i] : 1.f, bi = LN ? bet[i] : 0.f;
-  f32x16 accW0 = zero16(), accW1 = zero16();
-  float db0 = 0.f, db1 = 0.f, dg = 0.f, dbt = 0.f;
-  const int64_t ntiles = (E + 31) / 32;
+  for (int mt = 0; mt < 4; ++mt) accW[mt][0] = accW[mt][1] = zero4();
+  float db[4] = {0.f, 0.f, 0.f, 0.f}, dg[2] = {0.f, 0.f}, dbt[2] = {0.f, 0.f};
+  const int64_t ntiles = (E + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWaves + wave, nw = int64_t(gridDim.x) * kWaves;
   for (int64_t t = gw; t < ntiles; t += nw) {
-    const int64_t row0 = t * 32;
-    const int nrows = int(E - row0 < 32 ? E - row0 : 32);
-    load_tile<NX>(dXL, ldX, row0, nrows, T1, lane);
+    const int64_t row0 = t * TR;
+    const int nrows = int(E - row0 < TR ? E - row0 : TR);
+    load_tile<NX, LD66>(dXL, ldX, row0, nrows, T1, lane);
     load_norm_tile<LN>(P, row0, nrows, gam, bet, eps, T2, nullptr, nullptr, Rs, lane);
-    if (RES) load_tile<F>(dRes, F, row0, nrows, T3, lane);
+    if (RES) load_tile<F, LD34>(dRes, F, row0, nrows, T3, lane);
     wave_sync();
-    // dP_hat (C layout) = dXL W  (+ dRes Wp scale)
-    f32x16 acc = zero16();
+    // dP_hat (C layout: edge 4g+r, column nt*16+c) = dXL W (+ dRes scale Wp)
+    f32x4 acc[2] = {zero4(), zero4()};
 #pragma unroll
-    for (int s = 0; s < 32; ++s) acc = mfma(T1[i * LD65 + 2 * s + h], wB1[s], acc);
+    for (int s = 0; s < NX / 4; ++s) {
+      const float a = T1[c * LD66 + 4 * s + g];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma16(a, Wl[(4 * s + g) * LDW + nt * 16 + c], acc[nt]);
+    }
     if (RES) {
 #pragma unroll
-      for (int s = 0; s < 16; ++s) acc = mfma(T3[i * LD33 + 2 * s + h], wB2[s], acc);
-    }
-    // dW += dXL^T P_hat ; db += colsum(dXL)
+      for (int s = 0; s < F / 4; ++s) {
+        const float a = T3[c * LD34 + 4 * s + g];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int row = 2 * s + h;
-      const float xh = T2[row * LD33 + i];
-      const float ph = LN ? fmaxf(fmaf(xh, gi, bi), 0.f) : xh;
-      const float a0 = T1[row * LD65 + i], a1 = T1[row * LD65 + 32 + i];
-      accW0 = mfma(a0, ph, accW0);
-      accW1 = mfma(a1, ph, accW1);
-      db0 += a0;
-      db1 += a1;
-    }
-    float res[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = crow(r, h);
-      res[r] = RES ? T3[row * LD33 + i] : 0.f;
-    }
-    if (LN) {
-      wave_sync();
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = crow(r, h);
-        const float xh = T2[row * LD33 + i];
-        const float dy = (fmaf(xh, gi, bi) > 0.f) ? acc[r] : 0.f;
-        dg = fmaf(dy, xh, dg);
-        dbt += dy;
-        T3[row * LD33 + i] = dy * gi;
+        for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma16(a, Wq[(4 * s + g) * LDW + nt * 16 + c], acc[nt]);
       }
-      wave_sync();
-      {  // row sums: lane (i, h) takes columns [16h, 16h+16) of row i
-        float s1 = 0.f, s2 = 0.f;
+    }
+    // dW += dXL^T P_hat ; db += column sums of dXL
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const float g = T3[i * LD33 + 16 * h + k];
-          s1 += g;
-          s2 = fmaf(g, T2[i * LD33 + 16 * h + k], s2);
-        }
-        s1 += __shfl_xor(s1, 32);
-        s2 += __shfl_xor(s2, 32);
-        if (h == 0) {
-          Rs[32 + i] = s1 * (1.f / F);
-          Rs[64 + i] = s2 * (1.f / F);
-        }
+    for (int s = 0; s < TR / 4; ++s) {
+      const int row = 4 * s + g;
+      float ph[2];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const float xh = T2[row * LD34 + nt * 16 + c];
+        ph[nt] = LN ? fmaxf(fmaf(xh, gi[nt], bi[nt]), 0.f) : xh;
       }
-      wave_sync();
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = crow(r, h);
-        if (row < nrows) {
-          const float g = T3[row * LD33 + i], xh = T2[row * LD33 + i];
-          const float dx = Rs[row] * (g - Rs[32 + row] - xh * Rs[64 + row]);
-          dP[(row0 + row) * F + i] = dx + res[r];
-        }
+      for (int mt = 0; mt < 4; ++mt) {
+        const float a = T1[row * LD66 + mt * 16 + c];
+        db[mt] += a;
+        accW[mt][0] = mfma16(a, ph[0], accW[mt][0]);
+        accW[mt][1] = mfma16(a, ph[1], accW[mt][1]);
       }
-    } else {
+    }
+    // ReLU mask + LayerNorm backward in the C layout; row sums over 16 lanes x 2 column tiles
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = crow(r, h);
-        if (row < nrows) dP[(row0 + row) * F + i] = acc[r] + res[r];
+    for (int r = 0; r < 4; ++r) {
+      const int e = 4 * g + r;
+      float gv[2], xh[2];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        xh[nt] = T2[e * LD34 + nt * 16 + c];
+        float dy = acc[nt][r];
+        if (LN) {
+          dy = (fmaf(xh[nt], gi[nt], bi[nt]) > 0.f) ? dy : 0.f;
+          dg[nt] = fmaf(dy, xh[nt], dg[nt]);
+          dbt[nt] += dy;
+        }
+        gv[nt] = LN ? dy * gi[nt] : dy;
+        s1 += gv[nt];
+        s2 = fmaf(gv[nt], xh[nt], s2);
+      }
+      if (LN) {
+        s1 = sum16(s1) * (1.f / F);
+        s2 = sum16(s2) * (1.f / F);
+      }
+      if (e < nrows) {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int j = nt * 16 + c;
+          float dx = LN ? Rs[e] * (gv[nt] - s1 - xh[nt] * s2) : gv[nt];
+          if (RES) dx += T3[e * LD34 + j];
+          dP[(row0 + e) * F + j] = dx;
+        }
       }
     }
     wave_sync();
   }
-  // workgroup reduction (LDS reused): 32 accW + 2 db + 2 (dg, dbt) floats per lane
-  float v[36];
+  // workgroup reduction (LDS reused): 32 accW + 4 db + 2 dg + 2 dbt per lane
+  float v[40];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    v[r] = accW0[r];
-    v[16 + r] = accW1[r];
-  }
-  v[32] = db0;
-  v[33] = db1;
-  v[34] = dg;
-  v[35] = dbt;
-  wg_reduce<36>(v, lds, wave, lane);
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[(mt * 2 + nt) * 4 + r] = accW[mt][nt][r];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) v[32 + mt] = db[mt];
+  v[36] = dg[0];
+  v[37] = dg[1];
+  v[38] = dbt[0];
+  v[39] = dbt[1];
+  wg_reduce<40>(v, lds, wave, lane);
   if (wave == 0) {
     float* out = part + int64_t(blockIdx.x) * (NX * F + NX + 2 * F);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      out[crow(r, h) * F + i] = v[r];
-      out[(32 + crow(r, h)) * F + i] = v[16 + r];
-    }
-    const float t0 = v[32] + __shfl_xor(v[32], 32), t1 = v[33] + __shfl_xor(v[33], 32);
-    const float t2 = v[34] + __shfl_xor(v[34], 32), t3 = v[35] + __shfl_xor(v[35], 32);
-    if (h == 0) {
-      out[NX * F + i] = t0;
-      out[NX * F + 32 + i] = t1;
-      out[NX * F + NX + i] = t2;
-      out[NX * F + NX + F + i] = t3;
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[(mt * 16 + 4 * g + r) * F + nt * 16 + c] = v[(mt * 2 + nt) * 4 + r];
+    float tt[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) tt[k] = sum_groups(v[32 + k]);
+    if (g == 0) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) out[NX * F + mt * 16 + c] = tt[mt];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        out[NX * F + NX + nt * 16 + c] = tt[4 + nt];
+        out[NX * F + NX + F + nt * 16 + c] = tt[6 + nt];
+      }
     }
   }
 }
@@ -522,7 +597,7 @@ __global__ __launch_bounds__(kThreads) void segment_rowsum_kernel(const gasfm_wo
 }
 
 int grid_tiles(int64_t E) {
-  const int64_t tiles = (E + 31) / 32;
+  const int64_t tiles = (E + TR - 1) / TR;
   const int64_t g = (tiles + kWaves - 1) / kWaves;
   return int(g < 1 ? 1 : (g > kMaxGrid ? kMaxGrid : g));
 }
@@ -579,6 +654,7 @@ extern "C" int gasfm_edge_epilogue_bwd(const gasfm_work_item* items, int32_t n_i
   GASFM_REQUIRE(items && dPo && P && ln_w && ln_b && Wp && dSv && part_w, "gasfm_edge_epilogue_bwd: null pointer");
   GASFM_REQUIRE((P0 && dP0 && ldWp == 34) || (!P0 && ldWp == 32), "gasfm_edge_epilogue_bwd: ldWp=%d vs P0",
                 ldWp);
+  GASFM_REQUIRE(aligned16(dPo) && aligned16(P), "gasfm_edge_epilogue_bwd: dPo/P not 16-byte aligned");
   if (n_items <= 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int g = n_items < kMaxGrid * kWaves ? (n_items + kWaves - 1) / kWaves : kMaxGrid;
@@ -593,13 +669,14 @@ extern "C" int gasfm_edge_prologue_bwd(const float* dXL, int64_t ldX, const floa
                                        void* stream) {
   GASFM_REQUIRE(dXL && P && W && dP && part && ldX >= NX, "gasfm_edge_prologue_bwd: bad args");
   GASFM_REQUIRE(!dRes || Wp, "gasfm_edge_prologue_bwd: dRes needs Wp");
+  GASFM_REQUIRE(aligned16(dXL) && ldX % 4 == 0 && aligned16(P) && (!dRes || aligned16(dRes)),
+                "gasfm_edge_prologue_bwd: dXL/P/dRes not 16-byte aligned");
   if (E == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const size_t lds = size_t(kWaves) * (32 * LD65 + 2 * 32 * LD33 + 96) * sizeof(float);
   const int g = grid_tiles(E);
   const bool ln = ln_w != nullptr, res = dRes != nullptr;
 #define GASFM_LAUNCH(LNV, RESV)                                                                                 \
-  hipLaunchKernelGGL((edge_prologue_bwd_kernel<LNV, RESV>), dim3(g), dim3(kThreads), lds, st, dXL, ldX, P, dRes, \
+  hipLaunchKernelGGL((edge_prologue_bwd_kernel<LNV, RESV>), dim3(g), dim3(kThreads), 0, st, dXL, ldX, P, dRes, \
                      E, ln_w, ln_b, eps, W, Wp, ldWp, scale, dP, part)
   if (ln && res)
     GASFM_LAUNCH(true, true);
