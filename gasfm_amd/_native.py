@@ -51,6 +51,9 @@ _SIGS = {
     "gasfm_edge0_epilogue_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _f32, _vp, _vp,
                                         _vp, _vp, _vp]),
     "gasfm_edge0_prologue_bwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
+    "gasfm_node_part_rows": (_i32, [_i64]),
+    "gasfm_node_ln_linear_fwd": (_i32, [_vp, _i64, _i32, _vp, _vp, _f32, _vp, _vp, _i32, _i32, _vp, _i64, _vp]),
+    "gasfm_node_ln_linear_bwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp, _f32, _vp, _i32, _i32, _vp, _vp, _vp]),
 }
 
 _lib = None
@@ -262,3 +265,25 @@ def edge0_prologue_bwd(dXL, P, aux, ln_w, ln_b, eps, W0, dP, part):
     st = lib().gasfm_edge0_prologue_bwd(_p(dXL), _p(P), _p(aux), P.shape[0], _p(ln_w), _p(ln_b), eps, _p(W0),
                                         _p(dP), _p(part), _stream(P))
     check(st, "gasfm_edge0_prologue_bwd")
+
+
+# ---------------------------------------------------------------- point-node LayerNorm -> ReLU -> Linear
+def node_part_rows(N):
+    return lib().gasfm_node_part_rows(N)
+
+
+def node_ln_linear_fwd(X, ln_w, ln_b, eps, W, b, residual, Y):
+    _req(X, "X")
+    N, n_in = X.shape
+    st = lib().gasfm_node_ln_linear_fwd(_p(X), N, n_in, _p(ln_w), _p(ln_b), eps, _p(W), _p(b), W.shape[0],
+                                        int(residual), _p(Y), Y.stride(0), _stream(X))
+    check(st, "gasfm_node_ln_linear_fwd")
+
+
+def node_ln_linear_bwd(dY, X, ln_w, ln_b, eps, W, residual, dX, part):
+    _req(dY, "dY", W.shape[0])
+    _req(X, "X")
+    N, n_in = X.shape
+    st = lib().gasfm_node_ln_linear_bwd(_p(dY), _p(X), N, n_in, _p(ln_w), _p(ln_b), eps, _p(W), W.shape[0],
+                                        int(residual), _p(dX), _p(part), _stream(X))
+    check(st, "gasfm_node_ln_linear_bwd")

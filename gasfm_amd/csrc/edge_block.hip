@@ -30,47 +30,20 @@
 #include <hip/hip_runtime.h>
 
 #include "common.hpp"
+#include "tile.hpp"
 
 namespace gasfm {
 namespace {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
+using namespace tile;
 
-constexpr int kW = 64;           // wave
-constexpr int kWaves = 4;        // waves per workgroup
-constexpr int kThreads = kW * kWaves;
 constexpr int F = 32;            // projection feature width (n_feat_proj)
 constexpr int NX = 64;           // XL width: 32 (point conv) + 32 (camera conv)
-constexpr int TR = 16;           // edges per tile
 constexpr int LD34 = 34;         // LDS row stride of 32-wide tiles
 constexpr int LD66 = 66;         // LDS row stride of 64-wide tiles
 constexpr int LDW = 48;          // LDS row stride of staged weights (<= 32 columns)
 constexpr int LDW64 = 80;        // LDS row stride of staged 64-column weights
 constexpr int kMaxGrid = 2048;   // workgroups for the grid-stride kernels
-
-__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-}
-__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
-
-// Sum over the 16 lanes of a lane group (same l>>4): xor 1,2,4,8.
-__device__ __forceinline__ float sum16(float v) {
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
-  v += __shfl_xor(v, 8);
-  return v;
-}
-// Sum over the 4 lane groups (l>>4): xor 16, 32.
-__device__ __forceinline__ float sum_groups(float v) {
-  v += __shfl_xor(v, 16);
-  v += __shfl_xor(v, 32);
-  return v;
-}
 
 // Load a 16 x 32 tile of P (rows row0.., global stride 32): the 8 lanes 8k..8k+7 hold row
 // k + 8u (u = 0, 1).  Per row LayerNorm statistics by 3 xor-shuffles.  Writes x_hat
@@ -123,49 +96,6 @@ __device__ __forceinline__ void load_norm_tile(const float* __restrict__ P, int6
       if (Ph) Ph[r * LD34 + c + k] = (r < nrows) ? (LN ? fmaxf(fmaf(xh, gg[k], bb[k]), 0.f) : xh) : 0.f;
     }
     if (Rs && (lane & 7) == 0) Rs[r] = rstd;
-  }
-}
-
-// Row-major [16 x W] tile from global (stride ld) into LDS (stride LDT); rows >= nrows zero.
-template <int W, int LDT>
-__device__ __forceinline__ void load_tile(const float* __restrict__ X, int64_t ld, int64_t row0, int nrows,
-                                          float* T, int lane) {
-  constexpr int V = W / 4;            // float4 per row
-  constexpr int STEPS = TR * V / kW;  // float4 per lane
-  float4 v[STEPS];
-#pragma unroll
-  for (int u = 0; u < STEPS; ++u) {
-    const int q = lane + kW * u;
-    const int r = q / V, c = (q % V) * 4;
-    v[u] = (r < nrows) ? *reinterpret_cast<const float4*>(X + (row0 + r) * ld + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-#pragma unroll
-  for (int u = 0; u < STEPS; ++u) {
-    const int q = lane + kW * u;
-    const int r = q / V, c = (q % V) * 4;
-    float* d = T + r * LDT + c;
-    d[0] = v[u].x;
-    d[1] = v[u].y;
-    d[2] = v[u].z;
-    d[3] = v[u].w;
-  }
-}
-
-// Sum `N` floats per lane across the workgroup's waves (LDS scratch >= kWaves*N*kW floats);
-// wave 0 returns the totals in v.
-template <int N>
-__device__ __forceinline__ void wg_reduce(float (&v)[N], float* scratch, int wave, int lane) {
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < N; ++k) scratch[(wave * N + k) * kW + lane] = v[k];
-  __syncthreads();
-  if (wave == 0) {
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-      float s = 0.f;
-      for (int w = 0; w < kWaves; ++w) s += scratch[(w * N + k) * kW + lane];
-      v[k] = s;
-    }
   }
 }
 

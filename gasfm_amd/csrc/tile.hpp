@@ -1,0 +1,110 @@
+// Wave-level building blocks shared by the row-tile kernels (edge_block.hip, node_block.hip).
+//
+// A wavefront (64 lanes) owns a 16-row tile at a time.  GEMM-shaped parts use the exact-fp32
+// MFMA v_mfma_f32_16x16x4_f32 with lane l holding A[i = l&15][k = l>>4], B[k = l>>4][j = l&15]
+// and C[row = 4(l>>4) + r][col = l&15] (r = 0..3).  Row reductions over a 16-lane group use
+// xor-shuffles 1,2,4,8; reductions across the four lane groups use xor 16, 32.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace gasfm {
+namespace tile {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kW = 64;                  // wavefront
+constexpr int kWaves = 4;               // waves per workgroup
+constexpr int kThreads = kW * kWaves;
+constexpr int TR = 16;                  // rows per tile
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// Sum over the 16 lanes of a lane group (same l>>4).
+__device__ __forceinline__ float sum16(float v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 8);
+  return v;
+}
+// Sum over the 4 lane groups (l>>4).
+__device__ __forceinline__ float sum_groups(float v) {
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
+}
+
+// Row-major [16 x W] tile from global (row stride ld floats, 16-byte aligned) into LDS (row
+// stride LDT); rows >= nrows are zeros.  All global loads are issued before the LDS stores.
+template <int W, int LDT>
+__device__ __forceinline__ void load_tile(const float* __restrict__ X, int64_t ld, int64_t row0, int nrows,
+                                          float* T, int lane) {
+  constexpr int V = W / 4;            // float4 per row
+  constexpr int STEPS = TR * V / kW;  // float4 per lane
+  float4 v[STEPS];
+#pragma unroll
+  for (int u = 0; u < STEPS; ++u) {
+    const int q = lane + kW * u;
+    const int r = q / V, c = (q % V) * 4;
+    v[u] = (r < nrows) ? *reinterpret_cast<const float4*>(X + (row0 + r) * ld + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int u = 0; u < STEPS; ++u) {
+    const int q = lane + kW * u;
+    const int r = q / V, c = (q % V) * 4;
+    float* d = T + r * LDT + c;
+    d[0] = v[u].x;
+    d[1] = v[u].y;
+    d[2] = v[u].z;
+    d[3] = v[u].w;
+  }
+}
+
+// Sum `N` floats per lane across the workgroup's waves (LDS scratch >= kWaves*N*kW floats,
+// free for reuse); wave 0 returns the totals in v, summed in wave order (deterministic).
+template <int N>
+__device__ __forceinline__ void wg_reduce(float (&v)[N], float* scratch, int wave, int lane) {
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < N; ++k) scratch[(wave * N + k) * kW + lane] = v[k];
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      float s = 0.f;
+      for (int w = 0; w < kWaves; ++w) s += scratch[(w * N + k) * kW + lane];
+      v[k] = s;
+    }
+  }
+}
+
+// Same result as wg_reduce with only N*kW floats of scratch: the waves add into one buffer in
+// wave order, one barrier per wave.
+template <int N>
+__device__ __forceinline__ void wg_reduce_ordered(float (&v)[N], float* scratch, int wave, int lane) {
+  for (int w = 0; w < kWaves; ++w) {
+    __syncthreads();
+    if (wave == w) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) scratch[k * kW + lane] = (w == 0 ? 0.f : scratch[k * kW + lane]) + v[k];
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = scratch[k * kW + lane];
+  }
+}
+
+}  // namespace tile
+}  // namespace gasfm

@@ -54,9 +54,73 @@ def layer_norm(x, ln):
     return F.layer_norm(x, ln.normalized_shape, ln.weight, ln.bias, ln.eps)
 
 
+NODE_WIDTH = 64  # n_feat_scenepoint of every GASFM conf: the width node_block.hip is built for
+
+
+class NodeLnLinearFn(torch.autograd.Function):
+    """y = W relu(LN(x)) + b (+ x): one HIP kernel each way (csrc/node_block.hip).
+
+    Backward recomputes the LayerNorm statistics from x and returns dx plus the weight,
+    bias, gamma and beta gradients reduced deterministically (per-workgroup partials ->
+    gasfm_colsum)."""
+
+    @staticmethod
+    def forward(ctx, x, ln_w, ln_b, W, b, eps, residual):
+        from . import _native
+        x = x.contiguous()
+        W = W.contiguous()
+        y = torch.empty((x.shape[0], W.shape[0]), dtype=torch.float32, device=x.device)
+        _native.node_ln_linear_fwd(x, ln_w, ln_b, eps, W, b, residual, y)
+        ctx.save_for_backward(x, ln_w, ln_b, W)
+        ctx.eps, ctx.residual, ctx.has_b = eps, residual, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _native
+        x, ln_w, ln_b, W = ctx.saved_tensors
+        n_out, n_in = W.shape
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        rows = _native.node_part_rows(x.shape[0])
+        part = torch.empty((rows, n_out * n_in + n_out + 2 * n_in), dtype=torch.float32, device=x.device)
+        _native.node_ln_linear_bwd(dy, x, ln_w, ln_b, ctx.eps, W, ctx.residual, dx, part)
+        tot = _native.colsum(part)
+        o = n_out * n_in
+        dW = tot[:o].view(n_out, n_in)
+        db = tot[o:o + n_out] if ctx.has_b else None
+        dg = tot[o + n_out:o + n_out + n_in]
+        dbeta = tot[o + n_out + n_in:]
+        return dx, dg, dbeta, dW, db, None, None
+
+
+def _node_fusable(x, ln, lin):
+    return (x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and x.shape[1] == NODE_WIDTH
+            and tuple(ln.normalized_shape) == (NODE_WIDTH,) and ln.weight is not None and ln.bias is not None
+            and lin.in_features == NODE_WIDTH and lin.out_features in (32, 64))
+
+
+def ln_relu_linear(x, ln, lin, residual=False):
+    """lin(relu(ln(x))) (+ x when residual): the fused point-node kernel for 64-wide rows."""
+    if _node_fusable(x, ln, lin) and (not residual or lin.out_features == NODE_WIDTH):
+        return NodeLnLinearFn.apply(x, ln.weight, ln.bias, lin.weight, lin.bias, ln.eps, residual)
+    y = linear(F.relu(layer_norm(x, ln)), lin)
+    return x + y if residual else y
+
+
 def sequential(seq, x):
-    """Run a Sequential of Linear / LayerNorm / ReLU with the row-aware linear."""
-    for mod in seq:
+    """Run a Sequential of Linear / LayerNorm / ReLU with the row-aware linear; a
+    LayerNorm, ReLU, Linear run on 64-wide point rows goes through the fused node kernel."""
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        mod = mods[i]
+        if (isinstance(mod, LayerNorm) and i + 2 < len(mods) and isinstance(mods[i + 1], ReLU)
+                and isinstance(mods[i + 2], Linear) and _node_fusable(x, mod, mods[i + 2])):
+            x = ln_relu_linear(x, mod, mods[i + 2])
+            i += 3
+            continue
+        i += 1
         if isinstance(mod, Linear):
             x = linear(x, mod)
         elif isinstance(mod, LayerNorm):

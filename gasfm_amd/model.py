@@ -132,6 +132,8 @@ class _NodeAggregation(Module):
             x = dense.linear(x, getattr(self, self._proj_key))
         if prev is not None:
             x = prev + x
+        if self.use_norm_pre_mlp and len(self.mlp) == 1:
+            return dense.ln_relu_linear(x, self.norm_pre_mlp, self.mlp[0], residual=True)
         skip = x
         if self.use_norm_pre_mlp:
             x = F.relu(dense.layer_norm(x, self.norm_pre_mlp))
@@ -362,9 +364,9 @@ class GraphAttnSfMProjectionFeatureUpdate(Module):
 
     def node_terms(self, pts, view, glob):
         if self.normalize_global_features:
-            pts = F.relu(dense.layer_norm(pts, self.scenepoint_norm_layer))
-            view = F.relu(dense.layer_norm(view, self.view_norm_layer))
-            glob = F.relu(dense.layer_norm(glob, self.global_norm_layer))
+            return (dense.ln_relu_linear(pts, self.scenepoint_norm_layer, self.lin_scenepoint),
+                    dense.ln_relu_linear(view, self.view_norm_layer, self.lin_view),
+                    dense.ln_relu_linear(glob, self.global_norm_layer, self.lin_global))
         return dense.linear(pts, self.lin_scenepoint), dense.linear(view, self.lin_view), \
             dense.linear(glob, self.lin_global)
 

@@ -218,6 +218,26 @@ int gasfm_edge0_prologue_bwd(const float* dXL, const float* P, const float* aux,
                              const float* ln_w, const float* ln_b, float eps, const float* W0, float* dP,
                              float* part, void* stream);
 
+/* ---- point-node rows: LayerNorm -> ReLU -> Linear (-> + x), n_in = 64, n_out in {32, 64} ----
+ * Replaces the aten chains on the scene-point features (n rows x n_feat_scenepoint):
+ * the state projection Sequential(LayerNorm, ReLU, Linear) (layers.py:48-56, used at
+ * layers.py:403-404), the pre-MLP skip x + mlp(relu(norm_pre_mlp(x))) (layers.py:449-456) and
+ * lin_scenepoint(relu(scenepoint_norm_layer(x))) of the projection update (layers.py:928-935). */
+
+/* Rows of the [rows x (n_out*n_in + n_out + 2*n_in)] partial buffer gasfm_node_ln_linear_bwd
+ * writes: [dW n_out x n_in | db n_out | dgamma n_in | dbeta n_in] per workgroup. */
+int gasfm_node_part_rows(int64_t N);
+
+/* Y[i] = W relu(LN(X[i])) + b (+ X[i] if residual); b may be null. X: [N x 64] contiguous. */
+int gasfm_node_ln_linear_fwd(const float* X, int64_t N, int32_t n_in, const float* ln_w, const float* ln_b,
+                             float eps, const float* W, const float* b, int32_t n_out, int32_t residual,
+                             float* Y, int64_t ldY, void* stream);
+
+/* dX = LN_bwd(mask * (dY W)) (+ dY if residual) and the per-workgroup partials above. */
+int gasfm_node_ln_linear_bwd(const float* dY, const float* X, int64_t N, int32_t n_in, const float* ln_w,
+                             const float* ln_b, float eps, const float* W, int32_t n_out, int32_t residual,
+                             float* dX, float* part, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
