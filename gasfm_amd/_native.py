@@ -29,7 +29,7 @@ _SIGS = {
     "gasfm_gat_attn_fwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _f32, _i32,
                                   _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
     "gasfm_gat_attn_combine": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _i64, _vp]),
-    "gasfm_gat_attn_bwd_waves": (_i32, [_i32]),
+    "gasfm_gat_attn_bwd_waves": (_i32, [_i32, _i32, _i32]),
     "gasfm_gat_attn_bwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _f32, _vp,
                                   _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp]),
     "gasfm_gat_attn_bwd_combine": (_i32, [_vp, _i32, _i32, _vp, _vp, _i64, _vp]),
@@ -149,8 +149,8 @@ def attn_combine(combine, n_combine, H, C, part, bias, finalize, out, seg_max, s
     check(st, "gasfm_gat_attn_combine")
 
 
-def attn_bwd_waves(n_items):
-    return lib().gasfm_gat_attn_bwd_waves(n_items)
+def attn_bwd_waves(n_items, H, C):
+    return lib().gasfm_gat_attn_bwd_waves(n_items, H, C)
 
 
 def attn_bwd(XL, XR, att, bias, perm, items, n_items, H, C, slope, out, seg_max, seg_sum, gout, dXL, dXR,

@@ -68,7 +68,6 @@ class AttnPlan:
         self.max_piece = int(max_piece)
         self.n_items = int(items.shape[0])
         self.n_combine = int(combine.shape[0])
-        self.bwd_waves = _native.attn_bwd_waves(self.n_items) if self.n_items else 0
         self.tag = None  # graph name (proj2view, proj2scenepoint, ...) for timing / logs
 
     # ------------------------------------------------------------------ construction
@@ -204,7 +203,8 @@ def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, go
         dXL = (torch.empty if full else torch.zeros)((XL.shape[0], HC), dtype=torch.float32, device=dev)
     dXR = torch.empty((plan.num_targets, HC), dtype=torch.float32, device=dev)
     part = torch.empty((plan.n_slots, HC), dtype=torch.float32, device=dev) if plan.n_slots else None
-    datt_part = torch.empty((max(plan.bwd_waves, 1), 2 * HC), dtype=torch.float32, device=dev)
+    n_waves = _native.attn_bwd_waves(plan.n_items, heads, C)
+    datt_part = torch.empty((max(n_waves, 1), 2 * HC), dtype=torch.float32, device=dev)
     attf = att.reshape(-1).contiguous()
     if plan.n_items:
         _native.attn_bwd(XL, XR, attf, bias, plan.perm, plan.items, plan.n_items, heads, C, slope, out, smax,

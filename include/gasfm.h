@@ -118,8 +118,9 @@ int gasfm_gat_attn_combine(const gasfm_combine_item* combine, int32_t n_combine,
  * once), dXR[seg] for complete items (partials to part_dxr[slot] for split
  * items; merge with gasfm_gat_attn_bwd_combine) and one partial row per
  * wave into datt_part[n_waves, 2*H*C] = [d att | d bias] (n_waves from
- * gasfm_gat_attn_bwd_waves(); reduce with gasfm_colsum). */
-int gasfm_gat_attn_bwd_waves(int32_t n_items);
+ * gasfm_gat_attn_bwd_waves(), which sizes the grid from the current device's
+ * occupancy for this (H, C); reduce with gasfm_colsum). */
+int gasfm_gat_attn_bwd_waves(int32_t n_items, int32_t H, int32_t C);
 int gasfm_gat_attn_bwd(const float* XL, int64_t ldXL,
                        const float* XR, int64_t ldXR,
                        const float* att, const float* bias,
