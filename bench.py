@@ -151,7 +151,7 @@ def main():
     plan = data.graph_wrappers["proj2scenepoint"].plan
     e_local = plan.num_edges
     n_local = plan.num_targets
-    bytes_per_launch = attn_fwd_bytes(e_local, n_local, 4, 32, plan.perm is not None)
+    bytes_per_launch = attn_fwd_bytes(e_local, n_local, 4, 32, bool(timer.gathered))
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9 if kern_ms else None
 
     if rank == 0:

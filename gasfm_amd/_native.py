@@ -31,11 +31,11 @@ _SIGS = {
     "gasfm_gat_attn_combine": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _i64, _vp]),
     "gasfm_gat_attn_bwd_waves": (_i32, [_i32, _i32, _i32]),
     "gasfm_gat_attn_bwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _f32, _vp,
-                                  _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp]),
+                                  _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _vp]),
     "gasfm_gat_attn_bwd_combine": (_i32, [_vp, _i32, _i32, _vp, _vp, _i64, _vp]),
     "gasfm_colsum_ws_floats": (_i64, [_i64, _i32]),
     "gasfm_edge_part_floats": (_i32, [_i32, _i64, _i32]),
-    "gasfm_edge_prologue_fwd": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _i64, _vp]),
+    "gasfm_edge_prologue_fwd": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _i64, _vp, _vp]),
     "gasfm_edge_epilogue_fwd": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _i32, _vp, _vp, _vp, _vp,
                                        _f32, _vp, _vp]),
     "gasfm_edge_epilogue_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _i32, _f32, _vp, _vp, _vp,
@@ -154,11 +154,11 @@ def attn_bwd_waves(n_items, H, C):
 
 
 def attn_bwd(XL, XR, att, bias, perm, items, n_items, H, C, slope, out, seg_max, seg_sum, gout, dXL, dXR,
-             part_dxr, datt_part):
+             part_dxr, datt_part, xl_by_position=False):
     st = lib().gasfm_gat_attn_bwd(
         _p(XL), XL.stride(0), _p(XR), XR.stride(0), _p(att), _p(bias), _p(perm), _p(items), n_items, H, C,
         slope, _p(out), out.stride(0), _p(seg_max), _p(seg_sum), _p(gout), gout.stride(0), _p(dXL),
-        dXL.stride(0), _p(dXR), dXR.stride(0), _p(part_dxr), _p(datt_part), _stream(dXL))
+        dXL.stride(0), _p(dXR), dXR.stride(0), _p(part_dxr), _p(datt_part), int(xl_by_position), _stream(dXL))
     check(st, "gasfm_gat_attn_bwd")
 
 
@@ -192,10 +192,10 @@ def edge_part_floats(which, E, n_items=0):
     return lib().gasfm_edge_part_floats(which, E, n_items)
 
 
-def edge_prologue_fwd(P, ln_w, ln_b, eps, W, b, Y):
+def edge_prologue_fwd(P, ln_w, ln_b, eps, W, b, Y, pos=None):
     _req(P, "P", 32)
     st = lib().gasfm_edge_prologue_fwd(_p(P), P.shape[0], _p(ln_w), _p(ln_b), eps, _p(W), _p(b), _p(Y), Y.stride(0),
-                                       _stream(P))
+                                       _p(pos), _stream(P))
     check(st, "gasfm_edge_prologue_fwd")
 
 

@@ -33,6 +33,7 @@ class KernelTimer:
         self.select = select
         self.events = []
         self.enabled = False
+        self.gathered = None  # whether the timed launches read XL through perm
 
     def __call__(self, tag, HC):
         return self.enabled and self.select(tag, HC)
@@ -50,6 +51,10 @@ class AttnPlan:
     seg_ptr  int32 [N+1]   edge range of each destination segment
     perm     int32 [E]     source row of the k-th edge in segment order, or None
                            when segment order == source row order (identity)
+    pos      int32 [E]     inverse of perm (segment position of source row e) when perm
+                           is a permutation of the E source rows, else None.  Producers
+                           use it to write source rows directly in segment order, so the
+                           attention kernels stream them instead of gathering (xl_sorted).
     items    int32 [I, 4]  (seg, begin, end, slot) work items (see gasfm.h)
     combine  int32 [K, 4]  (seg, slot_begin, slot_count, slot_stride)
     """
@@ -69,6 +74,12 @@ class AttnPlan:
         self.n_items = int(items.shape[0])
         self.n_combine = int(combine.shape[0])
         self.tag = None  # graph name (proj2view, proj2scenepoint, ...) for timing / logs
+        self.pos = None
+        if perm is not None and self.src_rows == self.num_edges:
+            p = perm.numpy() if isinstance(perm, torch.Tensor) else perm
+            pos = np.empty(self.num_edges, dtype=np.int32)
+            pos[p] = np.arange(self.num_edges, dtype=np.int32)
+            self.pos = torch.from_numpy(pos)
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -103,7 +114,7 @@ class AttnPlan:
 
     def to(self, device, **kwargs):
         ret = copy.copy(self)
-        for k in ("seg_ptr", "perm", "items", "combine"):
+        for k in ("seg_ptr", "perm", "pos", "items", "combine"):
             v = getattr(self, k)
             if v is not None:
                 setattr(ret, k, v.to(device, **kwargs))
@@ -128,8 +139,11 @@ def _check(t, name, rows=None, cols=None):
         raise ValueError(f"{name}: has {t.shape[1]} columns, expected {cols}")
 
 
-def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True):
-    """Launch the forward kernels; returns (out, seg_max, seg_sum) for all plan targets."""
+def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True, xl_sorted=False):
+    """Launch the forward kernels; returns (out, seg_max, seg_sum) for all plan targets.
+
+    xl_sorted: XL rows are already in segment order (written through plan.pos), so the
+    kernel streams them (perm = NULL) instead of gathering."""
     if plan.all_partial:
         raise ValueError("all-partial plans go through attn_forward_partial")
     HC = att.numel()
@@ -147,11 +161,12 @@ def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True):
     if timed:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
-    _native.attn_fwd(XL, XR, attf, bias, plan.perm, plan.items, plan.n_items, heads, C, slope, finalize, out,
-                     smax, ssum, part)
+    _native.attn_fwd(XL, XR, attf, bias, None if xl_sorted else plan.perm, plan.items, plan.n_items, heads, C,
+                     slope, finalize, out, smax, ssum, part)
     if timed:
         ev[1].record()
         KERNEL_TIMER.events.append(ev)
+        KERNEL_TIMER.gathered = plan.perm is not None and not xl_sorted
     if plan.n_combine:
         _native.attn_combine(plan.combine, plan.n_combine, heads, C, part, bias, finalize, out, smax, ssum)
     return out, smax, ssum
@@ -191,8 +206,10 @@ def combine_partials(gathered, world, N, heads, bias, combine_items):
     return out, smax, ssum
 
 
-def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, gout, dXL=None):
-    """Launch the backward kernels; returns (dXL, dXR, datt[HC], dbias[HC])."""
+def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, gout, dXL=None, xl_sorted=False):
+    """Launch the backward kernels; returns (dXL, dXR, datt[HC], dbias[HC]).
+
+    dXL is always in source-row (edge) order; xl_sorted says XL itself is in segment order."""
     HC = att.numel()
     C = HC // heads
     dev = XL.device
@@ -208,7 +225,7 @@ def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, go
     attf = att.reshape(-1).contiguous()
     if plan.n_items:
         _native.attn_bwd(XL, XR, attf, bias, plan.perm, plan.items, plan.n_items, heads, C, slope, out, smax,
-                         ssum, gout, dXL, dXR, part, datt_part)
+                         ssum, gout, dXL, dXR, part, datt_part, xl_by_position=xl_sorted)
         if plan.n_combine:
             _native.attn_bwd_combine(plan.combine, plan.n_combine, HC, part, dXR)
         tot = _native.colsum(datt_part)

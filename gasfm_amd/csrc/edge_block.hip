@@ -108,7 +108,8 @@ __global__ __launch_bounds__(kThreads) void edge_prologue_fwd_kernel(const float
                                                                     const float* __restrict__ bet, float eps,
                                                                     const float* __restrict__ W,
                                                                     const float* __restrict__ b,
-                                                                    float* __restrict__ Y, int64_t ldY) {
+                                                                    float* __restrict__ Y, int64_t ldY,
+                                                                    const int32_t* __restrict__ pos) {
   __shared__ float Wt[F * LDW64];            // W^T: Wt[k][n] = W[n][k]
   __shared__ float tiles[kWaves][TR * LD34];
   for (int q = threadIdx.x; q < NX * F; q += kThreads) Wt[(q % F) * LDW64 + q / F] = W[q];
@@ -137,9 +138,13 @@ __global__ __launch_bounds__(kThreads) void edge_prologue_fwd_kernel(const float
     for (int r = 0; r < 4; ++r) {
       const int e = 4 * g + r;
       if (e < nrows) {
-        float* y = Y + (row0 + e) * ldY;
+        // point half (columns 0..31) goes to the edge's position in point order when pos != null
+        float* yp = Y + (pos ? int64_t(pos[row0 + e]) : row0 + e) * ldY;
+        float* yc = Y + (row0 + e) * ldY;
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) y[nt * 16 + c] = acc[nt][r] + bias[nt];
+        for (int nt = 0; nt < 2; ++nt) yp[nt * 16 + c] = acc[nt][r] + bias[nt];
+#pragma unroll
+        for (int nt = 2; nt < 4; ++nt) yc[nt * 16 + c] = acc[nt][r] + bias[nt];
       }
     }
     wave_sync();
@@ -547,7 +552,7 @@ extern "C" int gasfm_edge_part_floats(int32_t which, int64_t E, int32_t n_items)
 
 extern "C" int gasfm_edge_prologue_fwd(const float* P, int64_t E, const float* ln_w, const float* ln_b,
                                        float eps, const float* W, const float* b, float* Y, int64_t ldY,
-                                       void* stream) {
+                                       const int32_t* pos, void* stream) {
   GASFM_REQUIRE(E >= 0 && P && W && b && Y, "gasfm_edge_prologue_fwd: bad args");
   GASFM_REQUIRE(ldY >= NX, "gasfm_edge_prologue_fwd: ldY < 64");
   GASFM_REQUIRE(aligned16(P), "gasfm_edge_prologue_fwd: P not 16-byte aligned");
@@ -555,10 +560,10 @@ extern "C" int gasfm_edge_prologue_fwd(const float* P, int64_t E, const float* l
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (ln_w)
     hipLaunchKernelGGL(edge_prologue_fwd_kernel<true>, dim3(grid_tiles(E)), dim3(kThreads), 0, st, P, E, ln_w,
-                       ln_b, eps, W, b, Y, ldY);
+                       ln_b, eps, W, b, Y, ldY, pos);
   else
     hipLaunchKernelGGL(edge_prologue_fwd_kernel<false>, dim3(grid_tiles(E)), dim3(kThreads), 0, st, P, E, ln_w,
-                       ln_b, eps, W, b, Y, ldY);
+                       ln_b, eps, W, b, Y, ldY, pos);
   return launch_status("gasfm_edge_prologue_fwd");
 }
 

@@ -358,7 +358,8 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_kernel(
     const gasfm_work_item* __restrict__ items, int n_items, float slope, const float* __restrict__ out,
     int64_t ldOut, const float* __restrict__ seg_max, const float* __restrict__ seg_sum,
     const float* __restrict__ gout, int64_t ldG, float* __restrict__ dXL, int64_t ldDXL,
-    float* __restrict__ dXR, int64_t ldDXR, float* __restrict__ part_dxr, float* __restrict__ datt_part) {
+    float* __restrict__ dXR, int64_t ldDXR, float* __restrict__ part_dxr, float* __restrict__ datt_part,
+    int xl_pos) {
   const int lane = threadIdx.x & (kWave - 1);
   const int row = lane / G::LPE;
   const int li = lane % G::LPE;
@@ -413,7 +414,7 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_kernel(
         src[u] = 0;
         if (valid[u]) {
           src[u] = perm ? int64_t(perm[e]) : int64_t(e);
-          load_vec<G::VEC>(xl[u], XL + src[u] * ldXL + f0);
+          load_vec<G::VEC>(xl[u], XL + (xl_pos ? int64_t(e) : src[u]) * ldXL + f0);
         } else {
 #pragma unroll
           for (int v = 0; v < G::VEC; ++v) xl[u][v] = 0.f;
@@ -605,7 +606,7 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_generic(
     const float* __restrict__ out, int64_t ldOut, const float* __restrict__ seg_max,
     const float* __restrict__ seg_sum, const float* __restrict__ gout, int64_t ldG, float* __restrict__ dXL,
     int64_t ldDXL, float* __restrict__ dXR, int64_t ldDXR, float* __restrict__ part_dxr,
-    float* __restrict__ datt_part) {
+    float* __restrict__ datt_part, int xl_pos) {
   // one lane per feature f; per-head scalars recomputed per lane (serial over C) — slow but general.
   const int wave = wave_id_uniform();
   const int lane = threadIdx.x & (kWave - 1);
@@ -629,16 +630,17 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_generic(
       float dxr = 0.f, dat = 0.f;
       for (int e = w.begin; e < w.end; ++e) {
         const int64_t src = perm ? perm[e] : e;
+        const int64_t xs = xl_pos ? int64_t(e) : src;
         float p = 0.f, da = 0.f;
         for (int c = 0; c < C; ++c) {
           const int ff = h * C + c;
-          const float x = XL[src * ldXL + ff];
+          const float x = XL[xs * ldXL + ff];
           p = fmaf(leaky(x + XR[sg * ldXR + ff], slope), att[ff], p);
           da = fmaf(gout[sg * ldG + ff], x, da);
         }
         const float alpha = __expf(p - M) * inv;
         const float de = alpha * (da - delta);
-        const float z = XL[src * ldXL + f] + XR[sg * ldXR + f];
+        const float z = XL[xs * ldXL + f] + XR[sg * ldXR + f];
         const float dz = de * att[f] * (z > 0.f ? 1.f : slope);
         dXL[src * ldDXL + f] = fmaf(alpha, gout[sg * ldG + f], dz);
         dxr += dz;
@@ -792,7 +794,7 @@ extern "C" int gasfm_gat_attn_bwd(const float* XL, int64_t ldXL, const float* XR
                                   float slope, const float* out, int64_t ldOut, const float* seg_max,
                                   const float* seg_sum, const float* gout, int64_t ldG, float* dXL,
                                   int64_t ldDXL, float* dXR, int64_t ldDXR, float* part_dxr,
-                                  float* datt_part, void* stream) {
+                                  float* datt_part, int32_t xl_by_position, void* stream) {
   GASFM_REQUIRE(H > 0 && C > 0 && n_items >= 0, "gasfm_gat_attn_bwd: bad args");
   if (n_items == 0) return GASFM_OK;
   GASFM_REQUIRE(XL && XR && att && bias && items && out && seg_max && seg_sum && gout && dXL && dXR && datt_part,
@@ -809,13 +811,13 @@ extern "C" int gasfm_gat_attn_bwd(const float* XL, int64_t ldXL, const float* XR
       using G = decltype(g);
       hipLaunchKernelGGL((attn_bwd_kernel<G>), dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att, bias,
                          perm, items, n_items, slope, out, ldOut, seg_max, seg_sum, gout, ldG, dXL, ldDXL, dXR,
-                         ldDXR, part_dxr, datt_part);
+                         ldDXR, part_dxr, datt_part, int(xl_by_position != 0));
     });
   }
   if (!done) {
     hipLaunchKernelGGL(attn_bwd_generic, dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att, bias, perm,
                        items, n_items, H, C, slope, out, ldOut, seg_max, seg_sum, gout, ldG, dXL, ldDXL, dXR,
-                       ldDXR, part_dxr, datt_part);
+                       ldDXR, part_dxr, datt_part, int(xl_by_position != 0));
   }
   return launch_status("gasfm_gat_attn_bwd");
 }

@@ -29,10 +29,11 @@ def _colsum_parts(part, rows):
 
 class EdgePrologueFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, P, ln_w, ln_b, W, b, Wp, eps):
+    def forward(ctx, P, ln_w, ln_b, W, b, Wp, eps, pos=None):
+        """pos (point plan's inverse permutation): write the point half of XL in point order."""
         E = P.shape[0]
         XL = torch.empty((E, W.shape[0]), dtype=torch.float32, device=P.device)
-        _native.edge_prologue_fwd(P, ln_w, ln_b, eps, W.contiguous(), b.contiguous(), XL)
+        _native.edge_prologue_fwd(P, ln_w, ln_b, eps, W.contiguous(), b.contiguous(), XL, pos)
         ctx.eps = eps
         ctx.has_ln = ln_w is not None
         ctx.set_materialize_grads(False)
@@ -60,18 +61,21 @@ class EdgePrologueFn(torch.autograd.Function):
         db = tot[64 * 32:64 * 32 + 64]
         dgam = tot[64 * 32 + 64:64 * 32 + 96] if ctx.has_ln else None
         dbet = tot[64 * 32 + 96:] if ctx.has_ln else None
-        return dP, dgam, dbet, dW, db, None, None
+        return dP, dgam, dbet, dW, db, None, None, None
 
 
 class DualAttentionFn(torch.autograd.Function):
-    """Point- and camera-direction GATv2 attention over the two halves of XL [E, 64]."""
+    """Point- and camera-direction GATv2 attention over the two halves of XL [E, 64].
+
+    xl_sorted: the point half of XL is stored in point-segment order (EdgePrologueFn with
+    pos); its gradient is still returned in edge order."""
 
     @staticmethod
     def forward(ctx, XL, XR_pt, XR_cam, att_pt, att_cam, bias_pt, bias_cam, plan_pt, plan_cam, heads, slope,
-                plan_cam_partial=None, shard=None):
+                plan_cam_partial=None, shard=None, xl_sorted=False):
         h = XL.shape[1] // 2
         XLp, XLc = XL[:, :h], XL[:, h:]
-        out_p, mp, sp = attn_forward_raw(XLp, XR_pt, att_pt, bias_pt, plan_pt, heads, slope)
+        out_p, mp, sp = attn_forward_raw(XLp, XR_pt, att_pt, bias_pt, plan_pt, heads, slope, xl_sorted=xl_sorted)
         if shard is None:
             out_c, mc, sc = attn_forward_raw(XLc, XR_cam, att_cam, bias_cam, plan_cam, heads, slope)
         else:  # camera segments span ranks: local partials -> all-gather -> ordered combine
@@ -81,7 +85,7 @@ class DualAttentionFn(torch.autograd.Function):
             out_c, mc, sc = combine_partials(gathered, shard.world, N, heads, bias_cam,
                                              shard.combine_items(N, XL.device))
         ctx.plans = (plan_pt, plan_cam)
-        ctx.heads, ctx.slope = heads, slope
+        ctx.heads, ctx.slope, ctx.xl_sorted = heads, slope, xl_sorted
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(XL, XR_pt, XR_cam, att_pt, att_cam, bias_pt, bias_cam, out_p, mp, sp, out_c, mc, sc)
         return out_p, out_c
@@ -97,11 +101,11 @@ class DualAttentionFn(torch.autograd.Function):
             g_c = torch.zeros_like(out_c)
         dXL = torch.empty_like(XL)
         _, dXRp, dattp, dbp = attn_backward_raw(XL[:, :h], XR_pt, att_pt, bias_pt, plan_pt, ctx.heads, ctx.slope,
-                                                out_p, mp, sp, g_p, dXL=dXL[:, :h])
+                                                out_p, mp, sp, g_p, dXL=dXL[:, :h], xl_sorted=ctx.xl_sorted)
         _, dXRc, dattc, dbc = attn_backward_raw(XL[:, h:], XR_cam, att_cam, bias_cam, plan_cam, ctx.heads, ctx.slope,
                                                 out_c, mc, sc, g_c, dXL=dXL[:, h:])
         return (dXL, dXRp, dXRc, dattp.view_as(att_pt), dattc.view_as(att_cam), dbp, dbc, None, None, None, None,
-                None, None)
+                None, None, None)
 
 
 class EdgeEpilogueFn(torch.autograd.Function):

@@ -308,8 +308,9 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         a, b = self.proj2scenepoint.graph_conv.lin_l, self.proj2view.graph_conv.lin_l
         return torch.cat([a.weight, b.weight], 0), torch.cat([a.bias, b.bias], 0)
 
-    def forward_fused(self, XL, plans, prev_pt=None, prev_view=None, prev_glob=None):
-        """Node side of the update given XL = [lin_l_point(P_hat) | lin_l_camera(P_hat)] [E, 64]."""
+    def forward_fused(self, XL, plans, prev_pt=None, prev_view=None, prev_glob=None, xl_sorted=False):
+        """Node side of the update given XL = [lin_l_point(P_hat) | lin_l_camera(P_hat)] [E, 64]
+        (point half in point-segment order when xl_sorted)."""
         sp, sv = self.proj2scenepoint, self.proj2view
         pp, pc = plans["proj2scenepoint"], plans["proj2view"]
         shard = plans.get("_shard")
@@ -317,7 +318,8 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         XRc = replicated_to_local(sv.target_rows(prev_view, pc.num_targets), shard)
         cp, cc = sp.graph_conv, sv.graph_conv
         agg_p, agg_c = DualAttentionFn.apply(XL, XRp, XRc, cp.att, cc.att, cp.bias, cc.bias, pp, pc, cp.heads,
-                                             cp.negative_slope, plans.get("_partial", {}).get("proj2view"), shard)
+                                             cp.negative_slope, plans.get("_partial", {}).get("proj2view"), shard,
+                                             xl_sorted)
         pts = sp.tail(agg_p, prev_pt)
         view = sv.tail(agg_c, prev_view)
         return self._finish(pts, view, plans, prev_glob)
@@ -449,8 +451,9 @@ class GraphAttnSfMLayer(Module):
         gfu = self.global_feature_update
         pfu = self.projection_feature_update
         W, b = gfu.lin_l_stack()
-        XL, token = EdgePrologueFn.apply(P, ln.weight, ln.bias, W, b, pfu.lin_proj.weight, ln.eps)
-        pts, view, glob = gfu.forward_fused(XL, plans, prev_pt, prev_view, prev_glob)
+        pos = plans["proj2scenepoint"].pos
+        XL, token = EdgePrologueFn.apply(P, ln.weight, ln.bias, W, b, pfu.lin_proj.weight, ln.eps, pos)
+        pts, view, glob = gfu.forward_fused(XL, plans, prev_pt, prev_view, prev_glob, xl_sorted=pos is not None)
         sp, sv, sg = pfu.node_terms(pts, view, glob)
         shard = plans.get("_shard")
         sv, sg = replicated_to_local(sv, shard), replicated_to_local(sg, shard)
@@ -654,8 +657,9 @@ class GraphAttnSfMNet(Module):
             if P.is_cuda and P.shape[1] == 32 and fgu.fusable():
                 # raw (un-normalised) projection features (graph_attn_sfm.py:141-148): no LN prologue
                 W, b = fgu.lin_l_stack()
-                XL, _ = EdgePrologueFn.apply(P.contiguous(), None, None, W, b, None, 1e-5)
-                pts, view, _ = fgu.forward_fused(XL, plans, *args)
+                pos = plans["proj2scenepoint"].pos
+                XL, _ = EdgePrologueFn.apply(P.contiguous(), None, None, W, b, None, 1e-5, pos)
+                pts, view, _ = fgu.forward_fused(XL, plans, *args, xl_sorted=pos is not None)
             else:
                 pts, view, _ = fgu.forward_plan(P, plans, *args)
         return P, pts, view

@@ -119,7 +119,9 @@ int gasfm_gat_attn_combine(const gasfm_combine_item* combine, int32_t n_combine,
  * items; merge with gasfm_gat_attn_bwd_combine) and one partial row per
  * wave into datt_part[n_waves, 2*H*C] = [d att | d bias] (n_waves from
  * gasfm_gat_attn_bwd_waves(), which sizes the grid from the current device's
- * occupancy for this (H, C); reduce with gasfm_colsum). */
+ * occupancy for this (H, C); reduce with gasfm_colsum).  xl_by_position != 0:
+ * XL rows are stored in segment order (row j, as the forward reads them with
+ * perm = NULL) while dXL is still written at row perm[j] (edge order). */
 int gasfm_gat_attn_bwd_waves(int32_t n_items, int32_t H, int32_t C);
 int gasfm_gat_attn_bwd(const float* XL, int64_t ldXL,
                        const float* XR, int64_t ldXR,
@@ -133,7 +135,7 @@ int gasfm_gat_attn_bwd(const float* XL, int64_t ldXL,
                        float* dXL, int64_t ldDXL,
                        float* dXR, int64_t ldDXR,
                        float* part_dxr, float* datt_part,
-                       void* stream);
+                       int32_t xl_by_position, void* stream);
 
 /* dXR[seg] = sum_k part_dxr[slot_begin + k*slot_stride]  (ordered). */
 int gasfm_gat_attn_bwd_combine(const gasfm_combine_item* combine, int32_t n_combine,
@@ -155,9 +157,13 @@ int gasfm_edge_part_floats(int32_t which, int64_t E, int32_t n_items);
 
 /* XL[e] = W relu(LN(P[e])) + b  (ln_w == NULL: XL[e] = W P[e] + b, the final update).
  * Replaces LayerNorm+ReLU (layers.py:232-234) and both GATv2 lin_l on the edge rows
- * (layers.py:329, 426; PyG evaluates them on all E+N rows). W = [Wl_point; Wl_camera] [64x32]. */
+ * (layers.py:329, 426; PyG evaluates them on all E+N rows). W = [Wl_point; Wl_camera] [64x32].
+ * pos != NULL: the point half (columns 0..31) of edge e is written to row pos[e] (its position
+ * in point-segment order), so the point-direction attention streams it (perm = NULL forward,
+ * xl_by_position backward); the camera half stays at row e. */
 int gasfm_edge_prologue_fwd(const float* P, int64_t E, const float* ln_w, const float* ln_b, float eps,
-                            const float* W, const float* b, float* Y, int64_t ldY, void* stream);
+                            const float* W, const float* b, float* Y, int64_t ldY, const int32_t* pos,
+                            void* stream);
 
 /* P'[e] = P[e] + scale*(Wp [relu(LN(P[e])) | P0[e]] + bp + Sp[pt[e]] + Sv[cam[e]] + Sg)
  * (GraphAttnSfMProjectionFeatureUpdate.forward, layers.py:927-945, + residual 254-261;

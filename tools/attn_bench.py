@@ -44,20 +44,21 @@ def main():
     XL64 = torch.randn((E, 64), device=dev, generator=g)
     att = torch.randn((1, H, HC // H), device=dev, generator=g) * 0.3
     bias = torch.randn(HC, device=dev, generator=g)
-    for name, col in (("proj2scenepoint", 0), ("proj2view", 32)):
+    for name, col, srt in (("proj2scenepoint", 0, False), ("proj2scenepoint", 0, True), ("proj2view", 32, False)):
         plan = data.graph_wrappers[name].plan
         N = plan.num_targets
         XL = XL64[:, col:col + HC]
         XR = torch.randn((N, HC), device=dev, generator=g)
-        out, smax, ssum = attn_forward_raw(XL, XR, att, bias, plan, H, 0.2)
+        out, smax, ssum = attn_forward_raw(XL, XR, att, bias, plan, H, 0.2, xl_sorted=srt)
         gout = torch.randn_like(out)
-        t_f = _time(lambda: attn_forward_raw(XL, XR, att, bias, plan, H, 0.2), args.reps)
-        t_b = _time(lambda: attn_backward_raw(XL, XR, att, bias, plan, H, 0.2, out, smax, ssum, gout),
-                    args.reps)
-        perm = plan.perm is not None
+        t_f = _time(lambda: attn_forward_raw(XL, XR, att, bias, plan, H, 0.2, xl_sorted=srt), args.reps)
+        t_b = _time(lambda: attn_backward_raw(XL, XR, att, bias, plan, H, 0.2, out, smax, ssum, gout,
+                                              xl_sorted=srt), args.reps)
+        perm = plan.perm is not None and not srt
         fwd_bytes = E * 4 * HC + E * 4 * perm + 2 * N * 4 * HC + N * 8 * H + (N + 1) * 4
         bwd_bytes = 2 * E * 4 * HC + E * 4 * perm + N * (3 * 4 * HC + 8 * H) + (N + 1) * 4
-        print(json.dumps({"direction": name, "waves": os.environ.get("GASFM_ATTN_WAVES", "default"),
+        label = name + (" (XL in segment order)" if srt else "")
+        print(json.dumps({"direction": label, "waves": os.environ.get("GASFM_ATTN_WAVES", "default"),
                           "n_items": plan.n_items, "fwd_us": round(t_f, 1),
                           "fwd_GBps": round(fwd_bytes / t_f / 1e3, 1), "bwd_us": round(t_b, 1),
                           "bwd_GBps": round(bwd_bytes / t_b / 1e3, 1)}), flush=True)
