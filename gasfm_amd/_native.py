@@ -63,11 +63,12 @@ def lib():
     """Load libgasfm.so (raising loudly if absent)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB):
+        path = os.environ.get("GASFM_LIB") or LIB  # GASFM_LIB: an A/B build variant (build.build(out=...))
+        if not os.path.exists(path):
             raise ImportError(
-                f"gasfm native library not built: {LIB} missing. Run `python -m gasfm_amd.build` "
+                f"gasfm native library not built: {path} missing. Run `python -m gasfm_amd.build` "
                 "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
-        L = ctypes.CDLL(LIB)
+        L = ctypes.CDLL(path)
         for name, (res, args) in _SIGS.items():
             fn = getattr(L, name)
             fn.restype = res

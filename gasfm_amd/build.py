@@ -29,17 +29,23 @@ def _stale():
     return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
 
 
-def build(force=False, verbose=False):
-    if not force and not _stale():
+def build(force=False, verbose=False, defines=(), out=None):
+    """Compile and link libgasfm.so.  ``defines``/``out`` build an A/B variant (e.g.
+    ``defines=["GASFM_FWD_LOOKAHEAD=1"], out=".../libgasfm_la.so"``) that ``GASFM_LIB``
+    selects at load time; the default library is untouched."""
+    lib = out or LIB
+    if out is None and not force and not _stale():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     objs = []
-    build_dir = os.path.join(HERE, "_build")
+    tag = "" if out is None else "_" + os.path.splitext(os.path.basename(out))[0]
+    build_dir = os.path.join(HERE, "_build" + tag)
     os.makedirs(build_dir, exist_ok=True)
     procs = []
     for src in sources():
         obj = os.path.join(build_dir, os.path.basename(src) + ".o")
         cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-c", src, "-o", obj]
+        cmd += [f"-D{d}" for d in defines]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
@@ -48,13 +54,13 @@ def build(force=False, verbose=False):
         out, _ = p.communicate()
         if p.returncode != 0:
             raise RuntimeError(f"hipcc failed on {src}:\n{out.decode(errors='replace')}")
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     if r.returncode != 0:
         raise RuntimeError("link failed:\n" + r.stdout.decode(errors="replace"))
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":

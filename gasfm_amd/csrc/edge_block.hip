@@ -52,7 +52,8 @@ constexpr int kMaxGrid = 2048;   // workgroups for the grid-stride kernels
 template <bool LN>
 __device__ __forceinline__ void load_norm_tile(const float* __restrict__ P, int64_t row0, int nrows,
                                                const float* __restrict__ gam, const float* __restrict__ bet,
-                                               float eps, float* Xh, float* Ph, float* Raw, float* Rs, int lane) {
+                                               float eps, float* Xh, float* Ph, float* Raw, float* Rs, int lane,
+                                               float4* raw_regs = nullptr) {
   const int c = (lane & 7) * 4;
   float4 g4 = make_float4(1.f, 1.f, 1.f, 1.f), b4 = make_float4(0.f, 0.f, 0.f, 0.f);
   if (LN && Ph) {
@@ -64,6 +65,7 @@ __device__ __forceinline__ void load_norm_tile(const float* __restrict__ P, int6
   for (int u = 0; u < 2; ++u) {
     const int r = (lane >> 3) + 8 * u;
     v[u] = (r < nrows) ? *reinterpret_cast<const float4*>(P + (row0 + r) * F + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (raw_regs) raw_regs[u] = v[u];
   }
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -110,21 +112,29 @@ __global__ __launch_bounds__(kThreads) void edge_prologue_fwd_kernel(const float
                                                                     const float* __restrict__ b,
                                                                     float* __restrict__ Y, int64_t ldY,
                                                                     const int32_t* __restrict__ pos) {
+  constexpr int LD68 = 68;                   // 16-byte aligned rows for the float4 read-back
   __shared__ float Wt[F * LDW64];            // W^T: Wt[k][n] = W[n][k]
-  __shared__ float tiles[kWaves][TR * LD34];
+  __shared__ float tiles[kWaves][TR * LD34 + TR * LD68];
   for (int q = threadIdx.x; q < NX * F; q += kThreads) Wt[(q % F) * LDW64 + q / F] = W[q];
   __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
+  const int c4 = (lane & 15) * 4;            // row layout: row (lane>>4) + 4u, columns c4..c4+3
   float* T = tiles[wave];
-  float bias[4];
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) bias[nt] = b[nt * 16 + c];
+  float* Yt = T + TR * LD34;
+  const float4 bias = *reinterpret_cast<const float4*>(b + c4);
   const int64_t ntiles = (E + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWaves + wave, nw = int64_t(gridDim.x) * kWaves;
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row0 = t * TR;
     const int nrows = int(E - row0 < TR ? E - row0 : TR);
+    // destination rows first (the point half goes to the edge's position in point order)
+    int64_t dst[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = (lane >> 4) + 4 * u;
+      dst[u] = (pos && c4 < F && r < nrows) ? int64_t(pos[row0 + r]) : row0 + r;
+    }
     load_norm_tile<LN>(P, row0, nrows, gam, bet, eps, nullptr, T, nullptr, nullptr, lane);
     wave_sync();
     f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
@@ -134,17 +144,19 @@ __global__ __launch_bounds__(kThreads) void edge_prologue_fwd_kernel(const float
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma16(a, Wt[(4 * s + g) * LDW64 + nt * 16 + c], acc[nt]);
     }
+    // C layout -> LDS -> row layout: each store instruction writes whole 128-byte half rows
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int e = 4 * g + r;
-      if (e < nrows) {
-        // point half (columns 0..31) goes to the edge's position in point order when pos != null
-        float* yp = Y + (pos ? int64_t(pos[row0 + e]) : row0 + e) * ldY;
-        float* yc = Y + (row0 + e) * ldY;
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) yp[nt * 16 + c] = acc[nt][r] + bias[nt];
+      for (int nt = 0; nt < 4; ++nt) Yt[(4 * g + r) * LD68 + nt * 16 + c] = acc[nt][r];
+    wave_sync();
 #pragma unroll
-        for (int nt = 2; nt < 4; ++nt) yc[nt * 16 + c] = acc[nt][r] + bias[nt];
+    for (int u = 0; u < 4; ++u) {
+      const int r = (lane >> 4) + 4 * u;
+      if (r < nrows) {
+        const float4 y = *reinterpret_cast<const float4*>(Yt + r * LD68 + c4);
+        *reinterpret_cast<float4*>(Y + dst[u] * ldY + c4) =
+            make_float4(y.x + bias.x, y.y + bias.y, y.z + bias.z, y.w + bias.w);
       }
     }
     wave_sync();
@@ -160,36 +172,43 @@ __global__ __launch_bounds__(kThreads) void edge_epilogue_fwd_kernel(
     const int32_t* __restrict__ pt, int64_t E, const float* __restrict__ gam, const float* __restrict__ bet,
     float eps, const float* __restrict__ Wp, int ldWp, const float* __restrict__ bp, const float* __restrict__ Sp,
     const float* __restrict__ Sv, const float* __restrict__ Sg, float scale, float* __restrict__ Pout) {
+  constexpr int LD36 = 36;                   // 16-byte aligned rows for the float4 read-back
   __shared__ float Wt[F * LDW];              // Wt[k][n] = Wp[n][k], k < 32
-  __shared__ float tiles[kWaves][2 * TR * LD34 + 2 * TR];
-  __shared__ int32_t idx[kWaves][2 * TR];
+  __shared__ float tiles[kWaves][TR * LD34 + TR * LD36];
   for (int q = threadIdx.x; q < F * F; q += kThreads) Wt[(q % F) * LDW + q / F] = Wp[(q / F) * ldWp + q % F];
   __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
+  const int cc = (lane & 7) * 4;             // row layout: row (lane>>3) + 8u, columns cc..cc+3
   float* Ph = tiles[wave];
-  float* Raw = Ph + TR * LD34;
-  float* Q0 = Raw + TR * LD34;
-  int32_t* ix = idx[wave];
-  float w32[2], w33[2], cst[2];
+  float* Yt = Ph + TR * LD34;
+  float w32[4], w33[4], cst[4];
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const int j = nt * 16 + c;
-    w32[nt] = P0 ? Wp[j * ldWp + 32] : 0.f;
-    w33[nt] = P0 ? Wp[j * ldWp + 33] : 0.f;
-    cst[nt] = bp[j] + Sg[j];
+  for (int k = 0; k < 4; ++k) {
+    const int j = cc + k;
+    w32[k] = P0 ? Wp[j * ldWp + 32] : 0.f;
+    w33[k] = P0 ? Wp[j * ldWp + 33] : 0.f;
+    cst[k] = bp[j] + Sg[j];
   }
   const int64_t ntiles = (E + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWaves + wave, nw = int64_t(gridDim.x) * kWaves;
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row0 = t * TR;
     const int nrows = int(E - row0 < TR ? E - row0 : TR);
-    load_norm_tile<true>(P, row0, nrows, gam, bet, eps, nullptr, Ph, Raw, nullptr, lane);
-    if (P0 && lane < 2 * TR) Q0[lane] = (lane < 2 * nrows) ? P0[row0 * 2 + lane] : 0.f;
-    if (lane < 2 * TR) {
-      const int e = lane & 15;
-      ix[lane] = (e < nrows) ? (lane < TR ? cam[row0 + e] : pt[row0 + e]) : 0;
+    // node-term gathers first: their latency overlaps the LayerNorm and the MFMA
+    float4 sp[2], sv[2];
+    float2 q0[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = (lane >> 3) + 8 * u;
+      const bool live = r < nrows;
+      const int64_t ci = live ? cam[row0 + r] : 0, pi = live ? pt[row0 + r] : 0;
+      sp[u] = *reinterpret_cast<const float4*>(Sp + pi * F + cc);
+      sv[u] = *reinterpret_cast<const float4*>(Sv + ci * F + cc);
+      q0[u] = (P0 && live) ? *reinterpret_cast<const float2*>(P0 + (row0 + r) * 2) : make_float2(0.f, 0.f);
     }
+    float4 raw[2];
+    load_norm_tile<true>(P, row0, nrows, gam, bet, eps, nullptr, Ph, nullptr, nullptr, lane, raw);
     wave_sync();
     f32x4 acc[2] = {zero4(), zero4()};
 #pragma unroll
@@ -198,19 +217,29 @@ __global__ __launch_bounds__(kThreads) void edge_epilogue_fwd_kernel(
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma16(a, Wt[(4 * s + g) * LDW + nt * 16 + c], acc[nt]);
     }
+    // C layout -> LDS -> row layout: full 128-byte rows per store
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int e = 4 * g + r;
-      if (e < nrows) {
-        const int64_t vr = int64_t(ix[e]) * F, pr = int64_t(ix[TR + e]) * F;
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const int j = nt * 16 + c;
-          float y = acc[nt][r] + cst[nt];
-          if (P0) y = fmaf(w32[nt], Q0[2 * e], fmaf(w33[nt], Q0[2 * e + 1], y));
-          y += Sp[pr + j] + Sv[vr + j];
-          Pout[(row0 + e) * F + j] = fmaf(y, scale, Raw[e * LD34 + j]);
+      for (int nt = 0; nt < 2; ++nt) Yt[(4 * g + r) * LD36 + nt * 16 + c] = acc[nt][r];
+    wave_sync();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = (lane >> 3) + 8 * u;
+      if (r < nrows) {
+        const float4 y = *reinterpret_cast<const float4*>(Yt + r * LD36 + cc);
+        const float yy[4] = {y.x, y.y, y.z, y.w};
+        const float spv[4] = {sp[u].x, sp[u].y, sp[u].z, sp[u].w}, svv[4] = {sv[u].x, sv[u].y, sv[u].z, sv[u].w};
+        const float rw[4] = {raw[u].x, raw[u].y, raw[u].z, raw[u].w};
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float d = yy[k] + cst[k];
+          if (P0) d = fmaf(w32[k], q0[u].x, fmaf(w33[k], q0[u].y, d));
+          d += spv[k] + svv[k];
+          o[k] = fmaf(d, scale, rw[k]);
         }
+        *reinterpret_cast<float4*>(Pout + (row0 + r) * F + cc) = make_float4(o[0], o[1], o[2], o[3]);
       }
     }
     wave_sync();
@@ -554,8 +583,8 @@ extern "C" int gasfm_edge_prologue_fwd(const float* P, int64_t E, const float* l
                                        float eps, const float* W, const float* b, float* Y, int64_t ldY,
                                        const int32_t* pos, void* stream) {
   GASFM_REQUIRE(E >= 0 && P && W && b && Y, "gasfm_edge_prologue_fwd: bad args");
-  GASFM_REQUIRE(ldY >= NX, "gasfm_edge_prologue_fwd: ldY < 64");
-  GASFM_REQUIRE(aligned16(P), "gasfm_edge_prologue_fwd: P not 16-byte aligned");
+  GASFM_REQUIRE(ldY >= NX && ldY % 4 == 0, "gasfm_edge_prologue_fwd: ldY < 64 or not a multiple of 4");
+  GASFM_REQUIRE(aligned16(P) && aligned16(Y) && aligned16(b), "gasfm_edge_prologue_fwd: P/Y/b not 16-byte aligned");
   if (E == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (ln_w)
@@ -574,7 +603,9 @@ extern "C" int gasfm_edge_epilogue_fwd(const float* P, const float* P0, const in
   GASFM_REQUIRE(E >= 0 && P && cam && pt && ln_w && ln_b && Wp && bp && Sp && Sv && Sg && Pout,
                 "gasfm_edge_epilogue_fwd: null pointer");
   GASFM_REQUIRE((P0 && ldWp == 34) || (!P0 && ldWp == 32), "gasfm_edge_epilogue_fwd: ldWp=%d vs P0", ldWp);
-  GASFM_REQUIRE(aligned16(P), "gasfm_edge_epilogue_fwd: P not 16-byte aligned");
+  GASFM_REQUIRE(aligned16(P) && aligned16(Sp) && aligned16(Sv) && aligned16(Pout) &&
+                    (!P0 || reinterpret_cast<uintptr_t>(P0) % 8 == 0),
+                "gasfm_edge_epilogue_fwd: P/Sp/Sv/Pout not 16-byte aligned (P0 8-byte)");
   if (E == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(edge_epilogue_fwd_kernel, dim3(grid_tiles(E)), dim3(kThreads), 0, st, P, P0, cam, pt, E, ln_w,

@@ -127,8 +127,16 @@ __device__ __forceinline__ int wave_id_uniform() {
 // ------------------------------------------------------------------------------------------
 // forward
 // ------------------------------------------------------------------------------------------
+#ifndef GASFM_FWD_LOOKAHEAD
+#define GASFM_FWD_LOOKAHEAD 0
+#endif
+#ifndef GASFM_FWD_MINWAVES
+#define GASFM_FWD_MINWAVES 1
+#endif
+constexpr bool kFwdLookahead = GASFM_FWD_LOOKAHEAD != 0;
+
 template <class G>
-__global__ __launch_bounds__(kBlock) void attn_fwd_kernel(
+__global__ __launch_bounds__(kBlock, GASFM_FWD_MINWAVES) void attn_fwd_kernel(
     const float* __restrict__ XL, int64_t ldXL, const float* __restrict__ XR, int64_t ldXR,
     const float* __restrict__ att, const float* __restrict__ bias, const int32_t* __restrict__ perm,
     const gasfm_work_item* __restrict__ items, int n_items, float slope, int finalize,
@@ -144,10 +152,57 @@ __global__ __launch_bounds__(kBlock) void attn_fwd_kernel(
   float attv[G::VEC];
   load_vec<G::VEC>(attv, att + f0);
 
-  for (int it = wave_id_uniform(); it < n_items; it += nwaves) {
-    const gasfm_work_item w = items[it];
-    float xr[G::VEC];
-    load_vec<G::VEC>(xr, XR + int64_t(w.seg) * ldXR + f0);
+  // Chunk = EPR*U consecutive edges of an item (row `row` of the wave takes u*EPR + row).
+  auto load_chunk = [&](int e0, int end, float (&xl)[G::U][G::VEC], bool (&valid)[G::U]) {
+#pragma unroll
+    for (int u = 0; u < G::U; ++u) {
+      const int e = e0 + u * G::EPR + row;
+      valid[u] = e < end;
+      if (valid[u]) {
+        const int64_t src = perm ? int64_t(perm[e]) : int64_t(e);
+        load_vec<G::VEC>(xl[u], XL + src * ldXL + f0);
+      } else {
+#pragma unroll
+        for (int v = 0; v < G::VEC; ++v) xl[u][v] = 0.f;
+      }
+    }
+  };
+
+  // One-item lookahead: the next item's XR row and first chunk are requested before the
+  // current item is reduced and stored, so every wave keeps loads in flight across items
+  // (point segments average ~20 edges: one chunk per item).
+  int it = wave_id_uniform();
+  gasfm_work_item wn{0, 0, 0, -1};
+  float xrn[G::VEC], xln[G::U][G::VEC];
+  bool validn[G::U];
+  if (kFwdLookahead && it < n_items) {
+    wn = items[it];
+    load_vec<G::VEC>(xrn, XR + int64_t(wn.seg) * ldXR + f0);
+    load_chunk(wn.begin, wn.end, xln, validn);
+  }
+  for (; it < n_items; it += nwaves) {
+    gasfm_work_item w;
+    float xr[G::VEC], xl[G::U][G::VEC];
+    bool valid[G::U];
+    if constexpr (kFwdLookahead) {
+      w = wn;
+#pragma unroll
+      for (int v = 0; v < G::VEC; ++v) xr[v] = xrn[v];
+#pragma unroll
+      for (int u = 0; u < G::U; ++u) {
+        valid[u] = validn[u];
+#pragma unroll
+        for (int v = 0; v < G::VEC; ++v) xl[u][v] = xln[u][v];
+      }
+      if (it + nwaves < n_items) {
+        wn = items[it + nwaves];
+        load_vec<G::VEC>(xrn, XR + int64_t(wn.seg) * ldXR + f0);
+        load_chunk(wn.begin, wn.end, xln, validn);
+      }
+    } else {
+      w = items[it];
+      load_vec<G::VEC>(xr, XR + int64_t(w.seg) * ldXR + f0);
+    }
 
     float m[G::HPL], s[G::HPL], acc[G::VEC];
 #pragma unroll
@@ -159,20 +214,7 @@ __global__ __launch_bounds__(kBlock) void attn_fwd_kernel(
     for (int v = 0; v < G::VEC; ++v) acc[v] = 0.f;
 
     for (int e0 = w.begin; e0 < w.end; e0 += G::EPR * G::U) {
-      float xl[G::U][G::VEC];
-      bool valid[G::U];
-#pragma unroll
-      for (int u = 0; u < G::U; ++u) {
-        const int e = e0 + u * G::EPR + row;
-        valid[u] = e < w.end;
-        if (valid[u]) {
-          const int64_t src = perm ? int64_t(perm[e]) : int64_t(e);
-          load_vec<G::VEC>(xl[u], XL + src * ldXL + f0);
-        } else {
-#pragma unroll
-          for (int v = 0; v < G::VEC; ++v) xl[u][v] = 0.f;
-        }
-      }
+      if (!kFwdLookahead || e0 != w.begin) load_chunk(e0, w.end, xl, valid);
       // logits for the U rows, per held head
       float lg[G::U][G::HPL];
 #pragma unroll
