@@ -363,8 +363,42 @@ __global__ __launch_bounds__(kThreads) void edge_epilogue_bwd_kernel(
 // edge_prologue_bwd: dP = LN_bwd(mask * (W^T dXL + scale Wp[:, :32]^T dRes)) + dRes
 // part layout per workgroup: [64*32 dW][64 db][32 dgamma][32 dbeta]
 // =====================================================================================
-constexpr int PB_WAVE = TR * LD66 + 2 * TR * LD34 + TR;  // dXL, x_hat, dRes tiles + rstd
+constexpr int PB_WAVE = TR * LD66 + 2 * TR * LD34 + TR;  // dXL, x_hat (then dP), dRes tiles + rstd
 constexpr int PB_W = NX * LDW + F * LDW;                  // W [64 x 32], scale*Wp [32 x 32]
+
+// Register copy of one prologue_bwd tile: dXL 16x64 (lane row (l>>4)+4u, cols 4(l&15)), P and
+// dRes 16x32 (lane row (l>>3)+8u, cols 4(l&7)).  The next tile's copy is requested before the
+// current tile's MFMA work, so every wave keeps its loads in flight through its compute.
+struct PbTile {
+  float4 x[4], p[2], d[2];
+};
+
+template <bool RES>
+__device__ __forceinline__ void pb_issue(PbTile& T, const float* __restrict__ dXL, int64_t ldX,
+                                         const float* __restrict__ P, const float* __restrict__ dRes, int64_t row0,
+                                         int nrows, int lane) {
+  // Rows past the end re-read row 0 of the tile (always valid) and are zeroed afterwards: a
+  // conditional load would be lowered to a flat access through a pointer select.
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int r = (lane >> 4) + 4 * u;
+    const int rr = r < nrows ? r : 0;
+    T.x[u] = *reinterpret_cast<const float4*>(dXL + (row0 + rr) * ldX + (lane & 15) * 4);
+    if (r >= nrows) T.x[u] = z;
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int r = (lane >> 3) + 8 * u;
+    const int rr = r < nrows ? r : 0;
+    T.p[u] = *reinterpret_cast<const float4*>(P + (row0 + rr) * F + (lane & 7) * 4);
+    if (RES) T.d[u] = *reinterpret_cast<const float4*>(dRes + (row0 + rr) * F + (lane & 7) * 4);
+    if (r >= nrows) T.p[u] = T.d[u] = z;
+  }
+}
+
+__device__ __forceinline__ void st2(float* p, float a, float b) { *reinterpret_cast<float2*>(p) = make_float2(a, b); }
+
 template <bool LN, bool RES>
 __global__ __launch_bounds__(kThreads) void edge_prologue_bwd_kernel(
     const float* __restrict__ dXL, int64_t ldX, const float* __restrict__ P, const float* __restrict__ dRes,
@@ -380,10 +414,10 @@ __global__ __launch_bounds__(kThreads) void edge_prologue_bwd_kernel(
   __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
-  float* T1 = lds + PB_W + wave * PB_WAVE;  // dXL     16 x 66
-  float* T2 = T1 + TR * LD66;               // x_hat   16 x 34
-  float* T3 = T2 + TR * LD34;               // dRes    16 x 34
-  float* Rs = T3 + TR * LD34;               // rstd    16
+  float* T1 = lds + PB_W + wave * PB_WAVE;  // dXL            16 x 66
+  float* T2 = T1 + TR * LD66;               // x_hat -> dP    16 x 34
+  float* T3 = T2 + TR * LD34;               // dRes           16 x 34
+  float* Rs = T3 + TR * LD34;               // rstd           16
   float gi[2], bi[2];
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) {
@@ -396,12 +430,54 @@ __global__ __launch_bounds__(kThreads) void edge_prologue_bwd_kernel(
   float db[4] = {0.f, 0.f, 0.f, 0.f}, dg[2] = {0.f, 0.f}, dbt[2] = {0.f, 0.f};
   const int64_t ntiles = (E + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWaves + wave, nw = int64_t(gridDim.x) * kWaves;
+  auto rows_of = [&](int64_t t) { return int(E - t * TR < TR ? E - t * TR : TR); };
+  PbTile nxt;
+  if (gw < ntiles) pb_issue<RES>(nxt, dXL, ldX, P, dRes, gw * TR, rows_of(gw), lane);
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row0 = t * TR;
-    const int nrows = int(E - row0 < TR ? E - row0 : TR);
-    load_tile<NX, LD66>(dXL, ldX, row0, nrows, T1, lane);
-    load_norm_tile<LN>(P, row0, nrows, gam, bet, eps, T2, nullptr, nullptr, Rs, lane);
-    if (RES) load_tile<F, LD34>(dRes, F, row0, nrows, T3, lane);
+    const int nrows = rows_of(t);
+    // stage the current tile into LDS: dXL, x_hat (+ rstd), dRes
+    {
+      const PbTile& cur = nxt;  // consumed before the next pb_issue overwrites it
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float* d = T1 + ((lane >> 4) + 4 * u) * LD66 + (lane & 15) * 4;
+        st2(d, cur.x[u].x, cur.x[u].y);
+        st2(d + 2, cur.x[u].z, cur.x[u].w);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int r = (lane >> 3) + 8 * u;
+        const float x[4] = {cur.p[u].x, cur.p[u].y, cur.p[u].z, cur.p[u].w};
+        float mean = 0.f, rstd = 1.f;
+        if (LN) {
+          float sm = x[0] + x[1] + x[2] + x[3];
+          sm += __shfl_xor(sm, 1);
+          sm += __shfl_xor(sm, 2);
+          sm += __shfl_xor(sm, 4);
+          mean = sm * (1.f / F);
+          float q = 0.f;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) q = fmaf(x[k] - mean, x[k] - mean, q);
+          q += __shfl_xor(q, 1);
+          q += __shfl_xor(q, 2);
+          q += __shfl_xor(q, 4);
+          rstd = rsqrtf(q * (1.f / F) + eps);
+        }
+        const bool live = r < nrows;
+        float* d = T2 + r * LD34 + (lane & 7) * 4;
+        st2(d, live ? (x[0] - mean) * rstd : 0.f, live ? (x[1] - mean) * rstd : 0.f);
+        st2(d + 2, live ? (x[2] - mean) * rstd : 0.f, live ? (x[3] - mean) * rstd : 0.f);
+        if ((lane & 7) == 0) Rs[r] = rstd;
+        if (RES) {
+          float* q3 = T3 + r * LD34 + (lane & 7) * 4;
+          st2(q3, cur.d[u].x, cur.d[u].y);
+          st2(q3 + 2, cur.d[u].z, cur.d[u].w);
+        }
+      }
+    }
+    // request the next tile before this one's MFMA work
+    if (t + nw < ntiles) pb_issue<RES>(nxt, dXL, ldX, P, dRes, (t + nw) * TR, rows_of(t + nw), lane);
     wave_sync();
     // dP_hat (C layout: edge 4g+r, column nt*16+c) = dXL W (+ dRes scale Wp)
     f32x4 acc[2] = {zero4(), zero4()};
@@ -437,7 +513,8 @@ __global__ __launch_bounds__(kThreads) void edge_prologue_bwd_kernel(
         accW[mt][1] = mfma16(a, ph[1], accW[mt][1]);
       }
     }
-    // ReLU mask + LayerNorm backward in the C layout; row sums over 16 lanes x 2 column tiles
+    // ReLU mask + LayerNorm backward in the C layout; dx overwrites x_hat in place (each lane
+    // reads then writes only its own elements)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int e = 4 * g + r;
@@ -460,14 +537,29 @@ __global__ __launch_bounds__(kThreads) void edge_prologue_bwd_kernel(
         s1 = sum16(s1) * (1.f / F);
         s2 = sum16(s2) * (1.f / F);
       }
-      if (e < nrows) {
+      const float rs = Rs[e];
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const int j = nt * 16 + c;
-          float dx = LN ? Rs[e] * (gv[nt] - s1 - xh[nt] * s2) : gv[nt];
-          if (RES) dx += T3[e * LD34 + j];
-          dP[(row0 + e) * F + j] = dx;
+      for (int nt = 0; nt < 2; ++nt) T2[e * LD34 + nt * 16 + c] = LN ? rs * (gv[nt] - s1 - xh[nt] * s2) : gv[nt];
+    }
+    wave_sync();
+    // row layout: dP = dx (+ dRes), whole 128-byte rows per store
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = (lane >> 3) + 8 * u;
+      if (r < nrows) {
+        const int cc = (lane & 7) * 4;
+        const float2 a0 = *reinterpret_cast<const float2*>(T2 + r * LD34 + cc);
+        const float2 a1 = *reinterpret_cast<const float2*>(T2 + r * LD34 + cc + 2);
+        float4 o = make_float4(a0.x, a0.y, a1.x, a1.y);
+        if (RES) {
+          const float2 d0 = *reinterpret_cast<const float2*>(T3 + r * LD34 + cc);
+          const float2 d1 = *reinterpret_cast<const float2*>(T3 + r * LD34 + cc + 2);
+          o.x += d0.x;
+          o.y += d0.y;
+          o.z += d1.x;
+          o.w += d1.y;
         }
+        *reinterpret_cast<float4*>(dP + (row0 + r) * F + cc) = o;
       }
     }
     wave_sync();
@@ -635,8 +727,8 @@ extern "C" int gasfm_edge_prologue_bwd(const float* dXL, int64_t ldX, const floa
                                        void* stream) {
   GASFM_REQUIRE(dXL && P && W && dP && part && ldX >= NX, "gasfm_edge_prologue_bwd: bad args");
   GASFM_REQUIRE(!dRes || Wp, "gasfm_edge_prologue_bwd: dRes needs Wp");
-  GASFM_REQUIRE(aligned16(dXL) && ldX % 4 == 0 && aligned16(P) && (!dRes || aligned16(dRes)),
-                "gasfm_edge_prologue_bwd: dXL/P/dRes not 16-byte aligned");
+  GASFM_REQUIRE(aligned16(dXL) && ldX % 4 == 0 && aligned16(P) && (!dRes || aligned16(dRes)) && aligned16(dP),
+                "gasfm_edge_prologue_bwd: dXL/P/dRes/dP not 16-byte aligned");
   if (E == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int g = grid_tiles(E);
