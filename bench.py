@@ -38,6 +38,23 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1_pmc_attn_fwd.json")
+
+
+def pmc_traffic(E, N):
+    """HBM bytes per point-direction launch from the committed PMC pass (tools/pmc_traffic.sh:
+    2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction), when it was taken on this workload."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            r = json.load(f)
+    except (OSError, ValueError):
+        return None
+    w = r.get("workload", {})
+    if w.get("edges") != E or w.get("points") != N:
+        return None
+    return r["point"]["traffic_bytes"]
+
+
 def attn_fwd_bytes(E, N, H, HC, perm):
     """BASELINE.md algorithmic bytes of one fused edge-softmax + aggregation forward."""
     return E * 4 * HC + E * 4 * int(perm) + N * 4 * HC + N * 4 * HC + N * 8 * H + (N + 1) * 4
@@ -179,7 +196,10 @@ def main():
                        "parallelism": f"point-sharded x{world}" if world > 1 else "single GPU"},
             "roofline": {"kernel": "attn_fwd_kernel<32,8> point direction (proj2scenepoint), per launch",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                         "traffic": pmc_traffic(e_local, n_local),
+                         "traffic_source": "profiles/r1_pmc_attn_fwd.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                                           "passes of this bench, per launch)",
                          "algorithmic_bytes": bytes_per_launch, "mean_us": kern_ms * 1e3 if kern_ms else None,
                          "launches_timed": len(timer.events)},
             "cpu_baseline": cpu,
