@@ -97,7 +97,8 @@ def main():
     ap.add_argument("--n", type=int, default=200_000)
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-scale", type=float, default=0.05)
+    ap.add_argument("--eager", action="store_true", help="launch every kernel from Python (no hipGraph)")
+    ap.add_argument("--cpu-sample-scale", type=float, default=0.1)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -132,31 +133,44 @@ def main():
     cX = torch.randn((4, sc.n), generator=gen).to(dev)
     log(f"[rank {rank}] scene m={sc.m} n={sc.n} E={E} built+moved in {time.time() - t0:.1f}s")
 
-    def step():
+    cx = cX if world == 1 else cX[:, data.point_slice].contiguous()
+
+    def fwd_bwd():
         pred = model(data)
-        ps, pts = pred["Ps_norm"], pred["pts3D"]
-        cx = cX if world == 1 else cX[:, data.point_slice]
         # replicated outputs enter every rank's loss in full, local points once (distributed.py)
-        loss = (ps * cP).sum() + (pts * cx).sum()
+        loss = (pred["Ps_norm"] * cP).sum() + (pred["pts3D"] * cx).sum()
         loss.backward()
         if world > 1:
             model.sync_grads()
-        for p in model.parameters():
-            p.grad = None
+        return loss
 
-    for _ in range(args.warmup):
-        step()
-    timer = attention.KernelTimer(lambda tag, HC: tag == "proj2scenepoint" and HC == 32)
-    attention.KERNEL_TIMER = timer
+    from gasfm_amd.graph_step import CapturedStep
+    if args.eager:
+        for _ in range(args.warmup):
+            fwd_bwd()
+            for p in model.parameters():
+                p.grad = None
+
+        def step():
+            fwd_bwd()
+            for p in model.parameters():
+                p.grad = None
+        execution = "eager (one Python/autograd launch per kernel)"
+    else:
+        # warm-up steps run inside CapturedStep (before capture); every timed step replays
+        # the captured forward+backward (+ gradient all-reduce) as one hipGraph launch
+        captured = CapturedStep(fwd_bwd, model.parameters(), warmup=args.warmup)
+        step = captured
+        execution = ("hipGraph replay of the captured forward+backward step" if captured.captured
+                     else f"eager fallback ({captured.fallback_reason})")
+        log(f"[rank {rank}] {execution}")
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    timer.enabled = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    timer.enabled = False
     if world > 1:
         torch.distributed.barrier()
     dt = time.perf_counter() - t0
@@ -164,6 +178,16 @@ def main():
         t = torch.tensor([dt], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
+    # roofline kernel: HIP events around each point-direction attention forward launch on its
+    # stream, in eager steps right after the timed region (events cannot be read out of a
+    # replayed graph); same kernel, same inputs
+    timer = attention.KernelTimer(lambda tag, HC: tag == "proj2scenepoint" and HC == 32)
+    attention.KERNEL_TIMER = timer
+    timer.enabled = True
+    for _ in range(2):
+        fwd_bwd()
+    timer.enabled = False
+    attention.KERNEL_TIMER = None
     kern_ms = timer.mean_ms()
     plan = data.graph_wrappers["proj2scenepoint"].plan
     e_local = plan.num_edges
@@ -201,7 +225,9 @@ def main():
                          "traffic_source": "profiles/r1_pmc_attn_fwd.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                                            "passes of this bench, per launch)",
                          "algorithmic_bytes": bytes_per_launch, "mean_us": kern_ms * 1e3 if kern_ms else None,
-                         "launches_timed": len(timer.events)},
+                         "launches_timed": len(timer.events),
+                         "timing": "HIP events per launch, 2 eager steps after the timed region"},
+            "execution": execution,
             "cpu_baseline": cpu,
         }
         print(json.dumps(res), flush=True)

@@ -52,6 +52,9 @@ _SIGS = {
                                         _vp, _vp, _vp]),
     "gasfm_edge0_prologue_bwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
     "gasfm_node_part_rows": (_i32, [_i64]),
+    "gasfm_gvec_fwd": (_i32, [_vp, _i32, _vp, _vp, _f32, _vp, _vp, _i32, _vp, _vp, _vp]),
+    "gasfm_gvec_bwd_chunks": (_i32, [_i32]),
+    "gasfm_gvec_bwd": (_i32, [_vp, _vp, _i32, _vp, _vp, _f32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_node_ln_linear_fwd": (_i32, [_vp, _i64, _i32, _vp, _vp, _f32, _vp, _vp, _i32, _i32, _vp, _i64, _vp]),
     "gasfm_node_ln_linear_bwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp, _f32, _vp, _i32, _i32, _vp, _vp, _vp]),
 }
@@ -288,3 +291,23 @@ def node_ln_linear_bwd(dY, X, ln_w, ln_b, eps, W, residual, dX, part):
     st = lib().gasfm_node_ln_linear_bwd(_p(dY), _p(X), N, n_in, _p(ln_w), _p(ln_b), eps, _p(W), W.shape[0],
                                         int(residual), _p(dX), _p(part), _stream(X))
     check(st, "gasfm_node_ln_linear_bwd")
+
+
+# ---------------------------------------------------------------- global node (one row)
+def gvec_bwd_chunks(N):
+    return lib().gasfm_gvec_bwd_chunks(N)
+
+
+def gvec_fwd(x, ln_w, ln_b, eps, W, b, res, y):
+    _req(x, "x")
+    _req(W, "W")
+    st = lib().gasfm_gvec_fwd(_p(x), W.shape[1], _p(ln_w), _p(ln_b), eps, _p(W), _p(b), W.shape[0], _p(res), _p(y),
+                              _stream(x))
+    check(st, "gasfm_gvec_fwd")
+
+
+def gvec_bwd(dy, x, ln_w, ln_b, eps, W, resid, dx, dW, db, dgam, dbet, part):
+    _req(dy, "dy")
+    st = lib().gasfm_gvec_bwd(_p(dy), _p(x), W.shape[1], _p(ln_w), _p(ln_b), eps, _p(W), W.shape[0], int(resid),
+                              _p(dx), _p(dW), _p(db), _p(dgam), _p(dbet), _p(part), _stream(x))
+    check(st, "gasfm_gvec_bwd")

@@ -49,23 +49,29 @@ constexpr int kMaxGrid = 2048;   // workgroups for the grid-stride kernels
 // k + 8u (u = 0, 1).  Per row LayerNorm statistics by 3 xor-shuffles.  Writes x_hat
 // (pre-affine; identity when !LN) to Xh, relu(x_hat*g+b) (x when !LN) to Ph, raw values
 // to Raw (each optional, stride 34) and rstd to Rs.  Rows >= nrows are zeros.
+// Row layout of a 16 x 32 tile: lane l holds row (l>>3) + 8u (u = 0, 1), columns 4(l&7)..+3.
+__device__ __forceinline__ void load_rows32(const float* __restrict__ P, int64_t row0, int nrows, float4 (&v)[2],
+                                            int lane) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int r = (lane >> 3) + 8 * u;
+    v[u] = *reinterpret_cast<const float4*>(P + (row0 + (r < nrows ? r : 0)) * F + (lane & 7) * 4);  // see load_tile
+    if (r >= nrows) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// LayerNorm of the row-layout registers v (rows >= nrows written as zeros): x_hat (pre-affine;
+// identity when !LN) to Xh, relu(x_hat*g+b) (x when !LN) to Ph, raw values to Raw (each
+// optional, LDS stride 34) and rstd to Rs.  Row statistics by 3 xor-shuffles over 8 lanes.
 template <bool LN>
-__device__ __forceinline__ void load_norm_tile(const float* __restrict__ P, int64_t row0, int nrows,
-                                               const float* __restrict__ gam, const float* __restrict__ bet,
-                                               float eps, float* Xh, float* Ph, float* Raw, float* Rs, int lane,
-                                               float4* raw_regs = nullptr) {
+__device__ __forceinline__ void norm_rows32(const float4 (&v)[2], int nrows, const float* __restrict__ gam,
+                                            const float* __restrict__ bet, float eps, float* Xh, float* Ph,
+                                            float* Raw, float* Rs, int lane) {
   const int c = (lane & 7) * 4;
   float4 g4 = make_float4(1.f, 1.f, 1.f, 1.f), b4 = make_float4(0.f, 0.f, 0.f, 0.f);
   if (LN && Ph) {
     g4 = *reinterpret_cast<const float4*>(gam + c);
     b4 = *reinterpret_cast<const float4*>(bet + c);
-  }
-  float4 v[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int r = (lane >> 3) + 8 * u;
-    v[u] = (r < nrows) ? *reinterpret_cast<const float4*>(P + (row0 + r) * F + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    if (raw_regs) raw_regs[u] = v[u];
   }
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -99,6 +105,20 @@ __device__ __forceinline__ void load_norm_tile(const float* __restrict__ P, int6
     }
     if (Rs && (lane & 7) == 0) Rs[r] = rstd;
   }
+}
+
+template <bool LN>
+__device__ __forceinline__ void load_norm_tile(const float* __restrict__ P, int64_t row0, int nrows,
+                                               const float* __restrict__ gam, const float* __restrict__ bet,
+                                               float eps, float* Xh, float* Ph, float* Raw, float* Rs, int lane,
+                                               float4* raw_regs = nullptr) {
+  float4 v[2];
+  load_rows32(P, row0, nrows, v, lane);
+  if (raw_regs) {
+    raw_regs[0] = v[0];
+    raw_regs[1] = v[1];
+  }
+  norm_rows32<LN>(v, nrows, gam, bet, eps, Xh, Ph, Raw, Rs, lane);
 }
 
 // =====================================================================================
@@ -265,23 +285,52 @@ __global__ __launch_bounds__(kThreads) void edge_epilogue_bwd_kernel(
   float* Q0 = Ph + TR * LD34;
   // dP0[e][c'] = sum_j d[e][j] Wp[j][32+c']: lane (e = c, group g) sums j in [8g, 8g+8)
   float w2[8][2];
+  if (P0) {  // wave-uniform: the 16 loads issue together
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int j = 8 * g + k;
-    w2[k][0] = P0 ? Wp[j * ldWp + 32] * scale : 0.f;
-    w2[k][1] = P0 ? Wp[j * ldWp + 33] * scale : 0.f;
+    for (int k = 0; k < 8; ++k) {
+      const int j = 8 * g + k;
+      w2[k][0] = Wp[j * ldWp + 32] * scale;
+      w2[k][1] = Wp[j * ldWp + 33] * scale;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w2[k][0] = w2[k][1] = 0.f;
   }
   f32x4 accW[2][2] = {{zero4(), zero4()}, {zero4(), zero4()}};
   float accP0[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+  // register copy of the next tile: dP' and P rows (row layout), P0 (lanes < 2*nrows)
+  float4 nd[2], np[2];
+  float nq = 0.f;
+  auto issue = [&](int64_t row0, int nrows) {
+    load_rows32(dPo, row0, nrows, nd, lane);
+    load_rows32(P, row0, nrows, np, lane);
+    if (P0) {
+      nq = P0[row0 * 2 + (lane < 2 * nrows ? lane : 0)];
+      if (lane >= 2 * nrows) nq = 0.f;
+    }
+  };
   const int gw = blockIdx.x * kWaves + wave, nw = gridDim.x * kWaves;
   for (int it = gw; it < n_items; it += nw) {
     const gasfm_work_item w = items[it];
     float dsv[2] = {0.f, 0.f};
+    if (w.begin < w.end) issue(w.begin, w.end - w.begin < TR ? w.end - w.begin : TR);
     for (int64_t row0 = w.begin; row0 < w.end; row0 += TR) {
       const int nrows = int(w.end - row0 < TR ? w.end - row0 : TR);
-      load_tile<F, LD34>(dPo, F, row0, nrows, D, lane);
-      load_norm_tile<true>(P, row0, nrows, gam, bet, eps, nullptr, Ph, nullptr, nullptr, lane);
-      if (P0 && lane < 2 * TR) Q0[lane] = (lane < 2 * nrows) ? P0[row0 * 2 + lane] : 0.f;
+      // stage the prefetched tile, then request the next one before the MFMA work
+      {
+        const int cc = (lane & 7) * 4;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          float* d = D + ((lane >> 3) + 8 * u) * LD34 + cc;
+          d[0] = nd[u].x;
+          d[1] = nd[u].y;
+          d[2] = nd[u].z;
+          d[3] = nd[u].w;
+        }
+        norm_rows32<true>(np, nrows, gam, bet, eps, nullptr, Ph, nullptr, nullptr, lane);
+        if (lane < 2 * TR) Q0[lane] = nq;
+      }
+      if (row0 + TR < w.end) issue(row0 + TR, w.end - (row0 + TR) < TR ? int(w.end - (row0 + TR)) : TR);
       wave_sync();
 #pragma unroll
       for (int s = 0; s < TR / 4; ++s) {
@@ -400,7 +449,10 @@ __device__ __forceinline__ void pb_issue(PbTile& T, const float* __restrict__ dX
 __device__ __forceinline__ void st2(float* p, float a, float b) { *reinterpret_cast<float2*>(p) = make_float2(a, b); }
 
 template <bool LN, bool RES>
-__global__ __launch_bounds__(kThreads) void edge_prologue_bwd_kernel(
+#ifndef GASFM_PBWD_MINWAVES
+#define GASFM_PBWD_MINWAVES 1
+#endif
+__global__ __launch_bounds__(kThreads, GASFM_PBWD_MINWAVES) void edge_prologue_bwd_kernel(
     const float* __restrict__ dXL, int64_t ldX, const float* __restrict__ P, const float* __restrict__ dRes,
     int64_t E, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
     const float* __restrict__ W, const float* __restrict__ Wp, int ldWp, float scale, float* __restrict__ dP,

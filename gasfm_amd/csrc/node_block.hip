@@ -51,7 +51,8 @@ __device__ __forceinline__ void load_ln64(const float* __restrict__ X, int64_t r
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int r = (lane >> 4) + 4 * u;
-    v[u] = (r < nrows) ? *reinterpret_cast<const float4*>(X + (row0 + r) * FI + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    v[u] = *reinterpret_cast<const float4*>(X + (row0 + (r < nrows ? r : 0)) * FI + c);  // see load_tile
+    if (r >= nrows) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {

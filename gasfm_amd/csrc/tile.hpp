@@ -45,7 +45,8 @@ __device__ __forceinline__ float sum_groups(float v) {
 }
 
 // Row-major [16 x W] tile from global (row stride ld floats, 16-byte aligned) into LDS (row
-// stride LDT); rows >= nrows are zeros.  All global loads are issued before the LDS stores.
+// stride LDT); rows >= nrows are zeros (nrows >= 1).  All global loads are issued before the
+// LDS stores.
 template <int W, int LDT>
 __device__ __forceinline__ void load_tile(const float* __restrict__ X, int64_t ld, int64_t row0, int nrows,
                                           float* T, int lane) {
@@ -56,7 +57,10 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ X, int64_t l
   for (int u = 0; u < STEPS; ++u) {
     const int q = lane + kW * u;
     const int r = q / V, c = (q % V) * 4;
-    v[u] = (r < nrows) ? *reinterpret_cast<const float4*>(X + (row0 + r) * ld + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    // unconditional load of an in-range row, then zero: a load under a per-element condition
+    // is branched around with a vmcnt(0) wait each, serialising the tile's loads
+    v[u] = *reinterpret_cast<const float4*>(X + (row0 + (r < nrows ? r : 0)) * ld + c);
+    if (r >= nrows) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 #pragma unroll
   for (int u = 0; u < STEPS; ++u) {

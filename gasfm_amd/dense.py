@@ -44,10 +44,66 @@ class RowLinearFn(torch.autograd.Function):
         return dx, dW, db
 
 
+class GlobalLinearFn(torch.autograd.Function):
+    """ONE row: y = W h + b (+ res, or + x when resid_x), h = relu(LN(x)) when ln_w is given.
+
+    The global node's GEMV chains (csrc/global_vec.hip): one kernel forward, a slab pass plus
+    a one-workgroup finish backward, instead of LayerNorm/clamp/M=1 GEMM/add kernels."""
+
+    @staticmethod
+    def forward(ctx, x, ln_w, ln_b, W, b, res, eps, resid_x):
+        from . import _native
+        x1 = x.reshape(-1).contiguous()
+        W = W.contiguous()
+        y = torch.empty((1, W.shape[0]), dtype=torch.float32, device=x.device)
+        r = x1 if resid_x else (res.reshape(-1).contiguous() if res is not None else None)
+        _native.gvec_fwd(x1, ln_w, ln_b, eps, W, b, r, y)
+        ctx.save_for_backward(x1, ln_w, ln_b, W)
+        ctx.eps, ctx.resid_x = eps, resid_x
+        ctx.has_b, ctx.has_res, ctx.x_shape = b is not None, res is not None, x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _native
+        x1, ln_w, ln_b, W = ctx.saved_tensors
+        N, K = W.shape
+        dy1 = dy.reshape(-1).contiguous()
+        dev = x1.device
+        f = dict(dtype=torch.float32, device=dev)
+        dx = torch.empty(K, **f)
+        dW = torch.empty_like(W)
+        db = torch.empty(N, **f) if ctx.has_b else None
+        dg = torch.empty(K, **f) if ln_w is not None else None
+        dbt = torch.empty(K, **f) if ln_w is not None else None
+        part = torch.empty((_native.gvec_bwd_chunks(N), K), **f)
+        _native.gvec_bwd(dy1, x1, ln_w, ln_b, ctx.eps, W, ctx.resid_x, dx, dW, db, dg, dbt, part)
+        dres = dy if ctx.has_res else None
+        return dx.view(ctx.x_shape), dg, dbt, dW, db, dres, None, None
+
+
+GVEC_MAX_K = 4096
+
+
+def _gvec_ok(x, k):
+    return (x.is_cuda and x.dim() == 2 and x.shape[0] == 1 and x.dtype == torch.float32 and k % 64 == 0
+            and k <= GVEC_MAX_K)
+
+
 def linear(x, lin):
+    if _gvec_ok(x, lin.in_features):
+        return GlobalLinearFn.apply(x, None, None, lin.weight, lin.bias, None, 0.0, False)
     if x.is_cuda and x.dim() == 2 and x.shape[0] >= SPLITK_MIN_ROWS and torch.is_grad_enabled():
         return RowLinearFn.apply(x, lin.weight, lin.bias)
     return F.linear(x, lin.weight, lin.bias)
+
+
+def linear_res(x, lin, res):
+    """lin(x) + res (res may be None)."""
+    if _gvec_ok(x, lin.in_features) and (res is None or res.numel() == lin.out_features):
+        return GlobalLinearFn.apply(x, None, None, lin.weight, lin.bias, res, 0.0, False)
+    y = linear(x, lin)
+    return y if res is None else res + y
 
 
 def layer_norm(x, ln):
@@ -100,23 +156,34 @@ def _node_fusable(x, ln, lin):
             and lin.in_features == NODE_WIDTH and lin.out_features in (32, 64))
 
 
+def _gvec_ln_ok(x, ln, lin, residual):
+    return (_gvec_ok(x, lin.in_features) and ln.weight is not None and ln.bias is not None
+            and tuple(ln.normalized_shape) == (lin.in_features,)
+            and (not residual or lin.out_features == lin.in_features))
+
+
 def ln_relu_linear(x, ln, lin, residual=False):
-    """lin(relu(ln(x))) (+ x when residual): the fused point-node kernel for 64-wide rows."""
+    """lin(relu(ln(x))) (+ x when residual): the fused point-node kernel for 64-wide rows, the
+    global-vector kernel for a single row."""
     if _node_fusable(x, ln, lin) and (not residual or lin.out_features == NODE_WIDTH):
         return NodeLnLinearFn.apply(x, ln.weight, ln.bias, lin.weight, lin.bias, ln.eps, residual)
+    if _gvec_ln_ok(x, ln, lin, residual):
+        return GlobalLinearFn.apply(x, ln.weight, ln.bias, lin.weight, lin.bias, None, ln.eps, residual)
     y = linear(F.relu(layer_norm(x, ln)), lin)
     return x + y if residual else y
 
 
 def sequential(seq, x):
     """Run a Sequential of Linear / LayerNorm / ReLU with the row-aware linear; a
-    LayerNorm, ReLU, Linear run on 64-wide point rows goes through the fused node kernel."""
+    LayerNorm, ReLU, Linear run on 64-wide point rows or on the single global row goes
+    through a fused kernel."""
     mods = list(seq)
     i = 0
     while i < len(mods):
         mod = mods[i]
         if (isinstance(mod, LayerNorm) and i + 2 < len(mods) and isinstance(mods[i + 1], ReLU)
-                and isinstance(mods[i + 2], Linear) and _node_fusable(x, mod, mods[i + 2])):
+                and isinstance(mods[i + 2], Linear)
+                and (_node_fusable(x, mod, mods[i + 2]) or _gvec_ln_ok(x, mod, mods[i + 2], False))):
             x = ln_relu_linear(x, mod, mods[i + 2])
             i += 3
             continue

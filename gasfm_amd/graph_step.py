@@ -1,0 +1,76 @@
+"""Whole-step HIP graph capture: one graph launch per forward+backward.
+
+A GASFM step issues ~2,700 kernel launches (12 blocks of attention, edge, node and dense
+camera/global work, forward and backward).  Issued eagerly through Python and autograd, the
+host needs ~47 ms per step to enqueue them, as long as the GPU needs to run them at config 4,
+and far longer than the GPU needs at the per-rank size of an 8-GPU run (measured by
+tools/step_overhead.py).  Capturing the step once (torch.cuda.CUDAGraph = hipGraph on ROCm)
+and replaying it removes the host cost and the per-launch gaps.
+
+Requirements, all met by the GASFM path: fixed shapes per scene (plans are built once and
+cached), no host synchronisation inside forward/backward (plan building happens in the warm-up
+steps), every HIP kernel launched on torch's current stream (libgasfm's launches take
+torch.cuda.current_stream()), and RCCL collectives captured by torch's ProcessGroupNCCL.
+
+Usage::
+
+    def fwd_bwd():                 # returns the loss; leaves gradients in p.grad
+        loss = loss_fn(model(data))
+        loss.backward()
+        return loss
+    step = CapturedStep(fwd_bwd, params=model.parameters())
+    loss = step()                  # replays the graph; p.grad holds this step's gradients
+"""
+import torch
+
+
+class CapturedStep:
+    def __init__(self, fn, params, warmup=3, check=True, rtol=1e-5):
+        self.fn = fn
+        self.params = list(params)
+        self.graph = None
+        self.static_out = None
+        self.fallback_reason = None
+        self._capture(warmup, check, rtol)
+
+    def _zero(self):
+        for p in self.params:
+            p.grad = None
+
+    def _capture(self, warmup, check, rtol):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # lazy initialisation (plans, workspaces, BLAS handles) off-capture
+            for _ in range(max(1, warmup)):
+                self._zero()
+                ref = self.fn().detach().clone()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self._zero()
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g):
+                out = self.fn()
+            g.replay()
+            torch.cuda.synchronize()
+        except RuntimeError as e:  # capture unsupported for some op: run eagerly
+            self.fallback_reason = f"capture failed: {e}"
+            torch.cuda.synchronize()
+            return
+        if check:
+            a, b = float(out.detach().double()), float(ref.double())
+            if not abs(a - b) <= rtol * max(1.0, abs(b)):
+                self.fallback_reason = f"replayed loss {a!r} != eager loss {b!r}"
+                return
+        self.graph, self.static_out = g, out
+
+    @property
+    def captured(self):
+        return self.graph is not None
+
+    def __call__(self):
+        if self.graph is None:
+            self._zero()
+            return self.fn()
+        self.graph.replay()
+        return self.static_out

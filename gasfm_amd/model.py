@@ -205,13 +205,15 @@ class ViewAndScenePoint2Global(Module):
                                            plan_s2g_partial, c.heads, c.negative_slope, shard)
         x = torch.cat([v2g, s2g], dim=1)
         if hasattr(self, "proj_view_and_scenepoint2global"):
-            x = self.proj_view_and_scenepoint2global(x)
-        if prev is not None:
+            x = dense.linear_res(x, self.proj_view_and_scenepoint2global, prev)
+        elif prev is not None:
             x = prev + x
+        if self.use_norm_pre_mlp and len(self.mlp) == 1:
+            return dense.ln_relu_linear(x, self.norm_pre_mlp, self.mlp[0], residual=True)
         skip = x
         if self.use_norm_pre_mlp:
-            x = F.relu(self.norm_pre_mlp(x))
-        return skip + self.mlp(x)
+            x = F.relu(dense.layer_norm(x, self.norm_pre_mlp))
+        return skip + dense.sequential(self.mlp, x)
 
 
 class _Global2Node(Module):

@@ -245,6 +245,28 @@ int gasfm_node_ln_linear_bwd(const float* dY, const float* X, int64_t N, int32_t
                              const float* ln_b, float eps, const float* W, int32_t n_out, int32_t residual,
                              float* dX, float* part, void* stream);
 
+/* ---- global node (ONE row): LayerNorm -> ReLU -> Linear (+ residual) ----
+ * Replaces the M = 1 aten chains on the global feature vector: norm_and_proj_global2view /
+ * _global2scenepoint (layers.py:497-520), both convs' lin_r on those rows (PyG),
+ * proj_view_and_scenepoint2global + g (layers.py:527-528, 590-592), the pre-MLP skip
+ * (layers.py:594-603) and lin_global of the projection update (layers.py:928-935).
+ * K (input width) must be a multiple of 64 and <= 4096. */
+
+/* y[i] = W[i,:] . h + b[i] (+ res[i]), h = relu(LN(x)) if ln_w else x.  x: [K], W: [N x K]
+ * row-major, b / res may be null. */
+int gasfm_gvec_fwd(const float* x, int32_t K, const float* ln_w, const float* ln_b, float eps,
+                   const float* W, const float* b, int32_t N, const float* res, float* y, void* stream);
+
+/* Rows of the partial buffer gasfm_gvec_bwd needs: part is [gasfm_gvec_bwd_chunks(N) x K]. */
+int gasfm_gvec_bwd_chunks(int32_t N);
+
+/* Backward of the above: dW = dy (x) h, db = dy (db may be null), dx = LN_bwd(mask * W^T dy)
+ * (+ dy when resid, i.e. the residual was x itself; needs N == K), dgamma, dbeta.  Two
+ * launches (slab pass + one-workgroup finish), deterministic. */
+int gasfm_gvec_bwd(const float* dy, const float* x, int32_t K, const float* ln_w, const float* ln_b,
+                   float eps, const float* W, int32_t N, int32_t resid, float* dx, float* dW, float* db,
+                   float* dgamma, float* dbeta, float* part, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,76 @@
+"""Single-row (global node) LayerNorm -> ReLU -> Linear (+ residual) kernels vs fp64 torch.
+
+Shapes are the ones GASFM's global node uses (csrc/global_vec.hip header) plus the reduced
+widths of the small test conf.  Tolerance: output elementwise 2e-5 * max|ref| + 1e-6;
+gradients normwise 1e-4 (fp32 reductions over up to 2048 terms).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from gasfm_amd import dense
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(2048, 1024), (2048, 64), (1024, 1024), (64, 64), (1088, 2048), (2048, 2048), (2048, 32), (128, 64),
+          (192, 128)]
+
+
+def _close(got, ref, name, tol=1e-4):
+    err = (got.double().cpu() - ref).norm().item()
+    assert err <= tol * ref.norm().item() + 1e-9, f"{name}: {err:.3e} vs |ref| {ref.norm().item():.3e}"
+
+
+@pytest.mark.parametrize("K,N", SHAPES)
+@pytest.mark.parametrize("mode", ["ln", "ln_resid", "plain", "plain_res"])
+def test_gvec_matches_fp64(device, K, N, mode):
+    if mode == "ln_resid" and K != N:
+        pytest.skip("residual of the input needs N == K")
+    g = torch.Generator().manual_seed(K * 3 + N)
+    x = torch.randn(1, K, generator=g, dtype=torch.float64) * 1.5 + 0.3
+    W = torch.randn(N, K, generator=g, dtype=torch.float64) / K ** 0.5
+    b = torch.randn(N, generator=g, dtype=torch.float64)
+    gam = 1 + 0.2 * torch.randn(K, generator=g, dtype=torch.float64)
+    bet = 0.1 * torch.randn(K, generator=g, dtype=torch.float64)
+    res = torch.randn(1, N, generator=g, dtype=torch.float64)
+    dy = torch.randn(1, N, generator=g, dtype=torch.float64)
+    use_ln = mode.startswith("ln")
+    leaves64 = [t.clone().requires_grad_(True) for t in (x, W, b, gam, bet, res)]
+    x6, W6, b6, g6, bt6, r6 = leaves64
+    h = F.relu(F.layer_norm(x6, (K,), g6, bt6, 1e-5)) if use_ln else x6
+    y64 = F.linear(h, W6, b6)
+    if mode == "ln_resid":
+        y64 = y64 + x6
+    if mode == "plain_res":
+        y64 = y64 + r6
+    y64.backward(dy)
+    leaves = [t.float().to(device).requires_grad_(True) for t in (x, W, b, gam, bet, res)]
+    xd, Wd, bd, gd, btd, rd = leaves
+    y = dense.GlobalLinearFn.apply(xd, gd if use_ln else None, btd if use_ln else None, Wd, bd,
+                                   rd if mode == "plain_res" else None, 1e-5, mode == "ln_resid")
+    y.backward(dy.float().to(device))
+    scale = y64.abs().max().item()
+    torch.testing.assert_close(y.double().cpu(), y64.detach(), rtol=0, atol=2e-5 * scale + 1e-6)
+    names = ["x", "W", "b", "gamma", "beta", "res"]
+    for nm, a, r in zip(names, leaves, leaves64):
+        if r.grad is None:
+            assert a.grad is None or a.grad.abs().max().item() == 0, nm
+            continue
+        _close(a.grad, r.grad, f"{mode} K={K} N={N} d{nm}")
+
+
+def test_gvec_dispatch_and_determinism(device):
+    ln = torch.nn.LayerNorm(2048).to(device)
+    lin = torch.nn.Linear(2048, 2048).to(device)
+    x = torch.randn(1, 2048, device=device, requires_grad=True)
+    outs = []
+    for _ in range(2):
+        x.grad = None
+        lin.zero_grad()
+        y = dense.ln_relu_linear(x, ln, lin, residual=True)
+        assert type(y.grad_fn).__name__ == "GlobalLinearFnBackward"
+        y.square().sum().backward()
+        outs.append((y.detach().clone(), x.grad.clone(), lin.weight.grad.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    torch.testing.assert_close(outs[0][0], x + lin(F.relu(ln(x))), rtol=1e-5, atol=1e-5)

@@ -1,0 +1,50 @@
+"""Kernel-time breakdown of ONE replayed step from a rocprofv3 kernel-trace database.
+
+usage: python tools/step_breakdown.py <run_results.db> [step_index]
+Steps are delimited by the block-0 prologue kernel (first kernel of every forward).
+"""
+import re
+import sqlite3
+import sys
+from collections import defaultdict
+
+CATS = [
+    ("edge kernels", r"edge_|edge0_|segment_rowsum"),
+    ("attention", r"attn_"),
+    ("node kernels", r"node_(fwd|bwd)"),
+    ("global vec", r"gvec_"),
+    ("colsum", r"colsum"),
+    ("hipBLASLt GEMM", r"^Cijk_"),
+    ("torch LayerNorm", r"layer_norm|GammaBeta|GradInput|cuComputePartGrad|cuComputeGrad"),
+    ("torch reduce", r"reduce_kernel"),
+    ("torch add", r"CUDAFunctor_add"),
+    ("torch fill/copy/cat", r"Fill|copyBuffer|fillBuffer|CatArray|direct_copy|copy_kernel"),
+    ("torch relu/threshold/mul", r"clamp|threshold|BinaryFunctor|MulFunctor|elementwise_kernel_manual"),
+]
+
+
+def main():
+    db = sys.argv[1]
+    k = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, start, end from kernels order by start").fetchall()
+    st = [i for i, r in enumerate(rows) if "edge0_prologue_fwd" in r[0]]
+    seg = rows[st[k]:st[k + 1]]
+    tot = defaultdict(float)
+    cnt = defaultdict(int)
+    for n, s, e in seg:
+        for cat, pat in CATS:
+            if re.search(pat, n):
+                break
+        else:
+            cat = "other: " + re.sub(r"\(.*", "", n)[:50]
+        tot[cat] += (e - s) / 1e3
+        cnt[cat] += 1
+    span = (seg[-1][2] - seg[0][1]) / 1e3
+    print(f"step {k}: {len(seg)} kernels, span {span / 1e3:.2f} ms, busy {sum(tot.values()) / 1e3:.2f} ms")
+    for cat in sorted(tot, key=lambda x: -tot[x]):
+        print(f"  {tot[cat] / 1e3:7.2f} ms {cnt[cat]:5d} kernels  {cat}")
+
+
+if __name__ == "__main__":
+    main()
