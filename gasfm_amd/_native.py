@@ -43,7 +43,8 @@ _SIGS = {
     "gasfm_edge_prologue_bwd": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _vp, _i32, _f32, _vp, _vp,
                                        _vp]),
     "gasfm_segment_rowsum": (_i32, [_vp, _i32, _vp, _vp, _i64, _f32, _vp, _vp, _vp]),
-    "gasfm_colsum": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _vp]),
+    "gasfm_colsum_counters": (_i32, [_i32]),
+    "gasfm_colsum": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, _vp]),
     "gasfm_edge0_part_rows": (_i32, [_i32, _i64, _i32]),
     "gasfm_edge0_prologue_fwd": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
     "gasfm_edge0_epilogue_fwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp,
@@ -172,14 +173,28 @@ def attn_bwd_combine(combine, n_combine, HC, part_dxr, dXR):
     check(st, "gasfm_gat_attn_bwd_combine")
 
 
+_COUNTERS = {}
+
+
+def _counters(device, n):
+    """Per-device zeroed uint32 ticket counters for gasfm_colsum (self-resetting)."""
+    c = _COUNTERS.get(device)
+    if c is None or c.numel() < n:
+        c = torch.zeros(max(n, 256), dtype=torch.int32, device=device)
+        _COUNTERS[device] = c
+    return c
+
+
 def colsum(A, out=None):
-    """Deterministic column sum of a 2-D fp32 CUDA tensor (row stride may exceed cols)."""
+    """Deterministic column sum of a 2-D fp32 CUDA tensor (row stride may exceed cols); one launch."""
     assert A.dim() == 2 and A.stride(1) == 1 and A.dtype == torch.float32
     rows, cols = A.shape
     if out is None:
         out = torch.empty(cols, dtype=torch.float32, device=A.device)
-    ws = torch.empty(int(lib().gasfm_colsum_ws_floats(rows, cols)), dtype=torch.float32, device=A.device)
-    st = lib().gasfm_colsum(_p(A), rows, cols, max(A.stride(0), cols), _p(ws), _p(out), _stream(out))
+    L = lib()
+    ws = torch.empty(int(L.gasfm_colsum_ws_floats(rows, cols)), dtype=torch.float32, device=A.device)
+    cnt = _counters(A.device, L.gasfm_colsum_counters(cols))
+    st = L.gasfm_colsum(_p(A), rows, cols, max(A.stride(0), cols), _p(ws), _p(out), _p(cnt), _stream(out))
     check(st, "gasfm_colsum")
     return out
 

@@ -1,6 +1,8 @@
-// Deterministic column sums (bias / att gradients): two passes, no atomics.
-//   pass 1: block b sums rows [b*R/B, (b+1)*R/B) of every column into ws[b, :]
-//   pass 2: one block sums ws over b in order.
+// Deterministic column sums (bias / att / weight-gradient partials), ONE launch, no float atomics.
+//   block (b, chunk) sums rows [b*R/B, (b+1)*R/B) of a 1024-column chunk into ws[b, chunk];
+//   the last block of each chunk to finish (agent-scope release / relaxed ticket / acquire,
+//   cdna_hip_programming.md §3 split-K recipe; correct for any block-to-XCD placement) sums
+//   ws over b in block order and writes out[chunk].  B <= 64 keeps that serial sum short.
 // Replaces the implicit reductions autograd performs for GATv2Conv.bias /
 // GATv2Conv.att (PyG, layers.py:304-309 etc.) and LayerNorm/Linear biases.
 #include <hip/hip_runtime.h>
@@ -12,7 +14,7 @@
 namespace gasfm {
 
 constexpr int kColBlock = 256;
-constexpr int kMaxColBlocks = 1024;
+constexpr int kMaxColBlocks = 64;
 
 static int colsum_blocks(int64_t rows) {
   const int64_t b = (rows + 127) / 128;
@@ -23,8 +25,9 @@ static int colsum_blocks(int64_t rows) {
 // group (c4) and a row lane (rl); RL = 256 / (cols/4) row lanes stride the block's row
 // range with 4 independent loads in flight, then the row lanes are summed through LDS
 // in lane order.  Other shapes: thread per column, rows serial.
-__global__ __launch_bounds__(kColBlock) void colsum_pass1(const float* __restrict__ A, int64_t rows, int cols,
-                                                       int64_t ld, float* __restrict__ ws) {
+__global__ __launch_bounds__(kColBlock) void colsum_kernel(const float* __restrict__ A, int64_t rows, int cols,
+                                                        int64_t ld, float* __restrict__ ws, float* __restrict__ out,
+                                                        uint32_t* __restrict__ cnt) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
   const int nb = gridDim.x;
   const int64_t r0 = rows * blockIdx.x / nb, r1 = rows * (blockIdx.x + 1) / nb;
@@ -80,22 +83,30 @@ __global__ __launch_bounds__(kColBlock) void colsum_pass1(const float* __restric
       ws[int64_t(blockIdx.x) * cols + c] = acc;
     }
   }
-}
-
-// Pass 2: block handles 64 columns; 4 row lanes sum blocks b = rl, rl+4, ... then
-// the lanes are added in order (deterministic for a given launch geometry).
-__global__ __launch_bounds__(kColBlock) void colsum_pass2(const float* __restrict__ ws, int nb, int cols,
-                                                       float* __restrict__ out) {
-  __shared__ float sh[kColBlock];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rl = threadIdx.x >> 6;
-  float acc = 0.f;
-  if (c < cols) {
-#pragma unroll 4
-    for (int b = rl; b < nb; b += 4) acc += ws[int64_t(b) * cols + c];
-  }
-  sh[threadIdx.x] = acc;
+  // publish this block's slab: drain, barrier, one release, one relaxed ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (rl == 0 && c < cols) out[c] = ((sh[threadIdx.x] + sh[threadIdx.x + 64]) + sh[threadIdx.x + 128]) + sh[threadIdx.x + 192];
+  uint32_t* flag = reinterpret_cast<uint32_t*>(sh);  // the one LDS array (its pass-1 use is over)
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t t = __hip_atomic_fetch_add(cnt + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = (t == uint32_t(nb - 1)) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (flag[0] == 0u) return;
+  // last arriver of this chunk: acquire, then sum the nb slabs in block order
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < ccols; c += kColBlock) {
+    float acc = 0.f;
+    for (int b = 0; b < nb; ++b) acc += ws[int64_t(b) * cols + c];
+    out[cbase + c] = acc;
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(cnt + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace gasfm
@@ -106,19 +117,17 @@ extern "C" int64_t gasfm_colsum_ws_floats(int64_t rows, int32_t cols) {
   return int64_t(colsum_blocks(rows)) * cols;
 }
 
+extern "C" int32_t gasfm_colsum_counters(int32_t cols) { return (cols + 4 * kColBlock - 1) / (4 * kColBlock); }
+
 extern "C" int gasfm_colsum(const float* A, int64_t rows, int32_t cols, int64_t ld, float* ws, float* out,
-                            void* stream) {
+                            uint32_t* counters, void* stream) {
   GASFM_REQUIRE(rows >= 0 && cols > 0 && ld >= cols, "gasfm_colsum: rows=%lld cols=%d ld=%lld", (long long)rows,
                 cols, (long long)ld);
-  GASFM_REQUIRE(ws && out && (rows == 0 || A), "gasfm_colsum: null pointer");
+  GASFM_REQUIRE(ws && out && counters && (rows == 0 || A), "gasfm_colsum: null pointer");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int nb = colsum_blocks(rows);
   const int nchunk = (cols + 4 * kColBlock - 1) / (4 * kColBlock);
-  hipLaunchKernelGGL(colsum_pass1, dim3(nb, nchunk), dim3(kColBlock), 4 * kColBlock * sizeof(float), st, A, rows,
-                     cols, ld, ws);
-  int rc = launch_status("gasfm_colsum/pass1");
-  if (rc) return rc;
-  const int g2 = (cols + 63) / 64;
-  hipLaunchKernelGGL(colsum_pass2, dim3(g2), dim3(kColBlock), 0, st, ws, nb, cols, out);
-  return launch_status("gasfm_colsum/pass2");
+  hipLaunchKernelGGL(colsum_kernel, dim3(nb, nchunk), dim3(kColBlock), 4 * kColBlock * sizeof(float), st, A, rows,
+                     cols, ld, ws, out, counters);
+  return launch_status("gasfm_colsum");
 }

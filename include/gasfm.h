@@ -142,11 +142,15 @@ int gasfm_gat_attn_bwd_combine(const gasfm_combine_item* combine, int32_t n_comb
                                int32_t HC, const float* part_dxr,
                                float* dXR, int64_t ldDXR, void* stream);
 
-/* out[c] = sum_r A[r*ld + c] for c < cols (two-pass, deterministic).
- * ws must hold gasfm_colsum_ws_floats(rows, cols) floats. */
+/* out[c] = sum_r A[r*ld + c] for c < cols: ONE launch, deterministic (per-block partial slabs
+ * in ws, summed in block order by the last block of each column chunk).  ws must hold
+ * gasfm_colsum_ws_floats(rows, cols) floats; counters must hold gasfm_colsum_counters(cols)
+ * uint32 that are ZERO before the first call (the kernel resets them; one array per device,
+ * calls ordered on one stream). */
 int64_t gasfm_colsum_ws_floats(int64_t rows, int32_t cols);
+int32_t gasfm_colsum_counters(int32_t cols);
 int gasfm_colsum(const float* A, int64_t rows, int32_t cols, int64_t ld,
-                 float* ws, float* out, void* stream);
+                 float* ws, float* out, uint32_t* counters, void* stream);
 
 /* ---- fused per-edge block body (F = n_feat_proj = 32; XL width 64 = point|camera) ---- */
 
