@@ -52,7 +52,7 @@ _SIGS = {
     "gasfm_edge0_epilogue_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _f32, _vp, _vp,
                                         _vp, _vp, _vp]),
     "gasfm_edge0_prologue_bwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
-    "gasfm_node_part_rows": (_i32, [_i64]),
+    "gasfm_node_part_rows": (_i32, [_i64, _i32, _i32]),
     "gasfm_gvec_fwd": (_i32, [_vp, _i32, _vp, _vp, _f32, _vp, _vp, _i32, _vp, _vp, _vp]),
     "gasfm_gvec_bwd_chunks": (_i32, [_i32]),
     "gasfm_gvec_bwd": (_i32, [_vp, _vp, _i32, _vp, _vp, _f32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -287,8 +287,8 @@ def edge0_prologue_bwd(dXL, P, aux, ln_w, ln_b, eps, W0, dP, part):
 
 
 # ---------------------------------------------------------------- point-node LayerNorm -> ReLU -> Linear
-def node_part_rows(N):
-    return lib().gasfm_node_part_rows(N)
+def node_part_rows(N, n_out, residual):
+    return lib().gasfm_node_part_rows(N, n_out, int(residual))
 
 
 def node_ln_linear_fwd(X, ln_w, ln_b, eps, W, b, residual, Y):

@@ -24,6 +24,18 @@ inline int launch_status(const char* where) { return hip_status(hipGetLastError(
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// Workgroups of `fn` (block threads, dynamic LDS bytes) resident on the current device at once
+// (occupancy x CU count; occupancy.cpp, cached).
+int resident_blocks(const void* fn, int block, size_t lds);
+
+// Grid of a grid-stride kernel: enough workgroups for `units` work units of `per_block` each,
+// capped at what is resident at once.
+inline int resident_grid(const void* fn, int block, size_t lds, int64_t units, int per_block) {
+  const int64_t want = (units + per_block - 1) / per_block;
+  const int cap = resident_blocks(fn, block, lds);
+  return int(want < 1 ? 1 : (want > cap ? cap : want));
+}
+
 }  // namespace gasfm
 
 #define GASFM_REQUIRE(cond, ...)            \

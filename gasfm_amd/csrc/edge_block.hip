@@ -43,7 +43,6 @@ constexpr int LD34 = 34;         // LDS row stride of 32-wide tiles
 constexpr int LD66 = 66;         // LDS row stride of 64-wide tiles
 constexpr int LDW = 48;          // LDS row stride of staged weights (<= 32 columns)
 constexpr int LDW64 = 80;        // LDS row stride of staged 64-column weights
-constexpr int kMaxGrid = 2048;   // workgroups for the grid-stride kernels
 
 // Load a 16 x 32 tile of P (rows row0.., global stride 32): the 8 lanes 8k..8k+7 hold row
 // k + 8u (u = 0, 1).  Per row LayerNorm statistics by 3 xor-shuffles.  Writes x_hat
@@ -704,10 +703,15 @@ __global__ __launch_bounds__(kThreads) void segment_rowsum_kernel(const gasfm_wo
   }
 }
 
-int grid_tiles(int64_t E) {
-  const int64_t tiles = (E + TR - 1) / TR;
-  const int64_t g = (tiles + kWaves - 1) / kWaves;
-  return int(g < 1 ? 1 : (g > kMaxGrid ? kMaxGrid : g));
+// Grids: at most the workgroups resident at once (a grid-stride loop covers the rest); the
+// backward partial buffers have one row per workgroup, so their size follows the same grid.
+int64_t tiles_of(int64_t E) { return (E + TR - 1) / TR; }
+int grid_pbwd(int64_t E) {
+  return resident_grid(reinterpret_cast<const void*>(&edge_prologue_bwd_kernel<true, true>), kThreads, 0,
+                       tiles_of(E), kWaves);
+}
+int grid_ebwd(int n_items) {
+  return resident_grid(reinterpret_cast<const void*>(&edge_epilogue_bwd_kernel), kThreads, 0, n_items, kWaves);
 }
 
 }  // namespace
@@ -716,11 +720,8 @@ int grid_tiles(int64_t E) {
 using namespace gasfm;
 
 extern "C" int gasfm_edge_part_floats(int32_t which, int64_t E, int32_t n_items) {
-  // which: 0 = prologue_bwd partial row, 1 = epilogue_bwd partial row (ldWp = 34)
-  const int g = which == 1 ? (n_items < kMaxGrid * kWaves ? (n_items + kWaves - 1) / kWaves : kMaxGrid)
-                           : grid_tiles(E);
-  const int gg = g < 1 ? 1 : g;
-  return which == 0 ? gg * (NX * F + NX + 2 * F) : gg * 32 * 34;
+  // which: 0 = prologue_bwd partial rows, 1 = epilogue_bwd partial rows (ldWp = 34)
+  return which == 0 ? grid_pbwd(E) * (NX * F + NX + 2 * F) : grid_ebwd(n_items > 0 ? n_items : 1) * 32 * 34;
 }
 
 extern "C" int gasfm_edge_prologue_fwd(const float* P, int64_t E, const float* ln_w, const float* ln_b,
@@ -731,12 +732,17 @@ extern "C" int gasfm_edge_prologue_fwd(const float* P, int64_t E, const float* l
   GASFM_REQUIRE(aligned16(P) && aligned16(Y) && aligned16(b), "gasfm_edge_prologue_fwd: P/Y/b not 16-byte aligned");
   if (E == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (ln_w)
-    hipLaunchKernelGGL(edge_prologue_fwd_kernel<true>, dim3(grid_tiles(E)), dim3(kThreads), 0, st, P, E, ln_w,
-                       ln_b, eps, W, b, Y, ldY, pos);
-  else
-    hipLaunchKernelGGL(edge_prologue_fwd_kernel<false>, dim3(grid_tiles(E)), dim3(kThreads), 0, st, P, E, ln_w,
-                       ln_b, eps, W, b, Y, ldY, pos);
+  if (ln_w) {
+    const int g = resident_grid(reinterpret_cast<const void*>(&edge_prologue_fwd_kernel<true>), kThreads, 0,
+                                tiles_of(E), kWaves);
+    hipLaunchKernelGGL(edge_prologue_fwd_kernel<true>, dim3(g), dim3(kThreads), 0, st, P, E, ln_w, ln_b, eps, W, b,
+                       Y, ldY, pos);
+  } else {
+    const int g = resident_grid(reinterpret_cast<const void*>(&edge_prologue_fwd_kernel<false>), kThreads, 0,
+                                tiles_of(E), kWaves);
+    hipLaunchKernelGGL(edge_prologue_fwd_kernel<false>, dim3(g), dim3(kThreads), 0, st, P, E, ln_w, ln_b, eps, W, b,
+                       Y, ldY, pos);
+  }
   return launch_status("gasfm_edge_prologue_fwd");
 }
 
@@ -752,7 +758,9 @@ extern "C" int gasfm_edge_epilogue_fwd(const float* P, const float* P0, const in
                 "gasfm_edge_epilogue_fwd: P/Sp/Sv/Pout not 16-byte aligned (P0 8-byte)");
   if (E == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(edge_epilogue_fwd_kernel, dim3(grid_tiles(E)), dim3(kThreads), 0, st, P, P0, cam, pt, E, ln_w,
+  const int g = resident_grid(reinterpret_cast<const void*>(&edge_epilogue_fwd_kernel), kThreads, 0, tiles_of(E),
+                              kWaves);
+  hipLaunchKernelGGL(edge_epilogue_fwd_kernel, dim3(g), dim3(kThreads), 0, st, P, P0, cam, pt, E, ln_w,
                      ln_b, eps, Wp, ldWp, bp, Sp, Sv, Sg, scale, Pout);
   return launch_status("gasfm_edge_epilogue_fwd");
 }
@@ -767,7 +775,7 @@ extern "C" int gasfm_edge_epilogue_bwd(const gasfm_work_item* items, int32_t n_i
   GASFM_REQUIRE(aligned16(dPo) && aligned16(P), "gasfm_edge_epilogue_bwd: dPo/P not 16-byte aligned");
   if (n_items <= 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int g = n_items < kMaxGrid * kWaves ? (n_items + kWaves - 1) / kWaves : kMaxGrid;
+  const int g = grid_ebwd(n_items);
   hipLaunchKernelGGL(edge_epilogue_bwd_kernel, dim3(g), dim3(kThreads), 0, st, items, n_items, dPo, P, P0, ln_w,
                      ln_b, eps, Wp, ldWp, scale, dSv, part_dsv, dP0, part_w);
   return launch_status("gasfm_edge_epilogue_bwd");
@@ -783,7 +791,7 @@ extern "C" int gasfm_edge_prologue_bwd(const float* dXL, int64_t ldX, const floa
                 "gasfm_edge_prologue_bwd: dXL/P/dRes/dP not 16-byte aligned");
   if (E == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int g = grid_tiles(E);
+  const int g = grid_pbwd(E);
   const bool ln = ln_w != nullptr, res = dRes != nullptr;
 #define GASFM_LAUNCH(LNV, RESV)                                                                                 \
   hipLaunchKernelGGL((edge_prologue_bwd_kernel<LNV, RESV>), dim3(g), dim3(kThreads), 0, st, dXL, ldX, P, dRes, \
@@ -807,8 +815,8 @@ extern "C" int gasfm_segment_rowsum(const gasfm_work_item* items, int32_t n_item
   GASFM_REQUIRE(aligned16(X) && ldX % 4 == 0 && aligned16(out), "gasfm_segment_rowsum: alignment");
   if (n_items <= 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int waves = n_items < 8192 ? n_items : 8192;
-  hipLaunchKernelGGL(segment_rowsum_kernel, dim3((waves + kWaves - 1) / kWaves), dim3(kThreads), 0, st, items,
+  const int g = resident_grid(reinterpret_cast<const void*>(&segment_rowsum_kernel), kThreads, 0, n_items, kWaves);
+  hipLaunchKernelGGL(segment_rowsum_kernel, dim3(g), dim3(kThreads), 0, st, items,
                      n_items, perm, X, ldX, scale, out, part);
   return launch_status("gasfm_segment_rowsum");
 }

@@ -713,23 +713,6 @@ static int env_wave_cap() {
   return cap;
 }
 
-static int resident_blocks(const void* fn, size_t lds) {
-  static std::mutex mu;
-  static std::map<std::pair<const void*, size_t>, int> cache;
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = cache.find({fn, lds});
-  if (it != cache.end()) return it->second;
-  int per_cu = 0, dev = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds) != hipSuccess || per_cu < 1) per_cu = 1;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                              hipSuccess || cus < 1)
-    cus = 256;
-  (void)hipGetLastError();
-  const int v = per_cu * cus;
-  cache[{fn, lds}] = v;
-  return v;
-}
-
 static int grid_for(int n_items, int resident) {
   int waves = n_items > 0 ? n_items : 1;
   const int cap = env_wave_cap() ? env_wave_cap() : resident * (kBlock / kWave);
@@ -772,14 +755,14 @@ extern "C" int gasfm_gat_attn_fwd(const float* XL, int64_t ldXL, const float* XR
   if (vec_ok) {
     done = dispatch_shape(H, C, [&](auto g) {
       using G = decltype(g);
-      const int grid = grid_for(n_items, resident_blocks(reinterpret_cast<const void*>(&attn_fwd_kernel<G>), 0));
+      const int grid = grid_for(n_items, resident_blocks(reinterpret_cast<const void*>(&attn_fwd_kernel<G>), kBlock, 0));
       hipLaunchKernelGGL((attn_fwd_kernel<G>), dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att,
                          bias, perm, items, n_items, slope, finalize, out, ldOut, seg_max, seg_sum, ldStat, part);
     });
   }
   if (!done) {
     const size_t lds = (kBlock / kWave) * 2 * H * sizeof(float);
-    const int grid = grid_for(n_items, resident_blocks(reinterpret_cast<const void*>(&attn_fwd_generic), lds));
+    const int grid = grid_for(n_items, resident_blocks(reinterpret_cast<const void*>(&attn_fwd_generic), kBlock, lds));
     hipLaunchKernelGGL(attn_fwd_generic, dim3(grid), dim3(kBlock), lds, st,
                        XL, ldXL, XR, ldXR, att, bias, perm, items, n_items, H, C, slope, finalize, out, ldOut,
                        seg_max, seg_sum, ldStat, part);
@@ -816,10 +799,10 @@ extern "C" int gasfm_gat_attn_combine(const gasfm_combine_item* combine, int32_t
 // Backward grid: the same for the vectorised and the generic kernel of a shape, since the
 // caller sizes the per-wave datt/dbias partials (gasfm_gat_attn_bwd_waves) before the launch.
 static int bwd_grid(int n_items, int H, int C) {
-  int res = resident_blocks(reinterpret_cast<const void*>(&attn_bwd_generic), 0);
+  int res = resident_blocks(reinterpret_cast<const void*>(&attn_bwd_generic), kBlock, 0);
   dispatch_shape(H, C, [&](auto g) {
     using G = decltype(g);
-    const int r = resident_blocks(reinterpret_cast<const void*>(&attn_bwd_kernel<G>), 0);
+    const int r = resident_blocks(reinterpret_cast<const void*>(&attn_bwd_kernel<G>), kBlock, 0);
     res = r < res ? r : res;
   });
   return grid_for(n_items, res);

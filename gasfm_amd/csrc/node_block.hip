@@ -28,7 +28,6 @@ using namespace tile;
 constexpr int FI = 64;           // input width (n_feat_scenepoint)
 constexpr int LDX = 66;          // LDS row stride of 64-wide tiles
 constexpr int LDWB = 80;         // LDS row stride of the 64-column weights in the backward pass
-constexpr int kMaxGridNode = 1024;
 
 template <int FO>
 struct Fwd {
@@ -273,10 +272,17 @@ __global__ __launch_bounds__(kThreads) void node_bwd_kernel(const float* __restr
   }
 }
 
-int node_grid(int64_t N) {
-  const int64_t tiles = (N + TR - 1) / TR;
-  const int64_t g = (tiles + kWaves - 1) / kWaves;
-  return int(g < 1 ? 1 : (g > kMaxGridNode ? kMaxGridNode : g));
+int64_t tiles_of(int64_t N) { return (N + TR - 1) / TR; }
+
+template <class K>
+int grid_of(K kernel, int64_t N) {
+  return resident_grid(reinterpret_cast<const void*>(kernel), kThreads, 0, tiles_of(N), kWaves);
+}
+
+// backward grid (= partial rows) of the variant a call uses
+int bwd_grid(int64_t N, int n_out, int residual) {
+  if (n_out == 32) return grid_of(&node_bwd_kernel<32, false>, N);
+  return residual ? grid_of(&node_bwd_kernel<64, true>, N) : grid_of(&node_bwd_kernel<64, false>, N);
 }
 
 }  // namespace
@@ -284,7 +290,9 @@ int node_grid(int64_t N) {
 
 using namespace gasfm;
 
-extern "C" int gasfm_node_part_rows(int64_t N) { return node_grid(N); }
+extern "C" int gasfm_node_part_rows(int64_t N, int32_t n_out, int32_t residual) {
+  return bwd_grid(N, n_out, residual);
+}
 
 extern "C" int gasfm_node_ln_linear_fwd(const float* X, int64_t N, int32_t n_in, const float* ln_w,
                                         const float* ln_b, float eps, const float* W, const float* b, int32_t n_out,
@@ -298,15 +306,14 @@ extern "C" int gasfm_node_ln_linear_fwd(const float* X, int64_t N, int32_t n_in,
   GASFM_REQUIRE(X && ln_w && ln_b && W && Y, "gasfm_node_ln_linear_fwd: null pointer");
   GASFM_REQUIRE(aligned16(X) && aligned16(ln_w) && aligned16(ln_b), "gasfm_node_ln_linear_fwd: alignment");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int g = node_grid(N);
   if (n_out == 32)
-    hipLaunchKernelGGL((node_fwd_kernel<32, false>), dim3(g), dim3(kThreads), 0, st, X, N, ln_w, ln_b, eps, W, b, Y,
+    hipLaunchKernelGGL((node_fwd_kernel<32, false>), dim3(grid_of(&node_fwd_kernel<32, false>, N)), dim3(kThreads), 0, st, X, N, ln_w, ln_b, eps, W, b, Y,
                        ldY);
   else if (residual)
-    hipLaunchKernelGGL((node_fwd_kernel<64, true>), dim3(g), dim3(kThreads), 0, st, X, N, ln_w, ln_b, eps, W, b, Y,
+    hipLaunchKernelGGL((node_fwd_kernel<64, true>), dim3(grid_of(&node_fwd_kernel<64, true>, N)), dim3(kThreads), 0, st, X, N, ln_w, ln_b, eps, W, b, Y,
                        ldY);
   else
-    hipLaunchKernelGGL((node_fwd_kernel<64, false>), dim3(g), dim3(kThreads), 0, st, X, N, ln_w, ln_b, eps, W, b, Y,
+    hipLaunchKernelGGL((node_fwd_kernel<64, false>), dim3(grid_of(&node_fwd_kernel<64, false>, N)), dim3(kThreads), 0, st, X, N, ln_w, ln_b, eps, W, b, Y,
                        ldY);
   return launch_status("gasfm_node_ln_linear_fwd");
 }
@@ -322,7 +329,7 @@ extern "C" int gasfm_node_ln_linear_bwd(const float* dY, const float* X, int64_t
   GASFM_REQUIRE(dY && X && ln_w && ln_b && W && dX && part, "gasfm_node_ln_linear_bwd: null pointer");
   GASFM_REQUIRE(aligned16(dY) && aligned16(X), "gasfm_node_ln_linear_bwd: alignment");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int g = node_grid(N);
+  const int g = bwd_grid(N, n_out, residual);
   if (n_out == 32)
     hipLaunchKernelGGL((node_bwd_kernel<32, false>), dim3(g), dim3(kThreads), 0, st, dY, X, N, ln_w, ln_b, eps, W,
                        dX, part);

@@ -3,23 +3,30 @@
 torch's Linear backward computes dW = dY^T X as ONE GEMM with K = rows; for the
 GASFM point layers (M, N <= 64, K = 200k) hipBLASLt then runs one or two
 workgroups (measured 0.45-0.53 ms per call on MI355X, ~40 ms per training
-step).  ``linear`` keeps torch's forward / input-gradient GEMMs (MFMA through
-hipBLASLt, good shapes) and computes the weight gradient as a batched GEMM over
-row chunks followed by a sum (split-K), which fills the chip.
-Camera / global rows (<= a few thousand) go through plain torch.
+step), and for the camera layers (32x1024 / 1024x32 weights, K = 1000 cameras)
+24-48 workgroups at 39-56 us per call.  ``linear`` keeps torch's forward /
+input-gradient GEMMs (MFMA through hipBLASLt, good shapes) and computes the weight
+gradient as a batched GEMM over row chunks followed by a sum (split-K), which fills
+the chip.
+The single global row goes through csrc/global_vec.hip (GlobalLinearFn).
 """
 import torch
 import torch.nn.functional as F
 from torch.nn import LayerNorm, Linear, ReLU, Sequential
 
-SPLITK_MIN_ROWS = 16384
-_CHUNK = 2048
+SPLITK_MIN_ROWS = 256      # camera rows (m ~ 1000) and point rows (n ~ 200k)
+_MIN_CHUNK = 128           # rows per split-K slice at least ...
+_MAX_SLICES = 256          # ... and at most this many slices: a 32x64 weight gradient is only a
+                           # few output tiles, so the slice count sets the workgroup count (12
+                           # slices of 2k rows ran 24 workgroups at 55 us per call)
 
 
 def splitk_wgrad(dy, x):
     R, M = dy.shape
     N = x.shape[1]
-    B = max(1, min(256, R // _CHUNK))
+    if R < 16384 and M * N > 262144:
+        return dy.T @ x  # camera 1024x1024 weights: already 256 output tiles, no split
+    B = max(1, min(_MAX_SLICES, R // _MIN_CHUNK))
     R0 = (R // B) * B
     dW = torch.bmm(dy[:R0].reshape(B, R0 // B, M).transpose(1, 2), x[:R0].reshape(B, R0 // B, N)).sum(0)
     if R0 < R:
@@ -138,7 +145,7 @@ class NodeLnLinearFn(torch.autograd.Function):
         n_out, n_in = W.shape
         dy = dy.contiguous()
         dx = torch.empty_like(x)
-        rows = _native.node_part_rows(x.shape[0])
+        rows = _native.node_part_rows(x.shape[0], n_out, ctx.residual)
         part = torch.empty((rows, n_out * n_in + n_out + 2 * n_in), dtype=torch.float32, device=x.device)
         _native.node_ln_linear_bwd(dy, x, ln_w, ln_b, ctx.eps, W, ctx.residual, dx, part)
         tot = _native.colsum(part)

@@ -236,8 +236,9 @@ int gasfm_edge0_prologue_bwd(const float* dXL, const float* P, const float* aux,
  * lin_scenepoint(relu(scenepoint_norm_layer(x))) of the projection update (layers.py:928-935). */
 
 /* Rows of the [rows x (n_out*n_in + n_out + 2*n_in)] partial buffer gasfm_node_ln_linear_bwd
- * writes: [dW n_out x n_in | db n_out | dgamma n_in | dbeta n_in] per workgroup. */
-int gasfm_node_part_rows(int64_t N);
+ * writes for this (N, n_out, residual): [dW n_out x n_in | db n_out | dgamma n_in | dbeta n_in]
+ * per workgroup (the grid is sized to the resident workgroups of the current device). */
+int gasfm_node_part_rows(int64_t N, int32_t n_out, int32_t residual);
 
 /* Y[i] = W relu(LN(X[i])) + b (+ X[i] if residual); b may be null. X: [N x 64] contiguous. */
 int gasfm_node_ln_linear_fwd(const float* X, int64_t N, int32_t n_in, const float* ln_w, const float* ln_b,

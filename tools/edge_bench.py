@@ -85,7 +85,7 @@ def main():
         Y = torch.empty(n, n_out, device=dev)
         dY = rnd(n, n_out)
         dX = torch.empty_like(X)
-        nrows = _native.node_part_rows(n)
+        nrows = _native.node_part_rows(n, n_out, resid)
         npart = torch.empty(nrows, n_out * 64 + n_out + 128, device=dev)
         run(f"node_fwd<{n_out},{int(resid)}>",
             lambda: _native.node_ln_linear_fwd(X, g64, b64, 1e-5, Wn, bn, resid, Y), n * (256 + 4 * n_out))

@@ -1,0 +1,49 @@
+"""torch.profiler view of one eager step (op names + input shapes + device time), GPU box.
+
+usage: python tools/torch_prof.py [--n N]
+"""
+import argparse
+import os
+import sys
+
+import torch
+from torch.profiler import ProfilerActivity, profile
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import gasfm_amd  # noqa: E402
+from gasfm_amd import synthetic  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=25_000)
+    ap.add_argument("--rows", type=int, default=40)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    sc = synthetic.windowed_scene(1000, args.n, seed=4)
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf()).to(dev)
+    data = gasfm_amd.SceneData.from_synthetic(sc).to(dev)
+    cP = torch.randn((sc.m, 3, 4), device=dev)
+    cX = torch.randn((4, sc.n), device=dev)
+
+    def step():
+        p = net(data)
+        ((p["Ps_norm"] * cP).sum() + (p["pts3D"] * cX).sum()).backward()
+        for q in net.parameters():
+            q.grad = None
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+        step()
+        torch.cuda.synchronize()
+    ev = [e for e in prof.key_averages(group_by_input_shape=True) if e.self_device_time_total > 0]
+    ev.sort(key=lambda e: -e.self_device_time_total)
+    tot = sum(e.self_device_time_total for e in ev)
+    print(f"self device time total {tot / 1e3:.2f} ms")
+    for e in ev[:args.rows]:
+        print(f"{e.self_device_time_total / 1e3:7.3f} ms {e.count:5d}x  {e.key[:60]:60s} {str(e.input_shapes)[:90]}")
+
+
+if __name__ == "__main__":
+    main()
