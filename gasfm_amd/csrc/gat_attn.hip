@@ -518,30 +518,33 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_kernel(
 // dXR[seg] = ordered sum of its partial slots.  One workgroup per entry: thread t owns
 // column t % HC and slot group t / HC (R = 256/HC groups, or 1 with column loops for
 // HC > 256); the group sums are added in group order, so the result is deterministic.
+// grid = (combine entries, column blocks of CB = min(HC, 64)): R = kBlock / CB row groups take
+// slots k = grp, grp + R, ... and are added in group order (deterministic for a given HC).
 __global__ __launch_bounds__(kBlock) void attn_bwd_combine_kernel(const gasfm_combine_item* __restrict__ comb,
                                                              int n_comb, int HC,
                                                              const float* __restrict__ part,
                                                              float* __restrict__ dXR, int64_t ld) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
   const gasfm_combine_item ci = comb[blockIdx.x];
-  const int R = HC <= kBlock ? kBlock / HC : 1;
-  const int grp = threadIdx.x / (HC <= kBlock ? HC : kBlock);
-  for (int f0 = 0; f0 < HC; f0 += kBlock) {
-    const int f = f0 + (HC <= kBlock ? int(threadIdx.x % HC) : int(threadIdx.x));
-    float acc = 0.f;
-    if (grp < R && f < HC) {
-#pragma unroll 4
-      for (int k = grp; k < ci.slot_count; k += R)
-        acc += part[(int64_t(ci.slot_begin) + int64_t(k) * ci.slot_stride) * HC + f];
+  const int CB = HC < 64 ? HC : 64;
+  const int R = kBlock / CB;
+  const int grp = threadIdx.x / CB;
+  const int f = blockIdx.y * CB + int(threadIdx.x % CB);
+  float a0 = 0.f, a1 = 0.f;
+  if (grp < R && f < HC) {
+    int k = grp;
+    for (; k + R < ci.slot_count; k += 2 * R) {
+      a0 += part[(int64_t(ci.slot_begin) + int64_t(k) * ci.slot_stride) * HC + f];
+      a1 += part[(int64_t(ci.slot_begin) + int64_t(k + R) * ci.slot_stride) * HC + f];
     }
-    __syncthreads();
-    sh[threadIdx.x] = acc;
-    __syncthreads();
-    if (grp == 0 && f < HC) {
-      float t = 0.f;
-      for (int g = 0; g < R; ++g) t += sh[g * (HC <= kBlock ? HC : kBlock) + threadIdx.x];
-      dXR[int64_t(ci.seg) * ld + f] = t;
-    }
+    if (k < ci.slot_count) a0 += part[(int64_t(ci.slot_begin) + int64_t(k) * ci.slot_stride) * HC + f];
+  }
+  sh[threadIdx.x] = a0 + a1;
+  __syncthreads();
+  if (grp == 0 && f < HC) {
+    float t = 0.f;
+    for (int g = 0; g < R; ++g) t += sh[g * CB + threadIdx.x];
+    dXR[int64_t(ci.seg) * ld + f] = t;
   }
 }
 
@@ -852,7 +855,9 @@ extern "C" int gasfm_gat_attn_bwd_combine(const gasfm_combine_item* combine, int
   GASFM_REQUIRE(HC > 0 && n_combine >= 0, "gasfm_gat_attn_bwd_combine: bad args");
   if (n_combine == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(attn_bwd_combine_kernel, dim3(n_combine), dim3(kBlock), kBlock * sizeof(float), st, combine,
+  const int cb = HC < 64 ? HC : 64;
+  hipLaunchKernelGGL(attn_bwd_combine_kernel, dim3(n_combine, (HC + cb - 1) / cb), dim3(kBlock),
+                     kBlock * sizeof(float), st, combine,
                      n_combine, HC, part_dxr, dXR, ldDXR);
   return launch_status("gasfm_gat_attn_bwd_combine");
 }

@@ -1,8 +1,10 @@
 // Deterministic column sums (bias / att / weight-gradient partials), ONE launch, no float atomics.
 //   block (b, chunk) sums rows [b*R/B, (b+1)*R/B) of a 1024-column chunk into ws[b, chunk];
-//   the last block of each chunk to finish (agent-scope release / relaxed ticket / acquire,
-//   cdna_hip_programming.md §3 split-K recipe; correct for any block-to-XCD placement) sums
-//   ws over b in block order and writes out[chunk].  B <= 64 keeps that serial sum short.
+//   the last block of each chunk to finish sums ws over b in block order and writes
+//   out[chunk].  Hand-off (cdna_hip_programming.md §3 / Guideline 16, sc1 form; correct for any
+//   block-to-XCD placement): slabs stored write-through (sc1), drained, a relaxed agent-scope
+//   ticket, and sc1 loads in the reducer -- no L2 writeback fence.  B <= 64 keeps the serial
+//   sum short.
 // Replaces the implicit reductions autograd performs for GATv2Conv.bias /
 // GATv2Conv.att (PyG, layers.py:304-309 etc.) and LayerNorm/Linear biases.
 #include <hip/hip_runtime.h>
@@ -14,10 +16,20 @@
 namespace gasfm {
 
 constexpr int kColBlock = 256;
+constexpr int kChunkCols = 256;  // columns per block: 64 float4 column groups x 4 row lanes
 constexpr int kMaxColBlocks = 64;
 
+// write-through (sc1) store of 16 bytes as two agent-scope 8-byte atomic stores
+__device__ __forceinline__ void st_sc1(float* p, float4 v) {
+  uint64_t a, b;
+  __builtin_memcpy(&a, &v.x, 8);
+  __builtin_memcpy(&b, &v.z, 8);
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p) + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 static int colsum_blocks(int64_t rows) {
-  const int64_t b = (rows + 127) / 128;
+  const int64_t b = (rows + 15) / 16;  // >= 16 rows per block, <= 64 blocks per column chunk
   return int(b < 1 ? 1 : (b > kMaxColBlocks ? kMaxColBlocks : b));
 }
 
@@ -32,10 +44,10 @@ __global__ __launch_bounds__(kColBlock) void colsum_kernel(const float* __restri
   const int nb = gridDim.x;
   const int64_t r0 = rows * blockIdx.x / nb, r1 = rows * (blockIdx.x + 1) / nb;
   // blockIdx.y selects a chunk of up to 4*256 columns (wide partial matrices)
-  const int cbase = blockIdx.y * 4 * kColBlock;
+  const int cbase = blockIdx.y * kChunkCols;
   A += cbase;
   ws += cbase;
-  const int ccols = (cols - cbase) < 4 * kColBlock ? (cols - cbase) : 4 * kColBlock;
+  const int ccols = (cols - cbase) < kChunkCols ? (cols - cbase) : kChunkCols;
   const int C4 = ccols / 4;
   if ((cols & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0) {
     const int RL = kColBlock / C4;
@@ -74,37 +86,62 @@ __global__ __launch_bounds__(kColBlock) void colsum_kernel(const float* __restri
         t.z += v.z;
         t.w += v.w;
       }
-      reinterpret_cast<float4*>(ws + int64_t(blockIdx.x) * cols)[threadIdx.x] = t;
+      st_sc1(ws + int64_t(blockIdx.x) * cols + 4 * threadIdx.x, t);
     }
   } else {
     for (int c = threadIdx.x; c < ccols; c += kColBlock) {
       float acc = 0.f;
       for (int64_t r = r0; r < r1; ++r) acc += A[r * ld + c];
-      ws[int64_t(blockIdx.x) * cols + c] = acc;
+      __hip_atomic_store(ws + int64_t(blockIdx.x) * cols + c, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  // publish this block's slab: drain, barrier, one release, one relaxed ticket
+  // publish: the slab was stored write-through (sc1), so no release fence (which would write
+  // back every dirty L2 line of this XCD, e.g. the previous kernel's outputs): every wave
+  // drains its stores, barrier, one relaxed agent-scope ticket
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   uint32_t* flag = reinterpret_cast<uint32_t*>(sh);  // the one LDS array (its pass-1 use is over)
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t t = __hip_atomic_fetch_add(cnt + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     flag[0] = (t == uint32_t(nb - 1)) ? 1u : 0u;
   }
   __syncthreads();
   if (flag[0] == 0u) return;
-  // last arriver of this chunk: acquire, then sum the nb slabs in block order
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < ccols; c += kColBlock) {
+  // last arriver of this chunk: every slab load is an sc1 (agent-scope) load, so no acquire
+  // fence; slabs summed in block order (deterministic)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the ticket
+  // RL2 thread groups split the slabs (b = g, g + RL2, ...); 8 independent sc1 loads in flight
+  // per batch, added in b order; the groups are then added in group order through LDS
+  const int RL2 = kColBlock / ccols > 0 ? kColBlock / ccols : 1;
+  const int cg = ccols < kColBlock ? ccols : kColBlock;
+  const int gi = threadIdx.x / cg;
+  float* red = sh + 1;  // after the flag word
+  for (int c0 = 0; c0 < ccols; c0 += cg) {
+    const int c = c0 + int(threadIdx.x % cg);
     float acc = 0.f;
-    for (int b = 0; b < nb; ++b) acc += ws[int64_t(b) * cols + c];
-    out[cbase + c] = acc;
+    if (gi < RL2 && c < ccols) {
+      for (int b0 = gi; b0 < nb; b0 += 8 * RL2) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int b = b0 + u * RL2;
+          // ws is already offset by cbase; clamped address, value zeroed (no per-element branch)
+          v[u] = __hip_atomic_load(ws + int64_t(b < nb ? b : b0) * cols + c, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+          if (b >= nb) v[u] = 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u];
+      }
+    }
+    __syncthreads();
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (gi == 0 && c < ccols) {
+      float t = 0.f;
+      for (int g = 0; g < RL2; ++g) t += red[g * cg + threadIdx.x];
+      out[cbase + c] = t;
+    }
   }
   if (threadIdx.x == 0) __hip_atomic_store(cnt + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -117,7 +154,7 @@ extern "C" int64_t gasfm_colsum_ws_floats(int64_t rows, int32_t cols) {
   return int64_t(colsum_blocks(rows)) * cols;
 }
 
-extern "C" int32_t gasfm_colsum_counters(int32_t cols) { return (cols + 4 * kColBlock - 1) / (4 * kColBlock); }
+extern "C" int32_t gasfm_colsum_counters(int32_t cols) { return (cols + kChunkCols - 1) / kChunkCols; }
 
 extern "C" int gasfm_colsum(const float* A, int64_t rows, int32_t cols, int64_t ld, float* ws, float* out,
                             uint32_t* counters, void* stream) {
@@ -126,7 +163,7 @@ extern "C" int gasfm_colsum(const float* A, int64_t rows, int32_t cols, int64_t 
   GASFM_REQUIRE(ws && out && counters && (rows == 0 || A), "gasfm_colsum: null pointer");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int nb = colsum_blocks(rows);
-  const int nchunk = (cols + 4 * kColBlock - 1) / (4 * kColBlock);
+  const int nchunk = (cols + kChunkCols - 1) / kChunkCols;
   hipLaunchKernelGGL(colsum_kernel, dim3(nb, nchunk), dim3(kColBlock), 4 * kColBlock * sizeof(float), st, A, rows,
                      cols, ld, ws, out, counters);
   return launch_status("gasfm_colsum");
