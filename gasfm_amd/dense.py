@@ -21,6 +21,16 @@ _MAX_SLICES = 256          # ... and at most this many slices: a 32x64 weight gr
                            # slices of 2k rows ran 24 workgroups at 55 us per call)
 
 
+def _colsum(a):
+    """Column sums of a 2-D CUDA tensor: the one-launch gasfm_colsum for short, wide inputs
+    (split-K slices, camera rows); torch's reduction for tall ones (200k point rows), where
+    colsum's <= 64 row blocks per column chunk would leave the chip idle."""
+    if a.shape[0] > 4096:
+        return a.sum(0)
+    from . import _native
+    return _native.colsum(a.contiguous())
+
+
 def splitk_wgrad(dy, x):
     R, M = dy.shape
     N = x.shape[1]
@@ -28,7 +38,8 @@ def splitk_wgrad(dy, x):
         return dy.T @ x  # camera 1024x1024 weights: already 256 output tiles, no split
     B = max(1, min(_MAX_SLICES, R // _MIN_CHUNK))
     R0 = (R // B) * B
-    dW = torch.bmm(dy[:R0].reshape(B, R0 // B, M).transpose(1, 2), x[:R0].reshape(B, R0 // B, N)).sum(0)
+    dW = _colsum(torch.bmm(dy[:R0].reshape(B, R0 // B, M).transpose(1, 2), x[:R0].reshape(B, R0 // B, N))
+                 .reshape(B, M * N)).view(M, N)
     if R0 < R:
         dW = dW + dy[R0:].T @ x[R0:]
     return dW
@@ -47,7 +58,7 @@ class RowLinearFn(torch.autograd.Function):
         dy = dy.contiguous()
         dx = dy @ W if ctx.needs_input_grad[0] else None
         dW = splitk_wgrad(dy, x.contiguous()) if ctx.needs_input_grad[1] else None
-        db = dy.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
+        db = _colsum(dy) if ctx.has_b and ctx.needs_input_grad[2] else None
         return dx, dW, db
 
 
