@@ -159,7 +159,13 @@ def main():
     else:
         # warm-up steps run inside CapturedStep (before capture); every timed step replays
         # the captured forward+backward (+ gradient all-reduce) as one hipGraph launch
-        captured = CapturedStep(fwd_bwd, model.parameters(), warmup=args.warmup)
+        agree = None
+        if world > 1:
+            def agree(ok):  # AND over ranks, one collective outside the graph
+                t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+                torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
+                return bool(t.item())
+        captured = CapturedStep(fwd_bwd, model.parameters(), warmup=args.warmup, agree=agree)
         step = captured
         execution = ("hipGraph replay of the captured forward+backward step" if captured.captured
                      else f"eager fallback ({captured.fallback_reason})")

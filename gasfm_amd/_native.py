@@ -46,7 +46,7 @@ _SIGS = {
     "gasfm_colsum_counters": (_i32, [_i32]),
     "gasfm_colsum": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, _vp]),
     "gasfm_edge0_part_rows": (_i32, [_i32, _i64, _i32]),
-    "gasfm_edge0_prologue_fwd": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
+    "gasfm_edge0_prologue_fwd": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_edge0_epilogue_fwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp,
                                         _vp, _vp, _f32, _vp, _vp]),
     "gasfm_edge0_epilogue_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _f32, _vp, _vp,
@@ -253,10 +253,10 @@ def edge0_part_rows(which, E, n_items=0):
     return lib().gasfm_edge0_part_rows(which, E, n_items)
 
 
-def edge0_prologue_fwd(P, ln_w, ln_b, eps, W0, b0, XL):
+def edge0_prologue_fwd(P, ln_w, ln_b, eps, W0, b0, XL, pos=None):
     _req(P, "P", 2)
     st = lib().gasfm_edge0_prologue_fwd(_p(P), P.shape[0], _p(ln_w), _p(ln_b), eps, _p(W0), _p(b0), _p(XL),
-                                        _stream(P))
+                                        _p(pos), _stream(P))
     check(st, "gasfm_edge0_prologue_fwd")
 
 

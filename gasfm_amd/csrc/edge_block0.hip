@@ -69,7 +69,8 @@ __global__ __launch_bounds__(kT) void edge0_prologue_fwd_kernel(const float2* __
                                                                const float* __restrict__ ba, float eps,
                                                                const float* __restrict__ W0,
                                                                const float* __restrict__ b0,
-                                                               float4* __restrict__ XL) {
+                                                               float4* __restrict__ XL,
+                                                               const int32_t* __restrict__ pos) {
   float w[8][2], bb[8];
 #pragma unroll
   for (int o = 0; o < 8; ++o) {
@@ -85,7 +86,8 @@ __global__ __launch_bounds__(kT) void edge0_prologue_fwd_kernel(const float2* __
     float y[8];
 #pragma unroll
     for (int o = 0; o < 8; ++o) y[o] = fmaf(w[o][0], h0, fmaf(w[o][1], h1, bb[o]));
-    XL[2 * e] = make_float4(y[0], y[1], y[2], y[3]);
+    // point half at the edge's position in point order (pos), camera half at e
+    XL[2 * (pos ? int64_t(pos[e]) : e)] = make_float4(y[0], y[1], y[2], y[3]);
     XL[2 * e + 1] = make_float4(y[4], y[5], y[6], y[7]);
   }
 }
@@ -318,12 +320,13 @@ extern "C" int gasfm_edge0_part_rows(int32_t which, int64_t E, int32_t n_items) 
 }
 
 extern "C" int gasfm_edge0_prologue_fwd(const float* P, int64_t E, const float* ln_w, const float* ln_b, float eps,
-                                        const float* W0, const float* b0, float* XL, void* stream) {
+                                        const float* W0, const float* b0, float* XL, const int32_t* pos,
+                                        void* stream) {
   GASFM_REQUIRE(P && ln_w && ln_b && W0 && b0 && XL && aligned16(XL), "gasfm_edge0_prologue_fwd: bad args");
   if (E == 0) return GASFM_OK;
   hipLaunchKernelGGL(edge0_prologue_fwd_kernel, dim3(grid_for(E, kT)), dim3(kT), 0,
                      reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const float2*>(P), E, ln_w, ln_b, eps,
-                     W0, b0, reinterpret_cast<float4*>(XL));
+                     W0, b0, reinterpret_cast<float4*>(XL), pos);
   return launch_status("gasfm_edge0_prologue_fwd");
 }
 

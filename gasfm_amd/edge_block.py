@@ -154,10 +154,11 @@ class Block0PrologueFn(torch.autograd.Function):
     """Block 0: XL0 = [Wl_pt; Wl_cam] relu(LN_a(P)) + b for 2-wide P (layers.py:232-234, 329, 426)."""
 
     @staticmethod
-    def forward(ctx, P, ln_w, ln_b, W0, b0, eps):
+    def forward(ctx, P, ln_w, ln_b, W0, b0, eps, pos=None):
+        """pos (point plan's inverse permutation): write the point half of XL0 in point order."""
         E = P.shape[0]
         XL = torch.empty((E, 8), dtype=torch.float32, device=P.device)
-        _native.edge0_prologue_fwd(P, ln_w, ln_b, eps, W0.contiguous(), b0.contiguous(), XL)
+        _native.edge0_prologue_fwd(P, ln_w, ln_b, eps, W0.contiguous(), b0.contiguous(), XL, pos)
         ctx.eps = eps
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(P, ln_w, ln_b, W0)
@@ -174,7 +175,7 @@ class Block0PrologueFn(torch.autograd.Function):
         part = torch.empty((rows, 28), dtype=torch.float32, device=P.device)
         _native.edge0_prologue_bwd(dXL, P, aux, ln_w, ln_b, ctx.eps, W0.contiguous(), dP, part)
         tot = _native.colsum(part)
-        return dP, tot[24:26], tot[26:28], tot[:16].view(8, 2), tot[16:24], None
+        return dP, tot[24:26], tot[26:28], tot[:16].view(8, 2), tot[16:24], None, None
 
 
 class Block0EpilogueFn(torch.autograd.Function):

@@ -25,12 +25,22 @@ import torch
 
 
 class CapturedStep:
-    def __init__(self, fn, params, warmup=3, check=True, rtol=1e-5):
+    """fn captured once and replayed per call.
+
+    agree: for multi-process runs, a callable mapping this rank's bool to the AND over all
+    ranks (one collective outside the graph).  Capture success and the replay check are agreed
+    before any rank replays, so either every rank replays (and runs the captured collectives)
+    or every rank runs eagerly: a rank-local fallback would leave the ranks running different
+    collective sequences.
+    """
+
+    def __init__(self, fn, params, warmup=3, check=True, rtol=1e-5, agree=None):
         self.fn = fn
         self.params = list(params)
         self.graph = None
         self.static_out = None
         self.fallback_reason = None
+        self._agree = agree or (lambda ok: ok)
         self._capture(warmup, check, rtol)
 
     def _zero(self):
@@ -48,20 +58,29 @@ class CapturedStep:
         torch.cuda.synchronize()
         self._zero()
         g = torch.cuda.CUDAGraph()
+        ok = True
         try:
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g):  # records only: no collective runs during capture
                 out = self.fn()
-            g.replay()
-            torch.cuda.synchronize()
-        except RuntimeError as e:  # capture unsupported for some op: run eagerly
+        except RuntimeError as e:  # capture unsupported for some op
             self.fallback_reason = f"capture failed: {e}"
-            torch.cuda.synchronize()
+            ok = False
+        torch.cuda.synchronize()
+        if not self._agree(ok):
+            self.fallback_reason = self.fallback_reason or "capture failed on another rank"
+            self._zero()
             return
+        g.replay()
+        torch.cuda.synchronize()
         if check:
             a, b = float(out.detach().double()), float(ref.double())
-            if not abs(a - b) <= rtol * max(1.0, abs(b)):
+            ok = abs(a - b) <= rtol * max(1.0, abs(b))
+            if not ok:
                 self.fallback_reason = f"replayed loss {a!r} != eager loss {b!r}"
-                return
+        if not self._agree(ok):
+            self.fallback_reason = self.fallback_reason or "replay check failed on another rank"
+            self._zero()
+            return
         self.graph, self.static_out = g, out
 
     @property

@@ -437,8 +437,9 @@ class GraphAttnSfMLayer(Module):
         gfu = self.global_feature_update
         pfu = self.projection_feature_update
         W, b = gfu.lin_l_stack()
-        XL, token = Block0PrologueFn.apply(P.contiguous(), la.weight, la.bias, W, b, la.eps)
-        pts, view, glob = gfu.forward_fused(XL, plans, None, None, None)
+        pos = plans["proj2scenepoint"].pos
+        XL, token = Block0PrologueFn.apply(P.contiguous(), la.weight, la.bias, W, b, la.eps, pos)
+        pts, view, glob = gfu.forward_fused(XL, plans, None, None, None, xl_sorted=pos is not None)
         sp, sv, sg = pfu.node_terms(pts, view, glob)
         shard = plans.get("_shard")
         sv, sg = replicated_to_local(sv, shard), replicated_to_local(sg, shard)

@@ -205,9 +205,11 @@ int gasfm_segment_rowsum(const gasfm_work_item* items, int32_t n_items, const in
  * dbeta_a 2]), 1 -> edge0_epilogue_bwd ([dWp 64 | dWsk 64 | dbsk 32 | dgamma_b 2 | dbeta_b 2]). */
 int gasfm_edge0_part_rows(int32_t which, int64_t E, int32_t n_items);
 
-/* XL0[e] (8 floats) = W0 relu(LN_a(P[e])) + b0, W0 = [Wl_point; Wl_camera] [8 x 2]. */
+/* XL0[e] (8 floats) = W0 relu(LN_a(P[e])) + b0, W0 = [Wl_point; Wl_camera] [8 x 2].
+ * pos != NULL: the point half (4 floats) goes to row pos[e] (point-segment order), as in
+ * gasfm_edge_prologue_fwd. */
 int gasfm_edge0_prologue_fwd(const float* P, int64_t E, const float* ln_w, const float* ln_b, float eps,
-                             const float* W0, const float* b0, float* XL, void* stream);
+                             const float* W0, const float* b0, float* XL, const int32_t* pos, void* stream);
 
 /* P'[e] = Wsk relu(LN_b(P[e])) + bsk + scale*(Wp relu(LN_a(P[e])) + bp + Sp[pt] + Sv[cam] + Sg). */
 int gasfm_edge0_epilogue_fwd(const float* P, const int32_t* cam, const int32_t* pt, int64_t E,

@@ -197,3 +197,58 @@ def test_sharded_model_matches_single_gpu(device):
     # every parameter gradient ends bitwise identical on both ranks (replicated optimizer steps stay in sync)
     for k in g64:
         assert np.array_equal(res[0][4][k], res[1][4][k]), k
+
+
+def _worker_capture_agree(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import gasfm_amd
+        from gasfm_amd.graph_step import CapturedStep
+        from oracle.weights import deterministic_state_dict
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        sc = synthetic.scaled_config4(0.02, seed=5)
+        net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=2))
+        net.load_state_dict(deterministic_state_dict(net.state_dict()))
+        model = gd.ShardedGraphAttnSfMNet(net.to(dev))
+        data = gd.shard_scene(sc, rank, world, max_piece=64).to(dev)
+        cP = torch.ones((sc.m, 3, 4), device=dev)
+        cX = torch.ones((4, sc.n), device=dev)[:, data.point_slice].contiguous()
+
+        def fwd_bwd():
+            pred = model(data)
+            loss = (pred["Ps_norm"] * cP).sum() + (pred["pts3D"] * cX).sum()
+            loss.backward()
+            model.sync_grads()
+            return loss
+
+        def agree(ok):
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            return bool(t.item())
+
+        step = CapturedStep(fwd_bwd, net.parameters(), warmup=1, agree=agree)
+        loss = step()
+        g = net.equivariant_blocks[1].projection_feature_update.lin_proj.weight.grad
+        q.put((rank, step.captured, step.fallback_reason, float(loss), g.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_capture_fallback_is_agreed_across_ranks(device):
+    """gloo stages collectives through the host, so capture fails: every rank must fall back to
+    eager together (a rank-local fallback would desynchronise the collectives) and still step."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_capture_agree, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=600) for _ in procs), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [False, False], [r[2] for r in res]
+    assert np.array_equal(res[0][4], res[1][4])  # synced local-parameter gradient
