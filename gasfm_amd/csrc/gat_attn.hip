@@ -295,6 +295,148 @@ __global__ __launch_bounds__(kBlock, GASFM_FWD_MINWAVES) void attn_fwd_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// forward, XL streamed in segment order (perm == NULL) with direct-to-LDS prefetch.
+// Each wave owns a 5 KB LDS buffer: rows 0..31 of its item (8 lanes x 16 B per row, the image
+// is the lanes' load order, global_load_lds) + the XR row.  Per item: wait, copy the buffer to
+// registers, issue the NEXT item's rows into the same buffer (no VGPRs held while they fly),
+// then compute.  Items are wave-uniform scalar loads and no ordinary vector load is consumed
+// while the prefetch is in flight (hipcc would drain it with vmcnt(0)), except the extra
+// chunks of segments longer than 32 edges.  Geom<32,8> (the 32-wide convs) only.
+// ------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* lds_vptr;
+typedef const __attribute__((address_space(1))) void* glb_vptr;
+
+template <class G>
+__global__ __launch_bounds__(kBlock) void attn_fwd_glds_kernel(
+    const float* __restrict__ XL, int64_t ldXL, const float* __restrict__ XR, int64_t ldXR,
+    const float* __restrict__ att, const float* __restrict__ bias, const gasfm_work_item* __restrict__ items,
+    int n_items, float slope, int finalize, float* __restrict__ out, int64_t ldOut, float* __restrict__ seg_max,
+    float* __restrict__ seg_sum, int64_t ldStat, float* __restrict__ part) {
+  static_assert(G::VEC == 4 && G::LPE == 8 && G::EPR == 8 && G::U == 4 && G::HPL == 1, "Geom<32,8> only");
+  constexpr int LDP = G::HC + 2 * G::H;
+  __shared__ float4 lbuf[kBlock / kWave][5 * kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int row = lane / G::LPE;
+  const int li = lane % G::LPE;
+  const int f0 = li * G::VEC;
+  const int nwaves = gridDim.x * (blockDim.x / kWave);
+  float4* B = lbuf[threadIdx.x / kWave];
+  float attv[G::VEC], bv[G::VEC];  // in registers: no vector load inside the prefetch span
+  load_vec<G::VEC>(attv, att + f0);
+  if (finalize) load_vec<G::VEC>(bv, bias + f0);
+  auto issue = [&](const gasfm_work_item& w) {  // empty items issue nothing (their loop never runs)
+    if (w.begin >= w.end) return;
+    const int64_t safe = w.begin;
+#pragma unroll
+    for (int u = 0; u < G::U; ++u) {
+      const int64_t e = w.begin + u * G::EPR + row;
+      const float* src = XL + (e < w.end ? e : safe) * ldXL + f0;
+      __builtin_amdgcn_global_load_lds((glb_vptr)src, (lds_vptr)(B + u * kWave), 16, 0, 0);
+    }
+    __builtin_amdgcn_global_load_lds((glb_vptr)(XR + int64_t(w.seg) * ldXR + f0), (lds_vptr)(B + 4 * kWave), 16,
+                                     0, 0);
+  };
+  int it = wave_id_uniform();
+  gasfm_work_item wn{0, 0, 0, -1};
+  if (it < n_items) {
+    wn = items[it];
+    issue(wn);
+  }
+  for (; it < n_items; it += nwaves) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    float xl[G::U][G::VEC], xr[G::VEC];
+#pragma unroll
+    for (int u = 0; u < G::U; ++u) {
+      const float4 v = B[u * kWave + lane];
+      xl[u][0] = v.x;
+      xl[u][1] = v.y;
+      xl[u][2] = v.z;
+      xl[u][3] = v.w;
+    }
+    {
+      const float4 v = B[4 * kWave + lane];
+      xr[0] = v.x;
+      xr[1] = v.y;
+      xr[2] = v.z;
+      xr[3] = v.w;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const gasfm_work_item w = wn;
+    if (it + nwaves < n_items) {
+      wn = items[it + nwaves];
+      issue(wn);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch issue ahead of this item's compute
+    float m = -INFINITY, ssum = 0.f, acc[G::VEC] = {0.f, 0.f, 0.f, 0.f};
+    auto chunk = [&](int e0) {
+      bool valid[G::U];
+#pragma unroll
+      for (int u = 0; u < G::U; ++u) valid[u] = e0 + u * G::EPR + row < w.end;
+      float lg[G::U];
+#pragma unroll
+      for (int u = 0; u < G::U; ++u) {
+        float p = 0.f;
+#pragma unroll
+        for (int v = 0; v < G::VEC; ++v) p = fmaf(leaky(xl[u][v] + xr[v], slope), attv[v], p);
+        p = head_sum<G::LPH>(p);
+        lg[u] = valid[u] ? p : -INFINITY;
+      }
+      float cm = lg[0];
+#pragma unroll
+      for (int u = 1; u < G::U; ++u) cm = fmaxf(cm, lg[u]);
+      const float mn = fmaxf(m, cm);
+      const float f = safe_scale(m, mn);
+      ssum *= f;
+#pragma unroll
+      for (int v = 0; v < G::VEC; ++v) acc[v] *= f;
+#pragma unroll
+      for (int u = 0; u < G::U; ++u) {
+        const float pe = (lg[u] == -INFINITY) ? 0.f : __expf(lg[u] - mn);
+        ssum += pe;
+#pragma unroll
+        for (int v = 0; v < G::VEC; ++v) acc[v] = fmaf(pe, xl[u][v], acc[v]);
+      }
+      m = mn;
+    };
+    // first chunk straight from the prefetched registers: no vector-memory wait on this path
+    if (w.begin < w.end) chunk(w.begin);
+    // segments longer than 32 edges: further chunks with plain loads (these drain the prefetch)
+    for (int e0 = w.begin + G::EPR * G::U; e0 < w.end; e0 += G::EPR * G::U) {
+#pragma unroll
+      for (int u = 0; u < G::U; ++u) {
+        const int e = e0 + u * G::EPR + row;
+        load_vec<G::VEC>(xl[u], XL + int64_t(e < w.end ? e : e0) * ldXL + f0);
+      }
+      chunk(e0);
+    }
+    float mm[1] = {m}, ss[1] = {ssum};
+    reduce_rows<G>(mm, ss, acc);
+    if (row == 0) {
+      const bool head_leader = (li % G::LPH) == 0;
+      const int h0 = f0 / G::C;
+      if (w.slot < 0) {
+        float o[G::VEC];
+        const float inv = 1.f / (ss[0] + 1e-16f);
+#pragma unroll
+        for (int v = 0; v < G::VEC; ++v) o[v] = finalize ? fmaf(acc[v], inv, bv[v]) : acc[v];
+        store_vec<G::VEC>(out + int64_t(w.seg) * ldOut + f0, o);
+        if (head_leader) {
+          seg_max[int64_t(w.seg) * ldStat + h0] = mm[0];
+          seg_sum[int64_t(w.seg) * ldStat + h0] = ss[0];
+        }
+      } else {
+        float* pr = part + int64_t(w.slot) * LDP;
+        store_vec<G::VEC>(pr + f0, acc);
+        if (head_leader) {
+          pr[G::HC + h0] = mm[0];
+          pr[G::HC + G::H + h0] = ss[0];
+        }
+      }
+    }
+  }
+}
+
 // Ordered merge of partial states.  One workgroup per combine entry; rows of
 // the workgroup take slots k = row, row + R, ... in order and the row states
 // are merged in row order (first within a wave, then across waves via LDS),
@@ -716,6 +858,16 @@ static int env_wave_cap() {
   return cap;
 }
 
+// Direct-to-LDS forward for streamed (perm-free) 32-wide convs: default on (point direction
+// 165 -> 140 us, camera 109 -> 106 us on config 4); GASFM_ATTN_GLDS=0 selects the register path.
+static bool glds_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("GASFM_ATTN_GLDS");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 static int grid_for(int n_items, int resident) {
   int waves = n_items > 0 ? n_items : 1;
   const int cap = env_wave_cap() ? env_wave_cap() : resident * (kBlock / kWave);
@@ -755,7 +907,15 @@ extern "C" int gasfm_gat_attn_fwd(const float* XL, int64_t ldXL, const float* XR
                       aligned16(XL) && aligned16(XR) && aligned16(out) && aligned16(att) &&
                       aligned16(bias) && (!part || aligned16(part)) && ((H * C + 2 * H) % 4 == 0);
   bool done = false;
-  if (vec_ok) {
+  if (vec_ok && perm == nullptr && H * C == 32 && C == 8 && glds_enabled()) {
+    using G = Geom<32, 8>;
+    const int grid =
+        grid_for(n_items, resident_blocks(reinterpret_cast<const void*>(&attn_fwd_glds_kernel<G>), kBlock, 0));
+    hipLaunchKernelGGL((attn_fwd_glds_kernel<G>), dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att, bias,
+                       items, n_items, slope, finalize, out, ldOut, seg_max, seg_sum, ldStat, part);
+    done = true;
+  }
+  if (vec_ok && !done) {
     done = dispatch_shape(H, C, [&](auto g) {
       using G = decltype(g);
       const int grid = grid_for(n_items, resident_blocks(reinterpret_cast<const void*>(&attn_fwd_kernel<G>), kBlock, 0));
