@@ -657,9 +657,170 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_kernel(
   }
 }
 
-// dXR[seg] = ordered sum of its partial slots.  One workgroup per entry: thread t owns
-// column t % HC and slot group t / HC (R = 256/HC groups, or 1 with column loops for
-// HC > 256); the group sums are added in group order, so the result is deterministic.
+// ------------------------------------------------------------------------------------------
+// backward with direct-to-LDS prefetch (Geom<32,8>; XL read at segment position e, i.e.
+// perm == NULL or xl_by_position).  Per item, six global_load_lds into a wave-private buffer:
+// the 32 rows of the first chunk, one instruction whose lane groups fetch XR / gout / out /
+// seg_max / seg_sum of the segment, and perm of the 32 rows (the dXL destinations).  Empty
+// items still fetch their segment data (d bias sums gout over every segment).
+// ------------------------------------------------------------------------------------------
+template <class G>
+__global__ __launch_bounds__(kBlock) void attn_bwd_glds_kernel(
+    const float* __restrict__ XL, int64_t ldXL, const float* __restrict__ XR, int64_t ldXR,
+    const float* __restrict__ att, const float* __restrict__ bias, const int32_t* __restrict__ perm,
+    const gasfm_work_item* __restrict__ items, int n_items, float slope, const float* __restrict__ out,
+    int64_t ldOut, const float* __restrict__ seg_max, const float* __restrict__ seg_sum,
+    const float* __restrict__ gout, int64_t ldG, float* __restrict__ dXL, int64_t ldDXL,
+    float* __restrict__ dXR, int64_t ldDXR, float* __restrict__ part_dxr, float* __restrict__ datt_part) {
+  static_assert(G::VEC == 4 && G::LPE == 8 && G::EPR == 8 && G::U == 4 && G::HPL == 1 && G::LPH == 2,
+                "Geom<32,8> only");
+  constexpr int RB = G::U * kWave;  // float4 slots of the 32 rows
+  __shared__ float4 lbuf[kBlock / kWave][RB + kWave + kWave / 4];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int row = lane / G::LPE;
+  const int li = lane % G::LPE;
+  const int f0 = li * G::VEC;
+  const int h0 = f0 / G::C;
+  const int wave = wave_id_uniform();
+  const int nwaves = gridDim.x * (blockDim.x / kWave);
+  float4* B = lbuf[threadIdx.x / kWave];
+  int32_t* Bp = reinterpret_cast<int32_t*>(B + RB + kWave);
+  float attv[G::VEC], bv[G::VEC], datt[G::VEC], dbias[G::VEC];
+  load_vec<G::VEC>(attv, att + f0);
+  load_vec<G::VEC>(bv, bias + f0);
+#pragma unroll
+  for (int v = 0; v < G::VEC; ++v) datt[v] = dbias[v] = 0.f;
+  // segment-data lane groups: 0 XR, 1 gout, 2 out, 3 stats (lane 24 seg_max, 25 seg_sum)
+  const int grp = lane >> 3;
+  auto issue = [&](const gasfm_work_item& w) {
+    const int64_t sg = w.seg;
+    const float* src = XR + sg * ldXR + f0;
+    if (grp == 1) src = gout + sg * ldG + f0;
+    if (grp == 2) src = out + sg * ldOut + f0;
+    if (grp == 3 && li == 0) src = seg_max + sg * G::H;
+    if (grp == 3 && li == 1) src = seg_sum + sg * G::H;
+    __builtin_amdgcn_global_load_lds((glb_vptr)src, (lds_vptr)(B + RB), 16, 0, 0);
+    if (w.begin >= w.end) return;
+    const int64_t safe = w.begin;
+#pragma unroll
+    for (int u = 0; u < G::U; ++u) {
+      const int64_t e = w.begin + u * G::EPR + row;
+      __builtin_amdgcn_global_load_lds((glb_vptr)(XL + (e < w.end ? e : safe) * ldXL + f0),
+                                       (lds_vptr)(B + u * kWave), 16, 0, 0);
+    }
+    if (perm) {
+      const int64_t e = w.begin + lane;
+      __builtin_amdgcn_global_load_lds((glb_vptr)(perm + (e < w.end ? e : safe)), (lds_vptr)Bp, 4, 0, 0);
+    }
+  };
+  int it = wave;
+  gasfm_work_item wn{0, 0, 0, -1};
+  if (it < n_items) {
+    wn = items[it];
+    issue(wn);
+  }
+  for (; it < n_items; it += nwaves) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const gasfm_work_item w = wn;
+    float xl[G::U][G::VEC], xr[G::VEC], g[G::VEC], o[G::VEC];
+    int64_t dst[G::U];
+#pragma unroll
+    for (int u = 0; u < G::U; ++u) {
+      const float4 v = B[u * kWave + lane];
+      xl[u][0] = v.x;
+      xl[u][1] = v.y;
+      xl[u][2] = v.z;
+      xl[u][3] = v.w;
+      const int64_t e = w.begin + u * G::EPR + row;
+      dst[u] = perm ? int64_t(Bp[u * G::EPR + row]) : e;
+    }
+    {
+      const float4 a = B[RB + li], b = B[RB + 8 + li], c = B[RB + 16 + li];
+      xr[0] = a.x, xr[1] = a.y, xr[2] = a.z, xr[3] = a.w;
+      g[0] = b.x, g[1] = b.y, g[2] = b.z, g[3] = b.w;
+      o[0] = c.x, o[1] = c.y, o[2] = c.z, o[3] = c.w;
+    }
+    const float4 smx = B[RB + 24], ssm = B[RB + 25];
+    const float smxv[4] = {smx.x, smx.y, smx.z, smx.w}, ssmv[4] = {ssm.x, ssm.y, ssm.z, ssm.w};
+    const float M = smxv[h0], inv = 1.f / (ssmv[h0] + 1e-16f);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const bool first = it == 0 || items[it - 1].seg != w.seg;
+    if (it + nwaves < n_items) {
+      wn = items[it + nwaves];
+      issue(wn);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch issue ahead of this item's compute
+    // d bias = sum of gout over segments: each segment once (its first item) on row 0
+    if (row == 0 && first) {
+#pragma unroll
+      for (int v = 0; v < G::VEC; ++v) dbias[v] += g[v];
+    }
+    float d = 0.f;
+#pragma unroll
+    for (int v = 0; v < G::VEC; ++v) d = fmaf(g[v], o[v] - bv[v], d);
+    const float delta = head_sum<G::LPH>(d);
+    float dxr[G::VEC] = {0.f, 0.f, 0.f, 0.f};
+    auto chunk = [&](int e0) {
+#pragma unroll
+      for (int u = 0; u < G::U; ++u) {
+        const bool valid = e0 + u * G::EPR + row < w.end;
+        float z[G::VEC], dx[G::VEC];
+        float p = 0.f, da = 0.f;
+#pragma unroll
+        for (int v = 0; v < G::VEC; ++v) {
+          z[v] = xl[u][v] + xr[v];
+          p = fmaf(leaky(z[v], slope), attv[v], p);
+          da = fmaf(g[v], xl[u][v], da);
+        }
+        p = head_sum<G::LPH>(p);
+        da = head_sum<G::LPH>(da);
+        const float alpha = valid ? __expf(p - M) * inv : 0.f;
+        const float de = alpha * (da - delta);
+#pragma unroll
+        for (int v = 0; v < G::VEC; ++v) {
+          const float dz = de * attv[v] * (z[v] > 0.f ? 1.f : slope);
+          dx[v] = fmaf(alpha, g[v], dz);
+          dxr[v] += dz;
+          datt[v] = fmaf(de, leaky(z[v], slope), datt[v]);
+        }
+        if (valid) store_vec<G::VEC>(dXL + dst[u] * ldDXL + f0, dx);
+      }
+    };
+    if (w.begin < w.end) chunk(w.begin);
+    for (int e0 = w.begin + G::EPR * G::U; e0 < w.end; e0 += G::EPR * G::U) {  // long segments
+#pragma unroll
+      for (int u = 0; u < G::U; ++u) {
+        const int e = e0 + u * G::EPR + row;
+        const int ec = e < w.end ? e : e0;
+        load_vec<G::VEC>(xl[u], XL + int64_t(ec) * ldXL + f0);
+        dst[u] = perm ? int64_t(perm[ec]) : int64_t(e);
+      }
+      chunk(e0);
+    }
+#pragma unroll
+    for (int o2 = G::LPE; o2 < kWave; o2 <<= 1) {
+#pragma unroll
+      for (int v = 0; v < G::VEC; ++v) dxr[v] += __shfl_xor(dxr[v], o2);
+    }
+    if (row == 0) {
+      if (w.slot < 0)
+        store_vec<G::VEC>(dXR + int64_t(w.seg) * ldDXR + f0, dxr);
+      else
+        store_vec<G::VEC>(part_dxr + int64_t(w.slot) * G::HC + f0, dxr);
+    }
+  }
+#pragma unroll
+  for (int o2 = G::LPE; o2 < kWave; o2 <<= 1) {
+#pragma unroll
+    for (int v = 0; v < G::VEC; ++v) datt[v] += __shfl_xor(datt[v], o2);
+  }
+  if (row == 0) {
+    store_vec<G::VEC>(datt_part + int64_t(wave) * 2 * G::HC + f0, datt);
+    store_vec<G::VEC>(datt_part + int64_t(wave) * 2 * G::HC + G::HC + f0, dbias);
+  }
+}
+
+// dXR[seg] = ordered sum of its partial slots.
 // grid = (combine entries, column blocks of CB = min(HC, 64)): R = kBlock / CB row groups take
 // slots k = grp, grp + R, ... and are added in group order (deterministic for a given HC).
 __global__ __launch_bounds__(kBlock) void attn_bwd_combine_kernel(const gasfm_combine_item* __restrict__ comb,
@@ -968,6 +1129,10 @@ static int bwd_grid(int n_items, int H, int C) {
     const int r = resident_blocks(reinterpret_cast<const void*>(&attn_bwd_kernel<G>), kBlock, 0);
     res = r < res ? r : res;
   });
+  if (H * C == 32 && C == 8) {
+    const int r = resident_blocks(reinterpret_cast<const void*>(&attn_bwd_glds_kernel<Geom<32, 8>>), kBlock, 0);
+    res = r < res ? r : res;
+  }
   return grid_for(n_items, res);
 }
 
@@ -994,7 +1159,14 @@ extern "C" int gasfm_gat_attn_bwd(const float* XL, int64_t ldXL, const float* XR
                       aligned16(gout) && aligned16(dXL) && aligned16(dXR) && aligned16(att) &&
                       aligned16(bias) && aligned16(datt_part) && (!part_dxr || aligned16(part_dxr));
   bool done = false;
-  if (vec_ok) {
+  if (vec_ok && H * C == 32 && C == 8 && (perm == nullptr || xl_by_position) && glds_enabled() &&
+      aligned16(seg_max) && aligned16(seg_sum)) {
+    hipLaunchKernelGGL((attn_bwd_glds_kernel<Geom<32, 8>>), dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR,
+                       att, bias, perm, items, n_items, slope, out, ldOut, seg_max, seg_sum, gout, ldG, dXL, ldDXL,
+                       dXR, ldDXR, part_dxr, datt_part);
+    done = true;
+  }
+  if (vec_ok && !done) {
     done = dispatch_shape(H, C, [&](auto g) {
       using G = decltype(g);
       hipLaunchKernelGGL((attn_bwd_kernel<G>), dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att, bias,
