@@ -5,7 +5,7 @@ set -e
 ROOT=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "attn_fwd_kernel" --output-format csv \
+  timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "attn_fwd" --output-format csv \
     -d $ROOT/gpurun_out/pmc_$C -o run -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline \
     > $ROOT/gpurun_out/pmc_$C.log 2>&1
 done
