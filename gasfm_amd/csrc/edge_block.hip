@@ -62,16 +62,27 @@ __device__ __forceinline__ void load_rows32(const float* __restrict__ P, int64_t
 // LayerNorm of the row-layout registers v (rows >= nrows written as zeros): x_hat (pre-affine;
 // identity when !LN) to Xh, relu(x_hat*g+b) (x when !LN) to Ph, raw values to Raw (each
 // optional, LDS stride 34) and rstd to Rs.  Row statistics by 3 xor-shuffles over 8 lanes.
+// LayerNorm affine parameters of this lane's 4 columns (row layout), loaded once per kernel:
+// a per-tile reload is a plain load consumed at once, which drains any prefetch in flight.
+struct Affine4 {
+  float4 g, b;
+};
 template <bool LN>
-__device__ __forceinline__ void norm_rows32(const float4 (&v)[2], int nrows, const float* __restrict__ gam,
-                                            const float* __restrict__ bet, float eps, float* Xh, float* Ph,
-                                            float* Raw, float* Rs, int lane) {
-  const int c = (lane & 7) * 4;
-  float4 g4 = make_float4(1.f, 1.f, 1.f, 1.f), b4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (LN && Ph) {
-    g4 = *reinterpret_cast<const float4*>(gam + c);
-    b4 = *reinterpret_cast<const float4*>(bet + c);
+__device__ __forceinline__ Affine4 load_affine(const float* __restrict__ gam, const float* __restrict__ bet,
+                                               int lane) {
+  Affine4 a{make_float4(1.f, 1.f, 1.f, 1.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+  if (LN && gam) {
+    a.g = *reinterpret_cast<const float4*>(gam + (lane & 7) * 4);
+    a.b = *reinterpret_cast<const float4*>(bet + (lane & 7) * 4);
   }
+  return a;
+}
+
+template <bool LN>
+__device__ __forceinline__ void norm_rows32(const float4 (&v)[2], int nrows, const Affine4& af, float eps,
+                                            float* Xh, float* Ph, float* Raw, float* Rs, int lane) {
+  const int c = (lane & 7) * 4;
+  const float4 g4 = af.g, b4 = af.b;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int r = (lane >> 3) + 8 * u;
@@ -108,16 +119,15 @@ __device__ __forceinline__ void norm_rows32(const float4 (&v)[2], int nrows, con
 
 template <bool LN>
 __device__ __forceinline__ void load_norm_tile(const float* __restrict__ P, int64_t row0, int nrows,
-                                               const float* __restrict__ gam, const float* __restrict__ bet,
-                                               float eps, float* Xh, float* Ph, float* Raw, float* Rs, int lane,
-                                               float4* raw_regs = nullptr) {
+                                               const Affine4& af, float eps, float* Xh, float* Ph, float* Raw,
+                                               float* Rs, int lane, float4* raw_regs = nullptr) {
   float4 v[2];
   load_rows32(P, row0, nrows, v, lane);
   if (raw_regs) {
     raw_regs[0] = v[0];
     raw_regs[1] = v[1];
   }
-  norm_rows32<LN>(v, nrows, gam, bet, eps, Xh, Ph, Raw, Rs, lane);
+  norm_rows32<LN>(v, nrows, af, eps, Xh, Ph, Raw, Rs, lane);
 }
 
 // =====================================================================================
@@ -142,19 +152,39 @@ __global__ __launch_bounds__(kThreads) void edge_prologue_fwd_kernel(const float
   float* T = tiles[wave];
   float* Yt = T + TR * LD34;
   const float4 bias = *reinterpret_cast<const float4*>(b + c4);
+  const Affine4 af = load_affine<LN>(gam, bet, lane);
   const int64_t ntiles = (E + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWaves + wave, nw = int64_t(gridDim.x) * kWaves;
+  auto rows_of = [&](int64_t t) { return int(E - t * TR < TR ? E - t * TR : TR); };
+  // register copy of the next tile: P rows (row layout of load_rows32) and the point-order
+  // destinations of this lane's output rows (row (lane>>4) + 4u)
+  float4 np[2];
+  int32_t npos[4] = {0, 0, 0, 0};
+  auto issue = [&](int64_t t) {
+    const int64_t row0 = t * TR;
+    const int nrows = rows_of(t);
+    load_rows32(P, row0, nrows, np, lane);
+    if (pos) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = (lane >> 4) + 4 * u;
+        npos[u] = pos[row0 + (r < nrows ? r : 0)];  // clamped, no per-element branch
+      }
+    }
+  };
+  if (gw < ntiles) issue(gw);
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row0 = t * TR;
-    const int nrows = int(E - row0 < TR ? E - row0 : TR);
-    // destination rows first (the point half goes to the edge's position in point order)
+    const int nrows = rows_of(t);
     int64_t dst[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int r = (lane >> 4) + 4 * u;
-      dst[u] = (pos && c4 < F && r < nrows) ? int64_t(pos[row0 + r]) : row0 + r;
+      // the point half (columns 0..31) goes to the edge's position in point order
+      dst[u] = (pos && c4 < F) ? int64_t(npos[u]) : row0 + r;
     }
-    load_norm_tile<LN>(P, row0, nrows, gam, bet, eps, nullptr, T, nullptr, nullptr, lane);
+    norm_rows32<LN>(np, nrows, af, eps, nullptr, T, nullptr, nullptr, lane);
+    if (t + nw < ntiles) issue(t + nw);  // next tile in flight during this tile's MFMA and stores
     wave_sync();
     f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
@@ -201,6 +231,7 @@ __global__ __launch_bounds__(kThreads) void edge_epilogue_fwd_kernel(
   const int cc = (lane & 7) * 4;             // row layout: row (lane>>3) + 8u, columns cc..cc+3
   float* Ph = tiles[wave];
   float* Yt = Ph + TR * LD34;
+  const Affine4 af = load_affine<true>(gam, bet, lane);
   float w32[4], w33[4], cst[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -211,23 +242,42 @@ __global__ __launch_bounds__(kThreads) void edge_epilogue_fwd_kernel(
   }
   const int64_t ntiles = (E + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWaves + wave, nw = int64_t(gridDim.x) * kWaves;
-  for (int64_t t = gw; t < ntiles; t += nw) {
+  auto rows_of = [&](int64_t t) { return int(E - t * TR < TR ? E - t * TR : TR); };
+  // register copy of the next tile (row layout): P rows, P0 pairs, camera / point indices.
+  // With the indices one tile ahead, a tile's Sp / Sv gathers wait one latency, not two.
+  float4 np[2];
+  float2 nq[2];
+  int32_t ncam[2], npt[2];
+  auto issue = [&](int64_t t) {
     const int64_t row0 = t * TR;
-    const int nrows = int(E - row0 < TR ? E - row0 : TR);
-    // node-term gathers first: their latency overlaps the LayerNorm and the MFMA
-    float4 sp[2], sv[2];
-    float2 q0[2];
+    const int nrows = rows_of(t);
+    load_rows32(P, row0, nrows, np, lane);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int r = (lane >> 3) + 8 * u;
-      const bool live = r < nrows;
-      const int64_t ci = live ? cam[row0 + r] : 0, pi = live ? pt[row0 + r] : 0;
-      sp[u] = *reinterpret_cast<const float4*>(Sp + pi * F + cc);
-      sv[u] = *reinterpret_cast<const float4*>(Sv + ci * F + cc);
-      q0[u] = (P0 && live) ? *reinterpret_cast<const float2*>(P0 + (row0 + r) * 2) : make_float2(0.f, 0.f);
+      const int64_t e = row0 + (r < nrows ? r : 0);  // clamped, no per-element branch
+      ncam[u] = cam[e];
+      npt[u] = pt[e];
+      nq[u] = P0 ? *reinterpret_cast<const float2*>(P0 + e * 2) : make_float2(0.f, 0.f);
     }
+  };
+  if (gw < ntiles) issue(gw);
+  for (int64_t t = gw; t < ntiles; t += nw) {
+    const int64_t row0 = t * TR;
+    const int nrows = rows_of(t);
+    // this tile's node-term gathers: their latency overlaps the LayerNorm and the MFMA
+    float4 sp[2], sv[2];
+    float2 q0[2];
     float4 raw[2];
-    load_norm_tile<true>(P, row0, nrows, gam, bet, eps, nullptr, Ph, nullptr, nullptr, lane, raw);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      sp[u] = *reinterpret_cast<const float4*>(Sp + int64_t(npt[u]) * F + cc);
+      sv[u] = *reinterpret_cast<const float4*>(Sv + int64_t(ncam[u]) * F + cc);
+      q0[u] = nq[u];
+      raw[u] = np[u];
+    }
+    norm_rows32<true>(raw, nrows, af, eps, nullptr, Ph, nullptr, nullptr, lane);
+    if (t + nw < ntiles) issue(t + nw);
     wave_sync();
     f32x4 acc[2] = {zero4(), zero4()};
 #pragma unroll
@@ -297,6 +347,7 @@ __global__ __launch_bounds__(kThreads) void edge_epilogue_bwd_kernel(
   }
   f32x4 accW[2][2] = {{zero4(), zero4()}, {zero4(), zero4()}};
   float accP0[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+  const Affine4 af = load_affine<true>(gam, bet, lane);
   // register copy of the next tile: dP' and P rows (row layout), P0 (lanes < 2*nrows)
   float4 nd[2], np[2];
   float nq = 0.f;
@@ -326,7 +377,7 @@ __global__ __launch_bounds__(kThreads) void edge_epilogue_bwd_kernel(
           d[2] = nd[u].z;
           d[3] = nd[u].w;
         }
-        norm_rows32<true>(np, nrows, gam, bet, eps, nullptr, Ph, nullptr, nullptr, lane);
+        norm_rows32<true>(np, nrows, af, eps, nullptr, Ph, nullptr, nullptr, lane);
         if (lane < 2 * TR) Q0[lane] = nq;
       }
       if (row0 + TR < w.end) issue(row0 + TR, w.end - (row0 + TR) < TR ? int(w.end - (row0 + TR)) : TR);
