@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from Python (no hipGraph)")
     ap.add_argument("--cpu-sample-scale", type=float, default=0.1)
+    ap.add_argument("--dist", action="store_true",
+                    help="run the point-sharded RCCL path even at one rank (under torchrun --nproc-per-node 1)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -108,7 +110,8 @@ def main():
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    dist_on = world > 1 or args.dist
+    if dist_on:
         torch.distributed.init_process_group("nccl", device_id=dev)
         log(f"[rank {rank}] process group up (world {world})")
 
@@ -121,7 +124,7 @@ def main():
     conf = gasfm_amd.learning_conf(num_layers=args.layers)
     torch.manual_seed(0)
     net = gasfm_amd.GraphAttnSfMNet(conf)
-    if world > 1:
+    if dist_on:
         from gasfm_amd import distributed as gdist
         data = gdist.shard_scene(sc, rank, world).to(dev)
         model = gdist.ShardedGraphAttnSfMNet(net.to(dev))
@@ -133,14 +136,14 @@ def main():
     cX = torch.randn((4, sc.n), generator=gen).to(dev)
     log(f"[rank {rank}] scene m={sc.m} n={sc.n} E={E} built+moved in {time.time() - t0:.1f}s")
 
-    cx = cX if world == 1 else cX[:, data.point_slice].contiguous()
+    cx = cX if not dist_on else cX[:, data.point_slice].contiguous()
 
     def fwd_bwd():
         pred = model(data)
         # replicated outputs enter every rank's loss in full, local points once (distributed.py)
         loss = (pred["Ps_norm"] * cP).sum() + (pred["pts3D"] * cx).sum()
         loss.backward()
-        if world > 1:
+        if dist_on:
             model.sync_grads()
         return loss
 
@@ -160,7 +163,7 @@ def main():
         # warm-up steps run inside CapturedStep (before capture); every timed step replays
         # the captured forward+backward (+ gradient all-reduce) as one hipGraph launch
         agree = None
-        if world > 1:
+        if dist_on:
             def agree(ok):  # AND over ranks, one collective outside the graph
                 t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
                 torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
@@ -170,17 +173,17 @@ def main():
         execution = ("hipGraph replay of the captured forward+backward step" if captured.captured
                      else f"eager fallback ({captured.fallback_reason})")
         log(f"[rank {rank}] {execution}")
-    if world > 1:
+    if dist_on:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         torch.distributed.barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([dt], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
@@ -223,8 +226,8 @@ def main():
             "config": {"workload": f"config 4: m={sc.m} cameras, n={sc.n} points, E={E} projections, "
                                    f"{args.layers}-block GraphAttnSfMNet (learning_euc widths) fwd+bwd",
                        "cameras": sc.m, "points": sc.n, "edges": E, "blocks": args.layers,
-                       "parallelism": f"point-sharded x{world}" if world > 1 else "single GPU"},
-            "roofline": {"kernel": "attn_fwd_kernel<32,8> point direction (proj2scenepoint), per launch",
+                       "parallelism": f"point-sharded x{world}" if dist_on else "single GPU"},
+            "roofline": {"kernel": "attn_fwd_glds_kernel<32,8> point direction (proj2scenepoint), per launch",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                          "traffic": pmc_traffic(e_local, n_local),
@@ -237,7 +240,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dist_on:
         torch.distributed.destroy_process_group()
 
 

@@ -58,6 +58,14 @@ _SIGS = {
     "gasfm_gvec_bwd": (_i32, [_vp, _vp, _i32, _vp, _vp, _f32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_node_ln_linear_fwd": (_i32, [_vp, _i64, _i32, _vp, _vp, _f32, _vp, _vp, _i32, _i32, _vp, _i64, _vp]),
     "gasfm_node_ln_linear_bwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp, _f32, _vp, _i32, _i32, _vp, _vp, _vp]),
+    "gasfm_point_tail_part_shape": (_i32, [_i64, _i32, _vp]),
+    "gasfm_point_hub_part_shape": (_i32, [_i64, _i32, _i32, _vp]),
+    "gasfm_point_tail_fwd": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
+    "gasfm_point_tail_bwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_point_hub_fwd": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _vp, _vp, _vp]),
+    "gasfm_point_hub_bwd_c": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_point_hub_bwd_ab": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
 }
 
 _lib = None
@@ -326,3 +334,63 @@ def gvec_bwd(dy, x, ln_w, ln_b, eps, W, resid, dx, dW, db, dgam, dbet, part):
     st = lib().gasfm_gvec_bwd(_p(dy), _p(x), W.shape[1], _p(ln_w), _p(ln_b), eps, _p(W), W.shape[0], int(resid),
                               _p(dx), _p(dW), _p(db), _p(dgam), _p(dbet), _p(part), _stream(x))
     check(st, "gasfm_gvec_bwd")
+
+
+# ---------------------------------------------------------------- scene-point block chains (point_block.hip)
+def point_tail_part_shape(N, has_prev):
+    cols = ctypes.c_int32(0)
+    rows = lib().gasfm_point_tail_part_shape(N, int(has_prev), ctypes.byref(cols))
+    return rows, cols.value
+
+
+def point_hub_part_shape(N, which, has_res):
+    cols = ctypes.c_int32(0)
+    rows = lib().gasfm_point_hub_part_shape(N, int(which), int(has_res), ctypes.byref(cols))
+    return rows, cols.value
+
+
+def point_tail_fwd(prev, agg, Wp, bp, ln_w, ln_b, eps, Wm, bm, out):
+    _req(agg, "agg", 32)
+    if prev is not None:
+        _req(prev, "prev", 64)
+    st = lib().gasfm_point_tail_fwd(_p(prev), _p(agg), agg.shape[0], _p(Wp), _p(bp), _p(ln_w), _p(ln_b), eps,
+                                    _p(Wm), _p(bm), _p(out), _stream(agg))
+    check(st, "gasfm_point_tail_fwd")
+
+
+def point_tail_bwd(dout, prev, agg, Wp, bp, ln_w, ln_b, eps, Wm, dx, dagg, part):
+    _req(dout, "dout", 64)
+    _req(agg, "agg", 32)
+    if prev is not None:
+        _req(prev, "prev", 64)
+    st = lib().gasfm_point_tail_bwd(_p(dout), _p(prev), _p(agg), agg.shape[0], _p(Wp), _p(bp), _p(ln_w), _p(ln_b),
+                                    eps, _p(Wm), _p(dx), _p(dagg), _p(part), _stream(agg))
+    check(st, "gasfm_point_tail_bwd")
+
+
+def point_hub_fwd(X, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR):
+    _req(X, "X", 64)
+    st = lib().gasfm_point_hub_fwd(_p(X), X.shape[0], eps, _p(gA), _p(bA), _p(WA), _p(SA), _p(WB), _p(bB), _p(XL),
+                                   _p(gC), _p(bC), _p(WC), _p(bWC), _p(WD), _p(bD), _p(XR), _stream(X))
+    check(st, "gasfm_point_hub_fwd")
+
+
+def point_hub_bwd_c(X, eps, gC, bC, WC, bWC, WD, dXR, dRes, dX, part):
+    _req(X, "X", 64)
+    _req(dXR, "dXR", 32)
+    if dRes is not None:
+        _req(dRes, "dRes", 64)
+    st = lib().gasfm_point_hub_bwd_c(_p(X), X.shape[0], eps, _p(gC), _p(bC), _p(WC), _p(bWC), _p(WD), _p(dXR),
+                                     _p(dRes), _p(dX), _p(part), _stream(X))
+    check(st, "gasfm_point_hub_bwd_c")
+
+
+def point_hub_bwd_ab(X, eps, gA, bA, WA, WB, dSA, dXL, dRes, dX, part):
+    _req(X, "X", 64)
+    _req(dSA, "dSA", 32)
+    _req(dXL, "dXL", 64)
+    if dRes is not None:
+        _req(dRes, "dRes", 64)
+    st = lib().gasfm_point_hub_bwd_ab(_p(X), X.shape[0], eps, _p(gA), _p(bA), _p(WA), _p(WB), _p(dSA), _p(dXL),
+                                      _p(dRes), _p(dX), _p(part), _stream(X))
+    check(st, "gasfm_point_hub_bwd_ab")

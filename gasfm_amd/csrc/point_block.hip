@@ -1,0 +1,945 @@
+// Fused scene-point (64-wide row) chains of a GASFM block, gfx950.
+//
+// Every consumer of a block's point features p [n x 64] runs in ONE kernel per direction:
+//
+//   tail (produces p, reference Proj2ScenePoint.forward, code/models/layers.py:418-458):
+//     x = prev + W_p agg + b_p                     proj_proj2scenepoint + state skip  :438-444
+//     p = x + W_m relu(LN(x)) + b_m                norm_pre_mlp, ReLU, mlp, skip      :447-454
+//   hub (consumes p):
+//     s  = W_A relu(LN_A(p))                       ProjectionFeatureUpdate lin_scenepoint  :924-935
+//     xl = W_B p + b_B                             ViewAndScenePoint2Global scenepoint lin_l (:560-575)
+//     xr = W_D (W_C relu(LN_C(p)) + b_C) + b_D     NEXT block's norm_and_proj_scenepoint2proj
+//                                                  (:429) and its GATv2 lin_r (target rows)
+//   plus the identity output p -> next block's state skip (:442).
+//
+// The point tensor is 51 MB at config 4.  aten runs these chains as ~8 kernels forward
+// (LayerNorm, clamp, GEMMs, adds) and ~20 backward, re-reading p for every consumer, and
+// autograd sums the four gradients of p with three more full-size adds.  Here the backward
+// of the hub reads the four upstream gradients once and writes dp once (the skip gradient
+// arrives as the hub's identity output), and the tail's backward writes d prev (== dx) and
+// d agg in the same pass.
+//
+// Layout: wave = 16-row tile (tile.hpp); GEMMs on v_mfma_f32_16x16x4_f32 against weights
+// staged once per workgroup in LDS (row stride 80 for 64 columns, 48 for 32: == 16 mod 32,
+// conflict-free B reads).  LayerNorm statistics are recomputed from p in the backward pass.
+// Weight / bias / gamma / beta gradients leave as per-workgroup partial rows reduced by
+// gasfm_colsum in a fixed order (deterministic, no atomics).
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+#include "tile.hpp"
+
+namespace gasfm {
+namespace {
+
+using namespace tile;
+
+constexpr int FP = 64;  // n_feat_scenepoint
+constexpr int FA = 32;  // n_feat_proj (aggregation / projection width)
+constexpr int L66 = 66, L34 = 34, L80 = 80, L48 = 48;
+constexpr int kWaves8 = 8, kThreads8 = kWaves8 * kW;
+
+// partial-row layouts (floats)
+constexpr int TAIL_PART = FP * FP + FP * FA + 4 * FP;                 // dWm dWp dbm dbp dgam dbet
+
+// A-operand element (row i of a [rows x ld] matrix, column k) of a 16-row tile; rows past
+// nrows read row 0 and return 0 (unconditional load, see tile.hpp load_tile)
+__device__ __forceinline__ float ld_a(const float* __restrict__ P, int ld, int64_t row0, int nrows, int i, int k) {
+  const float v = P[(row0 + (i < nrows ? i : 0)) * ld + k];
+  return i < nrows ? v : 0.f;
+}
+
+// 16 x 64 tile of rows into LDS (row stride 66) with per-row mean / rstd (MS, RS)
+__device__ __forceinline__ void load_rows_stats(const float* __restrict__ X, int64_t row0, int nrows, float eps,
+                                                float* Raw, float* MS, float* RS, int lane) {
+  const int c = (lane & 15) * 4;
+  float4 v[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int r = (lane >> 4) + 4 * u;
+    v[u] = *reinterpret_cast<const float4*>(X + (row0 + (r < nrows ? r : 0)) * FP + c);
+    if (r >= nrows) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int r = (lane >> 4) + 4 * u;
+    const float x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Raw[r * L66 + c + k] = x[k];
+    const float mean = sum16(x[0] + x[1] + x[2] + x[3]) * (1.f / FP);
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q = fmaf(x[k] - mean, x[k] - mean, q);
+    const float rstd = rsqrtf(sum16(q) * (1.f / FP) + eps);
+    if ((lane & 15) == 0) {
+      MS[r] = mean;
+      RS[r] = rstd;
+    }
+  }
+}
+
+// LayerNorm + ReLU backward of one row held as 16 lanes x 4 column tiles (C layout):
+// returns dx, accumulates dgamma / dbeta.  dh: upstream gradient of relu(xh*g + b).
+__device__ __forceinline__ void ln_relu_bwd_row(const float (&xh)[4], const float (&dh)[4], const float (&g)[4],
+                                                const float (&b)[4], float rstd, float (&dg)[4], float (&db)[4],
+                                                float (&dx)[4]) {
+  float gv[4], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const float dy = fmaf(xh[nt], g[nt], b[nt]) > 0.f ? dh[nt] : 0.f;
+    dg[nt] = fmaf(dy, xh[nt], dg[nt]);
+    db[nt] += dy;
+    gv[nt] = dy * g[nt];
+    s1 += gv[nt];
+    s2 = fmaf(gv[nt], xh[nt], s2);
+  }
+  s1 = sum16(s1) * (1.f / FP);
+  s2 = sum16(s2) * (1.f / FP);
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) dx[nt] = rstd * (gv[nt] - s1 - xh[nt] * s2);
+}
+
+// ----------------------------------------------------------------------------- tail
+template <bool PREV>
+__global__ __launch_bounds__(kThreads) void point_tail_fwd_kernel(
+    const float* __restrict__ prev, const float* __restrict__ agg, int64_t N, const float* __restrict__ Wp,
+    const float* __restrict__ bp, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
+    const float* __restrict__ Wm, const float* __restrict__ bm, float* __restrict__ out) {
+  __shared__ float WpT[FA * L80];  // WpT[j][o] = Wp[o][j]
+  __shared__ float WmT[FP * L80];  // WmT[k][o] = Wm[o][k]
+  __shared__ float tiles[kWaves][TR * L34 + TR * L66];
+  for (int q = threadIdx.x; q < FP * FA; q += kThreads) WpT[(q % FA) * L80 + q / FA] = Wp[q];
+  for (int q = threadIdx.x; q < FP * FP; q += kThreads) WmT[(q % FP) * L80 + q / FP] = Wm[q];
+  __syncthreads();
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
+  const int c = lane & 15, g = lane >> 4;
+  float* Ag = tiles[wave];
+  float* Ph = Ag + TR * L34;
+  float bpv[4], bmv[4], gv[4], bv[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    bpv[nt] = bp[nt * 16 + c];
+    bmv[nt] = bm[nt * 16 + c];
+    gv[nt] = gam[nt * 16 + c];
+    bv[nt] = bet[nt * 16 + c];
+  }
+  const int64_t ntiles = (N + TR - 1) / TR;
+  const int64_t gw = int64_t(blockIdx.x) * kWaves + wave, nw = int64_t(gridDim.x) * kWaves;
+  for (int64_t t = gw; t < ntiles; t += nw) {
+    const int64_t row0 = t * TR;
+    const int nrows = int(N - row0 < TR ? N - row0 : TR);
+    load_tile<FA, L34>(agg, FA, row0, nrows, Ag, lane);
+    float pv[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = 4 * g + r;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) pv[nt][r] = PREV ? prev[(row0 + (e < nrows ? e : 0)) * FP + nt * 16 + c] : 0.f;
+    }
+    wave_sync();
+    f32x4 xa[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < FA / 4; ++s) {
+      const float a = Ag[c * L34 + 4 * s + g];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) xa[nt] = mfma16(a, WpT[(4 * s + g) * L80 + nt * 16 + c], xa[nt]);
+    }
+    float xv[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float s1 = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        xv[nt][r] = xa[nt][r] + bpv[nt] + pv[nt][r];
+        s1 += xv[nt][r];
+      }
+      const float mean = sum16(s1) * (1.f / FP);
+      float q = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) q = fmaf(xv[nt][r] - mean, xv[nt][r] - mean, q);
+      const float rstd = rsqrtf(sum16(q) * (1.f / FP) + eps);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        Ph[(4 * g + r) * L66 + nt * 16 + c] = fmaxf(fmaf((xv[nt][r] - mean) * rstd, gv[nt], bv[nt]), 0.f);
+    }
+    wave_sync();
+    f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < FP / 4; ++s) {
+      const float a = Ph[c * L66 + 4 * s + g];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma16(a, WmT[(4 * s + g) * L80 + nt * 16 + c], acc[nt]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = 4 * g + r;
+      if (e < nrows) {
+        float* o = out + (row0 + e) * FP;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) o[nt * 16 + c] = xv[nt][r] + acc[nt][r] + bmv[nt];
+      }
+    }
+    wave_sync();
+  }
+}
+
+// dx = dout + LN_bwd(mask * (dout W_m)) (== d prev), dagg = dx W_p; partial row per workgroup
+// [dWm 64x64 | dWp 64x32 | dbm 64 | dbp 64 | dgam 64 | dbet 64]
+template <bool PREV>
+__global__ __launch_bounds__(kThreads8) void point_tail_bwd_kernel(
+    const float* __restrict__ dout, const float* __restrict__ prev, const float* __restrict__ agg, int64_t N,
+    const float* __restrict__ Wp, const float* __restrict__ bp, const float* __restrict__ gam,
+    const float* __restrict__ bet, float eps, const float* __restrict__ Wm, float* __restrict__ dx,
+    float* __restrict__ dagg, float* __restrict__ part) {
+  constexpr int PW = 3 * TR * L66 + TR;  // per wave: D (dout), XH (LN-normalised x), DX (aliases the agg tile), rstd
+  constexpr int NRED = 64 + 32 + 16;
+  static_assert(NRED * kW <= kWaves8 * PW, "reduction scratch");
+  __shared__ float WpT[FA * L80];      // WpT[j][o] = Wp[o][j]   (x recompute)
+  __shared__ float WmL[FP * L80];      // WmL[o][i] = Wm[o][i]   (dout W_m)
+  __shared__ float WpL[FP * L48];      // WpL[o][j] = Wp[o][j]   (dx W_p)
+  __shared__ float tiles[kWaves8 * PW];
+  for (int q = threadIdx.x; q < FP * FA; q += kThreads8) {
+    WpT[(q % FA) * L80 + q / FA] = Wp[q];
+    WpL[(q / FA) * L48 + q % FA] = Wp[q];
+  }
+  for (int q = threadIdx.x; q < FP * FP; q += kThreads8) WmL[(q / FP) * L80 + q % FP] = Wm[q];
+  __syncthreads();
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
+  const int c = lane & 15, g = lane >> 4;
+  float* D = tiles + wave * PW;
+  float* XH = D + TR * L66;
+  float* DX = XH + TR * L66;
+  float* RSt = DX + TR * L66;
+  float* Ag = DX;  // agg tile, dead before DX is written
+  float bpv[4], gv[4], bv[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    bpv[nt] = bp[nt * 16 + c];
+    gv[nt] = gam[nt * 16 + c];
+    bv[nt] = bet[nt * 16 + c];
+  }
+  f32x4 dWm[4][4], dWp[4][2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) dWm[mt][nt] = zero4();
+    dWp[mt][0] = dWp[mt][1] = zero4();
+  }
+  float dbm[4] = {0.f, 0.f, 0.f, 0.f}, dbp[4] = {0.f, 0.f, 0.f, 0.f};
+  float dg[4] = {0.f, 0.f, 0.f, 0.f}, dbt[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t ntiles = (N + TR - 1) / TR;
+  const int64_t gw = int64_t(blockIdx.x) * kWaves8 + wave, nw = int64_t(gridDim.x) * kWaves8;
+  for (int64_t t = gw; t < ntiles; t += nw) {
+    const int64_t row0 = t * TR;
+    const int nrows = int(N - row0 < TR ? N - row0 : TR);
+    load_tile<FA, L34>(agg, FA, row0, nrows, Ag, lane);
+    load_tile<FP, L66>(dout, FP, row0, nrows, D, lane);
+    float pv[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = 4 * g + r;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) pv[nt][r] = PREV ? prev[(row0 + (e < nrows ? e : 0)) * FP + nt * 16 + c] : 0.f;
+    }
+    wave_sync();
+    // recompute x (C layout); x_hat and rstd to LDS
+    f32x4 xa[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < FA / 4; ++s) {
+      const float a = Ag[c * L34 + 4 * s + g];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) xa[nt] = mfma16(a, WpT[(4 * s + g) * L80 + nt * 16 + c], xa[nt]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = 4 * g + r;
+      float xr[4], s1 = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        xr[nt] = xa[nt][r] + bpv[nt] + pv[nt][r];
+        s1 += xr[nt];
+      }
+      const float mean = sum16(s1) * (1.f / FP);
+      float q = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) q = fmaf(xr[nt] - mean, xr[nt] - mean, q);
+      const float rstd = rsqrtf(sum16(q) * (1.f / FP) + eps);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) XH[e * L66 + nt * 16 + c] = (xr[nt] - mean) * rstd;
+      if (c == 0) RSt[e] = rstd;
+    }
+    wave_sync();
+    // d relu-out = dout W_m
+    f32x4 dph[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < FP / 4; ++s) {
+      const float a = D[c * L66 + 4 * s + g];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) dph[nt] = mfma16(a, WmL[(4 * s + g) * L80 + nt * 16 + c], dph[nt]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = 4 * g + r;
+      float xr[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) xr[nt] = XH[e * L66 + nt * 16 + c];
+      const float dh[4] = {dph[0][r], dph[1][r], dph[2][r], dph[3][r]};
+      float o[4];
+      ln_relu_bwd_row(xr, dh, gv, bv, RSt[e], dg, dbt, o);  // rows past nrows: dout rows are 0
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) o[nt] += D[e * L66 + nt * 16 + c];
+      if (e < nrows) {
+        float* d = dx + (row0 + e) * FP;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) d[nt * 16 + c] = o[nt];
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) DX[e * L66 + nt * 16 + c] = e < nrows ? o[nt] : 0.f;
+    }
+    wave_sync();
+    // dagg = dx W_p
+    f32x4 da[2] = {zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < FP / 4; ++s) {
+      const float a = DX[c * L66 + 4 * s + g];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) da[nt] = mfma16(a, WpL[(4 * s + g) * L48 + nt * 16 + c], da[nt]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = 4 * g + r;
+      if (e < nrows) {
+        float* d = dagg + (row0 + e) * FA;
+        d[c] = da[0][r];
+        d[16 + c] = da[1][r];
+      }
+    }
+    // dW_m += dout^T relu(LN x), dW_p += dx^T agg, biases (rows past nrows: dout, dx are 0)
+#pragma unroll
+    for (int s = 0; s < TR / 4; ++s) {
+      const int row = 4 * s + g;
+      float ph[4], ag[2];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) ph[nt] = fmaxf(fmaf(XH[row * L66 + nt * 16 + c], gv[nt], bv[nt]), 0.f);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) ag[nt] = ld_a(agg, FA, row0, nrows, row, nt * 16 + c);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const float a = D[row * L66 + mt * 16 + c];
+        dbm[mt] += a;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) dWm[mt][nt] = mfma16(a, ph[nt], dWm[mt][nt]);
+        const float a2 = DX[row * L66 + mt * 16 + c];
+        dbp[mt] += a2;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) dWp[mt][nt] = mfma16(a2, ag[nt], dWp[mt][nt]);
+      }
+    }
+    wave_sync();
+  }
+  float v[NRED];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) v[(mt * 4 + nt) * 4 + r] = dWm[mt][nt][r];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) v[64 + (mt * 2 + nt) * 4 + r] = dWp[mt][nt][r];
+    }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[96 + k] = dbm[k];
+    v[100 + k] = dbp[k];
+    v[104 + k] = dg[k];
+    v[108 + k] = dbt[k];
+  }
+  wg_reduce_ordered<NRED, kWaves8>(v, tiles, wave, lane);
+  if (wave == 0) {
+    float* out = part + int64_t(blockIdx.x) * TAIL_PART;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = mt * 16 + 4 * g + r;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) out[o * FP + nt * 16 + c] = v[(mt * 4 + nt) * 4 + r];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) out[FP * FP + o * FA + nt * 16 + c] = v[64 + (mt * 2 + nt) * 4 + r];
+      }
+    float tt[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) tt[k] = sum_groups(v[96 + k]);
+    if (g == 0) {
+      float* o = out + FP * FP + FP * FA;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[q * FP + k * 16 + c] = tt[q * 4 + k];
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- hub
+template <bool HC>
+__global__ __launch_bounds__(kThreads) void point_hub_fwd_kernel(
+    const float* __restrict__ X, int64_t N, float eps, const float* __restrict__ gA, const float* __restrict__ bA,
+    const float* __restrict__ WA, float* __restrict__ SA, const float* __restrict__ WB,
+    const float* __restrict__ bB, float* __restrict__ XL, const float* __restrict__ gC,
+    const float* __restrict__ bC, const float* __restrict__ WC, const float* __restrict__ bWC,
+    const float* __restrict__ WD, const float* __restrict__ bD, float* __restrict__ XR) {
+  __shared__ float WAt[FP * L48];               // WAt[k][j] = W_A[j][k]
+  __shared__ float WBt[FP * L80];               // WBt[k][o] = W_B[o][k]
+  __shared__ float WCt[HC ? FP * L48 : 1];      // WCt[k][j] = W_C[j][k]
+  __shared__ float WDt[HC ? FA * L48 : 1];      // WDt[k][j] = W_D[j][k]
+  __shared__ float GB[4 * FP];                  // gamma_A beta_A gamma_C beta_C
+  __shared__ float tiles[kWaves][TR * L66 + TR * L34 + 2 * TR];
+  for (int q = threadIdx.x; q < FA * FP; q += kThreads) WAt[(q % FP) * L48 + q / FP] = WA[q];
+  for (int q = threadIdx.x; q < FP * FP; q += kThreads) WBt[(q % FP) * L80 + q / FP] = WB[q];
+  if (HC) {
+    for (int q = threadIdx.x; q < FA * FP; q += kThreads) WCt[(q % FP) * L48 + q / FP] = WC[q];
+    for (int q = threadIdx.x; q < FA * FA; q += kThreads) WDt[(q % FA) * L48 + q / FA] = WD[q];
+  }
+  if (threadIdx.x < FP) {
+    GB[threadIdx.x] = gA[threadIdx.x];
+    GB[FP + threadIdx.x] = bA[threadIdx.x];
+    GB[2 * FP + threadIdx.x] = HC ? gC[threadIdx.x] : 0.f;
+    GB[3 * FP + threadIdx.x] = HC ? bC[threadIdx.x] : 0.f;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
+  const int c = lane & 15, g = lane >> 4;
+  float* Raw = tiles[wave];
+  float* Tt = Raw + TR * L66;
+  float* MS = Tt + TR * L34;
+  float* RS = MS + TR;
+  float bBv[4], bCv[2], bDv[2];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) bBv[nt] = bB[nt * 16 + c];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    bCv[nt] = HC ? bWC[nt * 16 + c] : 0.f;
+    bDv[nt] = HC ? bD[nt * 16 + c] : 0.f;
+  }
+  const int64_t ntiles = (N + TR - 1) / TR;
+  const int64_t gw = int64_t(blockIdx.x) * kWaves + wave, nw = int64_t(gridDim.x) * kWaves;
+  for (int64_t t = gw; t < ntiles; t += nw) {
+    const int64_t row0 = t * TR;
+    const int nrows = int(N - row0 < TR ? N - row0 : TR);
+    load_rows_stats(X, row0, nrows, eps, Raw, MS, RS, lane);
+    wave_sync();
+    const float mi = MS[c], ri = RS[c];
+    f32x4 accB[4] = {zero4(), zero4(), zero4(), zero4()}, accA[2] = {zero4(), zero4()}, accC[2] = {zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < FP / 4; ++s) {
+      const int k = 4 * s + g;
+      const float a = Raw[c * L66 + k];
+      const float xh = (a - mi) * ri;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) accB[nt] = mfma16(a, WBt[k * L80 + nt * 16 + c], accB[nt]);
+      const float pa = fmaxf(fmaf(xh, GB[k], GB[FP + k]), 0.f);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) accA[nt] = mfma16(pa, WAt[k * L48 + nt * 16 + c], accA[nt]);
+      if (HC) {
+        const float pc = fmaxf(fmaf(xh, GB[2 * FP + k], GB[3 * FP + k]), 0.f);
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) accC[nt] = mfma16(pc, WCt[k * L48 + nt * 16 + c], accC[nt]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = 4 * g + r;
+      if (e < nrows) {
+        float* xl = XL + (row0 + e) * FP;
+        float* sa = SA + (row0 + e) * FA;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) xl[nt * 16 + c] = accB[nt][r] + bBv[nt];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) sa[nt * 16 + c] = accA[nt][r];
+      }
+      if (HC) {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) Tt[e * L34 + nt * 16 + c] = accC[nt][r] + bCv[nt];
+      }
+    }
+    if (HC) {
+      wave_sync();
+      f32x4 accD[2] = {zero4(), zero4()};
+#pragma unroll
+      for (int s = 0; s < FA / 4; ++s) {
+        const float a = Tt[c * L34 + 4 * s + g];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) accD[nt] = mfma16(a, WDt[(4 * s + g) * L48 + nt * 16 + c], accD[nt]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int e = 4 * g + r;
+        if (e < nrows) {
+          float* xr = XR + (row0 + e) * FA;
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) xr[nt * 16 + c] = accD[nt][r] + bDv[nt];
+        }
+      }
+    }
+    wave_sync();
+  }
+}
+
+// The hub backward runs as two passes, each adding its terms to the incoming gradient of p:
+//   C pass:  dq = dRes + LN_C_bwd(mask (dt W_C)),  dt = dXR W_D       partials HC_* layout
+//   AB pass: dp = dq + dXL W_B + LN_A_bwd(mask (dSA W_A))               partials HA_* layout
+// (one pass would hold 144 weight-gradient accumulators and spill at 2 waves per SIMD; the
+// split costs one extra write + read of dq).
+constexpr int HA_WA = 0, HA_WB = HA_WA + FA * FP, HA_BB = HA_WB + FP * FP, HA_GA = HA_BB + FP, HA_BA = HA_GA + FP,
+              HA_PART = HA_BA + FP;
+constexpr int HC_WC = 0, HC_WD = HC_WC + FA * FP, HC_BC = HC_WD + FA * FA, HC_BD = HC_BC + FA, HC_GC = HC_BD + FA,
+              HC_BCL = HC_GC + FP, HC_PART = HC_BCL + FP;
+
+template <bool HR>
+__global__ __launch_bounds__(kThreads8) void point_hub_bwd_ab_kernel(
+    const float* __restrict__ X, int64_t N, float eps, const float* __restrict__ gA, const float* __restrict__ bA,
+    const float* __restrict__ WA, const float* __restrict__ WB, const float* __restrict__ dSA,
+    const float* __restrict__ dXL, const float* __restrict__ dRes, float* __restrict__ dX,
+    float* __restrict__ part) {
+  constexpr int PW = TR * L66 + 2 * TR;  // Raw, MS, RS
+  constexpr int NRED = 96 + 12;
+  static_assert(NRED * kW <= kWaves8 * PW, "reduction scratch");
+  __shared__ float WAl[FA * L80];        // W_A [32 x 64] row-major
+  __shared__ float WBl[FP * L80];        // W_B [64 x 64]
+  __shared__ float GB[2 * FP];           // gamma_A beta_A
+  __shared__ float tiles[kWaves8 * PW];
+  for (int q = threadIdx.x; q < FA * FP; q += kThreads8) WAl[(q / FP) * L80 + q % FP] = WA[q];
+  for (int q = threadIdx.x; q < FP * FP; q += kThreads8) WBl[(q / FP) * L80 + q % FP] = WB[q];
+  if (threadIdx.x < FP) {
+    GB[threadIdx.x] = gA[threadIdx.x];
+    GB[FP + threadIdx.x] = bA[threadIdx.x];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
+  const int c = lane & 15, g = lane >> 4;
+  float* Raw = tiles + wave * PW;
+  float* MS = Raw + TR * L66;
+  float* RS = MS + TR;
+  f32x4 dWA[2][4], dWB[4][4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    dWA[0][nt] = dWA[1][nt] = zero4();
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) dWB[mt][nt] = zero4();
+  }
+  float dbB[4] = {0.f, 0.f, 0.f, 0.f}, dgA[4] = {0.f, 0.f, 0.f, 0.f}, dbA[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t ntiles = (N + TR - 1) / TR;
+  const int64_t gw = int64_t(blockIdx.x) * kWaves8 + wave, nw = int64_t(gridDim.x) * kWaves8;
+  for (int64_t t = gw; t < ntiles; t += nw) {
+    const int64_t row0 = t * TR;
+    const int nrows = int(N - row0 < TR ? N - row0 : TR);
+    load_rows_stats(X, row0, nrows, eps, Raw, MS, RS, lane);
+    wave_sync();
+    // weight gradients over the tile's rows (row = 4s + g; rows past nrows: dSA, dXL read as 0)
+#pragma unroll
+    for (int s = 0; s < TR / 4; ++s) {
+      const int row = 4 * s + g;
+      const float mr = MS[row], rr = RS[row];
+      float xr[4], pa[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        xr[nt] = Raw[row * L66 + nt * 16 + c];
+        pa[nt] = fmaxf(fmaf((xr[nt] - mr) * rr, GB[nt * 16 + c], GB[FP + nt * 16 + c]), 0.f);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const float a = ld_a(dSA, FA, row0, nrows, row, mt * 16 + c);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) dWA[mt][nt] = mfma16(a, pa[nt], dWA[mt][nt]);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const float a = ld_a(dXL, FP, row0, nrows, row, mt * 16 + c);
+        dbB[mt] += a;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) dWB[mt][nt] = mfma16(a, xr[nt], dWB[mt][nt]);
+      }
+    }
+    // data gradient (C layout: row 4g+r, column nt*16+c)
+    f32x4 dxb[4] = {zero4(), zero4(), zero4(), zero4()}, dp[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < FP / 4; ++s) {
+      const float a = ld_a(dXL, FP, row0, nrows, c, 4 * s + g);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) dxb[nt] = mfma16(a, WBl[(4 * s + g) * L80 + nt * 16 + c], dxb[nt]);
+    }
+#pragma unroll
+    for (int s = 0; s < FA / 4; ++s) {
+      const float a = ld_a(dSA, FA, row0, nrows, c, 4 * s + g);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) dp[nt] = mfma16(a, WAl[(4 * s + g) * L80 + nt * 16 + c], dp[nt]);
+    }
+    float gc[4], bc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      gc[nt] = GB[nt * 16 + c];
+      bc[nt] = GB[FP + nt * 16 + c];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = 4 * g + r;
+      const float me = MS[e], re = RS[e];
+      float xh[4], t1[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) xh[nt] = (Raw[e * L66 + nt * 16 + c] - me) * re;
+      const float dh[4] = {dp[0][r], dp[1][r], dp[2][r], dp[3][r]};
+      ln_relu_bwd_row(xh, dh, gc, bc, re, dgA, dbA, t1);
+      if (e < nrows) {
+        float* d = dX + (row0 + e) * FP;
+        const float* dr = dRes + (row0 + e) * FP;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) d[nt * 16 + c] = dxb[nt][r] + t1[nt] + (HR ? dr[nt * 16 + c] : 0.f);
+      }
+    }
+    wave_sync();
+  }
+  float v[NRED];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) v[(mt * 4 + nt) * 4 + r] = dWA[mt][nt][r];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) v[32 + (mt * 4 + nt) * 4 + r] = dWB[mt][nt][r];
+    }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[96 + k] = dbB[k];
+    v[100 + k] = dgA[k];
+    v[104 + k] = dbA[k];
+  }
+  wg_reduce_ordered<NRED, kWaves8>(v, tiles, wave, lane);
+  if (wave == 0) {
+    float* out = part + int64_t(blockIdx.x) * HA_PART;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) out[HA_WA + (mt * 16 + 4 * g + r) * FP + nt * 16 + c] = v[(mt * 4 + nt) * 4 + r];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          out[HA_WB + (mt * 16 + 4 * g + r) * FP + nt * 16 + c] = v[32 + (mt * 4 + nt) * 4 + r];
+      }
+    float tt[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) tt[k] = sum_groups(v[96 + k]);
+    if (g == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        out[HA_BB + k * 16 + c] = tt[k];
+        out[HA_GA + k * 16 + c] = tt[4 + k];
+        out[HA_BA + k * 16 + c] = tt[8 + k];
+      }
+    }
+  }
+}
+
+template <bool HR>
+__global__ __launch_bounds__(kThreads8) void point_hub_bwd_c_kernel(
+    const float* __restrict__ X, int64_t N, float eps, const float* __restrict__ gC, const float* __restrict__ bC,
+    const float* __restrict__ WC, const float* __restrict__ bWC, const float* __restrict__ WD,
+    const float* __restrict__ dXR, const float* __restrict__ dRes, float* __restrict__ dX,
+    float* __restrict__ part) {
+  constexpr int PW = TR * L66 + 2 * TR * L34 + 2 * TR;  // Raw, Dt (dt), Tt (t), MS, RS
+  constexpr int NRED = 48 + 12;
+  static_assert(NRED * kW <= kWaves8 * PW, "reduction scratch");
+  __shared__ float WCl[FA * L80];        // W_C [32 x 64]
+  __shared__ float WCt[FP * L48];        // W_C^T
+  __shared__ float WDl[FA * L48];        // W_D [32 x 32]
+  __shared__ float GB[2 * FP];           // gamma_C beta_C
+  __shared__ float tiles[kWaves8 * PW];
+  for (int q = threadIdx.x; q < FA * FP; q += kThreads8) {
+    WCl[(q / FP) * L80 + q % FP] = WC[q];
+    WCt[(q % FP) * L48 + q / FP] = WC[q];
+  }
+  for (int q = threadIdx.x; q < FA * FA; q += kThreads8) WDl[(q / FA) * L48 + q % FA] = WD[q];
+  if (threadIdx.x < FP) {
+    GB[threadIdx.x] = gC[threadIdx.x];
+    GB[FP + threadIdx.x] = bC[threadIdx.x];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
+  const int c = lane & 15, g = lane >> 4;
+  float* Raw = tiles + wave * PW;
+  float* Dt = Raw + TR * L66;
+  float* Tt = Dt + TR * L34;
+  float* MS = Tt + TR * L34;
+  float* RS = MS + TR;
+  const float bWCv[2] = {bWC[c], bWC[16 + c]};
+  f32x4 dWC[2][4], dWD[2][2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) dWC[mt][nt] = zero4();
+    dWD[mt][0] = dWD[mt][1] = zero4();
+  }
+  float dbC[2] = {0.f, 0.f}, dbD[2] = {0.f, 0.f}, dgC[4] = {0.f, 0.f, 0.f, 0.f}, dbCl[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t ntiles = (N + TR - 1) / TR;
+  const int64_t gw = int64_t(blockIdx.x) * kWaves8 + wave, nw = int64_t(gridDim.x) * kWaves8;
+  for (int64_t t = gw; t < ntiles; t += nw) {
+    const int64_t row0 = t * TR;
+    const int nrows = int(N - row0 < TR ? N - row0 : TR);
+    load_rows_stats(X, row0, nrows, eps, Raw, MS, RS, lane);
+    wave_sync();
+    const float mi = MS[c], ri = RS[c];
+    // t = W_C relu(LN_C p) + b_C (recomputed), dt = dXR W_D
+    f32x4 ta[2] = {zero4(), zero4()}, da[2] = {zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < FP / 4; ++s) {
+      const int k = 4 * s + g;
+      const float pc = fmaxf(fmaf((Raw[c * L66 + k] - mi) * ri, GB[k], GB[FP + k]), 0.f);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) ta[nt] = mfma16(pc, WCt[k * L48 + nt * 16 + c], ta[nt]);
+    }
+#pragma unroll
+    for (int s = 0; s < FA / 4; ++s) {
+      const float a = ld_a(dXR, FA, row0, nrows, c, 4 * s + g);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) da[nt] = mfma16(a, WDl[(4 * s + g) * L48 + nt * 16 + c], da[nt]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        Tt[(4 * g + r) * L34 + nt * 16 + c] = ta[nt][r] + bWCv[nt];
+        Dt[(4 * g + r) * L34 + nt * 16 + c] = da[nt][r];
+      }
+    wave_sync();
+    // dW_C += dt^T relu(LN_C p), dW_D += dXR^T t (row = 4s + g; rows past nrows: dXR, dt are 0)
+#pragma unroll
+    for (int s = 0; s < TR / 4; ++s) {
+      const int row = 4 * s + g;
+      const float mr = MS[row], rr = RS[row];
+      float pc[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        pc[nt] = fmaxf(fmaf((Raw[row * L66 + nt * 16 + c] - mr) * rr, GB[nt * 16 + c], GB[FP + nt * 16 + c]), 0.f);
+      const float tt[2] = {Tt[row * L34 + c], Tt[row * L34 + 16 + c]};
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const float a = Dt[row * L34 + mt * 16 + c];
+        dbC[mt] += a;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) dWC[mt][nt] = mfma16(a, pc[nt], dWC[mt][nt]);
+        const float a2 = ld_a(dXR, FA, row0, nrows, row, mt * 16 + c);
+        dbD[mt] += a2;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) dWD[mt][nt] = mfma16(a2, tt[nt], dWD[mt][nt]);
+      }
+    }
+    // data gradient: dq = dRes + LN_C_bwd(mask (dt W_C))
+    f32x4 dp[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < FA / 4; ++s) {
+      const float a = Dt[c * L34 + 4 * s + g];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) dp[nt] = mfma16(a, WCl[(4 * s + g) * L80 + nt * 16 + c], dp[nt]);
+    }
+    float gc[4], bc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      gc[nt] = GB[nt * 16 + c];
+      bc[nt] = GB[FP + nt * 16 + c];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = 4 * g + r;
+      const float me = MS[e], re = RS[e];
+      float xh[4], t1[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) xh[nt] = (Raw[e * L66 + nt * 16 + c] - me) * re;
+      const float dh[4] = {dp[0][r], dp[1][r], dp[2][r], dp[3][r]};
+      ln_relu_bwd_row(xh, dh, gc, bc, re, dgC, dbCl, t1);
+      if (e < nrows) {
+        float* d = dX + (row0 + e) * FP;
+        const float* dr = dRes + (row0 + e) * FP;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) d[nt * 16 + c] = t1[nt] + (HR ? dr[nt * 16 + c] : 0.f);
+      }
+    }
+    wave_sync();
+  }
+  float v[NRED];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) v[(mt * 4 + nt) * 4 + r] = dWC[mt][nt][r];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) v[32 + (mt * 2 + nt) * 4 + r] = dWD[mt][nt][r];
+    }
+  v[48] = dbC[0];
+  v[49] = dbC[1];
+  v[50] = dbD[0];
+  v[51] = dbD[1];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[52 + k] = dgC[k];
+    v[56 + k] = dbCl[k];
+  }
+  wg_reduce_ordered<NRED, kWaves8>(v, tiles, wave, lane);
+  if (wave == 0) {
+    float* out = part + int64_t(blockIdx.x) * HC_PART;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int o = mt * 16 + 4 * g + r;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) out[HC_WC + o * FP + nt * 16 + c] = v[(mt * 4 + nt) * 4 + r];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) out[HC_WD + o * FA + nt * 16 + c] = v[32 + (mt * 2 + nt) * 4 + r];
+      }
+    float tt[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) tt[k] = sum_groups(v[48 + k]);
+    if (g == 0) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        out[HC_BC + k * 16 + c] = tt[k];
+        out[HC_BD + k * 16 + c] = tt[2 + k];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        out[HC_GC + k * 16 + c] = tt[4 + k];
+        out[HC_BCL + k * 16 + c] = tt[8 + k];
+      }
+    }
+  }
+}
+
+int64_t tiles_of(int64_t N) { return (N + TR - 1) / TR; }
+
+template <class K>
+int grid4(K kernel, int64_t N) {
+  return resident_grid(reinterpret_cast<const void*>(kernel), kThreads, 0, tiles_of(N), kWaves);
+}
+template <class K>
+int grid8(K kernel, int64_t N) {
+  return resident_grid(reinterpret_cast<const void*>(kernel), kThreads8, 0, tiles_of(N), kWaves8);
+}
+
+int tail_bwd_grid(int64_t N, bool has_prev) {
+  return has_prev ? grid8(&point_tail_bwd_kernel<true>, N) : grid8(&point_tail_bwd_kernel<false>, N);
+}
+int hub_ab_grid(int64_t N, bool hr) {
+  return hr ? grid8(&point_hub_bwd_ab_kernel<true>, N) : grid8(&point_hub_bwd_ab_kernel<false>, N);
+}
+int hub_c_grid(int64_t N, bool hr) {
+  return hr ? grid8(&point_hub_bwd_c_kernel<true>, N) : grid8(&point_hub_bwd_c_kernel<false>, N);
+}
+
+}  // namespace
+}  // namespace gasfm
+
+using namespace gasfm;
+
+extern "C" int32_t gasfm_point_tail_part_shape(int64_t N, int32_t has_prev, int32_t* cols) {
+  if (cols) *cols = TAIL_PART;
+  return N > 0 ? tail_bwd_grid(N, has_prev != 0) : 0;
+}
+
+extern "C" int32_t gasfm_point_hub_part_shape(int64_t N, int32_t which, int32_t has_res, int32_t* cols) {
+  if (cols) *cols = which ? HC_PART : HA_PART;
+  if (N <= 0) return 0;
+  return which ? hub_c_grid(N, has_res != 0) : hub_ab_grid(N, has_res != 0);
+}
+extern "C" int gasfm_point_tail_fwd(const float* prev, const float* agg, int64_t N, const float* Wp, const float* bp,
+                                    const float* ln_w, const float* ln_b, float eps, const float* Wm,
+                                    const float* bm, float* out, void* stream) {
+  GASFM_REQUIRE(N >= 0, "gasfm_point_tail_fwd: N < 0");
+  if (N == 0) return GASFM_OK;
+  GASFM_REQUIRE(agg && Wp && bp && ln_w && ln_b && Wm && bm && out, "gasfm_point_tail_fwd: null pointer");
+  GASFM_REQUIRE(aligned16(agg) && (!prev || aligned16(prev)), "gasfm_point_tail_fwd: alignment");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (prev)
+    hipLaunchKernelGGL(point_tail_fwd_kernel<true>, dim3(grid4(&point_tail_fwd_kernel<true>, N)), dim3(kThreads), 0,
+                       st, prev, agg, N, Wp, bp, ln_w, ln_b, eps, Wm, bm, out);
+  else
+    hipLaunchKernelGGL(point_tail_fwd_kernel<false>, dim3(grid4(&point_tail_fwd_kernel<false>, N)), dim3(kThreads),
+                       0, st, prev, agg, N, Wp, bp, ln_w, ln_b, eps, Wm, bm, out);
+  return launch_status("gasfm_point_tail_fwd");
+}
+
+extern "C" int gasfm_point_tail_bwd(const float* dout, const float* prev, const float* agg, int64_t N,
+                                    const float* Wp, const float* bp, const float* ln_w, const float* ln_b,
+                                    float eps, const float* Wm, float* dx, float* dagg, float* part, void* stream) {
+  GASFM_REQUIRE(N >= 0, "gasfm_point_tail_bwd: N < 0");
+  if (N == 0) return GASFM_OK;
+  GASFM_REQUIRE(dout && agg && Wp && bp && ln_w && ln_b && Wm && dx && dagg && part,
+                "gasfm_point_tail_bwd: null pointer");
+  GASFM_REQUIRE(aligned16(dout) && aligned16(agg), "gasfm_point_tail_bwd: alignment");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int gsz = tail_bwd_grid(N, prev != nullptr);
+  if (prev)
+    hipLaunchKernelGGL(point_tail_bwd_kernel<true>, dim3(gsz), dim3(kThreads8), 0, st, dout, prev, agg, N, Wp, bp,
+                       ln_w, ln_b, eps, Wm, dx, dagg, part);
+  else
+    hipLaunchKernelGGL(point_tail_bwd_kernel<false>, dim3(gsz), dim3(kThreads8), 0, st, dout, prev, agg, N, Wp, bp,
+                       ln_w, ln_b, eps, Wm, dx, dagg, part);
+  return launch_status("gasfm_point_tail_bwd");
+}
+
+extern "C" int gasfm_point_hub_fwd(const float* X, int64_t N, float eps, const float* gA, const float* bA,
+                                   const float* WA, float* SA, const float* WB, const float* bB, float* XL,
+                                   const float* gC, const float* bC, const float* WC, const float* bWC,
+                                   const float* WD, const float* bD, float* XR, void* stream) {
+  GASFM_REQUIRE(N >= 0, "gasfm_point_hub_fwd: N < 0");
+  const bool hc = gC != nullptr;
+  if (N == 0) return GASFM_OK;
+  GASFM_REQUIRE(X && gA && bA && WA && SA && WB && bB && XL, "gasfm_point_hub_fwd: null pointer");
+  GASFM_REQUIRE(!hc || (bC && WC && bWC && WD && bD && XR), "gasfm_point_hub_fwd: null pointer (C part)");
+  GASFM_REQUIRE(aligned16(X), "gasfm_point_hub_fwd: alignment");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hc)
+    hipLaunchKernelGGL(point_hub_fwd_kernel<true>, dim3(grid4(&point_hub_fwd_kernel<true>, N)), dim3(kThreads), 0,
+                       st, X, N, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR);
+  else
+    hipLaunchKernelGGL(point_hub_fwd_kernel<false>, dim3(grid4(&point_hub_fwd_kernel<false>, N)), dim3(kThreads), 0,
+                       st, X, N, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR);
+  return launch_status("gasfm_point_hub_fwd");
+}
+
+extern "C" int gasfm_point_hub_bwd_c(const float* X, int64_t N, float eps, const float* gC, const float* bC,
+                                     const float* WC, const float* bWC, const float* WD, const float* dXR,
+                                     const float* dRes, float* dX, float* part, void* stream) {
+  GASFM_REQUIRE(N >= 0, "gasfm_point_hub_bwd_c: N < 0");
+  if (N == 0) return GASFM_OK;
+  GASFM_REQUIRE(X && gC && bC && WC && bWC && WD && dXR && dX && part, "gasfm_point_hub_bwd_c: null pointer");
+  GASFM_REQUIRE(aligned16(X), "gasfm_point_hub_bwd_c: alignment");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const bool hr = dRes != nullptr;
+  if (hr)
+    hipLaunchKernelGGL(point_hub_bwd_c_kernel<true>, dim3(hub_c_grid(N, true)), dim3(kThreads8), 0, st, X, N, eps,
+                       gC, bC, WC, bWC, WD, dXR, dRes, dX, part);
+  else
+    hipLaunchKernelGGL(point_hub_bwd_c_kernel<false>, dim3(hub_c_grid(N, false)), dim3(kThreads8), 0, st, X, N,
+                       eps, gC, bC, WC, bWC, WD, dXR, dRes, dX, part);
+  return launch_status("gasfm_point_hub_bwd_c");
+}
+
+extern "C" int gasfm_point_hub_bwd_ab(const float* X, int64_t N, float eps, const float* gA, const float* bA,
+                                      const float* WA, const float* WB, const float* dSA, const float* dXL,
+                                      const float* dRes, float* dX, float* part, void* stream) {
+  GASFM_REQUIRE(N >= 0, "gasfm_point_hub_bwd_ab: N < 0");
+  if (N == 0) return GASFM_OK;
+  GASFM_REQUIRE(X && gA && bA && WA && WB && dSA && dXL && dX && part, "gasfm_point_hub_bwd_ab: null pointer");
+  GASFM_REQUIRE(aligned16(X), "gasfm_point_hub_bwd_ab: alignment");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const bool hr = dRes != nullptr;
+  if (hr)
+    hipLaunchKernelGGL(point_hub_bwd_ab_kernel<true>, dim3(hub_ab_grid(N, true)), dim3(kThreads8), 0, st, X, N,
+                       eps, gA, bA, WA, WB, dSA, dXL, dRes, dX, part);
+  else
+    hipLaunchKernelGGL(point_hub_bwd_ab_kernel<false>, dim3(hub_ab_grid(N, false)), dim3(kThreads8), 0, st, X, N,
+                       eps, gA, bA, WA, WB, dSA, dXL, dRes, dX, part);
+  return launch_status("gasfm_point_hub_bwd_ab");
+}

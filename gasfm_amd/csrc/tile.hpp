@@ -93,10 +93,10 @@ __device__ __forceinline__ void wg_reduce(float (&v)[N], float* scratch, int wav
 }
 
 // Same result as wg_reduce with only N*kW floats of scratch: the waves add into one buffer in
-// wave order, one barrier per wave.
-template <int N>
+// wave order, one barrier per wave.  NW = waves per workgroup.
+template <int N, int NW = kWaves>
 __device__ __forceinline__ void wg_reduce_ordered(float (&v)[N], float* scratch, int wave, int lane) {
-  for (int w = 0; w < kWaves; ++w) {
+  for (int w = 0; w < NW; ++w) {
     __syncthreads();
     if (wave == w) {
 #pragma unroll

@@ -81,7 +81,8 @@ class CapturedStep:
             self.fallback_reason = self.fallback_reason or "replay check failed on another rank"
             self._zero()
             return
-        self.graph, self.static_out = g, out
+        # detached: the captured autograd graph is not kept alive between replays
+        self.graph, self.static_out = g, out.detach()
 
     @property
     def captured(self):

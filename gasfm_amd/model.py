@@ -25,8 +25,8 @@ import torch
 import torch.nn.functional as F
 from torch.nn import Identity, LayerNorm, Linear, Module, ModuleList, ReLU, Sequential
 
-from . import dense, edge_ops
-from .attention import AttnPlan
+from . import dense, edge_ops, point_block
+from .attention import AttnPlan, gat_attention
 from .edge_block import Block0EpilogueFn, Block0PrologueFn, DualAttentionFn, EdgeEpilogueFn, EdgePrologueFn
 from .gatv2 import GATv2Conv
 
@@ -128,6 +128,8 @@ class _NodeAggregation(Module):
 
     def tail(self, x, prev):
         """Everything after the GATv2 aggregation: proj, state skip, LN+ReLU, MLP, skip."""
+        if point_block.tail_fusable(self, x, prev):
+            return point_block.tail(self, x, prev)
         if self.n_feat_agg != self.n_feat_out:
             x = dense.linear(x, getattr(self, self._proj_key))
         if prev is not None:
@@ -186,13 +188,18 @@ class ViewAndScenePoint2Global(Module):
             self.norm_pre_mlp = LayerNorm(n_feat_global_out)
         self.mlp = get_linear_layers((2 + n_hidden_layers_global_update) * [n_feat_global_out], norm=False)
 
-    def forward_plan(self, view, pts, plan_v2g, plan_s2g, prev, plan_s2g_partial=None, shard=None):
+    def forward_plan(self, view, pts, plan_v2g, plan_s2g, prev, plan_s2g_partial=None, shard=None, xl_pts=None):
+        """xl_pts: graph_conv_scenepoint2global.lin_l(pts) when already computed (PointHubFn)."""
         assert self.stateful == (prev is not None)
         xv = dense.sequential(self.norm_and_proj_global2view, prev) if prev is not None else None
         xp = dense.sequential(self.norm_and_proj_global2scenepoint, prev) if prev is not None else None
         v2g = self.graph_conv_view2global.attend(view, xv, plan_v2g)
         c = self.graph_conv_scenepoint2global
-        if shard is None:
+        if shard is None and xl_pts is not None:
+            XR = c.lin_r(torch.zeros((1, c.in_channels), device=pts.device)).expand(1, -1) if xp is None \
+                else dense.linear(xp, c.lin_r)
+            s2g = gat_attention(xl_pts, XR, c.att, c._bias(xl_pts), plan_s2g, c.heads, c.negative_slope)
+        elif shard is None:
             s2g = c.attend(pts, xp, plan_s2g)
         else:  # points are sharded, the global target is replicated
             if xp is None:
@@ -201,7 +208,8 @@ class ViewAndScenePoint2Global(Module):
             else:
                 XR = dense.linear(xp, c.lin_r)
             XR = replicated_to_local(XR, shard)
-            s2g = ShardedAttentionFn.apply(dense.linear(pts, c.lin_l), XR, c.att, c.bias, plan_s2g,
+            XLp = xl_pts if xl_pts is not None else dense.linear(pts, c.lin_l)
+            s2g = ShardedAttentionFn.apply(XLp, XR, c.att, c.bias, plan_s2g,
                                            plan_s2g_partial, c.heads, c.negative_slope, shard)
         x = torch.cat([v2g, s2g], dim=1)
         if hasattr(self, "proj_view_and_scenepoint2global"):
@@ -310,21 +318,35 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         a, b = self.proj2scenepoint.graph_conv.lin_l, self.proj2view.graph_conv.lin_l
         return torch.cat([a.weight, b.weight], 0), torch.cat([a.bias, b.bias], 0)
 
-    def forward_fused(self, XL, plans, prev_pt=None, prev_view=None, prev_glob=None, xl_sorted=False):
+    def forward_fused(self, XL, plans, prev_pt=None, prev_view=None, prev_glob=None, xl_sorted=False, carry=None,
+                      pfu=None, nxt=None):
         """Node side of the update given XL = [lin_l_point(P_hat) | lin_l_camera(P_hat)] [E, 64]
-        (point half in point-segment order when xl_sorted)."""
+        (point half in point-segment order when xl_sorted).
+
+        carry: per-forward dict through which PointHubFn hands the next block its point target
+        rows ("XRp") and state skip ("pts_skip"), and this block its "SA" / "XLs2g" terms;
+        pfu / nxt: this block's projection-feature update and the next Proj2ScenePoint (the
+        hub's consumers), None where there is no next consumer."""
         sp, sv = self.proj2scenepoint, self.proj2view
         pp, pc = plans["proj2scenepoint"], plans["proj2view"]
         shard = plans.get("_shard")
-        XRp = sp.target_rows(prev_pt, pp.num_targets)
+        if carry is not None and "XRp" in carry:
+            XRp, prev_pt = carry.pop("XRp"), carry.pop("pts_skip")
+        else:
+            XRp = sp.target_rows(prev_pt, pp.num_targets)
         XRc = replicated_to_local(sv.target_rows(prev_view, pc.num_targets), shard)
         cp, cc = sp.graph_conv, sv.graph_conv
         agg_p, agg_c = DualAttentionFn.apply(XL, XRp, XRc, cp.att, cc.att, cp.bias, cc.bias, pp, pc, cp.heads,
                                              cp.negative_slope, plans.get("_partial", {}).get("proj2view"), shard,
                                              xl_sorted)
         pts = sp.tail(agg_p, prev_pt)
+        if carry is not None and self.output_global:
+            hp = point_block.hub_params(pfu, self.view_and_scenepoint2global.graph_conv_scenepoint2global, nxt)
+            if hp is not None and point_block._rows_ok(pts, point_block.P_W):
+                skip, SA, XLs, XRn = point_block.hub(pts, hp)
+                carry.update(XRp=XRn, pts_skip=skip, SA=SA, XLs2g=XLs)
         view = sv.tail(agg_c, prev_view)
-        return self._finish(pts, view, plans, prev_glob)
+        return self._finish(pts, view, plans, prev_glob, carry)
 
     def forward_plan(self, P_hat, plans, prev_pt=None, prev_view=None, prev_glob=None):
         shard = plans.get("_shard")
@@ -333,12 +355,13 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
                                            plans.get("_partial", {}).get("proj2view"), shard)
         return self._finish(pts, view, plans, prev_glob)
 
-    def _finish(self, pts, view, plans, prev_glob):
+    def _finish(self, pts, view, plans, prev_glob, carry=None):
         glob = None
         if self.output_global or self.global2view_and_global2scenepoint_enabled:
             glob = self.view_and_scenepoint2global.forward_plan(
                 view, pts, plans["view2global"], plans["scenepoint2global"], prev_glob,
-                plans.get("_partial", {}).get("scenepoint2global"), plans.get("_shard"))
+                plans.get("_partial", {}).get("scenepoint2global"), plans.get("_shard"),
+                xl_pts=carry.pop("XLs2g", None) if carry is not None else None)
         if self.global2view_and_global2scenepoint_enabled:
             pts = self.global2scenepoint(glob, pts)
             view = self.global2view(glob, view)
@@ -366,9 +389,10 @@ class GraphAttnSfMProjectionFeatureUpdate(Module):
             self.mlp = get_linear_layers(n_hidden_layers_proj_update * [n_feat_proj_out] + [n_feat_proj_out],
                                          norm=False)
 
-    def node_terms(self, pts, view, glob):
+    def node_terms(self, pts, view, glob, sp=None):
+        """sp: the point term when PointHubFn already computed it."""
         if self.normalize_global_features:
-            return (dense.ln_relu_linear(pts, self.scenepoint_norm_layer, self.lin_scenepoint),
+            return (sp if sp is not None else dense.ln_relu_linear(pts, self.scenepoint_norm_layer, self.lin_scenepoint),
                     dense.ln_relu_linear(view, self.view_norm_layer, self.lin_view),
                     dense.ln_relu_linear(glob, self.global_norm_layer, self.lin_global))
         return dense.linear(pts, self.lin_scenepoint), dense.linear(view, self.lin_view), \
@@ -431,7 +455,7 @@ class GraphAttnSfMLayer(Module):
                 and self.prev_projfeat_norm_layer.normalized_shape == (2,)
                 and self.global_feature_update.fusable0())
 
-    def forward_fused0(self, P, plans, edges):
+    def forward_fused0(self, P, plans, edges, carry=None, nxt=None):
         """Block 0 (2-wide inputs, projected residual) with the block-0 HIP edge kernels."""
         la, lb = self.prev_projfeat_norm_layer, self.residual_skipconn_proj_norm_layer
         gfu = self.global_feature_update
@@ -439,8 +463,9 @@ class GraphAttnSfMLayer(Module):
         W, b = gfu.lin_l_stack()
         pos = plans["proj2scenepoint"].pos
         XL, token = Block0PrologueFn.apply(P.contiguous(), la.weight, la.bias, W, b, la.eps, pos)
-        pts, view, glob = gfu.forward_fused(XL, plans, None, None, None, xl_sorted=pos is not None)
-        sp, sv, sg = pfu.node_terms(pts, view, glob)
+        pts, view, glob = gfu.forward_fused(XL, plans, None, None, None, xl_sorted=pos is not None, carry=carry,
+                                            pfu=pfu, nxt=nxt)
+        sp, sv, sg = pfu.node_terms(pts, view, glob, carry.pop("SA", None) if carry is not None else None)
         shard = plans.get("_shard")
         sv, sg = replicated_to_local(sv, shard), replicated_to_local(sg, shard)
         sk = self.skip_projection.lin_proj
@@ -448,7 +473,7 @@ class GraphAttnSfMLayer(Module):
                                        la.weight, la.bias, lb.weight, lb.bias, sk.weight, sk.bias, la.eps, edges)
         return P_new, pts, view, glob
 
-    def forward_fused(self, P, plans, edges, prev_pt, prev_view, prev_glob, P0):
+    def forward_fused(self, P, plans, edges, prev_pt, prev_view, prev_glob, P0, carry=None, nxt=None):
         """Blocks >= 1 with the fused HIP edge kernels (see gasfm_amd/edge_block.py)."""
         ln = self.prev_projfeat_norm_layer
         gfu = self.global_feature_update
@@ -456,20 +481,26 @@ class GraphAttnSfMLayer(Module):
         W, b = gfu.lin_l_stack()
         pos = plans["proj2scenepoint"].pos
         XL, token = EdgePrologueFn.apply(P, ln.weight, ln.bias, W, b, pfu.lin_proj.weight, ln.eps, pos)
-        pts, view, glob = gfu.forward_fused(XL, plans, prev_pt, prev_view, prev_glob, xl_sorted=pos is not None)
-        sp, sv, sg = pfu.node_terms(pts, view, glob)
+        pts, view, glob = gfu.forward_fused(XL, plans, prev_pt, prev_view, prev_glob, xl_sorted=pos is not None,
+                                            carry=carry, pfu=pfu, nxt=nxt)
+        sp, sv, sg = pfu.node_terms(pts, view, glob, carry.pop("SA", None) if carry is not None else None)
         shard = plans.get("_shard")
         sv, sg = replicated_to_local(sv, shard), replicated_to_local(sg, shard)
         P_new = EdgeEpilogueFn.apply(P, P0 if self.add_skipconn_from_init_projfeat else None, token, sp, sv, sg,
                                      pfu.lin_proj.weight, pfu.lin_proj.bias, ln.weight, ln.bias, ln.eps, edges)
         return P_new, pts, view, glob
 
-    def forward_plan(self, P, plans, edges, prev_pt=None, prev_view=None, prev_glob=None, P0=None):
-        """P [E, F_in] edge features (cam-major) -> (P' [E, F_out], pts, view, glob)."""
+    def forward_plan(self, P, plans, edges, prev_pt=None, prev_view=None, prev_glob=None, P0=None, carry=None,
+                     nxt=None):
+        """P [E, F_in] edge features (cam-major) -> (P' [E, F_out], pts, view, glob).
+
+        carry / nxt: see GraphAttnSfMGlobalFeatureUpdate.forward_fused (fused CUDA path only)."""
         if P.is_cuda and self.fusable():
-            return self.forward_fused(P, plans, edges, prev_pt, prev_view, prev_glob, P0)
+            return self.forward_fused(P, plans, edges, prev_pt, prev_view, prev_glob, P0, carry, nxt)
         if P.is_cuda and prev_pt is None and prev_view is None and prev_glob is None and self.fusable0():
-            return self.forward_fused0(P, plans, edges)
+            return self.forward_fused0(P, plans, edges, carry, nxt)
+        if carry:
+            raise RuntimeError("point hub outputs pending for a block on the unfused path")
         if self.use_norm_proj_update:
             P_hat = edge_ops.layer_norm_relu(P, self.prev_projfeat_norm_layer)
         else:
@@ -651,18 +682,28 @@ class GraphAttnSfMNet(Module):
         P0 = P if self.add_skipconn_from_init_projfeat else None
         pts = view = glob = None
         sf = self.stateful_global_features
-        for blk in self.equivariant_blocks:
+        heads = self.view_head_enabled or self.scenepoint_head_enabled
+        fgu = self.final_global_update if heads else None
+        final_fused = fgu is not None and values.is_cuda and fgu.fusable() and self.equivariant_blocks[-1].fusable()
+        # consumers of each block's point output (PointHubFn): the next block's (or the fused
+        # final update's) Proj2ScenePoint; carry hands the hub outputs forward
+        carry = {} if (values.is_cuda and sf) else None
+        blocks = list(self.equivariant_blocks)
+        for i, blk in enumerate(blocks):
+            if i + 1 < len(blocks):
+                nxt = blocks[i + 1].global_feature_update.proj2scenepoint if blocks[i + 1].fusable() else None
+            else:
+                nxt = fgu.proj2scenepoint if final_fused else None
             P, pts, view, glob = blk.forward_plan(P, plans, edges, pts if sf else None, view if sf else None,
-                                                  glob if sf else None, P0=P0)
-        if self.view_head_enabled or self.scenepoint_head_enabled:
-            fgu = self.final_global_update
+                                                  glob if sf else None, P0=P0, carry=carry, nxt=nxt)
+        if heads:
             args = (pts if sf else None, view if sf else None, glob if sf else None)
             if P.is_cuda and P.shape[1] == 32 and fgu.fusable():
                 # raw (un-normalised) projection features (graph_attn_sfm.py:141-148): no LN prologue
                 W, b = fgu.lin_l_stack()
                 pos = plans["proj2scenepoint"].pos
                 XL, _ = EdgePrologueFn.apply(P.contiguous(), None, None, W, b, None, 1e-5, pos)
-                pts, view, _ = fgu.forward_fused(XL, plans, *args, xl_sorted=pos is not None)
+                pts, view, _ = fgu.forward_fused(XL, plans, *args, xl_sorted=pos is not None, carry=carry)
             else:
                 pts, view, _ = fgu.forward_plan(P, plans, *args)
         return P, pts, view

@@ -1,0 +1,169 @@
+"""Scene-point side of a GASFM block as two fused autograd Functions (csrc/point_block.hip).
+
+PointTailFn  -- the end of Proj2ScenePoint.forward (reference code/models/layers.py:438-454):
+                x = prev + proj_proj2scenepoint(agg);  p = x + mlp(relu(norm_pre_mlp(x)))
+PointHubFn   -- every consumer of the block output p, in one kernel forward and two backward:
+                skip = p                                          next block's state skip (:442)
+                SA   = lin_scenepoint(relu(scenepoint_norm_layer(p)))            (:928-935)
+                XL   = graph_conv_scenepoint2global.lin_l(p)                     (:560-575, PyG)
+                XR   = next.graph_conv.lin_r(next.norm_and_proj_scenepoint2proj(p))   (:429)
+
+Why one Function for all consumers: autograd sums the gradients of a tensor with several
+consumers using one full-size add per extra consumer ([n x 64], 51 MB at config 4, three per
+block).  Routing every consumer through PointHubFn makes its backward the only producer of
+dp: the C pass adds the next block's target-row gradient to the incoming skip gradient, the
+A+B pass adds lin_l and lin_scenepoint terms in place, and no add kernel runs.
+"""
+import torch
+
+from . import _native
+
+P_W = 64   # n_feat_scenepoint
+A_W = 32   # n_feat_proj
+
+
+def _f32(*shape, like):
+    return torch.empty(shape, dtype=torch.float32, device=like.device)
+
+
+class PointTailFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, prev, agg, Wp, bp, ln_w, ln_b, Wm, bm, eps):
+        agg = agg.contiguous()
+        prev = prev.contiguous() if prev is not None else None
+        Wp, Wm = Wp.contiguous(), Wm.contiguous()
+        out = _f32(agg.shape[0], P_W, like=agg)
+        _native.point_tail_fwd(prev, agg, Wp, bp, ln_w, ln_b, eps, Wm, bm, out)
+        ctx.save_for_backward(prev, agg, Wp, bp, ln_w, ln_b, Wm)
+        ctx.eps = eps
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        prev, agg, Wp, bp, ln_w, ln_b, Wm = ctx.saved_tensors
+        N = agg.shape[0]
+        dout = dout.contiguous()
+        dx = _f32(N, P_W, like=agg)
+        dagg = _f32(N, A_W, like=agg)
+        rows, cols = _native.point_tail_part_shape(N, prev is not None)
+        if rows == 0:
+            tot = torch.zeros(cols, dtype=torch.float32, device=agg.device)
+        else:
+            part = _f32(rows, cols, like=agg)
+            _native.point_tail_bwd(dout, prev, agg, Wp, bp, ln_w, ln_b, ctx.eps, Wm, dx, dagg, part)
+            tot = _native.colsum(part)
+        o = 0
+        dWm = tot[o:o + P_W * P_W].view(P_W, P_W)
+        o += P_W * P_W
+        dWp = tot[o:o + P_W * A_W].view(P_W, A_W)
+        o += P_W * A_W
+        dbm, dbp, dg, dbt = (tot[o + k * P_W:o + (k + 1) * P_W] for k in range(4))
+        return (dx if prev is not None else None), dagg, dWp, dbp, dg, dbt, dWm, dbm, None
+
+
+class PointHubFn(torch.autograd.Function):
+    """p -> (skip, SA, XL, XR); see the module docstring for the four consumers."""
+
+    @staticmethod
+    def forward(ctx, p, gA, bA, WA, WB, bB, gC, bC, WC, bWC, WD, bD, eps):
+        p = p.contiguous()
+        WA, WB, WC, WD = (w.contiguous() for w in (WA, WB, WC, WD))
+        N = p.shape[0]
+        SA, XL, XR = _f32(N, A_W, like=p), _f32(N, P_W, like=p), _f32(N, A_W, like=p)
+        _native.point_hub_fwd(p, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR)
+        ctx.save_for_backward(p, gA, bA, WA, WB, gC, bC, WC, bWC, WD)
+        ctx.eps = eps
+        ctx.set_materialize_grads(False)
+        return p.view_as(p), SA, XL, XR
+
+    @staticmethod
+    def backward(ctx, dskip, dSA, dXL, dXR):
+        p, gA, bA, WA, WB, gC, bC, WC, bWC, WD = ctx.saved_tensors
+        N = p.shape[0]
+        zeros = lambda w: torch.zeros((N, w), dtype=torch.float32, device=p.device)  # noqa: E731
+        dSA = dSA.contiguous() if dSA is not None else zeros(A_W)
+        dXL = dXL.contiguous() if dXL is not None else zeros(P_W)
+        dXR = dXR.contiguous() if dXR is not None else zeros(A_W)
+        dskip = dskip.contiguous() if dskip is not None else None
+        dp = _f32(N, P_W, like=p)
+        rc, cc = _native.point_hub_part_shape(N, 1, dskip is not None)
+        ra, ca = _native.point_hub_part_shape(N, 0, True)
+        if N == 0:
+            tc = torch.zeros(cc, dtype=torch.float32, device=p.device)
+            ta = torch.zeros(ca, dtype=torch.float32, device=p.device)
+        else:
+            part_c = _f32(rc, cc, like=p)
+            _native.point_hub_bwd_c(p, ctx.eps, gC, bC, WC, bWC, WD, dXR, dskip, dp, part_c)
+            part_a = _f32(ra, ca, like=p)
+            # in place: each element of dp is read (as dRes) and written by the same lane
+            _native.point_hub_bwd_ab(p, ctx.eps, gA, bA, WA, WB, dSA, dXL, dp, dp, part_a)
+            tc, ta = _native.colsum(part_c), _native.colsum(part_a)
+        o = 0
+        dWC = tc[o:o + A_W * P_W].view(A_W, P_W)
+        o += A_W * P_W
+        dWD = tc[o:o + A_W * A_W].view(A_W, A_W)
+        o += A_W * A_W
+        dbWC, dbD = tc[o:o + A_W], tc[o + A_W:o + 2 * A_W]
+        o += 2 * A_W
+        dgC, dbC = tc[o:o + P_W], tc[o + P_W:o + 2 * P_W]
+        o = 0
+        dWA = ta[o:o + A_W * P_W].view(A_W, P_W)
+        o += A_W * P_W
+        dWB = ta[o:o + P_W * P_W].view(P_W, P_W)
+        o += P_W * P_W
+        dbB, dgA, dbA = (ta[o + k * P_W:o + (k + 1) * P_W] for k in range(3))
+        return dp, dgA, dbA, dWA, dWB, dbB, dgC, dbC, dWC, dbWC, dWD, dbD, None
+
+
+def _is_ln(m, w):
+    return isinstance(m, torch.nn.LayerNorm) and tuple(m.normalized_shape) == (w,) and m.weight is not None \
+        and m.bias is not None
+
+
+def _is_lin(m, i, o, bias):
+    return isinstance(m, torch.nn.Linear) and m.in_features == i and m.out_features == o \
+        and ((m.bias is not None) == bias)
+
+
+def _rows_ok(t, w):
+    return t is not None and t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.shape[1] == w
+
+
+def tail_fusable(agg_mod, x, prev):
+    """Proj2ScenePoint with 32-wide aggregation, 64-wide points, norm_pre_mlp and a one-Linear mlp."""
+    if not (_rows_ok(x, A_W) and (prev is None or _rows_ok(prev, P_W))):
+        return False
+    proj = getattr(agg_mod, agg_mod._proj_key, None) if agg_mod.n_feat_agg != agg_mod.n_feat_out else None
+    return (proj is not None and _is_lin(proj, A_W, P_W, True) and agg_mod.use_norm_pre_mlp
+            and _is_ln(agg_mod.norm_pre_mlp, P_W) and len(agg_mod.mlp) == 1 and _is_lin(agg_mod.mlp[0], P_W, P_W, True))
+
+
+def tail(agg_mod, x, prev):
+    proj = getattr(agg_mod, agg_mod._proj_key)
+    ln, lin = agg_mod.norm_pre_mlp, agg_mod.mlp[0]
+    return PointTailFn.apply(prev, x, proj.weight, proj.bias, ln.weight, ln.bias, lin.weight, lin.bias, ln.eps)
+
+
+def hub_params(pfu, s2g_conv, nxt):
+    """(gA, bA, WA, WB, bB, gC, bC, WC, bWC, WD, bD, eps) or None when the shapes do not match.
+
+    pfu: this block's projection-feature update (scenepoint_norm_layer, lin_scenepoint);
+    s2g_conv: this block's graph_conv_scenepoint2global; nxt: the next Proj2ScenePoint."""
+    if pfu is None or s2g_conv is None or nxt is None or not pfu.normalize_global_features:
+        return None
+    lnA, linA = pfu.scenepoint_norm_layer, pfu.lin_scenepoint
+    linB = s2g_conv.lin_l
+    seq = getattr(nxt, nxt._state_key, None) if nxt.stateful else None
+    if seq is None or len(seq) != 3:
+        return None
+    lnC, linC, linD = seq[0], seq[2], nxt.graph_conv.lin_r
+    if not (_is_ln(lnA, P_W) and _is_lin(linA, P_W, A_W, False) and _is_lin(linB, P_W, P_W, True)
+            and _is_ln(lnC, P_W) and _is_lin(linC, P_W, A_W, True) and _is_lin(linD, A_W, A_W, True)
+            and lnA.eps == lnC.eps):
+        return None
+    return (lnA.weight, lnA.bias, linA.weight, linB.weight, linB.bias, lnC.weight, lnC.bias, linC.weight,
+            linC.bias, linD.weight, linD.bias, lnA.eps)
+
+
+def hub(p, params):
+    return PointHubFn.apply(p, *params)

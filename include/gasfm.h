@@ -252,6 +252,51 @@ int gasfm_node_ln_linear_bwd(const float* dY, const float* X, int64_t N, int32_t
                              const float* ln_b, float eps, const float* W, int32_t n_out, int32_t residual,
                              float* dX, float* part, void* stream);
 
+/* ---- scene-point block chains (n rows x 64; aggregation / projection width 32) ----
+ * tail: the end of Proj2ScenePoint.forward (layers.py:438-454)
+ *   x = prev + Wp agg + bp ; p = x + Wm relu(LN(x)) + bm          (prev may be null: block 0)
+ * hub: every consumer of p in one pass --
+ *   SA = WA relu(LN_A(p))           lin_scenepoint(relu(scenepoint_norm_layer(p))) (layers.py:928-935)
+ *   XL = WB p + bB                  graph_conv_scenepoint2global.lin_l (PyG, layers.py:560-575)
+ *   XR = WD (WC relu(LN_C(p)) + bWC) + bD    the next block's norm_and_proj_scenepoint2proj
+ *                                   (layers.py:429) and its graph_conv.lin_r; gC == null skips it
+ * Backward gradients of weights / biases / LayerNorm affines leave as per-workgroup partial
+ * rows ([rows x cols], shapes from the *_part_shape queries) for gasfm_colsum. */
+
+/* Partial buffer rows for gasfm_point_tail_bwd; *cols receives the row width:
+ * [dWm 64x64 | dWp 64x32 | dbm 64 | dbp 64 | dgamma 64 | dbeta 64]. */
+int gasfm_point_tail_part_shape(int64_t N, int32_t has_prev, int32_t* cols);
+
+/* Partial buffer rows for gasfm_point_hub_bwd_ab (which = 0):
+ *   [dWA 32x64 | dWB 64x64 | dbB 64 | dgamma_A 64 | dbeta_A 64]
+ * or gasfm_point_hub_bwd_c (which = 1):
+ *   [dWC 32x64 | dWD 32x32 | dbWC 32 | dbD 32 | dgamma_C 64 | dbeta_C 64]. */
+int gasfm_point_hub_part_shape(int64_t N, int32_t which, int32_t has_res, int32_t* cols);
+
+int gasfm_point_tail_fwd(const float* prev, const float* agg, int64_t N, const float* Wp, const float* bp,
+                         const float* ln_w, const float* ln_b, float eps, const float* Wm, const float* bm,
+                         float* out, void* stream);
+
+/* dx = dout + LN_bwd(mask (dout Wm)) (== d prev), dagg = dx Wp, partials. */
+int gasfm_point_tail_bwd(const float* dout, const float* prev, const float* agg, int64_t N, const float* Wp,
+                         const float* bp, const float* ln_w, const float* ln_b, float eps, const float* Wm,
+                         float* dx, float* dagg, float* part, void* stream);
+
+int gasfm_point_hub_fwd(const float* X, int64_t N, float eps, const float* gA, const float* bA, const float* WA,
+                        float* SA, const float* WB, const float* bB, float* XL, const float* gC, const float* bC,
+                        const float* WC, const float* bWC, const float* WD, const float* bD, float* XR,
+                        void* stream);
+
+/* dX = dRes + LN_C_bwd(mask (dXR WD WC)) (dRes may be null), partials. */
+int gasfm_point_hub_bwd_c(const float* X, int64_t N, float eps, const float* gC, const float* bC, const float* WC,
+                          const float* bWC, const float* WD, const float* dXR, const float* dRes, float* dX,
+                          float* part, void* stream);
+
+/* dX = dRes + dXL WB + LN_A_bwd(mask (dSA WA)) (dRes may be null), partials. */
+int gasfm_point_hub_bwd_ab(const float* X, int64_t N, float eps, const float* gA, const float* bA,
+                           const float* WA, const float* WB, const float* dSA, const float* dXL,
+                           const float* dRes, float* dX, float* part, void* stream);
+
 /* ---- global node (ONE row): LayerNorm -> ReLU -> Linear (+ residual) ----
  * Replaces the M = 1 aten chains on the global feature vector: norm_and_proj_global2view /
  * _global2scenepoint (layers.py:497-520), both convs' lin_r on those rows (PyG),

@@ -92,6 +92,37 @@ def main():
         run(f"node_bwd<{n_out},{int(resid)}>",
             lambda: _native.node_ln_linear_bwd(dY, X, g64, b64, 1e-5, Wn, resid, dX, npart),
             n * (4 * n_out + 512))
+    point_bench(run, rnd, n, dev)
+
+
+def point_bench(run, rnd, n, dev):
+    """Fused scene-point tail / hub kernels (csrc/point_block.hip) at n rows."""
+    from gasfm_amd import point_block as pb
+    X, agg = rnd(n, 64), rnd(n, 32)
+    g64, b64 = 1 + 0.1 * rnd(64), 0.1 * rnd(64)
+    Wp, bp, Wm, bm = rnd(64, 32) / 6, rnd(64), rnd(64, 64) / 8, rnd(64)
+    out = torch.empty(n, 64, device=dev)
+    run("point_tail_fwd", lambda: _native.point_tail_fwd(X, agg, Wp, bp, g64, b64, 1e-5, Wm, bm, out), n * 640)
+    dx, dagg = torch.empty(n, 64, device=dev), torch.empty(n, 32, device=dev)
+    rows, cols = _native.point_tail_part_shape(n, True)
+    part = torch.empty(rows, cols, device=dev)
+    dout = rnd(n, 64)
+    run("point_tail_bwd", lambda: _native.point_tail_bwd(dout, X, agg, Wp, bp, g64, b64, 1e-5, Wm, dx, dagg, part),
+        n * 1152)
+    WA, WB, bB, WC, bWC, WD, bD = rnd(32, 64) / 8, rnd(64, 64) / 8, rnd(64), rnd(32, 64) / 8, rnd(32), rnd(32, 32) / 6, rnd(32)
+    SA, XL, XR = torch.empty(n, 32, device=dev), torch.empty(n, 64, device=dev), torch.empty(n, 32, device=dev)
+    run("point_hub_fwd", lambda: _native.point_hub_fwd(X, 1e-5, g64, b64, WA, SA, WB, bB, XL, g64, b64, WC, bWC, WD,
+                                                        bD, XR), n * 768)
+    dSA, dXL, dXR, dsk = rnd(n, 32), rnd(n, 64), rnd(n, 32), rnd(n, 64)
+    rc, cc = _native.point_hub_part_shape(n, 1, True)
+    ra, ca = _native.point_hub_part_shape(n, 0, True)
+    pc_, pa_ = torch.empty(rc, cc, device=dev), torch.empty(ra, ca, device=dev)
+    dp = torch.empty(n, 64, device=dev)
+    run("point_hub_bwd_c", lambda: _native.point_hub_bwd_c(X, 1e-5, g64, b64, WC, bWC, WD, dXR, dsk, dp, pc_),
+        n * 640)
+    run("point_hub_bwd_ab", lambda: _native.point_hub_bwd_ab(X, 1e-5, g64, b64, WA, WB, dSA, dXL, dp, dp, pa_),
+        n * 1024)
+    del pb
 
 
 if __name__ == "__main__":

@@ -44,6 +44,15 @@ def main():
     print(f"step {k}: {len(seg)} kernels, span {span / 1e3:.2f} ms, busy {sum(tot.values()) / 1e3:.2f} ms")
     for cat in sorted(tot, key=lambda x: -tot[x]):
         print(f"  {tot[cat] / 1e3:7.2f} ms {cnt[cat]:5d} kernels  {cat}")
+    per = defaultdict(lambda: [0.0, 0])
+    for n, s, e in seg:
+        key = re.sub(r"\(.*", "", n)[:90]
+        per[key][0] += (e - s) / 1e3
+        per[key][1] += 1
+    print("top kernels (us total, count, us mean):")
+    for key in sorted(per, key=lambda x: -per[x][0])[:int(sys.argv[3]) if len(sys.argv) > 3 else 30]:
+        t, n = per[key]
+        print(f"  {t:9.1f} {n:5d} {t / n:8.2f}  {key}")
 
 
 if __name__ == "__main__":
