@@ -94,16 +94,12 @@ __device__ __forceinline__ void norm_rows32(const float4 (&v)[2], int nrows, con
     float mean = 0.f, rstd = 1.f;
     if (LN) {
       float s = x[0] + x[1] + x[2] + x[3];
-      s += __shfl_xor(s, 1);
-      s += __shfl_xor(s, 2);
-      s += __shfl_xor(s, 4);
+      s = group_sum<8>(s);
       mean = s * (1.f / F);
       float q = 0.f;
 #pragma unroll
       for (int k = 0; k < 4; ++k) q = fmaf(x[k] - mean, x[k] - mean, q);
-      q += __shfl_xor(q, 1);
-      q += __shfl_xor(q, 2);
-      q += __shfl_xor(q, 4);
+      q = group_sum<8>(q);
       rstd = rsqrtf(q * (1.f / F) + eps);
     }
     const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
@@ -554,16 +550,12 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINWAVES) void edge_prologue_b
         float mean = 0.f, rstd = 1.f;
         if (LN) {
           float sm = x[0] + x[1] + x[2] + x[3];
-          sm += __shfl_xor(sm, 1);
-          sm += __shfl_xor(sm, 2);
-          sm += __shfl_xor(sm, 4);
+          sm = group_sum<8>(sm);
           mean = sm * (1.f / F);
           float q = 0.f;
 #pragma unroll
           for (int k = 0; k < 4; ++k) q = fmaf(x[k] - mean, x[k] - mean, q);
-          q += __shfl_xor(q, 1);
-          q += __shfl_xor(q, 2);
-          q += __shfl_xor(q, 4);
+          q = group_sum<8>(q);
           rstd = rsqrtf(q * (1.f / F) + eps);
         }
         const bool live = r < nrows;
@@ -739,13 +731,10 @@ __global__ __launch_bounds__(kThreads) void segment_rowsum_kernel(const gasfm_wo
         acc.w += v[u].w;
       }
     }
-#pragma unroll
-    for (int o = 8; o < kW; o <<= 1) {
-      acc.x += __shfl_xor(acc.x, o);
-      acc.y += __shfl_xor(acc.y, o);
-      acc.z += __shfl_xor(acc.z, o);
-      acc.w += __shfl_xor(acc.w, o);
-    }
+    acc.x = xor_sum_from<8>(acc.x);
+    acc.y = xor_sum_from<8>(acc.y);
+    acc.z = xor_sum_from<8>(acc.z);
+    acc.w = xor_sum_from<8>(acc.w);
     if (row == 0) {
       const float4 r = make_float4(acc.x * scale, acc.y * scale, acc.z * scale, acc.w * scale);
       float* dst = (w.slot < 0) ? out + int64_t(w.seg) * F : part + int64_t(w.slot) * F;

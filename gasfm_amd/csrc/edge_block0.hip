@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include "common.hpp"
+#include "lanes.hpp"
 
 namespace gasfm {
 namespace {
@@ -48,9 +49,7 @@ template <int N>
 __device__ __forceinline__ void block_reduce_store(float (&v)[N], float* out, float* sh) {
   // wave reduce (xor over all 64 lanes), then waves in order through LDS
 #pragma unroll
-  for (int k = 0; k < N; ++k)
-#pragma unroll
-    for (int o = 1; o < kW; o <<= 1) v[k] += __shfl_xor(v[k], o);
+  for (int k = 0; k < N; ++k) v[k] = group_sum<kW>(v[k]);
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   if (lane == 0)
 #pragma unroll
@@ -187,13 +186,10 @@ __global__ __launch_bounds__(kT) void edge0_epilogue_bwd_kernel(
         qb0 = fmaf(d[k], wsk[k][0], qb0);
         qb1 = fmaf(d[k], wsk[k][1], qb1);
       }
-#pragma unroll
-      for (int o = 1; o < 8; o <<= 1) {
-        qa0 += __shfl_xor(qa0, o);
-        qa1 += __shfl_xor(qa1, o);
-        qb0 += __shfl_xor(qb0, o);
-        qb1 += __shfl_xor(qb1, o);
-      }
+      qa0 = group_sum<8>(qa0);
+      qa1 = group_sum<8>(qa1);
+      qb0 = group_sum<8>(qb0);
+      qb1 = group_sum<8>(qb1);
       // LN_b / ReLU backward of the skip branch (every lane of the row holds the same values)
       const float db0 = yb0 > 0.f ? qb0 : 0.f, db1 = yb1 > 0.f ? qb1 : 0.f;
       float dx0, dx1;
@@ -208,8 +204,7 @@ __global__ __launch_bounds__(kT) void edge0_epilogue_bwd_kernel(
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int o = 8; o < kW; o <<= 1) dsv[k] += __shfl_xor(dsv[k], o);
+      dsv[k] = xor_sum_from<8>(dsv[k]);
     if (row == 0) {
       const float4 r = make_float4(dsv[0] * scale, dsv[1] * scale, dsv[2] * scale, dsv[3] * scale);
       float* dst = (w.slot < 0) ? dSv + int64_t(w.seg) * 32 : part_dsv + int64_t(w.slot) * 32;
@@ -228,12 +223,9 @@ __global__ __launch_bounds__(kT) void edge0_epilogue_bwd_kernel(
   }
   float t[4] = {dgb[0], dgb[1], dbb[0], dbb[1]};
 #pragma unroll
-  for (int o = 8; o < kW; o <<= 1) {
+  for (int k = 0; k < 20; ++k) r[k] = xor_sum_from<8>(r[k]);
 #pragma unroll
-    for (int k = 0; k < 20; ++k) r[k] += __shfl_xor(r[k], o);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) t[k] += __shfl_xor(t[k], o);
-  }
+  for (int k = 0; k < 4; ++k) t[k] = xor_sum_from<8>(t[k]);
   const int wave = threadIdx.x / kW;
   float* sw = sh + wave * kPart0E;
   if (row == 0) {

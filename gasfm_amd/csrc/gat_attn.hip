@@ -31,6 +31,7 @@
 #include <cmath>
 
 #include "common.hpp"
+#include "lanes.hpp"
 
 namespace gasfm {
 
@@ -77,9 +78,7 @@ __device__ __forceinline__ void store_vec(float* p, const float (&d)[N]) {
 // Sum over the LPH lanes that share a head (lanes are contiguous within an edge row).
 template <int LPH>
 __device__ __forceinline__ float head_sum(float v) {
-#pragma unroll
-  for (int o = 1; o < LPH; o <<= 1) v += __shfl_xor(v, o);
-  return v;
+  return group_sum<LPH>(v);
 }
 
 __device__ __forceinline__ float safe_scale(float m_old, float m_new) {
@@ -104,20 +103,26 @@ __device__ __forceinline__ void merge_state(float (&m)[G::HPL], float (&s)[G::HP
 }
 
 // Combine the EPR row states of a wave (xor over the row bits of the lane id).
+template <class G, int O>
+__device__ __forceinline__ void reduce_rows_step(float (&m)[G::HPL], float (&s)[G::HPL], float (&a)[G::VEC]) {
+  if constexpr (O < kWave) {
+    if constexpr (O >= G::LPE) {
+      float m2[G::HPL], s2[G::HPL], a2[G::VEC];
+#pragma unroll
+      for (int hh = 0; hh < G::HPL; ++hh) {
+        m2[hh] = xor_lane<O>(m[hh]);
+        s2[hh] = xor_lane<O>(s[hh]);
+      }
+#pragma unroll
+      for (int v = 0; v < G::VEC; ++v) a2[v] = xor_lane<O>(a[v]);
+      merge_state<G>(m, s, a, m2, s2, a2);
+    }
+    reduce_rows_step<G, 2 * O>(m, s, a);
+  }
+}
 template <class G>
 __device__ __forceinline__ void reduce_rows(float (&m)[G::HPL], float (&s)[G::HPL], float (&a)[G::VEC]) {
-#pragma unroll
-  for (int o = G::LPE; o < kWave; o <<= 1) {
-    float m2[G::HPL], s2[G::HPL], a2[G::VEC];
-#pragma unroll
-    for (int hh = 0; hh < G::HPL; ++hh) {
-      m2[hh] = __shfl_xor(m[hh], o);
-      s2[hh] = __shfl_xor(s[hh], o);
-    }
-#pragma unroll
-    for (int v = 0; v < G::VEC; ++v) a2[v] = __shfl_xor(a[v], o);
-    merge_state<G>(m, s, a, m2, s2, a2);
-  }
+  reduce_rows_step<G, 1>(m, s, a);
 }
 
 __device__ __forceinline__ int wave_id_uniform() {
@@ -635,10 +640,7 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_kernel(
       }
     }
 #pragma unroll
-    for (int o2 = G::LPE; o2 < kWave; o2 <<= 1) {
-#pragma unroll
-      for (int v = 0; v < G::VEC; ++v) dxr[v] += __shfl_xor(dxr[v], o2);
-    }
+    for (int v = 0; v < G::VEC; ++v) dxr[v] = xor_sum_from<G::LPE>(dxr[v]);
     if (row == 0) {
       if (w.slot < 0)
         store_vec<G::VEC>(dXR + sg * ldDXR + f0, dxr);
@@ -647,10 +649,7 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_kernel(
     }
   }
 #pragma unroll
-  for (int o2 = G::LPE; o2 < kWave; o2 <<= 1) {
-#pragma unroll
-    for (int v = 0; v < G::VEC; ++v) datt[v] += __shfl_xor(datt[v], o2);
-  }
+  for (int v = 0; v < G::VEC; ++v) datt[v] = xor_sum_from<G::LPE>(datt[v]);
   if (row == 0) {
     store_vec<G::VEC>(datt_part + int64_t(wave) * 2 * G::HC + f0, datt);
     store_vec<G::VEC>(datt_part + int64_t(wave) * 2 * G::HC + G::HC + f0, dbias);
@@ -798,10 +797,7 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_glds_kernel(
       chunk(e0);
     }
 #pragma unroll
-    for (int o2 = G::LPE; o2 < kWave; o2 <<= 1) {
-#pragma unroll
-      for (int v = 0; v < G::VEC; ++v) dxr[v] += __shfl_xor(dxr[v], o2);
-    }
+    for (int v = 0; v < G::VEC; ++v) dxr[v] = xor_sum_from<G::LPE>(dxr[v]);
     if (row == 0) {
       if (w.slot < 0)
         store_vec<G::VEC>(dXR + int64_t(w.seg) * ldDXR + f0, dxr);
@@ -810,10 +806,7 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_glds_kernel(
     }
   }
 #pragma unroll
-  for (int o2 = G::LPE; o2 < kWave; o2 <<= 1) {
-#pragma unroll
-    for (int v = 0; v < G::VEC; ++v) datt[v] += __shfl_xor(datt[v], o2);
-  }
+  for (int v = 0; v < G::VEC; ++v) datt[v] = xor_sum_from<G::LPE>(datt[v]);
   if (row == 0) {
     store_vec<G::VEC>(datt_part + int64_t(wave) * 2 * G::HC + f0, datt);
     store_vec<G::VEC>(datt_part + int64_t(wave) * 2 * G::HC + G::HC + f0, dbias);

@@ -42,30 +42,13 @@ constexpr int kWaves8 = 8, kThreads8 = kWaves8 * kW;
 // partial-row layouts (floats)
 constexpr int TAIL_PART = FP * FP + FP * FA + 4 * FP;                 // dWm dWp dbm dbp dgam dbet
 
-// A-operand element (row i of a [rows x ld] matrix, column k) of a 16-row tile; rows past
-// nrows read row 0 and return 0 (unconditional load, see tile.hpp load_tile)
-__device__ __forceinline__ float ld_a(const float* __restrict__ P, int ld, int64_t row0, int nrows, int i, int k) {
-  const float v = P[(row0 + (i < nrows ? i : 0)) * ld + k];
-  return i < nrows ? v : 0.f;
-}
-
-// 16 x 64 tile of rows into LDS (row stride 66) with per-row mean / rstd (MS, RS)
-__device__ __forceinline__ void load_rows_stats(const float* __restrict__ X, int64_t row0, int nrows, float eps,
-                                                float* Raw, float* MS, float* RS, int lane) {
-  const int c = (lane & 15) * 4;
-  float4 v[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int r = (lane >> 4) + 4 * u;
-    v[u] = *reinterpret_cast<const float4*>(X + (row0 + (r < nrows ? r : 0)) * FP + c);
-    if (r >= nrows) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
+// per-row mean / rstd of a 64-wide tile in row layout (rows_load<64>: the 16 lanes of a lane
+// group hold one row) -> MS, RS
+__device__ __forceinline__ void row_stats64(const float4 (&v)[4], float eps, float* MS, float* RS, int lane) {
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int r = (lane >> 4) + 4 * u;
     const float x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) Raw[r * L66 + c + k] = x[k];
     const float mean = sum16(x[0] + x[1] + x[2] + x[3]) * (1.f / FP);
     float q = 0.f;
 #pragma unroll
@@ -99,22 +82,28 @@ __device__ __forceinline__ void ln_relu_bwd_row(const float (&xh)[4], const floa
   for (int nt = 0; nt < 4; ++nt) dx[nt] = rstd * (gv[nt] - s1 - xh[nt] * s2);
 }
 
+// Every kernel below: per 16-row tile, all global loads are issued first as coalesced float4
+// rows (tile.hpp rows_load), staged into the wave's LDS slice, consumed from LDS in the MFMA
+// A / B / C layouts, and the outputs leave through an LDS staging tile as float4 rows.
+
 // ----------------------------------------------------------------------------- tail
 template <bool PREV>
 __global__ __launch_bounds__(kThreads) void point_tail_fwd_kernel(
     const float* __restrict__ prev, const float* __restrict__ agg, int64_t N, const float* __restrict__ Wp,
     const float* __restrict__ bp, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
     const float* __restrict__ Wm, const float* __restrict__ bm, float* __restrict__ out) {
-  __shared__ float WpT[FA * L80];  // WpT[j][o] = Wp[o][j]
-  __shared__ float WmT[FP * L80];  // WmT[k][o] = Wm[o][k]
-  __shared__ float tiles[kWaves][TR * L34 + TR * L66];
+  constexpr int PW = TR * L34 + 2 * TR * L66;  // Ag, Pv (prev, then the output), Ph
+  __shared__ float WpT[FA * L80];              // WpT[j][o] = Wp[o][j]
+  __shared__ float WmT[FP * L80];              // WmT[k][o] = Wm[o][k]
+  __shared__ float tiles[kWaves * PW];
   for (int q = threadIdx.x; q < FP * FA; q += kThreads) WpT[(q % FA) * L80 + q / FA] = Wp[q];
   for (int q = threadIdx.x; q < FP * FP; q += kThreads) WmT[(q % FP) * L80 + q / FP] = Wm[q];
   __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
-  float* Ag = tiles[wave];
-  float* Ph = Ag + TR * L34;
+  float* Ag = tiles + wave * PW;
+  float* Pv = Ag + TR * L34;
+  float* Ph = Pv + TR * L66;
   float bpv[4], bmv[4], gv[4], bv[4];
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
@@ -128,14 +117,11 @@ __global__ __launch_bounds__(kThreads) void point_tail_fwd_kernel(
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row0 = t * TR;
     const int nrows = int(N - row0 < TR ? N - row0 : TR);
-    load_tile<FA, L34>(agg, FA, row0, nrows, Ag, lane);
-    float pv[4][4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int e = 4 * g + r;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) pv[nt][r] = PREV ? prev[(row0 + (e < nrows ? e : 0)) * FP + nt * 16 + c] : 0.f;
-    }
+    float4 va[2], vp[4];
+    rows_load<FA>(agg, FA, row0, nrows, va, lane);
+    if (PREV) rows_load<FP>(prev, FP, row0, nrows, vp, lane);
+    rows_to_lds<FA, L34>(Ag, va, lane);
+    if (PREV) rows_to_lds<FP, L66>(Pv, vp, lane);
     wave_sync();
     f32x4 xa[4] = {zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
@@ -147,10 +133,11 @@ __global__ __launch_bounds__(kThreads) void point_tail_fwd_kernel(
     float xv[4][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+      const int e = 4 * g + r;
       float s1 = 0.f;
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        xv[nt][r] = xa[nt][r] + bpv[nt] + pv[nt][r];
+        xv[nt][r] = xa[nt][r] + bpv[nt] + (PREV ? Pv[e * L66 + nt * 16 + c] : 0.f);
         s1 += xv[nt][r];
       }
       const float mean = sum16(s1) * (1.f / FP);
@@ -160,7 +147,7 @@ __global__ __launch_bounds__(kThreads) void point_tail_fwd_kernel(
       const float rstd = rsqrtf(sum16(q) * (1.f / FP) + eps);
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
-        Ph[(4 * g + r) * L66 + nt * 16 + c] = fmaxf(fmaf((xv[nt][r] - mean) * rstd, gv[nt], bv[nt]), 0.f);
+        Ph[e * L66 + nt * 16 + c] = fmaxf(fmaf((xv[nt][r] - mean) * rstd, gv[nt], bv[nt]), 0.f);
     }
     wave_sync();
     f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
@@ -171,14 +158,13 @@ __global__ __launch_bounds__(kThreads) void point_tail_fwd_kernel(
       for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma16(a, WmT[(4 * s + g) * L80 + nt * 16 + c], acc[nt]);
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int e = 4 * g + r;
-      if (e < nrows) {
-        float* o = out + (row0 + e) * FP;
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) o[nt * 16 + c] = xv[nt][r] + acc[nt][r] + bmv[nt];
-      }
-    }
+      for (int nt = 0; nt < 4; ++nt) Pv[(4 * g + r) * L66 + nt * 16 + c] = xv[nt][r] + acc[nt][r] + bmv[nt];
+    wave_sync();
+    float4 vo[4];
+    rows_from_lds<FP, L66>(Pv, vo, lane);
+    rows_store<FP>(out, FP, row0, nrows, vo, lane);
     wave_sync();
   }
 }
@@ -191,17 +177,14 @@ __global__ __launch_bounds__(kThreads8) void point_tail_bwd_kernel(
     const float* __restrict__ Wp, const float* __restrict__ bp, const float* __restrict__ gam,
     const float* __restrict__ bet, float eps, const float* __restrict__ Wm, float* __restrict__ dx,
     float* __restrict__ dagg, float* __restrict__ part) {
-  constexpr int PW = 3 * TR * L66 + TR;  // per wave: D (dout), XH (LN-normalised x), DX (aliases the agg tile), rstd
+  // per wave: D (dout; dagg staging at the end), XH (prev, then LN-normalised x), DX, Ag, rstd
+  constexpr int PW = 3 * TR * L66 + TR * L34 + TR;
   constexpr int NRED = 64 + 32 + 16;
   static_assert(NRED * kW <= kWaves8 * PW, "reduction scratch");
-  __shared__ float WpT[FA * L80];      // WpT[j][o] = Wp[o][j]   (x recompute)
   __shared__ float WmL[FP * L80];      // WmL[o][i] = Wm[o][i]   (dout W_m)
-  __shared__ float WpL[FP * L48];      // WpL[o][j] = Wp[o][j]   (dx W_p)
+  __shared__ float WpL[FP * L48];      // WpL[o][j] = Wp[o][j]   (dx W_p; read transposed for x)
   __shared__ float tiles[kWaves8 * PW];
-  for (int q = threadIdx.x; q < FP * FA; q += kThreads8) {
-    WpT[(q % FA) * L80 + q / FA] = Wp[q];
-    WpL[(q / FA) * L48 + q % FA] = Wp[q];
-  }
+  for (int q = threadIdx.x; q < FP * FA; q += kThreads8) WpL[(q / FA) * L48 + q % FA] = Wp[q];
   for (int q = threadIdx.x; q < FP * FP; q += kThreads8) WmL[(q / FP) * L80 + q % FP] = Wm[q];
   __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
@@ -209,8 +192,8 @@ __global__ __launch_bounds__(kThreads8) void point_tail_bwd_kernel(
   float* D = tiles + wave * PW;
   float* XH = D + TR * L66;
   float* DX = XH + TR * L66;
-  float* RSt = DX + TR * L66;
-  float* Ag = DX;  // agg tile, dead before DX is written
+  float* Ag = DX + TR * L66;
+  float* RSt = Ag + TR * L34;
   float bpv[4], gv[4], bv[4];
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
@@ -232,23 +215,30 @@ __global__ __launch_bounds__(kThreads8) void point_tail_bwd_kernel(
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row0 = t * TR;
     const int nrows = int(N - row0 < TR ? N - row0 : TR);
-    load_tile<FA, L34>(agg, FA, row0, nrows, Ag, lane);
-    load_tile<FP, L66>(dout, FP, row0, nrows, D, lane);
-    float pv[4][4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int e = 4 * g + r;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) pv[nt][r] = PREV ? prev[(row0 + (e < nrows ? e : 0)) * FP + nt * 16 + c] : 0.f;
+    {
+      float4 va[2], vd[4], vp[4];
+      rows_load<FA>(agg, FA, row0, nrows, va, lane);
+      rows_load<FP>(dout, FP, row0, nrows, vd, lane);
+      if (PREV) rows_load<FP>(prev, FP, row0, nrows, vp, lane);
+      rows_to_lds<FA, L34>(Ag, va, lane);
+      rows_to_lds<FP, L66>(D, vd, lane);
+      if (PREV) rows_to_lds<FP, L66>(XH, vp, lane);
     }
     wave_sync();
-    // recompute x (C layout); x_hat and rstd to LDS
+    // recompute x (C layout): agg W_p^T (W_p read transposed from WpL) + b_p + prev
     f32x4 xa[4] = {zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
     for (int s = 0; s < FA / 4; ++s) {
       const float a = Ag[c * L34 + 4 * s + g];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) xa[nt] = mfma16(a, WpT[(4 * s + g) * L80 + nt * 16 + c], xa[nt]);
+      for (int nt = 0; nt < 4; ++nt) xa[nt] = mfma16(a, WpL[(nt * 16 + c) * L48 + 4 * s + g], xa[nt]);
+    }
+    if (PREV) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) xa[nt][r] += XH[(4 * g + r) * L66 + nt * 16 + c];
+      wave_sync();  // prev read before XH is overwritten
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -256,7 +246,7 @@ __global__ __launch_bounds__(kThreads8) void point_tail_bwd_kernel(
       float xr[4], s1 = 0.f;
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        xr[nt] = xa[nt][r] + bpv[nt] + pv[nt][r];
+        xr[nt] = xa[nt][r] + bpv[nt];
         s1 += xr[nt];
       }
       const float mean = sum16(s1) * (1.f / FP);
@@ -269,7 +259,7 @@ __global__ __launch_bounds__(kThreads8) void point_tail_bwd_kernel(
       if (c == 0) RSt[e] = rstd;
     }
     wave_sync();
-    // d relu-out = dout W_m
+    // d relu-out = dout W_m; LayerNorm backward; dx = dout + ... (rows past nrows: dout is 0)
     f32x4 dph[4] = {zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
     for (int s = 0; s < FP / 4; ++s) {
@@ -280,49 +270,23 @@ __global__ __launch_bounds__(kThreads8) void point_tail_bwd_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int e = 4 * g + r;
-      float xr[4];
+      float xr[4], o[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) xr[nt] = XH[e * L66 + nt * 16 + c];
       const float dh[4] = {dph[0][r], dph[1][r], dph[2][r], dph[3][r]};
-      float o[4];
-      ln_relu_bwd_row(xr, dh, gv, bv, RSt[e], dg, dbt, o);  // rows past nrows: dout rows are 0
+      ln_relu_bwd_row(xr, dh, gv, bv, RSt[e], dg, dbt, o);
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) o[nt] += D[e * L66 + nt * 16 + c];
-      if (e < nrows) {
-        float* d = dx + (row0 + e) * FP;
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) d[nt * 16 + c] = o[nt];
-      }
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) DX[e * L66 + nt * 16 + c] = e < nrows ? o[nt] : 0.f;
+      for (int nt = 0; nt < 4; ++nt) DX[e * L66 + nt * 16 + c] = e < nrows ? o[nt] + D[e * L66 + nt * 16 + c] : 0.f;
     }
     wave_sync();
-    // dagg = dx W_p
-    f32x4 da[2] = {zero4(), zero4()};
-#pragma unroll
-    for (int s = 0; s < FP / 4; ++s) {
-      const float a = DX[c * L66 + 4 * s + g];
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) da[nt] = mfma16(a, WpL[(4 * s + g) * L48 + nt * 16 + c], da[nt]);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int e = 4 * g + r;
-      if (e < nrows) {
-        float* d = dagg + (row0 + e) * FA;
-        d[c] = da[0][r];
-        d[16 + c] = da[1][r];
-      }
-    }
-    // dW_m += dout^T relu(LN x), dW_p += dx^T agg, biases (rows past nrows: dout, dx are 0)
-#pragma unroll
+    // dW_m += dout^T relu(LN x), dW_p += dx^T agg, biases (rows past nrows: dout, dx, agg are 0)
+#pragma unroll 1
     for (int s = 0; s < TR / 4; ++s) {
       const int row = 4 * s + g;
-      float ph[4], ag[2];
+      float ph[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) ph[nt] = fmaxf(fmaf(XH[row * L66 + nt * 16 + c], gv[nt], bv[nt]), 0.f);
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) ag[nt] = ld_a(agg, FA, row0, nrows, row, nt * 16 + c);
+      const float ag[2] = {Ag[row * L34 + c], Ag[row * L34 + 16 + c]};
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const float a = D[row * L66 + mt * 16 + c];
@@ -334,6 +298,27 @@ __global__ __launch_bounds__(kThreads8) void point_tail_bwd_kernel(
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) dWp[mt][nt] = mfma16(a2, ag[nt], dWp[mt][nt]);
       }
+    }
+    // dagg = dx W_p, staged into D (dead) as 16 x 32
+    f32x4 da[2] = {zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < FP / 4; ++s) {
+      const float a = DX[c * L66 + 4 * s + g];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) da[nt] = mfma16(a, WpL[(4 * s + g) * L48 + nt * 16 + c], da[nt]);
+    }
+    wave_sync();
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) D[(4 * g + r) * L34 + nt * 16 + c] = da[nt][r];
+    wave_sync();
+    {
+      float4 vx[4], vg[2];
+      rows_from_lds<FP, L66>(DX, vx, lane);
+      rows_from_lds<FA, L34>(D, vg, lane);
+      rows_store<FP>(dx, FP, row0, nrows, vx, lane);
+      rows_store<FA>(dagg, FA, row0, nrows, vg, lane);
     }
     wave_sync();
   }
@@ -388,12 +373,13 @@ __global__ __launch_bounds__(kThreads) void point_hub_fwd_kernel(
     const float* __restrict__ bB, float* __restrict__ XL, const float* __restrict__ gC,
     const float* __restrict__ bC, const float* __restrict__ WC, const float* __restrict__ bWC,
     const float* __restrict__ WD, const float* __restrict__ bD, float* __restrict__ XR) {
+  constexpr int PW = TR * L66 + 2 * TR * L34 + 2 * TR;  // Raw (then XL staging), Tt (t, then XR), So (SA), MS, RS
   __shared__ float WAt[FP * L48];               // WAt[k][j] = W_A[j][k]
   __shared__ float WBt[FP * L80];               // WBt[k][o] = W_B[o][k]
   __shared__ float WCt[HC ? FP * L48 : 1];      // WCt[k][j] = W_C[j][k]
   __shared__ float WDt[HC ? FA * L48 : 1];      // WDt[k][j] = W_D[j][k]
   __shared__ float GB[4 * FP];                  // gamma_A beta_A gamma_C beta_C
-  __shared__ float tiles[kWaves][TR * L66 + TR * L34 + 2 * TR];
+  __shared__ float tiles[kWaves * PW];
   for (int q = threadIdx.x; q < FA * FP; q += kThreads) WAt[(q % FP) * L48 + q / FP] = WA[q];
   for (int q = threadIdx.x; q < FP * FP; q += kThreads) WBt[(q % FP) * L80 + q / FP] = WB[q];
   if (HC) {
@@ -409,9 +395,10 @@ __global__ __launch_bounds__(kThreads) void point_hub_fwd_kernel(
   __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
-  float* Raw = tiles[wave];
+  float* Raw = tiles + wave * PW;
   float* Tt = Raw + TR * L66;
-  float* MS = Tt + TR * L34;
+  float* So = Tt + TR * L34;
+  float* MS = So + TR * L34;
   float* RS = MS + TR;
   float bBv[4], bCv[2], bDv[2];
 #pragma unroll
@@ -426,7 +413,12 @@ __global__ __launch_bounds__(kThreads) void point_hub_fwd_kernel(
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row0 = t * TR;
     const int nrows = int(N - row0 < TR ? N - row0 : TR);
-    load_rows_stats(X, row0, nrows, eps, Raw, MS, RS, lane);
+    {
+      float4 vx[4];
+      rows_load<FP>(X, FP, row0, nrows, vx, lane);
+      row_stats64(vx, eps, MS, RS, lane);
+      rows_to_lds<FP, L66>(Raw, vx, lane);
+    }
     wave_sync();
     const float mi = MS[c], ri = RS[c];
     f32x4 accB[4] = {zero4(), zero4(), zero4(), zero4()}, accA[2] = {zero4(), zero4()}, accC[2] = {zero4(), zero4()};
@@ -446,40 +438,45 @@ __global__ __launch_bounds__(kThreads) void point_hub_fwd_kernel(
         for (int nt = 0; nt < 2; ++nt) accC[nt] = mfma16(pc, WCt[k * L48 + nt * 16 + c], accC[nt]);
       }
     }
+    wave_sync();  // Raw reads done: it becomes the XL staging tile
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int e = 4 * g + r;
-      if (e < nrows) {
-        float* xl = XL + (row0 + e) * FP;
-        float* sa = SA + (row0 + e) * FA;
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) xl[nt * 16 + c] = accB[nt][r] + bBv[nt];
+      for (int nt = 0; nt < 4; ++nt) Raw[e * L66 + nt * 16 + c] = accB[nt][r] + bBv[nt];
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) sa[nt * 16 + c] = accA[nt][r];
-      }
-      if (HC) {
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) Tt[e * L34 + nt * 16 + c] = accC[nt][r] + bCv[nt];
+      for (int nt = 0; nt < 2; ++nt) {
+        So[e * L34 + nt * 16 + c] = accA[nt][r];
+        if (HC) Tt[e * L34 + nt * 16 + c] = accC[nt][r] + bCv[nt];
       }
     }
+    wave_sync();
+    f32x4 accD[2] = {zero4(), zero4()};
     if (HC) {
-      wave_sync();
-      f32x4 accD[2] = {zero4(), zero4()};
 #pragma unroll
       for (int s = 0; s < FA / 4; ++s) {
         const float a = Tt[c * L34 + 4 * s + g];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) accD[nt] = mfma16(a, WDt[(4 * s + g) * L48 + nt * 16 + c], accD[nt]);
       }
+    }
+    {
+      float4 vl[4], vs[2];
+      rows_from_lds<FP, L66>(Raw, vl, lane);
+      rows_from_lds<FA, L34>(So, vs, lane);
+      rows_store<FP>(XL, FP, row0, nrows, vl, lane);
+      rows_store<FA>(SA, FA, row0, nrows, vs, lane);
+    }
+    if (HC) {
+      wave_sync();  // t reads done: Tt becomes the XR staging tile
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int e = 4 * g + r;
-        if (e < nrows) {
-          float* xr = XR + (row0 + e) * FA;
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt) xr[nt * 16 + c] = accD[nt][r] + bDv[nt];
-        }
-      }
+        for (int nt = 0; nt < 2; ++nt) Tt[(4 * g + r) * L34 + nt * 16 + c] = accD[nt][r] + bDv[nt];
+      wave_sync();
+      float4 vr[2];
+      rows_from_lds<FA, L34>(Tt, vr, lane);
+      rows_store<FA>(XR, FA, row0, nrows, vr, lane);
     }
     wave_sync();
   }
@@ -489,7 +486,8 @@ __global__ __launch_bounds__(kThreads) void point_hub_fwd_kernel(
 //   C pass:  dq = dRes + LN_C_bwd(mask (dt W_C)),  dt = dXR W_D       partials HC_* layout
 //   AB pass: dp = dq + dXL W_B + LN_A_bwd(mask (dSA W_A))               partials HA_* layout
 // (one pass would hold 144 weight-gradient accumulators and spill at 2 waves per SIMD; the
-// split costs one extra write + read of dq).
+// split costs one extra write + read of dq).  dX may alias dRes: a tile's dRes rows are in LDS
+// before any of its dX rows is stored.
 constexpr int HA_WA = 0, HA_WB = HA_WA + FA * FP, HA_BB = HA_WB + FP * FP, HA_GA = HA_BB + FP, HA_BA = HA_GA + FP,
               HA_PART = HA_BA + FP;
 constexpr int HC_WC = 0, HC_WD = HC_WC + FA * FP, HC_BC = HC_WD + FA * FA, HC_BD = HC_BC + FA, HC_GC = HC_BD + FA,
@@ -499,9 +497,8 @@ template <bool HR>
 __global__ __launch_bounds__(kThreads8) void point_hub_bwd_ab_kernel(
     const float* __restrict__ X, int64_t N, float eps, const float* __restrict__ gA, const float* __restrict__ bA,
     const float* __restrict__ WA, const float* __restrict__ WB, const float* __restrict__ dSA,
-    const float* __restrict__ dXL, const float* __restrict__ dRes, float* __restrict__ dX,
-    float* __restrict__ part) {
-  constexpr int PW = TR * L66 + 2 * TR;  // Raw, MS, RS
+    const float* __restrict__ dXL, const float* dRes, float* dX, float* __restrict__ part) {
+  constexpr int PW = 3 * TR * L66 + TR * L34 + 2 * TR;  // Raw, XLt (dXL), DXo (dRes, then dX), SAt (dSA), MS, RS
   constexpr int NRED = 96 + 12;
   static_assert(NRED * kW <= kWaves8 * PW, "reduction scratch");
   __shared__ float WAl[FA * L80];        // W_A [32 x 64] row-major
@@ -518,7 +515,10 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_ab_kernel(
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
   float* Raw = tiles + wave * PW;
-  float* MS = Raw + TR * L66;
+  float* XLt = Raw + TR * L66;
+  float* DXo = XLt + TR * L66;
+  float* SAt = DXo + TR * L66;
+  float* MS = SAt + TR * L34;
   float* RS = MS + TR;
   f32x4 dWA[2][4], dWB[4][4];
 #pragma unroll
@@ -533,10 +533,21 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_ab_kernel(
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row0 = t * TR;
     const int nrows = int(N - row0 < TR ? N - row0 : TR);
-    load_rows_stats(X, row0, nrows, eps, Raw, MS, RS, lane);
+    {
+      float4 vx[4], vl[4], vs[2], vr[4];
+      rows_load<FP>(X, FP, row0, nrows, vx, lane);
+      rows_load<FP>(dXL, FP, row0, nrows, vl, lane);
+      rows_load<FA>(dSA, FA, row0, nrows, vs, lane);
+      if (HR) rows_load<FP>(dRes, FP, row0, nrows, vr, lane);
+      row_stats64(vx, eps, MS, RS, lane);
+      rows_to_lds<FP, L66>(Raw, vx, lane);
+      rows_to_lds<FP, L66>(XLt, vl, lane);
+      rows_to_lds<FA, L34>(SAt, vs, lane);
+      if (HR) rows_to_lds<FP, L66>(DXo, vr, lane);
+    }
     wave_sync();
-    // weight gradients over the tile's rows (row = 4s + g; rows past nrows: dSA, dXL read as 0)
-#pragma unroll
+    // weight gradients over the tile's rows (row = 4s + g; rows past nrows: dSA, dXL are 0)
+#pragma unroll 1
     for (int s = 0; s < TR / 4; ++s) {
       const int row = 4 * s + g;
       const float mr = MS[row], rr = RS[row];
@@ -548,13 +559,13 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_ab_kernel(
       }
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
-        const float a = ld_a(dSA, FA, row0, nrows, row, mt * 16 + c);
+        const float a = SAt[row * L34 + mt * 16 + c];
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) dWA[mt][nt] = mfma16(a, pa[nt], dWA[mt][nt]);
       }
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
-        const float a = ld_a(dXL, FP, row0, nrows, row, mt * 16 + c);
+        const float a = XLt[row * L66 + mt * 16 + c];
         dbB[mt] += a;
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) dWB[mt][nt] = mfma16(a, xr[nt], dWB[mt][nt]);
@@ -564,13 +575,13 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_ab_kernel(
     f32x4 dxb[4] = {zero4(), zero4(), zero4(), zero4()}, dp[4] = {zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
     for (int s = 0; s < FP / 4; ++s) {
-      const float a = ld_a(dXL, FP, row0, nrows, c, 4 * s + g);
+      const float a = XLt[c * L66 + 4 * s + g];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) dxb[nt] = mfma16(a, WBl[(4 * s + g) * L80 + nt * 16 + c], dxb[nt]);
     }
 #pragma unroll
     for (int s = 0; s < FA / 4; ++s) {
-      const float a = ld_a(dSA, FA, row0, nrows, c, 4 * s + g);
+      const float a = SAt[c * L34 + 4 * s + g];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) dp[nt] = mfma16(a, WAl[(4 * s + g) * L80 + nt * 16 + c], dp[nt]);
     }
@@ -589,12 +600,17 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_ab_kernel(
       for (int nt = 0; nt < 4; ++nt) xh[nt] = (Raw[e * L66 + nt * 16 + c] - me) * re;
       const float dh[4] = {dp[0][r], dp[1][r], dp[2][r], dp[3][r]};
       ln_relu_bwd_row(xh, dh, gc, bc, re, dgA, dbA, t1);
-      if (e < nrows) {
-        float* d = dX + (row0 + e) * FP;
-        const float* dr = dRes + (row0 + e) * FP;
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) d[nt * 16 + c] = dxb[nt][r] + t1[nt] + (HR ? dr[nt * 16 + c] : 0.f);
+      for (int nt = 0; nt < 4; ++nt) {
+        float* d = DXo + e * L66 + nt * 16 + c;
+        *d = dxb[nt][r] + t1[nt] + (HR ? *d : 0.f);
       }
+    }
+    wave_sync();
+    {
+      float4 vo[4];
+      rows_from_lds<FP, L66>(DXo, vo, lane);
+      rows_store<FP>(dX, FP, row0, nrows, vo, lane);
     }
     wave_sync();
   }
@@ -645,9 +661,9 @@ template <bool HR>
 __global__ __launch_bounds__(kThreads8) void point_hub_bwd_c_kernel(
     const float* __restrict__ X, int64_t N, float eps, const float* __restrict__ gC, const float* __restrict__ bC,
     const float* __restrict__ WC, const float* __restrict__ bWC, const float* __restrict__ WD,
-    const float* __restrict__ dXR, const float* __restrict__ dRes, float* __restrict__ dX,
-    float* __restrict__ part) {
-  constexpr int PW = TR * L66 + 2 * TR * L34 + 2 * TR;  // Raw, Dt (dt), Tt (t), MS, RS
+    const float* __restrict__ dXR, const float* dRes, float* dX, float* __restrict__ part) {
+  // per wave: Raw, DXo (dRes, then dX), XRt (dXR), Dt (dt), Tt (t), MS, RS
+  constexpr int PW = 2 * TR * L66 + 3 * TR * L34 + 2 * TR;
   constexpr int NRED = 48 + 12;
   static_assert(NRED * kW <= kWaves8 * PW, "reduction scratch");
   __shared__ float WCl[FA * L80];        // W_C [32 x 64]
@@ -668,7 +684,9 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_c_kernel(
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
   float* Raw = tiles + wave * PW;
-  float* Dt = Raw + TR * L66;
+  float* DXo = Raw + TR * L66;
+  float* XRt = DXo + TR * L66;
+  float* Dt = XRt + TR * L34;
   float* Tt = Dt + TR * L34;
   float* MS = Tt + TR * L34;
   float* RS = MS + TR;
@@ -686,7 +704,16 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_c_kernel(
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row0 = t * TR;
     const int nrows = int(N - row0 < TR ? N - row0 : TR);
-    load_rows_stats(X, row0, nrows, eps, Raw, MS, RS, lane);
+    {
+      float4 vx[4], vq[2], vr[4];
+      rows_load<FP>(X, FP, row0, nrows, vx, lane);
+      rows_load<FA>(dXR, FA, row0, nrows, vq, lane);
+      if (HR) rows_load<FP>(dRes, FP, row0, nrows, vr, lane);
+      row_stats64(vx, eps, MS, RS, lane);
+      rows_to_lds<FP, L66>(Raw, vx, lane);
+      rows_to_lds<FA, L34>(XRt, vq, lane);
+      if (HR) rows_to_lds<FP, L66>(DXo, vr, lane);
+    }
     wave_sync();
     const float mi = MS[c], ri = RS[c];
     // t = W_C relu(LN_C p) + b_C (recomputed), dt = dXR W_D
@@ -700,7 +727,7 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_c_kernel(
     }
 #pragma unroll
     for (int s = 0; s < FA / 4; ++s) {
-      const float a = ld_a(dXR, FA, row0, nrows, c, 4 * s + g);
+      const float a = XRt[c * L34 + 4 * s + g];
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) da[nt] = mfma16(a, WDl[(4 * s + g) * L48 + nt * 16 + c], da[nt]);
     }
@@ -728,7 +755,7 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_c_kernel(
         dbC[mt] += a;
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) dWC[mt][nt] = mfma16(a, pc[nt], dWC[mt][nt]);
-        const float a2 = ld_a(dXR, FA, row0, nrows, row, mt * 16 + c);
+        const float a2 = XRt[row * L34 + mt * 16 + c];
         dbD[mt] += a2;
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) dWD[mt][nt] = mfma16(a2, tt[nt], dWD[mt][nt]);
@@ -757,12 +784,17 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_c_kernel(
       for (int nt = 0; nt < 4; ++nt) xh[nt] = (Raw[e * L66 + nt * 16 + c] - me) * re;
       const float dh[4] = {dp[0][r], dp[1][r], dp[2][r], dp[3][r]};
       ln_relu_bwd_row(xh, dh, gc, bc, re, dgC, dbCl, t1);
-      if (e < nrows) {
-        float* d = dX + (row0 + e) * FP;
-        const float* dr = dRes + (row0 + e) * FP;
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) d[nt * 16 + c] = t1[nt] + (HR ? dr[nt * 16 + c] : 0.f);
+      for (int nt = 0; nt < 4; ++nt) {
+        float* d = DXo + e * L66 + nt * 16 + c;
+        *d = t1[nt] + (HR ? *d : 0.f);
       }
+    }
+    wave_sync();
+    {
+      float4 vo[4];
+      rows_from_lds<FP, L66>(DXo, vo, lane);
+      rows_store<FP>(dX, FP, row0, nrows, vo, lane);
     }
     wave_sync();
   }

@@ -2,13 +2,15 @@
 //
 // A wavefront (64 lanes) owns a 16-row tile at a time.  GEMM-shaped parts use the exact-fp32
 // MFMA v_mfma_f32_16x16x4_f32 with lane l holding A[i = l&15][k = l>>4], B[k = l>>4][j = l&15]
-// and C[row = 4(l>>4) + r][col = l&15] (r = 0..3).  Row reductions over a 16-lane group use
-// xor-shuffles 1,2,4,8; reductions across the four lane groups use xor 16, 32.
+// and C[row = 4(l>>4) + r][col = l&15] (r = 0..3).  Row reductions over a 16-lane group are
+// DPP butterflies (lanes.hpp); reductions across the four lane groups use xor 16, 32.
 #pragma once
 
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+
+#include "lanes.hpp"
 
 namespace gasfm {
 namespace tile {
@@ -30,13 +32,7 @@ __device__ __forceinline__ void wave_sync() {
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
 // Sum over the 16 lanes of a lane group (same l>>4).
-__device__ __forceinline__ float sum16(float v) {
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
-  v += __shfl_xor(v, 8);
-  return v;
-}
+__device__ __forceinline__ float sum16(float v) { return group_sum<16>(v); }
 // Sum over the 4 lane groups (l>>4).
 __device__ __forceinline__ float sum_groups(float v) {
   v += __shfl_xor(v, 16);
@@ -71,6 +67,52 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ X, int64_t l
     d[1] = v[u].y;
     d[2] = v[u].z;
     d[3] = v[u].w;
+  }
+}
+
+// Row layout of a 16 x W tile (W = 32 or 64): lane l holds the float4 chunk l % (W/4) of rows
+// l / (W/4) + (64 / (W/4)) * u, u < W/16 -- every load / store is a coalesced 16-byte access.
+// rows_load issues all of a tile's loads before any use (clamped rows, zeroed past nrows).
+template <int W>
+__device__ __forceinline__ void rows_load(const float* __restrict__ P, int64_t ld, int64_t row0, int nrows,
+                                          float4 (&v)[W / 16], int lane) {
+  constexpr int V = W / 4, RS = kW / V;
+#pragma unroll
+  for (int u = 0; u < W / 16; ++u) {
+    const int r = lane / V + RS * u;
+    v[u] = *reinterpret_cast<const float4*>(P + (row0 + (r < nrows ? r : 0)) * ld + (lane % V) * 4);
+    if (r >= nrows) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+template <int W>
+__device__ __forceinline__ void rows_store(float* __restrict__ P, int64_t ld, int64_t row0, int nrows,
+                                           const float4 (&v)[W / 16], int lane) {
+  constexpr int V = W / 4, RS = kW / V;
+#pragma unroll
+  for (int u = 0; u < W / 16; ++u) {
+    const int r = lane / V + RS * u;
+    if (r < nrows) *reinterpret_cast<float4*>(P + (row0 + r) * ld + (lane % V) * 4) = v[u];
+  }
+}
+// LDS side (row stride LD, even: 8-byte aligned float2 accesses)
+template <int W, int LD>
+__device__ __forceinline__ void rows_to_lds(float* T, const float4 (&v)[W / 16], int lane) {
+  constexpr int V = W / 4, RS = kW / V;
+#pragma unroll
+  for (int u = 0; u < W / 16; ++u) {
+    float2* d = reinterpret_cast<float2*>(T + (lane / V + RS * u) * LD + (lane % V) * 4);
+    d[0] = make_float2(v[u].x, v[u].y);
+    d[1] = make_float2(v[u].z, v[u].w);
+  }
+}
+template <int W, int LD>
+__device__ __forceinline__ void rows_from_lds(const float* T, float4 (&v)[W / 16], int lane) {
+  constexpr int V = W / 4, RS = kW / V;
+#pragma unroll
+  for (int u = 0; u < W / 16; ++u) {
+    const float2* s = reinterpret_cast<const float2*>(T + (lane / V + RS * u) * LD + (lane % V) * 4);
+    const float2 a = s[0], b = s[1];
+    v[u] = make_float4(a.x, a.y, b.x, b.y);
   }
 }
 
