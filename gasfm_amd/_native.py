@@ -58,6 +58,16 @@ _SIGS = {
     "gasfm_gvec_bwd": (_i32, [_vp, _vp, _i32, _vp, _vp, _f32, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_node_ln_linear_fwd": (_i32, [_vp, _i64, _i32, _vp, _vp, _f32, _vp, _vp, _i32, _i32, _vp, _i64, _vp]),
     "gasfm_node_ln_linear_bwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp, _f32, _vp, _i32, _i32, _vp, _vp, _vp]),
+    "gasfm_view_tail_part_cols": (_i32, [_i32]),
+    "gasfm_view_hub_part_cols": (_i32, [_i32]),
+    "gasfm_view_scratch_floats": (_i64, [_i64, _i32]),
+    "gasfm_view_tail_fwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _vp]),
+    "gasfm_view_tail_bwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_view_hub_fwd": (_i32, [_vp, _i64, _i32, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  _vp, _vp, _vp, _vp]),
+    "gasfm_view_hub_bwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  _vp, _vp, _vp, _vp]),
     "gasfm_point_tail_part_shape": (_i32, [_i64, _i32, _vp]),
     "gasfm_point_hub_part_shape": (_i32, [_i64, _i32, _i32, _vp]),
     "gasfm_point_tail_fwd": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
@@ -394,3 +404,54 @@ def point_hub_bwd_ab(X, eps, gA, bA, WA, WB, dSA, dXL, dRes, dX, part):
     st = lib().gasfm_point_hub_bwd_ab(_p(X), X.shape[0], eps, _p(gA), _p(bA), _p(WA), _p(WB), _p(dSA), _p(dXL),
                                       _p(dRes), _p(dX), _p(part), _stream(X))
     check(st, "gasfm_point_hub_bwd_ab")
+
+
+# ---------------------------------------------------------------- camera-side block chains (view_block.hip)
+def view_tail_part_cols(D):
+    return lib().gasfm_view_tail_part_cols(D)
+
+
+def view_hub_part_cols(D):
+    return lib().gasfm_view_hub_part_cols(D)
+
+
+def view_scratch(m, D, device):
+    return torch.empty(max(1, int(lib().gasfm_view_scratch_floats(m, D))), dtype=torch.float32, device=device)
+
+
+def view_tail_fwd(prev, agg, Wp, bp, ln_w, ln_b, eps, bm, x, xb, h, rs, scratch):
+    _req(agg, "agg", 32)
+    D = x.shape[1]
+    if prev is not None:
+        _req(prev, "prev", D)
+    st = lib().gasfm_view_tail_fwd(_p(prev), _p(agg), agg.shape[0], D, _p(Wp), _p(bp), _p(ln_w), _p(ln_b), eps,
+                                   _p(bm), _p(x), _p(xb), _p(h), _p(rs), _p(scratch), _stream(agg))
+    check(st, "gasfm_view_tail_fwd")
+
+
+def view_tail_bwd(dv, dh, x, rs, agg, Wp, ln_w, ln_b, dx, dagg, part, scratch):
+    D = x.shape[1]
+    for t, n in ((dv, "dv"), (dh, "dh"), (x, "x")):
+        _req(t, n, D)
+    _req(agg, "agg", 32)
+    st = lib().gasfm_view_tail_bwd(_p(dv), _p(dh), _p(x), _p(rs), _p(agg), agg.shape[0], D, _p(Wp), _p(ln_w),
+                                   _p(ln_b), _p(dx), _p(dagg), _p(part), _p(scratch), _stream(agg))
+    check(st, "gasfm_view_tail_bwd")
+
+
+def view_hub_fwd(v, eps, gC, bC, Wv, gA, bA, Wa, ba, Wr, br, sv, t, xr, rs, scratch):
+    _req(v, "v")
+    st = lib().gasfm_view_hub_fwd(_p(v), v.shape[0], v.shape[1], eps, _p(gC), _p(bC), _p(Wv), _p(gA), _p(bA), _p(Wa),
+                                  _p(ba), _p(Wr), _p(br), _p(sv), _p(t), _p(xr), _p(rs), _p(scratch), _stream(v))
+    check(st, "gasfm_view_hub_fwd")
+
+
+def view_hub_bwd(v, rs, gC, bC, Wv, gA, bA, Wa, t, Wr, dsv, dxr, dxl, dacc, part, scratch):
+    _req(v, "v")
+    D = v.shape[1]
+    for a, n, w in ((t, "t", 32), (dsv, "dsv", 32), (dxr, "dxr", 32), (dxl, "dxl", D), (dacc, "dacc", D)):
+        _req(a, n, w)
+    st = lib().gasfm_view_hub_bwd(_p(v), _p(rs), v.shape[0], D, _p(gC), _p(bC), _p(Wv), _p(gA), _p(bA), _p(Wa),
+                                  _p(t), _p(Wr), _p(dsv), _p(dxr), _p(dxl), _p(dacc), _p(part), _p(scratch),
+                                  _stream(v))
+    check(st, "gasfm_view_hub_bwd")

@@ -25,7 +25,7 @@ import torch
 import torch.nn.functional as F
 from torch.nn import Identity, LayerNorm, Linear, Module, ModuleList, ReLU, Sequential
 
-from . import dense, edge_ops, point_block
+from . import dense, edge_ops, point_block, view_block
 from .attention import AttnPlan, gat_attention
 from .edge_block import Block0EpilogueFn, Block0PrologueFn, DualAttentionFn, EdgeEpilogueFn, EdgePrologueFn
 from .gatv2 import GATv2Conv
@@ -130,6 +130,8 @@ class _NodeAggregation(Module):
         """Everything after the GATv2 aggregation: proj, state skip, LN+ReLU, MLP, skip."""
         if point_block.tail_fusable(self, x, prev):
             return point_block.tail(self, x, prev)
+        if view_block.tail_fusable(self, x, prev):
+            return view_block.tail(self, x, prev)
         if self.n_feat_agg != self.n_feat_out:
             x = dense.linear(x, getattr(self, self._proj_key))
         if prev is not None:
@@ -188,12 +190,19 @@ class ViewAndScenePoint2Global(Module):
             self.norm_pre_mlp = LayerNorm(n_feat_global_out)
         self.mlp = get_linear_layers((2 + n_hidden_layers_global_update) * [n_feat_global_out], norm=False)
 
-    def forward_plan(self, view, pts, plan_v2g, plan_s2g, prev, plan_s2g_partial=None, shard=None, xl_pts=None):
-        """xl_pts: graph_conv_scenepoint2global.lin_l(pts) when already computed (PointHubFn)."""
+    def forward_plan(self, view, pts, plan_v2g, plan_s2g, prev, plan_s2g_partial=None, shard=None, xl_pts=None,
+                     xl_view=None):
+        """xl_pts / xl_view: the convs' lin_l(pts) / lin_l(view) when already computed (hubs)."""
         assert self.stateful == (prev is not None)
         xv = dense.sequential(self.norm_and_proj_global2view, prev) if prev is not None else None
         xp = dense.sequential(self.norm_and_proj_global2scenepoint, prev) if prev is not None else None
-        v2g = self.graph_conv_view2global.attend(view, xv, plan_v2g)
+        cv = self.graph_conv_view2global
+        if xl_view is not None:
+            XRv = cv.lin_r(torch.zeros((1, cv.in_channels), device=view.device)).expand(1, -1) if xv is None \
+                else dense.linear(xv, cv.lin_r)
+            v2g = gat_attention(xl_view, XRv, cv.att, cv._bias(xl_view), plan_v2g, cv.heads, cv.negative_slope)
+        else:
+            v2g = cv.attend(view, xv, plan_v2g)
         c = self.graph_conv_scenepoint2global
         if shard is None and xl_pts is not None:
             XR = c.lin_r(torch.zeros((1, c.in_channels), device=pts.device)).expand(1, -1) if xp is None \
@@ -323,10 +332,11 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         """Node side of the update given XL = [lin_l_point(P_hat) | lin_l_camera(P_hat)] [E, 64]
         (point half in point-segment order when xl_sorted).
 
-        carry: per-forward dict through which PointHubFn hands the next block its point target
-        rows ("XRp") and state skip ("pts_skip"), and this block its "SA" / "XLs2g" terms;
-        pfu / nxt: this block's projection-feature update and the next Proj2ScenePoint (the
-        hub's consumers), None where there is no next consumer."""
+        carry: per-forward dict through which PointHubFn / ViewHubFn hand the next block its
+        target rows ("XRp", "XRc") and state skips ("pts_skip", "view_skip"), and this block its
+        "SA" / "SV" / "XLs2g" / "XLv2g" terms; pfu / nxt: this block's projection-feature update
+        and the next block's (or the final) GraphAttnSfMGlobalFeatureUpdate, whose Proj2ScenePoint
+        and Proj2View are the hubs' next-block consumers (None: no next consumer)."""
         sp, sv = self.proj2scenepoint, self.proj2view
         pp, pc = plans["proj2scenepoint"], plans["proj2view"]
         shard = plans.get("_shard")
@@ -334,18 +344,27 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
             XRp, prev_pt = carry.pop("XRp"), carry.pop("pts_skip")
         else:
             XRp = sp.target_rows(prev_pt, pp.num_targets)
-        XRc = replicated_to_local(sv.target_rows(prev_view, pc.num_targets), shard)
+        if carry is not None and "XRc" in carry:
+            XRc, prev_view = carry.pop("XRc"), carry.pop("view_skip")
+        else:
+            XRc = sv.target_rows(prev_view, pc.num_targets)
+        XRc = replicated_to_local(XRc, shard)
         cp, cc = sp.graph_conv, sv.graph_conv
         agg_p, agg_c = DualAttentionFn.apply(XL, XRp, XRc, cp.att, cc.att, cp.bias, cc.bias, pp, pc, cp.heads,
                                              cp.negative_slope, plans.get("_partial", {}).get("proj2view"), shard,
                                              xl_sorted)
         pts = sp.tail(agg_p, prev_pt)
-        if carry is not None and self.output_global:
-            hp = point_block.hub_params(pfu, self.view_and_scenepoint2global.graph_conv_scenepoint2global, nxt)
+        view = sv.tail(agg_c, prev_view)
+        if carry is not None and self.output_global and nxt is not None:
+            vsg = self.view_and_scenepoint2global
+            hp = point_block.hub_params(pfu, vsg.graph_conv_scenepoint2global, nxt.proj2scenepoint)
             if hp is not None and point_block._rows_ok(pts, point_block.P_W):
                 skip, SA, XLs, XRn = point_block.hub(pts, hp)
                 carry.update(XRp=XRn, pts_skip=skip, SA=SA, XLs2g=XLs)
-        view = sv.tail(agg_c, prev_view)
+            hv = view_block.hub_params(pfu, vsg.graph_conv_view2global, nxt.proj2view)
+            if hv is not None and view_block._rows_ok(view, view.shape[1]):
+                skip, SV, XLv, XRn = view_block.hub(view, hv)
+                carry.update(XRc=XRn, view_skip=skip, SV=SV, XLv2g=XLv)
         return self._finish(pts, view, plans, prev_glob, carry)
 
     def forward_plan(self, P_hat, plans, prev_pt=None, prev_view=None, prev_glob=None):
@@ -361,7 +380,8 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
             glob = self.view_and_scenepoint2global.forward_plan(
                 view, pts, plans["view2global"], plans["scenepoint2global"], prev_glob,
                 plans.get("_partial", {}).get("scenepoint2global"), plans.get("_shard"),
-                xl_pts=carry.pop("XLs2g", None) if carry is not None else None)
+                xl_pts=carry.pop("XLs2g", None) if carry is not None else None,
+                xl_view=carry.pop("XLv2g", None) if carry is not None else None)
         if self.global2view_and_global2scenepoint_enabled:
             pts = self.global2scenepoint(glob, pts)
             view = self.global2view(glob, view)
@@ -389,11 +409,11 @@ class GraphAttnSfMProjectionFeatureUpdate(Module):
             self.mlp = get_linear_layers(n_hidden_layers_proj_update * [n_feat_proj_out] + [n_feat_proj_out],
                                          norm=False)
 
-    def node_terms(self, pts, view, glob, sp=None):
-        """sp: the point term when PointHubFn already computed it."""
+    def node_terms(self, pts, view, glob, sp=None, sv=None):
+        """sp / sv: the point / view terms when PointHubFn / ViewHubFn already computed them."""
         if self.normalize_global_features:
             return (sp if sp is not None else dense.ln_relu_linear(pts, self.scenepoint_norm_layer, self.lin_scenepoint),
-                    dense.ln_relu_linear(view, self.view_norm_layer, self.lin_view),
+                    sv if sv is not None else dense.ln_relu_linear(view, self.view_norm_layer, self.lin_view),
                     dense.ln_relu_linear(glob, self.global_norm_layer, self.lin_global))
         return dense.linear(pts, self.lin_scenepoint), dense.linear(view, self.lin_view), \
             dense.linear(glob, self.lin_global)
@@ -465,7 +485,8 @@ class GraphAttnSfMLayer(Module):
         XL, token = Block0PrologueFn.apply(P.contiguous(), la.weight, la.bias, W, b, la.eps, pos)
         pts, view, glob = gfu.forward_fused(XL, plans, None, None, None, xl_sorted=pos is not None, carry=carry,
                                             pfu=pfu, nxt=nxt)
-        sp, sv, sg = pfu.node_terms(pts, view, glob, carry.pop("SA", None) if carry is not None else None)
+        sp, sv, sg = pfu.node_terms(pts, view, glob, *((carry.pop("SA", None), carry.pop("SV", None))
+                                                         if carry is not None else (None, None)))
         shard = plans.get("_shard")
         sv, sg = replicated_to_local(sv, shard), replicated_to_local(sg, shard)
         sk = self.skip_projection.lin_proj
@@ -483,7 +504,8 @@ class GraphAttnSfMLayer(Module):
         XL, token = EdgePrologueFn.apply(P, ln.weight, ln.bias, W, b, pfu.lin_proj.weight, ln.eps, pos)
         pts, view, glob = gfu.forward_fused(XL, plans, prev_pt, prev_view, prev_glob, xl_sorted=pos is not None,
                                             carry=carry, pfu=pfu, nxt=nxt)
-        sp, sv, sg = pfu.node_terms(pts, view, glob, carry.pop("SA", None) if carry is not None else None)
+        sp, sv, sg = pfu.node_terms(pts, view, glob, *((carry.pop("SA", None), carry.pop("SV", None))
+                                                         if carry is not None else (None, None)))
         shard = plans.get("_shard")
         sv, sg = replicated_to_local(sv, shard), replicated_to_local(sg, shard)
         P_new = EdgeEpilogueFn.apply(P, P0 if self.add_skipconn_from_init_projfeat else None, token, sp, sv, sg,
@@ -685,15 +707,15 @@ class GraphAttnSfMNet(Module):
         heads = self.view_head_enabled or self.scenepoint_head_enabled
         fgu = self.final_global_update if heads else None
         final_fused = fgu is not None and values.is_cuda and fgu.fusable() and self.equivariant_blocks[-1].fusable()
-        # consumers of each block's point output (PointHubFn): the next block's (or the fused
-        # final update's) Proj2ScenePoint; carry hands the hub outputs forward
+        # consumers of each block's node outputs (PointHubFn, ViewHubFn): the next block's (or
+        # the fused final update's) Proj2ScenePoint / Proj2View; carry hands the hub outputs forward
         carry = {} if (values.is_cuda and sf) else None
         blocks = list(self.equivariant_blocks)
         for i, blk in enumerate(blocks):
             if i + 1 < len(blocks):
-                nxt = blocks[i + 1].global_feature_update.proj2scenepoint if blocks[i + 1].fusable() else None
+                nxt = blocks[i + 1].global_feature_update if blocks[i + 1].fusable() else None
             else:
-                nxt = fgu.proj2scenepoint if final_fused else None
+                nxt = fgu if final_fused else None
             P, pts, view, glob = blk.forward_plan(P, plans, edges, pts if sf else None, view if sf else None,
                                                   glob if sf else None, P0=P0, carry=carry, nxt=nxt)
         if heads:

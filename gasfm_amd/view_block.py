@@ -1,0 +1,167 @@
+"""Camera (view) side of a GASFM block as two fused autograd Functions (csrc/view_block.hip).
+
+ViewTailFn -- the end of Proj2View.forward (reference code/models/layers.py:345-360):
+              x = prev + proj_proj2view(agg);  view = x + mlp(relu(norm_pre_mlp(x)))
+              one kernel for x / x + b_m / relu(LN(x)), one hipBLASLt GEMM (addmm) for mlp.
+ViewHubFn  -- every consumer of the block's view features, as PointHubFn does for points
+              (point_block.py): the identity skip to the next block, lin_view(relu(view_norm_layer)),
+              the next block's lin_r(norm_and_proj_view2proj(view)) (one kernel) and
+              graph_conv_view2global.lin_l (addmm).  Its backward is the only producer of d view:
+              addmm(d skip, dXL, W_l) then one kernel adding both LayerNorm branches in place.
+
+The two D x D GEMMs of the camera side (m = 1000 rows, D = 1024) stay on hipBLASLt through
+torch; everything around them -- LayerNorms, ReLUs, the 32-wide projections, residual adds,
+bias / LayerNorm-affine gradient reductions -- runs in the four kernels.
+"""
+import torch
+
+from . import _native
+
+A_W = 32
+WIDTHS = tuple(range(64, 1025, 64))  # D: a multiple of 64 (one wave per 64 columns), <= 1024
+TR = 16
+
+
+def _f32(*shape, like):
+    return torch.empty(shape, dtype=torch.float32, device=like.device)
+
+
+class ViewTailFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, prev, agg, Wp, bp, ln_w, ln_b, Wm, bm, eps):
+        agg = agg.contiguous()
+        prev = prev.contiguous() if prev is not None else None
+        Wp, Wm = Wp.contiguous(), Wm.contiguous()
+        m, D = agg.shape[0], Wp.shape[0]
+        x, xb, h = _f32(m, D, like=agg), _f32(m, D, like=agg), _f32(m, D, like=agg)
+        rs = _f32(m, 2, like=agg)
+        _native.view_tail_fwd(prev, agg, Wp, bp, ln_w, ln_b, eps, bm, x, xb, h, rs,
+                              _native.view_scratch(m, D, agg.device))
+        view = torch.addmm(xb, h, Wm.t())
+        ctx.save_for_backward(agg, x, rs, h, Wp, ln_w, ln_b, Wm)
+        ctx.eps, ctx.has_prev = eps, prev is not None
+        return view
+
+    @staticmethod
+    def backward(ctx, dview):
+        agg, x, rs, h, Wp, ln_w, ln_b, Wm = ctx.saved_tensors
+        m, D = x.shape
+        dview = dview.contiguous()
+        dh = dview @ Wm
+        dWm = dview.t() @ h
+        dx, dagg = _f32(m, D, like=x), _f32(m, A_W, like=x)
+        cols = _native.view_tail_part_cols(D)
+        if m == 0:
+            tot = torch.zeros(cols, dtype=torch.float32, device=x.device)
+        else:
+            part = _f32((m + TR - 1) // TR, cols, like=x)
+            _native.view_tail_bwd(dview, dh, x, rs, agg, Wp, ln_w, ln_b, dx, dagg, part,
+                                  _native.view_scratch(m, D, x.device))
+            tot = _native.colsum(part)
+        dWp = tot[:D * A_W].view(D, A_W)
+        dbp, dg, dbt, dbm = (tot[D * A_W + k * D:D * A_W + (k + 1) * D] for k in range(4))
+        return (dx if ctx.has_prev else None), dagg, dWp, dbp, dg, dbt, dWm, dbm, None
+
+
+class ViewHubFn(torch.autograd.Function):
+    """v -> (skip, SV, XL, XR)."""
+
+    @staticmethod
+    def forward(ctx, v, gC, bC, Wv, Wl, bl, gA, bA, Wa, ba, Wr, br, eps):
+        v = v.contiguous()
+        Wv, Wl, Wa, Wr = (w.contiguous() for w in (Wv, Wl, Wa, Wr))
+        m = v.shape[0]
+        SV, t, XR = _f32(m, A_W, like=v), _f32(m, A_W, like=v), _f32(m, A_W, like=v)
+        rs = _f32(m, 2, like=v)
+        _native.view_hub_fwd(v, eps, gC, bC, Wv, gA, bA, Wa, ba, Wr, br, SV, t, XR, rs,
+                             _native.view_scratch(m, v.shape[1], v.device))
+        XL = torch.addmm(bl, v, Wl.t())
+        ctx.save_for_backward(v, rs, t, gC, bC, Wv, Wl, gA, bA, Wa, Wr)
+        ctx.eps = eps
+        ctx.set_materialize_grads(False)
+        return v.view_as(v), SV, XL, XR
+
+    @staticmethod
+    def backward(ctx, dskip, dSV, dXL, dXR):
+        v, rs, t, gC, bC, Wv, Wl, gA, bA, Wa, Wr = ctx.saved_tensors
+        m, D = v.shape
+        zeros = lambda w: torch.zeros((m, w), dtype=torch.float32, device=v.device)  # noqa: E731
+        dSV = dSV.contiguous() if dSV is not None else zeros(A_W)
+        dXR = dXR.contiguous() if dXR is not None else zeros(A_W)
+        dXL = dXL.contiguous() if dXL is not None else zeros(D)
+        dacc = torch.addmm(dskip, dXL, Wl) if dskip is not None else dXL @ Wl
+        dWl = dXL.t() @ v
+        cols = _native.view_hub_part_cols(D)
+        if m == 0:
+            tot = torch.zeros(cols, dtype=torch.float32, device=v.device)
+        else:
+            part = _f32((m + TR - 1) // TR, cols, like=v)
+            _native.view_hub_bwd(v, rs, gC, bC, Wv, gA, bA, Wa, t, Wr, dSV, dXR, dXL, dacc, part,
+                                 _native.view_scratch(m, D, v.device))
+            tot = _native.colsum(part)
+        o = 0
+        dWv = tot[o:o + A_W * D].view(A_W, D)
+        o += A_W * D
+        dWa = tot[o:o + A_W * D].view(A_W, D)
+        o += A_W * D
+        dgC, dbC, dgA, dbA, dbl = (tot[o + k * D:o + (k + 1) * D] for k in range(5))
+        o += 5 * D
+        dWr = tot[o:o + A_W * A_W].view(A_W, A_W)
+        o += A_W * A_W
+        dba, dbr = tot[o:o + A_W], tot[o + A_W:o + 2 * A_W]
+        return dacc, dgC, dbC, dWv, dWl, dbl, dgA, dbA, dWa, dba, dWr, dbr, None
+
+
+def _is_ln(mod, w):
+    return isinstance(mod, torch.nn.LayerNorm) and tuple(mod.normalized_shape) == (w,) and mod.weight is not None \
+        and mod.bias is not None
+
+
+def _is_lin(mod, i, o, bias):
+    return isinstance(mod, torch.nn.Linear) and mod.in_features == i and mod.out_features == o \
+        and ((mod.bias is not None) == bias)
+
+
+def _rows_ok(t, w):
+    return t is not None and t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.shape[1] == w
+
+
+def tail_fusable(agg_mod, x, prev):
+    """Proj2View with 32-wide aggregation, D-wide views (D in WIDTHS), norm_pre_mlp and a
+    one-Linear mlp."""
+    D = agg_mod.n_feat_out
+    if D not in WIDTHS or not (_rows_ok(x, A_W) and (prev is None or _rows_ok(prev, D))):
+        return False
+    proj = getattr(agg_mod, agg_mod._proj_key, None) if agg_mod.n_feat_agg != D else None
+    return (proj is not None and _is_lin(proj, A_W, D, True) and agg_mod.use_norm_pre_mlp
+            and _is_ln(agg_mod.norm_pre_mlp, D) and len(agg_mod.mlp) == 1 and _is_lin(agg_mod.mlp[0], D, D, True))
+
+
+def tail(agg_mod, x, prev):
+    proj = getattr(agg_mod, agg_mod._proj_key)
+    ln, lin = agg_mod.norm_pre_mlp, agg_mod.mlp[0]
+    return ViewTailFn.apply(prev, x, proj.weight, proj.bias, ln.weight, ln.bias, lin.weight, lin.bias, ln.eps)
+
+
+def hub_params(pfu, v2g_conv, nxt):
+    """(gC, bC, Wv, Wl, bl, gA, bA, Wa, ba, Wr, br, eps) or None when the shapes do not match.
+
+    pfu: this block's projection-feature update (view_norm_layer, lin_view); v2g_conv: this
+    block's graph_conv_view2global; nxt: the next Proj2View (norm_and_proj_view2proj, lin_r)."""
+    if pfu is None or v2g_conv is None or nxt is None or not pfu.normalize_global_features or not nxt.stateful:
+        return None
+    lnC, linV = pfu.view_norm_layer, pfu.lin_view
+    D = linV.in_features
+    seq = getattr(nxt, nxt._state_key, None)
+    if D not in WIDTHS or seq is None or len(seq) != 3:
+        return None
+    lnA, linA, linR, linL = seq[0], seq[2], nxt.graph_conv.lin_r, v2g_conv.lin_l
+    if not (_is_ln(lnC, D) and _is_lin(linV, D, A_W, False) and _is_lin(linL, D, D, True) and _is_ln(lnA, D)
+            and _is_lin(linA, D, A_W, True) and _is_lin(linR, A_W, A_W, True) and lnA.eps == lnC.eps):
+        return None
+    return (lnC.weight, lnC.bias, linV.weight, linL.weight, linL.bias, lnA.weight, lnA.bias, linA.weight, linA.bias,
+            linR.weight, linR.bias, lnC.eps)
+
+
+def hub(v, params):
+    return ViewHubFn.apply(v, *params)

@@ -297,6 +297,47 @@ int gasfm_point_hub_bwd_ab(const float* X, int64_t N, float eps, const float* gA
                            const float* WA, const float* WB, const float* dSA, const float* dXL,
                            const float* dRes, float* dX, float* part, void* stream);
 
+/* ---- camera (view) block chains (m rows x D, D a multiple of 64, <= 1024) ----
+ * tail: Proj2View.forward after the aggregation (layers.py:345-360):
+ *   x = prev + Wp agg + bp;  view = x + Wm relu(LN(x)) + bm
+ *   gasfm_view_tail_fwd writes x, xb = x + bm, h = relu(LN(x)) and the row (mean, rstd) of x
+ *   (rs, m x 2); the caller's GEMM computes view = xb + h Wm^T (hipBLASLt).
+ * hub: SV = Wv relu(LN_c(v)) (lin_view, layers.py:928-935), T = Wa relu(LN_a(v)) + ba and
+ *   XR = Wr T + br (the next block's norm_and_proj_view2proj + lin_r), row (mean, rstd) of v;
+ *   the caller's GEMM computes graph_conv_view2global.lin_l(v).
+ * Every kernel runs one wave per (16-row tile, 64-column block); whole-row quantities cross the
+ * column blocks through `scratch` (gasfm_view_scratch_floats(m, D) floats, caller-allocated).
+ * Gradients of weights / biases / LayerNorm affines leave as one partial row per tile
+ * (ceil(m/16) rows) for gasfm_colsum. */
+
+/* Partial-row widths: tail [dWp D x 32 | dbp D | dgamma D | dbeta D | dbm D];
+ * hub [dWv 32 x D | dWa 32 x D | dgamma_c | dbeta_c | dgamma_a | dbeta_a | dbl (each D) |
+ *      dWr 32 x 32 | dba 32 | dbr 32]. */
+int gasfm_view_tail_part_cols(int32_t D);
+int gasfm_view_hub_part_cols(int32_t D);
+int64_t gasfm_view_scratch_floats(int64_t m, int32_t D);
+
+int gasfm_view_tail_fwd(const float* prev, const float* agg, int64_t m, int32_t D, const float* Wp, const float* bp,
+                        const float* ln_w, const float* ln_b, float eps, const float* bm, float* x, float* xb,
+                        float* h, float* rs, float* scratch, void* stream);
+
+/* dx = dv + LN_bwd(mask dh) (dh = dv Wm from the caller's GEMM; == d prev), dagg = dx Wp, partials. */
+int gasfm_view_tail_bwd(const float* dv, const float* dh, const float* x, const float* rs, const float* agg,
+                        int64_t m, int32_t D, const float* Wp, const float* ln_w, const float* ln_b, float* dx,
+                        float* dagg, float* part, float* scratch, void* stream);
+
+int gasfm_view_hub_fwd(const float* v, int64_t m, int32_t D, float eps, const float* gC, const float* bC,
+                       const float* Wv, const float* gA, const float* bA, const float* Wa, const float* ba,
+                       const float* Wr, const float* br, float* sv, float* t, float* xr, float* rs, float* scratch,
+                       void* stream);
+
+/* dacc (in: d skip + dXL Wl, out: d v) += LN_c_bwd(mask dsv Wv) + LN_a_bwd(mask dt Wa), dt = dxr Wr;
+ * dxl is read for the lin_l bias gradient; partials. */
+int gasfm_view_hub_bwd(const float* v, const float* rs, int64_t m, int32_t D, const float* gC, const float* bC,
+                       const float* Wv, const float* gA, const float* bA, const float* Wa, const float* t,
+                       const float* Wr, const float* dsv, const float* dxr, const float* dxl, float* dacc,
+                       float* part, float* scratch, void* stream);
+
 /* ---- global node (ONE row): LayerNorm -> ReLU -> Linear (+ residual) ----
  * Replaces the M = 1 aten chains on the global feature vector: norm_and_proj_global2view /
  * _global2scenepoint (layers.py:497-520), both convs' lin_r on those rows (PyG),
