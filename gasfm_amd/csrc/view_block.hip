@@ -363,16 +363,18 @@ __global__ __launch_bounds__(kW) void view_tail_b2_kernel(const float* __restric
     for (int nt = 0; nt < 2; ++nt) dst[(4 * g + r) * VA + nt * 16 + c] = da[nt][r];
 }
 
-// out[16 x 32 tile] = sum over column blocks of the partial products (block order); one wave
-// per tile
-__global__ __launch_bounds__(kW) void view_rows32_sum_kernel(const float* __restrict__ PPt, int64_t m, int ncb,
-                                                             float* __restrict__ out) {
-  const int lane = threadIdx.x;
+// out[16 x 32 tile] = sum over column blocks of the partial products (block order); one
+// 256-thread workgroup per tile, 2 outputs per thread, the block loads in flight together
+constexpr int kSumThreads = 256;
+__global__ __launch_bounds__(kSumThreads) void view_rows32_sum_kernel(const float* __restrict__ PPt, int64_t m,
+                                                                      int ncb, float* __restrict__ out) {
   const int64_t row0 = int64_t(blockIdx.x) * TR;
   const int nrows = int(m - row0 < TR ? m - row0 : TR);
-  for (int i = lane; i < TR * VA; i += kW) {
+  const float* src = PPt + int64_t(blockIdx.x) * ncb * TR * VA;
+  for (int i = threadIdx.x; i < TR * VA; i += kSumThreads) {
     float s = 0.f;
-    for (int b = 0; b < ncb; ++b) s += PPt[(int64_t(blockIdx.x) * ncb + b) * TR * VA + i];
+#pragma unroll 8
+    for (int b = 0; b < ncb; ++b) s += src[b * TR * VA + i];
     if (i / VA < nrows) out[(row0 + i / VA) * VA + i % VA] = s;
   }
 }
@@ -439,20 +441,22 @@ __global__ __launch_bounds__(kW) void view_hub_proj_kernel(
     }
 }
 
-// sv = sum_b S_b, t = sum_b T_b + b_a, XR = t W_r^T + b_r; one wave per tile
-__global__ __launch_bounds__(kW) void view_hub_fin_kernel(const float* __restrict__ PP, int64_t m, int ncb,
-                                                          const float* __restrict__ ba,
-                                                          const float* __restrict__ Wr,
-                                                          const float* __restrict__ br, float* __restrict__ sv,
-                                                          float* __restrict__ to, float* __restrict__ xr) {
+// sv = sum_b S_b, t = sum_b T_b + b_a (block order), XR = t W_r^T + b_r; one 256-thread
+// workgroup per tile (4 outputs per thread), wave 0 runs the W_r product
+__global__ __launch_bounds__(kSumThreads) void view_hub_fin_kernel(const float* __restrict__ PP, int64_t m, int ncb,
+                                                                   const float* __restrict__ ba,
+                                                                   const float* __restrict__ Wr,
+                                                                   const float* __restrict__ br,
+                                                                   float* __restrict__ sv, float* __restrict__ to,
+                                                                   float* __restrict__ xr) {
   __shared__ float Tt[TR * L34];
-  const int lane = threadIdx.x, c = lane & 15, g = lane >> 4;
   const int64_t row0 = int64_t(blockIdx.x) * TR;
   const int nrows = int(m - row0 < TR ? m - row0 : TR);
   const float* src = PP + int64_t(blockIdx.x) * ncb * 2 * TR * VA;
-  for (int i = lane; i < 2 * TR * VA; i += kW) {
+  for (int i = threadIdx.x; i < 2 * TR * VA; i += kSumThreads) {
     const int which = i / (TR * VA), j = i % (TR * VA), e = j / VA, n = j % VA;
     float s = 0.f;
+#pragma unroll 8
     for (int b = 0; b < ncb; ++b) s += src[(b * 2 + which) * TR * VA + j];
     if (which) {
       s += ba[n];
@@ -462,7 +466,9 @@ __global__ __launch_bounds__(kW) void view_hub_fin_kernel(const float* __restric
       sv[(row0 + e) * VA + n] = s;
     }
   }
-  wave_sync();
+  __syncthreads();
+  if (threadIdx.x >= kW) return;
+  const int lane = threadIdx.x, c = lane & 15, g = lane >> 4;
   f32x4 accR[2] = {zero4(), zero4()};
 #pragma unroll
   for (int q = 0; q < VA / 4; ++q) {
@@ -817,7 +823,7 @@ extern "C" int gasfm_view_tail_bwd(const float* dv, const float* dh, const float
   hipLaunchKernelGGL(view_tail_b1_kernel, grid2(m, D), dim3(kW), 0, st, dv, dh, x, m, D, RSx, ln_w, ln_b, RSUM, part);
   hipLaunchKernelGGL(view_tail_b2_kernel, grid2(m, D), dim3(kW), 0, st, dv, dh, x, agg, m, D, RSx, RSUM, Wp, ln_w,
                      ln_b, dx, DA, part);
-  hipLaunchKernelGGL(view_rows32_sum_kernel, grid1(m), dim3(kW), 0, st, DA, m, int(ncb), dagg);
+  hipLaunchKernelGGL(view_rows32_sum_kernel, grid1(m), dim3(kSumThreads), 0, st, DA, m, int(ncb), dagg);
   return launch_status("gasfm_view_tail_bwd");
 }
 
@@ -837,7 +843,7 @@ extern "C" int gasfm_view_hub_fwd(const float* v, int64_t m, int32_t D, float ep
   hipLaunchKernelGGL(view_stats_kernel, grid2(m, D), dim3(kW), 0, st, v, m, D, SP);
   hipLaunchKernelGGL(view_hub_proj_kernel, grid2(m, D), dim3(kW), 0, st, v, m, D, eps, SP, gC, bC, Wv, gA, bA, Wa,
                      PP, reinterpret_cast<float2*>(rs));
-  hipLaunchKernelGGL(view_hub_fin_kernel, grid1(m), dim3(kW), 0, st, PP, m, int(ncb), ba, Wr, br, sv, t, xr);
+  hipLaunchKernelGGL(view_hub_fin_kernel, grid1(m), dim3(kSumThreads), 0, st, PP, m, int(ncb), ba, Wr, br, sv, t, xr);
   return launch_status("gasfm_view_hub_fwd");
 }
 
