@@ -68,6 +68,8 @@ _SIGS = {
                                   _vp, _vp, _vp, _vp]),
     "gasfm_view_hub_bwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp, _vp, _vp]),
+    "gasfm_pose_fwd": (_i32, [_vp, _i64, _i64, _vp, _vp]),
+    "gasfm_pose_bwd": (_i32, [_vp, _i64, _i64, _vp, _vp, _i64, _vp]),
     "gasfm_point_tail_part_shape": (_i32, [_i64, _i32, _vp]),
     "gasfm_point_hub_part_shape": (_i32, [_i64, _i32, _i32, _vp]),
     "gasfm_point_tail_fwd": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
@@ -455,3 +457,16 @@ def view_hub_bwd(v, rs, gC, bC, Wv, gA, bA, Wa, t, Wr, dsv, dxr, dxl, dacc, part
                                   _p(t), _p(Wr), _p(dsv), _p(dxr), _p(dxl), _p(dacc), _p(part), _p(scratch),
                                   _stream(v))
     check(st, "gasfm_view_hub_bwd")
+
+
+# ---------------------------------------------------------------- calibrated camera head (pose_head.hip)
+def pose_fwd(x, P):
+    if not x.is_cuda or x.dtype != torch.float32 or x.stride(1) != 1:
+        raise TypeError("pose x: expected a float32 CUDA tensor with unit column stride (no CPU fallback)")
+    check(lib().gasfm_pose_fwd(_p(x), x.stride(0), x.shape[0], _p(P), _stream(x)), "gasfm_pose_fwd")
+
+
+def pose_bwd(x, dP, dx):
+    _req(dP, "dP")
+    check(lib().gasfm_pose_bwd(_p(x), x.stride(0), x.shape[0], _p(dP), _p(dx), dx.stride(0), _stream(x)),
+          "gasfm_pose_bwd")

@@ -246,6 +246,7 @@ class GatAttentionFn(torch.autograd.Function):
         ctx.plan, ctx.heads, ctx.slope = plan, heads, slope
         ctx.save_for_backward(XL, XR, att, bias, out, smax, ssum)
         ctx.mark_non_differentiable(smax, ssum)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for the statistics outputs
         return out, smax, ssum
 
     @staticmethod

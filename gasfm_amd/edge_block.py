@@ -8,7 +8,8 @@ three differentiable ops whose forward AND backward are HIP kernels:
   EdgeEpilogueFn   (P, P0, token, Sp, Sv, Sg) -> P' = P + (Wp [P_hat|P0] + bp + Sp[pt] + Sv[cam] + Sg)/4
 
 P_hat = relu(LN(P)) is never materialised: both kernels recompute it from P.
-The `token` output of the prologue is a zero-stride placeholder whose gradient
+The `token` output of the prologue is a zero-stride placeholder (its one element is never
+read: an uninitialised 1x1 tensor, no fill kernel) whose gradient
 the epilogue's backward sets to dP' (the block-output gradient), so that the
 prologue's backward kernel can do the whole P-side backward in one pass:
   dP = LN_bwd(mask * (Wl^T dXL + Wp^T dP'/4)) + dP'      (identity residual, layers.py:254-261)
@@ -38,7 +39,7 @@ class EdgePrologueFn(torch.autograd.Function):
         ctx.has_ln = ln_w is not None
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(P, ln_w, ln_b, W, Wp)
-        token = P.new_zeros((1, 1)).expand(E, P.shape[1])
+        token = P.new_empty((1, 1)).expand(E, P.shape[1])
         return XL, token
 
     @staticmethod
@@ -162,7 +163,7 @@ class Block0PrologueFn(torch.autograd.Function):
         ctx.eps = eps
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(P, ln_w, ln_b, W0)
-        return XL, P.new_zeros((1, 1)).expand(E, 4)
+        return XL, P.new_empty((1, 1)).expand(E, 4)
 
     @staticmethod
     def backward(ctx, dXL, daux):

@@ -763,8 +763,30 @@ class GraphAttnSfMNet(Module):
             return {"Ps_norm": Ps}
         if self.rot_representation != "quat":
             raise NotImplementedError("only the quaternion head (all GASFM confs) is implemented")
+        if x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.shape[1] == 7:
+            return {"Ps_norm": QuatPoseFn.apply(x)}
         R = quaternion_to_matrix(x[:, :4])
         return {"Ps_norm": torch.cat((R, x[:, -3:].unsqueeze(-1)), dim=-1)}
+
+
+class QuatPoseFn(torch.autograd.Function):
+    """x [m, 7] -> [R(q) | t] [m, 3, 4] in one HIP kernel each way (csrc/pose_head.hip)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        from . import _native
+        P = torch.empty((x.shape[0], 3, 4), dtype=torch.float32, device=x.device)
+        _native.pose_fwd(x, P)
+        ctx.save_for_backward(x)
+        return P
+
+    @staticmethod
+    def backward(ctx, dP):
+        from . import _native
+        (x,) = ctx.saved_tensors
+        dx = torch.empty((x.shape[0], 7), dtype=torch.float32, device=x.device)
+        _native.pose_bwd(x, dP.contiguous(), dx)
+        return dx
 
 
 def quaternion_to_matrix(q):

@@ -338,6 +338,13 @@ int gasfm_view_hub_bwd(const float* v, const float* rs, int64_t m, int32_t D, co
                        const float* Wr, const float* dsv, const float* dxr, const float* dxl, float* dacc,
                        float* part, float* scratch, void* stream);
 
+/* ---- calibrated camera head (baseNet.py:38-56, rot_representation 'quat') ----
+ * P[c] = [R(q) | t] (3 x 4, row-major) from x[c] = (r, i, j, k, tx, ty, tz) (row stride ldx);
+ * R is pytorch3d's quaternion_to_matrix (real part first, normalised by |q|^2).  Backward writes
+ * dx[c] (7 values, row stride lddx). */
+int gasfm_pose_fwd(const float* x, int64_t ldx, int64_t m, float* P, void* stream);
+int gasfm_pose_bwd(const float* x, int64_t ldx, int64_t m, const float* dP, float* dx, int64_t lddx, void* stream);
+
 /* ---- global node (ONE row): LayerNorm -> ReLU -> Linear (+ residual) ----
  * Replaces the M = 1 aten chains on the global feature vector: norm_and_proj_global2view /
  * _global2scenepoint (layers.py:497-520), both convs' lin_r on those rows (PyG),
