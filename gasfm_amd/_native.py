@@ -68,6 +68,9 @@ _SIGS = {
                                   _vp, _vp, _vp, _vp]),
     "gasfm_view_hub_bwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp, _vp, _vp]),
+    "gasfm_gvec_multi_fwd": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp]),
+    "gasfm_gvec_multi_bwd": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp,
+                                    _vp, _vp, _f32, _vp]),
     "gasfm_pose_fwd": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "gasfm_pose_bwd": (_i32, [_vp, _i64, _i64, _vp, _vp, _i64, _vp]),
     "gasfm_point_tail_part_shape": (_i32, [_i64, _i32, _vp]),
@@ -470,3 +473,36 @@ def pose_bwd(x, dP, dx):
     _req(dP, "dP")
     check(lib().gasfm_pose_bwd(_p(x), x.stride(0), x.shape[0], _p(dP), _p(dx), dx.stride(0), _stream(x)),
           "gasfm_pose_bwd")
+
+
+# ---------------------------------------------------------------- batched single-row problems (global hub)
+def _ptrs(ts):
+    return (ctypes.c_void_p * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
+
+
+def _ints(v):
+    return (ctypes.c_int32 * len(v))(*v)
+
+
+def gvec_multi_fwd(probs, eps):
+    """probs: [(x, ln_w, ln_b, W, b, res, y)]; x / res / y 1-D rows, W [N, K]."""
+    cols = list(zip(*probs))
+    for W in cols[3]:
+        _req(W, "W")
+    K = [W.shape[1] for W in cols[3]]
+    N = [W.shape[0] for W in cols[3]]
+    st = lib().gasfm_gvec_multi_fwd(len(probs), *[_ptrs(c) for c in cols], _ints(K), _ints(N), eps,
+                                    _stream(cols[0][0]))
+    check(st, "gasfm_gvec_multi_fwd")
+
+
+def gvec_multi_bwd(probs, groups, eps):
+    """probs: [(dy, x, ln_w, ln_b, W, dW, db, dgam, dbet, part)]; groups: [(p0, np, dres, dx)]."""
+    dy, x, lw, lb, W, dW, db, dg, dbt, part = (list(c) for c in zip(*probs))
+    K = [w.shape[1] for w in W]
+    N = [w.shape[0] for w in W]
+    p0, npr, dres, dx = (list(c) for c in zip(*groups))
+    st = lib().gasfm_gvec_multi_bwd(len(probs), _ptrs(dy), _ptrs(x), _ptrs(lw), _ptrs(lb), _ptrs(W), _ints(K),
+                                    _ints(N), _ptrs(dW), _ptrs(db), _ptrs(dg), _ptrs(dbt), _ptrs(part), len(groups),
+                                    _ints(p0), _ints(npr), _ptrs(dres), _ptrs(dx), eps, _stream(x[0]))
+    check(st, "gasfm_gvec_multi_bwd")

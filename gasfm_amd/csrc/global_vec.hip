@@ -216,6 +216,240 @@ __global__ __launch_bounds__(kFinT) void gvec_bwd_finish_kernel(const float* __r
   }
 }
 
+
+// ---------------------------------------------------------------------------- batched problems
+// Several independent single-row problems in ONE launch (the global hub, model.py: the three
+// LayerNorm -> Linear consumers of a block's global row, then the two lin_r rows): the grid is
+// the concatenation of the per-problem grids, each workgroup finds its problem by block range.
+constexpr int kMaxProb = 4;
+
+struct GvFwdProb {
+  const float* x;
+  const float* gam;
+  const float* bet;
+  const float* W;
+  const float* b;
+  const float* res;
+  float* y;
+  int K, N, blk0;
+};
+struct GvFwdArgs {
+  GvFwdProb p[kMaxProb];
+  int nprob;
+  float eps;
+};
+
+__device__ __forceinline__ int find_prob(const int (&blk0)[kMaxProb], int nprob) {
+  int pi = 0;
+  while (pi + 1 < nprob && int(blockIdx.x) >= blk0[pi + 1]) ++pi;
+  return pi;
+}
+
+__global__ __launch_bounds__(kT) void gvec_multi_fwd_kernel(GvFwdArgs a) {
+  int blk0[kMaxProb];
+#pragma unroll
+  for (int q = 0; q < kMaxProb; ++q) blk0[q] = a.p[q].blk0;
+  const GvFwdProb& p = a.p[find_prob(blk0, a.nprob)];
+  __shared__ __attribute__((aligned(16))) float h[kMaxK];
+  __shared__ float scratch[kT / 64];
+  const int K = p.K;
+  if (p.gam) {
+    float mean, rstd;
+    row_stats<kT>(p.x, K, a.eps, scratch, mean, rstd);
+    for (int j = threadIdx.x; j < K; j += kT) h[j] = fmaxf(fmaf((p.x[j] - mean) * rstd, p.gam[j], p.bet[j]), 0.f);
+  } else {
+    for (int j = threadIdx.x; j < K; j += kT) h[j] = p.x[j];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = (int(blockIdx.x) - p.blk0) * (kT / 64) + wave;
+  if (i >= p.N) return;
+  const float* w = p.W + int64_t(i) * K;
+  float a0 = 0.f, a1 = 0.f;
+  int j = lane * 4;
+#pragma unroll 4
+  for (; j + 256 < K; j += 512) {
+    const float4 u = *reinterpret_cast<const float4*>(w + j);
+    const float4 v = *reinterpret_cast<const float4*>(w + j + 256);
+    const float4 hu = *reinterpret_cast<const float4*>(h + j);
+    const float4 hv = *reinterpret_cast<const float4*>(h + j + 256);
+    a0 = fmaf(u.x, hu.x, fmaf(u.y, hu.y, fmaf(u.z, hu.z, fmaf(u.w, hu.w, a0))));
+    a1 = fmaf(v.x, hv.x, fmaf(v.y, hv.y, fmaf(v.z, hv.z, fmaf(v.w, hv.w, a1))));
+  }
+  if (j < K) {
+    const float4 u = *reinterpret_cast<const float4*>(w + j);
+    const float4 hu = *reinterpret_cast<const float4*>(h + j);
+    a0 = fmaf(u.x, hu.x, fmaf(u.y, hu.y, fmaf(u.z, hu.z, fmaf(u.w, hu.w, a0))));
+  }
+  const float acc = wave_sum(a0 + a1);
+  if (lane == 0) p.y[i] = acc + (p.b ? p.b[i] : 0.f) + (p.res ? p.res[i] : 0.f);
+}
+
+struct GvBwdProb {
+  const float* dy;
+  const float* x;
+  const float* gam;
+  const float* bet;
+  const float* W;
+  float* dW;
+  float* db;
+  float* part;
+  int K, N, blk0, slabs;
+};
+struct GvBwdArgs {
+  GvBwdProb p[kMaxProb];
+  int nprob;
+  float eps;
+};
+
+// per problem exactly gvec_bwd_kernel: dW slab, db, part[chunk, j] = sum_{i in chunk} dy[i] W[i, j]
+__global__ __launch_bounds__(kT) void gvec_multi_bwd_kernel(GvBwdArgs a) {
+  int blk0[kMaxProb];
+#pragma unroll
+  for (int q = 0; q < kMaxProb; ++q) blk0[q] = a.p[q].blk0;
+  const GvBwdProb& p = a.p[find_prob(blk0, a.nprob)];
+  __shared__ float scratch[kT / 64];
+  __shared__ float red[kT / 64][kSlab];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int local = int(blockIdx.x) - p.blk0;
+  const int slab = local % p.slabs, chunk = local / p.slabs;
+  const int K = p.K, N = p.N;
+  const int j = slab * kSlab + lane;
+  float hj = p.x[j];
+  if (p.gam) {
+    float mean, rstd;
+    row_stats<kT>(p.x, K, a.eps, scratch, mean, rstd);
+    hj = fmaxf(fmaf((hj - mean) * rstd, p.gam[j], p.bet[j]), 0.f);
+  }
+  const int i0 = chunk * kChunk + wave * (kChunk / 4);
+  const int i1 = min(i0 + kChunk / 4, N);
+  constexpr int G = 16;
+  float a0 = 0.f, a1 = 0.f;
+  for (int ib = i0; ib < i1; ib += G) {
+    float w[G], d[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const int i = ib + u;
+      const bool live = i < i1;
+      const int ii = live ? i : i0;
+      d[u] = live ? p.dy[ii] : 0.f;
+      w[u] = p.W[int64_t(ii) * K + j];
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const int i = ib + u;
+      if (i < i1) p.dW[int64_t(i) * K + j] = d[u] * hj;
+      if (u & 1)
+        a1 = fmaf(d[u], w[u], a1);
+      else
+        a0 = fmaf(d[u], w[u], a0);
+    }
+  }
+  red[wave][lane] = a0 + a1;
+  __syncthreads();
+  if (wave == 0) {
+    float sacc = 0.f;
+#pragma unroll
+    for (int w = 0; w < kT / 64; ++w) sacc += red[w][lane];
+    p.part[int64_t(chunk) * K + j] = sacc;
+  }
+  if (p.db && slab == 0) {
+    for (int r = threadIdx.x; r < kChunk; r += kT) {
+      const int ii = chunk * kChunk + r;
+      if (ii < N) p.db[ii] = p.dy[ii];
+    }
+  }
+}
+
+// groups of problems that share the input row x: dx = dres + sum over the group's problems of
+// LN_bwd(mask * sum_c part[c]) (or the plain sum when the problem has no LayerNorm); dgamma,
+// dbeta per problem.  One 1024-thread workgroup per group.
+struct GvFinProb {
+  const float* part;
+  const float* gam;
+  const float* bet;
+  float* dgam;
+  float* dbet;
+  int nchunks;
+};
+struct GvFinGroup {
+  const float* x;
+  const float* dres;
+  float* dx;
+  int K, p0, np;
+};
+struct GvFinArgs {
+  GvFinProb p[kMaxProb];
+  GvFinGroup g[kMaxProb];
+  float eps;
+};
+
+__global__ __launch_bounds__(kFinT) void gvec_multi_finish_kernel(GvFinArgs a) {
+  __shared__ float scratch[kFinT / 64];
+  const GvFinGroup& G = a.g[blockIdx.x];
+  const int K = G.K;
+  constexpr int PER = kMaxK / kFinT;
+  float acc[PER], xh[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int j = threadIdx.x + u * kFinT;
+    acc[u] = (G.dres && j < K) ? G.dres[j] : 0.f;
+  }
+  bool stats = false;
+  float rstd = 1.f;
+  for (int q = G.p0; q < G.p0 + G.np; ++q) {
+    const GvFinProb& P = a.p[q];
+    float dh[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int j = threadIdx.x + u * kFinT;
+      float sacc = 0.f;
+      if (j < K)
+        for (int c = 0; c < P.nchunks; ++c) sacc += P.part[int64_t(c) * K + j];
+      dh[u] = sacc;
+    }
+    if (!P.gam) {
+#pragma unroll
+      for (int u = 0; u < PER; ++u) acc[u] += dh[u];
+      continue;
+    }
+    if (!stats) {
+      float mean;
+      row_stats<kFinT>(G.x, K, a.eps, scratch, mean, rstd);
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int j = threadIdx.x + u * kFinT;
+        xh[u] = j < K ? (G.x[j] - mean) * rstd : 0.f;
+      }
+      stats = true;
+    }
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int j = threadIdx.x + u * kFinT;
+      if (j < K) {
+        const float d = fmaf(xh[u], P.gam[j], P.bet[j]) > 0.f ? dh[u] : 0.f;
+        P.dgam[j] = d * xh[u];
+        P.dbet[j] = d;
+        dh[u] = d * P.gam[j];
+        s1 += dh[u];
+        s2 = fmaf(dh[u], xh[u], s2);
+      } else {
+        dh[u] = 0.f;
+      }
+    }
+    s1 = block_sum<kFinT>(s1, scratch) / K;
+    s2 = block_sum<kFinT>(s2, scratch) / K;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) acc[u] += rstd * (dh[u] - s1 - xh[u] * s2);
+  }
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int j = threadIdx.x + u * kFinT;
+    if (j < K) G.dx[j] = acc[u];
+  }
+}
+
 }  // namespace
 }  // namespace gasfm
 
@@ -250,4 +484,70 @@ extern "C" int gasfm_gvec_bwd(const float* dy, const float* x, int32_t K, const 
   hipLaunchKernelGGL(gvec_bwd_finish_kernel, dim3(1), dim3(kFinT), 0, st, part, chunks, K, x, ln_w, ln_b, eps, dy,
                      resid, dx, dgam, dbet);
   return launch_status("gasfm_gvec_bwd_finish");
+}
+
+static bool gv_shape_ok(int K, int N) { return K > 0 && K <= kMaxK && K % kSlab == 0 && N > 0; }
+
+extern "C" int gasfm_gvec_multi_fwd(int32_t nprob, const float* const* x, const float* const* ln_w,
+                                    const float* const* ln_b, const float* const* W, const float* const* b,
+                                    const float* const* res, float* const* y, const int32_t* K, const int32_t* N,
+                                    float eps, void* stream) {
+  GASFM_REQUIRE(nprob >= 1 && nprob <= kMaxProb, "gasfm_gvec_multi_fwd: nprob=%d", nprob);
+  GvFwdArgs a{};
+  a.nprob = nprob;
+  a.eps = eps;
+  int blocks = 0;
+  for (int q = 0; q < nprob; ++q) {
+    GASFM_REQUIRE(gv_shape_ok(K[q], N[q]), "gasfm_gvec_multi_fwd: problem %d K=%d N=%d", q, K[q], N[q]);
+    GASFM_REQUIRE(x[q] && W[q] && y[q] && (!ln_w[q] || ln_b[q]) && aligned16(W[q]),
+                  "gasfm_gvec_multi_fwd: problem %d pointers", q);
+    a.p[q] = GvFwdProb{x[q], ln_w[q], ln_b[q], W[q], b[q], res[q], y[q], K[q], N[q], blocks};
+    blocks += (N[q] + 3) / 4;
+  }
+  for (int q = nprob; q < kMaxProb; ++q) a.p[q].blk0 = blocks;
+  hipLaunchKernelGGL(gvec_multi_fwd_kernel, dim3(blocks), dim3(kT), 0, reinterpret_cast<hipStream_t>(stream), a);
+  return launch_status("gasfm_gvec_multi_fwd");
+}
+
+// Backward of a batch: per problem dW (and db when given), partials part[q] of
+// [gasfm_gvec_bwd_chunks(N[q]) x K[q]]; then groups of problems sharing x: group g covers
+// problems [g_p0[g], g_p0[g] + g_np[g]) and writes dx[g] = dres[g] (may be null) + the sum of the
+// group's LayerNorm (or plain) backward terms.
+extern "C" int gasfm_gvec_multi_bwd(int32_t nprob, const float* const* dy, const float* const* x,
+                                    const float* const* ln_w, const float* const* ln_b, const float* const* W,
+                                    const int32_t* K, const int32_t* N, float* const* dW, float* const* db,
+                                    float* const* dgam, float* const* dbet, float* const* part, int32_t ngroups,
+                                    const int32_t* g_p0, const int32_t* g_np, const float* const* dres,
+                                    float* const* dx, float eps, void* stream) {
+  GASFM_REQUIRE(nprob >= 1 && nprob <= kMaxProb && ngroups >= 1 && ngroups <= kMaxProb,
+                "gasfm_gvec_multi_bwd: nprob=%d ngroups=%d", nprob, ngroups);
+  GvBwdArgs a{};
+  a.nprob = nprob;
+  a.eps = eps;
+  GvFinArgs f{};
+  f.eps = eps;
+  int blocks = 0;
+  for (int q = 0; q < nprob; ++q) {
+    GASFM_REQUIRE(gv_shape_ok(K[q], N[q]), "gasfm_gvec_multi_bwd: problem %d K=%d N=%d", q, K[q], N[q]);
+    GASFM_REQUIRE(dy[q] && x[q] && W[q] && dW[q] && part[q] && (!ln_w[q] || (ln_b[q] && dgam[q] && dbet[q])),
+                  "gasfm_gvec_multi_bwd: problem %d pointers", q);
+    const int slabs = K[q] / kSlab, chunks = (N[q] + kChunk - 1) / kChunk;
+    a.p[q] = GvBwdProb{dy[q], x[q], ln_w[q], ln_b[q], W[q], dW[q], db[q], part[q], K[q], N[q], blocks, slabs};
+    blocks += slabs * chunks;
+    f.p[q] = GvFinProb{part[q], ln_w[q], ln_b[q], dgam[q], dbet[q], chunks};
+  }
+  for (int q = nprob; q < kMaxProb; ++q) a.p[q].blk0 = blocks;
+  for (int gi = 0; gi < ngroups; ++gi) {
+    const int p0 = g_p0[gi], np = g_np[gi];
+    GASFM_REQUIRE(p0 >= 0 && np >= 1 && p0 + np <= nprob && dx[gi], "gasfm_gvec_multi_bwd: group %d", gi);
+    for (int q = p0; q < p0 + np; ++q)
+      GASFM_REQUIRE(x[q] == x[p0] && K[q] == K[p0], "gasfm_gvec_multi_bwd: group %d mixes inputs", gi);
+    f.g[gi] = GvFinGroup{x[p0], dres[gi], dx[gi], K[p0], p0, np};
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(gvec_multi_bwd_kernel, dim3(blocks), dim3(kT), 0, st, a);
+  int s = launch_status("gasfm_gvec_multi_bwd");
+  if (s != GASFM_OK) return s;
+  hipLaunchKernelGGL(gvec_multi_finish_kernel, dim3(ngroups), dim3(kFinT), 0, st, f);
+  return launch_status("gasfm_gvec_multi_finish");
 }

@@ -103,6 +103,88 @@ class GlobalLinearFn(torch.autograd.Function):
 GVEC_MAX_K = 4096
 
 
+class GlobalHubFn(torch.autograd.Function):
+    """Every consumer of a block's global row g [1, G] in two launches each way.
+
+    (skip, SG, XRv, XRp) with
+      SG  = lin_global(relu(global_norm_layer(g)))              this block's projection update
+      XRv = lin_r_v(norm_and_proj_global2view(g))               next block's view2global target row
+      XRp = lin_r_p(norm_and_proj_global2scenepoint(g))         next block's scenepoint2global target row
+      skip = g                                                  next block's proj_view_and_scenepoint2global residual
+    (layers.py:497-520, 527-528, 590-592, 928-935).  Forward: the three LayerNorm -> Linear rows in one
+    batched gvec launch, the two lin_r rows in a second.  Backward: the lin_r rows (batched), then the
+    three LayerNorm rows with their dg contributions and the skip gradient summed in one finish pass --
+    no autograd accumulation over g's four consumers.
+    """
+
+    @staticmethod
+    def forward(ctx, g, gA, bA, WA, gB, bB, WB, bWB, gC, bC, WC, bWC, WD, bD, WE, bE, eps):
+        from . import _native
+        g1 = g.reshape(-1).contiguous()
+        W = [w.contiguous() for w in (WA, WB, WC, WD, WE)]
+        f = dict(dtype=torch.float32, device=g.device)
+        sg, xv, xp = torch.empty(W[0].shape[0], **f), torch.empty(W[1].shape[0], **f), torch.empty(W[2].shape[0], **f)
+        XRv, XRp = torch.empty(W[3].shape[0], **f), torch.empty(W[4].shape[0], **f)
+        _native.gvec_multi_fwd([(g1, gA, bA, W[0], None, None, sg), (g1, gB, bB, W[1], bWB, None, xv),
+                                (g1, gC, bC, W[2], bWC, None, xp)], eps)
+        _native.gvec_multi_fwd([(xv, None, None, W[3], bD, None, XRv), (xp, None, None, W[4], bE, None, XRp)], 0.0)
+        ctx.save_for_backward(g1, xv, xp, gA, bA, gB, bB, gC, bC, *W)
+        ctx.eps, ctx.g_shape = eps, g.shape
+        ctx.set_materialize_grads(False)
+        return g.view_as(g), sg.view(1, -1), XRv.view(1, -1), XRp.view(1, -1)
+
+    @staticmethod
+    def backward(ctx, dskip, dsg, dXRv, dXRp):
+        from . import _native
+        g1, xv, xp, gA, bA, gB, bB, gC, bC, WA, WB, WC, WD, WE = ctx.saved_tensors
+        f = dict(dtype=torch.float32, device=g1.device)
+        row = lambda t, n: t.reshape(-1).contiguous() if t is not None else torch.zeros(n, **f)  # noqa: E731
+        dsg, dXRv, dXRp = row(dsg, WA.shape[0]), row(dXRv, WD.shape[0]), row(dXRp, WE.shape[0])
+        dres = dskip.reshape(-1).contiguous() if dskip is not None else None
+        part = lambda W: torch.empty((_native.gvec_bwd_chunks(W.shape[0]), W.shape[1]), **f)  # noqa: E731
+        dWD, dWE = torch.empty_like(WD), torch.empty_like(WE)
+        dbD, dbE = torch.empty(WD.shape[0], **f), torch.empty(WE.shape[0], **f)
+        dxv, dxp = torch.empty_like(xv), torch.empty_like(xp)
+        _native.gvec_multi_bwd([(dXRv, xv, None, None, WD, dWD, dbD, None, None, part(WD)),
+                                (dXRp, xp, None, None, WE, dWE, dbE, None, None, part(WE))],
+                               [(0, 1, None, dxv), (1, 1, None, dxp)], 0.0)
+        dW = [torch.empty_like(w) for w in (WA, WB, WC)]
+        dbB, dbC = torch.empty(WB.shape[0], **f), torch.empty(WC.shape[0], **f)
+        dln = [torch.empty_like(t) for t in (gA, bA, gB, bB, gC, bC)]
+        dg = torch.empty_like(g1)
+        _native.gvec_multi_bwd([(dsg, g1, gA, bA, WA, dW[0], None, dln[0], dln[1], part(WA)),
+                                (dxv, g1, gB, bB, WB, dW[1], dbB, dln[2], dln[3], part(WB)),
+                                (dxp, g1, gC, bC, WC, dW[2], dbC, dln[4], dln[5], part(WC))],
+                               [(0, 3, dres, dg)], ctx.eps)
+        return (dg.view(ctx.g_shape), dln[0], dln[1], dW[0], dln[2], dln[3], dW[1], dbB, dln[4], dln[5], dW[2], dbC,
+                dWD, dbD, dWE, dbE, None)
+
+
+def global_hub_params(pfu, nvsg):
+    """GlobalHubFn parameters for this block's projection-feature update (pfu) and the next block's
+    ViewAndScenePoint2Global (nvsg), or None when the shapes are not the fused ones."""
+    if pfu is None or nvsg is None or not pfu.normalize_global_features or not nvsg.stateful:
+        return None
+    lnA, linA = pfu.global_norm_layer, pfu.lin_global
+    G = linA.in_features
+    seqs = (getattr(nvsg, "norm_and_proj_global2view", None), getattr(nvsg, "norm_and_proj_global2scenepoint", None))
+    if any(q is None or len(q) != 3 or not isinstance(q[0], LayerNorm) or not isinstance(q[2], Linear) for q in seqs):
+        return None
+    (lnB, _, linB), (lnC, _, linC) = seqs
+    linD, linE = nvsg.graph_conv_view2global.lin_r, nvsg.graph_conv_scenepoint2global.lin_r
+    ok = (G % 64 == 0 and G <= GVEC_MAX_K and linA.bias is None and all(
+        ln.weight is not None and ln.bias is not None and tuple(ln.normalized_shape) == (G,) and ln.eps == lnA.eps
+        for ln in (lnA, lnB, lnC)) and linB.in_features == G and linC.in_features == G
+        and linB.bias is not None and linC.bias is not None
+        and linD.in_features == linB.out_features and linE.in_features == linC.out_features
+        and linD.bias is not None and linE.bias is not None
+        and all(n % 64 == 0 and n <= GVEC_MAX_K for n in (linD.in_features, linE.in_features)))
+    if not ok:
+        return None
+    return (lnA.weight, lnA.bias, linA.weight, lnB.weight, lnB.bias, linB.weight, linB.bias, lnC.weight, lnC.bias,
+            linC.weight, linC.bias, linD.weight, linD.bias, linE.weight, linE.bias, lnA.eps)
+
+
 def _gvec_ok(x, k):
     return (x.is_cuda and x.dim() == 2 and x.shape[0] == 1 and x.dtype == torch.float32 and k % 64 == 0
             and k <= GVEC_MAX_K)

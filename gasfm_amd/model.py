@@ -191,34 +191,24 @@ class ViewAndScenePoint2Global(Module):
         self.mlp = get_linear_layers((2 + n_hidden_layers_global_update) * [n_feat_global_out], norm=False)
 
     def forward_plan(self, view, pts, plan_v2g, plan_s2g, prev, plan_s2g_partial=None, shard=None, xl_pts=None,
-                     xl_view=None):
-        """xl_pts / xl_view: the convs' lin_l(pts) / lin_l(view) when already computed (hubs)."""
+                     xl_view=None, pre_glob=None):
+        """xl_pts / xl_view: the convs' lin_l(pts) / lin_l(view) when already computed (hubs);
+        pre_glob: (XR_view2global, XR_scenepoint2global, skip of prev) from GlobalHubFn."""
         assert self.stateful == (prev is not None)
-        xv = dense.sequential(self.norm_and_proj_global2view, prev) if prev is not None else None
-        xp = dense.sequential(self.norm_and_proj_global2scenepoint, prev) if prev is not None else None
-        cv = self.graph_conv_view2global
-        if xl_view is not None:
-            XRv = cv.lin_r(torch.zeros((1, cv.in_channels), device=view.device)).expand(1, -1) if xv is None \
-                else dense.linear(xv, cv.lin_r)
-            v2g = gat_attention(xl_view, XRv, cv.att, cv._bias(xl_view), plan_v2g, cv.heads, cv.negative_slope)
+        cv, c = self.graph_conv_view2global, self.graph_conv_scenepoint2global
+        if pre_glob is not None:
+            XRv, XRp, prev = pre_glob
         else:
-            v2g = cv.attend(view, xv, plan_v2g)
-        c = self.graph_conv_scenepoint2global
-        if shard is None and xl_pts is not None:
-            XR = c.lin_r(torch.zeros((1, c.in_channels), device=pts.device)).expand(1, -1) if xp is None \
-                else dense.linear(xp, c.lin_r)
-            s2g = gat_attention(xl_pts, XR, c.att, c._bias(xl_pts), plan_s2g, c.heads, c.negative_slope)
-        elif shard is None:
-            s2g = c.attend(pts, xp, plan_s2g)
+            xv = dense.sequential(self.norm_and_proj_global2view, prev) if prev is not None else None
+            xp = dense.sequential(self.norm_and_proj_global2scenepoint, prev) if prev is not None else None
+            XRv, XRp = _target_row(cv, xv, view), _target_row(c, xp, pts)
+        XLv = xl_view if xl_view is not None else dense.linear(view, cv.lin_l)
+        v2g = gat_attention(XLv, XRv, cv.att, cv._bias(XLv), plan_v2g, cv.heads, cv.negative_slope)
+        XLp = xl_pts if xl_pts is not None else dense.linear(pts, c.lin_l)
+        if shard is None:
+            s2g = gat_attention(XLp, XRp, c.att, c._bias(XLp), plan_s2g, c.heads, c.negative_slope)
         else:  # points are sharded, the global target is replicated
-            if xp is None:
-                zero = torch.zeros((1, c.in_channels), device=pts.device)
-                XR = c.lin_r(zero).expand(1, -1)
-            else:
-                XR = dense.linear(xp, c.lin_r)
-            XR = replicated_to_local(XR, shard)
-            XLp = xl_pts if xl_pts is not None else dense.linear(pts, c.lin_l)
-            s2g = ShardedAttentionFn.apply(XLp, XR, c.att, c.bias, plan_s2g,
+            s2g = ShardedAttentionFn.apply(XLp, replicated_to_local(XRp, shard), c.att, c.bias, plan_s2g,
                                            plan_s2g_partial, c.heads, c.negative_slope, shard)
         x = torch.cat([v2g, s2g], dim=1)
         if hasattr(self, "proj_view_and_scenepoint2global"):
@@ -231,6 +221,14 @@ class ViewAndScenePoint2Global(Module):
         if self.use_norm_pre_mlp:
             x = F.relu(dense.layer_norm(x, self.norm_pre_mlp))
         return skip + dense.sequential(self.mlp, x)
+
+
+def _target_row(conv, x_tgt, ref):
+    """XR of a one-target GATv2 conv: lin_r(x_tgt), or lin_r(0) (== its bias) for the reference's
+    zero target features when stateless (dataset_utils.py:569-571)."""
+    if x_tgt is None:
+        return conv.lin_r(torch.zeros((1, conv.in_channels), device=ref.device)).expand(1, -1)
+    return dense.linear(x_tgt, conv.lin_r)
 
 
 class _Global2Node(Module):
@@ -365,7 +363,7 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
             if hv is not None and view_block._rows_ok(view, view.shape[1]):
                 skip, SV, XLv, XRn = view_block.hub(view, hv)
                 carry.update(XRc=XRn, view_skip=skip, SV=SV, XLv2g=XLv)
-        return self._finish(pts, view, plans, prev_glob, carry)
+        return self._finish(pts, view, plans, prev_glob, carry, pfu, nxt)
 
     def forward_plan(self, P_hat, plans, prev_pt=None, prev_view=None, prev_glob=None):
         shard = plans.get("_shard")
@@ -374,14 +372,21 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
                                            plans.get("_partial", {}).get("proj2view"), shard)
         return self._finish(pts, view, plans, prev_glob)
 
-    def _finish(self, pts, view, plans, prev_glob, carry=None):
+    def _finish(self, pts, view, plans, prev_glob, carry=None, pfu=None, nxt=None):
         glob = None
         if self.output_global or self.global2view_and_global2scenepoint_enabled:
+            pre_glob = carry.pop("pre_glob", None) if carry is not None else None
             glob = self.view_and_scenepoint2global.forward_plan(
                 view, pts, plans["view2global"], plans["scenepoint2global"], prev_glob,
                 plans.get("_partial", {}).get("scenepoint2global"), plans.get("_shard"),
                 xl_pts=carry.pop("XLs2g", None) if carry is not None else None,
-                xl_view=carry.pop("XLv2g", None) if carry is not None else None)
+                xl_view=carry.pop("XLv2g", None) if carry is not None else None, pre_glob=pre_glob)
+            if carry is not None and nxt is not None and getattr(nxt, "output_global", False) \
+                    and dense._gvec_ok(glob, glob.shape[1]):
+                hg = dense.global_hub_params(pfu, nxt.view_and_scenepoint2global)
+                if hg is not None:
+                    skip, SG, XRv, XRp = dense.GlobalHubFn.apply(glob, *hg)
+                    carry.update(SG=SG, pre_glob=(XRv, XRp, skip))
         if self.global2view_and_global2scenepoint_enabled:
             pts = self.global2scenepoint(glob, pts)
             view = self.global2view(glob, view)
@@ -409,12 +414,12 @@ class GraphAttnSfMProjectionFeatureUpdate(Module):
             self.mlp = get_linear_layers(n_hidden_layers_proj_update * [n_feat_proj_out] + [n_feat_proj_out],
                                          norm=False)
 
-    def node_terms(self, pts, view, glob, sp=None, sv=None):
-        """sp / sv: the point / view terms when PointHubFn / ViewHubFn already computed them."""
+    def node_terms(self, pts, view, glob, sp=None, sv=None, sg=None):
+        """sp / sv / sg: the point / view / global terms when the hubs already computed them."""
         if self.normalize_global_features:
             return (sp if sp is not None else dense.ln_relu_linear(pts, self.scenepoint_norm_layer, self.lin_scenepoint),
                     sv if sv is not None else dense.ln_relu_linear(view, self.view_norm_layer, self.lin_view),
-                    dense.ln_relu_linear(glob, self.global_norm_layer, self.lin_global))
+                    sg if sg is not None else dense.ln_relu_linear(glob, self.global_norm_layer, self.lin_global))
         return dense.linear(pts, self.lin_scenepoint), dense.linear(view, self.lin_view), \
             dense.linear(glob, self.lin_global)
 
@@ -485,8 +490,9 @@ class GraphAttnSfMLayer(Module):
         XL, token = Block0PrologueFn.apply(P.contiguous(), la.weight, la.bias, W, b, la.eps, pos)
         pts, view, glob = gfu.forward_fused(XL, plans, None, None, None, xl_sorted=pos is not None, carry=carry,
                                             pfu=pfu, nxt=nxt)
-        sp, sv, sg = pfu.node_terms(pts, view, glob, *((carry.pop("SA", None), carry.pop("SV", None))
-                                                         if carry is not None else (None, None)))
+        sp, sv, sg = pfu.node_terms(pts, view, glob, *((carry.pop("SA", None), carry.pop("SV", None),
+                                                          carry.pop("SG", None))
+                                                         if carry is not None else (None, None, None)))
         shard = plans.get("_shard")
         sv, sg = replicated_to_local(sv, shard), replicated_to_local(sg, shard)
         sk = self.skip_projection.lin_proj
@@ -504,8 +510,9 @@ class GraphAttnSfMLayer(Module):
         XL, token = EdgePrologueFn.apply(P, ln.weight, ln.bias, W, b, pfu.lin_proj.weight, ln.eps, pos)
         pts, view, glob = gfu.forward_fused(XL, plans, prev_pt, prev_view, prev_glob, xl_sorted=pos is not None,
                                             carry=carry, pfu=pfu, nxt=nxt)
-        sp, sv, sg = pfu.node_terms(pts, view, glob, *((carry.pop("SA", None), carry.pop("SV", None))
-                                                         if carry is not None else (None, None)))
+        sp, sv, sg = pfu.node_terms(pts, view, glob, *((carry.pop("SA", None), carry.pop("SV", None),
+                                                          carry.pop("SG", None))
+                                                         if carry is not None else (None, None, None)))
         shard = plans.get("_shard")
         sv, sg = replicated_to_local(sv, shard), replicated_to_local(sg, shard)
         P_new = EdgeEpilogueFn.apply(P, P0 if self.add_skipconn_from_init_projfeat else None, token, sp, sv, sg,

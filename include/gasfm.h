@@ -338,6 +338,22 @@ int gasfm_view_hub_bwd(const float* v, const float* rs, int64_t m, int32_t D, co
                        const float* Wr, const float* dsv, const float* dxr, const float* dxl, float* dacc,
                        float* part, float* scratch, void* stream);
 
+/* Batched single-row problems in ONE launch each way (the global hub: the LayerNorm -> Linear
+ * consumers of a block's global row, then the two lin_r rows).  Arrays of nprob (<= 4) entries,
+ * one per problem, as for gasfm_gvec_fwd / gasfm_gvec_bwd; null entries mean "absent" where the
+ * single-problem calls accept null.  Backward: per-problem dW / db / dgamma / dbeta and partials
+ * part[q] ([gasfm_gvec_bwd_chunks(N[q]) x K[q]]), then ngroups (<= 4) groups of problems that share
+ * their input row: group g covers problems [g_p0[g], g_p0[g] + g_np[g]) and writes
+ * dx[g] = dres[g] (may be null) + the sum of the group's backward terms. */
+int gasfm_gvec_multi_fwd(int32_t nprob, const float* const* x, const float* const* ln_w, const float* const* ln_b,
+                         const float* const* W, const float* const* b, const float* const* res, float* const* y,
+                         const int32_t* K, const int32_t* N, float eps, void* stream);
+int gasfm_gvec_multi_bwd(int32_t nprob, const float* const* dy, const float* const* x, const float* const* ln_w,
+                         const float* const* ln_b, const float* const* W, const int32_t* K, const int32_t* N,
+                         float* const* dW, float* const* db, float* const* dgam, float* const* dbet,
+                         float* const* part, int32_t ngroups, const int32_t* g_p0, const int32_t* g_np,
+                         const float* const* dres, float* const* dx, float eps, void* stream);
+
 /* ---- calibrated camera head (baseNet.py:38-56, rot_representation 'quat') ----
  * P[c] = [R(q) | t] (3 x 4, row-major) from x[c] = (r, i, j, k, tx, ty, tz) (row stride ldx);
  * R is pytorch3d's quaternion_to_matrix (real part first, normalised by |q|^2).  Backward writes

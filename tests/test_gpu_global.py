@@ -74,3 +74,35 @@ def test_gvec_dispatch_and_determinism(device):
     for a, b in zip(*outs):
         assert torch.equal(a, b)
     torch.testing.assert_close(outs[0][0], x + lin(F.relu(ln(x))), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("G,V,S", [(2048, 1024, 64), (128, 64, 64)])
+@pytest.mark.parametrize("with_skip", [True, False])
+def test_global_hub_matches_fp64(device, G, V, S, with_skip):
+    """GlobalHubFn (batched gvec launches) vs the fp64 composition of its four consumers."""
+    from gasfm_amd.dense import GlobalHubFn
+    gen = torch.Generator().manual_seed(G + V + with_skip)
+    r = lambda *s, sc=1.0, sh=0.0: torch.randn(*s, generator=gen, dtype=torch.float64) * sc + sh  # noqa: E731
+    ins = [r(1, G, sc=2, sh=0.1), r(G, sc=0.3, sh=1), r(G, sc=0.2), r(32, G, sc=G ** -0.5),
+           r(G, sc=0.3, sh=1), r(G, sc=0.2), r(V, G, sc=G ** -0.5), r(V, sc=0.1),
+           r(G, sc=0.3, sh=1), r(G, sc=0.2), r(S, G, sc=G ** -0.5), r(S, sc=0.1),
+           r(V, V, sc=V ** -0.5), r(V, sc=0.1), r(S, S, sc=S ** -0.5), r(S, sc=0.1)]
+    grads = [r(1, G) if with_skip else None, r(1, 32), r(1, V), r(1, S)]
+    ref = [t.clone().requires_grad_(True) for t in ins]
+    g, gA, bA, WA, gB, bB, WB, bWB, gC, bC, WC, bWC, WD, bD, WE, bE = ref
+    ln = lambda x, w, b: F.relu(F.layer_norm(x, (G,), w, b, 1e-5))  # noqa: E731
+    outs64 = (g, F.linear(ln(g, gA, bA), WA), F.linear(F.linear(ln(g, gB, bB), WB, bWB), WD, bD),
+              F.linear(F.linear(ln(g, gC, bC), WC, bWC), WE, bE))
+    torch.autograd.backward([o for o, d in zip(outs64, grads) if d is not None], [d for d in grads if d is not None])
+    got = [t.float().to(device).requires_grad_(True) for t in ins]
+    outs = GlobalHubFn.apply(*got, 1e-5)
+    for name, o, r64 in zip(("skip", "SG", "XRv", "XRp"), outs, outs64):
+        torch.testing.assert_close(o.double().cpu(), r64.detach(), rtol=0, atol=2e-5 * r64.abs().max().item() + 1e-5,
+                                   msg=name)
+    torch.autograd.backward([o for o, d in zip(outs, grads) if d is not None],
+                            [d.float().to(device) for d in grads if d is not None])
+    names = ("g", "gA", "bA", "WA", "gB", "bB", "WB", "bWB", "gC", "bC", "WC", "bWC", "WD", "bD", "WE", "bE")
+    for name, a, r64 in zip(names, got, ref):
+        ga, gr = a.grad.double().cpu(), r64.grad
+        err = (ga - gr).norm().item()
+        assert err <= 1e-4 * gr.norm().item() + 1e-6, f"{name}: {err:.3e} vs |ref| {gr.norm().item():.3e}"
