@@ -43,6 +43,13 @@ def main():
     print(f"self device time total {tot / 1e3:.2f} ms")
     for e in ev[:args.rows]:
         print(f"{e.self_device_time_total / 1e3:7.3f} ms {e.count:5d}x  {e.key[:60]:60s} {str(e.input_shapes)[:90]}")
+    # aten ops that launch device work, by launch count (the per-launch floor dominates small ops)
+    ops = [e for e in prof.key_averages(group_by_input_shape=True)
+           if e.key.startswith("aten::") and e.device_time_total > 0]
+    ops.sort(key=lambda e: -e.count)
+    print("\naten ops by count (with device time):")
+    for e in ops[:args.rows]:
+        print(f"{e.count:5d}x {e.device_time_total / 1e3:7.3f} ms  {e.key[:40]:40s} {str(e.input_shapes)[:100]}")
 
 
 if __name__ == "__main__":
