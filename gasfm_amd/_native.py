@@ -73,6 +73,10 @@ _SIGS = {
                                     _vp, _vp, _f32, _vp]),
     "gasfm_pose_fwd": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "gasfm_pose_bwd": (_i32, [_vp, _i64, _i64, _vp, _vp, _i64, _vp]),
+    "gasfm_esfm_part_rows": (_i32, [_i64]),
+    "gasfm_esfm_fwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _vp, _vp]),
+    "gasfm_esfm_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _i32, _i32,
+                              _vp, _vp, _vp, _vp, _vp]),
     "gasfm_point_tail_part_shape": (_i32, [_i64, _i32, _vp]),
     "gasfm_point_hub_part_shape": (_i32, [_i64, _i32, _i32, _vp]),
     "gasfm_point_tail_fwd": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
@@ -473,6 +477,43 @@ def pose_bwd(x, dP, dx):
     _req(dP, "dP")
     check(lib().gasfm_pose_bwd(_p(x), x.stride(0), x.shape[0], _p(dP), _p(dx), dx.stride(0), _stream(x)),
           "gasfm_pose_bwd")
+
+
+# ---------------------------------------------------------------- ESFMLoss (esfm_loss.hip)
+def _i32vec(t, name):
+    if not t.is_cuda or t.dtype != torch.int32 or t.dim() != 1 or not t.is_contiguous():
+        raise TypeError(f"{name}: expected a contiguous int32 CUDA vector")
+
+
+def esfm_part_rows(E):
+    return lib().gasfm_esfm_part_rows(E)
+
+
+def esfm_fwd(cam, pt, vals, P, X, margin, hinge_w, hinge, part):
+    E, n = cam.shape[0], X.shape[1]
+    _i32vec(cam, "cam"), _i32vec(pt, "pt")
+    _req(vals, "vals", 2), _req(P, "P", 12), _req(X, "pts3D", n)
+    if X.shape[0] != 4 or pt.shape[0] != E or vals.shape[0] != E:
+        raise ValueError("esfm_fwd: expected pts3D [4, n] and E-long cam / pt / values")
+    st = lib().gasfm_esfm_fwd(_p(cam), _p(pt), _p(vals), E, _p(P), _p(X), n, margin, hinge_w, int(hinge), _p(part),
+                              _stream(X))
+    check(st, "gasfm_esfm_fwd")
+
+
+def esfm_bwd(cptr, pptr, perm, cam, pt, vals, P, X, margin, hinge_w, hinge, equalize, valid_only, dloss, tot, dP,
+             dX):
+    E, n, m = cam.shape[0], X.shape[1], P.shape[0]
+    for t, name in ((cptr, "cam_ptr"), (pptr, "pt_ptr"), (cam, "cam"), (pt, "pt")):
+        _i32vec(t, name)
+    if perm is not None:
+        _i32vec(perm, "perm")
+    if cptr.shape[0] != m + 1 or pptr.shape[0] != n + 1 or (perm is not None and perm.shape[0] != E):
+        raise ValueError("esfm_bwd: CSR shapes do not match m / n / E")
+    _req(dP, "dP", 12), _req(dX, "dX", n)
+    st = lib().gasfm_esfm_bwd(_p(cptr), m, _p(pptr), _p(perm) if perm is not None else None, _p(cam), _p(pt),
+                              _p(vals), E, _p(P), _p(X), n, margin, hinge_w, int(hinge), int(equalize),
+                              int(valid_only), _p(dloss), _p(tot), _p(dP), _p(dX), _stream(X))
+    check(st, "gasfm_esfm_bwd")
 
 
 # ---------------------------------------------------------------- batched single-row problems (global hub)

@@ -1,0 +1,219 @@
+// ESFMLoss (code/loss_functions.py:85-123) as sparse per-edge kernels, gfx950.
+//
+// The reference forms the dense projections Ps @ pts3D ([m, 3, n]: 2.4 GB at config 4), masks them
+// with the dense valid-observation matrix and averages; its backward goes through a gradient hook
+// on the [m, 3, n] tensor.  Here every quantity is per visibility edge e = (c, p) (the same E
+// edges the network runs on, values[e] = the normalised measurement = norm_M at (c, p)):
+//   y_e   = P_c [X_p; w_p]                                        (3-vector)
+//   pos_e = y_z >= margin (hinge) or |y_z| >= margin (no hinge)    (geo_utils.py:721-726)
+//   l_e   = pos_e ? || y_xy / y_z - m_e || : (margin - y_z) * hinge_w
+//   loss  = sum_e l_e / E
+// Backward with the reference's hook (pts_grad_equalization_pre_perspective_divide,
+// loss_functions.py:104-113): with G_e = dloss * dl_e/dy_e / E,
+//   valid-only:  G'_e = pos_e ? normalize(G_e) / max(1, #pos) : G_e
+//   otherwise:   G'_e = normalize(G_e) / E
+//   none:        G'_e = G_e
+// then dP_c = sum_{e in c} G'_e [X_p; w_p]^T (one workgroup per camera, edges in order) and
+// d[X_p; w_p] = sum_{e in p} P_c^T G'_e (one thread per point, through the point CSR).
+// Deterministic: fixed-order sums, no atomics.
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+#include "lanes.hpp"
+
+namespace gasfm {
+namespace {
+
+constexpr int kT = 256;
+
+struct EsfmConf {
+  float margin, hinge_w;
+  int hinge, equalize, valid_only;
+};
+
+struct Proj {
+  float y[3];
+  bool pos;
+};
+
+__device__ __forceinline__ Proj project(const float* __restrict__ P, const float* __restrict__ X, int64_t n,
+                                        int c, int p, const EsfmConf& k) {
+  const float* pc = P + int64_t(c) * 12;
+  const float x0 = X[p], x1 = X[n + p], x2 = X[2 * n + p], x3 = X[3 * n + p];
+  Proj r;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) r.y[i] = fmaf(pc[4 * i], x0, fmaf(pc[4 * i + 1], x1, fmaf(pc[4 * i + 2], x2, pc[4 * i + 3] * x3)));
+  r.pos = k.hinge ? (r.y[2] >= k.margin) : (fabsf(r.y[2]) >= k.margin);
+  return r;
+}
+
+// per-edge loss value
+__device__ __forceinline__ float edge_value(const Proj& r, float mx, float my, const EsfmConf& k) {
+  if (!r.pos) return (k.margin - r.y[2]) * k.hinge_w;
+  const float u = r.y[0] / r.y[2] - mx, v = r.y[1] / r.y[2] - my;
+  return sqrtf(u * u + v * v);
+}
+
+// G'_e (see the header); scale = dloss / E, inv_pos = 1 / max(1, #pos)
+__device__ __forceinline__ void edge_grad(const Proj& r, float mx, float my, const EsfmConf& k, float scale,
+                                          float inv_pos, float inv_e, float (&g)[3]) {
+  float d[3];
+  if (r.pos) {
+    const float z = r.y[2], iz = 1.f / z;
+    const float u = r.y[0] * iz - mx, v = r.y[1] * iz - my;
+    const float err = sqrtf(u * u + v * v);
+    const float s = err > 0.f ? scale / err : 0.f;  // d||.||/d(u,v) = (u, v)/err (0 at err = 0, as torch)
+    d[0] = s * u * iz;
+    d[1] = s * v * iz;
+    d[2] = -s * (u * r.y[0] + v * r.y[1]) * iz * iz;
+  } else {
+    d[0] = d[1] = 0.f;
+    d[2] = -k.hinge_w * scale;
+  }
+  if (k.equalize && (r.pos || !k.valid_only)) {
+    const float nrm = sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    const float f = (k.valid_only ? inv_pos : inv_e) / fmaxf(nrm, 1e-12f);  // F.normalize eps
+#pragma unroll
+    for (int i = 0; i < 3; ++i) d[i] *= f;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) g[i] = d[i];
+}
+
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  v = group_sum<64>(v);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh[wave] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int w = 0; w < kT / 64; ++w) s += sh[w];
+  return s;
+}
+
+// per-workgroup partial (sum of l_e, count of pos_e) over a grid-stride slice of the edges
+__global__ __launch_bounds__(kT) void esfm_fwd_kernel(const int32_t* __restrict__ cam,
+                                                      const int32_t* __restrict__ pt,
+                                                      const float* __restrict__ vals, int64_t E,
+                                                      const float* __restrict__ P, const float* __restrict__ X,
+                                                      int64_t n, EsfmConf k, float* __restrict__ part) {
+  __shared__ float sh[kT / 64];
+  float s = 0.f, cnt = 0.f;
+  for (int64_t e = int64_t(blockIdx.x) * kT + threadIdx.x; e < E; e += int64_t(gridDim.x) * kT) {
+    const float2 m = reinterpret_cast<const float2*>(vals)[e];
+    const Proj r = project(P, X, n, cam[e], pt[e], k);
+    s += edge_value(r, m.x, m.y, k);
+    cnt += r.pos ? 1.f : 0.f;
+  }
+  s = block_sum(s, sh);
+  cnt = block_sum(cnt, sh);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = s;
+    part[2 * blockIdx.x + 1] = cnt;
+  }
+}
+
+// dP_c: one workgroup per camera over its contiguous edge range [cptr[c], cptr[c+1])
+__global__ __launch_bounds__(kT) void esfm_bwd_cam_kernel(const int32_t* __restrict__ cptr,
+                                                          const int32_t* __restrict__ cam,
+                                                          const int32_t* __restrict__ pt,
+                                                          const float* __restrict__ vals, int64_t E,
+                                                          const float* __restrict__ P, const float* __restrict__ X,
+                                                          int64_t n, EsfmConf k, const float* __restrict__ dloss,
+                                                          const float* __restrict__ tot, float* __restrict__ dP) {
+  __shared__ float sh[kT / 64 * 12];
+  const int c = blockIdx.x;
+  const float inv_e = 1.f / float(E), scale = dloss[0] * inv_e, inv_pos = 1.f / fmaxf(1.f, tot[1]);
+  float acc[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) acc[i] = 0.f;
+  for (int e = cptr[c] + threadIdx.x; e < cptr[c + 1]; e += kT) {
+    const float2 m = reinterpret_cast<const float2*>(vals)[e];
+    const int p = pt[e];
+    const Proj r = project(P, X, n, c, p, k);
+    float g[3];
+    edge_grad(r, m.x, m.y, k, scale, inv_pos, inv_e, g);
+    const float xs[4] = {X[p], X[n + p], X[2 * n + p], X[3 * n + p]};
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[4 * i + j] = fmaf(g[i], xs[j], acc[4 * i + j]);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) acc[i] = group_sum<64>(acc[i]);
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < 12; ++i) sh[wave * 12 + i] = acc[i];
+  __syncthreads();
+  if (threadIdx.x < 12) {
+    float s = 0.f;
+    for (int w = 0; w < kT / 64; ++w) s += sh[w * 12 + threadIdx.x];
+    dP[int64_t(c) * 12 + threadIdx.x] = s;
+  }
+}
+
+// d pts3D[:, p]: one thread per point over its edges in CSR order (perm: edge ids)
+__global__ __launch_bounds__(kT) void esfm_bwd_pt_kernel(const int32_t* __restrict__ pptr,
+                                                         const int32_t* __restrict__ perm,
+                                                         const int32_t* __restrict__ cam,
+                                                         const float* __restrict__ vals, int64_t E,
+                                                         const float* __restrict__ P, const float* __restrict__ X,
+                                                         int64_t n, EsfmConf k, const float* __restrict__ dloss,
+                                                         const float* __restrict__ tot, float* __restrict__ dX) {
+  const int64_t p = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (p >= n) return;
+  const float inv_e = 1.f / float(E), scale = dloss[0] * inv_e, inv_pos = 1.f / fmaxf(1.f, tot[1]);
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int q = pptr[p]; q < pptr[p + 1]; ++q) {
+    const int e = perm ? perm[q] : q;
+    const float2 m = reinterpret_cast<const float2*>(vals)[e];
+    const int c = cam[e];
+    const Proj r = project(P, X, n, c, int(p), k);
+    float g[3];
+    edge_grad(r, m.x, m.y, k, scale, inv_pos, inv_e, g);
+    const float* pc = P + int64_t(c) * 12;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = fmaf(pc[j], g[0], fmaf(pc[4 + j], g[1], fmaf(pc[8 + j], g[2], a[j])));
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dX[j * n + p] = a[j];
+}
+
+}  // namespace
+}  // namespace gasfm
+
+using namespace gasfm;
+
+extern "C" int32_t gasfm_esfm_part_rows(int64_t E) {
+  const int64_t b = (E + kT - 1) / kT;
+  return int32_t(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+}
+
+extern "C" int gasfm_esfm_fwd(const int32_t* cam, const int32_t* pt, const float* vals, int64_t E, const float* P,
+                              const float* X, int64_t n, float margin, float hinge_w, int32_t hinge, float* part,
+                              void* stream) {
+  GASFM_REQUIRE(E > 0 && n > 0, "gasfm_esfm_fwd: E=%lld n=%lld", (long long)E, (long long)n);
+  GASFM_REQUIRE(cam && pt && vals && P && X && part, "gasfm_esfm_fwd: null pointer");
+  GASFM_REQUIRE((reinterpret_cast<uintptr_t>(vals) & 7) == 0, "gasfm_esfm_fwd: vals must be 8-byte aligned");
+  const EsfmConf k{margin, hinge_w, hinge, 0, 0};
+  hipLaunchKernelGGL(esfm_fwd_kernel, dim3(gasfm_esfm_part_rows(E)), dim3(kT), 0,
+                     reinterpret_cast<hipStream_t>(stream), cam, pt, vals, E, P, X, n, k, part);
+  return launch_status("gasfm_esfm_fwd");
+}
+
+extern "C" int gasfm_esfm_bwd(const int32_t* cptr, int32_t m, const int32_t* pptr, const int32_t* perm,
+                              const int32_t* cam, const int32_t* pt, const float* vals, int64_t E, const float* P,
+                              const float* X, int64_t n, float margin, float hinge_w, int32_t hinge,
+                              int32_t equalize, int32_t valid_only, const float* dloss, const float* tot, float* dP,
+                              float* dX, void* stream) {
+  GASFM_REQUIRE(E > 0 && n > 0 && m > 0, "gasfm_esfm_bwd: E=%lld m=%d n=%lld", (long long)E, m, (long long)n);
+  GASFM_REQUIRE(cptr && pptr && cam && pt && vals && P && X && dloss && tot && dP && dX, "gasfm_esfm_bwd: null pointer");
+  const EsfmConf k{margin, hinge_w, hinge, equalize, valid_only};
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(esfm_bwd_cam_kernel, dim3(m), dim3(kT), 0, st, cptr, cam, pt, vals, E, P, X, n, k, dloss, tot,
+                     dP);
+  hipLaunchKernelGGL(esfm_bwd_pt_kernel, dim3(unsigned((n + kT - 1) / kT)), dim3(kT), 0, st, pptr, perm, cam, vals,
+                     E, P, X, n, k, dloss, tot, dX);
+  return launch_status("gasfm_esfm_bwd");
+}

@@ -1,0 +1,105 @@
+"""ESFMLoss over the visibility edges (csrc/esfm_loss.hip).
+
+Drop-in for the reference's ``loss_functions.ESFMLoss`` (code/loss_functions.py:69-123): same
+constructor (reads ``loss.infinity_pts_margin``, ``loss.pts_grad_equalization_pre_perspective_divide``,
+``loss.normalize_grad_wrt_valid_projections_only``, ``loss.hinge_loss``, ``loss.hinge_loss_weight``
+and asserts both heads are enabled), same ``forward(pred_dict, data, epoch=None)`` returning the
+scalar loss, and the same gradients, including the ones the reference's gradient hook on the
+projections imposes (loss_functions.py:104-113).
+
+The reference projects every point into every camera (``Ps @ pts3D``: [m, 3, n], 2.4 GB at
+m = 1000, n = 200k) and masks with the dense valid-observation matrix; here only the E observed
+(camera, point) pairs -- the same edges the network runs on -- are projected:
+  forward   one kernel -> per-workgroup (sum of loss terms, #valid-depth) -> colsum
+  backward  one workgroup per camera (dPs) + one thread per point (dpts3D), no atomics
+``#valid-depth`` stays on the device: the reference's ``.item()`` host sync (loss_functions.py:107)
+is gone, so the loss can sit inside a captured step.
+
+The measurement of edge e is ``data.x.values[e]``: M2sparse(normalize=True) (dataset_utils.py:116)
+stores exactly the entries of ``data.norm_M`` (geo_utils.normalize_M, geo_utils.py:689) at the
+valid positions, in the same cam-major order as ``data.x.indices``.
+"""
+import torch
+
+from . import _native
+
+
+class ESFMLossFn(torch.autograd.Function):
+    """(Ps [m, 3, 4], pts3D [4, n]) -> mean over the edges of the per-edge loss term."""
+
+    @staticmethod
+    def forward(ctx, Ps, pts3D, edges, vals, cam_ptr, pt_ptr, pt_perm, conf):
+        margin, hinge_w, hinge, equalize, valid_only = conf
+        cam, pt = edges
+        m = Ps.shape[0]
+        P = Ps.reshape(m, 12).contiguous()
+        X = pts3D.contiguous()
+        part = torch.empty((_native.esfm_part_rows(cam.shape[0]), 2), dtype=torch.float32, device=X.device)
+        _native.esfm_fwd(cam, pt, vals, P, X, margin, hinge_w, hinge, part)
+        tot = _native.colsum(part)  # (sum of terms, #valid-depth)
+        ctx.save_for_backward(P, X, cam, pt, vals, cam_ptr, pt_ptr, pt_perm, tot)
+        ctx.conf = conf
+        return tot[0] / cam.shape[0]
+
+    @staticmethod
+    def backward(ctx, dloss):
+        P, X, cam, pt, vals, cam_ptr, pt_ptr, pt_perm, tot = ctx.saved_tensors
+        margin, hinge_w, hinge, equalize, valid_only = ctx.conf
+        dP, dX = torch.empty_like(P), torch.empty_like(X)
+        dloss = dloss.reshape(1).to(torch.float32).contiguous()
+        _native.esfm_bwd(cam_ptr, pt_ptr, pt_perm, cam, pt, vals, P, X, margin, hinge_w, hinge, equalize, valid_only,
+                         dloss, tot, dP, dX)
+        return dP.view(-1, 3, 4), dX, None, None, None, None, None, None
+
+
+def _edge_tensors(data):
+    """int32 (cam, pt), contiguous float32 values and the camera / point CSRs of the network's own
+    plans (proj2view: camera segments over the cam-major edges; proj2scenepoint: point segments
+    with perm = edge ids in point order).  Cached on the proj2view plan, which is per device."""
+    gw = data.graph_wrappers
+    pv, ps = gw["proj2view"].plan, gw["proj2scenepoint"].plan
+    cache = getattr(pv, "_esfm_edges", None)
+    if cache is None:
+        if pv.perm is not None:
+            raise ValueError("ESFMLoss: proj2view plan must cover cam-major sorted edges")
+        idx = data.x.indices
+        cache = (idx[0].to(torch.int32).contiguous(), idx[1].to(torch.int32).contiguous())
+        pv._esfm_edges = cache
+    vals = data.x.values
+    if vals.dtype != torch.float32 or not vals.is_contiguous():
+        vals = vals.float().contiguous()
+    return cache, vals, pv.seg_ptr, ps.seg_ptr, ps.perm
+
+
+class ESFMLoss(torch.nn.Module):
+    def __init__(self, conf):
+        super().__init__()
+        assert conf.get_bool("model.view_head.enabled", default=False)
+        assert conf.get_bool("model.scenepoint_head.enabled", default=False)
+        self.infinity_pts_margin = conf.get_float("loss.infinity_pts_margin")
+        self.pts_grad_equalization_pre_perspective_divide = conf.get_bool(
+            "loss.pts_grad_equalization_pre_perspective_divide")
+        self.normalize_grad_wrt_valid_projections_only = False
+        if self.pts_grad_equalization_pre_perspective_divide:
+            self.normalize_grad_wrt_valid_projections_only = conf.get_bool(
+                "loss.normalize_grad_wrt_valid_projections_only")
+        self.hinge_loss = conf.get_bool("loss.hinge_loss")
+        self.hinge_loss_weight = conf.get_float("loss.hinge_loss_weight") if self.hinge_loss else 0
+
+    def kernel_conf(self):
+        return (float(self.infinity_pts_margin), float(self.hinge_loss_weight), bool(self.hinge_loss),
+                bool(self.pts_grad_equalization_pre_perspective_divide),
+                bool(self.normalize_grad_wrt_valid_projections_only))
+
+    def forward(self, pred_dict, data, epoch=None):
+        Ps, pts3D = pred_dict["Ps_norm"], pred_dict["pts3D"]
+        for t, name, shape in ((Ps, "Ps_norm", (3, 4)), (pts3D, "pts3D", None)):
+            if not t.is_cuda or t.dtype != torch.float32:
+                raise TypeError(f"ESFMLoss: {name} must be a float32 CUDA tensor (no CPU fallback)")
+        if Ps.dim() != 3 or tuple(Ps.shape[1:]) != (3, 4) or pts3D.dim() != 2 or pts3D.shape[0] != 4:
+            raise ValueError(f"ESFMLoss: expected Ps_norm [m, 3, 4] and pts3D [4, n], got {tuple(Ps.shape)}, "
+                             f"{tuple(pts3D.shape)}")
+        edges, vals, cam_ptr, pt_ptr, pt_perm = _edge_tensors(data)
+        if edges[0].shape[0] == 0:
+            raise ValueError("ESFMLoss: no valid observations (the reference's mean would be NaN)")
+        return ESFMLossFn.apply(Ps, pts3D, edges, vals, cam_ptr, pt_ptr, pt_perm, self.kernel_conf())

@@ -361,6 +361,27 @@ int gasfm_gvec_multi_bwd(int32_t nprob, const float* const* dy, const float* con
 int gasfm_pose_fwd(const float* x, int64_t ldx, int64_t m, float* P, void* stream);
 int gasfm_pose_bwd(const float* x, int64_t ldx, int64_t m, const float* dP, float* dx, int64_t lddx, void* stream);
 
+/* ---- ESFMLoss over the visibility edges (esfm_loss.hip) ----
+ * Replaces ESFMLoss.forward (code/loss_functions.py:85-123) and the gradient hook it registers
+ * (loss_functions.py:104-113), which form the dense projections Ps @ pts3D [m, 3, n].  Per edge
+ * e = (cam[e], pt[e]) with measurement vals[e] (= norm_M at that (camera, point)):
+ * y = P[cam] @ pts3D[:, pt] (P: [m, 12] row-major 3x4, pts3D: [4, n] row-major).
+ * Forward writes gasfm_esfm_part_rows(E) rows of (sum of loss terms, count of valid-depth
+ * projections); their column sums are (E * loss, #pos).  Backward reads dloss[0] and
+ * tot = (sum, #pos) from device memory and writes dP [m, 12] (cam_ptr: camera CSR over the
+ * camera-sorted edges) and dpts3D [4, n] (pt_ptr + perm: point CSR, perm = edge ids in point
+ * order, NULL = identity).  equalize / valid_only: pts_grad_equalization_pre_perspective_divide /
+ * normalize_grad_wrt_valid_projections_only; hinge selects the hinge_loss branch
+ * (geo_utils.get_positive_projected_pts_mask, geo_utils.py:721-726). */
+int32_t gasfm_esfm_part_rows(int64_t E);
+int gasfm_esfm_fwd(const int32_t* cam, const int32_t* pt, const float* vals, int64_t E, const float* P,
+                   const float* pts3D, int64_t n, float margin, float hinge_w, int32_t hinge, float* part,
+                   void* stream);
+int gasfm_esfm_bwd(const int32_t* cam_ptr, int32_t m, const int32_t* pt_ptr, const int32_t* perm, const int32_t* cam,
+                   const int32_t* pt, const float* vals, int64_t E, const float* P, const float* pts3D, int64_t n,
+                   float margin, float hinge_w, int32_t hinge, int32_t equalize, int32_t valid_only,
+                   const float* dloss, const float* tot, float* dP, float* dpts3D, void* stream);
+
 /* ---- global node (ONE row): LayerNorm -> ReLU -> Linear (+ residual) ----
  * Replaces the M = 1 aten chains on the global feature vector: norm_and_proj_global2view /
  * _global2scenepoint (layers.py:497-520), both convs' lin_r on those rows (PyG),

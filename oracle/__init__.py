@@ -13,6 +13,8 @@ pyg_gatv2     torch-CPU restatement of PyG ``GATv2Conv`` (the third-party op the
 gasfm_ref     functional fp64/fp32 restatement of ``GraphAttnSfMNet.forward``
               (code/models/graph_attn_sfm.py:117-185 and the layers it calls),
               driven directly by a reference-layout state_dict.
+esfm_loss     dense fp64 restatement of ESFMLoss (code/loss_functions.py:85-123, including
+              its gradient hook) and the same on the E observed pairs only.
 scenes        synthetic scene generators for BASELINE configs 1 and 4 and the
               CPU graph build (M2sparse, dataset_utils.py:116-156).
 

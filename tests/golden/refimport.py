@@ -85,6 +85,7 @@ def load(gatv2_cls=None):
     ns.SceneData = importlib.import_module("datasets.SceneData")
     ns.dataset_utils = importlib.import_module("utils.dataset_utils")
     ns.sparse_utils = importlib.import_module("utils.sparse_utils")
+    ns.loss_functions = importlib.import_module("loss_functions")
     return ns
 
 
@@ -108,6 +109,10 @@ class DictConf:
     def get_int(self, key, default=_MISSING):
         v = self._get(key, default)
         return None if v is None else int(v)
+
+    def get_float(self, key, default=_MISSING):
+        v = self._get(key, default)
+        return None if v is None else float(v)
 
     def get_bool(self, key, default=_MISSING):
         v = self._get(key, default)

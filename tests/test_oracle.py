@@ -130,3 +130,42 @@ def test_functional_full_width_nets(tag, layers):
         out = gasfm_ref.forward(sd, vals, g)
     np.testing.assert_allclose(out["Ps_norm"].numpy(), f["Ps_norm"], rtol=1e-10, atol=1e-12)
     np.testing.assert_allclose(out["pts3D"].numpy(), f["pts3D"], rtol=1e-10, atol=1e-12)
+
+
+# ---------------------------------------------------------------- ESFMLoss (loss_functions.py:85-123)
+def _esfm_case(f, i):
+    margin, eq, vo, hinge, w, dloss = f["variants"][i]
+    return float(margin), bool(eq), bool(vo), bool(hinge), float(w), float(dloss)
+
+
+@pytest.mark.parametrize("i", range(5))
+@pytest.mark.parametrize("form", ["dense", "edges"])
+def test_esfm_loss_restatement_reproduces_reference(i, form):
+    from oracle import esfm_loss
+    f = golden("esfm_loss.npz")
+    margin, eq, vo, hinge, w, dloss = _esfm_case(f, i)
+    m, n = int(f["m"]), int(f["n"])
+    Ps = torch.from_numpy(f["Ps"]).requires_grad_(True)
+    X = torch.from_numpy(f["pts3D"]).requires_grad_(True)
+    cam, pt = torch.from_numpy(f["cam"]), torch.from_numpy(f["pt"])
+    vals = torch.from_numpy(f["values"]).double()
+    if form == "dense":
+        nM, valid = esfm_loss.dense_measurements(cam, pt, vals, m, n)
+        loss = esfm_loss.esfm_loss(Ps, X, nM, valid, margin, hinge, w, eq, vo)
+    else:
+        loss = esfm_loss.esfm_loss_edges(Ps, X, cam, pt, vals, margin, hinge, w, eq, vo)
+    (loss * dloss).backward()
+    np.testing.assert_allclose(loss.item(), f[f"v{i}_loss"], rtol=1e-12)
+    np.testing.assert_allclose(Ps.grad.numpy(), f[f"v{i}_dPs"], rtol=1e-10, atol=1e-13)
+    np.testing.assert_allclose(X.grad.numpy(), f[f"v{i}_dpts3D"], rtol=1e-10, atol=1e-13)
+
+
+def test_esfm_sparse_values_are_norm_M_entries():
+    """x.values (what the HIP loss reads) == the reference's dense norm_M at the valid entries."""
+    f = golden("scene_config1.npz")
+    M, Ns = torch.from_numpy(f["M"]).double(), torch.from_numpy(f["Ns"]).double()
+    m = Ns.shape[0]
+    h = torch.cat([M.reshape(m, 2, -1), torch.ones(m, 1, M.shape[1], dtype=torch.float64)], dim=1)
+    nM = (Ns @ h)[:, :2, :]  # geo_utils.normalize_M
+    idx = torch.from_numpy(f["indices"])
+    np.testing.assert_allclose(nM[idx[0], :, idx[1]].numpy(), f["values"], rtol=1e-6, atol=1e-6)
