@@ -57,6 +57,11 @@ class AttnPlan:
                            attention kernels stream them instead of gathering (xl_sorted).
     items    int32 [I, 4]  (seg, begin, end, slot) work items (see gasfm.h)
     combine  int32 [K, 4]  (seg, slot_begin, slot_count, slot_stride)
+    combine_l1 int32 [K1, 4] first level of the long combines: (row, slot_begin, count, 1)
+                           merges ~sqrt(count) consecutive slots into partial row n_slots + k,
+                           and ``combine`` then merges those rows.  One workgroup per entry
+                           on both levels, so a single-target plan (points -> global: ~4k
+                           slots) is combined by ~64 workgroups instead of one.
     """
 
     def __init__(self, seg_ptr, perm, items, combine, n_slots, num_targets, num_edges, src_rows,
@@ -72,7 +77,10 @@ class AttnPlan:
         self.all_partial = bool(all_partial)
         self.max_piece = int(max_piece)
         self.n_items = int(items.shape[0])
-        self.n_combine = int(combine.shape[0])
+        self.combine, self.combine_l1 = _two_level(combine, self.n_slots)
+        self.n_combine = int(self.combine.shape[0])
+        self.n_l1 = 0 if self.combine_l1 is None else int(self.combine_l1.shape[0])
+        self.n_part_rows = self.n_slots + self.n_l1  # partial rows of both combine levels
         self.tag = None  # graph name (proj2view, proj2scenepoint, ...) for timing / logs
         self.pos = None
         if perm is not None and self.src_rows == self.num_edges:
@@ -114,7 +122,7 @@ class AttnPlan:
 
     def to(self, device, **kwargs):
         ret = copy.copy(self)
-        for k in ("seg_ptr", "perm", "pos", "items", "combine"):
+        for k in ("seg_ptr", "perm", "pos", "items", "combine", "combine_l1"):
             v = getattr(self, k)
             if v is not None:
                 setattr(ret, k, v.to(device, **kwargs))
@@ -126,6 +134,51 @@ class AttnPlan:
 
     def segment_lengths(self):
         return (self.seg_ptr[1:] - self.seg_ptr[:-1]).cpu().numpy()
+
+
+L1_THRESHOLD = 32  # combines of more slots are split into two levels
+
+
+def _two_level(combine, n_slots):
+    """Split combine entries with > L1_THRESHOLD slots into ordered groups of ~sqrt(count).
+
+    Returns (combine, combine_l1); level-1 entry k writes partial row n_slots + k, and the
+    rewritten level-2 entry merges its group rows in order (deterministic)."""
+    c = combine.numpy() if isinstance(combine, torch.Tensor) else np.asarray(combine)
+    if c.size == 0 or int(c[:, 2].max()) <= L1_THRESHOLD:
+        return combine, None
+    assert np.all(c[:, 3] == 1), "plan_work combines use unit slot stride"
+    top, l1 = [], []
+    for seg, b, cnt, st in c.tolist():
+        if cnt <= L1_THRESHOLD:
+            top.append((seg, b, cnt, st))
+            continue
+        g = int(np.ceil(np.sqrt(cnt)))
+        ng = -(-cnt // g)
+        first = n_slots + len(l1)
+        for k in range(ng):
+            lo = b + k * g
+            l1.append((first + k, lo, min(g, b + cnt - lo), 1))
+        top.append((seg, first, ng, 1))
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.int32).reshape(-1, 4)))
+    return t(top), t(l1)
+
+
+def combine_fwd_l1(plan, part, heads, C):
+    """Level-1 merge of packed partial rows (raw) in place: rows [n_slots, n_part_rows)."""
+    if plan.n_l1:
+        HC = heads * C
+        LDP = HC + 2 * heads
+        _native.attn_combine(plan.combine_l1, plan.n_l1, heads, C, part, None, False, part, part[:, HC:],
+                             part[:, HC + heads:], ldOut=LDP, ldStat=LDP)
+
+
+def bwd_combine(plan, part, HC, out):
+    """out[seg] = ordered sum of the plan's partial rows (both levels)."""
+    if plan.n_l1:
+        _native.attn_bwd_combine(plan.combine_l1, plan.n_l1, HC, part, part)
+    if plan.n_combine:
+        _native.attn_bwd_combine(plan.combine, plan.n_combine, HC, part, out)
 
 
 def _check(t, name, rows=None, cols=None):
@@ -155,7 +208,8 @@ def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True, xl_so
     out = torch.empty((N, HC), dtype=torch.float32, device=dev)
     smax = torch.empty((N, heads), dtype=torch.float32, device=dev)
     ssum = torch.empty((N, heads), dtype=torch.float32, device=dev)
-    part = torch.empty((plan.n_slots, HC + 2 * heads), dtype=torch.float32, device=dev) if plan.n_slots else None
+    part = (torch.empty((plan.n_part_rows, HC + 2 * heads), dtype=torch.float32, device=dev)
+            if plan.n_slots else None)
     attf = att.reshape(-1).contiguous()
     timed = KERNEL_TIMER is not None and KERNEL_TIMER(plan.tag, HC)
     if timed:
@@ -167,6 +221,7 @@ def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True, xl_so
         ev[1].record()
         KERNEL_TIMER.events.append(ev)
         KERNEL_TIMER.gathered = plan.perm is not None and not xl_sorted
+    combine_fwd_l1(plan, part, heads, C)
     if plan.n_combine:
         _native.attn_combine(plan.combine, plan.n_combine, heads, C, part, bias, finalize, out, smax, ssum)
     return out, smax, ssum
@@ -185,10 +240,11 @@ def attn_forward_partial(XL, XR, att, plan, heads, slope):
     _check(XL, "XL", plan.src_rows, HC)
     _check(XR, "XR", N if XR.stride(0) else 1, HC)
     LDP = HC + 2 * heads
-    part = torch.empty((max(plan.n_slots, N), LDP), dtype=torch.float32, device=XL.device)
+    part = torch.empty((max(plan.n_part_rows, N), LDP), dtype=torch.float32, device=XL.device)
     attf = att.reshape(-1).contiguous()
     _native.attn_fwd(XL, XR, attf, None, plan.perm, plan.items, plan.n_items, heads, C, slope, False, None, None,
                      None, part)
+    combine_fwd_l1(plan, part, heads, C)
     if plan.n_combine:  # merge split pieces (slots >= N) into rows [0, N), raw
         _native.attn_combine(plan.combine, plan.n_combine, heads, C, part, None, False, part, part[:, HC:],
                              part[:, HC + heads:], ldOut=LDP, ldStat=LDP)
@@ -219,15 +275,14 @@ def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, go
         full = plan.num_edges == XL.shape[0] == plan.src_rows
         dXL = (torch.empty if full else torch.zeros)((XL.shape[0], HC), dtype=torch.float32, device=dev)
     dXR = torch.empty((plan.num_targets, HC), dtype=torch.float32, device=dev)
-    part = torch.empty((plan.n_slots, HC), dtype=torch.float32, device=dev) if plan.n_slots else None
+    part = torch.empty((plan.n_part_rows, HC), dtype=torch.float32, device=dev) if plan.n_slots else None
     n_waves = _native.attn_bwd_waves(plan.n_items, heads, C)
     datt_part = torch.empty((max(n_waves, 1), 2 * HC), dtype=torch.float32, device=dev)
     attf = att.reshape(-1).contiguous()
     if plan.n_items:
         _native.attn_bwd(XL, XR, attf, bias, plan.perm, plan.items, plan.n_items, heads, C, slope, out, smax,
                          ssum, gout, dXL, dXR, part, datt_part, xl_by_position=xl_sorted)
-        if plan.n_combine:
-            _native.attn_bwd_combine(plan.combine, plan.n_combine, HC, part, dXR)
+        bwd_combine(plan, part, HC, dXR)
         tot = _native.colsum(datt_part)
         datt, dbias = tot[:HC], tot[HC:]
     else:

@@ -110,8 +110,38 @@ class AllReduceGrad(torch.autograd.Function):
         return ctx.shard.all_reduce_(g.contiguous().clone()), None
 
 
+class AllReduceGradN(torch.autograd.Function):
+    """Identity forward on several tensors; their gradients are summed over ranks with ONE
+    all-reduce of the concatenation (the view and global terms of the projection update reach
+    the edge backward together)."""
+
+    @staticmethod
+    def forward(ctx, shard, *xs):
+        ctx.shard = shard
+        ctx.shapes = [x.shape for x in xs]
+        ctx.devdtype = (xs[0].device, xs[0].dtype)
+        return tuple(x.view_as(x) for x in xs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        dev, dt = ctx.devdtype
+        flat = torch.cat([(g if g is not None else torch.zeros(sh, device=dev, dtype=dt)).reshape(-1)
+                          for g, sh in zip(gs, ctx.shapes)])
+        ctx.shard.all_reduce_(flat)
+        out, at = [], 0
+        for sh in ctx.shapes:
+            k = int(torch.Size(sh).numel())
+            out.append(flat[at:at + k].view(sh))
+            at += k
+        return (None,) + tuple(out)
+
+
 def replicated_to_local(x, shard):
     return x if shard is None else AllReduceGrad.apply(x, shard)
+
+
+def replicated_to_local_n(shard, *xs):
+    return xs if shard is None else AllReduceGradN.apply(shard, *xs)
 
 
 class ShardedAttentionFn(torch.autograd.Function):

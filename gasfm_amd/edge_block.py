@@ -19,7 +19,7 @@ torch and runs on MFMA through hipBLASLt.
 import torch
 
 from . import _native
-from .attention import attn_backward_raw, attn_forward_partial, attn_forward_raw, combine_partials
+from .attention import attn_backward_raw, attn_forward_partial, attn_forward_raw, bwd_combine, combine_partials
 
 PROJ_SCALE = 0.25  # the "/ 4" of layers.py:945
 
@@ -132,22 +132,20 @@ class EdgeEpilogueFn(torch.autograd.Function):
         pp = edges.plans["proj2scenepoint"]
         # camera side: dSv (+ dWp, dP0) in one pass over the camera work items
         dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
-        part_dsv = torch.empty((max(pc.n_slots, 1), 32), dtype=torch.float32, device=dev)
+        part_dsv = torch.empty((max(pc.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
         dP0 = torch.empty((P.shape[0], 2), dtype=torch.float32, device=dev) if P0 is not None else None
         wg = _native.edge_part_floats(1, P.shape[0], pc.n_items) // (32 * 34)
         part_w = torch.empty((wg, 32 * Wp.shape[1]), dtype=torch.float32, device=dev)
         _native.edge_epilogue_bwd(pc.items, pc.n_items, dPo, P, P0, ln_w, ln_b, ctx.eps, Wp, PROJ_SCALE, dSv,
                                   part_dsv, dP0, part_w)
-        if pc.n_combine:
-            _native.attn_bwd_combine(pc.combine, pc.n_combine, 32, part_dsv, dSv)
+        bwd_combine(pc, part_dsv, 32, dSv)
         dWp = _native.colsum(part_w).view(32, Wp.shape[1])
         dSg = _native.colsum(dSv)          # == d bias_proj: every edge belongs to one camera
         # point side: dSp = per-point sum of dP'/4 through the point permutation
         dSp = torch.empty((edges.n, 32), dtype=torch.float32, device=dev)
-        part_dsp = torch.empty((max(pp.n_slots, 1), 32), dtype=torch.float32, device=dev)
+        part_dsp = torch.empty((max(pp.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
         _native.segment_rowsum(pp.items, pp.n_items, pp.perm, dPo, PROJ_SCALE, dSp, part_dsp)
-        if pp.n_combine:
-            _native.attn_bwd_combine(pp.combine, pp.n_combine, 32, part_dsp, dSp)
+        bwd_combine(pp, part_dsp, 32, dSp)
         return (None, dP0, dPo, dSp, dSv, dSg.view(ctx.sg_shape), dWp, dSg.clone(), None, None, None, None)
 
 
@@ -201,20 +199,18 @@ class Block0EpilogueFn(torch.autograd.Function):
         E = P.shape[0]
         pc, pp = edges.plans["proj2view"], edges.plans["proj2scenepoint"]
         dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
-        part_dsv = torch.empty((max(pc.n_slots, 1), 32), dtype=torch.float32, device=dev)
+        part_dsv = torch.empty((max(pc.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
         aux = torch.empty((E, 4), dtype=torch.float32, device=dev)
         rows = _native.edge0_part_rows(1, E, pc.n_items)
         part = torch.empty((rows, 164), dtype=torch.float32, device=dev)
         _native.edge0_epilogue_bwd(pc.items, pc.n_items, dPo, P, lna_w, lna_b, lnb_w, lnb_b, ctx.eps,
                                    Wp.contiguous(), Wsk.contiguous(), PROJ_SCALE, dSv, part_dsv, aux, part)
-        if pc.n_combine:
-            _native.attn_bwd_combine(pc.combine, pc.n_combine, 32, part_dsv, dSv)
+        bwd_combine(pc, part_dsv, 32, dSv)
         tot = _native.colsum(part)
         dSg = _native.colsum(dSv)
         dSp = torch.empty((edges.n, 32), dtype=torch.float32, device=dev)
-        part_dsp = torch.empty((max(pp.n_slots, 1), 32), dtype=torch.float32, device=dev)
+        part_dsp = torch.empty((max(pp.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
         _native.segment_rowsum(pp.items, pp.n_items, pp.perm, dPo, PROJ_SCALE, dSp, part_dsp)
-        if pp.n_combine:
-            _native.attn_bwd_combine(pp.combine, pp.n_combine, 32, part_dsp, dSp)
+        bwd_combine(pp, part_dsp, 32, dSp)
         return (None, aux, dSp, dSv, dSg.view(ctx.sg_shape), tot[:64].view(32, 2), dSg.clone(), None, None,
                 tot[160:162], tot[162:164], tot[64:128].view(32, 2), tot[128:160], None, None)

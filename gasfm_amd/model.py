@@ -38,6 +38,14 @@ def replicated_to_local(x, shard):
     return AllReduceGrad.apply(x, shard)
 
 
+def replicated_to_local_n(shard, *xs):
+    """Several replicated tensors consumed locally: one gradient all-reduce for all of them."""
+    if shard is None:
+        return xs
+    from .distributed import AllReduceGradN
+    return AllReduceGradN.apply(shard, *xs)
+
+
 class _LazySharded:
     """ShardedAttentionFn, imported on first use (keeps torch.distributed out of the 1-GPU import path)."""
 
@@ -494,7 +502,7 @@ class GraphAttnSfMLayer(Module):
                                                           carry.pop("SG", None))
                                                          if carry is not None else (None, None, None)))
         shard = plans.get("_shard")
-        sv, sg = replicated_to_local(sv, shard), replicated_to_local(sg, shard)
+        sv, sg = replicated_to_local_n(shard, sv, sg)
         sk = self.skip_projection.lin_proj
         P_new = Block0EpilogueFn.apply(P.contiguous(), token, sp, sv, sg, pfu.lin_proj.weight, pfu.lin_proj.bias,
                                        la.weight, la.bias, lb.weight, lb.bias, sk.weight, sk.bias, la.eps, edges)
@@ -514,7 +522,7 @@ class GraphAttnSfMLayer(Module):
                                                           carry.pop("SG", None))
                                                          if carry is not None else (None, None, None)))
         shard = plans.get("_shard")
-        sv, sg = replicated_to_local(sv, shard), replicated_to_local(sg, shard)
+        sv, sg = replicated_to_local_n(shard, sv, sg)
         P_new = EdgeEpilogueFn.apply(P, P0 if self.add_skipconn_from_init_projfeat else None, token, sp, sv, sg,
                                      pfu.lin_proj.weight, pfu.lin_proj.bias, ln.weight, ln.bias, ln.eps, edges)
         return P_new, pts, view, glob
@@ -539,7 +547,7 @@ class GraphAttnSfMLayer(Module):
         x_cat = torch.cat([P_hat, P0], dim=1) if self.add_skipconn_from_init_projfeat else P_hat
         sp, sv, sg = pfu.node_terms(pts, view, glob)
         shard = plans.get("_shard")
-        sv, sg = replicated_to_local(sv, shard), replicated_to_local(sg, shard)
+        sv, sg = replicated_to_local_n(shard, sv, sg)
         delta = edge_ops.projection_update(x_cat, pfu.lin_proj, sp, sv, sg, edges)
         if pfu.n_hidden_layers_proj_update > 0:
             delta = pfu.mlp(F.relu(delta))

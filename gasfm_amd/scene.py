@@ -154,8 +154,10 @@ def build_graph_wrappers(indices, m, n, max_piece=None):
     s2g = AxialAggregationGraphWrapper(1, n, 1, torch.stack([torch.zeros_like(vp), vp]).to(dev), build_plan=False)
     # global graphs: sources are view / point feature rows selected through the plan's perm
     v2g.plan = AttnPlan.from_targets(torch.zeros_like(vv), 1, src=vv, src_rows=m, max_piece=8)
+    # ~4k pieces of >= 16 points: every wave streams a few 16-edge steps (a 256-edge piece is
+    # 16 dependent load rounds, ~27 us whatever n is); the two-level combine merges the pieces
     s2g.plan = AttnPlan.from_targets(torch.zeros_like(vp), 1, src=vp, src_rows=n,
-                                     max_piece=max(256, -(-vp.shape[0] // 1024)))
+                                     max_piece=min(256, max(16, -(-vp.shape[0] // 4096))))
     out = {"proj2view": p2v, "proj2scenepoint": p2s, "view2global": v2g, "scenepoint2global": s2g}
     for name, w in out.items():
         w.plan.tag = name

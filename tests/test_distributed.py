@@ -107,7 +107,12 @@ def _worker_collectives(rank, world, port, q):
         x = torch.ones(4, requires_grad=True)
         y = gd.AllReduceGrad.apply(x, shard)
         (y * (rank + 1)).sum().backward()
-        q.put((rank, g.tolist(), x.grad.tolist()))
+        # several tensors, one all-reduce; b's output is unused on rank 0 (None gradient)
+        a = torch.ones(2, 3, requires_grad=True)
+        b = torch.ones(5, requires_grad=True)
+        ya, yb = gd.AllReduceGradN.apply(shard, a, b)
+        ((ya * (rank + 1)).sum() + (yb.sum() * 10.0 if rank == 1 else 0.0)).backward()
+        q.put((rank, g.tolist(), x.grad.tolist(), a.grad.tolist(), b.grad.tolist()))
     finally:
         dist.destroy_process_group()
 
@@ -119,14 +124,15 @@ def test_collective_wrappers_gloo_world2():
     procs = [ctx.Process(target=_worker_collectives, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict((r, (g, gr)) for r, g, gr in (q.get(timeout=120) for _ in procs))
+    res = dict((r, (g, gr, ga, gb)) for r, g, gr, ga, gb in (q.get(timeout=120) for _ in procs))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     for r in range(2):
-        g, gr = res[r]
+        g, gr, ga, gb = res[r]
         assert g == [[1.0, 1.0]] * 3 + [[2.0, 2.0]] * 3  # rank-ordered gather
         assert gr == [3.0] * 4  # gradient summed over ranks (1 + 2)
+        assert ga == [[3.0] * 3] * 2 and gb == [10.0] * 5  # AllReduceGradN: one all-reduce, None -> 0
 
 
 def _worker_sharded_model(rank, world, port, q):

@@ -224,3 +224,32 @@ def test_pyg_call_form_repeated_sources(device):
     close(out, r_out)
     (r_out * g.double().cpu()).sum().backward()
     close(x.grad, xd.grad, atol=2e-5)
+
+
+@pytest.mark.parametrize("H,C,E,max_piece", [(4, 16, 20000, 16), (4, 256, 1000, 8), (4, 8, 5000, 4)])
+def test_single_target_two_level_combine(device, H, C, E, max_piece):
+    """Global-style star (every source -> one target through a source permutation) split into
+    hundreds of pieces: both combine levels in the forward and in the dXR backward sum."""
+    from gasfm_amd.attention import AttnPlan, GatAttentionFn
+    rng = np.random.default_rng(E + C)
+    HC = H * C
+    rows = E + 37
+    src = torch.from_numpy(np.sort(rng.choice(rows, size=E, replace=False)).astype(np.int64))
+    dst = torch.zeros(E, dtype=torch.int64)
+    plan = AttnPlan.from_targets(dst, 1, src=src, src_rows=rows, max_piece=max_piece).to(device)
+    assert plan.n_l1 > 1 and plan.n_part_rows == plan.n_slots + plan.n_l1
+    XL = torch.randn(rows, HC, device=device, requires_grad=True)
+    XR = torch.randn(1, HC, device=device, requires_grad=True)
+    att = (torch.randn(H, C, device=device) / C ** 0.5).requires_grad_(True)
+    bias = torch.randn(HC, device=device, requires_grad=True)
+    out, smax, ssum = GatAttentionFn.apply(XL, XR, att, bias, plan, H, 0.2)
+    gout = torch.randn(1, HC, device=device)
+    (out * gout).sum().backward()
+    r_out, r_max, r_sum, r_dXL, r_dXR, r_datt, r_dbias = oracle_attention(XL, XR, att, bias, dst, 1, gout, src=src)
+    close(out, r_out, msg="out")
+    close(smax, r_max, msg="seg_max")
+    close(ssum, r_sum, rtol=2e-4, msg="seg_sum")
+    close(XL.grad, r_dXL, msg="dXL")
+    close(XR.grad, r_dXR, atol=1e-4, msg="dXR")
+    close(att.grad, r_datt, atol=1e-4, msg="datt")
+    close(bias.grad, r_dbias, atol=1e-4, msg="dbias")

@@ -95,17 +95,16 @@ def test_prologue_without_ln(device):
 
 def test_segment_rowsum_matches_index_add(device):
     from gasfm_amd import _native
-    from gasfm_amd.attention import AttnPlan
+    from gasfm_amd.attention import AttnPlan, bwd_combine
     rng = np.random.default_rng(2)
     n, E = 500, 20000
     dst = torch.from_numpy(rng.integers(0, n, E))
     plan = AttnPlan.from_targets(dst, n, max_piece=16).to(device)
     X = torch.randn(E, 32, device=device)
     out = torch.empty(n, 32, device=device)
-    part = torch.empty(max(plan.n_slots, 1), 32, device=device)
+    part = torch.empty(max(plan.n_part_rows, 1), 32, device=device)
     _native.segment_rowsum(plan.items, plan.n_items, plan.perm, X, 0.25, out, part)
-    if plan.n_combine:
-        _native.attn_bwd_combine(plan.combine, plan.n_combine, 32, part, out)
+    bwd_combine(plan, part, 32, out)
     ref = torch.zeros(n, 32, dtype=torch.float64).index_add(0, dst, X.double().cpu()) * 0.25
     np.testing.assert_allclose(out.cpu().numpy(), ref.numpy(), atol=1e-5, rtol=1e-4)
 

@@ -63,7 +63,7 @@ def main():
         lambda: _native.edge_epilogue_fwd(P, P0, cam, pt, ln_w, ln_b, 1e-5, Wp, bp, Sp, Sv, Sg, 0.25, out),
         E * 272 + (n + m) * 128)
     dSv = torch.empty(m, 32, device=dev)
-    part_dsv = torch.empty(max(pc.n_slots, 1), 32, device=dev)
+    part_dsv = torch.empty(max(pc.n_part_rows, 1), 32, device=dev)
     dP0 = torch.empty(E, 2, device=dev)
     wg = _native.edge_part_floats(1, E, pc.n_items) // (32 * 34)
     part_w = torch.empty(wg, 32 * 34, device=dev)
