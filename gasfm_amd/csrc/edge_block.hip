@@ -140,7 +140,11 @@ __global__ __launch_bounds__(kThreads) void edge_prologue_fwd_kernel(const float
   constexpr int LD68 = 68;                   // 16-byte aligned rows for the float4 read-back
   __shared__ float Wt[F * LDW64];            // W^T: Wt[k][n] = W[n][k]
   __shared__ float tiles[kWaves][TR * LD34 + TR * LD68];
-  for (int q = threadIdx.x; q < NX * F; q += kThreads) Wt[(q % F) * LDW64 + q / F] = W[q];
+  {
+    tile::Stage<NX * F, kThreads> sw;
+    sw.load([&](int q) { return W[q]; });
+    sw.store([&](int q, float v) { Wt[(q % F) * LDW64 + q / F] = v; });
+  }
   __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
@@ -220,7 +224,11 @@ __global__ __launch_bounds__(kThreads) void edge_epilogue_fwd_kernel(
   constexpr int LD36 = 36;                   // 16-byte aligned rows for the float4 read-back
   __shared__ float Wt[F * LDW];              // Wt[k][n] = Wp[n][k], k < 32
   __shared__ float tiles[kWaves][TR * LD34 + TR * LD36];
-  for (int q = threadIdx.x; q < F * F; q += kThreads) Wt[(q % F) * LDW + q / F] = Wp[(q / F) * ldWp + q % F];
+  {
+    tile::Stage<F * F, kThreads> sw;
+    sw.load([&](int q) { return Wp[(q / F) * ldWp + q % F]; });
+    sw.store([&](int q, float v) { Wt[(q % F) * LDW + q / F] = v; });
+  }
   __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
@@ -506,9 +514,14 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINWAVES) void edge_prologue_b
   __shared__ float lds[PB_W + kWaves * PB_WAVE];
   float* Wl = lds;                  // B[k][j] = W[k][j]     (k < 64)
   float* Wq = lds + NX * LDW;       // B[k][j] = scale Wp[k][j] (k < 32)
-  for (int q = threadIdx.x; q < NX * F; q += kThreads) Wl[(q / F) * LDW + q % F] = W[q];
-  if (RES)
-    for (int q = threadIdx.x; q < F * F; q += kThreads) Wq[(q / F) * LDW + q % F] = scale * Wp[(q / F) * ldWp + q % F];
+  {
+    tile::Stage<NX * F, kThreads> sw;
+    tile::Stage<F * F, kThreads> sq;
+    sw.load([&](int q) { return W[q]; });
+    if (RES) sq.load([&](int q) { return Wp[(q / F) * ldWp + q % F]; });
+    sw.store([&](int q, float v) { Wl[(q / F) * LDW + q % F] = v; });
+    if (RES) sq.store([&](int q, float v) { Wq[(q / F) * LDW + q % F] = scale * v; });
+  }
   __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;

@@ -90,7 +90,11 @@ __global__ __launch_bounds__(kThreads) void node_fwd_kernel(const float* __restr
   constexpr int NT = FO / 16;
   __shared__ float Wt[FI * LDW];  // Wt[k][n] = W[n][k]
   __shared__ float tiles[kWaves][(RES ? 2 : 1) * TR * LDX];
-  for (int q = threadIdx.x; q < FO * FI; q += kThreads) Wt[(q % FI) * LDW + q / FI] = W[q];
+  {
+    tile::Stage<FO * FI, kThreads> sw;
+    sw.load([&](int q) { return W[q]; });
+    sw.store([&](int q, float v) { Wt[(q % FI) * LDW + q / FI] = v; });
+  }
   __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
@@ -149,7 +153,11 @@ __global__ __launch_bounds__(kThreads) void node_bwd_kernel(const float* __restr
   static_assert(NRED * kW <= LDS, "reduction scratch");
   __shared__ float lds[LDS];
   float* Wl = lds;  // Wl[k][j] = W[k][j]: B operand of dY W
-  for (int q = threadIdx.x; q < FO * FI; q += kThreads) Wl[(q / FI) * LDWB + q % FI] = W[q];
+  {
+    tile::Stage<FO * FI, kThreads> sw;
+    sw.load([&](int q) { return W[q]; });
+    sw.store([&](int q, float v) { Wl[(q / FI) * LDWB + q % FI] = v; });
+  }
   __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
@@ -248,7 +256,7 @@ __global__ __launch_bounds__(kThreads) void node_bwd_kernel(const float* __restr
     v[MT * 17 + nt] = dg[nt];
     v[MT * 17 + 4 + nt] = dbt[nt];
   }
-  wg_reduce_ordered<NRED>(v, lds, wave, lane);
+  wg_reduce_ordered<NRED, kWaves, LDS>(v, lds, wave, lane);
   if (wave == 0) {
     float* out = part + int64_t(blockIdx.x) * (FO * FI + FO + 2 * FI);
 #pragma unroll

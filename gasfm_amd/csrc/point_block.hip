@@ -37,7 +37,20 @@ using namespace tile;
 constexpr int FP = 64;  // n_feat_scenepoint
 constexpr int FA = 32;  // n_feat_proj (aggregation / projection width)
 constexpr int L66 = 66, L34 = 34, L80 = 80, L48 = 48;
-constexpr int kWaves8 = 8, kThreads8 = kWaves8 * kW;
+// A/B knobs (tools/point_bench.py): next-tile register prefetch in the forward / backward
+// kernels, and waves per backward workgroup (8: 2 waves per SIMD at <= 256 VGPRs each; 4: one
+// wave per SIMD, room for the prefetch registers without spilling)
+#ifndef GASFM_PT_FWD_PREFETCH
+#define GASFM_PT_FWD_PREFETCH 1
+#endif
+#ifndef GASFM_PT_BWD_PREFETCH
+#define GASFM_PT_BWD_PREFETCH 0
+#endif
+#ifndef GASFM_PT_BWD_WAVES
+#define GASFM_PT_BWD_WAVES 8
+#endif
+constexpr bool kFwdPf = GASFM_PT_FWD_PREFETCH != 0, kBwdPf = GASFM_PT_BWD_PREFETCH != 0;
+constexpr int kWaves8 = GASFM_PT_BWD_WAVES, kThreads8 = kWaves8 * kW;
 
 // partial-row layouts (floats)
 constexpr int TAIL_PART = FP * FP + FP * FA + 4 * FP;                 // dWm dWp dbm dbp dgam dbet
@@ -96,8 +109,14 @@ __global__ __launch_bounds__(kThreads) void point_tail_fwd_kernel(
   __shared__ float WpT[FA * L80];              // WpT[j][o] = Wp[o][j]
   __shared__ float WmT[FP * L80];              // WmT[k][o] = Wm[o][k]
   __shared__ float tiles[kWaves * PW];
-  for (int q = threadIdx.x; q < FP * FA; q += kThreads) WpT[(q % FA) * L80 + q / FA] = Wp[q];
-  for (int q = threadIdx.x; q < FP * FP; q += kThreads) WmT[(q % FP) * L80 + q / FP] = Wm[q];
+  {
+    Stage<FP * FA, kThreads> sp;
+    Stage<FP * FP, kThreads> sm;
+    sp.load([&](int q) { return Wp[q]; });
+    sm.load([&](int q) { return Wm[q]; });
+    sp.store([&](int q, float v) { WpT[(q % FA) * L80 + q / FA] = v; });
+    sm.store([&](int q, float v) { WmT[(q % FP) * L80 + q / FP] = v; });
+  }
   __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
@@ -114,14 +133,23 @@ __global__ __launch_bounds__(kThreads) void point_tail_fwd_kernel(
   }
   const int64_t ntiles = (N + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWaves + wave, nw = int64_t(gridDim.x) * kWaves;
+  // next-tile register prefetch: tile t + nw's rows are requested right after tile t's are
+  // staged, so their latency overlaps this tile's MFMA work
+  float4 va[2], vp[4];
+  auto fetch = [&](int64_t tt) {
+    const int64_t r0 = tt * TR;
+    const int nr = int(N - r0 < TR ? N - r0 : TR);
+    rows_load<FA>(agg, FA, r0, nr, va, lane);
+    if (PREV) rows_load<FP>(prev, FP, r0, nr, vp, lane);
+  };
+  if (kFwdPf && gw < ntiles) fetch(gw);
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row0 = t * TR;
     const int nrows = int(N - row0 < TR ? N - row0 : TR);
-    float4 va[2], vp[4];
-    rows_load<FA>(agg, FA, row0, nrows, va, lane);
-    if (PREV) rows_load<FP>(prev, FP, row0, nrows, vp, lane);
+    if constexpr (!kFwdPf) fetch(t);
     rows_to_lds<FA, L34>(Ag, va, lane);
     if (PREV) rows_to_lds<FP, L66>(Pv, vp, lane);
+    if (kFwdPf && t + nw < ntiles) fetch(t + nw);
     wave_sync();
     f32x4 xa[4] = {zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
@@ -184,8 +212,14 @@ __global__ __launch_bounds__(kThreads8) void point_tail_bwd_kernel(
   __shared__ float WmL[FP * L80];      // WmL[o][i] = Wm[o][i]   (dout W_m)
   __shared__ float WpL[FP * L48];      // WpL[o][j] = Wp[o][j]   (dx W_p; read transposed for x)
   __shared__ float tiles[kWaves8 * PW];
-  for (int q = threadIdx.x; q < FP * FA; q += kThreads8) WpL[(q / FA) * L48 + q % FA] = Wp[q];
-  for (int q = threadIdx.x; q < FP * FP; q += kThreads8) WmL[(q / FP) * L80 + q % FP] = Wm[q];
+  {
+    Stage<FP * FA, kThreads8> sp;
+    Stage<FP * FP, kThreads8> sm;
+    sp.load([&](int q) { return Wp[q]; });
+    sm.load([&](int q) { return Wm[q]; });
+    sp.store([&](int q, float v) { WpL[(q / FA) * L48 + q % FA] = v; });
+    sm.store([&](int q, float v) { WmL[(q / FP) * L80 + q % FP] = v; });
+  }
   __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
@@ -212,18 +246,23 @@ __global__ __launch_bounds__(kThreads8) void point_tail_bwd_kernel(
   float dg[4] = {0.f, 0.f, 0.f, 0.f}, dbt[4] = {0.f, 0.f, 0.f, 0.f};
   const int64_t ntiles = (N + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWaves8 + wave, nw = int64_t(gridDim.x) * kWaves8;
+  float4 va[2], vd[4], vp[4];  // next-tile register prefetch (see point_tail_fwd_kernel)
+  auto fetch = [&](int64_t tt) {
+    const int64_t r0 = tt * TR;
+    const int nr = int(N - r0 < TR ? N - r0 : TR);
+    rows_load<FA>(agg, FA, r0, nr, va, lane);
+    rows_load<FP>(dout, FP, r0, nr, vd, lane);
+    if (PREV) rows_load<FP>(prev, FP, r0, nr, vp, lane);
+  };
+  if (kBwdPf && gw < ntiles) fetch(gw);
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row0 = t * TR;
     const int nrows = int(N - row0 < TR ? N - row0 : TR);
-    {
-      float4 va[2], vd[4], vp[4];
-      rows_load<FA>(agg, FA, row0, nrows, va, lane);
-      rows_load<FP>(dout, FP, row0, nrows, vd, lane);
-      if (PREV) rows_load<FP>(prev, FP, row0, nrows, vp, lane);
-      rows_to_lds<FA, L34>(Ag, va, lane);
-      rows_to_lds<FP, L66>(D, vd, lane);
-      if (PREV) rows_to_lds<FP, L66>(XH, vp, lane);
-    }
+    if constexpr (!kBwdPf) fetch(t);
+    rows_to_lds<FA, L34>(Ag, va, lane);
+    rows_to_lds<FP, L66>(D, vd, lane);
+    if (PREV) rows_to_lds<FP, L66>(XH, vp, lane);
+    if (kBwdPf && t + nw < ntiles) fetch(t + nw);
     wave_sync();
     // recompute x (C layout): agg W_p^T (W_p read transposed from WpL) + b_p + prev
     f32x4 xa[4] = {zero4(), zero4(), zero4(), zero4()};
@@ -280,6 +319,7 @@ __global__ __launch_bounds__(kThreads8) void point_tail_bwd_kernel(
     }
     wave_sync();
     // dW_m += dout^T relu(LN x), dW_p += dx^T agg, biases (rows past nrows: dout, dx, agg are 0)
+#ifndef GASFM_PT_NODW
 #pragma unroll 1
     for (int s = 0; s < TR / 4; ++s) {
       const int row = 4 * s + g;
@@ -299,6 +339,7 @@ __global__ __launch_bounds__(kThreads8) void point_tail_bwd_kernel(
         for (int nt = 0; nt < 2; ++nt) dWp[mt][nt] = mfma16(a2, ag[nt], dWp[mt][nt]);
       }
     }
+#endif
     // dagg = dx W_p, staged into D (dead) as 16 x 32
     f32x4 da[2] = {zero4(), zero4()};
 #pragma unroll
@@ -339,7 +380,9 @@ __global__ __launch_bounds__(kThreads8) void point_tail_bwd_kernel(
     v[104 + k] = dg[k];
     v[108 + k] = dbt[k];
   }
-  wg_reduce_ordered<NRED, kWaves8>(v, tiles, wave, lane);
+#ifndef GASFM_PT_NORED
+  wg_reduce_ordered<NRED, kWaves8, kWaves8 * PW>(v, tiles, wave, lane);
+#endif
   if (wave == 0) {
     float* out = part + int64_t(blockIdx.x) * TAIL_PART;
 #pragma unroll
@@ -380,11 +423,22 @@ __global__ __launch_bounds__(kThreads) void point_hub_fwd_kernel(
   __shared__ float WDt[HC ? FA * L48 : 1];      // WDt[k][j] = W_D[j][k]
   __shared__ float GB[4 * FP];                  // gamma_A beta_A gamma_C beta_C
   __shared__ float tiles[kWaves * PW];
-  for (int q = threadIdx.x; q < FA * FP; q += kThreads) WAt[(q % FP) * L48 + q / FP] = WA[q];
-  for (int q = threadIdx.x; q < FP * FP; q += kThreads) WBt[(q % FP) * L80 + q / FP] = WB[q];
-  if (HC) {
-    for (int q = threadIdx.x; q < FA * FP; q += kThreads) WCt[(q % FP) * L48 + q / FP] = WC[q];
-    for (int q = threadIdx.x; q < FA * FA; q += kThreads) WDt[(q % FA) * L48 + q / FA] = WD[q];
+  {
+    Stage<FA * FP, kThreads> sa, sc;
+    Stage<FP * FP, kThreads> sb;
+    Stage<FA * FA, kThreads> sd;
+    sa.load([&](int q) { return WA[q]; });
+    sb.load([&](int q) { return WB[q]; });
+    if (HC) {
+      sc.load([&](int q) { return WC[q]; });
+      sd.load([&](int q) { return WD[q]; });
+    }
+    sa.store([&](int q, float v) { WAt[(q % FP) * L48 + q / FP] = v; });
+    sb.store([&](int q, float v) { WBt[(q % FP) * L80 + q / FP] = v; });
+    if (HC) {
+      sc.store([&](int q, float v) { WCt[(q % FP) * L48 + q / FP] = v; });
+      sd.store([&](int q, float v) { WDt[(q % FA) * L48 + q / FA] = v; });
+    }
   }
   if (threadIdx.x < FP) {
     GB[threadIdx.x] = gA[threadIdx.x];
@@ -410,15 +464,19 @@ __global__ __launch_bounds__(kThreads) void point_hub_fwd_kernel(
   }
   const int64_t ntiles = (N + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWaves + wave, nw = int64_t(gridDim.x) * kWaves;
+  float4 vx[4];  // next-tile register prefetch (see point_tail_fwd_kernel)
+  auto fetch = [&](int64_t tt) {
+    const int64_t r0 = tt * TR;
+    rows_load<FP>(X, FP, r0, int(N - r0 < TR ? N - r0 : TR), vx, lane);
+  };
+  if (kFwdPf && gw < ntiles) fetch(gw);
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row0 = t * TR;
     const int nrows = int(N - row0 < TR ? N - row0 : TR);
-    {
-      float4 vx[4];
-      rows_load<FP>(X, FP, row0, nrows, vx, lane);
-      row_stats64(vx, eps, MS, RS, lane);
-      rows_to_lds<FP, L66>(Raw, vx, lane);
-    }
+    if constexpr (!kFwdPf) fetch(t);
+    row_stats64(vx, eps, MS, RS, lane);
+    rows_to_lds<FP, L66>(Raw, vx, lane);
+    if (kFwdPf && t + nw < ntiles) fetch(t + nw);
     wave_sync();
     const float mi = MS[c], ri = RS[c];
     f32x4 accB[4] = {zero4(), zero4(), zero4(), zero4()}, accA[2] = {zero4(), zero4()}, accC[2] = {zero4(), zero4()};
@@ -505,8 +563,14 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_ab_kernel(
   __shared__ float WBl[FP * L80];        // W_B [64 x 64]
   __shared__ float GB[2 * FP];           // gamma_A beta_A
   __shared__ float tiles[kWaves8 * PW];
-  for (int q = threadIdx.x; q < FA * FP; q += kThreads8) WAl[(q / FP) * L80 + q % FP] = WA[q];
-  for (int q = threadIdx.x; q < FP * FP; q += kThreads8) WBl[(q / FP) * L80 + q % FP] = WB[q];
+  {
+    Stage<FA * FP, kThreads8> sa;
+    Stage<FP * FP, kThreads8> sb;
+    sa.load([&](int q) { return WA[q]; });
+    sb.load([&](int q) { return WB[q]; });
+    sa.store([&](int q, float v) { WAl[(q / FP) * L80 + q % FP] = v; });
+    sb.store([&](int q, float v) { WBl[(q / FP) * L80 + q % FP] = v; });
+  }
   if (threadIdx.x < FP) {
     GB[threadIdx.x] = gA[threadIdx.x];
     GB[FP + threadIdx.x] = bA[threadIdx.x];
@@ -530,21 +594,26 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_ab_kernel(
   float dbB[4] = {0.f, 0.f, 0.f, 0.f}, dgA[4] = {0.f, 0.f, 0.f, 0.f}, dbA[4] = {0.f, 0.f, 0.f, 0.f};
   const int64_t ntiles = (N + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWaves8 + wave, nw = int64_t(gridDim.x) * kWaves8;
+  float4 vx[4], vl[4], vs[2], vr[4];  // next-tile register prefetch (see point_tail_fwd_kernel)
+  auto fetch = [&](int64_t tt) {
+    const int64_t r0 = tt * TR;
+    const int nr = int(N - r0 < TR ? N - r0 : TR);
+    rows_load<FP>(X, FP, r0, nr, vx, lane);
+    rows_load<FP>(dXL, FP, r0, nr, vl, lane);
+    rows_load<FA>(dSA, FA, r0, nr, vs, lane);
+    if (HR) rows_load<FP>(dRes, FP, r0, nr, vr, lane);
+  };
+  if (kBwdPf && gw < ntiles) fetch(gw);
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row0 = t * TR;
     const int nrows = int(N - row0 < TR ? N - row0 : TR);
-    {
-      float4 vx[4], vl[4], vs[2], vr[4];
-      rows_load<FP>(X, FP, row0, nrows, vx, lane);
-      rows_load<FP>(dXL, FP, row0, nrows, vl, lane);
-      rows_load<FA>(dSA, FA, row0, nrows, vs, lane);
-      if (HR) rows_load<FP>(dRes, FP, row0, nrows, vr, lane);
-      row_stats64(vx, eps, MS, RS, lane);
-      rows_to_lds<FP, L66>(Raw, vx, lane);
-      rows_to_lds<FP, L66>(XLt, vl, lane);
-      rows_to_lds<FA, L34>(SAt, vs, lane);
-      if (HR) rows_to_lds<FP, L66>(DXo, vr, lane);
-    }
+    if constexpr (!kBwdPf) fetch(t);
+    row_stats64(vx, eps, MS, RS, lane);
+    rows_to_lds<FP, L66>(Raw, vx, lane);
+    rows_to_lds<FP, L66>(XLt, vl, lane);
+    rows_to_lds<FA, L34>(SAt, vs, lane);
+    if (HR) rows_to_lds<FP, L66>(DXo, vr, lane);
+    if (kBwdPf && t + nw < ntiles) fetch(t + nw);
     wave_sync();
     // weight gradients over the tile's rows (row = 4s + g; rows past nrows: dSA, dXL are 0)
 #pragma unroll 1
@@ -630,7 +699,9 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_ab_kernel(
     v[100 + k] = dgA[k];
     v[104 + k] = dbA[k];
   }
-  wg_reduce_ordered<NRED, kWaves8>(v, tiles, wave, lane);
+#ifndef GASFM_PT_NORED
+  wg_reduce_ordered<NRED, kWaves8, kWaves8 * PW>(v, tiles, wave, lane);
+#endif
   if (wave == 0) {
     float* out = part + int64_t(blockIdx.x) * HA_PART;
 #pragma unroll
@@ -671,11 +742,17 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_c_kernel(
   __shared__ float WDl[FA * L48];        // W_D [32 x 32]
   __shared__ float GB[2 * FP];           // gamma_C beta_C
   __shared__ float tiles[kWaves8 * PW];
-  for (int q = threadIdx.x; q < FA * FP; q += kThreads8) {
-    WCl[(q / FP) * L80 + q % FP] = WC[q];
-    WCt[(q % FP) * L48 + q / FP] = WC[q];
+  {
+    Stage<FA * FP, kThreads8> sc;
+    Stage<FA * FA, kThreads8> sd;
+    sc.load([&](int q) { return WC[q]; });
+    sd.load([&](int q) { return WD[q]; });
+    sc.store([&](int q, float v) {
+      WCl[(q / FP) * L80 + q % FP] = v;
+      WCt[(q % FP) * L48 + q / FP] = v;
+    });
+    sd.store([&](int q, float v) { WDl[(q / FA) * L48 + q % FA] = v; });
   }
-  for (int q = threadIdx.x; q < FA * FA; q += kThreads8) WDl[(q / FA) * L48 + q % FA] = WD[q];
   if (threadIdx.x < FP) {
     GB[threadIdx.x] = gC[threadIdx.x];
     GB[FP + threadIdx.x] = bC[threadIdx.x];
@@ -701,19 +778,24 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_c_kernel(
   float dbC[2] = {0.f, 0.f}, dbD[2] = {0.f, 0.f}, dgC[4] = {0.f, 0.f, 0.f, 0.f}, dbCl[4] = {0.f, 0.f, 0.f, 0.f};
   const int64_t ntiles = (N + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWaves8 + wave, nw = int64_t(gridDim.x) * kWaves8;
+  float4 vx[4], vq[2], vr[4];  // next-tile register prefetch (see point_tail_fwd_kernel)
+  auto fetch = [&](int64_t tt) {
+    const int64_t r0 = tt * TR;
+    const int nr = int(N - r0 < TR ? N - r0 : TR);
+    rows_load<FP>(X, FP, r0, nr, vx, lane);
+    rows_load<FA>(dXR, FA, r0, nr, vq, lane);
+    if (HR) rows_load<FP>(dRes, FP, r0, nr, vr, lane);
+  };
+  if (kBwdPf && gw < ntiles) fetch(gw);
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row0 = t * TR;
     const int nrows = int(N - row0 < TR ? N - row0 : TR);
-    {
-      float4 vx[4], vq[2], vr[4];
-      rows_load<FP>(X, FP, row0, nrows, vx, lane);
-      rows_load<FA>(dXR, FA, row0, nrows, vq, lane);
-      if (HR) rows_load<FP>(dRes, FP, row0, nrows, vr, lane);
-      row_stats64(vx, eps, MS, RS, lane);
-      rows_to_lds<FP, L66>(Raw, vx, lane);
-      rows_to_lds<FA, L34>(XRt, vq, lane);
-      if (HR) rows_to_lds<FP, L66>(DXo, vr, lane);
-    }
+    if constexpr (!kBwdPf) fetch(t);
+    row_stats64(vx, eps, MS, RS, lane);
+    rows_to_lds<FP, L66>(Raw, vx, lane);
+    rows_to_lds<FA, L34>(XRt, vq, lane);
+    if (HR) rows_to_lds<FP, L66>(DXo, vr, lane);
+    if (kBwdPf && t + nw < ntiles) fetch(t + nw);
     wave_sync();
     const float mi = MS[c], ri = RS[c];
     // t = W_C relu(LN_C p) + b_C (recomputed), dt = dXR W_D
@@ -817,7 +899,9 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_c_kernel(
     v[52 + k] = dgC[k];
     v[56 + k] = dbCl[k];
   }
-  wg_reduce_ordered<NRED, kWaves8>(v, tiles, wave, lane);
+#ifndef GASFM_PT_NORED
+  wg_reduce_ordered<NRED, kWaves8, kWaves8 * PW>(v, tiles, wave, lane);
+#endif
   if (wave == 0) {
     float* out = part + int64_t(blockIdx.x) * HC_PART;
 #pragma unroll

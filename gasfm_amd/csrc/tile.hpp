@@ -40,6 +40,33 @@ __device__ __forceinline__ float sum_groups(float v) {
   return v;
 }
 
+// Weight staging (once per workgroup): every thread issues ALL of its N / NT global loads before
+// the first LDS store.  The plain `for (q = threadIdx.x; q < N; q += NT) L[f(q)] = W[q]` form
+// compiles to one load + vmcnt(0) + branch per trip (the compiler cannot prove the trip
+// condition uniform), i.e. ~N / NT serialised memory round trips (~20 us per kernel measured
+// on the point kernels, paid before any tile work).  Requires blockDim.x == NT.
+template <int N, int NT>
+struct Stage {
+  static constexpr int IT = (N + NT - 1) / NT;
+  float v[IT];
+  template <class Src>
+  __device__ __forceinline__ void load(Src src) {
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const int q = int(threadIdx.x) + k * NT;
+      v[k] = src((N % NT == 0 || q < N) ? q : 0);
+    }
+  }
+  template <class Dst>
+  __device__ __forceinline__ void store(Dst dst) const {
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const int q = int(threadIdx.x) + k * NT;
+      if (N % NT == 0 || q < N) dst(q, v[k]);
+    }
+  }
+};
+
 // Row-major [16 x W] tile from global (row stride ld floats, 16-byte aligned) into LDS (row
 // stride LDT); rows >= nrows are zeros (nrows >= 1).  All global loads are issued before the
 // LDS stores.
@@ -134,21 +161,35 @@ __device__ __forceinline__ void wg_reduce(float (&v)[N], float* scratch, int wav
   }
 }
 
-// Same result as wg_reduce with only N*kW floats of scratch: the waves add into one buffer in
-// wave order, one barrier per wave.  NW = waves per workgroup.
-template <int N, int NW = kWaves>
+// Ordered workgroup sum of N floats per lane (wave 0 returns the totals in v), in chunks that
+// fit SF floats of LDS scratch: every wave stores its chunk values at once, then wave w' sums
+// the values k = w', w' + NW, ... over the waves in wave order (0 + v_0 + v_1 + ...: the same
+// bits as a serial wave-by-wave accumulation) in place, and wave 0 reads the totals back.
+// Three barriers per chunk; the earlier one-wave-at-a-time form serialised NW x N dependent
+// LDS read/write pairs (~25 us per launch for N = 112 over 8 waves, measured).
+template <int N, int NW, int SF>
 __device__ __forceinline__ void wg_reduce_ordered(float (&v)[N], float* scratch, int wave, int lane) {
-  for (int w = 0; w < NW; ++w) {
+  constexpr int CH = (SF / (NW * kW)) < N ? (SF / (NW * kW)) : N;  // values per chunk
+  static_assert(CH >= 1, "wg_reduce_ordered: scratch too small");
+#pragma unroll
+  for (int k0 = 0; k0 < N; k0 += CH) {
     __syncthreads();
-    if (wave == w) {
 #pragma unroll
-      for (int k = 0; k < N; ++k) scratch[k * kW + lane] = (w == 0 ? 0.f : scratch[k * kW + lane]) + v[k];
+    for (int k = 0; k < CH; ++k)
+      if (k0 + k < N) scratch[(wave * CH + k) * kW + lane] = v[k0 + k];
+    __syncthreads();
+    for (int k = wave; k < CH && k0 + k < N; k += NW) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s += scratch[(w * CH + k) * kW + lane];
+      scratch[k * kW + lane] = s;  // wave 0's slot of value k (only this wave touches k here)
     }
-  }
-  __syncthreads();
-  if (wave == 0) {
+    __syncthreads();
+    if (wave == 0) {
 #pragma unroll
-    for (int k = 0; k < N; ++k) v[k] = scratch[k * kW + lane];
+      for (int k = 0; k < CH; ++k)
+        if (k0 + k < N) v[k0 + k] = scratch[k * kW + lane];
+    }
   }
 }
 

@@ -31,9 +31,10 @@ def _time(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--n", type=int, default=200_000, help="points (25000: the per-rank load at 8 GPUs)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    sc = synthetic.config4()
+    sc = synthetic.config4() if args.n == 200_000 else synthetic.windowed_scene(1000, args.n, seed=4)
     data = SceneData.from_synthetic(sc).to(dev)
     E, m, n = sc.num_edges, sc.m, sc.n
     g = torch.Generator(device=dev).manual_seed(0)
