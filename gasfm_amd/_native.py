@@ -6,6 +6,7 @@ fallback for the attention path.  Host-only entry points (graph
 preprocessing) work without a GPU, so DataLoader workers can use them.
 """
 import ctypes
+import threading
 import os
 
 import numpy as np
@@ -35,15 +36,17 @@ _SIGS = {
     "gasfm_gat_attn_bwd_combine": (_i32, [_vp, _i32, _i32, _vp, _vp, _i64, _vp]),
     "gasfm_colsum_ws_floats": (_i64, [_i64, _i32]),
     "gasfm_edge_part_floats": (_i32, [_i32, _i64, _i32]),
-    "gasfm_edge_prologue_fwd": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _i64, _vp, _vp]),
+    "gasfm_edge_prologue_fwd": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     "gasfm_edge_epilogue_fwd": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _i32, _vp, _vp, _vp, _vp,
                                        _f32, _vp, _vp]),
     "gasfm_edge_epilogue_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _i32, _f32, _vp, _vp, _vp,
                                        _vp, _vp]),
-    "gasfm_edge_prologue_bwd": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _vp, _i32, _f32, _vp, _vp,
-                                       _vp]),
+    "gasfm_edge_prologue_bwd": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _i32, _f32, _vp,
+                                       _vp, _vp]),
     "gasfm_segment_rowsum": (_i32, [_vp, _i32, _vp, _vp, _i64, _f32, _vp, _vp, _vp]),
     "gasfm_colsum_counters": (_i32, [_i32]),
+    "gasfm_colsum_multi": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_colsum_multi_counters": (_i32, [_i32, _vp]),
     "gasfm_colsum": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, _vp]),
     "gasfm_edge0_part_rows": (_i32, [_i32, _i64, _i32]),
     "gasfm_edge0_prologue_fwd": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp]),
@@ -226,6 +229,89 @@ def colsum(A, out=None):
     return out
 
 
+# ---------------------------------------------------------------- batched weight-gradient sums
+# A backward pass ends with ~150 column sums of per-workgroup weight-gradient partials (one per
+# fused kernel).  Their results are parameter gradients that nothing reads before the backward
+# pass returns, so inside a pass they are queued and run as ONE batched launch
+# (gasfm_colsum_multi) from an autograd final callback: ~150 fewer kernel launches per step.
+# Only when the model forward saw every parameter's .grad unset (AccumulateGrad then adopts the
+# returned tensor instead of adding it to an existing gradient, so filling it later is safe);
+# otherwise, and outside a backward pass, param_colsum is colsum.
+_DEFER_FWD = False
+_PENDING = {}
+_PENDING_LOCK = threading.Lock()
+
+
+def defer_token(*targets):
+    """Captured by the fused Functions' forward (ctx.defer) and passed to param_colsum: true in
+    a deferring model forward when every tensor that receives a deferred sum is a leaf (a
+    parameter: no autograd node reads its gradient before the pass ends)."""
+    return _DEFER_FWD and all(t is None or t.is_leaf for t in targets)
+
+
+class deferring_param_grads:
+    """Set by GraphAttnSfMNet.forward for the duration of the forward."""
+
+    def __init__(self, enabled):
+        self.enabled = bool(enabled)
+
+    def __enter__(self):
+        global _DEFER_FWD
+        self.prev, _DEFER_FWD = _DEFER_FWD, self.enabled
+        return self
+
+    def __exit__(self, *exc):
+        global _DEFER_FWD
+        _DEFER_FWD = self.prev
+        return False
+
+
+def param_colsum(A, defer):
+    """colsum of weight-gradient partials; deferred to the end of the backward pass when
+    ``defer`` (see above) and called inside one."""
+    task = torch._C._current_graph_task_id() if defer else -1
+    if task < 0:
+        return colsum(A)
+    assert A.dim() == 2 and A.stride(1) == 1 and A.dtype == torch.float32
+    rows, cols = A.shape
+    L = lib()
+    out = torch.empty(cols, dtype=torch.float32, device=A.device)
+    ws = torch.empty(int(L.gasfm_colsum_ws_floats(rows, cols)), dtype=torch.float32, device=A.device)
+    job = (A, ws, out, rows, cols, max(A.stride(0), cols), torch.cuda.current_stream(A.device))
+    with _PENDING_LOCK:
+        jobs = _PENDING.get(task)
+        first = jobs is None
+        if first:
+            jobs = _PENDING[task] = []
+        jobs.append(job)
+    if first:
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: _flush_param_colsums(task))
+    return out
+
+
+def _flush_param_colsums(task):
+    with _PENDING_LOCK:
+        jobs = _PENDING.pop(task, [])
+    if not jobs:
+        return
+    stream = jobs[0][6]
+    assert all(j[6] == stream for j in jobs), "param_colsum: jobs queued on several streams"
+    n = len(jobs)
+    L = lib()
+    arr = lambda ty, xs: (ty * n)(*xs)  # noqa: E731
+    A = arr(ctypes.c_void_p, [j[0].data_ptr() for j in jobs])
+    ws = arr(ctypes.c_void_p, [j[1].data_ptr() for j in jobs])
+    out = arr(ctypes.c_void_p, [j[2].data_ptr() for j in jobs])
+    rows = arr(ctypes.c_int64, [j[3] for j in jobs])
+    cols = arr(ctypes.c_int32, [j[4] for j in jobs])
+    ld = arr(ctypes.c_int64, [j[5] for j in jobs])
+    dev = jobs[0][0].device
+    cnt = _counters(dev, L.gasfm_colsum_multi_counters(n, cols))
+    st = L.gasfm_colsum_multi(n, A, rows, cols, ld, ws, out, _p(cnt), ctypes.c_void_p(stream.cuda_stream))
+    check(st, "gasfm_colsum_multi")
+    # the partial buffers (jobs) are released only now, after the launch that reads them
+
+
 # ---------------------------------------------------------------- fused per-edge block kernels
 def _req(t, name, cols=None):
     if not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous():
@@ -238,10 +324,11 @@ def edge_part_floats(which, E, n_items=0):
     return lib().gasfm_edge_part_floats(which, E, n_items)
 
 
-def edge_prologue_fwd(P, ln_w, ln_b, eps, W, b, Y, pos=None):
+def edge_prologue_fwd(P, ln_w, ln_b, eps, W, b, Y, pos=None, W2=None, b2=None):
+    """W [64,32] / b [64], or the halves W [32,32] + W2 [32,32] and b [32] + b2 [32]."""
     _req(P, "P", 32)
-    st = lib().gasfm_edge_prologue_fwd(_p(P), P.shape[0], _p(ln_w), _p(ln_b), eps, _p(W), _p(b), _p(Y), Y.stride(0),
-                                       _p(pos), _stream(P))
+    st = lib().gasfm_edge_prologue_fwd(_p(P), P.shape[0], _p(ln_w), _p(ln_b), eps, _p(W), _p(W2), _p(b), _p(b2),
+                                       _p(Y), Y.stride(0), _p(pos), _stream(P))
     check(st, "gasfm_edge_prologue_fwd")
 
 
@@ -261,11 +348,11 @@ def edge_epilogue_bwd(items, n_items, dPo, P, P0, ln_w, ln_b, eps, Wp, scale, dS
     check(st, "gasfm_edge_epilogue_bwd")
 
 
-def edge_prologue_bwd(dXL, P, dRes, ln_w, ln_b, eps, W, Wp, scale, dP, part):
+def edge_prologue_bwd(dXL, P, dRes, ln_w, ln_b, eps, W, Wp, scale, dP, part, W2=None):
     _req(P, "P", 32)
     st = lib().gasfm_edge_prologue_bwd(_p(dXL), dXL.stride(0), _p(P), _p(dRes), P.shape[0], _p(ln_w), _p(ln_b), eps,
-                                       _p(W), _p(Wp), Wp.shape[1] if Wp is not None else 0, scale, _p(dP), _p(part),
-                                       _stream(P))
+                                       _p(W), _p(W2), _p(Wp), Wp.shape[1] if Wp is not None else 0, scale, _p(dP),
+                                       _p(part), _stream(P))
     check(st, "gasfm_edge_prologue_bwd")
 
 

@@ -262,7 +262,8 @@ def combine_partials(gathered, world, N, heads, bias, combine_items):
     return out, smax, ssum
 
 
-def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, gout, dXL=None, xl_sorted=False):
+def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, gout, dXL=None, xl_sorted=False,
+                      defer=False):
     """Launch the backward kernels; returns (dXL, dXR, datt[HC], dbias[HC]).
 
     dXL is always in source-row (edge) order; xl_sorted says XL itself is in segment order."""
@@ -283,7 +284,7 @@ def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, go
         _native.attn_bwd(XL, XR, attf, bias, plan.perm, plan.items, plan.n_items, heads, C, slope, out, smax,
                          ssum, gout, dXL, dXR, part, datt_part, xl_by_position=xl_sorted)
         bwd_combine(plan, part, HC, dXR)
-        tot = _native.colsum(datt_part)
+        tot = _native.param_colsum(datt_part, defer)  # datt | dbias: parameter gradients
         datt, dbias = tot[:HC], tot[HC:]
     else:
         dXR.zero_()
@@ -299,6 +300,7 @@ class GatAttentionFn(torch.autograd.Function):
     def forward(ctx, XL, XR, att, bias, plan, heads, slope):
         out, smax, ssum = attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True)
         ctx.plan, ctx.heads, ctx.slope = plan, heads, slope
+        ctx.defer = _native.defer_token(att, bias)
         ctx.save_for_backward(XL, XR, att, bias, out, smax, ssum)
         ctx.mark_non_differentiable(smax, ssum)
         ctx.set_materialize_grads(False)  # no zero-filled gradients for the statistics outputs
@@ -310,7 +312,8 @@ class GatAttentionFn(torch.autograd.Function):
         if gout is None:
             return None, None, None, None, None, None, None
         dXL, dXR, datt, dbias = attn_backward_raw(XL, XR, att, bias, ctx.plan, ctx.heads, ctx.slope, out, smax,
-                                                  ssum, gout)
+                                                  ssum, gout,
+                                                  defer=ctx.defer)
         return dXL, dXR, datt.view_as(att), dbias, None, None, None
 
 

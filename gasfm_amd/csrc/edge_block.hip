@@ -128,13 +128,17 @@ __device__ __forceinline__ void load_norm_tile(const float* __restrict__ P, int6
 
 // =====================================================================================
 // edge_prologue_fwd: XL[e] = W relu(LN(P[e])) + b     (W: [64 x 32], XL row stride ldY)
+// W / b may come as two halves (W2, b2 non-null: rows 32..63), i.e. the two convs' lin_l
+// parameters themselves, so the host does not concatenate them every forward
 // =====================================================================================
 template <bool LN>
 __global__ __launch_bounds__(kThreads) void edge_prologue_fwd_kernel(const float* __restrict__ P, int64_t E,
                                                                     const float* __restrict__ gam,
                                                                     const float* __restrict__ bet, float eps,
                                                                     const float* __restrict__ W,
+                                                                    const float* __restrict__ W2,
                                                                     const float* __restrict__ b,
+                                                                    const float* __restrict__ b2,
                                                                     float* __restrict__ Y, int64_t ldY,
                                                                     const int32_t* __restrict__ pos) {
   constexpr int LD68 = 68;                   // 16-byte aligned rows for the float4 read-back
@@ -142,7 +146,7 @@ __global__ __launch_bounds__(kThreads) void edge_prologue_fwd_kernel(const float
   __shared__ float tiles[kWaves][TR * LD34 + TR * LD68];
   {
     tile::Stage<NX * F, kThreads> sw;
-    sw.load([&](int q) { return W[q]; });
+    sw.load([&](int q) { return (W2 && q >= (NX / 2) * F) ? W2[q - (NX / 2) * F] : W[q]; });
     sw.store([&](int q, float v) { Wt[(q % F) * LDW64 + q / F] = v; });
   }
   __syncthreads();
@@ -151,7 +155,7 @@ __global__ __launch_bounds__(kThreads) void edge_prologue_fwd_kernel(const float
   const int c4 = (lane & 15) * 4;            // row layout: row (lane>>4) + 4u, columns c4..c4+3
   float* T = tiles[wave];
   float* Yt = T + TR * LD34;
-  const float4 bias = *reinterpret_cast<const float4*>(b + c4);
+  const float4 bias = *reinterpret_cast<const float4*>((b2 && c4 >= NX / 2) ? b2 + (c4 - NX / 2) : b + c4);
   const Affine4 af = load_affine<LN>(gam, bet, lane);
   const int64_t ntiles = (E + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWaves + wave, nw = int64_t(gridDim.x) * kWaves;
@@ -509,15 +513,15 @@ template <bool LN, bool RES>
 __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINWAVES) void edge_prologue_bwd_kernel(
     const float* __restrict__ dXL, int64_t ldX, const float* __restrict__ P, const float* __restrict__ dRes,
     int64_t E, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
-    const float* __restrict__ W, const float* __restrict__ Wp, int ldWp, float scale, float* __restrict__ dP,
-    float* __restrict__ part) {
+    const float* __restrict__ W, const float* __restrict__ W2, const float* __restrict__ Wp, int ldWp, float scale,
+    float* __restrict__ dP, float* __restrict__ part) {
   __shared__ float lds[PB_W + kWaves * PB_WAVE];
   float* Wl = lds;                  // B[k][j] = W[k][j]     (k < 64)
   float* Wq = lds + NX * LDW;       // B[k][j] = scale Wp[k][j] (k < 32)
   {
     tile::Stage<NX * F, kThreads> sw;
     tile::Stage<F * F, kThreads> sq;
-    sw.load([&](int q) { return W[q]; });
+    sw.load([&](int q) { return (W2 && q >= (NX / 2) * F) ? W2[q - (NX / 2) * F] : W[q]; });
     if (RES) sq.load([&](int q) { return Wp[(q / F) * ldWp + q % F]; });
     sw.store([&](int q, float v) { Wl[(q / F) * LDW + q % F] = v; });
     if (RES) sq.store([&](int q, float v) { Wq[(q / F) * LDW + q % F] = scale * v; });
@@ -778,9 +782,10 @@ extern "C" int gasfm_edge_part_floats(int32_t which, int64_t E, int32_t n_items)
 }
 
 extern "C" int gasfm_edge_prologue_fwd(const float* P, int64_t E, const float* ln_w, const float* ln_b,
-                                       float eps, const float* W, const float* b, float* Y, int64_t ldY,
-                                       const int32_t* pos, void* stream) {
-  GASFM_REQUIRE(E >= 0 && P && W && b && Y, "gasfm_edge_prologue_fwd: bad args");
+                                       float eps, const float* W, const float* W2, const float* b,
+                                       const float* b2, float* Y, int64_t ldY, const int32_t* pos, void* stream) {
+  GASFM_REQUIRE(E >= 0 && P && W && b && Y && (!W2) == (!b2), "gasfm_edge_prologue_fwd: bad args");
+  GASFM_REQUIRE(!b2 || (aligned16(b2) && aligned16(W2)), "gasfm_edge_prologue_fwd: W2/b2 not 16-byte aligned");
   GASFM_REQUIRE(ldY >= NX && ldY % 4 == 0, "gasfm_edge_prologue_fwd: ldY < 64 or not a multiple of 4");
   GASFM_REQUIRE(aligned16(P) && aligned16(Y) && aligned16(b), "gasfm_edge_prologue_fwd: P/Y/b not 16-byte aligned");
   if (E == 0) return GASFM_OK;
@@ -788,13 +793,13 @@ extern "C" int gasfm_edge_prologue_fwd(const float* P, int64_t E, const float* l
   if (ln_w) {
     const int g = resident_grid(reinterpret_cast<const void*>(&edge_prologue_fwd_kernel<true>), kThreads, 0,
                                 tiles_of(E), kWaves);
-    hipLaunchKernelGGL(edge_prologue_fwd_kernel<true>, dim3(g), dim3(kThreads), 0, st, P, E, ln_w, ln_b, eps, W, b,
-                       Y, ldY, pos);
+    hipLaunchKernelGGL(edge_prologue_fwd_kernel<true>, dim3(g), dim3(kThreads), 0, st, P, E, ln_w, ln_b, eps, W, W2, b,
+                       b2, Y, ldY, pos);
   } else {
     const int g = resident_grid(reinterpret_cast<const void*>(&edge_prologue_fwd_kernel<false>), kThreads, 0,
                                 tiles_of(E), kWaves);
-    hipLaunchKernelGGL(edge_prologue_fwd_kernel<false>, dim3(g), dim3(kThreads), 0, st, P, E, ln_w, ln_b, eps, W, b,
-                       Y, ldY, pos);
+    hipLaunchKernelGGL(edge_prologue_fwd_kernel<false>, dim3(g), dim3(kThreads), 0, st, P, E, ln_w, ln_b, eps, W, W2, b,
+                       b2, Y, ldY, pos);
   }
   return launch_status("gasfm_edge_prologue_fwd");
 }
@@ -836,8 +841,8 @@ extern "C" int gasfm_edge_epilogue_bwd(const gasfm_work_item* items, int32_t n_i
 
 extern "C" int gasfm_edge_prologue_bwd(const float* dXL, int64_t ldX, const float* P, const float* dRes, int64_t E,
                                        const float* ln_w, const float* ln_b, float eps, const float* W,
-                                       const float* Wp, int32_t ldWp, float scale, float* dP, float* part,
-                                       void* stream) {
+                                       const float* W2, const float* Wp, int32_t ldWp, float scale, float* dP,
+                                       float* part, void* stream) {
   GASFM_REQUIRE(dXL && P && W && dP && part && ldX >= NX, "gasfm_edge_prologue_bwd: bad args");
   GASFM_REQUIRE(!dRes || Wp, "gasfm_edge_prologue_bwd: dRes needs Wp");
   GASFM_REQUIRE(aligned16(dXL) && ldX % 4 == 0 && aligned16(P) && (!dRes || aligned16(dRes)) && aligned16(dP),
@@ -848,7 +853,7 @@ extern "C" int gasfm_edge_prologue_bwd(const float* dXL, int64_t ldX, const floa
   const bool ln = ln_w != nullptr, res = dRes != nullptr;
 #define GASFM_LAUNCH(LNV, RESV)                                                                                 \
   hipLaunchKernelGGL((edge_prologue_bwd_kernel<LNV, RESV>), dim3(g), dim3(kThreads), 0, st, dXL, ldX, P, dRes, \
-                     E, ln_w, ln_b, eps, W, Wp, ldWp, scale, dP, part)
+                     E, ln_w, ln_b, eps, W, W2, Wp, ldWp, scale, dP, part)
   if (ln && res)
     GASFM_LAUNCH(true, true);
   else if (ln)

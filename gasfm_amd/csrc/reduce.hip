@@ -37,14 +37,13 @@ static int colsum_blocks(int64_t rows) {
 // group (c4) and a row lane (rl); RL = 256 / (cols/4) row lanes stride the block's row
 // range with 4 independent loads in flight, then the row lanes are summed through LDS
 // in lane order.  Other shapes: thread per column, rows serial.
-__global__ __launch_bounds__(kColBlock) void colsum_kernel(const float* __restrict__ A, int64_t rows, int cols,
-                                                        int64_t ld, float* __restrict__ ws, float* __restrict__ out,
-                                                        uint32_t* __restrict__ cnt) {
-  extern __shared__ __attribute__((aligned(16))) float sh[];
-  const int nb = gridDim.x;
-  const int64_t r0 = rows * blockIdx.x / nb, r1 = rows * (blockIdx.x + 1) / nb;
-  // blockIdx.y selects a chunk of up to 4*256 columns (wide partial matrices)
-  const int cbase = blockIdx.y * kChunkCols;
+// One block of a colsum: row block bx of nb, column chunk by (counter cnt[by]).
+__device__ __forceinline__ void colsum_block(const float* __restrict__ A, int64_t rows, int cols, int64_t ld,
+                                             float* __restrict__ ws, float* __restrict__ out,
+                                             uint32_t* __restrict__ cnt, int bx, int nb, int by, float* sh) {
+  const int64_t r0 = rows * bx / nb, r1 = rows * (bx + 1) / nb;
+  // by selects a chunk of up to 256 columns (wide partial matrices)
+  const int cbase = by * kChunkCols;
   A += cbase;
   ws += cbase;
   const int ccols = (cols - cbase) < kChunkCols ? (cols - cbase) : kChunkCols;
@@ -86,13 +85,13 @@ __global__ __launch_bounds__(kColBlock) void colsum_kernel(const float* __restri
         t.z += v.z;
         t.w += v.w;
       }
-      st_sc1(ws + int64_t(blockIdx.x) * cols + 4 * threadIdx.x, t);
+      st_sc1(ws + int64_t(bx) * cols + 4 * threadIdx.x, t);
     }
   } else {
     for (int c = threadIdx.x; c < ccols; c += kColBlock) {
       float acc = 0.f;
       for (int64_t r = r0; r < r1; ++r) acc += A[r * ld + c];
-      __hip_atomic_store(ws + int64_t(blockIdx.x) * cols + c, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ws + int64_t(bx) * cols + c, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   // publish: the slab was stored write-through (sc1), so no release fence (which would write
@@ -102,7 +101,7 @@ __global__ __launch_bounds__(kColBlock) void colsum_kernel(const float* __restri
   __syncthreads();
   uint32_t* flag = reinterpret_cast<uint32_t*>(sh);  // the one LDS array (its pass-1 use is over)
   if (threadIdx.x == 0) {
-    const uint32_t t = __hip_atomic_fetch_add(cnt + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t t = __hip_atomic_fetch_add(cnt + by, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     flag[0] = (t == uint32_t(nb - 1)) ? 1u : 0u;
   }
   __syncthreads();
@@ -143,7 +142,40 @@ __global__ __launch_bounds__(kColBlock) void colsum_kernel(const float* __restri
       out[cbase + c] = t;
     }
   }
-  if (threadIdx.x == 0) __hip_atomic_store(cnt + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store(cnt + by, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kColBlock) void colsum_kernel(const float* __restrict__ A, int64_t rows, int cols,
+                                                        int64_t ld, float* __restrict__ ws, float* __restrict__ out,
+                                                        uint32_t* __restrict__ cnt) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  colsum_block(A, rows, cols, ld, ws, out, cnt, blockIdx.x, gridDim.x, blockIdx.y, sh);
+}
+
+// Several independent colsums in ONE launch (the weight-gradient partials of a whole backward
+// pass, flushed together: gasfm_amd._native.param_colsum).  The grid is the concatenation of
+// the jobs' (row block x column chunk) grids; a block finds its job by block range.
+constexpr int kMaxJobs = 48;
+struct ColsumJob {
+  const float* A;
+  float* ws;
+  float* out;
+  int64_t rows;
+  int64_t ld;
+  int cols, nb, nchunk, blk0, cnt0;
+};
+struct ColsumJobs {
+  ColsumJob j[kMaxJobs];
+  int n;
+};
+
+__global__ __launch_bounds__(kColBlock) void colsum_multi_kernel(ColsumJobs a, uint32_t* __restrict__ cnt) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  int q = 0;
+  while (q + 1 < a.n && int(blockIdx.x) >= a.j[q + 1].blk0) ++q;
+  const ColsumJob& J = a.j[q];
+  const int local = int(blockIdx.x) - J.blk0;
+  colsum_block(J.A, J.rows, J.cols, J.ld, J.ws, J.out, cnt + J.cnt0, local % J.nb, J.nb, local / J.nb, sh);
 }
 
 }  // namespace gasfm
@@ -167,4 +199,45 @@ extern "C" int gasfm_colsum(const float* A, int64_t rows, int32_t cols, int64_t 
   hipLaunchKernelGGL(colsum_kernel, dim3(nb, nchunk), dim3(kColBlock), 4 * kColBlock * sizeof(float), st, A, rows,
                      cols, ld, ws, out, counters);
   return launch_status("gasfm_colsum");
+}
+
+extern "C" int gasfm_colsum_multi(int32_t n, const float* const* A, const int64_t* rows, const int32_t* cols,
+                                  const int64_t* ld, float* const* ws, float* const* out, uint32_t* counters,
+                                  void* stream) {
+  GASFM_REQUIRE(n >= 0, "gasfm_colsum_multi: n=%d", n);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int base = 0; base < n; base += kMaxJobs) {
+    ColsumJobs a{};
+    int blocks = 0, cnt = 0;
+    a.n = (n - base) < kMaxJobs ? (n - base) : kMaxJobs;
+    for (int k = 0; k < a.n; ++k) {
+      const int i = base + k;
+      GASFM_REQUIRE(rows[i] >= 0 && cols[i] > 0 && ld[i] >= cols[i] && ws[i] && out[i] && (rows[i] == 0 || A[i]),
+                    "gasfm_colsum_multi: job %d rows=%lld cols=%d ld=%lld", i, (long long)rows[i], cols[i],
+                    (long long)ld[i]);
+      const int nb = colsum_blocks(rows[i]);
+      const int nchunk = (cols[i] + kChunkCols - 1) / kChunkCols;
+      a.j[k] = ColsumJob{A[i], ws[i], out[i], rows[i], ld[i], cols[i], nb, nchunk, blocks, cnt};
+      blocks += nb * nchunk;
+      cnt += nchunk;
+    }
+    if (blocks == 0) continue;
+    // each launch of the batch uses counters [0, cnt): launches on one stream run in order and
+    // every counter is reset by its last arriver
+    hipLaunchKernelGGL(colsum_multi_kernel, dim3(blocks), dim3(kColBlock), 4 * kColBlock * sizeof(float), st, a,
+                       counters);
+    const int s = launch_status("gasfm_colsum_multi");
+    if (s != GASFM_OK) return s;
+  }
+  return GASFM_OK;
+}
+
+extern "C" int32_t gasfm_colsum_multi_counters(int32_t n, const int32_t* cols) {
+  int best = 0;
+  for (int base = 0; base < n; base += kMaxJobs) {
+    int c = 0;
+    for (int i = base; i < n && i < base + kMaxJobs; ++i) c += (cols[i] + kChunkCols - 1) / kChunkCols;
+    best = c > best ? c : best;
+  }
+  return best;
 }

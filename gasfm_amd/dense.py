@@ -229,6 +229,7 @@ class NodeLnLinearFn(torch.autograd.Function):
         _native.node_ln_linear_fwd(x, ln_w, ln_b, eps, W, b, residual, y)
         ctx.save_for_backward(x, ln_w, ln_b, W)
         ctx.eps, ctx.residual, ctx.has_b = eps, residual, b is not None
+        ctx.defer = _native.defer_token(ln_w, ln_b, W, b)
         return y
 
     @staticmethod
@@ -241,7 +242,7 @@ class NodeLnLinearFn(torch.autograd.Function):
         rows = _native.node_part_rows(x.shape[0], n_out, ctx.residual)
         part = torch.empty((rows, n_out * n_in + n_out + 2 * n_in), dtype=torch.float32, device=x.device)
         _native.node_ln_linear_bwd(dy, x, ln_w, ln_b, ctx.eps, W, ctx.residual, dx, part)
-        tot = _native.colsum(part)
+        tot = _native.param_colsum(part, ctx.defer)
         o = n_out * n_in
         dW = tot[:o].view(n_out, n_in)
         db = tot[o:o + n_out] if ctx.has_b else None

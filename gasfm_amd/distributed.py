@@ -159,6 +159,7 @@ class ShardedAttentionFn(torch.autograd.Function):
         N = plan.num_targets
         out, smax, ssum = combine_partials(gathered, shard.world, N, heads, bias, shard.combine_items(N, XL.device))
         ctx.plan, ctx.heads, ctx.slope = plan, heads, slope
+        ctx.defer = _native.defer_token(att, bias)
         ctx.save_for_backward(XL, XR, att, bias, out, smax, ssum)
         return out
 
@@ -166,7 +167,7 @@ class ShardedAttentionFn(torch.autograd.Function):
     def backward(ctx, g):
         XL, XR, att, bias, out, smax, ssum = ctx.saved_tensors
         dXL, dXR, datt, dbias = attn_backward_raw(XL, XR, att, bias, ctx.plan, ctx.heads, ctx.slope, out, smax,
-                                                  ssum, g)
+                                                  ssum, g, defer=ctx.defer)
         return dXL, dXR, datt.view_as(att), dbias, None, None, None, None, None
 
 

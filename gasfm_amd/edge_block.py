@@ -24,30 +24,32 @@ from .attention import attn_backward_raw, attn_forward_partial, attn_forward_raw
 PROJ_SCALE = 0.25  # the "/ 4" of layers.py:945
 
 
-def _colsum_parts(part, rows):
-    return _native.colsum(part.view(rows, -1))
-
-
 class EdgePrologueFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, P, ln_w, ln_b, W, b, Wp, eps, pos=None):
-        """pos (point plan's inverse permutation): write the point half of XL in point order."""
+    def forward(ctx, P, ln_w, ln_b, W, b, Wp, eps, pos=None, W2=None, b2=None):
+        """XL = [W; W2] relu(LN(P)) + [b; b2]: W2/b2 given, W/b and W2/b2 are the point- and
+        camera-direction lin_l (each 32 x 32) as they are, else W [64 x 32] holds both.
+        pos (point plan's inverse permutation): write the point half of XL in point order."""
         E = P.shape[0]
-        XL = torch.empty((E, W.shape[0]), dtype=torch.float32, device=P.device)
-        _native.edge_prologue_fwd(P, ln_w, ln_b, eps, W.contiguous(), b.contiguous(), XL, pos)
+        XL = torch.empty((E, 64), dtype=torch.float32, device=P.device)
+        split = W2 is not None
+        _native.edge_prologue_fwd(P, ln_w, ln_b, eps, W.contiguous(), b.contiguous(), XL, pos,
+                                  W2.contiguous() if split else None, b2.contiguous() if split else None)
         ctx.eps = eps
         ctx.has_ln = ln_w is not None
+        ctx.split = split
+        ctx.defer = _native.defer_token(ln_w, ln_b, W, b, W2, b2)
         ctx.set_materialize_grads(False)
-        ctx.save_for_backward(P, ln_w, ln_b, W, Wp)
+        ctx.save_for_backward(P, ln_w, ln_b, W, Wp, W2)
         token = P.new_empty((1, 1)).expand(E, P.shape[1])
         return XL, token
 
     @staticmethod
     def backward(ctx, dXL, dtoken):
-        P, ln_w, ln_b, W, Wp = ctx.saved_tensors
+        P, ln_w, ln_b, W, Wp, W2 = ctx.saved_tensors
         E = P.shape[0]
         if dXL is None:
-            dXL = torch.zeros((E, W.shape[0]), dtype=torch.float32, device=P.device)
+            dXL = torch.zeros((E, 64), dtype=torch.float32, device=P.device)
         dXL = dXL.contiguous()
         dRes = None
         if dtoken is not None and dtoken.stride(0) != 0:
@@ -56,13 +58,16 @@ class EdgePrologueFn(torch.autograd.Function):
         rows = _native.edge_part_floats(0, E) // (64 * 32 + 64 + 64)
         part = torch.empty((rows, 64 * 32 + 64 + 64), dtype=torch.float32, device=P.device)
         _native.edge_prologue_bwd(dXL, P, dRes, ln_w, ln_b, ctx.eps, W.contiguous(),
-                                  Wp.contiguous() if dRes is not None else None, PROJ_SCALE, dP, part)
-        tot = _colsum_parts(part, rows)
+                                  Wp.contiguous() if dRes is not None else None, PROJ_SCALE, dP, part,
+                                  W2.contiguous() if W2 is not None else None)
+        tot = _native.param_colsum(part.view(rows, -1), ctx.defer)
         dW = tot[:64 * 32].view(64, 32)
         db = tot[64 * 32:64 * 32 + 64]
         dgam = tot[64 * 32 + 64:64 * 32 + 96] if ctx.has_ln else None
         dbet = tot[64 * 32 + 96:] if ctx.has_ln else None
-        return dP, dgam, dbet, dW, db, None, None, None
+        if ctx.split:
+            return dP, dgam, dbet, dW[:32], db[:32], None, None, None, dW[32:], db[32:]
+        return dP, dgam, dbet, dW, db, None, None, None, None, None
 
 
 class DualAttentionFn(torch.autograd.Function):
@@ -87,6 +92,7 @@ class DualAttentionFn(torch.autograd.Function):
                                              shard.combine_items(N, XL.device))
         ctx.plans = (plan_pt, plan_cam)
         ctx.heads, ctx.slope, ctx.xl_sorted = heads, slope, xl_sorted
+        ctx.defer = _native.defer_token(att_pt, att_cam, bias_pt, bias_cam)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(XL, XR_pt, XR_cam, att_pt, att_cam, bias_pt, bias_cam, out_p, mp, sp, out_c, mc, sc)
         return out_p, out_c
@@ -102,9 +108,10 @@ class DualAttentionFn(torch.autograd.Function):
             g_c = torch.zeros_like(out_c)
         dXL = torch.empty_like(XL)
         _, dXRp, dattp, dbp = attn_backward_raw(XL[:, :h], XR_pt, att_pt, bias_pt, plan_pt, ctx.heads, ctx.slope,
-                                                out_p, mp, sp, g_p, dXL=dXL[:, :h], xl_sorted=ctx.xl_sorted)
+                                                out_p, mp, sp, g_p, dXL=dXL[:, :h], xl_sorted=ctx.xl_sorted,
+                                                defer=ctx.defer)
         _, dXRc, dattc, dbc = attn_backward_raw(XL[:, h:], XR_cam, att_cam, bias_cam, plan_cam, ctx.heads, ctx.slope,
-                                                out_c, mc, sc, g_c, dXL=dXL[:, h:])
+                                                out_c, mc, sc, g_c, dXL=dXL[:, h:], defer=ctx.defer)
         return (dXL, dXRp, dXRc, dattp.view_as(att_pt), dattc.view_as(att_cam), dbp, dbc, None, None, None, None,
                 None, None, None)
 
@@ -119,6 +126,7 @@ class EdgeEpilogueFn(torch.autograd.Function):
         ctx.eps = eps
         ctx.edges = edges
         ctx.sg_shape = Sg.shape
+        ctx.defer = _native.defer_token(Wp)
         ctx.save_for_backward(P, P0, Wp_c, ln_w, ln_b)
         return out
 
@@ -139,7 +147,7 @@ class EdgeEpilogueFn(torch.autograd.Function):
         _native.edge_epilogue_bwd(pc.items, pc.n_items, dPo, P, P0, ln_w, ln_b, ctx.eps, Wp, PROJ_SCALE, dSv,
                                   part_dsv, dP0, part_w)
         bwd_combine(pc, part_dsv, 32, dSv)
-        dWp = _native.colsum(part_w).view(32, Wp.shape[1])
+        dWp = _native.param_colsum(part_w, ctx.defer).view(32, Wp.shape[1])
         dSg = _native.colsum(dSv)          # == d bias_proj: every edge belongs to one camera
         # point side: dSp = per-point sum of dP'/4 through the point permutation
         dSp = torch.empty((edges.n, 32), dtype=torch.float32, device=dev)

@@ -329,6 +329,11 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
             ok &= c.bias is not None
         return bool(ok)
 
+    def lin_l_pair(self):
+        """(point lin_l weight, bias), (camera lin_l weight, bias): XL = [point | camera]."""
+        a, b = self.proj2scenepoint.graph_conv.lin_l, self.proj2view.graph_conv.lin_l
+        return (a.weight, a.bias), (b.weight, b.bias)
+
     def lin_l_stack(self):
         a, b = self.proj2scenepoint.graph_conv.lin_l, self.proj2view.graph_conv.lin_l
         return torch.cat([a.weight, b.weight], 0), torch.cat([a.bias, b.bias], 0)
@@ -513,9 +518,9 @@ class GraphAttnSfMLayer(Module):
         ln = self.prev_projfeat_norm_layer
         gfu = self.global_feature_update
         pfu = self.projection_feature_update
-        W, b = gfu.lin_l_stack()
+        (W, b), (W2, b2) = gfu.lin_l_pair()
         pos = plans["proj2scenepoint"].pos
-        XL, token = EdgePrologueFn.apply(P, ln.weight, ln.bias, W, b, pfu.lin_proj.weight, ln.eps, pos)
+        XL, token = EdgePrologueFn.apply(P, ln.weight, ln.bias, W, b, pfu.lin_proj.weight, ln.eps, pos, W2, b2)
         pts, view, glob = gfu.forward_fused(XL, plans, prev_pt, prev_view, prev_glob, xl_sorted=pos is not None,
                                             carry=carry, pfu=pfu, nxt=nxt)
         sp, sv, sg = pfu.node_terms(pts, view, glob, *((carry.pop("SA", None), carry.pop("SV", None),
@@ -737,21 +742,34 @@ class GraphAttnSfMNet(Module):
             args = (pts if sf else None, view if sf else None, glob if sf else None)
             if P.is_cuda and P.shape[1] == 32 and fgu.fusable():
                 # raw (un-normalised) projection features (graph_attn_sfm.py:141-148): no LN prologue
-                W, b = fgu.lin_l_stack()
+                (W, b), (W2, b2) = fgu.lin_l_pair()
                 pos = plans["proj2scenepoint"].pos
-                XL, _ = EdgePrologueFn.apply(P.contiguous(), None, None, W, b, None, 1e-5, pos)
+                XL, _ = EdgePrologueFn.apply(P.contiguous(), None, None, W, b, None, 1e-5, pos, W2, b2)
                 pts, view, _ = fgu.forward_fused(XL, plans, *args, xl_sorted=pos is not None, carry=carry)
             else:
                 pts, view, _ = fgu.forward_plan(P, plans, *args)
         return P, pts, view
 
+    # Weight-gradient column sums of the backward pass run as one batched launch at its end
+    # (_native.param_colsum) when every parameter's .grad is unset at forward time (the usual
+    # zero_grad(set_to_none=True) loop); gradient accumulation into existing .grad tensors
+    # takes the immediate path.  False disables the batching.
+    batch_weight_grads = True
+
     def forward(self, data, shard=None, partial_plans=None):
+        from . import _native
         values = data.x.values
         device = values.device
         edges = self.edge_index_for(data, device)
         if shard is not None:
             edges = copy.copy(edges)
             edges.plans = dict(edges.plans, _shard=shard, _partial=partial_plans)
+        defer = (self.batch_weight_grads and values.is_cuda and torch.is_grad_enabled()
+                 and all(p.grad is None for p in self.parameters()))
+        with _native.deferring_param_grads(defer):
+            return self._forward_outputs(data, values, edges, device)
+
+    def _forward_outputs(self, data, values, edges, device):
         P, pts, view = self.forward_features(values, edges)
         pred = {}
         if self.depth_head_enabled:

@@ -36,6 +36,7 @@ class PointTailFn(torch.autograd.Function):
         _native.point_tail_fwd(prev, agg, Wp, bp, ln_w, ln_b, eps, Wm, bm, out)
         ctx.save_for_backward(prev, agg, Wp, bp, ln_w, ln_b, Wm)
         ctx.eps = eps
+        ctx.defer = _native.defer_token(Wp, bp, ln_w, ln_b, Wm, bm)
         return out
 
     @staticmethod
@@ -51,7 +52,7 @@ class PointTailFn(torch.autograd.Function):
         else:
             part = _f32(rows, cols, like=agg)
             _native.point_tail_bwd(dout, prev, agg, Wp, bp, ln_w, ln_b, ctx.eps, Wm, dx, dagg, part)
-            tot = _native.colsum(part)
+            tot = _native.param_colsum(part, ctx.defer)
         o = 0
         dWm = tot[o:o + P_W * P_W].view(P_W, P_W)
         o += P_W * P_W
@@ -73,6 +74,7 @@ class PointHubFn(torch.autograd.Function):
         _native.point_hub_fwd(p, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR)
         ctx.save_for_backward(p, gA, bA, WA, WB, gC, bC, WC, bWC, WD)
         ctx.eps = eps
+        ctx.defer = _native.defer_token(gA, bA, WA, WB, bB, gC, bC, WC, bWC, WD, bD)
         ctx.set_materialize_grads(False)
         return p.view_as(p), SA, XL, XR
 
@@ -97,7 +99,7 @@ class PointHubFn(torch.autograd.Function):
             part_a = _f32(ra, ca, like=p)
             # in place: each element of dp is read (as dRes) and written by the same lane
             _native.point_hub_bwd_ab(p, ctx.eps, gA, bA, WA, WB, dSA, dXL, dp, dp, part_a)
-            tc, ta = _native.colsum(part_c), _native.colsum(part_a)
+            tc, ta = _native.param_colsum(part_c, ctx.defer), _native.param_colsum(part_a, ctx.defer)
         o = 0
         dWC = tc[o:o + A_W * P_W].view(A_W, P_W)
         o += A_W * P_W

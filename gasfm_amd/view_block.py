@@ -40,6 +40,7 @@ class ViewTailFn(torch.autograd.Function):
         view = torch.addmm(xb, h, Wm.t())
         ctx.save_for_backward(agg, x, rs, h, Wp, ln_w, ln_b, Wm)
         ctx.eps, ctx.has_prev = eps, prev is not None
+        ctx.defer = _native.defer_token(Wp, bp, ln_w, ln_b, bm)
         return view
 
     @staticmethod
@@ -57,7 +58,7 @@ class ViewTailFn(torch.autograd.Function):
             part = _f32((m + TR - 1) // TR, cols, like=x)
             _native.view_tail_bwd(dview, dh, x, rs, agg, Wp, ln_w, ln_b, dx, dagg, part,
                                   _native.view_scratch(m, D, x.device))
-            tot = _native.colsum(part)
+            tot = _native.param_colsum(part, ctx.defer)
         dWp = tot[:D * A_W].view(D, A_W)
         dbp, dg, dbt, dbm = (tot[D * A_W + k * D:D * A_W + (k + 1) * D] for k in range(4))
         return (dx if ctx.has_prev else None), dagg, dWp, dbp, dg, dbt, dWm, dbm, None
@@ -78,6 +79,7 @@ class ViewHubFn(torch.autograd.Function):
         XL = torch.addmm(bl, v, Wl.t())
         ctx.save_for_backward(v, rs, t, gC, bC, Wv, Wl, gA, bA, Wa, Wr)
         ctx.eps = eps
+        ctx.defer = _native.defer_token(gC, bC, Wv, gA, bA, Wa, ba, Wr, br, bl)
         ctx.set_materialize_grads(False)
         return v.view_as(v), SV, XL, XR
 
@@ -98,7 +100,7 @@ class ViewHubFn(torch.autograd.Function):
             part = _f32((m + TR - 1) // TR, cols, like=v)
             _native.view_hub_bwd(v, rs, gC, bC, Wv, gA, bA, Wa, t, Wr, dSV, dXR, dXL, dacc, part,
                                  _native.view_scratch(m, D, v.device))
-            tot = _native.colsum(part)
+            tot = _native.param_colsum(part, ctx.defer)
         o = 0
         dWv = tot[o:o + A_W * D].view(A_W, D)
         o += A_W * D

@@ -152,6 +152,16 @@ int32_t gasfm_colsum_counters(int32_t cols);
 int gasfm_colsum(const float* A, int64_t rows, int32_t cols, int64_t ld,
                  float* ws, float* out, uint32_t* counters, void* stream);
 
+/* n independent colsums (job i: A[i] rows[i] x cols[i], row stride ld[i], workspace ws[i] of
+ * gasfm_colsum_ws_floats(rows[i], cols[i]) floats, result out[i]) in ONE launch per 48 jobs;
+ * counters: gasfm_colsum_multi_counters(n, cols) zeroed uint32 (self-resetting, shared with
+ * gasfm_colsum: one array per device, calls ordered on one stream).  Same per-job results,
+ * bit for bit, as gasfm_colsum.  Used for the weight-gradient partials of a backward pass. */
+int gasfm_colsum_multi(int32_t n, const float* const* A, const int64_t* rows, const int32_t* cols,
+                       const int64_t* ld, float* const* ws, float* const* out, uint32_t* counters,
+                       void* stream);
+int32_t gasfm_colsum_multi_counters(int32_t n, const int32_t* cols);
+
 /* ---- fused per-edge block body (F = n_feat_proj = 32; XL width 64 = point|camera) ---- */
 
 /* Floats of the per-workgroup partial buffer: which = 0 -> edge_prologue_bwd
@@ -166,8 +176,8 @@ int gasfm_edge_part_floats(int32_t which, int64_t E, int32_t n_items);
  * in point-segment order), so the point-direction attention streams it (perm = NULL forward,
  * xl_by_position backward); the camera half stays at row e. */
 int gasfm_edge_prologue_fwd(const float* P, int64_t E, const float* ln_w, const float* ln_b, float eps,
-                            const float* W, const float* b, float* Y, int64_t ldY, const int32_t* pos,
-                            void* stream);
+                            const float* W, const float* W2, const float* b, const float* b2, float* Y,
+                            int64_t ldY, const int32_t* pos, void* stream);
 
 /* P'[e] = P[e] + scale*(Wp [relu(LN(P[e])) | P0[e]] + bp + Sp[pt[e]] + Sv[cam[e]] + Sg)
  * (GraphAttnSfMProjectionFeatureUpdate.forward, layers.py:927-945, + residual 254-261;
@@ -190,8 +200,8 @@ int gasfm_edge_epilogue_bwd(const gasfm_work_item* items, int32_t n_items, const
  * per-workgroup partials of dW, db, dgamma, dbeta (LayerNorm/ReLU/lin_l backward). */
 int gasfm_edge_prologue_bwd(const float* dXL, int64_t ldX, const float* P, const float* dRes,
                             int64_t E, const float* ln_w, const float* ln_b, float eps,
-                            const float* W, const float* Wp, int32_t ldWp, float scale,
-                            float* dP, float* part, void* stream);
+                            const float* W, const float* W2, const float* Wp, int32_t ldWp,
+                            float scale, float* dP, float* part, void* stream);
 
 /* out[seg] = scale * sum_{edges of the item} X[src]  (32-wide rows; src via perm).
  * Replaces the index_add scatter of scenepoint_features[pt] (layers.py:940). */

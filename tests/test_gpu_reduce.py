@@ -22,3 +22,67 @@ def test_colsum_matches_fp64_and_is_deterministic(device, rows, cols):
 def test_colsum_strided_rows(device):
     A = torch.randn(999, 80, device=device)
     torch.testing.assert_close(_native.colsum(A[:, :64]), A[:, :64].sum(0), rtol=1e-5, atol=1e-4)
+
+
+def test_colsum_multi_bitwise_equals_colsum(device):
+    """One gasfm_colsum_multi launch over 60 jobs (two launches of <= 48) == 60 gasfm_colsum calls."""
+    import ctypes
+    g = torch.Generator().manual_seed(5)
+    shapes = [(int(r), int(c)) for r, c in zip(torch.randint(0, 3000, (60,), generator=g),
+                                                torch.randint(1, 3000, (60,), generator=g))]
+    As = [torch.randn(r, c, generator=g).to(device) for r, c in shapes]
+    ref = [_native.colsum(A) for A in As]
+    L = _native.lib()
+    n = len(As)
+    ws = [torch.empty(int(L.gasfm_colsum_ws_floats(r, c)), device=device) for r, c in shapes]
+    out = [torch.full((c,), float("nan"), device=device) for _, c in shapes]
+    arr = lambda ty, xs: (ty * n)(*xs)  # noqa: E731
+    cols = arr(ctypes.c_int32, [c for _, c in shapes])
+    cnt = _native._counters(torch.device(device), L.gasfm_colsum_multi_counters(n, cols))
+    for _ in range(2):  # the counters must reset
+        st = L.gasfm_colsum_multi(n, arr(ctypes.c_void_p, [a.data_ptr() for a in As]),
+                                  arr(ctypes.c_int64, [r for r, _ in shapes]), cols,
+                                  arr(ctypes.c_int64, [c for _, c in shapes]),
+                                  arr(ctypes.c_void_p, [w.data_ptr() for w in ws]),
+                                  arr(ctypes.c_void_p, [o.data_ptr() for o in out]), _native._p(cnt),
+                                  _native._stream(out[0]))
+        assert st == 0, _native.lib().gasfm_last_error()
+        torch.cuda.synchronize()
+        for a, b in zip(out, ref):
+            assert torch.equal(a, b)
+
+
+def test_batched_weight_grads_bitwise_equal_immediate(device):
+    """GraphAttnSfMNet: the end-of-backward batched weight-gradient sums give the same bits as the
+    immediate ones, and a second backward (accumulating into existing .grad) stays correct."""
+    import gasfm_amd
+    from gasfm_amd import synthetic
+    from oracle.weights import deterministic_state_dict
+    sc = synthetic.scaled_config4(0.02, seed=3)
+    data = gasfm_amd.SceneData.from_synthetic(sc).to(device)
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=3))
+    net.load_state_dict(deterministic_state_dict(net.state_dict()))
+    net = net.to(device)
+    g = torch.Generator().manual_seed(2)
+    cP = torch.randn((sc.m, 3, 4), generator=g).to(device)
+    cX = torch.randn((4, sc.n), generator=g).to(device)
+
+    def grads(batch, twice=False):
+        net.batch_weight_grads = batch
+        for p in net.parameters():
+            p.grad = None
+        for _ in range(2 if twice else 1):
+            pred = net(data)
+            ((pred["Ps_norm"] * cP).sum() + (pred["pts3D"] * cX).sum()).backward()
+        torch.cuda.synchronize()
+        return {k: p.grad.clone() for k, p in net.named_parameters()}
+
+    imm, bat = grads(False), grads(True)
+    assert not _native._PENDING, "a batch was left unflushed"
+    for k in imm:
+        assert torch.equal(imm[k], bat[k]), k
+    acc_imm, acc_bat = grads(False, twice=True), grads(True, twice=True)
+    for k in imm:
+        assert torch.equal(acc_imm[k], acc_bat[k]), k
+        torch.testing.assert_close(acc_bat[k], 2 * imm[k], rtol=1e-5, atol=1e-6)
+    net.batch_weight_grads = True
