@@ -48,6 +48,9 @@ _SIGS = {
     "gasfm_colsum_multi": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_colsum_multi_counters": (_i32, [_i32, _vp]),
     "gasfm_colsum": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, _vp]),
+    "gasfm_colsum_tall_ok": (_i32, [_i32]),
+    "gasfm_colsum_tall_ws_floats": (_i64, [_i64, _i32]),
+    "gasfm_colsum_tall": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp]),
     "gasfm_edge0_part_rows": (_i32, [_i32, _i64, _i32]),
     "gasfm_edge0_prologue_fwd": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_edge0_epilogue_fwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp,
@@ -128,8 +131,32 @@ def _p(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+_LAUNCH_STREAM = None   # set by launching_on(): libgasfm launches go there instead of torch's stream
+
+
 def _stream(t):
-    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+    s = _LAUNCH_STREAM
+    if s is None:
+        s = torch.cuda.current_stream(t.device)
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class launching_on:
+    """Route libgasfm launches (only those: torch ops and allocations stay on torch's current
+    stream) to ``stream`` inside the block; see gasfm_amd/streams.py."""
+
+    def __init__(self, stream):
+        self.stream = stream
+
+    def __enter__(self):
+        global _LAUNCH_STREAM
+        self.prev, _LAUNCH_STREAM = _LAUNCH_STREAM, self.stream
+        return self
+
+    def __exit__(self, *exc):
+        global _LAUNCH_STREAM
+        _LAUNCH_STREAM = self.prev
+        return False
 
 
 # ---------------------------------------------------------------- host graph preprocessing
@@ -207,10 +234,15 @@ _COUNTERS = {}
 
 
 def _counters(device, n):
-    """Per-device zeroed uint32 ticket counters for gasfm_colsum (self-resetting)."""
+    """Per-device zeroed uint32 ticket counters for gasfm_colsum (self-resetting).
+
+    Allocated once, large (a replacement allocated while a hipGraph is being captured would
+    leave the nodes captured before it pointing at the freed array)."""
     c = _COUNTERS.get(device)
     if c is None or c.numel() < n:
-        c = torch.zeros(max(n, 256), dtype=torch.int32, device=device)
+        if c is not None and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError(f"colsum counters: {n} needed during hipGraph capture, {c.numel()} allocated")
+        c = torch.zeros(max(n, 65536), dtype=torch.int32, device=device)
         _COUNTERS[device] = c
     return c
 
@@ -227,6 +259,28 @@ def colsum(A, out=None):
     st = L.gasfm_colsum(_p(A), rows, cols, max(A.stride(0), cols), _p(ws), _p(out), _p(cnt), _stream(out))
     check(st, "gasfm_colsum")
     return out
+
+
+def colsum_tall_ok(A):
+    return (A.dim() == 2 and A.is_contiguous() and A.dtype == torch.float32
+            and bool(lib().gasfm_colsum_tall_ok(A.shape[1])))
+
+
+def colsum_tall(A, out=None):
+    """Column sums of a contiguous tall [rows, cols] fp32 CUDA tensor (colsum_tall_ok)."""
+    rows, cols = A.shape
+    if out is None:
+        out = torch.empty(cols, dtype=torch.float32, device=A.device)
+    L = lib()
+    ws = torch.empty(max(1, int(L.gasfm_colsum_tall_ws_floats(rows, cols))), dtype=torch.float32, device=A.device)
+    # its own counter word, after the colsum ones (one array per device, self-resetting)
+    cnt = _counters(A.device, _TALL_COUNTER + 1)[_TALL_COUNTER:]
+    st = L.gasfm_colsum_tall(_p(A), rows, cols, _p(ws), _p(out), _p(cnt), _stream(out))
+    check(st, "gasfm_colsum_tall")
+    return out
+
+
+_TALL_COUNTER = 4095
 
 
 # ---------------------------------------------------------------- batched weight-gradient sums

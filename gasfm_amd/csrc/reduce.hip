@@ -178,9 +178,123 @@ __global__ __launch_bounds__(kColBlock) void colsum_multi_kernel(ColsumJobs a, u
   colsum_block(J.A, J.rows, J.cols, J.ld, J.ws, J.out, cnt + J.cnt0, local % J.nb, J.nb, local / J.nb, sh);
 }
 
+// ---------------------------------------------------------------- tall, narrow column sums
+// Column sums of a CONTIGUOUS [rows, cols] matrix with few columns and many rows (bias
+// gradients over E edge rows or n point rows: [4M, 2], [200k, 64], [200k, 3]).  The matrix is
+// read as a flat array: element f belongs to column f % cols.  Thread t of a block handles
+// flat elements t + 256 i; with S = lcm(cols, 256) and K = S / 256 accumulators, accumulator
+// i % K only ever sees column (t + 256 (i % K)) % cols, so every load is a coalesced dword
+// load and no index arithmetic is per element.  Block sums: the K x 256 accumulators go to
+// LDS at flat position q = t + 256 j (column q % cols) and fold by halving strides that are
+// multiples of cols (fixed order).  Then the colsum hand-off: slab ws[b, cols] stored
+// write-through, one ticket, and the last block folds the [nb, cols] slab with the same flat
+// routine.  Deterministic; one launch.
+constexpr int kTallBlock = 256;
+constexpr int kTallMaxK = 8;          // lcm(cols, 256) <= 2048
+constexpr int kTallMaxSlab = 16384;   // nb * cols floats the last block reads
+
+__host__ __device__ constexpr int gcd_i(int a, int b) { return b == 0 ? a : gcd_i(b, a % b); }
+
+__host__ __device__ inline int tall_k(int cols) { return cols / gcd_i(cols, kTallBlock); }
+
+// flat [n] -> per-column sums in lds[0, cols); every thread returns after the block barrier.
+// atomic: sc1 (agent-scope) loads for the slab written by other blocks.
+template <bool kAtomic>
+__device__ __forceinline__ void tall_block_sum(const float* __restrict__ A, int64_t n, int cols, int K,
+                                               float* __restrict__ lds) {
+  const int t = threadIdx.x;
+  const int U = K * ((8 + K - 1) / K);  // loads in flight per thread, a multiple of K
+  float acc[kTallMaxK];
+#pragma unroll
+  for (int j = 0; j < kTallMaxK; ++j) acc[j] = 0.f;
+  const int64_t step = int64_t(kTallBlock) * U;
+  int64_t base = 0;
+  for (; base + step <= n; base += step) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (u < U) {
+        const float* q = A + base + t + int64_t(kTallBlock) * u;
+        v[u] = kAtomic ? __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *q;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (u < U) acc[u % K] += v[u];
+  }
+  for (int u = 0; base + t + int64_t(kTallBlock) * u < n; ++u) {
+    const float* q = A + base + t + int64_t(kTallBlock) * u;
+    const float x = kAtomic ? __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *q;
+#pragma unroll
+    for (int j = 0; j < kTallMaxK; ++j)
+      if (j == u % K) acc[j] += x;
+  }
+  const int S = kTallBlock * K;
+#pragma unroll
+  for (int j = 0; j < kTallMaxK; ++j)
+    if (j < K) lds[t + kTallBlock * j] = acc[j];
+  __syncthreads();
+  for (int stride = S / 2; stride >= cols && stride % cols == 0; stride /= 2) {
+    for (int i = t; i < stride; i += kTallBlock) lds[i] += lds[i + stride];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kTallBlock) void colsum_tall_kernel(const float* __restrict__ A, int64_t rows, int cols,
+                                                                 float* __restrict__ ws, float* __restrict__ out,
+                                                                 uint32_t* __restrict__ cnt) {
+  __shared__ float lds[kTallBlock * kTallMaxK];
+  __shared__ uint32_t flag;
+  const int K = tall_k(cols);
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int64_t r0 = rows * b / nb, r1 = rows * (b + 1) / nb;
+  tall_block_sum<false>(A + r0 * cols, (r1 - r0) * cols, cols, K, lds);
+  if (threadIdx.x < cols)
+    __hip_atomic_store(ws + int64_t(b) * cols + threadIdx.x, lds[threadIdx.x], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t tk = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = (tk == uint32_t(nb - 1)) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (flag == 0u) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  tall_block_sum<true>(ws, int64_t(nb) * cols, cols, K, lds);
+  if (threadIdx.x < cols) out[threadIdx.x] = lds[threadIdx.x];
+  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+static int tall_blocks(int64_t rows, int cols) {
+  int64_t nb = (rows * cols + 8191) / 8192;  // >= 8k floats per block
+  const int64_t cap = kTallMaxSlab / cols < 1024 ? kTallMaxSlab / cols : 1024;
+  if (nb > cap) nb = cap;
+  return int(nb < 1 ? 1 : nb);
+}
+
 }  // namespace gasfm
 
 using namespace gasfm;
+
+extern "C" int32_t gasfm_colsum_tall_ok(int32_t cols) {
+  return cols > 0 && cols <= kTallBlock && tall_k(cols) <= kTallMaxK ? 1 : 0;
+}
+
+extern "C" int64_t gasfm_colsum_tall_ws_floats(int64_t rows, int32_t cols) {
+  return cols > 0 ? int64_t(tall_blocks(rows, cols)) * cols : 0;
+}
+
+extern "C" int gasfm_colsum_tall(const float* A, int64_t rows, int32_t cols, float* ws, float* out,
+                                 uint32_t* counter, void* stream) {
+  GASFM_REQUIRE(rows >= 0 && gasfm_colsum_tall_ok(cols), "gasfm_colsum_tall: rows=%lld cols=%d",
+                (long long)rows, cols);
+  GASFM_REQUIRE(ws && out && counter && (rows == 0 || A), "gasfm_colsum_tall: null pointer");
+  const int nb = tall_blocks(rows, cols);
+  hipLaunchKernelGGL(colsum_tall_kernel, dim3(nb), dim3(kTallBlock), 0, reinterpret_cast<hipStream_t>(stream), A,
+                     rows, cols, ws, out, counter);
+  return launch_status("gasfm_colsum_tall");
+}
 
 extern "C" int64_t gasfm_colsum_ws_floats(int64_t rows, int32_t cols) {
   return int64_t(colsum_blocks(rows)) * cols;

@@ -23,12 +23,15 @@ _MAX_SLICES = 256          # ... and at most this many slices: a 32x64 weight gr
 
 def _colsum(a):
     """Column sums of a 2-D CUDA tensor: the one-launch gasfm_colsum for short, wide inputs
-    (split-K slices, camera rows); torch's reduction for tall ones (200k point rows), where
-    colsum's <= 64 row blocks per column chunk would leave the chip idle."""
-    if a.shape[0] > 4096:
-        return a.sum(0)
+    (split-K slices, camera rows); gasfm_colsum_tall for tall, narrow ones (E edge or 200k
+    point rows), where colsum's <= 64 row blocks per column chunk would leave the chip idle.
+    Not torch's sum: its global reduction replayed from a captured hipGraph gave wrong sums
+    (DESIGN.md §5)."""
     from . import _native
-    return _native.colsum(a.contiguous())
+    a = a.contiguous()
+    if a.shape[0] > 4096 and _native.colsum_tall_ok(a):
+        return _native.colsum_tall(a)
+    return _native.colsum(a)
 
 
 def splitk_wgrad(dy, x):

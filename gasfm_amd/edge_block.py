@@ -78,7 +78,7 @@ class DualAttentionFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, XL, XR_pt, XR_cam, att_pt, att_cam, bias_pt, bias_cam, plan_pt, plan_cam, heads, slope,
-                plan_cam_partial=None, shard=None, xl_sorted=False):
+                plan_cam_partial=None, shard=None, xl_sorted=False, sec=None):
         h = XL.shape[1] // 2
         XLp, XLc = XL[:, :h], XL[:, h:]
         out_p, mp, sp = attn_forward_raw(XLp, XR_pt, att_pt, bias_pt, plan_pt, heads, slope, xl_sorted=xl_sorted)
@@ -92,6 +92,7 @@ class DualAttentionFn(torch.autograd.Function):
                                              shard.combine_items(N, XL.device))
         ctx.plans = (plan_pt, plan_cam)
         ctx.heads, ctx.slope, ctx.xl_sorted = heads, slope, xl_sorted
+        ctx.sec = sec  # streams.SideSection of this block: joined before the point-side gradient is read
         ctx.defer = _native.defer_token(att_pt, att_cam, bias_pt, bias_cam)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(XL, XR_pt, XR_cam, att_pt, att_cam, bias_pt, bias_cam, out_p, mp, sp, out_c, mc, sc)
@@ -101,6 +102,8 @@ class DualAttentionFn(torch.autograd.Function):
     def backward(ctx, g_p, g_c):
         XL, XR_pt, XR_cam, att_pt, att_cam, bias_pt, bias_cam, out_p, mp, sp, out_c, mc, sc = ctx.saved_tensors
         plan_pt, plan_cam = ctx.plans
+        if ctx.sec is not None:
+            ctx.sec.join()
         h = XL.shape[1] // 2
         if g_p is None:
             g_p = torch.zeros_like(out_p)
@@ -113,7 +116,7 @@ class DualAttentionFn(torch.autograd.Function):
         _, dXRc, dattc, dbc = attn_backward_raw(XL[:, h:], XR_cam, att_cam, bias_cam, plan_cam, ctx.heads, ctx.slope,
                                                 out_c, mc, sc, g_c, dXL=dXL[:, h:], defer=ctx.defer)
         return (dXL, dXRp, dXRc, dattp.view_as(att_pt), dattc.view_as(att_cam), dbp, dbc, None, None, None, None,
-                None, None, None)
+                None, None, None, None)
 
 
 class EdgeEpilogueFn(torch.autograd.Function):

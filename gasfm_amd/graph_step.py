@@ -24,6 +24,20 @@ Usage::
 import torch
 
 
+def _grad_mismatch(params, ref_grads, rtol):
+    for i, (p, r) in enumerate(zip(params, ref_grads)):
+        g = p.grad
+        if (g is None) != (r is None):
+            return f"parameter {i}: gradient presence differs"
+        if g is None:
+            continue
+        err = float((g.double() - r.double()).abs().max()) if g.numel() else 0.0
+        scale = float(r.double().abs().max()) if r.numel() else 0.0
+        if not err <= rtol * max(1.0, scale):
+            return f"parameter {i} {tuple(g.shape)}: max |diff| {err:.3g} vs max |ref| {scale:.3g}"
+    return None
+
+
 class CapturedStep:
     """fn captured once and replayed per call.
 
@@ -54,6 +68,8 @@ class CapturedStep:
             for _ in range(max(1, warmup)):
                 self._zero()
                 ref = self.fn().detach().clone()
+            ref_grads = [p.grad.detach().clone() if p.grad is not None else None for p in self.params] \
+                if check else None
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self._zero()
@@ -77,6 +93,12 @@ class CapturedStep:
             ok = abs(a - b) <= rtol * max(1.0, abs(b))
             if not ok:
                 self.fallback_reason = f"replayed loss {a!r} != eager loss {b!r}"
+            else:  # the gradients too: a replay can be wrong where the loss is right
+                bad = _grad_mismatch(self.params, ref_grads, rtol)
+                if bad is not None:
+                    ok = False
+                    self.fallback_reason = f"replayed gradient != eager gradient ({bad})"
+            del ref_grads
         if not self._agree(ok):
             self.fallback_reason = self.fallback_reason or "replay check failed on another rank"
             self._zero()

@@ -25,7 +25,7 @@ import torch
 import torch.nn.functional as F
 from torch.nn import Identity, LayerNorm, Linear, Module, ModuleList, ReLU, Sequential
 
-from . import dense, edge_ops, point_block, view_block
+from . import _native, dense, edge_ops, point_block, streams, view_block
 from .attention import AttnPlan, gat_attention
 from .edge_block import Block0EpilogueFn, Block0PrologueFn, DualAttentionFn, EdgeEpilogueFn, EdgePrologueFn
 from .gatv2 import GATv2Conv
@@ -134,10 +134,12 @@ class _NodeAggregation(Module):
             return conv.lin_r(zero).expand(num_targets, -1)
         return dense.linear(dense.sequential(getattr(self, self._state_key), prev), conv.lin_r)
 
-    def tail(self, x, prev):
-        """Everything after the GATv2 aggregation: proj, state skip, LN+ReLU, MLP, skip."""
+    def tail(self, x, prev, sec=None):
+        """Everything after the GATv2 aggregation: proj, state skip, LN+ReLU, MLP, skip.
+        sec: streams.SideSection the fused point tail runs in (None: torch's stream)."""
         if point_block.tail_fusable(self, x, prev):
-            return point_block.tail(self, x, prev)
+            return point_block.tail(self, x, prev, sec)
+        assert sec is None
         if view_block.tail_fusable(self, x, prev):
             return view_block.tail(self, x, prev)
         if self.n_feat_agg != self.n_feat_out:
@@ -361,21 +363,33 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
             XRc = sv.target_rows(prev_view, pc.num_targets)
         XRc = replicated_to_local(XRc, shard)
         cp, cc = sp.graph_conv, sv.graph_conv
+        hubs = carry is not None and self.output_global and nxt is not None
+        vsg = self.view_and_scenepoint2global if hubs else None
+        hp = point_block.hub_params(pfu, vsg.graph_conv_scenepoint2global, nxt.proj2scenepoint) if hubs else None
+        # point tail + hub on a side stream, concurrent with the camera tail + hub (streams.py)
+        sec = None
+        if hp is not None and point_block.tail_fusable(sp, XL.new_empty((0, cp.heads * cp.out_channels)), prev_pt):
+            sec = streams.section_for(XL.device, _native.defer_token())
         agg_p, agg_c = DualAttentionFn.apply(XL, XRp, XRc, cp.att, cc.att, cp.bias, cc.bias, pp, pc, cp.heads,
                                              cp.negative_slope, plans.get("_partial", {}).get("proj2view"), shard,
-                                             xl_sorted)
-        pts = sp.tail(agg_p, prev_pt)
+                                             xl_sorted, sec)
+        if sec is not None:
+            point_block.forward_buffers(sec, agg_p.shape[0], agg_p)
+            sec.fork()
+        # created in this order so that the backward runs the point hub (which forks the side
+        # stream) before the camera hub, and the point tail on the side stream after it
         view = sv.tail(agg_c, prev_view)
-        if carry is not None and self.output_global and nxt is not None:
-            vsg = self.view_and_scenepoint2global
-            hp = point_block.hub_params(pfu, vsg.graph_conv_scenepoint2global, nxt.proj2scenepoint)
-            if hp is not None and point_block._rows_ok(pts, point_block.P_W):
-                skip, SA, XLs, XRn = point_block.hub(pts, hp)
-                carry.update(XRp=XRn, pts_skip=skip, SA=SA, XLs2g=XLs)
+        if hubs:
             hv = view_block.hub_params(pfu, vsg.graph_conv_view2global, nxt.proj2view)
             if hv is not None and view_block._rows_ok(view, view.shape[1]):
                 skip, SV, XLv, XRn = view_block.hub(view, hv)
                 carry.update(XRc=XRn, view_skip=skip, SV=SV, XLv2g=XLv)
+        pts = sp.tail(agg_p, prev_pt, sec=sec)
+        if hp is not None and point_block._rows_ok(pts, point_block.P_W):
+            skip, SA, XLs, XRn = point_block.hub(pts, hp, sec)
+            carry.update(XRp=XRn, pts_skip=skip, SA=SA, XLs2g=XLs)
+        if sec is not None:
+            sec.join()
         return self._finish(pts, view, plans, prev_glob, carry, pfu, nxt)
 
     def forward_plan(self, P_hat, plans, prev_pt=None, prev_view=None, prev_glob=None):

@@ -162,6 +162,17 @@ int gasfm_colsum_multi(int32_t n, const float* const* A, const int64_t* rows, co
                        void* stream);
 int32_t gasfm_colsum_multi_counters(int32_t n, const int32_t* cols);
 
+/* Column sums of a CONTIGUOUS tall, narrow [rows, cols] matrix (bias gradients over E edge or n
+ * point rows), read as a flat coalesced stream: ONE launch, deterministic, up to 1024
+ * workgroups.  Valid when gasfm_colsum_tall_ok(cols) (cols <= 256 and lcm(cols, 256) <= 2048).
+ * ws: gasfm_colsum_tall_ws_floats(rows, cols) floats; counter: ONE zeroed uint32 (reset by
+ * the kernel; calls ordered on one stream).  Replaces torch's global sum reduction, whose
+ * replays inside a captured hipGraph were measured wrong. */
+int32_t gasfm_colsum_tall_ok(int32_t cols);
+int64_t gasfm_colsum_tall_ws_floats(int64_t rows, int32_t cols);
+int gasfm_colsum_tall(const float* A, int64_t rows, int32_t cols, float* ws, float* out,
+                      uint32_t* counter, void* stream);
+
 /* ---- fused per-edge block body (F = n_feat_proj = 32; XL width 64 = point|camera) ---- */
 
 /* Floats of the per-workgroup partial buffer: which = 0 -> edge_prologue_bwd

@@ -86,3 +86,36 @@ def test_batched_weight_grads_bitwise_equal_immediate(device):
         assert torch.equal(acc_imm[k], acc_bat[k]), k
         torch.testing.assert_close(acc_bat[k], 2 * imm[k], rtol=1e-5, atol=1e-6)
     net.batch_weight_grads = True
+
+
+@pytest.mark.parametrize("rows,cols", [(0, 2), (1, 2), (5, 3), (4097, 1), (4001638, 2), (200_000, 64),
+                                       (200_000, 3), (12_345, 256), (99_999, 12), (300_000, 7)])
+def test_colsum_tall_matches_fp64_and_is_deterministic(device, rows, cols):
+    """gasfm_colsum_tall (bias gradients over E edge / n point rows) vs fp64, repeated bitwise."""
+    assert _native.colsum_tall_ok(torch.empty(1, cols, device=device))
+    g = torch.Generator().manual_seed(rows + 3 * cols)
+    A = torch.randn(rows, cols, generator=g, dtype=torch.float64)
+    ref = A.sum(0)
+    Ad = A.float().to(device)
+    outs = [_native.colsum_tall(Ad) for _ in range(3)]
+    torch.testing.assert_close(outs[0].double().cpu(), ref, rtol=1e-5, atol=1e-5 * max(1, rows) ** 0.5)
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+
+
+def test_colsum_tall_in_captured_graph(device):
+    """Replayed from a hipGraph (where torch's global sum reduction was measured wrong), the
+    tall column sum equals the eager one on every replay."""
+    A = torch.randn(500_000, 2, device=device)
+    eager = _native.colsum_tall(A)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        _native.colsum_tall(A)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = _native.colsum_tall(A)
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, eager)
