@@ -80,6 +80,12 @@ _SIGS = {
     "gasfm_pose_fwd": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "gasfm_pose_bwd": (_i32, [_vp, _i64, _i64, _vp, _vp, _i64, _vp]),
     "gasfm_esfm_part_rows": (_i32, [_i64]),
+    "gasfm_scene_mask_words": (_i64, [_i32]),
+    "gasfm_scene_tiles": (_i64, [_i32, _i32]),
+    "gasfm_scan_i32": (_i32, [_vp, _i64, _vp, _vp]),
+    "gasfm_scene_mask": (_i32, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_scene_emit": (_i32, [_vp, _i64, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_scene_point_csr": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "gasfm_esfm_fwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _vp, _vp]),
     "gasfm_esfm_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _i32, _i32,
                               _vp, _vp, _vp, _vp, _vp]),
@@ -688,3 +694,52 @@ def gvec_multi_bwd(probs, groups, eps):
                                     _ints(N), _ptrs(dW), _ptrs(db), _ptrs(dg), _ptrs(dbt), _ptrs(part), len(groups),
                                     _ints(p0), _ints(npr), _ptrs(dres), _ptrs(dx), eps, _stream(x[0]))
     check(st, "gasfm_gvec_multi_bwd")
+
+
+# ---------------------------------------------------------------- device scene builder (scene_build.hip)
+def scan_i32(x):
+    """Exclusive scan of an int32 CUDA vector: returns out[L + 1] (out[L] = total)."""
+    _i32vec(x, "scan input")
+    out = torch.empty(x.shape[0] + 1, dtype=torch.int32, device=x.device)
+    check(lib().gasfm_scan_i32(_p(x), x.shape[0], _p(out), _stream(x)), "gasfm_scan_i32")
+    return out
+
+
+def scene_build(M, Ns=None):
+    """Dense M [2m, n] (CUDA fp32) -> dict of device tensors: cam, pt (int64 [E]), values [E, 2],
+    pt_count (int32 [n], the reference's cam_per_pts), cam_ptr (int32 [m+1]), pt_ptr (int32 [n+1]),
+    perm / pos (int32 [E]).  One host sync (E sizes the edge buffers)."""
+    if not M.is_cuda or M.dtype != torch.float32 or M.dim() != 2 or M.stride(1) != 1 or M.shape[0] % 2:
+        raise TypeError("scene_build: M must be a float32 CUDA [2m, n] matrix with unit column stride "
+                        "(no CPU fallback)")
+    m, n = M.shape[0] // 2, M.shape[1]
+    if Ns is not None:
+        if not Ns.is_cuda or Ns.dtype != torch.float32 or tuple(Ns.shape) != (m, 3, 3):
+            raise TypeError("scene_build: Ns must be a float32 CUDA [m, 3, 3] tensor")
+        Ns = Ns.contiguous()
+    L = lib()
+    dev = M.device
+    W, T = L.gasfm_scene_mask_words(n), L.gasfm_scene_tiles(m, n)
+    i32 = dict(dtype=torch.int32, device=dev)
+    mask = torch.empty(m * W, dtype=torch.int64, device=dev)
+    pt_valid = torch.empty(W, dtype=torch.int64, device=dev)
+    view_count, pt_count = torch.empty(n, **i32), torch.empty(n, **i32)
+    tile_count, tile_base = torch.empty(T, **i32), torch.empty(T + 1, **i32)
+    st = _stream(M)
+    check(L.gasfm_scene_mask(_p(M), M.stride(0), m, n, _p(mask), _p(view_count), _p(pt_valid), _p(pt_count),
+                             _p(tile_count), _p(tile_base), st), "gasfm_scene_mask")
+    E = int(tile_base[T].item())
+    cam = torch.empty(E, dtype=torch.int64, device=dev)
+    pt = torch.empty(E, dtype=torch.int64, device=dev)
+    vals = torch.empty((E, 2), dtype=torch.float32, device=dev)
+    word_base = torch.empty(m * W, **i32)
+    check(L.gasfm_scene_emit(_p(M), M.stride(0), _p(Ns) if Ns is not None else None, m, n, _p(mask), _p(pt_valid),
+                             _p(tile_base), _p(cam), _p(pt), _p(vals), _p(word_base), st), "gasfm_scene_emit")
+    pt_ptr = scan_i32(pt_count)
+    perm, pos = torch.empty(E, **i32), torch.empty(E, **i32)
+    if E:
+        check(L.gasfm_scene_point_csr(_p(mask), _p(pt_valid), _p(word_base), _p(pt_ptr), m, n, _p(perm), _p(pos),
+                                      st), "gasfm_scene_point_csr")
+    cam_ptr = tile_base[0::T // m].contiguous() if T else torch.zeros(m + 1, **i32)
+    return {"cam": cam, "pt": pt, "values": vals, "pt_count": pt_count, "cam_ptr": cam_ptr, "pt_ptr": pt_ptr,
+            "perm": perm, "pos": pos}

@@ -65,7 +65,7 @@ class AttnPlan:
     """
 
     def __init__(self, seg_ptr, perm, items, combine, n_slots, num_targets, num_edges, src_rows,
-                 all_partial=False, max_piece=DEFAULT_MAX_PIECE):
+                 all_partial=False, max_piece=DEFAULT_MAX_PIECE, pos=None):
         self.seg_ptr = seg_ptr
         self.perm = perm
         self.items = items
@@ -77,13 +77,19 @@ class AttnPlan:
         self.all_partial = bool(all_partial)
         self.max_piece = int(max_piece)
         self.n_items = int(items.shape[0])
+        dev = items.device
+        if isinstance(combine, torch.Tensor) and combine.device.type != "cpu":
+            combine = combine.cpu()  # the two-level split is host bookkeeping over <= N entries
         self.combine, self.combine_l1 = _two_level(combine, self.n_slots)
+        if dev.type != "cpu":
+            self.combine = self.combine.to(dev)
+            self.combine_l1 = None if self.combine_l1 is None else self.combine_l1.to(dev)
         self.n_combine = int(self.combine.shape[0])
         self.n_l1 = 0 if self.combine_l1 is None else int(self.combine_l1.shape[0])
         self.n_part_rows = self.n_slots + self.n_l1  # partial rows of both combine levels
         self.tag = None  # graph name (proj2view, proj2scenepoint, ...) for timing / logs
-        self.pos = None
-        if perm is not None and self.src_rows == self.num_edges:
+        self.pos = pos
+        if pos is None and perm is not None and self.src_rows == self.num_edges:
             p = perm.numpy() if isinstance(perm, torch.Tensor) else perm
             pos = np.empty(self.num_edges, dtype=np.int32)
             pos[p] = np.arange(self.num_edges, dtype=np.int32)

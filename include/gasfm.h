@@ -425,6 +425,42 @@ int gasfm_gvec_bwd(const float* dy, const float* x, int32_t K, const float* ln_w
                    float eps, const float* W, int32_t N, int32_t resid, float* dx, float* dW, float* db,
                    float* dgamma, float* dbeta, float* part, void* stream);
 
+/* ---- device-side scene graph builder (scene_build.hip) ------------------
+ * For a dense measurement matrix M [2m x n] (row stride ldM floats) already in HBM, builds on
+ * the device what the reference builds on the CPU per sample:
+ *   get_M_valid_points (dataset_utils.py:86-113), M2sparse + normalize_M (dataset_utils.py:116-156,
+ *   geo_utils.py:689-703), and the stable point-direction grouping of gasfm_build_csr.
+ * Workspace: mask [m x gasfm_scene_mask_words(n)] uint64 (one bit per camera/point),
+ * pt_valid [gasfm_scene_mask_words(n)] uint64, view_count / pt_count [n], tile_count
+ * [gasfm_scene_tiles(m, n)], tile_base [gasfm_scene_tiles(m, n) + 1], word_base [m x words].
+ * Requires m*n < 2^31 (int32 edge ids).  Deterministic (integer atomics only). */
+int64_t gasfm_scene_mask_words(int32_t n);
+int64_t gasfm_scene_tiles(int32_t m, int32_t n);
+
+/* Exclusive scan: out[0..L) = prefix sums of in, out[L] = total (int32).  One workgroup. */
+int gasfm_scan_i32(const int32_t* in, int64_t L, int32_t* out, void* stream);
+
+/* Pass 1: validity bits ((x, y) != (0, 0)), raw views per point (view_count), points with
+ * >= 2 views (pt_valid bits; pt_count = view_count or 0 = the reference's cam_per_pts), and
+ * the per-tile edge counts with their exclusive scan: E = tile_base[tiles]. */
+int gasfm_scene_mask(const float* M, int64_t ldM, int32_t m, int32_t n, uint64_t* mask,
+                     int32_t* view_count, uint64_t* pt_valid, int32_t* pt_count, int32_t* tile_count,
+                     int32_t* tile_base, void* stream);
+
+/* Pass 2: the E edges in the reference's nonzero() order (cam-major, point ascending):
+ * cam[E], pt[E] (int64, the reference's SparseMat.indices rows) and values [E x 2]
+ * (N_c [x, y, 1]^T rows 0..1 when Ns [m x 3 x 3] != NULL, raw (x, y) otherwise), plus
+ * word_base (edge id of the first edge of each mask word) for pass 3. */
+int gasfm_scene_emit(const float* M, int64_t ldM, const float* Ns, int32_t m, int32_t n,
+                     const uint64_t* mask, const uint64_t* pt_valid, const int32_t* tile_base,
+                     int64_t* cam, int64_t* pt, float* values, int32_t* word_base, void* stream);
+
+/* Pass 3: point-direction CSR given pt_ptr = exclusive scan of pt_count: perm[slot] = edge
+ * (stable, cameras ascending inside a point; == gasfm_build_csr on pt) and pos[edge] = slot. */
+int gasfm_scene_point_csr(const uint64_t* mask, const uint64_t* pt_valid, const int32_t* word_base,
+                          const int32_t* pt_ptr, int32_t m, int32_t n, int32_t* perm, int32_t* pos,
+                          void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -120,3 +120,21 @@ def test_conf_parser_roundtrip():
     assert c.get("dataset.test_set") == ["A", "B"]
     assert abs(c.get_float("train.lr") - 1e-4) < 1e-12
     assert c.get_int("model.missing", default=None) is None
+
+
+def test_device_plan_work_restatement_matches_host():
+    """scene_device.plan_work_device (torch ops; runs on CPU tensors here) == gasfm_plan_work."""
+    import torch
+    from gasfm_amd.scene_device import plan_work_device
+    rng = np.random.default_rng(0)
+    for trial in range(120):
+        N = int(rng.integers(0, 40))
+        mp = int(rng.integers(1, 20))
+        ap = bool(rng.integers(0, 2))
+        ln = rng.integers(0, 3 if trial % 5 == 0 else 70, size=N)
+        ptr = np.concatenate([[0], np.cumsum(ln)]).astype(np.int32)
+        items, comb, ns = _native.plan_work(ptr, mp, ap)
+        items2, comb2, ns2 = plan_work_device(torch.from_numpy(ptr), mp, ap)
+        assert ns == ns2
+        np.testing.assert_array_equal(items.reshape(-1, 4), items2.numpy().reshape(-1, 4))
+        np.testing.assert_array_equal(comb.reshape(-1, 4), comb2.numpy().reshape(-1, 4))

@@ -37,7 +37,7 @@ def main():
             if re.search(pat, n):
                 break
         else:
-            cat = "other: " + re.sub(r"\(.*", "", n)[:50]
+            cat = "other: " + re.sub(r"\(.*", "", n.replace("(anonymous namespace)::", ""))[:50]
         tot[cat] += (e - s) / 1e3
         cnt[cat] += 1
     span = (seg[-1][2] - seg[0][1]) / 1e3
@@ -46,7 +46,7 @@ def main():
         print(f"  {tot[cat] / 1e3:7.2f} ms {cnt[cat]:5d} kernels  {cat}")
     per = defaultdict(lambda: [0.0, 0])
     for n, s, e in seg:
-        key = re.sub(r"\(.*", "", n)[:90]
+        key = re.sub(r"\(.*", "", n.replace("(anonymous namespace)::", ""))[:90]
         per[key][0] += (e - s) / 1e3
         per[key][1] += 1
     print("top kernels (us total, count, us mean):")
