@@ -80,6 +80,7 @@ _SIGS = {
     "gasfm_pose_fwd": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "gasfm_pose_bwd": (_i32, [_vp, _i64, _i64, _vp, _vp, _i64, _vp]),
     "gasfm_esfm_part_rows": (_i32, [_i64]),
+    "gasfm_reproj_error": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp]),
     "gasfm_scene_mask_words": (_i64, [_i32]),
     "gasfm_scene_tiles": (_i64, [_i32, _i32]),
     "gasfm_scan_i32": (_i32, [_vp, _i64, _vp, _vp]),
@@ -661,6 +662,19 @@ def esfm_bwd(cptr, pptr, perm, cam, pt, vals, P, X, margin, hinge_w, hinge, equa
                               _p(vals), E, _p(P), _p(X), n, margin, hinge_w, int(hinge), int(equalize),
                               int(valid_only), _p(dloss), _p(tot), _p(dP), _p(dX), _stream(X))
     check(st, "gasfm_esfm_bwd")
+
+
+def reproj_error(cam, pt, xy, P, X, err=None):
+    """Per-workgroup (sum, count) of the non-NaN reprojection errors (and err[e] if given)."""
+    E, n = cam.shape[0], X.shape[1]
+    _i32vec(cam, "cam"), _i32vec(pt, "pt")
+    _req(xy, "xy", 2), _req(P, "P", 12), _req(X, "pts3D", n)
+    if X.shape[0] != 4 or pt.shape[0] != E or xy.shape[0] != E or (err is not None and err.shape[0] != E):
+        raise ValueError("reproj_error: expected pts3D [4, n] and E-long cam / pt / xy / err")
+    part = torch.empty((esfm_part_rows(E), 2), dtype=torch.float32, device=X.device)
+    st = lib().gasfm_reproj_error(_p(cam), _p(pt), _p(xy), E, _p(P), _p(X), n, _p(err), _p(part), _stream(X))
+    check(st, "gasfm_reproj_error")
+    return part
 
 
 # ---------------------------------------------------------------- batched single-row problems (global hub)

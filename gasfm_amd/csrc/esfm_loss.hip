@@ -180,6 +180,43 @@ __global__ __launch_bounds__(kT) void esfm_bwd_pt_kernel(const int32_t* __restri
   for (int j = 0; j < 4; ++j) dX[j * n + p] = a[j];
 }
 
+// compute_core_errors' "our_repro" (code/evaluation.py:8-31; geo_utils.py:371-391): per edge
+//   X = pts3D[:, p] / pts3D[3, p]   (pflat)      y = Ps_pix[c] X      err = ||xy - y_xy / y_z||
+// with Ps_pix = Ns^-1 Ps_norm (pixel-space cameras, caller-supplied) and xy the PIXEL
+// measurement of the edge.  err[e] is written when err != NULL; the workgroup partial is
+// (sum of the non-NaN errors, their count): np.nanmean's operands.  An inf error (y_z == 0,
+// y_xy != 0) is summed like numpy does.
+__global__ __launch_bounds__(kT) void reproj_kernel(const int32_t* __restrict__ cam, const int32_t* __restrict__ pt,
+                                                    const float* __restrict__ xy, int64_t E,
+                                                    const float* __restrict__ P, const float* __restrict__ X,
+                                                    int64_t n, float* __restrict__ err, float* __restrict__ part) {
+  __shared__ float sh[kT / 64];
+  float s = 0.f, cnt = 0.f;
+  for (int64_t e = int64_t(blockIdx.x) * kT + threadIdx.x; e < E; e += int64_t(gridDim.x) * kT) {
+    const float2 m = reinterpret_cast<const float2*>(xy)[e];
+    const int c = cam[e], p = pt[e];
+    const float w = X[3 * n + p];
+    const float x0 = X[p] / w, x1 = X[n + p] / w, x2 = X[2 * n + p] / w;
+    const float* pc = P + int64_t(c) * 12;
+    float y[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) y[i] = fmaf(pc[4 * i], x0, fmaf(pc[4 * i + 1], x1, fmaf(pc[4 * i + 2], x2, pc[4 * i + 3])));
+    const float u = m.x - y[0] / y[2], v = m.y - y[1] / y[2];
+    const float r = sqrtf(u * u + v * v);
+    if (err) err[e] = r;
+    if (!isnan(r)) {
+      s += r;
+      cnt += 1.f;
+    }
+  }
+  s = block_sum(s, sh);
+  cnt = block_sum(cnt, sh);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = s;
+    part[2 * blockIdx.x + 1] = cnt;
+  }
+}
+
 }  // namespace
 }  // namespace gasfm
 
@@ -216,4 +253,13 @@ extern "C" int gasfm_esfm_bwd(const int32_t* cptr, int32_t m, const int32_t* ppt
   hipLaunchKernelGGL(esfm_bwd_pt_kernel, dim3(unsigned((n + kT - 1) / kT)), dim3(kT), 0, st, pptr, perm, cam, vals,
                      E, P, X, n, k, dloss, tot, dX);
   return launch_status("gasfm_esfm_bwd");
+}
+
+extern "C" int gasfm_reproj_error(const int32_t* cam, const int32_t* pt, const float* xy, int64_t E, const float* P,
+                                  const float* pts3D, int64_t n, float* err, float* part, void* stream) {
+  GASFM_REQUIRE(E >= 0 && n >= 0 && (E == 0 || (cam && pt && xy && P && pts3D)) && part,
+                "gasfm_reproj_error: bad args");
+  hipLaunchKernelGGL(reproj_kernel, dim3(gasfm_esfm_part_rows(E)), dim3(kT), 0, (hipStream_t)stream, cam, pt, xy, E,
+                     P, pts3D, n, err, part);
+  return launch_status("gasfm_reproj_error");
 }

@@ -425,6 +425,15 @@ int gasfm_gvec_bwd(const float* dy, const float* x, int32_t K, const float* ln_w
                    float eps, const float* W, int32_t N, int32_t resid, float* dx, float* dW, float* db,
                    float* dgamma, float* dbeta, float* part, void* stream);
 
+/* Reprojection error of compute_core_errors' "our_repro" (code/evaluation.py:8-31 ->
+ * geo_utils.reprojection_error_with_points, geo_utils.py:371-391) over the E visibility edges:
+ * err_e = || xy_e - (P_c X)_xy / (P_c X)_z ||, X = pflat(pts3D[:, p]), P = Ps_pix [m x 12]
+ * (= Ns^-1 Ps_norm), xy = PIXEL measurements [E x 2].  err (optional, [E]) per edge;
+ * part [gasfm_esfm_part_rows(E) x 2] = per-workgroup (sum of non-NaN errors, their count), the
+ * operands of np.nanmean (finish with gasfm_colsum). */
+int gasfm_reproj_error(const int32_t* cam, const int32_t* pt, const float* xy, int64_t E, const float* P,
+                       const float* pts3D, int64_t n, float* err, float* part, void* stream);
+
 /* ---- device-side scene graph builder (scene_build.hip) ------------------
  * For a dense measurement matrix M [2m x n] (row stride ldM floats) already in HBM, builds on
  * the device what the reference builds on the CPU per sample:

@@ -169,3 +169,14 @@ def test_esfm_sparse_values_are_norm_M_entries():
     nM = (Ns @ h)[:, :2, :]  # geo_utils.normalize_M
     idx = torch.from_numpy(f["indices"])
     np.testing.assert_allclose(nM[idx[0], :, idx[1]].numpy(), f["values"], rtol=1e-6, atol=1e-6)
+
+
+def test_repro_oracle_matches_reference_core_errors():
+    """oracle/repro.py == the reference's compute_core_errors (tests/golden/core_errors.npz)."""
+    from oracle import repro
+    f = golden("core_errors.npz")
+    err, mean = repro.reprojection_errors(f["M"].astype(np.float64), f["Ns"].astype(np.float64),
+                                          f["Ps_norm"].astype(np.float64), f["pts3D"].astype(np.float64))
+    np.testing.assert_allclose(err[f["cam"], f["pt"]], f["edge_errors"], rtol=2e-5, atol=1e-3)
+    assert np.isnan(err[~repro.valid_points(f["M"])]).all()
+    np.testing.assert_allclose(mean, f["our_repro"], rtol=1e-5)

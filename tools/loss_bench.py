@@ -82,6 +82,8 @@ def main():
     fwd_bytes = 16 * E + 16 * n + 48 * m
     report("esfm_fwd", _time(lambda: _native.esfm_fwd(cam, pt, vals, P, X, margin, w, hinge, part), args.reps),
            fwd_bytes)
+    # compute_core_errors' reprojection error (gasfm_reproj_error): same bytes as esfm_fwd
+    report("reproj_error", _time(lambda: _native.reproj_error(cam, pt, vals, P, X), args.reps), fwd_bytes)
     tot = _native.colsum(part)
     dloss = torch.ones(1, device=dev)
     dP, dX = torch.empty_like(P), torch.empty_like(X)
