@@ -34,6 +34,7 @@ class KernelTimer:
         self.events = []
         self.enabled = False
         self.gathered = None  # whether the timed launches read XL through perm
+        self.launch = None    # closure re-issuing the last timed launch (same inputs / outputs)
 
     def __call__(self, tag, HC):
         return self.enabled and self.select(tag, HC)
@@ -43,6 +44,21 @@ class KernelTimer:
         if not self.events:
             return None
         return sum(a.elapsed_time(b) for a, b in self.events) / len(self.events)
+
+    def replay_ms(self, reps=20):
+        """Mean duration of ``reps`` back-to-back re-launches of the last timed kernel between
+        two HIP events on the launch stream: the kernel time without the per-launch event and
+        dispatch gaps that bracketing single launches adds (comparable to rocprof's durations)."""
+        if self.launch is None:
+            return None
+        self.launch()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            self.launch()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps
 
 
 class AttnPlan:
@@ -221,12 +237,15 @@ def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True, xl_so
     if timed:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
-    _native.attn_fwd(XL, XR, attf, bias, None if xl_sorted else plan.perm, plan.items, plan.n_items, heads, C,
-                     slope, finalize, out, smax, ssum, part)
+    def launch():
+        _native.attn_fwd(XL, XR, attf, bias, None if xl_sorted else plan.perm, plan.items, plan.n_items, heads, C,
+                         slope, finalize, out, smax, ssum, part)
+    launch()
     if timed:
         ev[1].record()
         KERNEL_TIMER.events.append(ev)
         KERNEL_TIMER.gathered = plan.perm is not None and not xl_sorted
+        KERNEL_TIMER.launch = launch
     combine_fwd_l1(plan, part, heads, C)
     if plan.n_combine:
         _native.attn_combine(plan.combine, plan.n_combine, heads, C, part, bias, finalize, out, smax, ssum)

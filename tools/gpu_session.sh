@@ -11,3 +11,5 @@ tail -1 gpurun_out/bench_default.log; echo "bench wall: ${SECONDS}s"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $ROOT/gpurun_out/prof_bench -o run -- python3 $ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $ROOT/gpurun_out/prof_bench.log 2>&1
 cd $ROOT && ls -R gpurun_out/prof_bench | head
+python tools/step_breakdown.py gpurun_out/prof_bench/run_results.db 3 30 > gpurun_out/prof_bench_breakdown.txt
+python tools/rocprof_summary.py gpurun_out/prof_bench/run_results.db gpurun_out/prof_bench_summary.csv 7 | tail -3
