@@ -94,8 +94,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--m", type=int, default=1000)
-    ap.add_argument("--n", type=int, default=200_000)
+    # --cameras / --points: spellings torchrun's own parser does not take for abbreviations
+    ap.add_argument("--m", "--cameras", dest="m", type=int, default=1000)
+    ap.add_argument("--n", "--points", dest="n", type=int, default=200_000)
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from Python (no hipGraph)")

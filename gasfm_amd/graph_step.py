@@ -76,7 +76,11 @@ class CapturedStep:
         g = torch.cuda.CUDAGraph()
         ok = True
         try:
-            with torch.cuda.graph(g):  # records only: no collective runs during capture
+            # thread_local: under torch.distributed, ProcessGroupNCCL's watchdog thread queries the
+            # events of earlier collectives while this thread captures; in the default "global"
+            # mode that query is an illegal call during capture (hipErrorStreamCaptureUnsupported)
+            # and the watchdog aborts the process
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):  # records only
                 out = self.fn()
         except RuntimeError as e:  # capture unsupported for some op
             self.fallback_reason = f"capture failed: {e}"

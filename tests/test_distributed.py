@@ -258,3 +258,24 @@ def test_capture_fallback_is_agreed_across_ranks(device):
         assert p.exitcode == 0
     assert [r[1] for r in res] == [False, False], [r[2] for r in res]
     assert np.array_equal(res[0][4], res[1][4])  # synced local-parameter gradient
+
+
+@pytest.mark.gpu
+def test_rccl_bench_captures_and_replays(tmp_path):
+    """bench.py's RCCL path (nccl process group, one rank) captures the whole step, collectives
+    included, into a hipGraph and replays it.  Regression: in the default "global" capture mode
+    ProcessGroupNCCL's watchdog thread querying events during the capture aborted the process."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(repo, "bench.py"),
+           "--gpus", "1", "--dist", "--cameras", "200", "--points", "20000", "--layers", "2", "--steps", "3", "--warmup", "2",
+           "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=repo, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "hipGraph replay" in r.stderr, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["execution"].startswith("hipGraph replay") and res["value"] > 0
