@@ -18,6 +18,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=25_000)
     ap.add_argument("--rows", type=int, default=40)
+    ap.add_argument("--stacks", action="store_true",
+                    help="also list the Python call sites of the aten ops that launch device work")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     sc = synthetic.windowed_scene(1000, args.n, seed=4)
@@ -34,7 +36,8 @@ def main():
     for _ in range(3):
         step()
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True,
+                 with_stack=args.stacks) as prof:
         step()
         torch.cuda.synchronize()
     ev = [e for e in prof.key_averages(group_by_input_shape=True) if e.self_device_time_total > 0]
@@ -50,6 +53,20 @@ def main():
     print("\naten ops by count (with device time):")
     for e in ops[:args.rows]:
         print(f"{e.count:5d}x {e.device_time_total / 1e3:7.3f} ms  {e.key[:40]:40s} {str(e.input_shapes)[:100]}")
+    if args.stacks:
+        # gasfm_amd call sites of aten ops with device work (excluding the libgasfm launches)
+        print("\naten ops with device work by gasfm_amd call site:")
+        from collections import defaultdict
+        agg = defaultdict(lambda: [0, 0.0])
+        for e in prof.events():
+            if not e.name.startswith("aten::") or e.device_time_total <= 0:
+                continue
+            st = [f for f in (e.stack or []) if "gasfm_amd" in f][:2]
+            key = (e.name, " <- ".join(st) if st else "(no gasfm_amd frame)")
+            agg[key][0] += 1
+            agg[key][1] += e.device_time_total
+        for (name, site), (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:args.rows]:
+            print(f"{n:5d}x {t / 1e3:7.3f} ms  {name[:28]:28s} {site[:200]}")
 
 
 if __name__ == "__main__":
