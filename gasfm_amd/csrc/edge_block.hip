@@ -508,7 +508,7 @@ __device__ __forceinline__ void st2(float* p, float a, float b) { *reinterpret_c
 
 template <bool LN, bool RES>
 #ifndef GASFM_PBWD_MINWAVES
-#define GASFM_PBWD_MINWAVES 1
+#define GASFM_PBWD_MINWAVES 3  // 162 VGPRs, no spills: 3 waves/SIMD (2 at 180); edge_bench 611 -> 588 us
 #endif
 __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINWAVES) void edge_prologue_bwd_kernel(
     const float* __restrict__ dXL, int64_t ldX, const float* __restrict__ P, const float* __restrict__ dRes,
