@@ -37,6 +37,17 @@ namespace {
 
 using namespace tile;
 
+// minimum waves per SIMD of the launch bounds (A/B knobs; tools/ab_lib.sh)
+#ifndef GASFM_PFWD_MINWAVES
+#define GASFM_PFWD_MINWAVES 1
+#endif
+#ifndef GASFM_EFWD_MINWAVES
+#define GASFM_EFWD_MINWAVES 1
+#endif
+#ifndef GASFM_EBWD_MINWAVES
+#define GASFM_EBWD_MINWAVES 1
+#endif
+
 constexpr int F = 32;            // projection feature width (n_feat_proj)
 constexpr int NX = 64;           // XL width: 32 (point conv) + 32 (camera conv)
 constexpr int LD34 = 34;         // LDS row stride of 32-wide tiles
@@ -132,7 +143,7 @@ __device__ __forceinline__ void load_norm_tile(const float* __restrict__ P, int6
 // parameters themselves, so the host does not concatenate them every forward
 // =====================================================================================
 template <bool LN>
-__global__ __launch_bounds__(kThreads) void edge_prologue_fwd_kernel(const float* __restrict__ P, int64_t E,
+__global__ __launch_bounds__(kThreads, GASFM_PFWD_MINWAVES) void edge_prologue_fwd_kernel(const float* __restrict__ P, int64_t E,
                                                                     const float* __restrict__ gam,
                                                                     const float* __restrict__ bet, float eps,
                                                                     const float* __restrict__ W,
@@ -220,7 +231,7 @@ __global__ __launch_bounds__(kThreads) void edge_prologue_fwd_kernel(const float
 // edge_epilogue_fwd: P'[e] = P[e] + scale (Wp [relu(LN(P[e])) | P0[e]] + bp + Sp[pt] + Sv[cam] + Sg)
 // Wp: [32 x ldWp] (ldWp = 34 with the init-feature skip, 32 without: P0 == null)
 // =====================================================================================
-__global__ __launch_bounds__(kThreads) void edge_epilogue_fwd_kernel(
+__global__ __launch_bounds__(kThreads, GASFM_EFWD_MINWAVES) void edge_epilogue_fwd_kernel(
     const float* __restrict__ P, const float* __restrict__ P0, const int32_t* __restrict__ cam,
     const int32_t* __restrict__ pt, int64_t E, const float* __restrict__ gam, const float* __restrict__ bet,
     float eps, const float* __restrict__ Wp, int ldWp, const float* __restrict__ bp, const float* __restrict__ Sp,
@@ -328,7 +339,7 @@ __global__ __launch_bounds__(kThreads) void edge_epilogue_fwd_kernel(
 //   d = dP' * scale;  dSv[cam] = sum_e d_e;  dWp += d^T [relu(LN(P)) | P0];  dP0[e] = Wp[:,32:34]^T d_e
 // part layout per workgroup: [32*ldWp] dWp
 // =====================================================================================
-__global__ __launch_bounds__(kThreads) void edge_epilogue_bwd_kernel(
+__global__ __launch_bounds__(kThreads, GASFM_EBWD_MINWAVES) void edge_epilogue_bwd_kernel(
     const gasfm_work_item* __restrict__ items, int n_items, const float* __restrict__ dPo,
     const float* __restrict__ P, const float* __restrict__ P0, const float* __restrict__ gam,
     const float* __restrict__ bet, float eps, const float* __restrict__ Wp, int ldWp, float scale,

@@ -309,6 +309,9 @@ __global__ __launch_bounds__(kBlock, GASFM_FWD_MINWAVES) void attn_fwd_kernel(
 // while the prefetch is in flight (hipcc would drain it with vmcnt(0)), except the extra
 // chunks of segments longer than 32 edges.  Geom<32,8> (the 32-wide convs) only.
 // ------------------------------------------------------------------------------------------
+#ifndef GASFM_GLDS_BWD_MINWAVES
+#define GASFM_GLDS_BWD_MINWAVES 1
+#endif
 typedef __attribute__((address_space(3))) void* lds_vptr;
 typedef const __attribute__((address_space(1))) void* glb_vptr;
 
@@ -664,7 +667,7 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_kernel(
 // items still fetch their segment data (d bias sums gout over every segment).
 // ------------------------------------------------------------------------------------------
 template <class G>
-__global__ __launch_bounds__(kBlock) void attn_bwd_glds_kernel(
+__global__ __launch_bounds__(kBlock, GASFM_GLDS_BWD_MINWAVES) void attn_bwd_glds_kernel(
     const float* __restrict__ XL, int64_t ldXL, const float* __restrict__ XR, int64_t ldXR,
     const float* __restrict__ att, const float* __restrict__ bias, const int32_t* __restrict__ perm,
     const gasfm_work_item* __restrict__ items, int n_items, float slope, const float* __restrict__ out,
