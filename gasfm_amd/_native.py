@@ -87,6 +87,7 @@ _SIGS = {
     "gasfm_scene_mask": (_i32, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_scene_emit": (_i32, [_vp, _i64, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_scene_point_csr": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
+    "gasfm_scene_homography": (_i32, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "gasfm_esfm_fwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _vp, _vp]),
     "gasfm_esfm_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _i32, _i32,
                               _vp, _vp, _vp, _vp, _vp]),
@@ -719,18 +720,17 @@ def scan_i32(x):
     return out
 
 
-def scene_build(M, Ns=None):
-    """Dense M [2m, n] (CUDA fp32) -> dict of device tensors: cam, pt (int64 [E]), values [E, 2],
-    pt_count (int32 [n], the reference's cam_per_pts), cam_ptr (int32 [m+1]), pt_ptr (int32 [n+1]),
-    perm / pos (int32 [E]).  One host sync (E sizes the edge buffers)."""
+def _check_M(M, what):
     if not M.is_cuda or M.dtype != torch.float32 or M.dim() != 2 or M.stride(1) != 1 or M.shape[0] % 2:
-        raise TypeError("scene_build: M must be a float32 CUDA [2m, n] matrix with unit column stride "
+        raise TypeError(f"{what}: M must be a float32 CUDA [2m, n] matrix with unit column stride "
                         "(no CPU fallback)")
+
+
+def scene_mask(M):
+    """gasfm_scene_mask on a dense M: (mask [m*W] int64 bits, pt_valid [W], pt_count int32 [n] (views of
+    points with >= 2, else 0), tile_base int32 [tiles + 1])."""
+    _check_M(M, "scene_mask")
     m, n = M.shape[0] // 2, M.shape[1]
-    if Ns is not None:
-        if not Ns.is_cuda or Ns.dtype != torch.float32 or tuple(Ns.shape) != (m, 3, 3):
-            raise TypeError("scene_build: Ns must be a float32 CUDA [m, 3, 3] tensor")
-        Ns = Ns.contiguous()
     L = lib()
     dev = M.device
     W, T = L.gasfm_scene_mask_words(n), L.gasfm_scene_tiles(m, n)
@@ -739,9 +739,42 @@ def scene_build(M, Ns=None):
     pt_valid = torch.empty(W, dtype=torch.int64, device=dev)
     view_count, pt_count = torch.empty(n, **i32), torch.empty(n, **i32)
     tile_count, tile_base = torch.empty(T, **i32), torch.empty(T + 1, **i32)
-    st = _stream(M)
     check(L.gasfm_scene_mask(_p(M), M.stride(0), m, n, _p(mask), _p(view_count), _p(pt_valid), _p(pt_count),
-                             _p(tile_count), _p(tile_base), st), "gasfm_scene_mask")
+                             _p(tile_count), _p(tile_base), _stream(M)), "gasfm_scene_mask")
+    return mask, pt_valid, pt_count, tile_base
+
+
+def scene_homography(M, Ns, R, Ninv):
+    """Rotational homography augmentation of a dense M (gasfm_scene_homography): new [2m, n] M."""
+    _check_M(M, "scene_homography")
+    m, n = M.shape[0] // 2, M.shape[1]
+    for t, name in ((Ns, "Ns"), (R, "R"), (Ninv, "Ninv")):
+        if not t.is_cuda or t.dtype != torch.float32 or tuple(t.shape) != (m, 3, 3) or not t.is_contiguous():
+            raise TypeError(f"scene_homography: {name} must be a contiguous float32 CUDA [m, 3, 3] tensor")
+    mask, pt_valid, _, _ = scene_mask(M)
+    out = torch.empty_like(M)
+    check(lib().gasfm_scene_homography(_p(M), M.stride(0), m, n, _p(mask), _p(pt_valid), _p(Ns), _p(R), _p(Ninv),
+                                       _p(out), out.stride(0), _stream(M)), "gasfm_scene_homography")
+    return out
+
+
+def scene_build(M, Ns=None):
+    """Dense M [2m, n] (CUDA fp32) -> dict of device tensors: cam, pt (int64 [E]), values [E, 2],
+    pt_count (int32 [n], the reference's cam_per_pts), cam_ptr (int32 [m+1]), pt_ptr (int32 [n+1]),
+    perm / pos (int32 [E]).  One host sync (E sizes the edge buffers)."""
+    _check_M(M, "scene_build")
+    m, n = M.shape[0] // 2, M.shape[1]
+    if Ns is not None:
+        if not Ns.is_cuda or Ns.dtype != torch.float32 or tuple(Ns.shape) != (m, 3, 3):
+            raise TypeError("scene_build: Ns must be a float32 CUDA [m, 3, 3] tensor")
+        Ns = Ns.contiguous()
+    L = lib()
+    dev = M.device
+    T = L.gasfm_scene_tiles(m, n)
+    i32 = dict(dtype=torch.int32, device=dev)
+    mask, pt_valid, pt_count, tile_base = scene_mask(M)
+    st = _stream(M)
+    W = L.gasfm_scene_mask_words(n)
     E = int(tile_base[T].item())
     cam = torch.empty(E, dtype=torch.int64, device=dev)
     pt = torch.empty(E, dtype=torch.int64, device=dev)

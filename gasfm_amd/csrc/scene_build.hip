@@ -210,6 +210,41 @@ __global__ __launch_bounds__(256) void scene_point_csr_kernel(const unsigned lon
   }
 }
 
+
+// rotational homography augmentation of the image points (SceneData.apply_rotational_homography_aug,
+// datasets/SceneData.py:355-440): grid (ceil(n/256), m), thread = (camera c, point p).
+//   valid (c, p) (mask bit and >= 2 views): (x', y') = pflat(Ninv_c R_c Ns_c [x, y, 1]^T)
+//   otherwise 0 (the reference's explicit zero-reset of ~valid_pts)
+__global__ __launch_bounds__(256) void scene_homography_kernel(const float* __restrict__ M, int64_t ldM, int n,
+                                                               int64_t W, const unsigned long long* __restrict__ mask,
+                                                               const unsigned long long* __restrict__ valid,
+                                                               const float* __restrict__ Ns, const float* __restrict__ R,
+                                                               const float* __restrict__ Ninv, float* __restrict__ out,
+                                                               int64_t ldO) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  const int64_t c = blockIdx.y;
+  if (p >= n) return;
+  const int w = p >> 6, b = p & 63;
+  const bool v = ((mask[c * W + w] >> b) & 1ull) && ((valid[w] >> b) & 1ull);
+  float ox = 0.f, oy = 0.f;
+  if (v) {
+    const float x = M[2 * c * ldM + p], y = M[(2 * c + 1) * ldM + p];
+    const float* N = Ns + c * 9;
+    const float* Rc = R + c * 9;
+    const float* Ni = Ninv + c * 9;
+    float a[3], q[3], d[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) a[i] = N[3 * i] * x + N[3 * i + 1] * y + N[3 * i + 2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) q[i] = Rc[3 * i] * a[0] + Rc[3 * i + 1] * a[1] + Rc[3 * i + 2] * a[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) d[i] = Ni[3 * i] * q[0] + Ni[3 * i + 1] * q[1] + Ni[3 * i + 2] * q[2];
+    ox = d[0] / d[2];
+    oy = d[1] / d[2];
+  }
+  out[2 * c * ldO + p] = ox;
+  out[(2 * c + 1) * ldO + p] = oy;
+}
 }  // namespace
 }  // namespace gasfm
 
@@ -276,4 +311,16 @@ extern "C" int gasfm_scene_point_csr(const uint64_t* mask, const uint64_t* pt_va
                      reinterpret_cast<const unsigned long long*>(mask),
                      reinterpret_cast<const unsigned long long*>(pt_valid), word_base, pt_ptr, m, n, W, perm, pos);
   return launch_status("gasfm_scene_point_csr");
+}
+
+extern "C" int gasfm_scene_homography(const float* M, int64_t ldM, int32_t m, int32_t n, const uint64_t* mask,
+                                      const uint64_t* pt_valid, const float* Ns, const float* R, const float* Ninv,
+                                      float* out, int64_t ldO, void* stream) {
+  GASFM_REQUIRE(m > 0 && n > 0 && ldM >= n && ldO >= n, "gasfm_scene_homography: m=%d n=%d", m, n);
+  GASFM_REQUIRE(M && mask && pt_valid && Ns && R && Ninv && out, "gasfm_scene_homography: null pointer");
+  GASFM_REQUIRE(m <= 65535, "gasfm_scene_homography: m=%d exceeds the grid's y extent", m);
+  hipLaunchKernelGGL(scene_homography_kernel, dim3((n + 255) / 256, m), dim3(256), 0, (hipStream_t)stream, M, ldM, n,
+                     gasfm_scene_mask_words(n), reinterpret_cast<const unsigned long long*>(mask),
+                     reinterpret_cast<const unsigned long long*>(pt_valid), Ns, R, Ninv, out, ldO);
+  return launch_status("gasfm_scene_homography");
 }

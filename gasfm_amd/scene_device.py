@@ -14,7 +14,15 @@ already in HBM, ``scene_from_dense_device`` builds the same ``SceneData`` on the
 Everything the model reads is bit-identical to the host builder (``SceneData(M, Ns, ...)``):
 edge order, indices, counts, plans; values agree to fp32 rounding of the 2x3 normalisation.
 Host syncs: the edge count, the item counts of the four plans, and the small combine lists.
+
+Per-sample transforms before the build (§8(f) rank 3), with M staying on the device:
+``sample_data_device`` (SceneData.sample_data) and ``apply_rotational_homography_aug_device``
+(SceneData.apply_rotational_homography_aug, image points through gasfm_scene_homography); their
+random draws come from the same numpy / torch CPU generators, in the reference's order.
 """
+import math
+
+import numpy as np
 import torch
 
 from . import _native
@@ -114,3 +122,106 @@ def scene_from_dense_device(M, Ns, Ps_gt=None, scene_name="scene", calibrated=Tr
     self.x = SparseMat(b["values"], torch.stack([b["cam"], b["pt"]]), cam_per_pts, pts_per_cam, (m, n, 2))
     self.graph_wrappers = graph_wrappers_device(b, m, n, max_piece)
     return self
+
+
+# ------------------------------------------------------------------ per-sample transforms on the device
+def _dense_M(data):
+    M = getattr(data, "M", None)
+    if M is None:
+        M = getattr(data, "_M", None)
+    if M is None:
+        raise ValueError("the scene carries no dense measurement matrix M")
+    return M
+
+
+def sample_indices(N, num_samples, adjacent):
+    """dataset_utils.sample_indices (utils/dataset_utils.py:25-40), same numpy RNG calls."""
+    if num_samples == 1:
+        return np.arange(N)
+    if num_samples < 1:
+        num_samples = int(np.ceil(num_samples * N))
+    num_samples = max(2, num_samples)
+    if num_samples >= N:
+        return np.arange(N)
+    if adjacent:
+        start = np.random.randint(0, N - num_samples + 1)
+        return np.arange(start, start + num_samples)
+    return np.random.choice(N, num_samples, replace=False)
+
+
+def sample_data_device(data, num_views, consecutive_views=True, max_piece=None):
+    """SceneData.sample_data (datasets/SceneData.py:306-353) with M on the device: the view subset's
+    rows, the points still seen in >= 2 of those views (gasfm_scene_mask's counts), then the
+    device graph build.  The view choice draws from numpy's global RNG exactly as the reference."""
+    M = _dense_M(data)
+    idx = sample_indices(len(data.y), num_views, adjacent=consecutive_views)
+    m_idx = np.sort(np.concatenate((2 * idx, 2 * idx + 1)))
+    dev = M.device
+    ti = torch.from_numpy(idx).to(dev)
+    y, Ns = data.y.to(dev)[ti], data.Ns.to(dev)[ti]
+    Ms = M.index_select(0, torch.from_numpy(m_idx).to(dev)).contiguous()
+    _, _, pt_count, _ = _native.scene_mask(Ms)
+    keep = torch.nonzero(pt_count > 0).view(-1)  # get_M_valid_points(M).any(dim=0)
+    Ms = Ms.index_select(1, keep).contiguous()
+    return scene_from_dense_device(Ms, Ns.contiguous(), y, data.scene_name,
+                                   calibrated=getattr(data, "calibrated", True), max_piece=max_piece)
+
+
+def _axis_angle_to_matrix(axis_angle):
+    """pytorch3d.transforms.axis_angle_to_matrix (published formula: axis-angle -> quaternion with
+    the small-angle series below 1e-6 -> quaternion_to_matrix, real part first)."""
+    angles = torch.norm(axis_angle, p=2, dim=-1, keepdim=True)
+    half = angles * 0.5
+    small = angles.abs() < 1e-6
+    safe = torch.where(small, torch.ones_like(angles), angles)
+    s = torch.where(small, 0.5 - angles * angles / 48, torch.sin(half) / safe)
+    q = torch.cat([torch.cos(half), axis_angle * s], dim=-1)
+    r, i, j, k = torch.unbind(q, -1)
+    two_s = 2.0 / (q * q).sum(-1)
+    o = torch.stack((1 - two_s * (j * j + k * k), two_s * (i * j - k * r), two_s * (i * k + j * r),
+                     two_s * (i * j + k * r), 1 - two_s * (i * i + k * k), two_s * (j * k - i * r),
+                     two_s * (i * k - j * r), two_s * (j * k + i * r), 1 - two_s * (i * i + j * j)), -1)
+    return o.reshape(q.shape[:-1] + (3, 3))
+
+
+def rotational_homography(num_views, inplane_rot_aug_max_angle=None, tilt_rot_aug_max_angle=None):
+    """R_aug [m, 3, 3] of SceneData.apply_rotational_homography_aug (SceneData.py:373-406), drawn from
+    torch's global CPU RNG in the reference's order (in-plane angle, tilt angle, tilt axis)."""
+    R = torch.eye(3)[None, :, :].repeat(num_views, 1, 1)
+    inplane = inplane_rot_aug_max_angle or 0
+    tilt = tilt_rot_aug_max_angle or 0
+    assert inplane >= 0 and tilt >= 0
+    if inplane > 0:
+        ang = inplane * (2 * torch.rand((num_views,), dtype=torch.float32) - 1)
+        vec = torch.zeros((num_views, 3), dtype=torch.float32)
+        vec[:, 2] = ang / 180. * math.pi
+        R = _axis_angle_to_matrix(vec) @ R
+    if tilt > 0:
+        ang = tilt * (2 * torch.rand((num_views,), dtype=torch.float32) - 1)
+        alpha = torch.rand((num_views,), dtype=torch.float32) * 2 * math.pi
+        axis = torch.zeros((num_views, 3), dtype=torch.float32)
+        axis[:, 0] = torch.cos(alpha)
+        axis[:, 1] = torch.sin(alpha)
+        R = _axis_angle_to_matrix(axis * ang[:, None] / 180. * math.pi) @ R
+    return R
+
+
+def apply_rotational_homography_aug_device(data, inplane_rot_aug_max_angle=None, tilt_rot_aug_max_angle=None,
+                                           max_piece=None):
+    """SceneData.apply_rotational_homography_aug (datasets/SceneData.py:355-440) with M on the device:
+    the per-camera 3x3 products (R_aug, H_aug = Ns^-1 R_aug Ns, y' = H_aug y) on the host in fp32
+    as the reference computes them, the image points through gasfm_scene_homography, then the
+    device graph build."""
+    M = _dense_M(data)
+    m = data.y.shape[0]
+    dev = M.device
+    Ns_c, y_c = data.Ns.float().cpu(), data.y.float().cpu()
+    if not (inplane_rot_aug_max_angle or tilt_rot_aug_max_angle):
+        return scene_from_dense_device(M, data.Ns.to(dev), data.y.to(dev), data.scene_name, max_piece=max_piece)
+    R = rotational_homography(m, inplane_rot_aug_max_angle, tilt_rot_aug_max_angle)
+    Ninv = torch.linalg.inv(Ns_c)
+    y = (Ninv @ R @ Ns_c) @ y_c
+    Mn = _native.scene_homography(M.contiguous(), Ns_c.to(dev).contiguous(), R.to(dev).contiguous(),
+                                  Ninv.to(dev).contiguous())
+    return scene_from_dense_device(Mn, Ns_c.to(dev), y.to(dev), data.scene_name,
+                                   calibrated=getattr(data, "calibrated", True), max_piece=max_piece)

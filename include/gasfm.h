@@ -470,6 +470,14 @@ int gasfm_scene_point_csr(const uint64_t* mask, const uint64_t* pt_valid, const 
                           const int32_t* pt_ptr, int32_t m, int32_t n, int32_t* perm, int32_t* pos,
                           void* stream);
 
+/* Rotational homography augmentation of the image points (SceneData.apply_rotational_homography_aug,
+ * datasets/SceneData.py:355-440): out[2c:2c+2, p] = pflat(Ninv_c R_c Ns_c [x, y, 1]^T)[:2] where
+ * (c, p) is valid (mask / pt_valid from gasfm_scene_mask on M), 0 elsewhere.  Ns, R, Ninv:
+ * [m x 3 x 3] row-major; out may not alias M. */
+int gasfm_scene_homography(const float* M, int64_t ldM, int32_t m, int32_t n, const uint64_t* mask,
+                           const uint64_t* pt_valid, const float* Ns, const float* R, const float* Ninv,
+                           float* out, int64_t ldO, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -180,3 +180,16 @@ def test_repro_oracle_matches_reference_core_errors():
     np.testing.assert_allclose(err[f["cam"], f["pt"]], f["edge_errors"], rtol=2e-5, atol=1e-3)
     assert np.isnan(err[~repro.valid_points(f["M"])]).all()
     np.testing.assert_allclose(mean, f["our_repro"], rtol=1e-5)
+
+
+def test_rotational_homography_draws_match_reference():
+    """rotational_homography draws torch's CPU RNG in the reference's order: with the fixture's seed
+    the camera update y' = Ns^-1 R Ns y reproduces the reference's augmented cameras."""
+    from gasfm_amd.scene_device import rotational_homography
+    f = golden("scene_aug.npz")
+    nv, _, tseed, inplane, tilt = f["params"]
+    Ns = torch.from_numpy(f["Ns"])[:int(nv)]  # config 1: every Ns is the same K^-1
+    torch.manual_seed(int(tseed))
+    R = rotational_homography(int(nv), inplane, tilt)
+    y = (torch.linalg.inv(Ns) @ R @ Ns) @ torch.from_numpy(f["s_y"])
+    np.testing.assert_allclose(y.numpy(), f["a_y"], rtol=2e-5, atol=1e-6)  # host BLAS rounding varies by CPU
