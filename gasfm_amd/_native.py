@@ -301,14 +301,17 @@ _TALL_COUNTER = 4095
 # otherwise, and outside a backward pass, param_colsum is colsum.
 _DEFER_FWD = False
 _PENDING = {}
+_SEEN = {}  # graph task -> ids of the parameters that already received a deferred sum in it
 _PENDING_LOCK = threading.Lock()
 
 
 def defer_token(*targets):
-    """Captured by the fused Functions' forward (ctx.defer) and passed to param_colsum: true in
-    a deferring model forward when every tensor that receives a deferred sum is a leaf (a
-    parameter: no autograd node reads its gradient before the pass ends)."""
-    return _DEFER_FWD and all(t is None or t.is_leaf for t in targets)
+    """Captured by the fused Functions' forward (ctx.defer) and passed to param_colsum: in a
+    deferring model forward, the tensors that receive the deferred sums when every one is a leaf
+    (a parameter: no autograd node reads its gradient before the pass ends); else False."""
+    if _DEFER_FWD and all(t is None or t.is_leaf for t in targets):
+        return tuple(t for t in targets if t is not None) or True
+    return False
 
 
 class deferring_param_grads:
@@ -334,6 +337,23 @@ def param_colsum(A, defer):
     task = torch._C._current_graph_task_id() if defer else -1
     if task < 0:
         return colsum(A)
+    if isinstance(defer, tuple):
+        # parameter -> the token (one per Function forward) whose sum it got first in this pass; the
+        # same token again is another output of the same Function (e.g. both attention directions)
+        with _PENDING_LOCK:
+            seen = _SEEN.setdefault(task, {})
+            again = any(seen.get(id(t), id(defer)) != id(defer) for t in defer)
+            for t in defer:
+                seen.setdefault(id(t), id(defer))
+        if again and os.environ.get("GASFM_DEBUG_DEFER"):
+            print("param_colsum: repeated targets", [tuple(t.shape) for t in defer], flush=True)
+        if again:
+            # a second contribution to these parameters in this pass (several forwards, one
+            # backward: train.py sums the scenes' losses).  AccumulateGrad adopts one sum and adds
+            # the other to it, so none may be left unfilled: fill the queued sums first (stream
+            # order puts them before any later add), then sum this one now.
+            _flush_param_colsums(task, final=False)
+            return colsum(A)
     assert A.dim() == 2 and A.stride(1) == 1 and A.dtype == torch.float32
     rows, cols = A.shape
     L = lib()
@@ -351,9 +371,11 @@ def param_colsum(A, defer):
     return out
 
 
-def _flush_param_colsums(task):
+def _flush_param_colsums(task, final=True):
     with _PENDING_LOCK:
         jobs = _PENDING.pop(task, [])
+        if final:
+            _SEEN.pop(task, None)
     if not jobs:
         return
     stream = jobs[0][6]

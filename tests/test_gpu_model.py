@@ -162,3 +162,45 @@ def test_side_stream_bitwise(device, capture):
     assert l1 == l2
     bad = [k for k in g1 if not torch.equal(g1[k], g2[k])]
     assert not bad, f"{len(bad)} of {len(g1)} gradients differ: {bad[:12]}"
+
+
+@pytest.mark.gpu
+def test_several_forwards_one_backward(device):
+    """train.py sums the losses of a batch of scenes and runs ONE backward: every parameter then
+    receives one gradient contribution per scene.  With the batched end-of-backward weight sums
+    (deferred colsums) the gradients must equal the undeferred ones, and both must equal the sum
+    of the per-scene backward passes.  (Regression: the second contribution was added to the
+    first, still-unfilled deferred sum: garbage, then NaN after an optimizer step.)"""
+    from gasfm_amd import synthetic
+    scenes = [gasfm_amd.SceneData.from_synthetic(synthetic.scaled_config4(s, seed=k)).to(device)
+              for s, k in ((0.01, 3), (0.015, 4), (0.008, 5))]
+    torch.manual_seed(0)
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=3)).to(device)
+    gen = torch.Generator().manual_seed(2)
+    funcs = [((torch.randn((d.x.shape[0], 3, 4), generator=gen).to(device)),
+              torch.randn((4, d.x.shape[1]), generator=gen).to(device)) for d in scenes]
+
+    def loss_of(d, f):
+        p = net(d)
+        return (p["Ps_norm"] * f[0]).sum() + (p["pts3D"] * f[1]).sum()
+
+    def grads(batched, defer):
+        net.batch_weight_grads = defer
+        for p in net.parameters():
+            p.grad = None
+        if batched:
+            sum(loss_of(d, f) for d, f in zip(scenes, funcs)).backward()
+        else:
+            for d, f in zip(scenes, funcs):
+                loss_of(d, f).backward()
+        torch.cuda.synchronize()
+        return {k: p.grad.detach().clone() for k, p in net.named_parameters() if p.grad is not None}
+
+    ref = grads(False, False)
+    for batched, defer in ((True, True), (True, False), (False, True)):
+        g = grads(batched, defer)
+        assert g.keys() == ref.keys()
+        for k in ref:
+            assert torch.isfinite(g[k]).all(), k
+            torch.testing.assert_close(g[k], ref[k], rtol=1e-4, atol=1e-5, msg=f"{k} batched={batched} defer={defer}")
+    net.batch_weight_grads = True

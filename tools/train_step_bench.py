@@ -1,0 +1,129 @@
+"""Multi-scene learning step (BASELINE config 3 shape) with the whole per-sample data path on the device.
+
+usage: python tools/train_step_bench.py [--scenes 12] [--batch 4] [--steps 10] [--host]
+
+Synthetic stand-ins for the 12 Euclidean training scenes (windowed visibility, m = 100 views,
+n = 20k points, dense M resident in HBM).  One step follows train.py:60-140 for a batch of
+scenes: per scene sample 10-20 consecutive views (SceneData.sample_data), rotational homography
+augmentation 15 / 20 degrees (conf rhaug-15-20), graph build, forward, ESFMLoss, the per-step
+core errors (compute_core_errors: a host sync per scene, as the reference's .item() calls), then
+one backward of the batch loss and an Adam step.  Every per-sample stage runs on the device
+(scene_device.py, loss.py, evaluation.py); --host instead samples on the CPU and builds the graph
+with the host builder (no augmentation), the way the reference's DataLoader workers feed the GPU.
+Prints one JSON line per mode: scenes/s and the mean ms per stage.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import gasfm_amd  # noqa: E402
+from gasfm_amd import evaluation, synthetic  # noqa: E402
+from gasfm_amd.conf import Conf  # noqa: E402
+from gasfm_amd.loss import ESFMLoss  # noqa: E402
+from gasfm_amd.scene_device import (apply_rotational_homography_aug_device, sample_data_device,  # noqa: E402
+                                    sample_indices, scene_from_dense_device)
+
+
+def make_scenes(k, m, n, dev):
+    out = []
+    for i in range(k):
+        sc = synthetic.windowed_scene(m, n, seed=100 + i)
+        M = torch.from_numpy(sc.dense_M()).to(dev)
+        out.append(scene_from_dense_device(M, torch.from_numpy(sc.Ns()).to(dev), torch.from_numpy(sc.Ps_gt()).to(dev),
+                                           f"train{i}"))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scenes", type=int, default=12)
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--views", type=int, default=100)
+    ap.add_argument("--points", type=int, default=20_000)
+    ap.add_argument("--host", action="store_true", help="also time the host-side data path")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    np.random.seed(0)
+    torch.manual_seed(0)
+    scenes = make_scenes(args.scenes, args.views, args.points, dev)
+    base = gasfm_amd.learning_conf()
+    conf = Conf({"dataset": {"calibrated": True}, "model": base.d["model"],
+                 "loss": {"infinity_pts_margin": 1e-4, "pts_grad_equalization_pre_perspective_divide": True,
+                          "normalize_grad_wrt_valid_projections_only": True, "hinge_loss": True,
+                          "hinge_loss_weight": 1.0},
+                 "eval": {"calc_reprojerr_with_gtposes_for_depth_pred": False}})
+    net = gasfm_amd.GraphAttnSfMNet(conf).to(dev)
+    lossf = ESFMLoss(conf)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+
+    def prep_device(full):
+        s = sample_data_device(full, int(np.random.randint(10, 21)))
+        return apply_rotational_homography_aug_device(s, 15, 20)
+
+    def prep_host(full):
+        idx = sample_indices(len(full.y), int(np.random.randint(10, 21)), adjacent=True)
+        m_idx = np.sort(np.concatenate((2 * idx, 2 * idx + 1)))
+        M = full._M.cpu().numpy()[m_idx]
+        xs = M.reshape(len(idx), 2, -1)
+        keep = ((np.abs(xs).sum(1) != 0).sum(0) >= 2)
+        d = gasfm_amd.SceneData(torch.from_numpy(np.ascontiguousarray(M[:, keep])), full.Ns.cpu()[idx],
+                                full.y.cpu()[idx], full.scene_name)
+        return d.to(dev)
+
+    def run(prep, steps, warmup):
+        t_prep = t_fb = t_opt = 0.0
+        n_done = 0
+        repro = []
+        for it in range(warmup + steps):
+            batch = [scenes[int(i)] for i in np.random.choice(len(scenes), args.batch, replace=False)]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            datas = [prep(s) for s in batch]
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            opt.zero_grad()
+            batch_loss = 0.0
+            for d in datas:
+                pred = net(d)
+                batch_loss = batch_loss + lossf(pred, d)
+                repro.append(evaluation.compute_core_errors(d, pred, conf)["our_repro"])
+                if os.environ.get("TSB_DEBUG"):
+                    print(it, d.x.shape, int(d.x.pts_per_cam.min()), "pred finite",
+                          bool(torch.isfinite(pred["Ps_norm"]).all()), bool(torch.isfinite(pred["pts3D"]).all()),
+                          "loss", float(batch_loss), "repro", repro[-1], flush=True)
+            batch_loss.backward()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            opt.step()
+            torch.cuda.synchronize()
+            t3 = time.perf_counter()
+            if it >= warmup:
+                t_prep += t1 - t0
+                t_fb += t2 - t1
+                t_opt += t3 - t2
+                n_done += len(datas)
+        tot = t_prep + t_fb + t_opt
+        return {"scenes_per_s": n_done / tot, "ms_per_step": 1e3 * tot / steps,
+                "ms_data_prep": 1e3 * t_prep / steps, "ms_fwd_bwd_loss_errors": 1e3 * t_fb / steps,
+                "ms_adam": 1e3 * t_opt / steps, "first_repro_px": float(repro[0]),
+                "last_repro_px": float(repro[-1])}
+
+    res = run(prep_device, args.steps, args.warmup)
+    print(json.dumps({"mode": "device data path (sample + rhaug + graph build on GPU)", "batch": args.batch,
+                      "scene": f"m={args.views} n={args.points}, 10-20 sampled views", **res}), flush=True)
+    if args.host:
+        res = run(prep_host, args.steps, args.warmup)
+        print(json.dumps({"mode": "host data path (CPU sampling + host graph build, no rhaug, then .to)",
+                          "batch": args.batch, "scene": f"m={args.views} n={args.points}", **res}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
