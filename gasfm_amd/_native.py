@@ -88,6 +88,7 @@ _SIGS = {
     "gasfm_scene_emit": (_i32, [_vp, _i64, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_scene_point_csr": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "gasfm_scene_homography": (_i32, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "gasfm_sum_n": (_i32, [_i32, _vp, _i64, _vp, _vp]),
     "gasfm_esfm_fwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _vp, _vp]),
     "gasfm_esfm_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _i32, _i32,
                               _vp, _vp, _vp, _vp, _vp]),
@@ -812,3 +813,21 @@ def scene_build(M, Ns=None):
     cam_ptr = tile_base[0::T // m].contiguous() if T else torch.zeros(m + 1, **i32)
     return {"cam": cam, "pt": pt, "values": vals, "pt_count": pt_count, "cam_ptr": cam_ptr, "pt_ptr": pt_ptr,
             "perm": perm, "pos": pos}
+
+
+def sum_n(tensors):
+    """Elementwise sum of same-shape contiguous fp32 CUDA tensors in one pass (gasfm_sum_n)."""
+    t0 = tensors[0]
+    for t in tensors:
+        _req(t, "sum_n input")
+        if t.shape != t0.shape:
+            raise ValueError("sum_n: shapes differ")
+    if t0.numel() % 4:  # the kernel streams float4s (odd E): pairwise adds on the device
+        out = tensors[0].clone()
+        for t in tensors[1:]:
+            out += t
+        return out
+    out = torch.empty_like(t0)
+    st = lib().gasfm_sum_n(len(tensors), _ptrs(tensors), t0.numel(), _p(out), _stream(t0))
+    check(st, "gasfm_sum_n")
+    return out

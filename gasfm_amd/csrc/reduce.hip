@@ -273,6 +273,28 @@ static int tall_blocks(int64_t rows, int cols) {
   return int(nb < 1 ? 1 : nb);
 }
 
+
+// dst = src[0] + src[1] + ... + src[n-1] (in index order; float4 per thread, grid-stride).  The
+// gradient of a tensor with n consumers in ONE pass: autograd would run n-1 full-size adds.
+constexpr int kMaxSumSrc = 16;
+struct SumSrcs {
+  const float* p[kMaxSumSrc];
+};
+
+__global__ __launch_bounds__(256) void sum_n_kernel(SumSrcs s, int n, int64_t count4, float* __restrict__ dst) {
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < count4; i += int64_t(gridDim.x) * 256) {
+    float4 acc = reinterpret_cast<const float4*>(s.p[0])[i];
+    for (int k = 1; k < n; ++k) {
+      const float4 v = reinterpret_cast<const float4*>(s.p[k])[i];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(dst)[i] = acc;
+  }
+}
+
 }  // namespace gasfm
 
 using namespace gasfm;
@@ -354,4 +376,21 @@ extern "C" int32_t gasfm_colsum_multi_counters(int32_t n, const int32_t* cols) {
     best = c > best ? c : best;
   }
   return best;
+}
+
+extern "C" int gasfm_sum_n(int32_t n, const float* const* src, int64_t count, float* dst, void* stream) {
+  GASFM_REQUIRE(n >= 1 && n <= kMaxSumSrc && count >= 0 && dst && src, "gasfm_sum_n: n=%d count=%lld", n,
+                (long long)count);
+  GASFM_REQUIRE(count % 4 == 0 && aligned16(dst), "gasfm_sum_n: count %% 4 and 16-byte alignment required");
+  SumSrcs s{};
+  for (int k = 0; k < n; ++k) {
+    GASFM_REQUIRE(src[k] && aligned16(src[k]), "gasfm_sum_n: source %d null or unaligned", k);
+    s.p[k] = src[k];
+  }
+  if (count == 0) return GASFM_OK;
+  const int64_t c4 = count / 4;
+  const int64_t want = (c4 + 255) / 256;
+  const int grid = int(want < 4096 ? want : 4096);
+  hipLaunchKernelGGL(sum_n_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, s, n, c4, dst);
+  return launch_status("gasfm_sum_n");
 }

@@ -639,6 +639,22 @@ def scene_plans(data, device):
     return plans
 
 
+class FanOutFn(torch.autograd.Function):
+    """x -> n identical views; the backward sums the consumers' gradients in one kernel
+    (gasfm_sum_n) where autograd would run n - 1 full-size adds."""
+
+    @staticmethod
+    def forward(ctx, x, n):
+        return tuple(x.view_as(x) for _ in range(n))
+
+    @staticmethod
+    def backward(ctx, *gs):
+        gs = [g.contiguous() for g in gs if g is not None]
+        if not gs:
+            return None, None
+        return (gs[0] if len(gs) == 1 else _native.sum_n(gs)), None
+
+
 class GraphAttnSfMNet(Module):
     """graph_attn_sfm.py:8-185 (BaseNet: baseNet.py:8-92)."""
 
@@ -735,7 +751,13 @@ class GraphAttnSfMNet(Module):
         plans = edges.plans
         lin = self.embed.post_embed_lin
         P = dense.linear(values, lin) if lin is not None else self.embed(values)
-        P0 = P if self.add_skipconn_from_init_projfeat else None
+        nb = len(self.equivariant_blocks)
+        p0s = [P if self.add_skipconn_from_init_projfeat else None] * nb
+        if self.add_skipconn_from_init_projfeat and P.is_cuda and P.requires_grad and torch.is_grad_enabled():
+            # the embedded input feeds block 0 and every block's projection update (layers.py:245-251):
+            # its gradient is summed in one pass instead of autograd's nb full-size adds
+            views = FanOutFn.apply(P.contiguous(), nb + 1)
+            P, p0s = views[0], list(views[1:])
         pts = view = glob = None
         sf = self.stateful_global_features
         heads = self.view_head_enabled or self.scenepoint_head_enabled
@@ -751,7 +773,7 @@ class GraphAttnSfMNet(Module):
             else:
                 nxt = fgu if final_fused else None
             P, pts, view, glob = blk.forward_plan(P, plans, edges, pts if sf else None, view if sf else None,
-                                                  glob if sf else None, P0=P0, carry=carry, nxt=nxt)
+                                                  glob if sf else None, P0=p0s[i], carry=carry, nxt=nxt)
         if heads:
             args = (pts if sf else None, view if sf else None, glob if sf else None)
             if P.is_cuda and P.shape[1] == 32 and fgu.fusable():

@@ -478,6 +478,11 @@ int gasfm_scene_homography(const float* M, int64_t ldM, int32_t m, int32_t n, co
                            const uint64_t* pt_valid, const float* Ns, const float* R, const float* Ninv,
                            float* out, int64_t ldO, void* stream);
 
+/* dst[i] = src[0][i] + ... + src[n-1][i] (index order), n <= 16, count % 4 == 0, 16-byte aligned
+ * rows: the gradient of a tensor with n consumers in one pass (the embedded projection input P0
+ * feeds every block's projection update, layers.py:245-251; autograd would add n-1 times). */
+int gasfm_sum_n(int32_t n, const float* const* src, int64_t count, float* dst, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
