@@ -2,7 +2,7 @@
 set -e
 V=$1
 for lib in libgasfm.so $V; do
-  echo "== $lib"; GASFM_LIB=$PWD/gasfm_amd/$lib timeout -k 10 200 python tools/edge_bench.py 2>&1 | grep -i "kernel" | head -12
+  echo "== $lib"; GASFM_LIB=$PWD/gasfm_amd/$lib timeout -k 10 200 python tools/edge_bench.py 2>&1 | grep -i "epilogue_fwd\|prologue_bwd" | head -4
 done
 for rep in 1 2; do
 for lib in libgasfm.so $V; do
