@@ -8,8 +8,9 @@ aggregation (and backward) in hand-written HIP for gfx950 (gasfm_amd/csrc).
 from .attention import AttnPlan, gat_attention  # noqa: F401
 from .conf import Conf, learning_conf, optim_conf  # noqa: F401
 from .gatv2 import GATv2Conv  # noqa: F401
+from .loss import ESFMLoss  # noqa: F401
 from .model import GraphAttnSfMNet  # noqa: F401
 from .scene import AxialAggregationGraphWrapper, SceneData, SparseMat, M2sparse  # noqa: F401
 
-__all__ = ["AttnPlan", "gat_attention", "Conf", "learning_conf", "optim_conf", "GATv2Conv", "GraphAttnSfMNet",
+__all__ = ["AttnPlan", "gat_attention", "Conf", "learning_conf", "optim_conf", "GATv2Conv", "ESFMLoss", "GraphAttnSfMNet",
            "AxialAggregationGraphWrapper", "SceneData", "SparseMat", "M2sparse"]

@@ -240,20 +240,30 @@ def attn_bwd_combine(combine, n_combine, HC, part_dxr, dXR):
 
 
 _COUNTERS = {}
+_COUNTER_POOL = 1 << 16
 
 
 def _counters(device, n):
-    """Per-device zeroed uint32 ticket counters for gasfm_colsum (self-resetting).
+    """A range of n zeroed uint32 ticket counters for one colsum launch (self-resetting: the last
+    arriver of each column chunk puts its counter back to 0).
 
-    Allocated once, large (a replacement allocated while a hipGraph is being captured would
-    leave the nodes captured before it pointing at the freed array)."""
+    Every call gets its OWN range from a per-device pool, handed out round-robin, so colsums that
+    run concurrently (on different streams, or on parallel branches of a captured graph) never
+    share a ticket: a range comes back only after the other ~65k counters have been handed out.
+    The pool is allocated once, large (a replacement allocated while a hipGraph is being captured
+    would leave the nodes captured before it pointing at the freed array)."""
+    n = max(1, int(n))
+    if n > _COUNTER_POOL:
+        raise ValueError(f"colsum counters: {n} requested, pool holds {_COUNTER_POOL}")
     c = _COUNTERS.get(device)
-    if c is None or c.numel() < n:
-        if c is not None and torch.cuda.is_current_stream_capturing():
-            raise RuntimeError(f"colsum counters: {n} needed during hipGraph capture, {c.numel()} allocated")
-        c = torch.zeros(max(n, 65536), dtype=torch.int32, device=device)
+    if c is None:
+        c = [torch.zeros(_COUNTER_POOL, dtype=torch.int32, device=device), 0]
         _COUNTERS[device] = c
-    return c
+    pool, at = c
+    if at + n > _COUNTER_POOL:
+        at = 0
+    c[1] = at + n
+    return pool[at:at + n]
 
 
 def colsum(A, out=None):
@@ -282,14 +292,11 @@ def colsum_tall(A, out=None):
         out = torch.empty(cols, dtype=torch.float32, device=A.device)
     L = lib()
     ws = torch.empty(max(1, int(L.gasfm_colsum_tall_ws_floats(rows, cols))), dtype=torch.float32, device=A.device)
-    # its own counter word, after the colsum ones (one array per device, self-resetting)
-    cnt = _counters(A.device, _TALL_COUNTER + 1)[_TALL_COUNTER:]
+    cnt = _counters(A.device, 1)
     st = L.gasfm_colsum_tall(_p(A), rows, cols, _p(ws), _p(out), _p(cnt), _stream(out))
     check(st, "gasfm_colsum_tall")
     return out
 
-
-_TALL_COUNTER = 4095
 
 
 # ---------------------------------------------------------------- batched weight-gradient sums
@@ -337,6 +344,11 @@ def param_colsum(A, defer):
     ``defer`` (see above) and called inside one."""
     task = torch._C._current_graph_task_id() if defer else -1
     if task < 0:
+        return colsum(A)
+    if isinstance(defer, tuple) and any(t.grad is not None for t in defer):
+        # the parameter already holds a gradient (retain_graph and a second backward, or two
+        # forwards backpropagated separately): AccumulateGrad ADDS the returned tensor to it at
+        # once, so it must be filled now
         return colsum(A)
     if isinstance(defer, tuple):
         # parameter -> the token (one per Function forward) whose sum it got first in this pass; the

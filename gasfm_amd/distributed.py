@@ -24,6 +24,8 @@ all-reduce of the 145 M replicated parameters.
 
 Loss convention: each rank's loss must contain the replicated outputs'
 (Ps_norm) term in full and its own points' (pts3D[:, point_slice]) term.
+``gasfm_amd.ESFMLoss`` on a sharded scene follows it: every rank computes the
+global loss (one 2-float all-reduce) and its Ps gradient is all-reduced.
 """
 import copy
 import fnmatch
@@ -217,6 +219,7 @@ def shard_scene(scene, rank, world, max_piece=None):
         p.tag = k + "_partial"
     data.point_slice = slice(p0, p1)
     data.n_global = n
+    data.n_edges_global = int(pt.shape[0])
     data.shard = ShardContext(rank, world)
     return data
 
@@ -241,14 +244,24 @@ class ShardedGraphAttnSfMNet(torch.nn.Module):
         return self.net.forward(data, shard=shard, partial_plans=data.partial_plans)
 
     def sync_grads(self):
-        params = dict(self.net.named_parameters())
-        grads = [params[k].grad for k in self.local_names if params[k].grad is not None]
-        if not grads or dist.get_world_size(self.group) == 1:
+        """One all-reduce of every rank-local parameter's gradient, in a fixed layout: a parameter
+        without a gradient on this rank contributes zeros (and gets the summed gradient), so all
+        ranks reduce buffers of the same size and order."""
+        if dist.get_world_size(self.group) == 1:
             return
-        flat = torch.cat([g.reshape(-1) for g in grads])
+        params = dict(self.net.named_parameters())
+        ps = [params[k] for k in self.local_names]
+        if not ps:
+            return
+        dev = ps[0].device
+        flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1).to(dev) for p in ps])
         shard = ShardContext(dist.get_rank(self.group), dist.get_world_size(self.group), self.group)
         shard.all_reduce_(flat)
         off = 0
-        for g in grads:
-            g.copy_(flat[off:off + g.numel()].view_as(g))
-            off += g.numel()
+        for p in ps:
+            g = flat[off:off + p.numel()].view_as(p)
+            if p.grad is None:
+                p.grad = g.clone()
+            else:
+                p.grad.copy_(g)
+            off += p.numel()

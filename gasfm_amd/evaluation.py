@@ -22,18 +22,22 @@ from .loss import _edge_tensors
 def _pixel_measurements(data):
     """[E, 2] pixel coordinates of the edges, gathered from the dense M once per scene/device."""
     pv = data.graph_wrappers["proj2view"].plan
-    xy = getattr(pv, "_pixel_xy", None)
-    if xy is None:
-        M = getattr(data, "M", None)
-        if M is None:
-            M = getattr(data, "_M", None)
-        if M is None:
-            raise ValueError("compute_core_errors: the scene carries no dense measurement matrix M")
-        idx = data.x.indices
-        M = M.to(idx.device)
-        xy = torch.stack([M[2 * idx[0], idx[1]], M[2 * idx[0] + 1, idx[1]]], 1).float().contiguous()
-        pv._pixel_xy = xy
-    return xy
+    M = getattr(data, "M", None)
+    if M is None:
+        M = getattr(data, "_M", None)
+    if M is None:
+        raise ValueError("compute_core_errors: the scene carries no dense measurement matrix M")
+    idx = data.x.indices
+    # keyed on both tensors' storage and version: an in-place edit of M (augmentation) or of the
+    # indices recomputes the gather
+    key = (M.data_ptr(), M._version, tuple(M.shape), idx.data_ptr(), idx._version)
+    cached = getattr(pv, "_pixel_xy", None)
+    if cached is None or cached[0] != key:
+        Md = M.to(idx.device)
+        xy = torch.stack([Md[2 * idx[0], idx[1]], Md[2 * idx[0] + 1, idx[1]]], 1).float().contiguous()
+        cached = (key, xy)
+        pv._pixel_xy = cached
+    return cached[1]
 
 
 def _pixel_cameras(data, Ps_norm):

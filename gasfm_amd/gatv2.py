@@ -9,7 +9,7 @@ add_self_loops=False).  Parameter names/shapes match PyG exactly
 
 Two call forms:
   forward(x, edge_index)   the PyG call used by the reference layer code
-                           (generic graphs; plan cached per edge_index tensor)
+                           (generic graphs; plan cached on the edge_index tensor)
   attend(x_src, x_tgt, plan)  the MI355X fast path used by gasfm_amd.model:
                            lin_l on source rows only, lin_r on target rows only
                            (PyG computes both on all E+N rows), then the fused
@@ -51,7 +51,6 @@ class GATv2Conv(torch.nn.Module):
             self.bias = torch.nn.Parameter(torch.empty(heads * out_channels))
         else:
             self.register_parameter("bias", None)
-        self._plan_cache = {}
         self.reset_parameters()
 
     def reset_parameters(self):
@@ -64,16 +63,6 @@ class GATv2Conv(torch.nn.Module):
         _glorot_(self.att)
         if self.bias is not None:
             torch.nn.init.zeros_(self.bias)
-
-    def __deepcopy__(self, memo):
-        # plans hold device tensors keyed by data_ptr: never carry them across copies
-        cls = self.__class__
-        new = cls.__new__(cls)
-        memo[id(self)] = new
-        import copy
-        for k, v in self.__dict__.items():
-            setattr(new, k, {} if k == "_plan_cache" else copy.deepcopy(v, memo))
-        return new
 
     def _bias(self, ref):
         if self.bias is not None:
@@ -101,20 +90,23 @@ class GATv2Conv(torch.nn.Module):
 
     # ------------------------------------------------------------------ PyG call form
     def _plan_for(self, edge_index, num_nodes):
-        key = (edge_index.data_ptr(), edge_index.shape[1], edge_index._version, num_nodes, str(edge_index.device))
-        plan = self._plan_cache.get(key)
-        if plan is None:
-            src, dst = edge_index[0].cpu(), edge_index[1].cpu()
-            unique_src = src.numel() == 0 or int(torch.bincount(src).max()) <= 1
-            if unique_src:
-                plan = AttnPlan.from_targets(dst, num_nodes, src=src, src_rows=num_nodes).to(edge_index.device)
-                plan.gather_src = None
-            else:
-                # repeated sources: gather per-edge source rows first (edge order == plan order)
-                plan = AttnPlan.from_targets(dst, num_nodes).to(edge_index.device)
-                plan.gather_src = src.to(edge_index.device)
-            self._plan_cache.clear()
-            self._plan_cache[key] = plan
+        """The attention plan of this edge_index TENSOR, cached on the tensor object itself (so a
+        new edge_index that the caching allocator places at a freed tensor's address never finds
+        that tensor's plan) and keyed on its version (an in-place edit rebuilds it)."""
+        key = (edge_index._version, int(num_nodes), tuple(edge_index.shape))
+        cached = getattr(edge_index, "_gasfm_plan", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        src, dst = edge_index[0].cpu(), edge_index[1].cpu()
+        unique_src = src.numel() == 0 or int(torch.bincount(src).max()) <= 1
+        if unique_src:
+            plan = AttnPlan.from_targets(dst, num_nodes, src=src, src_rows=num_nodes).to(edge_index.device)
+            plan.gather_src = None
+        else:
+            # repeated sources: gather per-edge source rows first (edge order == plan order)
+            plan = AttnPlan.from_targets(dst, num_nodes).to(edge_index.device)
+            plan.gather_src = src.to(edge_index.device)
+        edge_index._gasfm_plan = (key, plan)
         return plan
 
     def forward(self, x, edge_index):

@@ -20,6 +20,10 @@ Usage::
         return loss
     step = CapturedStep(fwd_bwd, params=model.parameters())
     loss = step()                  # replays the graph; p.grad holds this step's gradients
+
+After each replay every parameter's ``.grad`` is (re)set to the tensor the graph writes, so
+``optimizer.zero_grad()`` between steps is harmless; a replay does not accumulate into an
+existing gradient (each replay's gradients are that step's alone, as after zero_grad + backward).
 """
 import torch
 
@@ -109,6 +113,10 @@ class CapturedStep:
             return
         # detached: the captured autograd graph is not kept alive between replays
         self.graph, self.static_out = g, out.detach()
+        # the .grad tensors the captured backward writes into: re-attached after every replay, so
+        # an optimizer.zero_grad() (set_to_none=True by default, train.py:66) between steps cannot
+        # leave the replayed gradients in tensors no parameter references
+        self.static_grads = [p.grad for p in self.params]
 
     @property
     def captured(self):
@@ -119,4 +127,6 @@ class CapturedStep:
             self._zero()
             return self.fn()
         self.graph.replay()
+        for p, g in zip(self.params, self.static_grads):
+            p.grad = g
         return self.static_out

@@ -28,7 +28,11 @@ class ESFMLossFn(torch.autograd.Function):
     """(Ps [m, 3, 4], pts3D [4, n]) -> mean over the edges of the per-edge loss term."""
 
     @staticmethod
-    def forward(ctx, Ps, pts3D, edges, vals, cam_ptr, pt_ptr, pt_perm, conf):
+    def forward(ctx, Ps, pts3D, edges, vals, cam_ptr, pt_ptr, pt_perm, conf, shard=None, E_global=None):
+        """shard (gasfm_amd.distributed.ShardContext) / E_global: point-sharded scene.  Every rank
+        holds all cameras and its own points with ALL their edges, so the loss is the global one
+        from (sum of terms, #valid-depth) all-reduced over the ranks and divided by the global
+        edge count; backward: dpts3D is rank-local and complete, dPs is summed over the ranks."""
         margin, hinge_w, hinge, equalize, valid_only = conf
         cam, pt = edges
         m = Ps.shape[0]
@@ -37,34 +41,46 @@ class ESFMLossFn(torch.autograd.Function):
         part = torch.empty((_native.esfm_part_rows(cam.shape[0]), 2), dtype=torch.float32, device=X.device)
         _native.esfm_fwd(cam, pt, vals, P, X, margin, hinge_w, hinge, part)
         tot = _native.colsum(part)  # (sum of terms, #valid-depth)
+        E = cam.shape[0]
+        if shard is not None:
+            tot = shard.all_reduce_(tot)
+            E = int(E_global)
         ctx.save_for_backward(P, X, cam, pt, vals, cam_ptr, pt_ptr, pt_perm, tot)
-        ctx.conf = conf
-        return tot[0] / cam.shape[0]
+        ctx.conf, ctx.shard, ctx.E = conf, shard, E
+        return tot[0] / E
 
     @staticmethod
     def backward(ctx, dloss):
         P, X, cam, pt, vals, cam_ptr, pt_ptr, pt_perm, tot = ctx.saved_tensors
         margin, hinge_w, hinge, equalize, valid_only = ctx.conf
         dP, dX = torch.empty_like(P), torch.empty_like(X)
-        dloss = dloss.reshape(1).to(torch.float32).contiguous()
+        dloss = dloss.reshape(1).to(torch.float32)
+        if ctx.E != cam.shape[0]:
+            dloss = dloss * (cam.shape[0] / ctx.E)  # the kernels divide by the local edge count
+        dloss = dloss.contiguous()
         _native.esfm_bwd(cam_ptr, pt_ptr, pt_perm, cam, pt, vals, P, X, margin, hinge_w, hinge, equalize, valid_only,
                          dloss, tot, dP, dX)
-        return dP.view(-1, 3, 4), dX, None, None, None, None, None, None
+        if ctx.shard is not None:
+            ctx.shard.all_reduce_(dP)
+        return dP.view(-1, 3, 4), dX, None, None, None, None, None, None, None, None
 
 
 def _edge_tensors(data):
     """int32 (cam, pt), contiguous float32 values and the camera / point CSRs of the network's own
     plans (proj2view: camera segments over the cam-major edges; proj2scenepoint: point segments
-    with perm = edge ids in point order).  Cached on the proj2view plan, which is per device."""
+    with perm = edge ids in point order).  Cached on the proj2view plan, which is per device, keyed
+    on the index tensor's storage and version."""
     gw = data.graph_wrappers
     pv, ps = gw["proj2view"].plan, gw["proj2scenepoint"].plan
+    idx = data.x.indices
+    key = (idx.data_ptr(), idx._version, tuple(idx.shape))  # an in-place edit of the indices invalidates it
     cache = getattr(pv, "_esfm_edges", None)
-    if cache is None:
+    if cache is None or cache[0] != key:
         if pv.perm is not None:
             raise ValueError("ESFMLoss: proj2view plan must cover cam-major sorted edges")
-        idx = data.x.indices
-        cache = (idx[0].to(torch.int32).contiguous(), idx[1].to(torch.int32).contiguous())
+        cache = (key, (idx[0].to(torch.int32).contiguous(), idx[1].to(torch.int32).contiguous()))
         pv._esfm_edges = cache
+    cache = cache[1]
     vals = data.x.values
     if vals.dtype != torch.float32 or not vals.is_contiguous():
         vals = vals.float().contiguous()
@@ -102,4 +118,9 @@ class ESFMLoss(torch.nn.Module):
         edges, vals, cam_ptr, pt_ptr, pt_perm = _edge_tensors(data)
         if edges[0].shape[0] == 0:
             raise ValueError("ESFMLoss: no valid observations (the reference's mean would be NaN)")
-        return ESFMLossFn.apply(Ps, pts3D, edges, vals, cam_ptr, pt_ptr, pt_perm, self.kernel_conf())
+        shard = getattr(data, "shard", None)
+        E_global = getattr(data, "n_edges_global", None)
+        if shard is not None and E_global is None:
+            raise ValueError("ESFMLoss: a sharded scene must carry n_edges_global (distributed.shard_scene)")
+        return ESFMLossFn.apply(Ps, pts3D, edges, vals, cam_ptr, pt_ptr, pt_perm, self.kernel_conf(), shard,
+                                E_global)

@@ -279,3 +279,69 @@ def test_rccl_bench_captures_and_replays(tmp_path):
     assert "hipGraph replay" in r.stderr, r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["execution"].startswith("hipGraph replay") and res["value"] > 0
+
+
+def _esfm_conf():
+    import gasfm_amd
+    return gasfm_amd.Conf({"model": {"view_head": {"enabled": True}, "scenepoint_head": {"enabled": True}},
+                           "loss": {"infinity_pts_margin": 1e-4, "pts_grad_equalization_pre_perspective_divide": True,
+                                    "normalize_grad_wrt_valid_projections_only": True, "hinge_loss": True,
+                                    "hinge_loss_weight": 1.0}})
+
+
+def _worker_sharded_esfm(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import gasfm_amd
+        from oracle.weights import deterministic_state_dict
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        sc = synthetic.scaled_config4(0.02, seed=5)
+        net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=2))
+        net.load_state_dict(deterministic_state_dict(net.state_dict()))
+        model = gd.ShardedGraphAttnSfMNet(net.to(dev))
+        data = gd.shard_scene(sc, rank, world, max_piece=64).to(dev)
+        loss = gasfm_amd.ESFMLoss(_esfm_conf())(model(data), data)
+        loss.backward()
+        model.sync_grads()
+        grads = {k: p.grad.detach().cpu().numpy() for k, p in net.named_parameters()}
+        q.put((rank, float(loss), grads))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_esfm_loss_matches_single_gpu(device):
+    """ESFMLoss on a point-sharded scene: every rank gets the GLOBAL loss (sum and
+    #valid-depth all-reduced, divided by the global edge count) and, after sync_grads, every
+    parameter gradient equals the single-GPU one and is bitwise identical across ranks."""
+    import gasfm_amd
+    from oracle.weights import deterministic_state_dict
+    sc = synthetic.scaled_config4(0.02, seed=5)
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=2))
+    net.load_state_dict(deterministic_state_dict(net.state_dict()))
+    net = net.to(device)
+    data = gasfm_amd.SceneData.from_synthetic(sc, max_piece=64).to(device)
+    loss = gasfm_amd.ESFMLoss(_esfm_conf())(net(data), data)
+    loss.backward()
+    ref = {k: p.grad.detach().double().cpu().numpy() for k, p in net.named_parameters()}
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_sharded_esfm, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=600) for _ in procs), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, l, grads in res:
+        assert abs(l - float(loss)) <= 1e-5 * abs(float(loss)), (rank, l, float(loss))
+        for k, r in ref.items():
+            g = grads[k].astype(np.float64)
+            nr = np.linalg.norm(r)
+            assert np.linalg.norm(g - r) <= 1e-3 * nr + 1e-7, f"rank {rank} {k}: {np.linalg.norm(g - r):.3e} / {nr:.3e}"
+    for k in ref:
+        assert np.array_equal(res[0][2][k], res[1][2][k]), k
