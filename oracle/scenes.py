@@ -12,8 +12,11 @@ import torch
 from .gasfm_ref import Graph
 
 
-def graph_from_dense(M, Ns):
-    """M [2m, n] pixels (0 = unobserved), Ns [m, 3, 3] -> (values [E, 2] float64, Graph)."""
+def graph_from_dense(M, Ns, fp32_values=False):
+    """M [2m, n] pixels (0 = unobserved), Ns [m, 3, 3] -> (values [E, 2] float64, Graph).
+
+    fp32_values: normalise as the reference does on its float32 M / Ns (geo_utils.normalize_M,
+    geo_utils.py:689-703: a batched fp32 ``Ns @ [x; y; 1]``), then widen to float64."""
     M = np.asarray(M, dtype=np.float64)
     Ns = np.asarray(Ns, dtype=np.float64)
     m, n = M.shape[0] // 2, M.shape[1]
@@ -22,8 +25,14 @@ def graph_from_dense(M, Ns):
     valid[:, valid.sum(axis=0) < 2] = False
     cam, pt = np.nonzero(valid)                          # row-major == cam-major
     h = np.concatenate([M3, np.ones((m, n, 1))], axis=2)  # (m, n, 3)
-    norm = np.einsum("mij,mnj->mni", Ns, h)[:, :, :2]
-    values = norm[cam, pt]
+    if fp32_values:
+        M32 = torch.from_numpy(np.asarray(M, dtype=np.float32)).reshape(m, 2, n)
+        h32 = torch.cat([M32, torch.ones((m, 1, n), dtype=torch.float32)], 1)
+        norm32 = (torch.from_numpy(Ns.astype(np.float32)) @ h32).permute(0, 2, 1)[:, :, :2]
+        values = norm32.numpy()[cam, pt].astype(np.float64)
+    else:
+        norm = np.einsum("mij,mnj->mni", Ns, h)[:, :, :2]
+        values = norm[cam, pt]
     return values, graph_from_edges(cam, pt, m, n)
 
 

@@ -28,3 +28,8 @@ def tensor_for(key, shape):
 
 def deterministic_state_dict(template, dtype=torch.float32):
     return {k: torch.from_numpy(tensor_for(k, tuple(v.shape))).to(dtype) for k, v in template.items()}
+
+
+def probe_vector(key, n):
+    """Regenerable U(-1, 1) vector r for gradient projections G @ r (fixtures of full-width nets)."""
+    return np.random.default_rng(zlib.crc32(("probe/" + key).encode())).uniform(-1.0, 1.0, size=(n,))

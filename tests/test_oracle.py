@@ -193,3 +193,52 @@ def test_rotational_homography_draws_match_reference():
     R = rotational_homography(int(nv), inplane, tilt)
     y = (torch.linalg.inv(Ns) @ R @ Ns) @ torch.from_numpy(f["s_y"])
     np.testing.assert_allclose(y.numpy(), f["a_y"], rtol=2e-5, atol=1e-6)  # host BLAS rounding varies by CPU
+
+
+def _oracle_step(f, scenes_keys, layers, loss_conf):
+    """oracle fp64 forward of each scene + ESFMLoss restatement, summed, one backward."""
+    from oracle import esfm_loss
+    import gasfm_amd
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=layers))
+    sd = {k: v.clone().requires_grad_(True) for k, v in
+          deterministic_state_dict(net.state_dict(), torch.float64).items()}
+    del net
+    total = torch.zeros((), dtype=torch.float64)
+    losses = []
+    for Mk, Nk in scenes_keys:
+        vals, g = scenes.graph_from_dense(f[Mk], f[Nk], fp32_values=True)
+        vals = torch.as_tensor(vals, dtype=torch.float64)
+        r = gasfm_ref.forward(sd, vals, g, dtype=torch.float64)
+        loss = esfm_loss.esfm_loss_edges(r["Ps_norm"], r["pts3D"], g.cam, g.pt, vals, *loss_conf)
+        losses.append(float(loss.detach()))
+        total = total + loss
+    total.backward()
+    return losses, {k: v.grad for k, v in sd.items()}
+
+
+LOSS_CONF = (1e-4, True, 1.0, True, True)  # margin, hinge, hinge_w, equalize, valid_only
+
+
+def _check_projected(grads, f):
+    """normwise 1e-9 (fp64 vs fp64; the measurements normalised in fp32 on both sides)."""
+    from conftest import fixture_grad, project_grad
+    for k, g in grads.items():
+        ref, _ = fixture_grad(f, k)
+        got = project_grad(k, g if g is not None else torch.zeros(1))
+        assert np.linalg.norm(got - ref) <= 1e-9 * np.linalg.norm(ref) + 1e-15, k
+
+
+def test_oracle_training_step_matches_reference_config2():
+    """Config 2 (optim conf, 9 blocks, full width, ESFMLoss): the oracle's gradients == the reference's."""
+    f = golden("net_optim9_grads.npz")
+    losses, grads = _oracle_step(f, [("M", "Ns")], 9, LOSS_CONF)
+    np.testing.assert_allclose(losses[0], float(f["loss"][()]), rtol=1e-10)
+    _check_projected(grads, f)
+
+
+def test_oracle_training_step_matches_reference_config3():
+    """Config 3 (learning conf, 12 blocks): batch of two scenes, summed ESFMLoss, one backward."""
+    f = golden("train_step12.npz")
+    losses, grads = _oracle_step(f, [("M0", "Ns0"), ("M1", "Ns1")], 12, LOSS_CONF)
+    np.testing.assert_allclose(losses, [float(f["loss0"][()]), float(f["loss1"][()])], rtol=1e-10)
+    _check_projected(grads, f)
