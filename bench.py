@@ -12,7 +12,7 @@ timed wall time).  With N > 1 the scene's points are sharded over the ranks
 
 Also reported, on the same line:
   roofline      the fused edge-softmax + aggregation forward of the point direction
-                (attn_fwd_glds_kernel<32,8>, the north-star kernel), timed live with HIP
+                (attn_fwd_grp_kernel<4,1>, the north-star kernel), timed live with HIP
                 events around each of its launches on its stream right after the timed
                 region; achieved = SURVEY §8(d)'s algorithmic bytes / mean duration;
                 peak 8.0 TB/s.
@@ -231,7 +231,7 @@ def main():
                                    f"{args.layers}-block GraphAttnSfMNet (learning_euc widths) fwd+bwd",
                        "cameras": sc.m, "points": sc.n, "edges": E, "blocks": args.layers,
                        "parallelism": f"point-sharded x{world}" if dist_on else "single GPU"},
-            "roofline": {"kernel": "attn_fwd_glds_kernel<32,8> point direction (proj2scenepoint), per launch",
+            "roofline": {"kernel": "attn_fwd_grp_kernel<4,1> point direction (proj2scenepoint), per launch",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                          "traffic": pmc_traffic(e_local, n_local),

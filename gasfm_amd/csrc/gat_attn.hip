@@ -445,6 +445,139 @@ __global__ __launch_bounds__(kBlock) void attn_fwd_glds_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// forward, grouped items (Geom<32,8>, XL streamed in segment order, perm == NULL).
+// A wave task is 8 consecutive work items; lane group g (8 lanes = one 128-B edge row) owns
+// item g of the task and walks its edges U rows per iteration, keeping the segment's online
+// softmax state in its own lanes: no cross-row merge per item (the row-parallel kernels above
+// spend ~a chunk's worth of shuffles and exps merging 8 row states per item), and the 8 output
+// rows of a task are stored side by side.  Short point segments (~20 edges) then run at
+// ~(mean / padded max) lane occupancy instead of 20/32, with no per-item tail.
+// Pipelining: every iteration waits for its rows, issues the NEXT iteration's U rows (or, at
+// the last iteration of a task, the next task's first rows and XR rows), then computes.
+// ------------------------------------------------------------------------------------------
+template <int U, int MINW>
+__global__ __launch_bounds__(kBlock, MINW) void attn_fwd_grp_kernel(
+    const float* __restrict__ XL, int64_t ldXL, const float* __restrict__ XR, int64_t ldXR,
+    const float* __restrict__ att, const float* __restrict__ bias, const gasfm_work_item* __restrict__ items,
+    int n_items, float slope, int finalize, float* __restrict__ out, int64_t ldOut, float* __restrict__ seg_max,
+    float* __restrict__ seg_sum, int64_t ldStat, float* __restrict__ part) {
+  constexpr int HC = 32, H = 4, C = 8, LDP = HC + 2 * H, GR = 8;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane >> 3, li = lane & 7, f0 = li * 4, h = f0 / C;
+  const int nwaves = gridDim.x * (blockDim.x / kWave);
+  const int ntasks = (n_items + GR - 1) / GR;
+  float attv[4], bv[4] = {0.f, 0.f, 0.f, 0.f};
+  load_vec<4>(attv, att + f0);
+  if (finalize) load_vec<4>(bv, bias + f0);
+
+  auto item_of = [&](int t) {
+    const int i = t * GR + g;
+    gasfm_work_item w{-1, 0, 0, -1};
+    if (t < ntasks && i < n_items) w = items[i];
+    return w;
+  };
+  auto wave_max_len = [&](const gasfm_work_item& w) {
+    int l = w.end - w.begin;
+    l = max(l, __shfl_xor(l, 8));
+    l = max(l, __shfl_xor(l, 16));
+    l = max(l, __shfl_xor(l, 32));
+    return __builtin_amdgcn_readfirstlane(l);
+  };
+  auto issue = [&](const gasfm_work_item& w, int k, float (&x)[U][4]) {
+    const int64_t base = w.begin < w.end ? w.begin : 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = int64_t(w.begin) + k + u;
+      load_vec<4>(x[u], XL + (r < w.end ? r : base) * ldXL + f0);
+    }
+  };
+
+  int t = wave_id_uniform();
+  if (t >= ntasks) return;
+  gasfm_work_item w = item_of(t);
+  int L = wave_max_len(w);
+  float xr[4] = {0.f, 0.f, 0.f, 0.f}, nx[U][4];
+  if (w.seg >= 0) load_vec<4>(xr, XR + int64_t(w.seg) * ldXR + f0);
+  if (L > 0) issue(w, 0, nx);
+  for (; t < ntasks; t += nwaves) {
+    const gasfm_work_item wn = item_of(t + nwaves);  // consumed at this task's last iteration
+    int Ln = 0;
+    float xrn[4] = {0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, ssum = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
+    const int len = w.end - w.begin;
+    for (int k = 0; k < L; k += U) {
+      float xl[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) xl[u][v] = nx[u][v];
+      if (k + U < L) {
+        issue(w, k + U, nx);
+      } else {  // last iteration of this task: start the next one
+        Ln = wave_max_len(wn);
+        if (wn.seg >= 0) load_vec<4>(xrn, XR + int64_t(wn.seg) * ldXR + f0);
+        if (Ln > 0) issue(wn, 0, nx);
+      }
+      float lg[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float p = 0.f;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) p = fmaf(leaky(xl[u][v] + xr[v], slope), attv[v], p);
+        p += xor_lane<1>(p);  // the 2 lanes of a head
+        lg[u] = (k + u < len) ? p : -INFINITY;
+      }
+      float cm = lg[0];
+#pragma unroll
+      for (int u = 1; u < U; ++u) cm = fmaxf(cm, lg[u]);
+      const float mn = fmaxf(m, cm);
+      const float f = safe_scale(m, mn);
+      ssum *= f;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[v] *= f;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float pe = (lg[u] == -INFINITY) ? 0.f : __expf(lg[u] - mn);
+        ssum += pe;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[v] = fmaf(pe, xl[u][v], acc[v]);
+      }
+      m = mn;
+    }
+    if (L == 0) {  // every item of the task empty: the next task was not started above
+      Ln = wave_max_len(wn);
+      if (wn.seg >= 0) load_vec<4>(xrn, XR + int64_t(wn.seg) * ldXR + f0);
+      if (Ln > 0) issue(wn, 0, nx);
+    }
+    if (w.seg >= 0) {
+      const bool head_leader = (li & 1) == 0;
+      if (w.slot < 0) {
+        float o[4];
+        const float inv = 1.f / (ssum + 1e-16f);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) o[v] = finalize ? fmaf(acc[v], inv, bv[v]) : acc[v];
+        store_vec<4>(out + int64_t(w.seg) * ldOut + f0, o);
+        if (head_leader) {
+          seg_max[int64_t(w.seg) * ldStat + h] = m;
+          seg_sum[int64_t(w.seg) * ldStat + h] = ssum;
+        }
+      } else {
+        float* pr = part + int64_t(w.slot) * LDP;
+        store_vec<4>(pr + f0, acc);
+        if (head_leader) {
+          pr[HC + h] = m;
+          pr[HC + H + h] = ssum;
+        }
+      }
+    }
+    w = wn;
+    L = Ln;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) xr[v] = xrn[v];
+  }
+}
+
 // Ordered merge of partial states.  One workgroup per combine entry; rows of
 // the workgroup take slots k = row, row + R, ... in order and the row states
 // are merged in row order (first within a wave, then across waves via LDS),
@@ -1025,6 +1158,18 @@ static bool glds_enabled() {
   return on;
 }
 
+// Grouped-item forward (attn_fwd_grp_kernel<U, MINW>) for streamed 32-wide convs: GASFM_ATTN_GRP
+// = 4 / 8 (U rows per lane per iteration), 46 / 48 (U = 4 at >= 6 / 8 waves per SIMD), 0 = off
+// (direct-to-LDS kernel).
+static int grp_rows() {
+  static const int u = [] {
+    const char* e = std::getenv("GASFM_ATTN_GRP");
+    const int v = e ? std::atoi(e) : 4;
+    return (v == 8 || v == 4 || v == 46 || v == 48) ? v : 0;
+  }();
+  return u;
+}
+
 static int grid_for(int n_items, int resident) {
   int waves = n_items > 0 ? n_items : 1;
   const int cap = env_wave_cap() ? env_wave_cap() : resident * (kBlock / kWave);
@@ -1064,7 +1209,25 @@ extern "C" int gasfm_gat_attn_fwd(const float* XL, int64_t ldXL, const float* XR
                       aligned16(XL) && aligned16(XR) && aligned16(out) && aligned16(att) &&
                       aligned16(bias) && (!part || aligned16(part)) && ((H * C + 2 * H) % 4 == 0);
   bool done = false;
-  if (vec_ok && perm == nullptr && H * C == 32 && C == 8 && glds_enabled()) {
+  const int grp = grp_rows();
+  if (vec_ok && perm == nullptr && H * C == 32 && C == 8 && grp > 0) {
+    auto launch = [&](auto kern) {
+      const int tasks = (n_items + 7) / 8;
+      const int grid = grid_for(tasks, resident_blocks(reinterpret_cast<const void*>(kern), kBlock, 0));
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att, bias, items, n_items,
+                         slope, finalize, out, ldOut, seg_max, seg_sum, ldStat, part);
+    };
+    if (grp == 8)
+      launch(&attn_fwd_grp_kernel<8, 1>);
+    else if (grp == 46)
+      launch(&attn_fwd_grp_kernel<4, 6>);
+    else if (grp == 48)
+      launch(&attn_fwd_grp_kernel<4, 8>);
+    else
+      launch(&attn_fwd_grp_kernel<4, 1>);
+    done = true;
+  }
+  if (!done && vec_ok && perm == nullptr && H * C == 32 && C == 8 && glds_enabled()) {
     using G = Geom<32, 8>;
     const int grid =
         grid_for(n_items, resident_blocks(reinterpret_cast<const void*>(&attn_fwd_glds_kernel<G>), kBlock, 0));
