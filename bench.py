@@ -101,6 +101,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from Python (no hipGraph)")
     ap.add_argument("--cpu-sample-scale", type=float, default=0.1)
+    ap.add_argument("--proj-precision", choices=("fp32", "bf16"), default="fp32",
+                    help="bf16: the camera-side 1024x1024 projections on the bf16 MFMA kernel (BASELINE config 5)")
     ap.add_argument("--dist", action="store_true",
                     help="run the point-sharded RCCL path even at one rank (under torchrun --nproc-per-node 1)")
     args = ap.parse_args()
@@ -125,7 +127,7 @@ def main():
     E = sc.num_edges
     conf = gasfm_amd.learning_conf(num_layers=args.layers)
     torch.manual_seed(0)
-    net = gasfm_amd.GraphAttnSfMNet(conf)
+    net = gasfm_amd.GraphAttnSfMNet(conf).set_projection_precision(args.proj_precision)
     if dist_on:
         from gasfm_amd import distributed as gdist
         data = gdist.shard_scene(sc, rank, world).to(dev)
@@ -224,11 +226,13 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "fp32" if args.proj_precision == "fp32" else "bf16-proj",
             "data": "synthetic (config 4 generator: SfM-like windowed visibility, default_rng(4)); random-init "
                     "weights of the learning_euc GASFM architecture",
             "config": {"workload": f"config 4: m={sc.m} cameras, n={sc.n} points, E={E} projections, "
-                                   f"{args.layers}-block GraphAttnSfMNet (learning_euc widths) fwd+bwd",
+                                   f"{args.layers}-block GraphAttnSfMNet (learning_euc widths) fwd+bwd"
+                                   + ("" if args.proj_precision == "fp32" else
+                                      ", camera-side 1024x1024 projections in bf16 on MFMA (fp32 accumulate)"),
                        "cameras": sc.m, "points": sc.n, "edges": E, "blocks": args.layers,
                        "parallelism": f"point-sharded x{world}" if dist_on else "single GPU"},
             "roofline": {"kernel": "attn_fwd_grp_kernel<4,1> point direction (proj2scenepoint), per launch",

@@ -382,7 +382,7 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         if hubs:
             hv = view_block.hub_params(pfu, vsg.graph_conv_view2global, nxt.proj2view)
             if hv is not None and view_block._rows_ok(view, view.shape[1]):
-                skip, SV, XLv, XRn = view_block.hub(view, hv)
+                skip, SV, XLv, XRn = view_block.hub(view, hv, getattr(self, "_proj_bf16", False))
                 carry.update(XRc=XRn, view_skip=skip, SV=SV, XLv2g=XLv)
         pts = sp.tail(agg_p, prev_pt, sec=sec)
         if hp is not None and point_block._rows_ok(pts, point_block.P_W):
@@ -700,6 +700,9 @@ class GraphAttnSfMNet(Module):
         if batchnorm:
             raise NotImplementedError()
         n_feat_depth = conf.get_int("model.depth_head.n_feat") if self.depth_head_enabled else None
+        # not a reference key: "bf16" runs the m x 1024 x 1024 camera-side GEMMs on the bf16 MFMA
+        # kernel (BASELINE config 5); parameters and every other op stay fp32
+        self._projection_precision = conf.get_string("model.projection_precision", default="fp32")
 
         self.embed = EmbeddingLayer(pos_emb_n_freq, 2, post_embed_proj_dim=-1)
         d_emb = self.embed.d_out
@@ -733,6 +736,19 @@ class GraphAttnSfMNet(Module):
         if self.scenepoint_head_enabled:
             nh = conf.get_int("model.scenepoint_head.n_hidden_layers")
             self.scenepoint_head = get_linear_layers((1 + nh) * [n_feat_sp] + [3], norm=False)
+
+        self.set_projection_precision(self._projection_precision)
+
+    def set_projection_precision(self, precision):
+        """"fp32" (default: the reference's precision) or "bf16": the camera-side D x D products
+        (Proj2View's MLP, graph_conv_view2global.lin_l; layers.py:292-320, 352-358, 506-511) in
+        bf16 on MFMA with fp32 accumulation, forward and backward (BASELINE config 5)."""
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"projection precision {precision!r}: expected 'fp32' or 'bf16'")
+        self._projection_precision = precision
+        for mod in self.modules():
+            mod._proj_bf16 = precision == "bf16"
+        return self
 
     # ------------------------------------------------------------------ forward
     def edge_index_for(self, data, device):

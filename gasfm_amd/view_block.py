@@ -9,9 +9,12 @@ ViewHubFn  -- every consumer of the block's view features, as PointHubFn does fo
               graph_conv_view2global.lin_l (addmm).  Its backward is the only producer of d view:
               addmm(d skip, dXL, W_l) then one kernel adding both LayerNorm branches in place.
 
-The two D x D GEMMs of the camera side (m = 1000 rows, D = 1024) stay on hipBLASLt through
-torch; everything around them -- LayerNorms, ReLUs, the 32-wide projections, residual adds,
-bias / LayerNorm-affine gradient reductions -- runs in the four kernels.
+The two D x D GEMMs of the camera side (m = 1000 rows, D = 1024) run on hipBLASLt through torch
+in fp32, or -- BASELINE config 5's "bf16 projections on MFMA", ``bf16=True`` -- on the hand-written
+bf16 MFMA kernel (csrc/gemm_bf16.hip: operands rounded to bf16, fp32 accumulation, bias / skip
+fused), forward and both backward products.  Everything around them -- LayerNorms, ReLUs, the
+32-wide projections, residual adds, bias / LayerNorm-affine gradient reductions -- runs in the
+four kernels.
 """
 import torch
 
@@ -26,9 +29,18 @@ def _f32(*shape, like):
     return torch.empty(shape, dtype=torch.float32, device=like.device)
 
 
+def _mm(a, b, cin=None, bias=None, bf16=False):
+    """a @ b (+ cin) (+ bias): bf16 MFMA kernel or fp32 hipBLASLt."""
+    if bf16:
+        return _native.gemm_bf16(a, b, cin=cin, bias=bias)
+    if cin is not None:
+        return torch.addmm(cin if bias is None else cin + bias, a, b)
+    return torch.addmm(bias, a, b) if bias is not None else a @ b
+
+
 class ViewTailFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, prev, agg, Wp, bp, ln_w, ln_b, Wm, bm, eps):
+    def forward(ctx, prev, agg, Wp, bp, ln_w, ln_b, Wm, bm, eps, bf16=False):
         agg = agg.contiguous()
         prev = prev.contiguous() if prev is not None else None
         Wp, Wm = Wp.contiguous(), Wm.contiguous()
@@ -37,9 +49,9 @@ class ViewTailFn(torch.autograd.Function):
         rs = _f32(m, 2, like=agg)
         _native.view_tail_fwd(prev, agg, Wp, bp, ln_w, ln_b, eps, bm, x, xb, h, rs,
                               _native.view_scratch(m, D, agg.device))
-        view = torch.addmm(xb, h, Wm.t())
+        view = _mm(h, Wm.t(), cin=xb, bf16=bf16)
         ctx.save_for_backward(agg, x, rs, h, Wp, ln_w, ln_b, Wm)
-        ctx.eps, ctx.has_prev = eps, prev is not None
+        ctx.eps, ctx.has_prev, ctx.bf16 = eps, prev is not None, bf16
         ctx.defer = _native.defer_token(Wp, bp, ln_w, ln_b, bm)
         return view
 
@@ -48,8 +60,8 @@ class ViewTailFn(torch.autograd.Function):
         agg, x, rs, h, Wp, ln_w, ln_b, Wm = ctx.saved_tensors
         m, D = x.shape
         dview = dview.contiguous()
-        dh = dview @ Wm
-        dWm = dview.t() @ h
+        dh = _mm(dview, Wm, bf16=ctx.bf16)
+        dWm = _mm(dview.t(), h, bf16=ctx.bf16)
         dx, dagg = _f32(m, D, like=x), _f32(m, A_W, like=x)
         cols = _native.view_tail_part_cols(D)
         if m == 0:
@@ -61,14 +73,14 @@ class ViewTailFn(torch.autograd.Function):
             tot = _native.param_colsum(part, ctx.defer)
         dWp = tot[:D * A_W].view(D, A_W)
         dbp, dg, dbt, dbm = (tot[D * A_W + k * D:D * A_W + (k + 1) * D] for k in range(4))
-        return (dx if ctx.has_prev else None), dagg, dWp, dbp, dg, dbt, dWm, dbm, None
+        return (dx if ctx.has_prev else None), dagg, dWp, dbp, dg, dbt, dWm, dbm, None, None
 
 
 class ViewHubFn(torch.autograd.Function):
     """v -> (skip, SV, XL, XR)."""
 
     @staticmethod
-    def forward(ctx, v, gC, bC, Wv, Wl, bl, gA, bA, Wa, ba, Wr, br, eps):
+    def forward(ctx, v, gC, bC, Wv, Wl, bl, gA, bA, Wa, ba, Wr, br, eps, bf16=False):
         v = v.contiguous()
         Wv, Wl, Wa, Wr = (w.contiguous() for w in (Wv, Wl, Wa, Wr))
         m = v.shape[0]
@@ -76,9 +88,9 @@ class ViewHubFn(torch.autograd.Function):
         rs = _f32(m, 2, like=v)
         _native.view_hub_fwd(v, eps, gC, bC, Wv, gA, bA, Wa, ba, Wr, br, SV, t, XR, rs,
                              _native.view_scratch(m, v.shape[1], v.device))
-        XL = torch.addmm(bl, v, Wl.t())
+        XL = _mm(v, Wl.t(), bias=bl, bf16=bf16)
         ctx.save_for_backward(v, rs, t, gC, bC, Wv, Wl, gA, bA, Wa, Wr)
-        ctx.eps = eps
+        ctx.eps, ctx.bf16 = eps, bf16
         ctx.defer = _native.defer_token(gC, bC, Wv, gA, bA, Wa, ba, Wr, br, bl)
         ctx.set_materialize_grads(False)
         return v.view_as(v), SV, XL, XR
@@ -91,8 +103,8 @@ class ViewHubFn(torch.autograd.Function):
         dSV = dSV.contiguous() if dSV is not None else zeros(A_W)
         dXR = dXR.contiguous() if dXR is not None else zeros(A_W)
         dXL = dXL.contiguous() if dXL is not None else zeros(D)
-        dacc = torch.addmm(dskip, dXL, Wl) if dskip is not None else dXL @ Wl
-        dWl = dXL.t() @ v
+        dacc = _mm(dXL, Wl, cin=dskip, bf16=ctx.bf16)
+        dWl = _mm(dXL.t(), v, bf16=ctx.bf16)
         cols = _native.view_hub_part_cols(D)
         if m == 0:
             tot = torch.zeros(cols, dtype=torch.float32, device=v.device)
@@ -111,7 +123,7 @@ class ViewHubFn(torch.autograd.Function):
         dWr = tot[o:o + A_W * A_W].view(A_W, A_W)
         o += A_W * A_W
         dba, dbr = tot[o:o + A_W], tot[o + A_W:o + 2 * A_W]
-        return dacc, dgC, dbC, dWv, dWl, dbl, dgA, dbA, dWa, dba, dWr, dbr, None
+        return dacc, dgC, dbC, dWv, dWl, dbl, dgA, dbA, dWa, dba, dWr, dbr, None, None
 
 
 def _is_ln(mod, w):
@@ -142,7 +154,8 @@ def tail_fusable(agg_mod, x, prev):
 def tail(agg_mod, x, prev):
     proj = getattr(agg_mod, agg_mod._proj_key)
     ln, lin = agg_mod.norm_pre_mlp, agg_mod.mlp[0]
-    return ViewTailFn.apply(prev, x, proj.weight, proj.bias, ln.weight, ln.bias, lin.weight, lin.bias, ln.eps)
+    return ViewTailFn.apply(prev, x, proj.weight, proj.bias, ln.weight, ln.bias, lin.weight, lin.bias, ln.eps,
+                            getattr(agg_mod, "_proj_bf16", False))
 
 
 def hub_params(pfu, v2g_conv, nxt):
@@ -165,5 +178,5 @@ def hub_params(pfu, v2g_conv, nxt):
             linR.weight, linR.bias, lnC.eps)
 
 
-def hub(v, params):
-    return ViewHubFn.apply(v, *params)
+def hub(v, params, bf16=False):
+    return ViewHubFn.apply(v, *params, bf16)

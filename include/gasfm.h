@@ -483,6 +483,18 @@ int gasfm_scene_homography(const float* M, int64_t ldM, int32_t m, int32_t n, co
  * feeds every block's projection update, layers.py:245-251; autograd would add n-1 times). */
 int gasfm_sum_n(int32_t n, const float* const* src, int64_t count, float* dst, void* stream);
 
+/* bf16 MFMA GEMM with fp32 operands and result (BASELINE config 5's "bf16 projections on MFMA";
+ * replaces the m x 1024 x 1024 Linear products of Proj2View's MLP and graph_conv_view2global.lin_l,
+ * code/models/layers.py:292-320, 352-358, 506-511, forward and both backward products):
+ *   C[M,N] = A[M,K] . B[K,N] (+ Cin[M,N]) (+ bias[N]),  A(i,k) = A[i*sAm + k*sAk],
+ *   B(k,j) = B[k*sBk + j*sBn].  Operands are rounded to bf16 (nearest even) on the way into LDS,
+ * multiplied exactly and accumulated in fp32.  One of sAm / sAk and one of sBk / sBn must be 1;
+ * the extent along the unit stride and the other stride are multiples of 4, A and B 16-byte
+ * aligned.  C may alias Cin (same ld); it may not alias A or B. */
+int gasfm_gemm_bf16(int32_t M, int32_t N, int32_t K, const float* A, int64_t sAm, int64_t sAk,
+                    const float* B, int64_t sBk, int64_t sBn, const float* Cin, int64_t ldCin,
+                    const float* bias, float* C, int64_t ldC, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
