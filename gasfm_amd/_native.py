@@ -88,6 +88,10 @@ _SIGS = {
     "gasfm_scene_emit": (_i32, [_vp, _i64, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_scene_point_csr": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp]),
     "gasfm_scene_homography": (_i32, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "gasfm_outlier_counts": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp]),
+    "gasfm_outlier_mark": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp]),
+    "gasfm_outlier_moments": (_i32, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_outlier_apply": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     "gasfm_sum_n": (_i32, [_i32, _vp, _i64, _vp, _vp]),
     "gasfm_esfm_fwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _vp, _vp]),
     "gasfm_esfm_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _i32, _i32,
@@ -754,6 +758,74 @@ def scan_i32(x):
     out = torch.empty(x.shape[0] + 1, dtype=torch.int32, device=x.device)
     check(lib().gasfm_scan_i32(_p(x), x.shape[0], _p(out), _stream(x)), "gasfm_scan_i32")
     return out
+
+
+# ---------------------------------------------------------------- outlier injection (outliers.hip)
+def _dev_check(what, *ts):
+    for name, t, dt in ts:
+        if t is not None and (not t.is_cuda or t.dtype != dt or not t.is_contiguous()):
+            raise TypeError(f"{what}: {name} must be a contiguous {dt} CUDA tensor")
+
+
+def outlier_counts(state, cam_ptr, pt_ptr, perm, m, n):
+    """Inliers per view / per point and their minima: (cam_in [m], pt_in [n], mins [2]) int32."""
+    _dev_check("outlier_counts", ("state", state, torch.uint8), ("cam_ptr", cam_ptr, torch.int32),
+               ("pt_ptr", pt_ptr, torch.int32), ("perm", perm, torch.int32))
+    if cam_ptr.shape[0] != m + 1 or pt_ptr.shape[0] != n + 1:
+        raise ValueError("outlier_counts: cam_ptr / pt_ptr must have m + 1 / n + 1 entries")
+    dev = state.device
+    cam_in = torch.empty(m, dtype=torch.int32, device=dev)
+    pt_in = torch.empty(n, dtype=torch.int32, device=dev)
+    mins = torch.empty(2, dtype=torch.int32, device=dev)
+    check(lib().gasfm_outlier_counts(_p(state), _p(cam_ptr), _p(pt_ptr), _p(perm), m, n, _p(cam_in), _p(pt_in),
+                                     _p(mins), _stream(state)), "gasfm_outlier_counts")
+    return cam_in, pt_in, mins
+
+
+def outlier_mark(state, cam, pt, cam_in, pt_in, mode, counts=None):
+    """init (mode 0) / blacklist (mode 1) pass over the edge classes; returns counts [4] int32."""
+    _dev_check("outlier_mark", ("state", state, torch.uint8), ("cam", cam, torch.int64), ("pt", pt, torch.int64),
+               ("cam_in", cam_in, torch.int32), ("pt_in", pt_in, torch.int32))
+    E = state.shape[0]
+    if cam.shape[0] != E or pt.shape[0] != E:
+        raise ValueError("outlier_mark: cam / pt must have one entry per edge")
+    if counts is None:
+        counts = torch.empty(4, dtype=torch.int32, device=state.device)
+    check(lib().gasfm_outlier_mark(_p(state), _p(cam), _p(pt), _p(cam_in), _p(pt_in), E, mode, _p(counts),
+                                   _stream(state)), "gasfm_outlier_mark")
+    return counts
+
+
+def outlier_moments(values, state, cam_ptr, m):
+    """(mu [m, 2], sigma [m, 2, 2], scale_tril [m, 2, 2], pivots [m, 2] int32) of the inliers."""
+    _dev_check("outlier_moments", ("values", values, torch.float32), ("state", state, torch.uint8),
+               ("cam_ptr", cam_ptr, torch.int32))
+    if values.dim() != 2 or values.shape[1] != 2 or values.shape[0] != state.shape[0] or cam_ptr.shape[0] != m + 1:
+        raise ValueError("outlier_moments: values [E, 2], state [E], cam_ptr [m + 1]")
+    dev = values.device
+    mu = torch.empty((m, 2), dtype=torch.float32, device=dev)
+    sigma = torch.empty((m, 2, 2), dtype=torch.float32, device=dev)
+    tril = torch.empty((m, 2, 2), dtype=torch.float32, device=dev)
+    piv = torch.empty((m, 2), dtype=torch.int32, device=dev)
+    check(lib().gasfm_outlier_moments(_p(values), _p(state), _p(cam_ptr), m, _p(mu), _p(sigma), _p(tril), _p(piv),
+                                      _stream(values)), "gasfm_outlier_moments")
+    return mu, sigma, tril, piv
+
+
+def outlier_apply(idx, cam, pt, z, mu, tril, M, pix=None):
+    """Write mu[cam] + scale_tril[cam] z[k] for the outlier edges idx (ascending) into M (and pix)."""
+    _dev_check("outlier_apply", ("idx", idx, torch.int64), ("cam", cam, torch.int64), ("pt", pt, torch.int64),
+               ("z", z, torch.float32), ("mu", mu, torch.float32), ("scale_tril", tril, torch.float32),
+               ("pix", pix, torch.float32))
+    _check_M(M, "outlier_apply")
+    k = idx.shape[0]
+    if z.numel() != 2 * k:
+        raise ValueError(f"outlier_apply: z has {z.numel()} values for {k} outliers")
+    m = M.shape[0] // 2
+    if mu.shape != (m, 2) or tril.shape != (m, 2, 2):
+        raise ValueError("outlier_apply: mu [m, 2], scale_tril [m, 2, 2]")
+    check(lib().gasfm_outlier_apply(_p(idx), k, _p(cam), _p(pt), _p(z), _p(mu), _p(tril), _p(M), M.stride(0),
+                                    _p(pix), _stream(M)), "gasfm_outlier_apply")
 
 
 def _check_M(M, what):

@@ -495,6 +495,41 @@ int gasfm_gemm_bf16(int32_t M, int32_t N, int32_t K, const float* A, int64_t sAm
                     const float* B, int64_t sBk, int64_t sBn, const float* Cin, int64_t ldCin,
                     const float* bias, float* C, int64_t ldC, void* stream);
 
+/* ---- outlier injection (outliers.hip) -----------------------------------
+ * Replaces OutlierInjector / inject_outliers (code/utils/dataset_utils.py:159-461), the per-sample
+ * transform of the outlier-injected training loop (train.py:73-81, BASELINE config 5).  The
+ * partition of the E projections (camera-major M2sparse order) is one byte per edge:
+ * 0 fixed inlier, 1 fixed outlier, 2 free inlier, 3 free outlier (bit 0 = outlier).  The random
+ * choices between the passes are the caller's (the reference's numpy draws). */
+
+/* Inliers per view (cam_in [m], segments cam_ptr [m+1]) and per point (pt_in [n], CSR pt_ptr
+ * [n+1] with perm slot -> edge, NULL = identity); mins[0] / mins[1] = their minima. */
+int gasfm_outlier_counts(const uint8_t* state, const int32_t* cam_ptr, const int32_t* pt_ptr,
+                         const int32_t* perm, int32_t m, int32_t n, int32_t* cam_in, int32_t* pt_in,
+                         int32_t* mins, void* stream);
+
+/* mode 0 (init_fixed_inliers_and_outliers, :253-275): state = 0 where pt_in[pt] < 3 or
+ * cam_in[cam] < 9, else 2 (cam_in / pt_in = all projections).  mode 1
+ * (blacklist_problematic_outliers, :307-320): a free outlier whose point has < 2 or whose view
+ * has < 8 remaining inliers (cam_in / pt_in from gasfm_outlier_counts) becomes 0.
+ * counts[0..3] = edges per class afterwards. */
+int gasfm_outlier_mark(uint8_t* state, const int64_t* cam, const int64_t* pt, const int32_t* cam_in,
+                       const int32_t* pt_in, int64_t E, int32_t mode, int32_t* counts, void* stream);
+
+/* Per view over the inliers of the pixel values [E x 2] (sparse_moment_estimation,
+ * sparse_utils.py:151-165): mu [m x 2], sigma [m x 2 x 2] = sum x x^T / (N - 1), and
+ * scale_tril [m x 2 x 2] with sigma = T T^T from the LDL^T factorisation of LAPACK sytf2
+ * (lower, Bunch-Kaufman; pivots [m x 2] as torch.linalg.ldl_factor reports them, negative =
+ * 2x2 block, then scale_tril is NaN) with the reference's row flip (:378-392). */
+int gasfm_outlier_moments(const float* values, const uint8_t* state, const int32_t* cam_ptr, int32_t m,
+                          float* mu, float* sigma, float* scale_tril, int32_t* pivots, void* stream);
+
+/* Outlier k (edge idx[k], ascending): value = mu[cam] + scale_tril[cam] z[k] (z [n_out x 2]),
+ * written into the dense pixel matrix M [2m x ldM] and, if pix != NULL, pix [E x 2] (:397-433). */
+int gasfm_outlier_apply(const int64_t* idx, int64_t n_out, const int64_t* cam, const int64_t* pt,
+                        const float* z, const float* mu, const float* scale_tril, float* M, int64_t ldM,
+                        float* pix, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
