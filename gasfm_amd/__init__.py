@@ -10,9 +10,10 @@ from .conf import Conf, learning_conf, optim_conf  # noqa: F401
 from .gatv2 import GATv2Conv  # noqa: F401
 from .loss import ESFMLoss  # noqa: F401
 from .model import GraphAttnSfMNet  # noqa: F401
+from .ba import euc_ba, proj_ba  # noqa: F401
 from .outliers import OutlierInjector, inject_outliers  # noqa: F401
 from .scene import AxialAggregationGraphWrapper, SceneData, SparseMat, M2sparse  # noqa: F401
 
 __all__ = ["AttnPlan", "gat_attention", "Conf", "learning_conf", "optim_conf", "GATv2Conv", "ESFMLoss", "GraphAttnSfMNet",
            "AxialAggregationGraphWrapper", "SceneData", "SparseMat", "M2sparse",
-           "OutlierInjector", "inject_outliers"]
+           "OutlierInjector", "inject_outliers", "euc_ba", "proj_ba"]

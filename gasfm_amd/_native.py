@@ -92,6 +92,17 @@ _SIGS = {
     "gasfm_outlier_mark": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp]),
     "gasfm_outlier_moments": (_i32, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_outlier_apply": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
+    "gasfm_ba_partials": (_i64, [_i64]),
+    "gasfm_ba_eval": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _vp,
+                             _vp]),
+    "gasfm_ba_sum": (_i32, [_vp, _i64, _vp, _vp]),
+    "gasfm_ba_normals": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_ba_damp": (_i32, [_i32, _i32, _i32, _vp, _vp, ctypes.c_double, _vp, _vp, _vp, _vp]),
+    "gasfm_ba_schur": (_i32, [_i32, _i32, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp,
+                              _vp, _vp, _vp, _vp]),
+    "gasfm_ba_backsub": (_i32, [_i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_ba_model": (_i32, [_i32, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_ba_dlt": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_sum_n": (_i32, [_i32, _vp, _i64, _vp, _vp]),
     "gasfm_esfm_fwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _vp, _vp]),
     "gasfm_esfm_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _i32, _i32,

@@ -120,3 +120,36 @@ def config4(m=1000, n=200_000, seed=4):
 def scaled_config4(scale, seed=4):
     """config 4 with m and n scaled by `scale` (parity tests at oracle-friendly sizes)."""
     return windowed_scene(max(16, int(1000 * scale)), max(64, int(200_000 * scale)), seed=seed)
+
+
+def rotation_look_at(center, target=np.zeros(3), up=np.array([0.0, 0.0, 1.0])):
+    """Camera-to-world orientation R (columns: camera x, y, z axes in world coordinates) of a camera
+    at ``center`` looking at ``target``; P = K R^T [I | -center] (geo_utils.get_camera_matrix)."""
+    z = target - center
+    z = z / np.linalg.norm(z)
+    x = np.cross(z, up)
+    x = x / np.linalg.norm(x)
+    y = np.cross(z, x)
+    return np.stack([x, y, z], axis=1)
+
+
+def ba_scene(m, n, views_per_point, noise_px=0.0, seed=0, radius=4.0, f=800.0):
+    """Bundle-adjustment test scene (BASELINE config-4 style windowed visibility): m cameras on a
+    circle of ``radius`` looking at points uniform in [-1, 1]^3, point j seen by
+    ``views_per_point`` consecutive cameras; returns dict(xs [m, n, 2] pixels (0 = unseen),
+    Rs, ts (camera centres), Ks, Xs [n, 3]) -- the euc_ba inputs (ba_functions.py:6)."""
+    rng = np.random.default_rng(seed)
+    ang = np.linspace(0, 2 * np.pi, m, endpoint=False)
+    ts = np.stack([radius * np.cos(ang), radius * np.sin(ang), 0.3 * rng.standard_normal(m)], 1)
+    Rs = np.stack([rotation_look_at(c) for c in ts])
+    Ks = np.repeat(np.array([[f, 0.0, 500.0], [0.0, f, 500.0], [0.0, 0.0, 1.0]])[None], m, axis=0)
+    Xs = rng.uniform(-1, 1, size=(n, 3))
+    xs = np.zeros((m, n, 2))
+    start = rng.integers(0, m, size=n)
+    j = np.repeat(np.arange(n), views_per_point)
+    c = (np.repeat(start, views_per_point) + np.tile(np.arange(views_per_point), n)) % m
+    q = np.einsum("eij,ej->ei", Ks[c] @ Rs[c].transpose(0, 2, 1), Xs[j] - ts[c])
+    xs[c, j] = q[:, :2] / q[:, 2:3]
+    if noise_px:
+        xs[c, j] += noise_px * rng.standard_normal((c.shape[0], 2))
+    return {"xs": xs, "Rs": Rs, "ts": ts, "Ks": Ks, "Xs": Xs}

@@ -530,6 +530,55 @@ int gasfm_outlier_apply(const int64_t* idx, int64_t n_out, const int64_t* cam, c
                         const float* z, const float* mu, const float* scale_tril, float* M, int64_t ldM,
                         float* pix, void* stream);
 
+/* ---- bundle adjustment (bundle_adjust.hip) --------------------------------
+ * The reference's Ceres problem (bundle_adjustment/custom_cpp_cost_functions.cpp:56-222; driven by
+ * code/utils/ba_functions.py:6-137 / ceres_utils.py:127-245) as device passes of a trust-region
+ * Levenberg-Marquardt with the points eliminated (DENSE_SCHUR), fp64.  cp = 6: Euclidean camera
+ * deltas (angle-axis, t) with cam0 [m x 6] and K [m x 5] (K00 K01 K02 K11 K12); cp = 12:
+ * projective P deltas (column-major 3 x 4), K unused.  Edges are camera-major (cam_ptr [m+1]);
+ * the point CSR (pt_ptr [n+1], perm slot -> edge, NULL = identity) lists cameras ascending.
+ * Huber(0.1) enters through Ceres' corrector (residual and Jacobian scaled by sqrt(rho')). */
+int64_t gasfm_ba_partials(int64_t E);  /* per-workgroup partial count of eval / model */
+
+/* cost partials (1/2 rho per edge, summed per workgroup) at (cam0 + dcam, X0 + dX); with jac:
+ * corrected residuals fres [E x 2] and Jacobians Jc [E x 2 x cp], Jp [E x 2 x 3], columns
+ * scaled by sc [m x cp] / sp [n x 3] (NULL = 1). */
+int gasfm_ba_eval(int32_t cp, const double* cam0, const double* K, const double* X0, const double* dcam,
+                  const double* dX, const int32_t* cidx, const int32_t* pidx, const double* obs, int64_t E,
+                  const double* sc, const double* sp, int32_t jac, double* fres, double* Jc, double* Jp,
+                  double* part, void* stream);
+/* out[0] = sum of part[0..count) in a fixed order (one workgroup). */
+int gasfm_ba_sum(const double* part, int64_t count, double* out, void* stream);
+/* U [m x cp x cp] = Jc^T Jc and gc [m x cp] = Jc^T f per camera; V [n x 3 x 3], gp [n x 3] per point. */
+int gasfm_ba_normals(int32_t cp, int32_t m, int32_t n, const int32_t* cam_ptr, const int32_t* pt_ptr,
+                     const int32_t* perm, const double* fres, const double* Jc, const double* Jp, double* U,
+                     double* gc, double* V, double* gp, void* stream);
+/* LM damping: Ud = U + clamp(diag U, 1e-6, 1e32) / radius; Vinv = (V + same)^-1; *bad = 1 if a point
+ * block is not positive definite (the caller zeroes *bad). */
+int gasfm_ba_damp(int32_t cp, int32_t m, int32_t n, const double* U, const double* V, double radius,
+                  double* Ud, double* Vinv, int32_t* bad, void* stream);
+/* Reduced camera system: Y [E x cp x 3] workspace, S [(m cp) x (m cp)] dense row-major, rhs [m cp].
+ * Camera-pair blocks (a <= b) blk_ab [nblk x 2] with pair ranges blk_ptr [nblk+1] into the edge
+ * pairs (pe1 [P] on camera a, pe2 [P] on camera b, same point). */
+int gasfm_ba_schur(int32_t cp, int32_t m, const int32_t* cam_ptr, const int32_t* cidx, const int32_t* pidx,
+                   int64_t E, const double* Jc, const double* Jp, const double* Vinv, const double* gc,
+                   const double* gp, const double* Ud, const int32_t* blk_ptr, const int32_t* blk_ab,
+                   int64_t nblk, const int32_t* pe1, const int32_t* pe2, double* Y, double* S, double* rhs,
+                   void* stream);
+/* dp [n x 3] = Vinv (-gp - sum_e W_e^T dc[cam]) for the camera step dc [m x cp]. */
+int gasfm_ba_backsub(int32_t cp, int32_t n, const int32_t* pt_ptr, const int32_t* perm, const int32_t* cidx,
+                     const double* Jc, const double* Jp, const double* Vinv, const double* gp, const double* dc,
+                     double* dp, void* stream);
+/* model cost change partials: -(mr . (f + mr / 2)), mr = Jc dc + Jp dp, per workgroup. */
+int gasfm_ba_model(int32_t cp, const int32_t* cidx, const int32_t* pidx, int64_t E, const double* Jc,
+                   const double* Jp, const double* fres, const double* dc, const double* dp, double* part,
+                   void* stream);
+/* DLT triangulation (geo_utils.dlt_triangulation, code/utils/geo_utils.py:611-656): X [n x 4],
+ * X[3] = 1, NaN for points in < 2 views; nP [m x 3 x 4] normalised cameras, nx [E x 2]
+ * normalised observations. */
+int gasfm_ba_dlt(int32_t n, const int32_t* pt_ptr, const int32_t* perm, const int32_t* cidx, const double* nP,
+                 const double* nx, double* X, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
