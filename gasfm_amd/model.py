@@ -846,11 +846,14 @@ class GraphAttnSfMNet(Module):
             elif self.normalize_output == "Frobenius":
                 Ps = Ps / Ps.norm(dim=(1, 2), p="fro", keepdim=True)
             return {"Ps_norm": Ps}
-        if self.rot_representation != "quat":
-            raise NotImplementedError("only the quaternion head (all GASFM confs) is implemented")
-        if x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.shape[1] == 7:
+        if self.rot_representation == "6d":
+            R = rotation_6d_to_matrix(x[:, :6])
+        elif self.rot_representation == "svd":
+            R = project_to_rot(x[:, :9].reshape(-1, 3, 3))
+        elif x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.shape[1] == 7:
             return {"Ps_norm": QuatPoseFn.apply(x)}
-        R = quaternion_to_matrix(x[:, :4])
+        else:
+            R = quaternion_to_matrix(x[:, :4])
         return {"Ps_norm": torch.cat((R, x[:, -3:].unsqueeze(-1)), dim=-1)}
 
 
@@ -872,6 +875,23 @@ class QuatPoseFn(torch.autograd.Function):
         dx = torch.empty((x.shape[0], 7), dtype=torch.float32, device=x.device)
         _native.pose_bwd(x, dP.contiguous(), dx)
         return dx
+
+
+def rotation_6d_to_matrix(d6):
+    """pytorch3d.transforms.rotation_6d_to_matrix (baseNet.py:43; published formula: Gram-Schmidt of
+    the two 3-vectors, rows b1, b2, b1 x b2)."""
+    a1, a2 = d6[..., :3], d6[..., 3:]
+    b1 = F.normalize(a1, dim=-1)
+    b2 = F.normalize(a2 - (b1 * a2).sum(-1, keepdim=True) * b1, dim=-1)
+    return torch.stack((b1, b2, torch.cross(b1, b2, dim=-1)), dim=-2)
+
+
+def project_to_rot(m):
+    """geo_utils.project_to_rot (code/utils/geo_utils.py:25-31): the nearest rotation U diag(1, 1, det) V^T."""
+    u, _, v = torch.svd(m)
+    vt = v.transpose(1, 2)
+    det = torch.det(u @ vt).view(-1, 1, 1)
+    return u @ torch.cat((vt[:, :2, :], vt[:, -1:, :] * det), 1)
 
 
 def quaternion_to_matrix(q):
