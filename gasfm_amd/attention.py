@@ -106,10 +106,15 @@ class AttnPlan:
         self.tag = None  # graph name (proj2view, proj2scenepoint, ...) for timing / logs
         self.pos = pos
         if pos is None and perm is not None and self.src_rows == self.num_edges:
-            p = perm.numpy() if isinstance(perm, torch.Tensor) else perm
-            pos = np.empty(self.num_edges, dtype=np.int32)
-            pos[p] = np.arange(self.num_edges, dtype=np.int32)
-            self.pos = torch.from_numpy(pos)
+            if isinstance(perm, torch.Tensor) and perm.device.type != "cpu":
+                pos = torch.empty(self.num_edges, dtype=torch.int32, device=perm.device)
+                pos[perm.long()] = torch.arange(self.num_edges, dtype=torch.int32, device=perm.device)
+                self.pos = pos
+            else:
+                p = perm.numpy() if isinstance(perm, torch.Tensor) else perm
+                pos = np.empty(self.num_edges, dtype=np.int32)
+                pos[p] = np.arange(self.num_edges, dtype=np.int32)
+                self.pos = torch.from_numpy(pos)
 
     # ------------------------------------------------------------------ construction
     @classmethod

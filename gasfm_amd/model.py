@@ -211,7 +211,7 @@ class ViewAndScenePoint2Global(Module):
         else:
             xv = dense.sequential(self.norm_and_proj_global2view, prev) if prev is not None else None
             xp = dense.sequential(self.norm_and_proj_global2scenepoint, prev) if prev is not None else None
-            XRv, XRp = _target_row(cv, xv, view), _target_row(c, xp, pts)
+            XRv, XRp = _target_row(cv, xv, view, plan_v2g.num_targets), _target_row(c, xp, pts, plan_s2g.num_targets)
         XLv = xl_view if xl_view is not None else dense.linear(view, cv.lin_l)
         v2g = gat_attention(XLv, XRv, cv.att, cv._bias(XLv), plan_v2g, cv.heads, cv.negative_slope)
         XLp = xl_pts if xl_pts is not None else dense.linear(pts, c.lin_l)
@@ -233,12 +233,22 @@ class ViewAndScenePoint2Global(Module):
         return skip + dense.sequential(self.mlp, x)
 
 
-def _target_row(conv, x_tgt, ref):
-    """XR of a one-target GATv2 conv: lin_r(x_tgt), or lin_r(0) (== its bias) for the reference's
-    zero target features when stateless (dataset_utils.py:569-571)."""
+def _target_row(conv, x_tgt, ref, n=1):
+    """XR of a one-target GATv2 conv (n targets for a SceneBatch): lin_r(x_tgt), or lin_r(0) (== its
+    bias) for the reference's zero target features when stateless (dataset_utils.py:569-571)."""
     if x_tgt is None:
-        return conv.lin_r(torch.zeros((1, conv.in_channels), device=ref.device)).expand(1, -1)
+        return conv.lin_r(torch.zeros((1, conv.in_channels), device=ref.device)).expand(n, -1)
     return dense.linear(x_tgt, conv.lin_r)
+
+
+def _fold_global(sv, sg, plans):
+    """SceneBatch (batch.py): the per-edge global term of scene s, Sg[s], added to the per-camera
+    term of its cameras (every camera belongs to one scene), so the edge kernels see one scene:
+    Sv'[c] = Sv[c] + Sg[scene(c)], Sg' = 0."""
+    soc = plans.get("_scene_of_cam")
+    if soc is None or sg is None or sg.shape[0] == 1:
+        return sv, sg
+    return sv + sg.index_select(0, soc), torch.zeros((1, sg.shape[1]), dtype=sg.dtype, device=sg.device)
 
 
 class _Global2Node(Module):
@@ -522,6 +532,7 @@ class GraphAttnSfMLayer(Module):
                                                          if carry is not None else (None, None, None)))
         shard = plans.get("_shard")
         sv, sg = replicated_to_local_n(shard, sv, sg)
+        sv, sg = _fold_global(sv, sg, plans)
         sk = self.skip_projection.lin_proj
         P_new = Block0EpilogueFn.apply(P.contiguous(), token, sp, sv, sg, pfu.lin_proj.weight, pfu.lin_proj.bias,
                                        la.weight, la.bias, lb.weight, lb.bias, sk.weight, sk.bias, la.eps, edges)
@@ -542,6 +553,7 @@ class GraphAttnSfMLayer(Module):
                                                          if carry is not None else (None, None, None)))
         shard = plans.get("_shard")
         sv, sg = replicated_to_local_n(shard, sv, sg)
+        sv, sg = _fold_global(sv, sg, plans)
         P_new = EdgeEpilogueFn.apply(P, P0 if self.add_skipconn_from_init_projfeat else None, token, sp, sv, sg,
                                      pfu.lin_proj.weight, pfu.lin_proj.bias, ln.weight, ln.bias, ln.eps, edges)
         return P_new, pts, view, glob
@@ -567,6 +579,7 @@ class GraphAttnSfMLayer(Module):
         sp, sv, sg = pfu.node_terms(pts, view, glob)
         shard = plans.get("_shard")
         sv, sg = replicated_to_local_n(shard, sv, sg)
+        sv, sg = _fold_global(sv, sg, plans)
         delta = edge_ops.projection_update(x_cat, pfu.lin_proj, sp, sv, sg, edges)
         if pfu.n_hidden_layers_proj_update > 0:
             delta = pfu.mlp(F.relu(delta))
@@ -758,8 +771,12 @@ class GraphAttnSfMNet(Module):
         if key not in cache:
             cache.clear()
             idx = x.indices.to(device)
+            plans = scene_plans(data, device)
+            soc = getattr(data, "scene_of_cam", None)
+            if soc is not None:  # a SceneBatch (batch.py): one global row per scene
+                plans["_scene_of_cam"] = soc.to(device)
             cache[key] = EdgeIndex(idx[0].to(torch.int32).contiguous(), idx[1].to(torch.int32).contiguous(),
-                                   x.shape[0], x.shape[1], scene_plans(data, device))
+                                   x.shape[0], x.shape[1], plans)
         return cache[key]
 
     def forward_features(self, values, edges):

@@ -149,10 +149,21 @@ def sample_indices(N, num_samples, adjacent):
     return np.random.choice(N, num_samples, replace=False)
 
 
-def sample_data_device(data, num_views, consecutive_views=True, max_piece=None):
+class DenseScene:
+    """A sampled scene before its graph is built (``sample_data_device(..., build=False)``): the
+    dense M with Ns / y, enough for ``apply_rotational_homography_aug_device`` (which builds the
+    graph once, instead of once per transform)."""
+
+    def __init__(self, M, Ns, y, scene_name, calibrated=True):
+        self._M, self.Ns, self.y, self.scene_name, self.calibrated = M, Ns, y, scene_name, calibrated
+        self.device = M.device
+
+
+def sample_data_device(data, num_views, consecutive_views=True, max_piece=None, build=True):
     """SceneData.sample_data (datasets/SceneData.py:306-353) with M on the device: the view subset's
     rows, the points still seen in >= 2 of those views (gasfm_scene_mask's counts), then the
-    device graph build.  The view choice draws from numpy's global RNG exactly as the reference."""
+    device graph build (``build=False``: a DenseScene for a following transform that builds it).
+    The view choice draws from numpy's global RNG exactly as the reference."""
     M = _dense_M(data)
     idx = sample_indices(len(data.y), num_views, adjacent=consecutive_views)
     m_idx = np.sort(np.concatenate((2 * idx, 2 * idx + 1)))
@@ -163,6 +174,8 @@ def sample_data_device(data, num_views, consecutive_views=True, max_piece=None):
     _, _, pt_count, _ = _native.scene_mask(Ms)
     keep = torch.nonzero(pt_count > 0).view(-1)  # get_M_valid_points(M).any(dim=0)
     Ms = Ms.index_select(1, keep).contiguous()
+    if not build:
+        return DenseScene(Ms, Ns.contiguous(), y, data.scene_name, getattr(data, "calibrated", True))
     return scene_from_dense_device(Ms, Ns.contiguous(), y, data.scene_name,
                                    calibrated=getattr(data, "calibrated", True), max_piece=max_piece)
 

@@ -7,7 +7,9 @@ n = 20k points, dense M resident in HBM).  One step follows train.py:60-140 for 
 scenes: per scene sample 10-20 consecutive views (SceneData.sample_data), rotational homography
 augmentation 15 / 20 degrees (conf rhaug-15-20), graph build, forward, ESFMLoss, the per-step
 core errors (compute_core_errors: a host sync per scene, as the reference's .item() calls), then
-one backward of the batch loss and an Adam step.  Every per-sample stage runs on the device
+one backward of the batch loss and an Adam step.  The batch's forwards run as ONE forward over the
+union of the scene graphs (gasfm_amd/batch.py); --per-scene also times train.py's one forward per
+scene.  Every per-sample stage runs on the device
 (scene_device.py, loss.py, evaluation.py); --host instead samples on the CPU and builds the graph
 with the host builder (no augmentation), the way the reference's DataLoader workers feed the GPU.
 Prints one JSON line per mode: scenes/s and the mean ms per stage.
@@ -24,6 +26,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import gasfm_amd  # noqa: E402
 from gasfm_amd import evaluation, synthetic  # noqa: E402
+from gasfm_amd.batch import forward_batch  # noqa: E402
 from gasfm_amd.conf import Conf  # noqa: E402
 from gasfm_amd.loss import ESFMLoss  # noqa: E402
 from gasfm_amd.scene_device import (apply_rotational_homography_aug_device, sample_data_device,  # noqa: E402
@@ -49,6 +52,8 @@ def main():
     ap.add_argument("--views", type=int, default=100)
     ap.add_argument("--points", type=int, default=20_000)
     ap.add_argument("--host", action="store_true", help="also time the host-side data path")
+    ap.add_argument("--per-scene", action="store_true",
+                    help="also time one forward per scene (train.py's loop) beside the batched union forward")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     np.random.seed(0)
@@ -62,10 +67,11 @@ def main():
                  "eval": {"calc_reprojerr_with_gtposes_for_depth_pred": False}})
     net = gasfm_amd.GraphAttnSfMNet(conf).to(dev)
     lossf = ESFMLoss(conf)
-    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    # torch's fused Adam (one kernel chain over all 145M parameters; train.py uses Adam's default foreach)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4, fused=True)
 
     def prep_device(full):
-        s = sample_data_device(full, int(np.random.randint(10, 21)))
+        s = sample_data_device(full, int(np.random.randint(10, 21)), build=False)  # graph built once, after rhaug
         return apply_rotational_homography_aug_device(s, 15, 20)
 
     def prep_host(full):
@@ -78,7 +84,7 @@ def main():
                                 full.y.cpu()[idx], full.scene_name)
         return d.to(dev)
 
-    def run(prep, steps, warmup):
+    def run(prep, steps, warmup, batched=True):
         t_prep = t_fb = t_opt = 0.0
         n_done = 0
         repro = []
@@ -91,8 +97,9 @@ def main():
             t1 = time.perf_counter()
             opt.zero_grad()
             batch_loss = 0.0
-            for d in datas:
-                pred = net(d)
+            preds = forward_batch(net, datas) if batched else None
+            for k, d in enumerate(datas):
+                pred = preds[k] if batched else net(d)
                 batch_loss = batch_loss + lossf(pred, d)
                 repro.append(evaluation.compute_core_errors(d, pred, conf)["our_repro"])
                 if os.environ.get("TSB_DEBUG"):
@@ -117,8 +124,13 @@ def main():
                 "last_repro_px": float(repro[-1])}
 
     res = run(prep_device, args.steps, args.warmup)
-    print(json.dumps({"mode": "device data path (sample + rhaug + graph build on GPU)", "batch": args.batch,
-                      "scene": f"m={args.views} n={args.points}, 10-20 sampled views", **res}), flush=True)
+    print(json.dumps({"mode": "device data path (sample + rhaug + graph build on GPU), batch as one union forward",
+                      "batch": args.batch, "scene": f"m={args.views} n={args.points}, 10-20 sampled views", **res}),
+          flush=True)
+    if args.per_scene:
+        res = run(prep_device, args.steps, args.warmup, batched=False)
+        print(json.dumps({"mode": "device data path, one forward per scene (train.py's loop)", "batch": args.batch,
+                          "scene": f"m={args.views} n={args.points}, 10-20 sampled views", **res}), flush=True)
     if args.host:
         res = run(prep_host, args.steps, args.warmup)
         print(json.dumps({"mode": "host data path (CPU sampling + host graph build, no rhaug, then .to)",
