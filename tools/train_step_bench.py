@@ -7,7 +7,8 @@ n = 20k points, dense M resident in HBM).  One step follows train.py:60-140 for 
 scenes: per scene sample 10-20 consecutive views (SceneData.sample_data), rotational homography
 augmentation 15 / 20 degrees (conf rhaug-15-20), graph build, forward, ESFMLoss, the per-step
 core errors (compute_core_errors: a host sync per scene, as the reference's .item() calls), then
-one backward of the batch loss and an Adam step.  The batch's forwards run as ONE forward over the
+one backward of the batch loss and an Adam step (--outliers 0.1: config 5's outlier injection, the
+model on the injected scene, the loss on the clean one).  The batch's forwards run as ONE forward over the
 union of the scene graphs (gasfm_amd/batch.py); --per-scene also times train.py's one forward per
 scene.  Every per-sample stage runs on the device
 (scene_device.py, loss.py, evaluation.py); --host instead samples on the CPU and builds the graph
@@ -27,6 +28,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import gasfm_amd  # noqa: E402
 from gasfm_amd import evaluation, synthetic  # noqa: E402
 from gasfm_amd.batch import forward_batch  # noqa: E402
+from gasfm_amd.outliers import inject_outliers  # noqa: E402
 from gasfm_amd.conf import Conf  # noqa: E402
 from gasfm_amd.loss import ESFMLoss  # noqa: E402
 from gasfm_amd.scene_device import (apply_rotational_homography_aug_device, sample_data_device,  # noqa: E402
@@ -52,6 +54,8 @@ def main():
     ap.add_argument("--views", type=int, default=100)
     ap.add_argument("--points", type=int, default=20_000)
     ap.add_argument("--host", action="store_true", help="also time the host-side data path")
+    ap.add_argument("--outliers", type=float, default=0.0,
+                    help="outlier injection rate (config 5: rhaug-15-20 + 0.1 outliers), 0 = off")
     ap.add_argument("--per-scene", action="store_true",
                     help="also time one forward per scene (train.py's loop) beside the batched union forward")
     args = ap.parse_args()
@@ -93,13 +97,18 @@ def main():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             datas = [prep(s) for s in batch]
+            # config 5: the model sees the outlier-injected scene, the loss the clean one (train.py:73-90)
+            inputs = datas if not args.outliers else [inject_outliers(d, args.outliers, log=lambda s: None)
+                                                      for d in datas]
+            keep = [k for k, d in enumerate(inputs) if d is not None]
+            datas, inputs = [datas[k] for k in keep], [inputs[k] for k in keep]
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             opt.zero_grad()
             batch_loss = 0.0
-            preds = forward_batch(net, datas) if batched else None
+            preds = forward_batch(net, inputs) if batched else None
             for k, d in enumerate(datas):
-                pred = preds[k] if batched else net(d)
+                pred = preds[k] if batched else net(inputs[k])
                 batch_loss = batch_loss + lossf(pred, d)
                 repro.append(evaluation.compute_core_errors(d, pred, conf)["our_repro"])
                 if os.environ.get("TSB_DEBUG"):
@@ -124,7 +133,8 @@ def main():
                 "last_repro_px": float(repro[-1])}
 
     res = run(prep_device, args.steps, args.warmup)
-    print(json.dumps({"mode": "device data path (sample + rhaug + graph build on GPU), batch as one union forward",
+    tag = f" + {args.outliers:g} outlier injection" if args.outliers else ""
+    print(json.dumps({"mode": "device data path (sample + rhaug" + tag + " + graph build on GPU), batch as one union forward",
                       "batch": args.batch, "scene": f"m={args.views} n={args.points}, 10-20 sampled views", **res}),
           flush=True)
     if args.per_scene:
