@@ -61,6 +61,31 @@ def attn_fwd_bytes(E, N, H, HC, perm):
     return E * 4 * HC + E * 4 * int(perm) + N * 4 * HC + N * 4 * HC + N * 8 * H + (N + 1) * 4
 
 
+def host_threads():
+    """Every core this process may run on (sched affinity), capped only by an OMP_NUM_THREADS the
+    host sets for its share of the machine (the GPU boxes export 16 per GPU)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(omp))) if omp.isdigit() and int(omp) > 0 else n
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+# The CPU port's cost is linear in the edge count: its time per step is E-sized tensor ops
+# (gathers, index_add, [E, 64] GEMMs) plus camera-sized ops that also shrink with the sample
+# (m = 1000 x scale cameras).  tools/cpu_baseline_scaling.py measured edges/s at scales
+# 0.05 .. 1.0 (profiles/r2_cpu_baseline_scaling.json): the full config-4 workload runs within
+# 16 % of the 10 % sample's edges/s (51.3k vs 59.4k edges/s, 78 s per full step on 16 EPYC 9575F
+# threads), so the bench times the sample (a ~16 % optimistic CPU number) and reports its edges/s.
 def cpu_baseline(sample_scale, threads):
     """Oracle (reference + PyG op sequence, torch CPU fp32) fwd+bwd edges/s on a sample scene."""
     import gasfm_amd
@@ -86,7 +111,8 @@ def cpu_baseline(sample_scale, threads):
     return {"value": sc.num_edges / t, "unit": "edges/s", "cores": threads, "kind": "port",
             "sample": f"scaled config 4 (m={sc.m}, n={sc.n}, E={sc.num_edges}), 12 blocks, fp32, fwd+bwd, "
                       f"median of 3 after 1 warm-up, {t:.2f} s/step, "
-                      f"torch {torch.__version__} CPU threads={threads}"}
+                      f"torch {torch.__version__} CPU threads={threads} on {cpu_model()}; edges/s of the sample "
+                      f"stands for config 4 (linear in E: profiles/r2_cpu_baseline_scaling.json)"}
 
 
 def main():
@@ -213,8 +239,7 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            aff = len(os.sched_getaffinity(0))
-            cpu = cpu_baseline(args.cpu_sample_scale, max(1, min(aff, 16)))
+            cpu = cpu_baseline(args.cpu_sample_scale, host_threads())
         res = {
             "metric": "GAT-stack edges/sec (fwd+bwd) on cam/point scene graph; 1/2/4/8 MI355X",
             "value": E * args.steps / dt,
