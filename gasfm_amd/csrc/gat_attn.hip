@@ -1170,6 +1170,16 @@ static int grp_rows() {
   return u;
 }
 
+// Minimum fill (wave tasks / resident waves) for the grouped-item forward (A/B knob
+// GASFM_ATTN_GRP_MIN_FILL; 0 = always grouped when enabled).
+static double grp_min_fill() {
+  static const double f = [] {
+    const char* e = std::getenv("GASFM_ATTN_GRP_MIN_FILL");
+    return e ? std::atof(e) : 0.5;
+  }();
+  return f;
+}
+
 static int grid_for(int n_items, int resident) {
   int waves = n_items > 0 ? n_items : 1;
   const int cap = env_wave_cap() ? env_wave_cap() : resident * (kBlock / kWave);
@@ -1210,7 +1220,19 @@ extern "C" int gasfm_gat_attn_fwd(const float* XL, int64_t ldXL, const float* XR
                       aligned16(bias) && (!part || aligned16(part)) && ((H * C + 2 * H) % 4 == 0);
   bool done = false;
   const int grp = grp_rows();
-  if (vec_ok && perm == nullptr && H * C == 32 && C == 8 && grp > 0) {
+  // The grouped kernel packs 8 items into one wave task: right for many short segments (points,
+  // ~20 edges each), wrong when that leaves the chip underfilled -- the camera direction of a
+  // 1/8-points shard has ~2k items of up to 256 edges, i.e. 250 tasks = 72 workgroups (46 us vs
+  // 20 us for the point direction).  Below grp_min_fill() of the resident waves, one item per
+  // wave (the direct-to-LDS kernel) instead.
+  const bool grp_fills = [&] {
+    if (grp <= 0) return false;
+    const int tasks = (n_items + 7) / 8;
+    const int res = resident_blocks(reinterpret_cast<const void*>(&attn_fwd_grp_kernel<4, 1>), kBlock, 0) *
+                    (kBlock / kWave);
+    return double(tasks) >= grp_min_fill() * double(res);
+  }();
+  if (vec_ok && perm == nullptr && H * C == 32 && C == 8 && grp_fills) {
     auto launch = [&](auto kern) {
       const int tasks = (n_items + 7) / 8;
       const int grid = grid_for(tasks, resident_blocks(reinterpret_cast<const void*>(kern), kBlock, 0));
