@@ -131,6 +131,11 @@ def main():
                     help="bf16: the camera-side 1024x1024 projections on the bf16 MFMA kernel (BASELINE config 5)")
     ap.add_argument("--dist", action="store_true",
                     help="run the point-sharded RCCL path even at one rank (under torchrun --nproc-per-node 1)")
+    ap.add_argument("--no-cam-shard", action="store_true",
+                    help="N > 1: shard the points only (the view chain replicated on every rank)")
+    ap.add_argument("--emulate-world", type=int, default=0, metavar="W",
+                    help="per-rank proxy: rank 0's shard of a W-GPU step on this one GPU, collectives replaced by "
+                         "local copies (timing of the per-rank compute; numerically meaningless)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -141,6 +146,8 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist_on = world > 1 or args.dist
+    emul = args.emulate_world > 1 and not dist_on
+    cams = not args.no_cam_shard
     if dist_on:
         torch.distributed.init_process_group("nccl", device_id=dev)
         log(f"[rank {rank}] process group up (world {world})")
@@ -154,10 +161,13 @@ def main():
     conf = gasfm_amd.learning_conf(num_layers=args.layers)
     torch.manual_seed(0)
     net = gasfm_amd.GraphAttnSfMNet(conf).set_projection_precision(args.proj_precision)
-    if dist_on:
+    if dist_on or emul:
         from gasfm_amd import distributed as gdist
-        data = gdist.shard_scene(sc, rank, world).to(dev)
-        model = gdist.ShardedGraphAttnSfMNet(net.to(dev))
+        if emul:
+            data = gdist.shard_scene(sc, 0, args.emulate_world, cameras=cams, emulate=True).to(dev)
+        else:
+            data = gdist.shard_scene(sc, rank, world, cameras=cams and world > 1).to(dev)
+        model = gdist.ShardedGraphAttnSfMNet(net.to(dev), cameras=data.shard.cams is not None)
     else:
         data = gasfm_amd.SceneData.from_synthetic(sc).to(dev)
         model = net.to(dev)
@@ -166,14 +176,14 @@ def main():
     cX = torch.randn((4, sc.n), generator=gen).to(dev)
     log(f"[rank {rank}] scene m={sc.m} n={sc.n} E={E} built+moved in {time.time() - t0:.1f}s")
 
-    cx = cX if not dist_on else cX[:, data.point_slice].contiguous()
+    cx = cX if not (dist_on or emul) else cX[:, data.point_slice].contiguous()
 
     def fwd_bwd():
         pred = model(data)
         # replicated outputs enter every rank's loss in full, local points once (distributed.py)
         loss = (pred["Ps_norm"] * cP).sum() + (pred["pts3D"] * cx).sum()
         loss.backward()
-        if dist_on:
+        if dist_on or emul:
             model.sync_grads()
         return loss
 
@@ -259,7 +269,11 @@ def main():
                                    + ("" if args.proj_precision == "fp32" else
                                       ", camera-side 1024x1024 projections in bf16 on MFMA (fp32 accumulate)"),
                        "cameras": sc.m, "points": sc.n, "edges": E, "blocks": args.layers,
-                       "parallelism": f"point-sharded x{world}" if dist_on else "single GPU"},
+                       "parallelism": (f"emulated rank 0 of {args.emulate_world} ({'points + cameras' if cams else 'points'}"
+                                       " sharded; collectives replaced by local copies: per-rank compute only)"
+                                       if emul else
+                                       f"{'point+camera' if data.shard.cams is not None else 'point'}-sharded x{world}"
+                                       if dist_on else "single GPU")},
             "roofline": {"kernel": "attn_fwd_grp_kernel<4,1> point direction (proj2scenepoint), per launch",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,

@@ -73,7 +73,7 @@ _SIGS = {
     "gasfm_view_hub_fwd": (_i32, [_vp, _i64, _i32, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp, _vp, _vp]),
     "gasfm_view_hub_bwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                  _vp, _vp, _vp, _vp]),
+                                  _vp, _vp, _vp, _vp, _vp]),
     "gasfm_gvec_multi_fwd": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp]),
     "gasfm_gvec_multi_bwd": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp,
                                     _vp, _vp, _f32, _vp]),
@@ -655,14 +655,17 @@ def view_hub_fwd(v, eps, gC, bC, Wv, gA, bA, Wa, ba, Wr, br, sv, t, xr, rs, scra
     check(st, "gasfm_view_hub_fwd")
 
 
-def view_hub_bwd(v, rs, gC, bC, Wv, gA, bA, Wa, t, Wr, dsv, dxr, dxl, dacc, part, scratch):
+def view_hub_bwd(v, rs, gC, bC, Wv, gA, bA, Wa, t, Wr, dsv, dxr, dxl, dacc, part, scratch, dres=None):
+    """dres (d skip, or None) is added to dacc in the kernel's second pass."""
     _req(v, "v")
     D = v.shape[1]
     for a, n, w in ((t, "t", 32), (dsv, "dsv", 32), (dxr, "dxr", 32), (dxl, "dxl", D), (dacc, "dacc", D)):
         _req(a, n, w)
+    if dres is not None:
+        _req(dres, "dres", D)
     st = lib().gasfm_view_hub_bwd(_p(v), _p(rs), v.shape[0], D, _p(gC), _p(bC), _p(Wv), _p(gA), _p(bA), _p(Wa),
-                                  _p(t), _p(Wr), _p(dsv), _p(dxr), _p(dxl), _p(dacc), _p(part), _p(scratch),
-                                  _stream(v))
+                                  _p(t), _p(Wr), _p(dsv), _p(dxr), _p(dxl), _p(dres), _p(dacc), _p(part),
+                                  _p(scratch), _stream(v))
     check(st, "gasfm_view_hub_bwd")
 
 

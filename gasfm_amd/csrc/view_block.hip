@@ -704,7 +704,8 @@ __global__ __launch_bounds__(kW) void view_hub_b2_kernel(
     const float* __restrict__ v, int64_t m, int D, const float2* __restrict__ RSv, const float* __restrict__ gC,
     const float* __restrict__ bC, const float* __restrict__ Wv, const float* __restrict__ gA,
     const float* __restrict__ bA, const float* __restrict__ Wa, const float* __restrict__ dsv,
-    const float* __restrict__ DT, const float4* __restrict__ RSUM, float* __restrict__ dacc) {
+    const float* __restrict__ DT, const float4* __restrict__ RSUM, const float* __restrict__ dres,
+    float* __restrict__ dacc) {
   __shared__ float Vs[TR * L66];
   __shared__ float Sd[TR * L34], Dt[TR * L34];
   __shared__ float MS[TR], RS[TR];
@@ -757,9 +758,10 @@ __global__ __launch_bounds__(kW) void view_hub_b2_kernel(
       const float xh = (Vs[e * L66 + nt * 16 + c] - me) * re;
       const float gvc = (fmaf(xh, gc[nt], bc[nt]) > 0.f ? dhc[nt][r] : 0.f) * gc[nt];
       const float gva = (fmaf(xh, ga[nt], bav[nt]) > 0.f ? dha[nt][r] : 0.f) * ga[nt];
-      if (e < s.nrows)
-        dacc[(s.row0 + e) * D + s.col0 + nt * 16 + c] +=
-            re * (gvc - sm.x - xh * sm.y) + re * (gva - sm.z - xh * sm.w);
+      if (e < s.nrows) {
+        const int64_t o = (s.row0 + e) * D + s.col0 + nt * 16 + c;
+        dacc[o] += re * (gvc - sm.x - xh * sm.y) + re * (gva - sm.z - xh * sm.w) + (dres ? dres[o] : 0.f);
+      }
     }
   }
 }
@@ -850,7 +852,8 @@ extern "C" int gasfm_view_hub_fwd(const float* v, int64_t m, int32_t D, float ep
 extern "C" int gasfm_view_hub_bwd(const float* v, const float* rs, int64_t m, int32_t D, const float* gC,
                                   const float* bC, const float* Wv, const float* gA, const float* bA, const float* Wa,
                                   const float* t, const float* Wr, const float* dsv, const float* dxr,
-                                  const float* dxl, float* dacc, float* part, float* scratch, void* stream) {
+                                  const float* dxl, const float* dres, float* dacc, float* part, float* scratch,
+                                  void* stream) {
   GASFM_REQUIRE(m >= 0 && width_ok(D), "gasfm_view_hub_bwd: m=%lld D=%d", (long long)m, D);
   if (m == 0) return GASFM_OK;
   GASFM_REQUIRE(v && rs && gC && bC && Wv && gA && bA && Wa && t && Wr && dsv && dxr && dxl && dacc && part &&
@@ -867,6 +870,6 @@ extern "C" int gasfm_view_hub_bwd(const float* v, const float* rs, int64_t m, in
   hipLaunchKernelGGL(view_hub_b1_kernel, grid2(m, D), dim3(kW), 0, st, v, m, D, RSv, gC, bC, Wv, gA, bA, Wa, dsv, DT,
                      dxl, RSUM, part);
   hipLaunchKernelGGL(view_hub_b2_kernel, grid2(m, D), dim3(kW), 0, st, v, m, D, RSv, gC, bC, Wv, gA, bA, Wa, dsv, DT,
-                     RSUM, dacc);
+                     RSUM, dres, dacc);
   return launch_status("gasfm_view_hub_bwd");
 }

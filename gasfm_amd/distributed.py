@@ -26,6 +26,22 @@ Loss convention: each rank's loss must contain the replicated outputs'
 (Ps_norm) term in full and its own points' (pts3D[:, point_slice]) term.
 ``gasfm_amd.ESFMLoss`` on a sharded scene follows it: every rank computes the
 global loss (one 2-float all-reduce) and its Ps gradient is all-reduced.
+
+Camera sharding (``shard_scene(..., cameras=True)``, the default of bench.py at N > 1):
+the m x 1024 view chain (Proj2View tail + MLP, the view hub, view->global lin_l,
+the final update's view tail and the view head) is split too: rank r owns the
+camera rows [r*ceil(m/W), ...) and runs the 1024 x 1024 GEMMs and view kernels on
+them only.  Per block, forward: the camera aggregate (replicated after the
+all-gather combine) is sliced to the own rows (``OwnRowsFn``; backward: one
+all-gather of the own-row gradients); the view hub's 32-wide outputs that every
+rank's edges read (the projection-update term SV and the next block's camera
+target rows XR) are all-gathered in ONE collective (``GatherRowsFn``); the
+view->global and points->global attentions exchange their partial softmax states
+in ONE all-gather (``ShardedGlobalAttentionFn``).  Backward: the (SV, SG, next
+XR) gradients are all-reduced in one collective (``AllReduceGradN``), the two
+global target rows in one more.  The view-side parameters then hold partial
+gradients like the point-side ones: ``sync_grads`` all-reduces every parameter
+except the replicated global chain's (``REPLICATED_CAM_PATTERNS``).
 """
 import copy
 import fnmatch
@@ -58,13 +74,54 @@ LOCAL_PARAM_PATTERNS = (
 )
 
 
-def is_local_param(name):
+# camera sharding: the only parameters whose gradients are computed identically on every rank
+# (the global node's chain, from replicated inputs and all-reduced boundary gradients, and the
+# attention biases, whose gradients are sums of replicated output gradients)
+REPLICATED_CAM_PATTERNS = (
+    "*view_and_scenepoint2global.norm_and_proj_global2view.*",
+    "*view_and_scenepoint2global.norm_and_proj_global2scenepoint.*",
+    "*view_and_scenepoint2global.graph_conv_view2global.lin_r.*",
+    "*view_and_scenepoint2global.graph_conv_scenepoint2global.lin_r.*",
+    "*view_and_scenepoint2global.graph_conv_view2global.bias",
+    "*view_and_scenepoint2global.graph_conv_scenepoint2global.bias",
+    "*view_and_scenepoint2global.proj_view_and_scenepoint2global.*",
+    "*view_and_scenepoint2global.norm_pre_mlp.*",
+    "*view_and_scenepoint2global.mlp.*",
+    "*projection_feature_update.global_norm_layer.*",
+    "*projection_feature_update.lin_global.*",
+    "*proj2view.graph_conv.bias",
+    # block 0 is stateless: its camera target rows are lin_r(0), the same replicated row everywhere
+    "equivariant_blocks.0.global_feature_update.proj2view.graph_conv.lin_r.*",
+)
+
+
+def is_local_param(name, cameras=False):
+    """True when the parameter's gradient is partial per rank (summed by ``sync_grads``)."""
+    if cameras:
+        return not any(fnmatch.fnmatchcase(name, p) for p in REPLICATED_CAM_PATTERNS)
     return any(fnmatch.fnmatchcase(name, p) for p in LOCAL_PARAM_PATTERNS)
 
 
+def camera_rows(m, world, rank):
+    """Contiguous equal camera chunks: (c0, c1, chunk) of rank ``rank``; the last chunk may be short."""
+    chunk = -(-m // world)
+    c0 = min(m, rank * chunk)
+    return c0, min(m, c0 + chunk), chunk
+
+
 class ShardContext:
-    def __init__(self, rank, world, group=None):
+    """rank / world / process group of a sharded scene.
+
+    cams: (c0, c1, chunk, m) when the camera rows are sharded too (None: replicated views).
+    emulate: no process group -- all_gather returns ``world`` copies of this rank's tensor and
+    all_reduce_ is the identity.  Runs one rank's share of an N-GPU step on one GPU with the real
+    kernels and tensor shapes (the per-rank proxy of bench.py --emulate-world); numerically
+    meaningless."""
+
+    def __init__(self, rank, world, group=None, cams=None, emulate=False):
         self.rank, self.world, self.group = rank, world, group
+        self.cams = cams
+        self.emulate = bool(emulate)
         self._combine_cache = {}
 
     def combine_items(self, N, device):
@@ -81,6 +138,10 @@ class ShardContext:
 
     def all_gather(self, t):
         t = t.contiguous()
+        if self.emulate:  # one copy kernel of the gathered size (stands in for the RCCL kernel)
+            out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            out.view((self.world,) + tuple(t.shape)).copy_(t.unsqueeze(0).expand((self.world,) + tuple(t.shape)))
+            return out
         if self._staged(t):
             parts = [torch.empty_like(t, device="cpu") for _ in range(self.world)]
             dist.all_gather(parts, t.cpu(), group=self.group)
@@ -90,6 +151,8 @@ class ShardContext:
         return out
 
     def all_reduce_(self, t):
+        if self.emulate:
+            return t
         if self._staged(t):
             c = t.cpu()
             dist.all_reduce(c, group=self.group)
@@ -138,6 +201,67 @@ class AllReduceGradN(torch.autograd.Function):
         return (None,) + tuple(out)
 
 
+def _pad_rows(x, rows):
+    if x.shape[0] == rows:
+        return x.contiguous()
+    return torch.cat([x, x.new_zeros((rows - x.shape[0],) + tuple(x.shape[1:]))])
+
+
+class OwnRowsFn(torch.autograd.Function):
+    """Replicated camera rows [m, ...] -> this rank's rows [c0, c1); the backward all-gathers the
+    own-row gradients (each rank's slice is the full gradient of its rows)."""
+
+    @staticmethod
+    def forward(ctx, x, shard):
+        ctx.shard = shard
+        c0, c1, _, _ = shard.cams
+        return x[c0:c1]
+
+    @staticmethod
+    def backward(ctx, g):
+        shard = ctx.shard
+        _, _, chunk, m = shard.cams
+        return shard.all_gather(_pad_rows(g, chunk))[:m], None
+
+
+class GatherRowsFn(torch.autograd.Function):
+    """Own camera rows of several [own, w_k] tensors -> the full [m, w_k] tensors, with ONE
+    all-gather of their concatenation; the backward slices the own rows of each gradient (the
+    gradients arriving here are already summed over ranks: AllReduceGradN downstream, or
+    replicated losses)."""
+
+    @staticmethod
+    def forward(ctx, shard, *xs):
+        ctx.shard = shard
+        ctx.widths = [x.shape[1] for x in xs]
+        ctx.shapes = [x.shape for x in xs]
+        _, _, chunk, m = shard.cams
+        flat = torch.cat([x.reshape(x.shape[0], -1) for x in xs], 1) if len(xs) > 1 else xs[0].reshape(
+            xs[0].shape[0], -1)
+        full = shard.all_gather(_pad_rows(flat, chunk))[:m]
+        out, at = [], 0
+        for x in xs:
+            k = int(np.prod(x.shape[1:]))
+            out.append(full[:, at:at + k].reshape((m,) + tuple(x.shape[1:])).contiguous())
+            at += k
+        return tuple(out)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        c0, c1, _, _ = ctx.shard.cams
+        return (None,) + tuple(None if g is None else g[c0:c1].contiguous() for g in gs)
+
+
+def own_rows(x, shard):
+    return x if shard is None or shard.cams is None else OwnRowsFn.apply(x, shard)
+
+
+def gather_rows(shard, *xs):
+    if shard is None or shard.cams is None:
+        return xs
+    return GatherRowsFn.apply(shard, *xs)
+
+
 def replicated_to_local(x, shard):
     return x if shard is None else AllReduceGrad.apply(x, shard)
 
@@ -173,6 +297,44 @@ class ShardedAttentionFn(torch.autograd.Function):
         return dXL, dXR, datt.view_as(att), dbias, None, None, None, None, None
 
 
+class ShardedGlobalAttentionFn(torch.autograd.Function):
+    """The view->global and points->global GATv2 attentions of a block (one replicated target
+    each) when both the views and the points are sharded: each rank attends over its own views /
+    points, the two packed partial rows go out in ONE all-gather and are merged in rank order
+    (identical on all ranks).  Backward: local edges against the global statistics; the two
+    target-row gradients (partial per rank) are summed in ONE all-reduce."""
+
+    @staticmethod
+    def forward(ctx, XLv, XRv, att_v, bias_v, XLp, XRp, att_p, bias_p, plans, heads, slope, shard):
+        plan_v, plan_vp, plan_p, plan_pp = plans
+        part_v = attn_forward_partial(XLv, XRv, att_v, plan_vp, heads, slope)
+        part_p = attn_forward_partial(XLp, XRp, att_p, plan_pp, heads, slope)
+        wv, wp = part_v.shape[1], part_p.shape[1]
+        g = shard.all_gather(torch.cat([part_v, part_p], 1))
+        items = shard.combine_items(1, XLv.device)
+        out_v, mv, sv = combine_partials(g[:, :wv].contiguous(), shard.world, 1, heads, bias_v, items)
+        out_p, mp, sp = combine_partials(g[:, wv:wv + wp].contiguous(), shard.world, 1, heads, bias_p, items)
+        ctx.plans, ctx.heads, ctx.slope, ctx.shard = (plan_v, plan_p), heads, slope, shard
+        ctx.defer = _native.defer_token(att_v, bias_v, att_p, bias_p)
+        ctx.save_for_backward(XLv, XRv, att_v, bias_v, out_v, mv, sv, XLp, XRp, att_p, bias_p, out_p, mp, sp)
+        return out_v, out_p
+
+    @staticmethod
+    def backward(ctx, gv, gp):
+        XLv, XRv, att_v, bias_v, out_v, mv, sv, XLp, XRp, att_p, bias_p, out_p, mp, sp = ctx.saved_tensors
+        plan_v, plan_p = ctx.plans
+        gv = gv if gv is not None else torch.zeros_like(out_v)
+        gp = gp if gp is not None else torch.zeros_like(out_p)
+        dXLv, dXRv, dattv, dbv = attn_backward_raw(XLv, XRv, att_v, bias_v, plan_v, ctx.heads, ctx.slope, out_v, mv,
+                                                   sv, gv, defer=ctx.defer)
+        dXLp, dXRp, dattp, dbp = attn_backward_raw(XLp, XRp, att_p, bias_p, plan_p, ctx.heads, ctx.slope, out_p, mp,
+                                                   sp, gp, defer=ctx.defer)
+        wv = dXRv.shape[1]
+        flat = ctx.shard.all_reduce_(torch.cat([dXRv, dXRp], 1))
+        return (dXLv, flat[:, :wv], dattv.view_as(att_v), dbv, dXLp, flat[:, wv:], dattp.view_as(att_p), dbp,
+                None, None, None, None)
+
+
 def partition_points(pt, n, world):
     """Contiguous point ranges with ~equal edge counts: returns boundaries [world+1]."""
     counts = np.bincount(np.asarray(pt), minlength=n)
@@ -185,10 +347,12 @@ def partition_points(pt, n, world):
     return np.maximum.accumulate(np.asarray(bounds))
 
 
-def shard_scene(scene, rank, world, max_piece=None):
+def shard_scene(scene, rank, world, max_piece=None, cameras=False, emulate=False):
     """Rank-local SceneData of a synthetic (or any cam-major) scene.
 
     scene: object with m, n, cam, pt (cam-major sorted) and normalized_values().
+    cameras: shard the camera (view) rows too (module docstring).  emulate: a ShardContext
+    without a process group (see ShardContext).
     """
     cam = np.asarray(scene.cam)
     pt = np.asarray(scene.pt)
@@ -217,10 +381,23 @@ def shard_scene(scene, rank, world, max_piece=None):
     }
     for k, p in data.partial_plans.items():
         p.tag = k + "_partial"
+    cams = None
+    if cameras:
+        c0, c1, chunk = camera_rows(m, world, rank)
+        cams = (c0, c1, chunk, m)
+        own = vv[(vv >= c0) & (vv < c1)] - c0
+        kw8 = {"max_piece": 8}
+        plan = AttnPlan.from_targets(torch.zeros_like(own), 1, src=own, src_rows=c1 - c0, **kw8)
+        plan.tag = "view2global"
+        gw["view2global"].plan = plan
+        data.partial_plans["view2global"] = AttnPlan.from_targets(torch.zeros_like(own), 1, src=own,
+                                                                  src_rows=c1 - c0, all_partial=True, **kw8)
+        data.partial_plans["view2global"].tag = "view2global_partial"
+        data.camera_slice = slice(c0, c1)
     data.point_slice = slice(p0, p1)
     data.n_global = n
     data.n_edges_global = int(pt.shape[0])
-    data.shard = ShardContext(rank, world)
+    data.shard = ShardContext(rank, world, cams=cams, emulate=emulate)
     return data
 
 
@@ -232,22 +409,29 @@ class ShardedGraphAttnSfMNet(torch.nn.Module):
     backward (sums the gradients of rank-local parameters over the ranks).
     """
 
-    def __init__(self, net, group=None):
+    def __init__(self, net, group=None, cameras=False):
+        """cameras: the scenes come from shard_scene(..., cameras=True) (view rows sharded too):
+        every parameter outside the global chain then carries a partial gradient."""
         super().__init__()
         self.net = net
         self.group = group
-        self.local_names = [k for k, _ in net.named_parameters() if is_local_param(k)]
+        self.cameras = cameras
+        self.local_names = [k for k, _ in net.named_parameters() if is_local_param(k, cameras)]
+        self._emulate = None
 
     def forward(self, data):
         shard = data.shard
+        if (shard.cams is not None) != self.cameras:
+            raise ValueError("ShardedGraphAttnSfMNet(cameras=...) must match shard_scene(..., cameras=...)")
         shard.group = self.group
+        self._emulate = shard if shard.emulate else None
         return self.net.forward(data, shard=shard, partial_plans=data.partial_plans)
 
     def sync_grads(self):
         """One all-reduce of every rank-local parameter's gradient, in a fixed layout: a parameter
         without a gradient on this rank contributes zeros (and gets the summed gradient), so all
         ranks reduce buffers of the same size and order."""
-        if dist.get_world_size(self.group) == 1:
+        if self._emulate is None and dist.get_world_size(self.group) == 1:
             return
         params = dict(self.net.named_parameters())
         ps = [params[k] for k in self.local_names]
@@ -255,13 +439,11 @@ class ShardedGraphAttnSfMNet(torch.nn.Module):
             return
         dev = ps[0].device
         flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1).to(dev) for p in ps])
-        shard = ShardContext(dist.get_rank(self.group), dist.get_world_size(self.group), self.group)
+        shard = self._emulate or ShardContext(dist.get_rank(self.group), dist.get_world_size(self.group), self.group)
         shard.all_reduce_(flat)
+        # the summed gradients stay in the bucket: each .grad becomes a view of it (a copy back per
+        # parameter was ~620 copy launches per step with the camera chain sharded)
         off = 0
         for p in ps:
-            g = flat[off:off + p.numel()].view_as(p)
-            if p.grad is None:
-                p.grad = g.clone()
-            else:
-                p.grad.copy_(g)
+            p.grad = flat[off:off + p.numel()].view_as(p)
             off += p.numel()

@@ -46,6 +46,25 @@ def replicated_to_local_n(shard, *xs):
     return AllReduceGradN.apply(shard, *xs)
 
 
+def _cam_sharded(shard):
+    return shard is not None and shard.cams is not None
+
+
+def _wrap_boundary(shard, sv, sg, carry):
+    """sv / sg (replicated, read by the local edges) get their gradients summed over ranks by ONE
+    all-reduce -- together with the next block's camera target rows XRc when the view hub left
+    them in carry (their gradient, from the next block's camera attention on the local edges, is
+    partial too), so that block skips its own all-reduce."""
+    if shard is None:
+        return sv, sg
+    if carry is not None and "XRc" in carry and not carry.get("XRc_wrapped", False):
+        sv, sg, xrc = replicated_to_local_n(shard, sv, sg, carry["XRc"])
+        carry["XRc"] = xrc
+        carry["XRc_wrapped"] = True
+        return sv, sg
+    return replicated_to_local_n(shard, sv, sg)
+
+
 class _LazySharded:
     """ShardedAttentionFn, imported on first use (keeps torch.distributed out of the 1-GPU import path)."""
 
@@ -201,9 +220,11 @@ class ViewAndScenePoint2Global(Module):
         self.mlp = get_linear_layers((2 + n_hidden_layers_global_update) * [n_feat_global_out], norm=False)
 
     def forward_plan(self, view, pts, plan_v2g, plan_s2g, prev, plan_s2g_partial=None, shard=None, xl_pts=None,
-                     xl_view=None, pre_glob=None):
+                     xl_view=None, pre_glob=None, plan_v2g_partial=None):
         """xl_pts / xl_view: the convs' lin_l(pts) / lin_l(view) when already computed (hubs);
-        pre_glob: (XR_view2global, XR_scenepoint2global, skip of prev) from GlobalHubFn."""
+        pre_glob: (XR_view2global, XR_scenepoint2global, skip of prev) from GlobalHubFn.
+        Camera-sharded (shard.cams): view holds this rank's camera rows and both attentions
+        exchange partial states in one all-gather (distributed.ShardedGlobalAttentionFn)."""
         assert self.stateful == (prev is not None)
         cv, c = self.graph_conv_view2global, self.graph_conv_scenepoint2global
         if pre_glob is not None:
@@ -213,14 +234,22 @@ class ViewAndScenePoint2Global(Module):
             xp = dense.sequential(self.norm_and_proj_global2scenepoint, prev) if prev is not None else None
             XRv, XRp = _target_row(cv, xv, view, plan_v2g.num_targets), _target_row(c, xp, pts, plan_s2g.num_targets)
         XLv = xl_view if xl_view is not None else dense.linear(view, cv.lin_l)
-        v2g = gat_attention(XLv, XRv, cv.att, cv._bias(XLv), plan_v2g, cv.heads, cv.negative_slope)
         XLp = xl_pts if xl_pts is not None else dense.linear(pts, c.lin_l)
+        if _cam_sharded(shard):
+            from .distributed import ShardedGlobalAttentionFn
+            v2g, s2g = ShardedGlobalAttentionFn.apply(
+                XLv, XRv, cv.att, cv._bias(XLv), XLp, XRp, c.att, c.bias,
+                (plan_v2g, plan_v2g_partial, plan_s2g, plan_s2g_partial), c.heads, c.negative_slope, shard)
+            return self._global_tail(torch.cat([v2g, s2g], dim=1), prev)
+        v2g = gat_attention(XLv, XRv, cv.att, cv._bias(XLv), plan_v2g, cv.heads, cv.negative_slope)
         if shard is None:
             s2g = gat_attention(XLp, XRp, c.att, c._bias(XLp), plan_s2g, c.heads, c.negative_slope)
         else:  # points are sharded, the global target is replicated
             s2g = ShardedAttentionFn.apply(XLp, replicated_to_local(XRp, shard), c.att, c.bias, plan_s2g,
                                            plan_s2g_partial, c.heads, c.negative_slope, shard)
-        x = torch.cat([v2g, s2g], dim=1)
+        return self._global_tail(torch.cat([v2g, s2g], dim=1), prev)
+
+    def _global_tail(self, x, prev):
         if hasattr(self, "proj_view_and_scenepoint2global"):
             x = dense.linear_res(x, self.proj_view_and_scenepoint2global, prev)
         elif prev is not None:
@@ -367,11 +396,17 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
             XRp, prev_pt = carry.pop("XRp"), carry.pop("pts_skip")
         else:
             XRp = sp.target_rows(prev_pt, pp.num_targets)
+        cams = _cam_sharded(shard)
         if carry is not None and "XRc" in carry:
             XRc, prev_view = carry.pop("XRc"), carry.pop("view_skip")
+            wrapped = carry.pop("XRc_wrapped", False)
         else:
+            if cams and prev_view is not None:
+                raise RuntimeError("camera-sharded execution needs the fused view hubs (stateful block without carry)")
             XRc = sv.target_rows(prev_view, pc.num_targets)
-        XRc = replicated_to_local(XRc, shard)
+            wrapped = False
+        if not wrapped:
+            XRc = replicated_to_local(XRc, shard)
         cp, cc = sp.graph_conv, sv.graph_conv
         hubs = carry is not None and self.output_global and nxt is not None
         vsg = self.view_and_scenepoint2global if hubs else None
@@ -386,6 +421,9 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         if sec is not None:
             point_block.forward_buffers(sec, agg_p.shape[0], agg_p)
             sec.fork()
+        if cams:  # this rank's camera rows only from here on (distributed.py, camera sharding)
+            from .distributed import own_rows
+            agg_c = own_rows(agg_c, shard)
         # created in this order so that the backward runs the point hub (which forks the side
         # stream) before the camera hub, and the point tail on the side stream after it
         view = sv.tail(agg_c, prev_view)
@@ -393,7 +431,12 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
             hv = view_block.hub_params(pfu, vsg.graph_conv_view2global, nxt.proj2view)
             if hv is not None and view_block._rows_ok(view, view.shape[1]):
                 skip, SV, XLv, XRn = view_block.hub(view, hv, getattr(self, "_proj_bf16", False))
+                if cams:  # every rank's edges read all cameras' SV and XR: one all-gather
+                    from .distributed import gather_rows
+                    SV, XRn = gather_rows(shard, SV, XRn)
                 carry.update(XRc=XRn, view_skip=skip, SV=SV, XLv2g=XLv)
+            elif cams:
+                raise RuntimeError("camera-sharded execution needs the fused view hub shapes")
         pts = sp.tail(agg_p, prev_pt, sec=sec)
         if hp is not None and point_block._rows_ok(pts, point_block.P_W):
             skip, SA, XLs, XRn = point_block.hub(pts, hp, sec)
@@ -417,7 +460,8 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
                 view, pts, plans["view2global"], plans["scenepoint2global"], prev_glob,
                 plans.get("_partial", {}).get("scenepoint2global"), plans.get("_shard"),
                 xl_pts=carry.pop("XLs2g", None) if carry is not None else None,
-                xl_view=carry.pop("XLv2g", None) if carry is not None else None, pre_glob=pre_glob)
+                xl_view=carry.pop("XLv2g", None) if carry is not None else None, pre_glob=pre_glob,
+                plan_v2g_partial=plans.get("_partial", {}).get("view2global"))
             if carry is not None and nxt is not None and getattr(nxt, "output_global", False) \
                     and dense._gvec_ok(glob, glob.shape[1]):
                 hg = dense.global_hub_params(pfu, nxt.view_and_scenepoint2global)
@@ -530,8 +574,7 @@ class GraphAttnSfMLayer(Module):
         sp, sv, sg = pfu.node_terms(pts, view, glob, *((carry.pop("SA", None), carry.pop("SV", None),
                                                           carry.pop("SG", None))
                                                          if carry is not None else (None, None, None)))
-        shard = plans.get("_shard")
-        sv, sg = replicated_to_local_n(shard, sv, sg)
+        sv, sg = _wrap_boundary(plans.get("_shard"), sv, sg, carry)
         sv, sg = _fold_global(sv, sg, plans)
         sk = self.skip_projection.lin_proj
         P_new = Block0EpilogueFn.apply(P.contiguous(), token, sp, sv, sg, pfu.lin_proj.weight, pfu.lin_proj.bias,
@@ -551,8 +594,7 @@ class GraphAttnSfMLayer(Module):
         sp, sv, sg = pfu.node_terms(pts, view, glob, *((carry.pop("SA", None), carry.pop("SV", None),
                                                           carry.pop("SG", None))
                                                          if carry is not None else (None, None, None)))
-        shard = plans.get("_shard")
-        sv, sg = replicated_to_local_n(shard, sv, sg)
+        sv, sg = _wrap_boundary(plans.get("_shard"), sv, sg, carry)
         sv, sg = _fold_global(sv, sg, plans)
         P_new = EdgeEpilogueFn.apply(P, P0 if self.add_skipconn_from_init_projfeat else None, token, sp, sv, sg,
                                      pfu.lin_proj.weight, pfu.lin_proj.bias, ln.weight, ln.bias, ln.eps, edges)
@@ -847,7 +889,12 @@ class GraphAttnSfMNet(Module):
             pred["depths"] = SparseMat(self.depth_head(P), x.indices, x.cam_per_pts, x.pts_per_cam,
                                        [x.shape[0], x.shape[1], 1])
         if self.view_head_enabled:
-            pred.update(self.extract_view_outputs(self.view_head(F.relu(view))))
+            out = self.extract_view_outputs(self.view_head(F.relu(view)))
+            shard = edges.plans.get("_shard")
+            if _cam_sharded(shard):  # this rank's camera rows -> all cameras (one all-gather)
+                from .distributed import gather_rows
+                out = {k: gather_rows(shard, v)[0] for k, v in out.items()}
+            pred.update(out)
         if self.scenepoint_head_enabled:
             n_out = dense.sequential(self.scenepoint_head, F.relu(pts)).T
             pred["pts3D"] = torch.cat([n_out, torch.ones(1, n_out.shape[1], dtype=n_out.dtype, device=device)])

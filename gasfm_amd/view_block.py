@@ -49,7 +49,8 @@ class ViewTailFn(torch.autograd.Function):
         rs = _f32(m, 2, like=agg)
         _native.view_tail_fwd(prev, agg, Wp, bp, ln_w, ln_b, eps, bm, x, xb, h, rs,
                               _native.view_scratch(m, D, agg.device))
-        view = _mm(h, Wm.t(), cin=xb, bf16=bf16)
+        # fp32: xb + h Wm^T accumulated in place (torch's addmm with a separate input first copies it)
+        view = _mm(h, Wm.t(), cin=xb, bf16=True) if bf16 else xb.addmm_(h, Wm.t())
         ctx.save_for_backward(agg, x, rs, h, Wp, ln_w, ln_b, Wm)
         ctx.eps, ctx.has_prev, ctx.bf16 = eps, prev is not None, bf16
         ctx.defer = _native.defer_token(Wp, bp, ln_w, ln_b, bm)
@@ -103,7 +104,12 @@ class ViewHubFn(torch.autograd.Function):
         dSV = dSV.contiguous() if dSV is not None else zeros(A_W)
         dXR = dXR.contiguous() if dXR is not None else zeros(A_W)
         dXL = dXL.contiguous() if dXL is not None else zeros(D)
-        dacc = _mm(dXL, Wl, cin=dskip, bf16=ctx.bf16)
+        dres = None
+        if ctx.bf16:
+            dacc = _mm(dXL, Wl, cin=dskip, bf16=True)
+        else:  # d skip is added by the hub kernel's second pass (no addmm input copy)
+            dacc = dXL @ Wl
+            dres = dskip.contiguous() if dskip is not None else None
         dWl = _mm(dXL.t(), v, bf16=ctx.bf16)
         cols = _native.view_hub_part_cols(D)
         if m == 0:
@@ -111,7 +117,7 @@ class ViewHubFn(torch.autograd.Function):
         else:
             part = _f32((m + TR - 1) // TR, cols, like=v)
             _native.view_hub_bwd(v, rs, gC, bC, Wv, gA, bA, Wa, t, Wr, dSV, dXR, dXL, dacc, part,
-                                 _native.view_scratch(m, D, v.device))
+                                 _native.view_scratch(m, D, v.device), dres=dres)
             tot = _native.param_colsum(part, ctx.defer)
         o = 0
         dWv = tot[o:o + A_W * D].view(A_W, D)

@@ -352,12 +352,13 @@ int gasfm_view_hub_fwd(const float* v, int64_t m, int32_t D, float eps, const fl
                        const float* Wr, const float* br, float* sv, float* t, float* xr, float* rs, float* scratch,
                        void* stream);
 
-/* dacc (in: d skip + dXL Wl, out: d v) += LN_c_bwd(mask dsv Wv) + LN_a_bwd(mask dt Wa), dt = dxr Wr;
- * dxl is read for the lin_l bias gradient; partials. */
+/* dacc (in: dXL Wl, out: d v) += dres + LN_c_bwd(mask dsv Wv) + LN_a_bwd(mask dt Wa), dt = dxr Wr;
+ * dres (d skip, may be null) is added in the same pass (no addmm input copy); dxl is read for the
+ * lin_l bias gradient; partials. */
 int gasfm_view_hub_bwd(const float* v, const float* rs, int64_t m, int32_t D, const float* gC, const float* bC,
                        const float* Wv, const float* gA, const float* bA, const float* Wa, const float* t,
-                       const float* Wr, const float* dsv, const float* dxr, const float* dxl, float* dacc,
-                       float* part, float* scratch, void* stream);
+                       const float* Wr, const float* dsv, const float* dxr, const float* dxl, const float* dres,
+                       float* dacc, float* part, float* scratch, void* stream);
 
 /* Batched single-row problems in ONE launch each way (the global hub: the LayerNorm -> Linear
  * consumers of a block's global row, then the two lin_r rows).  Arrays of nprob (<= 4) entries,

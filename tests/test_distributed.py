@@ -68,6 +68,35 @@ def test_local_param_classification():
     assert n_local < 1_000_000  # the bucket is ~1 MB of fp32, not the 145 M replicated params
 
 
+def test_camera_rows_and_cam_param_classification():
+    import gasfm_amd
+    for m, world in ((1000, 8), (1000, 3), (10, 4)):
+        rows = [gd.camera_rows(m, world, r) for r in range(world)]
+        assert rows[0][0] == 0 and rows[-1][1] == m
+        assert all(a[1] == b[0] for a, b in zip(rows[:-1], rows[1:]))
+        assert all(r[2] == -(-m // world) for r in rows)
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf())
+    names = [k for k, _ in net.named_parameters()]
+    part = {k for k in names if gd.is_local_param(k, cameras=True)}
+    blk = "equivariant_blocks.3."
+    # the view chain and every point-side parameter carry partial gradients ...
+    for k in ("global_feature_update.proj2view.mlp.0.weight", "global_feature_update.proj2view.norm_and_proj_view2proj.2.weight",
+              "global_feature_update.proj2view.graph_conv.lin_r.weight", "projection_feature_update.lin_view.weight",
+              "global_feature_update.view_and_scenepoint2global.graph_conv_view2global.lin_l.weight",
+              "global_feature_update.view_and_scenepoint2global.graph_conv_view2global.att",
+              "projection_feature_update.lin_proj.weight"):
+        assert blk + k in part, k
+    assert "view_head.0.weight" in part and "scenepoint_head.4.bias" in part
+    # ... the global chain does not
+    for k in ("global_feature_update.view_and_scenepoint2global.mlp.0.weight",
+              "global_feature_update.view_and_scenepoint2global.proj_view_and_scenepoint2global.weight",
+              "global_feature_update.view_and_scenepoint2global.graph_conv_view2global.lin_r.weight",
+              "projection_feature_update.lin_global.weight", "global_feature_update.proj2view.graph_conv.bias"):
+        assert blk + k not in part, k
+    # every point-sharding local parameter stays partial under camera sharding
+    assert {k for k in names if gd.is_local_param(k)} <= part
+
+
 def _partial_state(logits, vals):
     m = logits.max(0).values
     e = torch.exp(logits - m)
@@ -135,7 +164,7 @@ def test_collective_wrappers_gloo_world2():
         assert ga == [[3.0] * 3] * 2 and gb == [10.0] * 5  # AllReduceGradN: one all-reduce, None -> 0
 
 
-def _worker_sharded_model(rank, world, port, q):
+def _worker_sharded_model(rank, world, port, q, cameras=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -146,8 +175,8 @@ def _worker_sharded_model(rank, world, port, q):
         sc = synthetic.scaled_config4(0.02, seed=5)
         net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=3))
         net.load_state_dict(deterministic_state_dict(net.state_dict()))
-        model = gd.ShardedGraphAttnSfMNet(net.to(dev))
-        data = gd.shard_scene(sc, rank, world, max_piece=64).to(dev)
+        model = gd.ShardedGraphAttnSfMNet(net.to(dev), cameras=cameras)
+        data = gd.shard_scene(sc, rank, world, max_piece=64, cameras=cameras).to(dev)
         g = torch.Generator().manual_seed(1)
         cP = torch.randn((sc.m, 3, 4), generator=g).to(dev)
         cX = torch.randn((4, sc.n), generator=g).to(dev)
@@ -164,8 +193,10 @@ def _worker_sharded_model(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_sharded_model_matches_single_gpu(device):
-    """2 ranks (gloo staging, one GPU) vs the single-GPU forward, and both vs the fp64 oracle's grads."""
+@pytest.mark.parametrize("cameras", [False, True], ids=["points", "points+cameras"])
+def test_sharded_model_matches_single_gpu(device, cameras):
+    """2 ranks (gloo staging, one GPU) vs the single-GPU forward, and both vs the fp64 oracle's grads;
+    points sharded, and points + camera rows sharded (the view chain split over the ranks)."""
     import gasfm_amd
     from conftest import check_grad, oracle_grads
     from oracle.weights import deterministic_state_dict
@@ -185,7 +216,7 @@ def test_sharded_model_matches_single_gpu(device):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_sharded_model, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker_sharded_model, args=(r, 2, port, q, cameras)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=600) for _ in procs]
