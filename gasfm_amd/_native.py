@@ -37,8 +37,8 @@ _SIGS = {
     "gasfm_colsum_ws_floats": (_i64, [_i64, _i32]),
     "gasfm_edge_part_floats": (_i32, [_i32, _i64, _i32]),
     "gasfm_edge_prologue_fwd": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
-    "gasfm_edge_epilogue_fwd": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _i32, _vp, _vp, _vp, _vp,
-                                       _f32, _vp, _vp]),
+    "gasfm_edge_epilogue_fwd": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _i32, _vp, _vp, _vp, _i64,
+                                       _vp, _f32, _vp, _vp]),
     "gasfm_edge_epilogue_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _i32, _f32, _vp, _vp, _vp,
                                        _vp, _vp]),
     "gasfm_edge_prologue_bwd": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _i32, _f32, _vp,
@@ -54,7 +54,7 @@ _SIGS = {
     "gasfm_edge0_part_rows": (_i32, [_i32, _i64, _i32]),
     "gasfm_edge0_prologue_fwd": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_edge0_epilogue_fwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp,
-                                        _vp, _vp, _f32, _vp, _vp]),
+                                        _vp, _i64, _vp, _f32, _vp, _vp]),
     "gasfm_edge0_epilogue_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _f32, _vp, _vp,
                                         _vp, _vp, _vp]),
     "gasfm_edge0_prologue_bwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
@@ -71,7 +71,7 @@ _SIGS = {
                                    _vp]),
     "gasfm_view_tail_bwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_view_hub_fwd": (_i32, [_vp, _i64, _i32, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                  _vp, _vp, _vp, _vp]),
+                                  _vp, _i32, _vp, _vp, _vp]),
     "gasfm_view_hub_bwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp, _vp, _vp, _vp]),
     "gasfm_gvec_multi_fwd": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp]),
@@ -445,12 +445,23 @@ def edge_prologue_fwd(P, ln_w, ln_b, eps, W, b, Y, pos=None, W2=None, b2=None):
     check(st, "gasfm_edge_prologue_fwd")
 
 
+def _rows32(t, name):
+    """[rows, 32] float32 CUDA rows with unit column stride (row stride >= 32: a column slice of a
+    gathered [SV | XR] block is fine); returns the row stride."""
+    if not t.is_cuda or t.dtype != torch.float32 or t.dim() != 2 or t.shape[1] != 32 or t.stride(1) != 1 \
+            or (t.shape[0] > 1 and t.stride(0) < 32):
+        raise TypeError(f"{name}: expected [rows, 32] float32 CUDA rows with unit column stride")
+    return t.stride(0) if t.shape[0] > 1 else 32
+
+
 def edge_epilogue_fwd(P, P0, cam, pt, ln_w, ln_b, eps, Wp, bp, Sp, Sv, Sg, scale, out):
     _req(P, "P", 32)
-    for t, n in ((Sp, "Sp"), (Sv, "Sv"), (Sg, "Sg"), (Wp, "Wp")):
+    for t, n in ((Sp, "Sp"), (Sg, "Sg"), (Wp, "Wp")):
         _req(t, n)
+    ldSv = _rows32(Sv, "Sv")
     st = lib().gasfm_edge_epilogue_fwd(_p(P), _p(P0), _p(cam), _p(pt), P.shape[0], _p(ln_w), _p(ln_b), eps, _p(Wp),
-                                       Wp.shape[1], _p(bp), _p(Sp), _p(Sv), _p(Sg), scale, _p(out), _stream(P))
+                                       Wp.shape[1], _p(bp), _p(Sp), _p(Sv), ldSv, _p(Sg), scale, _p(out),
+                                       _stream(P))
     check(st, "gasfm_edge_epilogue_fwd")
 
 
@@ -489,11 +500,12 @@ def edge0_prologue_fwd(P, ln_w, ln_b, eps, W0, b0, XL, pos=None):
 
 def edge0_epilogue_fwd(P, cam, pt, lna_w, lna_b, lnb_w, lnb_b, eps, Wp, bp, Wsk, bsk, Sp, Sv, Sg, scale, out):
     _req(P, "P", 2)
-    for t, n in ((Sp, "Sp"), (Sv, "Sv"), (Sg, "Sg")):
+    for t, n in ((Sp, "Sp"), (Sg, "Sg")):
         _req(t, n)
+    ldSv = _rows32(Sv, "Sv")
     st = lib().gasfm_edge0_epilogue_fwd(_p(P), _p(cam), _p(pt), P.shape[0], _p(lna_w), _p(lna_b), _p(lnb_w),
-                                        _p(lnb_b), eps, _p(Wp), _p(bp), _p(Wsk), _p(bsk), _p(Sp), _p(Sv), _p(Sg),
-                                        scale, _p(out), _stream(P))
+                                        _p(lnb_b), eps, _p(Wp), _p(bp), _p(Wsk), _p(bsk), _p(Sp), _p(Sv), ldSv,
+                                        _p(Sg), scale, _p(out), _stream(P))
     check(st, "gasfm_edge0_epilogue_fwd")
 
 
@@ -649,9 +661,14 @@ def view_tail_bwd(dv, dh, x, rs, agg, Wp, ln_w, ln_b, dx, dagg, part, scratch):
 
 
 def view_hub_fwd(v, eps, gC, bC, Wv, gA, bA, Wa, ba, Wr, br, sv, t, xr, rs, scratch):
+    """sv / xr: [m, 32] with a common row stride (two column halves of one [m, 64] block, or two
+    contiguous tensors)."""
     _req(v, "v")
+    ldo = _rows32(sv, "sv")
+    if _rows32(xr, "xr") != ldo:
+        raise ValueError("view_hub_fwd: sv and xr need the same row stride")
     st = lib().gasfm_view_hub_fwd(_p(v), v.shape[0], v.shape[1], eps, _p(gC), _p(bC), _p(Wv), _p(gA), _p(bA), _p(Wa),
-                                  _p(ba), _p(Wr), _p(br), _p(sv), _p(t), _p(xr), _p(rs), _p(scratch), _stream(v))
+                                  _p(ba), _p(Wr), _p(br), _p(sv), _p(t), _p(xr), ldo, _p(rs), _p(scratch), _stream(v))
     check(st, "gasfm_view_hub_fwd")
 
 

@@ -257,11 +257,12 @@ def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True, xl_so
     return out, smax, ssum
 
 
-def attn_forward_partial(XL, XR, att, plan, heads, slope):
+def attn_forward_partial(XL, XR, att, plan, heads, slope, dst=None):
     """Un-normalised per-segment partials of an all-partial plan.
 
     Returns a packed [N, H*C + 2H] buffer (acc | max | sum) per destination segment —
-    what one rank contributes before the cross-rank combine.
+    what one rank contributes before the cross-rank combine.  dst: an [N, H*C + 2H] row view
+    (unit column stride) the merged rows are written to instead (a collective's send buffer).
     """
     assert plan.all_partial
     HC = att.numel()
@@ -274,11 +275,20 @@ def attn_forward_partial(XL, XR, att, plan, heads, slope):
     attf = att.reshape(-1).contiguous()
     _native.attn_fwd(XL, XR, attf, None, plan.perm, plan.items, plan.n_items, heads, C, slope, False, None, None,
                      None, part)
+    out = part if dst is None else dst
+    if plan.n_items == 0:  # no local edges: the empty state (acc 0, max -inf, sum 0)
+        out[:N, :HC] = 0.0
+        out[:N, HC:HC + heads] = -float("inf")
+        out[:N, HC + heads:] = 0.0
+        return out[:N]
     combine_fwd_l1(plan, part, heads, C)
     if plan.n_combine:  # merge split pieces (slots >= N) into rows [0, N), raw
-        _native.attn_combine(plan.combine, plan.n_combine, heads, C, part, None, False, part, part[:, HC:],
-                             part[:, HC + heads:], ldOut=LDP, ldStat=LDP)
-    return part[:N]
+        ld = out.stride(0) if N > 1 else LDP
+        _native.attn_combine(plan.combine, plan.n_combine, heads, C, part, None, False, out, out[:, HC:],
+                             out[:, HC + heads:], ldOut=ld, ldStat=ld)
+    elif dst is not None:
+        dst.copy_(part[:N])
+    return out[:N]
 
 
 def combine_partials(gathered, world, N, heads, bias, combine_items):
@@ -293,10 +303,12 @@ def combine_partials(gathered, world, N, heads, bias, combine_items):
 
 
 def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, gout, dXL=None, xl_sorted=False,
-                      defer=False):
+                      defer=False, dXR=None):
     """Launch the backward kernels; returns (dXL, dXR, datt[HC], dbias[HC]).
 
-    dXL is always in source-row (edge) order; xl_sorted says XL itself is in segment order."""
+    dXL is always in source-row (edge) order; xl_sorted says XL itself is in segment order.
+    dXR: optional [num_targets, HC] row view (unit column stride) to write the target-row
+    gradient into."""
     HC = att.numel()
     C = HC // heads
     dev = XL.device
@@ -305,7 +317,8 @@ def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, go
         # every source row is written exactly once when the plan's edges cover all rows
         full = plan.num_edges == XL.shape[0] == plan.src_rows
         dXL = (torch.empty if full else torch.zeros)((XL.shape[0], HC), dtype=torch.float32, device=dev)
-    dXR = torch.empty((plan.num_targets, HC), dtype=torch.float32, device=dev)
+    if dXR is None:
+        dXR = torch.empty((plan.num_targets, HC), dtype=torch.float32, device=dev)
     part = torch.empty((plan.n_part_rows, HC), dtype=torch.float32, device=dev) if plan.n_slots else None
     n_waves = _native.attn_bwd_waves(plan.n_items, heads, C)
     datt_part = torch.empty((max(n_waves, 1), 2 * HC), dtype=torch.float32, device=dev)

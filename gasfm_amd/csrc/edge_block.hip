@@ -253,7 +253,8 @@ __global__ __launch_bounds__(kThreads, GASFM_EFWD_MINWAVES) void edge_epilogue_f
     const float* __restrict__ P, const float* __restrict__ P0, const int32_t* __restrict__ cam,
     const int32_t* __restrict__ pt, int64_t E, const float* __restrict__ gam, const float* __restrict__ bet,
     float eps, const float* __restrict__ Wp, int ldWp, const float* __restrict__ bp, const float* __restrict__ Sp,
-    const float* __restrict__ Sv, const float* __restrict__ Sg, float scale, float* __restrict__ Pout) {
+    const float* __restrict__ Sv, int64_t ldSv, const float* __restrict__ Sg, float scale,
+    float* __restrict__ Pout) {
   constexpr int LD36 = 36;                   // 16-byte aligned rows for the float4 read-back
   __shared__ float Wt[F * LDW];              // Wt[k][n] = Wp[n][k], k < 32
   __shared__ float tiles[kWaves][TR * LD34 + TR * LD36];
@@ -318,7 +319,7 @@ __global__ __launch_bounds__(kThreads, GASFM_EFWD_MINWAVES) void edge_epilogue_f
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       sp[u] = *reinterpret_cast<const float4*>(Sp + int64_t(npt[u]) * F + cc);
-      sv[u] = *reinterpret_cast<const float4*>(Sv + int64_t(ncam[u]) * F + cc);
+      sv[u] = *reinterpret_cast<const float4*>(Sv + int64_t(ncam[u]) * ldSv + cc);
       q0[u] = nq[u];
       raw[u] = np[u];
     }
@@ -845,10 +846,11 @@ extern "C" int gasfm_edge_prologue_fwd(const float* P, int64_t E, const float* l
 extern "C" int gasfm_edge_epilogue_fwd(const float* P, const float* P0, const int32_t* cam, const int32_t* pt,
                                        int64_t E, const float* ln_w, const float* ln_b, float eps, const float* Wp,
                                        int32_t ldWp, const float* bp, const float* Sp, const float* Sv,
-                                       const float* Sg, float scale, float* Pout, void* stream) {
+                                       int64_t ldSv, const float* Sg, float scale, float* Pout, void* stream) {
   GASFM_REQUIRE(E >= 0 && P && cam && pt && ln_w && ln_b && Wp && bp && Sp && Sv && Sg && Pout,
                 "gasfm_edge_epilogue_fwd: null pointer");
   GASFM_REQUIRE((P0 && ldWp == 34) || (!P0 && ldWp == 32), "gasfm_edge_epilogue_fwd: ldWp=%d vs P0", ldWp);
+  GASFM_REQUIRE(ldSv >= 32 && ldSv % 4 == 0, "gasfm_edge_epilogue_fwd: ldSv=%lld", (long long)ldSv);
   GASFM_REQUIRE(aligned16(P) && aligned16(Sp) && aligned16(Sv) && aligned16(Pout) &&
                     (!P0 || reinterpret_cast<uintptr_t>(P0) % 8 == 0),
                 "gasfm_edge_epilogue_fwd: P/Sp/Sv/Pout not 16-byte aligned (P0 8-byte)");
@@ -857,7 +859,7 @@ extern "C" int gasfm_edge_epilogue_fwd(const float* P, const float* P0, const in
   const int g = resident_grid(reinterpret_cast<const void*>(&edge_epilogue_fwd_kernel), kThreads, 0, tiles_of(E),
                               kWaves);
   hipLaunchKernelGGL(edge_epilogue_fwd_kernel, dim3(g), dim3(kThreads), 0, st, P, P0, cam, pt, E, ln_w,
-                     ln_b, eps, Wp, ldWp, bp, Sp, Sv, Sg, scale, Pout);
+                     ln_b, eps, Wp, ldWp, bp, Sp, Sv, ldSv, Sg, scale, Pout);
   return launch_status("gasfm_edge_epilogue_fwd");
 }
 

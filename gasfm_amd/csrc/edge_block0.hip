@@ -97,7 +97,8 @@ __global__ __launch_bounds__(kT) void edge0_epilogue_fwd_kernel(
     const float* __restrict__ ga, const float* __restrict__ ba, const float* __restrict__ gb,
     const float* __restrict__ bbt, float eps, const float* __restrict__ Wp, const float* __restrict__ bp,
     const float* __restrict__ Wsk, const float* __restrict__ bsk, const float* __restrict__ Sp,
-    const float* __restrict__ Sv, const float* __restrict__ Sg, float scale, float* __restrict__ Pout) {
+    const float* __restrict__ Sv, int64_t ldSv, const float* __restrict__ Sg, float scale,
+    float* __restrict__ Pout) {
   const int lane = threadIdx.x & (kW - 1);
   const int c0 = 4 * (lane & 7);
   float wp[4][2], wsk[4][2], cst[4], bs[4];
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(kT) void edge0_epilogue_fwd_kernel(
     const float ha0 = fmaxf(fmaf(l.xh0, ga0, ba0), 0.f), ha1 = fmaxf(fmaf(l.xh1, ga1, ba1), 0.f);
     const float hb0 = fmaxf(fmaf(l.xh0, gb0, bb0), 0.f), hb1 = fmaxf(fmaf(l.xh1, gb1, bb1), 0.f);
     const float4 sp = *reinterpret_cast<const float4*>(Sp + int64_t(pt[e]) * 32 + c0);
-    const float4 sv = *reinterpret_cast<const float4*>(Sv + int64_t(cam[e]) * 32 + c0);
+    const float4 sv = *reinterpret_cast<const float4*>(Sv + int64_t(cam[e]) * ldSv + c0);
     const float spv[4] = {sp.x, sp.y, sp.z, sp.w}, svv[4] = {sv.x, sv.y, sv.z, sv.w};
     float o[4];
 #pragma unroll
@@ -326,14 +327,14 @@ extern "C" int gasfm_edge0_epilogue_fwd(const float* P, const int32_t* cam, cons
                                         const float* ln_a_w, const float* ln_a_b, const float* ln_b_w,
                                         const float* ln_b_b, float eps, const float* Wp, const float* bp,
                                         const float* Wsk, const float* bsk, const float* Sp, const float* Sv,
-                                        const float* Sg, float scale, float* Pout, void* stream) {
+                                        int64_t ldSv, const float* Sg, float scale, float* Pout, void* stream) {
   GASFM_REQUIRE(P && cam && pt && Wp && bp && Wsk && bsk && Sp && Sv && Sg && Pout && aligned16(Sp) &&
-                    aligned16(Sv) && aligned16(Pout),
+                    aligned16(Sv) && aligned16(Pout) && ldSv >= 32 && ldSv % 4 == 0,
                 "gasfm_edge0_epilogue_fwd: bad args");
   if (E == 0) return GASFM_OK;
   hipLaunchKernelGGL(edge0_epilogue_fwd_kernel, dim3(grid_for(E, kT / 8)), dim3(kT), 0,
                      reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const float2*>(P), cam, pt, E, ln_a_w,
-                     ln_a_b, ln_b_w, ln_b_b, eps, Wp, bp, Wsk, bsk, Sp, Sv, Sg, scale, Pout);
+                     ln_a_b, ln_b_w, ln_b_b, eps, Wp, bp, Wsk, bsk, Sp, Sv, ldSv, Sg, scale, Pout);
   return launch_status("gasfm_edge0_epilogue_fwd");
 }
 

@@ -448,7 +448,7 @@ __global__ __launch_bounds__(kSumThreads) void view_hub_fin_kernel(const float* 
                                                                    const float* __restrict__ Wr,
                                                                    const float* __restrict__ br,
                                                                    float* __restrict__ sv, float* __restrict__ to,
-                                                                   float* __restrict__ xr) {
+                                                                   float* __restrict__ xr, int ldo) {
   __shared__ float Tt[TR * L34];
   const int64_t row0 = int64_t(blockIdx.x) * TR;
   const int nrows = int(m - row0 < TR ? m - row0 : TR);
@@ -463,7 +463,7 @@ __global__ __launch_bounds__(kSumThreads) void view_hub_fin_kernel(const float* 
       Tt[e * L34 + n] = s;
       if (e < nrows) to[(row0 + e) * VA + n] = s;
     } else if (e < nrows) {
-      sv[(row0 + e) * VA + n] = s;
+      sv[(row0 + e) * ldo + n] = s;
     }
   }
   __syncthreads();
@@ -481,7 +481,7 @@ __global__ __launch_bounds__(kSumThreads) void view_hub_fin_kernel(const float* 
     const int e = 4 * g + r;
     if (e < nrows) {
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) xr[(row0 + e) * VA + nt * 16 + c] = accR[nt][r] + br[nt * 16 + c];
+      for (int nt = 0; nt < 2; ++nt) xr[(row0 + e) * ldo + nt * 16 + c] = accR[nt][r] + br[nt * 16 + c];
     }
   }
 }
@@ -832,12 +832,12 @@ extern "C" int gasfm_view_tail_bwd(const float* dv, const float* dh, const float
 extern "C" int gasfm_view_hub_fwd(const float* v, int64_t m, int32_t D, float eps, const float* gC, const float* bC,
                                   const float* Wv, const float* gA, const float* bA, const float* Wa,
                                   const float* ba, const float* Wr, const float* br, float* sv, float* t, float* xr,
-                                  float* rs, float* scratch, void* stream) {
+                                  int32_t ldo, float* rs, float* scratch, void* stream) {
   GASFM_REQUIRE(m >= 0 && width_ok(D), "gasfm_view_hub_fwd: m=%lld D=%d", (long long)m, D);
   if (m == 0) return GASFM_OK;
   GASFM_REQUIRE(v && gC && bC && Wv && gA && bA && Wa && ba && Wr && br && sv && t && xr && rs && scratch,
                 "gasfm_view_hub_fwd: null pointer");
-  GASFM_REQUIRE(aligned16(v), "gasfm_view_hub_fwd: alignment");
+  GASFM_REQUIRE(aligned16(v) && ldo >= VA, "gasfm_view_hub_fwd: alignment / ldo=%d", ldo);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t ncb = D / CB;
   float2* SP = reinterpret_cast<float2*>(scratch);
@@ -845,7 +845,7 @@ extern "C" int gasfm_view_hub_fwd(const float* v, int64_t m, int32_t D, float ep
   hipLaunchKernelGGL(view_stats_kernel, grid2(m, D), dim3(kW), 0, st, v, m, D, SP);
   hipLaunchKernelGGL(view_hub_proj_kernel, grid2(m, D), dim3(kW), 0, st, v, m, D, eps, SP, gC, bC, Wv, gA, bA, Wa,
                      PP, reinterpret_cast<float2*>(rs));
-  hipLaunchKernelGGL(view_hub_fin_kernel, grid1(m), dim3(kSumThreads), 0, st, PP, m, int(ncb), ba, Wr, br, sv, t, xr);
+  hipLaunchKernelGGL(view_hub_fin_kernel, grid1(m), dim3(kSumThreads), 0, st, PP, m, int(ncb), ba, Wr, br, sv, t, xr, ldo);
   return launch_status("gasfm_view_hub_fwd");
 }
 

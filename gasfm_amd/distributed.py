@@ -124,6 +124,14 @@ class ShardContext:
         self.emulate = bool(emulate)
         self._combine_cache = {}
 
+    def pack_items(self, specs, device):
+        """Combine items (seg 0, slot_begin, count, stride) for rows inside gathered send blocks."""
+        key = (tuple(specs), str(device))
+        if key not in self._combine_cache:
+            self._combine_cache[key] = [torch.tensor([[0, b, c, s]], dtype=torch.int32).to(device)
+                                        for b, c, s in specs]
+        return self._combine_cache[key]
+
     def combine_items(self, N, device):
         key = (N, str(device))
         if key not in self._combine_cache:
@@ -224,25 +232,42 @@ class OwnRowsFn(torch.autograd.Function):
         return shard.all_gather(_pad_rows(g, chunk))[:m], None
 
 
+def _packed_block(xs):
+    """The [rows, sum of widths] block when the 2-D tensors xs are consecutive column ranges of one
+    row-major buffer (ViewHubFn(packed=True)'s SV | XR), else None."""
+    if len(xs) < 2 or any(x.dim() != 2 or x.stride(1) != 1 for x in xs):
+        return None
+    rows, tot = xs[0].shape[0], sum(x.shape[1] for x in xs)
+    at = 0
+    for x in xs:
+        if x.shape[0] != rows or (rows > 1 and x.stride(0) != tot) or \
+                x.data_ptr() != xs[0].data_ptr() + at * x.element_size():
+            return None
+        at += x.shape[1]
+    return xs[0].as_strided((rows, tot), (tot, 1))
+
+
 class GatherRowsFn(torch.autograd.Function):
     """Own camera rows of several [own, w_k] tensors -> the full [m, w_k] tensors, with ONE
-    all-gather of their concatenation; the backward slices the own rows of each gradient (the
-    gradients arriving here are already summed over ranks: AllReduceGradN downstream, or
-    replicated losses)."""
+    all-gather of their concatenation (no concatenation when they already are one row block:
+    ViewHubFn(packed=True)); 2-D outputs are column views of the gathered block.  The backward
+    slices the own rows of each gradient (the gradients arriving here are already summed over
+    ranks: AllReduceGradN downstream, or replicated losses)."""
 
     @staticmethod
     def forward(ctx, shard, *xs):
         ctx.shard = shard
-        ctx.widths = [x.shape[1] for x in xs]
-        ctx.shapes = [x.shape for x in xs]
         _, _, chunk, m = shard.cams
-        flat = torch.cat([x.reshape(x.shape[0], -1) for x in xs], 1) if len(xs) > 1 else xs[0].reshape(
-            xs[0].shape[0], -1)
+        flat = _packed_block(xs)
+        if flat is None:
+            flat = torch.cat([x.reshape(x.shape[0], -1) for x in xs], 1) if len(xs) > 1 else xs[0].reshape(
+                xs[0].shape[0], -1)
         full = shard.all_gather(_pad_rows(flat, chunk))[:m]
         out, at = [], 0
         for x in xs:
             k = int(np.prod(x.shape[1:]))
-            out.append(full[:, at:at + k].reshape((m,) + tuple(x.shape[1:])).contiguous())
+            o = full[:, at:at + k]
+            out.append(o if x.dim() == 2 else o.reshape((m,) + tuple(x.shape[1:])))
             at += k
         return tuple(out)
 
@@ -306,33 +331,58 @@ class ShardedGlobalAttentionFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, XLv, XRv, att_v, bias_v, XLp, XRp, att_p, bias_p, plans, heads, slope, shard):
+        """-> [1, HCv + HCp]: the two aggregates side by side (the global MLP's input)."""
         plan_v, plan_vp, plan_p, plan_pp = plans
-        part_v = attn_forward_partial(XLv, XRv, att_v, plan_vp, heads, slope)
-        part_p = attn_forward_partial(XLp, XRp, att_p, plan_pp, heads, slope)
-        wv, wp = part_v.shape[1], part_p.shape[1]
-        g = shard.all_gather(torch.cat([part_v, part_p], 1))
-        items = shard.combine_items(1, XLv.device)
-        out_v, mv, sv = combine_partials(g[:, :wv].contiguous(), shard.world, 1, heads, bias_v, items)
-        out_p, mp, sp = combine_partials(g[:, wv:wv + wp].contiguous(), shard.world, 1, heads, bias_p, items)
-        ctx.plans, ctx.heads, ctx.slope, ctx.shard = (plan_v, plan_p), heads, slope, shard
+        HCv, HCp = att_v.numel(), att_p.numel()
+        Lv, Lp = HCv + 2 * heads, HCp + 2 * heads
+        dev = XLv.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        B, ov = _pack_layout(Lv, Lp)
+        # both partial rows straight into one send block: v at float 0, p at float ov, B floats
+        # per rank, so that in the gathered [W*B] buffer rank r's rows are slots r*B/Lv (v) and
+        # (r*B + ov)/Lp (p) of row width Lv / Lp: the combines read them in place
+        pack = torch.empty(B, **f32)
+        attn_forward_partial(XLv, XRv, att_v, plan_vp, heads, slope, dst=pack[:Lv].view(1, Lv))
+        attn_forward_partial(XLp, XRp, att_p, plan_pp, heads, slope, dst=pack[ov:ov + Lp].view(1, Lp))
+        g = shard.all_gather(pack.view(1, B)).view(-1)
+        xcat = torch.empty((1, HCv + HCp), **f32)
+        stats = torch.empty((4, heads), **f32)
+        W = shard.world
+        items = shard.pack_items(((0, W, B // Lv), (ov // Lp, W, B // Lp)), dev)
+        _native.attn_combine(items[0], 1, heads, HCv // heads, g.view(-1, Lv), bias_v, True, xcat[:, :HCv],
+                             stats[0:1], stats[1:2])
+        _native.attn_combine(items[1], 1, heads, HCp // heads, g.view(-1, Lp), bias_p, True, xcat[:, HCv:],
+                             stats[2:3], stats[3:4])
+        ctx.plans, ctx.heads, ctx.slope, ctx.shard, ctx.HCv = (plan_v, plan_p), heads, slope, shard, HCv
         ctx.defer = _native.defer_token(att_v, bias_v, att_p, bias_p)
-        ctx.save_for_backward(XLv, XRv, att_v, bias_v, out_v, mv, sv, XLp, XRp, att_p, bias_p, out_p, mp, sp)
-        return out_v, out_p
+        ctx.save_for_backward(XLv, XRv, att_v, bias_v, XLp, XRp, att_p, bias_p, xcat, stats)
+        return xcat
 
     @staticmethod
-    def backward(ctx, gv, gp):
-        XLv, XRv, att_v, bias_v, out_v, mv, sv, XLp, XRp, att_p, bias_p, out_p, mp, sp = ctx.saved_tensors
+    def backward(ctx, g):
+        XLv, XRv, att_v, bias_v, XLp, XRp, att_p, bias_p, xcat, stats = ctx.saved_tensors
         plan_v, plan_p = ctx.plans
-        gv = gv if gv is not None else torch.zeros_like(out_v)
-        gp = gp if gp is not None else torch.zeros_like(out_p)
-        dXLv, dXRv, dattv, dbv = attn_backward_raw(XLv, XRv, att_v, bias_v, plan_v, ctx.heads, ctx.slope, out_v, mv,
-                                                   sv, gv, defer=ctx.defer)
-        dXLp, dXRp, dattp, dbp = attn_backward_raw(XLp, XRp, att_p, bias_p, plan_p, ctx.heads, ctx.slope, out_p, mp,
-                                                   sp, gp, defer=ctx.defer)
-        wv = dXRv.shape[1]
-        flat = ctx.shard.all_reduce_(torch.cat([dXRv, dXRp], 1))
-        return (dXLv, flat[:, :wv], dattv.view_as(att_v), dbv, dXLp, flat[:, wv:], dattp.view_as(att_p), dbp,
+        HCv = ctx.HCv
+        g = g.contiguous()
+        flat = torch.empty_like(xcat)  # [dXRv | dXRp]: the all-reduce payload, written in place
+        dXLv, _, dattv, dbv = attn_backward_raw(XLv, XRv, att_v, bias_v, plan_v, ctx.heads, ctx.slope,
+                                                xcat[:, :HCv], stats[0:1], stats[1:2], g[:, :HCv],
+                                                defer=ctx.defer, dXR=flat[:, :HCv])
+        dXLp, _, dattp, dbp = attn_backward_raw(XLp, XRp, att_p, bias_p, plan_p, ctx.heads, ctx.slope,
+                                                xcat[:, HCv:], stats[2:3], stats[3:4], g[:, HCv:],
+                                                defer=ctx.defer, dXR=flat[:, HCv:])
+        ctx.shard.all_reduce_(flat)
+        return (dXLv, flat[:, :HCv], dattv.view_as(att_v), dbv, dXLp, flat[:, HCv:], dattp.view_as(att_p), dbp,
                 None, None, None, None)
+
+
+def _pack_layout(a, b):
+    """(B, ov): a send block of B floats holding an a-float row at 0 and a b-float row at ov, with
+    B a multiple of both a and b and ov of b (rows stay addressable as slots after the gather)."""
+    from math import gcd
+    lcm = a * b // gcd(a, b)
+    ov = -(-a // b) * b
+    return lcm * max(1, -(-(ov + b) // lcm)), ov
 
 
 def partition_points(pt, n, world):

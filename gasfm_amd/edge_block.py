@@ -24,6 +24,11 @@ from .attention import attn_backward_raw, attn_forward_partial, attn_forward_raw
 PROJ_SCALE = 0.25  # the "/ 4" of layers.py:945
 
 
+def _rows(t):
+    """Row block with unit column stride (a column slice of a gathered [SV | XR] block stays a view)."""
+    return t if t.dim() == 2 and t.stride(1) == 1 and t.stride(0) >= t.shape[1] else t.contiguous()
+
+
 class EdgePrologueFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, P, ln_w, ln_b, W, b, Wp, eps, pos=None, W2=None, b2=None):
@@ -125,7 +130,7 @@ class EdgeEpilogueFn(torch.autograd.Function):
         out = torch.empty_like(P)
         Wp_c = Wp.contiguous()
         _native.edge_epilogue_fwd(P, P0, edges.cam, edges.pt, ln_w, ln_b, eps, Wp_c, bp.contiguous(),
-                                  Sp.contiguous(), Sv.contiguous(), Sg.reshape(-1).contiguous(), PROJ_SCALE, out)
+                                  Sp.contiguous(), _rows(Sv), Sg.reshape(-1).contiguous(), PROJ_SCALE, out)
         ctx.eps = eps
         ctx.edges = edges
         ctx.sg_shape = Sg.shape
@@ -196,7 +201,7 @@ class Block0EpilogueFn(torch.autograd.Function):
         out = torch.empty((P.shape[0], Wp.shape[0]), dtype=torch.float32, device=P.device)
         _native.edge0_epilogue_fwd(P, edges.cam, edges.pt, lna_w, lna_b, lnb_w, lnb_b, eps, Wp.contiguous(),
                                    bp.contiguous(), Wsk.contiguous(), bsk.contiguous(), Sp.contiguous(),
-                                   Sv.contiguous(), Sg.reshape(-1).contiguous(), PROJ_SCALE, out)
+                                   _rows(Sv), Sg.reshape(-1).contiguous(), PROJ_SCALE, out)
         ctx.eps, ctx.edges, ctx.sg_shape = eps, edges, Sg.shape
         ctx.save_for_backward(P, lna_w, lna_b, lnb_w, lnb_b, Wp, Wsk)
         return out

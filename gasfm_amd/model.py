@@ -237,10 +237,10 @@ class ViewAndScenePoint2Global(Module):
         XLp = xl_pts if xl_pts is not None else dense.linear(pts, c.lin_l)
         if _cam_sharded(shard):
             from .distributed import ShardedGlobalAttentionFn
-            v2g, s2g = ShardedGlobalAttentionFn.apply(
+            x = ShardedGlobalAttentionFn.apply(
                 XLv, XRv, cv.att, cv._bias(XLv), XLp, XRp, c.att, c.bias,
                 (plan_v2g, plan_v2g_partial, plan_s2g, plan_s2g_partial), c.heads, c.negative_slope, shard)
-            return self._global_tail(torch.cat([v2g, s2g], dim=1), prev)
+            return self._global_tail(x, prev)
         v2g = gat_attention(XLv, XRv, cv.att, cv._bias(XLv), plan_v2g, cv.heads, cv.negative_slope)
         if shard is None:
             s2g = gat_attention(XLp, XRp, c.att, c._bias(XLp), plan_s2g, c.heads, c.negative_slope)
@@ -430,7 +430,7 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         if hubs:
             hv = view_block.hub_params(pfu, vsg.graph_conv_view2global, nxt.proj2view)
             if hv is not None and view_block._rows_ok(view, view.shape[1]):
-                skip, SV, XLv, XRn = view_block.hub(view, hv, getattr(self, "_proj_bf16", False))
+                skip, SV, XLv, XRn = view_block.hub(view, hv, getattr(self, "_proj_bf16", False), packed=cams)
                 if cams:  # every rank's edges read all cameras' SV and XR: one all-gather
                     from .distributed import gather_rows
                     SV, XRn = gather_rows(shard, SV, XRn)

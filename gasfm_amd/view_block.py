@@ -81,11 +81,18 @@ class ViewHubFn(torch.autograd.Function):
     """v -> (skip, SV, XL, XR)."""
 
     @staticmethod
-    def forward(ctx, v, gC, bC, Wv, Wl, bl, gA, bA, Wa, ba, Wr, br, eps, bf16=False):
+    def forward(ctx, v, gC, bC, Wv, Wl, bl, gA, bA, Wa, ba, Wr, br, eps, bf16=False, packed=False):
+        """packed: SV and XR are the two column halves of one [m, 64] block (the camera-sharded
+        path all-gathers that block as it is: distributed.GatherRowsFn)."""
         v = v.contiguous()
         Wv, Wl, Wa, Wr = (w.contiguous() for w in (Wv, Wl, Wa, Wr))
         m = v.shape[0]
-        SV, t, XR = _f32(m, A_W, like=v), _f32(m, A_W, like=v), _f32(m, A_W, like=v)
+        t = _f32(m, A_W, like=v)
+        if packed:
+            blk = _f32(m, 2 * A_W, like=v)
+            SV, XR = blk[:, :A_W], blk[:, A_W:]
+        else:
+            SV, XR = _f32(m, A_W, like=v), _f32(m, A_W, like=v)
         rs = _f32(m, 2, like=v)
         _native.view_hub_fwd(v, eps, gC, bC, Wv, gA, bA, Wa, ba, Wr, br, SV, t, XR, rs,
                              _native.view_scratch(m, v.shape[1], v.device))
@@ -129,7 +136,7 @@ class ViewHubFn(torch.autograd.Function):
         dWr = tot[o:o + A_W * A_W].view(A_W, A_W)
         o += A_W * A_W
         dba, dbr = tot[o:o + A_W], tot[o + A_W:o + 2 * A_W]
-        return dacc, dgC, dbC, dWv, dWl, dbl, dgA, dbA, dWa, dba, dWr, dbr, None, None
+        return dacc, dgC, dbC, dWv, dWl, dbl, dgA, dbA, dWa, dba, dWr, dbr, None, None, None
 
 
 def _is_ln(mod, w):
@@ -184,5 +191,5 @@ def hub_params(pfu, v2g_conv, nxt):
             linR.weight, linR.bias, lnC.eps)
 
 
-def hub(v, params, bf16=False):
-    return ViewHubFn.apply(v, *params, bf16)
+def hub(v, params, bf16=False, packed=False):
+    return ViewHubFn.apply(v, *params, bf16, packed)

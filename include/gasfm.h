@@ -192,11 +192,13 @@ int gasfm_edge_prologue_fwd(const float* P, int64_t E, const float* ln_w, const 
 
 /* P'[e] = P[e] + scale*(Wp [relu(LN(P[e])) | P0[e]] + bp + Sp[pt[e]] + Sv[cam[e]] + Sg)
  * (GraphAttnSfMProjectionFeatureUpdate.forward, layers.py:927-945, + residual 254-261;
- * scale = 1/4).  Wp [32 x ldWp], ldWp = 34 with P0 [E x 2], 32 without. */
+ * scale = 1/4).  Wp [32 x ldWp], ldWp = 34 with P0 [E x 2], 32 without.  Sv rows are ldSv
+ * floats apart (32, or 64 when Sv is the first half of a gathered [SV | XR] row block). */
 int gasfm_edge_epilogue_fwd(const float* P, const float* P0, const int32_t* cam, const int32_t* pt,
                             int64_t E, const float* ln_w, const float* ln_b, float eps,
                             const float* Wp, int32_t ldWp, const float* bp, const float* Sp,
-                            const float* Sv, const float* Sg, float scale, float* Pout, void* stream);
+                            const float* Sv, int64_t ldSv, const float* Sg, float scale, float* Pout,
+                            void* stream);
 
 /* Backward of the epilogue's reductions over the camera work items (contiguous
  * edges of one camera): dSv[cam] (partials to part_dsv for split items),
@@ -237,7 +239,7 @@ int gasfm_edge0_epilogue_fwd(const float* P, const int32_t* cam, const int32_t* 
                              const float* ln_a_w, const float* ln_a_b, const float* ln_b_w,
                              const float* ln_b_b, float eps, const float* Wp, const float* bp,
                              const float* Wsk, const float* bsk, const float* Sp, const float* Sv,
-                             const float* Sg, float scale, float* Pout, void* stream);
+                             int64_t ldSv, const float* Sg, float scale, float* Pout, void* stream);
 
 /* Camera work items: dSv (+ partial slots), aux[e] = (dP_hat_a (2), dP from the skip branch (2)),
  * per-workgroup partials of dWp, dWsk, dbsk, dgamma_b, dbeta_b. */
@@ -347,10 +349,12 @@ int gasfm_view_tail_bwd(const float* dv, const float* dh, const float* x, const 
                         int64_t m, int32_t D, const float* Wp, const float* ln_w, const float* ln_b, float* dx,
                         float* dagg, float* part, float* scratch, void* stream);
 
+/* sv and xr rows are ldo floats apart (32; 64 writes them side by side as one [m x 64] block,
+ * the camera-sharded path's all-gather payload); t is [m x 32]. */
 int gasfm_view_hub_fwd(const float* v, int64_t m, int32_t D, float eps, const float* gC, const float* bC,
                        const float* Wv, const float* gA, const float* bA, const float* Wa, const float* ba,
-                       const float* Wr, const float* br, float* sv, float* t, float* xr, float* rs, float* scratch,
-                       void* stream);
+                       const float* Wr, const float* br, float* sv, float* t, float* xr, int32_t ldo, float* rs,
+                       float* scratch, void* stream);
 
 /* dacc (in: dXL Wl, out: d v) += dres + LN_c_bwd(mask dsv Wv) + LN_a_bwd(mask dt Wa), dt = dxr Wr;
  * dres (d skip, may be null) is added in the same pass (no addmm input copy); dxl is read for the
