@@ -26,8 +26,8 @@ namespace gasfm {
 namespace {
 
 constexpr int kT = 256;       // threads per workgroup (4 waves)
-constexpr int kSlab = 64;     // columns per backward workgroup
-constexpr int kChunk = 256;   // rows per backward workgroup (64 per wave)
+constexpr int kSlab = 256;    // columns per backward workgroup (4 per lane)
+constexpr int kChunk = 128;   // rows per backward workgroup (32 per wave, requested at once)
 constexpr int kMaxK = 4096;
 constexpr int kFinT = 1024;   // finish kernel threads
 
@@ -106,64 +106,158 @@ __global__ __launch_bounds__(kT) void gvec_fwd_kernel(const float* __restrict__ 
   if (lane == 0) y[i] = acc + (b ? b[i] : 0.f) + (res ? res[i] : 0.f);
 }
 
-// dW[i, j] = dy[i] h[j];  part[chunk, j] = sum_{i in chunk} dy[i] W[i, j];  db[i] = dy[i]
+// One backward workgroup: columns [slab*kSlab, +kSlab) (4 per lane, float4), rows
+// [chunk*kChunk, +kChunk) (kChunk/4 per wave, all of a wave's W rows requested at once):
+//   dW[i, j] = dy[i] h[j];  part[chunk, j] = sum_{i in chunk} dy[i] W[i, j];  db[i] = dy[i]
+// h = relu(LN(x)) (or x); the W loads are issued before the LayerNorm statistics of x so both
+// latencies overlap.  Clamped in-range addresses, values zeroed: no per-load branch.
+__device__ __forceinline__ void gvec_bwd_body(const float* __restrict__ dy, const float* __restrict__ x, int K,
+                                              const float* __restrict__ gam, const float* __restrict__ bet,
+                                              float eps, const float* __restrict__ W, int N, float* __restrict__ dW,
+                                              float* __restrict__ db, float* __restrict__ part, int slab, int chunk,
+                                              float* scratch, float4* red) {
+  constexpr int RW = kChunk / (kT / 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = slab * kSlab + 4 * lane;
+  const bool jok = j < K;
+  const int jc = jok ? j : 0;
+  const int i0 = chunk * kChunk + wave * RW;
+  float4 w[RW];
+  float d[RW];
+#pragma unroll
+  for (int u = 0; u < RW; ++u) {
+    const int i = i0 + u;
+    const int ii = i < N ? i : N - 1;
+    w[u] = *reinterpret_cast<const float4*>(W + int64_t(ii) * K + jc);
+    d[u] = dy[ii];
+  }
+  float4 h = *reinterpret_cast<const float4*>(x + jc);
+  if (gam) {
+    float mean, rstd;
+    row_stats<kT>(x, K, eps, scratch, mean, rstd);
+    const float4 g4 = *reinterpret_cast<const float4*>(gam + jc), b4 = *reinterpret_cast<const float4*>(bet + jc);
+    h = make_float4(fmaxf(fmaf((h.x - mean) * rstd, g4.x, b4.x), 0.f), fmaxf(fmaf((h.y - mean) * rstd, g4.y, b4.y), 0.f),
+                    fmaxf(fmaf((h.z - mean) * rstd, g4.z, b4.z), 0.f), fmaxf(fmaf((h.w - mean) * rstd, g4.w, b4.w), 0.f));
+  }
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+#pragma unroll
+  for (int u = 0; u < RW; ++u) {
+    const int i = i0 + u;
+    const float du = i < N ? d[u] : 0.f;
+    if (i < N && jok)
+      *reinterpret_cast<float4*>(dW + int64_t(i) * K + j) = make_float4(du * h.x, du * h.y, du * h.z, du * h.w);
+    float4& a = (u & 1) ? a1 : a0;
+    a.x = fmaf(du, w[u].x, a.x);
+    a.y = fmaf(du, w[u].y, a.y);
+    a.z = fmaf(du, w[u].z, a.z);
+    a.w = fmaf(du, w[u].w, a.w);
+  }
+  red[wave * 64 + lane] = make_float4(a0.x + a1.x, a0.y + a1.y, a0.z + a1.z, a0.w + a1.w);
+  __syncthreads();
+  if (wave == 0 && jok) {
+    float4 s4 = red[lane];
+#pragma unroll
+    for (int q = 1; q < kT / 64; ++q) {
+      const float4 r = red[q * 64 + lane];
+      s4.x += r.x;
+      s4.y += r.y;
+      s4.z += r.z;
+      s4.w += r.w;
+    }
+    *reinterpret_cast<float4*>(part + int64_t(chunk) * K + j) = s4;
+  }
+  if (db && slab == 0) {
+    for (int r = threadIdx.x; r < kChunk; r += kT) {
+      const int ii = chunk * kChunk + r;
+      if (ii < N) db[ii] = dy[ii];
+    }
+  }
+}
+
 __global__ __launch_bounds__(kT) void gvec_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                       int K, const float* __restrict__ gam,
                                                       const float* __restrict__ bet, float eps,
                                                       const float* __restrict__ W, int N, float* __restrict__ dW,
                                                       float* __restrict__ db, float* __restrict__ part) {
   __shared__ float scratch[kT / 64];
-  __shared__ float red[kT / 64][kSlab];
+  __shared__ float4 red[kT];
+  gvec_bwd_body(dy, x, K, gam, bet, eps, W, N, dW, db, part, blockIdx.x, blockIdx.y, scratch, red);
+}
+
+// NV sums over the workgroup in ONE barrier round (fixed order: deterministic); scratch holds
+// nT/64 x NV floats.  Results broadcast to every thread.
+template <int nT, int NV>
+__device__ __forceinline__ void block_sums(float (&v)[NV], float* scratch) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int j = blockIdx.x * kSlab + lane;
-  float hj = x[j];
-  if (gam) {
-    float mean, rstd;
-    row_stats<kT>(x, K, eps, scratch, mean, rstd);
-    hj = fmaxf(fmaf((hj - mean) * rstd, gam[j], bet[j]), 0.f);
-  }
-  const int i0 = blockIdx.y * kChunk + wave * (kChunk / 4);
-  const int i1 = min(i0 + kChunk / 4, N);
-  // 16 rows per group: all 16 loads issued before any use (memory-level parallelism)
-  constexpr int G = 16;
-  float a0 = 0.f, a1 = 0.f;
-  for (int ib = i0; ib < i1; ib += G) {
-    float w[G], d[G];
 #pragma unroll
-    for (int u = 0; u < G; ++u) {
-      const int i = ib + u;
-      const bool live = i < i1;
-      const int ii = live ? i : i0;  // in-range address; value discarded
-      d[u] = live ? dy[ii] : 0.f;
-      w[u] = W[int64_t(ii) * K + j];
-    }
-#pragma unroll
-    for (int u = 0; u < G; ++u) {
-      const int i = ib + u;
-      if (i < i1) dW[int64_t(i) * K + j] = d[u] * hj;
-      if (u & 1)
-        a1 = fmaf(d[u], w[u], a1);
-      else
-        a0 = fmaf(d[u], w[u], a0);
-    }
-  }
-  red[wave][lane] = a0 + a1;
+  for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
   __syncthreads();
-  if (wave == 0) {
-    float s = 0.f;
+  if (lane == 0) {
 #pragma unroll
-    for (int w = 0; w < kT / 64; ++w) s += red[w][lane];
-    part[int64_t(blockIdx.y) * K + j] = s;
+    for (int k = 0; k < NV; ++k) scratch[wave * NV + k] = v[k];
   }
-  if (db && blockIdx.x == 0) {
-    for (int r = threadIdx.x; r < kChunk; r += kT) {
-      const int ii = blockIdx.y * kChunk + r;
-      if (ii < N) db[ii] = dy[ii];
-    }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < nT / 64; ++w) t += scratch[w * NV + k];
+    v[k] = t;
   }
 }
 
-// dh = sum_c part[c, :];  dx = LN_bwd(mask * dh) (+ dy if resid); dgamma, dbeta
+// dh[u] = sum over the nchunks partial rows of column threadIdx.x + u*kFinT (chunk order), the
+// chunk loop unrolled so that its loads are in flight together
+template <int PER>
+__device__ __forceinline__ void sum_parts(const float* __restrict__ part, int nchunks, int K, float (&dh)[PER]) {
+#pragma unroll
+  for (int u = 0; u < PER; ++u) dh[u] = 0.f;
+  int c = 0;
+  for (; c + 4 <= nchunks; c += 4) {
+    float t[4][PER];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int j = threadIdx.x + u * kFinT;
+        t[q][u] = j < K ? part[int64_t(c + q) * K + j] : 0.f;
+      }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int u = 0; u < PER; ++u) dh[u] += t[q][u];
+  }
+  for (; c < nchunks; ++c)
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int j = threadIdx.x + u * kFinT;
+      dh[u] += j < K ? part[int64_t(c) * K + j] : 0.f;
+    }
+}
+
+// mean / rstd of the single row x (PER values per thread already loaded): two-pass, one barrier
+// round per pass
+template <int PER>
+__device__ __forceinline__ void row_stats_reg(const float (&xv)[PER], int K, float eps, float* scratch, float& mean,
+                                              float& rstd) {
+  float s[1] = {0.f};
+#pragma unroll
+  for (int u = 0; u < PER; ++u) s[0] += xv[u];  // out-of-range entries are 0
+  block_sums<kFinT, 1>(s, scratch);
+  mean = s[0] / K;
+  float q[1] = {0.f};
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int j = threadIdx.x + u * kFinT;
+    const float d = j < K ? xv[u] - mean : 0.f;
+    q[0] = fmaf(d, d, q[0]);
+  }
+  block_sums<kFinT, 1>(q, scratch);
+  rstd = rsqrtf(q[0] / K + eps);
+}
+
+// dh = sum_c part[c, :];  dx = LN_bwd(mask * dh) (+ dy if resid); dgamma, dbeta.  Every global
+// load is issued before the first barrier; the two LayerNorm-backward row sums share one round.
 __global__ __launch_bounds__(kFinT) void gvec_bwd_finish_kernel(const float* __restrict__ part, int nchunks,
                                                                 int K, const float* __restrict__ x,
                                                                 const float* __restrict__ gam,
@@ -171,47 +265,48 @@ __global__ __launch_bounds__(kFinT) void gvec_bwd_finish_kernel(const float* __r
                                                                 const float* __restrict__ dy, int resid,
                                                                 float* __restrict__ dx, float* __restrict__ dgam,
                                                                 float* __restrict__ dbet) {
-  __shared__ float scratch[kFinT / 64];
+  __shared__ float scratch[(kFinT / 64) * 2];
   constexpr int PER = kMaxK / kFinT;
-  float dh[PER], xh[PER];
+  float dh[PER], xv[PER], gv[PER], bv[PER], rv[PER];
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
     const int j = threadIdx.x + u * kFinT;
-    float s = 0.f;
-    if (j < K)
-      for (int c = 0; c < nchunks; ++c) s += part[int64_t(c) * K + j];
-    dh[u] = s;
+    const bool in = j < K;
+    xv[u] = in ? x[j] : 0.f;
+    gv[u] = (in && gam) ? gam[j] : 0.f;
+    bv[u] = (in && gam) ? bet[j] : 0.f;
+    rv[u] = (in && resid) ? dy[j] : 0.f;
   }
+  sum_parts<PER>(part, nchunks, K, dh);
   if (gam) {
     float mean, rstd;
-    row_stats<kFinT>(x, K, eps, scratch, mean, rstd);
-    float s1 = 0.f, s2 = 0.f;
+    row_stats_reg<PER>(xv, K, eps, scratch, mean, rstd);
+    float xh[PER], sv[2] = {0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int j = threadIdx.x + u * kFinT;
-      xh[u] = 0.f;
+      xh[u] = (xv[u] - mean) * rstd;
+      const float d = (j < K && fmaf(xh[u], gv[u], bv[u]) > 0.f) ? dh[u] : 0.f;
       if (j < K) {
-        xh[u] = (x[j] - mean) * rstd;
-        const float d = fmaf(xh[u], gam[j], bet[j]) > 0.f ? dh[u] : 0.f;
         dgam[j] = d * xh[u];
         dbet[j] = d;
-        dh[u] = d * gam[j];  // now g = dh * gamma
-        s1 += dh[u];
-        s2 = fmaf(dh[u], xh[u], s2);
       }
+      dh[u] = d * gv[u];  // now g = dh * gamma
+      sv[0] += dh[u];
+      sv[1] = fmaf(dh[u], xh[u], sv[1]);
     }
-    s1 = block_sum<kFinT>(s1, scratch) / K;
-    s2 = block_sum<kFinT>(s2, scratch) / K;
+    block_sums<kFinT, 2>(sv, scratch);
+    const float s1 = sv[0] / K, s2 = sv[1] / K;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int j = threadIdx.x + u * kFinT;
-      if (j < K) dx[j] = rstd * (dh[u] - s1 - xh[u] * s2) + (resid ? dy[j] : 0.f);
+      if (j < K) dx[j] = rstd * (dh[u] - s1 - xh[u] * s2) + rv[u];
     }
   } else {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int j = threadIdx.x + u * kFinT;
-      if (j < K) dx[j] = dh[u] + (resid ? dy[j] : 0.f);
+      if (j < K) dx[j] = dh[u] + rv[u];
     }
   }
 }
@@ -309,56 +404,10 @@ __global__ __launch_bounds__(kT) void gvec_multi_bwd_kernel(GvBwdArgs a) {
   for (int q = 0; q < kMaxProb; ++q) blk0[q] = a.p[q].blk0;
   const GvBwdProb& p = a.p[find_prob(blk0, a.nprob)];
   __shared__ float scratch[kT / 64];
-  __shared__ float red[kT / 64][kSlab];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ float4 red[kT];
   const int local = int(blockIdx.x) - p.blk0;
-  const int slab = local % p.slabs, chunk = local / p.slabs;
-  const int K = p.K, N = p.N;
-  const int j = slab * kSlab + lane;
-  float hj = p.x[j];
-  if (p.gam) {
-    float mean, rstd;
-    row_stats<kT>(p.x, K, a.eps, scratch, mean, rstd);
-    hj = fmaxf(fmaf((hj - mean) * rstd, p.gam[j], p.bet[j]), 0.f);
-  }
-  const int i0 = chunk * kChunk + wave * (kChunk / 4);
-  const int i1 = min(i0 + kChunk / 4, N);
-  constexpr int G = 16;
-  float a0 = 0.f, a1 = 0.f;
-  for (int ib = i0; ib < i1; ib += G) {
-    float w[G], d[G];
-#pragma unroll
-    for (int u = 0; u < G; ++u) {
-      const int i = ib + u;
-      const bool live = i < i1;
-      const int ii = live ? i : i0;
-      d[u] = live ? p.dy[ii] : 0.f;
-      w[u] = p.W[int64_t(ii) * K + j];
-    }
-#pragma unroll
-    for (int u = 0; u < G; ++u) {
-      const int i = ib + u;
-      if (i < i1) p.dW[int64_t(i) * K + j] = d[u] * hj;
-      if (u & 1)
-        a1 = fmaf(d[u], w[u], a1);
-      else
-        a0 = fmaf(d[u], w[u], a0);
-    }
-  }
-  red[wave][lane] = a0 + a1;
-  __syncthreads();
-  if (wave == 0) {
-    float sacc = 0.f;
-#pragma unroll
-    for (int w = 0; w < kT / 64; ++w) sacc += red[w][lane];
-    p.part[int64_t(chunk) * K + j] = sacc;
-  }
-  if (p.db && slab == 0) {
-    for (int r = threadIdx.x; r < kChunk; r += kT) {
-      const int ii = chunk * kChunk + r;
-      if (ii < N) p.db[ii] = p.dy[ii];
-    }
-  }
+  gvec_bwd_body(p.dy, p.x, p.K, p.gam, p.bet, a.eps, p.W, p.N, p.dW, p.db, p.part, local % p.slabs,
+                local / p.slabs, scratch, red);
 }
 
 // groups of problems that share the input row x: dx = dres + sum over the group's problems of
@@ -385,63 +434,66 @@ struct GvFinArgs {
 };
 
 __global__ __launch_bounds__(kFinT) void gvec_multi_finish_kernel(GvFinArgs a) {
-  __shared__ float scratch[kFinT / 64];
+  // every problem's partial sums, gamma / beta and the shared row x are loaded before the first
+  // barrier; the LayerNorm-backward row sums of all problems of the group share one round
+  __shared__ float scratch[(kFinT / 64) * 2 * kMaxProb];
   const GvFinGroup& G = a.g[blockIdx.x];
   const int K = G.K;
   constexpr int PER = kMaxK / kFinT;
-  float acc[PER], xh[PER];
+  float acc[PER], xv[PER];
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
     const int j = threadIdx.x + u * kFinT;
     acc[u] = (G.dres && j < K) ? G.dres[j] : 0.f;
+    xv[u] = j < K ? G.x[j] : 0.f;
   }
-  bool stats = false;
-  float rstd = 1.f;
-  for (int q = G.p0; q < G.p0 + G.np; ++q) {
-    const GvFinProb& P = a.p[q];
-    float dh[PER];
+  float dh[kMaxProb][PER];
+  bool any_ln = false;
 #pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int j = threadIdx.x + u * kFinT;
-      float sacc = 0.f;
-      if (j < K)
-        for (int c = 0; c < P.nchunks; ++c) sacc += P.part[int64_t(c) * K + j];
-      dh[u] = sacc;
+  for (int q = 0; q < kMaxProb; ++q) {
+    if (q < G.np) {
+      sum_parts<PER>(a.p[G.p0 + q].part, a.p[G.p0 + q].nchunks, K, dh[q]);
+      any_ln |= a.p[G.p0 + q].gam != nullptr;
     }
+  }
+  float mean = 0.f, rstd = 1.f;
+  if (any_ln) row_stats_reg<PER>(xv, K, a.eps, scratch, mean, rstd);
+  float xh[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) xh[u] = (xv[u] - mean) * rstd;
+  float sv[2 * kMaxProb];
+#pragma unroll
+  for (int q = 0; q < kMaxProb; ++q) {
+    sv[2 * q] = sv[2 * q + 1] = 0.f;
+    if (q >= G.np) continue;
+    const GvFinProb& P = a.p[G.p0 + q];
     if (!P.gam) {
 #pragma unroll
-      for (int u = 0; u < PER; ++u) acc[u] += dh[u];
+      for (int u = 0; u < PER; ++u) acc[u] += dh[q][u];
       continue;
     }
-    if (!stats) {
-      float mean;
-      row_stats<kFinT>(G.x, K, a.eps, scratch, mean, rstd);
-#pragma unroll
-      for (int u = 0; u < PER; ++u) {
-        const int j = threadIdx.x + u * kFinT;
-        xh[u] = j < K ? (G.x[j] - mean) * rstd : 0.f;
-      }
-      stats = true;
-    }
-    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int j = threadIdx.x + u * kFinT;
+      float d = 0.f, g = 0.f;
       if (j < K) {
-        const float d = fmaf(xh[u], P.gam[j], P.bet[j]) > 0.f ? dh[u] : 0.f;
+        g = P.gam[j];
+        d = fmaf(xh[u], g, P.bet[j]) > 0.f ? dh[q][u] : 0.f;
         P.dgam[j] = d * xh[u];
         P.dbet[j] = d;
-        dh[u] = d * P.gam[j];
-        s1 += dh[u];
-        s2 = fmaf(dh[u], xh[u], s2);
-      } else {
-        dh[u] = 0.f;
       }
+      dh[q][u] = d * g;
+      sv[2 * q] += dh[q][u];
+      sv[2 * q + 1] = fmaf(dh[q][u], xh[u], sv[2 * q + 1]);
     }
-    s1 = block_sum<kFinT>(s1, scratch) / K;
-    s2 = block_sum<kFinT>(s2, scratch) / K;
+  }
+  if (any_ln) block_sums<kFinT, 2 * kMaxProb>(sv, scratch);
 #pragma unroll
-    for (int u = 0; u < PER; ++u) acc[u] += rstd * (dh[u] - s1 - xh[u] * s2);
+  for (int q = 0; q < kMaxProb; ++q) {
+    if (q >= G.np || !a.p[G.p0 + q].gam) continue;
+    const float s1 = sv[2 * q] / K, s2 = sv[2 * q + 1] / K;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) acc[u] += rstd * (dh[q][u] - s1 - xh[u] * s2);
   }
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
@@ -459,7 +511,7 @@ extern "C" int gasfm_gvec_bwd_chunks(int32_t N) { return N <= 0 ? 0 : (N + kChun
 
 extern "C" int gasfm_gvec_fwd(const float* x, int32_t K, const float* ln_w, const float* ln_b, float eps,
                               const float* W, const float* b, int32_t N, const float* res, float* y, void* stream) {
-  GASFM_REQUIRE(K > 0 && K <= kMaxK && K % kSlab == 0 && N > 0, "gasfm_gvec_fwd: K=%d (multiple of 64, <= %d), N=%d",
+  GASFM_REQUIRE(K > 0 && K <= kMaxK && K % 64 == 0 && N > 0, "gasfm_gvec_fwd: K=%d (multiple of 64, <= %d), N=%d",
                 K, kMaxK, N);
   GASFM_REQUIRE(x && W && y && (!ln_w || ln_b), "gasfm_gvec_fwd: null pointer");
   GASFM_REQUIRE(aligned16(W), "gasfm_gvec_fwd: W not 16-byte aligned");
@@ -471,13 +523,13 @@ extern "C" int gasfm_gvec_fwd(const float* x, int32_t K, const float* ln_w, cons
 extern "C" int gasfm_gvec_bwd(const float* dy, const float* x, int32_t K, const float* ln_w, const float* ln_b,
                               float eps, const float* W, int32_t N, int32_t resid, float* dx, float* dW, float* db,
                               float* dgam, float* dbet, float* part, void* stream) {
-  GASFM_REQUIRE(K > 0 && K <= kMaxK && K % kSlab == 0 && N > 0, "gasfm_gvec_bwd: K=%d, N=%d", K, N);
+  GASFM_REQUIRE(K > 0 && K <= kMaxK && K % 64 == 0 && N > 0, "gasfm_gvec_bwd: K=%d, N=%d", K, N);
   GASFM_REQUIRE(dy && x && W && dx && dW && part && (!ln_w || (ln_b && dgam && dbet)),
                 "gasfm_gvec_bwd: null pointer");
   GASFM_REQUIRE(!resid || N == K, "gasfm_gvec_bwd: residual needs N == K");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int chunks = (N + kChunk - 1) / kChunk;
-  hipLaunchKernelGGL(gvec_bwd_kernel, dim3(K / kSlab, chunks), dim3(kT), 0, st, dy, x, K, ln_w, ln_b, eps, W, N, dW, db,
+  hipLaunchKernelGGL(gvec_bwd_kernel, dim3((K + kSlab - 1) / kSlab, chunks), dim3(kT), 0, st, dy, x, K, ln_w, ln_b, eps, W, N, dW, db,
                      part);
   int s = launch_status("gasfm_gvec_bwd");
   if (s != GASFM_OK) return s;
@@ -486,7 +538,7 @@ extern "C" int gasfm_gvec_bwd(const float* dy, const float* x, int32_t K, const 
   return launch_status("gasfm_gvec_bwd_finish");
 }
 
-static bool gv_shape_ok(int K, int N) { return K > 0 && K <= kMaxK && K % kSlab == 0 && N > 0; }
+static bool gv_shape_ok(int K, int N) { return K > 0 && K <= kMaxK && K % 64 == 0 && N > 0; }
 
 extern "C" int gasfm_gvec_multi_fwd(int32_t nprob, const float* const* x, const float* const* ln_w,
                                     const float* const* ln_b, const float* const* W, const float* const* b,
@@ -531,7 +583,7 @@ extern "C" int gasfm_gvec_multi_bwd(int32_t nprob, const float* const* dy, const
     GASFM_REQUIRE(gv_shape_ok(K[q], N[q]), "gasfm_gvec_multi_bwd: problem %d K=%d N=%d", q, K[q], N[q]);
     GASFM_REQUIRE(dy[q] && x[q] && W[q] && dW[q] && part[q] && (!ln_w[q] || (ln_b[q] && dgam[q] && dbet[q])),
                   "gasfm_gvec_multi_bwd: problem %d pointers", q);
-    const int slabs = K[q] / kSlab, chunks = (N[q] + kChunk - 1) / kChunk;
+    const int slabs = (K[q] + kSlab - 1) / kSlab, chunks = (N[q] + kChunk - 1) / kChunk;
     a.p[q] = GvBwdProb{dy[q], x[q], ln_w[q], ln_b[q], W[q], dW[q], db[q], part[q], K[q], N[q], blocks, slabs};
     blocks += slabs * chunks;
     f.p[q] = GvFinProb{part[q], ln_w[q], ln_b[q], dgam[q], dbet[q], chunks};
