@@ -39,7 +39,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1_pmc_attn_fwd.json")
+PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r2_pmc_attn_fwd.json")
 
 
 def pmc_traffic(E, N):
@@ -278,7 +278,7 @@ def main():
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                          "traffic": pmc_traffic(e_local, n_local),
-                         "traffic_source": "profiles/r1_pmc_attn_fwd.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                         "traffic_source": "profiles/r2_pmc_attn_fwd.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                                            "passes of this bench, per launch)",
                          "algorithmic_bytes": bytes_per_launch, "mean_us": kern_ms * 1e3 if kern_ms else None,
                          "mean_us_back_to_back": b2b_ms * 1e3 if b2b_ms else None,

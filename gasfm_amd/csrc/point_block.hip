@@ -409,24 +409,27 @@ __global__ __launch_bounds__(kThreads8) void point_tail_bwd_kernel(
 }
 
 // ----------------------------------------------------------------------------- hub
+// With the C part (the usual case) 8 waves share the 50 KB of staged weights: 121 KB of LDS, one
+// workgroup = 2 waves per SIMD (4 waves were 1 per SIMD at 87 KB).
 template <bool HC>
-__global__ __launch_bounds__(kThreads) void point_hub_fwd_kernel(
+__global__ __launch_bounds__(HC ? kThreads8 : kThreads) void point_hub_fwd_kernel(
     const float* __restrict__ X, int64_t N, float eps, const float* __restrict__ gA, const float* __restrict__ bA,
     const float* __restrict__ WA, float* __restrict__ SA, const float* __restrict__ WB,
     const float* __restrict__ bB, float* __restrict__ XL, const float* __restrict__ gC,
     const float* __restrict__ bC, const float* __restrict__ WC, const float* __restrict__ bWC,
     const float* __restrict__ WD, const float* __restrict__ bD, float* __restrict__ XR) {
+  constexpr int NW = HC ? kWaves8 : kWaves, NT = NW * kW;
   constexpr int PW = TR * L66 + 2 * TR * L34 + 2 * TR;  // Raw (then XL staging), Tt (t, then XR), So (SA), MS, RS
   __shared__ float WAt[FP * L48];               // WAt[k][j] = W_A[j][k]
   __shared__ float WBt[FP * L80];               // WBt[k][o] = W_B[o][k]
   __shared__ float WCt[HC ? FP * L48 : 1];      // WCt[k][j] = W_C[j][k]
   __shared__ float WDt[HC ? FA * L48 : 1];      // WDt[k][j] = W_D[j][k]
   __shared__ float GB[4 * FP];                  // gamma_A beta_A gamma_C beta_C
-  __shared__ float tiles[kWaves * PW];
+  __shared__ float tiles[NW * PW];
   {
-    Stage<FA * FP, kThreads> sa, sc;
-    Stage<FP * FP, kThreads> sb;
-    Stage<FA * FA, kThreads> sd;
+    Stage<FA * FP, NT> sa, sc;
+    Stage<FP * FP, NT> sb;
+    Stage<FA * FA, NT> sd;
     sa.load([&](int q) { return WA[q]; });
     sb.load([&](int q) { return WB[q]; });
     if (HC) {
@@ -463,7 +466,7 @@ __global__ __launch_bounds__(kThreads) void point_hub_fwd_kernel(
     bDv[nt] = HC ? bD[nt * 16 + c] : 0.f;
   }
   const int64_t ntiles = (N + TR - 1) / TR;
-  const int64_t gw = int64_t(blockIdx.x) * kWaves + wave, nw = int64_t(gridDim.x) * kWaves;
+  const int64_t gw = int64_t(blockIdx.x) * NW + wave, nw = int64_t(gridDim.x) * NW;
   float4 vx[4];  // next-tile register prefetch (see point_tail_fwd_kernel)
   auto fetch = [&](int64_t tt) {
     const int64_t r0 = tt * TR;
@@ -1016,7 +1019,7 @@ extern "C" int gasfm_point_hub_fwd(const float* X, int64_t N, float eps, const f
   GASFM_REQUIRE(aligned16(X), "gasfm_point_hub_fwd: alignment");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (hc)
-    hipLaunchKernelGGL(point_hub_fwd_kernel<true>, dim3(grid4(&point_hub_fwd_kernel<true>, N)), dim3(kThreads), 0,
+    hipLaunchKernelGGL(point_hub_fwd_kernel<true>, dim3(grid8(&point_hub_fwd_kernel<true>, N)), dim3(kThreads8), 0,
                        st, X, N, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR);
   else
     hipLaunchKernelGGL(point_hub_fwd_kernel<false>, dim3(grid4(&point_hub_fwd_kernel<false>, N)), dim3(kThreads), 0,

@@ -1,4 +1,5 @@
-"""Per-launch HBM traffic of attn_fwd_kernel<32,8> from two rocprofv3 --pmc passes.
+"""Per-launch HBM traffic of the 32-wide attention forward (attn_fwd_grp_kernel / the glds
+Geom<32,8> kernel) from two rocprofv3 --pmc passes.
 
 usage: python tools/pmc_summary.py <FETCH_SIZE dir> <WRITE_SIZE dir> <out.json>
 
@@ -25,7 +26,8 @@ def per_launch(d, counter):
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if "Geom<32, 8>" not in row["Kernel_Name"] or row["Counter_Name"] != counter:
+                name = row["Kernel_Name"]
+                if not ("attn_fwd_grp_kernel" in name or "Geom<32, 8>" in name) or row["Counter_Name"] != counter:
                     continue
                 k = int(row["Dispatch_Id"])
                 vals[k] = vals.get(k, 0.0) + float(row["Counter_Value"])

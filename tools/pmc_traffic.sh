@@ -9,4 +9,4 @@ for C in FETCH_SIZE WRITE_SIZE; do
     -d $ROOT/gpurun_out/pmc_$C -o run -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline \
     > $ROOT/gpurun_out/pmc_$C.log 2>&1
 done
-cd $ROOT && python tools/pmc_summary.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE gpurun_out/pmc_attn_fwd.json
+cd $ROOT && python tools/pmc_summary.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE gpurun_out/pmc_attn_fwd.json && cp gpurun_out/pmc_attn_fwd.json profiles/r2_pmc_attn_fwd.json
