@@ -102,6 +102,40 @@ def is_local_param(name, cameras=False):
     return any(fnmatch.fnmatchcase(name, p) for p in LOCAL_PARAM_PATTERNS)
 
 
+class AsyncGradReducer:
+    """Overlaps the camera-sharded path's large weight-gradient all-reduces with the rest of the
+    backward: a post-accumulate-grad hook on each 1024 x 1024 view-side weight (Proj2View's MLP,
+    graph_conv_view2global.lin_l, the view head: 113 of the 120 MB of partial gradients at the
+    learning conf) hands its fresh .grad over as soon as autograd has set it; it is all-reduced
+    in place, asynchronously on RCCL's stream, while the backward of the blocks below runs.
+    ``sync_grads`` waits for them and leaves them out of its bucket.  Armed only when every .grad
+    was unset at forward time (each hooked .grad is then that pass's gradient alone)."""
+
+    def __init__(self, shard):
+        self.shard = shard
+        self.works = []
+        self.ptrs = set()
+
+    def launch(self, t):
+        if t.data_ptr() in self.ptrs:  # a second accumulation into a tensor already in flight
+            raise RuntimeError("camera-sharded backward: a parameter's gradient was accumulated twice in one pass "
+                               "(several forwards before one backward); run forward/backward/sync_grads per step")
+        sh = self.shard
+        if sh.emulate:
+            self.ptrs.add(t.data_ptr())
+            return
+        if sh._staged(t):  # gloo: synchronous host staging
+            sh.all_reduce_(t)
+        else:
+            self.works.append(dist.all_reduce(t, group=sh.group, async_op=True))
+        self.ptrs.add(t.data_ptr())
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.works.clear()
+
+
 def camera_rows(m, world, rank):
     """Contiguous equal camera chunks: (c0, c1, chunk) of rank ``rank``; the last chunk may be short."""
     chunk = -(-m // world)
@@ -468,6 +502,15 @@ class ShardedGraphAttnSfMNet(torch.nn.Module):
         self.cameras = cameras
         self.local_names = [k for k, _ in net.named_parameters() if is_local_param(k, cameras)]
         self._emulate = None
+        self._reducer = None
+        if cameras:  # the large partial gradients are all-reduced as soon as they exist
+            for k, p in net.named_parameters():
+                if k in self.local_names and p.dim() == 2 and p.numel() >= 1 << 20:
+                    p.register_post_accumulate_grad_hook(self._reduce_hook)
+
+    def _reduce_hook(self, p):
+        if self._reducer is not None:
+            self._reducer.launch(p.grad)
 
     def forward(self, data):
         shard = data.shard
@@ -475,16 +518,25 @@ class ShardedGraphAttnSfMNet(torch.nn.Module):
             raise ValueError("ShardedGraphAttnSfMNet(cameras=...) must match shard_scene(..., cameras=...)")
         shard.group = self.group
         self._emulate = shard if shard.emulate else None
+        self._reducer = None
+        if self.cameras and torch.is_grad_enabled() and all(p.grad is None for p in self.net.parameters()):
+            self._reducer = AsyncGradReducer(shard)
         return self.net.forward(data, shard=shard, partial_plans=data.partial_plans)
 
     def sync_grads(self):
         """One all-reduce of every rank-local parameter's gradient, in a fixed layout: a parameter
         without a gradient on this rank contributes zeros (and gets the summed gradient), so all
         ranks reduce buffers of the same size and order."""
+        red = getattr(self, "_reducer", None)
+        self._reducer = None
+        if red is not None:
+            red.wait()
         if self._emulate is None and dist.get_world_size(self.group) == 1:
             return
         params = dict(self.net.named_parameters())
-        ps = [params[k] for k in self.local_names]
+        done = red.ptrs if red is not None else ()
+        ps = [params[k] for k in self.local_names
+              if params[k].grad is None or params[k].grad.data_ptr() not in done]
         if not ps:
             return
         dev = ps[0].device
