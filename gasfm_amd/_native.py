@@ -116,6 +116,7 @@ _SIGS = {
     "gasfm_point_hub_bwd_c": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_point_hub_bwd_ab": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_gemm_bf16": (_i32, [_i32, _i32, _i32, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _i64, _vp]),
+    "gasfm_gemm_f32": (_i32, [_i32, _i32, _i32, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _i64, _vp]),
 }
 
 _lib = None
@@ -949,27 +950,37 @@ def sum_n(tensors):
     return out
 
 
+def _gemm(fn, what, a, b, cin=None, bias=None, out=None):
+    for t, nm in ((a, what + " a"), (b, what + " b")):
+        if not (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2):
+            raise ValueError(f"{nm}: fp32 CUDA matrix required")
+    M, K = a.shape
+    K2, N = b.shape
+    if K2 != K:
+        raise ValueError(f"{what}: inner dimensions {K} and {K2} differ")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    if cin is not None and (cin.shape != (M, N) or cin.stride(1) != 1):
+        raise ValueError(f"{what}: cin must be [M, N] with unit column stride")
+    if bias is not None and (bias.shape != (N,) or not bias.is_contiguous()):
+        raise ValueError(f"{what}: bias must be a contiguous [N] vector")
+    if out.shape != (M, N) or out.stride(1) != 1:
+        raise ValueError(f"{what}: out must be [M, N] with unit column stride")
+    st = fn(M, N, K, _p(a), a.stride(0), a.stride(1), _p(b), b.stride(0), b.stride(1), _p(cin),
+            cin.stride(0) if cin is not None else 0, _p(bias), _p(out), out.stride(0), _stream(out))
+    check(st, what)
+    return out
+
+
 def gemm_bf16(a, b, cin=None, bias=None, out=None):
     """out = a @ b (+ cin) (+ bias) on bf16 MFMA with fp32 accumulation (gasfm_gemm_bf16).
 
     a [M, K], b [K, N]: fp32 CUDA tensors, each with a unit stride along one dimension (plain
     row-major tensors and their .t() views both qualify: x @ W.t(), dy @ W, dy.t() @ x)."""
-    for t, what in ((a, "gemm_bf16 a"), (b, "gemm_bf16 b")):
-        if not (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2):
-            raise ValueError(f"{what}: fp32 CUDA matrix required")
-    M, K = a.shape
-    K2, N = b.shape
-    if K2 != K:
-        raise ValueError(f"gemm_bf16: inner dimensions {K} and {K2} differ")
-    if out is None:
-        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
-    if cin is not None and (cin.shape != (M, N) or cin.stride(1) != 1):
-        raise ValueError("gemm_bf16: cin must be [M, N] with unit column stride")
-    if bias is not None and (bias.shape != (N,) or not bias.is_contiguous()):
-        raise ValueError("gemm_bf16: bias must be a contiguous [N] vector")
-    if out.stride(1) != 1:
-        raise ValueError("gemm_bf16: out must have a unit column stride")
-    st = lib().gasfm_gemm_bf16(M, N, K, _p(a), a.stride(0), a.stride(1), _p(b), b.stride(0), b.stride(1), _p(cin),
-                               cin.stride(0) if cin is not None else 0, _p(bias), _p(out), out.stride(0), _stream(out))
-    check(st, "gasfm_gemm_bf16")
-    return out
+    return _gemm(lib().gasfm_gemm_bf16, "gasfm_gemm_bf16", a, b, cin, bias, out)
+
+
+def gemm_f32(a, b, cin=None, bias=None, out=None):
+    """out = a @ b (+ cin) (+ bias) in fp32 on v_mfma_f32_16x16x4_f32 (gasfm_gemm_f32); same
+    operand rules as gemm_bf16.  out may be cin (accumulate in place)."""
+    return _gemm(lib().gasfm_gemm_f32, "gasfm_gemm_f32", a, b, cin, bias, out)

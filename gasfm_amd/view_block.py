@@ -16,6 +16,8 @@ fused), forward and both backward products.  Everything around them -- LayerNorm
 32-wide projections, residual adds, bias / LayerNorm-affine gradient reductions -- runs in the
 four kernels.
 """
+import os
+
 import torch
 
 from . import _native
@@ -29,13 +31,25 @@ def _f32(*shape, like):
     return torch.empty(shape, dtype=torch.float32, device=like.device)
 
 
-def _mm(a, b, cin=None, bias=None, bf16=False):
-    """a @ b (+ cin) (+ bias): bf16 MFMA kernel or fp32 hipBLASLt."""
+# fp32 camera-side GEMMs: "torch" = hipBLASLt (default), "hip" = csrc/gemm_f32.hip.  Measured
+# (tools/gemm_bench.py, MI355X): at m = 1000 hipBLASLt 25-28 us vs 35-43 us for the HIP kernel;
+# at m = 125 the HIP kernel 12-16 us vs 19 us standalone, but the whole emulated rank-of-8 step
+# 10.33 ms vs 9.97 ms with hipBLASLt, so hipBLASLt stays the default.
+FP32_GEMM = os.environ.get("GASFM_VIEW_GEMM", "torch")
+
+
+def _mm(a, b, cin=None, bias=None, bf16=False, out=None):
+    """a @ b (+ cin) (+ bias): the bf16 MFMA kernel, the fp32 MFMA kernel or fp32 hipBLASLt;
+    out may be cin (accumulate in place)."""
     if bf16:
-        return _native.gemm_bf16(a, b, cin=cin, bias=bias)
+        return _native.gemm_bf16(a, b, cin=cin, bias=bias, out=out)
+    if FP32_GEMM == "hip":
+        return _native.gemm_f32(a, b, cin=cin, bias=bias, out=out)
     if cin is not None:
-        return torch.addmm(cin if bias is None else cin + bias, a, b)
-    return torch.addmm(bias, a, b) if bias is not None else a @ b
+        if out is cin and bias is None:
+            return cin.addmm_(a, b)
+        return torch.addmm(cin if bias is None else cin + bias, a, b, out=out)
+    return torch.addmm(bias, a, b, out=out) if bias is not None else torch.mm(a, b, out=out)
 
 
 class ViewTailFn(torch.autograd.Function):
@@ -49,8 +63,8 @@ class ViewTailFn(torch.autograd.Function):
         rs = _f32(m, 2, like=agg)
         _native.view_tail_fwd(prev, agg, Wp, bp, ln_w, ln_b, eps, bm, x, xb, h, rs,
                               _native.view_scratch(m, D, agg.device))
-        # fp32: xb + h Wm^T accumulated in place (torch's addmm with a separate input first copies it)
-        view = _mm(h, Wm.t(), cin=xb, bf16=True) if bf16 else xb.addmm_(h, Wm.t())
+        # xb + h Wm^T accumulated in place (torch's addmm with a separate input first copies it)
+        view = _mm(h, Wm.t(), cin=xb, bf16=bf16, out=xb)
         ctx.save_for_backward(agg, x, rs, h, Wp, ln_w, ln_b, Wm)
         ctx.eps, ctx.has_prev, ctx.bf16 = eps, prev is not None, bf16
         ctx.defer = _native.defer_token(Wp, bp, ln_w, ln_b, bm)
@@ -112,9 +126,9 @@ class ViewHubFn(torch.autograd.Function):
         dXR = dXR.contiguous() if dXR is not None else zeros(A_W)
         dXL = dXL.contiguous() if dXL is not None else zeros(D)
         dres = None
-        if ctx.bf16:
-            dacc = _mm(dXL, Wl, cin=dskip, bf16=True)
-        else:  # d skip is added by the hub kernel's second pass (no addmm input copy)
+        if ctx.bf16 or FP32_GEMM == "hip":  # the MFMA kernels add d skip in their epilogue
+            dacc = _mm(dXL, Wl, cin=dskip.contiguous() if dskip is not None else None, bf16=ctx.bf16)
+        else:  # hipBLASLt: d skip is added by the hub kernel's second pass (no addmm input copy)
             dacc = dXL @ Wl
             dres = dskip.contiguous() if dskip is not None else None
         dWl = _mm(dXL.t(), v, bf16=ctx.bf16)

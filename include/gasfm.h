@@ -500,6 +500,13 @@ int gasfm_gemm_bf16(int32_t M, int32_t N, int32_t K, const float* A, int64_t sAm
                     const float* B, int64_t sBk, int64_t sBn, const float* Cin, int64_t ldCin,
                     const float* bias, float* C, int64_t ldC, void* stream);
 
+/* The same product in fp32 on v_mfma_f32_16x16x4_f32 (exact products, fixed-order fp32 sums):
+ * the camera-side D x D Linear layers at m = 1000 (one GPU) and m = 125 (a camera shard of 8).
+ * Replaces torch.addmm / mm (hipBLASLt) at layers.py:292-320, 352-358, 506-511. C may equal Cin. */
+int gasfm_gemm_f32(int32_t M, int32_t N, int32_t K, const float* A, int64_t sAm, int64_t sAk,
+                   const float* B, int64_t sBk, int64_t sBn, const float* Cin, int64_t ldCin,
+                   const float* bias, float* C, int64_t ldC, void* stream);
+
 /* ---- outlier injection (outliers.hip) -----------------------------------
  * Replaces OutlierInjector / inject_outliers (code/utils/dataset_utils.py:159-461), the per-sample
  * transform of the outlier-injected training loop (train.py:73-81, BASELINE config 5).  The
