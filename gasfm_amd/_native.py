@@ -33,6 +33,10 @@ _SIGS = {
     "gasfm_gat_attn_bwd_waves": (_i32, [_i32, _i32, _i32]),
     "gasfm_gat_attn_bwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _f32, _vp,
                                   _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _vp]),
+    "gasfm_gat_attn_bwd_lanes": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _f32, _vp,
+                                  _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _vp]),
+    "gasfm_gat_attn_fwd_lanes": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _f32, _i32,
+                                  _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
     "gasfm_gat_attn_bwd_combine": (_i32, [_vp, _i32, _i32, _vp, _vp, _i64, _vp]),
     "gasfm_colsum_ws_floats": (_i64, [_i64, _i32]),
     "gasfm_edge_part_floats": (_i32, [_i32, _i64, _i32]),
@@ -218,10 +222,12 @@ def plan_work(seg_ptr, max_piece, all_partial=False):
 
 # ---------------------------------------------------------------- device kernels
 def attn_fwd(XL, XR, att, bias, perm, items, n_items, H, C, slope, finalize, out, seg_max, seg_sum, part=None,
-             ldStat=None):
-    """part: packed partial rows [slots, H*C + 2H] (acc | max | sum) or None."""
+             ldStat=None, lanes=False):
+    """part: packed partial rows [slots, H*C + 2H] (acc | max | sum) or None.  lanes: the
+    lane-per-item kernel (H = 4, C = 1; short items: block 0's point direction)."""
     ldStat = H if ldStat is None else ldStat
-    st = lib().gasfm_gat_attn_fwd(
+    fn = lib().gasfm_gat_attn_fwd_lanes if lanes else lib().gasfm_gat_attn_fwd
+    st = fn(
         _p(XL), XL.stride(0), _p(XR), XR.stride(0), _p(att), _p(bias), _p(perm), _p(items), n_items, H, C,
         slope, int(finalize), _p(out), out.stride(0) if out is not None else 0, _p(seg_max), _p(seg_sum), ldStat,
         _p(part), _stream(XL))
@@ -242,8 +248,9 @@ def attn_bwd_waves(n_items, H, C):
 
 
 def attn_bwd(XL, XR, att, bias, perm, items, n_items, H, C, slope, out, seg_max, seg_sum, gout, dXL, dXR,
-             part_dxr, datt_part, xl_by_position=False):
-    st = lib().gasfm_gat_attn_bwd(
+             part_dxr, datt_part, xl_by_position=False, lanes=False):
+    fn = lib().gasfm_gat_attn_bwd_lanes if lanes else lib().gasfm_gat_attn_bwd
+    st = fn(
         _p(XL), XL.stride(0), _p(XR), XR.stride(0), _p(att), _p(bias), _p(perm), _p(items), n_items, H, C,
         slope, _p(out), out.stride(0), _p(seg_max), _p(seg_sum), _p(gout), gout.stride(0), _p(dXL),
         dXL.stride(0), _p(dXR), dXR.stride(0), _p(part_dxr), _p(datt_part), int(xl_by_position), _stream(dXL))

@@ -20,6 +20,17 @@ import torch
 from . import _native
 
 DEFAULT_MAX_PIECE = 256
+LANES_MAX_AVG = 32  # 4-wide convs with <= this many edges per item on average: one lane per item
+# The lane-per-item forward replaced a 226 us launch by a 43 us one at config 4; the lane-per-item
+# backward measured 193 us against 153 us for the wave-per-item kernel (its dXL rows are scattered
+# into edge order either way), so the backward keeps the general kernel unless this is set.
+BWD_LANES = False
+
+
+def _lanes(plan, heads, HC):
+    """Block 0's point direction (H*C = 4, ~20-edge items): the lane-per-item kernels
+    (csrc/attn_lanes.hip)."""
+    return HC == 4 and heads == 4 and plan.num_edges <= LANES_MAX_AVG * plan.n_items
 
 # Optional live kernel timer (bench.py): callable(tag, HC) -> bool selecting which
 # attention launches to bracket with HIP events on the launch stream.
@@ -244,7 +255,7 @@ def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True, xl_so
         ev[0].record()
     def launch():
         _native.attn_fwd(XL, XR, attf, bias, None if xl_sorted else plan.perm, plan.items, plan.n_items, heads, C,
-                         slope, finalize, out, smax, ssum, part)
+                         slope, finalize, out, smax, ssum, part, lanes=_lanes(plan, heads, HC))
     launch()
     if timed:
         ev[1].record()
@@ -325,7 +336,8 @@ def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, go
     attf = att.reshape(-1).contiguous()
     if plan.n_items:
         _native.attn_bwd(XL, XR, attf, bias, plan.perm, plan.items, plan.n_items, heads, C, slope, out, smax,
-                         ssum, gout, dXL, dXR, part, datt_part, xl_by_position=xl_sorted)
+                         ssum, gout, dXL, dXR, part, datt_part, xl_by_position=xl_sorted,
+                         lanes=BWD_LANES and _lanes(plan, heads, HC))
         bwd_combine(plan, part, HC, dXR)
         tot = _native.param_colsum(datt_part, defer)  # datt | dbias: parameter gradients
         datt, dbias = tot[:HC], tot[HC:]

@@ -113,6 +113,20 @@ int gasfm_gat_attn_combine(const gasfm_combine_item* combine, int32_t n_combine,
                            float* out, int64_t ldOut, float* seg_max, float* seg_sum,
                            int64_t ldStat, void* stream);
 
+/* Lane-per-item variants of gasfm_gat_attn_fwd / _bwd for H = 4, C = 1 (block 0's 4-wide convs)
+ * with short items (the point direction, ~20 edges per point): same arguments, outputs and
+ * partial layouts; the backward's datt_part has gasfm_gat_attn_bwd_waves(n_items, 4, 1) rows. */
+int gasfm_gat_attn_fwd_lanes(const float* XL, int64_t ldXL, const float* XR, int64_t ldXR, const float* att,
+                             const float* bias, const int32_t* perm, const gasfm_work_item* items, int32_t n_items,
+                             int32_t H, int32_t C, float slope, int32_t finalize, float* out, int64_t ldOut,
+                             float* seg_max, float* seg_sum, int64_t ldStat, float* part, void* stream);
+int gasfm_gat_attn_bwd_lanes(const float* XL, int64_t ldXL, const float* XR, int64_t ldXR, const float* att,
+                             const float* bias, const int32_t* perm, const gasfm_work_item* items, int32_t n_items,
+                             int32_t H, int32_t C, float slope, const float* out, int64_t ldOut,
+                             const float* seg_max, const float* seg_sum, const float* gout, int64_t ldG, float* dXL,
+                             int64_t ldDXL, float* dXR, int64_t ldDXR, float* part_dxr, float* datt_part,
+                             int32_t xl_by_position, void* stream);
+
 /* Backward of the above given dOut (gout), the forward's finalized out and
  * per-segment stats.  Writes dXL[src_j] for every edge (each row exactly
  * once), dXR[seg] for complete items (partials to part_dxr[slot] for split
