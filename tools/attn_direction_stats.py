@@ -6,7 +6,8 @@ Every block's forward launches its two edge-sized GATv2 attentions in a fixed or
 direction (proj2scenepoint, the bench's roofline kernel) first, then the camera direction
 (proj2view) -- followed by the global graphs' small kernels (Geom<1024,256>, Geom<64,16>).  The
 k-th edge-sized forward launch of a step is therefore the point direction for even k; the
-backward visits a block's convs in the reverse order (camera, then point).  Prints per
+backward (DualAttentionFn.backward) also runs the point direction first, then the camera
+direction.  (Round-2 profiles before this note labelled the backward the other way round.)  Prints per
 (kernel, direction): launches, mean / min / max microseconds and workgroups, over the steps
 after the first ``steps_to_skip`` (default 2, the warm-up).
 """
@@ -33,11 +34,11 @@ def main():
                 continue
             if re.search(r"Geom<(1024, 256|64, 16)>", name):
                 continue  # the global graphs (views -> global, points -> global)
-            kern = re.sub(r"\(.*", "", name.replace("void ", "").replace("gasfm::", ""))
+            kern = re.sub(r"\(.*", "", name.replace("void ", "").replace("(anonymous namespace)::", "").replace("gasfm::", ""))
             kind = "bwd" if "bwd" in kern else "fwd"
             k = seen[kind]
             seen[kind] += 1
-            point = (k % 2 == 0) if kind == "fwd" else (k % 2 == 1)
+            point = k % 2 == 0
             stats[(kind, kern, "point (proj2scenepoint)" if point else "camera (proj2view)")].append(((e - s) / 1e3,
                                                                                                      wgs))
     print(f"{'pass':4s} {'kernel':44s} {'direction':24s} {'launches':>8s} {'mean_us':>8s} {'min_us':>8s} "
