@@ -145,7 +145,12 @@ def test_config3_device_data_path_step_matches_oracle(device):
         total.backward()
         refs[dt] = (float(total.detach()), {k: (v.grad if v.grad is not None else torch.zeros_like(v))
                                             for k, v in sd.items()})
-    np.testing.assert_allclose(float(batch_loss.detach()), refs[torch.float64][0], rtol=1e-4)
+    # loss: 1e-4 relative, or 10x the fp32 oracle's own deviation from fp64 when that is larger (the
+    # loss sums reprojection ratios over sampled scenes; fp32 rounding of the 12-block forward is
+    # amplified there, differently for each summation order)
+    l64, l32 = refs[torch.float64][0], refs[torch.float32][0]
+    rtol = max(1e-4, 10 * abs(l32 - l64) / abs(l64))
+    np.testing.assert_allclose(float(batch_loss.detach()), l64, rtol=rtol)
     r64 = {k: project_grad(k, v) for k, v in refs[torch.float64][1].items()}
     floor = 1e-6 * max(np.linalg.norm(v) for v in r64.values()) + 1e-9
     for k, gv in got.items():
