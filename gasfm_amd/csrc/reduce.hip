@@ -28,8 +28,12 @@ __device__ __forceinline__ void st_sc1(float* p, float4 v) {
   __hip_atomic_store(reinterpret_cast<uint64_t*>(p) + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// >= 64 rows per block (each of a 256-column chunk's 4 row lanes requests its 16 rows at once),
+// <= 64 blocks per column chunk.  Round 1 used 16 rows per block: 4x the workgroups, each a
+// full load / publish / ticket / reduce latency chain, and 4x the slabs for the last arriver to
+// fold (the end-of-backward batched sums ran at ~1 TB/s).
 static int colsum_blocks(int64_t rows) {
-  const int64_t b = (rows + 15) / 16;  // >= 16 rows per block, <= 64 blocks per column chunk
+  const int64_t b = (rows + 63) / 64;
   return int(b < 1 ? 1 : (b > kMaxColBlocks ? kMaxColBlocks : b));
 }
 
@@ -54,6 +58,18 @@ __device__ __forceinline__ void colsum_block(const float* __restrict__ A, int64_
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (rl < RL) {
       int64_t r = r0 + rl;
+      for (; r + 15 * RL < r1; r += 16 * RL) {
+        float4 v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = *reinterpret_cast<const float4*>(A + (r + u * RL) * ld + 4 * c4);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          acc.x += v[u].x;
+          acc.y += v[u].y;
+          acc.z += v[u].z;
+          acc.w += v[u].w;
+        }
+      }
       for (; r + 3 * RL < r1; r += 4 * RL) {
         float4 v[4];
 #pragma unroll
