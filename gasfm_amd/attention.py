@@ -212,7 +212,12 @@ def combine_fwd_l1(plan, part, heads, C):
 
 
 def bwd_combine(plan, part, HC, out):
-    """out[seg] = ordered sum of the plan's partial rows (both levels)."""
+    """out[seg] = ordered sum of the plan's partial rows (both levels).  A single-target plan's
+    (view->global, points->global: hundreds to thousands of pieces) sum is a column sum of all
+    its slots: one last-arriver colsum launch instead of the two combine levels."""
+    if plan.num_targets == 1 and plan.n_slots > 0 and out.shape[0] == 1:
+        _native.colsum(part[:plan.n_slots], out=out.view(-1))
+        return
     if plan.n_l1:
         _native.attn_bwd_combine(plan.combine_l1, plan.n_l1, HC, part, part)
     if plan.n_combine:
