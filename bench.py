@@ -133,6 +133,8 @@ def main():
                     help="run the point-sharded RCCL path even at one rank (under torchrun --nproc-per-node 1)")
     ap.add_argument("--no-cam-shard", action="store_true",
                     help="N > 1: shard the points only (the view chain replicated on every rank)")
+    ap.add_argument("--cam-shard-1", action="store_true",
+                    help="with --dist at one rank: run the camera-sharded code path anyway (RCCL capture test)")
     ap.add_argument("--emulate-world", type=int, default=0, metavar="W",
                     help="per-rank proxy: rank 0's shard of a W-GPU step on this one GPU, collectives replaced by "
                          "local copies (timing of the per-rank compute; numerically meaningless)")
@@ -166,7 +168,7 @@ def main():
         if emul:
             data = gdist.shard_scene(sc, 0, args.emulate_world, cameras=cams, emulate=True).to(dev)
         else:
-            data = gdist.shard_scene(sc, rank, world, cameras=cams and world > 1).to(dev)
+            data = gdist.shard_scene(sc, rank, world, cameras=cams and (world > 1 or args.cam_shard_1)).to(dev)
         model = gdist.ShardedGraphAttnSfMNet(net.to(dev), cameras=data.shard.cams is not None)
     else:
         data = gasfm_amd.SceneData.from_synthetic(sc).to(dev)

@@ -292,7 +292,8 @@ def test_capture_fallback_is_agreed_across_ranks(device):
 
 
 @pytest.mark.gpu
-def test_rccl_bench_captures_and_replays(tmp_path):
+@pytest.mark.parametrize("cams", [False, True], ids=["points", "points+cameras"])
+def test_rccl_bench_captures_and_replays(tmp_path, cams):
     """bench.py's RCCL path (nccl process group, one rank) captures the whole step, collectives
     included, into a hipGraph and replays it.  Regression: in the default "global" capture mode
     ProcessGroupNCCL's watchdog thread querying events during the capture aborted the process."""
@@ -304,12 +305,15 @@ def test_rccl_bench_captures_and_replays(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(repo, "bench.py"),
            "--gpus", "1", "--dist", "--cameras", "200", "--points", "20000", "--layers", "2", "--steps", "3", "--warmup", "2",
-           "--no-cpu-baseline"]
+           "--no-cpu-baseline"] + (["--cam-shard-1"] if cams else [])
     r = subprocess.run(cmd, cwd=repo, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "hipGraph replay" in r.stderr, r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["execution"].startswith("hipGraph replay") and res["value"] > 0
+    # camera sharding: RCCL all-gathers of the view rows and the overlapped (async) weight-gradient
+    # all-reduces, issued from post-accumulate-grad hooks, inside the captured graph
+    assert ("point+camera" in res["config"]["parallelism"]) == cams
 
 
 def _esfm_conf():
