@@ -235,11 +235,12 @@ def _check(t, name, rows=None, cols=None):
         raise ValueError(f"{name}: has {t.shape[1]} columns, expected {cols}")
 
 
-def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True, xl_sorted=False):
+def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True, xl_sorted=False, out=None):
     """Launch the forward kernels; returns (out, seg_max, seg_sum) for all plan targets.
 
     xl_sorted: XL rows are already in segment order (written through plan.pos), so the
-    kernel streams them (perm = NULL) instead of gathering."""
+    kernel streams them (perm = NULL) instead of gathering.  out: optional [N, HC] row view
+    (unit column stride) to write the aggregates into."""
     if plan.all_partial:
         raise ValueError("all-partial plans go through attn_forward_partial")
     HC = att.numel()
@@ -248,7 +249,8 @@ def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True, xl_so
     dev = XL.device
     _check(XL, "XL", plan.src_rows, HC)
     _check(XR, "XR", N if XR.stride(0) else 1, HC)
-    out = torch.empty((N, HC), dtype=torch.float32, device=dev)
+    if out is None:
+        out = torch.empty((N, HC), dtype=torch.float32, device=dev)
     smax = torch.empty((N, heads), dtype=torch.float32, device=dev)
     ssum = torch.empty((N, heads), dtype=torch.float32, device=dev)
     part = (torch.empty((plan.n_part_rows, HC + 2 * heads), dtype=torch.float32, device=dev)
@@ -375,6 +377,35 @@ class GatAttentionFn(torch.autograd.Function):
                                                   ssum, gout,
                                                   defer=ctx.defer)
         return dXL, dXR, datt.view_as(att), dbias, None, None, None
+
+
+class GlobalPairFn(torch.autograd.Function):
+    """The view->global and points->global attentions of a block (one target each) written side by
+    side into the global MLP's [1, HCv + HCp] input: no concatenation kernel either way."""
+
+    @staticmethod
+    def forward(ctx, XLv, XRv, att_v, bias_v, XLp, XRp, att_p, bias_p, plan_v, plan_p, heads, slope):
+        HCv, HCp = att_v.numel(), att_p.numel()
+        x = torch.empty((1, HCv + HCp), dtype=torch.float32, device=XLv.device)
+        _, mv, sv = attn_forward_raw(XLv, XRv, att_v, bias_v, plan_v, heads, slope, out=x[:, :HCv])
+        _, mp, sp = attn_forward_raw(XLp, XRp, att_p, bias_p, plan_p, heads, slope, out=x[:, HCv:])
+        ctx.plans, ctx.heads, ctx.slope, ctx.HCv = (plan_v, plan_p), heads, slope, HCv
+        ctx.defer = _native.defer_token(att_v, bias_v, att_p, bias_p)
+        ctx.save_for_backward(XLv, XRv, att_v, bias_v, XLp, XRp, att_p, bias_p, x, mv, sv, mp, sp)
+        return x
+
+    @staticmethod
+    def backward(ctx, g):
+        XLv, XRv, att_v, bias_v, XLp, XRp, att_p, bias_p, x, mv, sv, mp, sp = ctx.saved_tensors
+        plan_v, plan_p = ctx.plans
+        HCv = ctx.HCv
+        g = g.contiguous()
+        dXLv, dXRv, dattv, dbv = attn_backward_raw(XLv, XRv, att_v, bias_v, plan_v, ctx.heads, ctx.slope,
+                                                   x[:, :HCv], mv, sv, g[:, :HCv], defer=ctx.defer)
+        dXLp, dXRp, dattp, dbp = attn_backward_raw(XLp, XRp, att_p, bias_p, plan_p, ctx.heads, ctx.slope,
+                                                   x[:, HCv:], mp, sp, g[:, HCv:], defer=ctx.defer)
+        return (dXLv, dXRv, dattv.view_as(att_v), dbv, dXLp, dXRp, dattp.view_as(att_p), dbp, None, None, None,
+                None)
 
 
 def gat_attention(XL, XR, att, bias, plan, heads, negative_slope=0.2):

@@ -241,6 +241,12 @@ class ViewAndScenePoint2Global(Module):
                 XLv, XRv, cv.att, cv._bias(XLv), XLp, XRp, c.att, c.bias,
                 (plan_v2g, plan_v2g_partial, plan_s2g, plan_s2g_partial), c.heads, c.negative_slope, shard)
             return self._global_tail(x, prev)
+        if shard is None and XLv.is_cuda and plan_v2g.num_targets == 1 and plan_s2g.num_targets == 1 \
+                and cv.heads == c.heads and cv.negative_slope == c.negative_slope:
+            from .attention import GlobalPairFn
+            x = GlobalPairFn.apply(XLv, XRv, cv.att, cv._bias(XLv), XLp, XRp, c.att, c._bias(XLp), plan_v2g, plan_s2g,
+                                   c.heads, c.negative_slope)
+            return self._global_tail(x, prev)
         v2g = gat_attention(XLv, XRv, cv.att, cv._bias(XLv), plan_v2g, cv.heads, cv.negative_slope)
         if shard is None:
             s2g = gat_attention(XLp, XRp, c.att, c._bias(XLp), plan_s2g, c.heads, c.negative_slope)
