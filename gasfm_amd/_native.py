@@ -119,6 +119,9 @@ _SIGS = {
                                    _vp, _vp, _vp]),
     "gasfm_point_hub_bwd_c": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_point_hub_bwd_ab": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_point_head_part_shape": (_i32, [_i64, _i32, _vp]),
+    "gasfm_point_head_fwd": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_point_head_bwd": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_gemm_bf16": (_i32, [_i32, _i32, _i32, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _i64, _vp]),
     "gasfm_gemm_f32": (_i32, [_i32, _i32, _i32, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _i64, _vp]),
 }
@@ -633,6 +636,46 @@ def point_hub_bwd_ab(X, eps, gA, bA, WA, WB, dSA, dXL, dRes, dX, part):
     st = lib().gasfm_point_hub_bwd_ab(_p(X), X.shape[0], eps, _p(gA), _p(bA), _p(WA), _p(WB), _p(dSA), _p(dXL),
                                       _p(dRes), _p(dX), _p(part), _stream(X))
     check(st, "gasfm_point_hub_bwd_ab")
+
+
+# ---------------------------------------------------------------- scene-point head (point_head.hip)
+def point_head_part_shape(N, which):
+    cols = ctypes.c_int32(0)
+    rows = lib().gasfm_point_head_part_shape(N, int(which), ctypes.byref(cols))
+    return rows, cols.value
+
+
+def _head_weights(W1, b1, W2, b2, W3, b3=None):
+    shapes = ((W1, (64, 64)), (b1, (64,)), (W2, (64, 64)), (b2, (64,)), (W3, (3, 64))) + \
+        (((b3, (3,)),) if b3 is not None else ())
+    for t, shape in shapes:
+        if tuple(t.shape) != shape or not t.is_contiguous() or t.dtype != torch.float32:
+            raise ValueError(f"point head: weight {tuple(t.shape)} is not a contiguous fp32 {shape}")
+
+
+def point_head_fwd(P, W1, b1, W2, b2, W3, b3, out):
+    _req(P, "P", 64)
+    _head_weights(W1, b1, W2, b2, W3, b3)
+    N = P.shape[0]
+    if tuple(out.shape) != (4, N) or not out.is_contiguous():
+        raise ValueError("point_head_fwd: out must be a contiguous [4, N]")
+    st = lib().gasfm_point_head_fwd(_p(P), N, _p(W1), _p(b1), _p(W2), _p(b2), _p(W3), _p(b3), _p(out), _stream(P))
+    check(st, "gasfm_point_head_fwd")
+
+
+def point_head_bwd(P, W1, b1, W2, b2, W3, dout, dP, part_a, part_b):
+    _req(P, "P", 64)
+    _req(dP, "dP", 64)
+    _head_weights(W1, b1, W2, b2, W3)
+    N = P.shape[0]
+    if tuple(dout.shape) != (4, N) or not dout.is_contiguous():
+        raise ValueError("point_head_bwd: dout must be a contiguous [4, N]")
+    for part, which in ((part_a, 0), (part_b, 1)):
+        if tuple(part.shape) != point_head_part_shape(N, which) or not part.is_contiguous():
+            raise ValueError("point_head_bwd: partial buffer of the wrong shape")
+    st = lib().gasfm_point_head_bwd(_p(P), N, _p(W1), _p(b1), _p(W2), _p(b2), _p(W3), _p(dout), _p(dP),
+                                    _p(part_a), _p(part_b), _stream(P))
+    check(st, "gasfm_point_head_bwd")
 
 
 # ---------------------------------------------------------------- camera-side block chains (view_block.hip)

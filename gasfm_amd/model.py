@@ -901,7 +901,9 @@ class GraphAttnSfMNet(Module):
                 from .distributed import gather_rows
                 out = {k: gather_rows(shard, v)[0] for k, v in out.items()}
             pred.update(out)
-        if self.scenepoint_head_enabled:
+        if self.scenepoint_head_enabled and point_block.head_fusable(self.scenepoint_head, pts):
+            pred["pts3D"] = point_block.head(self.scenepoint_head, pts)
+        elif self.scenepoint_head_enabled:
             n_out = dense.sequential(self.scenepoint_head, F.relu(pts)).T
             pred["pts3D"] = torch.cat([n_out, torch.ones(1, n_out.shape[1], dtype=n_out.dtype, device=device)])
         return pred

@@ -244,3 +244,55 @@ def hub_params(pfu, s2g_conv, nxt):
 
 def hub(p, params, sec=None):
     return PointHubFn.apply(p, *params, sec)
+
+
+class PointHeadFn(torch.autograd.Function):
+    """pts3D = [scenepoint_head(relu(p))^T ; 1] (reference code/models/graph_attn_sfm.py:170-174)
+    in one forward kernel and two backward kernels (csrc/point_head.hip); the scene-point head
+    is Linear(64,64) ReLU Linear(64,64) ReLU Linear(64,3) (layers.py:10-44, norm=False)."""
+
+    @staticmethod
+    def forward(ctx, p, W1, b1, W2, b2, W3, b3):
+        p = p.contiguous()
+        N = p.shape[0]
+        out = _f32(4, N, like=p)
+        _native.point_head_fwd(p, W1, b1, W2, b2, W3, b3, out)
+        ctx.save_for_backward(p, W1, b1, W2, b2, W3)
+        ctx.defer = _native.defer_token(W1, b1, W2, b2, W3, b3)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        p, W1, b1, W2, b2, W3 = ctx.saved_tensors
+        N = p.shape[0]
+        ra, ca = _native.point_head_part_shape(N, 0)
+        rb, cb = _native.point_head_part_shape(N, 1)
+        dp = _f32(N, P_W, like=p)
+        if N == 0:
+            ta = torch.zeros(ca, dtype=torch.float32, device=p.device)
+            tb = torch.zeros(cb, dtype=torch.float32, device=p.device)
+        else:
+            part_a, part_b = _f32(ra, ca, like=p), _f32(rb, cb, like=p)
+            _native.point_head_bwd(p, W1, b1, W2, b2, W3, dout.contiguous(), dp, part_a, part_b)
+            ta, tb = _native.param_colsum(part_a, ctx.defer), _native.param_colsum(part_b, ctx.defer)
+        dW1, db1 = ta[:P_W * P_W].view(P_W, P_W), ta[P_W * P_W:]
+        o = P_W * P_W
+        dW2, dW3 = tb[:o].view(P_W, P_W), tb[o:o + 3 * P_W].view(3, P_W)
+        o += 3 * P_W
+        db2, db3 = tb[o:o + P_W], tb[o + P_W:o + P_W + 3]
+        return dp, dW1, db1, dW2, db2, dW3, db3
+
+
+def head_fusable(seq, p):
+    """The configuration's scene-point head: two 64-wide hidden layers, 3 outputs, no norms."""
+    mods = list(seq)
+    return (_rows_ok(p, P_W) and len(mods) == 5 and _is_lin(mods[0], P_W, P_W, True)
+            and isinstance(mods[1], torch.nn.ReLU) and _is_lin(mods[2], P_W, P_W, True)
+            and isinstance(mods[3], torch.nn.ReLU) and _is_lin(mods[4], P_W, 3, True)
+            and all(m.weight.dtype == torch.float32 and m.weight.is_contiguous() and m.bias.is_contiguous()
+                    for m in (mods[0], mods[2], mods[4])))
+
+
+def head(seq, p):
+    l1, l2, l3 = seq[0], seq[2], seq[4]
+    return PointHeadFn.apply(p, l1.weight, l1.bias, l2.weight, l2.bias, l3.weight, l3.bias)

@@ -334,6 +334,25 @@ int gasfm_point_hub_bwd_ab(const float* X, int64_t N, float eps, const float* gA
                            const float* WA, const float* WB, const float* dSA, const float* dXL,
                            const float* dRes, float* dX, float* part, void* stream);
 
+/* ---- scene-point head (point_head.hip): replaces the aten run of
+ *   pts3D = [scenepoint_head(relu(p))^T ; 1]   (graph_attn_sfm.py:170-174, layers.py:10-44,
+ *   norm=False, 2 hidden layers: Linear(64,64) ReLU Linear(64,64) ReLU Linear(64,3)).
+ * P [N x 64] row-major; W1, W2 [64 x 64], W3 [3 x 64] (torch Linear [out, in]); out / dout [4 x N]. */
+
+/* Partial rows for gasfm_point_head_bwd: which = 0 -> part_a [dW1 64x64 | db1 64],
+ * which = 1 -> part_b [dW2 64x64 | dW3 3x64 | db2 64 | db3 3]; *cols receives the row width. */
+int gasfm_point_head_part_shape(int64_t N, int32_t which, int32_t* cols);
+
+/* out[0:3] = (relu(relu(relu(P) W1^T + b1) W2^T + b2) W3^T + b3)^T, out[3] = 1. */
+int gasfm_point_head_fwd(const float* P, int64_t N, const float* W1, const float* b1, const float* W2,
+                         const float* b2, const float* W3, const float* b3, float* out, void* stream);
+
+/* dP and the weight-gradient partials (column sums give dW1, db1, dW2, dW3, db2, db3) from
+ * dout rows 0-2 (row 3, the constant ones, has no gradient). */
+int gasfm_point_head_bwd(const float* P, int64_t N, const float* W1, const float* b1, const float* W2,
+                         const float* b2, const float* W3, const float* dout, float* dP, float* part_a,
+                         float* part_b, void* stream);
+
 /* ---- camera (view) block chains (m rows x D, D a multiple of 64, <= 1024) ----
  * tail: Proj2View.forward after the aggregation (layers.py:345-360):
  *   x = prev + Wp agg + bp;  view = x + Wm relu(LN(x)) + bm
