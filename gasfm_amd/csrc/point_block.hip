@@ -935,11 +935,271 @@ __global__ __launch_bounds__(kThreads8) void point_hub_bwd_c_kernel(
   }
 }
 
+// ----------------------------------------------------------------------------- forward, register-resident
+// The forward kernels above stage every 16-row tile through LDS twice per layer (rows in, C layout
+// out, A layout back in).  Computing the TRANSPOSED products Y^T = W X^T instead keeps a tile in
+// registers from load to store: with A = W and B = X^T, v_mfma_f32_16x16x4_f32 leaves lane
+// (g = lane>>4, c = lane&15) holding Y[row c][16 ot + 4 g + r] (r < 4) -- 16 features of row c --
+// and those registers are exactly the B operand of the next layer when its k index is permuted
+// to k = 16 u + 4 g + j at step (u, j) (any consistent k order gives the same sum).  The weights
+// are staged once per workgroup pre-permuted to match, as float4 slabs read with one conflict-free
+// ds_read_b128 per 4 MFMAs.  Rows load and store as float4 (64 B per row per slab).  Row
+// statistics: 16 values per lane, then a sum over the 4 lane groups.  Only weights live in LDS
+// (24-37 KB per workgroup), so occupancy is set by VGPRs.
+#ifndef GASFM_PT_FWD_T
+#define GASFM_PT_FWD_T 1
+#endif
+#ifndef GASFM_PT_FWD_T_MINW
+#define GASFM_PT_FWD_T_MINW 1
+#endif
+// 1: re-read the weight slabs from LDS every tile (a compiler memory barrier at the top of the
+// tile loop keeps them from being hoisted into registers: ~100 fewer VGPRs, more waves per SIMD);
+// 0: the compiler keeps them in VGPRs across tiles
+#ifndef GASFM_PT_FWD_T_LDSW
+#define GASFM_PT_FWD_T_LDSW 1
+#endif
+// waves per workgroup (4, 8 and 16 measured: 16 slowest, 4 and 8 within 1 us)
+#ifndef GASFM_PT_FWD_T_WAVES
+#define GASFM_PT_FWD_T_WAVES 4
+#endif
+constexpr int kWavesT = GASFM_PT_FWD_T_WAVES, kThreadsT = kWavesT * kW;
+
+// W [O x K] (torch Linear [out, in]) -> float4 slabs Q[(ot * (K/16) + u) * 64 + 16 g + c] =
+// (W[16 ot + c][16 u + 4 g + j], j < 4)
+template <int O, int K, int NT>
+__device__ __forceinline__ void stage_slabs(const float* __restrict__ W, float* Q) {
+  Stage<O * K, NT> s;
+  s.load([&](int q) { return W[q]; });
+  s.store([&](int q, float v) {
+    const int o = q / K, k = q % K;
+    Q[(((o / 16) * (K / 16) + k / 16) * 64 + ((k % 16) / 4) * 16 + o % 16) * 4 + k % 4] = v;
+  });
+}
+
+// acc[ot] += W . X^T over K = 16 KU (X as k-slabs xk[u] = X[row c][16 u + 4 g + j])
+template <int OT, int KU>
+__device__ __forceinline__ void layer_t(const float4* __restrict__ Q, const f32x4 (&xk)[KU], f32x4 (&acc)[OT],
+                                        int lane) {
+  // the OT accumulators interleaved (consecutive MFMAs independent: a dependent chain waits the
+  // full pipeline latency per step), and the next k-slab's weights read from LDS while this one's
+  // MFMAs run
+  float4 w[OT];
+#pragma unroll
+  for (int ot = 0; ot < OT; ++ot) w[ot] = Q[ot * KU * 64 + lane];
+#pragma unroll
+  for (int u = 0; u < KU; ++u) {
+    float4 wn[OT];
+    if (u + 1 < KU) {
+#pragma unroll
+      for (int ot = 0; ot < OT; ++ot) wn[ot] = Q[(ot * KU + u + 1) * 64 + lane];
+    }
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) acc[ot] = mfma16(w[ot].x, xk[u][0], acc[ot]);
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) acc[ot] = mfma16(w[ot].y, xk[u][1], acc[ot]);
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) acc[ot] = mfma16(w[ot].z, xk[u][2], acc[ot]);
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) acc[ot] = mfma16(w[ot].w, xk[u][3], acc[ot]);
+    if (u + 1 < KU) {
+#pragma unroll
+      for (int ot = 0; ot < OT; ++ot) w[ot] = wn[ot];
+    }
+  }
+}
+
+// per-feature vector V[64] (LDS) at this lane's features 16 ot + 4 g + r
+__device__ __forceinline__ f32x4 vec_at(const float* V, int ot, int g) {
+  const float4 v = *reinterpret_cast<const float4*>(V + 16 * ot + 4 * g);
+  return f32x4{v.x, v.y, v.z, v.w};
+}
+
+// slab u of row c (clamped to a valid row; rows past nrows are computed and not stored)
+template <int W>
+__device__ __forceinline__ void slabs_load(const float* __restrict__ X, int64_t row0, int nrows, f32x4 (&v)[W / 16],
+                                           int lane) {
+  const int c = lane & 15, g = lane >> 4;
+  const float* p = X + (row0 + (c < nrows ? c : nrows - 1)) * W + 4 * g;
+#pragma unroll
+  for (int u = 0; u < W / 16; ++u) {
+    const float4 t = *reinterpret_cast<const float4*>(p + 16 * u);
+    v[u] = f32x4{t.x, t.y, t.z, t.w};
+  }
+}
+template <int W>
+__device__ __forceinline__ void slabs_store(float* __restrict__ X, int64_t row0, int nrows, const f32x4 (&v)[W / 16],
+                                            int lane) {
+  const int c = lane & 15, g = lane >> 4;
+  if (c >= nrows) return;
+  float* p = X + (row0 + c) * W + 4 * g;
+#pragma unroll
+  for (int u = 0; u < W / 16; ++u) *reinterpret_cast<float4*>(p + 16 * u) = make_float4(v[u][0], v[u][1], v[u][2], v[u][3]);
+}
+
+// mean and rstd of the 64-wide rows held as 4 slabs per lane (row c over the 4 lane groups)
+__device__ __forceinline__ void slab_stats(const f32x4 (&x)[4], float eps, float& mean, float& rstd) {
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) s += (x[u][0] + x[u][1]) + (x[u][2] + x[u][3]);
+  mean = sum_groups(s) * (1.f / FP);
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q = fmaf(x[u][j] - mean, x[u][j] - mean, q);
+  rstd = rsqrtf(sum_groups(q) * (1.f / FP) + eps);
+}
+
+template <bool PREV>
+__global__ __launch_bounds__(kThreadsT, GASFM_PT_FWD_T_MINW) void point_tail_fwd_t_kernel(
+    const float* __restrict__ prev, const float* __restrict__ agg, int64_t N, const float* __restrict__ Wp,
+    const float* __restrict__ bp, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
+    const float* __restrict__ Wm, const float* __restrict__ bm, float* __restrict__ out) {
+  __shared__ float4 WpQ[FP * FA / 4], WmQ[FP * FP / 4];
+  __shared__ float V[4 * FP];  // b_p gamma beta b_m
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW, g = lane >> 4;
+  const int64_t ntiles = (N + TR - 1) / TR;
+  const int64_t gw = int64_t(blockIdx.x) * kWavesT + wave, nw = int64_t(gridDim.x) * kWavesT;
+  f32x4 na[2], np[4];  // next tile's rows, requested before this tile's MFMA work
+  auto fetch = [&](int64_t tt) {
+    const int64_t r0 = tt * TR;
+    const int nr = int(N - r0 < TR ? N - r0 : TR);
+    slabs_load<FA>(agg, r0, nr, na, lane);
+    if (PREV) slabs_load<FP>(prev, r0, nr, np, lane);
+  };
+  if (gw < ntiles) fetch(gw);  // the first tile's rows fly while the weights are staged
+  stage_slabs<FP, FA, kThreadsT>(Wp, reinterpret_cast<float*>(WpQ));
+  stage_slabs<FP, FP, kThreadsT>(Wm, reinterpret_cast<float*>(WmQ));
+  if (threadIdx.x < FP) {
+    V[threadIdx.x] = bp[threadIdx.x];
+    V[FP + threadIdx.x] = gam[threadIdx.x];
+    V[2 * FP + threadIdx.x] = bet[threadIdx.x];
+    V[3 * FP + threadIdx.x] = bm[threadIdx.x];
+  }
+  __syncthreads();
+  for (int64_t t = gw; t < ntiles; t += nw) {
+    const int64_t row0 = t * TR;
+    const int nrows = int(N - row0 < TR ? N - row0 : TR);
+    if (GASFM_PT_FWD_T_LDSW) asm volatile("" ::: "memory");
+    f32x4 ag[2] = {na[0], na[1]}, pv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pv[u] = PREV ? np[u] : zero4();
+    if (t + nw < ntiles) fetch(t + nw);
+    f32x4 x[4];
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot) x[ot] = vec_at(V, ot, g) + pv[ot];  // b_p + prev, then + W_p agg
+    layer_t<4, 2>(WpQ, ag, x, lane);
+    f32x4 gm[4], bt[4];
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot) {
+      gm[ot] = vec_at(V + FP, ot, g);
+      bt[ot] = vec_at(V + 2 * FP, ot, g);
+    }
+    float mean, rstd;
+    slab_stats(x, eps, mean, rstd);
+    f32x4 h[4];
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) h[ot][j] = fmaxf(fmaf((x[ot][j] - mean) * rstd, gm[ot][j], bt[ot][j]), 0.f);
+    f32x4 y[4];
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot) y[ot] = vec_at(V + 3 * FP, ot, g);  // b_m, then + W_m h
+    layer_t<4, 4>(WmQ, h, y, lane);
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot) y[ot] = x[ot] + y[ot];
+    slabs_store<FP>(out, row0, nrows, y, lane);
+  }
+}
+
+template <bool HC>
+__global__ __launch_bounds__(kThreadsT, GASFM_PT_FWD_T_MINW) void point_hub_fwd_t_kernel(
+    const float* __restrict__ X, int64_t N, float eps, const float* __restrict__ gA, const float* __restrict__ bA,
+    const float* __restrict__ WA, float* __restrict__ SA, const float* __restrict__ WB,
+    const float* __restrict__ bB, float* __restrict__ XL, const float* __restrict__ gC,
+    const float* __restrict__ bC, const float* __restrict__ WC, const float* __restrict__ bWC,
+    const float* __restrict__ WD, const float* __restrict__ bD, float* __restrict__ XR) {
+  __shared__ float4 WAQ[FA * FP / 4], WBQ[FP * FP / 4], WCQ[HC ? FA * FP / 4 : 1], WDQ[HC ? FA * FA / 4 : 1];
+  __shared__ float V[5 * FP + 2 * FA];  // gamma_A beta_A gamma_C beta_C b_B | b_C b_D
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW, g = lane >> 4;
+  const int64_t ntiles = (N + TR - 1) / TR;
+  const int64_t gw = int64_t(blockIdx.x) * kWavesT + wave, nw = int64_t(gridDim.x) * kWavesT;
+  f32x4 nx[4];
+  auto fetch = [&](int64_t tt) {
+    const int64_t r0 = tt * TR;
+    slabs_load<FP>(X, r0, int(N - r0 < TR ? N - r0 : TR), nx, lane);
+  };
+  if (gw < ntiles) fetch(gw);  // the first tile's rows fly while the weights are staged
+  stage_slabs<FA, FP, kThreadsT>(WA, reinterpret_cast<float*>(WAQ));
+  stage_slabs<FP, FP, kThreadsT>(WB, reinterpret_cast<float*>(WBQ));
+  if (HC) {
+    stage_slabs<FA, FP, kThreadsT>(WC, reinterpret_cast<float*>(WCQ));
+    stage_slabs<FA, FA, kThreadsT>(WD, reinterpret_cast<float*>(WDQ));
+  }
+  if (threadIdx.x < FP) {
+    V[threadIdx.x] = gA[threadIdx.x];
+    V[FP + threadIdx.x] = bA[threadIdx.x];
+    V[2 * FP + threadIdx.x] = HC ? gC[threadIdx.x] : 0.f;
+    V[3 * FP + threadIdx.x] = HC ? bC[threadIdx.x] : 0.f;
+    V[4 * FP + threadIdx.x] = bB[threadIdx.x];
+    if (threadIdx.x < FA) {
+      V[5 * FP + threadIdx.x] = HC ? bWC[threadIdx.x] : 0.f;
+      V[5 * FP + FA + threadIdx.x] = HC ? bD[threadIdx.x] : 0.f;
+    }
+  }
+  __syncthreads();
+  for (int64_t t = gw; t < ntiles; t += nw) {
+    const int64_t row0 = t * TR;
+    const int nrows = int(N - row0 < TR ? N - row0 : TR);
+    if (GASFM_PT_FWD_T_LDSW) asm volatile("" ::: "memory");
+    f32x4 p[4] = {nx[0], nx[1], nx[2], nx[3]};
+    if (t + nw < ntiles) fetch(t + nw);
+    float mean, rstd;
+    slab_stats(p, eps, mean, rstd);
+    {
+      f32x4 xl[4];
+#pragma unroll
+      for (int ot = 0; ot < 4; ++ot) xl[ot] = vec_at(V + 4 * FP, ot, g);  // b_B, then + W_B p
+      layer_t<4, 4>(WBQ, p, xl, lane);
+      slabs_store<FP>(XL, row0, nrows, xl, lane);
+    }
+    f32x4 h[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f32x4 gm = vec_at(V, u, g), bt = vec_at(V + FP, u, g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) h[u][j] = fmaxf(fmaf((p[u][j] - mean) * rstd, gm[j], bt[j]), 0.f);
+    }
+    {
+      f32x4 sa[2] = {zero4(), zero4()};
+      layer_t<2, 4>(WAQ, h, sa, lane);
+      slabs_store<FA>(SA, row0, nrows, sa, lane);
+    }
+    if (HC) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const f32x4 gm = vec_at(V + 2 * FP, u, g), bt = vec_at(V + 3 * FP, u, g);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) h[u][j] = fmaxf(fmaf((p[u][j] - mean) * rstd, gm[j], bt[j]), 0.f);
+      }
+      f32x4 tq[2] = {vec_at(V + 5 * FP, 0, g), vec_at(V + 5 * FP, 1, g)};  // b_C, then + W_C h
+      layer_t<2, 4>(WCQ, h, tq, lane);
+      f32x4 xr[2] = {vec_at(V + 5 * FP + FA, 0, g), vec_at(V + 5 * FP + FA, 1, g)};  // b_D, then + W_D t
+      layer_t<2, 2>(WDQ, tq, xr, lane);
+      slabs_store<FA>(XR, row0, nrows, xr, lane);
+    }
+  }
+}
+
 int64_t tiles_of(int64_t N) { return (N + TR - 1) / TR; }
 
 template <class K>
 int grid4(K kernel, int64_t N) {
   return resident_grid(reinterpret_cast<const void*>(kernel), kThreads, 0, tiles_of(N), kWaves);
+}
+template <class K>
+int gridT(K kernel, int64_t N) {
+  return resident_grid(reinterpret_cast<const void*>(kernel), kThreadsT, 0, tiles_of(N), kWavesT);
 }
 template <class K>
 int grid8(K kernel, int64_t N) {
@@ -979,6 +1239,15 @@ extern "C" int gasfm_point_tail_fwd(const float* prev, const float* agg, int64_t
   GASFM_REQUIRE(agg && Wp && bp && ln_w && ln_b && Wm && bm && out, "gasfm_point_tail_fwd: null pointer");
   GASFM_REQUIRE(aligned16(agg) && (!prev || aligned16(prev)), "gasfm_point_tail_fwd: alignment");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (GASFM_PT_FWD_T) {
+    if (prev)
+      hipLaunchKernelGGL(point_tail_fwd_t_kernel<true>, dim3(gridT(&point_tail_fwd_t_kernel<true>, N)),
+                         dim3(kThreadsT), 0, st, prev, agg, N, Wp, bp, ln_w, ln_b, eps, Wm, bm, out);
+    else
+      hipLaunchKernelGGL(point_tail_fwd_t_kernel<false>, dim3(gridT(&point_tail_fwd_t_kernel<false>, N)),
+                         dim3(kThreadsT), 0, st, prev, agg, N, Wp, bp, ln_w, ln_b, eps, Wm, bm, out);
+    return launch_status("gasfm_point_tail_fwd");
+  }
   if (prev)
     hipLaunchKernelGGL(point_tail_fwd_kernel<true>, dim3(grid4(&point_tail_fwd_kernel<true>, N)), dim3(kThreads), 0,
                        st, prev, agg, N, Wp, bp, ln_w, ln_b, eps, Wm, bm, out);
@@ -1018,6 +1287,15 @@ extern "C" int gasfm_point_hub_fwd(const float* X, int64_t N, float eps, const f
   GASFM_REQUIRE(!hc || (bC && WC && bWC && WD && bD && XR), "gasfm_point_hub_fwd: null pointer (C part)");
   GASFM_REQUIRE(aligned16(X), "gasfm_point_hub_fwd: alignment");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (GASFM_PT_FWD_T) {
+    if (hc)
+      hipLaunchKernelGGL(point_hub_fwd_t_kernel<true>, dim3(gridT(&point_hub_fwd_t_kernel<true>, N)), dim3(kThreadsT),
+                         0, st, X, N, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR);
+    else
+      hipLaunchKernelGGL(point_hub_fwd_t_kernel<false>, dim3(gridT(&point_hub_fwd_t_kernel<false>, N)),
+                         dim3(kThreadsT), 0, st, X, N, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR);
+    return launch_status("gasfm_point_hub_fwd");
+  }
   if (hc)
     hipLaunchKernelGGL(point_hub_fwd_kernel<true>, dim3(grid8(&point_hub_fwd_kernel<true>, N)), dim3(kThreads8), 0,
                        st, X, N, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR);

@@ -76,6 +76,13 @@ class CapturedStep:
                 if check else None
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            # let ProcessGroupNCCL's watchdog (100 ms poll) retire the warm-up collectives, all
+            # complete after the synchronize, before capture starts: a one-rank RCCL run once
+            # aborted in the watchdog mid-capture (1 in ~10 runs of
+            # test_rccl_bench_captures_and_replays), thread_local capture mode notwithstanding
+            import time
+            time.sleep(0.5)
         self._zero()
         g = torch.cuda.CUDAGraph()
         ok = True

@@ -70,7 +70,10 @@ def test_config2_optim9_training_step_matches_reference(device):
     loss = ESFMLoss(conf)(pred, data)
     np.testing.assert_allclose(float(loss.detach()), float(f["loss"].reshape(-1)[0]), rtol=1e-4)
     loss.backward()
-    check_fixture_grads(grads_of(net), f, "config 2: ")
+    # absolute floor 1e-6 x the step's largest gradient norm, as config 3: a gradient ~1e-6 of the
+    # step's scale (e.g. a deep block's view->global att, |g| ~4e-6) is resolved by fp32 only to that
+    # floor, and moves with the kernels' fp32 summation order
+    check_fixture_grads(grads_of(net), f, "config 2: ", step_atol=1e-6)
 
 
 def test_config3_learning12_batch_step_matches_reference(device):
