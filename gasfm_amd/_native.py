@@ -122,6 +122,9 @@ _SIGS = {
     "gasfm_point_head_part_shape": (_i32, [_i64, _i32, _vp]),
     "gasfm_point_head_fwd": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_point_head_bwd": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_embed2_part_rows": (_i32, [_i64]),
+    "gasfm_embed2_fwd": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp]),
+    "gasfm_embed2_bwd": (_i32, [_vp, _vp, _i64, _vp, _vp]),
     "gasfm_gemm_bf16": (_i32, [_i32, _i32, _i32, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _i64, _vp]),
     "gasfm_gemm_f32": (_i32, [_i32, _i32, _i32, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _i64, _vp]),
 }
@@ -636,6 +639,30 @@ def point_hub_bwd_ab(X, eps, gA, bA, WA, WB, dSA, dXL, dRes, dX, part):
     st = lib().gasfm_point_hub_bwd_ab(_p(X), X.shape[0], eps, _p(gA), _p(bA), _p(WA), _p(WB), _p(dSA), _p(dXL),
                                       _p(dRes), _p(dX), _p(part), _stream(X))
     check(st, "gasfm_point_hub_bwd_ab")
+
+
+# ---------------------------------------------------------------- input embedding (embed.hip)
+def embed2_fwd(X, W, b, Y):
+    _req(X, "values", 2)
+    _req(Y, "P", 2)
+    st = lib().gasfm_embed2_fwd(_p(X), X.shape[0], _p(W), _p(b), _p(Y), _stream(X))
+    check(st, "gasfm_embed2_fwd")
+
+
+def embed2_bwd(X, dY, defer=False):
+    """(dW [2, 2], db [2]) of P = X W^T + b from dP; column sums through param_colsum."""
+    _req(X, "values", 2)
+    _req(dY, "dP", 2)
+    E = X.shape[0]
+    rows = lib().gasfm_embed2_part_rows(E)
+    if rows == 0:
+        tot = torch.zeros(6, dtype=torch.float32, device=X.device)
+    else:
+        part = torch.empty((rows, 6), dtype=torch.float32, device=X.device)
+        st = lib().gasfm_embed2_bwd(_p(X), _p(dY), E, _p(part), _stream(X))
+        check(st, "gasfm_embed2_bwd")
+        tot = param_colsum(part, defer)
+    return tot[:4].view(2, 2), tot[4:]
 
 
 # ---------------------------------------------------------------- scene-point head (point_head.hip)

@@ -700,6 +700,35 @@ def scene_plans(data, device):
     return plans
 
 
+class Embed2Fn(torch.autograd.Function):
+    """P = values W^T + b for the Linear(2, 2) input embedding (layers.py:992-1015,
+    graph_attn_sfm.py:53) in one streaming kernel each way (csrc/embed.hip) instead of a
+    hipBLASLt tile sweep and a split-K batched GEMM over E rows."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        _native.embed2_fwd(x, W.contiguous(), b.contiguous(), y)
+        ctx.save_for_backward(x, W)
+        ctx.defer = _native.defer_token(W, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        dy = dy.contiguous()
+        dW, db = _native.embed2_bwd(x, dy, ctx.defer)
+        return (dy @ W if ctx.needs_input_grad[0] else None), dW, db
+
+
+def _embed(values, lin):
+    if (values.is_cuda and values.dtype == torch.float32 and values.dim() == 2 and values.shape[1] == 2
+            and lin.in_features == 2 and lin.out_features == 2 and lin.bias is not None):
+        return Embed2Fn.apply(values, lin.weight, lin.bias)
+    return dense.linear(values, lin)
+
+
 class FanOutFn(torch.autograd.Function):
     """x -> n identical views; the backward sums the consumers' gradients in one kernel
     (gasfm_sum_n) where autograd would run n - 1 full-size adds."""
@@ -831,7 +860,7 @@ class GraphAttnSfMNet(Module):
         """Block stack + final update on raw tensors; returns (P, pts, view) after the final update."""
         plans = edges.plans
         lin = self.embed.post_embed_lin
-        P = dense.linear(values, lin) if lin is not None else self.embed(values)
+        P = _embed(values, lin) if lin is not None else self.embed(values)
         nb = len(self.equivariant_blocks)
         p0s = [P if self.add_skipconn_from_init_projfeat else None] * nb
         if self.add_skipconn_from_init_projfeat and P.is_cuda and P.requires_grad and torch.is_grad_enabled():

@@ -334,6 +334,14 @@ int gasfm_point_hub_bwd_ab(const float* X, int64_t N, float eps, const float* gA
                            const float* WA, const float* WB, const float* dSA, const float* dXL,
                            const float* dRes, float* dX, float* part, void* stream);
 
+/* ---- input embedding (embed.hip): P = values W^T + b, the Linear(2, 2) of EmbeddingLayer
+ * (layers.py:992-1015, graph_attn_sfm.py:53); values, P [E x 2] row-major, W [2 x 2], b [2]. */
+int gasfm_embed2_fwd(const float* values, int64_t E, const float* W, const float* b, float* P, void* stream);
+/* Partial rows (6 floats: dW00 dW01 dW10 dW11 db0 db1) of gasfm_embed2_bwd; their column sums
+ * are dW and db. */
+int32_t gasfm_embed2_part_rows(int64_t E);
+int gasfm_embed2_bwd(const float* values, const float* dP, int64_t E, float* part, void* stream);
+
 /* ---- scene-point head (point_head.hip): replaces the aten run of
  *   pts3D = [scenepoint_head(relu(p))^T ; 1]   (graph_attn_sfm.py:170-174, layers.py:10-44,
  *   norm=False, 2 hidden layers: Linear(64,64) ReLU Linear(64,64) ReLU Linear(64,3)).
