@@ -16,6 +16,8 @@ from collections import defaultdict
 ALGO_MB = {  # config 4 algorithmic bytes per launch, DESIGN.md §5
     "edge_prologue_fwd_kernel<true>": 1550, "edge_epilogue_fwd_kernel": 1110, "edge_epilogue_bwd_kernel": 1090,
     "segment_rowsum_kernel": 554, "edge_prologue_bwd_kernel<true, true>": 2560,
+    "point_tail_fwd_t_kernel<true>": 128, "point_hub_fwd_t_kernel<true>": 154, "point_head_fwd_kernel": 54,
+    "embed2_fwd_kernel": 64, "embed2_bwd_kernel": 64,
 }
 
 
