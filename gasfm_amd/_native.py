@@ -25,6 +25,10 @@ _f32 = ctypes.c_float
 _SIGS = {
     "gasfm_last_error": (ctypes.c_char_p, []),
     "gasfm_version": (_i32, []),
+    "gasfm_dispatch_counts": (_i32, [_vp, _i32]),
+    "gasfm_dispatch_reset": (None, []),
+    "gasfm_tuning_set": (_i32, [_i32, ctypes.c_double]),
+    "gasfm_tuning_get": (ctypes.c_double, [_i32]),
     "gasfm_build_csr": (_i32, [_vp, _i64, _i32, _vp, _vp]),
     "gasfm_plan_work": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_gat_attn_fwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _f32, _i32,
@@ -109,8 +113,8 @@ _SIGS = {
     "gasfm_ba_dlt": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_sum_n": (_i32, [_i32, _vp, _i64, _vp, _vp]),
     "gasfm_esfm_fwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _vp, _vp]),
-    "gasfm_esfm_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _i32, _i32,
-                              _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_esfm_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _i32,
+                              _i32, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_point_tail_part_shape": (_i32, [_i64, _i32, _vp]),
     "gasfm_point_hub_part_shape": (_i32, [_i64, _i32, _i32, _vp]),
     "gasfm_point_tail_fwd": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
@@ -192,6 +196,67 @@ class launching_on:
     def __exit__(self, *exc):
         global _LAUNCH_STREAM
         _LAUNCH_STREAM = self.prev
+        return False
+
+
+# ---------------------------------------------------------------- kernel-choice record, tuning
+# mirrors the GASFM_K_* / GASFM_TUNE_* enums of include/gasfm.h
+KERNELS = {
+    "attn_fwd_grp": 0, "attn_fwd_glds": 1, "attn_fwd_vec": 2, "attn_fwd_generic": 3, "attn_fwd_lanes": 4,
+    "attn_bwd_glds": 5, "attn_bwd_vec": 6, "attn_bwd_generic": 7, "attn_bwd_lanes": 8,
+    "attn_combine_vec": 9, "attn_combine_generic": 10, "attn_bwd_grp": 11,
+}
+TUNING = {"attn_grp_rows": 0, "attn_grp_min_fill": 1, "attn_glds": 2, "attn_wave_cap": 3, "attn_grp_bwd": 4}
+
+
+def dispatch_counts():
+    """{kernel name: launches since the last reset} of the size-dependent dispatches."""
+    n = len(KERNELS) + 8
+    buf = (_i64 * n)()
+    lib().gasfm_dispatch_counts(buf, n)
+    return {k: int(buf[i]) for k, i in KERNELS.items()}
+
+
+def dispatch_reset():
+    lib().gasfm_dispatch_reset()
+
+
+def tuning_get(key):
+    return float(lib().gasfm_tuning_get(TUNING[key]))
+
+
+def tuning_set(key, value):
+    check(lib().gasfm_tuning_set(TUNING[key], float(value)), "gasfm_tuning_set")
+
+
+class tuned:
+    """Context manager: set dispatch thresholds, restore them on exit."""
+
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        self.prev = {k: tuning_get(k) for k in self.kv}
+        for k, v in self.kv.items():
+            tuning_set(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.prev.items():
+            tuning_set(k, v)
+        return False
+
+
+class dispatch_record:
+    """Context manager: ``rec.counts`` = launches per kernel inside the block."""
+
+    def __enter__(self):
+        self.start = dispatch_counts()
+        return self
+
+    def __exit__(self, *exc):
+        end = dispatch_counts()
+        self.counts = {k: end[k] - self.start[k] for k in end}
         return False
 
 
@@ -799,8 +864,10 @@ def esfm_fwd(cam, pt, vals, P, X, margin, hinge_w, hinge, part):
 
 
 def esfm_bwd(cptr, pptr, perm, cam, pt, vals, P, X, margin, hinge_w, hinge, equalize, valid_only, dloss, tot, dP,
-             dX):
+             dX, E_norm=None):
+    """E_norm: the edge count of the mean (default the local E; the global count on a sharded scene)."""
     E, n, m = cam.shape[0], X.shape[1], P.shape[0]
+    E_norm = E if E_norm is None else int(E_norm)
     for t, name in ((cptr, "cam_ptr"), (pptr, "pt_ptr"), (cam, "cam"), (pt, "pt")):
         _i32vec(t, name)
     if perm is not None:
@@ -809,7 +876,7 @@ def esfm_bwd(cptr, pptr, perm, cam, pt, vals, P, X, margin, hinge_w, hinge, equa
         raise ValueError("esfm_bwd: CSR shapes do not match m / n / E")
     _req(dP, "dP", 12), _req(dX, "dX", n)
     st = lib().gasfm_esfm_bwd(_p(cptr), m, _p(pptr), _p(perm) if perm is not None else None, _p(cam), _p(pt),
-                              _p(vals), E, _p(P), _p(X), n, margin, hinge_w, int(hinge), int(equalize),
+                              _p(vals), E, E_norm, _p(P), _p(X), n, margin, hinge_w, int(hinge), int(equalize),
                               int(valid_only), _p(dloss), _p(tot), _p(dP), _p(dX), _stream(X))
     check(st, "gasfm_esfm_bwd")
 

@@ -300,12 +300,14 @@ def attn_forward_partial(XL, XR, att, plan, heads, slope, dst=None):
         out[:N, HC + heads:] = 0.0
         return out[:N]
     combine_fwd_l1(plan, part, heads, C)
+    if dst is not None and (N > 1 or not plan.n_combine):
+        # unsplit segments wrote their partial straight into part row seg (slot == seg); the
+        # combine below only rewrites the split ones (all of them when N == 1)
+        dst.copy_(part[:N])
     if plan.n_combine:  # merge split pieces (slots >= N) into rows [0, N), raw
         ld = out.stride(0) if N > 1 else LDP
         _native.attn_combine(plan.combine, plan.n_combine, heads, C, part, None, False, out, out[:, HC:],
                              out[:, HC + heads:], ldOut=ld, ldStat=ld)
-    elif dst is not None:
-        dst.copy_(part[:N])
     return out[:N]
 
 

@@ -199,6 +199,7 @@ extern "C" int gasfm_gat_attn_fwd_lanes(const float* XL, int64_t ldXL, const flo
                     aligned16(att) && (!out || aligned16(out)) && (!part || aligned16(part)) && (!bias || aligned16(bias)),
                 "gasfm_gat_attn_fwd_lanes: 16-byte rows required");
   const int grid = resident_grid(reinterpret_cast<const void*>(&attn_fwd_lanes_kernel), kT, 0, n_items, kT);
+  note_dispatch(GASFM_K_ATTN_FWD_LANES);
   hipLaunchKernelGGL(attn_fwd_lanes_kernel, dim3(grid), dim3(kT), 0, reinterpret_cast<hipStream_t>(stream), XL, ldXL,
                      XR, ldXR, att, bias, perm, items, n_items, slope, finalize, out, ldOut, seg_max, seg_sum, ldStat,
                      part);
@@ -225,6 +226,7 @@ extern "C" int gasfm_gat_attn_bwd_lanes(const float* XL, int64_t ldXL, const flo
                 "gasfm_gat_attn_bwd_lanes: 16-byte rows required");
   const int waves = gasfm_gat_attn_bwd_waves(n_items, H, C);
   GASFM_REQUIRE(waves > 0 && waves % (kT / 64) == 0, "gasfm_gat_attn_bwd_lanes: wave count %d", waves);
+  note_dispatch(GASFM_K_ATTN_BWD_LANES);
   hipLaunchKernelGGL(attn_bwd_lanes_kernel, dim3(waves / (kT / 64)), dim3(kT), 0,
                      reinterpret_cast<hipStream_t>(stream), XL, ldXL, XR, ldXR, att, bias, perm, items, n_items, slope,
                      out, ldOut, seg_max, seg_sum, gout, ldG, dXL, ldDXL, dXR, ldDXR, part_dxr, datt_part,

@@ -12,6 +12,10 @@ namespace gasfm {
 
 void set_error(const char* fmt, ...);
 
+// Kernel-choice record and run-time thresholds (dispatch.cpp; GASFM_K_* / GASFM_TUNE_* in gasfm.h).
+void note_dispatch(int kernel_id);
+double tune(int key);
+
 inline int hip_status(hipError_t e, const char* where) {
   if (e == hipSuccess) return GASFM_OK;
   set_error("%s: %s", where, hipGetErrorString(e));

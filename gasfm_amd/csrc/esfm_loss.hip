@@ -9,7 +9,8 @@
 //   l_e   = pos_e ? || y_xy / y_z - m_e || : (margin - y_z) * hinge_w
 //   loss  = sum_e l_e / E
 // Backward with the reference's hook (pts_grad_equalization_pre_perspective_divide,
-// loss_functions.py:104-113): with G_e = dloss * dl_e/dy_e / E,
+// loss_functions.py:104-113): with G_e = dloss * dl_e/dy_e / E (E = E_norm: the global edge count
+// when a point-sharded rank passes its own edges),
 //   valid-only:  G'_e = pos_e ? normalize(G_e) / max(1, #pos) : G_e
 //   otherwise:   G'_e = normalize(G_e) / E
 //   none:        G'_e = G_e
@@ -117,13 +118,13 @@ __global__ __launch_bounds__(kT) void esfm_fwd_kernel(const int32_t* __restrict_
 __global__ __launch_bounds__(kT) void esfm_bwd_cam_kernel(const int32_t* __restrict__ cptr,
                                                           const int32_t* __restrict__ cam,
                                                           const int32_t* __restrict__ pt,
-                                                          const float* __restrict__ vals, int64_t E,
+                                                          const float* __restrict__ vals, int64_t E_norm,
                                                           const float* __restrict__ P, const float* __restrict__ X,
                                                           int64_t n, EsfmConf k, const float* __restrict__ dloss,
                                                           const float* __restrict__ tot, float* __restrict__ dP) {
   __shared__ float sh[kT / 64 * 12];
   const int c = blockIdx.x;
-  const float inv_e = 1.f / float(E), scale = dloss[0] * inv_e, inv_pos = 1.f / fmaxf(1.f, tot[1]);
+  const float inv_e = 1.f / float(E_norm), scale = dloss[0] * inv_e, inv_pos = 1.f / fmaxf(1.f, tot[1]);
   float acc[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) acc[i] = 0.f;
@@ -157,13 +158,13 @@ __global__ __launch_bounds__(kT) void esfm_bwd_cam_kernel(const int32_t* __restr
 __global__ __launch_bounds__(kT) void esfm_bwd_pt_kernel(const int32_t* __restrict__ pptr,
                                                          const int32_t* __restrict__ perm,
                                                          const int32_t* __restrict__ cam,
-                                                         const float* __restrict__ vals, int64_t E,
+                                                         const float* __restrict__ vals, int64_t E_norm,
                                                          const float* __restrict__ P, const float* __restrict__ X,
                                                          int64_t n, EsfmConf k, const float* __restrict__ dloss,
                                                          const float* __restrict__ tot, float* __restrict__ dX) {
   const int64_t p = int64_t(blockIdx.x) * kT + threadIdx.x;
   if (p >= n) return;
-  const float inv_e = 1.f / float(E), scale = dloss[0] * inv_e, inv_pos = 1.f / fmaxf(1.f, tot[1]);
+  const float inv_e = 1.f / float(E_norm), scale = dloss[0] * inv_e, inv_pos = 1.f / fmaxf(1.f, tot[1]);
   float a[4] = {0.f, 0.f, 0.f, 0.f};
   for (int q = pptr[p]; q < pptr[p + 1]; ++q) {
     const int e = perm ? perm[q] : q;
@@ -240,18 +241,19 @@ extern "C" int gasfm_esfm_fwd(const int32_t* cam, const int32_t* pt, const float
 }
 
 extern "C" int gasfm_esfm_bwd(const int32_t* cptr, int32_t m, const int32_t* pptr, const int32_t* perm,
-                              const int32_t* cam, const int32_t* pt, const float* vals, int64_t E, const float* P,
-                              const float* X, int64_t n, float margin, float hinge_w, int32_t hinge,
+                              const int32_t* cam, const int32_t* pt, const float* vals, int64_t E, int64_t E_norm,
+                              const float* P, const float* X, int64_t n, float margin, float hinge_w, int32_t hinge,
                               int32_t equalize, int32_t valid_only, const float* dloss, const float* tot, float* dP,
                               float* dX, void* stream) {
-  GASFM_REQUIRE(E > 0 && n > 0 && m > 0, "gasfm_esfm_bwd: E=%lld m=%d n=%lld", (long long)E, m, (long long)n);
+  GASFM_REQUIRE(E > 0 && n > 0 && m > 0 && E_norm >= E, "gasfm_esfm_bwd: E=%lld E_norm=%lld m=%d n=%lld",
+                (long long)E, (long long)E_norm, m, (long long)n);
   GASFM_REQUIRE(cptr && pptr && cam && pt && vals && P && X && dloss && tot && dP && dX, "gasfm_esfm_bwd: null pointer");
   const EsfmConf k{margin, hinge_w, hinge, equalize, valid_only};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(esfm_bwd_cam_kernel, dim3(m), dim3(kT), 0, st, cptr, cam, pt, vals, E, P, X, n, k, dloss, tot,
-                     dP);
+  hipLaunchKernelGGL(esfm_bwd_cam_kernel, dim3(m), dim3(kT), 0, st, cptr, cam, pt, vals, E_norm, P, X, n, k, dloss,
+                     tot, dP);
   hipLaunchKernelGGL(esfm_bwd_pt_kernel, dim3(unsigned((n + kT - 1) / kT)), dim3(kT), 0, st, pptr, perm, cam, vals,
-                     E, P, X, n, k, dloss, tot, dX);
+                     E_norm, P, X, n, k, dloss, tot, dX);
   return launch_status("gasfm_esfm_bwd");
 }
 

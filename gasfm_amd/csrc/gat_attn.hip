@@ -1140,45 +1140,25 @@ __global__ __launch_bounds__(kBlock) void attn_bwd_generic(
 // point-direction forward 278 us at 8192 waves vs 193 us at the 7168 that fit).  The grid is
 // the occupancy limit of the kernel x CU count; GASFM_ATTN_WAVES caps it (tuning sweeps).
 static int env_wave_cap() {
-  static const int cap = [] {
-    const char* e = std::getenv("GASFM_ATTN_WAVES");
-    const int v = e ? std::atoi(e) : 0;
-    return v > 0 ? v : 0;
-  }();
-  return cap;
+  const int v = int(tune(GASFM_TUNE_ATTN_WAVE_CAP));
+  return v > 0 ? v : 0;
 }
 
 // Direct-to-LDS forward for streamed (perm-free) 32-wide convs: default on (point direction
 // 165 -> 140 us, camera 109 -> 106 us on config 4); GASFM_ATTN_GLDS=0 selects the register path.
-static bool glds_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("GASFM_ATTN_GLDS");
-    return !e || std::atoi(e) != 0;
-  }();
-  return on;
-}
+static bool glds_enabled() { return tune(GASFM_TUNE_ATTN_GLDS) != 0.0; }
 
 // Grouped-item forward (attn_fwd_grp_kernel<U, MINW>) for streamed 32-wide convs: GASFM_ATTN_GRP
 // = 4 / 8 (U rows per lane per iteration), 46 / 48 (U = 4 at >= 6 / 8 waves per SIMD), 0 = off
 // (direct-to-LDS kernel).
 static int grp_rows() {
-  static const int u = [] {
-    const char* e = std::getenv("GASFM_ATTN_GRP");
-    const int v = e ? std::atoi(e) : 4;
-    return (v == 8 || v == 4 || v == 46 || v == 48) ? v : 0;
-  }();
-  return u;
+  const int v = int(tune(GASFM_TUNE_ATTN_GRP_ROWS));
+  return (v == 8 || v == 4 || v == 46 || v == 48) ? v : 0;
 }
 
 // Minimum fill (wave tasks / resident waves) for the grouped-item forward (A/B knob
 // GASFM_ATTN_GRP_MIN_FILL; 0 = always grouped when enabled).
-static double grp_min_fill() {
-  static const double f = [] {
-    const char* e = std::getenv("GASFM_ATTN_GRP_MIN_FILL");
-    return e ? std::atof(e) : 0.5;
-  }();
-  return f;
-}
+static double grp_min_fill() { return tune(GASFM_TUNE_ATTN_GRP_MIN_FILL); }
 
 static int grid_for(int n_items, int resident) {
   int waves = n_items > 0 ? n_items : 1;
@@ -1239,6 +1219,7 @@ extern "C" int gasfm_gat_attn_fwd(const float* XL, int64_t ldXL, const float* XR
       hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att, bias, items, n_items,
                          slope, finalize, out, ldOut, seg_max, seg_sum, ldStat, part);
     };
+    note_dispatch(GASFM_K_ATTN_FWD_GRP);
     if (grp == 8)
       launch(&attn_fwd_grp_kernel<8, 1>);
     else if (grp == 46)
@@ -1253,6 +1234,7 @@ extern "C" int gasfm_gat_attn_fwd(const float* XL, int64_t ldXL, const float* XR
     using G = Geom<32, 8>;
     const int grid =
         grid_for(n_items, resident_blocks(reinterpret_cast<const void*>(&attn_fwd_glds_kernel<G>), kBlock, 0));
+    note_dispatch(GASFM_K_ATTN_FWD_GLDS);
     hipLaunchKernelGGL((attn_fwd_glds_kernel<G>), dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att, bias,
                        items, n_items, slope, finalize, out, ldOut, seg_max, seg_sum, ldStat, part);
     done = true;
@@ -1261,6 +1243,7 @@ extern "C" int gasfm_gat_attn_fwd(const float* XL, int64_t ldXL, const float* XR
     done = dispatch_shape(H, C, [&](auto g) {
       using G = decltype(g);
       const int grid = grid_for(n_items, resident_blocks(reinterpret_cast<const void*>(&attn_fwd_kernel<G>), kBlock, 0));
+      note_dispatch(GASFM_K_ATTN_FWD_VEC);
       hipLaunchKernelGGL((attn_fwd_kernel<G>), dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att,
                          bias, perm, items, n_items, slope, finalize, out, ldOut, seg_max, seg_sum, ldStat, part);
     });
@@ -1268,6 +1251,7 @@ extern "C" int gasfm_gat_attn_fwd(const float* XL, int64_t ldXL, const float* XR
   if (!done) {
     const size_t lds = (kBlock / kWave) * 2 * H * sizeof(float);
     const int grid = grid_for(n_items, resident_blocks(reinterpret_cast<const void*>(&attn_fwd_generic), kBlock, lds));
+    note_dispatch(GASFM_K_ATTN_FWD_GENERIC);
     hipLaunchKernelGGL(attn_fwd_generic, dim3(grid), dim3(kBlock), lds, st,
                        XL, ldXL, XR, ldXR, att, bias, perm, items, n_items, H, C, slope, finalize, out, ldOut,
                        seg_max, seg_sum, ldStat, part);
@@ -1289,12 +1273,14 @@ extern "C" int gasfm_gat_attn_combine(const gasfm_combine_item* combine, int32_t
       using G = decltype(g);
       const int threads = 1024;
       const size_t lds = size_t(threads / kWave) * G::LPE * (G::VEC + 2 * G::HPL) * sizeof(float);
+      note_dispatch(GASFM_K_ATTN_COMBINE_VEC);
       hipLaunchKernelGGL((attn_combine_kernel<G>), dim3(n_combine), dim3(threads), lds, st, combine, part, bias,
                          finalize, out, ldOut, seg_max, seg_sum, ldStat);
     });
   }
   if (!done) {
     const int grid = (n_combine + (kBlock / kWave) - 1) / (kBlock / kWave);
+    note_dispatch(GASFM_K_ATTN_COMBINE_GENERIC);
     hipLaunchKernelGGL(attn_combine_generic, dim3(grid), dim3(kBlock), 0, st, combine, n_combine, H, C, part, bias,
                        finalize, out, ldOut, seg_max, seg_sum, ldStat);
   }
@@ -1342,6 +1328,7 @@ extern "C" int gasfm_gat_attn_bwd(const float* XL, int64_t ldXL, const float* XR
   bool done = false;
   if (vec_ok && H * C == 32 && C == 8 && (perm == nullptr || xl_by_position) && glds_enabled() &&
       aligned16(seg_max) && aligned16(seg_sum)) {
+    note_dispatch(GASFM_K_ATTN_BWD_GLDS);
     hipLaunchKernelGGL((attn_bwd_glds_kernel<Geom<32, 8>>), dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR,
                        att, bias, perm, items, n_items, slope, out, ldOut, seg_max, seg_sum, gout, ldG, dXL, ldDXL,
                        dXR, ldDXR, part_dxr, datt_part);
@@ -1350,12 +1337,14 @@ extern "C" int gasfm_gat_attn_bwd(const float* XL, int64_t ldXL, const float* XR
   if (vec_ok && !done) {
     done = dispatch_shape(H, C, [&](auto g) {
       using G = decltype(g);
+      note_dispatch(GASFM_K_ATTN_BWD_VEC);
       hipLaunchKernelGGL((attn_bwd_kernel<G>), dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att, bias,
                          perm, items, n_items, slope, out, ldOut, seg_max, seg_sum, gout, ldG, dXL, ldDXL, dXR,
                          ldDXR, part_dxr, datt_part, int(xl_by_position != 0));
     });
   }
   if (!done) {
+    note_dispatch(GASFM_K_ATTN_BWD_GENERIC);
     hipLaunchKernelGGL(attn_bwd_generic, dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att, bias, perm,
                        items, n_items, H, C, slope, out, ldOut, seg_max, seg_sum, gout, ldG, dXL, ldDXL, dXR,
                        ldDXR, part_dxr, datt_part, int(xl_by_position != 0));

@@ -54,12 +54,11 @@ class ESFMLossFn(torch.autograd.Function):
         P, X, cam, pt, vals, cam_ptr, pt_ptr, pt_perm, tot = ctx.saved_tensors
         margin, hinge_w, hinge, equalize, valid_only = ctx.conf
         dP, dX = torch.empty_like(P), torch.empty_like(X)
-        dloss = dloss.reshape(1).to(torch.float32)
-        if ctx.E != cam.shape[0]:
-            dloss = dloss * (cam.shape[0] / ctx.E)  # the kernels divide by the local edge count
-        dloss = dloss.contiguous()
+        dloss = dloss.reshape(1).to(torch.float32).contiguous()
+        # E_norm = the global edge count on a sharded scene: the un-equalized terms and the equalized
+        # (normalize(G) / E) branch both divide by it, as loss_functions.py:110 divides by sum(valid_pts)
         _native.esfm_bwd(cam_ptr, pt_ptr, pt_perm, cam, pt, vals, P, X, margin, hinge_w, hinge, equalize, valid_only,
-                         dloss, tot, dP, dX)
+                         dloss, tot, dP, dX, E_norm=ctx.E)
         if ctx.shard is not None:
             ctx.shard.all_reduce_(dP)
         return dP.view(-1, 3, 4), dX, None, None, None, None, None, None, None, None

@@ -210,4 +210,9 @@ def inject_outliers(scene_data, outlier_injection_rate, z=None, generator=None, 
     out = scene_from_dense_device(M_new, Ns, y, scene_data.scene_name,
                                   calibrated=getattr(scene_data, "calibrated", True), max_piece=max_piece)
     out.outliers_mask = inj.outliers_mask
+    # the reference passes these through to the rebuilt SceneData (dataset_utils.py:451-459); outlier
+    # injection moves measurements of existing observations only, so the depth targets still apply
+    for k in ("store_depth_targets", "depths"):
+        if getattr(scene_data, k, None) is not None:
+            setattr(out, k, getattr(scene_data, k))
     return out

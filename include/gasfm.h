@@ -57,6 +57,45 @@ typedef struct gasfm_combine_item {
 const char* gasfm_last_error(void);
 int gasfm_version(void);
 
+/* ---- kernel-choice record and tuning (host) ----------------------------- */
+
+/* Kernels picked by the size / occupancy dependent dispatches.  Every launch
+ * through such a dispatch bumps its counter at launch time (a captured graph
+ * counts once per capture).  Test and profiling infrastructure only: the
+ * reference has no counterpart. */
+enum {
+  GASFM_K_ATTN_FWD_GRP = 0,      /* grouped items, 8 segments per wave task (32-wide, streamed XL) */
+  GASFM_K_ATTN_FWD_GLDS = 1,     /* one item per wave, direct-to-LDS prefetch (32-wide, streamed) */
+  GASFM_K_ATTN_FWD_VEC = 2,      /* one item per wave, registers (any tabulated (H, C), perm ok) */
+  GASFM_K_ATTN_FWD_GENERIC = 3,  /* any (H, C) */
+  GASFM_K_ATTN_FWD_LANES = 4,    /* one lane per item (H = 4, C = 1) */
+  GASFM_K_ATTN_BWD_GLDS = 5,
+  GASFM_K_ATTN_BWD_VEC = 6,
+  GASFM_K_ATTN_BWD_GENERIC = 7,
+  GASFM_K_ATTN_BWD_LANES = 8,
+  GASFM_K_ATTN_COMBINE_VEC = 9,
+  GASFM_K_ATTN_COMBINE_GENERIC = 10,
+  GASFM_K_ATTN_BWD_GRP = 11,     /* grouped items backward (32-wide, streamed XL) */
+  GASFM_K_COUNT = 16
+};
+
+/* Copies min(n, GASFM_K_COUNT) counters into out; returns GASFM_K_COUNT. */
+int gasfm_dispatch_counts(int64_t* out, int32_t n);
+void gasfm_dispatch_reset(void);
+
+/* Dispatch thresholds (initialised from the environment variable named in
+ * the comment; gasfm_tuning_set overrides them for the rest of the process). */
+enum {
+  GASFM_TUNE_ATTN_GRP_ROWS = 0,      /* GASFM_ATTN_GRP: 4 / 8 / 46 / 48, 0 = grouped forward off */
+  GASFM_TUNE_ATTN_GRP_MIN_FILL = 1,  /* GASFM_ATTN_GRP_MIN_FILL: grouped when tasks >= fill x resident waves */
+  GASFM_TUNE_ATTN_GLDS = 2,          /* GASFM_ATTN_GLDS: direct-to-LDS kernels on (1) / off (0) */
+  GASFM_TUNE_ATTN_WAVE_CAP = 3,      /* GASFM_ATTN_WAVES: cap on item-loop waves, 0 = occupancy */
+  GASFM_TUNE_ATTN_GRP_BWD = 4,       /* grouped backward on (1) / off (0) */
+  GASFM_TUNE_COUNT = 8
+};
+int gasfm_tuning_set(int32_t key, double value);
+double gasfm_tuning_get(int32_t key);
+
 /* ---- graph preprocessing (host, CPU; usable in DataLoader workers) ------ */
 
 /* Counting-sort CSR build: ptr[n+1] = segment offsets of `key` (values in
@@ -439,15 +478,17 @@ int gasfm_pose_bwd(const float* x, int64_t ldx, int64_t m, const float* dP, floa
  * camera-sorted edges) and dpts3D [4, n] (pt_ptr + perm: point CSR, perm = edge ids in point
  * order, NULL = identity).  equalize / valid_only: pts_grad_equalization_pre_perspective_divide /
  * normalize_grad_wrt_valid_projections_only; hinge selects the hinge_loss branch
- * (geo_utils.get_positive_projected_pts_mask, geo_utils.py:721-726). */
+ * (geo_utils.get_positive_projected_pts_mask, geo_utils.py:721-726).  E_norm: the edge count the
+ * mean divides by (E on one GPU; the GLOBAL count on a point-sharded scene, where each rank
+ * passes its own edges: loss_functions.py:110 divides by the global sum(valid_pts)). */
 int32_t gasfm_esfm_part_rows(int64_t E);
 int gasfm_esfm_fwd(const int32_t* cam, const int32_t* pt, const float* vals, int64_t E, const float* P,
                    const float* pts3D, int64_t n, float margin, float hinge_w, int32_t hinge, float* part,
                    void* stream);
 int gasfm_esfm_bwd(const int32_t* cam_ptr, int32_t m, const int32_t* pt_ptr, const int32_t* perm, const int32_t* cam,
-                   const int32_t* pt, const float* vals, int64_t E, const float* P, const float* pts3D, int64_t n,
-                   float margin, float hinge_w, int32_t hinge, int32_t equalize, int32_t valid_only,
-                   const float* dloss, const float* tot, float* dP, float* dpts3D, void* stream);
+                   const int32_t* pt, const float* vals, int64_t E, int64_t E_norm, const float* P,
+                   const float* pts3D, int64_t n, float margin, float hinge_w, int32_t hinge, int32_t equalize,
+                   int32_t valid_only, const float* dloss, const float* tot, float* dP, float* dpts3D, void* stream);
 
 /* ---- global node (ONE row): LayerNorm -> ReLU -> Linear (+ residual) ----
  * Replaces the M = 1 aten chains on the global feature vector: norm_and_proj_global2view /

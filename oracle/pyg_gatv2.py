@@ -108,12 +108,13 @@ def gatv2_segment_reference(XL, XR, att, bias, dst, num_targets, negative_slope=
     z = F.leaky_relu(XR.index_select(0, dst) + XL, negative_slope)
     e = (z * att.view(1, H, C)).sum(-1)
     idx = dst.view(-1, 1).expand(-1, H)
-    emax = torch.full((num_targets, H), -math.inf, dtype=XL.dtype).scatter_reduce(
+    dev = XL.device  # the checker may run on the device in fp64 at full config-4 size
+    emax = torch.full((num_targets, H), -math.inf, dtype=XL.dtype, device=dev).scatter_reduce(
         0, idx, e.detach(), reduce="amax", include_self=True)
     emax_g = emax.index_select(0, dst)
     ex = (e - emax_g).exp()
-    esum = torch.zeros((num_targets, H), dtype=XL.dtype).scatter_add(0, idx, ex)
+    esum = torch.zeros((num_targets, H), dtype=XL.dtype, device=dev).scatter_add(0, idx, ex)
     alpha = ex / (esum.index_select(0, dst) + 1e-16)
-    out = torch.zeros((num_targets, H, C), dtype=XL.dtype).index_add(0, dst, XL * alpha.unsqueeze(-1))
+    out = torch.zeros((num_targets, H, C), dtype=XL.dtype, device=dev).index_add(0, dst, XL * alpha.unsqueeze(-1))
     out = out.view(num_targets, H * C) + bias
     return out, emax, esum

@@ -316,15 +316,15 @@ def test_rccl_bench_captures_and_replays(tmp_path, cams):
     assert ("point+camera" in res["config"]["parallelism"]) == cams
 
 
-def _esfm_conf():
+def _esfm_conf(valid_only=True):
     import gasfm_amd
     return gasfm_amd.Conf({"model": {"view_head": {"enabled": True}, "scenepoint_head": {"enabled": True}},
                            "loss": {"infinity_pts_margin": 1e-4, "pts_grad_equalization_pre_perspective_divide": True,
-                                    "normalize_grad_wrt_valid_projections_only": True, "hinge_loss": True,
+                                    "normalize_grad_wrt_valid_projections_only": valid_only, "hinge_loss": True,
                                     "hinge_loss_weight": 1.0}})
 
 
-def _worker_sharded_esfm(rank, world, port, q):
+def _worker_sharded_esfm(rank, world, port, q, valid_only=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -337,7 +337,7 @@ def _worker_sharded_esfm(rank, world, port, q):
         net.load_state_dict(deterministic_state_dict(net.state_dict()))
         model = gd.ShardedGraphAttnSfMNet(net.to(dev))
         data = gd.shard_scene(sc, rank, world, max_piece=64).to(dev)
-        loss = gasfm_amd.ESFMLoss(_esfm_conf())(model(data), data)
+        loss = gasfm_amd.ESFMLoss(_esfm_conf(valid_only))(model(data), data)
         loss.backward()
         model.sync_grads()
         grads = {k: p.grad.detach().cpu().numpy() for k, p in net.named_parameters()}
@@ -347,10 +347,13 @@ def _worker_sharded_esfm(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_sharded_esfm_loss_matches_single_gpu(device):
+@pytest.mark.parametrize("valid_only", [True, False])
+def test_sharded_esfm_loss_matches_single_gpu(device, valid_only):
     """ESFMLoss on a point-sharded scene: every rank gets the GLOBAL loss (sum and
     #valid-depth all-reduced, divided by the global edge count) and, after sync_grads, every
-    parameter gradient equals the single-GPU one and is bitwise identical across ranks."""
+    parameter gradient equals the single-GPU one and is bitwise identical across ranks.
+    valid_only=False: the equalized gradients divide by the GLOBAL edge count
+    (loss_functions.py:110), not the rank's own."""
     import gasfm_amd
     from oracle.weights import deterministic_state_dict
     sc = synthetic.scaled_config4(0.02, seed=5)
@@ -358,14 +361,14 @@ def test_sharded_esfm_loss_matches_single_gpu(device):
     net.load_state_dict(deterministic_state_dict(net.state_dict()))
     net = net.to(device)
     data = gasfm_amd.SceneData.from_synthetic(sc, max_piece=64).to(device)
-    loss = gasfm_amd.ESFMLoss(_esfm_conf())(net(data), data)
+    loss = gasfm_amd.ESFMLoss(_esfm_conf(valid_only))(net(data), data)
     loss.backward()
     ref = {k: p.grad.detach().double().cpu().numpy() for k, p in net.named_parameters()}
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_sharded_esfm, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker_sharded_esfm, args=(r, 2, port, q, valid_only)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted((q.get(timeout=600) for _ in procs), key=lambda t: t[0])
