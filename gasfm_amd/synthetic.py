@@ -117,6 +117,19 @@ def config4(m=1000, n=200_000, seed=4):
     return windowed_scene(m, n, seed=seed)
 
 
+CONFIG2_M, CONFIG2_N, CONFIG2_EXTRA = 133, 23674, 4
+
+
+def config2_standin(seed=2):
+    """Synthetic stand-in for BASELINE config 2's single scene, AlcatrazCourtyard
+    (optim_euc_gasfm.conf:6; single_scene_optimization.py:15-123).  The dataset file
+    (datasets/Euclidean/AlcatrazCourtyard.npz, README.md:70-76) is not available offline, so its
+    size is taken from the published dataset statistics as recalled (133 views, 23,674 points:
+    UNVERIFIED here) and the track length, unknown offline, is set to 2 + Poisson(4) views per
+    point (~6): E ~ 142k.  Values and visibility are synthetic (windowed SfM-like generator)."""
+    return windowed_scene(CONFIG2_M, CONFIG2_N, mean_extra=CONFIG2_EXTRA, seed=seed)
+
+
 def scaled_config4(scale, seed=4):
     """config 4 with m and n scaled by `scale` (parity tests at oracle-friendly sizes)."""
     return windowed_scene(max(16, int(1000 * scale)), max(64, int(200_000 * scale)), seed=seed)
