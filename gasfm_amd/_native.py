@@ -49,8 +49,14 @@ _SIGS = {
                                        _vp, _f32, _vp, _vp]),
     "gasfm_edge_epilogue_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _i32, _f32, _vp, _vp, _vp,
                                        _vp, _vp]),
+    "gasfm_edge_cam_bwd_part_rows": (_i32, [_i32]),
+    "gasfm_edge_cam_bwd_part_cols": (_i32, []),
+    "gasfm_edge_cam_fwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32,
+                                  _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
+    "gasfm_edge_cam_bwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _vp, _i64,
+                                  _vp, _i64, _vp, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _vp]),
     "gasfm_edge_prologue_bwd": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _i32, _f32, _vp,
-                                       _vp, _vp]),
+                                       _vp, _vp, _i64, _vp]),
     "gasfm_segment_rowsum": (_i32, [_vp, _i32, _vp, _vp, _i64, _f32, _vp, _vp, _vp]),
     "gasfm_colsum_counters": (_i32, [_i32]),
     "gasfm_colsum_multi": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -551,12 +557,44 @@ def edge_epilogue_bwd(items, n_items, dPo, P, P0, ln_w, ln_b, eps, Wp, scale, dS
     check(st, "gasfm_edge_epilogue_bwd")
 
 
-def edge_prologue_bwd(dXL, P, dRes, ln_w, ln_b, eps, W, Wp, scale, dP, part, W2=None):
+def edge_prologue_bwd(dXL, P, dRes, ln_w, ln_b, eps, W, Wp, scale, dP, part, W2=None, dXLc=None):
+    """dXLc: the camera half of dXL in its own [E, 32] buffer (dXL then holds the point half)."""
     _req(P, "P", 32)
     st = lib().gasfm_edge_prologue_bwd(_p(dXL), dXL.stride(0), _p(P), _p(dRes), P.shape[0], _p(ln_w), _p(ln_b), eps,
                                        _p(W), _p(W2), _p(Wp), Wp.shape[1] if Wp is not None else 0, scale, _p(dP),
-                                       _p(part), _stream(P))
+                                       _p(part), _p(dXLc), dXLc.stride(0) if dXLc is not None else 0, _stream(P))
     check(st, "gasfm_edge_prologue_bwd")
+
+
+def edge_cam_fwd(P, ln_w, ln_b, eps, Wpt, bpt, Wc, bc, XLp, pos, XR, att, bias, slope, plan_items, n_items,
+                 finalize, out, seg_max, seg_sum, part, ldStat=4):
+    """Edge prologue + camera-direction attention forward (csrc/edge_cam.hip): XLp [E, 32] (point
+    half of lin_l, written through pos), camera aggregates into out / seg_max / seg_sum (complete
+    items) or packed partial rows part [slots, 40]."""
+    _req(P, "P", 32)
+    ldXR = _rows32(XR, "XR")
+    st = lib().gasfm_edge_cam_fwd(_p(P), _p(ln_w), _p(ln_b), eps, _p(Wpt), _p(bpt), _p(Wc), _p(bc), _p(XLp),
+                                  XLp.stride(0), _p(pos), _p(XR), ldXR, _p(att), _p(bias), slope, _p(plan_items),
+                                  n_items, int(finalize), _p(out), out.stride(0) if out is not None else 0,
+                                  _p(seg_max), _p(seg_sum), ldStat, _p(part), _stream(P))
+    check(st, "gasfm_edge_cam_fwd")
+
+
+def edge_cam_bwd_part_shape(n_items):
+    L = lib()
+    return int(L.gasfm_edge_cam_bwd_part_rows(n_items)), int(L.gasfm_edge_cam_bwd_part_cols())
+
+
+def edge_cam_bwd(P, ln_w, ln_b, eps, Wc, bc, XR, att, bias, slope, out, seg_max, seg_sum, gout, plan_items, n_items,
+                 dXLc, dXR, part_dxr, part, ldStat=4):
+    """Camera-attention backward with XLc recomputed from P: dXLc [E, 32], dXR, [datt | dbias] partials."""
+    _req(P, "P", 32)
+    ldXR = _rows32(XR, "XR")
+    st = lib().gasfm_edge_cam_bwd(_p(P), _p(ln_w), _p(ln_b), eps, _p(Wc), _p(bc), _p(XR), ldXR, _p(att), _p(bias),
+                                  slope, _p(out), out.stride(0), _p(seg_max), _p(seg_sum), ldStat, _p(gout),
+                                  gout.stride(0), _p(plan_items), n_items, _p(dXLc), dXLc.stride(0), _p(dXR),
+                                  dXR.stride(0), _p(part_dxr), _p(part), _stream(P))
+    check(st, "gasfm_edge_cam_bwd")
 
 
 def segment_rowsum(items, n_items, perm, X, scale, out, part):

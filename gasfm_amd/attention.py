@@ -361,9 +361,12 @@ class GatAttentionFn(torch.autograd.Function):
     """out[i] = sum_{j->i} softmax_j(att . leaky_relu(XL[j] + XR[i])) XL[j] + bias."""
 
     @staticmethod
-    def forward(ctx, XL, XR, att, bias, plan, heads, slope):
-        out, smax, ssum = attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True)
+    def forward(ctx, XL, XR, att, bias, plan, heads, slope, xl_sorted=False, sec=None):
+        """xl_sorted: XL rows in segment order (written through plan.pos); the XL gradient is still
+        returned in source-row (edge) order.  sec: streams.SideSection joined before backward."""
+        out, smax, ssum = attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True, xl_sorted=xl_sorted)
         ctx.plan, ctx.heads, ctx.slope = plan, heads, slope
+        ctx.xl_sorted, ctx.sec = xl_sorted, sec
         ctx.defer = _native.defer_token(att, bias)
         ctx.save_for_backward(XL, XR, att, bias, out, smax, ssum)
         ctx.mark_non_differentiable(smax, ssum)
@@ -374,11 +377,12 @@ class GatAttentionFn(torch.autograd.Function):
     def backward(ctx, gout, _gm, _gs):
         XL, XR, att, bias, out, smax, ssum = ctx.saved_tensors
         if gout is None:
-            return None, None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None, None
+        if ctx.sec is not None:
+            ctx.sec.join()
         dXL, dXR, datt, dbias = attn_backward_raw(XL, XR, att, bias, ctx.plan, ctx.heads, ctx.slope, out, smax,
-                                                  ssum, gout,
-                                                  defer=ctx.defer)
-        return dXL, dXR, datt.view_as(att), dbias, None, None, None
+                                                  ssum, gout, xl_sorted=ctx.xl_sorted, defer=ctx.defer)
+        return dXL, dXR, datt.view_as(att), dbias, None, None, None, None, None
 
 
 class GlobalPairFn(torch.autograd.Function):

@@ -520,17 +520,18 @@ struct PbTile {
 };
 
 template <bool RES>
-__device__ __forceinline__ void pb_issue(PbTile& T, const float* __restrict__ dXL, int64_t ldX,
-                                         const float* __restrict__ P, const float* __restrict__ dRes, int64_t row0,
+__device__ __forceinline__ void pb_issue(PbTile& T, const float* __restrict__ dXL, int64_t ldX, int64_t row0,
+                                         const float* __restrict__ P, const float* __restrict__ dRes,
                                          int nrows, int lane) {
   // Rows past the end re-read row 0 of the tile (always valid) and are zeroed afterwards: a
   // conditional load would be lowered to a flat access through a pointer select.
+  // dXL: this lane's column block of the gradient (the point or the camera half, see the kernel)
   const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int r = (lane >> 4) + 4 * u;
     const int rr = r < nrows ? r : 0;
-    T.x[u] = *reinterpret_cast<const float4*>(dXL + (row0 + rr) * ldX + (lane & 15) * 4);
+    T.x[u] = *reinterpret_cast<const float4*>(dXL + (row0 + rr) * ldX);
     if (r >= nrows) T.x[u] = z;
   }
 #pragma unroll
@@ -553,7 +554,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINWAVES) void edge_prologue_b
     const float* __restrict__ dXL, int64_t ldX, const float* __restrict__ P, const float* __restrict__ dRes,
     int64_t E, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
     const float* __restrict__ W, const float* __restrict__ W2, const float* __restrict__ Wp, int ldWp, float scale,
-    float* __restrict__ dP, float* __restrict__ part) {
+    float* __restrict__ dP, float* __restrict__ part, const float* __restrict__ dXLc, int64_t ldC) {
   __shared__ float lds[PB_W + kWaves * PB_WAVE];
   float* Wl = lds;                  // B[k][j] = W[k][j]     (k < 64)
   float* Wq = lds + NX * LDW;       // B[k][j] = scale Wp[k][j] (k < 32)
@@ -585,8 +586,13 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINWAVES) void edge_prologue_b
   const int64_t ntiles = (E + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWaves + wave, nw = int64_t(gridDim.x) * kWaves;
   auto rows_of = [&](int64_t t) { return int(E - t * TR < TR ? E - t * TR : TR); };
+  // columns (lane & 15) * 4 .. + 3 of the 64-wide dXL: from dXL itself, or its camera half from dXLc
+  // when the two halves live in separate [E, 32] buffers (edge_cam.hip writes dXLc)
+  const int c4 = (lane & 15) * 4;
+  const float* dxl = (dXLc && c4 >= F) ? dXLc + (c4 - F) : dXL + c4;
+  const int64_t ldx = (dXLc && c4 >= F) ? ldC : ldX;
   PbTile nxt;
-  if (gw < ntiles) pb_issue<RES>(nxt, dXL, ldX, P, dRes, gw * TR, rows_of(gw), lane);
+  if (gw < ntiles) pb_issue<RES>(nxt, dxl, ldx, gw * TR, P, dRes, rows_of(gw), lane);
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row0 = t * TR;
     const int nrows = rows_of(t);
@@ -627,7 +633,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINWAVES) void edge_prologue_b
       }
     }
     // request the next tile before this one's MFMA work
-    if (t + nw < ntiles) pb_issue<RES>(nxt, dXL, ldX, P, dRes, (t + nw) * TR, rows_of(t + nw), lane);
+    if (t + nw < ntiles) pb_issue<RES>(nxt, dxl, ldx, (t + nw) * TR, P, dRes, rows_of(t + nw), lane);
     wave_sync();
     // dP_hat (C layout: edge 4g+r, column nt*16+c) = dXL W (+ dRes scale Wp)
     f32x4 acc[2] = {zero4(), zero4()};
@@ -882,8 +888,9 @@ extern "C" int gasfm_edge_epilogue_bwd(const gasfm_work_item* items, int32_t n_i
 extern "C" int gasfm_edge_prologue_bwd(const float* dXL, int64_t ldX, const float* P, const float* dRes, int64_t E,
                                        const float* ln_w, const float* ln_b, float eps, const float* W,
                                        const float* W2, const float* Wp, int32_t ldWp, float scale, float* dP,
-                                       float* part, void* stream) {
-  GASFM_REQUIRE(dXL && P && W && dP && part && ldX >= NX, "gasfm_edge_prologue_bwd: bad args");
+                                       float* part, const float* dXLc, int64_t ldC, void* stream) {
+  GASFM_REQUIRE(dXL && P && W && dP && part && ldX >= (dXLc ? F : NX), "gasfm_edge_prologue_bwd: bad args");
+  GASFM_REQUIRE(!dXLc || (ldC >= F && ldC % 4 == 0 && aligned16(dXLc)), "gasfm_edge_prologue_bwd: dXLc rows");
   GASFM_REQUIRE(!dRes || Wp, "gasfm_edge_prologue_bwd: dRes needs Wp");
   GASFM_REQUIRE(aligned16(dXL) && ldX % 4 == 0 && aligned16(P) && (!dRes || aligned16(dRes)) && aligned16(dP),
                 "gasfm_edge_prologue_bwd: dXL/P/dRes/dP not 16-byte aligned");
@@ -893,7 +900,7 @@ extern "C" int gasfm_edge_prologue_bwd(const float* dXL, int64_t ldX, const floa
   const bool ln = ln_w != nullptr, res = dRes != nullptr;
 #define GASFM_LAUNCH(LNV, RESV)                                                                                 \
   hipLaunchKernelGGL((edge_prologue_bwd_kernel<LNV, RESV>), dim3(g), dim3(kThreads), 0, st, dXL, ldX, P, dRes, \
-                     E, ln_w, ln_b, eps, W, W2, Wp, ldWp, scale, dP, part)
+                     E, ln_w, ln_b, eps, W, W2, Wp, ldWp, scale, dP, part, dXLc, ldC)
   if (ln && res)
     GASFM_LAUNCH(true, true);
   else if (ln)

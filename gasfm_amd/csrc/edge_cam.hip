@@ -1,0 +1,485 @@
+// Edge prologue with the CAMERA-direction GATv2 attention fused in, and the camera attention's
+// backward recomputing its source rows, gfx950.
+//
+// A block's edge prologue computes both convs' lin_l on P_hat = relu(LN(P)) (layers.py:232-234;
+// PyG's lin_l) -- XL = [XLp | XLc], 32 + 32 features per edge -- and the camera direction's
+// attention (Proj2View, layers.py:329-335) then reduces XLc over each camera's edges.  The edges
+// are camera-major, so a camera segment is a contiguous run of the prologue's own 16-edge tiles:
+//
+//   edge_cam_fwd   over the camera plan's work items (one camera, <= max_piece edges each):
+//                  XLp is written (in point-segment order through pos, as edge_prologue_fwd does)
+//                  and XLc is consumed by an online softmax in registers -- never stored.
+//   edge_cam_bwd   the camera attention's backward (gat_attn.hip attn_bwd_*): XLc recomputed from
+//                  P (LayerNorm + 16 MFMAs per tile) instead of read back, dXLc written for
+//                  gasfm_edge_prologue_bwd (which takes the two halves of dXL separately), dXR per
+//                  camera, d att / d bias per workgroup.
+// HBM per edge and block: the forward writes 256 B less (XLc) and the camera attention's forward
+// read of XLc (128 B) is gone; the backward reads P (128 B) where it read XLc (128 B).
+//
+// MFMA orientation: the TRANSPOSED products XL^T = W P_hat^T (A = W from LDS, B = P_hat^T from the
+// wave's LDS tile) leave lane (g = l >> 4, c = l & 15) holding features 16 ot + 4 g + r (r < 4) of
+// EDGE c: one edge per lane column.  A head (8 features) is then 4 of the lane's registers plus
+// the same 4 of lane l ^ 16, the per-edge softmax state is one per lane and head, and a lane's
+// XLp / dXLc features are one float4 store per 16-feature tile (a row is 8 lanes x 16 B).
+//
+// Semantics are those of gasfm_gat_attn_fwd / _bwd on the camera plan: complete items write
+// out[seg] (finalized with bias, or the raw acc), split items packed partial rows [acc 32 | max 4 |
+// sum 4] for gasfm_gat_attn_combine; empty segments give out = bias, max = -inf, sum = 0; d bias
+// sums gout over every segment (once, at its first item).
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+#include "tile.hpp"
+
+namespace gasfm {
+namespace {
+
+using namespace tile;
+
+constexpr int F = 32;       // projection features (n_feat_proj) = HC of both convs (H = 4, C = 8)
+constexpr int H = 4;
+constexpr int NX = 64;      // [point | camera] lin_l outputs
+constexpr int LD34 = 34;    // LDS row stride of the P_hat tile
+constexpr int LDA = 36;     // LDS row stride of staged weights W[out][in] (A operand, 2-way banks)
+constexpr int PART = F + 2 * H;  // packed partial row
+
+__device__ __forceinline__ float leaky(float z, float slope) { return z > 0.f ? z : z * slope; }
+
+// max over the 16 lanes of a row (DPP, as lanes.hpp's sums)
+__device__ __forceinline__ float row_max16(float v) {
+  v = fmaxf(v, xor_lane<1>(v));
+  v = fmaxf(v, xor_lane<2>(v));
+  v = fmaxf(v, dpp_mov<0x141>(v));  // row_half_mirror: quad 0 <-> quad 1 of each half-row
+  v = fmaxf(v, xor_lane<8>(v));
+  return v;
+}
+
+// Rows of a 16 x 32 tile in row layout: lane l holds row (l >> 3) + 8u (u = 0, 1), columns
+// 4 (l & 7) .. + 3.  Rows >= nrows re-read row 0 (always valid) and are zeroed.
+__device__ __forceinline__ void load_rows(const float* __restrict__ X, int64_t ld, int64_t row0, int nrows,
+                                          float4 (&v)[2], int lane) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int r = (lane >> 3) + 8 * u;
+    v[u] = *reinterpret_cast<const float4*>(X + (row0 + (r < nrows ? r : 0)) * ld + (lane & 7) * 4);
+    if (r >= nrows) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// relu(LN(P)) of the row-layout registers into the wave's LDS tile (row stride 34); rows >= nrows
+// are zeros.  LN == false: the raw rows (the final update, graph_attn_sfm.py:141-148).
+template <bool LN>
+__device__ __forceinline__ void phat_to_lds(const float4 (&v)[2], int nrows, float4 g4, float4 b4, float eps,
+                                            float* T, int lane) {
+  const int cc = (lane & 7) * 4;
+  const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int r = (lane >> 3) + 8 * u;
+    const float x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+    float mean = 0.f, rstd = 1.f;
+    if (LN) {
+      mean = group_sum<8>(x[0] + x[1] + x[2] + x[3]) * (1.f / F);
+      float q = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q = fmaf(x[k] - mean, x[k] - mean, q);
+      rstd = rsqrtf(group_sum<8>(q) * (1.f / F) + eps);
+    }
+    float ph[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float xh = LN ? (x[k] - mean) * rstd : x[k];
+      ph[k] = (r < nrows) ? (LN ? fmaxf(fmaf(xh, gg[k], bb[k]), 0.f) : xh) : 0.f;
+    }
+    float2* d = reinterpret_cast<float2*>(T + r * LD34 + cc);
+    d[0] = make_float2(ph[0], ph[1]);
+    d[1] = make_float2(ph[2], ph[3]);
+  }
+}
+
+// acc[ot] += W[16 ot + c][k] P_hat[edge c][k] over k < 32: A = W rows (LDS, stride LDA), B = P_hat^T
+template <int OT>
+__device__ __forceinline__ void xl_t(const float* Wl, const float* T, f32x4 (&acc)[OT], int c, int g) {
+#pragma unroll
+  for (int s = 0; s < F / 4; ++s) {
+    const float b = T[c * LD34 + 4 * s + g];
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) acc[ot] = mfma16(Wl[(16 * ot + c) * LDA + 4 * s + g], b, acc[ot]);
+  }
+}
+
+// =============================================================================================
+// forward
+// =============================================================================================
+template <bool LN>
+__global__ __launch_bounds__(kThreads, 2) void edge_cam_fwd_kernel(
+    const float* __restrict__ P, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
+    const float* __restrict__ Wpt, const float* __restrict__ bpt, const float* __restrict__ Wc,
+    const float* __restrict__ bc, float* __restrict__ XLp, int64_t ldXLp, const int32_t* __restrict__ pos,
+    const float* __restrict__ XR, int64_t ldXR, const float* __restrict__ att, const float* __restrict__ bias,
+    float slope, const gasfm_work_item* __restrict__ items, int n_items, int finalize, float* __restrict__ out,
+    int64_t ldOut, float* __restrict__ seg_max, float* __restrict__ seg_sum, int64_t ldStat,
+    float* __restrict__ part) {
+  __shared__ float Wl[NX * LDA];                  // Wl[n][k] = [Wpt; Wc][n][k]
+  __shared__ float tiles[kWaves][TR * LD34];
+  {
+    Stage<NX * F, kThreads> sw;
+    sw.load([&](int q) { return q < F * F ? Wpt[q] : Wc[q - F * F]; });
+    sw.store([&](int q, float v) { Wl[(q / F) * LDA + q % F] = v; });
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
+  const int c = lane & 15, g = lane >> 4;
+  float* T = tiles[wave];
+  float4 g4 = make_float4(1.f, 1.f, 1.f, 1.f), b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (LN) {
+    g4 = *reinterpret_cast<const float4*>(gam + (lane & 7) * 4);
+    b4 = *reinterpret_cast<const float4*>(bet + (lane & 7) * 4);
+  }
+  // this lane's features: point 16 ot + 4 g + r (ot = 0, 1); camera 16 q + 4 g + r (q = 0, 1),
+  // head 2 q + (g >> 1)
+  float bp[2][4], bcv[2][4], attv[2][4], biasv[2][4];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 16 * q + 4 * g + r;
+      bp[q][r] = bpt[f];
+      bcv[q][r] = bc[f];
+      attv[q][r] = att[f];
+      biasv[q][r] = finalize ? bias[f] : 0.f;
+    }
+  const int gw = blockIdx.x * kWaves + wave, nw = gridDim.x * kWaves;
+
+  float4 np[2];
+  int32_t npos = 0;  // point-order row of this lane's edge (column c)
+  auto issue = [&](int64_t row0, int nrows) {
+    load_rows(P, F, row0, nrows, np, lane);
+    if (pos) npos = pos[row0 + (c < nrows ? c : 0)];
+  };
+  auto rows_at = [](const gasfm_work_item& w, int64_t row0) { return int(w.end - row0 < TR ? w.end - row0 : TR); };
+
+  gasfm_work_item w{0, 0, 0, -1};
+  if (gw < n_items) {
+    w = items[gw];
+    if (w.begin < w.end) issue(w.begin, rows_at(w, w.begin));
+  }
+  for (int it = gw; it < n_items; it += nw) {
+    const int64_t seg = w.seg;
+    float xr[2][4];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(XR + seg * ldXR + 16 * q + 4 * g);
+      xr[q][0] = v.x, xr[q][1] = v.y, xr[q][2] = v.z, xr[q][3] = v.w;
+    }
+    float m[2] = {-INFINITY, -INFINITY}, s[2] = {0.f, 0.f};
+    float a[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    gasfm_work_item wn{0, 0, 0, -1};
+    const bool more = it + nw < n_items;
+    if (more) wn = items[it + nw];
+    if (w.begin >= w.end && more && wn.begin < wn.end) issue(wn.begin, rows_at(wn, wn.begin));
+    for (int64_t row0 = w.begin; row0 < w.end; row0 += TR) {
+      const int nrows = rows_at(w, row0);
+      phat_to_lds<LN>(np, nrows, g4, b4, eps, T, lane);
+      const int64_t dst = pos ? int64_t(npos) : row0 + c;
+      if (row0 + TR < w.end)
+        issue(row0 + TR, rows_at(w, row0 + TR));
+      else if (more && wn.begin < wn.end)
+        issue(wn.begin, rows_at(wn, wn.begin));
+      wave_sync();
+      f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+      xl_t<4>(Wl, T, acc, c, g);
+      const bool valid = c < nrows;
+      // point half: this lane's 2 x 4 features of edge c (non-temporal: streamed once by the point
+      // attention)
+      if (valid) {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int ot = 0; ot < 2; ++ot)
+          __builtin_nontemporal_store(v4f{acc[ot][0] + bp[ot][0], acc[ot][1] + bp[ot][1], acc[ot][2] + bp[ot][2],
+                                          acc[ot][3] + bp[ot][3]},
+                                      reinterpret_cast<v4f*>(XLp + dst * ldXLp + 16 * ot + 4 * g));
+      }
+      // camera half: logits of edge c, online softmax per head
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        float xl[4], p = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          xl[r] = acc[2 + q][r] + bcv[q][r];
+          p = fmaf(leaky(xl[r] + xr[q][r], slope), attv[q][r], p);
+        }
+        p += __shfl_xor(p, 16);  // the head's other 4 features
+        if (valid) {
+          const float mn = fmaxf(m[q], p);
+          const float sc = __expf(m[q] - mn), wt = __expf(p - mn);
+          s[q] = fmaf(s[q], sc, wt);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) a[q][r] = fmaf(a[q][r], sc, wt * xl[r]);
+          m[q] = mn;
+        }
+      }
+      wave_sync();  // T is rewritten by the next tile
+    }
+    // merge the 16 edge columns' states
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float M = row_max16(m[q]);
+      const float f = (m[q] > -INFINITY) ? __expf(m[q] - M) : 0.f;
+      const float S = group_sum<16>(s[q] * f);
+      float A[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) A[r] = group_sum<16>(a[q][r] * f);
+      if (c == 0) {
+        const int f0 = 16 * q + 4 * g, h = 2 * q + (g >> 1);
+        if (w.slot < 0) {
+          const float inv = 1.f / (S + 1e-16f);
+          float4 o;
+          if (finalize)
+            o = make_float4(fmaf(A[0], inv, biasv[q][0]), fmaf(A[1], inv, biasv[q][1]), fmaf(A[2], inv, biasv[q][2]),
+                            fmaf(A[3], inv, biasv[q][3]));
+          else
+            o = make_float4(A[0], A[1], A[2], A[3]);
+          *reinterpret_cast<float4*>(out + seg * ldOut + f0) = o;
+          if ((g & 1) == 0) {
+            seg_max[seg * ldStat + h] = M;
+            seg_sum[seg * ldStat + h] = S;
+          }
+        } else {
+          float* pr = part + int64_t(w.slot) * PART;
+          *reinterpret_cast<float4*>(pr + f0) = make_float4(A[0], A[1], A[2], A[3]);
+          if ((g & 1) == 0) {
+            pr[F + h] = M;
+            pr[F + H + h] = S;
+          }
+        }
+      }
+    }
+    w = wn;
+  }
+}
+
+// =============================================================================================
+// backward of the camera attention, XLc recomputed from P
+// =============================================================================================
+// per workgroup partial row: [32 datt | 32 dbias]
+constexpr int BP_PART = 2 * F;
+
+template <bool LN>
+__global__ __launch_bounds__(kThreads, 2) void edge_cam_bwd_kernel(
+    const float* __restrict__ P, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
+    const float* __restrict__ Wc, const float* __restrict__ bc, const float* __restrict__ XR, int64_t ldXR,
+    const float* __restrict__ att, const float* __restrict__ bias, float slope, const float* __restrict__ out,
+    int64_t ldOut, const float* __restrict__ seg_max, const float* __restrict__ seg_sum, int64_t ldStat,
+    const float* __restrict__ gout, int64_t ldG, const gasfm_work_item* __restrict__ items, int n_items,
+    float* __restrict__ dXLc, int64_t ldD, float* __restrict__ dXR, int64_t ldDXR, float* __restrict__ part_dxr,
+    float* __restrict__ part) {
+  __shared__ float Wl[F * LDA];  // Wl[n][k] = Wc[n][k]
+  __shared__ float tiles[kWaves][TR * LD34];
+  {
+    Stage<F * F, kThreads> sw;
+    sw.load([&](int q) { return Wc[q]; });
+    sw.store([&](int q, float v) { Wl[(q / F) * LDA + q % F] = v; });
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
+  const int c = lane & 15, g = lane >> 4;
+  float* T = tiles[wave];
+  float4 g4 = make_float4(1.f, 1.f, 1.f, 1.f), b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (LN) {
+    g4 = *reinterpret_cast<const float4*>(gam + (lane & 7) * 4);
+    b4 = *reinterpret_cast<const float4*>(bet + (lane & 7) * 4);
+  }
+  float bcv[2][4], attv[2][4], biasv[2][4], datt[2][4], dbias[2][4];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 16 * q + 4 * g + r;
+      bcv[q][r] = bc[f];
+      attv[q][r] = att[f];
+      biasv[q][r] = bias[f];
+      datt[q][r] = dbias[q][r] = 0.f;
+    }
+  const int gw = blockIdx.x * kWaves + wave, nw = gridDim.x * kWaves;
+
+  float4 np[2];
+  auto issue = [&](int64_t row0, int nrows) { load_rows(P, F, row0, nrows, np, lane); };
+  auto rows_at = [](const gasfm_work_item& w, int64_t row0) { return int(w.end - row0 < TR ? w.end - row0 : TR); };
+  gasfm_work_item w{0, 0, 0, -1};
+  if (gw < n_items) {
+    w = items[gw];
+    if (w.begin < w.end) issue(w.begin, rows_at(w, w.begin));
+  }
+  for (int it = gw; it < n_items; it += nw) {
+    const int64_t seg = w.seg;
+    // per-camera constants: XR, gout, out - bias at this lane's features; per head the forward's
+    // max, 1 / (sum + 1e-16) and delta = sum_j alpha_j (g . XL_j) = g . (out - bias)
+    float xr[2][4], gv[2][4], M[2], inv[2], delta[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int f0 = 16 * q + 4 * g, h = 2 * q + (g >> 1);
+      const float4 x4 = *reinterpret_cast<const float4*>(XR + seg * ldXR + f0);
+      const float4 g4v = *reinterpret_cast<const float4*>(gout + seg * ldG + f0);
+      const float4 o4 = *reinterpret_cast<const float4*>(out + seg * ldOut + f0);
+      xr[q][0] = x4.x, xr[q][1] = x4.y, xr[q][2] = x4.z, xr[q][3] = x4.w;
+      gv[q][0] = g4v.x, gv[q][1] = g4v.y, gv[q][2] = g4v.z, gv[q][3] = g4v.w;
+      const float o[4] = {o4.x, o4.y, o4.z, o4.w};
+      float d = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) d = fmaf(gv[q][r], o[r] - biasv[q][r], d);
+      delta[q] = d + __shfl_xor(d, 16);
+      M[q] = seg_max[seg * ldStat + h];
+      inv[q] = 1.f / (seg_sum[seg * ldStat + h] + 1e-16f);
+    }
+    const bool first = it == 0 || items[it - 1].seg != w.seg;
+    if (first && c == 0) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dbias[q][r] += gv[q][r];
+    }
+    float dxr[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    gasfm_work_item wn{0, 0, 0, -1};
+    const bool more = it + nw < n_items;
+    if (more) wn = items[it + nw];
+    if (w.begin >= w.end && more && wn.begin < wn.end) issue(wn.begin, rows_at(wn, wn.begin));
+    for (int64_t row0 = w.begin; row0 < w.end; row0 += TR) {
+      const int nrows = rows_at(w, row0);
+      phat_to_lds<LN>(np, nrows, g4, b4, eps, T, lane);
+      if (row0 + TR < w.end)
+        issue(row0 + TR, rows_at(w, row0 + TR));
+      else if (more && wn.begin < wn.end)
+        issue(wn.begin, rows_at(wn, wn.begin));
+      wave_sync();
+      f32x4 xc[2] = {zero4(), zero4()};
+      xl_t<2>(Wl, T, xc, c, g);
+      const bool valid = c < nrows;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        float xl[4], z[4], lz[4], p = 0.f, da = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          xl[r] = xc[q][r] + bcv[q][r];
+          z[r] = xl[r] + xr[q][r];
+          lz[r] = leaky(z[r], slope);
+          p = fmaf(lz[r], attv[q][r], p);
+          da = fmaf(gv[q][r], xl[r], da);
+        }
+        p += __shfl_xor(p, 16);
+        da += __shfl_xor(da, 16);
+        const float alpha = valid ? __expf(p - M[q]) * inv[q] : 0.f;
+        const float de = alpha * (da - delta[q]);
+        float dx[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float dz = de * attv[q][r] * (z[r] > 0.f ? 1.f : slope);
+          dx[r] = fmaf(alpha, gv[q][r], dz);
+          dxr[q][r] += dz;
+          datt[q][r] = fmaf(de, lz[r], datt[q][r]);
+        }
+        if (valid)
+          *reinterpret_cast<float4*>(dXLc + (row0 + c) * ldD + 16 * q + 4 * g) = make_float4(dx[0], dx[1], dx[2], dx[3]);
+      }
+      wave_sync();  // T is rewritten by the next tile
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = group_sum<16>(dxr[q][r]);
+      if (c == 0) {
+        float* d = (w.slot < 0) ? dXR + seg * ldDXR : part_dxr + int64_t(w.slot) * F;
+        *reinterpret_cast<float4*>(d + 16 * q + 4 * g) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+    w = wn;
+  }
+  // d att / d bias: sum over the 16 edge columns, then over the workgroup's waves (ordered)
+  float v[16];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[q * 4 + r] = group_sum<16>(datt[q][r]);
+      v[8 + q * 4 + r] = group_sum<16>(dbias[q][r]);
+    }
+  wg_reduce_ordered<16, kWaves, kWaves * TR * LD34>(v, &tiles[0][0], wave, lane);
+  if (wave == 0 && c == 0) {
+    float* o = part + int64_t(blockIdx.x) * BP_PART;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      *reinterpret_cast<float4*>(o + 16 * q + 4 * g) = make_float4(v[q * 4], v[q * 4 + 1], v[q * 4 + 2], v[q * 4 + 3]);
+      *reinterpret_cast<float4*>(o + F + 16 * q + 4 * g) =
+          make_float4(v[8 + q * 4], v[8 + q * 4 + 1], v[8 + q * 4 + 2], v[8 + q * 4 + 3]);
+    }
+  }
+}
+
+int grid_cam_bwd(int n_items) {
+  return resident_grid(reinterpret_cast<const void*>(&edge_cam_bwd_kernel<true>), kThreads, 0, n_items, kWaves);
+}
+
+}  // namespace
+}  // namespace gasfm
+
+using namespace gasfm;
+
+extern "C" int32_t gasfm_edge_cam_bwd_part_rows(int32_t n_items) { return grid_cam_bwd(n_items > 0 ? n_items : 1); }
+extern "C" int32_t gasfm_edge_cam_bwd_part_cols(void) { return BP_PART; }
+
+extern "C" int gasfm_edge_cam_fwd(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
+                                  const float* bpt, const float* Wc, const float* bc, float* XLp, int64_t ldXLp,
+                                  const int32_t* pos, const float* XR, int64_t ldXR, const float* att,
+                                  const float* bias, float slope, const gasfm_work_item* items, int32_t n_items,
+                                  int32_t finalize, float* out, int64_t ldOut, float* seg_max, float* seg_sum,
+                                  int64_t ldStat, float* part, void* stream) {
+  GASFM_REQUIRE(n_items >= 0 && P && Wpt && bpt && Wc && bc && XLp && XR && att && items,
+                "gasfm_edge_cam_fwd: null pointer");
+  GASFM_REQUIRE((out && seg_max && seg_sum && (bias || !finalize)) || part, "gasfm_edge_cam_fwd: no outputs");
+  GASFM_REQUIRE(ldXLp >= F && ldXLp % 4 == 0 && ldXR >= F && ldXR % 4 == 0 && (!out || (ldOut >= F && ldOut % 4 == 0)) &&
+                    aligned16(P) && aligned16(XLp) && aligned16(XR) && (!out || aligned16(out)) &&
+                    (!part || aligned16(part)) && (!ln_w || (aligned16(ln_w) && aligned16(ln_b))),
+                "gasfm_edge_cam_fwd: 16-byte rows required");
+  if (n_items == 0) return GASFM_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  auto launch = [&](auto kern) {
+    const int grid = resident_grid(reinterpret_cast<const void*>(kern), kThreads, 0, n_items, kWaves);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, st, P, ln_w, ln_b, eps, Wpt, bpt, Wc, bc, XLp, ldXLp,
+                       pos, XR, ldXR, att, bias, slope, items, n_items, finalize, out, ldOut, seg_max, seg_sum,
+                       ldStat, part);
+  };
+  if (ln_w)
+    launch(&edge_cam_fwd_kernel<true>);
+  else
+    launch(&edge_cam_fwd_kernel<false>);
+  return launch_status("gasfm_edge_cam_fwd");
+}
+
+extern "C" int gasfm_edge_cam_bwd(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wc,
+                                  const float* bc, const float* XR, int64_t ldXR, const float* att, const float* bias,
+                                  float slope, const float* out, int64_t ldOut, const float* seg_max,
+                                  const float* seg_sum, int64_t ldStat, const float* gout, int64_t ldG,
+                                  const gasfm_work_item* items, int32_t n_items, float* dXLc, int64_t ldD, float* dXR,
+                                  int64_t ldDXR, float* part_dxr, float* part, void* stream) {
+  GASFM_REQUIRE(n_items >= 0 && P && Wc && bc && XR && att && bias && out && seg_max && seg_sum && gout && items &&
+                    dXLc && dXR && part,
+                "gasfm_edge_cam_bwd: null pointer");
+  GASFM_REQUIRE(ldXR % 4 == 0 && ldOut % 4 == 0 && ldG % 4 == 0 && ldD % 4 == 0 && ldDXR % 4 == 0 && aligned16(P) &&
+                    aligned16(XR) && aligned16(out) && aligned16(gout) && aligned16(dXLc) && aligned16(dXR) &&
+                    (!part_dxr || aligned16(part_dxr)) && (!ln_w || (aligned16(ln_w) && aligned16(ln_b))),
+                "gasfm_edge_cam_bwd: 16-byte rows required");
+  if (n_items == 0) return GASFM_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int grid = grid_cam_bwd(n_items);
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, st, P, ln_w, ln_b, eps, Wc, bc, XR, ldXR, att, bias, slope,
+                       out, ldOut, seg_max, seg_sum, ldStat, gout, ldG, items, n_items, dXLc, ldD, dXR, ldDXR,
+                       part_dxr, part);
+  };
+  if (ln_w)
+    launch(&edge_cam_bwd_kernel<true>);
+  else
+    launch(&edge_cam_bwd_kernel<false>);
+  return launch_status("gasfm_edge_cam_bwd");
+}

@@ -19,7 +19,8 @@ torch and runs on MFMA through hipBLASLt.
 import torch
 
 from . import _native
-from .attention import attn_backward_raw, attn_forward_partial, attn_forward_raw, bwd_combine, combine_partials
+from .attention import (attn_backward_raw, attn_forward_partial, attn_forward_raw, bwd_combine, combine_fwd_l1,
+                        combine_partials)
 
 PROJ_SCALE = 0.25  # the "/ 4" of layers.py:945
 
@@ -73,6 +74,104 @@ class EdgePrologueFn(torch.autograd.Function):
         if ctx.split:
             return dP, dgam, dbet, dW[:32], db[:32], None, None, None, dW[32:], db[32:]
         return dP, dgam, dbet, dW, db, None, None, None, None, None
+
+
+class EdgeCamFn(torch.autograd.Function):
+    """EdgePrologueFn + the camera half of DualAttentionFn in one pass (csrc/edge_cam.hip):
+
+        P -> (XLp [E, 32] = Wpt relu(LN(P)) + bpt  (point order when pos is given),
+              camera aggregates out_c [m, 32],
+              token)
+
+    XLc = Wc relu(LN(P)) + bc, the camera conv's lin_l rows, lives only in registers: the
+    backward recomputes it from P.  token: as EdgePrologueFn's (its gradient is the block
+    output's gradient dP', which the backward folds into dP with Wp).  plan_cam_partial / shard:
+    point-sharded execution (camera segments span ranks: local partial rows, all-gather, ordered
+    combine), as DualAttentionFn."""
+
+    @staticmethod
+    def forward(ctx, P, ln_w, ln_b, Wpt, bpt, Wc, bc, Wp, eps, pos, XR, att, bias, plan, heads, slope,
+                plan_partial=None, shard=None):
+        E, dev = P.shape[0], P.device
+        HC = att.numel()
+        if heads != 4 or HC != 32:
+            raise ValueError("EdgeCamFn: the fused kernels are for H = 4, C = 8")
+        attf = att.reshape(-1).contiguous()
+        XLp = torch.empty((E, 32), dtype=torch.float32, device=dev)
+        N = plan.num_targets
+        LDP = HC + 2 * heads
+        if shard is None:
+            out = torch.empty((N, HC), dtype=torch.float32, device=dev)
+            smax = torch.empty((N, heads), dtype=torch.float32, device=dev)
+            ssum = torch.empty((N, heads), dtype=torch.float32, device=dev)
+            part = torch.empty((plan.n_part_rows, LDP), dtype=torch.float32, device=dev) if plan.n_slots else None
+            _native.edge_cam_fwd(P, ln_w, ln_b, eps, Wpt, bpt, Wc, bc, XLp, pos, XR, attf, bias, slope, plan.items,
+                                 plan.n_items, True, out, smax, ssum, part)
+            combine_fwd_l1(plan, part, heads, HC // heads)
+            if plan.n_combine:
+                _native.attn_combine(plan.combine, plan.n_combine, heads, HC // heads, part, bias, True, out, smax,
+                                     ssum)
+        else:  # local partial rows (attention.attn_forward_partial) -> all-gather -> ordered combine
+            pp = plan_partial
+            part = torch.empty((max(pp.n_part_rows, N), LDP), dtype=torch.float32, device=dev)
+            if pp.n_items:
+                _native.edge_cam_fwd(P, ln_w, ln_b, eps, Wpt, bpt, Wc, bc, XLp, pos, XR, attf, None, slope, pp.items,
+                                     pp.n_items, False, None, None, None, part)
+                combine_fwd_l1(pp, part, heads, HC // heads)
+                if pp.n_combine:
+                    _native.attn_combine(pp.combine, pp.n_combine, heads, HC // heads, part, None, False, part,
+                                         part[:, HC:], part[:, HC + heads:], ldOut=LDP, ldStat=LDP)
+            else:
+                part[:N, :HC] = 0.0
+                part[:N, HC:HC + heads] = -float("inf")
+                part[:N, HC + heads:] = 0.0
+            gathered = shard.all_gather(part[:N])
+            out, smax, ssum = combine_partials(gathered, shard.world, N, heads, bias, shard.combine_items(N, dev))
+        ctx.eps, ctx.heads, ctx.slope, ctx.plan = eps, heads, slope, plan
+        ctx.att_shape = att.shape
+        ctx.has_ln = ln_w is not None
+        ctx.defer = _native.defer_token(ln_w, ln_b, Wpt, bpt, Wc, bc, att, bias)
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum)
+        token = P.new_empty((1, 1)).expand(E, P.shape[1])
+        return XLp, out, token
+
+    @staticmethod
+    def backward(ctx, dXLp, g_c, dtoken):
+        P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum = ctx.saved_tensors
+        plan = ctx.plan
+        E, dev = P.shape[0], P.device
+        dXLp = torch.zeros((E, 32), dtype=torch.float32, device=dev) if dXLp is None else dXLp.contiguous()
+        g_c = torch.zeros_like(out) if g_c is None else (g_c if g_c.stride(1) == 1 else g_c.contiguous())
+        dRes = dtoken.contiguous() if (dtoken is not None and dtoken.stride(0) != 0) else None
+        # camera attention backward (XLc recomputed from P): dXLc, dXR, [datt | dbias] partials
+        dXLc = torch.empty((E, 32), dtype=torch.float32, device=dev)
+        dXR = torch.empty((plan.num_targets, 32), dtype=torch.float32, device=dev)
+        part_dxr = torch.empty((plan.n_part_rows, 32), dtype=torch.float32, device=dev) if plan.n_slots else None
+        rows, cols = _native.edge_cam_bwd_part_shape(plan.n_items)
+        part_a = (torch.empty if plan.n_items else torch.zeros)((rows, cols), dtype=torch.float32, device=dev)
+        if plan.n_items:
+            _native.edge_cam_bwd(P, ln_w, ln_b, ctx.eps, Wc.contiguous(), bc.contiguous(), XR, attf, bias, ctx.slope, out,
+                                 smax, ssum, g_c, plan.items, plan.n_items, dXLc, dXR, part_dxr, part_a)
+            bwd_combine(plan, part_dxr, 32, dXR)
+        else:  # no local edges
+            dXLc.zero_()
+            dXR.zero_()
+        # prologue backward on [dXLp | dXLc] (+ the block output's residual gradient)
+        dP = torch.empty_like(P)
+        prow = _native.edge_part_floats(0, E) // (64 * 32 + 64 + 64)
+        part = torch.empty((prow, 64 * 32 + 64 + 64), dtype=torch.float32, device=dev)
+        _native.edge_prologue_bwd(dXLp, P, dRes, ln_w, ln_b, ctx.eps, Wpt.contiguous(),
+                                  Wp.contiguous() if dRes is not None else None, PROJ_SCALE, dP, part, Wc.contiguous(),
+                                  dXLc=dXLc)
+        ta = _native.param_colsum(part_a, ctx.defer)
+        tot = _native.param_colsum(part, ctx.defer)
+        o = 64 * 32
+        dW, db = tot[:o].view(64, 32), tot[o:o + 64]
+        dgam = tot[o + 64:o + 96] if ctx.has_ln else None
+        dbet = tot[o + 96:o + 128] if ctx.has_ln else None
+        return (dP, dgam, dbet, dW[:32], db[:32], dW[32:], db[32:], None, None, None, dXR,
+                ta[:32].view(ctx.att_shape), ta[32:], None, None, None, None, None)
 
 
 class DualAttentionFn(torch.autograd.Function):

@@ -20,15 +20,22 @@ Dense per-node projections (view 1024 / global 2048 widths) run on MFMA through
 torch (hipBLASLt).
 """
 import copy
+import os
 
 import torch
 import torch.nn.functional as F
 from torch.nn import Identity, LayerNorm, Linear, Module, ModuleList, ReLU, Sequential
 
 from . import _native, dense, edge_ops, point_block, streams, view_block
-from .attention import AttnPlan, gat_attention
-from .edge_block import Block0EpilogueFn, Block0PrologueFn, DualAttentionFn, EdgeEpilogueFn, EdgePrologueFn
+from .attention import AttnPlan, GatAttentionFn, gat_attention
+from .edge_block import (Block0EpilogueFn, Block0PrologueFn, DualAttentionFn, EdgeCamFn, EdgeEpilogueFn,
+                         EdgePrologueFn)
 from .gatv2 import GATv2Conv
+
+
+# Edge prologue with the camera attention fused in (edge_block.EdgeCamFn, csrc/edge_cam.hip) for the
+# 32-wide blocks; GASFM_EDGE_CAM=0 selects the separate prologue + DualAttentionFn kernels (A/B).
+EDGE_CAM = os.environ.get("GASFM_EDGE_CAM", "1") != "0"
 
 
 def replicated_to_local(x, shard):
@@ -386,9 +393,10 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         return torch.cat([a.weight, b.weight], 0), torch.cat([a.bias, b.bias], 0)
 
     def forward_fused(self, XL, plans, prev_pt=None, prev_view=None, prev_glob=None, xl_sorted=False, carry=None,
-                      pfu=None, nxt=None):
+                      pfu=None, nxt=None, attend=None):
         """Node side of the update given XL = [lin_l_point(P_hat) | lin_l_camera(P_hat)] [E, 64]
-        (point half in point-segment order when xl_sorted).
+        (point half in point-segment order when xl_sorted), or attend(XRp, XRc, sec) -> (point
+        aggregates, camera aggregates) (the fused prologue + camera attention, edge_cam_attend).
 
         carry: per-forward dict through which PointHubFn / ViewHubFn hand the next block its
         target rows ("XRp", "XRc") and state skips ("pts_skip", "view_skip"), and this block its
@@ -419,11 +427,14 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         hp = point_block.hub_params(pfu, vsg.graph_conv_scenepoint2global, nxt.proj2scenepoint) if hubs else None
         # point tail + hub on a side stream, concurrent with the camera tail + hub (streams.py)
         sec = None
-        if hp is not None and point_block.tail_fusable(sp, XL.new_empty((0, cp.heads * cp.out_channels)), prev_pt):
-            sec = streams.section_for(XL.device, _native.defer_token())
-        agg_p, agg_c = DualAttentionFn.apply(XL, XRp, XRc, cp.att, cc.att, cp.bias, cc.bias, pp, pc, cp.heads,
-                                             cp.negative_slope, plans.get("_partial", {}).get("proj2view"), shard,
-                                             xl_sorted, sec)
+        if hp is not None and point_block.tail_fusable(sp, XRp.new_empty((0, cp.heads * cp.out_channels)), prev_pt):
+            sec = streams.section_for(XRp.device, _native.defer_token())
+        if attend is not None:
+            agg_p, agg_c = attend(XRp, XRc, sec)
+        else:
+            agg_p, agg_c = DualAttentionFn.apply(XL, XRp, XRc, cp.att, cc.att, cp.bias, cc.bias, pp, pc, cp.heads,
+                                                 cp.negative_slope, plans.get("_partial", {}).get("proj2view"), shard,
+                                                 xl_sorted, sec)
         if sec is not None:
             point_block.forward_buffers(sec, agg_p.shape[0], agg_p)
             sec.fork()
@@ -450,6 +461,32 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         if sec is not None:
             sec.join()
         return self._finish(pts, view, plans, prev_glob, carry, pfu, nxt)
+
+    def cam_fusable(self, plans):
+        """The fused prologue + camera attention (EdgeCamFn) applies: both convs H = 4, C = 8, and
+        the camera plan over the camera-major edges themselves (no permutation)."""
+        cp, cc = self.proj2scenepoint.graph_conv, self.proj2view.graph_conv
+        return (EDGE_CAM and cc.heads == 4 and cc.out_channels == 8 and cp.heads == 4 and cp.out_channels == 8
+                and plans["proj2view"].perm is None)
+
+    def edge_cam_attend(self, P, ln_w, ln_b, eps, Wp, plans, holder):
+        """attend callback of forward_fused: EdgeCamFn on P (lin_l of both convs, the camera
+        attention; XLp written in point order) then the point attention on XLp.  The prologue's
+        token (see EdgePrologueFn) is left in holder["token"]."""
+        (W, b), (W2, b2) = self.lin_l_pair()
+        pp, pc = plans["proj2scenepoint"], plans["proj2view"]
+        cp, cc = self.proj2scenepoint.graph_conv, self.proj2view.graph_conv
+        pos = pp.pos
+
+        def attend(XRp, XRc, sec):
+            XLp, agg_c, token = EdgeCamFn.apply(P, ln_w, ln_b, W, b, W2, b2, Wp, eps, pos, XRc, cc.att, cc.bias, pc,
+                                                cc.heads, cc.negative_slope,
+                                                plans.get("_partial", {}).get("proj2view"), plans.get("_shard"))
+            holder["token"] = token
+            agg_p = GatAttentionFn.apply(XLp, XRp, cp.att, cp.bias, pp, cp.heads, cp.negative_slope, pos is not None,
+                                         sec)[0]
+            return agg_p, agg_c
+        return attend
 
     def forward_plan(self, P_hat, plans, prev_pt=None, prev_view=None, prev_glob=None):
         shard = plans.get("_shard")
@@ -592,11 +629,18 @@ class GraphAttnSfMLayer(Module):
         ln = self.prev_projfeat_norm_layer
         gfu = self.global_feature_update
         pfu = self.projection_feature_update
-        (W, b), (W2, b2) = gfu.lin_l_pair()
         pos = plans["proj2scenepoint"].pos
-        XL, token = EdgePrologueFn.apply(P, ln.weight, ln.bias, W, b, pfu.lin_proj.weight, ln.eps, pos, W2, b2)
-        pts, view, glob = gfu.forward_fused(XL, plans, prev_pt, prev_view, prev_glob, xl_sorted=pos is not None,
-                                            carry=carry, pfu=pfu, nxt=nxt)
+        if gfu.cam_fusable(plans):
+            holder = {}
+            attend = gfu.edge_cam_attend(P, ln.weight, ln.bias, ln.eps, pfu.lin_proj.weight, plans, holder)
+            pts, view, glob = gfu.forward_fused(None, plans, prev_pt, prev_view, prev_glob, carry=carry, pfu=pfu,
+                                                nxt=nxt, attend=attend)
+            token = holder["token"]
+        else:
+            (W, b), (W2, b2) = gfu.lin_l_pair()
+            XL, token = EdgePrologueFn.apply(P, ln.weight, ln.bias, W, b, pfu.lin_proj.weight, ln.eps, pos, W2, b2)
+            pts, view, glob = gfu.forward_fused(XL, plans, prev_pt, prev_view, prev_glob, xl_sorted=pos is not None,
+                                                carry=carry, pfu=pfu, nxt=nxt)
         sp, sv, sg = pfu.node_terms(pts, view, glob, *((carry.pop("SA", None), carry.pop("SV", None),
                                                           carry.pop("SG", None))
                                                          if carry is not None else (None, None, None)))
@@ -888,10 +932,14 @@ class GraphAttnSfMNet(Module):
             args = (pts if sf else None, view if sf else None, glob if sf else None)
             if P.is_cuda and P.shape[1] == 32 and fgu.fusable():
                 # raw (un-normalised) projection features (graph_attn_sfm.py:141-148): no LN prologue
-                (W, b), (W2, b2) = fgu.lin_l_pair()
                 pos = plans["proj2scenepoint"].pos
-                XL, _ = EdgePrologueFn.apply(P.contiguous(), None, None, W, b, None, 1e-5, pos, W2, b2)
-                pts, view, _ = fgu.forward_fused(XL, plans, *args, xl_sorted=pos is not None, carry=carry)
+                if fgu.cam_fusable(plans):
+                    attend = fgu.edge_cam_attend(P.contiguous(), None, None, 1e-5, None, plans, {})
+                    pts, view, _ = fgu.forward_fused(None, plans, *args, carry=carry, attend=attend)
+                else:
+                    (W, b), (W2, b2) = fgu.lin_l_pair()
+                    XL, _ = EdgePrologueFn.apply(P.contiguous(), None, None, W, b, None, 1e-5, pos, W2, b2)
+                    pts, view, _ = fgu.forward_fused(XL, plans, *args, xl_sorted=pos is not None, carry=carry)
             else:
                 pts, view, _ = fgu.forward_plan(P, plans, *args)
         return P, pts, view

@@ -118,6 +118,35 @@ int gasfm_plan_work(const int32_t* seg_ptr, int32_t N, int32_t max_piece,
                     gasfm_combine_item* combine, int32_t* n_combine,
                     int32_t* n_slots);
 
+/* ---- edge prologue + camera-direction attention (device, edge_cam.hip) --
+ * One pass over the camera plan's work items (contiguous edges of one camera) replaces
+ * gasfm_edge_prologue_fwd + gasfm_gat_attn_fwd on the camera half of XL (the lin_l of both convs,
+ * layers.py:232-234 + PyG; Proj2View's attention, layers.py:329-335): XLp [E, 32] = Wpt
+ * relu(LN(P)) + bpt is written (row pos[e] when pos != NULL, else row e), XLc = Wc relu(LN(P)) + bc
+ * is consumed in registers, and the camera aggregates are written exactly as gasfm_gat_attn_fwd
+ * writes them for these items (H = 4, C = 8; out / seg_max / seg_sum, or packed partial rows of
+ * 40 floats).  ln_w == NULL: no LayerNorm (the final update's raw features). */
+int gasfm_edge_cam_fwd(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
+                       const float* bpt, const float* Wc, const float* bc, float* XLp, int64_t ldXLp,
+                       const int32_t* pos, const float* XR, int64_t ldXR, const float* att, const float* bias,
+                       float slope, const gasfm_work_item* items, int32_t n_items, int32_t finalize, float* out,
+                       int64_t ldOut, float* seg_max, float* seg_sum, int64_t ldStat, float* part, void* stream);
+/* Backward of the camera attention above (gasfm_gat_attn_bwd on these items) with XLc recomputed
+ * from P instead of read: given the camera aggregates' gradient gout and the forward's out /
+ * seg_max / seg_sum, writes dXLc [E, 32] (row stride ldD; gasfm_edge_prologue_bwd's camera half),
+ * dXR[seg] for complete items (split items: part_dxr[slot], merge with
+ * gasfm_gat_attn_bwd_combine) and one partial row per workgroup
+ * part[gasfm_edge_cam_bwd_part_rows(n_items), gasfm_edge_cam_bwd_part_cols()] = [datt 32 | dbias 32]
+ * (reduce with gasfm_colsum). */
+int32_t gasfm_edge_cam_bwd_part_rows(int32_t n_items);
+int32_t gasfm_edge_cam_bwd_part_cols(void);
+int gasfm_edge_cam_bwd(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wc,
+                       const float* bc, const float* XR, int64_t ldXR, const float* att, const float* bias,
+                       float slope, const float* out, int64_t ldOut, const float* seg_max, const float* seg_sum,
+                       int64_t ldStat, const float* gout, int64_t ldG, const gasfm_work_item* items,
+                       int32_t n_items, float* dXLc, int64_t ldD, float* dXR, int64_t ldDXR, float* part_dxr,
+                       float* part, void* stream);
+
 /* ---- fused GATv2 edge-softmax + aggregation (device) ------------------- */
 
 /* Forward of PyG GATv2Conv's message/softmax/aggregate on pre-projected
@@ -263,11 +292,14 @@ int gasfm_edge_epilogue_bwd(const gasfm_work_item* items, int32_t n_items, const
                             float* part_dsv, float* dP0, float* part_w, void* stream);
 
 /* dP = LN_bwd(relu_mask * (W^T dXL + scale*Wp[:, :32]^T dRes)) + dRes, and the
- * per-workgroup partials of dW, db, dgamma, dbeta (LayerNorm/ReLU/lin_l backward). */
+ * per-workgroup partials of dW, db, dgamma, dbeta (LayerNorm/ReLU/lin_l backward).
+ * dXLc != NULL: dXL holds only the point half ([E, >= 32], row stride ldX) and dXLc the camera
+ * half ([E, >= 32], row stride ldC), as gasfm_edge_cam_bwd writes it. */
 int gasfm_edge_prologue_bwd(const float* dXL, int64_t ldX, const float* P, const float* dRes,
                             int64_t E, const float* ln_w, const float* ln_b, float eps,
                             const float* W, const float* W2, const float* Wp, int32_t ldWp,
-                            float scale, float* dP, float* part, void* stream);
+                            float scale, float* dP, float* part, const float* dXLc, int64_t ldC,
+                            void* stream);
 
 /* out[seg] = scale * sum_{edges of the item} X[src]  (32-wide rows; src via perm).
  * Replaces the index_add scatter of scenepoint_features[pt] (layers.py:940). */
