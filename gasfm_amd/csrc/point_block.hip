@@ -1191,6 +1191,305 @@ __global__ __launch_bounds__(kThreadsT, GASFM_PT_FWD_T_MINW) void point_hub_fwd_
   }
 }
 
+// ----------------------------------------------------------------------------- backward, register-resident
+// The backward needs every row tensor in two register layouts:
+//   T (slab) layout  lane (g, c), f32x4 v[u]:  V[row c][16 u + 4 g + j]      (k = features along g)
+//   C layout         lane (g, c), f32x4 v[ft]: V[row 4 g + r][16 ft + c]     (k = rows along g)
+// A product over FEATURES (Y = X W^T) takes X in T layout; with X as the A operand the result
+// lands in C layout (layer_c), with X as the B operand in T layout (layer_t).  A weight gradient
+// (dW = dY^T X, K = rows) takes BOTH operands in C layout with the row index in the order 4 g + s
+// at step s: no LDS at all.  So the loaded tensors are read in the layouts their consumers want
+// (T: 16-B loads of 64-B row chunks; C: 4-B loads, 64 contiguous bytes per row per instruction --
+// the second layout of a tensor comes from L1 / L2), the computed ones come out of the products
+// in the layout needed, and only dx, consumed by both kinds of product, goes through a per-wave
+// LDS transpose (16 x 64).  LDS holds the weight slabs and that transpose tile (~49 KB per
+// 4-wave workgroup, the old kernels staged every tile: ~150 KB per 8-wave workgroup), and no MFMA
+// operand of a row tile is read from LDS.
+#ifndef GASFM_PT_BWD_R
+#define GASFM_PT_BWD_R 1
+#endif
+// 1 wave per SIMD (~210 VGPRs + 116 AGPRs) with the next tile's rows requested one tile ahead;
+// 2 waves per SIMD spills (256 VGPRs, 52 spilled): 110 vs 86 us at n = 200k without the prefetch
+#ifndef GASFM_PT_BWD_R_MINW
+#define GASFM_PT_BWD_R_MINW 1
+#endif
+constexpr int kWavesR = 4, kThreadsR = kWavesR * kW;
+constexpr int LDX = FP + 4;  // transpose tile row stride: the C-layout writes of the 4 lane groups hit 4 bank quarters
+
+// float4 slabs of W^T for W [O x K] (out index k, K index o): Q[((k/16) (O/16) + o/16) 64 + 16 ((o%16)/4)
+// + k%16][o%4] = W[o][k], i.e. stage_slabs of the transpose (W is read in its own row-major order)
+template <int O, int K, int NT>
+__device__ __forceinline__ void stage_slabs_tr(const float* __restrict__ W, float* Q) {
+  Stage<O * K, NT> s;
+  s.load([&](int q) { return W[q]; });
+  s.store([&](int q, float v) {
+    const int o = q / K, k = q % K;
+    Q[(((k / 16) * (O / 16) + o / 16) * 64 + ((o % 16) / 4) * 16 + k % 16) * 4 + o % 4] = v;
+  });
+}
+
+// acc[ot] += X W^T with X (T-layout k-slabs) as the A operand: acc[ot][r] = Y[row 4 g + r][16 ot + c]
+template <int OT, int KU>
+__device__ __forceinline__ void layer_c(const float4* __restrict__ Q, const f32x4 (&xk)[KU], f32x4 (&acc)[OT],
+                                        int lane) {
+#pragma unroll
+  for (int u = 0; u < KU; ++u) {
+    float4 w[OT];
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) w[ot] = Q[(ot * KU + u) * 64 + lane];
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) acc[ot] = mfma16(xk[u][0], w[ot].x, acc[ot]);
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) acc[ot] = mfma16(xk[u][1], w[ot].y, acc[ot]);
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) acc[ot] = mfma16(xk[u][2], w[ot].z, acc[ot]);
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) acc[ot] = mfma16(xk[u][3], w[ot].w, acc[ot]);
+  }
+}
+
+// C-layout rows: v[ft][r] = X[row0 + 4 g + r][16 ft + c]; rows >= nrows read a valid row (cl_mask zeroes
+// them where the values are consumed: a select right after the load would wait for it, so a load
+// issued a tile ahead must not be masked in place)
+template <int W>
+__device__ __forceinline__ void cl_load(const float* __restrict__ X, int64_t row0, int nrows, f32x4 (&v)[W / 16],
+                                        int lane) {
+  const int c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int rr = 4 * g + r;
+    const float* p = X + (row0 + (rr < nrows ? rr : 0)) * W + c;
+#pragma unroll
+    for (int ft = 0; ft < W / 16; ++ft) v[ft][r] = p[16 * ft];
+  }
+}
+template <int NF>
+__device__ __forceinline__ void cl_mask(f32x4 (&v)[NF], int nrows, int g) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int ft = 0; ft < NF; ++ft) v[ft][r] = 4 * g + r < nrows ? v[ft][r] : 0.f;
+}
+
+// C layout -> T layout of a 16 x 64 tile through the wave's LDS tile X (stride LDX)
+__device__ __forceinline__ void c_to_t64(const f32x4 (&v)[4], float* X, f32x4 (&o)[4], int lane) {
+  const int c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int ft = 0; ft < 4; ++ft)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) X[(4 * g + r) * LDX + 16 * ft + c] = v[ft][r];
+  // one wave's LDS instructions execute in order: a compiler barrier suffices (a wavefront fence
+  // would also wait for the global loads in flight)
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const float4 t = *reinterpret_cast<const float4*>(X + c * LDX + 16 * u + 4 * g);
+    o[u] = f32x4{t.x, t.y, t.z, t.w};
+  }
+}
+
+// LayerNorm statistics of the C-layout rows 4 g + r (64 features: 4 regs x 16 lanes)
+__device__ __forceinline__ void cl_stats(const f32x4 (&x)[4], float eps, float (&mean)[4], float (&rstd)[4]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    mean[r] = sum16((x[0][r] + x[1][r]) + (x[2][r] + x[3][r])) * (1.f / FP);
+    float q = 0.f;
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot) q = fmaf(x[ot][r] - mean[r], x[ot][r] - mean[r], q);
+    rstd[r] = rsqrtf(sum16(q) * (1.f / FP) + eps);
+  }
+}
+
+// LayerNorm + ReLU backward of the C-layout rows (xh: normalised x, dh: gradient of relu(xh g + b));
+// rows >= nrows give 0.  Accumulates dgamma / dbeta per lane feature 16 ot + c.
+__device__ __forceinline__ void cl_ln_relu_bwd(const f32x4 (&xh)[4], const f32x4 (&dh)[4], const float (&gm)[4],
+                                               const float (&bt)[4], const float (&rstd)[4], int nrows, int g,
+                                               float (&dg)[4], float (&db)[4], f32x4 (&dx)[4]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const bool live = 4 * g + r < nrows;
+    float s1 = 0.f, s2 = 0.f, gv[4];
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot) {
+      const float dy = (live && fmaf(xh[ot][r], gm[ot], bt[ot]) > 0.f) ? dh[ot][r] : 0.f;
+      dg[ot] = fmaf(dy, xh[ot][r], dg[ot]);
+      db[ot] += dy;
+      gv[ot] = dy * gm[ot];
+      s1 += gv[ot];
+      s2 = fmaf(gv[ot], xh[ot][r], s2);
+    }
+    s1 = sum16(s1) * (1.f / FP);
+    s2 = sum16(s2) * (1.f / FP);
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot) dx[ot][r] = rstd[r] * (gv[ot] - s1 - xh[ot][r] * s2);
+  }
+}
+
+// dx = dout + LN_bwd(mask * (dout W_m)) (== d prev), dagg = dx W_p; partial row per workgroup in the
+// TAIL_PART layout of point_tail_bwd_kernel.  Per tile: x = agg W_p^T (+ b_p + prev) in C layout
+// (agg T-layout as A), h = relu(LN x); dh = dout W_m in C layout (dout T-layout as A); dx (C);
+// dW_m += dout^T h and dW_p += dx^T agg from C-layout registers; dx -> T layout (LDS), stored;
+// dagg = dx W_p in T layout (dx as B), stored.
+template <bool PREV>
+__global__ __launch_bounds__(kThreadsR, GASFM_PT_BWD_R_MINW) void point_tail_bwd_r_kernel(
+    const float* __restrict__ dout, const float* __restrict__ prev, const float* __restrict__ agg, int64_t N,
+    const float* __restrict__ Wp, const float* __restrict__ bp, const float* __restrict__ gam,
+    const float* __restrict__ bet, float eps, const float* __restrict__ Wm, float* __restrict__ dx,
+    float* __restrict__ dagg, float* __restrict__ part) {
+  constexpr int NRED = 64 + 32 + 16;
+  constexpr int OQ = 0, OQT = FP * FA, OMT = 2 * FP * FA, OX = OMT + FP * FP, NLDS = OX + kWavesR * TR * LDX;
+  __shared__ __attribute__((aligned(16))) float lds[NLDS];
+  float4* WpQ = reinterpret_cast<float4*>(lds + OQ);    // slabs of W_p   (out o, k j)
+  float4* WpTQ = reinterpret_cast<float4*>(lds + OQT);  // slabs of W_p^T (out j, k o)
+  float4* WmTQ = reinterpret_cast<float4*>(lds + OMT);  // slabs of W_m^T (out i, k o)
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
+  const int c = lane & 15, g = lane >> 4;
+  stage_slabs<FP, FA, kThreadsR>(Wp, lds + OQ);
+  stage_slabs_tr<FP, FA, kThreadsR>(Wp, lds + OQT);
+  stage_slabs_tr<FP, FP, kThreadsR>(Wm, lds + OMT);
+  float bpC[4], gmC[4], btC[4];
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot) {
+    bpC[ot] = bp[16 * ot + c];
+    gmC[ot] = gam[16 * ot + c];
+    btC[ot] = bet[16 * ot + c];
+  }
+  __syncthreads();
+  float* X = lds + OX + wave * TR * LDX;
+  f32x4 dWm[4][4], dWp[4][2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) dWm[mt][nt] = zero4();
+    dWp[mt][0] = dWp[mt][1] = zero4();
+  }
+  float dbm[4] = {0.f, 0.f, 0.f, 0.f}, dbp[4] = {0.f, 0.f, 0.f, 0.f};
+  float dg[4] = {0.f, 0.f, 0.f, 0.f}, dbt[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t ntiles = (N + TR - 1) / TR;
+  const int64_t gw = int64_t(blockIdx.x) * kWavesR + wave, nw = int64_t(gridDim.x) * kWavesR;
+  // every row of tile t + nw is requested before tile t's work (one tile of loads in flight)
+  f32x4 n_agT[2], n_dT[4], n_pC[4], n_dC[4], n_agC[2];
+  auto fetch = [&](int64_t tt) {
+    const int64_t r0 = tt * TR;
+    const int nr = int(N - r0 < TR ? N - r0 : TR);
+    slabs_load<FA>(agg, r0, nr, n_agT, lane);
+    if (PREV) cl_load<FP>(prev, r0, nr, n_pC, lane);
+    slabs_load<FP>(dout, r0, nr, n_dT, lane);
+    cl_load<FP>(dout, r0, nr, n_dC, lane);
+    cl_load<FA>(agg, r0, nr, n_agC, lane);
+  };
+  if (gw < ntiles) fetch(gw);
+  for (int64_t t = gw; t < ntiles; t += nw) {
+    const int64_t row0 = t * TR;
+    const int nrows = int(N - row0 < TR ? N - row0 : TR);
+    asm volatile("" ::: "memory");  // weight slabs re-read from LDS per tile (not hoisted into VGPRs)
+    f32x4 agT[2] = {n_agT[0], n_agT[1]}, dT[4], x[4], dC[4], agC[2] = {n_agC[0], n_agC[1]};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      dT[u] = n_dT[u];
+      dC[u] = n_dC[u];
+      x[u] = PREV ? n_pC[u] : zero4();
+    }
+    // unconditional (the last tile re-reads itself): a load under a branch makes the loop header
+    // wait for every outstanding load
+    fetch(t + nw < ntiles ? t + nw : t);
+    cl_mask(dC, nrows, g);
+    cl_mask(agC, nrows, g);
+    if (PREV) cl_mask(x, nrows, g);
+    // phase 1: x (C layout) and its LayerNorm
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot) x[ot] += bpC[ot];
+    layer_c<4, 2>(WpQ, agT, x, lane);
+    float mean[4], rstd[4];
+    cl_stats(x, eps, mean, rstd);
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) x[ot][r] = (x[ot][r] - mean[r]) * rstd[r];  // x_hat from here on
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 2: dh = dout W_m (C layout)
+    f32x4 dh[4] = {zero4(), zero4(), zero4(), zero4()};
+    layer_c<4, 4>(WmTQ, dT, dh, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 3: LayerNorm backward -> dx (C layout), bias sums
+    f32x4 dxc[4];
+    cl_ln_relu_bwd(x, dh, gmC, btC, rstd, nrows, g, dg, dbt, dxc);
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot) {
+      dxc[ot] += dC[ot];  // rows >= nrows: 0 + 0
+      dbm[ot] += (dC[ot][0] + dC[ot][1]) + (dC[ot][2] + dC[ot][3]);
+      dbp[ot] += (dxc[ot][0] + dxc[ot][1]) + (dxc[ot][2] + dxc[ot][3]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 4: weight gradients over the tile's rows (step s: row 4 g + s; rows past nrows: dout,
+    // dx are 0); h = relu(x_hat g + b) recomputed here (not live through phases 2-3)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float hs[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) hs[nt] = fmaxf(fmaf(x[nt][s], gmC[nt], btC[nt]), 0.f);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) dWm[mt][nt] = mfma16(dC[mt][s], hs[nt], dWm[mt][nt]);
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) dWp[mt][nt] = mfma16(dxc[mt][s], agC[nt][s], dWp[mt][nt]);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 dxT[4];
+    c_to_t64(dxc, X, dxT, lane);
+    slabs_store<FP>(dx, row0, nrows, dxT, lane);
+    f32x4 da[2] = {zero4(), zero4()};
+    layer_t<2, 4>(WpTQ, dxT, da, lane);
+    slabs_store<FA>(dagg, row0, nrows, da, lane);
+    __builtin_amdgcn_wave_barrier();  // this tile's transpose reads before the next tile's writes
+    asm volatile("" ::: "memory");
+  }
+  float v[NRED];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) v[(mt * 4 + nt) * 4 + r] = dWm[mt][nt][r];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) v[64 + (mt * 2 + nt) * 4 + r] = dWp[mt][nt][r];
+    }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[96 + k] = dbm[k];
+    v[100 + k] = dbp[k];
+    v[104 + k] = dg[k];
+    v[108 + k] = dbt[k];
+  }
+  wg_reduce_ordered<NRED, kWavesR, NLDS>(v, lds, wave, lane);
+  if (wave == 0) {
+    float* out = part + int64_t(blockIdx.x) * TAIL_PART;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = mt * 16 + 4 * g + r;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) out[o * FP + nt * 16 + c] = v[(mt * 4 + nt) * 4 + r];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) out[FP * FP + o * FA + nt * 16 + c] = v[64 + (mt * 2 + nt) * 4 + r];
+      }
+    float tt[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) tt[k] = sum_groups(v[96 + k]);
+    if (g == 0) {
+      float* o = out + FP * FP + FP * FA;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[q * FP + k * 16 + c] = tt[q * 4 + k];
+    }
+  }
+}
+
 int64_t tiles_of(int64_t N) { return (N + TR - 1) / TR; }
 
 template <class K>
@@ -1206,7 +1505,13 @@ int grid8(K kernel, int64_t N) {
   return resident_grid(reinterpret_cast<const void*>(kernel), kThreads8, 0, tiles_of(N), kWaves8);
 }
 
+template <class K>
+int gridR(K kernel, int64_t N) {
+  return resident_grid(reinterpret_cast<const void*>(kernel), kThreadsR, 0, tiles_of(N), kWavesR);
+}
 int tail_bwd_grid(int64_t N, bool has_prev) {
+  if (GASFM_PT_BWD_R)
+    return has_prev ? gridR(&point_tail_bwd_r_kernel<true>, N) : gridR(&point_tail_bwd_r_kernel<false>, N);
   return has_prev ? grid8(&point_tail_bwd_kernel<true>, N) : grid8(&point_tail_bwd_kernel<false>, N);
 }
 int hub_ab_grid(int64_t N, bool hr) {
@@ -1267,6 +1572,15 @@ extern "C" int gasfm_point_tail_bwd(const float* dout, const float* prev, const 
   GASFM_REQUIRE(aligned16(dout) && aligned16(agg), "gasfm_point_tail_bwd: alignment");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int gsz = tail_bwd_grid(N, prev != nullptr);
+  if (GASFM_PT_BWD_R) {
+    if (prev)
+      hipLaunchKernelGGL(point_tail_bwd_r_kernel<true>, dim3(gsz), dim3(kThreadsR), 0, st, dout, prev, agg, N, Wp,
+                         bp, ln_w, ln_b, eps, Wm, dx, dagg, part);
+    else
+      hipLaunchKernelGGL(point_tail_bwd_r_kernel<false>, dim3(gsz), dim3(kThreadsR), 0, st, dout, prev, agg, N, Wp,
+                         bp, ln_w, ln_b, eps, Wm, dx, dagg, part);
+    return launch_status("gasfm_point_tail_bwd");
+  }
   if (prev)
     hipLaunchKernelGGL(point_tail_bwd_kernel<true>, dim3(gsz), dim3(kThreads8), 0, st, dout, prev, agg, N, Wp, bp,
                        ln_w, ln_b, eps, Wm, dx, dagg, part);

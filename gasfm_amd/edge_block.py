@@ -13,8 +13,11 @@ read: an uninitialised 1x1 tensor, no fill kernel) whose gradient
 the epilogue's backward sets to dP' (the block-output gradient), so that the
 prologue's backward kernel can do the whole P-side backward in one pass:
   dP = LN_bwd(mask * (Wl^T dXL + Wp^T dP'/4)) + dP'      (identity residual, layers.py:254-261)
-Node-level work between them (per-point / per-camera / global MLPs) stays in
-torch and runs on MFMA through hipBLASLt.
+For the 32-wide blocks the prologue and the camera-direction attention are one kernel
+(EdgeCamFn, csrc/edge_cam.hip).  Node-level work between them runs in the fused point /
+view / global kernels (point_block.py, view_block.py, dense.py: csrc/point_block.hip,
+view_block.hip, global_vec.hip); only the camera side's two m x 1024 x 1024 GEMMs per block
+go through hipBLASLt (or the HIP MFMA GEMMs, view_block._mm).
 """
 import torch
 

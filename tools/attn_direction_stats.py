@@ -2,12 +2,14 @@
 
 usage: python tools/attn_direction_stats.py <run_results.db> [steps_to_skip]
 
-Every block's forward launches its two edge-sized GATv2 attentions in a fixed order -- the point
-direction (proj2scenepoint, the bench's roofline kernel) first, then the camera direction
-(proj2view) -- followed by the global graphs' small kernels (Geom<1024,256>, Geom<64,16>).  The
-k-th edge-sized forward launch of a step is therefore the point direction for even k; the
-backward (DualAttentionFn.backward) also runs the point direction first, then the camera
-direction.  (Round-2 profiles before this note labelled the backward the other way round.)  Prints per
+Launches are labelled by the block structure of the kernel sequence, not by a global parity:
+  * blocks whose prologue is edge_cam_fwd (csrc/edge_cam.hip) run the camera direction inside
+    that fused kernel, so their one edge-sized attention forward is the point direction; the
+    same holds in the backward, where edge_cam_bwd follows the point-direction backward;
+  * a block with a separate prologue (block 0: edge0_prologue_fwd, or edge_prologue_fwd when
+    GASFM_EDGE_CAM=0) launches DualAttentionFn's two attentions point first, then camera, in
+    both passes.
+The global graphs' small kernels (Geom<1024,256>, Geom<64,16>) are skipped.  Prints per
 (kernel, direction): launches, mean / min / max microseconds and workgroups, over the steps
 after the first ``steps_to_skip`` (default 2, the warm-up).
 """
@@ -27,18 +29,33 @@ def main():
         print("not enough steps in the trace")
         return
     stats = defaultdict(list)
+    edge_sized = lambda n: (re.search(r"attn_(fwd|bwd)", n) and "combine" not in n
+                            and not re.search(r"Geom<(1024, 256|64, 16)>", n))
     for a, b in zip(starts[skip:], starts[skip + 1:] + [len(rows)]):
-        seen = defaultdict(int)
-        for name, s, e, wgs in rows[a:b]:
-            if not re.search(r"attn_(fwd|bwd)", name) or "combine" in name:
+        seg = rows[a:b]
+        fused_fwd = False  # current forward block's prologue is edge_cam_fwd
+        k_fwd = 0          # edge-sized forward launches since the block's prologue
+        k_bwd = 0          # unfused backward launches since the last backward edge kernel
+        for i, (name, s, e, wgs) in enumerate(seg):
+            if re.search(r"edge_cam_fwd|edge_prologue_fwd|edge0_prologue_fwd", name):
+                fused_fwd, k_fwd = "edge_cam_fwd" in name, 0
                 continue
-            if re.search(r"Geom<(1024, 256|64, 16)>", name):
-                continue  # the global graphs (views -> global, points -> global)
+            if re.search(r"edge_cam_bwd|edge_prologue_bwd|edge0_prologue_bwd|edge_epilogue_bwd|edge0_epilogue_bwd",
+                         name):
+                k_bwd = 0
+                continue
+            if not edge_sized(name):
+                continue
             kern = re.sub(r"\(.*", "", name.replace("void ", "").replace("(anonymous namespace)::", "").replace("gasfm::", ""))
-            kind = "bwd" if "bwd" in kern else "fwd"
-            k = seen[kind]
-            seen[kind] += 1
-            point = k % 2 == 0
+            if "bwd" in kern:
+                nxt = [r[0] for r in seg[i + 1:i + 4]]
+                point = any("edge_cam_bwd" in n for n in nxt) or k_bwd % 2 == 0
+                k_bwd += 1
+                kind = "bwd"
+            else:
+                point = fused_fwd or k_fwd % 2 == 0
+                k_fwd += 1
+                kind = "fwd"
             stats[(kind, kern, "point (proj2scenepoint)" if point else "camera (proj2view)")].append(((e - s) / 1e3,
                                                                                                      wgs))
     print(f"{'pass':4s} {'kernel':44s} {'direction':24s} {'launches':>8s} {'mean_us':>8s} {'min_us':>8s} "

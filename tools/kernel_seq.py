@@ -22,7 +22,7 @@ def main():
     st = [i for i, r in enumerate(rows) if "edge0_prologue_fwd" in r[0]]
     seg = rows[st[step]:st[step + 1]]
     if blk >= 0:
-        idx = [i for i, r in enumerate(seg) if "edge_prologue_fwd_kernel<true>" in r[0]]
+        idx = [i for i, r in enumerate(seg) if "edge_prologue_fwd_kernel<true>" in r[0] or "edge_cam_fwd_kernel<true>" in r[0]]
         seg = seg[idx[blk]:idx[blk + 1]]
     else:
         first_bwd = next(i for i, r in enumerate(seg) if "bwd" in r[0])
