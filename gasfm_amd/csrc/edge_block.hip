@@ -68,18 +68,21 @@ constexpr int LDW = 48;          // LDS row stride of staged weights (<= 32 colu
 constexpr int LDW64 = 80;        // LDS row stride of staged 64-column weights
 
 // Load a 16 x 32 tile of P (rows row0.., global stride 32): the 8 lanes 8k..8k+7 hold row
-// k + 8u (u = 0, 1).  Per row LayerNorm statistics by 3 xor-shuffles.  Writes x_hat
-// (pre-affine; identity when !LN) to Xh, relu(x_hat*g+b) (x when !LN) to Ph, raw values
-// to Raw (each optional, stride 34) and rstd to Rs.  Rows >= nrows are zeros.
-// Row layout of a 16 x 32 tile: lane l holds row (l>>3) + 8u (u = 0, 1), columns 4(l&7)..+3.
+// k + 8u (u = 0, 1).  Row layout of a 16 x 32 tile: lane l holds row (l>>3) + 8u (u = 0, 1),
+// columns 4(l&7)..+3.  Rows >= nrows re-read row 0 of the tile and are NOT zeroed here: the
+// loads are a prefetch one tile ahead, and a select on the loaded registers right after them
+// makes the wave wait for the loads at once (s_waitcnt vmcnt), i.e. no prefetch at all.  The
+// consumers mask dead rows (norm_rows32 writes zeros for them; mask_rows32 for raw rows).
 __device__ __forceinline__ void load_rows32(const float* __restrict__ P, int64_t row0, int nrows, float4 (&v)[2],
                                             int lane) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int r = (lane >> 3) + 8 * u;
     v[u] = *reinterpret_cast<const float4*>(P + (row0 + (r < nrows ? r : 0)) * F + (lane & 7) * 4);  // see load_tile
-    if (r >= nrows) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+}
+__device__ __forceinline__ float4 mask_row(float4 v, bool live) {
+  return live ? v : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 // LayerNorm of the row-layout registers v (rows >= nrows written as zeros): x_hat (pre-affine;
@@ -134,19 +137,6 @@ __device__ __forceinline__ void norm_rows32(const float4 (&v)[2], int nrows, con
     }
     if (Rs && (lane & 7) == 0) Rs[r] = rstd;
   }
-}
-
-template <bool LN>
-__device__ __forceinline__ void load_norm_tile(const float* __restrict__ P, int64_t row0, int nrows,
-                                               const Affine4& af, float eps, float* Xh, float* Ph, float* Raw,
-                                               float* Rs, int lane, float4* raw_regs = nullptr) {
-  float4 v[2];
-  load_rows32(P, row0, nrows, v, lane);
-  if (raw_regs) {
-    raw_regs[0] = v[0];
-    raw_regs[1] = v[1];
-  }
-  norm_rows32<LN>(v, nrows, af, eps, Xh, Ph, Raw, Rs, lane);
 }
 
 // =====================================================================================
@@ -211,7 +201,9 @@ __global__ __launch_bounds__(kThreads, GASFM_PFWD_MINWAVES) void edge_prologue_f
       dst[u] = (pos && c4 < F) ? int64_t(npos[u]) : row0 + r;
     }
     norm_rows32<LN>(np, nrows, af, eps, nullptr, T, nullptr, nullptr, lane);
-    if (t + nw < ntiles) issue(t + nw);  // next tile in flight during this tile's MFMA and stores
+    // next tile in flight during this tile's MFMA and stores (unconditional: the last tile
+    // re-reads itself; a load under a branch makes the join wait for every outstanding load)
+    issue(t + nw < ntiles ? t + nw : t);
     wave_sync();
     f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
@@ -324,7 +316,7 @@ __global__ __launch_bounds__(kThreads, GASFM_EFWD_MINWAVES) void edge_epilogue_f
       raw[u] = np[u];
     }
     norm_rows32<true>(raw, nrows, af, eps, nullptr, Ph, nullptr, nullptr, lane);
-    if (t + nw < t_hi) issue(t + nw);
+    issue(t + nw < t_hi ? t + nw : t);  // unconditional (see edge_prologue_fwd)
     wave_sync();
     f32x4 acc[2] = {zero4(), zero4()};
 #pragma unroll
@@ -398,36 +390,56 @@ __global__ __launch_bounds__(kThreads, GASFM_EBWD_MINWAVES) void edge_epilogue_b
   // register copy of the next tile: dP' and P rows (row layout), P0 (lanes < 2*nrows)
   float4 nd[2], np[2];
   float nq = 0.f;
+  // dead rows masked where staged (see load_rows32); branch-free: without P0 the P0 load reads
+  // P's first words and is not used (a load under a branch makes the join wait for every load)
+  const float* p0p = P0 ? P0 : P;
   auto issue = [&](int64_t row0, int nrows) {
     load_rows32(dPo, row0, nrows, nd, lane);
     load_rows32(P, row0, nrows, np, lane);
-    if (P0) {
-      nq = P0[row0 * 2 + (lane < 2 * nrows ? lane : 0)];
-      if (lane >= 2 * nrows) nq = 0.f;
-    }
+    nq = p0p[row0 * 2 + (lane < 2 * nrows ? lane : 0)];
   };
+  auto rows_at = [](const gasfm_work_item& w, int64_t row0) { return int(w.end - row0 < TR ? w.end - row0 : TR); };
   const int gw = blockIdx.x * kWaves + wave, nw = gridDim.x * kWaves;
+  gasfm_work_item w{0, 0, 0, -1};
+  if (gw < n_items) {
+    w = items[gw];
+    if (w.begin < w.end) issue(w.begin, rows_at(w, w.begin));
+  }
   for (int it = gw; it < n_items; it += nw) {
-    const gasfm_work_item w = items[it];
     float dsv[2] = {0.f, 0.f};
-    if (w.begin < w.end) issue(w.begin, w.end - w.begin < TR ? w.end - w.begin : TR);
+    gasfm_work_item wn{0, 0, 0, -1};
+    const bool more = it + nw < n_items;
+    if (more) wn = items[it + nw];
+    if (w.begin >= w.end && more && wn.begin < wn.end) issue(wn.begin, rows_at(wn, wn.begin));
     for (int64_t row0 = w.begin; row0 < w.end; row0 += TR) {
-      const int nrows = int(w.end - row0 < TR ? w.end - row0 : TR);
+      const int nrows = rows_at(w, row0);
       // stage the prefetched tile, then request the next one before the MFMA work
       {
         const int cc = (lane & 7) * 4;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           float* d = D + ((lane >> 3) + 8 * u) * LD34 + cc;
-          d[0] = nd[u].x;
-          d[1] = nd[u].y;
-          d[2] = nd[u].z;
-          d[3] = nd[u].w;
+          const float4 v = mask_row(nd[u], (lane >> 3) + 8 * u < nrows);
+          d[0] = v.x;
+          d[1] = v.y;
+          d[2] = v.z;
+          d[3] = v.w;
         }
         norm_rows32<true>(np, nrows, af, eps, nullptr, Ph, nullptr, nullptr, lane);
-        if (lane < 2 * TR) Q0[lane] = nq;
+        if (lane < 2 * TR) Q0[lane] = (P0 && lane < 2 * nrows) ? nq : 0.f;
       }
-      if (row0 + TR < w.end) issue(row0 + TR, w.end - (row0 + TR) < TR ? int(w.end - (row0 + TR)) : TR);
+      {  // the next tile: this item's, else the next item's first; the last one re-reads itself
+        int64_t r1 = row0;
+        int n1 = nrows;
+        if (row0 + TR < w.end) {
+          r1 = row0 + TR;
+          n1 = rows_at(w, r1);
+        } else if (more && wn.begin < wn.end) {
+          r1 = wn.begin;
+          n1 = rows_at(wn, r1);
+        }
+        issue(r1, n1);
+      }
       wave_sync();
 #pragma unroll
       for (int s = 0; s < TR / 4; ++s) {
@@ -470,6 +482,7 @@ __global__ __launch_bounds__(kThreads, GASFM_EBWD_MINWAVES) void edge_epilogue_b
       dst[c] = dsv[0];
       dst[16 + c] = dsv[1];
     }
+    w = wn;
   }
   float v[20];
 #pragma unroll
@@ -526,13 +539,12 @@ __device__ __forceinline__ void pb_issue(PbTile& T, const float* __restrict__ dX
   // Rows past the end re-read row 0 of the tile (always valid) and are zeroed afterwards: a
   // conditional load would be lowered to a flat access through a pointer select.
   // dXL: this lane's column block of the gradient (the point or the camera half, see the kernel)
-  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  // Dead rows are masked where the tile is staged, not here (see load_rows32).
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int r = (lane >> 4) + 4 * u;
     const int rr = r < nrows ? r : 0;
     T.x[u] = *reinterpret_cast<const float4*>(dXL + (row0 + rr) * ldX);
-    if (r >= nrows) T.x[u] = z;
   }
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -540,7 +552,6 @@ __device__ __forceinline__ void pb_issue(PbTile& T, const float* __restrict__ dX
     const int rr = r < nrows ? r : 0;
     T.p[u] = *reinterpret_cast<const float4*>(P + (row0 + rr) * F + (lane & 7) * 4);
     if (RES) T.d[u] = *reinterpret_cast<const float4*>(dRes + (row0 + rr) * F + (lane & 7) * 4);
-    if (r >= nrows) T.p[u] = T.d[u] = z;
   }
 }
 
@@ -602,8 +613,9 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINWAVES) void edge_prologue_b
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         float* d = T1 + ((lane >> 4) + 4 * u) * LD66 + (lane & 15) * 4;
-        st2(d, cur.x[u].x, cur.x[u].y);
-        st2(d + 2, cur.x[u].z, cur.x[u].w);
+        const float4 x = mask_row(cur.x[u], (lane >> 4) + 4 * u < nrows);
+        st2(d, x.x, x.y);
+        st2(d + 2, x.z, x.w);
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -627,13 +639,18 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINWAVES) void edge_prologue_b
         if ((lane & 7) == 0) Rs[r] = rstd;
         if (RES) {
           float* q3 = T3 + r * LD34 + (lane & 7) * 4;
-          st2(q3, cur.d[u].x, cur.d[u].y);
-          st2(q3 + 2, cur.d[u].z, cur.d[u].w);
+          const float4 d3 = mask_row(cur.d[u], live);
+          st2(q3, d3.x, d3.y);
+          st2(q3 + 2, d3.z, d3.w);
         }
       }
     }
-    // request the next tile before this one's MFMA work
-    if (t + nw < ntiles) pb_issue<RES>(nxt, dxl, ldx, (t + nw) * TR, P, dRes, rows_of(t + nw), lane);
+    // request the next tile before this one's MFMA work (unconditional: the last tile re-reads
+    // itself; a load under a branch makes the join wait for every outstanding load)
+    {
+      const int64_t tn = t + nw < ntiles ? t + nw : t;
+      pb_issue<RES>(nxt, dxl, ldx, tn * TR, P, dRes, rows_of(tn), lane);
+    }
     wave_sync();
     // dP_hat (C layout: edge 4g+r, column nt*16+c) = dXL W (+ dRes scale Wp)
     f32x4 acc[2] = {zero4(), zero4()};

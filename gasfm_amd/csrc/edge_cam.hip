@@ -55,14 +55,15 @@ __device__ __forceinline__ float row_max16(float v) {
 }
 
 // Rows of a 16 x 32 tile in row layout: lane l holds row (l >> 3) + 8u (u = 0, 1), columns
-// 4 (l & 7) .. + 3.  Rows >= nrows re-read row 0 (always valid) and are zeroed.
+// 4 (l & 7) .. + 3.  Rows >= nrows re-read row 0 (always valid); phat_to_lds writes zeros for
+// them.  No select on the loaded registers here: these loads are the next tile's prefetch, and
+// a select right after them would make the wave wait for them at once.
 __device__ __forceinline__ void load_rows(const float* __restrict__ X, int64_t ld, int64_t row0, int nrows,
                                           float4 (&v)[2], int lane) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int r = (lane >> 3) + 8 * u;
     v[u] = *reinterpret_cast<const float4*>(X + (row0 + (r < nrows ? r : 0)) * ld + (lane & 7) * 4);
-    if (r >= nrows) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
@@ -153,9 +154,12 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_fwd_kernel(
 
   float4 np[2];
   int32_t npos = 0;  // point-order row of this lane's edge (column c)
+  // branch-free: without pos the index load reads P's first words and is not used (a load under a
+  // branch makes the join wait for every load in flight)
+  const int32_t* posp = pos ? pos : reinterpret_cast<const int32_t*>(P);
   auto issue = [&](int64_t row0, int nrows) {
     load_rows(P, F, row0, nrows, np, lane);
-    if (pos) npos = pos[row0 + (c < nrows ? c : 0)];
+    npos = posp[row0 + (c < nrows ? c : 0)];
   };
   auto rows_at = [](const gasfm_work_item& w, int64_t row0) { return int(w.end - row0 < TR ? w.end - row0 : TR); };
 
@@ -182,10 +186,18 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_fwd_kernel(
       const int nrows = rows_at(w, row0);
       phat_to_lds<LN>(np, nrows, g4, b4, eps, T, lane);
       const int64_t dst = pos ? int64_t(npos) : row0 + c;
-      if (row0 + TR < w.end)
-        issue(row0 + TR, rows_at(w, row0 + TR));
-      else if (more && wn.begin < wn.end)
-        issue(wn.begin, rows_at(wn, wn.begin));
+      {  // the next tile (this item's, else the next item's first; the last one re-reads itself)
+        int64_t r1 = row0;
+        int n1 = nrows;
+        if (row0 + TR < w.end) {
+          r1 = row0 + TR;
+          n1 = rows_at(w, r1);
+        } else if (more && wn.begin < wn.end) {
+          r1 = wn.begin;
+          n1 = rows_at(wn, r1);
+        }
+        issue(r1, n1);
+      }
       wave_sync();
       f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
       xl_t<4>(Wl, T, acc, c, g);
@@ -347,10 +359,18 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_bwd_kernel(
     for (int64_t row0 = w.begin; row0 < w.end; row0 += TR) {
       const int nrows = rows_at(w, row0);
       phat_to_lds<LN>(np, nrows, g4, b4, eps, T, lane);
-      if (row0 + TR < w.end)
-        issue(row0 + TR, rows_at(w, row0 + TR));
-      else if (more && wn.begin < wn.end)
-        issue(wn.begin, rows_at(wn, wn.begin));
+      {  // the next tile (see edge_cam_fwd_kernel)
+        int64_t r1 = row0;
+        int n1 = nrows;
+        if (row0 + TR < w.end) {
+          r1 = row0 + TR;
+          n1 = rows_at(w, r1);
+        } else if (more && wn.begin < wn.end) {
+          r1 = wn.begin;
+          n1 = rows_at(wn, r1);
+        }
+        issue(r1, n1);
+      }
       wave_sync();
       f32x4 xc[2] = {zero4(), zero4()};
       xl_t<2>(Wl, T, xc, c, g);
