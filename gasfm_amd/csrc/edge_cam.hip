@@ -109,11 +109,94 @@ __device__ __forceinline__ void xl_t(const float* Wl, const float* T, f32x4 (&ac
   }
 }
 
+// ---- register-resident front end (GASFM_EDGE_CAM_R, default): no P_hat tile in LDS.
+// P rows are loaded straight into the B-operand layout of the transposed product ("slabs": lane
+// (g, c) holds P[edge c][16 u + 4 g + j], j < 4, u = 0, 1 -- the k index of MFMA step (u, j) is
+// 16 u + 4 g + j), the LayerNorm runs on those registers (a row's 32 features: 8 per lane, then
+// the 4 lane groups), and the weights are staged once per workgroup as float4 slabs in the same
+// k order (one ds_read_b128 per 4 MFMAs; was a ds_read_b32 per MFMA operand and a 16 x 34 LDS
+// tile write + read per 16 edges).  The accumulators come out exactly as xl_t's (lane (g, c):
+// features 16 ot + 4 g + r of edge c).
+#ifndef GASFM_EDGE_CAM_R
+#define GASFM_EDGE_CAM_R 1
+#endif
+constexpr bool kCamR = GASFM_EDGE_CAM_R != 0;
+#ifndef GASFM_CAM_MINW
+#define GASFM_CAM_MINW 3  // minimum waves per SIMD (168 VGPRs): fwd 282 -> 251 us, bwd 270 -> 236 us vs 2 (tools/edge_bench.py)
+#endif
+
+// W [O x 32] rows (o < O) -> slabs Q[(ot * 2 + u) * 64 + 16 g + c] = (W[16 ot + c][16 u + 4 g + j], j < 4)
+template <int O, int NT, class Src>
+__device__ __forceinline__ void stage_slabs32(Src src, float* Q) {
+  Stage<O * F, NT> st;
+  st.load([&](int q) { return src(q); });
+  st.store([&](int q, float v) {
+    const int o = q / F, k = q % F;
+    Q[(((o / 16) * 2 + k / 16) * 64 + ((k % 16) / 4) * 16 + o % 16) * 4 + k % 4] = v;
+  });
+}
+
+// P rows of edge c (clamped to a valid row; dead rows are computed and never stored)
+__device__ __forceinline__ void load_slabs32(const float* __restrict__ X, int64_t row0, int nrows, f32x4 (&v)[2],
+                                             int lane) {
+  const int c = lane & 15, g = lane >> 4;
+  const float* p = X + (row0 + (c < nrows ? c : 0)) * F + 4 * g;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const float4 t = *reinterpret_cast<const float4*>(p + 16 * u);
+    v[u] = f32x4{t.x, t.y, t.z, t.w};
+  }
+}
+
+// relu(LN(P)) (LN) or P (the final update) in place on the slabs; g8 / b8: gamma / beta at this
+// lane's features 16 u + 4 g + j
+template <bool LN>
+__device__ __forceinline__ void phat_slabs(f32x4 (&v)[2], const float (&g8)[2][4], const float (&b8)[2][4],
+                                           float eps) {
+  if (!LN) return;
+  float sm = (v[0][0] + v[0][1]) + (v[0][2] + v[0][3]) + ((v[1][0] + v[1][1]) + (v[1][2] + v[1][3]));
+  sm += __shfl_xor(sm, 16);
+  sm += __shfl_xor(sm, 32);
+  const float mean = sm * (1.f / F);
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q = fmaf(v[u][j] - mean, v[u][j] - mean, q);
+  q += __shfl_xor(q, 16);
+  q += __shfl_xor(q, 32);
+  const float rstd = rsqrtf(q * (1.f / F) + eps);
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[u][j] = fmaxf(fmaf((v[u][j] - mean) * rstd, g8[u][j], b8[u][j]), 0.f);
+}
+
+// acc[ot] += W P_hat^T (A = W slabs, B = P_hat slabs): acc[ot][r] = feature 16 ot + 4 g + r of edge c
+template <int OT>
+__device__ __forceinline__ void xl_slabs(const float4* __restrict__ Q, const f32x4 (&x)[2], f32x4 (&acc)[OT],
+                                         int lane) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float4 w[OT];
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) w[ot] = Q[(ot * 2 + u) * 64 + lane];
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) acc[ot] = mfma16(w[ot].x, x[u][0], acc[ot]);
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) acc[ot] = mfma16(w[ot].y, x[u][1], acc[ot]);
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) acc[ot] = mfma16(w[ot].z, x[u][2], acc[ot]);
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) acc[ot] = mfma16(w[ot].w, x[u][3], acc[ot]);
+  }
+}
+
 // =============================================================================================
 // forward
 // =============================================================================================
 template <bool LN>
-__global__ __launch_bounds__(kThreads, 2) void edge_cam_fwd_kernel(
+__global__ __launch_bounds__(kThreads, GASFM_CAM_MINW) void edge_cam_fwd_kernel(
     const float* __restrict__ P, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
     const float* __restrict__ Wpt, const float* __restrict__ bpt, const float* __restrict__ Wc,
     const float* __restrict__ bc, float* __restrict__ XLp, int64_t ldXLp, const int32_t* __restrict__ pos,
@@ -121,9 +204,11 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_fwd_kernel(
     float slope, const gasfm_work_item* __restrict__ items, int n_items, int finalize, float* __restrict__ out,
     int64_t ldOut, float* __restrict__ seg_max, float* __restrict__ seg_sum, int64_t ldStat,
     float* __restrict__ part) {
-  __shared__ float Wl[NX * LDA];                  // Wl[n][k] = [Wpt; Wc][n][k]
-  __shared__ float tiles[kWaves][TR * LD34];
-  {
+  __shared__ __attribute__((aligned(16))) float Wl[kCamR ? NX * F : NX * LDA];  // slabs, or Wl[n][k] = [Wpt; Wc][n][k]
+  __shared__ float tiles[kCamR ? 1 : kWaves][TR * LD34];
+  if (kCamR) {
+    stage_slabs32<NX, kThreads>([&](int q) { return q < F * F ? Wpt[q] : Wc[q - F * F]; }, Wl);
+  } else {
     Stage<NX * F, kThreads> sw;
     sw.load([&](int q) { return q < F * F ? Wpt[q] : Wc[q - F * F]; });
     sw.store([&](int q, float v) { Wl[(q / F) * LDA + q % F] = v; });
@@ -131,11 +216,19 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_fwd_kernel(
   __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
-  float* T = tiles[wave];
+  float* T = tiles[kCamR ? 0 : wave];
   float4 g4 = make_float4(1.f, 1.f, 1.f, 1.f), b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float g8[2][4], b8[2][4];  // gamma / beta at the slab features 16 u + 4 g + j
   if (LN) {
     g4 = *reinterpret_cast<const float4*>(gam + (lane & 7) * 4);
     b4 = *reinterpret_cast<const float4*>(bet + (lane & 7) * 4);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        g8[u][j] = gam[16 * u + 4 * g + j];
+        b8[u][j] = bet[16 * u + 4 * g + j];
+      }
   }
   // this lane's features: point 16 ot + 4 g + r (ot = 0, 1); camera 16 q + 4 g + r (q = 0, 1),
   // head 2 q + (g >> 1)
@@ -153,12 +246,16 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_fwd_kernel(
   const int gw = blockIdx.x * kWaves + wave, nw = gridDim.x * kWaves;
 
   float4 np[2];
+  f32x4 ns[2];
   int32_t npos = 0;  // point-order row of this lane's edge (column c)
   // branch-free: without pos the index load reads P's first words and is not used (a load under a
   // branch makes the join wait for every load in flight)
   const int32_t* posp = pos ? pos : reinterpret_cast<const int32_t*>(P);
   auto issue = [&](int64_t row0, int nrows) {
-    load_rows(P, F, row0, nrows, np, lane);
+    if (kCamR)
+      load_slabs32(P, row0, nrows, ns, lane);
+    else
+      load_rows(P, F, row0, nrows, np, lane);
     npos = posp[row0 + (c < nrows ? c : 0)];
   };
   auto rows_at = [](const gasfm_work_item& w, int64_t row0) { return int(w.end - row0 < TR ? w.end - row0 : TR); };
@@ -184,7 +281,8 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_fwd_kernel(
     if (w.begin >= w.end && more && wn.begin < wn.end) issue(wn.begin, rows_at(wn, wn.begin));
     for (int64_t row0 = w.begin; row0 < w.end; row0 += TR) {
       const int nrows = rows_at(w, row0);
-      phat_to_lds<LN>(np, nrows, g4, b4, eps, T, lane);
+      f32x4 ph[2] = {ns[0], ns[1]};
+      if (!kCamR) phat_to_lds<LN>(np, nrows, g4, b4, eps, T, lane);
       const int64_t dst = pos ? int64_t(npos) : row0 + c;
       {  // the next tile (this item's, else the next item's first; the last one re-reads itself)
         int64_t r1 = row0;
@@ -198,9 +296,14 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_fwd_kernel(
         }
         issue(r1, n1);
       }
-      wave_sync();
       f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
-      xl_t<4>(Wl, T, acc, c, g);
+      if (kCamR) {
+        phat_slabs<LN>(ph, g8, b8, eps);
+        xl_slabs<4>(reinterpret_cast<const float4*>(Wl), ph, acc, lane);
+      } else {
+        wave_sync();
+        xl_t<4>(Wl, T, acc, c, g);
+      }
       const bool valid = c < nrows;
       // point half: this lane's 2 x 4 features of edge c (non-temporal: streamed once by the point
       // attention)
@@ -231,7 +334,7 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_fwd_kernel(
           m[q] = mn;
         }
       }
-      wave_sync();  // T is rewritten by the next tile
+      if (!kCamR) wave_sync();  // T is rewritten by the next tile
     }
     // merge the 16 edge columns' states
 #pragma unroll
@@ -278,7 +381,7 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_fwd_kernel(
 constexpr int BP_PART = 2 * F;
 
 template <bool LN>
-__global__ __launch_bounds__(kThreads, 2) void edge_cam_bwd_kernel(
+__global__ __launch_bounds__(kThreads, GASFM_CAM_MINW) void edge_cam_bwd_kernel(
     const float* __restrict__ P, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
     const float* __restrict__ Wc, const float* __restrict__ bc, const float* __restrict__ XR, int64_t ldXR,
     const float* __restrict__ att, const float* __restrict__ bias, float slope, const float* __restrict__ out,
@@ -286,9 +389,11 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_bwd_kernel(
     const float* __restrict__ gout, int64_t ldG, const gasfm_work_item* __restrict__ items, int n_items,
     float* __restrict__ dXLc, int64_t ldD, float* __restrict__ dXR, int64_t ldDXR, float* __restrict__ part_dxr,
     float* __restrict__ part) {
-  __shared__ float Wl[F * LDA];  // Wl[n][k] = Wc[n][k]
-  __shared__ float tiles[kWaves][TR * LD34];
-  {
+  __shared__ __attribute__((aligned(16))) float Wl[kCamR ? F * F : F * LDA];  // slabs, or Wl[n][k] = Wc[n][k]
+  __shared__ float tiles[kWaves][TR * LD34];  // (also the final reduction's scratch)
+  if (kCamR) {
+    stage_slabs32<F, kThreads>([&](int q) { return Wc[q]; }, Wl);
+  } else {
     Stage<F * F, kThreads> sw;
     sw.load([&](int q) { return Wc[q]; });
     sw.store([&](int q, float v) { Wl[(q / F) * LDA + q % F] = v; });
@@ -298,9 +403,17 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_bwd_kernel(
   const int c = lane & 15, g = lane >> 4;
   float* T = tiles[wave];
   float4 g4 = make_float4(1.f, 1.f, 1.f, 1.f), b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float g8[2][4], b8[2][4];  // gamma / beta at the slab features 16 u + 4 g + j
   if (LN) {
     g4 = *reinterpret_cast<const float4*>(gam + (lane & 7) * 4);
     b4 = *reinterpret_cast<const float4*>(bet + (lane & 7) * 4);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        g8[u][j] = gam[16 * u + 4 * g + j];
+        b8[u][j] = bet[16 * u + 4 * g + j];
+      }
   }
   float bcv[2][4], attv[2][4], biasv[2][4], datt[2][4], dbias[2][4];
 #pragma unroll
@@ -316,7 +429,13 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_bwd_kernel(
   const int gw = blockIdx.x * kWaves + wave, nw = gridDim.x * kWaves;
 
   float4 np[2];
-  auto issue = [&](int64_t row0, int nrows) { load_rows(P, F, row0, nrows, np, lane); };
+  f32x4 ns[2];
+  auto issue = [&](int64_t row0, int nrows) {
+    if (kCamR)
+      load_slabs32(P, row0, nrows, ns, lane);
+    else
+      load_rows(P, F, row0, nrows, np, lane);
+  };
   auto rows_at = [](const gasfm_work_item& w, int64_t row0) { return int(w.end - row0 < TR ? w.end - row0 : TR); };
   gasfm_work_item w{0, 0, 0, -1};
   if (gw < n_items) {
@@ -358,7 +477,8 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_bwd_kernel(
     if (w.begin >= w.end && more && wn.begin < wn.end) issue(wn.begin, rows_at(wn, wn.begin));
     for (int64_t row0 = w.begin; row0 < w.end; row0 += TR) {
       const int nrows = rows_at(w, row0);
-      phat_to_lds<LN>(np, nrows, g4, b4, eps, T, lane);
+      f32x4 ph[2] = {ns[0], ns[1]};
+      if (!kCamR) phat_to_lds<LN>(np, nrows, g4, b4, eps, T, lane);
       {  // the next tile (see edge_cam_fwd_kernel)
         int64_t r1 = row0;
         int n1 = nrows;
@@ -371,9 +491,14 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_bwd_kernel(
         }
         issue(r1, n1);
       }
-      wave_sync();
       f32x4 xc[2] = {zero4(), zero4()};
-      xl_t<2>(Wl, T, xc, c, g);
+      if (kCamR) {
+        phat_slabs<LN>(ph, g8, b8, eps);
+        xl_slabs<2>(reinterpret_cast<const float4*>(Wl), ph, xc, lane);
+      } else {
+        wave_sync();
+        xl_t<2>(Wl, T, xc, c, g);
+      }
       const bool valid = c < nrows;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -401,7 +526,7 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_bwd_kernel(
         if (valid)
           *reinterpret_cast<float4*>(dXLc + (row0 + c) * ldD + 16 * q + 4 * g) = make_float4(dx[0], dx[1], dx[2], dx[3]);
       }
-      wave_sync();  // T is rewritten by the next tile
+      if (!kCamR) wave_sync();  // T is rewritten by the next tile
     }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {

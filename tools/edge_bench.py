@@ -75,6 +75,25 @@ def main():
     part = torch.empty(rows, 64 * 32 + 128, device=dev)
     run("edge_prologue_bwd(LN, RES)",
         lambda: _native.edge_prologue_bwd(dXL, P, dPo, ln_w, ln_b, 1e-5, W, Wp, 0.25, dP, part), E * 640)
+    # prologue + camera attention (csrc/edge_cam.hip) on the camera plan, and its backward
+    XLp = torch.empty(E, 32, device=dev)
+    XRc, att, bias = rnd(m, 32), rnd(32) / 4, rnd(32)
+    co, cmax, csum = torch.empty(m, 32, device=dev), torch.empty(m, 4, device=dev), torch.empty(m, 4, device=dev)
+    cpart = torch.empty(max(pc.n_part_rows, 1), 40, device=dev)
+    run("edge_cam_fwd(LN, pos)",
+        lambda: _native.edge_cam_fwd(P, ln_w, ln_b, 1e-5, W[:32].contiguous(), b[:32].contiguous(),
+                                     W[32:].contiguous(), b[32:].contiguous(), XLp, pp.pos, XRc, att, bias, 0.2,
+                                     pc.items, pc.n_items, True, co, cmax, csum, cpart),
+        E * (128 + 128 + 4) + m * 128)
+    dXLc, dXRc = torch.empty(E, 32, device=dev), torch.empty(m, 32, device=dev)
+    pdxr = torch.empty(max(pc.n_part_rows, 1), 32, device=dev)
+    r_, c_ = _native.edge_cam_bwd_part_shape(pc.n_items)
+    cbp = torch.empty(r_, c_, device=dev)
+    gout = rnd(m, 32)
+    run("edge_cam_bwd(LN)",
+        lambda: _native.edge_cam_bwd(P, ln_w, ln_b, 1e-5, W[32:].contiguous(), b[32:].contiguous(), XRc, att, bias,
+                                     0.2, co, cmax, csum, gout, pc.items, pc.n_items, dXLc, dXRc, pdxr, cbp),
+        E * (128 + 128) + m * 256)
     dSp = torch.empty(n, 32, device=dev)
     run("segment_rowsum", lambda: _native.segment_rowsum(pp.items, pp.n_items, pp.perm, dPo, 0.25, dSp, None),
         E * 132 + n * 128)
