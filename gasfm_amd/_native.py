@@ -51,6 +51,11 @@ _SIGS = {
                                        _vp, _vp]),
     "gasfm_edge_cam_bwd_part_rows": (_i32, [_i32]),
     "gasfm_edge_cam_bwd_part_cols": (_i32, []),
+    "gasfm_edge_cam_pbwd_part_rows": (_i32, [_i32]),
+    "gasfm_edge_cam_pbwd_part_cols": (_i32, []),
+    "gasfm_edge_cam_pbwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _f32, _vp, _i64, _vp, _vp, _f32, _vp,
+                                   _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _vp, _i64, _vp,
+                                   _vp, _vp]),
     "gasfm_edge_cam_fwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32,
                                   _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
     "gasfm_edge_cam_bwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _vp, _i64,
@@ -595,6 +600,26 @@ def edge_cam_bwd(P, ln_w, ln_b, eps, Wc, bc, XR, att, bias, slope, out, seg_max,
                                   gout.stride(0), _p(plan_items), n_items, _p(dXLc), dXLc.stride(0), _p(dXR),
                                   dXR.stride(0), _p(part_dxr), _p(part), _stream(P))
     check(st, "gasfm_edge_cam_bwd")
+
+
+def edge_cam_pbwd_part_shape(n_items):
+    L = lib()
+    return int(L.gasfm_edge_cam_pbwd_part_rows(n_items)), int(L.gasfm_edge_cam_pbwd_part_cols())
+
+
+def edge_cam_pbwd(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, scale, XR, att, bias, slope, out, seg_max, seg_sum, gout,
+                  plan_items, n_items, dXLp, dRes, dP, dXR, part_dxr, part, ldStat=4):
+    """The camera attention's backward and the block's edge prologue backward in one pass
+    (csrc/edge_cam.hip edge_cam_pbwd): dP, dXR (+ split partials), part rows
+    [dW 64x32 | db 64 | dgamma 32 | dbeta 32 | datt 32 | dbias 32] per workgroup."""
+    _req(P, "P", 32)
+    ldXR = _rows32(XR, "XR")
+    st = lib().gasfm_edge_cam_pbwd(_p(P), _p(ln_w), _p(ln_b), eps, _p(Wpt), _p(Wc), _p(bc), _p(Wp),
+                                   Wp.stride(0) if Wp is not None else 0, scale, _p(XR), ldXR, _p(att), _p(bias),
+                                   slope, _p(out), out.stride(0), _p(seg_max), _p(seg_sum), ldStat, _p(gout),
+                                   gout.stride(0), _p(plan_items), n_items, _p(dXLp), dXLp.stride(0), _p(dRes),
+                                   _p(dP), _p(dXR), dXR.stride(0), _p(part_dxr), _p(part), _stream(P))
+    check(st, "gasfm_edge_cam_pbwd")
 
 
 def segment_rowsum(items, n_items, perm, X, scale, out, part):

@@ -561,6 +561,368 @@ __global__ __launch_bounds__(kThreads, GASFM_CAM_MINW) void edge_cam_bwd_kernel(
   }
 }
 
+// =============================================================================================
+// backward, fused: camera attention + edge prologue of the block in ONE pass over the camera
+// plan's items (gasfm_edge_cam_pbwd).  Per 16-edge tile:
+//   XLc = Wc relu(LN(P)) + bc recomputed (T layout, as edge_cam_bwd), the camera attention's
+//   backward -> dXLc in registers (T layout: the A operand of the next products as it stands);
+//   dP_hat = dXLp Wpt + dXLc Wc + dRes (scale Wp[:, :32])  (C layout, A = T-layout rows);
+//   dP = LN_bwd(mask * dP_hat) + dRes  (C layout, stored), dgamma, dbeta;
+//   dW += [dXLp | dXLc]^T relu(LN(P)), db  (C-layout operands; dXLc through a per-wave LDS
+//   transpose, dXLp / P / dRes re-read in C layout from L1).
+// Replaces edge_cam_bwd + edge_prologue_bwd: dXLc (128 B per edge) is neither written nor read
+// back, and P is read once.  Semantics: exactly those two kernels' (same partial-row layouts,
+// concatenated: [dW 64x32 | db 64 | dgamma 32 | dbeta 32 | datt 32 | dbias 32] per workgroup).
+// =============================================================================================
+constexpr int PB2_PRO = NX * F + NX + 2 * F;  // the prologue_bwd part row
+constexpr int PB2_PART = PB2_PRO + BP_PART;
+constexpr int LDT = F + 4;                    // transpose tile row stride
+
+// C-layout rows of a [*, 32] tensor: v[ft][r] = X[row0 + 4 g + r][16 ft + c] (rows clamped, not masked)
+__device__ __forceinline__ void cl_load32(const float* __restrict__ X, int64_t ld, int64_t row0, int nrows,
+                                          f32x4 (&v)[2], int lane) {
+  const int c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int rr = 4 * g + r;
+    const float* p = X + (row0 + (rr < nrows ? rr : 0)) * ld + c;
+    v[0][r] = p[0];
+    v[1][r] = p[16];
+  }
+}
+
+// acc[nt] += X M^T, X (T-layout slabs, K = 32) as the A operand: acc[nt][r] = Y[row 4 g + r][16 nt + c]
+__device__ __forceinline__ void prod_c2(const float4* __restrict__ Q, const f32x4 (&x)[2], f32x4 (&acc)[2],
+                                        int lane) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float4 w[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) w[nt] = Q[(nt * 2 + u) * 64 + lane];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma16(x[u][0], w[nt].x, acc[nt]);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma16(x[u][1], w[nt].y, acc[nt]);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma16(x[u][2], w[nt].z, acc[nt]);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma16(x[u][3], w[nt].w, acc[nt]);
+  }
+}
+
+template <bool LN, bool RES>
+__global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
+    const float* __restrict__ P, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
+    const float* __restrict__ Wpt, const float* __restrict__ Wc, const float* __restrict__ bc,
+    const float* __restrict__ Wp, int ldWp, float scale, const float* __restrict__ XR, int64_t ldXR,
+    const float* __restrict__ att, const float* __restrict__ bias, float slope, const float* __restrict__ out,
+    int64_t ldOut, const float* __restrict__ seg_max, const float* __restrict__ seg_sum, int64_t ldStat,
+    const float* __restrict__ gout, int64_t ldG, const gasfm_work_item* __restrict__ items, int n_items,
+    const float* __restrict__ dXLp, int64_t ldXp, const float* __restrict__ dRes, float* __restrict__ dP,
+    float* __restrict__ dXR, int64_t ldDXR, float* __restrict__ part_dxr, float* __restrict__ part) {
+  // LDS: weight slabs (Wc for XLc; Wpt^T, Wc^T, (scale Wp)^T for dP_hat), the per-feature vectors,
+  // and per wave four 16 x 32 transpose tiles (T -> C layout of P, dXLp, dRes, dXLc)
+  constexpr int QW = F * F;  // floats per 32 x 32 slab set
+  constexpr int OV = 4 * QW, OT = OV + 4 * F, WT = 4 * TR * LDT;
+  constexpr int NL = OT + kWaves * WT;
+  __shared__ __attribute__((aligned(16))) float lds[NL];
+  float* WcQ = lds;
+  float* WptTQ = lds + QW;
+  float* WcTQ = lds + 2 * QW;
+  float* WqTQ = lds + 3 * QW;
+  float* V = lds + OV;  // [gamma | beta | bc | att] (32 each)
+  stage_slabs32<F, kThreads>([&](int q) { return Wc[q]; }, WcQ);
+  stage_slabs32<F, kThreads>([&](int q) { return Wpt[(q % F) * F + q / F]; }, WptTQ);
+  stage_slabs32<F, kThreads>([&](int q) { return Wc[(q % F) * F + q / F]; }, WcTQ);
+  if (RES) stage_slabs32<F, kThreads>([&](int q) { return scale * Wp[(q % F) * ldWp + q / F]; }, WqTQ);
+  if (threadIdx.x < F) {
+    V[threadIdx.x] = LN ? gam[threadIdx.x] : 1.f;
+    V[F + threadIdx.x] = LN ? bet[threadIdx.x] : 0.f;
+    V[2 * F + threadIdx.x] = bc[threadIdx.x];
+    V[3 * F + threadIdx.x] = att[threadIdx.x];
+  }
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
+  const int c = lane & 15, g = lane >> 4;
+  float* Tt = lds + OT + wave * WT;  // tiles 0: P, 1: dXLp, 2: dRes, 3: dXLc
+  const float gC[2] = {LN ? gam[c] : 1.f, LN ? gam[16 + c] : 1.f}, bC[2] = {LN ? bet[c] : 0.f, LN ? bet[16 + c] : 0.f};
+  __syncthreads();
+  // T-layout vector at this lane's features 16 q + 4 g .. + 3
+  auto vecT = [&](int which, int q) {
+    const float4 t = *reinterpret_cast<const float4*>(V + which * F + 16 * q + 4 * g);
+    return f32x4{t.x, t.y, t.z, t.w};
+  };
+  // T -> C layout through tile k of this wave: writes the two slabs, returns the C-layout rows
+  auto to_c = [&](int k, const f32x4 (&t)[2], f32x4 (&o)[2]) {
+    float* T = Tt + k * TR * LDT;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      *reinterpret_cast<float4*>(T + c * LDT + 16 * u + 4 * g) = make_float4(t[u][0], t[u][1], t[u][2], t[u][3]);
+    // one wave's LDS instructions execute in order: a compiler barrier suffices
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[ft][r] = T[(4 * g + r) * LDT + 16 * ft + c];
+  };
+  f32x4 accW[4][2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) accW[mt][0] = accW[mt][1] = zero4();
+  float db[4] = {0.f, 0.f, 0.f, 0.f}, dg[2] = {0.f, 0.f}, dbt[2] = {0.f, 0.f};
+  f32x4 datt[2] = {zero4(), zero4()}, dbias[2] = {zero4(), zero4()};
+  const int gw = blockIdx.x * kWaves + wave, nw = gridDim.x * kWaves;
+
+  // next tile's rows of P, dXLp, dRes in T layout, one tile ahead (clamped, masked where consumed)
+  f32x4 nPT[2], nXT[2], nRT[2];
+  auto issue = [&](int64_t row0, int nrows) {
+    load_slabs32(P, row0, nrows, nPT, lane);
+    const float* p = dXLp + (row0 + (c < nrows ? c : 0)) * ldXp + 4 * g;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const float4 t = *reinterpret_cast<const float4*>(p + 16 * u);
+      nXT[u] = f32x4{t.x, t.y, t.z, t.w};
+    }
+    if (RES) load_slabs32(dRes, row0, nrows, nRT, lane);
+  };
+  auto rows_at = [](const gasfm_work_item& w, int64_t row0) { return int(w.end - row0 < TR ? w.end - row0 : TR); };
+  gasfm_work_item w{0, 0, 0, -1};
+  if (gw < n_items) {
+    w = items[gw];
+    if (w.begin < w.end) issue(w.begin, rows_at(w, w.begin));
+  }
+  for (int it = gw; it < n_items; it += nw) {
+    const int64_t seg = w.seg;
+    // per-camera constants of the attention backward (edge_cam_bwd_kernel)
+    f32x4 xr[2], gv[2];
+    float M[2], inv[2], delta[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int f0 = 16 * q + 4 * g, h = 2 * q + (g >> 1);
+      const float4 x4 = *reinterpret_cast<const float4*>(XR + seg * ldXR + f0);
+      const float4 g4v = *reinterpret_cast<const float4*>(gout + seg * ldG + f0);
+      const float4 o4 = *reinterpret_cast<const float4*>(out + seg * ldOut + f0);
+      const float4 b4 = *reinterpret_cast<const float4*>(bias + f0);
+      xr[q] = f32x4{x4.x, x4.y, x4.z, x4.w};
+      gv[q] = f32x4{g4v.x, g4v.y, g4v.z, g4v.w};
+      float d = fmaf(g4v.x, o4.x - b4.x, fmaf(g4v.y, o4.y - b4.y, fmaf(g4v.z, o4.z - b4.z, g4v.w * (o4.w - b4.w))));
+      delta[q] = d + __shfl_xor(d, 16);
+      M[q] = seg_max[seg * ldStat + h];
+      inv[q] = 1.f / (seg_sum[seg * ldStat + h] + 1e-16f);
+    }
+    const bool first = it == 0 || items[it - 1].seg != w.seg;
+    if (first && c == 0) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) dbias[q] += gv[q];
+    }
+    f32x4 dxr[2] = {zero4(), zero4()};
+    gasfm_work_item wn{0, 0, 0, -1};
+    const bool more = it + nw < n_items;
+    if (more) wn = items[it + nw];
+    if (w.begin >= w.end && more && wn.begin < wn.end) issue(wn.begin, rows_at(wn, wn.begin));
+    for (int64_t row0 = w.begin; row0 < w.end; row0 += TR) {
+      const int nrows = rows_at(w, row0);
+      f32x4 PT[2] = {nPT[0], nPT[1]}, XT[2] = {nXT[0], nXT[1]}, RT[2];
+      if (RES) {
+        RT[0] = nRT[0];
+        RT[1] = nRT[1];
+      }
+      {  // the next tile (this item's, else the next item's first; the last one re-reads itself)
+        int64_t r1 = row0;
+        int n1 = nrows;
+        if (row0 + TR < w.end) {
+          r1 = row0 + TR;
+          n1 = rows_at(w, r1);
+        } else if (more && wn.begin < wn.end) {
+          r1 = wn.begin;
+          n1 = rows_at(wn, r1);
+        }
+        issue(r1, n1);
+      }
+      const bool valid = c < nrows;
+      // C layouts of P, dXLp, dRes (raw) through LDS, before P's slabs are normalised in place
+      f32x4 PC[2], XC[2], RC[2];
+      to_c(0, PT, PC);
+      to_c(1, XT, XC);
+      if (RES) to_c(2, RT, RC);
+      // ---- camera attention backward (T layout: edge c, features 16 q + 4 g + r)
+      if (LN) {
+        float gs[2][4], bs[2][4];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const f32x4 a = vecT(0, q), b = vecT(1, q);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            gs[q][r] = a[r];
+            bs[q][r] = b[r];
+          }
+        }
+        phat_slabs<LN>(PT, gs, bs, eps);
+      }
+      f32x4 xc[2] = {vecT(2, 0), vecT(2, 1)};  // b_c, then + Wc P_hat^T
+      xl_slabs<2>(reinterpret_cast<const float4*>(WcQ), PT, xc, lane);
+      f32x4 dXc[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const f32x4 at = vecT(3, q);
+        float z[4], lz[4], p = 0.f, da = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          z[r] = xc[q][r] + xr[q][r];
+          lz[r] = leaky(z[r], slope);
+          p = fmaf(lz[r], at[r], p);
+          da = fmaf(gv[q][r], xc[q][r], da);
+        }
+        p += __shfl_xor(p, 16);
+        da += __shfl_xor(da, 16);
+        const float alpha = valid ? __expf(p - M[q]) * inv[q] : 0.f;
+        const float de = alpha * (da - delta[q]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float dz = de * at[r] * (z[r] > 0.f ? 1.f : slope);
+          dXc[q][r] = fmaf(alpha, gv[q][r], dz);  // 0 for invalid edges
+          dxr[q][r] += dz;
+          datt[q][r] = fmaf(de, lz[r], datt[q][r]);
+        }
+      }
+      // ---- dP_hat (C layout) = dXLp Wpt + dXLc Wc (+ dRes scale Wp)
+      f32x4 dph[2] = {zero4(), zero4()};
+      prod_c2(reinterpret_cast<const float4*>(WptTQ), XT, dph, lane);
+      prod_c2(reinterpret_cast<const float4*>(WcTQ), dXc, dph, lane);
+      if (RES) prod_c2(reinterpret_cast<const float4*>(WqTQ), RT, dph, lane);
+      f32x4 XcC[2];
+      to_c(3, dXc, XcC);
+      // ---- LayerNorm statistics of the C-layout rows, LN backward, dP
+      f32x4 ph[2];  // relu(LN(P)) (C layout) for the weight gradient
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool live = 4 * g + r < nrows;
+        float mean = 0.f, rstd = 1.f;
+        if (LN) {
+          mean = sum16(PC[0][r] + PC[1][r]) * (1.f / F);
+          const float d0 = PC[0][r] - mean, d1 = PC[1][r] - mean;
+          rstd = rsqrtf(sum16(fmaf(d0, d0, d1 * d1)) * (1.f / F) + eps);
+        }
+        float xh[2], gvv[2], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          xh[nt] = LN ? (PC[nt][r] - mean) * rstd : PC[nt][r];
+          ph[nt][r] = LN ? fmaxf(fmaf(xh[nt], gC[nt], bC[nt]), 0.f) : xh[nt];
+          float dy = live ? dph[nt][r] : 0.f;
+          if (LN) {
+            dy = (fmaf(xh[nt], gC[nt], bC[nt]) > 0.f) ? dy : 0.f;
+            dg[nt] = fmaf(dy, xh[nt], dg[nt]);
+            dbt[nt] += dy;
+          }
+          gvv[nt] = LN ? dy * gC[nt] : dy;
+          s1 += gvv[nt];
+          s2 = fmaf(gvv[nt], xh[nt], s2);
+        }
+        if (LN) {
+          s1 = sum16(s1) * (1.f / F);
+          s2 = sum16(s2) * (1.f / F);
+        }
+        if (live) {
+          float* d = dP + (row0 + 4 * g + r) * F + c;
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            float v = LN ? rstd * (gvv[nt] - s1 - xh[nt] * s2) : gvv[nt];
+            if (RES) v += RC[nt][r];
+            d[16 * nt] = v;
+          }
+        }
+      }
+      // ---- dW += [dXLp | dXLc]^T relu(LN(P)), db (C layout, row 4 g + s at step s)
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) XC[ft][r] = 4 * g + r < nrows ? XC[ft][r] : 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const float a = mt < 2 ? XC[mt][s2] : XcC[mt - 2][s2];
+          db[mt] += a;
+          accW[mt][0] = mfma16(a, ph[0][s2], accW[mt][0]);
+          accW[mt][1] = mfma16(a, ph[1][s2], accW[mt][1]);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();  // this tile's transpose reads before the next tile's writes
+      asm volatile("" ::: "memory");
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = group_sum<16>(dxr[q][r]);
+      if (c == 0) {
+        float* d = (w.slot < 0) ? dXR + seg * ldDXR : part_dxr + int64_t(w.slot) * F;
+        *reinterpret_cast<float4*>(d + 16 * q + 4 * g) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+    w = wn;
+  }
+  // workgroup reduction: 32 accW + 4 db + 2 dg + 2 dbt (C layout) + 16 (datt, dbias summed over
+  // the 16 edge columns first)
+  constexpr int NV = 56;
+  float v[NV];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[(mt * 2 + nt) * 4 + r] = accW[mt][nt][r];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) v[32 + mt] = db[mt];
+  v[36] = dg[0];
+  v[37] = dg[1];
+  v[38] = dbt[0];
+  v[39] = dbt[1];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[40 + q * 4 + r] = group_sum<16>(datt[q][r]);
+      v[48 + q * 4 + r] = group_sum<16>(dbias[q][r]);
+    }
+  wg_reduce_ordered<NV, kWaves, NL>(v, lds, wave, lane);
+  if (wave == 0) {
+    float* o = part + int64_t(blockIdx.x) * PB2_PART;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[(mt * 16 + 4 * g + r) * F + nt * 16 + c] = v[(mt * 2 + nt) * 4 + r];
+    float tt[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) tt[k] = sum_groups(v[32 + k]);
+    if (g == 0) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) o[NX * F + mt * 16 + c] = tt[mt];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        o[NX * F + NX + nt * 16 + c] = tt[4 + nt];
+        o[NX * F + NX + F + nt * 16 + c] = tt[6 + nt];
+      }
+    }
+    if (c == 0) {
+      float* oa = o + PB2_PRO;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        *reinterpret_cast<float4*>(oa + 16 * q + 4 * g) =
+            make_float4(v[40 + q * 4], v[40 + q * 4 + 1], v[40 + q * 4 + 2], v[40 + q * 4 + 3]);
+        *reinterpret_cast<float4*>(oa + F + 16 * q + 4 * g) =
+            make_float4(v[48 + q * 4], v[48 + q * 4 + 1], v[48 + q * 4 + 2], v[48 + q * 4 + 3]);
+      }
+    }
+  }
+}
+
+int grid_cam_pbwd(int n_items) {
+  return resident_grid(reinterpret_cast<const void*>(&edge_cam_pbwd_kernel<true, true>), kThreads, 0, n_items,
+                       kWaves);
+}
+
 int grid_cam_bwd(int n_items) {
   return resident_grid(reinterpret_cast<const void*>(&edge_cam_bwd_kernel<true>), kThreads, 0, n_items, kWaves);
 }
@@ -627,4 +989,41 @@ extern "C" int gasfm_edge_cam_bwd(const float* P, const float* ln_w, const float
   else
     launch(&edge_cam_bwd_kernel<false>);
   return launch_status("gasfm_edge_cam_bwd");
+}
+
+extern "C" int32_t gasfm_edge_cam_pbwd_part_rows(int32_t n_items) { return grid_cam_pbwd(n_items > 0 ? n_items : 1); }
+extern "C" int32_t gasfm_edge_cam_pbwd_part_cols(void) { return PB2_PART; }
+
+extern "C" int gasfm_edge_cam_pbwd(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
+                                   const float* Wc, const float* bc, const float* Wp, int32_t ldWp, float scale,
+                                   const float* XR, int64_t ldXR, const float* att, const float* bias, float slope,
+                                   const float* out, int64_t ldOut, const float* seg_max, const float* seg_sum,
+                                   int64_t ldStat, const float* gout, int64_t ldG, const gasfm_work_item* items,
+                                   int32_t n_items, const float* dXLp, int64_t ldXp, const float* dRes, float* dP,
+                                   float* dXR, int64_t ldDXR, float* part_dxr, float* part, void* stream) {
+  GASFM_REQUIRE(n_items >= 0 && P && Wpt && Wc && bc && XR && att && bias && out && seg_max && seg_sum && gout &&
+                    items && dXLp && dP && dXR && part && (!dRes || (Wp && ldWp >= F)),
+                "gasfm_edge_cam_pbwd: null pointer");
+  GASFM_REQUIRE(ldXR % 4 == 0 && ldOut % 4 == 0 && ldG % 4 == 0 && ldXp % 4 == 0 && ldXp >= F && ldDXR % 4 == 0 &&
+                    aligned16(P) && aligned16(XR) && aligned16(out) && aligned16(gout) && aligned16(dXLp) &&
+                    aligned16(dP) && aligned16(dXR) && (!dRes || aligned16(dRes)) &&
+                    (!part_dxr || aligned16(part_dxr)) && (!ln_w || (aligned16(ln_w) && aligned16(ln_b))),
+                "gasfm_edge_cam_pbwd: 16-byte rows required");
+  if (n_items == 0) return GASFM_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int grid = grid_cam_pbwd(n_items);
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, st, P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, ldWp, scale, XR,
+                       ldXR, att, bias, slope, out, ldOut, seg_max, seg_sum, ldStat, gout, ldG, items, n_items, dXLp,
+                       ldXp, dRes, dP, dXR, ldDXR, part_dxr, part);
+  };
+  if (ln_w && dRes)
+    launch(&edge_cam_pbwd_kernel<true, true>);
+  else if (ln_w)
+    launch(&edge_cam_pbwd_kernel<true, false>);
+  else if (dRes)
+    launch(&edge_cam_pbwd_kernel<false, true>);
+  else
+    launch(&edge_cam_pbwd_kernel<false, false>);
+  return launch_status("gasfm_edge_cam_pbwd");
 }

@@ -19,6 +19,8 @@ view / global kernels (point_block.py, view_block.py, dense.py: csrc/point_block
 view_block.hip, global_vec.hip); only the camera side's two m x 1024 x 1024 GEMMs per block
 go through hipBLASLt (or the HIP MFMA GEMMs, view_block._mm).
 """
+import os
+
 import torch
 
 from . import _native
@@ -26,6 +28,9 @@ from .attention import (attn_backward_raw, attn_forward_partial, attn_forward_ra
                         combine_partials)
 
 PROJ_SCALE = 0.25  # the "/ 4" of layers.py:945
+# EdgeCamFn's backward as ONE kernel (gasfm_edge_cam_pbwd: camera attention backward + edge
+# prologue backward, dXLc never stored); 0 selects the two kernels edge_cam_bwd + edge_prologue_bwd
+CAM_PBWD = os.environ.get("GASFM_CAM_PBWD", "1") != "0"
 
 
 def _rows(t):
@@ -147,6 +152,8 @@ class EdgeCamFn(torch.autograd.Function):
         dXLp = torch.zeros((E, 32), dtype=torch.float32, device=dev) if dXLp is None else dXLp.contiguous()
         g_c = torch.zeros_like(out) if g_c is None else (g_c if g_c.stride(1) == 1 else g_c.contiguous())
         dRes = dtoken.contiguous() if (dtoken is not None and dtoken.stride(0) != 0) else None
+        if CAM_PBWD and plan.n_items:
+            return EdgeCamFn._backward_fused(ctx, dXLp, g_c, dRes)
         # camera attention backward (XLc recomputed from P): dXLc, dXR, [datt | dbias] partials
         dXLc = torch.empty((E, 32), dtype=torch.float32, device=dev)
         dXR = torch.empty((plan.num_targets, 32), dtype=torch.float32, device=dev)
@@ -173,6 +180,30 @@ class EdgeCamFn(torch.autograd.Function):
         dW, db = tot[:o].view(64, 32), tot[o:o + 64]
         dgam = tot[o + 64:o + 96] if ctx.has_ln else None
         dbet = tot[o + 96:o + 128] if ctx.has_ln else None
+        return (dP, dgam, dbet, dW[:32], db[:32], dW[32:], db[32:], None, None, None, dXR,
+                ta[:32].view(ctx.att_shape), ta[32:], None, None, None, None, None)
+
+    @staticmethod
+    def _backward_fused(ctx, dXLp, g_c, dRes):
+        """Camera attention backward + prologue backward in one kernel (gasfm_edge_cam_pbwd)."""
+        P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum = ctx.saved_tensors
+        plan = ctx.plan
+        dev = P.device
+        dXR = torch.empty((plan.num_targets, 32), dtype=torch.float32, device=dev)
+        part_dxr = torch.empty((plan.n_part_rows, 32), dtype=torch.float32, device=dev) if plan.n_slots else None
+        rows, cols = _native.edge_cam_pbwd_part_shape(plan.n_items)
+        part = torch.empty((rows, cols), dtype=torch.float32, device=dev)
+        dP = torch.empty_like(P)
+        _native.edge_cam_pbwd(P, ln_w, ln_b, ctx.eps, Wpt.contiguous(), Wc.contiguous(), bc.contiguous(),
+                              Wp.contiguous() if dRes is not None else None, PROJ_SCALE, XR, attf, bias, ctx.slope,
+                              out, smax, ssum, g_c, plan.items, plan.n_items, dXLp, dRes, dP, dXR, part_dxr, part)
+        bwd_combine(plan, part_dxr, 32, dXR)
+        tot = _native.param_colsum(part, ctx.defer)
+        o = 64 * 32
+        dW, db = tot[:o].view(64, 32), tot[o:o + 64]
+        dgam = tot[o + 64:o + 96] if ctx.has_ln else None
+        dbet = tot[o + 96:o + 128] if ctx.has_ln else None
+        ta = tot[o + 128:]
         return (dP, dgam, dbet, dW[:32], db[:32], dW[32:], db[32:], None, None, None, dXR,
                 ta[:32].view(ctx.att_shape), ta[32:], None, None, None, None, None)
 

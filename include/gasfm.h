@@ -147,6 +147,26 @@ int gasfm_edge_cam_bwd(const float* P, const float* ln_w, const float* ln_b, flo
                        int32_t n_items, float* dXLc, int64_t ldD, float* dXR, int64_t ldDXR, float* part_dxr,
                        float* part, void* stream);
 
+/* The camera attention's backward and the block's edge prologue backward in ONE pass over the
+ * camera plan's items (gasfm_edge_cam_bwd followed by gasfm_edge_prologue_bwd with dXLc, without
+ * storing dXLc): dP [E, 32], dXR per camera (split items: part_dxr rows for
+ * gasfm_gat_attn_bwd_combine), and per workgroup the partial row
+ * [dW 64x32 | db 64 | dgamma 32 | dbeta 32 | datt 32 | dbias 32]
+ * (part[gasfm_edge_cam_pbwd_part_rows(n_items), gasfm_edge_cam_pbwd_part_cols()]).
+ * dXLp: the point half of dXL in edge order (row stride ldXp); dRes / Wp (row stride ldWp) / scale:
+ * the block output's residual gradient and lin_proj, as in gasfm_edge_prologue_bwd (dRes may be null).
+ * Replaces (reference): the autograd of Proj2View's GATv2Conv and of the LayerNorm + lin_l on the
+ * projection features (layers.py:232-234, 329-335). */
+int32_t gasfm_edge_cam_pbwd_part_rows(int32_t n_items);
+int32_t gasfm_edge_cam_pbwd_part_cols(void);
+int gasfm_edge_cam_pbwd(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
+                        const float* Wc, const float* bc, const float* Wp, int32_t ldWp, float scale,
+                        const float* XR, int64_t ldXR, const float* att, const float* bias, float slope,
+                        const float* out, int64_t ldOut, const float* seg_max, const float* seg_sum,
+                        int64_t ldStat, const float* gout, int64_t ldG, const gasfm_work_item* items,
+                        int32_t n_items, const float* dXLp, int64_t ldXp, const float* dRes, float* dP,
+                        float* dXR, int64_t ldDXR, float* part_dxr, float* part, void* stream);
+
 /* ---- fused GATv2 edge-softmax + aggregation (device) ------------------- */
 
 /* Forward of PyG GATv2Conv's message/softmax/aggregate on pre-projected
