@@ -51,6 +51,9 @@ _SIGS = {
                                        _vp, _vp]),
     "gasfm_edge_cam_bwd_part_rows": (_i32, [_i32]),
     "gasfm_edge_cam_bwd_part_cols": (_i32, []),
+    "gasfm_edge_seam_fwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _f32, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _f32, _vp, _vp,
+                                   _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _i32,
+                                   _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
     "gasfm_edge_cam_pbwd_part_rows": (_i32, [_i32]),
     "gasfm_edge_cam_pbwd_part_cols": (_i32, []),
     "gasfm_edge_cam_pbwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _f32, _vp, _i64, _vp, _vp, _f32, _vp,
@@ -600,6 +603,23 @@ def edge_cam_bwd(P, ln_w, ln_b, eps, Wc, bc, XR, att, bias, slope, out, seg_max,
                                   gout.stride(0), _p(plan_items), n_items, _p(dXLc), dXLc.stride(0), _p(dXR),
                                   dXR.stride(0), _p(part_dxr), _p(part), _stream(P))
     check(st, "gasfm_edge_cam_bwd")
+
+
+def edge_seam_fwd(Pb, P0, pt, lnw_b, lnb_b, eps_b, Wp, bp, Sp, Sv, Sg, scale, Pout, ln_w, ln_b, eps, Wpt, bpt, Wc, bc,
+                  XLp, pos, XR, att, bias, slope, plan_items, n_items, finalize, out, seg_max, seg_sum, part,
+                  ldStat=4):
+    """Block b's edge epilogue (P' = Pout) + block b+1's prologue and camera attention forward in one
+    pass (csrc/edge_cam.hip edge_seam_fwd); outputs as edge_cam_fwd's plus Pout."""
+    _req(Pb, "Pb", 32)
+    ldXR = _rows32(XR, "XR")
+    ldSv = _rows32(Sv, "Sv")
+    st = lib().gasfm_edge_seam_fwd(_p(Pb), _p(P0), _p(pt), _p(lnw_b), _p(lnb_b), eps_b, _p(Wp), Wp.stride(0), _p(bp),
+                                   _p(Sp), _p(Sv), ldSv, _p(Sg), scale, _p(Pout), _p(ln_w), _p(ln_b), eps, _p(Wpt),
+                                   _p(bpt), _p(Wc), _p(bc), _p(XLp), XLp.stride(0), _p(pos), _p(XR), ldXR, _p(att),
+                                   _p(bias), slope, _p(plan_items), n_items, int(finalize), _p(out),
+                                   out.stride(0) if out is not None else 0, _p(seg_max), _p(seg_sum), ldStat, _p(part),
+                                   _stream(Pb))
+    check(st, "gasfm_edge_seam_fwd")
 
 
 def edge_cam_pbwd_part_shape(n_items):

@@ -84,6 +84,39 @@ class EdgePrologueFn(torch.autograd.Function):
         return dP, dgam, dbet, dW, db, None, None, None, None, None
 
 
+def _cam_attention_fwd(launch, bias, plan, heads, HC, plan_partial, shard, dev):
+    """Run a camera-item kernel (launch(items, n_items, finalize, out, smax, ssum, part)) and finish
+    the camera attention: split pieces combined (one GPU), or the rank's partial rows all-gathered
+    and merged in rank order (point-sharded).  Returns (out, seg_max, seg_sum)."""
+    N = plan.num_targets
+    LDP = HC + 2 * heads
+    if shard is None:
+        out = torch.empty((N, HC), dtype=torch.float32, device=dev)
+        smax = torch.empty((N, heads), dtype=torch.float32, device=dev)
+        ssum = torch.empty((N, heads), dtype=torch.float32, device=dev)
+        part = torch.empty((plan.n_part_rows, LDP), dtype=torch.float32, device=dev) if plan.n_slots else None
+        launch(plan.items, plan.n_items, True, out, smax, ssum, part)
+        combine_fwd_l1(plan, part, heads, HC // heads)
+        if plan.n_combine:
+            _native.attn_combine(plan.combine, plan.n_combine, heads, HC // heads, part, bias, True, out, smax, ssum)
+        return out, smax, ssum
+    # local partial rows (attention.attn_forward_partial) -> all-gather -> ordered combine
+    pp = plan_partial
+    part = torch.empty((max(pp.n_part_rows, N), LDP), dtype=torch.float32, device=dev)
+    if pp.n_items:
+        launch(pp.items, pp.n_items, False, None, None, None, part)
+        combine_fwd_l1(pp, part, heads, HC // heads)
+        if pp.n_combine:
+            _native.attn_combine(pp.combine, pp.n_combine, heads, HC // heads, part, None, False, part,
+                                 part[:, HC:], part[:, HC + heads:], ldOut=LDP, ldStat=LDP)
+    else:
+        part[:N, :HC] = 0.0
+        part[:N, HC:HC + heads] = -float("inf")
+        part[:N, HC + heads:] = 0.0
+    gathered = shard.all_gather(part[:N])
+    return combine_partials(gathered, shard.world, N, heads, bias, shard.combine_items(N, dev))
+
+
 class EdgeCamFn(torch.autograd.Function):
     """EdgePrologueFn + the camera half of DualAttentionFn in one pass (csrc/edge_cam.hip):
 
@@ -106,35 +139,11 @@ class EdgeCamFn(torch.autograd.Function):
             raise ValueError("EdgeCamFn: the fused kernels are for H = 4, C = 8")
         attf = att.reshape(-1).contiguous()
         XLp = torch.empty((E, 32), dtype=torch.float32, device=dev)
-        N = plan.num_targets
-        LDP = HC + 2 * heads
-        if shard is None:
-            out = torch.empty((N, HC), dtype=torch.float32, device=dev)
-            smax = torch.empty((N, heads), dtype=torch.float32, device=dev)
-            ssum = torch.empty((N, heads), dtype=torch.float32, device=dev)
-            part = torch.empty((plan.n_part_rows, LDP), dtype=torch.float32, device=dev) if plan.n_slots else None
-            _native.edge_cam_fwd(P, ln_w, ln_b, eps, Wpt, bpt, Wc, bc, XLp, pos, XR, attf, bias, slope, plan.items,
-                                 plan.n_items, True, out, smax, ssum, part)
-            combine_fwd_l1(plan, part, heads, HC // heads)
-            if plan.n_combine:
-                _native.attn_combine(plan.combine, plan.n_combine, heads, HC // heads, part, bias, True, out, smax,
-                                     ssum)
-        else:  # local partial rows (attention.attn_forward_partial) -> all-gather -> ordered combine
-            pp = plan_partial
-            part = torch.empty((max(pp.n_part_rows, N), LDP), dtype=torch.float32, device=dev)
-            if pp.n_items:
-                _native.edge_cam_fwd(P, ln_w, ln_b, eps, Wpt, bpt, Wc, bc, XLp, pos, XR, attf, None, slope, pp.items,
-                                     pp.n_items, False, None, None, None, part)
-                combine_fwd_l1(pp, part, heads, HC // heads)
-                if pp.n_combine:
-                    _native.attn_combine(pp.combine, pp.n_combine, heads, HC // heads, part, None, False, part,
-                                         part[:, HC:], part[:, HC + heads:], ldOut=LDP, ldStat=LDP)
-            else:
-                part[:N, :HC] = 0.0
-                part[:N, HC:HC + heads] = -float("inf")
-                part[:N, HC + heads:] = 0.0
-            gathered = shard.all_gather(part[:N])
-            out, smax, ssum = combine_partials(gathered, shard.world, N, heads, bias, shard.combine_items(N, dev))
+
+        def launch(items, n_items, finalize, out, smax, ssum, part):
+            _native.edge_cam_fwd(P, ln_w, ln_b, eps, Wpt, bpt, Wc, bc, XLp, pos, XR, attf, bias if finalize else None,
+                                 slope, items, n_items, finalize, out, smax, ssum, part)
+        out, smax, ssum = _cam_attention_fwd(launch, bias, plan, heads, HC, plan_partial, shard, dev)
         ctx.eps, ctx.heads, ctx.slope, ctx.plan = eps, heads, slope, plan
         ctx.att_shape = att.shape
         ctx.has_ln = ln_w is not None
@@ -146,14 +155,33 @@ class EdgeCamFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dXLp, g_c, dtoken):
-        P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum = ctx.saved_tensors
-        plan = ctx.plan
-        E, dev = P.shape[0], P.device
-        dXLp = torch.zeros((E, 32), dtype=torch.float32, device=dev) if dXLp is None else dXLp.contiguous()
-        g_c = torch.zeros_like(out) if g_c is None else (g_c if g_c.stride(1) == 1 else g_c.contiguous())
         dRes = dtoken.contiguous() if (dtoken is not None and dtoken.stride(0) != 0) else None
-        if CAM_PBWD and plan.n_items:
-            return EdgeCamFn._backward_fused(ctx, dXLp, g_c, dRes)
+        return _cam_backward(ctx, ctx.saved_tensors, dXLp, g_c, dRes)
+
+
+def _cam_backward(ctx, saved, dXLp, g_c, dRes):
+    """EdgeCamFn's backward from its saved state (ctx attributes eps, heads, slope, plan, att_shape,
+    has_ln, defer): the 18 input gradients of EdgeCamFn.forward."""
+    P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum = saved
+    plan = ctx.plan
+    E, dev = P.shape[0], P.device
+    dXLp = torch.zeros((E, 32), dtype=torch.float32, device=dev) if dXLp is None else dXLp.contiguous()
+    g_c = torch.zeros_like(out) if g_c is None else (g_c if g_c.stride(1) == 1 else g_c.contiguous())
+    if CAM_PBWD and plan.n_items:
+        # camera attention backward + prologue backward in one kernel (gasfm_edge_cam_pbwd)
+        dXR = torch.empty((plan.num_targets, 32), dtype=torch.float32, device=dev)
+        part_dxr = torch.empty((plan.n_part_rows, 32), dtype=torch.float32, device=dev) if plan.n_slots else None
+        rows, cols = _native.edge_cam_pbwd_part_shape(plan.n_items)
+        part = torch.empty((rows, cols), dtype=torch.float32, device=dev)
+        dP = torch.empty_like(P)
+        _native.edge_cam_pbwd(P, ln_w, ln_b, ctx.eps, Wpt.contiguous(), Wc.contiguous(), bc.contiguous(),
+                              Wp.contiguous() if dRes is not None else None, PROJ_SCALE, XR, attf, bias, ctx.slope,
+                              out, smax, ssum, g_c, plan.items, plan.n_items, dXLp, dRes, dP, dXR, part_dxr, part)
+        bwd_combine(plan, part_dxr, 32, dXR)
+        tot = _native.param_colsum(part, ctx.defer)
+        o = 64 * 32
+        ta = tot[o + 128:]
+    else:
         # camera attention backward (XLc recomputed from P): dXLc, dXR, [datt | dbias] partials
         dXLc = torch.empty((E, 32), dtype=torch.float32, device=dev)
         dXR = torch.empty((plan.num_targets, 32), dtype=torch.float32, device=dev)
@@ -161,8 +189,8 @@ class EdgeCamFn(torch.autograd.Function):
         rows, cols = _native.edge_cam_bwd_part_shape(plan.n_items)
         part_a = (torch.empty if plan.n_items else torch.zeros)((rows, cols), dtype=torch.float32, device=dev)
         if plan.n_items:
-            _native.edge_cam_bwd(P, ln_w, ln_b, ctx.eps, Wc.contiguous(), bc.contiguous(), XR, attf, bias, ctx.slope, out,
-                                 smax, ssum, g_c, plan.items, plan.n_items, dXLc, dXR, part_dxr, part_a)
+            _native.edge_cam_bwd(P, ln_w, ln_b, ctx.eps, Wc.contiguous(), bc.contiguous(), XR, attf, bias, ctx.slope,
+                                 out, smax, ssum, g_c, plan.items, plan.n_items, dXLc, dXR, part_dxr, part_a)
             bwd_combine(plan, part_dxr, 32, dXR)
         else:  # no local edges
             dXLc.zero_()
@@ -177,35 +205,11 @@ class EdgeCamFn(torch.autograd.Function):
         ta = _native.param_colsum(part_a, ctx.defer)
         tot = _native.param_colsum(part, ctx.defer)
         o = 64 * 32
-        dW, db = tot[:o].view(64, 32), tot[o:o + 64]
-        dgam = tot[o + 64:o + 96] if ctx.has_ln else None
-        dbet = tot[o + 96:o + 128] if ctx.has_ln else None
-        return (dP, dgam, dbet, dW[:32], db[:32], dW[32:], db[32:], None, None, None, dXR,
-                ta[:32].view(ctx.att_shape), ta[32:], None, None, None, None, None)
-
-    @staticmethod
-    def _backward_fused(ctx, dXLp, g_c, dRes):
-        """Camera attention backward + prologue backward in one kernel (gasfm_edge_cam_pbwd)."""
-        P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum = ctx.saved_tensors
-        plan = ctx.plan
-        dev = P.device
-        dXR = torch.empty((plan.num_targets, 32), dtype=torch.float32, device=dev)
-        part_dxr = torch.empty((plan.n_part_rows, 32), dtype=torch.float32, device=dev) if plan.n_slots else None
-        rows, cols = _native.edge_cam_pbwd_part_shape(plan.n_items)
-        part = torch.empty((rows, cols), dtype=torch.float32, device=dev)
-        dP = torch.empty_like(P)
-        _native.edge_cam_pbwd(P, ln_w, ln_b, ctx.eps, Wpt.contiguous(), Wc.contiguous(), bc.contiguous(),
-                              Wp.contiguous() if dRes is not None else None, PROJ_SCALE, XR, attf, bias, ctx.slope,
-                              out, smax, ssum, g_c, plan.items, plan.n_items, dXLp, dRes, dP, dXR, part_dxr, part)
-        bwd_combine(plan, part_dxr, 32, dXR)
-        tot = _native.param_colsum(part, ctx.defer)
-        o = 64 * 32
-        dW, db = tot[:o].view(64, 32), tot[o:o + 64]
-        dgam = tot[o + 64:o + 96] if ctx.has_ln else None
-        dbet = tot[o + 96:o + 128] if ctx.has_ln else None
-        ta = tot[o + 128:]
-        return (dP, dgam, dbet, dW[:32], db[:32], dW[32:], db[32:], None, None, None, dXR,
-                ta[:32].view(ctx.att_shape), ta[32:], None, None, None, None, None)
+    dW, db = tot[:o].view(64, 32), tot[o:o + 64]
+    dgam = tot[o + 64:o + 96] if ctx.has_ln else None
+    dbet = tot[o + 96:o + 128] if ctx.has_ln else None
+    return (dP, dgam, dbet, dW[:32], db[:32], dW[32:], db[32:], None, None, None, dXR,
+            ta[:32].view(ctx.att_shape), ta[32:], None, None, None, None, None)
 
 
 class DualAttentionFn(torch.autograd.Function):
@@ -273,29 +277,112 @@ class EdgeEpilogueFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dPo):
-        P, P0, Wp, ln_w, ln_b = ctx.saved_tensors
-        edges = ctx.edges
-        dPo = dPo.contiguous()
-        dev = P.device
-        pc = edges.plans["proj2view"]
-        pp = edges.plans["proj2scenepoint"]
-        # camera side: dSv (+ dWp, dP0) in one pass over the camera work items
-        dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
-        part_dsv = torch.empty((max(pc.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
-        dP0 = torch.empty((P.shape[0], 2), dtype=torch.float32, device=dev) if P0 is not None else None
-        wg = _native.edge_part_floats(1, P.shape[0], pc.n_items) // (32 * 34)
-        part_w = torch.empty((wg, 32 * Wp.shape[1]), dtype=torch.float32, device=dev)
-        _native.edge_epilogue_bwd(pc.items, pc.n_items, dPo, P, P0, ln_w, ln_b, ctx.eps, Wp, PROJ_SCALE, dSv,
-                                  part_dsv, dP0, part_w)
-        bwd_combine(pc, part_dsv, 32, dSv)
-        dWp = _native.param_colsum(part_w, ctx.defer).view(32, Wp.shape[1])
-        dSg = _native.colsum(dSv)          # == d bias_proj: every edge belongs to one camera
-        # point side: dSp = per-point sum of dP'/4 through the point permutation
-        dSp = torch.empty((edges.n, 32), dtype=torch.float32, device=dev)
-        part_dsp = torch.empty((max(pp.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
-        _native.segment_rowsum(pp.items, pp.n_items, pp.perm, dPo, PROJ_SCALE, dSp, part_dsp)
-        bwd_combine(pp, part_dsp, 32, dSp)
-        return (None, dP0, dPo, dSp, dSv, dSg.view(ctx.sg_shape), dWp, dSg.clone(), None, None, None, None)
+        return _epilogue_backward(ctx, ctx.saved_tensors, dPo)
+
+
+def _epilogue_backward(ctx, saved, dPo):
+    """EdgeEpilogueFn's backward from its saved state (ctx attributes eps, edges, sg_shape, defer):
+    the 12 input gradients of EdgeEpilogueFn.forward (the block input's through the token)."""
+    P, P0, Wp, ln_w, ln_b = saved
+    edges = ctx.edges
+    dPo = dPo.contiguous()
+    dev = P.device
+    pc = edges.plans["proj2view"]
+    pp = edges.plans["proj2scenepoint"]
+    # camera side: dSv (+ dWp, dP0) in one pass over the camera work items
+    dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
+    part_dsv = torch.empty((max(pc.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
+    dP0 = torch.empty((P.shape[0], 2), dtype=torch.float32, device=dev) if P0 is not None else None
+    wg = _native.edge_part_floats(1, P.shape[0], pc.n_items) // (32 * 34)
+    part_w = torch.empty((wg, 32 * Wp.shape[1]), dtype=torch.float32, device=dev)
+    _native.edge_epilogue_bwd(pc.items, pc.n_items, dPo, P, P0, ln_w, ln_b, ctx.eps, Wp, PROJ_SCALE, dSv,
+                              part_dsv, dP0, part_w)
+    bwd_combine(pc, part_dsv, 32, dSv)
+    dWp = _native.param_colsum(part_w, ctx.defer).view(32, Wp.shape[1])
+    dSg = _native.colsum(dSv)          # == d bias_proj: every edge belongs to one camera
+    # point side: dSp = per-point sum of dP'/4 through the point permutation
+    dSp = torch.empty((edges.n, 32), dtype=torch.float32, device=dev)
+    part_dsp = torch.empty((max(pp.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
+    _native.segment_rowsum(pp.items, pp.n_items, pp.perm, dPo, PROJ_SCALE, dSp, part_dsp)
+    bwd_combine(pp, part_dsp, 32, dSp)
+    return (None, dP0, dPo, dSp, dSv, dSg.view(ctx.sg_shape), dWp, dSg.clone(), None, None, None, None)
+
+
+class SeamFn(torch.autograd.Function):
+    """Block b's EdgeEpilogueFn and block b+1's EdgeCamFn as ONE forward kernel
+    (gasfm_edge_seam_fwd: P' is written once and never read back); the backward is the two
+    Functions' own backwards in autograd's order (EdgeCamFn's, then EdgeEpilogueFn's on the
+    resulting dP').
+
+    Inputs: the 12 of EdgeEpilogueFn.forward, then the 18 of EdgeCamFn.forward (whose P is this
+    Function's own output P').  Outputs: (P', XLp, camera aggregates, token)."""
+
+    @staticmethod
+    def forward(ctx, P, P0, token, Sp, Sv, Sg, Wp, bp, lnw_b, lnb_b, eps_b, edges,
+                ln_w, ln_b, Wpt, bpt, Wc, bc, Wp_n, eps, pos, XR, att, bias, plan, heads, slope, plan_partial, shard):
+        E, dev = P.shape[0], P.device
+        HC = att.numel()
+        if heads != 4 or HC != 32:
+            raise ValueError("SeamFn: the fused kernels are for H = 4, C = 8")
+        attf = att.reshape(-1).contiguous()
+        XLp = torch.empty((E, 32), dtype=torch.float32, device=dev)
+        Pn = torch.empty_like(P)
+        Wp_c, Sp_c, Sv_r, Sg_f = Wp.contiguous(), Sp.contiguous(), _rows(Sv), Sg.reshape(-1).contiguous()
+        bp_c = bp.contiguous()
+
+        def launch(items, n_items, finalize, out, smax, ssum, part):
+            _native.edge_seam_fwd(P, P0, edges.pt, lnw_b, lnb_b, eps_b, Wp_c, bp_c, Sp_c, Sv_r, Sg_f, PROJ_SCALE, Pn,
+                                  ln_w, ln_b, eps, Wpt, bpt, Wc, bc, XLp, pos, XR, attf, bias if finalize else None,
+                                  slope, items, n_items, finalize, out, smax, ssum, part)
+        out, smax, ssum = _cam_attention_fwd(launch, bias, plan, heads, HC, plan_partial, shard, dev)
+        # EdgeEpilogueFn's state
+        ctx.e_eps, ctx.edges, ctx.sg_shape = eps_b, edges, Sg.shape
+        ctx.e_defer = _native.defer_token(Wp)
+        # EdgeCamFn's state
+        ctx.eps, ctx.heads, ctx.slope, ctx.plan = eps, heads, slope, plan
+        ctx.att_shape = att.shape
+        ctx.has_ln = ln_w is not None
+        ctx.defer = _native.defer_token(ln_w, ln_b, Wpt, bpt, Wc, bc, att, bias)
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(P, P0, Wp_c, lnw_b, lnb_b, Pn, ln_w, ln_b, Wpt, Wc, bc, Wp_n, XR, attf, bias, out, smax,
+                              ssum)
+        ctx.n_epi = 5
+        token_n = P.new_empty((1, 1)).expand(E, P.shape[1])
+        return Pn, XLp, out, token_n
+
+    @staticmethod
+    def backward(ctx, gPn, dXLp, g_c, dtoken):
+        saved = ctx.saved_tensors
+        epi, cam = saved[:ctx.n_epi], saved[ctx.n_epi:]
+        dRes = dtoken.contiguous() if (dtoken is not None and dtoken.stride(0) != 0) else None
+        gc = _cam_backward(ctx, cam, dXLp, g_c, dRes)
+        dPn = gc[0] if gPn is None else gc[0] + gPn
+        ectx = _EpiState(ctx.e_eps, ctx.edges, ctx.sg_shape, ctx.e_defer)
+        ge = _epilogue_backward(ectx, epi, dPn)
+        return ge + gc[1:] + (None,) * 0
+
+
+class _EpiState:
+    def __init__(self, eps, edges, sg_shape, defer):
+        self.eps, self.edges, self.sg_shape, self.defer = eps, edges, sg_shape, defer
+
+
+class PendingEpilogue:
+    """Block b's EdgeEpilogueFn.apply arguments, held so that block b+1 can run it together with
+    its own prologue (SeamFn); materialize() runs it alone (any other consumer of P')."""
+
+    def __init__(self, args):
+        self.args = args
+        self._P = None
+
+    def materialize(self):
+        if self._P is None:
+            self._P = EdgeEpilogueFn.apply(*self.args)
+        return self._P
+
+
+def materialize(P):
+    return P.materialize() if isinstance(P, PendingEpilogue) else P
 
 
 class Block0PrologueFn(torch.autograd.Function):

@@ -29,13 +29,16 @@ from torch.nn import Identity, LayerNorm, Linear, Module, ModuleList, ReLU, Sequ
 from . import _native, dense, edge_ops, point_block, streams, view_block
 from .attention import AttnPlan, GatAttentionFn, gat_attention
 from .edge_block import (Block0EpilogueFn, Block0PrologueFn, DualAttentionFn, EdgeCamFn, EdgeEpilogueFn,
-                         EdgePrologueFn)
+                         EdgePrologueFn, PendingEpilogue, SeamFn, materialize)
 from .gatv2 import GATv2Conv
 
 
 # Edge prologue with the camera attention fused in (edge_block.EdgeCamFn, csrc/edge_cam.hip) for the
 # 32-wide blocks; GASFM_EDGE_CAM=0 selects the separate prologue + DualAttentionFn kernels (A/B).
 EDGE_CAM = os.environ.get("GASFM_EDGE_CAM", "1") != "0"
+# A 32-wide block's edge epilogue is left pending (edge_block.PendingEpilogue) and run in one kernel
+# with the next block's prologue + camera attention (SeamFn, gasfm_edge_seam_fwd); 0: separately.
+EDGE_SEAM = os.environ.get("GASFM_EDGE_SEAM", "1") != "0"
 
 
 def replicated_to_local(x, shard):
@@ -283,6 +286,15 @@ def _target_row(conv, x_tgt, ref, n=1):
     return dense.linear(x_tgt, conv.lin_r)
 
 
+def _seam_ok(args):
+    """The epilogue's shapes are the seam kernel's: P [E, 32] with P0 [E, 2] or none, lin_proj
+    [32, 32 (+2)], a LayerNorm, the one-row (or folded) global term."""
+    P, P0, _, sp, sv, sg, W, b, ln_w, ln_b = args[:10]
+    return (P.is_cuda and P.dtype == torch.float32 and P.dim() == 2 and P.shape[1] == 32 and ln_w is not None
+            and tuple(W.shape) == ((32, 34) if P0 is not None else (32, 32)) and sg.numel() == 32
+            and sp.shape[1] == 32 and sv.shape[1] == 32)
+
+
 def _fold_global(sv, sg, plans):
     """SceneBatch (batch.py): the per-edge global term of scene s, Sg[s], added to the per-camera
     term of its cameras (every camera belongs to one scene), so the edge kernels see one scene:
@@ -479,9 +491,15 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         pos = pp.pos
 
         def attend(XRp, XRc, sec):
-            XLp, agg_c, token = EdgeCamFn.apply(P, ln_w, ln_b, W, b, W2, b2, Wp, eps, pos, XRc, cc.att, cc.bias, pc,
-                                                cc.heads, cc.negative_slope,
-                                                plans.get("_partial", {}).get("proj2view"), plans.get("_shard"))
+            cam_args = (ln_w, ln_b, W, b, W2, b2, Wp, eps, pos, XRc, cc.att, cc.bias, pc, cc.heads, cc.negative_slope,
+                        plans.get("_partial", {}).get("proj2view"), plans.get("_shard"))
+            if isinstance(P, PendingEpilogue):  # the previous block's epilogue in the same kernel
+                Pn, XLp, agg_c, token = SeamFn.apply(*P.args, *cam_args)
+                P._P = Pn
+                holder["P"] = Pn
+            else:
+                XLp, agg_c, token = EdgeCamFn.apply(P, *cam_args)
+                holder["P"] = P
             holder["token"] = token
             agg_p = GatAttentionFn.apply(XLp, XRp, cp.att, cp.bias, pp, cp.heads, cp.negative_slope, pos is not None,
                                          sec)[0]
@@ -625,7 +643,9 @@ class GraphAttnSfMLayer(Module):
         return P_new, pts, view, glob
 
     def forward_fused(self, P, plans, edges, prev_pt, prev_view, prev_glob, P0, carry=None, nxt=None):
-        """Blocks >= 1 with the fused HIP edge kernels (see gasfm_amd/edge_block.py)."""
+        """Blocks >= 1 with the fused HIP edge kernels (see gasfm_amd/edge_block.py).  P may be the
+        previous block's PendingEpilogue; with EDGE_SEAM this block's own epilogue is returned
+        pending as well (the caller's next consumer runs or materializes it)."""
         ln = self.prev_projfeat_norm_layer
         gfu = self.global_feature_update
         pfu = self.projection_feature_update
@@ -636,7 +656,9 @@ class GraphAttnSfMLayer(Module):
             pts, view, glob = gfu.forward_fused(None, plans, prev_pt, prev_view, prev_glob, carry=carry, pfu=pfu,
                                                 nxt=nxt, attend=attend)
             token = holder["token"]
+            P = holder["P"]
         else:
+            P = materialize(P)
             (W, b), (W2, b2) = gfu.lin_l_pair()
             XL, token = EdgePrologueFn.apply(P, ln.weight, ln.bias, W, b, pfu.lin_proj.weight, ln.eps, pos, W2, b2)
             pts, view, glob = gfu.forward_fused(XL, plans, prev_pt, prev_view, prev_glob, xl_sorted=pos is not None,
@@ -646,15 +668,21 @@ class GraphAttnSfMLayer(Module):
                                                          if carry is not None else (None, None, None)))
         sv, sg = _wrap_boundary(plans.get("_shard"), sv, sg, carry)
         sv, sg = _fold_global(sv, sg, plans)
-        P_new = EdgeEpilogueFn.apply(P, P0 if self.add_skipconn_from_init_projfeat else None, token, sp, sv, sg,
-                                     pfu.lin_proj.weight, pfu.lin_proj.bias, ln.weight, ln.bias, ln.eps, edges)
-        return P_new, pts, view, glob
+        args = (P, P0 if self.add_skipconn_from_init_projfeat else None, token, sp, sv, sg, pfu.lin_proj.weight,
+                pfu.lin_proj.bias, ln.weight, ln.bias, ln.eps, edges)
+        if EDGE_SEAM and _seam_ok(args):
+            return PendingEpilogue(args), pts, view, glob
+        return EdgeEpilogueFn.apply(*args), pts, view, glob
 
     def forward_plan(self, P, plans, edges, prev_pt=None, prev_view=None, prev_glob=None, P0=None, carry=None,
                      nxt=None):
         """P [E, F_in] edge features (cam-major) -> (P' [E, F_out], pts, view, glob).
 
-        carry / nxt: see GraphAttnSfMGlobalFeatureUpdate.forward_fused (fused CUDA path only)."""
+        carry / nxt: see GraphAttnSfMGlobalFeatureUpdate.forward_fused (fused CUDA path only).  On
+        the fused path P and P' may be PendingEpilogue handles (edge_block.SeamFn)."""
+        if isinstance(P, PendingEpilogue) and self.fusable():
+            return self.forward_fused(P, plans, edges, prev_pt, prev_view, prev_glob, P0, carry, nxt)
+        P = materialize(P)
         if P.is_cuda and self.fusable():
             return self.forward_fused(P, plans, edges, prev_pt, prev_view, prev_glob, P0, carry, nxt)
         if P.is_cuda and prev_pt is None and prev_view is None and prev_glob is None and self.fusable0():
@@ -930,19 +958,24 @@ class GraphAttnSfMNet(Module):
                                                   glob if sf else None, P0=p0s[i], carry=carry, nxt=nxt)
         if heads:
             args = (pts if sf else None, view if sf else None, glob if sf else None)
-            if P.is_cuda and P.shape[1] == 32 and fgu.fusable():
-                # raw (un-normalised) projection features (graph_attn_sfm.py:141-148): no LN prologue
-                pos = plans["proj2scenepoint"].pos
-                if fgu.cam_fusable(plans):
-                    attend = fgu.edge_cam_attend(P.contiguous(), None, None, 1e-5, None, plans, {})
-                    pts, view, _ = fgu.forward_fused(None, plans, *args, carry=carry, attend=attend)
-                else:
+            pend = isinstance(P, PendingEpilogue)
+            if (pend or P.is_cuda) and fgu.fusable() and fgu.cam_fusable(plans) and (pend or P.shape[1] == 32):
+                # raw (un-normalised) projection features (graph_attn_sfm.py:141-148): no LN prologue;
+                # a pending last-block epilogue runs in the same kernel (SeamFn)
+                holder = {}
+                attend = fgu.edge_cam_attend(P if pend else P.contiguous(), None, None, 1e-5, None, plans, holder)
+                pts, view, _ = fgu.forward_fused(None, plans, *args, carry=carry, attend=attend)
+                P = holder["P"]
+            else:
+                P = materialize(P)
+                if P.is_cuda and P.shape[1] == 32 and fgu.fusable():
+                    pos = plans["proj2scenepoint"].pos
                     (W, b), (W2, b2) = fgu.lin_l_pair()
                     XL, _ = EdgePrologueFn.apply(P.contiguous(), None, None, W, b, None, 1e-5, pos, W2, b2)
                     pts, view, _ = fgu.forward_fused(XL, plans, *args, xl_sorted=pos is not None, carry=carry)
-            else:
-                pts, view, _ = fgu.forward_plan(P, plans, *args)
-        return P, pts, view
+                else:
+                    pts, view, _ = fgu.forward_plan(P, plans, *args)
+        return materialize(P), pts, view
 
     # Weight-gradient column sums of the backward pass run as one batched launch at its end
     # (_native.param_colsum) when every parameter's .grad is unset at forward time (the usual

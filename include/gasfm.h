@@ -147,6 +147,23 @@ int gasfm_edge_cam_bwd(const float* P, const float* ln_w, const float* ln_b, flo
                        int32_t n_items, float* dXLc, int64_t ldD, float* dXR, int64_t ldDXR, float* part_dxr,
                        float* part, void* stream);
 
+/* Block b's edge epilogue and block b+1's edge prologue + camera-direction attention forward in ONE
+ * pass over block b+1's camera plan items (gasfm_edge_epilogue_fwd of block b followed by
+ * gasfm_edge_cam_fwd of block b+1 on its output, without reading that output back):
+ *   Pout = Pb + scale (Wp [relu(LN_b(Pb)) | P0] + bp + Sp[pt] + Sv[cam] + Sg)   (stored)
+ * and every output of gasfm_edge_cam_fwd for P = Pout (ln_w / ln_b: block b+1's LayerNorm, null =
+ * none).  Replaces (reference): GraphAttnSfMProjectionFeatureUpdate + the residual of block b
+ * (layers.py:911-956, 254-261) and block b+1's LayerNorm, lin_l and Proj2View GATv2Conv forward
+ * (layers.py:232-234, 329-335). */
+int gasfm_edge_seam_fwd(const float* Pb, const float* P0, const int32_t* pt, const float* ln_wb, const float* ln_bb,
+                        float eps_b, const float* Wp, int32_t ldWp, const float* bp, const float* Sp, const float* Sv,
+                        int64_t ldSv, const float* Sg, float scale, float* Pout, const float* ln_w,
+                        const float* ln_b, float eps, const float* Wpt, const float* bpt, const float* Wc,
+                        const float* bc, float* XLp, int64_t ldXLp, const int32_t* pos, const float* XR,
+                        int64_t ldXR, const float* att, const float* bias, float slope,
+                        const gasfm_work_item* items, int32_t n_items, int32_t finalize, float* out, int64_t ldOut,
+                        float* seg_max, float* seg_sum, int64_t ldStat, float* part, void* stream);
+
 /* The camera attention's backward and the block's edge prologue backward in ONE pass over the
  * camera plan's items (gasfm_edge_cam_bwd followed by gasfm_edge_prologue_bwd with dXLc, without
  * storing dXLc): dP [E, 32], dXR per camera (split items: part_dxr rows for

@@ -85,6 +85,13 @@ def main():
                                      W[32:].contiguous(), b[32:].contiguous(), XLp, pp.pos, XRc, att, bias, 0.2,
                                      pc.items, pc.n_items, True, co, cmax, csum, cpart),
         E * (128 + 128 + 4) + m * 128)
+    Pn = torch.empty_like(P)
+    run("edge_seam_fwd(epilogue + cam)",
+        lambda: _native.edge_seam_fwd(P, P0, pt, ln_w, ln_b, 1e-5, Wp, bp, Sp, Sv, Sg, 0.25, Pn, ln_w, ln_b, 1e-5,
+                                      W[:32].contiguous(), b[:32].contiguous(), W[32:].contiguous(),
+                                      b[32:].contiguous(), XLp, pp.pos, XRc, att, bias, 0.2, pc.items, pc.n_items,
+                                      True, co, cmax, csum, cpart),
+        E * (128 + 8 + 4 + 128 + 128 + 128 + 4) + (n + m) * 128)
     dXLc, dXRc = torch.empty(E, 32, device=dev), torch.empty(m, 32, device=dev)
     pdxr = torch.empty(max(pc.n_part_rows, 1), 32, device=dev)
     r_, c_ = _native.edge_cam_bwd_part_shape(pc.n_items)

@@ -58,6 +58,9 @@ def main():
                     help="outlier injection rate (config 5: rhaug-15-20 + 0.1 outliers), 0 = off")
     ap.add_argument("--per-scene", action="store_true",
                     help="also time one forward per scene (train.py's loop) beside the batched union forward")
+    ap.add_argument("--capture-floor", action="store_true",
+                    help="also time one FIXED batch's forward + loss + backward captured as a hipGraph and "
+                         "replayed (the GPU-side floor of the union step, without the host's launch cost)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     np.random.seed(0)
@@ -137,6 +140,43 @@ def main():
     print(json.dumps({"mode": "device data path (sample + rhaug" + tag + " + graph build on GPU), batch as one union forward",
                       "batch": args.batch, "scene": f"m={args.views} n={args.points}, 10-20 sampled views", **res}),
           flush=True)
+    if args.capture_floor:
+        from gasfm_amd.batch import SceneBatch
+        from gasfm_amd.graph_step import CapturedStep
+        batch = [scenes[int(i)] for i in np.random.choice(len(scenes), args.batch, replace=False)]
+        datas = [prep_device(s) for s in batch]
+        union = SceneBatch(datas)
+
+        def fwd_bwd():
+            preds = union.split(net(union))
+            loss = sum(lossf(p, d) for p, d in zip(preds, datas))
+            loss.backward()
+            return loss
+
+        step = CapturedStep(fwd_bwd, net.parameters())
+        E = int(union.x.indices.shape[1])
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(20):
+            step()
+        torch.cuda.synchronize()
+        t_rep = (time.perf_counter() - t0) / 20
+        for _ in range(2):
+            opt.zero_grad()
+            fwd_bwd()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            opt.zero_grad()
+            fwd_bwd()
+        torch.cuda.synchronize()
+        t_eager = (time.perf_counter() - t0) / 5
+        print(json.dumps({"mode": "one fixed union batch: forward + ESFMLoss + backward, hipGraph replay vs eager",
+                          "batch": args.batch, "edges": E, "captured": step.captured,
+                          "fallback": step.fallback_reason, "ms_replay": 1e3 * t_rep, "ms_eager": 1e3 * t_eager}),
+              flush=True)
     if args.per_scene:
         res = run(prep_device, args.steps, args.warmup, batched=False)
         print(json.dumps({"mode": "device data path, one forward per scene (train.py's loop)", "batch": args.batch,
