@@ -137,6 +137,7 @@ _SIGS = {
                                    _vp, _vp, _vp]),
     "gasfm_point_hub_bwd_c": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_point_hub_bwd_ab": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_point_hub_bwd": (_i32, [_vp, _i64, _f32] + [_vp] * 17),
     "gasfm_point_head_part_shape": (_i32, [_i64, _i32, _vp]),
     "gasfm_point_head_fwd": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_point_head_bwd": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -787,6 +788,20 @@ def point_hub_bwd_ab(X, eps, gA, bA, WA, WB, dSA, dXL, dRes, dX, part):
     st = lib().gasfm_point_hub_bwd_ab(_p(X), X.shape[0], eps, _p(gA), _p(bA), _p(WA), _p(WB), _p(dSA), _p(dXL),
                                       _p(dRes), _p(dX), _p(part), _stream(X))
     check(st, "gasfm_point_hub_bwd_ab")
+
+
+def point_hub_bwd(X, eps, gA, bA, WA, WB, gC, bC, WC, bWC, WD, dSA, dXL, dXR, dRes, dX, part_a, part_c):
+    """The whole point-hub backward in one pass (gasfm_point_hub_bwd)."""
+    _req(X, "X", 64)
+    _req(dSA, "dSA", 32)
+    _req(dXL, "dXL", 64)
+    _req(dXR, "dXR", 32)
+    if dRes is not None:
+        _req(dRes, "dRes", 64)
+    st = lib().gasfm_point_hub_bwd(_p(X), X.shape[0], eps, _p(gA), _p(bA), _p(WA), _p(WB), _p(gC), _p(bC), _p(WC),
+                                   _p(bWC), _p(WD), _p(dSA), _p(dXL), _p(dXR), _p(dRes), _p(dX), _p(part_a),
+                                   _p(part_c), _stream(X))
+    check(st, "gasfm_point_hub_bwd")
 
 
 # ---------------------------------------------------------------- input embedding (embed.hip)

@@ -1490,6 +1490,321 @@ __global__ __launch_bounds__(kThreadsR, GASFM_PT_BWD_R_MINW) void point_tail_bwd
   }
 }
 
+// The whole hub backward (the C and AB passes above) in ONE register-resident pass.  Per tile:
+//   t   = W_C relu(LN_C p) + b_C                     C layout (relu(LN_C p) T-layout as A)
+//   dt  = dXR W_D                                    C layout (weight / bias gradients) and T layout
+//                                                    (the A operand of dt W_C), both from dXR (T)
+//   dp  = dXL W_B + (LN_A_bwd(mask (dSA W_A)) + (LN_C_bwd(mask (dt W_C)) + dRes))   C layout
+//   dW_C += dt^T relu(LN_C p), dW_D += dXR^T t, dW_A += dSA^T relu(LN_A p), dW_B += dXL^T p
+// The rows are requested one tile ahead in the T layout (the products over features); the
+// C layout the weight gradients and the LayerNorm backward need is read back from a per-wave
+// LDS copy of the tile (one write per row chunk, read just before use: the 256 architected VGPRs
+// of a wave could not also hold a second, C-layout load of every tile).  The LayerNorm statistics
+// come from the T rows and reach the C layout by lane shuffles.  dRes is read in the C layout at
+// the top of its tile (before the next tile's requests), dp stored from the C layout.  Both
+// passes' partial rows are written (HA_* into part_a, HC_* into part_c), so the colsums and the
+// Python side are those of the two-pass form.  Algorithmic bytes per row:
+// p 256 + dSA 128 + dXL 256 + dXR 128 + dRes 256 + dp 256 = 1,280 (the two passes: 2,048).
+#ifndef GASFM_PT_HUB_BWD_R
+#define GASFM_PT_HUB_BWD_R 1
+#endif
+#ifndef GASFM_PT_HUB_BWD_R_MINW
+#define GASFM_PT_HUB_BWD_R_MINW 1
+#endif
+constexpr int LDA = FA + 4;  // 32-wide LDS tile row stride (4 lane groups -> 4 bank quarters)
+
+// C-layout rows out (rows >= nrows not written)
+template <int W>
+__device__ __forceinline__ void cl_store(float* X, int64_t row0, int nrows, const f32x4 (&v)[W / 16], int lane) {
+  const int c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (4 * g + r >= nrows) continue;
+    float* p = X + (row0 + 4 * g + r) * W + c;
+#pragma unroll
+    for (int ft = 0; ft < W / 16; ++ft) p[16 * ft] = v[ft][r];
+  }
+}
+
+// T-layout rows (row c, features 16 u + 4 g + j) into the wave's LDS tile (row stride LD)
+template <int W, int LD>
+__device__ __forceinline__ void t_to_lds(const f32x4 (&v)[W / 16], float* X, int lane) {
+  const int c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int u = 0; u < W / 16; ++u)
+    *reinterpret_cast<float4*>(X + c * LD + 16 * u + 4 * g) = make_float4(v[u][0], v[u][1], v[u][2], v[u][3]);
+}
+
+template <bool HR>
+__global__ __launch_bounds__(kThreadsR, GASFM_PT_HUB_BWD_R_MINW) void point_hub_bwd_r_kernel(
+    const float* __restrict__ X, int64_t N, float eps, const float* __restrict__ gA, const float* __restrict__ bA,
+    const float* __restrict__ WA, const float* __restrict__ WB, const float* __restrict__ gC,
+    const float* __restrict__ bC, const float* __restrict__ WC, const float* __restrict__ bWC,
+    const float* __restrict__ WD, const float* __restrict__ dSA, const float* __restrict__ dXL,
+    const float* __restrict__ dXR, const float* dRes, float* dX, float* __restrict__ part_a,
+    float* __restrict__ part_c) {
+  constexpr int OC = 0, ODT = OC + FA * FP, OCT = ODT + FA * FA, OAT = OCT + FA * FP, OBT = OAT + FA * FP,
+                OV = OBT + FP * FP, OT = OV + 6 * FP;
+  constexpr int TW = TR * (2 * LDX + 2 * LDA);  // per wave: p, dXL (64 wide), dSA, dXR (32 wide)
+  constexpr int NLDS = OT + kWavesR * TW;
+  constexpr int NRED = 144 + 24;
+  __shared__ __attribute__((aligned(16))) float lds[NLDS];
+  const float4* WCQ = reinterpret_cast<const float4*>(lds + OC);     // slabs of W_C   (out t,  k p)
+  const float4* WDTQ = reinterpret_cast<const float4*>(lds + ODT);   // slabs of W_D^T (out t,  k xr)
+  const float4* WCTQ = reinterpret_cast<const float4*>(lds + OCT);   // slabs of W_C^T (out p,  k t)
+  const float4* WATQ = reinterpret_cast<const float4*>(lds + OAT);   // slabs of W_A^T (out p,  k sa)
+  const float4* WBTQ = reinterpret_cast<const float4*>(lds + OBT);   // slabs of W_B^T (out p,  k xl)
+  const float* V = lds + OV;  // gamma_C beta_C gamma_A beta_A b_C(32) (pad)
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
+  const int c = lane & 15, g = lane >> 4;
+  float* Tp = lds + OT + wave * TW;
+  float* Tl = Tp + TR * LDX;
+  float* Ts = Tl + TR * LDX;
+  float* Tr = Ts + TR * LDA;
+  const int64_t ntiles = (N + TR - 1) / TR;
+  const int64_t gw = int64_t(blockIdx.x) * kWavesR + wave, nw = int64_t(gridDim.x) * kWavesR;
+  f32x4 n_pT[4], n_rT[2], n_sT[2], n_lT[4];  // the next tile's T-layout rows
+  auto fetch = [&](int64_t tt) {
+    const int64_t r0 = tt * TR;
+    const int nr = int(N - r0 < TR ? N - r0 : TR);
+    slabs_load<FP>(X, r0, nr, n_pT, lane);
+    slabs_load<FA>(dXR, r0, nr, n_rT, lane);
+    slabs_load<FA>(dSA, r0, nr, n_sT, lane);
+    slabs_load<FP>(dXL, r0, nr, n_lT, lane);
+  };
+  if (gw < ntiles) fetch(gw);  // the first tile's rows fly while the weights are staged
+  stage_slabs<FA, FP, kThreadsR>(WC, lds + OC);
+  stage_slabs_tr<FA, FA, kThreadsR>(WD, lds + ODT);
+  stage_slabs_tr<FA, FP, kThreadsR>(WC, lds + OCT);
+  stage_slabs_tr<FA, FP, kThreadsR>(WA, lds + OAT);
+  stage_slabs_tr<FP, FP, kThreadsR>(WB, lds + OBT);
+  if (threadIdx.x < FP) {
+    lds[OV + threadIdx.x] = gC[threadIdx.x];
+    lds[OV + FP + threadIdx.x] = bC[threadIdx.x];
+    lds[OV + 2 * FP + threadIdx.x] = gA[threadIdx.x];
+    lds[OV + 3 * FP + threadIdx.x] = bA[threadIdx.x];
+    if (threadIdx.x < FA) lds[OV + 4 * FP + threadIdx.x] = bWC[threadIdx.x];
+  }
+  __syncthreads();
+  f32x4 dWA[2][4], dWB[4][4], dWC[2][4], dWD[2][2];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    dWA[0][nt] = dWA[1][nt] = dWC[0][nt] = dWC[1][nt] = zero4();
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) dWB[mt][nt] = zero4();
+  }
+  dWD[0][0] = dWD[0][1] = dWD[1][0] = dWD[1][1] = zero4();
+  float dbB[4] = {0.f, 0.f, 0.f, 0.f}, dgA[4] = {0.f, 0.f, 0.f, 0.f}, dbA[4] = {0.f, 0.f, 0.f, 0.f};
+  float dgC[4] = {0.f, 0.f, 0.f, 0.f}, dbCl[4] = {0.f, 0.f, 0.f, 0.f}, dbC[2] = {0.f, 0.f}, dbD[2] = {0.f, 0.f};
+  for (int64_t t = gw; t < ntiles; t += nw) {
+    const int64_t row0 = t * TR;
+    const int nrows = int(N - row0 < TR ? N - row0 : TR);
+    asm volatile("" ::: "memory");  // weight slabs re-read from LDS per tile (not hoisted into VGPRs)
+    f32x4 pT[4], rT[2] = {n_rT[0], n_rT[1]}, sT[2] = {n_sT[0], n_sT[1]}, lT[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      pT[u] = n_pT[u];
+      lT[u] = n_lT[u];
+    }
+    // dRes of this tile, then the next tile's rows (unconditional: the last tile re-reads itself;
+    // a load under a branch makes the loop header wait for every outstanding load)
+    f32x4 acc[4];
+    if (HR) cl_load<FP>(dRes, row0, nrows, acc, lane);
+    fetch(t + nw < ntiles ? t + nw : t);
+    t_to_lds<FP, LDX>(pT, Tp, lane);
+    t_to_lds<FP, LDX>(lT, Tl, lane);
+    t_to_lds<FA, LDA>(sT, Ts, lane);
+    t_to_lds<FA, LDA>(rT, Tr, lane);
+    // phase 1: statistics of the row c (T layout), t = W_C relu(LN_C p) + b_C (C layout)
+    float mean, rstd;
+    slab_stats(pT, eps, mean, rstd);
+    f32x4 tC[2] = {zero4(), zero4()};
+    {
+      f32x4 pc[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const f32x4 gm = vec_at(V, u, g), bt = vec_at(V + FP, u, g);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pc[u][j] = fmaxf(fmaf((pT[u][j] - mean) * rstd, gm[j], bt[j]), 0.f);
+      }
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft) tC[ft] += V[4 * FP + 16 * ft + c];
+      layer_c<2, 4>(WCQ, pc, tC, lane);
+    }
+    float meanC[4], rstdC[4];  // row 4 g + r lives on lane c = 4 g + r
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      meanC[r] = __shfl(mean, 4 * g + r);
+      rstdC[r] = __shfl(rstd, 4 * g + r);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 2: dt (C and T layouts), dt W_C, LN_C backward onto dRes
+    f32x4 dtC[2] = {zero4(), zero4()};
+    f32x4 xh[4];
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xh[ot][r] = (Tp[(4 * g + r) * LDX + 16 * ot + c] - meanC[r]) * rstdC[r];
+    {
+      f32x4 dtT[2] = {zero4(), zero4()}, dp[4] = {zero4(), zero4(), zero4(), zero4()}, dq[4];
+      layer_c<2, 2>(WDTQ, rT, dtC, lane);
+      layer_t<2, 2>(WDTQ, rT, dtT, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      layer_c<4, 2>(WCTQ, dtT, dp, lane);
+      float gm[4], bt[4];
+#pragma unroll
+      for (int ot = 0; ot < 4; ++ot) {
+        gm[ot] = V[16 * ot + c];
+        bt[ot] = V[FP + 16 * ot + c];
+      }
+      cl_ln_relu_bwd(xh, dp, gm, bt, rstdC, nrows, g, dgC, dbCl, dq);
+#pragma unroll
+      for (int ot = 0; ot < 4; ++ot) acc[ot] = HR ? dq[ot] + acc[ot] : dq[ot];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 3: dSA W_A, LN_A backward; dXL W_B accumulated on top; dp stored
+    {
+      f32x4 dp[4] = {zero4(), zero4(), zero4(), zero4()}, da[4];
+      layer_c<4, 2>(WATQ, sT, dp, lane);
+      float gm[4], bt[4];
+#pragma unroll
+      for (int ot = 0; ot < 4; ++ot) {
+        gm[ot] = V[2 * FP + 16 * ot + c];
+        bt[ot] = V[3 * FP + 16 * ot + c];
+      }
+      cl_ln_relu_bwd(xh, dp, gm, bt, rstdC, nrows, g, dgA, dbA, da);
+#pragma unroll
+      for (int ot = 0; ot < 4; ++ot) acc[ot] = da[ot] + acc[ot];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    layer_c<4, 4>(WBTQ, lT, acc, lane);
+    cl_store<FP>(dX, row0, nrows, acc, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 4: weight gradients over the tile's rows (step s: row 4 g + s, C-layout operands read
+    // from the LDS copies; dead rows: the A operands are masked to 0), bias sums
+    cl_mask(dtC, nrows, g);
+#pragma unroll
+    for (int ft = 0; ft < 2; ++ft) dbC[ft] += (dtC[ft][0] + dtC[ft][1]) + (dtC[ft][2] + dtC[ft][3]);
+    float gAv[4], bAv[4], gCv[4], bCv[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      gCv[nt] = V[16 * nt + c];
+      bCv[nt] = V[FP + 16 * nt + c];
+      gAv[nt] = V[2 * FP + 16 * nt + c];
+      bAv[nt] = V[3 * FP + 16 * nt + c];
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int row = 4 * g + s;
+      const bool live = row < nrows;
+      float pa[4], pc[4], pr[4], la[4], sa[2], ra[2];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        pa[nt] = fmaxf(fmaf(xh[nt][s], gAv[nt], bAv[nt]), 0.f);
+        pc[nt] = fmaxf(fmaf(xh[nt][s], gCv[nt], bCv[nt]), 0.f);
+        pr[nt] = Tp[row * LDX + 16 * nt + c];
+        la[nt] = live ? Tl[row * LDX + 16 * nt + c] : 0.f;
+        dbB[nt] += la[nt];
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        sa[mt] = live ? Ts[row * LDA + 16 * mt + c] : 0.f;
+        ra[mt] = live ? Tr[row * LDA + 16 * mt + c] : 0.f;
+        dbD[mt] += ra[mt];
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          dWA[mt][nt] = mfma16(sa[mt], pa[nt], dWA[mt][nt]);
+          dWC[mt][nt] = mfma16(dtC[mt][s], pc[nt], dWC[mt][nt]);
+        }
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) dWD[mt][nt] = mfma16(ra[mt], tC[nt][s], dWD[mt][nt]);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) dWB[mt][nt] = mfma16(la[mt], pr[nt], dWB[mt][nt]);
+    }
+    __builtin_amdgcn_wave_barrier();  // this tile's LDS reads before the next tile's writes
+    asm volatile("" ::: "memory");
+  }
+  float v[NRED];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        v[(mt * 4 + nt) * 4 + r] = dWA[mt][nt][r];
+        v[96 + (mt * 4 + nt) * 4 + r] = dWC[mt][nt][r];
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) v[32 + (mt * 4 + nt) * 4 + r] = dWB[mt][nt][r];
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) v[128 + (mt * 2 + nt) * 4 + r] = dWD[mt][nt][r];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[144 + k] = dbB[k];
+    v[148 + k] = dgA[k];
+    v[152 + k] = dbA[k];
+    v[156 + k] = dgC[k];
+    v[160 + k] = dbCl[k];
+  }
+  v[164] = dbC[0];
+  v[165] = dbC[1];
+  v[166] = dbD[0];
+  v[167] = dbD[1];
+  wg_reduce_ordered<NRED, kWavesR, NLDS>(v, lds, wave, lane);
+  if (wave == 0) {
+    float* oa = part_a + int64_t(blockIdx.x) * HA_PART;
+    float* oc = part_c + int64_t(blockIdx.x) * HC_PART;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const int o = mt * 16 + 4 * g + r;
+          oa[HA_WA + o * FP + nt * 16 + c] = v[(mt * 4 + nt) * 4 + r];
+          oc[HC_WC + o * FP + nt * 16 + c] = v[96 + (mt * 4 + nt) * 4 + r];
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) oa[HA_WB + (mt * 16 + 4 * g + r) * FP + nt * 16 + c] = v[32 + (mt * 4 + nt) * 4 + r];
+      }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) oc[HC_WD + (mt * 16 + 4 * g + r) * FA + nt * 16 + c] = v[128 + (mt * 2 + nt) * 4 + r];
+    float tt[24];
+#pragma unroll
+    for (int k = 0; k < 24; ++k) tt[k] = sum_groups(v[144 + k]);
+    if (g == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        oa[HA_BB + k * 16 + c] = tt[k];
+        oa[HA_GA + k * 16 + c] = tt[4 + k];
+        oa[HA_BA + k * 16 + c] = tt[8 + k];
+        oc[HC_GC + k * 16 + c] = tt[12 + k];
+        oc[HC_BCL + k * 16 + c] = tt[16 + k];
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        oc[HC_BC + k * 16 + c] = tt[20 + k];
+        oc[HC_BD + k * 16 + c] = tt[22 + k];
+      }
+    }
+  }
+}
+
 int64_t tiles_of(int64_t N) { return (N + TR - 1) / TR; }
 
 template <class K>
@@ -1520,6 +1835,10 @@ int hub_ab_grid(int64_t N, bool hr) {
 int hub_c_grid(int64_t N, bool hr) {
   return hr ? grid8(&point_hub_bwd_c_kernel<true>, N) : grid8(&point_hub_bwd_c_kernel<false>, N);
 }
+// the one-pass hub backward: both partial buffers have its grid's rows (whether dRes is given or not),
+// and the two-pass entry points launch that many workgroups too while it is the default (their
+// partial buffers come from gasfm_point_hub_part_shape)
+int hub_r_grid(int64_t N) { return gridR(&point_hub_bwd_r_kernel<true>, N); }
 
 }  // namespace
 }  // namespace gasfm
@@ -1534,6 +1853,7 @@ extern "C" int32_t gasfm_point_tail_part_shape(int64_t N, int32_t has_prev, int3
 extern "C" int32_t gasfm_point_hub_part_shape(int64_t N, int32_t which, int32_t has_res, int32_t* cols) {
   if (cols) *cols = which ? HC_PART : HA_PART;
   if (N <= 0) return 0;
+  if (GASFM_PT_HUB_BWD_R) return hub_r_grid(N);
   return which ? hub_c_grid(N, has_res != 0) : hub_ab_grid(N, has_res != 0);
 }
 extern "C" int gasfm_point_tail_fwd(const float* prev, const float* agg, int64_t N, const float* Wp, const float* bp,
@@ -1629,10 +1949,10 @@ extern "C" int gasfm_point_hub_bwd_c(const float* X, int64_t N, float eps, const
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const bool hr = dRes != nullptr;
   if (hr)
-    hipLaunchKernelGGL(point_hub_bwd_c_kernel<true>, dim3(hub_c_grid(N, true)), dim3(kThreads8), 0, st, X, N, eps,
+    hipLaunchKernelGGL(point_hub_bwd_c_kernel<true>, dim3((GASFM_PT_HUB_BWD_R ? hub_r_grid(N) : hub_c_grid(N, true))), dim3(kThreads8), 0, st, X, N, eps,
                        gC, bC, WC, bWC, WD, dXR, dRes, dX, part);
   else
-    hipLaunchKernelGGL(point_hub_bwd_c_kernel<false>, dim3(hub_c_grid(N, false)), dim3(kThreads8), 0, st, X, N,
+    hipLaunchKernelGGL(point_hub_bwd_c_kernel<false>, dim3((GASFM_PT_HUB_BWD_R ? hub_r_grid(N) : hub_c_grid(N, false))), dim3(kThreads8), 0, st, X, N,
                        eps, gC, bC, WC, bWC, WD, dXR, dRes, dX, part);
   return launch_status("gasfm_point_hub_bwd_c");
 }
@@ -1647,10 +1967,39 @@ extern "C" int gasfm_point_hub_bwd_ab(const float* X, int64_t N, float eps, cons
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const bool hr = dRes != nullptr;
   if (hr)
-    hipLaunchKernelGGL(point_hub_bwd_ab_kernel<true>, dim3(hub_ab_grid(N, true)), dim3(kThreads8), 0, st, X, N,
+    hipLaunchKernelGGL(point_hub_bwd_ab_kernel<true>, dim3((GASFM_PT_HUB_BWD_R ? hub_r_grid(N) : hub_ab_grid(N, true))), dim3(kThreads8), 0, st, X, N,
                        eps, gA, bA, WA, WB, dSA, dXL, dRes, dX, part);
   else
-    hipLaunchKernelGGL(point_hub_bwd_ab_kernel<false>, dim3(hub_ab_grid(N, false)), dim3(kThreads8), 0, st, X, N,
+    hipLaunchKernelGGL(point_hub_bwd_ab_kernel<false>, dim3((GASFM_PT_HUB_BWD_R ? hub_r_grid(N) : hub_ab_grid(N, false))), dim3(kThreads8), 0, st, X, N,
                        eps, gA, bA, WA, WB, dSA, dXL, dRes, dX, part);
   return launch_status("gasfm_point_hub_bwd_ab");
+}
+
+extern "C" int gasfm_point_hub_bwd(const float* X, int64_t N, float eps, const float* gA, const float* bA,
+                                   const float* WA, const float* WB, const float* gC, const float* bC,
+                                   const float* WC, const float* bWC, const float* WD, const float* dSA,
+                                   const float* dXL, const float* dXR, const float* dRes, float* dX, float* part_a,
+                                   float* part_c, void* stream) {
+  GASFM_REQUIRE(N >= 0, "gasfm_point_hub_bwd: N < 0");
+  if (N == 0) return GASFM_OK;
+  GASFM_REQUIRE(X && gA && bA && WA && WB && gC && bC && WC && bWC && WD && dSA && dXL && dXR && dX && part_a &&
+                    part_c,
+                "gasfm_point_hub_bwd: null pointer");
+  GASFM_REQUIRE(aligned16(X) && aligned16(dSA) && aligned16(dXL) && aligned16(dXR),
+                "gasfm_point_hub_bwd: alignment");
+  GASFM_REQUIRE(dX != X && dX != dSA && dX != dXL && dX != dXR, "gasfm_point_hub_bwd: dX aliases an input");
+  if (!GASFM_PT_HUB_BWD_R) {  // the two-pass form: C pass into dX, AB pass in place
+    const int st = gasfm_point_hub_bwd_c(X, N, eps, gC, bC, WC, bWC, WD, dXR, dRes, dX, part_c, stream);
+    if (st != GASFM_OK) return st;
+    return gasfm_point_hub_bwd_ab(X, N, eps, gA, bA, WA, WB, dSA, dXL, dX, dX, part_a, stream);
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int gsz = hub_r_grid(N);
+  if (dRes)
+    hipLaunchKernelGGL(point_hub_bwd_r_kernel<true>, dim3(gsz), dim3(kThreadsR), 0, st, X, N, eps, gA, bA, WA, WB,
+                       gC, bC, WC, bWC, WD, dSA, dXL, dXR, dRes, dX, part_a, part_c);
+  else
+    hipLaunchKernelGGL(point_hub_bwd_r_kernel<false>, dim3(gsz), dim3(kThreadsR), 0, st, X, N, eps, gA, bA, WA, WB,
+                       gC, bC, WC, bWC, WD, dSA, dXL, dXR, dRes, dX, part_a, part_c);
+  return launch_status("gasfm_point_hub_bwd");
 }

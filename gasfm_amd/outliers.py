@@ -26,7 +26,10 @@ The selection is bit-identical to the reference's for the same numpy seed (the d
 reference's own ``np.random.choice`` calls, in order; only the list lengths reach the host), and
 the injected values agree to fp32 rounding for the same Gaussian draws ``z``
 (tests/golden/outliers.npz, made by the reference's code).  Host syncs: the four class counts
-after every pass (the loop is data-dependent) and the nonzero() list lengths.
+after every marking pass (the loop is data-dependent and the numpy draw sizes depend on them),
+one for the initial counts and minima, and one for all deferred checks at the end; a selection is
+flipped by its ranks (a cumulative count over the class, no nonzero() list), the checks between
+passes (the reference's verify_* asserts) are collected on the device and tested once.
 """
 import numpy as np
 import torch
@@ -57,12 +60,19 @@ class OutlierInjector:
         self.cam_ptr, self.pt_ptr, self.perm = b["cam_ptr"], b["pt_ptr"], b["perm"]
         self.state = torch.empty(self.cam.shape[0], dtype=torch.uint8, device=M.device)
         self.counts = [0, 0, 0, 0]
+        self._checks = []  # [views min, points min] inlier-count minima, tested once (_run_checks)
         self._all_cam = (self.cam_ptr[1:] - self.cam_ptr[:-1]).contiguous()
         self._all_pt = (self.pt_ptr[1:] - self.pt_ptr[:-1]).contiguous()
-        mins = torch.stack([self._all_cam.min(), self._all_pt.min()]).tolist() if self.n_proj_total else [0, 0]
-        # verify_enough_points_per_view / verify_enough_views_per_point (:240-251)
-        assert mins[0] >= MIN_N_POINTS_PER_VIEW and mins[1] >= MIN_N_VIEWS_PER_POINT
-        self._init_partition()
+        # verify_enough_points_per_view / verify_enough_views_per_point (:240-251) and the initial
+        # partition's counts in one host read
+        c = _native.outlier_mark(self.state, self.cam, self.pt, self._all_cam, self._all_pt, 0)
+        if self.n_proj_total:
+            mins = torch.stack([self._all_cam.min(), self._all_pt.min()]).to(c.dtype)
+            vals = torch.cat([mins, c.view(-1)]).tolist()
+        else:
+            vals = [0, 0] + c.view(-1).tolist()
+        assert vals[0] >= MIN_N_POINTS_PER_VIEW and vals[1] >= MIN_N_VIEWS_PER_POINT
+        self.counts = [int(v) for v in vals[2:]]
 
     # ---- counts (the reference's n_* properties, :182-226)
     @property
@@ -107,21 +117,42 @@ class OutlierInjector:
         return cam_in, pt_in, mins
 
     def _flip(self, frm, to, size):
-        """state[nonzero(state == frm)[np.random.choice(...)]] = to (:303, :330): one numpy draw."""
+        """state[nonzero(state == frm)[np.random.choice(...)]] = to (:303, :330): one numpy draw.
+        The k-th edge of class frm (edge order, as nonzero lists them) has rank k = its inclusive
+        running count - 1; the edges whose rank was drawn flip -- no host sync."""
         pop = self.counts[frm]
         sel = self.rng.choice(pop, size=(size,), replace=False)
         if size:
-            idx = torch.nonzero(self.state == frm).view(-1)
-            assert idx.shape[0] == pop
-            self.state[idx[torch.from_numpy(np.asarray(sel, dtype=np.int64)).to(idx.device)]] = to
+            dev = self.state.device
+            cls = self.state == frm
+            rank = torch.cumsum(cls, 0, dtype=torch.int32).sub_(1).clamp_(min=0).long()
+            chosen = torch.zeros(pop, dtype=torch.bool, device=dev)
+            sel_t = torch.from_numpy(np.asarray(sel, dtype=np.int64)).pin_memory().to(dev, non_blocking=True)
+            chosen[sel_t] = True
+            self.state.masked_fill_(cls & chosen[rank], to)
             self.counts[frm] -= size
             self.counts[to] += size
 
     def _verify_inliers(self):
-        # verify_enough_points_per_view / _views_per_point on the remaining inliers (:322-324, :336-337)
+        # verify_enough_points_per_view / _views_per_point on the remaining inliers (:322-324,
+        # :336-337): recorded on the device, tested once by _run_checks
         _, _, mins = self._inlier_counts()
-        mins = mins.tolist()
-        assert mins[0] >= MIN_N_POINTS_PER_VIEW and mins[1] >= MIN_N_VIEWS_PER_POINT
+        self._checks.append(mins)
+
+    def _run_checks(self, extra=None):
+        """The deferred verify_* asserts in one host read; extra: a tensor whose entries must all be > 0."""
+        has_mins = bool(self._checks)
+        parts = [torch.stack(self._checks).to(torch.int64).min(0).values] if has_mins else []
+        if extra is not None:
+            parts.append(extra.to(torch.int64).view(-1))
+        self._checks = []
+        if not parts:
+            return
+        v = torch.cat(parts).tolist()
+        if has_mins:
+            assert v[0] >= MIN_N_POINTS_PER_VIEW and v[1] >= MIN_N_VIEWS_PER_POINT
+            v = v[2:]
+        assert all(x > 0 for x in v), "outlier injection: a view lost too many inliers or the LDL needed a 2x2 pivot"
 
     def sample_more_outliers(self, n_new_outliers):
         self._flip(FREE_IN, FREE_OUT, n_new_outliers)
@@ -172,6 +203,7 @@ class OutlierInjector:
                 continue
             assert self.n_outliers >= self.target_n_outliers
             self.remove_surplus_outlier_candidates()
+            self._run_checks()
             return self.outliers_mask
 
     def inject_outliers(self, z=None, generator=None):
@@ -181,11 +213,11 @@ class OutlierInjector:
         dev = self.M.device
         mu, sigma, tril, piv = _native.outlier_moments(self.values, self.state, self.cam_ptr, self.n_views)
         _, _, mins = self._inlier_counts()
-        assert int(mins[0]) >= MIN_N_POINTS_PER_VIEW  # :375
-        assert bool((piv > 0).all()), "LDL factorisation needed a 2x2 pivot block (dataset_utils.py:383)"
-        idx = torch.nonzero(self.outliers_mask).view(-1)
-        n_out = int(idx.shape[0])
-        assert n_out == self.n_outliers
+        # :375 (>= 8 inliers per view) and the LDL's 1x1 pivots (dataset_utils.py:383), one host read
+        self._run_checks(extra=torch.stack([(mins[0] >= MIN_N_POINTS_PER_VIEW).to(torch.int64),
+                                            (piv > 0).all().to(torch.int64)]))
+        n_out = self.n_outliers
+        idx = torch.nonzero_static(self.outliers_mask, size=n_out).view(-1)
         if z is None:
             z = torch.randn((n_out, 2, 1), device=dev, generator=generator)
         z = z.to(dev, torch.float32).reshape(n_out, 2).contiguous()

@@ -139,9 +139,8 @@ class PointHubFn(torch.autograd.Function):
             part_c = _take(sec, "hub_part_c", (rc, cc), p)
             part_a = _take(sec, "hub_part_a", (ra, ca), p)
             with _on_side(sec, (), (), keep + (part_c, part_a)):
-                _native.point_hub_bwd_c(p, ctx.eps, gC, bC, WC, bWC, WD, dXR, dskip, dp, part_c)
-                # in place: each element of dp is read (as dRes) and written by the same lane
-                _native.point_hub_bwd_ab(p, ctx.eps, gA, bA, WA, WB, dSA, dXL, dp, dp, part_a)
+                _native.point_hub_bwd(p, ctx.eps, gA, bA, WA, WB, gC, bC, WC, bWC, WD, dSA, dXL, dXR, dskip, dp,
+                                      part_a, part_c)
             tc, ta = _native.param_colsum(part_c, ctx.defer), _native.param_colsum(part_a, ctx.defer)
         o = 0
         dWC = tc[o:o + A_W * P_W].view(A_W, P_W)

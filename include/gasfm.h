@@ -442,6 +442,15 @@ int gasfm_point_hub_bwd_ab(const float* X, int64_t N, float eps, const float* gA
                            const float* WA, const float* WB, const float* dSA, const float* dXL,
                            const float* dRes, float* dX, float* part, void* stream);
 
+/* The whole hub backward in one pass (both of the above; the two-pass form when the library is
+ * built with GASFM_PT_HUB_BWD_R=0): dX = dRes + dXL WB + LN_A_bwd(mask (dSA WA))
+ * + LN_C_bwd(mask (dXR WD WC)); dRes may be null or alias dX, dX must not alias the other inputs.
+ * part_a / part_c: the which = 0 / which = 1 partial layouts above, gasfm_point_hub_part_shape rows. */
+int gasfm_point_hub_bwd(const float* X, int64_t N, float eps, const float* gA, const float* bA, const float* WA,
+                        const float* WB, const float* gC, const float* bC, const float* WC, const float* bWC,
+                        const float* WD, const float* dSA, const float* dXL, const float* dXR, const float* dRes,
+                        float* dX, float* part_a, float* part_c, void* stream);
+
 /* ---- input embedding (embed.hip): P = values W^T + b, the Linear(2, 2) of EmbeddingLayer
  * (layers.py:992-1015, graph_attn_sfm.py:53); values, P [E x 2] row-major, W [2 x 2], b [2]. */
 int gasfm_embed2_fwd(const float* values, int64_t E, const float* W, const float* b, float* P, void* stream);

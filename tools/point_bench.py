@@ -1,4 +1,4 @@
-"""Point-side kernel microbench (GPU box): tail fwd/bwd and hub fwd/bwd_c/bwd_ab at n = 25k and
+"""Point-side kernel microbench (GPU box): tail fwd/bwd and hub fwd/bwd_c/bwd_ab/bwd at n = 25k and
 200k rows (the per-rank and whole config-4 point counts), mean of 20 launches with HIP events.
 
 usage: [GASFM_LIB=variant.so] python tools/point_bench.py
@@ -47,8 +47,12 @@ def main():
         dXR, dSA, dXL, dskip, dp = r(N, 32), r(N, 32), r(N, 64), r(N, 64), r(N, 64)
         t_hc = timeit(lambda: _native.point_hub_bwd_c(X, 1e-5, gC, bC, WC, bWC, WD, dXR, dskip, dp, pc))
         t_ha = timeit(lambda: _native.point_hub_bwd_ab(X, 1e-5, gA, bA, WA, WB, dSA, dXL, dp, dp, pa))
+        dp2 = r(N, 64)
+        t_h1 = timeit(lambda: _native.point_hub_bwd(X, 1e-5, gA, bA, WA, WB, gC, bC, WC, bWC, WD, dSA, dXL, dXR,
+                                                    dskip, dp2, pa, pc))
         print(f"kernel us N={N}: tail_fwd {t_tf:.1f} tail_bwd {t_tb:.1f} hub_fwd {t_hf:.1f} "
-              f"hub_bwd_c {t_hc:.1f} hub_bwd_ab {t_ha:.1f} (part rows tail {rows}, hub {rc}/{ra})", flush=True)
+              f"hub_bwd_c {t_hc:.1f} hub_bwd_ab {t_ha:.1f} hub_bwd (one pass) {t_h1:.1f} "
+              f"(part rows tail {rows}, hub {rc}/{ra})", flush=True)
 
 
 if __name__ == "__main__":
