@@ -13,13 +13,32 @@ forward and backward are the HIP kernels of gasfm_amd/csrc/gat_attn.hip; no
 PyTorch or CPU fallback exists (a missing library raises).
 """
 import copy
+import os
 
 import numpy as np
 import torch
 
 from . import _native
 
-DEFAULT_MAX_PIECE = 256
+DEFAULT_MAX_PIECE = 256  # edges per work item
+_MAX_PIECE_ENV = os.environ.get("GASFM_MAX_PIECE")  # A/B knob: a fixed camera-direction piece length
+
+
+def camera_max_piece(num_edges):
+    """Edges per work item of a camera-direction plan over num_edges edges.
+
+    256 (DEFAULT_MAX_PIECE), halved down to 64 while the plan would hold fewer than ~4 items per
+    resident wave of the camera-item edge kernels (512 workgroups x 4 waves): a 1/8-points shard
+    (~500 edges per camera) otherwise runs edge_cam_pbwd / edge_seam_fwd / edge_epilogue_bwd at
+    about one 16-tile item per wave.  Rank 0 of 8 (bench.py --emulate-world 8): 9.92 ms at 256,
+    9.33 at 128, 9.26 at 64; the whole config-4 scene stays at 256 (31.94 vs 32.15 ms at 128).
+    """
+    if _MAX_PIECE_ENV:
+        return int(_MAX_PIECE_ENV)
+    mp = DEFAULT_MAX_PIECE
+    while mp > 64 and num_edges < 8192 * mp:
+        mp //= 2
+    return mp
 LANES_MAX_AVG = 32  # 4-wide convs with <= this many edges per item on average: one lane per item
 # The lane-per-item forward replaced a 226 us launch by a 43 us one at config 4; the lane-per-item
 # backward measured 193 us against 153 us for the wave-per-item kernel (its dXL rows are scattered

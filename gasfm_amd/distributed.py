@@ -51,7 +51,7 @@ import torch
 import torch.distributed as dist
 
 from . import _native
-from .attention import AttnPlan, attn_backward_raw, attn_forward_partial, combine_partials
+from .attention import AttnPlan, attn_backward_raw, attn_forward_partial, camera_max_piece, combine_partials
 from .scene import MIN_N_POINTS_PER_VIEW, MIN_N_VIEWS_PER_POINT, SceneData, build_graph_wrappers
 
 # parameters whose gradient comes from rank-local computation (edges / points); everything
@@ -455,9 +455,9 @@ def shard_scene(scene, rank, world, max_piece=None, cameras=False, emulate=False
     gw["view2global"].plan = AttnPlan.from_targets(torch.zeros_like(vv), 1, src=vv, src_rows=m, max_piece=8)
     gw["view2global"].plan.tag = "view2global"
     # partial (exchange) plans for the camera direction and the points -> global graph
-    kw = {} if max_piece is None else {"max_piece": max_piece}
     data.partial_plans = {
-        "proj2view": AttnPlan.from_targets(lcam, m, all_partial=True, **kw),
+        "proj2view": AttnPlan.from_targets(lcam, m, all_partial=True,
+                                           max_piece=camera_max_piece(len(lcam)) if max_piece is None else max_piece),
         "scenepoint2global": AttnPlan.from_targets(
             torch.zeros(gw["scenepoint2global"].plan.num_edges, dtype=torch.int64), 1,
             src=gw["scenepoint2global"].valid_indices[1], src_rows=p1 - p0, all_partial=True,

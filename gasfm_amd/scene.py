@@ -19,7 +19,7 @@ import copy
 import numpy as np
 import torch
 
-from .attention import AttnPlan
+from .attention import AttnPlan, camera_max_piece
 
 MIN_N_VIEWS_PER_POINT = 2   # utils/constants.py:2
 MIN_N_POINTS_PER_VIEW = 8   # utils/constants.py:6
@@ -144,7 +144,8 @@ def build_graph_wrappers(indices, m, n, max_piece=None):
     """The four aggregation graphs of SceneData.create_axial_aggregation_graphs (SceneData.py:153-239)."""
     cam, pt = indices[0], indices[1]
     dev = indices.device
-    p2v = AxialAggregationGraphWrapper(m, n, 1, indices, max_piece)
+    p2v = AxialAggregationGraphWrapper(m, n, 1, indices,
+                                       camera_max_piece(int(indices.shape[1])) if max_piece is None else max_piece)
     p2s = AxialAggregationGraphWrapper(m, n, 0, indices, max_piece)
     pts_per_cam = torch.bincount(cam, minlength=m)
     cam_per_pts = torch.bincount(pt, minlength=n)

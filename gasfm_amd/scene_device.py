@@ -26,7 +26,7 @@ import numpy as np
 import torch
 
 from . import _native
-from .attention import DEFAULT_MAX_PIECE, AttnPlan
+from .attention import DEFAULT_MAX_PIECE, AttnPlan, camera_max_piece
 from .scene import (MIN_N_POINTS_PER_VIEW, MIN_N_VIEWS_PER_POINT, AxialAggregationGraphWrapper, SceneData,
                     SparseMat)
 
@@ -90,7 +90,8 @@ def graph_wrappers_device(b, m, n, max_piece=None):
     p2v = AxialAggregationGraphWrapper(m, n, 1, indices, build_plan=False)
     p2s = AxialAggregationGraphWrapper(m, n, 0, indices, build_plan=False)
     # camera direction: edges are cam-major already (seg_ptr = cam_ptr, no permutation)
-    p2v.plan = _plan(b["cam_ptr"], None, None, m, E, E, mp, "proj2view")
+    p2v.plan = _plan(b["cam_ptr"], None, None, m, E, E, camera_max_piece(E) if max_piece is None else max_piece,
+                     "proj2view")
     # point direction: the stable point CSR; a point-sorted edge list needs no permutation
     # (AttnPlan.from_targets takes its sorted branch then)
     sorted_pt = E <= 1 or bool((pt[1:] >= pt[:-1]).all())

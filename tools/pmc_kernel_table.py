@@ -18,6 +18,10 @@ ALGO_MB = {  # config 4 algorithmic bytes per launch, DESIGN.md §5
     "segment_rowsum_kernel": 554, "edge_prologue_bwd_kernel<true, true>": 2560,
     "point_tail_fwd_t_kernel<true>": 128, "point_hub_fwd_t_kernel<true>": 154, "point_head_fwd_kernel": 54,
     "embed2_fwd_kernel": 64, "embed2_bwd_kernel": 64,
+    # round 3: fused camera-attention + prologue backward, forward seam, point backward
+    "edge_cam_pbwd_kernel<true, true>": 2049, "edge_seam_fwd_kernel<true>": 1601,
+    "point_hub_bwd_r_kernel<true>": 256, "point_tail_bwd_r_kernel<true>": 205,
+    "attn_bwd_glds_kernel<gasfm::Geom<32, 8> >": 1120,
 }
 
 
