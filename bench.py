@@ -11,11 +11,15 @@ timed wall time).  With N > 1 the scene's points are sharded over the ranks
 (gasfm_amd.distributed) — strong scaling: the scene is fixed.
 
 Also reported, on the same line:
-  roofline      the fused edge-softmax + aggregation forward of the point direction
-                (attn_fwd_grp_kernel<4,1>, the north-star kernel), timed live with HIP
-                events around each of its launches on its stream right after the timed
-                region; achieved = SURVEY §8(d)'s algorithmic bytes / mean duration;
-                peak 8.0 TB/s.
+  roofline      the step's dominant kernel: the fused camera-attention + edge-prologue
+                backward (edge_cam_pbwd_kernel<LN,RES>, ~23 % of the step), timed live with
+                HIP events around each of its launches on its stream right after the timed
+                region.  Its MFMA floor (12,288 fp32 FLOP per edge at 157.3 TF/s) is above its
+                HBM floor (512 B per edge at 8 TB/s), so achieved = FLOP / mean duration
+                against the fp32 MFMA peak; the HBM rate is reported beside it.
+  roofline_attention  the fused edge-softmax + aggregation forward of the point direction
+                (attn_fwd_grp_kernel<4,1>, the north-star GATv2 kernel), timed the same way;
+                achieved = SURVEY §8(d)'s algorithmic bytes / mean duration; peak 8.0 TB/s.
   cpu_baseline  the oracle's torch-CPU restatement of the reference + PyG op sequence
                 (oracle.gasfm_ref with PYG_FAITHFUL) on a bounded sample scene,
                 rank 0 at N=1 only.
@@ -33,6 +37,10 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+MFMA_F32_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_16x16x4_f32): 64 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz
+PBWD_FLOP_PER_EDGE = 12288  # XLc recompute 2,048 + dP_hat (3 products, K = 32) 6,144 + dW (64 x 32) 4,096
+PBWD_BYTES_PER_EDGE = 512  # P, dXL point half, dRes read, dP written (camera rows once: + 160 B per camera)
+PMC_KERNELS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r3_pmc_kernels.txt")
 
 
 def log(*a):
@@ -54,6 +62,47 @@ def pmc_traffic(E, N):
     if w.get("edges") != E or w.get("points") != N:
         return None
     return r["point"]["traffic_bytes"]
+
+
+def pmc_kernel_traffic(name, E):
+    """HBM bytes per launch of ``name`` from the committed per-kernel PMC table (tools/pmc_kernels.sh
+    on this bench: 2 x FETCH_SIZE + WRITE_SIZE), when it was taken on the config-4 workload."""
+    if E != 4001638:
+        return None
+    try:
+        with open(PMC_KERNELS) as f:
+            for line in f:
+                if line.startswith(name):
+                    return float(line.split()[-3]) * 1e6  # total MB column
+    except (OSError, ValueError, IndexError):
+        return None
+    return None
+
+
+class LaunchTimer:
+    """HIP events around every call of a gasfm_amd._native launcher (module attribute swapped in place,
+    restored by close()) whose arguments ``select`` accepts, on the stream the launch goes to."""
+
+    def __init__(self, name, select):
+        from gasfm_amd import _native
+        self.mod, self.name, self.orig = _native, name, getattr(_native, name)
+        self.events = []
+
+        def wrapped(*a, **k):
+            if not select(*a, **k):
+                return self.orig(*a, **k)
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+            r = self.orig(*a, **k)
+            ev[1].record()
+            self.events.append(ev)
+            return r
+        setattr(_native, name, wrapped)
+
+    def close(self):
+        setattr(self.mod, self.name, self.orig)
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in self.events) / len(self.events) if self.events else None
 
 
 def attn_fwd_bytes(E, N, H, HC, perm):
@@ -236,10 +285,17 @@ def main():
     timer = attention.KernelTimer(lambda tag, HC: tag == "proj2scenepoint" and HC == 32)
     attention.KERNEL_TIMER = timer
     timer.enabled = True
+    # the dominant kernel: edge_cam_pbwd with LayerNorm and the residual term (blocks 1..11)
+    pbwd = LaunchTimer("edge_cam_pbwd", lambda *a, **k: a[1] is not None and a[7] is not None)
     for _ in range(2):
         fwd_bwd()
     timer.enabled = False
     attention.KERNEL_TIMER = None
+    pbwd_ms = pbwd.close()
+    pbwd_launches = len(pbwd.events)
+    e_cam = data.graph_wrappers["proj2view"].plan.num_edges
+    pbwd_tfs = PBWD_FLOP_PER_EDGE * e_cam / (pbwd_ms * 1e-3) / 1e12 if pbwd_ms else None
+    pbwd_gbs = PBWD_BYTES_PER_EDGE * e_cam / (pbwd_ms * 1e-3) / 1e9 if pbwd_ms else None
     kern_ms = timer.mean_ms()
     b2b_ms = timer.replay_ms(20)
     plan = data.graph_wrappers["proj2scenepoint"].plan
@@ -276,7 +332,22 @@ def main():
                                        if emul else
                                        f"{'point+camera' if data.shard.cams is not None else 'point'}-sharded x{world}"
                                        if dist_on else "single GPU")},
-            "roofline": {"kernel": "attn_fwd_grp_kernel<4,1> point direction (proj2scenepoint), per launch",
+            "roofline": {"kernel": "edge_cam_pbwd_kernel<true,true>: camera-attention + edge-prologue backward "
+                                   "(the step's largest kernel), per launch",
+                         "bound": "mfma", "achieved": pbwd_tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+                         "frac": (pbwd_tfs / MFMA_F32_PEAK_TFS) if pbwd_tfs else None,
+                         "traffic": pmc_kernel_traffic("edge_cam_pbwd_kernel<true, true>", e_cam),
+                         "traffic_source": "profiles/r3_pmc_kernels.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                                           "passes of this bench, per launch; 1.00x the algorithmic bytes)",
+                         "flop_per_launch": PBWD_FLOP_PER_EDGE * e_cam,
+                         "algorithmic_bytes": PBWD_BYTES_PER_EDGE * e_cam,
+                         "hbm_achieved_GBps": pbwd_gbs,
+                         "hbm_frac": (pbwd_gbs / HBM_PEAK_GBS) if pbwd_gbs else None,
+                         "mean_us": pbwd_ms * 1e3 if pbwd_ms else None, "launches_timed": pbwd_launches,
+                         "timing": "HIP events on the launch stream around each of its launches in 2 eager steps "
+                                   "after the timed region (agrees with the rocprof durations inside the replayed "
+                                   "step)"},
+            "roofline_attention": {"kernel": "attn_fwd_grp_kernel<4,1> point direction (proj2scenepoint), per launch",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                          "traffic": pmc_traffic(e_local, n_local),

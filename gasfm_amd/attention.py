@@ -25,7 +25,9 @@ _MAX_PIECE_ENV = os.environ.get("GASFM_MAX_PIECE")  # A/B knob: a fixed camera-d
 
 
 def camera_max_piece(num_edges):
-    """Edges per work item of a camera-direction plan over num_edges edges.
+    """Edges per work item of a point shard's camera-direction plan over num_edges edges
+    (distributed.shard_scene; whole scenes and training batches keep DEFAULT_MAX_PIECE: a training
+    batch is host-bound and measured 6 ms per step slower with the extra split pieces' launches).
 
     256 (DEFAULT_MAX_PIECE), halved down to 64 while the plan would hold fewer than ~4 items per
     resident wave of the camera-item edge kernels (512 workgroups x 4 waves): a 1/8-points shard
@@ -111,7 +113,9 @@ class AttnPlan:
     """
 
     def __init__(self, seg_ptr, perm, items, combine, n_slots, num_targets, num_edges, src_rows,
-                 all_partial=False, max_piece=DEFAULT_MAX_PIECE, pos=None):
+                 all_partial=False, max_piece=DEFAULT_MAX_PIECE, pos=None, combine_l1=False):
+        """combine_l1: the level-1 entries when ``combine`` is already split in two levels
+        (scene_device.plan_work_device, on the device; None: one level); False: split here."""
         self.seg_ptr = seg_ptr
         self.perm = perm
         self.items = items
@@ -124,12 +128,15 @@ class AttnPlan:
         self.max_piece = int(max_piece)
         self.n_items = int(items.shape[0])
         dev = items.device
-        if isinstance(combine, torch.Tensor) and combine.device.type != "cpu":
-            combine = combine.cpu()  # the two-level split is host bookkeeping over <= N entries
-        self.combine, self.combine_l1 = _two_level(combine, self.n_slots)
-        if dev.type != "cpu":
-            self.combine = self.combine.to(dev)
-            self.combine_l1 = None if self.combine_l1 is None else self.combine_l1.to(dev)
+        if combine_l1 is not False:
+            self.combine, self.combine_l1 = combine, combine_l1
+        else:
+            if isinstance(combine, torch.Tensor) and combine.device.type != "cpu":
+                combine = combine.cpu()  # the two-level split is host bookkeeping over <= N entries
+            self.combine, self.combine_l1 = _two_level(combine, self.n_slots)
+            if dev.type != "cpu":
+                self.combine = self.combine.to(dev)
+                self.combine_l1 = None if self.combine_l1 is None else self.combine_l1.to(dev)
         self.n_combine = int(self.combine.shape[0])
         self.n_l1 = 0 if self.combine_l1 is None else int(self.combine_l1.shape[0])
         self.n_part_rows = self.n_slots + self.n_l1  # partial rows of both combine levels

@@ -23,8 +23,23 @@ equal the per-scene forwards up to fp32 summation order (tests/test_gpu_batch.py
 """
 import torch
 
-from .scene import AxialAggregationGraphWrapper, SparseMat
-from .scene_device import _plan
+from .attention import DEFAULT_MAX_PIECE
+from .scene import MIN_N_POINTS_PER_VIEW, MIN_N_VIEWS_PER_POINT, AxialAggregationGraphWrapper, SparseMat
+from .scene_device import _piece_counts_host, _piece_stats, _plan
+
+
+def _scene_arrays(d):
+    """(cam_ptr, pt_ptr, perm, pos, point-sorted flag) of one scene: from the device scene build when
+    the scene's graph wrappers were never built (scene_device: they are built on first use), else
+    from its plans.  The flag is a device bool or a Python bool."""
+    b = d.__dict__.get("_scene_build")
+    if b is not None and "graph_wrappers" not in d.__dict__:
+        pt = b["pt"]
+        srt = (pt[1:] >= pt[:-1]).all() if pt.shape[0] > 1 else True
+        return b["cam_ptr"], b["pt_ptr"], b["perm"], b["pos"], srt
+    gw = d.graph_wrappers
+    p = gw["proj2scenepoint"].plan
+    return gw["proj2view"].plan.seg_ptr, p.seg_ptr, p.perm, p.pos, p.perm is None
 
 
 class SceneBatch:
@@ -54,47 +69,59 @@ class SceneBatch:
         self.scene_name = "batch(" + ",".join(getattr(d, "scene_name", "?") for d in datas) + ")"
         self.scene_of_cam = torch.repeat_interleave(torch.arange(self.B, **i64),
                                                     torch.tensor(ms, **i64)).contiguous()
-        pw = [d.graph_wrappers for d in datas]
-        mp = max(w["proj2view"].plan.max_piece for w in pw)
+        arrs = [_scene_arrays(d) for d in datas]
+        mp = DEFAULT_MAX_PIECE if max_piece is None else max_piece
 
-        def cat_ptr(name):
-            parts = [w[name].plan.seg_ptr.to(torch.int64) for w in pw]
-            return torch.cat([parts[0]] + [p[1:] + self.edge_off[i] for i, p in enumerate(parts) if i > 0]
+        def cat_ptr(parts):
+            parts = [q.to(dev, torch.int64) for q in parts]
+            return torch.cat([parts[0]] + [q[1:] + self.edge_off[i] for i, q in enumerate(parts) if i > 0]
                              ).to(torch.int32).contiguous()
 
-        def cat_perm(attr):
-            out = []
-            for i, w in enumerate(pw):
-                p = getattr(w["proj2scenepoint"].plan, attr)
-                if p is None:
-                    p = torch.arange(Es[i], dtype=torch.int32, device=dev)
-                out.append(p.to(torch.int32) + self.edge_off[i])
-            return torch.cat(out).contiguous()
-
+        cam_ptr, pt_ptr = cat_ptr([a[0] for a in arrs]), cat_ptr([a[1] for a in arrs])
+        # every host scalar of the union's plans in ONE read: per-scene point-sortedness, valid view /
+        # point counts per scene, the piece statistics of the two edge plans
+        valid_v = ppc.view(-1) >= MIN_N_POINTS_PER_VIEW
+        valid_p = cpp.view(-1) >= MIN_N_VIEWS_PER_POINT
+        scene_of_pt = torch.repeat_interleave(torch.arange(self.B, **i64), torch.tensor(ns, **i64))
+        cnt_v = torch.zeros(self.B, **i64).index_add_(0, self.scene_of_cam, valid_v.to(torch.int64))
+        cnt_p = torch.zeros(self.B, **i64).index_add_(0, scene_of_pt, valid_p.to(torch.int64))
+        srt = torch.stack([torch.as_tensor(a[4], device=dev).to(torch.int64) for a in arrs])
+        st_c = _piece_stats((cam_ptr[1:] - cam_ptr[:-1]).to(torch.int64), mp)[3]
+        st_p = _piece_stats((pt_ptr[1:] - pt_ptr[:-1]).to(torch.int64), mp)[3]
+        vals_h = torch.cat([srt, cnt_v, cnt_p, st_c, st_p]).tolist()
+        B = self.B
+        sorted_h, cv, cp = vals_h[:B], vals_h[B:2 * B], vals_h[2 * B:3 * B]
         indices = torch.stack([cam, pt])
         p2v = AxialAggregationGraphWrapper(M, N, 1, indices, build_plan=False)
         p2s = AxialAggregationGraphWrapper(M, N, 0, indices, build_plan=False)
-        p2v.plan = _plan(cat_ptr("proj2view"), None, None, M, E, E, mp, "proj2view")
-        sorted_pt = all(w["proj2scenepoint"].plan.perm is None for w in pw)
-        perm, pos = (None, None) if sorted_pt else (cat_perm("perm"), cat_perm("pos"))
-        p2s.plan = _plan(cat_ptr("proj2scenepoint"), perm, pos, N, E, E, mp, "proj2scenepoint")
-        # global graphs: B targets, scene s's sources (valid views / points) in segment s
-        vv = [w["view2global"].valid_indices[0].to(dev) + self.cam_off[i] for i, w in enumerate(pw)]
-        vp = [w["scenepoint2global"].valid_indices[1].to(dev) + self.pt_off[i] for i, w in enumerate(pw)]
+        p2v.plan = _plan(cam_ptr, None, None, M, E, E, mp, "proj2view", counts=vals_h[3 * B:3 * B + 4])
+
+        def cat_perm(k):
+            out = []
+            for i, a in enumerate(arrs):
+                q = a[k] if not sorted_h[i] and a[k] is not None else torch.arange(Es[i], dtype=torch.int32,
+                                                                                     device=dev)
+                out.append(q.to(dev, torch.int32) + self.edge_off[i])
+            return torch.cat(out).contiguous()
+
+        perm, pos = (None, None) if all(sorted_h) else (cat_perm(2), cat_perm(3))
+        p2s.plan = _plan(pt_ptr, perm, pos, N, E, E, mp, "proj2scenepoint", counts=vals_h[3 * B + 4:3 * B + 8])
+        # global graphs: B targets, scene s's sources (valid views / points, union indices) in segment s
         gw = {}
-        for name, src, rows, tgt_dim in (("view2global", vv, M, 0), ("scenepoint2global", vp, N, 1)):
-            counts = torch.tensor([int(s.shape[0]) for s in src], **i64)
-            seg_ptr = torch.zeros(self.B + 1, **i64)
-            seg_ptr[1:] = torch.cumsum(counts, 0)
-            s_all = torch.cat(src).contiguous()
-            tgt = torch.repeat_interleave(torch.arange(self.B, **i64), counts)
+        for name, valid, counts, rows, tgt_dim in (("view2global", valid_v, cv, M, 0),
+                                                  ("scenepoint2global", valid_p, cp, N, 1)):
+            k = int(sum(counts))
+            s_all = torch.nonzero_static(valid, size=k).view(-1)
+            ct = torch.tensor(counts, **i64)
+            seg_ptr = torch.zeros(B + 1, **i64)
+            seg_ptr[1:] = torch.cumsum(ct, 0)
+            tgt = torch.repeat_interleave(torch.arange(B, **i64), ct, output_size=k)
             vi = torch.stack([s_all, tgt]) if tgt_dim == 0 else torch.stack([tgt, s_all])
-            w = AxialAggregationGraphWrapper(M if tgt_dim == 0 else self.B, self.B if tgt_dim == 0 else N,
+            w = AxialAggregationGraphWrapper(M if tgt_dim == 0 else B, B if tgt_dim == 0 else N,
                                              tgt_dim, vi, build_plan=False)
-            k = int(s_all.shape[0])
-            piece = 8 if name == "view2global" else min(256, max(16, -(-max(int(c) for c in counts) // 4096)))
-            w.plan = _plan(seg_ptr.to(torch.int32).contiguous(), s_all.to(torch.int32).contiguous(), None, self.B, k,
-                           rows, piece, name)
+            piece = 8 if name == "view2global" else min(256, max(16, -(-max(counts) // 4096)))
+            w.plan = _plan(seg_ptr.to(torch.int32).contiguous(), s_all.to(torch.int32).contiguous(), None, B, k,
+                           rows, piece, name, counts=_piece_counts_host(counts, piece))
             gw[name] = w
         self.graph_wrappers = {"proj2view": p2v, "proj2scenepoint": p2s, **gw}
 

@@ -446,7 +446,8 @@ def shard_scene(scene, rank, world, max_piece=None, cameras=False, emulate=False
     sel = (pt >= p0) & (pt < p1)
     vals = scene.normalized_values()[sel]
     lcam, lpt = cam[sel], pt[sel] - p0
-    data = SceneData.from_sparse(lcam, lpt, vals, m, p1 - p0, scene_name=f"shard{rank}", max_piece=max_piece)
+    data = SceneData.from_sparse(lcam, lpt, vals, m, p1 - p0, scene_name=f"shard{rank}", max_piece=max_piece,
+                                 cam_max_piece=camera_max_piece(len(lcam)) if max_piece is None else None)
     gw = data.graph_wrappers
     # view validity is a GLOBAL property (>= 8 points over all ranks): replicated view2global plan
     pts_per_cam = np.bincount(cam, minlength=m)

@@ -16,12 +16,12 @@ which every GASFM configuration disables; it raises like the reference does with
 import torch
 
 from . import _native
-from .loss import _edge_tensors
+from .loss import _edge_tensors, scene_csr
 
 
 def _pixel_measurements(data):
     """[E, 2] pixel coordinates of the edges, gathered from the dense M once per scene/device."""
-    pv = data.graph_wrappers["proj2view"].plan
+    caches = scene_csr(data)[0]
     M = getattr(data, "M", None)
     if M is None:
         M = getattr(data, "_M", None)
@@ -31,12 +31,12 @@ def _pixel_measurements(data):
     # keyed on both tensors' storage and version: an in-place edit of M (augmentation) or of the
     # indices recomputes the gather
     key = (M.data_ptr(), M._version, tuple(M.shape), idx.data_ptr(), idx._version)
-    cached = getattr(pv, "_pixel_xy", None)
+    cached = caches.get("pixel_xy")
     if cached is None or cached[0] != key:
         Md = M.to(idx.device)
         xy = torch.stack([Md[2 * idx[0], idx[1]], Md[2 * idx[0] + 1, idx[1]]], 1).float().contiguous()
         cached = (key, xy)
-        pv._pixel_xy = cached
+        caches["pixel_xy"] = cached
     return cached[1]
 
 

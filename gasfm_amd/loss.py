@@ -64,26 +64,38 @@ class ESFMLossFn(torch.autograd.Function):
         return dP.view(-1, 3, 4), dX, None, None, None, None, None, None, None, None
 
 
-def _edge_tensors(data):
-    """int32 (cam, pt), contiguous float32 values and the camera / point CSRs of the network's own
-    plans (proj2view: camera segments over the cam-major edges; proj2scenepoint: point segments
-    with perm = edge ids in point order).  Cached on the proj2view plan, which is per device, keyed
-    on the index tensor's storage and version."""
+def scene_csr(data):
+    """(cache dict, camera CSR, point CSR, point-order edge ids or None) of a scene: from the device
+    scene build while its graph wrappers are not built (scene_device builds them on first use), else
+    from the network's own plans (proj2view: camera segments over the cam-major edges;
+    proj2scenepoint: point segments with perm = edge ids in point order).  The cache dict lives as
+    long as that source (per device)."""
+    b = data.__dict__.get("_scene_build")
+    if b is not None and "graph_wrappers" not in data.__dict__:
+        return b.setdefault("caches", {}), b["cam_ptr"], b["pt_ptr"], b["perm"]
     gw = data.graph_wrappers
     pv, ps = gw["proj2view"].plan, gw["proj2scenepoint"].plan
+    if pv.perm is not None:
+        raise ValueError("ESFMLoss: proj2view plan must cover cam-major sorted edges")
+    if "_caches" not in pv.__dict__:
+        pv._caches = {}
+    return pv._caches, pv.seg_ptr, ps.seg_ptr, ps.perm
+
+
+def _edge_tensors(data):
+    """int32 (cam, pt), contiguous float32 values and the camera / point CSRs (scene_csr).  The int32
+    indices are cached, keyed on the index tensor's storage and version."""
+    caches, cam_ptr, pt_ptr, pt_perm = scene_csr(data)
     idx = data.x.indices
     key = (idx.data_ptr(), idx._version, tuple(idx.shape))  # an in-place edit of the indices invalidates it
-    cache = getattr(pv, "_esfm_edges", None)
+    cache = caches.get("esfm_edges")
     if cache is None or cache[0] != key:
-        if pv.perm is not None:
-            raise ValueError("ESFMLoss: proj2view plan must cover cam-major sorted edges")
         cache = (key, (idx[0].to(torch.int32).contiguous(), idx[1].to(torch.int32).contiguous()))
-        pv._esfm_edges = cache
-    cache = cache[1]
+        caches["esfm_edges"] = cache
     vals = data.x.values
     if vals.dtype != torch.float32 or not vals.is_contiguous():
         vals = vals.float().contiguous()
-    return cache, vals, pv.seg_ptr, ps.seg_ptr, ps.perm
+    return cache[1], vals, cam_ptr, pt_ptr, pt_perm
 
 
 class ESFMLoss(torch.nn.Module):

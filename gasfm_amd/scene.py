@@ -19,7 +19,7 @@ import copy
 import numpy as np
 import torch
 
-from .attention import AttnPlan, camera_max_piece
+from .attention import AttnPlan
 
 MIN_N_VIEWS_PER_POINT = 2   # utils/constants.py:2
 MIN_N_POINTS_PER_VIEW = 8   # utils/constants.py:6
@@ -140,12 +140,13 @@ class AxialAggregationGraphWrapper:
         return ret
 
 
-def build_graph_wrappers(indices, m, n, max_piece=None):
-    """The four aggregation graphs of SceneData.create_axial_aggregation_graphs (SceneData.py:153-239)."""
+def build_graph_wrappers(indices, m, n, max_piece=None, cam_max_piece=None):
+    """The four aggregation graphs of SceneData.create_axial_aggregation_graphs (SceneData.py:153-239).
+    cam_max_piece: the camera direction's work-item length when it differs from max_piece
+    (attention.camera_max_piece for a point shard)."""
     cam, pt = indices[0], indices[1]
     dev = indices.device
-    p2v = AxialAggregationGraphWrapper(m, n, 1, indices,
-                                       camera_max_piece(int(indices.shape[1])) if max_piece is None else max_piece)
+    p2v = AxialAggregationGraphWrapper(m, n, 1, indices, max_piece if cam_max_piece is None else cam_max_piece)
     p2s = AxialAggregationGraphWrapper(m, n, 0, indices, max_piece)
     pts_per_cam = torch.bincount(cam, minlength=m)
     cam_per_pts = torch.bincount(pt, minlength=n)
@@ -183,7 +184,8 @@ class SceneData:
         self.graph_wrappers = build_graph_wrappers(self.x.indices, self.x.shape[0], self.x.shape[1], max_piece)
 
     @classmethod
-    def from_sparse(cls, cam, pt, values, m, n, scene_name="synthetic", Ps_gt=None, max_piece=None):
+    def from_sparse(cls, cam, pt, values, m, n, scene_name="synthetic", Ps_gt=None, max_piece=None,
+                    cam_max_piece=None):
         self = cls.__new__(cls)
         self.scene_name = scene_name
         self.calibrated = True
@@ -202,7 +204,7 @@ class SceneData:
         pts_per_cam = torch.bincount(cam, minlength=m).unsqueeze(1)
         self.device = vals.device
         self.x = SparseMat(vals, indices, cam_per_pts, pts_per_cam, (m, n, vals.shape[1]))
-        self.graph_wrappers = build_graph_wrappers(indices, m, n, max_piece)
+        self.graph_wrappers = build_graph_wrappers(indices, m, n, max_piece, cam_max_piece)
         return self
 
     @classmethod
@@ -210,10 +212,24 @@ class SceneData:
         return cls.from_sparse(scene.cam, scene.pt, scene.normalized_values(), scene.m, scene.n,
                                scene_name="synthetic", Ps_gt=torch.from_numpy(scene.Ps_gt()), max_piece=max_piece)
 
+    def __getattr__(self, name):
+        # scenes built on the device (scene_device.scene_from_dense_device) build their four graph
+        # wrappers on first use: the batched training path (batch.SceneBatch) reads the scene-build
+        # arrays instead, and a scene that only feeds the loss never needs them
+        if name == "graph_wrappers":
+            lazy = self.__dict__.pop("_lazy_graph", None)
+            if lazy is not None:
+                self.graph_wrappers = lazy()
+                return self.graph_wrappers
+        raise AttributeError(name)
+
     def to(self, device, *args, dense_on_demand=False, **kwargs):
+        if "_lazy_graph" in self.__dict__:
+            self.graph_wrappers  # noqa: B018 (built before the copy: its closure holds this device's arrays)
         ret = copy.copy(self)
+        ret.__dict__.pop("_scene_build", None)  # the copy reads its (moved) plans
         for key, attr in self.__dict__.items():
-            if key.startswith("__") or (dense_on_demand and key in ("_M", "_norm_M")):
+            if key.startswith("__") or key == "_scene_build" or (dense_on_demand and key in ("_M", "_norm_M")):
                 continue
             if isinstance(attr, (SparseMat, AxialAggregationGraphWrapper)) or torch.is_tensor(attr):
                 setattr(ret, key, attr.to(device, *args, **kwargs))

@@ -123,18 +123,31 @@ def test_conf_parser_roundtrip():
 
 
 def test_device_plan_work_restatement_matches_host():
-    """scene_device.plan_work_device (torch ops; runs on CPU tensors here) == gasfm_plan_work."""
+    """scene_device.plan_work_device (torch ops; runs on CPU tensors here) == gasfm_plan_work followed
+    by attention._two_level, with the host scalars read by the function itself or passed in (from
+    _piece_stats, or _piece_counts_host for host-known lengths)."""
     import torch
-    from gasfm_amd.scene_device import plan_work_device
+    from gasfm_amd.attention import _two_level
+    from gasfm_amd.scene_device import _piece_counts_host, _piece_stats, plan_work_device
     rng = np.random.default_rng(0)
-    for trial in range(120):
+    n_two_level = 0
+    for trial in range(160):
         N = int(rng.integers(0, 40))
         mp = int(rng.integers(1, 20))
         ap = bool(rng.integers(0, 2))
-        ln = rng.integers(0, 3 if trial % 5 == 0 else 70, size=N)
+        ln = rng.integers(0, 3 if trial % 5 == 0 else (70 if trial % 3 else 400), size=N)
         ptr = np.concatenate([[0], np.cumsum(ln)]).astype(np.int32)
         items, comb, ns = _native.plan_work(ptr, mp, ap)
-        items2, comb2, ns2 = plan_work_device(torch.from_numpy(ptr), mp, ap)
-        assert ns == ns2
-        np.testing.assert_array_equal(items.reshape(-1, 4), items2.numpy().reshape(-1, 4))
-        np.testing.assert_array_equal(comb.reshape(-1, 4), comb2.numpy().reshape(-1, 4))
+        top, l1 = _two_level(torch.from_numpy(comb.reshape(-1, 4)), ns)
+        counts = _piece_counts_host([int(v) for v in ln], mp)
+        assert counts == _piece_stats(torch.from_numpy(ln.astype(np.int64)), mp)[3].tolist()
+        for cts in (None, counts):
+            items2, top2, l12, ns2 = plan_work_device(torch.from_numpy(ptr), mp, ap, cts)
+            assert ns == ns2
+            np.testing.assert_array_equal(items.reshape(-1, 4), items2.numpy().reshape(-1, 4))
+            np.testing.assert_array_equal(top.numpy().reshape(-1, 4), top2.numpy().reshape(-1, 4))
+            assert (l1 is None) == (l12 is None)
+            if l1 is not None:
+                np.testing.assert_array_equal(l1.numpy(), l12.numpy())
+        n_two_level += l1 is not None
+    assert n_two_level > 10

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--top", type=int, default=45)
+    ap.add_argument("--per-scene", action="store_true", help="one forward per scene (default: the union batch)")
+    ap.add_argument("--prep", action="store_true", help="profile the device data path instead (sample + rhaug + "
+                                                        "0.1 outlier injection)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     np.random.seed(0)
@@ -45,15 +48,28 @@ def main():
     net = gasfm_amd.GraphAttnSfMNet(conf).to(dev)
     lossf = ESFMLoss(conf)
 
+    from gasfm_amd.batch import forward_batch
+    from gasfm_amd.outliers import inject_outliers
+
+    def prep():
+        return [apply_rotational_homography_aug_device(sample_data_device(s, int(np.random.randint(10, 21))), 15, 20)
+                for s in scenes[:args.batch]]
+
     def step():
-        datas = [apply_rotational_homography_aug_device(sample_data_device(s, int(np.random.randint(10, 21))), 15, 20)
-                 for s in scenes[:args.batch]]
+        if args.prep:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            datas = [inject_outliers(d, 0.1, log=lambda s: None) for d in prep()]
+            torch.cuda.synchronize()
+            return time.perf_counter() - t0
+        datas = prep()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         net.zero_grad()
         tot = 0.0
-        for d in datas:
-            pred = net(d)
+        preds = None if args.per_scene else forward_batch(net, datas)
+        for k, d in enumerate(datas):
+            pred = net(d) if args.per_scene else preds[k]
             tot = tot + lossf(pred, d)
             evaluation.compute_core_errors(d, pred, conf)
         tot.backward()
@@ -68,7 +84,7 @@ def main():
         pr.enable()
         ts.append(step())
         pr.disable()
-    print("fwd+loss+errors+bwd ms per step:", [round(1e3 * t, 1) for t in ts])
+    print("data prep" if args.prep else "fwd+loss+errors+bwd", "ms per step:", [round(1e3 * t, 1) for t in ts])
     st = pstats.Stats(pr)
     st.sort_stats("tottime").print_stats(args.top)
     st.sort_stats("cumulative").print_stats(args.top)
