@@ -172,6 +172,31 @@ __device__ __forceinline__ void phat_slabs(f32x4 (&v)[2], const float (&g8)[2][4
     for (int j = 0; j < 4; ++j) v[u][j] = fmaxf(fmaf((v[u][j] - mean) * rstd, g8[u][j], b8[u][j]), 0.f);
 }
 
+// phat_slabs that also returns the row statistics (mean, rstd of edge c; 0 / 1 without LN)
+template <bool LN>
+__device__ __forceinline__ void phat_slabs_st(f32x4 (&v)[2], const float (&g8)[2][4], const float (&b8)[2][4],
+                                              float eps, float& mean, float& rstd) {
+  mean = 0.f;
+  rstd = 1.f;
+  if (!LN) return;
+  float sm = (v[0][0] + v[0][1]) + (v[0][2] + v[0][3]) + ((v[1][0] + v[1][1]) + (v[1][2] + v[1][3]));
+  sm += __shfl_xor(sm, 16);
+  sm += __shfl_xor(sm, 32);
+  mean = sm * (1.f / F);
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q = fmaf(v[u][j] - mean, v[u][j] - mean, q);
+  q += __shfl_xor(q, 16);
+  q += __shfl_xor(q, 32);
+  rstd = rsqrtf(q * (1.f / F) + eps);
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[u][j] = fmaxf(fmaf((v[u][j] - mean) * rstd, g8[u][j], b8[u][j]), 0.f);
+}
+
 // acc[ot] += W P_hat^T (A = W slabs, B = P_hat slabs): acc[ot][r] = feature 16 ot + 4 g + r of edge c
 template <int OT>
 __device__ __forceinline__ void xl_slabs(const float4* __restrict__ Q, const f32x4 (&x)[2], f32x4 (&acc)[OT],
@@ -283,7 +308,7 @@ __global__ __launch_bounds__(kThreads, GASFM_CAM_MINW) void edge_cam_fwd_kernel(
       const int nrows = rows_at(w, row0);
       f32x4 ph[2] = {ns[0], ns[1]};
       if (!kCamR) phat_to_lds<LN>(np, nrows, g4, b4, eps, T, lane);
-      const int64_t dst = pos ? int64_t(npos) : row0 + c;
+      const int64_t dst = pos ? int64_t(npos) : row0 + (c < nrows ? c : 0);
       {  // the next tile (this item's, else the next item's first; the last one re-reads itself)
         int64_t r1 = row0;
         int n1 = nrows;
@@ -404,6 +429,14 @@ struct SeamEpi {
 
 #ifndef GASFM_SEAM_MINW
 #define GASFM_SEAM_MINW 2
+#endif
+// 1: no per-tile branches.  A lane past the item's end computes the item's first edge (its loads
+// read that row), so its P' / XL stores go to that edge's rows with the same values (duplicate,
+// identical writes), and its softmax update is a select.  0 (default): guarded stores and update.
+// tools/edge_bench.py, same box: 468-472 us with 1 vs 454-459 with 0 (the branch-free form of
+// edge_cam_pbwd, GASFM_PBWD_V2, gained 5 %: 645-649 vs 683-692 us).
+#ifndef GASFM_SEAM_V2
+#define GASFM_SEAM_V2 0
 #endif
 template <bool LN>
 __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kernel(
@@ -534,10 +567,11 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
           pn[q][r] = fmaf(d, ep.scale, pb[q][r]);
         }
       }
-      if (valid) {
+      if (GASFM_SEAM_V2 || valid) {
+        const int64_t prow = row0 + (valid ? c : 0);
 #pragma unroll
         for (int q = 0; q < 2; ++q)
-          *reinterpret_cast<float4*>(ep.Pout + (row0 + c) * F + 16 * q + 4 * g) =
+          *reinterpret_cast<float4*>(ep.Pout + prow * F + 16 * q + 4 * g) =
               make_float4(pn[q][0], pn[q][1], pn[q][2], pn[q][3]);
       }
       // ---- prologue + camera attention of block b+1 on P' (edge_cam_fwd_kernel)
@@ -556,7 +590,7 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
       }
       f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
       xl_slabs<4>(reinterpret_cast<const float4*>(Wl), pn, acc, lane);
-      if (valid) {
+      if (GASFM_SEAM_V2 || valid) {
         typedef float v4f __attribute__((ext_vector_type(4)));
 #pragma unroll
         for (int ot = 0; ot < 2; ++ot) {
@@ -575,7 +609,14 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
           p = fmaf(leaky(xl[r] + xr[q][r], slope), atq[r], p);
         }
         p += __shfl_xor(p, 16);  // the head's other 4 features
-        if (valid) {
+        if (GASFM_SEAM_V2) {
+          const float mn = valid ? fmaxf(m[q], p) : m[q];
+          const float sc = valid ? __expf(m[q] - mn) : 1.f, wt = valid ? __expf(p - mn) : 0.f;
+          s[q] = fmaf(s[q], sc, wt);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) a[q][r] = fmaf(a[q][r], sc, wt * xl[r]);
+          m[q] = mn;
+        } else if (valid) {
           const float mn = fmaxf(m[q], p);
           const float sc = __expf(m[q] - mn), wt = __expf(p - mn);
           s[q] = fmaf(s[q], sc, wt);
@@ -825,6 +866,15 @@ __global__ __launch_bounds__(kThreads, GASFM_CAM_MINW) void edge_cam_bwd_kernel(
 // back, and P is read once.  Semantics: exactly those two kernels' (same partial-row layouts,
 // concatenated: [dW 64x32 | db 64 | dgamma 32 | dbeta 32 | datt 32 | dbias 32] per workgroup).
 // =============================================================================================
+// 1: the C-layout LayerNorm statistics are the T-layout ones (computed for XLc) moved across by lane
+// shuffles, and dP is stored through a bounds-checked buffer descriptor per work item (rows past
+// the item's end are dropped by the range check): no per-row branch splits the tile's code, so
+// the LayerNorm backward and the dW MFMAs schedule together (~900 -> ~700 instructions per tile;
+// 683-692 -> 645-649 us in tools/edge_bench.py, same box).  0: C-layout statistics recomputed,
+// per-row guarded stores.
+#ifndef GASFM_PBWD_V2
+#define GASFM_PBWD_V2 1
+#endif
 constexpr int PB2_PRO = NX * F + NX + 2 * F;  // the prologue_bwd part row
 constexpr int PB2_PART = PB2_PRO + BP_PART;
 constexpr int LDT = F + 4;                    // transpose tile row stride
@@ -943,6 +993,10 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
   }
   for (int it = gw; it < n_items; it += nw) {
     const int64_t seg = w.seg;
+    // dP's descriptor for this item's rows (wave-uniform inputs made provably uniform)
+    const int64_t ibeg = __builtin_amdgcn_readfirstlane(int(w.begin));
+    const int ilen = __builtin_amdgcn_readfirstlane(int(w.end - w.begin));
+    const auto dPrs = __builtin_amdgcn_make_buffer_rsrc(dP + ibeg * F, 0, ilen * F * 4, 0x00020000);
     // per-camera constants of the attention backward (edge_cam_bwd_kernel)
     f32x4 xr[2], gv[2];
     float M[2], inv[2], delta[2];
@@ -996,6 +1050,7 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
       to_c(1, XT, XC);
       if (RES) to_c(2, RT, RC);
       // ---- camera attention backward (T layout: edge c, features 16 q + 4 g + r)
+      float tmean = 0.f, trstd = 1.f;  // LayerNorm statistics of edge c (T layout)
       if (LN) {
         float gs[2][4], bs[2][4];
 #pragma unroll
@@ -1007,7 +1062,7 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
             bs[q][r] = b[r];
           }
         }
-        phat_slabs<LN>(PT, gs, bs, eps);
+        phat_slabs_st<LN>(PT, gs, bs, eps, tmean, trstd);
       }
       f32x4 xc[2] = {vecT(2, 0), vecT(2, 1)};  // b_c, then + Wc P_hat^T
       xl_slabs<2>(reinterpret_cast<const float4*>(WcQ), PT, xc, lane);
@@ -1044,11 +1099,15 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
       to_c(3, dXc, XcC);
       // ---- LayerNorm statistics of the C-layout rows, LN backward, dP
       f32x4 ph[2];  // relu(LN(P)) (C layout) for the weight gradient
+      float dv[4][2];  // dP (C layout) for the branch-free stores (GASFM_PBWD_V2)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const bool live = 4 * g + r < nrows;
         float mean = 0.f, rstd = 1.f;
-        if (LN) {
+        if (LN && GASFM_PBWD_V2) {
+          mean = __shfl(tmean, 4 * g + r);  // edge 4 g + r's statistics live on lane c = 4 g + r
+          rstd = __shfl(trstd, 4 * g + r);
+        } else if (LN) {
           mean = sum16(PC[0][r] + PC[1][r]) * (1.f / F);
           const float d0 = PC[0][r] - mean, d1 = PC[1][r] - mean;
           rstd = rsqrtf(sum16(fmaf(d0, d0, d1 * d1)) * (1.f / F) + eps);
@@ -1072,15 +1131,26 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
           s1 = sum16(s1) * (1.f / F);
           s2 = sum16(s2) * (1.f / F);
         }
-        if (live) {
-          float* d = dP + (row0 + 4 * g + r) * F + c;
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
-            float v = LN ? rstd * (gvv[nt] - s1 - xh[nt] * s2) : gvv[nt];
-            if (RES) v += RC[nt][r];
-            d[16 * nt] = v;
-          }
+        for (int nt = 0; nt < 2; ++nt) {
+          float v = LN ? rstd * (gvv[nt] - s1 - xh[nt] * s2) : gvv[nt];
+          if (RES) v += RC[nt][r];
+          dv[r][nt] = v;
         }
+        if (!GASFM_PBWD_V2 && live) {
+          float* d = dP + (row0 + 4 * g + r) * F + c;
+          d[0] = dv[r][0];
+          d[16] = dv[r][1];
+        }
+      }
+      if (GASFM_PBWD_V2) {
+        // rows past the item's end fall outside the descriptor's range: the hardware drops them
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt)
+            __builtin_amdgcn_raw_buffer_store_b32(  // (the builtin's data operand is a 32-bit integer)
+                __float_as_uint(dv[r][nt]), dPrs, int(((row0 - ibeg + 4 * g + r) * F + 16 * nt + c) * 4), 0, 0);
       }
       // ---- dW += [dXLp | dXLc]^T relu(LN(P)), db (C layout, row 4 g + s at step s)
 #pragma unroll

@@ -101,6 +101,14 @@ def main():
         lambda: _native.edge_cam_bwd(P, ln_w, ln_b, 1e-5, W[32:].contiguous(), b[32:].contiguous(), XRc, att, bias,
                                      0.2, co, cmax, csum, gout, pc.items, pc.n_items, dXLc, dXRc, pdxr, cbp),
         E * (128 + 128) + m * 256)
+    dXLp_in, dRes_in = rnd(E, 32), rnd(E, 32)
+    rp, cp_ = _native.edge_cam_pbwd_part_shape(pc.n_items)
+    pbp = torch.empty(rp, cp_, device=dev)
+    run("edge_cam_pbwd(LN, RES)",
+        lambda: _native.edge_cam_pbwd(P, ln_w, ln_b, 1e-5, W[:32].contiguous(), W[32:].contiguous(),
+                                      b[32:].contiguous(), Wp, 0.25, XRc, att, bias, 0.2, co, cmax, csum, gout,
+                                      pc.items, pc.n_items, dXLp_in, dRes_in, dP, dXRc, pdxr, pbp),
+        E * 512 + m * 256)
     dSp = torch.empty(n, 32, device=dev)
     run("segment_rowsum", lambda: _native.segment_rowsum(pp.items, pp.n_items, pp.perm, dPo, 0.25, dSp, None),
         E * 132 + n * 128)
