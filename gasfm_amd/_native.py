@@ -146,6 +146,8 @@ _SIGS = {
     "gasfm_embed2_bwd": (_i32, [_vp, _vp, _i64, _vp, _vp]),
     "gasfm_gemm_bf16": (_i32, [_i32, _i32, _i32, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _i64, _vp]),
     "gasfm_gemm_f32": (_i32, [_i32, _i32, _i32, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _i64, _vp]),
+    "gasfm_gemm_f32_smallm_ok": (_i32, [_i32, _i32, _i32, _i32]),
+    "gasfm_gemm_f32_smallm": (_i32, [_i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp]),
 }
 
 _lib = None
@@ -1220,6 +1222,43 @@ def gemm_bf16(a, b, cin=None, bias=None, out=None):
     a [M, K], b [K, N]: fp32 CUDA tensors, each with a unit stride along one dimension (plain
     row-major tensors and their .t() views both qualify: x @ W.t(), dy @ W, dy.t() @ x)."""
     return _gemm(lib().gasfm_gemm_bf16, "gasfm_gemm_bf16", a, b, cin, bias, out)
+
+
+def gemm_f32_smallm(a, b, cin=None, bias=None, out=None):
+    """out = a @ b (+ cin) (+ bias) on the small-row-count fp32 MFMA kernels (csrc/gemm_smallm.hip),
+    or None when the operand form / shape is not one of theirs: a @ W.t() (mode 0: a, W row-major),
+    a @ W (mode 1, no epilogue), A.t() @ B (mode 2: A, B row-major, short K, no epilogue)."""
+    if not (a.is_cuda and b.is_cuda and a.dtype == torch.float32 and b.dtype == torch.float32
+            and a.dim() == 2 and b.dim() == 2 and a.shape[1] == b.shape[0]):
+        return None
+    M, K = a.shape
+    N = b.shape[1]
+    L = lib()
+    if a.stride(1) == 1 and a.stride(0) % 4 == 0:
+        if b.stride(0) == 1 and b.stride(1) % 4 == 0:  # b = W.t(), W [N, K] row-major
+            mode, A, lda, B, ldb = 0, a, a.stride(0), b, b.stride(1)
+        elif b.stride(1) == 1 and cin is None and bias is None:  # b = W [K, N] row-major
+            mode, A, lda, B, ldb = 1, a, a.stride(0), b, b.stride(0)
+        else:
+            return None
+        I, J = M, N
+    elif a.stride(0) == 1 and b.stride(1) == 1 and cin is None and bias is None:  # a = A.t(), A [K, M]
+        mode, A, lda, B, ldb = 2, a, a.stride(1), b, b.stride(0)
+        I, J = M, N
+    else:
+        return None
+    if not L.gasfm_gemm_f32_smallm_ok(mode, I, J, K):
+        return None
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    if out.shape != (M, N) or out.stride(1) != 1 or (cin is not None and (cin.shape != (M, N) or cin.stride(1) != 1)):
+        return None
+    if bias is not None and (bias.shape != (N,) or not bias.is_contiguous()):
+        return None
+    st = L.gasfm_gemm_f32_smallm(mode, I, J, K, _p(A), lda, _p(B), ldb, _p(bias), _p(cin),
+                                 cin.stride(0) if cin is not None else 0, _p(out), out.stride(0), _stream(out))
+    check(st, "gasfm_gemm_f32_smallm")
+    return out
 
 
 def gemm_f32(a, b, cin=None, bias=None, out=None):

@@ -36,6 +36,10 @@ def _f32(*shape, like):
 # at m = 125 the HIP kernel 12-16 us vs 19 us standalone, but the whole emulated rank-of-8 step
 # 10.33 ms vs 9.97 ms with hipBLASLt, so hipBLASLt stays the default.
 FP32_GEMM = os.environ.get("GASFM_VIEW_GEMM", "torch")
+# fp32 products with at most this many camera rows (a camera-sharded rank's 125, a training
+# batch's ~60) go to csrc/gemm_smallm.hip (1,024 waves of 16 x 32 tiles x K-quarters) instead of
+# hipBLASLt, whose 125 x 1024 x 1024 tiles take ~11.5 us; 0 disables
+SMALLM_ROWS = int(os.environ.get("GASFM_SMALLM_ROWS", "256"))
 
 
 def _mm(a, b, cin=None, bias=None, bf16=False, out=None):
@@ -45,6 +49,12 @@ def _mm(a, b, cin=None, bias=None, bf16=False, out=None):
         return _native.gemm_bf16(a, b, cin=cin, bias=bias, out=out)
     if FP32_GEMM == "hip":
         return _native.gemm_f32(a, b, cin=cin, bias=bias, out=out)
+    # the row count is a's rows (x W^T, dy W) or the shared K (dy^T x)
+    rows = a.shape[0] if a.stride(1) == 1 else a.shape[1]
+    if rows <= SMALLM_ROWS:
+        y = _native.gemm_f32_smallm(a, b, cin=cin, bias=bias, out=out)
+        if y is not None:
+            return y
     if cin is not None:
         if out is cin and bias is None:
             return cin.addmm_(a, b)
@@ -129,7 +139,7 @@ class ViewHubFn(torch.autograd.Function):
         if ctx.bf16 or FP32_GEMM == "hip":  # the MFMA kernels add d skip in their epilogue
             dacc = _mm(dXL, Wl, cin=dskip.contiguous() if dskip is not None else None, bf16=ctx.bf16)
         else:  # hipBLASLt: d skip is added by the hub kernel's second pass (no addmm input copy)
-            dacc = dXL @ Wl
+            dacc = _mm(dXL, Wl)
             dres = dskip.contiguous() if dskip is not None else None
         dWl = _mm(dXL.t(), v, bf16=ctx.bf16)
         cols = _native.view_hub_part_cols(D)

@@ -667,6 +667,17 @@ int gasfm_gemm_f32(int32_t M, int32_t N, int32_t K, const float* A, int64_t sAm,
                    const float* B, int64_t sBk, int64_t sBn, const float* Cin, int64_t ldCin,
                    const float* bias, float* C, int64_t ldC, void* stream);
 
+/* fp32 MFMA GEMMs for small row counts (gemm_smallm.hip: a camera-sharded rank's m / W view rows):
+ *   mode 0  C[M,N] = A[M,K] W[N,K]^T (+ bias[N]) (+ Cin[M,N]); A, W row-major (lda, ldb)
+ *   mode 1  C[M,N] = A[M,K] W[K,N]; bias / Cin must be null
+ *   mode 2  C[M,N] = A[K,M]^T B[K,N] (K: rows, any); bias / Cin must be null
+ * gasfm_gemm_f32_smallm_ok says whether (mode, M, N, K) is supported (modes 0 / 1: K % 64 == 0,
+ * N % 32 == 0; mode 2: M % 16 == 0, N % 128 == 0).  Cin may alias C. */
+int32_t gasfm_gemm_f32_smallm_ok(int32_t mode, int32_t M, int32_t N, int32_t K);
+int gasfm_gemm_f32_smallm(int32_t mode, int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B,
+                          int64_t ldb, const float* bias, const float* Cin, int64_t ldCin, float* C, int64_t ldC,
+                          void* stream);
+
 /* ---- outlier injection (outliers.hip) -----------------------------------
  * Replaces OutlierInjector / inject_outliers (code/utils/dataset_utils.py:159-461), the per-sample
  * transform of the outlier-injected training loop (train.py:73-81, BASELINE config 5).  The

@@ -1,4 +1,4 @@
-"""gasfm_gemm_f32 vs torch (hipBLASLt) on the camera-side shapes: y = x W^T, dx = dy W, dW = dy^T x
+"""gasfm_gemm_f32 and gasfm_gemm_f32_smallm vs torch (hipBLASLt) on the camera-side shapes: y = x W^T, dx = dy W, dW = dy^T x
 at m = 1000 and m = 125 (HIP events, 50 back-to-back launches each)."""
 import torch
 
@@ -24,13 +24,16 @@ def main():
         x = torch.randn(m, D, device=dev)
         dy = torch.randn(m, D, device=dev)
         fl = 2 * m * D * D
-        for name, hip, ref in (
-                ("fwd  x W^T", lambda: _native.gemm_f32(x, W.t()), lambda: x @ W.t()),
-                ("dgrad dy W", lambda: _native.gemm_f32(dy, W), lambda: dy @ W),
-                ("wgrad dy^T x", lambda: _native.gemm_f32(dy.t(), x), lambda: dy.t() @ x)):
+        for name, hip, ref, sm in (
+                ("fwd  x W^T", lambda: _native.gemm_f32(x, W.t()), lambda: x @ W.t(),
+                 lambda: _native.gemm_f32_smallm(x, W.t())),
+                ("dgrad dy W", lambda: _native.gemm_f32(dy, W), lambda: dy @ W, lambda: _native.gemm_f32_smallm(dy, W)),
+                ("wgrad dy^T x", lambda: _native.gemm_f32(dy.t(), x), lambda: dy.t() @ x,
+                 lambda: _native.gemm_f32_smallm(dy.t(), x))):
             th, tr = t(hip), t(ref)
+            ts = t(sm) if m <= 256 else float("nan")
             print(f"m={m:5d} {name:14s} hip {th:7.2f} us ({fl / th / 1e6:6.1f} TF/s)   torch {tr:7.2f} us "
-                  f"({fl / tr / 1e6:6.1f} TF/s)", flush=True)
+                  f"({fl / tr / 1e6:6.1f} TF/s)   smallm {ts:7.2f} us", flush=True)
 
 
 if __name__ == "__main__":
