@@ -80,3 +80,35 @@ def test_batch_structure(device):
     assert b.graph_wrappers["scenepoint2global"].plan.num_targets == 2
     key = b.x.indices[0] * b.x.shape[1] + b.x.indices[1]
     assert bool((key[1:] > key[:-1]).all())  # still camera-major
+
+
+def test_batch_reads_scene_build_arrays_without_building_graphs(device):
+    """Device-built scenes build their graph wrappers on first use (scene_device, round 3): the union
+    batch and ESFMLoss read the scene-build arrays, so no per-scene plan is built, and the union's
+    plans -- hence the outputs -- are bitwise those of a batch built from the scenes' plans."""
+    torch.manual_seed(2)
+    conf = _conf()
+    net = gasfm_amd.GraphAttnSfMNet(conf).to(device)
+    lossf = ESFMLoss(conf)
+    datas = _scenes(device)
+    assert all("graph_wrappers" not in d.__dict__ for d in datas)
+    with torch.no_grad():
+        pred = forward_batch(net, datas)
+        loss = sum(lossf(p, d) for p, d in zip(pred, datas))
+    assert all("graph_wrappers" not in d.__dict__ for d in datas)
+    lazy = SceneBatch(datas)
+    for d in datas:
+        d.graph_wrappers  # noqa: B018  (build them: SceneBatch then reads the plans)
+    eager = SceneBatch(datas)
+    for name in ("proj2view", "proj2scenepoint", "view2global", "scenepoint2global"):
+        a, b = lazy.graph_wrappers[name].plan, eager.graph_wrappers[name].plan
+        for k in ("seg_ptr", "items", "combine"):
+            assert torch.equal(getattr(a, k).cpu(), getattr(b, k).cpu()), (name, k)
+        assert (a.perm is None) == (b.perm is None) and (a.perm is None or torch.equal(a.perm.cpu(), b.perm.cpu()))
+        assert (a.n_slots, a.n_items, a.n_part_rows) == (b.n_slots, b.n_items, b.n_part_rows)
+    with torch.no_grad():
+        pred2 = forward_batch(net, datas)
+        loss2 = sum(lossf(p, d) for p, d in zip(pred2, datas))
+    for p, q in zip(pred, pred2):
+        assert torch.equal(p["Ps_norm"], q["Ps_norm"]) and torch.equal(p["pts3D"], q["pts3D"])
+    assert torch.equal(loss, loss2)
