@@ -151,3 +151,41 @@ def test_device_plan_work_restatement_matches_host():
                 np.testing.assert_array_equal(l1.numpy(), l12.numpy())
         n_two_level += l1 is not None
     assert n_two_level > 10
+
+
+def test_lazy_graph_wrappers_and_scene_csr():
+    """SceneData built on the device carries a graph-wrapper builder instead of the wrappers
+    (scene_device.scene_from_dense_device): the builder runs once, on first access, and before a
+    .to() copy; loss.scene_csr reads the scene-build arrays until then, the plans afterwards."""
+    import torch
+    from gasfm_amd import SceneData, synthetic
+    from gasfm_amd.loss import scene_csr
+    sc = synthetic.scaled_config4(0.002, seed=1)
+    host = SceneData.from_synthetic(sc)
+    gw = host.graph_wrappers
+    calls = []
+    d = SceneData.__new__(SceneData)
+    d.__dict__.update({k: v for k, v in host.__dict__.items() if k != "graph_wrappers"})
+    pv, ps = gw["proj2view"].plan, gw["proj2scenepoint"].plan
+    perm = ps.perm if ps.perm is not None else torch.arange(ps.num_edges, dtype=torch.int32)
+    d._scene_build = {"cam_ptr": pv.seg_ptr, "pt_ptr": ps.seg_ptr, "perm": perm, "pos": ps.pos,
+                      "pt": host.x.indices[1].to(torch.int32)}
+    d._lazy_graph = lambda: calls.append(1) or gw
+    caches, cam_ptr, pt_ptr, pt_perm = scene_csr(d)
+    assert calls == [] and cam_ptr is pv.seg_ptr and pt_ptr is ps.seg_ptr and pt_perm is perm
+    caches["x"] = 1
+    assert scene_csr(d)[0] is caches  # one cache per source
+    assert d.graph_wrappers is gw and calls == [1]
+    assert d.graph_wrappers is gw and calls == [1]  # built once
+    assert scene_csr(d)[1] is pv.seg_ptr  # from the plans now
+    d2 = SceneData.__new__(SceneData)
+    d2.__dict__.update(d.__dict__)
+    d2.__dict__.pop("graph_wrappers")
+    d2._lazy_graph = lambda: calls.append(2) or gw
+    moved = d2.to("cpu")
+    assert calls == [1, 2] and "_scene_build" not in moved.__dict__ and "_lazy_graph" not in moved.__dict__
+    try:
+        SceneData.__new__(SceneData).graph_wrappers
+        raise AssertionError("expected AttributeError")
+    except AttributeError:
+        pass
