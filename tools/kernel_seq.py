@@ -2,7 +2,8 @@
 to the previous kernel's end, workgroups, name.
 
 usage: python tools/kernel_seq.py <run_results.db> [block] [step]
-The forward of block b starts at its edge_prologue_fwd<true>; the listing runs to the next one
+The forward of block b starts at its prologue (edge_prologue_fwd<true>, edge_cam_fwd<true> or the
+forward seam edge_seam_fwd); the listing runs to the next one
 (pass block -1 for the whole backward of the step instead)."""
 import re
 import sqlite3
@@ -22,7 +23,8 @@ def main():
     st = [i for i, r in enumerate(rows) if "edge0_prologue_fwd" in r[0]]
     seg = rows[st[step]:st[step + 1]]
     if blk >= 0:
-        idx = [i for i, r in enumerate(seg) if "edge_prologue_fwd_kernel<true>" in r[0] or "edge_cam_fwd_kernel<true>" in r[0]]
+        idx = [i for i, r in enumerate(seg) if "edge_prologue_fwd_kernel<true>" in r[0] or "edge_cam_fwd_kernel<true>" in r[0]
+               or "edge_seam_fwd_kernel" in r[0]]
         seg = seg[idx[blk]:idx[blk + 1]]
     else:
         first_bwd = next(i for i, r in enumerate(seg) if "bwd" in r[0])
