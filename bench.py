@@ -40,6 +40,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_F32_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_16x16x4_f32): 64 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz
 PBWD_FLOP_PER_EDGE = 12288  # XLc recompute 2,048 + dP_hat (3 products, K = 32) 6,144 + dW (64 x 32) 4,096
 PBWD_BYTES_PER_EDGE = 512  # P, dXL point half, dRes read, dP written (camera rows once: + 160 B per camera)
+# with the edge epilogue's backward folded in (edge_block.EPI_FOLD, edge_cam_pbwd<.., EPI, DWP>): + dWp
+# (32 x 34: 2,176) + dP0 (2 x 32 dots: 128) FLOP, + P0 read 8 + dP0 written 8 bytes per edge
+PBWD_FOLD_FLOP_PER_EDGE = PBWD_FLOP_PER_EDGE + 2176 + 128
+PBWD_FOLD_BYTES_PER_EDGE = PBWD_BYTES_PER_EDGE + 16
 PMC_KERNELS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r3_pmc_kernels.txt")
 
 
@@ -285,8 +289,15 @@ def main():
     timer = attention.KernelTimer(lambda tag, HC: tag == "proj2scenepoint" and HC == 32)
     attention.KERNEL_TIMER = timer
     timer.enabled = True
-    # the dominant kernel: edge_cam_pbwd with LayerNorm and the residual term (blocks 1..11)
-    pbwd = LaunchTimer("edge_cam_pbwd", lambda *a, **k: a[1] is not None and a[7] is not None)
+    # the dominant kernel: edge_cam_pbwd with LayerNorm and the residual term (blocks 1..11); with the
+    # epilogue fold, its launches that carry both epilogue parts (blocks 2..11)
+    from gasfm_amd import edge_block
+    fold = edge_block.EPI_FOLD
+    pbwd = LaunchTimer("edge_cam_pbwd", lambda *a, **k: a[1] is not None and a[7] is not None
+                       and (not fold or (k.get("epi") is not None and k.get("dwp") is not None)))
+    flop_e = PBWD_FOLD_FLOP_PER_EDGE if fold else PBWD_FLOP_PER_EDGE
+    bytes_e = PBWD_FOLD_BYTES_PER_EDGE if fold else PBWD_BYTES_PER_EDGE
+    pbwd_name = "edge_cam_pbwd_kernel<true, true, true, true>" if fold else "edge_cam_pbwd_kernel<true, true, false, false>"
     for _ in range(2):
         fwd_bwd()
     timer.enabled = False
@@ -294,8 +305,8 @@ def main():
     pbwd_ms = pbwd.close()
     pbwd_launches = len(pbwd.events)
     e_cam = data.graph_wrappers["proj2view"].plan.num_edges
-    pbwd_tfs = PBWD_FLOP_PER_EDGE * e_cam / (pbwd_ms * 1e-3) / 1e12 if pbwd_ms else None
-    pbwd_gbs = PBWD_BYTES_PER_EDGE * e_cam / (pbwd_ms * 1e-3) / 1e9 if pbwd_ms else None
+    pbwd_tfs = flop_e * e_cam / (pbwd_ms * 1e-3) / 1e12 if pbwd_ms else None
+    pbwd_gbs = bytes_e * e_cam / (pbwd_ms * 1e-3) / 1e9 if pbwd_ms else None
     kern_ms = timer.mean_ms()
     b2b_ms = timer.replay_ms(20)
     plan = data.graph_wrappers["proj2scenepoint"].plan
@@ -332,15 +343,16 @@ def main():
                                        if emul else
                                        f"{'point+camera' if data.shard.cams is not None else 'point'}-sharded x{world}"
                                        if dist_on else "single GPU")},
-            "roofline": {"kernel": "edge_cam_pbwd_kernel<true,true>: camera-attention + edge-prologue backward "
-                                   "(the step's largest kernel), per launch",
+            "roofline": {"kernel": pbwd_name + ": camera-attention + edge-prologue backward"
+                                   + (" + the edge epilogue's backward (dSv, dP0 of the previous block, dWp of this "
+                                      "one)" if fold else "") + " (the step's largest kernel), per launch",
                          "bound": "mfma", "achieved": pbwd_tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": (pbwd_tfs / MFMA_F32_PEAK_TFS) if pbwd_tfs else None,
-                         "traffic": pmc_kernel_traffic("edge_cam_pbwd_kernel<true, true>", e_cam),
+                         "traffic": pmc_kernel_traffic(pbwd_name, e_cam),
                          "traffic_source": "profiles/r3_pmc_kernels.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                                            "passes of this bench, per launch; 1.00x the algorithmic bytes)",
-                         "flop_per_launch": PBWD_FLOP_PER_EDGE * e_cam,
-                         "algorithmic_bytes": PBWD_BYTES_PER_EDGE * e_cam,
+                         "flop_per_launch": flop_e * e_cam,
+                         "algorithmic_bytes": bytes_e * e_cam,
                          "hbm_achieved_GBps": pbwd_gbs,
                          "hbm_frac": (pbwd_gbs / HBM_PEAK_GBS) if pbwd_gbs else None,
                          "mean_us": pbwd_ms * 1e3 if pbwd_ms else None, "launches_timed": pbwd_launches,

@@ -59,6 +59,9 @@ _SIGS = {
     "gasfm_edge_cam_pbwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _f32, _vp, _i64, _vp, _vp, _f32, _vp,
                                    _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _vp, _i64, _vp,
                                    _vp, _vp]),
+    "gasfm_edge_cam_pbwd_ex": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _f32, _vp, _i64, _vp, _vp, _f32,
+                                      _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _vp, _i64,
+                                      _vp, _vp, _i64, _vp, _i32, _f32, _vp, _vp, _vp, _vp, _i32, _vp]),
     "gasfm_edge_cam_fwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32,
                                   _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
     "gasfm_edge_cam_bwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _vp, _i64,
@@ -625,23 +628,44 @@ def edge_seam_fwd(Pb, P0, pt, lnw_b, lnb_b, eps_b, Wp, bp, Sp, Sv, Sg, scale, Po
     check(st, "gasfm_edge_seam_fwd")
 
 
-def edge_cam_pbwd_part_shape(n_items):
+def edge_cam_pbwd_part_shape(n_items, dwp_cols=0):
+    """(rows, cols) of edge_cam_pbwd's part buffer; dwp_cols = 32 or 34 with the dWp block (dwp)."""
     L = lib()
-    return int(L.gasfm_edge_cam_pbwd_part_rows(n_items)), int(L.gasfm_edge_cam_pbwd_part_cols())
+    return int(L.gasfm_edge_cam_pbwd_part_rows(n_items)), int(L.gasfm_edge_cam_pbwd_part_cols()) + 32 * dwp_cols
 
 
 def edge_cam_pbwd(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, scale, XR, att, bias, slope, out, seg_max, seg_sum, gout,
-                  plan_items, n_items, dXLp, dRes, dP, dXR, part_dxr, part, ldStat=4):
+                  plan_items, n_items, dXLp, dRes, dP, dXR, part_dxr, part, ldStat=4, epi=None, dwp=None):
     """The camera attention's backward and the block's edge prologue backward in one pass
     (csrc/edge_cam.hip edge_cam_pbwd): dP, dXR (+ split partials), part rows
-    [dW 64x32 | db 64 | dgamma 32 | dbeta 32 | datt 32 | dbias 32] per workgroup."""
+    [dW 64x32 | db 64 | dgamma 32 | dbeta 32 | datt 32 | dbias 32] per workgroup.
+
+    epi = (We, scale_e, dSv, part_dsv, dP0 or None): also the previous block's edge-epilogue
+    gradients from this dP (dSv rows / split-camera partial rows of the same plan, dP0).
+    dwp = P0 or None (requires ln_w and dRes): also this block's lin_proj weight gradient,
+    [32 x (32 | 34)] appended to each part row (part has edge_cam_pbwd_part_shape(n, dwp=...) columns)."""
     _req(P, "P", 32)
     ldXR = _rows32(XR, "XR")
-    st = lib().gasfm_edge_cam_pbwd(_p(P), _p(ln_w), _p(ln_b), eps, _p(Wpt), _p(Wc), _p(bc), _p(Wp),
-                                   Wp.stride(0) if Wp is not None else 0, scale, _p(XR), ldXR, _p(att), _p(bias),
-                                   slope, _p(out), out.stride(0), _p(seg_max), _p(seg_sum), ldStat, _p(gout),
-                                   gout.stride(0), _p(plan_items), n_items, _p(dXLp), dXLp.stride(0), _p(dRes),
-                                   _p(dP), _p(dXR), dXR.stride(0), _p(part_dxr), _p(part), _stream(P))
+    We = dSv = part_dsv = dP0 = None
+    scale_e, ldWe = 0.0, 0
+    if epi is not None:
+        We, scale_e, dSv, part_dsv, dP0 = epi
+        _req(dSv, "dSv", 32)
+        if dP0 is not None:
+            _req(dP0, "dP0", 2)
+        ldWe = We.stride(0)
+    P0, ldWpo = None, 0
+    if dwp is not False and dwp is not None:
+        P0 = dwp if isinstance(dwp, torch.Tensor) else None
+        ldWpo = 34 if P0 is not None else 32
+    if P0 is not None:
+        _req(P0, "P0", 2)
+    st = lib().gasfm_edge_cam_pbwd_ex(_p(P), _p(ln_w), _p(ln_b), eps, _p(Wpt), _p(Wc), _p(bc), _p(Wp),
+                                      Wp.stride(0) if Wp is not None else 0, scale, _p(XR), ldXR, _p(att), _p(bias),
+                                      slope, _p(out), out.stride(0), _p(seg_max), _p(seg_sum), ldStat, _p(gout),
+                                      gout.stride(0), _p(plan_items), n_items, _p(dXLp), dXLp.stride(0), _p(dRes),
+                                      _p(dP), _p(dXR), dXR.stride(0), _p(part_dxr), _p(part), part.stride(0), _p(We),
+                                      ldWe, scale_e, _p(dSv), _p(part_dsv), _p(dP0), _p(P0), ldWpo, _stream(P))
     check(st, "gasfm_edge_cam_pbwd")
 
 

@@ -438,6 +438,19 @@ struct SeamEpi {
 #ifndef GASFM_SEAM_V2
 #define GASFM_SEAM_V2 0
 #endif
+// 1: the Sp[pt] rows of the next tile are gathered half a tile ahead (issued after this tile's P'
+// store, from the next tile's point indices, which are loaded first of the next tile's requests);
+// 0: gathered at the start of their own tile, hidden only behind LN_b and the epilogue product.
+#ifndef GASFM_SEAM_SPPF
+#define GASFM_SEAM_SPPF 1
+#endif
+// 1: the P' and XL stores are unconditional (a lane past the item's end rewrites its clamped row
+// with that row's own values, as in GASFM_SEAM_V2), so no store sits under a branch and the
+// compiler's vmcnt bookkeeping stays exact (a store under a branch makes every later wait assume
+// the store-free path, i.e. wait for younger loads too)
+#ifndef GASFM_SEAM_UST
+#define GASFM_SEAM_UST 1
+#endif
 template <bool LN>
 __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kernel(
     SeamEpi ep, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
@@ -482,19 +495,40 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
   float2 nq = make_float2(0.f, 0.f);
   const int32_t* posp = pos ? pos : reinterpret_cast<const int32_t*>(ep.P);
   const float* p0p = ep.P0 ? ep.P0 : ep.P;
+  f32x4 nsp[2];  // GASFM_SEAM_SPPF: Sp[pt] of the next tile
   auto issue = [&](int64_t row0, int nrows) {
-    load_slabs32(ep.P, row0, nrows, ns, lane);
     const int64_t e = row0 + (c < nrows ? c : 0);
+    if (GASFM_SEAM_SPPF) npt = ep.pt[e];  // first: waiting for it does not wait for the P rows
+    load_slabs32(ep.P, row0, nrows, ns, lane);
     npos = posp[e];
-    npt = ep.pt[e];
+    if (!GASFM_SEAM_SPPF) npt = ep.pt[e];
     nq = *reinterpret_cast<const float2*>(p0p + e * 2);
+  };
+  auto issue_sp = [&]() {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float4 t = *reinterpret_cast<const float4*>(ep.Sp + int64_t(npt) * F + 16 * q + 4 * g);
+      nsp[q] = f32x4{t.x, t.y, t.z, t.w};
+    }
+  };
+  // an item's first tile outside the tile loop: the Sp rows before the P rows, so that (as on the
+  // loop's own path, where the tile's stores follow them) younger requests follow the Sp rows when
+  // the loop is entered -- the compiler's wait counts are the minimum over the entering paths
+  auto issue_first = [&](int64_t row0, int nrows) {
+    if (GASFM_SEAM_SPPF) {
+      npt = ep.pt[row0 + (c < nrows ? c : 0)];
+      issue_sp();
+    }
+    issue(row0, nrows);
   };
   auto rows_at = [](const gasfm_work_item& w, int64_t row0) { return int(w.end - row0 < TR ? w.end - row0 : TR); };
 
   gasfm_work_item w{0, 0, 0, -1};
   if (gw < n_items) {
     w = items[gw];
-    if (w.begin < w.end) issue(w.begin, rows_at(w, w.begin));
+    if (w.begin < w.end) {
+      issue_first(w.begin, rows_at(w, w.begin));
+    }
   }
   for (int it = gw; it < n_items; it += nw) {
     const int64_t seg = w.seg;
@@ -511,10 +545,17 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
     gasfm_work_item wn{0, 0, 0, -1};
     const bool more = it + nw < n_items;
     if (more) wn = items[it + nw];
-    if (w.begin >= w.end && more && wn.begin < wn.end) issue(wn.begin, rows_at(wn, wn.begin));
+    if (w.begin >= w.end && more && wn.begin < wn.end) {
+      issue_first(wn.begin, rows_at(wn, wn.begin));
+    }
     for (int64_t row0 = w.begin; row0 < w.end; row0 += TR) {
       const int nrows = rows_at(w, row0);
       f32x4 pb[2] = {ns[0], ns[1]};
+      f32x4 sp[2];
+      if (GASFM_SEAM_SPPF) {
+        sp[0] = nsp[0];
+        sp[1] = nsp[1];
+      }
       const int64_t dst = pos ? int64_t(npos) : row0 + c;
       const int32_t ptc = npt;
       const float2 q0 = nq;
@@ -530,12 +571,12 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
         }
         issue(r1, n1);
       }
-      // Sp[pt] of edge c: its latency overlaps LN_b and the epilogue product
-      f32x4 sp[2];
+      if (!GASFM_SEAM_SPPF) {  // Sp[pt] of edge c: its latency overlaps LN_b and the epilogue product
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const float4 t = *reinterpret_cast<const float4*>(ep.Sp + int64_t(ptc) * F + 16 * q + 4 * g);
-        sp[q] = f32x4{t.x, t.y, t.z, t.w};
+        for (int q = 0; q < 2; ++q) {
+          const float4 t = *reinterpret_cast<const float4*>(ep.Sp + int64_t(ptc) * F + 16 * q + 4 * g);
+          sp[q] = f32x4{t.x, t.y, t.z, t.w};
+        }
       }
       const bool valid = c < nrows;
       // ---- epilogue of block b (T layout)
@@ -563,11 +604,18 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
         for (int r = 0; r < 4; ++r) {
           float d = y[q][r] + cs[r];
           d = fmaf(w32[r], q0.x, fmaf(w33[r], q0.y, d));
-          d += sp[q][r] + sv[q][r];
+          // (d + Sv) + Sp: the gathered Sp row is consumed last (not hoisted to the tile's top)
+          d = GASFM_SEAM_SPPF ? (d + sv[q][r]) + sp[q][r] : d + (sp[q][r] + sv[q][r]);
           pn[q][r] = fmaf(d, ep.scale, pb[q][r]);
         }
       }
-      if (GASFM_SEAM_V2 || valid) {
+      if (GASFM_SEAM_SPPF) {
+        // not hoisted towards the point-index load it waits for: the address is formed from npt
+        // only once P' exists
+        asm volatile("" : "+v"(npt) : "v"(pn[0][0]), "v"(pn[1][3]));
+        issue_sp();
+      }
+      if (GASFM_SEAM_V2 || GASFM_SEAM_UST || valid) {
         const int64_t prow = row0 + (valid ? c : 0);
 #pragma unroll
         for (int q = 0; q < 2; ++q)
@@ -590,7 +638,7 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
       }
       f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
       xl_slabs<4>(reinterpret_cast<const float4*>(Wl), pn, acc, lane);
-      if (GASFM_SEAM_V2 || valid) {
+      if (GASFM_SEAM_V2 || GASFM_SEAM_UST || valid) {
         typedef float v4f __attribute__((ext_vector_type(4)));
 #pragma unroll
         for (int ot = 0; ot < 2; ++ot) {
@@ -878,6 +926,26 @@ __global__ __launch_bounds__(kThreads, GASFM_CAM_MINW) void edge_cam_bwd_kernel(
 constexpr int PB2_PRO = NX * F + NX + 2 * F;  // the prologue_bwd part row
 constexpr int PB2_PART = PB2_PRO + BP_PART;
 constexpr int LDT = F + 4;                    // transpose tile row stride
+constexpr int PB_NDW = 20;                    // (DWP) per-lane dWp sums: 16 MFMA values + 4 P0 terms
+
+// The edge epilogues' backward folded into edge_cam_pbwd (round 3).  With SeamFn, the kernel that
+// produces block b+1's dP is the one place where block b's epilogue gradient dP' (= that dP) is in
+// registers in camera order, and block b's own edge_cam_pbwd later holds both dRes (= dP') and
+// relu(LN_b(P_b)):
+//   EPI (block b+1's launch): dSv_b[cam] = scale_e sum_e dP[e] (per camera item; split cameras as
+//     partial rows), dP0_b[e] = scale_e We[:, 32:34]^T dP[e]
+//   DWP (block b's launch): dWp_b = scale sum_e dRes[e]^T [relu(LN(P[e])) | P0[e]] as part rows
+// which is everything edge_epilogue_bwd computed except dSp (segment_rowsum, point order).
+struct PbwdEpi {
+  const float* We;    // EPI: the previous block's lin_proj weight [32 x ldWe]
+  int ldWe;
+  float scale;        // EPI: the previous block's epilogue scale
+  float* dSv;         // EPI: [m, 32]
+  float* part_dsv;    // EPI: split-camera partial rows
+  float* dP0;         // EPI: [E, 2] or null (no P0 skip input)
+  const float* P0;    // DWP: [E, 2] or null
+  int ldWpo;          // DWP: dWp row width in the part row (34 with P0, 32 without)
+};
 
 // C-layout rows of a [*, 32] tensor: v[ft][r] = X[row0 + 4 g + r][16 ft + c] (rows clamped, not masked)
 __device__ __forceinline__ void cl_load32(const float* __restrict__ X, int64_t ld, int64_t row0, int nrows,
@@ -911,8 +979,22 @@ __device__ __forceinline__ void prod_c2(const float4* __restrict__ Q, const f32x
   }
 }
 
-template <bool LN, bool RES>
-__global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
+#ifndef GASFM_PBWD_MINW
+#define GASFM_PBWD_MINW 2
+#endif
+// EPI's dP0: 1 = dP back to the T layout through tile 0 (a dot per lane, 2 cross-group sums per
+// row tile); 0 = eight 16-lane DPP sums per tile.  DWP's LDS sums: 1 = float4 read-modify-writes
+// (lane-major), 0 = scalar.  tools/gpu_pbwd_ab.sh, same box (us per launch, EPI+DWP): 785-790 with
+// (1, 1), 792-798 with (0, 1), 775 with (1, 0, the default), 788-791 with (0, 0); the unfolded
+// kernel 655-672 there, i.e. the fold adds ~110 us where edge_epilogue_bwd took ~220.
+#ifndef GASFM_PBWD_EPI_T
+#define GASFM_PBWD_EPI_T 1
+#endif
+#ifndef GASFM_PBWD_LW4
+#define GASFM_PBWD_LW4 0
+#endif
+template <bool LN, bool RES, bool EPI, bool DWP>
+__global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kernel(
     const float* __restrict__ P, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
     const float* __restrict__ Wpt, const float* __restrict__ Wc, const float* __restrict__ bc,
     const float* __restrict__ Wp, int ldWp, float scale, const float* __restrict__ XR, int64_t ldXR,
@@ -920,18 +1002,22 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
     int64_t ldOut, const float* __restrict__ seg_max, const float* __restrict__ seg_sum, int64_t ldStat,
     const float* __restrict__ gout, int64_t ldG, const gasfm_work_item* __restrict__ items, int n_items,
     const float* __restrict__ dXLp, int64_t ldXp, const float* __restrict__ dRes, float* __restrict__ dP,
-    float* __restrict__ dXR, int64_t ldDXR, float* __restrict__ part_dxr, float* __restrict__ part) {
+    float* __restrict__ dXR, int64_t ldDXR, float* __restrict__ part_dxr, float* __restrict__ part, int64_t ldPart,
+    PbwdEpi ep) {
+  static_assert(!DWP || (LN && RES), "edge_cam_pbwd: the epilogue weight gradient needs relu(LN(P)) and dRes");
   // LDS: weight slabs (Wc for XLc; Wpt^T, Wc^T, (scale Wp)^T for dP_hat), the per-feature vectors,
-  // and per wave four 16 x 32 transpose tiles (T -> C layout of P, dXLp, dRes, dXLc)
+  // per wave four 16 x 32 transpose tiles (T -> C layout of P, dXLp, dRes, dXLc), and (DWP) per
+  // wave the lanes' running dWp sums
   constexpr int QW = F * F;  // floats per 32 x 32 slab set
-  constexpr int OV = 4 * QW, OT = OV + 4 * F, WT = 4 * TR * LDT;
-  constexpr int NL = OT + kWaves * WT;
+  constexpr int OV = 4 * QW, OT = OV + (EPI ? 6 : 4) * F, WT = 4 * TR * LDT;
+  constexpr int OD = OT + kWaves * WT;
+  constexpr int NL = OD + (DWP ? kWaves * PB_NDW * kW : 0);
   __shared__ __attribute__((aligned(16))) float lds[NL];
   float* WcQ = lds;
   float* WptTQ = lds + QW;
   float* WcTQ = lds + 2 * QW;
   float* WqTQ = lds + 3 * QW;
-  float* V = lds + OV;  // [gamma | beta | bc | att] (32 each)
+  float* V = lds + OV;  // [gamma | beta | bc | att] (32 each), (EPI) [scale_e We[:, 32] | scale_e We[:, 33]]
   stage_slabs32<F, kThreads>([&](int q) { return Wc[q]; }, WcQ);
   stage_slabs32<F, kThreads>([&](int q) { return Wpt[(q % F) * F + q / F]; }, WptTQ);
   stage_slabs32<F, kThreads>([&](int q) { return Wc[(q % F) * F + q / F]; }, WcTQ);
@@ -941,10 +1027,19 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
     V[F + threadIdx.x] = LN ? bet[threadIdx.x] : 0.f;
     V[2 * F + threadIdx.x] = bc[threadIdx.x];
     V[3 * F + threadIdx.x] = att[threadIdx.x];
+    if (EPI) {
+      V[4 * F + threadIdx.x] = ep.dP0 ? ep.scale * ep.We[threadIdx.x * ep.ldWe + 32] : 0.f;
+      V[5 * F + threadIdx.x] = ep.dP0 ? ep.scale * ep.We[threadIdx.x * ep.ldWe + 33] : 0.f;
+    }
   }
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
   float* Tt = lds + OT + wave * WT;  // tiles 0: P, 1: dXLp, 2: dRes, 3: dXLc
+  float* Lw = lds + OD + wave * PB_NDW * kW;  // (DWP) value k of this lane at Lw[lane * PB_NDW + k]
+  if (DWP) {
+#pragma unroll
+    for (int k = 0; k < PB_NDW; ++k) Lw[lane * PB_NDW + k] = 0.f;
+  }
   const float gC[2] = {LN ? gam[c] : 1.f, LN ? gam[16 + c] : 1.f}, bC[2] = {LN ? bet[c] : 0.f, LN ? bet[16 + c] : 0.f};
   __syncthreads();
   // T-layout vector at this lane's features 16 q + 4 g .. + 3
@@ -975,6 +1070,8 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
 
   // next tile's rows of P, dXLp, dRes in T layout, one tile ahead (clamped, masked where consumed)
   f32x4 nPT[2], nXT[2], nRT[2];
+  float2 nP0 = make_float2(0.f, 0.f);  // (DWP) P0 of edge c (a dummy read of P without P0)
+  const float* p0p = (DWP && ep.P0) ? ep.P0 : P;
   auto issue = [&](int64_t row0, int nrows) {
     load_slabs32(P, row0, nrows, nPT, lane);
     const float* p = dXLp + (row0 + (c < nrows ? c : 0)) * ldXp + 4 * g;
@@ -984,6 +1081,7 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
       nXT[u] = f32x4{t.x, t.y, t.z, t.w};
     }
     if (RES) load_slabs32(dRes, row0, nrows, nRT, lane);
+    if (DWP) nP0 = *reinterpret_cast<const float2*>(p0p + (row0 + (c < nrows ? c : 0)) * 2);
   };
   auto rows_at = [](const gasfm_work_item& w, int64_t row0) { return int(w.end - row0 < TR ? w.end - row0 : TR); };
   gasfm_work_item w{0, 0, 0, -1};
@@ -997,6 +1095,10 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
     const int64_t ibeg = __builtin_amdgcn_readfirstlane(int(w.begin));
     const int ilen = __builtin_amdgcn_readfirstlane(int(w.end - w.begin));
     const auto dPrs = __builtin_amdgcn_make_buffer_rsrc(dP + ibeg * F, 0, ilen * F * 4, 0x00020000);
+    // (EPI) dP0 rows of this item; without dP0 an empty range (every store dropped)
+    const auto dP0rs = __builtin_amdgcn_make_buffer_rsrc(EPI && ep.dP0 ? ep.dP0 + ibeg * 2 : dP, 0,
+                                                         EPI && ep.dP0 ? ilen * 8 : 0, 0x00020000);
+    float dsv[2] = {0.f, 0.f};  // (EPI) this item's column sums of dP
     // per-camera constants of the attention backward (edge_cam_bwd_kernel)
     f32x4 xr[2], gv[2];
     float M[2], inv[2], delta[2];
@@ -1031,6 +1133,7 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
         RT[0] = nRT[0];
         RT[1] = nRT[1];
       }
+      const float2 p0t = nP0;
       {  // the next tile (this item's, else the next item's first; the last one re-reads itself)
         int64_t r1 = row0;
         int n1 = nrows;
@@ -1049,6 +1152,11 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
       to_c(0, PT, PC);
       to_c(1, XT, XC);
       if (RES) to_c(2, RT, RC);
+      if (DWP) {  // edge c's P0 in tile 2's padding columns 32, 33 (read back in C layout by the dWp sums)
+        float* T2 = Tt + 2 * TR * LDT + c * LDT + 32;
+        T2[0] = p0t.x;
+        T2[1] = p0t.y;
+      }
       // ---- camera attention backward (T layout: edge c, features 16 q + 4 g + r)
       float tmean = 0.f, trstd = 1.f;  // LayerNorm statistics of edge c (T layout)
       if (LN) {
@@ -1152,6 +1260,46 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
             __builtin_amdgcn_raw_buffer_store_b32(  // (the builtin's data operand is a 32-bit integer)
                 __float_as_uint(dv[r][nt]), dPrs, int(((row0 - ibeg + 4 * g + r) * F + 16 * nt + c) * 4), 0, 0);
       }
+      if (EPI) {
+        // the previous block's epilogue: column sums of dP (dSv), and dP0 = scale_e We[:, 32:34]^T dP
+        // per row: dP through tile 0 (free since P's transpose) back to the T layout, lane (g, c)
+        // dots row c's features 16 u + 4 g .. + 3, the 4 lane groups summed; group 0 stores the
+        // row's pair (the other groups an out-of-range offset)
+        float* T0 = Tt;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool live = 4 * g + r < nrows;
+          dsv[0] += live ? dv[r][0] : 0.f;
+          dsv[1] += live ? dv[r][1] : 0.f;
+          if (!GASFM_PBWD_EPI_T) {  // A/B: 16-lane sums per row (DPP), lanes c = 0, 1 store
+            const float s0 = sum16(fmaf(dv[r][0], V[4 * F + c], dv[r][1] * V[4 * F + 16 + c]));
+            const float s1 = sum16(fmaf(dv[r][0], V[5 * F + c], dv[r][1] * V[5 * F + 16 + c]));
+            const int off = c < 2 ? int(((row0 - ibeg + 4 * g + r) * 2 + c) * 4) : 0x7ffffff0;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(c ? s1 : s0), dP0rs, off, 0, 0);
+          } else {
+            T0[(4 * g + r) * LDT + c] = dv[r][0];
+            T0[(4 * g + r) * LDT + 16 + c] = dv[r][1];
+          }
+        }
+      }
+      if (EPI && GASFM_PBWD_EPI_T) {
+        float* T0 = Tt;
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const float4 d4 = *reinterpret_cast<const float4*>(T0 + c * LDT + 16 * u + 4 * g);
+          const f32x4 a = vecT(4, u), b = vecT(5, u);
+          s0 = fmaf(d4.x, a[0], fmaf(d4.y, a[1], fmaf(d4.z, a[2], fmaf(d4.w, a[3], s0))));
+          s1 = fmaf(d4.x, b[0], fmaf(d4.y, b[1], fmaf(d4.z, b[2], fmaf(d4.w, b[3], s1))));
+        }
+        s0 = sum_groups(s0);
+        s1 = sum_groups(s1);
+        const int off = g == 0 ? int((row0 - ibeg + c) * 8) : 0x7ffffff0;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s0), dP0rs, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s1), dP0rs, off + 4, 0, 0);
+      }
       // ---- dW += [dXLp | dXLc]^T relu(LN(P)), db (C layout, row 4 g + s at step s)
 #pragma unroll
       for (int ft = 0; ft < 2; ++ft)
@@ -1167,6 +1315,47 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
           accW[mt][1] = mfma16(a, ph[1][s2], accW[mt][1]);
         }
       }
+      if (DWP) {
+        // this block's epilogue: dWp += dRes^T [relu(LN(P)) | P0] (dead rows zeroed), one 16-feature
+        // half of dRes at a time, its rows and P0 re-read from tile 2 (no registers held across the
+        // tile), the products added into the lanes' LDS sums
+        const float* T2 = Tt + 2 * TR * LDT;
+#pragma unroll
+        for (int ft = 0; ft < 2; ++ft) {
+          float rr[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) rr[r] = 4 * g + r < nrows ? T2[(4 * g + r) * LDT + 16 * ft + c] : 0.f;
+          f32x4 ap[2] = {zero4(), zero4()};
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) ap[nt] = mfma16(rr[s2], ph[nt][s2], ap[nt]);
+          float a0[2] = {0.f, 0.f};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            a0[0] = fmaf(rr[r], T2[(4 * g + r) * LDT + 32], a0[0]);
+            a0[1] = fmaf(rr[r], T2[(4 * g + r) * LDT + 33], a0[1]);
+          }
+          // this half's 10 sums: [ap[0] | ap[1] | a0] at Lw[lane * 20 + 10 ft ..] (lane stride 20
+          // floats: a 16-lane b128 access touches 16 distinct bank quads)
+          float* q = Lw + lane * PB_NDW + 10 * ft;
+          if (!GASFM_PBWD_LW4) {  // A/B: scalar read-modify-writes
+#pragma unroll
+            for (int k = 0; k < 8; ++k) q[k] += ap[k / 4][k % 4];
+            q[8] += a0[0];
+            q[9] += a0[1];
+          } else {
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            const float4 o = *reinterpret_cast<const float4*>(q + 4 * nt);
+            *reinterpret_cast<float4*>(q + 4 * nt) =
+                make_float4(o.x + ap[nt][0], o.y + ap[nt][1], o.z + ap[nt][2], o.w + ap[nt][3]);
+          }
+          const float2 o2 = *reinterpret_cast<const float2*>(q + 8);
+          *reinterpret_cast<float2*>(q + 8) = make_float2(o2.x + a0[0], o2.y + a0[1]);
+          }
+        }
+      }
       __builtin_amdgcn_wave_barrier();  // this tile's transpose reads before the next tile's writes
       asm volatile("" ::: "memory");
     }
@@ -1180,12 +1369,29 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
         *reinterpret_cast<float4*>(d + 16 * q + 4 * g) = make_float4(v[0], v[1], v[2], v[3]);
       }
     }
+    if (EPI) {
+      const float s0 = sum_groups(dsv[0]) * ep.scale, s1 = sum_groups(dsv[1]) * ep.scale;
+      if (g == 0) {
+        float* d = (w.slot < 0) ? ep.dSv + seg * F : ep.part_dsv + int64_t(w.slot) * F;
+        d[c] = s0;
+        d[16 + c] = s1;
+      }
+    }
     w = wn;
   }
   // workgroup reduction: 32 accW + 4 db + 2 dg + 2 dbt (C layout) + 16 (datt, dbias summed over
-  // the 16 edge columns first)
-  constexpr int NV = 56;
+  // the 16 edge columns first) (+ DWP: the lanes' 20 dWp sums, read before the scratch is reused)
+  constexpr int NV = 56 + (DWP ? PB_NDW : 0);
   float v[NV];
+  if (DWP) {  // v[56 + (ft * 2 + nt) * 4 + r] = the MFMA sums, v[72 + ft * 2 + j] = the P0 terms
+#pragma unroll
+    for (int ft = 0; ft < 2; ++ft) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[56 + ft * 8 + k] = Lw[lane * PB_NDW + 10 * ft + k];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) v[72 + ft * 2 + j] = Lw[lane * PB_NDW + 10 * ft + 8 + j];
+    }
+  }
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -1207,7 +1413,26 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
     }
   wg_reduce_ordered<NV, kWaves, NL>(v, lds, wave, lane);
   if (wave == 0) {
-    float* o = part + int64_t(blockIdx.x) * PB2_PART;
+    float* o = part + int64_t(blockIdx.x) * ldPart;
+    if (DWP) {  // [32 x ldWpo] after the prologue/attention part, scaled as the epilogue's
+      float* od = o + PB2_PART;
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            od[(16 * ft + 4 * g + r) * ep.ldWpo + 16 * nt + c] = v[56 + (ft * 2 + nt) * 4 + r] * scale;
+      float t0[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t0[k] = sum_groups(v[72 + k]);
+      if (ep.P0 && g == 0) {
+#pragma unroll
+        for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) od[(16 * ft + c) * ep.ldWpo + 32 + j] = t0[ft * 2 + j] * scale;
+      }
+    }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -1240,8 +1465,8 @@ __global__ __launch_bounds__(kThreads, 2) void edge_cam_pbwd_kernel(
 }
 
 int grid_cam_pbwd(int n_items) {
-  return resident_grid(reinterpret_cast<const void*>(&edge_cam_pbwd_kernel<true, true>), kThreads, 0, n_items,
-                       kWaves);
+  return resident_grid(reinterpret_cast<const void*>(&edge_cam_pbwd_kernel<true, true, false, false>), kThreads, 0,
+                       n_items, kWaves);
 }
 
 int grid_cam_bwd(int n_items) {
@@ -1315,13 +1540,16 @@ extern "C" int gasfm_edge_cam_bwd(const float* P, const float* ln_w, const float
 extern "C" int32_t gasfm_edge_cam_pbwd_part_rows(int32_t n_items) { return grid_cam_pbwd(n_items > 0 ? n_items : 1); }
 extern "C" int32_t gasfm_edge_cam_pbwd_part_cols(void) { return PB2_PART; }
 
-extern "C" int gasfm_edge_cam_pbwd(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
-                                   const float* Wc, const float* bc, const float* Wp, int32_t ldWp, float scale,
-                                   const float* XR, int64_t ldXR, const float* att, const float* bias, float slope,
-                                   const float* out, int64_t ldOut, const float* seg_max, const float* seg_sum,
-                                   int64_t ldStat, const float* gout, int64_t ldG, const gasfm_work_item* items,
-                                   int32_t n_items, const float* dXLp, int64_t ldXp, const float* dRes, float* dP,
-                                   float* dXR, int64_t ldDXR, float* part_dxr, float* part, void* stream) {
+extern "C" int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const float* ln_b, float eps,
+                                      const float* Wpt, const float* Wc, const float* bc, const float* Wp, int32_t ldWp,
+                                      float scale, const float* XR, int64_t ldXR, const float* att, const float* bias,
+                                      float slope, const float* out, int64_t ldOut, const float* seg_max,
+                                      const float* seg_sum, int64_t ldStat, const float* gout, int64_t ldG,
+                                      const gasfm_work_item* items, int32_t n_items, const float* dXLp, int64_t ldXp,
+                                      const float* dRes, float* dP, float* dXR, int64_t ldDXR, float* part_dxr,
+                                      float* part, int64_t ldPart, const float* We, int32_t ldWe, float scale_e,
+                                      float* dSv_e, float* part_dsv_e, float* dP0_e, const float* P0, int32_t ldWpo,
+                                      void* stream) {
   GASFM_REQUIRE(n_items >= 0 && P && Wpt && Wc && bc && XR && att && bias && out && seg_max && seg_sum && gout &&
                     items && dXLp && dP && dXR && part && (!dRes || (Wp && ldWp >= F)),
                 "gasfm_edge_cam_pbwd: null pointer");
@@ -1330,23 +1558,53 @@ extern "C" int gasfm_edge_cam_pbwd(const float* P, const float* ln_w, const floa
                     aligned16(dP) && aligned16(dXR) && (!dRes || aligned16(dRes)) &&
                     (!part_dxr || aligned16(part_dxr)) && (!ln_w || (aligned16(ln_w) && aligned16(ln_b))),
                 "gasfm_edge_cam_pbwd: 16-byte rows required");
+  const bool epi = dSv_e != nullptr, dwp = ldWpo > 0;
+  GASFM_REQUIRE(!epi || (We && ldWe >= F + (dP0_e ? 2 : 0) && (ln_w != nullptr) == (dRes != nullptr)),
+                "gasfm_edge_cam_pbwd: the previous epilogue's outputs need its lin_proj weight (and LN == RES)");
+  GASFM_REQUIRE(!dwp || (ln_w && dRes && ldWpo == (P0 ? F + 2 : F)),
+                "gasfm_edge_cam_pbwd: the epilogue weight gradient needs LN, dRes and ldWpo = 32 (+2 with P0)");
+  GASFM_REQUIRE(ldPart >= PB2_PART + (dwp ? int64_t(F) * ldWpo : 0), "gasfm_edge_cam_pbwd: part row too narrow");
   if (n_items == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int grid = grid_cam_pbwd(n_items);
+  const PbwdEpi ep{We, ldWe, scale_e, dSv_e, part_dsv_e, dP0_e, P0, ldWpo};
   auto launch = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, st, P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, ldWp, scale, XR,
                        ldXR, att, bias, slope, out, ldOut, seg_max, seg_sum, ldStat, gout, ldG, items, n_items, dXLp,
-                       ldXp, dRes, dP, dXR, ldDXR, part_dxr, part);
+                       ldXp, dRes, dP, dXR, ldDXR, part_dxr, part, ldPart, ep);
   };
-  if (ln_w && dRes)
-    launch(&edge_cam_pbwd_kernel<true, true>);
-  else if (ln_w)
-    launch(&edge_cam_pbwd_kernel<true, false>);
-  else if (dRes)
-    launch(&edge_cam_pbwd_kernel<false, true>);
-  else
-    launch(&edge_cam_pbwd_kernel<false, false>);
+  if (ln_w && dRes) {
+    if (epi && dwp)
+      launch(&edge_cam_pbwd_kernel<true, true, true, true>);
+    else if (epi)
+      launch(&edge_cam_pbwd_kernel<true, true, true, false>);
+    else if (dwp)
+      launch(&edge_cam_pbwd_kernel<true, true, false, true>);
+    else
+      launch(&edge_cam_pbwd_kernel<true, true, false, false>);
+  } else if (ln_w) {
+    launch(&edge_cam_pbwd_kernel<true, false, false, false>);
+  } else if (dRes) {
+    launch(&edge_cam_pbwd_kernel<false, true, false, false>);
+  } else if (epi) {
+    launch(&edge_cam_pbwd_kernel<false, false, true, false>);
+  } else {
+    launch(&edge_cam_pbwd_kernel<false, false, false, false>);
+  }
   return launch_status("gasfm_edge_cam_pbwd");
+}
+
+extern "C" int gasfm_edge_cam_pbwd(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
+                                   const float* Wc, const float* bc, const float* Wp, int32_t ldWp, float scale,
+                                   const float* XR, int64_t ldXR, const float* att, const float* bias, float slope,
+                                   const float* out, int64_t ldOut, const float* seg_max, const float* seg_sum,
+                                   int64_t ldStat, const float* gout, int64_t ldG, const gasfm_work_item* items,
+                                   int32_t n_items, const float* dXLp, int64_t ldXp, const float* dRes, float* dP,
+                                   float* dXR, int64_t ldDXR, float* part_dxr, float* part, void* stream) {
+  return gasfm_edge_cam_pbwd_ex(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, ldWp, scale, XR, ldXR, att, bias, slope, out,
+                                ldOut, seg_max, seg_sum, ldStat, gout, ldG, items, n_items, dXLp, ldXp, dRes, dP, dXR,
+                                ldDXR, part_dxr, part, PB2_PART, nullptr, 0, 0.f, nullptr, nullptr, nullptr, nullptr, 0,
+                                stream);
 }
 
 extern "C" int gasfm_edge_seam_fwd(const float* Pb, const float* P0, const int32_t* pt, const float* ln_wb,

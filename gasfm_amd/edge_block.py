@@ -31,6 +31,10 @@ PROJ_SCALE = 0.25  # the "/ 4" of layers.py:945
 # EdgeCamFn's backward as ONE kernel (gasfm_edge_cam_pbwd: camera attention backward + edge
 # prologue backward, dXLc never stored); 0 selects the two kernels edge_cam_bwd + edge_prologue_bwd
 CAM_PBWD = os.environ.get("GASFM_CAM_PBWD", "1") != "0"
+# The edge epilogue's backward folded into edge_cam_pbwd (round 3): block b's lin_proj weight
+# gradient in block b's own edge_cam_pbwd (it holds dRes = dP' and relu(LN_b(P_b))), dSv / dP0 in
+# block b+1's (the kernel that produces dP').  0: edge_epilogue_bwd as before.
+EPI_FOLD = os.environ.get("GASFM_EPI_FOLD", "1") != "0"
 
 
 def _rows(t):
@@ -132,7 +136,10 @@ class EdgeCamFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, P, ln_w, ln_b, Wpt, bpt, Wc, bc, Wp, eps, pos, XR, att, bias, plan, heads, slope,
-                plan_partial=None, shard=None):
+                plan_partial=None, shard=None, P0=None, dwp=False):
+        """dwp: the backward also returns Wp's gradient, the block's edge-epilogue weight gradient
+        scale sum_e dP'[e]^T [relu(LN(P[e])) | P0[e]] (dP' = the token's gradient), which the
+        epilogue then leaves out (EdgeEpilogueFn's wp_by_cam)."""
         E, dev = P.shape[0], P.device
         HC = att.numel()
         if heads != 4 or HC != 32:
@@ -147,9 +154,10 @@ class EdgeCamFn(torch.autograd.Function):
         ctx.eps, ctx.heads, ctx.slope, ctx.plan = eps, heads, slope, plan
         ctx.att_shape = att.shape
         ctx.has_ln = ln_w is not None
-        ctx.defer = _native.defer_token(ln_w, ln_b, Wpt, bpt, Wc, bc, att, bias)
+        ctx.dwp = bool(dwp)
+        ctx.defer = _native.defer_token(ln_w, ln_b, Wpt, bpt, Wc, bc, att, bias, Wp if dwp else None)
         ctx.set_materialize_grads(False)
-        ctx.save_for_backward(P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum)
+        ctx.save_for_backward(P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum, P0)
         token = P.new_empty((1, 1)).expand(E, P.shape[1])
         return XLp, out, token
 
@@ -159,28 +167,49 @@ class EdgeCamFn(torch.autograd.Function):
         return _cam_backward(ctx, ctx.saved_tensors, dXLp, g_c, dRes)
 
 
-def _cam_backward(ctx, saved, dXLp, g_c, dRes):
+def _dwp_torch(P, ln_w, ln_b, eps, dRes, P0):
+    """The epilogue weight gradient scale dRes^T [relu(LN(P)) | P0] with torch ops (the EdgeCamFn
+    backward paths without edge_cam_pbwd)."""
+    ph = torch.relu(torch.nn.functional.layer_norm(P, (P.shape[1],), ln_w, ln_b, eps))
+    if P0 is not None:
+        ph = torch.cat([ph, P0], dim=1)
+    return PROJ_SCALE * (dRes.t() @ ph)
+
+
+def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None):
     """EdgeCamFn's backward from its saved state (ctx attributes eps, heads, slope, plan, att_shape,
-    has_ln, defer): the 18 input gradients of EdgeCamFn.forward."""
-    P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum = saved
+    has_ln, dwp, defer): the 20 input gradients of EdgeCamFn.forward.  epi: the previous block's
+    epilogue outputs to fill from dP (edge_cam_pbwd's EPI), or None; ctx.epi_done tells whether
+    they were filled."""
+    P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum, P0 = saved
     plan = ctx.plan
     E, dev = P.shape[0], P.device
     dXLp = torch.zeros((E, 32), dtype=torch.float32, device=dev) if dXLp is None else dXLp.contiguous()
     g_c = torch.zeros_like(out) if g_c is None else (g_c if g_c.stride(1) == 1 else g_c.contiguous())
+    dwp = ctx.dwp and dRes is not None and ln_w is not None
+    ctx.epi_done = False
+    dWp = None
     if CAM_PBWD and plan.n_items:
         # camera attention backward + prologue backward in one kernel (gasfm_edge_cam_pbwd)
         dXR = torch.empty((plan.num_targets, 32), dtype=torch.float32, device=dev)
         part_dxr = torch.empty((plan.n_part_rows, 32), dtype=torch.float32, device=dev) if plan.n_slots else None
-        rows, cols = _native.edge_cam_pbwd_part_shape(plan.n_items)
+        wcols = (34 if P0 is not None else 32) if dwp else 0
+        rows, cols = _native.edge_cam_pbwd_part_shape(plan.n_items, wcols)
         part = torch.empty((rows, cols), dtype=torch.float32, device=dev)
         dP = torch.empty_like(P)
+        use_epi = epi is not None and (ln_w is None) == (dRes is None)
         _native.edge_cam_pbwd(P, ln_w, ln_b, ctx.eps, Wpt.contiguous(), Wc.contiguous(), bc.contiguous(),
                               Wp.contiguous() if dRes is not None else None, PROJ_SCALE, XR, attf, bias, ctx.slope,
-                              out, smax, ssum, g_c, plan.items, plan.n_items, dXLp, dRes, dP, dXR, part_dxr, part)
+                              out, smax, ssum, g_c, plan.items, plan.n_items, dXLp, dRes, dP, dXR, part_dxr, part,
+                              epi=epi if use_epi else None,
+                              dwp=(P0 if P0 is not None else True) if dwp else None)
+        ctx.epi_done = use_epi
         bwd_combine(plan, part_dxr, 32, dXR)
         tot = _native.param_colsum(part, ctx.defer)
         o = 64 * 32
-        ta = tot[o + 128:]
+        ta = tot[o + 128:o + 192]
+        if dwp:
+            dWp = tot[o + 192:o + 192 + 32 * wcols].view(32, wcols)
     else:
         # camera attention backward (XLc recomputed from P): dXLc, dXR, [datt | dbias] partials
         dXLc = torch.empty((E, 32), dtype=torch.float32, device=dev)
@@ -205,11 +234,15 @@ def _cam_backward(ctx, saved, dXLp, g_c, dRes):
         ta = _native.param_colsum(part_a, ctx.defer)
         tot = _native.param_colsum(part, ctx.defer)
         o = 64 * 32
+        if dwp:
+            dWp = _dwp_torch(P, ln_w, ln_b, ctx.eps, dRes, P0) if plan.n_items else torch.zeros_like(Wp)
+    if dwp and dWp is None:  # no local edges
+        dWp = torch.zeros_like(Wp)
     dW, db = tot[:o].view(64, 32), tot[o:o + 64]
     dgam = tot[o + 64:o + 96] if ctx.has_ln else None
     dbet = tot[o + 96:o + 128] if ctx.has_ln else None
-    return (dP, dgam, dbet, dW[:32], db[:32], dW[32:], db[32:], None, None, None, dXR,
-            ta[:32].view(ctx.att_shape), ta[32:], None, None, None, None, None)
+    return (dP, dgam, dbet, dW[:32], db[:32], dW[32:], db[32:], dWp, None, None, dXR,
+            ta[:32].view(ctx.att_shape), ta[32:], None, None, None, None, None, None, None)
 
 
 class DualAttentionFn(torch.autograd.Function):
@@ -263,7 +296,8 @@ class DualAttentionFn(torch.autograd.Function):
 
 class EdgeEpilogueFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, P, P0, token, Sp, Sv, Sg, Wp, bp, ln_w, ln_b, eps, edges):
+    def forward(ctx, P, P0, token, Sp, Sv, Sg, Wp, bp, ln_w, ln_b, eps, edges, wp_by_cam=False):
+        """wp_by_cam: Wp's gradient is returned by the block's EdgeCamFn / SeamFn (its dwp), not here."""
         out = torch.empty_like(P)
         Wp_c = Wp.contiguous()
         _native.edge_epilogue_fwd(P, P0, edges.cam, edges.pt, ln_w, ln_b, eps, Wp_c, bp.contiguous(),
@@ -271,6 +305,7 @@ class EdgeEpilogueFn(torch.autograd.Function):
         ctx.eps = eps
         ctx.edges = edges
         ctx.sg_shape = Sg.shape
+        ctx.wp_by_cam = bool(wp_by_cam)
         ctx.defer = _native.defer_token(Wp)
         ctx.save_for_backward(P, P0, Wp_c, ln_w, ln_b)
         return out
@@ -280,32 +315,39 @@ class EdgeEpilogueFn(torch.autograd.Function):
         return _epilogue_backward(ctx, ctx.saved_tensors, dPo)
 
 
-def _epilogue_backward(ctx, saved, dPo):
-    """EdgeEpilogueFn's backward from its saved state (ctx attributes eps, edges, sg_shape, defer):
-    the 12 input gradients of EdgeEpilogueFn.forward (the block input's through the token)."""
+def _epilogue_backward(ctx, saved, dPo, folded=None):
+    """EdgeEpilogueFn's backward from its saved state (ctx attributes eps, edges, sg_shape,
+    wp_by_cam, defer): the 13 input gradients of EdgeEpilogueFn.forward (the block input's through
+    the token).  folded: (dSv, part_dsv, dP0) already filled by the next block's edge_cam_pbwd
+    (SeamFn), so edge_epilogue_bwd does not run (Wp's gradient is then the block's EdgeCamFn's)."""
     P, P0, Wp, ln_w, ln_b = saved
     edges = ctx.edges
     dPo = dPo.contiguous()
     dev = P.device
     pc = edges.plans["proj2view"]
     pp = edges.plans["proj2scenepoint"]
-    # camera side: dSv (+ dWp, dP0) in one pass over the camera work items
-    dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
-    part_dsv = torch.empty((max(pc.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
-    dP0 = torch.empty((P.shape[0], 2), dtype=torch.float32, device=dev) if P0 is not None else None
-    wg = _native.edge_part_floats(1, P.shape[0], pc.n_items) // (32 * 34)
-    part_w = torch.empty((wg, 32 * Wp.shape[1]), dtype=torch.float32, device=dev)
-    _native.edge_epilogue_bwd(pc.items, pc.n_items, dPo, P, P0, ln_w, ln_b, ctx.eps, Wp, PROJ_SCALE, dSv,
-                              part_dsv, dP0, part_w)
+    dWp = None
+    if folded is not None:
+        dSv, part_dsv, dP0 = folded
+    else:
+        # camera side: dSv (+ dWp, dP0) in one pass over the camera work items
+        dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
+        part_dsv = torch.empty((max(pc.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
+        dP0 = torch.empty((P.shape[0], 2), dtype=torch.float32, device=dev) if P0 is not None else None
+        wg = _native.edge_part_floats(1, P.shape[0], pc.n_items) // (32 * 34)
+        part_w = torch.empty((wg, 32 * Wp.shape[1]), dtype=torch.float32, device=dev)
+        _native.edge_epilogue_bwd(pc.items, pc.n_items, dPo, P, P0, ln_w, ln_b, ctx.eps, Wp, PROJ_SCALE, dSv,
+                                  part_dsv, dP0, part_w)
+        if not ctx.wp_by_cam:
+            dWp = _native.param_colsum(part_w, ctx.defer).view(32, Wp.shape[1])
     bwd_combine(pc, part_dsv, 32, dSv)
-    dWp = _native.param_colsum(part_w, ctx.defer).view(32, Wp.shape[1])
     dSg = _native.colsum(dSv)          # == d bias_proj: every edge belongs to one camera
     # point side: dSp = per-point sum of dP'/4 through the point permutation
     dSp = torch.empty((edges.n, 32), dtype=torch.float32, device=dev)
     part_dsp = torch.empty((max(pp.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
     _native.segment_rowsum(pp.items, pp.n_items, pp.perm, dPo, PROJ_SCALE, dSp, part_dsp)
     bwd_combine(pp, part_dsp, 32, dSp)
-    return (None, dP0, dPo, dSp, dSv, dSg.view(ctx.sg_shape), dWp, dSg.clone(), None, None, None, None)
+    return (None, dP0, dPo, dSp, dSv, dSg.view(ctx.sg_shape), dWp, dSg.clone(), None, None, None, None, None)
 
 
 class SeamFn(torch.autograd.Function):
@@ -314,12 +356,17 @@ class SeamFn(torch.autograd.Function):
     Functions' own backwards in autograd's order (EdgeCamFn's, then EdgeEpilogueFn's on the
     resulting dP').
 
-    Inputs: the 12 of EdgeEpilogueFn.forward, then the 18 of EdgeCamFn.forward (whose P is this
-    Function's own output P').  Outputs: (P', XLp, camera aggregates, token)."""
+    Inputs: the 13 of EdgeEpilogueFn.forward, then the 20 of EdgeCamFn.forward (whose P is this
+    Function's own output P').  Outputs: (P', XLp, camera aggregates, token).
+
+    With EPI_FOLD and block b's lin_proj gradient taken by block b's own EdgeCamFn / SeamFn
+    (wp_by_cam), the backward's edge_cam_pbwd also fills block b's dSv and dP0 from the dP' it
+    produces, and edge_epilogue_bwd does not run."""
 
     @staticmethod
-    def forward(ctx, P, P0, token, Sp, Sv, Sg, Wp, bp, lnw_b, lnb_b, eps_b, edges,
-                ln_w, ln_b, Wpt, bpt, Wc, bc, Wp_n, eps, pos, XR, att, bias, plan, heads, slope, plan_partial, shard):
+    def forward(ctx, P, P0, token, Sp, Sv, Sg, Wp, bp, lnw_b, lnb_b, eps_b, edges, wp_by_cam,
+                ln_w, ln_b, Wpt, bpt, Wc, bc, Wp_n, eps, pos, XR, att, bias, plan, heads, slope, plan_partial, shard,
+                P0_n=None, dwp_n=False):
         E, dev = P.shape[0], P.device
         HC = att.numel()
         if heads != 4 or HC != 32:
@@ -337,15 +384,17 @@ class SeamFn(torch.autograd.Function):
         out, smax, ssum = _cam_attention_fwd(launch, bias, plan, heads, HC, plan_partial, shard, dev)
         # EdgeEpilogueFn's state
         ctx.e_eps, ctx.edges, ctx.sg_shape = eps_b, edges, Sg.shape
+        ctx.e_wp_by_cam = bool(wp_by_cam)
         ctx.e_defer = _native.defer_token(Wp)
         # EdgeCamFn's state
         ctx.eps, ctx.heads, ctx.slope, ctx.plan = eps, heads, slope, plan
         ctx.att_shape = att.shape
         ctx.has_ln = ln_w is not None
-        ctx.defer = _native.defer_token(ln_w, ln_b, Wpt, bpt, Wc, bc, att, bias)
+        ctx.dwp = bool(dwp_n)
+        ctx.defer = _native.defer_token(ln_w, ln_b, Wpt, bpt, Wc, bc, att, bias, Wp_n if dwp_n else None)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(P, P0, Wp_c, lnw_b, lnb_b, Pn, ln_w, ln_b, Wpt, Wc, bc, Wp_n, XR, attf, bias, out, smax,
-                              ssum)
+                              ssum, P0_n)
         ctx.n_epi = 5
         token_n = P.new_empty((1, 1)).expand(E, P.shape[1])
         return Pn, XLp, out, token_n
@@ -355,16 +404,30 @@ class SeamFn(torch.autograd.Function):
         saved = ctx.saved_tensors
         epi, cam = saved[:ctx.n_epi], saved[ctx.n_epi:]
         dRes = dtoken.contiguous() if (dtoken is not None and dtoken.stride(0) != 0) else None
-        gc = _cam_backward(ctx, cam, dXLp, g_c, dRes)
+        edges = ctx.edges
+        folded = None
+        if EPI_FOLD and ctx.e_wp_by_cam and gPn is None and ctx.plan is edges.plans["proj2view"]:
+            # block b's dSv / dP0 from the dP' this launch produces (edge_cam_pbwd EPI)
+            P_b, P0_b, Wp_b = epi[0], epi[1], epi[2]
+            dev = P_b.device
+            dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
+            part_dsv = torch.empty((max(ctx.plan.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
+            dP0 = torch.empty((P_b.shape[0], 2), dtype=torch.float32, device=dev) if P0_b is not None else None
+            folded = (dSv, part_dsv, dP0)
+        gc = _cam_backward(ctx, cam, dXLp, g_c, dRes,
+                           epi=None if folded is None else (Wp_b, PROJ_SCALE) + folded)
+        if not ctx.epi_done:
+            folded = None
         dPn = gc[0] if gPn is None else gc[0] + gPn
-        ectx = _EpiState(ctx.e_eps, ctx.edges, ctx.sg_shape, ctx.e_defer)
-        ge = _epilogue_backward(ectx, epi, dPn)
-        return ge + gc[1:] + (None,) * 0
+        ectx = _EpiState(ctx.e_eps, edges, ctx.sg_shape, ctx.e_defer, ctx.e_wp_by_cam)
+        ge = _epilogue_backward(ectx, epi, dPn, folded)
+        return ge + gc[1:]
 
 
 class _EpiState:
-    def __init__(self, eps, edges, sg_shape, defer):
+    def __init__(self, eps, edges, sg_shape, defer, wp_by_cam=False):
         self.eps, self.edges, self.sg_shape, self.defer = eps, edges, sg_shape, defer
+        self.wp_by_cam = wp_by_cam
 
 
 class PendingEpilogue:

@@ -26,7 +26,7 @@ import torch
 import torch.nn.functional as F
 from torch.nn import Identity, LayerNorm, Linear, Module, ModuleList, ReLU, Sequential
 
-from . import _native, dense, edge_ops, point_block, streams, view_block
+from . import _native, dense, edge_block, edge_ops, point_block, streams, view_block
 from .attention import AttnPlan, GatAttentionFn, gat_attention
 from .edge_block import (Block0EpilogueFn, Block0PrologueFn, DualAttentionFn, EdgeCamFn, EdgeEpilogueFn,
                          EdgePrologueFn, PendingEpilogue, SeamFn, materialize)
@@ -481,10 +481,11 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         return (EDGE_CAM and cc.heads == 4 and cc.out_channels == 8 and cp.heads == 4 and cp.out_channels == 8
                 and plans["proj2view"].perm is None)
 
-    def edge_cam_attend(self, P, ln_w, ln_b, eps, Wp, plans, holder):
+    def edge_cam_attend(self, P, ln_w, ln_b, eps, Wp, plans, holder, P0=None, dwp=False):
         """attend callback of forward_fused: EdgeCamFn on P (lin_l of both convs, the camera
         attention; XLp written in point order) then the point attention on XLp.  The prologue's
-        token (see EdgePrologueFn) is left in holder["token"]."""
+        token (see EdgePrologueFn) is left in holder["token"].  dwp: the camera Function returns
+        the block's lin_proj gradient (EdgeCamFn's dwp; P0 its skip input)."""
         (W, b), (W2, b2) = self.lin_l_pair()
         pp, pc = plans["proj2scenepoint"], plans["proj2view"]
         cp, cc = self.proj2scenepoint.graph_conv, self.proj2view.graph_conv
@@ -492,7 +493,7 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
 
         def attend(XRp, XRc, sec):
             cam_args = (ln_w, ln_b, W, b, W2, b2, Wp, eps, pos, XRc, cc.att, cc.bias, pc, cc.heads, cc.negative_slope,
-                        plans.get("_partial", {}).get("proj2view"), plans.get("_shard"))
+                        plans.get("_partial", {}).get("proj2view"), plans.get("_shard"), P0, dwp)
             if isinstance(P, PendingEpilogue):  # the previous block's epilogue in the same kernel
                 Pn, XLp, agg_c, token = SeamFn.apply(*P.args, *cam_args)
                 P._P = Pn
@@ -650,9 +651,14 @@ class GraphAttnSfMLayer(Module):
         gfu = self.global_feature_update
         pfu = self.projection_feature_update
         pos = plans["proj2scenepoint"].pos
+        P0e = P0 if self.add_skipconn_from_init_projfeat else None
+        dwp = False
         if gfu.cam_fusable(plans):
             holder = {}
-            attend = gfu.edge_cam_attend(P, ln.weight, ln.bias, ln.eps, pfu.lin_proj.weight, plans, holder)
+            # the block's lin_proj gradient from its edge_cam_pbwd (edge_block.EPI_FOLD)
+            dwp = edge_block.EPI_FOLD and edge_block.CAM_PBWD and ln.weight is not None
+            attend = gfu.edge_cam_attend(P, ln.weight, ln.bias, ln.eps, pfu.lin_proj.weight, plans, holder,
+                                         P0e if dwp else None, dwp)
             pts, view, glob = gfu.forward_fused(None, plans, prev_pt, prev_view, prev_glob, carry=carry, pfu=pfu,
                                                 nxt=nxt, attend=attend)
             token = holder["token"]
@@ -668,8 +674,8 @@ class GraphAttnSfMLayer(Module):
                                                          if carry is not None else (None, None, None)))
         sv, sg = _wrap_boundary(plans.get("_shard"), sv, sg, carry)
         sv, sg = _fold_global(sv, sg, plans)
-        args = (P, P0 if self.add_skipconn_from_init_projfeat else None, token, sp, sv, sg, pfu.lin_proj.weight,
-                pfu.lin_proj.bias, ln.weight, ln.bias, ln.eps, edges)
+        args = (P, P0e, token, sp, sv, sg, pfu.lin_proj.weight, pfu.lin_proj.bias, ln.weight, ln.bias, ln.eps, edges,
+                dwp)
         if EDGE_SEAM and _seam_ok(args):
             return PendingEpilogue(args), pts, view, glob
         return EdgeEpilogueFn.apply(*args), pts, view, glob

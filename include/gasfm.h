@@ -183,6 +183,26 @@ int gasfm_edge_cam_pbwd(const float* P, const float* ln_w, const float* ln_b, fl
                         int64_t ldStat, const float* gout, int64_t ldG, const gasfm_work_item* items,
                         int32_t n_items, const float* dXLp, int64_t ldXp, const float* dRes, float* dP,
                         float* dXR, int64_t ldDXR, float* part_dxr, float* part, void* stream);
+/* gasfm_edge_cam_pbwd with the edge epilogue's backward folded in (round 3; replaces
+ * gasfm_edge_epilogue_bwd's dSv / dP0 / dWp, reference: the autograd of lin_proj and of the
+ * Sv[cam] gather in GraphAttnSfMProjectionFeatureUpdate, layers.py:911-956):
+ *   dSv_e != null (EPI): the PREVIOUS block's epilogue gradients from this launch's dP (= that
+ *     epilogue's dP'): dSv_e[cam] = scale_e sum_e dP[e] (split items: part_dsv_e rows, same slots as
+ *     part_dxr), dP0_e[e] = scale_e We[:, 32:34]^T dP[e] (dP0_e may be null; We row stride ldWe);
+ *     requires (ln_w == null) == (dRes == null);
+ *   ldWpo > 0 (DWP): THIS block's lin_proj gradient scale sum_e dRes[e]^T [relu(LN(P[e])) | P0[e]]
+ *     as a [32 x ldWpo] block after the gasfm_edge_cam_pbwd_part_cols() floats of each part row
+ *     (ldWpo = 34 with P0 [E, 2], 32 without); requires ln_w and dRes.
+ * part rows have stride ldPart (>= part_cols + 32 ldWpo). */
+int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
+                           const float* Wc, const float* bc, const float* Wp, int32_t ldWp, float scale,
+                           const float* XR, int64_t ldXR, const float* att, const float* bias, float slope,
+                           const float* out, int64_t ldOut, const float* seg_max, const float* seg_sum,
+                           int64_t ldStat, const float* gout, int64_t ldG, const gasfm_work_item* items,
+                           int32_t n_items, const float* dXLp, int64_t ldXp, const float* dRes, float* dP,
+                           float* dXR, int64_t ldDXR, float* part_dxr, float* part, int64_t ldPart,
+                           const float* We, int32_t ldWe, float scale_e, float* dSv_e, float* part_dsv_e,
+                           float* dP0_e, const float* P0, int32_t ldWpo, void* stream);
 
 /* ---- fused GATv2 edge-softmax + aggregation (device) ------------------- */
 

@@ -8,8 +8,12 @@ attention, on camera plans with complete and split (partial + combined) items, a
 without the LayerNorm (the final update's raw features, graph_attn_sfm.py:141-148).
 Tolerance (fp32 vs fp64): |d| <= 1e-5 + 1e-4 |ref| for XLp, the aggregates, dP and dXR; weight /
 attention gradients (sums over every edge) within 1e-4 of their largest element.
-The model-level check runs the 3-block net with and without the fusion (GASFM_EDGE_CAM) and
-against the fp64 functional oracle.
+With the LayerNorm and the residual, EdgeCamFn also returns the block's lin_proj gradient (dwp,
+the folded edge-epilogue weight gradient PROJ_SCALE sum_e dP'[e]^T [relu(LN(P[e])) | P0[e]],
+layers.py:945-956), checked like the other weight gradients.
+The model-level checks run the 3-block net with and without the fusion (GASFM_EDGE_CAM) and
+against the fp64 functional oracle, and the 4-block net with the edge epilogue's backward folded
+into edge_cam_pbwd (edge_block.EPI_FOLD) against the unfolded one.
 """
 import numpy as np
 import pytest
@@ -56,13 +60,15 @@ def test_edge_cam_fn_vs_fp64(device, ln, max_piece, res):
     Wpt, Wc, Wp = rnd(32, 32, sc=0.2), rnd(32, 32, sc=0.2), rnd(32, 34, sc=0.2)
     bpt, bc = rnd(32, sc=0.1), rnd(32, sc=0.1)
     XR, att, bias = rnd(m, 32), rnd(1, 4, 8, sc=0.35), rnd(32, sc=0.1)
-    leaves = [t for t in (P, ln_w, ln_b, Wpt, bpt, Wc, bc, XR, att, bias) if t is not None]
+    dwp = ln and res
+    P0 = rnd(E, 2)
+    leaves = [t for t in (P, ln_w, ln_b, Wpt, bpt, Wc, bc, XR, att, bias, Wp if dwp else None) if t is not None]
     for t in leaves:
         t.requires_grad_(True)
     gXLp, gout, dres = rnd(E, 32), rnd(m, 32), (rnd(E, 32) if res else None)
     with _native.dispatch_record():
         XLp, out_c, token = EdgeCamFn.apply(P, ln_w, ln_b, Wpt, bpt, Wc, bc, Wp, 1e-5, pp.pos, XR, att, bias, pc, 4,
-                                            0.2)
+                                            0.2, None, None, P0 if dwp else None, dwp)
     outs, grads = [XLp, out_c], [gXLp, gout]
     if res:
         outs.append(token)
@@ -79,8 +85,9 @@ def test_edge_cam_fn_vs_fp64(device, ln, max_piece, res):
     out_r, _, _ = gatv2_segment_reference(xlc.view(-1, 4, 8), XRd.view(-1, 4, 8), attd.view(4, 8), biasd,
                                           cam.to(device), m)
     L = (xlp * gXLp.double()).sum() + (out_r * gout.double()).sum()
+    Wpd = Wp.detach().double().requires_grad_(True)
     if res:  # the block output P + (Wp [P_hat | P0] + ...) / 4 as seen from this prologue
-        L = L + (dres.double() * (Pd + PROJ_SCALE * (x @ Wp[:, :32].double().T))).sum()
+        L = L + (dres.double() * (Pd + PROJ_SCALE * (x @ Wpd[:, :32].T + P0.double() @ Wpd[:, 32:].T))).sum()
     L.backward()
     XLp_edge = XLp[pp.pos.long()]  # row pos[e] holds edge e
     close(XLp_edge, xlp, msg="XLp")
@@ -93,6 +100,8 @@ def test_edge_cam_fn_vs_fp64(device, ln, max_piece, res):
     if ln:
         close_sum(got[id(ln_w)], lwd.grad, msg="dgamma")
         close_sum(got[id(ln_b)], lbd.grad, msg="dbeta")
+    if dwp:
+        close_sum(got[id(Wp)], Wpd.grad, msg="dWp (folded epilogue)")
 
 
 @pytest.mark.parametrize("fused", [True, False])
@@ -130,3 +139,48 @@ def test_three_block_net_fused_vs_oracle(device, fused):
             check_grad(p.grad, g64[k], k, g32[k])
     finally:
         model.EDGE_CAM = prev
+
+
+def test_epilogue_fold_vs_unfolded(device, monkeypatch):
+    """The 4-block net (three seams) with the edge epilogue's backward folded into edge_cam_pbwd
+    against the same net with edge_epilogue_bwd: identical forward, no edge_epilogue_bwd launch left,
+    the lin_proj gradients (now edge_cam_pbwd's) within 1e-4 normwise of the unfolded ones, and every
+    parameter gradient within 1e-3 normwise of the unfolded one or within 10x the unfolded one's own
+    distance from the fp64 oracle (the smallest gradients, blocks down, amplify the summation-order
+    differences past 1e-3).  test_three_block_net_fused_vs_oracle checks the folded path (the default)
+    against the fp64 oracle alone."""
+    from conftest import oracle_grads
+    from gasfm_amd import edge_block
+    from oracle.weights import deterministic_state_dict
+    sc = synthetic.scaled_config4(0.05, seed=11)
+    data = gasfm_amd.SceneData.from_synthetic(sc).to(device)
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=4))
+    sd = deterministic_state_dict(net.state_dict(), torch.float64)
+    net.load_state_dict({k: v.float() for k, v in sd.items()})
+    net = net.to(device)
+    gen = torch.Generator().manual_seed(3)
+    cP = torch.randn((sc.m, 3, 4), generator=gen, dtype=torch.float64)
+    cX = torch.randn((4, sc.n), generator=gen, dtype=torch.float64)
+    calls = []
+    orig = _native.edge_epilogue_bwd
+    monkeypatch.setattr(_native, "edge_epilogue_bwd", lambda *a, **k: (calls.append(1), orig(*a, **k))[1])
+    res = {}
+    for fold in (False, True):
+        monkeypatch.setattr(edge_block, "EPI_FOLD", fold)
+        calls.clear()
+        net.zero_grad(set_to_none=True)
+        pred = net(data)
+        ((pred["Ps_norm"] * cP.float().to(device)).sum() + (pred["pts3D"] * cX.float().to(device)).sum()).backward()
+        torch.cuda.synchronize()
+        res[fold] = (pred["Ps_norm"].detach().clone(), {k: p.grad.detach().double().cpu() for k, p in net.named_parameters()},
+                     len(calls))
+    assert torch.equal(res[True][0], res[False][0])
+    assert res[False][2] == 3 and res[True][2] == 0, (res[False][2], res[True][2])
+    (g64, _), _ = oracle_grads(sd, sc, cP, cX)
+    for k, g0 in res[False][1].items():
+        g1 = res[True][1][k]
+        err = float((g1 - g0).norm())
+        if k.endswith("lin_proj.weight") and "projection_feature_update" in k:
+            assert err <= 1e-4 * float(g0.norm()) + 1e-9, (k, err, float(g0.norm()))
+        own = float((g0 - torch.from_numpy(g64[k])).norm())
+        assert err <= max(1e-3 * float(g0.norm()), 10 * own) + 1e-9, (k, err, own, float(g0.norm()))

@@ -109,6 +109,18 @@ def main():
                                       b[32:].contiguous(), Wp, 0.25, XRc, att, bias, 0.2, co, cmax, csum, gout,
                                       pc.items, pc.n_items, dXLp_in, dRes_in, dP, dXRc, pdxr, pbp),
         E * 512 + m * 256)
+    # with the edge epilogue's backward folded in (edge_block.EPI_FOLD): EPI, DWP, both
+    P0f, dP0f, dSvf = rnd(E, 2), torch.empty(E, 2, device=dev), torch.empty(m, 32, device=dev)
+    pdsv = torch.empty(max(pc.n_part_rows, 1), 32, device=dev)
+    rpw, cpw = _native.edge_cam_pbwd_part_shape(pc.n_items, 34)
+    pbw = torch.empty(rpw, cpw, device=dev)
+    for tag, epi, dwp in (("EPI", True, False), ("DWP", False, True), ("EPI+DWP", True, True)):
+        run(f"edge_cam_pbwd(LN, RES, {tag})",
+            lambda epi=epi, dwp=dwp: _native.edge_cam_pbwd(
+                P, ln_w, ln_b, 1e-5, W[:32].contiguous(), W[32:].contiguous(), b[32:].contiguous(), Wp, 0.25, XRc,
+                att, bias, 0.2, co, cmax, csum, gout, pc.items, pc.n_items, dXLp_in, dRes_in, dP, dXRc, pdxr, pbw,
+                epi=(Wp, 0.25, dSvf, pdsv, dP0f) if epi else None, dwp=P0f if dwp else None),
+            E * 528 + m * 256)
     dSp = torch.empty(n, 32, device=dev)
     run("segment_rowsum", lambda: _native.segment_rowsum(pp.items, pp.n_items, pp.perm, dPo, 0.25, dSp, None),
         E * 132 + n * 128)

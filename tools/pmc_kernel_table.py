@@ -22,6 +22,9 @@ ALGO_MB = {  # config 4 algorithmic bytes per launch, DESIGN.md §5
     "edge_cam_pbwd_kernel<true, true>": 2049, "edge_seam_fwd_kernel<true>": 1601,
     "point_hub_bwd_r_kernel<true>": 256, "point_tail_bwd_r_kernel<true>": 205,
     "attn_bwd_glds_kernel<gasfm::Geom<32, 8> >": 1120,
+    # round 3, edge epilogue backward folded into edge_cam_pbwd (+ P0 read, dP0 written: 16 B per edge)
+    "edge_cam_pbwd_kernel<true, true, false, false>": 2049, "edge_cam_pbwd_kernel<true, true, true, true>": 2113,
+    "edge_cam_pbwd_kernel<true, true, false, true>": 2081,
 }
 
 
