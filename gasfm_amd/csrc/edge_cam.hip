@@ -1011,7 +1011,8 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   constexpr int QW = F * F;  // floats per 32 x 32 slab set
   constexpr int OV = 4 * QW, OT = OV + (EPI ? 6 : 4) * F, WT = 4 * TR * LDT;
   constexpr int OD = OT + kWaves * WT;
-  constexpr int NL = OD + (DWP ? kWaves * PB_NDW * kW : 0);
+  constexpr int NLS = (DWP ? PB_NDW : 0) + (EPI ? 2 : 0);  // per-lane LDS sums
+  constexpr int NL = OD + kWaves * NLS * kW;
   __shared__ __attribute__((aligned(16))) float lds[NL];
   float* WcQ = lds;
   float* WptTQ = lds + QW;
@@ -1035,11 +1036,11 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
   float* Tt = lds + OT + wave * WT;  // tiles 0: P, 1: dXLp, 2: dRes, 3: dXLc
-  float* Lw = lds + OD + wave * PB_NDW * kW;  // (DWP) value k of this lane at Lw[lane * PB_NDW + k]
-  if (DWP) {
+  // (DWP) value k of this lane's dWp sums at Lw[k]; (EPI) the item's dSv column sums at Ls[0, 1]
+  float* Lw = lds + OD + (wave * kW + lane) * NLS;
+  float* Ls = Lw + (DWP ? PB_NDW : 0);
 #pragma unroll
-    for (int k = 0; k < PB_NDW; ++k) Lw[lane * PB_NDW + k] = 0.f;
-  }
+  for (int k = 0; k < NLS; ++k) Lw[k] = 0.f;
   const float gC[2] = {LN ? gam[c] : 1.f, LN ? gam[16 + c] : 1.f}, bC[2] = {LN ? bet[c] : 0.f, LN ? bet[16 + c] : 0.f};
   __syncthreads();
   // T-layout vector at this lane's features 16 q + 4 g .. + 3
@@ -1098,7 +1099,6 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
     // (EPI) dP0 rows of this item; without dP0 an empty range (every store dropped)
     const auto dP0rs = __builtin_amdgcn_make_buffer_rsrc(EPI && ep.dP0 ? ep.dP0 + ibeg * 2 : dP, 0,
                                                          EPI && ep.dP0 ? ilen * 8 : 0, 0x00020000);
-    float dsv[2] = {0.f, 0.f};  // (EPI) this item's column sums of dP
     // per-camera constants of the attention backward (edge_cam_bwd_kernel)
     f32x4 xr[2], gv[2];
     float M[2], inv[2], delta[2];
@@ -1269,8 +1269,9 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const bool live = 4 * g + r < nrows;
-          dsv[0] += live ? dv[r][0] : 0.f;
-          dsv[1] += live ? dv[r][1] : 0.f;
+          // the item's column sums of dP (dSv) live in LDS: no registers held across tiles
+          Ls[0] += live ? dv[r][0] : 0.f;
+          Ls[1] += live ? dv[r][1] : 0.f;
           if (!GASFM_PBWD_EPI_T) {  // A/B: 16-lane sums per row (DPP), lanes c = 0, 1 store
             const float s0 = sum16(fmaf(dv[r][0], V[4 * F + c], dv[r][1] * V[4 * F + 16 + c]));
             const float s1 = sum16(fmaf(dv[r][0], V[5 * F + c], dv[r][1] * V[5 * F + 16 + c]));
@@ -1338,7 +1339,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
           }
           // this half's 10 sums: [ap[0] | ap[1] | a0] at Lw[lane * 20 + 10 ft ..] (lane stride 20
           // floats: a 16-lane b128 access touches 16 distinct bank quads)
-          float* q = Lw + lane * PB_NDW + 10 * ft;
+          float* q = Lw + 10 * ft;
           if (!GASFM_PBWD_LW4) {  // A/B: scalar read-modify-writes
 #pragma unroll
             for (int k = 0; k < 8; ++k) q[k] += ap[k / 4][k % 4];
@@ -1370,7 +1371,8 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
       }
     }
     if (EPI) {
-      const float s0 = sum_groups(dsv[0]) * ep.scale, s1 = sum_groups(dsv[1]) * ep.scale;
+      const float s0 = sum_groups(Ls[0]) * ep.scale, s1 = sum_groups(Ls[1]) * ep.scale;
+      Ls[0] = Ls[1] = 0.f;
       if (g == 0) {
         float* d = (w.slot < 0) ? ep.dSv + seg * F : ep.part_dsv + int64_t(w.slot) * F;
         d[c] = s0;
@@ -1387,9 +1389,9 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
 #pragma unroll
     for (int ft = 0; ft < 2; ++ft) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[56 + ft * 8 + k] = Lw[lane * PB_NDW + 10 * ft + k];
+      for (int k = 0; k < 8; ++k) v[56 + ft * 8 + k] = Lw[10 * ft + k];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) v[72 + ft * 2 + j] = Lw[lane * PB_NDW + 10 * ft + 8 + j];
+      for (int j = 0; j < 2; ++j) v[72 + ft * 2 + j] = Lw[10 * ft + 8 + j];
     }
   }
 #pragma unroll
