@@ -59,6 +59,9 @@ _SIGS = {
     "gasfm_edge_cam_pbwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _f32, _vp, _i64, _vp, _vp, _f32, _vp,
                                    _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _vp, _i64, _vp,
                                    _vp, _vp]),
+    "gasfm_edge0_seam_fwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _f32,
+                                    _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32,
+                                    _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
     "gasfm_edge_cam_pbwd_ex": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _f32, _vp, _i64, _vp, _vp, _f32,
                                       _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _vp, _i64,
                                       _vp, _vp, _i64, _vp, _i32, _f32, _vp, _vp, _vp, _vp, _i32, _vp]),
@@ -626,6 +629,24 @@ def edge_seam_fwd(Pb, P0, pt, lnw_b, lnb_b, eps_b, Wp, bp, Sp, Sv, Sg, scale, Po
                                    out.stride(0) if out is not None else 0, _p(seg_max), _p(seg_sum), ldStat, _p(part),
                                    _stream(Pb))
     check(st, "gasfm_edge_seam_fwd")
+
+
+def edge0_seam_fwd(P, pt, lna_w, lna_b, lnb_w, lnb_b, eps0, Wp, bp, Wsk, bsk, Sp, Sv, Sg, scale, Pout, ln_w, ln_b, eps,
+                   Wpt, bpt, Wc, bc, XLp, pos, XR, att, bias, slope, plan_items, n_items, finalize, out, seg_max,
+                   seg_sum, part, ldStat=4):
+    """Block 0's edge epilogue (2-wide P, edge0_epilogue_fwd) + block 1's prologue and camera
+    attention forward in one pass (csrc/edge_cam.hip edge_seam_fwd, EP0); outputs as
+    edge_seam_fwd's."""
+    _req(P, "P", 2)
+    ldXR = _rows32(XR, "XR")
+    ldSv = _rows32(Sv, "Sv")
+    st = lib().gasfm_edge0_seam_fwd(_p(P), _p(pt), _p(lna_w), _p(lna_b), _p(lnb_w), _p(lnb_b), eps0, _p(Wp), _p(bp),
+                                    _p(Wsk), _p(bsk), _p(Sp), _p(Sv), ldSv, _p(Sg), scale, _p(Pout), _p(ln_w), _p(ln_b),
+                                    eps, _p(Wpt), _p(bpt), _p(Wc), _p(bc), _p(XLp), XLp.stride(0), _p(pos), _p(XR),
+                                    ldXR, _p(att), _p(bias), slope, _p(plan_items), n_items, int(finalize), _p(out),
+                                    out.stride(0) if out is not None else 0, _p(seg_max), _p(seg_sum), ldStat,
+                                    _p(part), _stream(P))
+    check(st, "gasfm_edge0_seam_fwd")
 
 
 def edge_cam_pbwd_part_shape(n_items, dwp_cols=0):

@@ -425,6 +425,11 @@ struct SeamEpi {
   const float* Sg;    // [32]
   float scale;
   float* Pout;        // P' [E, 32]
+  // block 0's epilogue (EP0): P [E, 2], gam / bet = LN_a, Wp [32 x 2], and
+  const float* gb;    // LN_b [2]
+  const float* bb;
+  const float* Wsk;   // skip projection [32 x 2]
+  const float* bsk;   // [32]
 };
 
 #ifndef GASFM_SEAM_MINW
@@ -451,7 +456,10 @@ struct SeamEpi {
 #ifndef GASFM_SEAM_UST
 #define GASFM_SEAM_UST 1
 #endif
-template <bool LN>
+// EP0: block 0's epilogue (edge0_epilogue_fwd, 2-wide P) as the seam's first half:
+//   P' = Wsk relu(LN_b(P)) + bsk + scale (Wp relu(LN_a(P)) + bp + Sg + Sp[pt] + Sv[cam])
+// computed per lane on its 8 features (2-wide products: no MFMA), in edge0_epilogue_fwd's order.
+template <bool LN, bool EP0>
 __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kernel(
     SeamEpi ep, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
     const float* __restrict__ Wpt, const float* __restrict__ bpt, const float* __restrict__ Wc,
@@ -461,19 +469,20 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
     int64_t ldOut, float* __restrict__ seg_max, float* __restrict__ seg_sum, int64_t ldStat,
     float* __restrict__ part) {
   // vector table (32 floats each): 0 gamma_b 1 beta_b 2 bp+Sg 3 Wp[:,32] 4 Wp[:,33] 5 gamma 6 beta
-  // 7 bpt 8 bc 9 att 10 bias
+  // 7 bpt 8 bc 9 att 10 bias; EP0: 0 Wsk[:,0] 1 Wsk[:,1] 2 bp+Sg 3 Wp[:,0] 4 Wp[:,1] 11 bsk
   __shared__ __attribute__((aligned(16))) float Wl[NX * F];   // [Wpt; Wc] slabs
-  __shared__ __attribute__((aligned(16))) float WpQ[F * F];   // Wp_b[:, :32] slabs
-  __shared__ __attribute__((aligned(16))) float V[11 * F];
+  __shared__ __attribute__((aligned(16))) float WpQ[EP0 ? 4 : F * F];  // Wp_b[:, :32] slabs
+  __shared__ __attribute__((aligned(16))) float V[12 * F];
   stage_slabs32<NX, kThreads>([&](int q) { return q < F * F ? Wpt[q] : Wc[q - F * F]; }, Wl);
-  stage_slabs32<F, kThreads>([&](int q) { return ep.Wp[(q / F) * ep.ldWp + q % F]; }, WpQ);
+  if (!EP0) stage_slabs32<F, kThreads>([&](int q) { return ep.Wp[(q / F) * ep.ldWp + q % F]; }, WpQ);
   if (threadIdx.x < F) {
     const int f = threadIdx.x;
-    V[f] = ep.gam[f];
-    V[F + f] = ep.bet[f];
+    V[f] = EP0 ? ep.Wsk[2 * f] : ep.gam[f];
+    V[F + f] = EP0 ? ep.Wsk[2 * f + 1] : ep.bet[f];
     V[2 * F + f] = ep.bp[f] + ep.Sg[f];
-    V[3 * F + f] = ep.P0 ? ep.Wp[f * ep.ldWp + 32] : 0.f;
-    V[4 * F + f] = ep.P0 ? ep.Wp[f * ep.ldWp + 33] : 0.f;
+    V[3 * F + f] = EP0 ? ep.Wp[2 * f] : (ep.P0 ? ep.Wp[f * ep.ldWp + 32] : 0.f);
+    V[4 * F + f] = EP0 ? ep.Wp[2 * f + 1] : (ep.P0 ? ep.Wp[f * ep.ldWp + 33] : 0.f);
+    V[11 * F + f] = EP0 ? ep.bsk[f] : 0.f;
     V[5 * F + f] = LN ? gam[f] : 1.f;
     V[6 * F + f] = LN ? bet[f] : 0.f;
     V[7 * F + f] = bpt[f];
@@ -484,6 +493,10 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
   __syncthreads();
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int c = lane & 15, g = lane >> 4;
+  // (EP0) LN_a and LN_b over the 2 input features
+  const float ga0 = EP0 ? ep.gam[0] : 0.f, ga1 = EP0 ? ep.gam[1] : 0.f, ba0 = EP0 ? ep.bet[0] : 0.f,
+              ba1 = EP0 ? ep.bet[1] : 0.f, gb0 = EP0 ? ep.gb[0] : 0.f, gb1 = EP0 ? ep.gb[1] : 0.f,
+              bb0 = EP0 ? ep.bb[0] : 0.f, bb1 = EP0 ? ep.bb[1] : 0.f;
   auto vec = [&](int which, int q) {
     const float4 t = *reinterpret_cast<const float4*>(V + which * F + 16 * q + 4 * g);
     return f32x4{t.x, t.y, t.z, t.w};
@@ -494,12 +507,12 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
   int32_t npos = 0, npt = 0;
   float2 nq = make_float2(0.f, 0.f);
   const int32_t* posp = pos ? pos : reinterpret_cast<const int32_t*>(ep.P);
-  const float* p0p = ep.P0 ? ep.P0 : ep.P;
+  const float* p0p = EP0 ? ep.P : (ep.P0 ? ep.P0 : ep.P);  // EP0: the 2-wide P row itself
   f32x4 nsp[2];  // GASFM_SEAM_SPPF: Sp[pt] of the next tile
   auto issue = [&](int64_t row0, int nrows) {
     const int64_t e = row0 + (c < nrows ? c : 0);
     if (GASFM_SEAM_SPPF) npt = ep.pt[e];  // first: waiting for it does not wait for the P rows
-    load_slabs32(ep.P, row0, nrows, ns, lane);
+    if (!EP0) load_slabs32(ep.P, row0, nrows, ns, lane);
     npos = posp[e];
     if (!GASFM_SEAM_SPPF) npt = ep.pt[e];
     nq = *reinterpret_cast<const float2*>(p0p + e * 2);
@@ -580,33 +593,52 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
       }
       const bool valid = c < nrows;
       // ---- epilogue of block b (T layout)
-      f32x4 ph[2] = {pb[0], pb[1]};
-      {
-        float gs[2][4], bs[2][4];
+      f32x4 pn[2];  // P' (this block's output, the next block's input)
+      if (EP0) {
+        // block 0: 2-wide P (q0), LN_a / LN_b over its 2 features (edge0_epilogue_fwd's order)
+        const float mean = 0.5f * (q0.x + q0.y);
+        const float d0 = q0.x - mean, d1 = q0.y - mean;
+        const float rs = rsqrtf(0.5f * (d0 * d0 + d1 * d1) + ep.eps);
+        const float xh0 = d0 * rs, xh1 = d1 * rs;
+        const float ha0 = fmaxf(fmaf(xh0, ga0, ba0), 0.f), ha1 = fmaxf(fmaf(xh1, ga1, ba1), 0.f);
+        const float hb0 = fmaxf(fmaf(xh0, gb0, bb0), 0.f), hb1 = fmaxf(fmaf(xh1, gb1, bb1), 0.f);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          const f32x4 ga = vec(0, q), be = vec(1, q);
+          const f32x4 ka = vec(0, q), kb = vec(1, q), cs = vec(2, q), wa = vec(3, q), wb = vec(4, q), bs = vec(11, q);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            gs[q][r] = ga[r];
-            bs[q][r] = be[r];
+            const float d = fmaf(wa[r], ha0, fmaf(wb[r], ha1, cs[r])) + sp[q][r] + sv[q][r];
+            pn[q][r] = fmaf(d, ep.scale, fmaf(ka[r], hb0, fmaf(kb[r], hb1, bs[r])));
           }
         }
-        phat_slabs<true>(ph, gs, bs, ep.eps);
-      }
-      f32x4 y[2] = {zero4(), zero4()};
-      xl_slabs<2>(reinterpret_cast<const float4*>(WpQ), ph, y, lane);
-      f32x4 pn[2];  // P' (this block's output, the next block's input)
+      } else {
+        f32x4 ph[2] = {pb[0], pb[1]};
+        {
+          float gs[2][4], bs[2][4];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const f32x4 cs = vec(2, q), w32 = vec(3, q), w33 = vec(4, q);
+          for (int q = 0; q < 2; ++q) {
+            const f32x4 ga = vec(0, q), be = vec(1, q);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float d = y[q][r] + cs[r];
-          d = fmaf(w32[r], q0.x, fmaf(w33[r], q0.y, d));
-          // (d + Sv) + Sp: the gathered Sp row is consumed last (not hoisted to the tile's top)
-          d = GASFM_SEAM_SPPF ? (d + sv[q][r]) + sp[q][r] : d + (sp[q][r] + sv[q][r]);
-          pn[q][r] = fmaf(d, ep.scale, pb[q][r]);
+            for (int r = 0; r < 4; ++r) {
+              gs[q][r] = ga[r];
+              bs[q][r] = be[r];
+            }
+          }
+          phat_slabs<true>(ph, gs, bs, ep.eps);
+        }
+        f32x4 y[2] = {zero4(), zero4()};
+        xl_slabs<2>(reinterpret_cast<const float4*>(WpQ), ph, y, lane);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const f32x4 cs = vec(2, q), w32 = vec(3, q), w33 = vec(4, q);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float d = y[q][r] + cs[r];
+            d = fmaf(w32[r], q0.x, fmaf(w33[r], q0.y, d));
+            // (d + Sv) + Sp: the gathered Sp row is consumed last (not hoisted to the tile's top)
+            d = GASFM_SEAM_SPPF ? (d + sv[q][r]) + sp[q][r] : d + (sp[q][r] + sv[q][r]);
+            pn[q][r] = fmaf(d, ep.scale, pb[q][r]);
+          }
         }
       }
       if (GASFM_SEAM_SPPF) {
@@ -1630,7 +1662,8 @@ extern "C" int gasfm_edge_seam_fwd(const float* Pb, const float* P0, const int32
                 "gasfm_edge_seam_fwd: aligned rows required");
   if (n_items == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const SeamEpi ep{Pb, P0, pt, ln_wb, ln_bb, eps_b, Wp, ldWp, bp, Sp, Sv, ldSv, Sg, scale, Pout};
+  const SeamEpi ep{Pb, P0, pt, ln_wb, ln_bb, eps_b, Wp, ldWp, bp, Sp, Sv, ldSv, Sg, scale, Pout,
+                   nullptr, nullptr, nullptr, nullptr};
   auto launch = [&](auto kern) {
     const int grid = resident_grid(reinterpret_cast<const void*>(kern), kThreads, 0, n_items, kWaves);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, st, ep, ln_w, ln_b, eps, Wpt, bpt, Wc, bc, XLp, ldXLp,
@@ -1638,8 +1671,38 @@ extern "C" int gasfm_edge_seam_fwd(const float* Pb, const float* P0, const int32
                        ldStat, part);
   };
   if (ln_w)
-    launch(&edge_seam_fwd_kernel<true>);
+    launch(&edge_seam_fwd_kernel<true, false>);
   else
-    launch(&edge_seam_fwd_kernel<false>);
+    launch(&edge_seam_fwd_kernel<false, false>);
   return launch_status("gasfm_edge_seam_fwd");
+}
+
+extern "C" int gasfm_edge0_seam_fwd(const float* P, const int32_t* pt, const float* ln_a_w, const float* ln_a_b,
+                                    const float* ln_b_w, const float* ln_b_b, float eps0, const float* Wp,
+                                    const float* bp, const float* Wsk, const float* bsk, const float* Sp,
+                                    const float* Sv, int64_t ldSv, const float* Sg, float scale, float* Pout,
+                                    const float* ln_w, const float* ln_b, float eps, const float* Wpt,
+                                    const float* bpt, const float* Wc, const float* bc, float* XLp, int64_t ldXLp,
+                                    const int32_t* pos, const float* XR, int64_t ldXR, const float* att,
+                                    const float* bias, float slope, const gasfm_work_item* items, int32_t n_items,
+                                    int32_t finalize, float* out, int64_t ldOut, float* seg_max, float* seg_sum,
+                                    int64_t ldStat, float* part, void* stream) {
+  GASFM_REQUIRE(n_items >= 0 && P && pt && ln_a_w && ln_a_b && ln_b_w && ln_b_b && Wp && bp && Wsk && bsk && Sp &&
+                    Sv && Sg && Pout && ln_w && ln_b && Wpt && bpt && Wc && bc && XLp && XR && att && items,
+                "gasfm_edge0_seam_fwd: null pointer");
+  GASFM_REQUIRE((out && seg_max && seg_sum && (bias || !finalize)) || part, "gasfm_edge0_seam_fwd: no outputs");
+  GASFM_REQUIRE(ldXLp >= F && ldXLp % 4 == 0 && ldXR >= F && ldXR % 4 == 0 && ldSv >= F && ldSv % 4 == 0 &&
+                    (!out || (ldOut >= F && ldOut % 4 == 0)) && reinterpret_cast<uintptr_t>(P) % 8 == 0 &&
+                    aligned16(Pout) && aligned16(Sp) && aligned16(Sv) && aligned16(XLp) && aligned16(XR) &&
+                    (!out || aligned16(out)) && (!part || aligned16(part)),
+                "gasfm_edge0_seam_fwd: aligned rows required");
+  if (n_items == 0) return GASFM_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const SeamEpi ep{P, nullptr, pt, ln_a_w, ln_a_b, eps0, Wp, 2, bp, Sp, Sv, ldSv, Sg, scale, Pout,
+                   ln_b_w, ln_b_b, Wsk, bsk};
+  const auto kern = &edge_seam_fwd_kernel<true, true>;
+  const int grid = resident_grid(reinterpret_cast<const void*>(kern), kThreads, 0, n_items, kWaves);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, st, ep, ln_w, ln_b, eps, Wpt, bpt, Wc, bc, XLp, ldXLp, pos,
+                     XR, ldXR, att, bias, slope, items, n_items, finalize, out, ldOut, seg_max, seg_sum, ldStat, part);
+  return launch_status("gasfm_edge0_seam_fwd");
 }

@@ -431,16 +431,21 @@ class _EpiState:
 
 
 class PendingEpilogue:
-    """Block b's EdgeEpilogueFn.apply arguments, held so that block b+1 can run it together with
-    its own prologue (SeamFn); materialize() runs it alone (any other consumer of P')."""
+    """Block b's EdgeEpilogueFn.apply arguments (block0: Block0EpilogueFn's), held so that block b+1
+    can run it together with its own prologue (SeamFn / Seam0Fn); materialize() runs it alone (any
+    other consumer of P')."""
 
-    def __init__(self, args):
+    def __init__(self, args, block0=False):
         self.args = args
+        self.block0 = block0
         self._P = None
+
+    def seam_fn(self):
+        return Seam0Fn if self.block0 else SeamFn
 
     def materialize(self):
         if self._P is None:
-            self._P = EdgeEpilogueFn.apply(*self.args)
+            self._P = (Block0EpilogueFn if self.block0 else EdgeEpilogueFn).apply(*self.args)
         return self._P
 
 
@@ -491,25 +496,83 @@ class Block0EpilogueFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dPo):
-        P, lna_w, lna_b, lnb_w, lnb_b, Wp, Wsk = ctx.saved_tensors
-        edges = ctx.edges
-        dPo = dPo.contiguous()
-        dev = P.device
-        E = P.shape[0]
-        pc, pp = edges.plans["proj2view"], edges.plans["proj2scenepoint"]
-        dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
-        part_dsv = torch.empty((max(pc.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
-        aux = torch.empty((E, 4), dtype=torch.float32, device=dev)
-        rows = _native.edge0_part_rows(1, E, pc.n_items)
-        part = torch.empty((rows, 164), dtype=torch.float32, device=dev)
-        _native.edge0_epilogue_bwd(pc.items, pc.n_items, dPo, P, lna_w, lna_b, lnb_w, lnb_b, ctx.eps,
-                                   Wp.contiguous(), Wsk.contiguous(), PROJ_SCALE, dSv, part_dsv, aux, part)
-        bwd_combine(pc, part_dsv, 32, dSv)
-        tot = _native.colsum(part)
-        dSg = _native.colsum(dSv)
-        dSp = torch.empty((edges.n, 32), dtype=torch.float32, device=dev)
-        part_dsp = torch.empty((max(pp.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
-        _native.segment_rowsum(pp.items, pp.n_items, pp.perm, dPo, PROJ_SCALE, dSp, part_dsp)
-        bwd_combine(pp, part_dsp, 32, dSp)
-        return (None, aux, dSp, dSv, dSg.view(ctx.sg_shape), tot[:64].view(32, 2), dSg.clone(), None, None,
-                tot[160:162], tot[162:164], tot[64:128].view(32, 2), tot[128:160], None, None)
+        return _epilogue0_backward(ctx, ctx.saved_tensors, dPo)
+
+
+def _epilogue0_backward(ctx, saved, dPo):
+    """Block0EpilogueFn's backward from its saved state (ctx attributes eps, edges, sg_shape): its 15
+    input gradients."""
+    P, lna_w, lna_b, lnb_w, lnb_b, Wp, Wsk = saved
+    edges = ctx.edges
+    dPo = dPo.contiguous()
+    dev = P.device
+    E = P.shape[0]
+    pc, pp = edges.plans["proj2view"], edges.plans["proj2scenepoint"]
+    dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
+    part_dsv = torch.empty((max(pc.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
+    aux = torch.empty((E, 4), dtype=torch.float32, device=dev)
+    rows = _native.edge0_part_rows(1, E, pc.n_items)
+    part = torch.empty((rows, 164), dtype=torch.float32, device=dev)
+    _native.edge0_epilogue_bwd(pc.items, pc.n_items, dPo, P, lna_w, lna_b, lnb_w, lnb_b, ctx.eps,
+                               Wp.contiguous(), Wsk.contiguous(), PROJ_SCALE, dSv, part_dsv, aux, part)
+    bwd_combine(pc, part_dsv, 32, dSv)
+    tot = _native.colsum(part)
+    dSg = _native.colsum(dSv)
+    dSp = torch.empty((edges.n, 32), dtype=torch.float32, device=dev)
+    part_dsp = torch.empty((max(pp.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
+    _native.segment_rowsum(pp.items, pp.n_items, pp.perm, dPo, PROJ_SCALE, dSp, part_dsp)
+    bwd_combine(pp, part_dsp, 32, dSp)
+    return (None, aux, dSp, dSv, dSg.view(ctx.sg_shape), tot[:64].view(32, 2), dSg.clone(), None, None,
+            tot[160:162], tot[162:164], tot[64:128].view(32, 2), tot[128:160], None, None)
+
+
+class Seam0Fn(torch.autograd.Function):
+    """Block 0's Block0EpilogueFn and block 1's EdgeCamFn as ONE forward kernel
+    (gasfm_edge0_seam_fwd: P_1 is written once and never read back); the backward is the two
+    Functions' own backwards in autograd's order.
+
+    Inputs: the 15 of Block0EpilogueFn.forward, then the 19 of EdgeCamFn.forward after P (whose P
+    is this Function's own output P_1).  Outputs: (P_1, XLp, camera aggregates, token)."""
+
+    @staticmethod
+    def forward(ctx, P, token, Sp, Sv, Sg, Wp, bp, lna_w, lna_b, lnb_w, lnb_b, Wsk, bsk, eps0, edges,
+                ln_w, ln_b, Wpt, bpt, Wc, bc, Wp_n, eps, pos, XR, att, bias, plan, heads, slope, plan_partial, shard,
+                P0_n=None, dwp_n=False):
+        E, dev = P.shape[0], P.device
+        HC = att.numel()
+        if heads != 4 or HC != 32 or ln_w is None:
+            raise ValueError("Seam0Fn: the fused kernels are for H = 4, C = 8 with the block's LayerNorm")
+        attf = att.reshape(-1).contiguous()
+        XLp = torch.empty((E, 32), dtype=torch.float32, device=dev)
+        Pn = torch.empty((E, Wp.shape[0]), dtype=torch.float32, device=dev)
+        Pc, Wp_c, Wsk_c = P.contiguous(), Wp.contiguous(), Wsk.contiguous()
+        args0 = (Pc, edges.pt, lna_w, lna_b, lnb_w, lnb_b, eps0, Wp_c, bp.contiguous(), Wsk_c, bsk.contiguous(),
+                 Sp.contiguous(), _rows(Sv), Sg.reshape(-1).contiguous(), PROJ_SCALE, Pn)
+
+        def launch(items, n_items, finalize, out, smax, ssum, part):
+            _native.edge0_seam_fwd(*args0, ln_w, ln_b, eps, Wpt, bpt, Wc, bc, XLp, pos, XR, attf,
+                                   bias if finalize else None, slope, items, n_items, finalize, out, smax, ssum, part)
+        out, smax, ssum = _cam_attention_fwd(launch, bias, plan, heads, HC, plan_partial, shard, dev)
+        # Block0EpilogueFn's state
+        ctx.e_eps, ctx.edges, ctx.sg_shape = eps0, edges, Sg.shape
+        # EdgeCamFn's state
+        ctx.eps, ctx.heads, ctx.slope, ctx.plan = eps, heads, slope, plan
+        ctx.att_shape = att.shape
+        ctx.has_ln = True
+        ctx.dwp = bool(dwp_n)
+        ctx.defer = _native.defer_token(ln_w, ln_b, Wpt, bpt, Wc, bc, att, bias, Wp_n if dwp_n else None)
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(Pc, lna_w, lna_b, lnb_w, lnb_b, Wp_c, Wsk_c, Pn, ln_w, ln_b, Wpt, Wc, bc, Wp_n, XR,
+                              attf, bias, out, smax, ssum, P0_n)
+        token_n = P.new_empty((1, 1)).expand(E, Pn.shape[1])
+        return Pn, XLp, out, token_n
+
+    @staticmethod
+    def backward(ctx, gPn, dXLp, g_c, dtoken):
+        saved = ctx.saved_tensors
+        epi, cam = saved[:7], saved[7:]
+        dRes = dtoken.contiguous() if (dtoken is not None and dtoken.stride(0) != 0) else None
+        gc = _cam_backward(ctx, cam, dXLp, g_c, dRes)
+        dPn = gc[0] if gPn is None else gc[0] + gPn
+        ectx = _EpiState(ctx.e_eps, ctx.edges, ctx.sg_shape, None)
+        return _epilogue0_backward(ectx, epi, dPn) + gc[1:]

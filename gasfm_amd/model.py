@@ -295,6 +295,15 @@ def _seam_ok(args):
             and sp.shape[1] == 32 and sv.shape[1] == 32)
 
 
+def _seam0_ok(args):
+    """Block 0's epilogue shapes are the block-0 seam kernel's: P [E, 2], lin_proj and the skip
+    projection [32, 2], the one-row (or folded) global term."""
+    P, _, sp, sv, sg, W, _, _, _, _, _, Wsk = args[:12]
+    return (P.is_cuda and P.dtype == torch.float32 and P.dim() == 2 and P.shape[1] == 2
+            and tuple(W.shape) == (32, 2) and tuple(Wsk.shape) == (32, 2) and sg.numel() == 32
+            and sp.shape[1] == 32 and sv.shape[1] == 32)
+
+
 def _fold_global(sv, sg, plans):
     """SceneBatch (batch.py): the per-edge global term of scene s, Sg[s], added to the per-camera
     term of its cameras (every camera belongs to one scene), so the edge kernels see one scene:
@@ -494,13 +503,16 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         def attend(XRp, XRc, sec):
             cam_args = (ln_w, ln_b, W, b, W2, b2, Wp, eps, pos, XRc, cc.att, cc.bias, pc, cc.heads, cc.negative_slope,
                         plans.get("_partial", {}).get("proj2view"), plans.get("_shard"), P0, dwp)
-            if isinstance(P, PendingEpilogue):  # the previous block's epilogue in the same kernel
-                Pn, XLp, agg_c, token = SeamFn.apply(*P.args, *cam_args)
-                P._P = Pn
+            Pe = P
+            if isinstance(Pe, PendingEpilogue) and Pe.block0 and ln_w is None:
+                Pe = Pe.materialize()  # the block-0 seam is built for a LayerNorm prologue only
+            if isinstance(Pe, PendingEpilogue):  # the previous block's epilogue in the same kernel
+                Pn, XLp, agg_c, token = Pe.seam_fn().apply(*Pe.args, *cam_args)
+                Pe._P = Pn
                 holder["P"] = Pn
             else:
-                XLp, agg_c, token = EdgeCamFn.apply(P, *cam_args)
-                holder["P"] = P
+                XLp, agg_c, token = EdgeCamFn.apply(Pe, *cam_args)
+                holder["P"] = Pe
             holder["token"] = token
             agg_p = GatAttentionFn.apply(XLp, XRp, cp.att, cp.bias, pp, cp.heads, cp.negative_slope, pos is not None,
                                          sec)[0]
@@ -639,9 +651,11 @@ class GraphAttnSfMLayer(Module):
         sv, sg = _wrap_boundary(plans.get("_shard"), sv, sg, carry)
         sv, sg = _fold_global(sv, sg, plans)
         sk = self.skip_projection.lin_proj
-        P_new = Block0EpilogueFn.apply(P.contiguous(), token, sp, sv, sg, pfu.lin_proj.weight, pfu.lin_proj.bias,
-                                       la.weight, la.bias, lb.weight, lb.bias, sk.weight, sk.bias, la.eps, edges)
-        return P_new, pts, view, glob
+        args = (P.contiguous(), token, sp, sv, sg, pfu.lin_proj.weight, pfu.lin_proj.bias, la.weight, la.bias,
+                lb.weight, lb.bias, sk.weight, sk.bias, la.eps, edges)
+        if EDGE_SEAM and _seam0_ok(args):  # run with block 1's prologue (edge_block.Seam0Fn)
+            return PendingEpilogue(args, block0=True), pts, view, glob
+        return Block0EpilogueFn.apply(*args), pts, view, glob
 
     def forward_fused(self, P, plans, edges, prev_pt, prev_view, prev_glob, P0, carry=None, nxt=None):
         """Blocks >= 1 with the fused HIP edge kernels (see gasfm_amd/edge_block.py).  P may be the

@@ -164,6 +164,20 @@ int gasfm_edge_seam_fwd(const float* Pb, const float* P0, const int32_t* pt, con
                         const gasfm_work_item* items, int32_t n_items, int32_t finalize, float* out, int64_t ldOut,
                         float* seg_max, float* seg_sum, int64_t ldStat, float* part, void* stream);
 
+/* Block 0's edge epilogue (2-wide P: P' = Wsk relu(LN_b(P)) + bsk + scale (Wp relu(LN_a(P)) + bp +
+ * Sg + Sp[pt] + Sv[cam]), gasfm_edge0_epilogue_fwd) and block 1's prologue + camera attention
+ * (gasfm_edge_cam_fwd) in ONE pass, as gasfm_edge_seam_fwd for the 32-wide blocks (round 3).
+ * Replaces (reference): layers.py:245-261 / 911-956 of block 0 and 232-234, 329-335 of block 1. */
+int gasfm_edge0_seam_fwd(const float* P, const int32_t* pt, const float* ln_a_w, const float* ln_a_b,
+                         const float* ln_b_w, const float* ln_b_b, float eps0, const float* Wp, const float* bp,
+                         const float* Wsk, const float* bsk, const float* Sp, const float* Sv, int64_t ldSv,
+                         const float* Sg, float scale, float* Pout, const float* ln_w, const float* ln_b, float eps,
+                         const float* Wpt, const float* bpt, const float* Wc, const float* bc, float* XLp,
+                         int64_t ldXLp, const int32_t* pos, const float* XR, int64_t ldXR, const float* att,
+                         const float* bias, float slope, const gasfm_work_item* items, int32_t n_items,
+                         int32_t finalize, float* out, int64_t ldOut, float* seg_max, float* seg_sum, int64_t ldStat,
+                         float* part, void* stream);
+
 /* The camera attention's backward and the block's edge prologue backward in ONE pass over the
  * camera plan's items (gasfm_edge_cam_bwd followed by gasfm_edge_prologue_bwd with dXLc, without
  * storing dXLc): dP [E, 32], dXR per camera (split items: part_dxr rows for

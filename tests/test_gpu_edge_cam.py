@@ -184,3 +184,39 @@ def test_epilogue_fold_vs_unfolded(device, monkeypatch):
             assert err <= 1e-4 * float(g0.norm()) + 1e-9, (k, err, float(g0.norm()))
         own = float((g0 - torch.from_numpy(g64[k])).norm())
         assert err <= max(1e-3 * float(g0.norm()), 10 * own) + 1e-9, (k, err, own, float(g0.norm()))
+
+
+def test_block0_seam_vs_separate(device, monkeypatch):
+    """Block 0's epilogue run inside block 1's prologue + camera attention kernel (Seam0Fn,
+    gasfm_edge0_seam_fwd) against the separate Block0EpilogueFn + EdgeCamFn launches (EDGE_SEAM
+    off): one block-0 seam launch, the same outputs (the block-0 epilogue in the same operation
+    order) within 1e-5, and every parameter gradient within 1e-3 normwise."""
+    from oracle.weights import deterministic_state_dict
+    sc = synthetic.scaled_config4(0.05, seed=13)
+    data = gasfm_amd.SceneData.from_synthetic(sc).to(device)
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=3))
+    sd = deterministic_state_dict(net.state_dict(), torch.float64)
+    net.load_state_dict({k: v.float() for k, v in sd.items()})
+    net = net.to(device)
+    gen = torch.Generator().manual_seed(5)
+    cP = torch.randn((sc.m, 3, 4), generator=gen).to(device)
+    cX = torch.randn((4, sc.n), generator=gen).to(device)
+    calls = []
+    orig = _native.edge0_seam_fwd
+    monkeypatch.setattr(_native, "edge0_seam_fwd", lambda *a, **k: (calls.append(1), orig(*a, **k))[1])
+    res = {}
+    for seam in (False, True):
+        monkeypatch.setattr(model, "EDGE_SEAM", seam)
+        calls.clear()
+        net.zero_grad(set_to_none=True)
+        pred = net(data)
+        ((pred["Ps_norm"] * cP).sum() + (pred["pts3D"] * cX).sum()).backward()
+        torch.cuda.synchronize()
+        res[seam] = (pred["Ps_norm"].detach().clone(), pred["pts3D"].detach().clone(),
+                     {k: p.grad.detach().double().cpu() for k, p in net.named_parameters()}, len(calls))
+    assert res[False][3] == 0 and res[True][3] == 1, (res[False][3], res[True][3])
+    close(res[True][0], res[False][0], msg="Ps_norm")
+    close(res[True][1], res[False][1], msg="pts3D")
+    for k, g0 in res[False][2].items():
+        err = float((res[True][2][k] - g0).norm())
+        assert err <= 1e-3 * float(g0.norm()) + 1e-9, (k, err, float(g0.norm()))
