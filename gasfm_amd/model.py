@@ -39,6 +39,8 @@ EDGE_CAM = os.environ.get("GASFM_EDGE_CAM", "1") != "0"
 # A 32-wide block's edge epilogue is left pending (edge_block.PendingEpilogue) and run in one kernel
 # with the next block's prologue + camera attention (SeamFn, gasfm_edge_seam_fwd); 0: separately.
 EDGE_SEAM = os.environ.get("GASFM_EDGE_SEAM", "1") != "0"
+# Block 0's (2-wide) epilogue likewise inside block 1's prologue kernel (Seam0Fn, gasfm_edge0_seam_fwd).
+EDGE_SEAM0 = os.environ.get("GASFM_EDGE_SEAM0", "1") != "0"
 
 
 def replicated_to_local(x, shard):
@@ -653,7 +655,7 @@ class GraphAttnSfMLayer(Module):
         sk = self.skip_projection.lin_proj
         args = (P.contiguous(), token, sp, sv, sg, pfu.lin_proj.weight, pfu.lin_proj.bias, la.weight, la.bias,
                 lb.weight, lb.bias, sk.weight, sk.bias, la.eps, edges)
-        if EDGE_SEAM and _seam0_ok(args):  # run with block 1's prologue (edge_block.Seam0Fn)
+        if EDGE_SEAM and EDGE_SEAM0 and _seam0_ok(args):  # run with block 1's prologue (edge_block.Seam0Fn)
             return PendingEpilogue(args, block0=True), pts, view, glob
         return Block0EpilogueFn.apply(*args), pts, view, glob
 
