@@ -188,9 +188,11 @@ def test_epilogue_fold_vs_unfolded(device, monkeypatch):
 
 def test_block0_seam_vs_separate(device, monkeypatch):
     """Block 0's epilogue run inside block 1's prologue + camera attention kernel (Seam0Fn,
-    gasfm_edge0_seam_fwd) against the separate Block0EpilogueFn + EdgeCamFn launches (EDGE_SEAM
-    off): one block-0 seam launch, the same outputs (the block-0 epilogue in the same operation
-    order) within 1e-5, and every parameter gradient within 1e-3 normwise."""
+    gasfm_edge0_seam_fwd) against the separate launches (EDGE_SEAM off: Block0EpilogueFn +
+    EdgeCamFn, and the 32-wide epilogues unseamed as well): one block-0 seam launch, the same
+    outputs within 1e-5, and every parameter gradient within 1e-3 normwise or within 10x the
+    unseamed one's own distance from the fp64 oracle (as test_epilogue_fold_vs_unfolded)."""
+    from conftest import oracle_grads
     from oracle.weights import deterministic_state_dict
     sc = synthetic.scaled_config4(0.05, seed=13)
     data = gasfm_amd.SceneData.from_synthetic(sc).to(device)
@@ -199,8 +201,8 @@ def test_block0_seam_vs_separate(device, monkeypatch):
     net.load_state_dict({k: v.float() for k, v in sd.items()})
     net = net.to(device)
     gen = torch.Generator().manual_seed(5)
-    cP = torch.randn((sc.m, 3, 4), generator=gen).to(device)
-    cX = torch.randn((4, sc.n), generator=gen).to(device)
+    cP = torch.randn((sc.m, 3, 4), generator=gen, dtype=torch.float64)
+    cX = torch.randn((4, sc.n), generator=gen, dtype=torch.float64)
     calls = []
     orig = _native.edge0_seam_fwd
     monkeypatch.setattr(_native, "edge0_seam_fwd", lambda *a, **k: (calls.append(1), orig(*a, **k))[1])
@@ -210,13 +212,15 @@ def test_block0_seam_vs_separate(device, monkeypatch):
         calls.clear()
         net.zero_grad(set_to_none=True)
         pred = net(data)
-        ((pred["Ps_norm"] * cP).sum() + (pred["pts3D"] * cX).sum()).backward()
+        ((pred["Ps_norm"] * cP.float().to(device)).sum() + (pred["pts3D"] * cX.float().to(device)).sum()).backward()
         torch.cuda.synchronize()
         res[seam] = (pred["Ps_norm"].detach().clone(), pred["pts3D"].detach().clone(),
                      {k: p.grad.detach().double().cpu() for k, p in net.named_parameters()}, len(calls))
     assert res[False][3] == 0 and res[True][3] == 1, (res[False][3], res[True][3])
     close(res[True][0], res[False][0], msg="Ps_norm")
     close(res[True][1], res[False][1], msg="pts3D")
+    (g64, _), _ = oracle_grads(sd, sc, cP, cX)
     for k, g0 in res[False][2].items():
         err = float((res[True][2][k] - g0).norm())
-        assert err <= 1e-3 * float(g0.norm()) + 1e-9, (k, err, float(g0.norm()))
+        own = float((g0 - torch.from_numpy(g64[k])).norm())
+        assert err <= max(1e-3 * float(g0.norm()), 10 * own) + 1e-9, (k, err, own, float(g0.norm()))
