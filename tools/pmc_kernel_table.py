@@ -25,6 +25,8 @@ ALGO_MB = {  # config 4 algorithmic bytes per launch, DESIGN.md §5
     # round 3, edge epilogue backward folded into edge_cam_pbwd (+ P0 read, dP0 written: 16 B per edge)
     "edge_cam_pbwd_kernel<true, true, false, false>": 2049, "edge_cam_pbwd_kernel<true, true, true, true>": 2113,
     "edge_cam_pbwd_kernel<true, true, false, true>": 2081,
+    # the seam kernel's two modes (32-wide epilogue / block 0's 2-wide one: P 8 + P' 128 + XL 128 + pt, pos 8)
+    "edge_seam_fwd_kernel<true, false>": 1601, "edge_seam_fwd_kernel<true, true>": 1088,
 }
 
 
