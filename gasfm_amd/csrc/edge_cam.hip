@@ -1022,6 +1022,13 @@ __device__ __forceinline__ void prod_c2(const float4* __restrict__ Q, const f32x
 #ifndef GASFM_PBWD_EPI_T
 #define GASFM_PBWD_EPI_T 1
 #endif
+// 1: the camera item's XR and gout rows (8 VGPRs each, live across the item's tiles) parked in the
+// wave's LDS and re-read per tile; 0 (default): held in registers.  tools/gpu_pbwd_ab.sh, same box:
+// config 4 30.36-30.40 ms with 1 vs 30.23-30.26 with 0 (the unfolded kernel's 4 spills go, the
+// folded one keeps its 18, and the per-tile LDS reads cost more).
+#ifndef GASFM_PBWD_ITEM_LDS
+#define GASFM_PBWD_ITEM_LDS 0
+#endif
 #ifndef GASFM_PBWD_LW4
 #define GASFM_PBWD_LW4 0
 #endif
@@ -1044,7 +1051,8 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   constexpr int OV = 4 * QW, OT = OV + (EPI ? 6 : 4) * F, WT = 4 * TR * LDT;
   constexpr int OD = OT + kWaves * WT;
   constexpr int NLS = (DWP ? PB_NDW : 0) + (EPI ? 2 : 0);  // per-lane LDS sums
-  constexpr int NL = OD + kWaves * NLS * kW;
+  constexpr int OX = OD + kWaves * NLS * kW;                 // per wave: the item's [XR | gout] rows
+  constexpr int NL = OX + (GASFM_PBWD_ITEM_LDS ? kWaves * 2 * F : 0);
   __shared__ __attribute__((aligned(16))) float lds[NL];
   float* WcQ = lds;
   float* WptTQ = lds + QW;
@@ -1071,6 +1079,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   // (DWP) value k of this lane's dWp sums at Lw[k]; (EPI) the item's dSv column sums at Ls[0, 1]
   float* Lw = lds + OD + (wave * kW + lane) * NLS;
   float* Ls = Lw + (DWP ? PB_NDW : 0);
+  float* Xi = lds + OX + wave * 2 * F;  // (GASFM_PBWD_ITEM_LDS) [XR | gout] of the wave's camera item
 #pragma unroll
   for (int k = 0; k < NLS; ++k) Lw[k] = 0.f;
   const float gC[2] = {LN ? gam[c] : 1.f, LN ? gam[16 + c] : 1.f}, bC[2] = {LN ? bet[c] : 0.f, LN ? bet[16 + c] : 0.f};
@@ -1143,6 +1152,10 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
       const float4 b4 = *reinterpret_cast<const float4*>(bias + f0);
       xr[q] = f32x4{x4.x, x4.y, x4.z, x4.w};
       gv[q] = f32x4{g4v.x, g4v.y, g4v.z, g4v.w};
+      if (GASFM_PBWD_ITEM_LDS && c == 0) {
+        *reinterpret_cast<float4*>(Xi + f0) = x4;
+        *reinterpret_cast<float4*>(Xi + F + f0) = g4v;
+      }
       float d = fmaf(g4v.x, o4.x - b4.x, fmaf(g4v.y, o4.y - b4.y, fmaf(g4v.z, o4.z - b4.z, g4v.w * (o4.w - b4.w))));
       delta[q] = d + __shfl_xor(d, 16);
       M[q] = seg_max[seg * ldStat + h];
@@ -1210,13 +1223,20 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const f32x4 at = vecT(3, q);
+        f32x4 xrq = xr[q], gvq = gv[q];
+        if (GASFM_PBWD_ITEM_LDS) {
+          const float4 t0 = *reinterpret_cast<const float4*>(Xi + 16 * q + 4 * g);
+          const float4 t1 = *reinterpret_cast<const float4*>(Xi + F + 16 * q + 4 * g);
+          xrq = f32x4{t0.x, t0.y, t0.z, t0.w};
+          gvq = f32x4{t1.x, t1.y, t1.z, t1.w};
+        }
         float z[4], lz[4], p = 0.f, da = 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          z[r] = xc[q][r] + xr[q][r];
+          z[r] = xc[q][r] + xrq[r];
           lz[r] = leaky(z[r], slope);
           p = fmaf(lz[r], at[r], p);
-          da = fmaf(gv[q][r], xc[q][r], da);
+          da = fmaf(gvq[r], xc[q][r], da);
         }
         p += __shfl_xor(p, 16);
         da += __shfl_xor(da, 16);
@@ -1225,7 +1245,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float dz = de * at[r] * (z[r] > 0.f ? 1.f : slope);
-          dXc[q][r] = fmaf(alpha, gv[q][r], dz);  // 0 for invalid edges
+          dXc[q][r] = fmaf(alpha, gvq[r], dz);  // 0 for invalid edges
           dxr[q][r] += dz;
           datt[q][r] = fmaf(de, lz[r], datt[q][r]);
         }
