@@ -42,10 +42,13 @@ def camera_max_piece(num_edges):
         mp //= 2
     return mp
 LANES_MAX_AVG = 32  # 4-wide convs with <= this many edges per item on average: one lane per item
-# The lane-per-item forward replaced a 226 us launch by a 43 us one at config 4; the lane-per-item
-# backward measured 193 us against 153 us for the wave-per-item kernel (its dXL rows are scattered
-# into edge order either way), so the backward keeps the general kernel unless this is set.
-BWD_LANES = False
+# The lane-per-item forward replaced a 226 us launch by a 43 us one at config 4.  The backward with
+# one lane per item measured 193 us against 153 us for the wave-per-item kernel (its dXL rows are
+# scattered into edge order either way); with a group of 8 lanes per item (round 3: a group's rows
+# per step are one 128-B line) it takes 98 us against the wave-per-item kernel's 134 us in the
+# config-4 step (tools/gpu_lanes_ab.sh), so it is the default; GASFM_ATTN_BWD_LANES=0 restores the
+# general kernel.
+BWD_LANES = os.environ.get("GASFM_ATTN_BWD_LANES", "1") != "0"
 
 
 def _lanes(plan, heads, HC):

@@ -104,6 +104,14 @@ __global__ __launch_bounds__(kT) void attn_fwd_lanes_kernel(
 
 //   alpha = exp(l - M) / (S + 1e-16);  delta = g . (out - bias) per head;  de = alpha (g x - delta)
 //   dz = de att leaky'(z);  dXL = alpha g + dz;  dXR = sum dz;  datt += de leaky(z)
+// G lanes per work item (round 3: G = 8, GASFM_ATTN_BWD_LANES_G): lane `sub` of the group takes the
+// item's edges sub, sub + G, ...; a group's G rows per step are consecutive (one 128-B line of the
+// point-ordered XL half, where G = 1 reads 64 lines per instruction), the per-item dXR sums over
+// the group's lanes (xor butterfly, fixed order).
+#ifndef GASFM_ATTN_BWD_LANES_G
+#define GASFM_ATTN_BWD_LANES_G 8
+#endif
+template <int G>
 __global__ __launch_bounds__(kT) void attn_bwd_lanes_kernel(
     const float* __restrict__ XL, int64_t ldXL, const float* __restrict__ XR, int64_t ldXR,
     const float* __restrict__ att, const float* __restrict__ bias, const int32_t* __restrict__ perm,
@@ -114,8 +122,9 @@ __global__ __launch_bounds__(kT) void attn_bwd_lanes_kernel(
   const float4 a4 = ld4(att), b4 = ld4(bias);
   const float a[4] = {a4.x, a4.y, a4.z, a4.w}, bv[4] = {b4.x, b4.y, b4.z, b4.w};
   float datt[4] = {0.f, 0.f, 0.f, 0.f}, dbias[4] = {0.f, 0.f, 0.f, 0.f};
-  const int nthreads = gridDim.x * kT;
-  for (int it = blockIdx.x * kT + threadIdx.x; it < n_items; it += nthreads) {
+  const int sub = threadIdx.x & (G - 1);
+  const int ngroups = gridDim.x * (kT / G);
+  for (int it = (blockIdx.x * kT + threadIdx.x) / G; it < n_items; it += ngroups) {
     const gasfm_work_item w = items[it];
     const int64_t sg = w.seg;
     const float4 xr4 = ld4(XR + sg * ldXR), g4 = ld4(gout + sg * ldG), o4 = ld4(out + sg * ldOut);
@@ -129,23 +138,23 @@ __global__ __launch_bounds__(kT) void attn_bwd_lanes_kernel(
       delta[h] = g[h] * (o[h] - bv[h]);
       dxr[h] = 0.f;
     }
-    if (it == 0 || items[it - 1].seg != w.seg) {
+    if (sub == 0 && (it == 0 || items[it - 1].seg != w.seg)) {
 #pragma unroll
       for (int h = 0; h < 4; ++h) dbias[h] += g[h];
     }
     const int last = w.end - 1;
-    for (int e0 = w.begin; e0 < w.end; e0 += kU) {
+    for (int e0 = w.begin + sub; e0 < w.end; e0 += G * kU) {
       float4 x[kU];
       int64_t src[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const int e = e0 + u < last ? e0 + u : last;
+        const int e = e0 + G * u < last ? e0 + G * u : last;
         src[u] = perm ? int64_t(perm[e]) : int64_t(e);
         x[u] = ld4(XL + (xl_pos ? int64_t(e) : src[u]) * ldXL);
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        if (e0 + u >= w.end) break;
+        if (e0 + G * u >= w.end) break;
         float dx[4];
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
@@ -162,10 +171,16 @@ __global__ __launch_bounds__(kT) void attn_bwd_lanes_kernel(
         *reinterpret_cast<float4*>(dXL + src[u] * ldDXL) = make_float4(dx[0], dx[1], dx[2], dx[3]);
       }
     }
-    if (w.slot < 0)
-      *reinterpret_cast<float4*>(dXR + sg * ldDXR) = make_float4(dxr[0], dxr[1], dxr[2], dxr[3]);
-    else
-      *reinterpret_cast<float4*>(part_dxr + int64_t(w.slot) * 4) = make_float4(dxr[0], dxr[1], dxr[2], dxr[3]);
+    if (G > 1) {
+#pragma unroll
+      for (int h = 0; h < 4; ++h) dxr[h] = group_sum<G>(dxr[h]);
+    }
+    if (sub == 0) {
+      if (w.slot < 0)
+        *reinterpret_cast<float4*>(dXR + sg * ldDXR) = make_float4(dxr[0], dxr[1], dxr[2], dxr[3]);
+      else
+        *reinterpret_cast<float4*>(part_dxr + int64_t(w.slot) * 4) = make_float4(dxr[0], dxr[1], dxr[2], dxr[3]);
+    }
   }
   // per-wave partial row [datt 4 | dbias 4] (lane sums in xor-butterfly order: deterministic)
 #pragma unroll
@@ -227,7 +242,7 @@ extern "C" int gasfm_gat_attn_bwd_lanes(const float* XL, int64_t ldXL, const flo
   const int waves = gasfm_gat_attn_bwd_waves(n_items, H, C);
   GASFM_REQUIRE(waves > 0 && waves % (kT / 64) == 0, "gasfm_gat_attn_bwd_lanes: wave count %d", waves);
   note_dispatch(GASFM_K_ATTN_BWD_LANES);
-  hipLaunchKernelGGL(attn_bwd_lanes_kernel, dim3(waves / (kT / 64)), dim3(kT), 0,
+  hipLaunchKernelGGL(attn_bwd_lanes_kernel<GASFM_ATTN_BWD_LANES_G>, dim3(waves / (kT / 64)), dim3(kT), 0,
                      reinterpret_cast<hipStream_t>(stream), XL, ldXL, XR, ldXR, att, bias, perm, items, n_items, slope,
                      out, ldOut, seg_max, seg_sum, gout, ldG, dXL, ldDXL, dXR, ldDXR, part_dxr, datt_part,
                      int(xl_by_position != 0));
