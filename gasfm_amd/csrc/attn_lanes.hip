@@ -38,6 +38,13 @@ __device__ __forceinline__ float comp(const float4& v, int h) {
   return h == 0 ? v.x : (h == 1 ? v.y : (h == 2 ? v.z : v.w));
 }
 
+// G lanes per work item (GASFM_ATTN_FWD_LANES_G; 1 = one lane per item): lane `sub` runs the online
+// softmax over the item's edges sub, sub + G, ..., then the group's (max, sum, acc) states merge by
+// an xor butterfly (fixed order).
+#ifndef GASFM_ATTN_FWD_LANES_G
+#define GASFM_ATTN_FWD_LANES_G 8
+#endif
+template <int G>
 __global__ __launch_bounds__(kT) void attn_fwd_lanes_kernel(
     const float* __restrict__ XL, int64_t ldXL, const float* __restrict__ XR, int64_t ldXR,
     const float* __restrict__ att, const float* __restrict__ bias, const int32_t* __restrict__ perm,
@@ -46,8 +53,9 @@ __global__ __launch_bounds__(kT) void attn_fwd_lanes_kernel(
     float* __restrict__ part) {
   const float4 a4 = ld4(att);
   const float a[4] = {a4.x, a4.y, a4.z, a4.w};
-  const int nthreads = gridDim.x * kT;
-  for (int it = blockIdx.x * kT + threadIdx.x; it < n_items; it += nthreads) {
+  const int sub = threadIdx.x & (G - 1);
+  const int ngroups = gridDim.x * (kT / G);
+  for (int it = (blockIdx.x * kT + threadIdx.x) / G; it < n_items; it += ngroups) {
     const gasfm_work_item w = items[it];
     const float4 xr4 = ld4(XR + int64_t(w.seg) * ldXR);
     const float xr[4] = {xr4.x, xr4.y, xr4.z, xr4.w};
@@ -59,17 +67,17 @@ __global__ __launch_bounds__(kT) void attn_fwd_lanes_kernel(
       acc[h] = 0.f;
     }
     const int last = w.end - 1;
-    for (int e0 = w.begin; e0 < w.end; e0 += kU) {
+    for (int e0 = w.begin + sub; e0 < w.end; e0 += G * kU) {
       float4 x[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        const int e = e0 + u < last ? e0 + u : last;
+        const int e = e0 + G * u < last ? e0 + G * u : last;
         const int64_t src = perm ? int64_t(perm[e]) : int64_t(e);
         x[u] = ld4(XL + src * ldXL);
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        if (e0 + u >= w.end) break;
+        if (e0 + G * u >= w.end) break;
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
           const float xv = comp(x[u], h);
@@ -83,6 +91,22 @@ __global__ __launch_bounds__(kT) void attn_fwd_lanes_kernel(
         }
       }
     }
+    if (G > 1) {  // merge the group's states (a lane without edges has m = -inf, s = acc = 0)
+#pragma unroll
+      for (int o = 1; o < G; o *= 2) {
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const float m2 = __shfl_xor(m[h], o), s2 = __shfl_xor(s[h], o), a2 = __shfl_xor(acc[h], o);
+          const float mn = fmaxf(m[h], m2);
+          const float f1 = m[h] == -INFINITY ? 0.f : __expf(m[h] - mn);
+          const float f2 = m2 == -INFINITY ? 0.f : __expf(m2 - mn);
+          s[h] = fmaf(s[h], f1, s2 * f2);
+          acc[h] = fmaf(acc[h], f1, a2 * f2);
+          m[h] = mn;
+        }
+      }
+    }
+    if (sub != 0) continue;
     if (w.slot < 0) {
       float o[4];
 #pragma unroll
@@ -213,9 +237,10 @@ extern "C" int gasfm_gat_attn_fwd_lanes(const float* XL, int64_t ldXL, const flo
   GASFM_REQUIRE(ldXL % 4 == 0 && ldXR % 4 == 0 && (!out || ldOut % 4 == 0) && aligned16(XL) && aligned16(XR) &&
                     aligned16(att) && (!out || aligned16(out)) && (!part || aligned16(part)) && (!bias || aligned16(bias)),
                 "gasfm_gat_attn_fwd_lanes: 16-byte rows required");
-  const int grid = resident_grid(reinterpret_cast<const void*>(&attn_fwd_lanes_kernel), kT, 0, n_items, kT);
+  constexpr int G = GASFM_ATTN_FWD_LANES_G;
+  const int grid = resident_grid(reinterpret_cast<const void*>(&attn_fwd_lanes_kernel<G>), kT, 0, n_items, kT / G);
   note_dispatch(GASFM_K_ATTN_FWD_LANES);
-  hipLaunchKernelGGL(attn_fwd_lanes_kernel, dim3(grid), dim3(kT), 0, reinterpret_cast<hipStream_t>(stream), XL, ldXL,
+  hipLaunchKernelGGL(attn_fwd_lanes_kernel<G>, dim3(grid), dim3(kT), 0, reinterpret_cast<hipStream_t>(stream), XL, ldXL,
                      XR, ldXR, att, bias, perm, items, n_items, slope, finalize, out, ldOut, seg_max, seg_sum, ldStat,
                      part);
   return launch_status("gasfm_gat_attn_fwd_lanes");
