@@ -81,6 +81,7 @@ _SIGS = {
     "gasfm_colsum_tall": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp]),
     "gasfm_edge0_part_rows": (_i32, [_i32, _i64, _i32]),
     "gasfm_edge0_prologue_fwd": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_edge0_prologue_fwd_rows": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_edge0_epilogue_fwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp,
                                         _vp, _i64, _vp, _f32, _vp, _vp]),
     "gasfm_edge0_epilogue_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _f32, _vp, _vp,
@@ -706,6 +707,15 @@ def edge0_prologue_fwd(P, ln_w, ln_b, eps, W0, b0, XL, pos=None):
     st = lib().gasfm_edge0_prologue_fwd(_p(P), P.shape[0], _p(ln_w), _p(ln_b), eps, _p(W0), _p(b0), _p(XL),
                                         _p(pos), _stream(P))
     check(st, "gasfm_edge0_prologue_fwd")
+
+
+def edge0_prologue_fwd_rows(P, ln_w, ln_b, eps, W0, b0, XL, perm):
+    _req(P, "P", 2)
+    if perm.dtype != torch.int32 or perm.numel() != P.shape[0] or perm.device != P.device:
+        raise ValueError("edge0_prologue_fwd_rows: perm must be int32 [E] on P's device")
+    st = lib().gasfm_edge0_prologue_fwd_rows(_p(P), P.shape[0], _p(ln_w), _p(ln_b), eps, _p(W0), _p(b0), _p(XL),
+                                             _p(perm), _stream(P))
+    check(st, "gasfm_edge0_prologue_fwd_rows")
 
 
 def edge0_epilogue_fwd(P, cam, pt, lna_w, lna_b, lnb_w, lnb_b, eps, Wp, bp, Wsk, bsk, Sp, Sv, Sg, scale, out):

@@ -91,6 +91,43 @@ __global__ __launch_bounds__(kT) void edge0_prologue_fwd_kernel(const float2* __
   }
 }
 
+// The same XL0 written row by row: row r holds the point half of edge perm[r] (perm = the point
+// plan's permutation, the inverse of pos) and the camera half of edge r, so each thread stores one
+// whole 32-B row and the rows of a wave are one contiguous 2 KB run.  The scattered variant above
+// stores the point halves as 16-B pieces at random rows (partial-line writes); here the only random
+// access is the 8-B read of P[perm[r]] (32 B per edge of P in total: the array sits in L2 / MALL).
+// Both halves are the same float operations on the same P row as above: bitwise the same XL0.
+__global__ __launch_bounds__(kT) void edge0_prologue_fwd_rows_kernel(const float2* __restrict__ P, int64_t E,
+                                                                    const float* __restrict__ ga,
+                                                                    const float* __restrict__ ba, float eps,
+                                                                    const float* __restrict__ W0,
+                                                                    const float* __restrict__ b0,
+                                                                    float4* __restrict__ XL,
+                                                                    const int32_t* __restrict__ perm) {
+  float w[8][2], bb[8];
+#pragma unroll
+  for (int o = 0; o < 8; ++o) {
+    w[o][0] = W0[2 * o];
+    w[o][1] = W0[2 * o + 1];
+    bb[o] = b0[o];
+  }
+  const float g0 = ga[0], g1 = ga[1], e0 = ba[0], e1 = ba[1];
+  for (int64_t r = blockIdx.x * int64_t(kT) + threadIdx.x; r < E; r += int64_t(gridDim.x) * kT) {
+    const float2 pc = P[r];
+    const float2 pp = P[perm[r]];
+    const LN2 lp = ln2(pp.x, pp.y, eps), lc = ln2(pc.x, pc.y, eps);
+    const float hp0 = fmaxf(fmaf(lp.xh0, g0, e0), 0.f), hp1 = fmaxf(fmaf(lp.xh1, g1, e1), 0.f);
+    const float hc0 = fmaxf(fmaf(lc.xh0, g0, e0), 0.f), hc1 = fmaxf(fmaf(lc.xh1, g1, e1), 0.f);
+    float y[8];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) y[o] = fmaf(w[o][0], hp0, fmaf(w[o][1], hp1, bb[o]));
+#pragma unroll
+    for (int o = 4; o < 8; ++o) y[o] = fmaf(w[o][0], hc0, fmaf(w[o][1], hc1, bb[o]));
+    XL[2 * r] = make_float4(y[0], y[1], y[2], y[3]);
+    XL[2 * r + 1] = make_float4(y[4], y[5], y[6], y[7]);
+  }
+}
+
 // 8 lanes per edge (lane owns output columns c = 4*(lane&7) .. +3), 8 edges per wave step.
 __global__ __launch_bounds__(kT) void edge0_epilogue_fwd_kernel(
     const float2* __restrict__ P, const int32_t* __restrict__ cam, const int32_t* __restrict__ pt, int64_t E,
@@ -321,6 +358,18 @@ extern "C" int gasfm_edge0_prologue_fwd(const float* P, int64_t E, const float* 
                      reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const float2*>(P), E, ln_w, ln_b, eps,
                      W0, b0, reinterpret_cast<float4*>(XL), pos);
   return launch_status("gasfm_edge0_prologue_fwd");
+}
+
+extern "C" int gasfm_edge0_prologue_fwd_rows(const float* P, int64_t E, const float* ln_w, const float* ln_b,
+                                             float eps, const float* W0, const float* b0, float* XL,
+                                             const int32_t* perm, void* stream) {
+  GASFM_REQUIRE(P && ln_w && ln_b && W0 && b0 && XL && perm && aligned16(XL),
+                "gasfm_edge0_prologue_fwd_rows: bad args");
+  if (E == 0) return GASFM_OK;
+  hipLaunchKernelGGL(edge0_prologue_fwd_rows_kernel, dim3(grid_for(E, kT)), dim3(kT), 0,
+                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const float2*>(P), E, ln_w, ln_b, eps,
+                     W0, b0, reinterpret_cast<float4*>(XL), perm);
+  return launch_status("gasfm_edge0_prologue_fwd_rows");
 }
 
 extern "C" int gasfm_edge0_epilogue_fwd(const float* P, const int32_t* cam, const int32_t* pt, int64_t E,

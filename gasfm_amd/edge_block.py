@@ -35,6 +35,9 @@ CAM_PBWD = os.environ.get("GASFM_CAM_PBWD", "1") != "0"
 # gradient in block b's own edge_cam_pbwd (it holds dRes = dP' and relu(LN_b(P_b))), dSv / dP0 in
 # block b+1's (the kernel that produces dP').  0: edge_epilogue_bwd as before.
 EPI_FOLD = os.environ.get("GASFM_EPI_FOLD", "1") != "0"
+# Block 0's prologue writes XL0 row by row through the point plan's permutation (one 32-B store
+# per row, gasfm_edge0_prologue_fwd_rows) instead of scattering the point halves through pos.
+E0_ROWS = os.environ.get("GASFM_E0_ROWS", "1") != "0"
 
 
 def _rows(t):
@@ -457,11 +460,15 @@ class Block0PrologueFn(torch.autograd.Function):
     """Block 0: XL0 = [Wl_pt; Wl_cam] relu(LN_a(P)) + b for 2-wide P (layers.py:232-234, 329, 426)."""
 
     @staticmethod
-    def forward(ctx, P, ln_w, ln_b, W0, b0, eps, pos=None):
-        """pos (point plan's inverse permutation): write the point half of XL0 in point order."""
+    def forward(ctx, P, ln_w, ln_b, W0, b0, eps, pos=None, perm=None):
+        """pos (point plan's inverse permutation): write the point half of XL0 in point order.
+        perm (the point plan's permutation, pos's inverse): the same XL0 written row by row."""
         E = P.shape[0]
         XL = torch.empty((E, 8), dtype=torch.float32, device=P.device)
-        _native.edge0_prologue_fwd(P, ln_w, ln_b, eps, W0.contiguous(), b0.contiguous(), XL, pos)
+        if pos is not None and perm is not None and E0_ROWS:
+            _native.edge0_prologue_fwd_rows(P, ln_w, ln_b, eps, W0.contiguous(), b0.contiguous(), XL, perm)
+        else:
+            _native.edge0_prologue_fwd(P, ln_w, ln_b, eps, W0.contiguous(), b0.contiguous(), XL, pos)
         ctx.eps = eps
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(P, ln_w, ln_b, W0)
@@ -478,7 +485,7 @@ class Block0PrologueFn(torch.autograd.Function):
         part = torch.empty((rows, 28), dtype=torch.float32, device=P.device)
         _native.edge0_prologue_bwd(dXL, P, aux, ln_w, ln_b, ctx.eps, W0.contiguous(), dP, part)
         tot = _native.colsum(part)
-        return dP, tot[24:26], tot[26:28], tot[:16].view(8, 2), tot[16:24], None, None
+        return dP, tot[24:26], tot[26:28], tot[:16].view(8, 2), tot[16:24], None, None, None
 
 
 class Block0EpilogueFn(torch.autograd.Function):

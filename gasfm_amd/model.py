@@ -643,8 +643,10 @@ class GraphAttnSfMLayer(Module):
         gfu = self.global_feature_update
         pfu = self.projection_feature_update
         W, b = gfu.lin_l_stack()
-        pos = plans["proj2scenepoint"].pos
-        XL, token = Block0PrologueFn.apply(P.contiguous(), la.weight, la.bias, W, b, la.eps, pos)
+        pp = plans["proj2scenepoint"]
+        pos = pp.pos
+        perm = pp.perm if pos is not None and pp.src_rows == pp.num_edges else None
+        XL, token = Block0PrologueFn.apply(P.contiguous(), la.weight, la.bias, W, b, la.eps, pos, perm)
         pts, view, glob = gfu.forward_fused(XL, plans, None, None, None, xl_sorted=pos is not None, carry=carry,
                                             pfu=pfu, nxt=nxt)
         sp, sv, sg = pfu.node_terms(pts, view, glob, *((carry.pop("SA", None), carry.pop("SV", None),

@@ -390,6 +390,13 @@ int gasfm_edge0_part_rows(int32_t which, int64_t E, int32_t n_items);
 int gasfm_edge0_prologue_fwd(const float* P, int64_t E, const float* ln_w, const float* ln_b, float eps,
                              const float* W0, const float* b0, float* XL, const int32_t* pos, void* stream);
 
+/* The same XL0 (bitwise) written row by row: row r = [point half of edge perm[r] | camera half of
+ * edge r], perm = the point plan's permutation (the inverse of pos above), so every row is one
+ * contiguous 32-B store instead of a scattered 16-B point half. */
+int gasfm_edge0_prologue_fwd_rows(const float* P, int64_t E, const float* ln_w, const float* ln_b, float eps,
+                                  const float* W0, const float* b0, float* XL, const int32_t* perm,
+                                  void* stream);
+
 /* P'[e] = Wsk relu(LN_b(P[e])) + bsk + scale*(Wp relu(LN_a(P[e])) + bp + Sp[pt] + Sv[cam] + Sg). */
 int gasfm_edge0_epilogue_fwd(const float* P, const int32_t* cam, const int32_t* pt, int64_t E,
                              const float* ln_a_w, const float* ln_a_b, const float* ln_b_w,

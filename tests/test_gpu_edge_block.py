@@ -164,3 +164,35 @@ def test_block0_edge_body_fwd_bwd(device):
         err32 = float((r32[k].grad.double() - ref[k].grad).norm())
         got = float((dev[k].grad.double().cpu() - ref[k].grad).norm())
         assert got <= max(1e-5 * float(ref[k].grad.norm()) + 1e-6, 4 * err32), (k, got, err32)
+
+
+@pytest.mark.parametrize("m,n,per_pt", [(30, 2000, 5), (200, 40000, 20)])
+def test_block0_prologue_rows_equals_scatter(device, m, n, per_pt):
+    """gasfm_edge0_prologue_fwd_rows (row r = point half of edge perm[r] | camera half of edge r)
+    writes bitwise the XL0 of gasfm_edge0_prologue_fwd with pos (the point half scattered to row
+    pos[e]); the model's Block0PrologueFn takes the row form when the point plan has a permutation."""
+    from gasfm_amd import _native
+    from gasfm_amd.edge_block import Block0PrologueFn
+    sc, data = _graph(m, n, per_pt, seed=11)
+    pp = data.to(device).graph_wrappers["proj2scenepoint"].plan
+    E = sc.num_edges
+    assert pp.perm is not None and pp.pos is not None and pp.src_rows == E
+    g = torch.Generator().manual_seed(4)
+    P = torch.randn(E, 2, generator=g).to(device)
+    P[::97, 1] = P[::97, 0]  # exercise x0 == x1 rows (rstd = 1/sqrt(eps))
+    lnw, lnb = (1 + 0.1 * torch.randn(2, generator=g)).to(device), (0.1 * torch.randn(2, generator=g)).to(device)
+    W0, b0 = torch.randn(8, 2, generator=g).to(device), (0.1 * torch.randn(8, generator=g)).to(device)
+    XL_s = torch.full((E, 8), float("nan"), device=device)
+    XL_r = torch.full((E, 8), float("nan"), device=device)
+    _native.edge0_prologue_fwd(P, lnw, lnb, 1e-5, W0, b0, XL_s, pp.pos)
+    _native.edge0_prologue_fwd_rows(P, lnw, lnb, 1e-5, W0, b0, XL_r, pp.perm)
+    torch.cuda.synchronize()
+    assert torch.equal(XL_s, XL_r)
+    XL_f, _ = Block0PrologueFn.apply(P, lnw, lnb, W0, b0, 1e-5, pp.pos, pp.perm)
+    assert torch.equal(XL_f, XL_s)
+    # against fp64: point half in point order, camera half in edge order
+    Pd = P.double()
+    h = F.relu(F.layer_norm(Pd, (2,), lnw.double(), lnb.double(), 1e-5)) @ W0.double().T + b0.double()
+    perm = pp.perm.long()
+    ref = torch.cat([h[perm, :4], h[:, 4:]], 1)
+    np.testing.assert_allclose(XL_r.double().cpu().numpy(), ref.cpu().numpy(), atol=1e-3, rtol=1e-4)
