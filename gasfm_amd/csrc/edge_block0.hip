@@ -19,6 +19,10 @@
 #include "common.hpp"
 #include "lanes.hpp"
 
+#ifndef GASFM_E0_EPI_U
+#define GASFM_E0_EPI_U 4  // edge0_epilogue_bwd: 8-edge row groups whose loads are in flight together
+#endif
+
 namespace gasfm {
 namespace {
 
@@ -172,6 +176,7 @@ __global__ __launch_bounds__(kT) void edge0_epilogue_fwd_kernel(
 // One wave per camera work item; 8 lanes per edge (4 columns each), 8 edges per step.
 // part row per workgroup: [dWp 64 | dWsk 64 | dbsk 32 | dgamma_b 2 | dbeta_b 2]
 constexpr int kPart0E = 64 + 64 + 32 + 4;
+constexpr int kU = GASFM_E0_EPI_U;
 __global__ __launch_bounds__(kT) void edge0_epilogue_bwd_kernel(
     const gasfm_work_item* __restrict__ items, int n_items, const float* __restrict__ dPo,
     const float2* __restrict__ P, const float* __restrict__ ga, const float* __restrict__ ba,
@@ -196,48 +201,60 @@ __global__ __launch_bounds__(kT) void edge0_epilogue_bwd_kernel(
   for (int it = __builtin_amdgcn_readfirstlane(blockIdx.x * (kT / kW) + threadIdx.x / kW); it < n_items; it += nw) {
     const gasfm_work_item w = items[it];
     float dsv[4] = {};
-    for (int e0 = w.begin; e0 < w.end; e0 += 8) {
-      const int e = e0 + row;
-      const bool valid = e < w.end;
-      float4 d4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      float2 p = make_float2(0.f, 1.f);
-      if (valid) {
-        d4 = *reinterpret_cast<const float4*>(dPo + int64_t(e) * 32 + c0);
-        p = P[e];
-      }
-      const float d[4] = {d4.x, d4.y, d4.z, d4.w};
-      const LN2 l = ln2(p.x, p.y, eps);
-      const float ya0 = fmaf(l.xh0, ga0, ba0), ya1 = fmaf(l.xh1, ga1, ba1);
-      const float yb0 = fmaf(l.xh0, gb0, bb0), yb1 = fmaf(l.xh1, gb1, bb1);
-      const float ha0 = fmaxf(ya0, 0.f), ha1 = fmaxf(ya1, 0.f), hb0 = fmaxf(yb0, 0.f), hb1 = fmaxf(yb1, 0.f);
-      float qa0 = 0.f, qa1 = 0.f, qb0 = 0.f, qb1 = 0.f;
+    // kU row groups of 8 edges per step: their loads are issued together (kU x 1 KB of dP' per wave
+    // in flight instead of one), then consumed in edge order (the sums' order is unchanged)
+    for (int e0 = w.begin; e0 < w.end; e0 += 8 * kU) {
+      float4 d4[kU];
+      float2 pv[kU];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        dsv[k] += d[k];
-        dwp[k][0] = fmaf(d[k], ha0, dwp[k][0]);
-        dwp[k][1] = fmaf(d[k], ha1, dwp[k][1]);
-        dwsk[k][0] = fmaf(d[k], hb0, dwsk[k][0]);
-        dwsk[k][1] = fmaf(d[k], hb1, dwsk[k][1]);
-        dbsk[k] += d[k];
-        qa0 = fmaf(d[k], wp[k][0], qa0);
-        qa1 = fmaf(d[k], wp[k][1], qa1);
-        qb0 = fmaf(d[k], wsk[k][0], qb0);
-        qb1 = fmaf(d[k], wsk[k][1], qb1);
+      for (int u = 0; u < kU; ++u) {
+        const int e = e0 + 8 * u + row;
+        d4[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        pv[u] = make_float2(0.f, 1.f);
+        if (e < w.end) {
+          d4[u] = *reinterpret_cast<const float4*>(dPo + int64_t(e) * 32 + c0);
+          pv[u] = P[e];
+        }
       }
-      qa0 = group_sum<8>(qa0);
-      qa1 = group_sum<8>(qa1);
-      qb0 = group_sum<8>(qb0);
-      qb1 = group_sum<8>(qb1);
-      // LN_b / ReLU backward of the skip branch (every lane of the row holds the same values)
-      const float db0 = yb0 > 0.f ? qb0 : 0.f, db1 = yb1 > 0.f ? qb1 : 0.f;
-      float dx0, dx1;
-      ln2_bwd(l, db0 * gb0, db1 * gb1, dx0, dx1);
-      if ((lane & 7) == 0 && valid) {
-        dgb[0] = fmaf(db0, l.xh0, dgb[0]);
-        dgb[1] = fmaf(db1, l.xh1, dgb[1]);
-        dbb[0] += db0;
-        dbb[1] += db1;
-        aux[e] = make_float4(qa0, qa1, dx0, dx1);
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int e = e0 + 8 * u + row;
+        const bool valid = e < w.end;
+        const float2 p = pv[u];
+        const float d[4] = {d4[u].x, d4[u].y, d4[u].z, d4[u].w};
+        const LN2 l = ln2(p.x, p.y, eps);
+        const float ya0 = fmaf(l.xh0, ga0, ba0), ya1 = fmaf(l.xh1, ga1, ba1);
+        const float yb0 = fmaf(l.xh0, gb0, bb0), yb1 = fmaf(l.xh1, gb1, bb1);
+        const float ha0 = fmaxf(ya0, 0.f), ha1 = fmaxf(ya1, 0.f), hb0 = fmaxf(yb0, 0.f), hb1 = fmaxf(yb1, 0.f);
+        float qa0 = 0.f, qa1 = 0.f, qb0 = 0.f, qb1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          dsv[k] += d[k];
+          dwp[k][0] = fmaf(d[k], ha0, dwp[k][0]);
+          dwp[k][1] = fmaf(d[k], ha1, dwp[k][1]);
+          dwsk[k][0] = fmaf(d[k], hb0, dwsk[k][0]);
+          dwsk[k][1] = fmaf(d[k], hb1, dwsk[k][1]);
+          dbsk[k] += d[k];
+          qa0 = fmaf(d[k], wp[k][0], qa0);
+          qa1 = fmaf(d[k], wp[k][1], qa1);
+          qb0 = fmaf(d[k], wsk[k][0], qb0);
+          qb1 = fmaf(d[k], wsk[k][1], qb1);
+        }
+        qa0 = group_sum<8>(qa0);
+        qa1 = group_sum<8>(qa1);
+        qb0 = group_sum<8>(qb0);
+        qb1 = group_sum<8>(qb1);
+        // LN_b / ReLU backward of the skip branch (every lane of the row holds the same values)
+        const float db0 = yb0 > 0.f ? qb0 : 0.f, db1 = yb1 > 0.f ? qb1 : 0.f;
+        float dx0, dx1;
+        ln2_bwd(l, db0 * gb0, db1 * gb1, dx0, dx1);
+        if ((lane & 7) == 0 && valid) {
+          dgb[0] = fmaf(db0, l.xh0, dgb[0]);
+          dgb[1] = fmaf(db1, l.xh1, dgb[1]);
+          dbb[0] += db0;
+          dbb[1] += db1;
+          aux[e] = make_float4(qa0, qa1, dx0, dx1);
+        }
       }
     }
 #pragma unroll
