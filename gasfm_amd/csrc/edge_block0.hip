@@ -207,21 +207,18 @@ __global__ __launch_bounds__(kT) void edge0_epilogue_bwd_kernel(
       float4 d4[kU];
       float2 pv[kU];
 #pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int e = e0 + 8 * u + row;
-        d4[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        pv[u] = make_float2(0.f, 1.f);
-        if (e < w.end) {
-          d4[u] = *reinterpret_cast<const float4*>(dPo + int64_t(e) * 32 + c0);
-          pv[u] = P[e];
-        }
+      for (int u = 0; u < kU; ++u) {  // unconditional loads (rows past the item re-read its last edge)
+        const int ec = min(e0 + 8 * u + row, w.end - 1);
+        d4[u] = *reinterpret_cast<const float4*>(dPo + int64_t(ec) * 32 + c0);
+        pv[u] = P[ec];
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int e = e0 + 8 * u + row;
-        const bool valid = e < w.end;
-        const float2 p = pv[u];
-        const float d[4] = {d4[u].x, d4[u].y, d4[u].z, d4[u].w};
+        const bool valid = e < w.end;  // dead rows masked at the consumers
+        const float2 p = valid ? pv[u] : make_float2(0.f, 1.f);
+        const float4 dv = valid ? d4[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float d[4] = {dv.x, dv.y, dv.z, dv.w};
         const LN2 l = ln2(p.x, p.y, eps);
         const float ya0 = fmaf(l.xh0, ga0, ba0), ya1 = fmaf(l.xh1, ga1, ba1);
         const float yb0 = fmaf(l.xh0, gb0, bb0), yb1 = fmaf(l.xh1, gb1, bb1);
