@@ -1302,6 +1302,9 @@ def gemm_f32_smallm(a, b, cin=None, bias=None, out=None):
         I, J = M, N
     else:
         return None
+    # modes 0 / 1 read float4 runs of A (and of W in mode 0): a misaligned view falls back to hipBLASLt
+    if mode in (0, 1) and (A.data_ptr() % 16 or (mode == 0 and B.data_ptr() % 16)):
+        return None
     if not L.gasfm_gemm_f32_smallm_ok(mode, I, J, K):
         return None
     if out is None:

@@ -569,7 +569,9 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
         sp[0] = nsp[0];
         sp[1] = nsp[1];
       }
-      const int64_t dst = pos ? int64_t(npos) : row0 + c;
+      // lanes past the item's end hold row0's values (clamped loads) and store them to row0's own
+      // row: with pos == nullptr, row0 + c would belong to the next item (another wave's rows)
+      const int64_t dst = pos ? int64_t(npos) : row0 + (c < nrows ? c : 0);
       const int32_t ptc = npt;
       const float2 q0 = nq;
       {  // the next tile (this item's, else the next item's first; the last one re-reads itself)

@@ -115,11 +115,19 @@ class AsyncGradReducer:
         self.shard = shard
         self.works = []
         self.ptrs = set()
+        # the forward's capture state: the hooks run on autograd's device thread, under the stream
+        # autograd guards for the AccumulateGrad node.  A hook that saw no capture while the
+        # forward was captured would issue its all-reduce outside the graph (eagerly, once, on
+        # gradients not yet computed) and put its Work on the watchdog's list mid-capture.
+        self.capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
 
     def launch(self, t):
         if t.data_ptr() in self.ptrs:  # a second accumulation into a tensor already in flight
             raise RuntimeError("camera-sharded backward: a parameter's gradient was accumulated twice in one pass "
                                "(several forwards before one backward); run forward/backward/sync_grads per step")
+        if t.is_cuda and torch.cuda.is_current_stream_capturing() != self.capturing:
+            raise RuntimeError("camera-sharded backward: a gradient hook ran on a stream whose capture state differs "
+                               "from the forward's; its all-reduce would not be part of the captured step")
         sh = self.shard
         if sh.emulate:
             self.ptrs.add(t.data_ptr())

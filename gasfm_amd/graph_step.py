@@ -28,6 +28,32 @@ existing gradient (each replay's gradients are that step's alone, as after zero_
 import torch
 
 
+def retire_collectives():
+    """Block until ProcessGroupNCCL's watchdog has retired every collective issued so far.
+
+    The watchdog thread keeps each eager collective's Work on a list and polls its end event
+    (hipEventQuery, every 100 ms) until it sees it complete.  A camera-sharded step issues
+    asynchronous all-reduces (distributed.AsyncGradReducer) on the process group's internal RCCL
+    stream; inside the capture that same stream joins the graph.  A watchdog poll of a warm-up
+    Work's end event -- recorded on that stream before the capture -- that lands while the
+    stream is capturing fails, and the watchdog rethrows it (SIGABRT from
+    ProcessGroupNCCL.cpp's Watchdog::run).  Whether a poll hit that window was timing: ~1 capture
+    in 10.  After torch.cuda.synchronize() every Work has completed, so the watchdog empties its
+    list on its next poll; ``_wait_for_pending_works`` returns once the list is empty.  Works
+    created during a capture are never listed, so nothing is polled until the capture ends."""
+    dist = torch.distributed
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    from torch.distributed import distributed_c10d as c10d
+    for pg in list(c10d._world.pg_map.keys()):
+        try:
+            nccl = dist.get_backend(pg) == "nccl"
+        except (RuntimeError, ValueError):
+            nccl = False
+        if nccl:
+            pg._wait_for_pending_works()
+
+
 def _grad_mismatch(params, ref_grads, rtol):
     for i, (p, r) in enumerate(zip(params, ref_grads)):
         g = p.grad
@@ -76,22 +102,16 @@ class CapturedStep:
                 if check else None
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        retire_collectives()
         self._zero()
         g = torch.cuda.CUDAGraph()
         ok = True
         try:
-            # Under torch.distributed, ProcessGroupNCCL's watchdog thread polls (every 100 ms) the
-            # end events of the warm-up collectives until it has seen each one complete, so a poll
-            # can land inside the capture window.  In "global" mode that hipEventQuery is an
-            # illegal call during capture; HIP's "thread_local" mode still refused it now and then
-            # (a one-rank RCCL run aborted in the watchdog in ~1 of 10 captures).  "relaxed"
-            # prohibits nothing on any thread, so the watchdog's query of an event recorded
-            # before the capture is answered normally whenever it runs.  The captured step
-            # itself makes no unsafe call (no host sync, no allocation outside torch's graph
-            # pool), which the replay check below verifies.
-            mode = "relaxed" if (torch.distributed.is_available() and torch.distributed.is_initialized()) \
-                else "thread_local"
-            with torch.cuda.graph(g, capture_error_mode=mode):  # records only
+            # thread_local: unsafe calls (host syncs, event queries) are refused on this thread
+            # while it captures.  ProcessGroupNCCL's watchdog thread queries nothing during the
+            # capture: every warm-up collective was retired from its list above, and collectives
+            # issued while capturing are never put on it (they belong to the graph).
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):  # records only
                 out = self.fn()
         except RuntimeError as e:  # capture unsupported for some op
             self.fallback_reason = f"capture failed: {e}"

@@ -152,7 +152,8 @@ class OutlierInjector:
         if has_mins:
             assert v[0] >= MIN_N_POINTS_PER_VIEW and v[1] >= MIN_N_VIEWS_PER_POINT
             v = v[2:]
-        assert all(x > 0 for x in v), "outlier injection: a view lost too many inliers or the LDL needed a 2x2 pivot"
+        assert all(x > 0 for x in v), ("outlier injection: a view lost too many inliers, the LDL needed a 2x2 pivot, or the outlier "
+                                    "count drifted from the device mask")
 
     def sample_more_outliers(self, n_new_outliers):
         self._flip(FREE_IN, FREE_OUT, n_new_outliers)
@@ -213,11 +214,15 @@ class OutlierInjector:
         dev = self.M.device
         mu, sigma, tril, piv = _native.outlier_moments(self.values, self.state, self.cam_ptr, self.n_views)
         _, _, mins = self._inlier_counts()
-        # :375 (>= 8 inliers per view) and the LDL's 1x1 pivots (dataset_utils.py:383), one host read
-        self._run_checks(extra=torch.stack([(mins[0] >= MIN_N_POINTS_PER_VIEW).to(torch.int64),
-                                            (piv > 0).all().to(torch.int64)]))
         n_out = self.n_outliers
-        idx = torch.nonzero_static(self.outliers_mask, size=n_out).view(-1)
+        mask = self.outliers_mask
+        # :375 (>= 8 inliers per view), the LDL's 1x1 pivots (dataset_utils.py:383) and the host
+        # outlier count agreeing with the device mask (nonzero_static below would silently truncate
+        # or pad with -1 otherwise), one host read
+        self._run_checks(extra=torch.stack([(mins[0] >= MIN_N_POINTS_PER_VIEW).to(torch.int64),
+                                            (piv > 0).all().to(torch.int64),
+                                            (mask.sum() == n_out).to(torch.int64)]))
+        idx = torch.nonzero_static(mask, size=n_out).view(-1)
         if z is None:
             z = torch.randn((n_out, 2, 1), device=dev, generator=generator)
         z = z.to(dev, torch.float32).reshape(n_out, 2).contiguous()

@@ -16,12 +16,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "reference: needs /root/reference (build container only)")
 
 
+# multi-process and subprocess tests (spawned ranks, torchrun children) run last: under -x a
+# failure there must not keep the single-process kernel / model / config parity suites from running
+_RUN_LAST = ("test_distributed.py",)
+
+
 def pytest_collection_modifyitems(config, items):
     has_gpu = torch.cuda.is_available()
     skip_gpu = pytest.mark.skip(reason="no HIP device")
     for it in items:
         if "gpu" in it.keywords and not has_gpu:
             it.add_marker(skip_gpu)
+    items.sort(key=lambda it: os.path.basename(str(it.fspath)) in _RUN_LAST)  # stable: order kept otherwise
 
 
 def golden(name):
