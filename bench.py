@@ -307,6 +307,7 @@ def main():
     e_cam = data.graph_wrappers["proj2view"].plan.num_edges
     pbwd_tfs = flop_e * e_cam / (pbwd_ms * 1e-3) / 1e12 if pbwd_ms else None
     pbwd_gbs = bytes_e * e_cam / (pbwd_ms * 1e-3) / 1e9 if pbwd_ms else None
+    pbwd_traffic = pmc_kernel_traffic(pbwd_name, e_cam)
     kern_ms = timer.mean_ms()
     b2b_ms = timer.replay_ms(20)
     plan = data.graph_wrappers["proj2scenepoint"].plan
@@ -348,9 +349,11 @@ def main():
                                       "one)" if fold else "") + " (the step's largest kernel), per launch",
                          "bound": "mfma", "achieved": pbwd_tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": (pbwd_tfs / MFMA_F32_PEAK_TFS) if pbwd_tfs else None,
-                         "traffic": pmc_kernel_traffic(pbwd_name, e_cam),
+                         "traffic": pbwd_traffic,
                          "traffic_source": "profiles/r3_pmc_kernels.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
-                                           "passes of this bench, per launch; 1.00x the algorithmic bytes)",
+                                           "passes of this bench, per launch"
+                                           + (f"; {pbwd_traffic / (bytes_e * e_cam):.2f}x the algorithmic bytes)"
+                                              if pbwd_traffic else "; not taken on this workload)"),
                          "flop_per_launch": flop_e * e_cam,
                          "algorithmic_bytes": bytes_e * e_cam,
                          "hbm_achieved_GBps": pbwd_gbs,
