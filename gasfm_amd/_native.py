@@ -106,6 +106,10 @@ _SIGS = {
     "gasfm_gvec_multi_fwd": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp]),
     "gasfm_gvec_multi_bwd": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp,
                                     _vp, _vp, _f32, _vp]),
+    "gasfm_gchain_fwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_gchain_scratch_floats": (_i64, [_vp]),
+    "gasfm_gchain_counters": (_i32, [_vp]),
+    "gasfm_gchain_bwd": (_i32, [_vp] * 17),
     "gasfm_pose_fwd": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "gasfm_pose_bwd": (_i32, [_vp, _i64, _i64, _vp, _vp, _i64, _vp]),
     "gasfm_esfm_part_rows": (_i32, [_i64]),
@@ -1080,6 +1084,62 @@ def gvec_multi_bwd(probs, groups, eps):
                                     _ints(N), _ptrs(dW), _ptrs(db), _ptrs(dg), _ptrs(dbt), _ptrs(part), len(groups),
                                     _ints(p0), _ints(npr), _ptrs(dres), _ptrs(dx), eps, _stream(x[0]))
     check(st, "gasfm_gvec_multi_bwd")
+
+
+# ---------------------------------------------------------------- the global node's chain (global_chain.hip)
+_GC_DIMS = ("G", "Kc", "NA", "NB", "NC", "ND", "NE")
+_GC_W = ("W1", "b1", "gM", "bM", "W2", "b2", "gA", "bA", "WA", "gB", "bB", "WB", "bWB", "gC", "bC", "WC", "bWC",
+         "WD", "bD", "WE", "bE")
+_GC_D = tuple("d" + k for k in _GC_W)
+
+
+class _GChain(ctypes.Structure):
+    _fields_ = [(k, _i32) for k in _GC_DIMS] + [("eps_m", _f32), ("eps_h", _f32)] + [(k, _vp) for k in _GC_W]
+
+
+class _GChainGrads(ctypes.Structure):
+    _fields_ = [(k, _vp) for k in _GC_D]
+
+
+def gchain_struct(w, eps_m, eps_h):
+    """gasfm_gchain of the weights dict w (keys _GC_W; the hub's B..E absent for the last block)."""
+    c = _GChain()
+    W1, WA = w["W1"], w["WA"]
+    hub = w.get("WB") is not None
+    dims = dict(G=W1.shape[0], Kc=W1.shape[1], NA=WA.shape[0], NB=w["WB"].shape[0] if hub else 0,
+                NC=w["WC"].shape[0] if hub else 0, ND=w["WD"].shape[0] if hub else 0,
+                NE=w["WE"].shape[0] if hub else 0)
+    for k, v in dims.items():
+        setattr(c, k, int(v))
+    c.eps_m, c.eps_h = float(eps_m), float(eps_h)
+    for k in _GC_W:
+        t = w.get(k)
+        if t is not None:
+            _req(t, k)
+            setattr(c, k, t.data_ptr())
+    return c
+
+
+def gchain_fwd(c, xcat, prev, x1, g, sg, xv, xp, xrv, xrp):
+    st = lib().gasfm_gchain_fwd(ctypes.addressof(c), _p(xcat), _p(prev), _p(x1), _p(g), _p(sg), _p(xv), _p(xp),
+                                _p(xrv), _p(xrp), _stream(g))
+    check(st, "gasfm_gchain_fwd")
+
+
+def gchain_bwd(c, xcat, x1, g, xv, xp, dskip, dsg, dxrv, dxrp, dxcat, dprev, grads):
+    """grads: dict d<weight> -> tensor (gradient buffers to fill)."""
+    d = _GChainGrads()
+    for k in _GC_D:
+        t = grads.get(k)
+        if t is not None:
+            setattr(d, k, t.data_ptr())
+    L = lib()
+    ws = torch.empty(int(L.gasfm_gchain_scratch_floats(ctypes.addressof(c))), dtype=torch.float32, device=g.device)
+    cnt = _counters(g.device, L.gasfm_gchain_counters(ctypes.addressof(c)))
+    st = L.gasfm_gchain_bwd(ctypes.addressof(c), _p(xcat), _p(x1), _p(g), _p(xv), _p(xp), _p(dskip), _p(dsg),
+                            _p(dxrv), _p(dxrp), _p(dxcat), _p(dprev), ctypes.addressof(d), _p(ws), _p(cnt),
+                            _stream(g))
+    check(st, "gasfm_gchain_bwd")
 
 
 # ---------------------------------------------------------------- device scene builder (scene_build.hip)

@@ -1,0 +1,566 @@
+// The global node's chain of one GASFM block -- a single row of G = 2048 features -- forward and
+// backward in four launches each way, gfx950.
+//
+// Per block (code/models/layers.py):
+//   F1  x1  = W1 xcat + b1 (+ prev)              proj_view_and_scenepoint2global + skip  :527-528, 590-592
+//   F2  g   = x1 + W2 relu(LN_M(x1)) + b2        norm_pre_mlp, mlp, skip                 :594-603
+//   F3  SG  = WA relu(LN_A(g))                   lin_global of the projection update      :928-935
+//       xv  = WB relu(LN_B(g)) + bWB             next block's norm_and_proj_global2view   :497-505
+//       xp  = WC relu(LN_C(g)) + bWC             next block's norm_and_proj_global2scenepoint :512-520
+//   F4  XRv = WD xv + bD,  XRp = WE xp + bE      the next block's two GATv2 lin_r rows (PyG)
+// (the last block's chain ends at F3 with SG only).  Round 3 ran this as gvec launches with a
+// one-workgroup "finish" kernel after every backward GEMV (12 launches per block, ~100 us); here:
+//
+//   gnode_fwd   one wave per output row; the wave's W row is requested FIRST, into registers,
+//               and the workgroup's LayerNorm of the input row (recomputed by every workgroup)
+//               runs while it is in flight.
+//   gnode_bwd   a workgroup per (problem, 32-column slab of K, chunk of 32*RPT rows of N):
+//                 dW[rows, slab] = dy[rows] (x) h[slab]   (h = relu(LN(x)) or x)
+//                 dh[slab]       = sum over rows of dy[n] W[n, slab]
+//               chunk partials of dh are handed to the slab's last-arriving workgroup (write-
+//               through stores, one relaxed agent-scope ticket per slab: reduce.hip's hand-off),
+//               which sums them in chunk order: dh leaves FINAL, no finish launch.  The LayerNorm
+//               backward that follows a level (F3's LN_A/B/C into dg, F2's LN_M into dx1) needs
+//               row sums over the whole vector, so the NEXT level's workgroups each recompute it
+//               from the raw dh vectors ("finish" prologue) -- redundantly, while their own W
+//               slab is in flight -- and one designated workgroup writes the finished vector and
+//               the LayerNorm gamma / beta gradients.
+// No float atomics; every sum has a fixed order: deterministic, identical on every rank.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.hpp"
+
+namespace gasfm {
+namespace {
+
+constexpr int kFT = 256;              // forward: 4 waves, one output row each
+constexpr int kBT = 256;              // backward: 8 float4 column lanes x 32 row lanes
+constexpr int kSW = 32;               // backward slab width (columns of K)
+constexpr int kMaxK = 2048;           // widest row (G)
+constexpr int kPer = kMaxK / 256;     // row values per thread in the full-row prologues
+constexpr int kMaxProb = 3;
+constexpr int kMaxRaw = 3;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// NV sums over a 256-thread workgroup in one barrier round, fixed order; results to every thread
+template <int NV>
+__device__ __forceinline__ void block_sums(float (&v)[NV], float* scratch) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) scratch[wave * NV + k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = scratch[k] + scratch[NV + k] + scratch[2 * NV + k] + scratch[3 * NV + k];
+}
+
+// mean / rstd of a row held as kPer strided values per thread (j = tid + 256 u; 0 past K)
+__device__ __forceinline__ void row_stats(const float (&xv)[kPer], int K, float eps, float* scratch, float& mean,
+                                          float& rstd) {
+  float s[1] = {0.f};
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) s[0] += xv[u];
+  block_sums<1>(s, scratch);
+  mean = s[0] / K;
+  float q[1] = {0.f};
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int j = int(threadIdx.x) + 256 * u;
+    const float d = j < K ? xv[u] - mean : 0.f;
+    q[0] = fmaf(d, d, q[0]);
+  }
+  block_sums<1>(q, scratch);
+  rstd = rsqrtf(q[0] / K + eps);
+}
+
+__device__ __forceinline__ void load_row(const float* __restrict__ x, int K, float (&xv)[kPer]) {
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int j = int(threadIdx.x) + 256 * u;
+    xv[u] = j < K ? x[j] : 0.f;
+  }
+}
+
+template <int NP>
+__device__ __forceinline__ int find_prob(const int (&blk0)[NP], int nprob) {
+  int pi = 0;
+  while (pi + 1 < nprob && int(blockIdx.x) >= blk0[pi + 1]) ++pi;
+  return pi;
+}
+
+// ---------------------------------------------------------------------------------- forward
+struct GnFwdProb {
+  const float* x;    // [K] input row
+  const float* gam;  // [K] LayerNorm (null: h = x)
+  const float* bet;
+  const float* W;    // [N, K]
+  const float* b;    // [N] or null
+  const float* res;  // [N] or null
+  float* y;          // [N]
+  int K, N, blk0;
+  float eps;
+};
+struct GnFwdArgs {
+  GnFwdProb p[kMaxProb];
+  int nprob;
+};
+
+template <int KI>  // float4 per lane of a W row: K <= 256 KI
+__global__ __launch_bounds__(kFT) void gnode_fwd_kernel(GnFwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float h[kMaxK];
+  __shared__ float scratch[8];
+  int blk0[kMaxProb];
+#pragma unroll
+  for (int q = 0; q < kMaxProb; ++q) blk0[q] = a.p[q].blk0;
+  const GnFwdProb& p = a.p[find_prob(blk0, a.nprob)];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int K = p.K;
+  const int i = (int(blockIdx.x) - p.blk0) * (kFT / 64) + wave;
+  const int ic = i < p.N ? i : p.N - 1;
+  // the wave's W row first (clamped in-range addresses; lanes past K multiply h = 0 below)
+  float4 w[KI];
+  const float* wr = p.W + int64_t(ic) * K;
+#pragma unroll
+  for (int u = 0; u < KI; ++u) {
+    const int j = 4 * lane + 256 * u;
+    w[u] = *reinterpret_cast<const float4*>(wr + (j < K ? j : 0));
+  }
+  float xv[kPer];
+  load_row(p.x, K, xv);
+  if (p.gam) {
+    float mean, rstd;
+    row_stats(xv, K, p.eps, scratch, mean, rstd);
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int j = int(threadIdx.x) + 256 * u;
+      if (j < kMaxK) h[j] = j < K ? fmaxf(fmaf((xv[u] - mean) * rstd, p.gam[j], p.bet[j]), 0.f) : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int j = int(threadIdx.x) + 256 * u;
+      if (j < kMaxK) h[j] = xv[u];
+    }
+  }
+  __syncthreads();
+  float acc = 0.f;
+#pragma unroll
+  for (int u = 0; u < KI; ++u) {
+    const int j = 4 * lane + 256 * u;
+    if (j < kMaxK) {
+      const float4 hv = *reinterpret_cast<const float4*>(h + j);  // 0 past K
+      acc = fmaf(w[u].x, hv.x, fmaf(w[u].y, hv.y, fmaf(w[u].z, hv.z, fmaf(w[u].w, hv.w, acc))));
+    }
+  }
+  acc = wave_sum(acc);
+  if (lane == 0 && i < p.N) p.y[i] = acc + (p.b ? p.b[i] : 0.f) + (p.res ? p.res[i] : 0.f);
+}
+
+int launch_fwd(GnFwdArgs& a, hipStream_t st) {
+  int blocks = 0, kmax = 0;
+  for (int q = 0; q < a.nprob; ++q) {
+    a.p[q].blk0 = blocks;
+    blocks += (a.p[q].N + 3) / 4;
+    kmax = a.p[q].K > kmax ? a.p[q].K : kmax;
+  }
+  for (int q = a.nprob; q < kMaxProb; ++q) a.p[q].blk0 = blocks;
+  if (kmax <= 256)
+    hipLaunchKernelGGL(gnode_fwd_kernel<1>, dim3(blocks), dim3(kFT), 0, st, a);
+  else if (kmax <= 1024)
+    hipLaunchKernelGGL(gnode_fwd_kernel<4>, dim3(blocks), dim3(kFT), 0, st, a);
+  else if (kmax <= 1280)
+    hipLaunchKernelGGL(gnode_fwd_kernel<5>, dim3(blocks), dim3(kFT), 0, st, a);
+  else
+    hipLaunchKernelGGL(gnode_fwd_kernel<8>, dim3(blocks), dim3(kFT), 0, st, a);
+  return launch_status("gasfm_gchain_fwd");
+}
+
+// --------------------------------------------------------------------------------- backward
+struct GnBwdProb {
+  const float* dy;   // [N] plain output gradient (null: the level's finish vector)
+  const float* x;    // [K] forward input row
+  const float* gam;  // [K] LayerNorm of x (null: h = x)
+  const float* bet;
+  const float* W;    // [N, K]
+  float* dW;         // [N, K]
+  float* db;         // [N] or null
+  float* dh;         // [K] W^T dy (final)
+  float* ws;         // [chunks, K] chunk partials
+  uint32_t* cnt;     // [slabs] self-resetting tickets
+  int K, N, blk0, slabs, chunks;
+  float eps;
+};
+// dy = dres + sum_q LN_q backward of raw_q (relu mask), LN_q over the row x [F]
+struct GnFinish {
+  const float* x;
+  const float* dres;
+  const float* raw[kMaxRaw];
+  const float* gam[kMaxRaw];
+  const float* bet[kMaxRaw];
+  float* dgam[kMaxRaw];
+  float* dbet[kMaxRaw];
+  float* out;  // [F] the finished vector (designated workgroup), or null
+  int F, nraw;
+  float eps;
+};
+struct GnBwdArgs {
+  GnBwdProb p[kMaxProb];
+  GnFinish f;
+  int nprob;
+};
+
+__device__ __forceinline__ void st_sc1(float* p, float4 v) {
+  uint64_t a, b;
+  __builtin_memcpy(&a, &v.x, 8);
+  __builtin_memcpy(&b, &v.z, 8);
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p) + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int RPT>  // rows per thread: a chunk is 32 RPT rows
+__global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float dfull[kMaxK];  // the finished dy (finish levels)
+  __shared__ float dys[32 * RPT];
+  __shared__ float4 red[kBT];
+  __shared__ float scratch[4 * 2 * kMaxRaw + 8];
+  __shared__ uint32_t flag;
+  int blk0[kMaxProb];
+#pragma unroll
+  for (int q = 0; q < kMaxProb; ++q) blk0[q] = a.p[q].blk0;
+  const int pi = find_prob(blk0, a.nprob);
+  const GnBwdProb& p = a.p[pi];
+  const int local = int(blockIdx.x) - p.blk0;
+  const int slab = local % p.slabs, chunk = local / p.slabs;
+  const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int K = p.K, N = p.N;
+  const int col = slab * kSW + 4 * cl;
+  const int row0 = chunk * 32 * RPT;
+  // 1. this workgroup's W slab rows, in flight through the prologues
+  float4 w[RPT];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int n = row0 + rl + 32 * r;
+    w[r] = *reinterpret_cast<const float4*>(p.W + int64_t(n < N ? n : N - 1) * K + col);
+  }
+  // 2. dy of the chunk's rows
+  const bool designated = pi == 0 && local == 0;
+  if (p.dy) {
+    for (int t = threadIdx.x; t < 32 * RPT; t += kBT) dys[t] = row0 + t < N ? p.dy[row0 + t] : 0.f;
+  } else {
+    const GnFinish& f = a.f;
+    const int F = f.F;
+    float xv[kPer], acc[kPer];
+    load_row(f.x, F, xv);
+    if (f.dres)
+      load_row(f.dres, F, acc);
+    else
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) acc[u] = 0.f;
+    float mean, rstd;
+    row_stats(xv, F, f.eps, scratch, mean, rstd);
+    float xh[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) xh[u] = (xv[u] - mean) * rstd;
+    float gv[kMaxRaw][kPer], sv[2 * kMaxRaw];
+#pragma unroll
+    for (int q = 0; q < kMaxRaw; ++q) {
+      sv[2 * q] = sv[2 * q + 1] = 0.f;
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) gv[q][u] = 0.f;
+      if (q >= f.nraw) continue;
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) {
+        const int j = int(threadIdx.x) + 256 * u;
+        if (j < F) {
+          const float ga = f.gam[q][j];
+          const float d = fmaf(xh[u], ga, f.bet[q][j]) > 0.f ? f.raw[q][j] : 0.f;
+          if (designated) {
+            f.dgam[q][j] = d * xh[u];
+            f.dbet[q][j] = d;
+          }
+          gv[q][u] = d * ga;
+          sv[2 * q] += gv[q][u];
+          sv[2 * q + 1] = fmaf(gv[q][u], xh[u], sv[2 * q + 1]);
+        }
+      }
+    }
+    block_sums<2 * kMaxRaw>(sv, scratch);
+#pragma unroll
+    for (int q = 0; q < kMaxRaw; ++q) {
+      if (q >= f.nraw) continue;
+      const float s1 = sv[2 * q] / F, s2 = sv[2 * q + 1] / F;
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) acc[u] += rstd * (gv[q][u] - s1 - xh[u] * s2);
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int j = int(threadIdx.x) + 256 * u;
+      if (j < F) {
+        dfull[j] = acc[u];
+        if (designated && f.out) f.out[j] = acc[u];
+      }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < 32 * RPT; t += kBT) dys[t] = row0 + t < N ? dfull[row0 + t] : 0.f;
+  }
+  // 3. h over the slab's 4 columns of this thread
+  float4 h4;
+  {
+    const float4 x4 = *reinterpret_cast<const float4*>(p.x + col);
+    if (p.gam) {
+      float xv[kPer];
+      load_row(p.x, K, xv);
+      float mean, rstd;
+      row_stats(xv, K, p.eps, scratch, mean, rstd);
+      const float4 g4 = *reinterpret_cast<const float4*>(p.gam + col);
+      const float4 b4 = *reinterpret_cast<const float4*>(p.bet + col);
+      h4 = make_float4(fmaxf(fmaf((x4.x - mean) * rstd, g4.x, b4.x), 0.f),
+                       fmaxf(fmaf((x4.y - mean) * rstd, g4.y, b4.y), 0.f),
+                       fmaxf(fmaf((x4.z - mean) * rstd, g4.z, b4.z), 0.f),
+                       fmaxf(fmaf((x4.w - mean) * rstd, g4.w, b4.w), 0.f));
+    } else {
+      h4 = x4;
+    }
+  }
+  __syncthreads();  // dys
+  // 4. dW rows and this thread's share of dh
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int n = row0 + rl + 32 * r;
+    const float d = dys[rl + 32 * r];  // 0 past N
+    s.x = fmaf(d, w[r].x, s.x);
+    s.y = fmaf(d, w[r].y, s.y);
+    s.z = fmaf(d, w[r].z, s.z);
+    s.w = fmaf(d, w[r].w, s.w);
+    if (n < N)
+      *reinterpret_cast<float4*>(p.dW + int64_t(n) * K + col) = make_float4(d * h4.x, d * h4.y, d * h4.z, d * h4.w);
+  }
+  if (p.db && slab == 0)
+    for (int t = threadIdx.x; t < 32 * RPT; t += kBT)
+      if (row0 + t < N) p.db[row0 + t] = dys[t];
+  // 5. the 32 row lanes summed in lane order
+  red[threadIdx.x] = s;
+  __syncthreads();
+  float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (threadIdx.x < 8) {
+#pragma unroll 8
+    for (int l = 0; l < 32; ++l) {
+      const float4 v = red[l * 8 + threadIdx.x];
+      tot.x += v.x;
+      tot.y += v.y;
+      tot.z += v.z;
+      tot.w += v.w;
+    }
+  }
+  if (p.chunks == 1) {
+    if (threadIdx.x < 8) *reinterpret_cast<float4*>(p.dh + col) = tot;
+    return;
+  }
+  // 6. hand the chunk partial to the slab's last arriver (write-through stores, one ticket)
+  if (threadIdx.x < 8) st_sc1(p.ws + int64_t(chunk) * K + col, tot);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = __hip_atomic_fetch_add(p.cnt + slab, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = t == uint32_t(p.chunks - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (flag == 0u) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (threadIdx.x < kSW) {
+    const int c = slab * kSW + int(threadIdx.x);
+    float acc = 0.f;
+    for (int ch = 0; ch < p.chunks; ++ch)
+      acc += __hip_atomic_load(p.ws + int64_t(ch) * K + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    p.dh[c] = acc;
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(p.cnt + slab, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int kRPT = 8;  // 256 rows per chunk
+
+int chunks_of(int N) { return (N + 32 * kRPT - 1) / (32 * kRPT); }
+
+// fills blk0 / slabs / chunks / ws / cnt of the level's problems; ws and cnt advance
+int launch_bwd(GnBwdArgs& a, float*& ws, uint32_t*& cnt, hipStream_t st, const char* where) {
+  int blocks = 0;
+  for (int q = 0; q < a.nprob; ++q) {
+    GnBwdProb& p = a.p[q];
+    p.blk0 = blocks;
+    p.slabs = p.K / kSW;
+    p.chunks = chunks_of(p.N);
+    p.ws = ws;
+    p.cnt = cnt;
+    ws += int64_t(p.chunks) * p.K;
+    cnt += p.slabs;
+    blocks += p.slabs * p.chunks;
+  }
+  for (int q = a.nprob; q < kMaxProb; ++q) a.p[q].blk0 = blocks;
+  hipLaunchKernelGGL(gnode_bwd_kernel<kRPT>, dim3(blocks), dim3(kBT), 0, st, a);
+  return launch_status(where);
+}
+
+bool hub_on(const gasfm_gchain* c) { return c->NB > 0; }
+
+}  // namespace
+}  // namespace gasfm
+
+using namespace gasfm;
+
+static int gchain_check(const gasfm_gchain* c) {
+  GASFM_REQUIRE(c, "gasfm_gchain: null parameters");
+  GASFM_REQUIRE(c->G > 0 && c->G <= kMaxK && c->G % kSW == 0 && c->Kc > 0 && c->Kc <= kMaxK && c->Kc % kSW == 0 &&
+                    c->NA > 0 && c->NA <= kMaxK,
+                "gasfm_gchain: G=%d Kc=%d NA=%d (multiples of %d, <= %d)", c->G, c->Kc, c->NA, kSW, kMaxK);
+  GASFM_REQUIRE(c->W1 && c->b1 && c->gM && c->bM && c->W2 && c->b2 && c->gA && c->bA && c->WA,
+                "gasfm_gchain: null weight");
+  if (c->NB > 0) {
+    GASFM_REQUIRE(c->NB <= kMaxK && c->NB % kSW == 0 && c->NC > 0 && c->NC <= kMaxK && c->NC % kSW == 0 &&
+                      c->ND > 0 && c->ND <= kMaxK && c->NE > 0 && c->NE <= kMaxK,
+                  "gasfm_gchain: NB=%d NC=%d ND=%d NE=%d", c->NB, c->NC, c->ND, c->NE);
+    GASFM_REQUIRE(c->gB && c->bB && c->WB && c->bWB && c->gC && c->bC && c->WC && c->bWC && c->WD && c->bD && c->WE &&
+                      c->bE,
+                  "gasfm_gchain: null hub weight");
+  }
+  const void* ws[] = {c->W1, c->W2, c->WA, c->WB, c->WC, c->WD, c->WE};
+  for (const void* p : ws) GASFM_REQUIRE(!p || aligned16(p), "gasfm_gchain: weights must be 16-byte aligned");
+  return GASFM_OK;
+}
+
+extern "C" int64_t gasfm_gchain_scratch_floats(const gasfm_gchain* c) {
+  if (!c) return 0;
+  // raw vectors: dh_D, dh_E, dh_A, dh_B, dh_C, dh_2, dg, dx1; chunk partials of the widest level
+  const int64_t vec = int64_t(c->NB) + c->NC + 6 * int64_t(c->G);
+  const int64_t l1 = int64_t(chunks_of(c->ND)) * c->NB + int64_t(chunks_of(c->NE)) * c->NC;
+  const int64_t l2 = int64_t(chunks_of(c->NA) + chunks_of(c->NB) + chunks_of(c->NC)) * c->G;
+  const int64_t l3 = int64_t(chunks_of(c->G)) * c->G;
+  const int64_t l4 = int64_t(chunks_of(c->G)) * c->Kc;
+  return vec + l1 + l2 + l3 + l4 + 64;
+}
+
+extern "C" int32_t gasfm_gchain_counters(const gasfm_gchain* c) {
+  if (!c) return 0;
+  return (c->NB + c->NC + 4 * c->G + c->Kc) / kSW + 8;
+}
+
+extern "C" int gasfm_gchain_fwd(const gasfm_gchain* c, const float* xcat, const float* prev, float* x1, float* g,
+                                float* sg, float* xv, float* xp, float* xrv, float* xrp, void* stream) {
+  const int s0 = gchain_check(c);
+  if (s0 != GASFM_OK) return s0;
+  GASFM_REQUIRE(xcat && x1 && g && sg && (!hub_on(c) || (xv && xp && xrv && xrp)), "gasfm_gchain_fwd: null output");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  GnFwdArgs a{};
+  a.nprob = 1;
+  a.p[0] = GnFwdProb{xcat, nullptr, nullptr, c->W1, c->b1, prev, x1, c->Kc, c->G, 0, 0.f};
+  int s = launch_fwd(a, st);
+  if (s != GASFM_OK) return s;
+  a.p[0] = GnFwdProb{x1, c->gM, c->bM, c->W2, c->b2, x1, g, c->G, c->G, 0, c->eps_m};
+  s = launch_fwd(a, st);
+  if (s != GASFM_OK) return s;
+  a.p[0] = GnFwdProb{g, c->gA, c->bA, c->WA, nullptr, nullptr, sg, c->G, c->NA, 0, c->eps_h};
+  if (hub_on(c)) {
+    a.nprob = 3;
+    a.p[1] = GnFwdProb{g, c->gB, c->bB, c->WB, c->bWB, nullptr, xv, c->G, c->NB, 0, c->eps_h};
+    a.p[2] = GnFwdProb{g, c->gC, c->bC, c->WC, c->bWC, nullptr, xp, c->G, c->NC, 0, c->eps_h};
+  }
+  s = launch_fwd(a, st);
+  if (s != GASFM_OK || !hub_on(c)) return s;
+  a.nprob = 2;
+  a.p[0] = GnFwdProb{xv, nullptr, nullptr, c->WD, c->bD, nullptr, xrv, c->NB, c->ND, 0, 0.f};
+  a.p[1] = GnFwdProb{xp, nullptr, nullptr, c->WE, c->bE, nullptr, xrp, c->NC, c->NE, 0, 0.f};
+  return launch_fwd(a, st);
+}
+
+extern "C" int gasfm_gchain_bwd(const gasfm_gchain* c, const float* xcat, const float* x1, const float* g,
+                                const float* xv, const float* xp, const float* dskip, const float* dsg,
+                                const float* dxrv, const float* dxrp, float* dxcat, float* dprev,
+                                const gasfm_gchain_grads* d, float* scratch, uint32_t* counters, void* stream) {
+  const int s0 = gchain_check(c);
+  if (s0 != GASFM_OK) return s0;
+  GASFM_REQUIRE(d && xcat && x1 && g && dsg && dxcat && scratch && counters, "gasfm_gchain_bwd: null pointer");
+  GASFM_REQUIRE(d->dW1 && d->db1 && d->dgM && d->dbM && d->dW2 && d->db2 && d->dgA && d->dbA && d->dWA,
+                "gasfm_gchain_bwd: null gradient");
+  const bool hub = hub_on(c);
+  if (hub)
+    GASFM_REQUIRE(xv && xp && dxrv && dxrp && d->dgB && d->dbB && d->dWB && d->dbWB && d->dgC && d->dbC && d->dWC &&
+                      d->dbWC && d->dWD && d->dbD && d->dWE && d->dbE,
+                  "gasfm_gchain_bwd: null hub pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  float* dhD = scratch;
+  float* dhE = dhD + c->NB;
+  float* dhA = dhE + c->NC;
+  float* dhB = dhA + c->G;
+  float* dhC = dhB + c->G;
+  float* dh2 = dhC + c->G;
+  float* dg = dh2 + c->G;
+  float* dx1 = dprev ? dprev : dg + c->G;
+  float* ws = dg + 2 * c->G;
+  uint32_t* cnt = counters;
+  int s;
+  if (hub) {  // B1: the two lin_r rows
+    GnBwdArgs a{};
+    a.nprob = 2;
+    a.p[0] = GnBwdProb{dxrv, xv, nullptr, nullptr, c->WD, d->dWD, d->dbD, dhD, nullptr, nullptr, c->NB, c->ND};
+    a.p[1] = GnBwdProb{dxrp, xp, nullptr, nullptr, c->WE, d->dWE, d->dbE, dhE, nullptr, nullptr, c->NC, c->NE};
+    s = launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(lin_r)");
+    if (s != GASFM_OK) return s;
+  }
+  {  // B2: the LayerNorm -> Linear consumers of g (raw dh, LayerNorm backward deferred)
+    GnBwdArgs a{};
+    a.nprob = hub ? 3 : 1;
+    a.p[0] = GnBwdProb{dsg, g, c->gA, c->bA, c->WA, d->dWA, nullptr, dhA, nullptr, nullptr, c->G, c->NA};
+    a.p[0].eps = c->eps_h;
+    if (hub) {
+      a.p[1] = GnBwdProb{dhD, g, c->gB, c->bB, c->WB, d->dWB, d->dbWB, dhB, nullptr, nullptr, c->G, c->NB};
+      a.p[2] = GnBwdProb{dhE, g, c->gC, c->bC, c->WC, d->dWC, d->dbWC, dhC, nullptr, nullptr, c->G, c->NC};
+      a.p[1].eps = a.p[2].eps = c->eps_h;
+    }
+    s = launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(hub)");
+    if (s != GASFM_OK) return s;
+  }
+  {  // B3: dg = dskip + LN_A/B/C backward (every workgroup), then the MLP Linear
+    GnBwdArgs a{};
+    a.nprob = 1;
+    a.p[0] = GnBwdProb{nullptr, x1, c->gM, c->bM, c->W2, d->dW2, d->db2, dh2, nullptr, nullptr, c->G, c->G};
+    a.p[0].eps = c->eps_m;
+    GnFinish& f = a.f;
+    f.x = g;
+    f.dres = dskip;
+    f.F = c->G;
+    f.eps = c->eps_h;
+    f.nraw = hub ? 3 : 1;
+    f.raw[0] = dhA, f.gam[0] = c->gA, f.bet[0] = c->bA, f.dgam[0] = d->dgA, f.dbet[0] = d->dbA;
+    if (hub) {
+      f.raw[1] = dhB, f.gam[1] = c->gB, f.bet[1] = c->bB, f.dgam[1] = d->dgB, f.dbet[1] = d->dbB;
+      f.raw[2] = dhC, f.gam[2] = c->gC, f.bet[2] = c->bC, f.dgam[2] = d->dgC, f.dbet[2] = d->dbC;
+    }
+    f.out = dg;
+    s = launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(mlp)");
+    if (s != GASFM_OK) return s;
+  }
+  // B4: dx1 = dg + LN_M backward (every workgroup), then proj_view_and_scenepoint2global
+  GnBwdArgs a{};
+  a.nprob = 1;
+  a.p[0] = GnBwdProb{nullptr, xcat, nullptr, nullptr, c->W1, d->dW1, d->db1, dxcat, nullptr, nullptr, c->Kc, c->G};
+  GnFinish& f = a.f;
+  f.x = x1;
+  f.dres = dg;
+  f.F = c->G;
+  f.eps = c->eps_m;
+  f.nraw = 1;
+  f.raw[0] = dh2, f.gam[0] = c->gM, f.bet[0] = c->bM, f.dgam[0] = d->dgM, f.dbet[0] = d->dbM;
+  f.out = dx1;
+  return launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(proj)");
+}

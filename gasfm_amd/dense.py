@@ -188,6 +188,114 @@ def global_hub_params(pfu, nvsg):
             linC.weight, linC.bias, linD.weight, linD.bias, linE.weight, linE.bias, lnA.eps)
 
 
+_GC_W = ("W1", "b1", "gM", "bM", "W2", "b2", "gA", "bA", "WA", "gB", "bB", "WB", "bWB", "gC", "bC", "WC", "bWC",
+         "WD", "bD", "WE", "bE")
+GCHAIN_MAX = 2048
+
+
+class GlobalChainFn(torch.autograd.Function):
+    """A block's whole global-node chain on ONE row (csrc/global_chain.hip), four launches each way:
+    ViewAndScenePoint2Global's tail (layers.py:527-528, 590-603) and every consumer of its output g
+    -- lin_global of the block's projection update (layers.py:928-935) and, when the next block has
+    a global update, its norm_and_proj_global2view / _global2scenepoint (layers.py:497-520) and the
+    two lin_r rows of its global convs.  Replaces the linear_res / ln_relu_linear GlobalLinearFns
+    and GlobalHubFn (12 backward launches per block, each GEMV followed by a one-workgroup finish).
+
+    apply(xcat [1, Kc], prev [1, G] or None, *weights (_GC_W order; the hub's B..E None for the last
+    block), eps_m, eps_h) -> (g, SG, XRv, XRp), or (g, SG) without the hub."""
+
+    @staticmethod
+    def forward(ctx, xcat, prev, *args):
+        from . import _native
+        ws, eps_m, eps_h = args[:-2], args[-2], args[-1]
+        w = {k: (t.contiguous() if t is not None else None) for k, t in zip(_GC_W, ws)}
+        c = _native.gchain_struct(w, eps_m, eps_h)
+        hub = w["WB"] is not None
+        f = dict(dtype=torch.float32, device=xcat.device)
+        x1c = xcat.reshape(-1).contiguous()
+        pv = prev.reshape(-1).contiguous() if prev is not None else None
+        G = c.G
+        x1, g, sg = torch.empty(G, **f), torch.empty(G, **f), torch.empty(c.NA, **f)
+        xv = xp = xrv = xrp = None
+        if hub:
+            xv, xp, xrv, xrp = (torch.empty(n, **f) for n in (c.NB, c.NC, c.ND, c.NE))
+        _native.gchain_fwd(c, x1c, pv, x1, g, sg, xv, xp, xrv, xrp)
+        ctx.save_for_backward(x1c, x1, g, xv, xp, *(w[k] for k in _GC_W))
+        ctx.eps = (eps_m, eps_h)
+        ctx.hub, ctx.has_prev = hub, prev is not None
+        ctx.shapes = (xcat.shape, prev.shape if prev is not None else None)
+        ctx.set_materialize_grads(False)
+        if hub:
+            return g.view(1, G), sg.view(1, -1), xrv.view(1, -1), xrp.view(1, -1)
+        return g.view(1, G), sg.view(1, -1)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        from . import _native
+        x1c, x1, g, xv, xp, *wl = ctx.saved_tensors
+        w = dict(zip(_GC_W, wl))
+        c = _native.gchain_struct(w, *ctx.eps)
+        f = dict(dtype=torch.float32, device=g.device)
+        row = lambda t, n: t.reshape(-1).contiguous() if t is not None else torch.zeros(n, **f)  # noqa: E731
+        dskip = grads[0].reshape(-1).contiguous() if grads[0] is not None else None
+        dsg = row(grads[1], c.NA)
+        dxrv = dxrp = None
+        if ctx.hub:
+            dxrv, dxrp = row(grads[2], c.ND), row(grads[3], c.NE)
+        d = {"d" + k: (torch.empty_like(t) if t is not None else None) for k, t in w.items()}
+        dxcat = torch.empty(c.Kc, **f)
+        dprev = torch.empty(c.G, **f) if ctx.has_prev else None
+        _native.gchain_bwd(c, x1c, x1, g, xv, xp, dskip, dsg, dxrv, dxrp, dxcat, dprev, d)
+        xs, ps = ctx.shapes
+        return (dxcat.view(xs), dprev.view(ps) if dprev is not None else None,
+                *(d["d" + k] for k in _GC_W), None, None)
+
+
+def _ln_of(ln, G):
+    return (isinstance(ln, LayerNorm) and tuple(ln.normalized_shape) == (G,) and ln.weight is not None
+            and ln.bias is not None)
+
+
+def chain_params(vsg, pfu, nvsg):
+    """(weights in _GC_W order, eps_m, eps_h) of GlobalChainFn for ViewAndScenePoint2Global vsg's tail
+    plus the consumers of its output: pfu's lin_global and, unless nvsg is None (the last block),
+    the next block's global update nvsg; None when the shapes are not the fused kernels'."""
+    if not hasattr(vsg, "proj_view_and_scenepoint2global") or not vsg.use_norm_pre_mlp or len(vsg.mlp) != 1:
+        return None
+    p1, lnM, l2 = vsg.proj_view_and_scenepoint2global, vsg.norm_pre_mlp, vsg.mlp[0]
+    G, Kc = p1.out_features, p1.in_features
+    fit = lambda n: n % 32 == 0 and 0 < n <= GCHAIN_MAX  # noqa: E731
+    if not (fit(G) and fit(Kc) and p1.bias is not None and isinstance(l2, Linear) and l2.in_features == G
+            and l2.out_features == G and l2.bias is not None and _ln_of(lnM, G)):
+        return None
+    if pfu is None or not pfu.normalize_global_features:
+        return None
+    lnA, linA = pfu.global_norm_layer, pfu.lin_global
+    if not (_ln_of(lnA, G) and linA.bias is None and linA.in_features == G and linA.out_features <= GCHAIN_MAX):
+        return None
+    w = dict(W1=p1.weight, b1=p1.bias, gM=lnM.weight, bM=lnM.bias, W2=l2.weight, b2=l2.bias, gA=lnA.weight,
+             bA=lnA.bias, WA=linA.weight)
+    if nvsg is not None:
+        hp = global_hub_params(pfu, nvsg)
+        if hp is None:
+            return None
+        _, _, _, gB, bB, WB, bWB, gC, bC, WC, bWC, WD, bD, WE, bE, _ = hp
+        if not (fit(WB.shape[0]) and fit(WC.shape[0]) and WD.shape[0] <= GCHAIN_MAX and WE.shape[0] <= GCHAIN_MAX):
+            return None
+        w.update(gB=gB, bB=bB, WB=WB, bWB=bWB, gC=gC, bC=bC, WC=WC, bWC=bWC, WD=WD, bD=bD, WE=WE, bE=bE)
+    return tuple(w.get(k) for k in _GC_W), lnM.eps, lnA.eps
+
+
+def global_chain(x, prev, params):
+    """GlobalChainFn on a single row x [1, Kc] (prev [1, G] or None) when it fits, else None."""
+    if not (x.is_cuda and x.dim() == 2 and x.shape[0] == 1 and x.dtype == torch.float32):
+        return None
+    if prev is not None and not (prev.numel() == params[0][0].shape[0] and prev.is_cuda):
+        return None
+    ws, eps_m, eps_h = params
+    return GlobalChainFn.apply(x, prev, *ws, eps_m, eps_h)
+
+
 def _gvec_ok(x, k):
     return (x.is_cuda and x.dim() == 2 and x.shape[0] == 1 and x.dtype == torch.float32 and k % 64 == 0
             and k <= GVEC_MAX_K)

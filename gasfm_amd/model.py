@@ -41,6 +41,9 @@ EDGE_CAM = os.environ.get("GASFM_EDGE_CAM", "1") != "0"
 EDGE_SEAM = os.environ.get("GASFM_EDGE_SEAM", "1") != "0"
 # Block 0's (2-wide) epilogue likewise inside block 1's prologue kernel (Seam0Fn, gasfm_edge0_seam_fwd).
 EDGE_SEAM0 = os.environ.get("GASFM_EDGE_SEAM0", "1") != "0"
+# A block's whole global-node chain (its tail and every consumer of g) as one GlobalChainFn
+# (csrc/global_chain.hip, round 4); GASFM_GLOBAL_CHAIN=0: the GlobalLinearFn / GlobalHubFn path.
+GLOBAL_CHAIN = os.environ.get("GASFM_GLOBAL_CHAIN", "1") != "0"
 
 
 def replicated_to_local(x, shard):
@@ -232,11 +235,13 @@ class ViewAndScenePoint2Global(Module):
         self.mlp = get_linear_layers((2 + n_hidden_layers_global_update) * [n_feat_global_out], norm=False)
 
     def forward_plan(self, view, pts, plan_v2g, plan_s2g, prev, plan_s2g_partial=None, shard=None, xl_pts=None,
-                     xl_view=None, pre_glob=None, plan_v2g_partial=None):
+                     xl_view=None, pre_glob=None, plan_v2g_partial=None, chain=None):
         """xl_pts / xl_view: the convs' lin_l(pts) / lin_l(view) when already computed (hubs);
         pre_glob: (XR_view2global, XR_scenepoint2global, skip of prev) from GlobalHubFn.
         Camera-sharded (shard.cams): view holds this rank's camera rows and both attentions
-        exchange partial states in one all-gather (distributed.ShardedGlobalAttentionFn)."""
+        exchange partial states in one all-gather (distributed.ShardedGlobalAttentionFn).
+        chain: dense.chain_params of this update and the consumers of its output; the tail then runs
+        as one GlobalChainFn and forward_plan returns its (g, SG[, XRv, XRp]) tuple."""
         assert self.stateful == (prev is not None)
         cv, c = self.graph_conv_view2global, self.graph_conv_scenepoint2global
         if pre_glob is not None:
@@ -252,22 +257,26 @@ class ViewAndScenePoint2Global(Module):
             x = ShardedGlobalAttentionFn.apply(
                 XLv, XRv, cv.att, cv._bias(XLv), XLp, XRp, c.att, c.bias,
                 (plan_v2g, plan_v2g_partial, plan_s2g, plan_s2g_partial), c.heads, c.negative_slope, shard)
-            return self._global_tail(x, prev)
+            return self._global_tail(x, prev, chain)
         if shard is None and XLv.is_cuda and plan_v2g.num_targets == 1 and plan_s2g.num_targets == 1 \
                 and cv.heads == c.heads and cv.negative_slope == c.negative_slope:
             from .attention import GlobalPairFn
             x = GlobalPairFn.apply(XLv, XRv, cv.att, cv._bias(XLv), XLp, XRp, c.att, c._bias(XLp), plan_v2g, plan_s2g,
                                    c.heads, c.negative_slope)
-            return self._global_tail(x, prev)
+            return self._global_tail(x, prev, chain)
         v2g = gat_attention(XLv, XRv, cv.att, cv._bias(XLv), plan_v2g, cv.heads, cv.negative_slope)
         if shard is None:
             s2g = gat_attention(XLp, XRp, c.att, c._bias(XLp), plan_s2g, c.heads, c.negative_slope)
         else:  # points are sharded, the global target is replicated
             s2g = ShardedAttentionFn.apply(XLp, replicated_to_local(XRp, shard), c.att, c.bias, plan_s2g,
                                            plan_s2g_partial, c.heads, c.negative_slope, shard)
-        return self._global_tail(torch.cat([v2g, s2g], dim=1), prev)
+        return self._global_tail(torch.cat([v2g, s2g], dim=1), prev, chain)
 
-    def _global_tail(self, x, prev):
+    def _global_tail(self, x, prev, chain=None):
+        if chain is not None:
+            out = dense.global_chain(x, prev, chain)
+            if out is not None:
+                return out
         if hasattr(self, "proj_view_and_scenepoint2global"):
             x = dense.linear_res(x, self.proj_view_and_scenepoint2global, prev)
         elif prev is not None:
@@ -532,13 +541,25 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         glob = None
         if self.output_global or self.global2view_and_global2scenepoint_enabled:
             pre_glob = carry.pop("pre_glob", None) if carry is not None else None
+            chain = None
+            if GLOBAL_CHAIN and carry is not None and pfu is not None and self.output_global:
+                nv = nxt.view_and_scenepoint2global if nxt is not None and getattr(nxt, "output_global", False) \
+                    else None
+                chain = dense.chain_params(self.view_and_scenepoint2global, pfu, nv)
             glob = self.view_and_scenepoint2global.forward_plan(
                 view, pts, plans["view2global"], plans["scenepoint2global"], prev_glob,
                 plans.get("_partial", {}).get("scenepoint2global"), plans.get("_shard"),
                 xl_pts=carry.pop("XLs2g", None) if carry is not None else None,
                 xl_view=carry.pop("XLv2g", None) if carry is not None else None, pre_glob=pre_glob,
-                plan_v2g_partial=plans.get("_partial", {}).get("view2global"))
-            if carry is not None and nxt is not None and getattr(nxt, "output_global", False) \
+                plan_v2g_partial=plans.get("_partial", {}).get("view2global"), chain=chain)
+            if isinstance(glob, tuple):  # GlobalChainFn: g with its consumers' rows
+                if len(glob) == 4:
+                    glob, SG, XRv, XRp = glob
+                    carry.update(SG=SG, pre_glob=(XRv, XRp, glob))
+                else:
+                    glob, SG = glob
+                    carry.update(SG=SG)
+            elif carry is not None and nxt is not None and getattr(nxt, "output_global", False) \
                     and dense._gvec_ok(glob, glob.shape[1]):
                 hg = dense.global_hub_params(pfu, nxt.view_and_scenepoint2global)
                 if hg is not None:

@@ -631,6 +631,45 @@ int gasfm_gvec_bwd(const float* dy, const float* x, int32_t K, const float* ln_w
                    float eps, const float* W, int32_t N, int32_t resid, float* dx, float* dW, float* db,
                    float* dgamma, float* dbeta, float* part, void* stream);
 
+/* ---- the global node's whole chain of one block (global_chain.hip, round 4) ----
+ * Replaces, as ONE forward / backward pair of four launches each, the per-block single-row chain
+ * ViewAndScenePoint2Global's tail (layers.py:527-528, 590-603: x1 = W1 xcat + b1 (+ prev),
+ * g = x1 + W2 relu(LN_M(x1)) + b2) and every consumer of g: lin_global of the projection update
+ * (layers.py:928-935: SG = WA relu(LN_A(g))), the next block's norm_and_proj_global2view /
+ * _global2scenepoint (layers.py:497-520: xv = WB relu(LN_B(g)) + bWB, xp = WC relu(LN_C(g)) + bWC)
+ * and the two lin_r rows of the next block's global GATv2 convs (PyG: XRv = WD xv + bD,
+ * XRp = WE xp + bE).  NB = 0 (and NC = ND = NE = 0): the last block, whose g has SG only.
+ * Widths G, Kc, NB, NC: multiples of 32, <= 2048.  All weights row-major [out, in], 16-byte aligned. */
+typedef struct gasfm_gchain {
+  int32_t G, Kc, NA, NB, NC, ND, NE;
+  float eps_m, eps_h; /* norm_pre_mlp eps; the hub LayerNorms' (shared) eps */
+  const float *W1, *b1, *gM, *bM, *W2, *b2;
+  const float *gA, *bA, *WA;
+  const float *gB, *bB, *WB, *bWB, *gC, *bC, *WC, *bWC;
+  const float *WD, *bD, *WE, *bE;
+} gasfm_gchain;
+typedef struct gasfm_gchain_grads {
+  float *dW1, *db1, *dgM, *dbM, *dW2, *db2;
+  float *dgA, *dbA, *dWA;
+  float *dgB, *dbB, *dWB, *dbWB, *dgC, *dbC, *dWC, *dbWC;
+  float *dWD, *dbD, *dWE, *dbE;
+} gasfm_gchain_grads;
+
+/* Forward: xcat [Kc], prev [G] or NULL -> x1, g [G], sg [NA] (and xv [NB], xp [NC], xrv [ND],
+ * xrp [NE] when NB > 0). */
+int gasfm_gchain_fwd(const gasfm_gchain* c, const float* xcat, const float* prev, float* x1, float* g, float* sg,
+                     float* xv, float* xp, float* xrv, float* xrp, void* stream);
+/* Scratch floats and ticket counters (zeroed, self-resetting) gasfm_gchain_bwd needs. */
+int64_t gasfm_gchain_scratch_floats(const gasfm_gchain* c);
+int32_t gasfm_gchain_counters(const gasfm_gchain* c);
+/* Backward from d g (dskip, may be NULL), d SG, d XRv, d XRp -> d xcat [Kc], d prev [G] (may be
+ * NULL when the forward had no prev) and every parameter gradient (grads of absent hub terms
+ * ignored).  Deterministic (no float atomics). */
+int gasfm_gchain_bwd(const gasfm_gchain* c, const float* xcat, const float* x1, const float* g, const float* xv,
+                     const float* xp, const float* dskip, const float* dsg, const float* dxrv, const float* dxrp,
+                     float* dxcat, float* dprev, const gasfm_gchain_grads* d, float* scratch, uint32_t* counters,
+                     void* stream);
+
 /* Reprojection error of compute_core_errors' "our_repro" (code/evaluation.py:8-31 ->
  * geo_utils.reprojection_error_with_points, geo_utils.py:371-391) over the E visibility edges:
  * err_e = || xy_e - (P_c X)_xy / (P_c X)_z ||, X = pflat(pts3D[:, p]), P = Ps_pix [m x 12]

@@ -106,3 +106,75 @@ def test_global_hub_matches_fp64(device, G, V, S, with_skip):
         ga, gr = a.grad.double().cpu(), r64.grad
         err = (ga - gr).norm().item()
         assert err <= 1e-4 * gr.norm().item() + 1e-6, f"{name}: {err:.3e} vs |ref| {gr.norm().item():.3e}"
+
+
+@pytest.mark.parametrize("G,Kc,V,S", [(2048, 1088, 1024, 64), (128, 128, 64, 64)])
+@pytest.mark.parametrize("hub", [True, False], ids=["hub", "last_block"])
+@pytest.mark.parametrize("with_prev", [True, False], ids=["prev", "no_prev"])
+def test_global_chain_matches_fp64(device, G, Kc, V, S, hub, with_prev):
+    """GlobalChainFn (csrc/global_chain.hip: the block's global tail + every consumer of g, four
+    launches each way) vs the fp64 composition of layers.py:527-603 and its consumers (:497-520,
+    :928-935, the next convs' lin_r).  Tolerances as the gvec tests: outputs 2e-5 * max|ref|,
+    gradients normwise 1e-4."""
+    gen = torch.Generator().manual_seed(G + Kc + 2 * hub + with_prev)
+    r = lambda *s, sc=1.0, sh=0.0: torch.randn(*s, generator=gen, dtype=torch.float64) * sc + sh  # noqa: E731
+    names = ["xcat", "prev", "W1", "b1", "gM", "bM", "W2", "b2", "gA", "bA", "WA",
+             "gB", "bB", "WB", "bWB", "gC", "bC", "WC", "bWC", "WD", "bD", "WE", "bE"]
+    vals = [r(1, Kc, sc=1.5, sh=0.1), r(1, G, sc=2), r(G, Kc, sc=Kc ** -0.5), r(G, sc=0.1), r(G, sc=0.3, sh=1),
+            r(G, sc=0.2), r(G, G, sc=G ** -0.5), r(G, sc=0.1), r(G, sc=0.3, sh=1), r(G, sc=0.2), r(32, G, sc=G ** -0.5),
+            r(G, sc=0.3, sh=1), r(G, sc=0.2), r(V, G, sc=G ** -0.5), r(V, sc=0.1),
+            r(G, sc=0.3, sh=1), r(G, sc=0.2), r(S, G, sc=G ** -0.5), r(S, sc=0.1),
+            r(V, V, sc=V ** -0.5), r(V, sc=0.1), r(S, S, sc=S ** -0.5), r(S, sc=0.1)]
+    present = {k: (with_prev or k != "prev") and (hub or k in names[:11]) for k in names}
+    ref = {k: v.clone().requires_grad_(True) for k, v in zip(names, vals) if present[k]}
+    ln = lambda x, w, b: F.relu(F.layer_norm(x, (G,), w, b, 1e-5))  # noqa: E731
+    x1 = F.linear(ref["xcat"], ref["W1"], ref["b1"]) + (ref["prev"] if with_prev else 0)
+    g = x1 + F.linear(ln(x1, ref["gM"], ref["bM"]), ref["W2"], ref["b2"])
+    outs64 = [g, F.linear(ln(g, ref["gA"], ref["bA"]), ref["WA"])]
+    if hub:
+        outs64 += [F.linear(F.linear(ln(g, ref["gB"], ref["bB"]), ref["WB"], ref["bWB"]), ref["WD"], ref["bD"]),
+                   F.linear(F.linear(ln(g, ref["gC"], ref["bC"]), ref["WC"], ref["bWC"]), ref["WE"], ref["bE"])]
+    douts = [r(*o.shape) for o in outs64]
+    torch.autograd.backward(outs64, douts)
+    got = {k: v.detach().float().to(device).requires_grad_(True) for k, v in ref.items()}
+    ws = [got.get(k) for k in names[2:]]
+    outs = dense.GlobalChainFn.apply(got["xcat"], got.get("prev"), *ws, 1e-5, 1e-5)
+    assert len(outs) == len(outs64)
+    for name, o, r64 in zip(("g", "SG", "XRv", "XRp"), outs, outs64):
+        torch.testing.assert_close(o.double().cpu(), r64.detach(), rtol=0, atol=2e-5 * r64.abs().max().item() + 1e-5,
+                                   msg=name)
+    torch.autograd.backward(list(outs), [d.float().to(device) for d in douts])
+    for k, a in got.items():
+        ga, gr = a.grad.double().cpu(), ref[k].grad
+        err = (ga - gr).norm().item()
+        assert err <= 1e-4 * gr.norm().item() + 1e-6, f"{k}: {err:.3e} vs |ref| {gr.norm().item():.3e}"
+    # deterministic: a second backward gives bitwise the same gradients
+    first = {k: a.grad.clone() for k, a in got.items()}
+    for a in got.values():
+        a.grad = None
+    outs = dense.GlobalChainFn.apply(got["xcat"], got.get("prev"), *ws, 1e-5, 1e-5)
+    torch.autograd.backward(list(outs), [d.float().to(device) for d in douts])
+    for k, a in got.items():
+        assert torch.equal(a.grad, first[k]), k
+
+
+def test_model_uses_global_chain(device):
+    """The learning conf's blocks run their global node through GlobalChainFn (hub blocks and the
+    last block's lin_global-only chain)."""
+    import gasfm_amd
+    from gasfm_amd import synthetic
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=3)).to(device)
+    sc = synthetic.scaled_config4(0.01, seed=2)
+    data = gasfm_amd.SceneData.from_synthetic(sc).to(device)
+    pred = net(data)
+    seen, todo = set(), [pred["Ps_norm"].grad_fn]
+    names = []
+    while todo:
+        fn = todo.pop()
+        if fn is None or fn in seen:
+            continue
+        seen.add(fn)
+        names.append(type(fn).__name__)
+        todo.extend(f for f, _ in fn.next_functions)
+    assert names.count("GlobalChainFnBackward") == 3, names.count("GlobalChainFnBackward")
+    assert "GlobalHubFnBackward" not in names
