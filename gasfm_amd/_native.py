@@ -106,6 +106,14 @@ _SIGS = {
     "gasfm_gvec_multi_fwd": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp]),
     "gasfm_gvec_multi_bwd": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp,
                                     _vp, _vp, _f32, _vp]),
+    "gasfm_view_chain_ok": (_i32, [_i64, _i32]),
+    "gasfm_view_chain_scratch_floats": (_i64, [_i64, _i32]),
+    "gasfm_view_chain_counters": (_i32, [_i64]),
+    "gasfm_view_chain_tail_fwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                         _vp]),
+    "gasfm_view_chain_hub_fwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 15 + [_i32, _vp, _vp]),
+    "gasfm_view_chain_hub_bwd": (_i32, [_vp, _vp, _i64, _i32] + [_vp] * 17),
+    "gasfm_view_chain_tail_bwd": (_i32, [_vp] * 5 + [_i64, _i32] + [_vp] * 12),
     "gasfm_gchain_fwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_gchain_scratch_floats": (_i64, [_vp]),
     "gasfm_gchain_counters": (_i32, [_vp]),
@@ -972,6 +980,65 @@ def view_hub_fwd(v, eps, gC, bC, Wv, gA, bA, Wa, ba, Wr, br, sv, t, xr, rs, scra
     st = lib().gasfm_view_hub_fwd(_p(v), v.shape[0], v.shape[1], eps, _p(gC), _p(bC), _p(Wv), _p(gA), _p(bA), _p(Wa),
                                   _p(ba), _p(Wr), _p(br), _p(sv), _p(t), _p(xr), ldo, _p(rs), _p(scratch), _stream(v))
     check(st, "gasfm_view_hub_fwd")
+
+
+def view_chain_ok(m, D):
+    return bool(lib().gasfm_view_chain_ok(m, D))
+
+
+def _vc_scratch(m, D, device):
+    return torch.empty(max(1, int(lib().gasfm_view_chain_scratch_floats(m, D))), dtype=torch.float32, device=device)
+
+
+def view_chain_tail_fwd(prev, agg, Wp, bp, ln_w, ln_b, eps, Wm, bm, view, x, h, rs):
+    _req(agg, "agg", 32)
+    m, D = view.shape
+    for t, n in ((view, "view"), (x, "x"), (h, "h"), (Wm, "Wm"), (Wp, "Wp")) + (((prev, "prev"),) if prev is not None else ()):
+        _req(t, n)
+    st = lib().gasfm_view_chain_tail_fwd(_p(prev), _p(agg), m, D, _p(Wp), _p(bp), _p(ln_w), _p(ln_b), eps, _p(Wm),
+                                         _p(bm), _p(view), _p(x), _p(h), _p(rs), _stream(agg))
+    check(st, "gasfm_view_chain_tail_fwd")
+
+
+def view_chain_hub_fwd(v, eps, Wl, bl, gC, bC, Wv, gA, bA, Wa, ba, Wr, br, XL, sv, t, xr, rs):
+    _req(v, "v")
+    ldo = _rows32(sv, "sv")
+    if _rows32(xr, "xr") != ldo:
+        raise ValueError("view_chain_hub_fwd: sv and xr need the same row stride")
+    for a, n in ((Wl, "Wl"), (Wv, "Wv"), (Wa, "Wa"), (XL, "XL")):
+        _req(a, n)
+    st = lib().gasfm_view_chain_hub_fwd(_p(v), v.shape[0], v.shape[1], eps, _p(Wl), _p(bl), _p(gC), _p(bC), _p(Wv),
+                                        _p(gA), _p(bA), _p(Wa), _p(ba), _p(Wr), _p(br), _p(XL), _p(sv), _p(t), _p(xr),
+                                        ldo, _p(rs), _stream(v))
+    check(st, "gasfm_view_chain_hub_fwd")
+
+
+def view_chain_hub_bwd(v, rs, gC, bC, Wv, gA, bA, Wa, t, Wr, Wl, dsv, dxr, dxl, dres, dacc, dWl, part):
+    _req(v, "v")
+    m, D = v.shape
+    for a, n, w in ((t, "t", 32), (dsv, "dsv", 32), (dxr, "dxr", 32), (dxl, "dxl", D), (dacc, "dacc", D),
+                    (dWl, "dWl", D)):
+        _req(a, n, w)
+    if dres is not None:
+        _req(dres, "dres", D)
+    scratch = _vc_scratch(m, D, v.device)
+    st = lib().gasfm_view_chain_hub_bwd(_p(v), _p(rs), m, D, _p(gC), _p(bC), _p(Wv), _p(gA), _p(bA), _p(Wa), _p(t),
+                                        _p(Wr), _p(Wl), _p(dsv), _p(dxr), _p(dxl), _p(dres), _p(dacc), _p(dWl),
+                                        _p(part), _p(scratch), _stream(v))
+    check(st, "gasfm_view_chain_hub_bwd")
+
+
+def view_chain_tail_bwd(dv, x, h, rs, agg, Wp, ln_w, ln_b, Wm, dh, dWm, dx, dagg, part):
+    m, D = x.shape
+    for a, n in ((dv, "dv"), (x, "x"), (h, "h"), (dh, "dh"), (dx, "dx"), (dWm, "dWm")):
+        _req(a, n, D)
+    _req(agg, "agg", 32)
+    scratch = _vc_scratch(m, D, x.device)
+    cnt = _counters(x.device, lib().gasfm_view_chain_counters(m))
+    st = lib().gasfm_view_chain_tail_bwd(_p(dv), _p(x), _p(h), _p(rs), _p(agg), m, D, _p(Wp), _p(ln_w), _p(ln_b),
+                                         _p(Wm), _p(dh), _p(dWm), _p(dx), _p(dagg), _p(part), _p(scratch), _p(cnt),
+                                         _stream(x))
+    check(st, "gasfm_view_chain_tail_bwd")
 
 
 def view_hub_bwd(v, rs, gC, bC, Wv, gA, bA, Wa, t, Wr, dsv, dxr, dxl, dacc, part, scratch, dres=None):

@@ -40,6 +40,14 @@ FP32_GEMM = os.environ.get("GASFM_VIEW_GEMM", "torch")
 # batch's ~60) go to csrc/gemm_smallm.hip (1,024 waves of 16 x 32 tiles x K-quarters) instead of
 # hipBLASLt, whose 125 x 1024 x 1024 tiles take ~11.5 us; 0 disables
 SMALLM_ROWS = int(os.environ.get("GASFM_SMALLM_ROWS", "256"))
+# fp32 camera sides of at most 256 rows (view_chain_ok) run as csrc/view_chain.hip: the D x D GEMMs
+# with the view kernels as their prologues / epilogues, 2 launches forward and 4 backward per block
+# (round 3: 7 and 10); GASFM_VIEW_CHAIN=0 keeps the separate view kernels + GEMMs
+VIEW_CHAIN = os.environ.get("GASFM_VIEW_CHAIN", "1") != "0"
+
+
+def _chain_ok(m, D, bf16):
+    return VIEW_CHAIN and not bf16 and FP32_GEMM == "torch" and m > 0 and _native.view_chain_ok(m, D)
 
 
 def _mm(a, b, cin=None, bias=None, bf16=False, out=None):
@@ -69,12 +77,18 @@ class ViewTailFn(torch.autograd.Function):
         prev = prev.contiguous() if prev is not None else None
         Wp, Wm = Wp.contiguous(), Wm.contiguous()
         m, D = agg.shape[0], Wp.shape[0]
-        x, xb, h = _f32(m, D, like=agg), _f32(m, D, like=agg), _f32(m, D, like=agg)
+        x, h = _f32(m, D, like=agg), _f32(m, D, like=agg)
         rs = _f32(m, 2, like=agg)
-        _native.view_tail_fwd(prev, agg, Wp, bp, ln_w, ln_b, eps, bm, x, xb, h, rs,
-                              _native.view_scratch(m, D, agg.device))
-        # xb + h Wm^T accumulated in place (torch's addmm with a separate input first copies it)
-        view = _mm(h, Wm.t(), cin=xb, bf16=bf16, out=xb)
+        ctx.chain = _chain_ok(m, D, bf16)
+        if ctx.chain:
+            view = _f32(m, D, like=agg)
+            _native.view_chain_tail_fwd(prev, agg, Wp, bp, ln_w, ln_b, eps, Wm, bm, view, x, h, rs)
+        else:
+            xb = _f32(m, D, like=agg)
+            _native.view_tail_fwd(prev, agg, Wp, bp, ln_w, ln_b, eps, bm, x, xb, h, rs,
+                                  _native.view_scratch(m, D, agg.device))
+            # xb + h Wm^T accumulated in place (torch's addmm with a separate input first copies it)
+            view = _mm(h, Wm.t(), cin=xb, bf16=bf16, out=xb)
         ctx.save_for_backward(agg, x, rs, h, Wp, ln_w, ln_b, Wm)
         ctx.eps, ctx.has_prev, ctx.bf16 = eps, prev is not None, bf16
         ctx.defer = _native.defer_token(Wp, bp, ln_w, ln_b, bm)
@@ -85,6 +99,15 @@ class ViewTailFn(torch.autograd.Function):
         agg, x, rs, h, Wp, ln_w, ln_b, Wm = ctx.saved_tensors
         m, D = x.shape
         dview = dview.contiguous()
+        if ctx.chain:
+            dh, dx, dagg = _f32(m, D, like=x), _f32(m, D, like=x), _f32(m, A_W, like=x)
+            dWm = torch.empty_like(Wm)
+            part = _f32((m + TR - 1) // TR, _native.view_tail_part_cols(D), like=x)
+            _native.view_chain_tail_bwd(dview, x, h, rs, agg, Wp, ln_w, ln_b, Wm, dh, dWm, dx, dagg, part)
+            tot = _native.param_colsum(part, ctx.defer)
+            dWp = tot[:D * A_W].view(D, A_W)
+            dbp, dg, dbt, dbm = (tot[D * A_W + k * D:D * A_W + (k + 1) * D] for k in range(4))
+            return (dx if ctx.has_prev else None), dagg, dWp, dbp, dg, dbt, dWm, dbm, None, None
         dh = _mm(dview, Wm, bf16=ctx.bf16)
         dWm = _mm(dview.t(), h, bf16=ctx.bf16)
         dx, dagg = _f32(m, D, like=x), _f32(m, A_W, like=x)
@@ -118,9 +141,14 @@ class ViewHubFn(torch.autograd.Function):
         else:
             SV, XR = _f32(m, A_W, like=v), _f32(m, A_W, like=v)
         rs = _f32(m, 2, like=v)
-        _native.view_hub_fwd(v, eps, gC, bC, Wv, gA, bA, Wa, ba, Wr, br, SV, t, XR, rs,
-                             _native.view_scratch(m, v.shape[1], v.device))
-        XL = _mm(v, Wl.t(), bias=bl, bf16=bf16)
+        ctx.chain = _chain_ok(m, v.shape[1], bf16)
+        if ctx.chain:
+            XL = _f32(m, Wl.shape[0], like=v)
+            _native.view_chain_hub_fwd(v, eps, Wl, bl, gC, bC, Wv, gA, bA, Wa, ba, Wr, br, XL, SV, t, XR, rs)
+        else:
+            _native.view_hub_fwd(v, eps, gC, bC, Wv, gA, bA, Wa, ba, Wr, br, SV, t, XR, rs,
+                                 _native.view_scratch(m, v.shape[1], v.device))
+            XL = _mm(v, Wl.t(), bias=bl, bf16=bf16)
         ctx.save_for_backward(v, rs, t, gC, bC, Wv, Wl, gA, bA, Wa, Wr)
         ctx.eps, ctx.bf16 = eps, bf16
         ctx.defer = _native.defer_token(gC, bC, Wv, gA, bA, Wa, ba, Wr, br, bl)
@@ -136,20 +164,27 @@ class ViewHubFn(torch.autograd.Function):
         dXR = dXR.contiguous() if dXR is not None else zeros(A_W)
         dXL = dXL.contiguous() if dXL is not None else zeros(D)
         dres = None
-        if ctx.bf16 or FP32_GEMM == "hip":  # the MFMA kernels add d skip in their epilogue
+        if ctx.chain:
+            dacc, dWl = _f32(m, D, like=v), torch.empty_like(Wl)
+            part = _f32((m + TR - 1) // TR, _native.view_hub_part_cols(D), like=v)
+            _native.view_chain_hub_bwd(v, rs, gC, bC, Wv, gA, bA, Wa, t, Wr, Wl, dSV, dXR, dXL,
+                                       dskip.contiguous() if dskip is not None else None, dacc, dWl, part)
+            tot = _native.param_colsum(part, ctx.defer)
+        elif ctx.bf16 or FP32_GEMM == "hip":  # the MFMA kernels add d skip in their epilogue
             dacc = _mm(dXL, Wl, cin=dskip.contiguous() if dskip is not None else None, bf16=ctx.bf16)
         else:  # hipBLASLt: d skip is added by the hub kernel's second pass (no addmm input copy)
             dacc = _mm(dXL, Wl)
             dres = dskip.contiguous() if dskip is not None else None
-        dWl = _mm(dXL.t(), v, bf16=ctx.bf16)
-        cols = _native.view_hub_part_cols(D)
-        if m == 0:
-            tot = torch.zeros(cols, dtype=torch.float32, device=v.device)
-        else:
-            part = _f32((m + TR - 1) // TR, cols, like=v)
-            _native.view_hub_bwd(v, rs, gC, bC, Wv, gA, bA, Wa, t, Wr, dSV, dXR, dXL, dacc, part,
-                                 _native.view_scratch(m, D, v.device), dres=dres)
-            tot = _native.param_colsum(part, ctx.defer)
+        if not ctx.chain:
+            dWl = _mm(dXL.t(), v, bf16=ctx.bf16)
+            cols = _native.view_hub_part_cols(D)
+            if m == 0:
+                tot = torch.zeros(cols, dtype=torch.float32, device=v.device)
+            else:
+                part = _f32((m + TR - 1) // TR, cols, like=v)
+                _native.view_hub_bwd(v, rs, gC, bC, Wv, gA, bA, Wa, t, Wr, dSV, dXR, dXL, dacc, part,
+                                     _native.view_scratch(m, D, v.device), dres=dres)
+                tot = _native.param_colsum(part, ctx.defer)
         o = 0
         dWv = tot[o:o + A_W * D].view(A_W, D)
         o += A_W * D

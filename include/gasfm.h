@@ -563,6 +563,38 @@ int gasfm_view_hub_bwd(const float* v, const float* rs, int64_t m, int32_t D, co
                        const float* Wr, const float* dsv, const float* dxr, const float* dxl, const float* dres,
                        float* dacc, float* part, float* scratch, void* stream);
 
+/* ---- the camera side for SMALL row counts (view_chain.hip, round 4) ----
+ * A camera-sharded rank's own rows (m / W) or a training batch's cameras: the same arithmetic as
+ * gasfm_view_tail_* / gasfm_view_hub_* plus the D x D products they leave to a GEMM (Proj2View's
+ * mlp, layers.py:345-360; graph_conv_view2global.lin_l, layers.py:551-556), with the GEMMs carrying
+ * the view kernels as prologue / epilogue: 2 launches forward, 4 backward per block.  Applies
+ * when gasfm_view_chain_ok(m, D): m <= 256, D in {256, 512, 1024}.  Parameter partial rows use
+ * the gasfm_view_tail_part_cols / gasfm_view_hub_part_cols layouts. */
+int32_t gasfm_view_chain_ok(int64_t m, int32_t D);
+int64_t gasfm_view_chain_scratch_floats(int64_t m, int32_t D);
+int32_t gasfm_view_chain_counters(int64_t m);
+/* view = x + bm + relu(LN(x)) Wm^T, x = prev + agg Wp^T + bp; saves x, h = relu(LN(x)), rs. */
+int gasfm_view_chain_tail_fwd(const float* prev, const float* agg, int64_t m, int32_t D, const float* Wp,
+                              const float* bp, const float* ln_w, const float* ln_b, float eps, const float* Wm,
+                              const float* bm, float* view, float* x, float* h, float* rs, void* stream);
+/* XL = v Wl^T + bl; sv = relu(LN_c v) Wv^T; t = relu(LN_a v) Wa^T + ba; xr = t Wr^T + br (sv / xr
+ * row stride ldo); rs = row (mean, rstd) of v. */
+int gasfm_view_chain_hub_fwd(const float* v, int64_t m, int32_t D, float eps, const float* Wl, const float* bl,
+                             const float* gC, const float* bC, const float* Wv, const float* gA, const float* bA,
+                             const float* Wa, const float* ba, const float* Wr, const float* br, float* XL, float* sv,
+                             float* t, float* xr, int32_t ldo, float* rs, void* stream);
+/* dacc = d v = dres + dxl Wl + LN_c_bwd(mask dsv Wv) + LN_a_bwd(mask (dxr Wr) Wa); dWl = dxl^T v;
+ * the other parameter gradients as partial rows. */
+int gasfm_view_chain_hub_bwd(const float* v, const float* rs, int64_t m, int32_t D, const float* gC, const float* bC,
+                             const float* Wv, const float* gA, const float* bA, const float* Wa, const float* t,
+                             const float* Wr, const float* Wl, const float* dsv, const float* dxr, const float* dxl,
+                             const float* dres, float* dacc, float* dWl, float* part, float* scratch, void* stream);
+/* dh = dv Wm, dWm = dv^T h, dx = dv + LN_bwd(mask dh) (= d prev), dagg = dx Wp; partial rows. */
+int gasfm_view_chain_tail_bwd(const float* dv, const float* x, const float* h, const float* rs, const float* agg,
+                              int64_t m, int32_t D, const float* Wp, const float* ln_w, const float* ln_b,
+                              const float* Wm, float* dh, float* dWm, float* dx, float* dagg, float* part,
+                              float* scratch, uint32_t* counters, void* stream);
+
 /* Batched single-row problems in ONE launch each way (the global hub: the LayerNorm -> Linear
  * consumers of a block's global row, then the two lin_r rows).  Arrays of nprob (<= 4) entries,
  * one per problem, as for gasfm_gvec_fwd / gasfm_gvec_bwd; null entries mean "absent" where the
