@@ -112,12 +112,12 @@ _SIGS = {
     "gasfm_view_chain_tail_fwd": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _vp,
                                          _vp]),
     "gasfm_view_chain_hub_fwd": (_i32, [_vp, _i64, _i32, _f32] + [_vp] * 15 + [_i32, _vp, _vp]),
-    "gasfm_view_chain_hub_bwd": (_i32, [_vp, _vp, _i64, _i32] + [_vp] * 17),
+    "gasfm_view_chain_hub_bwd": (_i32, [_vp, _vp, _i64, _i32] + [_vp] * 18),
     "gasfm_view_chain_tail_bwd": (_i32, [_vp] * 5 + [_i64, _i32] + [_vp] * 12),
     "gasfm_gchain_fwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_gchain_scratch_floats": (_i64, [_vp]),
     "gasfm_gchain_counters": (_i32, [_vp]),
-    "gasfm_gchain_bwd": (_i32, [_vp] * 17),
+    "gasfm_gchain_bwd": (_i32, [_vp] * 16),
     "gasfm_pose_fwd": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "gasfm_pose_bwd": (_i32, [_vp, _i64, _i64, _vp, _vp, _i64, _vp]),
     "gasfm_esfm_part_rows": (_i32, [_i64]),

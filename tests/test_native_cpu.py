@@ -189,3 +189,19 @@ def test_lazy_graph_wrappers_and_scene_csr():
         raise AssertionError("expected AttributeError")
     except AttributeError:
         pass
+
+
+def test_binding_arity_matches_header():
+    """Every ctypes signature in _native._SIGS has as many parameters as its declaration in
+    include/gasfm.h (a short argtypes list fails only at call time, on the GPU)."""
+    import re
+    text = re.sub(r"/\*.*?\*/", "", open(os.path.join(REPO, "include", "gasfm.h")).read(), flags=re.S)
+    bad = []
+    for m in re.finditer(r"\b(gasfm_\w+)\s*\(([^;{]*?)\)\s*;", text):
+        name, args = m.group(1), m.group(2).strip()
+        if name not in _native._SIGS:
+            continue
+        n = 0 if args in ("", "void") else args.count(",") + 1
+        if n != len(_native._SIGS[name][1]):
+            bad.append((name, n, len(_native._SIGS[name][1])))
+    assert not bad, bad
