@@ -21,10 +21,12 @@
 //               through stores, one relaxed agent-scope ticket per slab: reduce.hip's hand-off),
 //               which sums them in chunk order: dh leaves FINAL, no finish launch.  The LayerNorm
 //               backward that follows a level (F3's LN_A/B/C into dg, F2's LN_M into dx1) needs
-//               row sums over the whole vector, so the NEXT level's workgroups each recompute it
-//               from the raw dh vectors ("finish" prologue) -- redundantly, while their own W
-//               slab is in flight -- and one designated workgroup writes the finished vector and
-//               the LayerNorm gamma / beta gradients.
+//               row sums over the whole vector: the level's LAST workgroup (a second ticket, over
+//               every slab of the launch) runs it once -- every load issued before the first use,
+//               one reduction round for all the LayerNorms -- and writes the finished vector and
+//               the LayerNorm gamma / beta gradients; the next level reads a plain dy.
+//   Every phase issues all of its global loads before the first use (clamped addresses): a load
+//   behind a branch or behind a store to a possibly-aliasing pointer costs a full round trip.
 // No float atomics; every sum has a fixed order: deterministic, identical on every rank.
 #include <hip/hip_runtime.h>
 
@@ -128,7 +130,8 @@ __global__ __launch_bounds__(kFT) void gnode_fwd_kernel(GnFwdArgs a) {
   const int K = p.K;
   const int i = (int(blockIdx.x) - p.blk0) * (kFT / 64) + wave;
   const int ic = i < p.N ? i : p.N - 1;
-  // the wave's W row first (clamped in-range addresses; lanes past K multiply h = 0 below)
+  // every load of the kernel first: the wave's W row, the input row and its LayerNorm affine
+  // (clamped in-range addresses; values past K are zeroed where consumed)
   float4 w[KI];
   const float* wr = p.W + int64_t(ic) * K;
 #pragma unroll
@@ -136,22 +139,31 @@ __global__ __launch_bounds__(kFT) void gnode_fwd_kernel(GnFwdArgs a) {
     const int j = 4 * lane + 256 * u;
     w[u] = *reinterpret_cast<const float4*>(wr + (j < K ? j : 0));
   }
-  float xv[kPer];
-  load_row(p.x, K, xv);
-  if (p.gam) {
+  const bool ln = p.gam != nullptr;
+  const float* gp = ln ? p.gam : p.x;
+  const float* bp = ln ? p.bet : p.x;
+  float xv[kPer], gv[kPer], bv[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int j = int(threadIdx.x) + 256 * u, jc = j < K ? j : 0;
+    xv[u] = p.x[jc];
+    gv[u] = gp[jc];
+    bv[u] = bp[jc];
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; ++u)
+    if (int(threadIdx.x) + 256 * u >= K) xv[u] = 0.f;
+  if (ln) {
     float mean, rstd;
     row_stats(xv, K, p.eps, scratch, mean, rstd);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int j = int(threadIdx.x) + 256 * u;
-      if (j < kMaxK) h[j] = j < K ? fmaxf(fmaf((xv[u] - mean) * rstd, p.gam[j], p.bet[j]), 0.f) : 0.f;
+      h[j] = j < K ? fmaxf(fmaf((xv[u] - mean) * rstd, gv[u], bv[u]), 0.f) : 0.f;
     }
   } else {
 #pragma unroll
-    for (int u = 0; u < kPer; ++u) {
-      const int j = int(threadIdx.x) + 256 * u;
-      if (j < kMaxK) h[j] = xv[u];
-    }
+    for (int u = 0; u < kPer; ++u) h[int(threadIdx.x) + 256 * u] = xv[u];
   }
   __syncthreads();
   float acc = 0.f;
@@ -188,7 +200,7 @@ int launch_fwd(GnFwdArgs& a, hipStream_t st) {
 
 // --------------------------------------------------------------------------------- backward
 struct GnBwdProb {
-  const float* dy;   // [N] plain output gradient (null: the level's finish vector)
+  const float* dy;   // [N] output gradient (final)
   const float* x;    // [K] forward input row
   const float* gam;  // [K] LayerNorm of x (null: h = x)
   const float* bet;
@@ -201,7 +213,9 @@ struct GnBwdProb {
   int K, N, blk0, slabs, chunks;
   float eps;
 };
-// dy = dres + sum_q LN_q backward of raw_q (relu mask), LN_q over the row x [F]
+// Run by the launch's last workgroup once every dh is final:
+//   out = dres + sum_q LN_q backward of raw_q (relu mask), LN_q over the row x [F]
+// (raw_q: dh of problem q of this launch), plus the LayerNorms' gamma / beta gradients.
 struct GnFinish {
   const float* x;
   const float* dres;
@@ -210,8 +224,9 @@ struct GnFinish {
   const float* bet[kMaxRaw];
   float* dgam[kMaxRaw];
   float* dbet[kMaxRaw];
-  float* out;  // [F] the finished vector (designated workgroup), or null
-  int F, nraw;
+  float* out;
+  uint32_t* cnt;  // the launch's ticket (null: no finish)
+  int F, nraw, slabs;
   float eps;
 };
 struct GnBwdArgs {
@@ -227,10 +242,69 @@ __device__ __forceinline__ void st_sc1(float* p, float4 v) {
   __hip_atomic_store(reinterpret_cast<uint64_t*>(p), a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(reinterpret_cast<uint64_t*>(p) + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the launch's finish (one workgroup, F <= kMaxK): every load first, one reduction round for all
+// the LayerNorms' row sums
+__device__ void gnode_finish(const GnFinish& f, float* scratch) {
+  const int F = f.F;
+  float xv[kPer], acc[kPer], raw[kMaxRaw][kPer], ga[kMaxRaw][kPer], be[kMaxRaw][kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int j = int(threadIdx.x) + 256 * u, jc = j < F ? j : 0;
+    xv[u] = f.x[jc];
+    acc[u] = f.dres ? f.dres[jc] : 0.f;
+#pragma unroll
+    for (int q = 0; q < kMaxRaw; ++q) {
+      const bool on = q < f.nraw;
+      raw[q][u] = on ? ld_sc1(f.raw[q] + jc) : 0.f;
+      ga[q][u] = on ? f.gam[q][jc] : 0.f;
+      be[q][u] = on ? f.bet[q][jc] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; ++u)
+    if (int(threadIdx.x) + 256 * u >= F) xv[u] = 0.f;
+  float mean, rstd;
+  row_stats(xv, F, f.eps, scratch, mean, rstd);
+  float xh[kPer], sv[2 * kMaxRaw];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) xh[u] = (xv[u] - mean) * rstd;
+#pragma unroll
+  for (int q = 0; q < kMaxRaw; ++q) {
+    sv[2 * q] = sv[2 * q + 1] = 0.f;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int j = int(threadIdx.x) + 256 * u;
+      const float d = (j < F && q < f.nraw && fmaf(xh[u], ga[q][u], be[q][u]) > 0.f) ? raw[q][u] : 0.f;
+      if (j < F && q < f.nraw) {
+        f.dgam[q][j] = d * xh[u];
+        f.dbet[q][j] = d;
+      }
+      raw[q][u] = d * ga[q][u];  // now gv
+      sv[2 * q] += raw[q][u];
+      sv[2 * q + 1] = fmaf(raw[q][u], xh[u], sv[2 * q + 1]);
+    }
+  }
+  block_sums<2 * kMaxRaw>(sv, scratch);
+#pragma unroll
+  for (int q = 0; q < kMaxRaw; ++q) {
+    if (q >= f.nraw) continue;
+    const float s1 = sv[2 * q] / F, s2 = sv[2 * q + 1] / F;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) acc[u] += rstd * (raw[q][u] - s1 - xh[u] * s2);
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int j = int(threadIdx.x) + 256 * u;
+    if (j < F) f.out[j] = acc[u];
+  }
+}
 
 template <int RPT>  // rows per thread: a chunk is 32 RPT rows
 __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) float dfull[kMaxK];  // the finished dy (finish levels)
   __shared__ float dys[32 * RPT];
   __shared__ float4 red[kBT];
   __shared__ float scratch[4 * 2 * kMaxRaw + 8];
@@ -246,95 +320,52 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
   const int K = p.K, N = p.N;
   const int col = slab * kSW + 4 * cl;
   const int row0 = chunk * 32 * RPT;
-  // 1. this workgroup's W slab rows, in flight through the prologues
+  // 1. every load first: the workgroup's W slab rows, the chunk's dy, the input row (+ affine)
   float4 w[RPT];
 #pragma unroll
   for (int r = 0; r < RPT; ++r) {
     const int n = row0 + rl + 32 * r;
     w[r] = *reinterpret_cast<const float4*>(p.W + int64_t(n < N ? n : N - 1) * K + col);
   }
-  // 2. dy of the chunk's rows
-  const bool designated = pi == 0 && local == 0;
-  if (p.dy) {
-    for (int t = threadIdx.x; t < 32 * RPT; t += kBT) dys[t] = row0 + t < N ? p.dy[row0 + t] : 0.f;
-  } else {
-    const GnFinish& f = a.f;
-    const int F = f.F;
-    float xv[kPer], acc[kPer];
-    load_row(f.x, F, xv);
-    if (f.dres)
-      load_row(f.dres, F, acc);
-    else
+  float dyv[(32 * RPT + kBT - 1) / kBT];
 #pragma unroll
-      for (int u = 0; u < kPer; ++u) acc[u] = 0.f;
-    float mean, rstd;
-    row_stats(xv, F, f.eps, scratch, mean, rstd);
-    float xh[kPer];
-#pragma unroll
-    for (int u = 0; u < kPer; ++u) xh[u] = (xv[u] - mean) * rstd;
-    float gv[kMaxRaw][kPer], sv[2 * kMaxRaw];
-#pragma unroll
-    for (int q = 0; q < kMaxRaw; ++q) {
-      sv[2 * q] = sv[2 * q + 1] = 0.f;
-#pragma unroll
-      for (int u = 0; u < kPer; ++u) gv[q][u] = 0.f;
-      if (q >= f.nraw) continue;
-#pragma unroll
-      for (int u = 0; u < kPer; ++u) {
-        const int j = int(threadIdx.x) + 256 * u;
-        if (j < F) {
-          const float ga = f.gam[q][j];
-          const float d = fmaf(xh[u], ga, f.bet[q][j]) > 0.f ? f.raw[q][j] : 0.f;
-          if (designated) {
-            f.dgam[q][j] = d * xh[u];
-            f.dbet[q][j] = d;
-          }
-          gv[q][u] = d * ga;
-          sv[2 * q] += gv[q][u];
-          sv[2 * q + 1] = fmaf(gv[q][u], xh[u], sv[2 * q + 1]);
-        }
-      }
-    }
-    block_sums<2 * kMaxRaw>(sv, scratch);
-#pragma unroll
-    for (int q = 0; q < kMaxRaw; ++q) {
-      if (q >= f.nraw) continue;
-      const float s1 = sv[2 * q] / F, s2 = sv[2 * q + 1] / F;
-#pragma unroll
-      for (int u = 0; u < kPer; ++u) acc[u] += rstd * (gv[q][u] - s1 - xh[u] * s2);
-    }
+  for (int k = 0; k < (32 * RPT + kBT - 1) / kBT; ++k) {
+    const int t = int(threadIdx.x) + k * kBT, n = row0 + t;
+    dyv[k] = p.dy[n < N ? n : N - 1];
+  }
+  const float4 x4 = *reinterpret_cast<const float4*>(p.x + col);
+  const bool ln = p.gam != nullptr;
+  float4 g4 = x4, b4 = x4;
+  float xv[kPer];
+  if (ln) {
+    g4 = *reinterpret_cast<const float4*>(p.gam + col);
+    b4 = *reinterpret_cast<const float4*>(p.bet + col);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int j = int(threadIdx.x) + 256 * u;
-      if (j < F) {
-        dfull[j] = acc[u];
-        if (designated && f.out) f.out[j] = acc[u];
-      }
+      xv[u] = p.x[j < K ? j : 0];
     }
-    __syncthreads();
-    for (int t = threadIdx.x; t < 32 * RPT; t += kBT) dys[t] = row0 + t < N ? dfull[row0 + t] : 0.f;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u)
+      if (int(threadIdx.x) + 256 * u >= K) xv[u] = 0.f;
   }
-  // 3. h over the slab's 4 columns of this thread
-  float4 h4;
-  {
-    const float4 x4 = *reinterpret_cast<const float4*>(p.x + col);
-    if (p.gam) {
-      float xv[kPer];
-      load_row(p.x, K, xv);
-      float mean, rstd;
-      row_stats(xv, K, p.eps, scratch, mean, rstd);
-      const float4 g4 = *reinterpret_cast<const float4*>(p.gam + col);
-      const float4 b4 = *reinterpret_cast<const float4*>(p.bet + col);
-      h4 = make_float4(fmaxf(fmaf((x4.x - mean) * rstd, g4.x, b4.x), 0.f),
-                       fmaxf(fmaf((x4.y - mean) * rstd, g4.y, b4.y), 0.f),
-                       fmaxf(fmaf((x4.z - mean) * rstd, g4.z, b4.z), 0.f),
-                       fmaxf(fmaf((x4.w - mean) * rstd, g4.w, b4.w), 0.f));
-    } else {
-      h4 = x4;
-    }
+#pragma unroll
+  for (int k = 0; k < (32 * RPT + kBT - 1) / kBT; ++k) {
+    const int t = int(threadIdx.x) + k * kBT;
+    if (t < 32 * RPT) dys[t] = row0 + t < N ? dyv[k] : 0.f;
+  }
+  // 2. h over the thread's 4 slab columns
+  float4 h4 = x4;
+  if (ln) {
+    float mean, rstd;
+    row_stats(xv, K, p.eps, scratch, mean, rstd);
+    h4 = make_float4(fmaxf(fmaf((x4.x - mean) * rstd, g4.x, b4.x), 0.f),
+                     fmaxf(fmaf((x4.y - mean) * rstd, g4.y, b4.y), 0.f),
+                     fmaxf(fmaf((x4.z - mean) * rstd, g4.z, b4.z), 0.f),
+                     fmaxf(fmaf((x4.w - mean) * rstd, g4.w, b4.w), 0.f));
   }
   __syncthreads();  // dys
-  // 4. dW rows and this thread's share of dh
+  // 3. dW rows and this thread's share of dh
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int r = 0; r < RPT; ++r) {
@@ -350,7 +381,7 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
   if (p.db && slab == 0)
     for (int t = threadIdx.x; t < 32 * RPT; t += kBT)
       if (row0 + t < N) p.db[row0 + t] = dys[t];
-  // 5. the 32 row lanes summed in lane order
+  // 4. the 32 row lanes summed in lane order
   red[threadIdx.x] = s;
   __syncthreads();
   float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -364,29 +395,59 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
       tot.w += v.w;
     }
   }
-  if (p.chunks == 1) {
-    if (threadIdx.x < 8) *reinterpret_cast<float4*>(p.dh + col) = tot;
-    return;
+  const bool fin = a.f.cnt != nullptr;
+  if (p.chunks > 1) {
+    // 5. the chunk partial to the slab's last arriver (write-through stores, one ticket)
+    if (threadIdx.x < 8) st_sc1(p.ws + int64_t(chunk) * K + col, tot);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t t = __hip_atomic_fetch_add(p.cnt + slab, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag = t == uint32_t(p.chunks - 1) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (flag == 0u) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (threadIdx.x < 8) {
+      constexpr int MAXC = 16;
+      float4 v[MAXC];
+#pragma unroll
+      for (int ch = 0; ch < MAXC; ++ch) {
+        const float* q = p.ws + int64_t(ch < p.chunks ? ch : 0) * K + col;
+        v[ch] = make_float4(ld_sc1(q), ld_sc1(q + 1), ld_sc1(q + 2), ld_sc1(q + 3));
+      }
+      tot = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int ch = 0; ch < MAXC; ++ch)
+        if (ch < p.chunks) {
+          tot.x += v[ch].x;
+          tot.y += v[ch].y;
+          tot.z += v[ch].z;
+          tot.w += v[ch].w;
+        }
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(p.cnt + slab, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // 6. hand the chunk partial to the slab's last arriver (write-through stores, one ticket)
-  if (threadIdx.x < 8) st_sc1(p.ws + int64_t(chunk) * K + col, tot);
+  // 6. the slab's final dh (write-through when the launch's finish reads it)
+  if (threadIdx.x < 8) {
+    if (fin)
+      st_sc1(p.dh + col, tot);
+    else
+      *reinterpret_cast<float4*>(p.dh + col) = tot;
+  }
+  if (!fin) return;
+  // 7. the launch's last slab runs the finish
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t t = __hip_atomic_fetch_add(p.cnt + slab, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag = t == uint32_t(p.chunks - 1) ? 1u : 0u;
+    const uint32_t t = __hip_atomic_fetch_add(a.f.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = t == uint32_t(a.f.slabs - 1) ? 1u : 0u;
   }
   __syncthreads();
   if (flag == 0u) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (threadIdx.x < kSW) {
-    const int c = slab * kSW + int(threadIdx.x);
-    float acc = 0.f;
-    for (int ch = 0; ch < p.chunks; ++ch)
-      acc += __hip_atomic_load(p.ws + int64_t(ch) * K + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    p.dh[c] = acc;
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(p.cnt + slab, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  gnode_finish(a.f, scratch);
+  if (threadIdx.x == 0) __hip_atomic_store(a.f.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 constexpr int kRPT = 8;  // 256 rows per chunk
@@ -408,6 +469,11 @@ int launch_bwd(GnBwdArgs& a, float*& ws, uint32_t*& cnt, hipStream_t st, const c
     blocks += p.slabs * p.chunks;
   }
   for (int q = a.nprob; q < kMaxProb; ++q) a.p[q].blk0 = blocks;
+  if (a.f.nraw > 0) {
+    a.f.cnt = cnt++;
+    a.f.slabs = 0;
+    for (int q = 0; q < a.nprob; ++q) a.f.slabs += a.p[q].slabs;
+  }
   hipLaunchKernelGGL(gnode_bwd_kernel<kRPT>, dim3(blocks), dim3(kBT), 0, st, a);
   return launch_status(where);
 }
@@ -452,7 +518,7 @@ extern "C" int64_t gasfm_gchain_scratch_floats(const gasfm_gchain* c) {
 
 extern "C" int32_t gasfm_gchain_counters(const gasfm_gchain* c) {
   if (!c) return 0;
-  return (c->NB + c->NC + 4 * c->G + c->Kc) / kSW + 8;
+  return (c->NB + c->NC + 4 * c->G + c->Kc) / kSW + 8;  // per-slab tickets + one per finishing level
 }
 
 extern "C" int gasfm_gchain_fwd(const gasfm_gchain* c, const float* xcat, const float* prev, float* x1, float* g,
@@ -517,7 +583,8 @@ extern "C" int gasfm_gchain_bwd(const gasfm_gchain* c, const float* xcat, const 
     s = launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(lin_r)");
     if (s != GASFM_OK) return s;
   }
-  {  // B2: the LayerNorm -> Linear consumers of g (raw dh, LayerNorm backward deferred)
+  {  // B2: the LayerNorm -> Linear consumers of g; its last workgroup finishes dg = dskip + their
+     // LayerNorm backwards (and the LayerNorms' gamma / beta gradients)
     GnBwdArgs a{};
     a.nprob = hub ? 3 : 1;
     a.p[0] = GnBwdProb{dsg, g, c->gA, c->bA, c->WA, d->dWA, nullptr, dhA, nullptr, nullptr, c->G, c->NA};
@@ -527,14 +594,6 @@ extern "C" int gasfm_gchain_bwd(const gasfm_gchain* c, const float* xcat, const 
       a.p[2] = GnBwdProb{dhE, g, c->gC, c->bC, c->WC, d->dWC, d->dbWC, dhC, nullptr, nullptr, c->G, c->NC};
       a.p[1].eps = a.p[2].eps = c->eps_h;
     }
-    s = launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(hub)");
-    if (s != GASFM_OK) return s;
-  }
-  {  // B3: dg = dskip + LN_A/B/C backward (every workgroup), then the MLP Linear
-    GnBwdArgs a{};
-    a.nprob = 1;
-    a.p[0] = GnBwdProb{nullptr, x1, c->gM, c->bM, c->W2, d->dW2, d->db2, dh2, nullptr, nullptr, c->G, c->G};
-    a.p[0].eps = c->eps_m;
     GnFinish& f = a.f;
     f.x = g;
     f.dres = dskip;
@@ -547,20 +606,28 @@ extern "C" int gasfm_gchain_bwd(const gasfm_gchain* c, const float* xcat, const 
       f.raw[2] = dhC, f.gam[2] = c->gC, f.bet[2] = c->bC, f.dgam[2] = d->dgC, f.dbet[2] = d->dbC;
     }
     f.out = dg;
+    s = launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(hub)");
+    if (s != GASFM_OK) return s;
+  }
+  {  // B3: the MLP Linear on dg; its last workgroup finishes dx1 = dg + LN_M backward
+    GnBwdArgs a{};
+    a.nprob = 1;
+    a.p[0] = GnBwdProb{dg, x1, c->gM, c->bM, c->W2, d->dW2, d->db2, dh2, nullptr, nullptr, c->G, c->G};
+    a.p[0].eps = c->eps_m;
+    GnFinish& f = a.f;
+    f.x = x1;
+    f.dres = dg;
+    f.F = c->G;
+    f.eps = c->eps_m;
+    f.nraw = 1;
+    f.raw[0] = dh2, f.gam[0] = c->gM, f.bet[0] = c->bM, f.dgam[0] = d->dgM, f.dbet[0] = d->dbM;
+    f.out = dx1;
     s = launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(mlp)");
     if (s != GASFM_OK) return s;
   }
-  // B4: dx1 = dg + LN_M backward (every workgroup), then proj_view_and_scenepoint2global
+  // B4: proj_view_and_scenepoint2global on dx1 (= d prev): d xcat
   GnBwdArgs a{};
   a.nprob = 1;
-  a.p[0] = GnBwdProb{nullptr, xcat, nullptr, nullptr, c->W1, d->dW1, d->db1, dxcat, nullptr, nullptr, c->Kc, c->G};
-  GnFinish& f = a.f;
-  f.x = x1;
-  f.dres = dg;
-  f.F = c->G;
-  f.eps = c->eps_m;
-  f.nraw = 1;
-  f.raw[0] = dh2, f.gam[0] = c->gM, f.bet[0] = c->bM, f.dgam[0] = d->dgM, f.dbet[0] = d->dbM;
-  f.out = dx1;
+  a.p[0] = GnBwdProb{dx1, xcat, nullptr, nullptr, c->W1, d->dW1, d->db1, dxcat, nullptr, nullptr, c->Kc, c->G};
   return launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(proj)");
 }

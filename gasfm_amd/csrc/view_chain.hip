@@ -752,111 +752,168 @@ __device__ __forceinline__ void st_sc1(float* p, float v) {
 }
 
 // dx[:, cols] = dv + rstd (gv - S1 - x_hat S2) (= d prev), the tile's dWp / dbp column partials,
-// and d agg = dx Wp: each (tile, column block) writes its 16 x 32 partial; the tile's last-arriving
-// workgroup sums them in column-block order.  One workgroup (1 wave) per (tile, 32 columns).
-__global__ __launch_bounds__(kWv) void vc_tail_bwd2_kernel(const float* __restrict__ dv, const float* __restrict__ dh,
-                                                           const float* __restrict__ x, const float2* __restrict__ rsx,
-                                                           const float* __restrict__ agg, int64_t m, int D,
-                                                           const float* __restrict__ gam,
-                                                           const float* __restrict__ bet, const float* __restrict__ Wp,
-                                                           const float2* __restrict__ RSUMT, float* __restrict__ dx,
-                                                           float* __restrict__ dagg, float* __restrict__ ws,
-                                                           uint32_t* __restrict__ cnt, float* __restrict__ part) {
-  __shared__ float DX[TR][CW + 1], AG[TR][VA + 1];
+// and d agg = dx Wp.  A workgroup (4 waves) per (tile, 128 columns), wave w one 32-column block;
+// the waves' d agg partials are summed in LDS (wave order), the group partial handed to the tile's
+// last-arriving workgroup (write-through stores, one ticket), which sums the groups in order.
+// Every global load of a phase is issued before its first use (clamped rows, masked where used).
+constexpr int TB2_T = 256, TB2_W = TB2_T / kWv, TB2_COLS = TB2_W * CW;
+__global__ __launch_bounds__(TB2_T) void vc_tail_bwd2_kernel(const float* __restrict__ dv, const float* __restrict__ dh,
+                                                             const float* __restrict__ x,
+                                                             const float2* __restrict__ rsx,
+                                                             const float* __restrict__ agg, int64_t m, int D,
+                                                             const float* __restrict__ gam,
+                                                             const float* __restrict__ bet,
+                                                             const float* __restrict__ Wp,
+                                                             const float2* __restrict__ RSUMT, float* __restrict__ dx,
+                                                             float* __restrict__ dagg, float* __restrict__ ws,
+                                                             uint32_t* __restrict__ cnt, float* __restrict__ part) {
+  __shared__ float DX[TB2_W][TR][CW + 1], AG[TR][VA + 1], DA[TB2_W][TR * VA];
   __shared__ float S1[TR], S2[TR];
   __shared__ uint32_t flag;
-  const int lane = threadIdx.x, c = lane & 15, g = lane >> 4;
-  const Tile t = tile_of(blockIdx.x, m, D);
-  const int ncb = t.ncb;
-  float* out = part + int64_t(t.tile) * tail_cols(D);
-  if (lane < TR) {
-    float a = 0.f, b = 0.f;
-    if (lane < t.nrows)
-      for (int q = 0; q < ncb; ++q) {
-        const float2 p = RSUMT[(t.row0 + lane) * ncb + q];
-        a += p.x;
-        b += p.y;
-      }
-    S1[lane] = a / D;
-    S2[lane] = b / D;
-  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  const int ncb = D / CW, ngrp = D / TB2_COLS;
+  const int tile = blockIdx.x / ngrp, grp = blockIdx.x % ngrp;
+  const int64_t row0 = int64_t(tile) * TR;
+  const int nrows = int(m - row0 < TR ? m - row0 : TR);
+  const int col0 = grp * TB2_COLS + wave * CW;
+  float* out = part + int64_t(tile) * tail_cols(D);
+  // ---- every load first
+  float xv[2][4], hv[2][4], dvv[2][4], gv[2], bv[2];
+  float2 st[4];
+  float wpv[CW / 4][2];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int rr = 4 * g + r;
-    const int64_t rw = t.row0 + (rr < t.nrows ? rr : 0);
-    AG[rr][c] = rr < t.nrows ? agg[rw * VA + c] : 0.f;
-    AG[rr][16 + c] = rr < t.nrows ? agg[rw * VA + 16 + c] : 0.f;
-  }
-  __syncthreads();
+  for (int r = 0; r < 4; ++r) st[r] = rsx[row0 + (4 * g + r < nrows ? 4 * g + r : 0)];
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
-    const int cl = 16 * tt + c, col = t.col0 + cl;
-    const float gv = gam[col], bv = bet[col];
+    const int col = col0 + 16 * tt + c;
+    gv[tt] = gam[col];
+    bv[tt] = bet[col];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t e = (row0 + (4 * g + r < nrows ? 4 * g + r : 0)) * D + col;
+      xv[tt][r] = x[e];
+      hv[tt][r] = dh[e];
+      dvv[tt][r] = dv[e];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < CW / 4; ++q)
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) wpv[q][tt] = Wp[(col0 + 4 * q + g) * VA + 16 * tt + c];
+  {  // row sums of the LayerNorm backward: thread (row = tid >> 4, k = tid & 15) sums blocks k, k + 16, ..
+    const int row = int(threadIdx.x) >> 4, k = int(threadIdx.x) & 15;
+    const int64_t rw = row0 + (row < nrows ? row : 0);
+    float a = 0.f, b = 0.f;
+    for (int q = k; q < ncb; q += 16) {
+      const float2 p = RSUMT[rw * ncb + q];
+      a += p.x;
+      b += p.y;
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      a += __shfl_xor(a, o);
+      b += __shfl_xor(b, o);
+    }
+    if (k == 0) {
+      S1[row] = a / D;
+      S2[row] = b / D;
+    }
+  }
+  if (wave == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = 4 * g + r;
+      const int64_t rw = row0 + (rr < nrows ? rr : 0);
+      const float a0 = agg[rw * VA + c], a1 = agg[rw * VA + 16 + c];
+      AG[rr][c] = rr < nrows ? a0 : 0.f;
+      AG[rr][16 + c] = rr < nrows ? a1 : 0.f;
+    }
+  }
+  __syncthreads();
+  // ---- dx, its column partials
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const int cl = 16 * tt + c, col = col0 + cl;
     float dbp = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int rr = 4 * g + r;
-      float o = 0.f;
-      if (rr < t.nrows) {
-        const int64_t e = (t.row0 + rr) * D + col;
-        const float2 st = rsx[t.row0 + rr];
-        const float xh = (x[e] - st.x) * st.y;
-        const float gvv = (fmaf(xh, gv, bv) > 0.f ? dh[e] : 0.f) * gv;
-        o = dv[e] + st.y * (gvv - S1[rr] - xh * S2[rr]);
-        dx[e] = o;
-      }
-      DX[rr][cl] = o;
+      const float xh = (xv[tt][r] - st[r].x) * st[r].y;
+      const float gvv = (fmaf(xh, gv[tt], bv[tt]) > 0.f ? hv[tt][r] : 0.f) * gv[tt];
+      const float o = rr < nrows ? dvv[tt][r] + st[r].y * (gvv - S1[rr] - xh * S2[rr]) : 0.f;
+      if (rr < nrows) dx[(row0 + rr) * D + col] = o;
+      DX[wave][rr][cl] = o;
       dbp += o;
     }
     dbp += __shfl_xor(dbp, 16);
     dbp += __shfl_xor(dbp, 32);
     if (g == 0) out[int64_t(D) * VA + col] = dbp;
   }
-  __syncthreads();
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   // dWp[col][j] = sum_r dx[r][col] agg[r][j]: A[i = col][k = r], B[k = r][j]
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     f32x4 w2[2] = {z4(), z4()};
 #pragma unroll
     for (int q = 0; q < TR / 4; ++q) {
-      const float a = DX[4 * q + g][16 * mt + c];
+      const float a = DX[wave][4 * q + g][16 * mt + c];
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) w2[tt] = mfma(a, AG[4 * q + g][16 * tt + c], w2[tt]);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt) out[int64_t(t.col0 + 16 * mt + 4 * g + r) * VA + 16 * tt + c] = w2[tt][r];
+      for (int tt = 0; tt < 2; ++tt) out[int64_t(col0 + 16 * mt + 4 * g + r) * VA + 16 * tt + c] = w2[tt][r];
   }
-  // d agg partial: A[i = r][k = col] = dx, B[k = col][j] = Wp[col][j]
+  // d agg partial of the wave's columns: A[i = r][k = col] = dx, B[k = col][j] = Wp[col][j]
   f32x4 da[2] = {z4(), z4()};
 #pragma unroll
   for (int q = 0; q < CW / 4; ++q) {
-    const float a = DX[c][4 * q + g];
+    const float a = DX[wave][c][4 * q + g];
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt) da[tt] = mfma(a, Wp[(t.col0 + 4 * q + g) * VA + 16 * tt + c], da[tt]);
+    for (int tt = 0; tt < 2; ++tt) da[tt] = mfma(a, wpv[q][tt], da[tt]);
   }
-  float* slot = ws + (int64_t(t.tile) * ncb + t.cb) * TR * VA;
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt) st_sc1(slot + (4 * g + r) * VA + 16 * tt + c, da[tt][r]);
+    for (int tt = 0; tt < 2; ++tt) DA[wave][(4 * g + r) * VA + 16 * tt + c] = da[tt][r];
+  __syncthreads();
+  // the group partial (waves summed in order), 2 values per thread, handed over write-through
+  float* slot = ws + (int64_t(tile) * ngrp + grp) * TR * VA;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = int(threadIdx.x) + k * TB2_T;
+    float v = DA[0][i];
+#pragma unroll
+    for (int w = 1; w < TB2_W; ++w) v += DA[w][i];
+    st_sc1(slot + i, v);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) {
-    const uint32_t k = __hip_atomic_fetch_add(cnt + t.tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag = k == uint32_t(ncb - 1) ? 1u : 0u;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t k = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = k == uint32_t(ngrp - 1) ? 1u : 0u;
   }
   __syncthreads();
   if (flag == 0u) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const float* base = ws + int64_t(t.tile) * ncb * TR * VA;
-  for (int i = lane; i < TR * VA; i += kWv) {
+  const float* base = ws + int64_t(tile) * ngrp * TR * VA;
+  constexpr int MAXG = MAXD / TB2_COLS;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = int(threadIdx.x) + k * TB2_T;
+    float v[MAXG];
+#pragma unroll
+    for (int q = 0; q < MAXG; ++q)
+      v[q] = __hip_atomic_load(base + int64_t(q < ngrp ? q : 0) * TR * VA + i, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     float s = 0.f;
-    for (int q = 0; q < ncb; ++q)
-      s += __hip_atomic_load(base + int64_t(q) * TR * VA + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (i / VA < t.nrows) dagg[(t.row0 + i / VA) * VA + i % VA] = s;
+#pragma unroll
+    for (int q = 0; q < MAXG; ++q) s += q < ngrp ? v[q] : 0.f;
+    if (i / VA < nrows) dagg[(row0 + i / VA) * VA + i % VA] = s;
   }
-  if (lane == 0) __hip_atomic_store(cnt + t.tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store(cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace
@@ -1026,7 +1083,7 @@ extern "C" int gasfm_view_chain_tail_bwd(const float* dv, const float* x, const 
     kq_tail_bwd1<8>(m, g1, st, dv, x, h, rsx, ln_w, ln_b, Wm, dh, dWm, RSUMT, part);
   int s = launch_status("gasfm_view_chain_tail_bwd1");
   if (s != GASFM_OK) return s;
-  hipLaunchKernelGGL(vc_tail_bwd2_kernel, dim3(unsigned(T * ncb)), dim3(kWv), 0, st, dv, dh, x, rsx, agg, m, D, ln_w,
+  hipLaunchKernelGGL(vc_tail_bwd2_kernel, dim3(unsigned(T * (D / TB2_COLS))), dim3(TB2_T), 0, st, dv, dh, x, rsx, agg, m, D, ln_w,
                      ln_b, Wp, RSUMT, dx, dagg, ws, counters, part);
   return launch_status("gasfm_view_chain_tail_bwd2");
 }
