@@ -72,6 +72,39 @@ __device__ __forceinline__ Tile tile_of(int b, int64_t m, int D) {
   return t;
 }
 
+// 16 x D rows (row0.., clamped to valid rows) as KU float4 per thread, and their LDS stores
+template <int KU>
+__device__ __forceinline__ void rows_load(const float* __restrict__ A, int64_t lda, const Tile& t, float4 (&v)[KU]) {
+  constexpr int V = KU * 32;
+#pragma unroll
+  for (int q = 0; q < KU; ++q) {
+    const int idx = int(threadIdx.x) + q * NT, r = idx / V, c4 = idx % V;
+    v[q] = *reinterpret_cast<const float4*>(A + (t.row0 + (r < t.nrows ? r : 0)) * lda + 4 * c4);
+  }
+}
+template <int KU>
+__device__ __forceinline__ void rows_store(float* X, const float4 (&v)[KU]) {
+  constexpr int V = KU * 32;
+#pragma unroll
+  for (int q = 0; q < KU; ++q) {
+    const int idx = int(threadIdx.x) + q * NT, r = idx / V, c4 = idx % V;
+    *reinterpret_cast<float4*>(X + r * LDX + 4 * c4) = v[q];
+  }
+}
+// a [D] LayerNorm affine pair staged as [gamma | beta] in LDS GB (threads 0..D/4-1: gamma, D/4..D/2-1: beta)
+template <int KU>
+__device__ __forceinline__ float4 affine_load(const float* __restrict__ gam, const float* __restrict__ bet) {
+  constexpr int D = KU * 128;
+  const int t = int(threadIdx.x);
+  const int tc = t < D / 2 ? t : 0;
+  return *reinterpret_cast<const float4*>((tc < D / 4 ? gam : bet) + 4 * (tc % (D / 4)));
+}
+template <int KU>
+__device__ __forceinline__ void affine_store(float* GB, const float4& v) {
+  constexpr int D = KU * 128;
+  if (int(threadIdx.x) < D / 2) *reinterpret_cast<float4*>(GB + 4 * threadIdx.x) = v;
+}
+
 // 16 x D rows (row0.., clamped to valid rows) into LDS X (row stride LDX), float4 loads, all
 // issued before the stores
 template <int KU>
@@ -172,35 +205,49 @@ __global__ __launch_bounds__(NT) void vc_tail_fwd_kernel(const float* __restrict
   __shared__ __attribute__((aligned(16))) float X[TR * LDX];
   __shared__ float RED[NWV * 2 * 4 * kWv];
   __shared__ float XO[TR][CW + 1];
+  __shared__ __attribute__((aligned(16))) float GB[2 * MAXD];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   const Tile t = tile_of(blockIdx.x, m, D);
   const int k0 = wave * KU * 16;
-  float4 bw[2][KU];
-  prefetch_wt<KU>(Wm, D, t.col0, k0, bw);
-  // x = prev + agg Wp^T + bp over the tile's whole rows: wave w owns column tiles w, w + 8, ...
-  if (PREV) rows_to_lds<KU>(prev, D, t, X);
+  // every load in the order of use (vmcnt counts in issue order: waiting for the prologue's
+  // operands must not wait for the GEMM's W slab, requested last): prev rows, agg, the prologue's
+  // Wp rows and bias, the LayerNorm affine, then Wm
+  float4 pv[KU];
+  if (PREV) rows_load<KU>(prev, D, t, pv);
   float4 ag[2];
   {
     const int64_t r = t.row0 + (c < t.nrows ? c : 0);
     ag[0] = *reinterpret_cast<const float4*>(agg + r * VA + 4 * g);
     ag[1] = *reinterpret_cast<const float4*>(agg + r * VA + 16 + 4 * g);
   }
-  __syncthreads();
+  float4 wp[KU][2];
+  float bpv[KU];
 #pragma unroll
-  for (int q = 0; q < KU; ++q) {  // D / 16 column tiles over 8 waves
+  for (int q = 0; q < KU; ++q) {  // D / 16 column tiles over 8 waves: wave w owns tiles w, w + 8, ...
     const int col = (wave + NWV * q) * 16 + c;
-    const float4 w0 = *reinterpret_cast<const float4*>(Wp + col * VA + 4 * g);
-    const float4 w1 = *reinterpret_cast<const float4*>(Wp + col * VA + 16 + 4 * g);
+    wp[q][0] = *reinterpret_cast<const float4*>(Wp + col * VA + 4 * g);
+    wp[q][1] = *reinterpret_cast<const float4*>(Wp + col * VA + 16 + 4 * g);
+    bpv[q] = bp[col];
+  }
+  const float4 gb = affine_load<KU>(gam, bet);
+  float4 bw[2][KU];
+  prefetch_wt<KU>(Wm, D, t.col0, k0, bw);
+  if (PREV) rows_store<KU>(X, pv);
+  affine_store<KU>(GB, gb);
+  __syncthreads();
+  // x = prev + agg Wp^T + bp over the tile's whole rows
+#pragma unroll
+  for (int q = 0; q < KU; ++q) {
+    const int col = (wave + NWV * q) * 16 + c;
     f32x4 xa = z4();
 #pragma unroll
-    for (int j = 0; j < 4; ++j) xa = mfma(f4(ag[0], j), f4(w0, j), xa);
+    for (int j = 0; j < 4; ++j) xa = mfma(f4(ag[0], j), f4(wp[q][0], j), xa);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) xa = mfma(f4(ag[1], j), f4(w1, j), xa);
-    const float b = bp[col];
+    for (int j = 0; j < 4; ++j) xa = mfma(f4(ag[1], j), f4(wp[q][1], j), xa);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float* d = X + (4 * g + r) * LDX + col;
-      *d = xa[r] + b + (PREV ? *d : 0.f);
+      *d = xa[r] + bpv[q] + (PREV ? *d : 0.f);
     }
   }
   __syncthreads();
@@ -211,7 +258,7 @@ __global__ __launch_bounds__(NT) void vc_tail_fwd_kernel(const float* __restrict
   {
     const float xown = xs[t.cb];  // column col0 + seg
     XO[row][seg] = xown;
-    const float hown = fmaxf(fmaf((xown - mean) * rstd, gam[t.col0 + seg], bet[t.col0 + seg]), 0.f);
+    const float hown = fmaxf(fmaf((xown - mean) * rstd, GB[t.col0 + seg], GB[D + t.col0 + seg]), 0.f);
     if (row < t.nrows) {
       xo[(t.row0 + row) * D + t.col0 + seg] = xown;
       ho[(t.row0 + row) * D + t.col0 + seg] = hown;
@@ -221,7 +268,7 @@ __global__ __launch_bounds__(NT) void vc_tail_fwd_kernel(const float* __restrict
 #pragma unroll
   for (int i = 0; i < KU * 4; ++i) {
     const int col = seg + 32 * i;
-    X[row * LDX + col] = fmaxf(fmaf((xs[i] - mean) * rstd, gam[col], bet[col]), 0.f);
+    X[row * LDX + col] = fmaxf(fmaf((xs[i] - mean) * rstd, GB[col], GB[D + col]), 0.f);
   }
   __syncthreads();
   f32x4 acc[2] = {z4(), z4()};
@@ -256,6 +303,7 @@ __global__ __launch_bounds__(NT) void vc_hub_fwd_kernel(const float* __restrict_
   __shared__ __attribute__((aligned(16))) float X[TR * LDX];
   __shared__ float RED[NWV * 2 * 4 * kWv];
   __shared__ float Tt[TR][VA + 2];
+  __shared__ __attribute__((aligned(16))) float GB[2 * MAXD];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   const int ncb = D / CW, T = int((m + TR - 1) / TR);
   const int b = blockIdx.x;
@@ -263,8 +311,10 @@ __global__ __launch_bounds__(NT) void vc_hub_fwd_kernel(const float* __restrict_
   float4 bw[2][KU];
   if (b < T * ncb) {  // ---- XL = v Wl^T + bl
     const Tile t = tile_of(b, m, D);
+    float4 vr[KU];
+    rows_load<KU>(v, D, t, vr);  // before the W slab: waiting for the rows does not wait for it
     prefetch_wt<KU>(Wl, D, t.col0, k0, bw);
-    rows_to_lds<KU>(v, D, t, X);
+    rows_store<KU>(X, vr);
     __syncthreads();
     f32x4 acc[2] = {z4(), z4()};
     gemm_lds_wt<KU>(X, bw, k0, acc);
@@ -282,19 +332,21 @@ __global__ __launch_bounds__(NT) void vc_hub_fwd_kernel(const float* __restrict_
   }
   const bool branch_a = b >= T * ncb + T;  // t / XR role
   const Tile t = tile_of((b - T * ncb - (branch_a ? T : 0)) * ncb, m, D);
+  float4 vr[KU];
+  rows_load<KU>(v, D, t, vr);
+  const float4 gbv = affine_load<KU>(branch_a ? gA : gC, branch_a ? bA : bC);
   prefetch_wt<KU>(branch_a ? Wa : Wv, D, 0, k0, bw);
-  rows_to_lds<KU>(v, D, t, X);
+  rows_store<KU>(X, vr);
+  affine_store<KU>(GB, gbv);
   __syncthreads();
   float xs[KU * 4], mean, rstd;
   tile_stats<KU>(X, eps, xs, mean, rstd);
   const int row = int(threadIdx.x) >> 5, seg = int(threadIdx.x) & 31;
   if (!branch_a && seg == 0 && row < t.nrows) rso[t.row0 + row] = make_float2(mean, rstd);
-  const float* gg = branch_a ? gA : gC;
-  const float* bb = branch_a ? bA : bC;
 #pragma unroll
   for (int i = 0; i < KU * 4; ++i) {
     const int col = seg + 32 * i;
-    X[row * LDX + col] = fmaxf(fmaf((xs[i] - mean) * rstd, gg[col], bb[col]), 0.f);
+    X[row * LDX + col] = fmaxf(fmaf((xs[i] - mean) * rstd, GB[col], GB[D + col]), 0.f);
   }
   __syncthreads();
   f32x4 acc[2] = {z4(), z4()};
@@ -423,8 +475,10 @@ __device__ __forceinline__ void tile_dt(const float* __restrict__ dxr, const flo
     for (int r2 = 0; r2 < 4; ++r2) DT[4 * g + r2][16 * tt + c] = d2[tt][r2];
 }
 
-// roles: [0, T ncb) dacc[:, cols] = dXL Wl (+ dres), then (waves 0-1) the LayerNorm-branch row-sum
-// partials and parameter partials of the columns; [T ncb, + D/16 x D/WGT) dWl = dXL^T v
+// roles: [0, T ncb) dacc[:, cols] = dXL Wl (+ dres); [T ncb, + T ncb / 4) the LayerNorm-branch
+// work of 4 column blocks (wave w: block 4 q + w / 2, branch c (w even: dsv, Wv) or a (w odd:
+// dt = dxr Wr, Wa)): row-sum partials RSUM[row][cb] and the tile's parameter partials;
+// [.., + D/16 x D/WGT) dWl = dXL^T v.  The three roles share nothing: they run side by side.
 template <int KU, int KQ>
 __global__ __launch_bounds__(NT) void vc_hub_bwd1_kernel(
     const float* __restrict__ v, const float2* __restrict__ rsv, int64_t m, const float* __restrict__ gC,
@@ -435,88 +489,173 @@ __global__ __launch_bounds__(NT) void vc_hub_bwd1_kernel(
     float* __restrict__ dacc, float* __restrict__ dWl, float4* __restrict__ RSUM, float* __restrict__ part) {
   constexpr int D = KU * 128;
   __shared__ float RED[NWV * 2 * 4 * kWv];
-  __shared__ float DT[TR][VA + 2], SD[TR][VA + 2];
-  __shared__ float HB[2][TR * CW];
+  __shared__ float SB[NWV][TR][VA + 2];  // per wave: its branch's 16 x 32 left operand (dsv or dt)
+  __shared__ float HB[NWV][TR * CW];     // per wave: relu(LN_b v) rows of its columns
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   const int ncb = D / CW, T = int((m + TR - 1) / TR);
   const int b = blockIdx.x;
-  if (b >= T * ncb) {  // ---- dWl[o][i] = sum_r dXL[r][o] v[r][i]
-    const int q = b - T * ncb, nwj = D / WGT;
+  if (b >= T * ncb + T * (ncb / 4)) {  // ---- dWl[o][i] = sum_r dXL[r][o] v[r][i]
+    const int q = b - T * ncb - T * (ncb / 4), nwj = D / WGT;
     const int i0 = (q / nwj) * TR, j0 = (q % nwj) * WGT + wave * CW;
     wgrad_tile<KQ>(dxl, D, v, D, int(m), i0, j0, dWl, D);
     return;
   }
-  const Tile t = tile_of(b, m, D);
-  const int k0 = wave * KU * 16;
-  f32x4 acc[2] = {z4(), z4()};
-  gemm_gw<KU>(dxl, D, t, Wl, D, k0, acc);
-  reduce_waves(RED, acc);
-  const HubPart P(D);
-  float* out = part + int64_t(t.tile) * P.cols;
-  if (wave == 0) {
+  if (b < T * ncb) {  // ---- dacc = dXL Wl (+ dres)
+    const Tile t = tile_of(b, m, D);
+    const int k0 = wave * KU * 16;
+    float dr[2][4];
+    if (wave == 0) {  // the epilogue's d skip rows, requested before the product
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      const int col = t.col0 + 16 * tt + c;
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rr = 4 * g + r;
+          dr[tt][r] = dres ? dres[(t.row0 + (rr < t.nrows ? rr : 0)) * D + t.col0 + 16 * tt + c] : 0.f;
+        }
+    }
+    f32x4 acc[2] = {z4(), z4()};
+    gemm_gw<KU>(dxl, D, t, Wl, D, k0, acc);
+    reduce_waves(RED, acc);
+    if (wave != 0) return;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rr = 4 * g + r;
-        if (rr < t.nrows) {
-          const int64_t o = (t.row0 + rr) * D + col;
-          dacc[o] = acc[tt][r] + (dres ? dres[o] : 0.f);
-        }
+        if (rr < t.nrows) dacc[(t.row0 + rr) * D + t.col0 + 16 * tt + c] = acc[tt][r] + dr[tt][r];
       }
-    }
     return;
   }
-  if (wave > 2) return;
-  // waves 1 and 2: branch c (dsv, Wv) and branch a (dt = dxr Wr, Wa) of the columns
-  const bool ba_ = wave == 2;
-  float(*S)[VA + 2] = ba_ ? DT : SD;
-  if (ba_) {
-    tile_dt(dxr, Wr, t, DT);
-  } else {
+  // ---- branch work
+  const int q0 = b - T * ncb;
+  const int tile = q0 / (ncb / 4);
+  const int cb = (q0 % (ncb / 4)) * 4 + (wave >> 1);
+  const bool ba_ = wave & 1;
+  const Tile t = tile_of(tile * ncb + cb, m, D);
+  const HubPart P(D);
+  float* out = part + int64_t(t.tile) * P.cols;
+  // every load first (clamped rows; masked where consumed)
+  float sl[4][2], wrv[VA / 4][2], wbv[VA / 4][2], vv[2][4], dlv[2][4], gg[2], bb[2];
+  float2 st[4];
+  const float* Wb = ba_ ? Wa : Wv;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int rr = 4 * g + r;
-      const int64_t rw = t.row0 + (rr < t.nrows ? rr : 0);
-      SD[rr][c] = rr < t.nrows ? dsv[rw * VA + c] : 0.f;
-      SD[rr][16 + c] = rr < t.nrows ? dsv[rw * VA + 16 + c] : 0.f;
+  for (int r = 0; r < 4; ++r) {
+    const int rr = 4 * g + r;
+    const int64_t rw = t.row0 + (rr < t.nrows ? rr : 0);
+    st[r] = rsv[rw];
+    // branch c: the dsv rows; branch a: the dxr rows (dt = dxr Wr below)
+    const float* src = ba_ ? dxr : dsv;
+    sl[r][0] = src[rw * VA + c];
+    sl[r][1] = src[rw * VA + 16 + c];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      vv[tt][r] = v[rw * D + t.col0 + 16 * tt + c];
+      dlv[tt][r] = ba_ ? 0.f : dxl[rw * D + t.col0 + 16 * tt + c];
     }
+  }
+#pragma unroll
+  for (int q = 0; q < VA / 4; ++q)
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      wbv[q][tt] = Wb[(4 * q + g) * D + t.col0 + 16 * tt + c];
+      wrv[q][tt] = ba_ ? Wr[(4 * q + g) * VA + 16 * tt + c] : 0.f;
+    }
+  const float* gptr = ba_ ? gA : gC;
+  const float* bptr = ba_ ? bA : bC;
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    gg[tt] = gptr[t.col0 + 16 * tt + c];
+    bb[tt] = bptr[t.col0 + 16 * tt + c];
+  }
+  float(*S)[VA + 2] = SB[wave];
+  // the branch's left operand rows in LDS (zero past nrows)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int rr = 4 * g + r;
+    S[rr][c] = rr < t.nrows ? sl[r][0] : 0.f;
+    S[rr][16 + c] = rr < t.nrows ? sl[r][1] : 0.f;
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  const float* Wb = ba_ ? Wa : Wv;
-  const float* gg = ba_ ? gA : gC;
-  const float* bbv = ba_ ? bA : bC;
+  if (ba_) {  // dt = dxr Wr (C layout) replaces the dxr rows
+    f32x4 d2[2] = {z4(), z4()};
+#pragma unroll
+    for (int q = 0; q < VA / 4; ++q) {
+      const float a = S[c][4 * q + g];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) d2[tt] = mfma(a, wrv[q][tt], d2[tt]);
+    }
+    if (t.cb == 0) {  // dWr = dxr^T t, dbr = sum dxr (the dxr rows still in S)
+      float tv[4][2];
+#pragma unroll
+      for (int q = 0; q < TR / 4; ++q) {
+        const int rr = 4 * q + g;
+        const int64_t rw = t.row0 + (rr < t.nrows ? rr : 0);
+        tv[q][0] = rr < t.nrows ? t_in[rw * VA + c] : 0.f;
+        tv[q][1] = rr < t.nrows ? t_in[rw * VA + 16 + c] : 0.f;
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        f32x4 wr[2] = {z4(), z4()};
+#pragma unroll
+        for (int q = 0; q < TR / 4; ++q) {
+          const float a = S[4 * q + g][16 * mt + c];
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt) wr[tt] = mfma(a, tv[q][tt], wr[tt]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt) out[P.WR + (16 * mt + 4 * g + r) * VA + 16 * tt + c] = wr[tt][r];
+      }
+      if (lane < VA) {
+        float sr = 0.f;
+#pragma unroll
+        for (int rr = 0; rr < TR; ++rr) sr += S[rr][lane];
+        out[P.BR + lane] = sr;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) S[4 * g + r][16 * tt + c] = d2[tt][r];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (t.cb == 0 && lane < VA) {
+      float sa = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < TR; ++rr) sa += S[rr][lane];
+      out[P.BAB + lane] = sa;
+    }
+  }
   // dh[r][col] = sum_n S[r][n] Wb[n][col]  (C layout: rows 4g + r, column c of tile tt)
   f32x4 dh[2] = {z4(), z4()};
 #pragma unroll
   for (int q = 0; q < VA / 4; ++q) {
     const float a = S[c][4 * q + g];
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt) dh[tt] = mfma(a, Wb[(4 * q + g) * D + t.col0 + 16 * tt + c], dh[tt]);
+    for (int tt = 0; tt < 2; ++tt) dh[tt] = mfma(a, wbv[q][tt], dh[tt]);
   }
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
   float dgp[2] = {0.f, 0.f}, dbp[2] = {0.f, 0.f}, dlp[2] = {0.f, 0.f};
-  f32x4 hcol[2];  // relu(LN_b v) in C layout, for dW of the branch
+  float* H = HB[wave];
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
-    const int col = t.col0 + 16 * tt + c;
-    const float gv = gg[col], bv = bbv[col];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int rr = 4 * g + r;
-      const int64_t rw = t.row0 + (rr < t.nrows ? rr : 0);
-      const float2 st = rsv[rw];
-      const float xh = (v[rw * D + col] - st.x) * st.y;
-      const float pre = fmaf(xh, gv, bv);
-      const float dy = (rr < t.nrows && pre > 0.f) ? dh[tt][r] : 0.f;
-      hcol[tt][r] = rr < t.nrows ? fmaxf(pre, 0.f) : 0.f;
+      const bool live = rr < t.nrows;
+      const float xh = (vv[tt][r] - st[r].x) * st[r].y;
+      const float pre = fmaf(xh, gg[tt], bb[tt]);
+      const float dy = (live && pre > 0.f) ? dh[tt][r] : 0.f;
+      H[rr * CW + 16 * tt + c] = live ? fmaxf(pre, 0.f) : 0.f;
       dgp[tt] = fmaf(dy, xh, dgp[tt]);
       dbp[tt] += dy;
-      s1[r] = fmaf(dy, gv, s1[r]);
-      s2[r] = fmaf(dy * gv, xh, s2[r]);
-      if (!ba_ && rr < t.nrows) dlp[tt] += dxl[rw * D + col];
+      s1[r] = fmaf(dy, gg[tt], s1[r]);
+      s2[r] = fmaf(dy * gg[tt], xh, s2[r]);
+      dlp[tt] += live ? dlv[tt][r] : 0.f;
     }
   }
   // row partial sums over the 32 columns (16 lanes c, 2 tiles) -> RSUM[row][cb], branch c in
@@ -550,15 +689,9 @@ __global__ __launch_bounds__(NT) void vc_hub_bwd1_kernel(
       if (!ba_) out[P.BL + col] = l;
     }
   }
-  // dW_b[n][col] = sum_r S[r][n] relu(LN_b v)[r][col]: A[i = n][k = r] = S[r][n], B[k = r][j] = h
-  // h goes through a per-wave LDS slot (C layout -> rows)
-  float* H = HB[ba_ ? 1 : 0];
-#pragma unroll
-  for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) H[(4 * g + r) * CW + 16 * tt + c] = hcol[tt][r];
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // dW_b[n][col] = sum_r S[r][n] relu(LN_b v)[r][col]: A[i = n][k = r] = S[r][n], B[k = r][j] = h
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     f32x4 w2[2] = {z4(), z4()};
@@ -573,34 +706,6 @@ __global__ __launch_bounds__(NT) void vc_hub_bwd1_kernel(
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt)
         out[(ba_ ? P.WA : P.WV) + int64_t(16 * mt + 4 * g + r) * D + t.col0 + 16 * tt + c] = w2[tt][r];
-  }
-  if (ba_ && t.cb == 0) {  // dWr = dxr^T t, dbr = sum dxr, dba = sum dt over the tile
-    f32x4 wr[2][2] = {{z4(), z4()}, {z4(), z4()}};
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int q = 0; q < TR / 4; ++q) {
-        const int rr = 4 * q + g;
-        const int64_t rw = t.row0 + (rr < t.nrows ? rr : 0);
-        const float a = rr < t.nrows ? dxr[rw * VA + 16 * mt + c] : 0.f;
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) wr[mt][tt] = mfma(a, rr < t.nrows ? t_in[rw * VA + 16 * tt + c] : 0.f, wr[mt][tt]);
-      }
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) out[P.WR + (16 * mt + 4 * g + r) * VA + 16 * tt + c] = wr[mt][tt][r];
-    if (lane < VA) {
-      float sr = 0.f, sa = 0.f;
-      for (int rr = 0; rr < t.nrows; ++rr) {
-        sr += dxr[(t.row0 + rr) * VA + lane];
-        sa += DT[rr][lane];
-      }
-      out[P.BR + lane] = sr;
-      out[P.BAB + lane] = sa;
-    }
   }
 }
 
@@ -695,6 +800,25 @@ __global__ __launch_bounds__(NT) void vc_tail_bwd1_kernel(const float* __restric
   }
   const Tile t = tile_of(b, m, D);
   const int k0 = wave * KU * 16;
+  // wave 0's epilogue operands, requested before the product
+  float xv[2][4], dvv[2][4], gv2[2], bv2[2];
+  float2 st[4];
+  if (wave == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) st[r] = rsx[t.row0 + (4 * g + r < t.nrows ? 4 * g + r : 0)];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int col = t.col0 + 16 * tt + c;
+      gv2[tt] = gam[col];
+      bv2[tt] = bet[col];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t o = (t.row0 + (4 * g + r < t.nrows ? 4 * g + r : 0)) * D + col;
+        xv[tt][r] = x[o];
+        dvv[tt][r] = dv[o];
+      }
+    }
+  }
   f32x4 acc[2] = {z4(), z4()};
   gemm_gw<KU>(dv, D, t, Wm, D, k0, acc);
   reduce_waves(RED, acc);
@@ -704,21 +828,19 @@ __global__ __launch_bounds__(NT) void vc_tail_bwd1_kernel(const float* __restric
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     const int col = t.col0 + 16 * tt + c;
-    const float gv = gam[col], bv = bet[col];
+    const float gv = gv2[tt], bv = bv2[tt];
     float dgp = 0.f, dbp = 0.f, dmp = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int rr = 4 * g + r;
-      const int64_t rw = t.row0 + (rr < t.nrows ? rr : 0);
-      const int64_t o = rw * D + col;
-      const float2 st = rsx[rw];
-      const float xh = (x[o] - st.x) * st.y;
+      const bool live = rr < t.nrows;
+      const float xh = (xv[tt][r] - st[r].x) * st[r].y;
       const float d = acc[tt][r];
-      if (rr < t.nrows) dh[o] = d;
-      const float dy = (rr < t.nrows && fmaf(xh, gv, bv) > 0.f) ? d : 0.f;
+      if (live) dh[(t.row0 + rr) * D + col] = d;
+      const float dy = (live && fmaf(xh, gv, bv) > 0.f) ? d : 0.f;
       dgp = fmaf(dy, xh, dgp);
       dbp += dy;
-      if (rr < t.nrows) dmp += dv[o];
+      dmp += live ? dvv[tt][r] : 0.f;
       s1[r] = fmaf(dy, gv, s1[r]);
       s2[r] = fmaf(dy * gv, xh, s2[r]);
     }
@@ -1041,7 +1163,7 @@ extern "C" int gasfm_view_chain_hub_bwd(const float* v, const float* rs, int64_t
   const int T = int((m + TR - 1) / TR);
   float4* RSUM = reinterpret_cast<float4*>(scratch);
   const float2* rsv = reinterpret_cast<const float2*>(rs);
-  const dim3 g1(unsigned(T * (D / CW) + (D / TR) * (D / WGT)));
+  const dim3 g1(unsigned(T * (D / CW) + T * (D / CW / 4) + (D / TR) * (D / WGT)));
   if (D == 256)
     kq_hub_bwd1<2>(m, g1, st, v, rsv, gC, bC, Wv, gA, bA, Wa, t, Wr, Wl, dsv, dxr, dxl, dres, dacc, dWl, RSUM, part);
   else if (D == 512)
