@@ -118,6 +118,10 @@ _SIGS = {
     "gasfm_gchain_scratch_floats": (_i64, [_vp]),
     "gasfm_gchain_counters": (_i32, [_vp]),
     "gasfm_gchain_bwd": (_i32, [_vp] * 16),
+    "gasfm_gatt_scratch_floats": (_i64, [_i32, _vp]),
+    "gasfm_gatt_fwd": (_i32, [_i32, _vp, _f32, _vp, _vp, _vp]),
+    "gasfm_gatt_bwd": (_i32, [_i32, _vp, _f32, _vp, _vp, _vp]),
+    "gasfm_gatt_merge": (_i32, [_i32, _vp, _i32, _i64, _vp]),
     "gasfm_pose_fwd": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "gasfm_pose_bwd": (_i32, [_vp, _i64, _i64, _vp, _vp, _i64, _vp]),
     "gasfm_esfm_part_rows": (_i32, [_i64]),
@@ -1207,6 +1211,71 @@ def gchain_bwd(c, xcat, x1, g, xv, xp, dskip, dsg, dxrv, dxrp, dxcat, dprev, gra
                             _p(dxrv), _p(dxrp), _p(dxcat), _p(dprev), ctypes.addressof(d), _p(ws), _p(cnt),
                             _stream(g))
     check(st, "gasfm_gchain_bwd")
+
+
+# ---------------------------------------------------------------- global GATv2 convs (global_attn.hip)
+class _GattProb(ctypes.Structure):
+    _fields_ = [("XL", _vp), ("ldXL", _i64), ("src", _vp), ("S", _i32), ("HC", _i32), ("XR", _vp), ("att", _vp),
+                ("bias", _vp), ("out", _vp), ("smax", _vp), ("ssum", _vp), ("part", _vp), ("gout", _vp),
+                ("dXL", _vp), ("ldDXL", _i64), ("dXR", _vp), ("datt", _vp)]
+
+
+def _gatt_probs(probs):
+    """probs: dicts with XL [rows, HC] (unit column stride), src (int32 CUDA vector or None), S, XR,
+    att, bias and the outputs of the direction; returns a ctypes array."""
+    arr = (_GattProb * len(probs))()
+    for q, d in enumerate(probs):
+        XL = d["XL"]
+        if not XL.is_cuda or XL.dtype != torch.float32 or XL.stride(1) != 1:
+            raise TypeError("gatt: XL must be a float32 CUDA tensor with unit column stride")
+        src = d.get("src")
+        if src is not None and (src.dtype != torch.int32 or not src.is_contiguous()):
+            raise TypeError("gatt: src must be a contiguous int32 tensor")
+        a = arr[q]
+        a.XL, a.ldXL, a.src, a.S, a.HC = XL.data_ptr(), XL.stride(0), _p(src), int(d["S"]), int(d["att"].numel())
+        for k in ("XR", "att", "bias", "out", "smax", "ssum", "part", "gout", "dXR", "datt"):
+            setattr(a, k, _p(d.get(k)))
+        dXL = d.get("dXL")
+        if dXL is not None:
+            if dXL.stride(1) != 1:
+                raise TypeError("gatt: dXL must have unit column stride")
+            a.dXL, a.ldDXL = dXL.data_ptr(), dXL.stride(0)
+    return arr
+
+
+def gatt_fwd(probs, slope):
+    """One launch: both global convs' forward (gasfm_gatt_fwd)."""
+    arr = _gatt_probs(probs)
+    L = lib()
+    dev = probs[0]["XL"].device
+    ws = torch.empty(int(L.gasfm_gatt_scratch_floats(len(probs), ctypes.addressof(arr))), dtype=torch.float32, device=dev)
+    cnt = _counters(dev, len(probs))
+    check(L.gasfm_gatt_fwd(len(probs), ctypes.addressof(arr), float(slope), _p(ws), _p(cnt), _stream(probs[0]["XL"])),
+          "gasfm_gatt_fwd")
+
+
+def gatt_bwd(probs, slope):
+    """One launch: both global convs' backward (gasfm_gatt_bwd)."""
+    arr = _gatt_probs(probs)
+    L = lib()
+    dev = probs[0]["XL"].device
+    ws = torch.empty(int(L.gasfm_gatt_scratch_floats(len(probs), ctypes.addressof(arr))), dtype=torch.float32, device=dev)
+    cnt = _counters(dev, len(probs))
+    check(L.gasfm_gatt_bwd(len(probs), ctypes.addressof(arr), float(slope), _p(ws), _p(cnt), _stream(probs[0]["XL"])),
+          "gasfm_gatt_bwd")
+
+
+def gatt_merge(probs, nrows, stride):
+    """One launch: merge the nrows gathered partial rows of each problem (probs[q]["part"]: the first
+    row; rank r's at + r * stride floats) into its out / smax / ssum (gasfm_gatt_merge)."""
+    arr = (_GattProb * len(probs))()
+    for q, d in enumerate(probs):
+        a = arr[q]
+        a.HC = int(d["bias"].numel())
+        for k in ("bias", "out", "smax", "ssum", "part"):
+            setattr(a, k, _p(d[k]))
+    check(lib().gasfm_gatt_merge(len(probs), ctypes.addressof(arr), int(nrows), int(stride), _stream(d["bias"])),
+          "gasfm_gatt_merge")
 
 
 # ---------------------------------------------------------------- device scene builder (scene_build.hip)

@@ -49,6 +49,33 @@ LANES_MAX_AVG = 32  # 4-wide convs with <= this many edges per item on average: 
 # config-4 step (tools/gpu_lanes_ab.sh), so it is the default; GASFM_ATTN_BWD_LANES=0 restores the
 # general kernel.
 BWD_LANES = os.environ.get("GASFM_ATTN_BWD_LANES", "1") != "0"
+# The two convs onto the global node as ONE forward and ONE backward launch (global_attn.hip, round
+# 4) instead of an attention kernel + ordered combines per conv (~6 launches each way per block);
+# GASFM_GLOBAL_ATTN=0 restores the general plan kernels (the A/B knob).
+GLOBAL_ATTN = os.environ.get("GASFM_GLOBAL_ATTN", "1") != "0"
+
+
+def gatt_ok(plan, heads, XL, XR, att):
+    """Whether the fused global-conv kernels take this single-target conv (H = 4, C in {16, 256})."""
+    HC = att.numel()
+    if not GLOBAL_ATTN or plan.num_targets != 1 or heads != 4 or HC not in (64, 1024):
+        return False
+    if XL.dim() != 2 or XL.shape[1] != HC or XL.stride(1) != 1 or XL.stride(0) % 4 or XL.data_ptr() % 16:
+        return False
+    if XL.shape[0] < plan.src_rows or (plan.perm is not None and plan.perm.dtype != torch.int32):
+        return False
+    return XR.numel() == HC and XR.is_contiguous() and XR.data_ptr() % 16 == 0
+
+
+def gatt_prob(plan, XL, XR, att, bias, **kw):
+    return dict(XL=XL, src=plan.perm, S=plan.num_edges, XR=XR, att=att.reshape(-1), bias=bias, **kw)
+
+
+def gatt_dxl(plan, XL, HC):
+    """The dXL buffer of a fused global conv: only source rows are written, so zero-filled unless
+    the plan's sources cover every row."""
+    full = plan.num_edges == XL.shape[0] == plan.src_rows
+    return (torch.empty if full else torch.zeros)((XL.shape[0], HC), dtype=torch.float32, device=XL.device)
 
 
 def _lanes(plan, heads, HC):
@@ -422,8 +449,15 @@ class GlobalPairFn(torch.autograd.Function):
     def forward(ctx, XLv, XRv, att_v, bias_v, XLp, XRp, att_p, bias_p, plan_v, plan_p, heads, slope):
         HCv, HCp = att_v.numel(), att_p.numel()
         x = torch.empty((1, HCv + HCp), dtype=torch.float32, device=XLv.device)
-        _, mv, sv = attn_forward_raw(XLv, XRv, att_v, bias_v, plan_v, heads, slope, out=x[:, :HCv])
-        _, mp, sp = attn_forward_raw(XLp, XRp, att_p, bias_p, plan_p, heads, slope, out=x[:, HCv:])
+        ctx.fused = gatt_ok(plan_v, heads, XLv, XRv, att_v) and gatt_ok(plan_p, heads, XLp, XRp, att_p)
+        if ctx.fused:
+            st = torch.empty((4, heads), dtype=torch.float32, device=XLv.device)
+            mv, sv, mp, sp = st[0:1], st[1:2], st[2:3], st[3:4]
+            _native.gatt_fwd([gatt_prob(plan_v, XLv, XRv, att_v, bias_v, out=x[:, :HCv], smax=mv, ssum=sv),
+                              gatt_prob(plan_p, XLp, XRp, att_p, bias_p, out=x[:, HCv:], smax=mp, ssum=sp)], slope)
+        else:
+            _, mv, sv = attn_forward_raw(XLv, XRv, att_v, bias_v, plan_v, heads, slope, out=x[:, :HCv])
+            _, mp, sp = attn_forward_raw(XLp, XRp, att_p, bias_p, plan_p, heads, slope, out=x[:, HCv:])
         ctx.plans, ctx.heads, ctx.slope, ctx.HCv = (plan_v, plan_p), heads, slope, HCv
         ctx.defer = _native.defer_token(att_v, bias_v, att_p, bias_p)
         ctx.save_for_backward(XLv, XRv, att_v, bias_v, XLp, XRp, att_p, bias_p, x, mv, sv, mp, sp)
@@ -435,6 +469,20 @@ class GlobalPairFn(torch.autograd.Function):
         plan_v, plan_p = ctx.plans
         HCv = ctx.HCv
         g = g.contiguous()
+        if ctx.fused:
+            HCp = x.shape[1] - HCv
+            dXLv, dXLp = gatt_dxl(plan_v, XLv, HCv), gatt_dxl(plan_p, XLp, HCp)
+            dXR = torch.empty((1, HCv + HCp), dtype=torch.float32, device=x.device)
+            dab = torch.empty(2 * (HCv + HCp), dtype=torch.float32, device=x.device)  # datt|dbias, v then p
+            _native.gatt_bwd([gatt_prob(plan_v, XLv, XRv, att_v, bias_v, out=x[:, :HCv], smax=mv, ssum=sv,
+                                         gout=g[:, :HCv], dXL=dXLv, dXR=dXR[:, :HCv], datt=dab[:2 * HCv]),
+                              gatt_prob(plan_p, XLp, XRp, att_p, bias_p, out=x[:, HCv:], smax=mp, ssum=sp,
+                                         gout=g[:, HCv:], dXL=dXLp, dXR=dXR[:, HCv:], datt=dab[2 * HCv:])],
+                             ctx.slope)
+            o = 2 * HCv
+            return (dXLv, dXR[:, :HCv].view_as(XRv), dab[:HCv].view_as(att_v), dab[HCv:o].view_as(bias_v), dXLp,
+                    dXR[:, HCv:].view_as(XRp), dab[o:o + HCp].view_as(att_p), dab[o + HCp:].view_as(bias_p), None,
+                    None, None, None)
         dXLv, dXRv, dattv, dbv = attn_backward_raw(XLv, XRv, att_v, bias_v, plan_v, ctx.heads, ctx.slope,
                                                    x[:, :HCv], mv, sv, g[:, :HCv], defer=ctx.defer)
         dXLp, dXRp, dattp, dbp = attn_backward_raw(XLp, XRp, att_p, bias_p, plan_p, ctx.heads, ctx.slope,

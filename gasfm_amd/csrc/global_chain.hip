@@ -365,22 +365,31 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
                      fmaxf(fmaf((x4.w - mean) * rstd, g4.w, b4.w), 0.f));
   }
   __syncthreads();  // dys
-  // 3. dW rows and this thread's share of dh
+  // 3. this thread's share of dh (the dW rows are stored last: a ticket's s_waitcnt vmcnt(0)
+  // would otherwise wait for them too)
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  float dr[RPT];
 #pragma unroll
   for (int r = 0; r < RPT; ++r) {
-    const int n = row0 + rl + 32 * r;
     const float d = dys[rl + 32 * r];  // 0 past N
+    dr[r] = d;
     s.x = fmaf(d, w[r].x, s.x);
     s.y = fmaf(d, w[r].y, s.y);
     s.z = fmaf(d, w[r].z, s.z);
     s.w = fmaf(d, w[r].w, s.w);
-    if (n < N)
-      *reinterpret_cast<float4*>(p.dW + int64_t(n) * K + col) = make_float4(d * h4.x, d * h4.y, d * h4.z, d * h4.w);
   }
-  if (p.db && slab == 0)
-    for (int t = threadIdx.x; t < 32 * RPT; t += kBT)
-      if (row0 + t < N) p.db[row0 + t] = dys[t];
+  auto store_dw = [&]() {
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      const int n = row0 + rl + 32 * r;
+      const float d = dr[r];
+      if (n < N)
+        *reinterpret_cast<float4*>(p.dW + int64_t(n) * K + col) = make_float4(d * h4.x, d * h4.y, d * h4.z, d * h4.w);
+    }
+    if (p.db && slab == 0)
+      for (int t = threadIdx.x; t < 32 * RPT; t += kBT)
+        if (row0 + t < N) p.db[row0 + t] = dys[t];
+  };
   // 4. the 32 row lanes summed in lane order
   red[threadIdx.x] = s;
   __syncthreads();
@@ -406,7 +415,10 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
       flag = t == uint32_t(p.chunks - 1) ? 1u : 0u;
     }
     __syncthreads();
-    if (flag == 0u) return;
+    if (flag == 0u) {
+      store_dw();
+      return;
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (threadIdx.x < 8) {
       constexpr int MAXC = 16;
@@ -435,7 +447,10 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
     else
       *reinterpret_cast<float4*>(p.dh + col) = tot;
   }
-  if (!fin) return;
+  if (!fin) {
+    store_dw();
+    return;
+  }
   // 7. the launch's last slab runs the finish
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -444,10 +459,12 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
     flag = t == uint32_t(a.f.slabs - 1) ? 1u : 0u;
   }
   __syncthreads();
-  if (flag == 0u) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  gnode_finish(a.f, scratch);
-  if (threadIdx.x == 0) __hip_atomic_store(a.f.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (flag != 0u) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    gnode_finish(a.f, scratch);
+    if (threadIdx.x == 0) __hip_atomic_store(a.f.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  store_dw();
 }
 
 constexpr int kRPT = 8;  // 256 rows per chunk

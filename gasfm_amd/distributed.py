@@ -51,7 +51,8 @@ import torch
 import torch.distributed as dist
 
 from . import _native
-from .attention import AttnPlan, attn_backward_raw, attn_forward_partial, camera_max_piece, combine_partials
+from .attention import (AttnPlan, attn_backward_raw, attn_forward_partial, camera_max_piece, combine_partials,
+                        gatt_dxl, gatt_ok, gatt_prob)
 from .scene import MIN_N_POINTS_PER_VIEW, MIN_N_VIEWS_PER_POINT, SceneData, build_graph_wrappers
 
 # parameters whose gradient comes from rank-local computation (edges / points); everything
@@ -384,17 +385,27 @@ class ShardedGlobalAttentionFn(torch.autograd.Function):
         # per rank, so that in the gathered [W*B] buffer rank r's rows are slots r*B/Lv (v) and
         # (r*B + ov)/Lp (p) of row width Lv / Lp: the combines read them in place
         pack = torch.empty(B, **f32)
-        attn_forward_partial(XLv, XRv, att_v, plan_vp, heads, slope, dst=pack[:Lv].view(1, Lv))
-        attn_forward_partial(XLp, XRp, att_p, plan_pp, heads, slope, dst=pack[ov:ov + Lp].view(1, Lp))
+        ctx.fused = gatt_ok(plan_v, heads, XLv, XRv, att_v) and gatt_ok(plan_p, heads, XLp, XRp, att_p)
+        if ctx.fused:  # both partial rows from one launch (global_attn.hip)
+            _native.gatt_fwd([gatt_prob(plan_v, XLv, XRv, att_v, bias_v, part=pack[:Lv]),
+                              gatt_prob(plan_p, XLp, XRp, att_p, bias_p, part=pack[ov:ov + Lp])], slope)
+        else:
+            attn_forward_partial(XLv, XRv, att_v, plan_vp, heads, slope, dst=pack[:Lv].view(1, Lv))
+            attn_forward_partial(XLp, XRp, att_p, plan_pp, heads, slope, dst=pack[ov:ov + Lp].view(1, Lp))
         g = shard.all_gather(pack.view(1, B)).view(-1)
         xcat = torch.empty((1, HCv + HCp), **f32)
         stats = torch.empty((4, heads), **f32)
         W = shard.world
-        items = shard.pack_items(((0, W, B // Lv), (ov // Lp, W, B // Lp)), dev)
-        _native.attn_combine(items[0], 1, heads, HCv // heads, g.view(-1, Lv), bias_v, True, xcat[:, :HCv],
-                             stats[0:1], stats[1:2])
-        _native.attn_combine(items[1], 1, heads, HCp // heads, g.view(-1, Lp), bias_p, True, xcat[:, HCv:],
-                             stats[2:3], stats[3:4])
+        if ctx.fused:  # both merges in one launch
+            _native.gatt_merge([dict(part=g, bias=bias_v, out=xcat[:, :HCv], smax=stats[0], ssum=stats[1]),
+                                dict(part=g[ov:], bias=bias_p, out=xcat[:, HCv:], smax=stats[2], ssum=stats[3])],
+                               W, B)
+        else:
+            items = shard.pack_items(((0, W, B // Lv), (ov // Lp, W, B // Lp)), dev)
+            _native.attn_combine(items[0], 1, heads, HCv // heads, g.view(-1, Lv), bias_v, True, xcat[:, :HCv],
+                                 stats[0:1], stats[1:2])
+            _native.attn_combine(items[1], 1, heads, HCp // heads, g.view(-1, Lp), bias_p, True, xcat[:, HCv:],
+                                 stats[2:3], stats[3:4])
         ctx.plans, ctx.heads, ctx.slope, ctx.shard, ctx.HCv = (plan_v, plan_p), heads, slope, shard, HCv
         ctx.defer = _native.defer_token(att_v, bias_v, att_p, bias_p)
         ctx.save_for_backward(XLv, XRv, att_v, bias_v, XLp, XRp, att_p, bias_p, xcat, stats)
@@ -407,6 +418,21 @@ class ShardedGlobalAttentionFn(torch.autograd.Function):
         HCv = ctx.HCv
         g = g.contiguous()
         flat = torch.empty_like(xcat)  # [dXRv | dXRp]: the all-reduce payload, written in place
+        if ctx.fused:
+            HCp = xcat.shape[1] - HCv
+            dXLv, dXLp = gatt_dxl(plan_v, XLv, HCv), gatt_dxl(plan_p, XLp, HCp)
+            dab = torch.empty(2 * (HCv + HCp), dtype=torch.float32, device=xcat.device)
+            _native.gatt_bwd([gatt_prob(plan_v, XLv, XRv, att_v, bias_v, out=xcat[:, :HCv], smax=stats[0],
+                                        ssum=stats[1], gout=g[:, :HCv], dXL=dXLv, dXR=flat[:, :HCv],
+                                        datt=dab[:2 * HCv]),
+                              gatt_prob(plan_p, XLp, XRp, att_p, bias_p, out=xcat[:, HCv:], smax=stats[2],
+                                        ssum=stats[3], gout=g[:, HCv:], dXL=dXLp, dXR=flat[:, HCv:],
+                                        datt=dab[2 * HCv:])], ctx.slope)
+            ctx.shard.all_reduce_(flat)
+            o = 2 * HCv
+            return (dXLv, flat[:, :HCv].view_as(XRv), dab[:HCv].view_as(att_v), dab[HCv:o].view_as(bias_v), dXLp,
+                    flat[:, HCv:].view_as(XRp), dab[o:o + HCp].view_as(att_p), dab[o + HCp:].view_as(bias_p), None,
+                    None, None, None)
         dXLv, _, dattv, dbv = attn_backward_raw(XLv, XRv, att_v, bias_v, plan_v, ctx.heads, ctx.slope,
                                                 xcat[:, :HCv], stats[0:1], stats[1:2], g[:, :HCv],
                                                 defer=ctx.defer, dXR=flat[:, :HCv])

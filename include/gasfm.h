@@ -702,6 +702,39 @@ int gasfm_gchain_bwd(const gasfm_gchain* c, const float* xcat, const float* x1, 
                      float* dxcat, float* dprev, const gasfm_gchain_grads* d, float* scratch, uint32_t* counters,
                      void* stream);
 
+/* ---- the two GATv2 convs onto the single global node (global_attn.hip, round 4) ----
+ * graph_conv_view2global / graph_conv_scenepoint2global (layers.py:550-556, 566-572; PyG GATv2Conv,
+ * H = 4 heads, one target): e_j = att . leaky(XL[src_j] + XR), alpha = softmax_j(e_j) per head,
+ * out = sum_j alpha_j XL[src_j] + bias.  Up to two problems (views C = 256, points C = 16) per
+ * launch.  src NULL = rows 0..S-1.  Forward writes out [HC] and the statistics smax / ssum [H]
+ * (the softmax max and sum), or, when part != NULL (a sharded rank), the packed partial row
+ * [acc HC | max H | sum H] instead.  Backward (from gout, the saved out / smax / ssum) writes the
+ * dXL rows of the S sources (other rows untouched), dXR [HC] and datt [2 HC] = datt | dbias
+ * (dbias = gout).  S = 0 is allowed (a rank without sources: the empty state / zero gradients).
+ * XL, XR, att, bias, out, gout, dXL, datt 16-byte aligned; ldXL, ldDXL multiples of 4. */
+typedef struct gasfm_gatt_prob {
+  const float* XL;
+  int64_t ldXL;
+  const int32_t* src;
+  int32_t S, HC;
+  const float *XR, *att, *bias;
+  float *out, *smax, *ssum, *part;
+  const float* gout;
+  float* dXL;
+  int64_t ldDXL;
+  float *dXR, *datt;
+} gasfm_gatt_prob;
+int64_t gasfm_gatt_scratch_floats(int32_t nprob, const gasfm_gatt_prob* probs);
+/* counters: nprob zeroed self-resetting tickets. */
+int gasfm_gatt_fwd(int32_t nprob, const gasfm_gatt_prob* probs, float slope, float* scratch, uint32_t* counters,
+                   void* stream);
+int gasfm_gatt_bwd(int32_t nprob, const gasfm_gatt_prob* probs, float slope, float* scratch, uint32_t* counters,
+                   void* stream);
+/* The sharded forward's merge of the gathered partial rows: problem q's row of rank r at
+ * probs[q].part + r * stride floats (r < nrows), merged (max, rescaled sums) into out / smax / ssum
+ * (+ bias), the same on every rank.  One workgroup per problem, one launch. */
+int gasfm_gatt_merge(int32_t nprob, const gasfm_gatt_prob* probs, int32_t nrows, int64_t stride, void* stream);
+
 /* Reprojection error of compute_core_errors' "our_repro" (code/evaluation.py:8-31 ->
  * geo_utils.reprojection_error_with_points, geo_utils.py:371-391) over the E visibility edges:
  * err_e = || xy_e - (P_c X)_xy / (P_c X)_z ||, X = pflat(pts3D[:, p]), P = Ps_pix [m x 12]

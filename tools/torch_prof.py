@@ -1,6 +1,6 @@
 """torch.profiler view of one eager step (op names + input shapes + device time), GPU box.
 
-usage: python tools/torch_prof.py [--n N]
+usage: python tools/torch_prof.py [--n N] [--emulate-world W] [--stacks]
 """
 import argparse
 import os
@@ -18,19 +18,30 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=25_000)
     ap.add_argument("--rows", type=int, default=40)
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="rank 0 of a W-way points + cameras shard (bench.py --emulate-world)")
     ap.add_argument("--stacks", action="store_true",
                     help="also list the Python call sites of the aten ops that launch device work")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     sc = synthetic.windowed_scene(1000, args.n, seed=4)
     net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf()).to(dev)
-    data = gasfm_amd.SceneData.from_synthetic(sc).to(dev)
     cP = torch.randn((sc.m, 3, 4), device=dev)
     cX = torch.randn((4, sc.n), device=dev)
+    if args.emulate_world > 1:
+        from gasfm_amd import distributed as gdist
+        data = gdist.shard_scene(sc, 0, args.emulate_world, cameras=True, emulate=True).to(dev)
+        model = gdist.ShardedGraphAttnSfMNet(net, cameras=True)
+        cX = cX[:, data.point_slice].contiguous()
+    else:
+        data = gasfm_amd.SceneData.from_synthetic(sc).to(dev)
+        model = net
 
     def step():
-        p = net(data)
+        p = model(data)
         ((p["Ps_norm"] * cP).sum() + (p["pts3D"] * cX).sum()).backward()
+        if args.emulate_world > 1:
+            model.sync_grads()
         for q in net.parameters():
             q.grad = None
     for _ in range(3):
