@@ -20,11 +20,14 @@
 //               chunk partials of dh are handed to the slab's last-arriving workgroup (write-
 //               through stores, one relaxed agent-scope ticket per slab: reduce.hip's hand-off),
 //               which sums them in chunk order: dh leaves FINAL, no finish launch.  The LayerNorm
-//               backward that follows a level (F3's LN_A/B/C into dg, F2's LN_M into dx1) needs
-//               row sums over the whole vector: the level's LAST workgroup (a second ticket, over
-//               every slab of the launch) runs it once -- every load issued before the first use,
-//               one reduction round for all the LayerNorms -- and writes the finished vector and
-//               the LayerNorm gamma / beta gradients; the next level reads a plain dy.
+//               backward that follows a level (F3's LN_A/B/C into dg, F2's LN_M into dx1) is split
+//               by where its operands are: the slab's last arriver, holding the final dh of its 32
+//               columns, writes gv = relu'(.) gamma dh, the gamma / beta gradients of those columns
+//               and their two row-sum partials (sum gv, sum gv xh); the NEXT level's workgroups sum
+//               the partials in slab order (the same order in every workgroup) and finish dy for
+//               their own chunk of rows in a prologue that overlaps their W slab loads.  No
+//               launch-wide ticket and no one-workgroup tail (round 4's first version ran the
+//               LayerNorm backward in the level's last workgroup: ~9 us of the 18 us B2 / B3).
 //   Every phase issues all of its global loads before the first use (clamped addresses): a load
 //   behind a branch or behind a store to a possibly-aliasing pointer costs a full round trip.
 // No float atomics; every sum has a fixed order: deterministic, identical on every rank.
@@ -200,38 +203,41 @@ int launch_fwd(GnFwdArgs& a, hipStream_t st) {
 
 // --------------------------------------------------------------------------------- backward
 struct GnBwdProb {
-  const float* dy;   // [N] output gradient (final)
+  const float* dy;   // [N] output gradient (final; unused when the launch has a prologue)
   const float* x;    // [K] forward input row
   const float* gam;  // [K] LayerNorm of x (null: h = x)
   const float* bet;
   const float* W;    // [N, K]
   float* dW;         // [N, K]
-  float* db;         // [N] or null
-  float* dh;         // [K] W^T dy (final)
+  float* db;         // [N] or null (= dy, written by the slab-0 workgroups)
+  float* dh;         // [K] W^T dy, or with lnfin gv = relu'(.) gam (W^T dy) (final)
   float* ws;         // [chunks, K] chunk partials
   uint32_t* cnt;     // [slabs] self-resetting tickets
   int K, N, blk0, slabs, chunks;
   float eps;
+  // lnfin: the slab's last arriver also runs its columns' share of the LayerNorm backward of x:
+  // gv (into dh), dgam / dbet, and the two row-sum partials (sum gv, sum gv xh) into lnp[slab]
+  float* dgam;
+  float* dbet;
+  float* lnp;        // [slabs][2]
+  float* stats;      // (mean, rstd) of x, written by slab 0 (null: not needed)
+  int lnfin;
 };
-// Run by the launch's last workgroup once every dh is final:
-//   out = dres + sum_q LN_q backward of raw_q (relu mask), LN_q over the row x [F]
-// (raw_q: dh of problem q of this launch), plus the LayerNorms' gamma / beta gradients.
-struct GnFinish {
+// The launch's prologue (the previous level's LayerNorm backward, finished per row here):
+//   dy[n] = dres[n] + sum_q rstd (gv_q[n] - S1_q / F - xh[n] S2_q / F),  xh = (x - mean) rstd,
+//   S1_q / S2_q = the previous level's lnp rows summed in slab order (same order in every workgroup)
+struct GnPro {
+  const float* gv[kMaxRaw];
+  const float* lnp[kMaxRaw];
+  const float* stats;  // (mean, rstd) of x
   const float* x;
-  const float* dres;
-  const float* raw[kMaxRaw];
-  const float* gam[kMaxRaw];
-  const float* bet[kMaxRaw];
-  float* dgam[kMaxRaw];
-  float* dbet[kMaxRaw];
-  float* out;
-  uint32_t* cnt;  // the launch's ticket (null: no finish)
-  int F, nraw, slabs;
-  float eps;
+  const float* dres;   // or null
+  float* out;          // or null: dy rows written by the slab-0 workgroups (d prev)
+  int nq, F, slabs;
 };
 struct GnBwdArgs {
   GnBwdProb p[kMaxProb];
-  GnFinish f;
+  GnPro pro;
   int nprob;
 };
 
@@ -246,65 +252,9 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// the launch's finish (one workgroup, F <= kMaxK): every load first, one reduction round for all
-// the LayerNorms' row sums
-__device__ void gnode_finish(const GnFinish& f, float* scratch) {
-  const int F = f.F;
-  float xv[kPer], acc[kPer], raw[kMaxRaw][kPer], ga[kMaxRaw][kPer], be[kMaxRaw][kPer];
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int j = int(threadIdx.x) + 256 * u, jc = j < F ? j : 0;
-    xv[u] = f.x[jc];
-    acc[u] = f.dres ? f.dres[jc] : 0.f;
-#pragma unroll
-    for (int q = 0; q < kMaxRaw; ++q) {
-      const bool on = q < f.nraw;
-      raw[q][u] = on ? ld_sc1(f.raw[q] + jc) : 0.f;
-      ga[q][u] = on ? f.gam[q][jc] : 0.f;
-      be[q][u] = on ? f.bet[q][jc] : 0.f;
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < kPer; ++u)
-    if (int(threadIdx.x) + 256 * u >= F) xv[u] = 0.f;
-  float mean, rstd;
-  row_stats(xv, F, f.eps, scratch, mean, rstd);
-  float xh[kPer], sv[2 * kMaxRaw];
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) xh[u] = (xv[u] - mean) * rstd;
-#pragma unroll
-  for (int q = 0; q < kMaxRaw; ++q) {
-    sv[2 * q] = sv[2 * q + 1] = 0.f;
-#pragma unroll
-    for (int u = 0; u < kPer; ++u) {
-      const int j = int(threadIdx.x) + 256 * u;
-      const float d = (j < F && q < f.nraw && fmaf(xh[u], ga[q][u], be[q][u]) > 0.f) ? raw[q][u] : 0.f;
-      if (j < F && q < f.nraw) {
-        f.dgam[q][j] = d * xh[u];
-        f.dbet[q][j] = d;
-      }
-      raw[q][u] = d * ga[q][u];  // now gv
-      sv[2 * q] += raw[q][u];
-      sv[2 * q + 1] = fmaf(raw[q][u], xh[u], sv[2 * q + 1]);
-    }
-  }
-  block_sums<2 * kMaxRaw>(sv, scratch);
-#pragma unroll
-  for (int q = 0; q < kMaxRaw; ++q) {
-    if (q >= f.nraw) continue;
-    const float s1 = sv[2 * q] / F, s2 = sv[2 * q + 1] / F;
-#pragma unroll
-    for (int u = 0; u < kPer; ++u) acc[u] += rstd * (raw[q][u] - s1 - xh[u] * s2);
-  }
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int j = int(threadIdx.x) + 256 * u;
-    if (j < F) f.out[j] = acc[u];
-  }
-}
-
 template <int RPT>  // rows per thread: a chunk is 32 RPT rows
 __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
+  static_assert(32 * RPT == kBT, "one dy row per thread");
   __shared__ float dys[32 * RPT];
   __shared__ float4 red[kBT];
   __shared__ float scratch[4 * 2 * kMaxRaw + 8];
@@ -320,18 +270,33 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
   const int K = p.K, N = p.N;
   const int col = slab * kSW + 4 * cl;
   const int row0 = chunk * 32 * RPT;
-  // 1. every load first: the workgroup's W slab rows, the chunk's dy, the input row (+ affine)
+  const int nrow = row0 + int(threadIdx.x), nrc = nrow < N ? nrow : N - 1;  // this thread's dy row
+  const GnPro& pr = a.pro;
+  const bool pro = pr.nq > 0;
+  // 1. every load first: the prologue's operands (they gate dy), the workgroup's W slab rows, the
+  // input row (+ affine)
+  float dres = 0.f, xr = 0.f, gvr[kMaxRaw], lp[2 * kMaxRaw], st0 = 0.f, st1 = 0.f, dyv = 0.f;
+  if (pro) {
+    dres = pr.dres ? pr.dres[nrc] : 0.f;
+    xr = pr.x[nrc];
+    st0 = pr.stats[0];
+    st1 = pr.stats[1];
+    const int tc = int(threadIdx.x) < pr.slabs ? int(threadIdx.x) : 0;
+#pragma unroll
+    for (int q = 0; q < kMaxRaw; ++q) {
+      const bool on = q < pr.nq;
+      gvr[q] = on ? pr.gv[q][nrc] : 0.f;
+      lp[2 * q] = on ? pr.lnp[q][2 * tc] : 0.f;
+      lp[2 * q + 1] = on ? pr.lnp[q][2 * tc + 1] : 0.f;
+    }
+  } else {
+    dyv = p.dy[nrc];
+  }
   float4 w[RPT];
 #pragma unroll
   for (int r = 0; r < RPT; ++r) {
     const int n = row0 + rl + 32 * r;
     w[r] = *reinterpret_cast<const float4*>(p.W + int64_t(n < N ? n : N - 1) * K + col);
-  }
-  float dyv[(32 * RPT + kBT - 1) / kBT];
-#pragma unroll
-  for (int k = 0; k < (32 * RPT + kBT - 1) / kBT; ++k) {
-    const int t = int(threadIdx.x) + k * kBT, n = row0 + t;
-    dyv[k] = p.dy[n < N ? n : N - 1];
   }
   const float4 x4 = *reinterpret_cast<const float4*>(p.x + col);
   const bool ln = p.gam != nullptr;
@@ -349,23 +314,34 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
     for (int u = 0; u < kPer; ++u)
       if (int(threadIdx.x) + 256 * u >= K) xv[u] = 0.f;
   }
+  // 2. dy of the chunk's rows
+  if (pro) {
+    if (int(threadIdx.x) >= pr.slabs) {
 #pragma unroll
-  for (int k = 0; k < (32 * RPT + kBT - 1) / kBT; ++k) {
-    const int t = int(threadIdx.x) + k * kBT;
-    if (t < 32 * RPT) dys[t] = row0 + t < N ? dyv[k] : 0.f;
+      for (int k = 0; k < 2 * kMaxRaw; ++k) lp[k] = 0.f;
+    }
+    block_sums<2 * kMaxRaw>(lp, scratch);
+    const float xh = (xr - st0) * st1, invF = 1.f / pr.F;
+    float d = dres;
+#pragma unroll
+    for (int q = 0; q < kMaxRaw; ++q)
+      if (q < pr.nq) d += st1 * (gvr[q] - lp[2 * q] * invF - xh * lp[2 * q + 1] * invF);
+    dyv = d;
+    if (slab == 0 && pr.out && nrow < N) pr.out[nrow] = d;
   }
-  // 2. h over the thread's 4 slab columns
-  float4 h4 = x4;
+  dys[threadIdx.x] = nrow < N ? dyv : 0.f;
+  // 3. h over the thread's 4 slab columns
+  float4 h4 = x4, xh4 = x4;
+  float mean = 0.f, rstd = 0.f;
   if (ln) {
-    float mean, rstd;
+    __syncthreads();  // the prologue's block_sums scratch before row_stats reuses it
     row_stats(xv, K, p.eps, scratch, mean, rstd);
-    h4 = make_float4(fmaxf(fmaf((x4.x - mean) * rstd, g4.x, b4.x), 0.f),
-                     fmaxf(fmaf((x4.y - mean) * rstd, g4.y, b4.y), 0.f),
-                     fmaxf(fmaf((x4.z - mean) * rstd, g4.z, b4.z), 0.f),
-                     fmaxf(fmaf((x4.w - mean) * rstd, g4.w, b4.w), 0.f));
+    xh4 = make_float4((x4.x - mean) * rstd, (x4.y - mean) * rstd, (x4.z - mean) * rstd, (x4.w - mean) * rstd);
+    h4 = make_float4(fmaxf(fmaf(xh4.x, g4.x, b4.x), 0.f), fmaxf(fmaf(xh4.y, g4.y, b4.y), 0.f),
+                     fmaxf(fmaf(xh4.z, g4.z, b4.z), 0.f), fmaxf(fmaf(xh4.w, g4.w, b4.w), 0.f));
   }
   __syncthreads();  // dys
-  // 3. this thread's share of dh (the dW rows are stored last: a ticket's s_waitcnt vmcnt(0)
+  // 4. this thread's share of dh (the dW rows are stored last: a ticket's s_waitcnt vmcnt(0)
   // would otherwise wait for them too)
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   float dr[RPT];
@@ -386,11 +362,9 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
       if (n < N)
         *reinterpret_cast<float4*>(p.dW + int64_t(n) * K + col) = make_float4(d * h4.x, d * h4.y, d * h4.z, d * h4.w);
     }
-    if (p.db && slab == 0)
-      for (int t = threadIdx.x; t < 32 * RPT; t += kBT)
-        if (row0 + t < N) p.db[row0 + t] = dys[t];
+    if (p.db && slab == 0 && nrow < N) p.db[nrow] = dys[threadIdx.x];
   };
-  // 4. the 32 row lanes summed in lane order
+  // 5. the 32 row lanes summed in lane order
   red[threadIdx.x] = s;
   __syncthreads();
   float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -404,9 +378,8 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
       tot.w += v.w;
     }
   }
-  const bool fin = a.f.cnt != nullptr;
   if (p.chunks > 1) {
-    // 5. the chunk partial to the slab's last arriver (write-through stores, one ticket)
+    // 6. the chunk partial to the slab's last arriver (write-through stores, one ticket)
     if (threadIdx.x < 8) st_sc1(p.ws + int64_t(chunk) * K + col, tot);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -440,29 +413,40 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
     }
     if (threadIdx.x == 0) __hip_atomic_store(p.cnt + slab, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // 6. the slab's final dh (write-through when the launch's finish reads it)
+  // 7. the slab's final dh, or its columns of the LayerNorm backward of x
   if (threadIdx.x < 8) {
-    if (fin)
-      st_sc1(p.dh + col, tot);
-    else
+    if (p.lnfin) {
+      const float t4[4] = {tot.x, tot.y, tot.z, tot.w};
+      const float xh[4] = {xh4.x, xh4.y, xh4.z, xh4.w};
+      const float gg[4] = {g4.x, g4.y, g4.z, g4.w};
+      const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
+      float d[4], gv[4], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        d[k] = fmaf(xh[k], gg[k], bb[k]) > 0.f ? t4[k] : 0.f;
+        gv[k] = d[k] * gg[k];
+        s1 += gv[k];
+        s2 = fmaf(gv[k], xh[k], s2);
+      }
+      *reinterpret_cast<float4*>(p.dh + col) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+      *reinterpret_cast<float4*>(p.dgam + col) = make_float4(d[0] * xh[0], d[1] * xh[1], d[2] * xh[2], d[3] * xh[3]);
+      *reinterpret_cast<float4*>(p.dbet + col) = make_float4(d[0], d[1], d[2], d[3]);
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) {
+        s1 += __shfl_xor(s1, o);
+        s2 += __shfl_xor(s2, o);
+      }
+      if (threadIdx.x == 0) {
+        p.lnp[2 * slab] = s1;
+        p.lnp[2 * slab + 1] = s2;
+        if (slab == 0 && p.stats) {
+          p.stats[0] = mean;
+          p.stats[1] = rstd;
+        }
+      }
+    } else {
       *reinterpret_cast<float4*>(p.dh + col) = tot;
-  }
-  if (!fin) {
-    store_dw();
-    return;
-  }
-  // 7. the launch's last slab runs the finish
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t t = __hip_atomic_fetch_add(a.f.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag = t == uint32_t(a.f.slabs - 1) ? 1u : 0u;
-  }
-  __syncthreads();
-  if (flag != 0u) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    gnode_finish(a.f, scratch);
-    if (threadIdx.x == 0) __hip_atomic_store(a.f.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   store_dw();
 }
@@ -486,11 +470,6 @@ int launch_bwd(GnBwdArgs& a, float*& ws, uint32_t*& cnt, hipStream_t st, const c
     blocks += p.slabs * p.chunks;
   }
   for (int q = a.nprob; q < kMaxProb; ++q) a.p[q].blk0 = blocks;
-  if (a.f.nraw > 0) {
-    a.f.cnt = cnt++;
-    a.f.slabs = 0;
-    for (int q = 0; q < a.nprob; ++q) a.f.slabs += a.p[q].slabs;
-  }
   hipLaunchKernelGGL(gnode_bwd_kernel<kRPT>, dim3(blocks), dim3(kBT), 0, st, a);
   return launch_status(where);
 }
@@ -524,18 +503,20 @@ static int gchain_check(const gasfm_gchain* c) {
 
 extern "C" int64_t gasfm_gchain_scratch_floats(const gasfm_gchain* c) {
   if (!c) return 0;
-  // raw vectors: dh_D, dh_E, dh_A, dh_B, dh_C, dh_2, dg, dx1; chunk partials of the widest level
-  const int64_t vec = int64_t(c->NB) + c->NC + 6 * int64_t(c->G);
+  // vectors: dh_D, dh_E, gv_A, gv_B, gv_C, gv_2; LayerNorm row-sum partials and statistics; chunk
+  // partials of every level (each level its own range)
+  const int64_t vec = int64_t(c->NB) + c->NC + 4 * int64_t(c->G);
+  const int64_t lnp = 4 * 2 * int64_t(c->G / kSW) + 8;
   const int64_t l1 = int64_t(chunks_of(c->ND)) * c->NB + int64_t(chunks_of(c->NE)) * c->NC;
   const int64_t l2 = int64_t(chunks_of(c->NA) + chunks_of(c->NB) + chunks_of(c->NC)) * c->G;
   const int64_t l3 = int64_t(chunks_of(c->G)) * c->G;
   const int64_t l4 = int64_t(chunks_of(c->G)) * c->Kc;
-  return vec + l1 + l2 + l3 + l4 + 64;
+  return vec + lnp + l1 + l2 + l3 + l4 + 64;
 }
 
 extern "C" int32_t gasfm_gchain_counters(const gasfm_gchain* c) {
   if (!c) return 0;
-  return (c->NB + c->NC + 4 * c->G + c->Kc) / kSW + 8;  // per-slab tickets + one per finishing level
+  return (c->NB + c->NC + 4 * c->G + c->Kc) / kSW + 8;  // per-slab tickets
 }
 
 extern "C" int gasfm_gchain_fwd(const gasfm_gchain* c, const float* xcat, const float* prev, float* x1, float* g,
@@ -581,70 +562,76 @@ extern "C" int gasfm_gchain_bwd(const gasfm_gchain* c, const float* xcat, const 
                       d->dbWC && d->dWD && d->dbD && d->dWE && d->dbE,
                   "gasfm_gchain_bwd: null hub pointer");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int slabsG = c->G / kSW;
   float* dhD = scratch;
   float* dhE = dhD + c->NB;
-  float* dhA = dhE + c->NC;
-  float* dhB = dhA + c->G;
-  float* dhC = dhB + c->G;
-  float* dh2 = dhC + c->G;
-  float* dg = dh2 + c->G;
-  float* dx1 = dprev ? dprev : dg + c->G;
-  float* ws = dg + 2 * c->G;
+  float* gvA = dhE + c->NC;
+  float* gvB = gvA + c->G;
+  float* gvC = gvB + c->G;
+  float* gv2 = gvC + c->G;
+  float* lnA = gv2 + c->G;  // [slabsG][2] each
+  float* lnB = lnA + 2 * slabsG;
+  float* lnC = lnB + 2 * slabsG;
+  float* ln2 = lnC + 2 * slabsG;
+  float* stg = ln2 + 2 * slabsG;  // (mean, rstd) of g, then of x1
+  float* st1 = stg + 2;
+  float* ws = stg + 8;
   uint32_t* cnt = counters;
   int s;
   if (hub) {  // B1: the two lin_r rows
     GnBwdArgs a{};
     a.nprob = 2;
-    a.p[0] = GnBwdProb{dxrv, xv, nullptr, nullptr, c->WD, d->dWD, d->dbD, dhD, nullptr, nullptr, c->NB, c->ND};
-    a.p[1] = GnBwdProb{dxrp, xp, nullptr, nullptr, c->WE, d->dWE, d->dbE, dhE, nullptr, nullptr, c->NC, c->NE};
+    a.p[0] = GnBwdProb{dxrv, xv, nullptr, nullptr, c->WD, d->dWD, d->dbD, dhD};
+    a.p[0].K = c->NB, a.p[0].N = c->ND;
+    a.p[1] = GnBwdProb{dxrp, xp, nullptr, nullptr, c->WE, d->dWE, d->dbE, dhE};
+    a.p[1].K = c->NC, a.p[1].N = c->NE;
     s = launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(lin_r)");
     if (s != GASFM_OK) return s;
   }
-  {  // B2: the LayerNorm -> Linear consumers of g; its last workgroup finishes dg = dskip + their
-     // LayerNorm backwards (and the LayerNorms' gamma / beta gradients)
+  {  // B2: the LayerNorm -> Linear consumers of g; each slab's last arriver runs its columns of
+     // their LayerNorm backwards (gv, gamma / beta gradients, row-sum partials)
     GnBwdArgs a{};
     a.nprob = hub ? 3 : 1;
-    a.p[0] = GnBwdProb{dsg, g, c->gA, c->bA, c->WA, d->dWA, nullptr, dhA, nullptr, nullptr, c->G, c->NA};
-    a.p[0].eps = c->eps_h;
+    auto lnprob = [&](const float* dy, const float* gam, const float* bet, const float* W, float* dW, float* db,
+                      int N, float* gv, float* dgam, float* dbet, float* lnp, float* stats) {
+      GnBwdProb p{dy, g, gam, bet, W, dW, db, gv};
+      p.K = c->G, p.N = N, p.eps = c->eps_h;
+      p.dgam = dgam, p.dbet = dbet, p.lnp = lnp, p.stats = stats, p.lnfin = 1;
+      return p;
+    };
+    a.p[0] = lnprob(dsg, c->gA, c->bA, c->WA, d->dWA, nullptr, c->NA, gvA, d->dgA, d->dbA, lnA, stg);
     if (hub) {
-      a.p[1] = GnBwdProb{dhD, g, c->gB, c->bB, c->WB, d->dWB, d->dbWB, dhB, nullptr, nullptr, c->G, c->NB};
-      a.p[2] = GnBwdProb{dhE, g, c->gC, c->bC, c->WC, d->dWC, d->dbWC, dhC, nullptr, nullptr, c->G, c->NC};
-      a.p[1].eps = a.p[2].eps = c->eps_h;
+      a.p[1] = lnprob(dhD, c->gB, c->bB, c->WB, d->dWB, d->dbWB, c->NB, gvB, d->dgB, d->dbB, lnB, nullptr);
+      a.p[2] = lnprob(dhE, c->gC, c->bC, c->WC, d->dWC, d->dbWC, c->NC, gvC, d->dgC, d->dbC, lnC, nullptr);
     }
-    GnFinish& f = a.f;
-    f.x = g;
-    f.dres = dskip;
-    f.F = c->G;
-    f.eps = c->eps_h;
-    f.nraw = hub ? 3 : 1;
-    f.raw[0] = dhA, f.gam[0] = c->gA, f.bet[0] = c->bA, f.dgam[0] = d->dgA, f.dbet[0] = d->dbA;
-    if (hub) {
-      f.raw[1] = dhB, f.gam[1] = c->gB, f.bet[1] = c->bB, f.dgam[1] = d->dgB, f.dbet[1] = d->dbB;
-      f.raw[2] = dhC, f.gam[2] = c->gC, f.bet[2] = c->bC, f.dgam[2] = d->dgC, f.dbet[2] = d->dbC;
-    }
-    f.out = dg;
     s = launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(hub)");
     if (s != GASFM_OK) return s;
   }
-  {  // B3: the MLP Linear on dg; its last workgroup finishes dx1 = dg + LN_M backward
+  {  // B3: the MLP Linear on dg (= dskip + the hub LayerNorms' backward, finished per row in the
+     // prologue; written to db2, which IS dg); the slab last arrivers run LN_M's columns
     GnBwdArgs a{};
     a.nprob = 1;
-    a.p[0] = GnBwdProb{dg, x1, c->gM, c->bM, c->W2, d->dW2, d->db2, dh2, nullptr, nullptr, c->G, c->G};
-    a.p[0].eps = c->eps_m;
-    GnFinish& f = a.f;
-    f.x = x1;
-    f.dres = dg;
-    f.F = c->G;
-    f.eps = c->eps_m;
-    f.nraw = 1;
-    f.raw[0] = dh2, f.gam[0] = c->gM, f.bet[0] = c->bM, f.dgam[0] = d->dgM, f.dbet[0] = d->dbM;
-    f.out = dx1;
+    GnBwdProb& p = a.p[0];
+    p = GnBwdProb{nullptr, x1, c->gM, c->bM, c->W2, d->dW2, d->db2, gv2};
+    p.K = c->G, p.N = c->G, p.eps = c->eps_m;
+    p.dgam = d->dgM, p.dbet = d->dbM, p.lnp = ln2, p.stats = st1, p.lnfin = 1;
+    GnPro& pr = a.pro;
+    pr.nq = hub ? 3 : 1;
+    pr.gv[0] = gvA, pr.lnp[0] = lnA;
+    pr.gv[1] = gvB, pr.lnp[1] = lnB;
+    pr.gv[2] = gvC, pr.lnp[2] = lnC;
+    pr.stats = stg, pr.x = g, pr.dres = dskip, pr.out = nullptr, pr.F = c->G, pr.slabs = slabsG;
     s = launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(mlp)");
     if (s != GASFM_OK) return s;
   }
-  // B4: proj_view_and_scenepoint2global on dx1 (= d prev): d xcat
+  // B4: proj_view_and_scenepoint2global on dx1 = dg + LN_M backward (prologue; = d b1 = d prev)
   GnBwdArgs a{};
   a.nprob = 1;
-  a.p[0] = GnBwdProb{dx1, xcat, nullptr, nullptr, c->W1, d->dW1, d->db1, dxcat, nullptr, nullptr, c->Kc, c->G};
+  a.p[0] = GnBwdProb{nullptr, xcat, nullptr, nullptr, c->W1, d->dW1, d->db1, dxcat};
+  a.p[0].K = c->Kc, a.p[0].N = c->G;
+  GnPro& pr = a.pro;
+  pr.nq = 1;
+  pr.gv[0] = gv2, pr.lnp[0] = ln2;
+  pr.stats = st1, pr.x = x1, pr.dres = d->db2, pr.out = dprev, pr.F = c->G, pr.slabs = slabsG;
   return launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(proj)");
 }

@@ -70,7 +70,8 @@ def test_global_pair_matches_fp64(device, nv, Sv, sub_v, npt, Sp, sub_p):
     for nm, a, r in zip(names, got, leaves64):
         ga, gr = a.grad.double().cpu(), r.grad
         err = (ga - gr).norm().item()
-        assert err <= 1e-4 * gr.norm().item() + 1e-7, f"{nm}: {err:.3e} vs |ref| {gr.norm().item():.3e}"
+        # + 1e-5: with one source alpha = 1 and dXR, datt vanish analytically (fp32 leaves ~1e-6)
+        assert err <= 1e-4 * gr.norm().item() + 1e-5, f"{nm}: {err:.3e} vs |ref| {gr.norm().item():.3e}"
     if sub_v:  # rows that are not sources get exactly zero
         mask = torch.ones(nv, dtype=torch.bool)
         mask[v["src"]] = False
