@@ -1034,6 +1034,20 @@ __device__ __forceinline__ void prod_c2(const float4* __restrict__ Q, const f32x
 #ifndef GASFM_PBWD_LW4
 #define GASFM_PBWD_LW4 0
 #endif
+// 1: no exec-mask branches inside the tile loop (round 4).  The work item is made wave-uniform
+// (scalar registers), so the next-tile choice is a scalar select; the dead-row masks of the
+// attention weights, the LayerNorm backward input, the dW / dWp operands and the dSv sums are
+// multiplications by a 0 / 1 factor (every masked value is finite: dead rows are clamped copies of
+// a live row) instead of selects the compiler turned into branches around LDS reads and v_exp,
+// each of which ended a basic block and with it the scheduler's freedom to interleave the MFMA
+// chains with the VALU work.
+#ifndef GASFM_PBWD_BF
+#define GASFM_PBWD_BF 0
+#endif
+__device__ __forceinline__ gasfm_work_item uniform_item(const gasfm_work_item& w) {
+  return gasfm_work_item{__builtin_amdgcn_readfirstlane(w.seg), __builtin_amdgcn_readfirstlane(w.begin),
+                         __builtin_amdgcn_readfirstlane(w.end), __builtin_amdgcn_readfirstlane(w.slot)};
+}
 template <bool LN, bool RES, bool EPI, bool DWP>
 __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kernel(
     const float* __restrict__ P, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
@@ -1131,6 +1145,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   gasfm_work_item w{0, 0, 0, -1};
   if (gw < n_items) {
     w = items[gw];
+    if (GASFM_PBWD_BF) w = uniform_item(w);
     if (w.begin < w.end) issue(w.begin, rows_at(w, w.begin));
   }
   for (int it = gw; it < n_items; it += nw) {
@@ -1172,6 +1187,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
     gasfm_work_item wn{0, 0, 0, -1};
     const bool more = it + nw < n_items;
     if (more) wn = items[it + nw];
+    if (GASFM_PBWD_BF) wn = uniform_item(wn);
     if (w.begin >= w.end && more && wn.begin < wn.end) issue(wn.begin, rows_at(wn, wn.begin));
     for (int64_t row0 = w.begin; row0 < w.end; row0 += TR) {
       const int nrows = rows_at(w, row0);
@@ -1181,7 +1197,12 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
         RT[1] = nRT[1];
       }
       const float2 p0t = nP0;
-      {  // the next tile (this item's, else the next item's first; the last one re-reads itself)
+      if (GASFM_PBWD_BF) {  // the same choice as scalar selects (w, wn are wave-uniform)
+        const bool in_item = row0 + TR < w.end, nx = more && wn.begin < wn.end;
+        const int64_t r1 = in_item ? row0 + TR : (nx ? int64_t(wn.begin) : row0);
+        const int64_t e1 = in_item ? int64_t(w.end) : (nx ? int64_t(wn.end) : int64_t(w.end));
+        issue(r1, int(e1 - r1 < TR ? e1 - r1 : TR));
+      } else {  // the next tile (this item's, else the next item's first; the last one re-reads itself)
         int64_t r1 = row0;
         int n1 = nrows;
         if (row0 + TR < w.end) {
@@ -1194,6 +1215,11 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
         issue(r1, n1);
       }
       const bool valid = c < nrows;
+      // (GASFM_PBWD_BF) 0 / 1 factors: edge c live (T layout), rows 4 g + r live (C layout)
+      const float vmask = valid ? 1.f : 0.f;
+      float lm[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lm[r] = 4 * g + r < nrows ? 1.f : 0.f;
       // C layouts of P, dXLp, dRes (raw) through LDS, before P's slabs are normalised in place
       f32x4 PC[2], XC[2], RC[2];
       to_c(0, PT, PC);
@@ -1242,7 +1268,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
         }
         p += __shfl_xor(p, 16);
         da += __shfl_xor(da, 16);
-        const float alpha = valid ? __expf(p - M[q]) * inv[q] : 0.f;
+        const float alpha = GASFM_PBWD_BF ? __expf(p - M[q]) * inv[q] * vmask : (valid ? __expf(p - M[q]) * inv[q] : 0.f);
         const float de = alpha * (da - delta[q]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1279,7 +1305,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
         for (int nt = 0; nt < 2; ++nt) {
           xh[nt] = LN ? (PC[nt][r] - mean) * rstd : PC[nt][r];
           ph[nt][r] = LN ? fmaxf(fmaf(xh[nt], gC[nt], bC[nt]), 0.f) : xh[nt];
-          float dy = live ? dph[nt][r] : 0.f;
+          float dy = GASFM_PBWD_BF ? dph[nt][r] * lm[r] : (live ? dph[nt][r] : 0.f);
           if (LN) {
             dy = (fmaf(xh[nt], gC[nt], bC[nt]) > 0.f) ? dy : 0.f;
             dg[nt] = fmaf(dy, xh[nt], dg[nt]);
@@ -1324,8 +1350,8 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
         for (int r = 0; r < 4; ++r) {
           const bool live = 4 * g + r < nrows;
           // the item's column sums of dP (dSv) live in LDS: no registers held across tiles
-          Ls[0] += live ? dv[r][0] : 0.f;
-          Ls[1] += live ? dv[r][1] : 0.f;
+          Ls[0] += GASFM_PBWD_BF ? dv[r][0] * lm[r] : (live ? dv[r][0] : 0.f);
+          Ls[1] += GASFM_PBWD_BF ? dv[r][1] * lm[r] : (live ? dv[r][1] : 0.f);
           if (!GASFM_PBWD_EPI_T) {  // A/B: 16-lane sums per row (DPP), lanes c = 0, 1 store
             const float s0 = sum16(fmaf(dv[r][0], V[4 * F + c], dv[r][1] * V[4 * F + 16 + c]));
             const float s1 = sum16(fmaf(dv[r][0], V[5 * F + c], dv[r][1] * V[5 * F + 16 + c]));
@@ -1359,7 +1385,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
 #pragma unroll
       for (int ft = 0; ft < 2; ++ft)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) XC[ft][r] = 4 * g + r < nrows ? XC[ft][r] : 0.f;
+        for (int r = 0; r < 4; ++r) XC[ft][r] = GASFM_PBWD_BF ? XC[ft][r] * lm[r] : (4 * g + r < nrows ? XC[ft][r] : 0.f);
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2) {
 #pragma unroll
@@ -1379,7 +1405,9 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
         for (int ft = 0; ft < 2; ++ft) {
           float rr[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) rr[r] = 4 * g + r < nrows ? T2[(4 * g + r) * LDT + 16 * ft + c] : 0.f;
+          for (int r = 0; r < 4; ++r)
+            rr[r] = GASFM_PBWD_BF ? T2[(4 * g + r) * LDT + 16 * ft + c] * lm[r]
+                                  : (4 * g + r < nrows ? T2[(4 * g + r) * LDT + 16 * ft + c] : 0.f);
           f32x4 ap[2] = {zero4(), zero4()};
 #pragma unroll
           for (int s2 = 0; s2 < 4; ++s2)

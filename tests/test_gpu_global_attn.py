@@ -67,11 +67,17 @@ def test_global_pair_matches_fp64(device, nv, Sv, sub_v, npt, Sp, sub_p):
     torch.testing.assert_close(x.double().cpu(), x64.detach(), rtol=0, atol=2e-5 * x64.abs().max().item() + 1e-6)
     x.backward(gx.float().to(device))
     names = ("XLv", "XRv", "att_v", "bias_v", "XLp", "XRp", "att_p", "bias_p")
-    for nm, a, r in zip(names, got, leaves64):
+    # absolute floor per conv: with one source alpha = 1 and dXR, datt vanish analytically; fp32
+    # leaves the cancellation of gout . XL against gout . (out - bias), a rounding of the size
+    # eps32 |gout| |XL[src]| (measured 2.4e-5 for att_v at C = 256, where this floor is 1.2e-4)
+    HCv = ov.shape[1]
+    floor = [1e-5 + 2.0 ** -23 * gx[:, sl].norm().item() * d["XL"][d["src"]].norm().item()
+             for sl, d in ((slice(0, HCv), v), (slice(HCv, None), p))]
+    for k, (nm, a, r) in enumerate(zip(names, got, leaves64)):
         ga, gr = a.grad.double().cpu(), r.grad
         err = (ga - gr).norm().item()
-        # + 1e-5: with one source alpha = 1 and dXR, datt vanish analytically (fp32 leaves ~1e-6)
-        assert err <= 1e-4 * gr.norm().item() + 1e-5, f"{nm}: {err:.3e} vs |ref| {gr.norm().item():.3e}"
+        bound = 1e-4 * gr.norm().item() + floor[k // 4]
+        assert err <= bound, f"{nm}: {err:.3e} vs |ref| {gr.norm().item():.3e} (bound {bound:.3e})"
     if sub_v:  # rows that are not sources get exactly zero
         mask = torch.ones(nv, dtype=torch.bool)
         mask[v["src"]] = False
@@ -172,9 +178,10 @@ def test_merge_of_gathered_rows_matches_fp64(device, W):
         probs = []
         for d, off, L in ((v, 0, Lv), (p, ov, Lp)):
             n = d["XL"].shape[0]
-            lo, hi = (n * r) // W, (n * (r + 1)) // W
-            if W == 8 and r == 5:
-                lo = hi  # a rank without sources
+            bounds = [(n * k) // W for k in range(W + 1)]
+            if W == 8:
+                bounds[6] = bounds[5]  # rank 5 owns no sources (rank 6 takes its range)
+            lo, hi = bounds[r], bounds[r + 1]
             XL = d["XL"][lo:hi].float().to(device)
             probs.append(dict(XL=XL if hi > lo else torch.empty((0, L - 2 * H), device=device), src=None, S=hi - lo,
                               XR=d["XR"].float().to(device), att=d["att"].float().to(device).reshape(-1),
