@@ -64,7 +64,7 @@ _SIGS = {
                                     _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
     "gasfm_edge_cam_pbwd_ex": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _f32, _vp, _i64, _vp, _vp, _f32,
                                       _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _vp, _i64,
-                                      _vp, _vp, _i64, _vp, _i32, _f32, _vp, _vp, _vp, _vp, _i32, _vp]),
+                                      _vp, _vp, _i64, _vp, _i32, _f32, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     "gasfm_edge_cam_fwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32,
                                   _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
     "gasfm_edge_cam_bwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _vp, _i64,
@@ -673,7 +673,8 @@ def edge_cam_pbwd_part_shape(n_items, dwp_cols=0):
 
 
 def edge_cam_pbwd(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, scale, XR, att, bias, slope, out, seg_max, seg_sum, gout,
-                  plan_items, n_items, dXLp, dRes, dP, dXR, part_dxr, part, ldStat=4, epi=None, dwp=None):
+                  plan_items, n_items, dXLp, dRes, dP, dXR, part_dxr, part, ldStat=4, epi=None, dwp=None,
+                  dxl_pos=None):
     """The camera attention's backward and the block's edge prologue backward in one pass
     (csrc/edge_cam.hip edge_cam_pbwd): dP, dXR (+ split partials), part rows
     [dW 64x32 | db 64 | dgamma 32 | dbeta 32 | datt 32 | dbias 32] per workgroup.
@@ -681,7 +682,8 @@ def edge_cam_pbwd(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, scale, XR, att, bias, slo
     epi = (We, scale_e, dSv, part_dsv, dP0 or None): also the previous block's edge-epilogue
     gradients from this dP (dSv rows / split-camera partial rows of the same plan, dP0).
     dwp = P0 or None (requires ln_w and dRes): also this block's lin_proj weight gradient,
-    [32 x (32 | 34)] appended to each part row (part has edge_cam_pbwd_part_shape(n, dwp=...) columns)."""
+    [32 x (32 | 34)] appended to each part row (part has edge_cam_pbwd_part_shape(n, dwp=...) columns).
+    dxl_pos (int32 [E] or None): dXLp rows in point-segment order, edge e's at dxl_pos[e]."""
     _req(P, "P", 32)
     ldXR = _rows32(XR, "XR")
     We = dSv = part_dsv = dP0 = None
@@ -703,7 +705,8 @@ def edge_cam_pbwd(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, scale, XR, att, bias, slo
                                       slope, _p(out), out.stride(0), _p(seg_max), _p(seg_sum), ldStat, _p(gout),
                                       gout.stride(0), _p(plan_items), n_items, _p(dXLp), dXLp.stride(0), _p(dRes),
                                       _p(dP), _p(dXR), dXR.stride(0), _p(part_dxr), _p(part), part.stride(0), _p(We),
-                                      ldWe, scale_e, _p(dSv), _p(part_dsv), _p(dP0), _p(P0), ldWpo, _stream(P))
+                                      ldWe, scale_e, _p(dSv), _p(part_dsv), _p(dP0), _p(P0), ldWpo, _p(dxl_pos),
+                                      _stream(P))
     check(st, "gasfm_edge_cam_pbwd")
 
 

@@ -379,10 +379,12 @@ def combine_partials(gathered, world, N, heads, bias, combine_items):
 
 
 def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, gout, dXL=None, xl_sorted=False,
-                      defer=False, dXR=None):
+                      defer=False, dXR=None, dxl_sorted=False):
     """Launch the backward kernels; returns (dXL, dXR, datt[HC], dbias[HC]).
 
-    dXL is always in source-row (edge) order; xl_sorted says XL itself is in segment order.
+    dXL is in source-row (edge) order; xl_sorted says XL itself is in segment order.  dxl_sorted
+    (with xl_sorted, round 4): dXL in segment order too, the layout of XL (row j = source row
+    plan.perm[j]): written streaming instead of scattered through perm.
     dXR: optional [num_targets, HC] row view (unit column stride) to write the target-row
     gradient into."""
     HC = att.numel()
@@ -400,7 +402,8 @@ def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, go
     datt_part = torch.empty((max(n_waves, 1), 2 * HC), dtype=torch.float32, device=dev)
     attf = att.reshape(-1).contiguous()
     if plan.n_items:
-        _native.attn_bwd(XL, XR, attf, bias, plan.perm, plan.items, plan.n_items, heads, C, slope, out, smax,
+        perm = None if (dxl_sorted and xl_sorted) else plan.perm
+        _native.attn_bwd(XL, XR, attf, bias, perm, plan.items, plan.n_items, heads, C, slope, out, smax,
                          ssum, gout, dXL, dXR, part, datt_part, xl_by_position=xl_sorted,
                          lanes=BWD_LANES and _lanes(plan, heads, HC))
         bwd_combine(plan, part, HC, dXR)
@@ -417,12 +420,15 @@ class GatAttentionFn(torch.autograd.Function):
     """out[i] = sum_{j->i} softmax_j(att . leaky_relu(XL[j] + XR[i])) XL[j] + bias."""
 
     @staticmethod
-    def forward(ctx, XL, XR, att, bias, plan, heads, slope, xl_sorted=False, sec=None):
-        """xl_sorted: XL rows in segment order (written through plan.pos); the XL gradient is still
-        returned in source-row (edge) order.  sec: streams.SideSection joined before backward."""
+    def forward(ctx, XL, XR, att, bias, plan, heads, slope, xl_sorted=False, sec=None, dxl_sorted=False):
+        """xl_sorted: XL rows in segment order (written through plan.pos); the XL gradient is
+        returned in source-row (edge) order, or with dxl_sorted in XL's own (segment) order, for a
+        producer whose backward reads it through plan.pos (edge_cam_pbwd's dxl_pos).
+        sec: streams.SideSection joined before backward."""
         out, smax, ssum = attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True, xl_sorted=xl_sorted)
         ctx.plan, ctx.heads, ctx.slope = plan, heads, slope
         ctx.xl_sorted, ctx.sec = xl_sorted, sec
+        ctx.dxl_sorted = bool(dxl_sorted) and bool(xl_sorted)
         ctx.defer = _native.defer_token(att, bias)
         ctx.save_for_backward(XL, XR, att, bias, out, smax, ssum)
         ctx.mark_non_differentiable(smax, ssum)
@@ -433,12 +439,13 @@ class GatAttentionFn(torch.autograd.Function):
     def backward(ctx, gout, _gm, _gs):
         XL, XR, att, bias, out, smax, ssum = ctx.saved_tensors
         if gout is None:
-            return None, None, None, None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None, None, None
         if ctx.sec is not None:
             ctx.sec.join()
         dXL, dXR, datt, dbias = attn_backward_raw(XL, XR, att, bias, ctx.plan, ctx.heads, ctx.slope, out, smax,
-                                                  ssum, gout, xl_sorted=ctx.xl_sorted, defer=ctx.defer)
-        return dXL, dXR, datt.view_as(att), dbias, None, None, None, None, None
+                                                  ssum, gout, xl_sorted=ctx.xl_sorted, defer=ctx.defer,
+                                                  dxl_sorted=ctx.dxl_sorted)
+        return dXL, dXR, datt.view_as(att), dbias, None, None, None, None, None, None
 
 
 class GlobalPairFn(torch.autograd.Function):

@@ -1058,7 +1058,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
     const float* __restrict__ gout, int64_t ldG, const gasfm_work_item* __restrict__ items, int n_items,
     const float* __restrict__ dXLp, int64_t ldXp, const float* __restrict__ dRes, float* __restrict__ dP,
     float* __restrict__ dXR, int64_t ldDXR, float* __restrict__ part_dxr, float* __restrict__ part, int64_t ldPart,
-    PbwdEpi ep) {
+    PbwdEpi ep, const int32_t* __restrict__ dxl_pos) {
   static_assert(!DWP || (LN && RES), "edge_cam_pbwd: the epilogue weight gradient needs relu(LN(P)) and dRes");
   // LDS: weight slabs (Wc for XLc; Wpt^T, Wc^T, (scale Wp)^T for dP_hat), the per-feature vectors,
   // per wave four 16 x 32 transpose tiles (T -> C layout of P, dXLp, dRes, dXLc), and (DWP) per
@@ -1130,23 +1130,38 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   f32x4 nPT[2], nXT[2], nRT[2];
   float2 nP0 = make_float2(0.f, 0.f);  // (DWP) P0 of edge c (a dummy read of P without P0)
   const float* p0p = (DWP && ep.P0) ? ep.P0 : P;
+  // dxl_pos (round 4): dXLp in point-segment order, edge e's row at dxl_pos[e] (the point attention's
+  // backward then writes it streaming instead of scattering it).  The next tile's position is the
+  // first load of issue(); its dXLp row is requested by issue_x() half a tile later, once the
+  // position has arrived (waiting for it there does not wait for the loads issued after it).
+  // Without dxl_pos the row is edge row0 + c; the "position" load then reads P as a dummy.
+  const int32_t* posp = dxl_pos ? dxl_pos : reinterpret_cast<const int32_t*>(P);
+  int npos = 0;
+  int64_t xrow = 0;  // the next tile's edge row of lane c (clamped)
   auto issue = [&](int64_t row0, int nrows) {
+    xrow = row0 + (c < nrows ? c : 0);
+    npos = posp[xrow];
     load_slabs32(P, row0, nrows, nPT, lane);
-    const float* p = dXLp + (row0 + (c < nrows ? c : 0)) * ldXp + 4 * g;
+    if (RES) load_slabs32(dRes, row0, nrows, nRT, lane);
+    if (DWP) nP0 = *reinterpret_cast<const float2*>(p0p + xrow * 2);
+  };
+  auto issue_x = [&]() {
+    const float* p = dXLp + (dxl_pos ? int64_t(npos) : xrow) * ldXp + 4 * g;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const float4 t = *reinterpret_cast<const float4*>(p + 16 * u);
       nXT[u] = f32x4{t.x, t.y, t.z, t.w};
     }
-    if (RES) load_slabs32(dRes, row0, nrows, nRT, lane);
-    if (DWP) nP0 = *reinterpret_cast<const float2*>(p0p + (row0 + (c < nrows ? c : 0)) * 2);
   };
   auto rows_at = [](const gasfm_work_item& w, int64_t row0) { return int(w.end - row0 < TR ? w.end - row0 : TR); };
   gasfm_work_item w{0, 0, 0, -1};
   if (gw < n_items) {
     w = items[gw];
     if (GASFM_PBWD_BF) w = uniform_item(w);
-    if (w.begin < w.end) issue(w.begin, rows_at(w, w.begin));
+    if (w.begin < w.end) {
+      issue(w.begin, rows_at(w, w.begin));
+      issue_x();
+    }
   }
   for (int it = gw; it < n_items; it += nw) {
     const int64_t seg = w.seg;
@@ -1188,7 +1203,10 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
     const bool more = it + nw < n_items;
     if (more) wn = items[it + nw];
     if (GASFM_PBWD_BF) wn = uniform_item(wn);
-    if (w.begin >= w.end && more && wn.begin < wn.end) issue(wn.begin, rows_at(wn, wn.begin));
+    if (w.begin >= w.end && more && wn.begin < wn.end) {
+      issue(wn.begin, rows_at(wn, wn.begin));
+      issue_x();
+    }
     for (int64_t row0 = w.begin; row0 < w.end; row0 += TR) {
       const int nrows = rows_at(w, row0);
       f32x4 PT[2] = {nPT[0], nPT[1]}, XT[2] = {nXT[0], nXT[1]}, RT[2];
@@ -1278,6 +1296,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
           datt[q][r] = fmaf(de, lz[r], datt[q][r]);
         }
       }
+      issue_x();  // the next tile's dXLp rows (its position was loaded at the top of this tile)
       // ---- dP_hat (C layout) = dXLp Wpt + dXLc Wc (+ dRes scale Wp)
       f32x4 dph[2] = {zero4(), zero4()};
       prod_c2(reinterpret_cast<const float4*>(WptTQ), XT, dph, lane);
@@ -1633,7 +1652,7 @@ extern "C" int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const f
                                       const float* dRes, float* dP, float* dXR, int64_t ldDXR, float* part_dxr,
                                       float* part, int64_t ldPart, const float* We, int32_t ldWe, float scale_e,
                                       float* dSv_e, float* part_dsv_e, float* dP0_e, const float* P0, int32_t ldWpo,
-                                      void* stream) {
+                                      const int32_t* dxl_pos, void* stream) {
   GASFM_REQUIRE(n_items >= 0 && P && Wpt && Wc && bc && XR && att && bias && out && seg_max && seg_sum && gout &&
                     items && dXLp && dP && dXR && part && (!dRes || (Wp && ldWp >= F)),
                 "gasfm_edge_cam_pbwd: null pointer");
@@ -1655,7 +1674,7 @@ extern "C" int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const f
   auto launch = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, st, P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, ldWp, scale, XR,
                        ldXR, att, bias, slope, out, ldOut, seg_max, seg_sum, ldStat, gout, ldG, items, n_items, dXLp,
-                       ldXp, dRes, dP, dXR, ldDXR, part_dxr, part, ldPart, ep);
+                       ldXp, dRes, dP, dXR, ldDXR, part_dxr, part, ldPart, ep, dxl_pos);
   };
   if (ln_w && dRes) {
     if (epi && dwp)
@@ -1688,7 +1707,7 @@ extern "C" int gasfm_edge_cam_pbwd(const float* P, const float* ln_w, const floa
   return gasfm_edge_cam_pbwd_ex(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, ldWp, scale, XR, ldXR, att, bias, slope, out,
                                 ldOut, seg_max, seg_sum, ldStat, gout, ldG, items, n_items, dXLp, ldXp, dRes, dP, dXR,
                                 ldDXR, part_dxr, part, PB2_PART, nullptr, 0, 0.f, nullptr, nullptr, nullptr, nullptr, 0,
-                                stream);
+                                nullptr, stream);
 }
 
 extern "C" int gasfm_edge_seam_fwd(const float* Pb, const float* P0, const int32_t* pt, const float* ln_wb,

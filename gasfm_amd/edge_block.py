@@ -35,6 +35,17 @@ CAM_PBWD = os.environ.get("GASFM_CAM_PBWD", "1") != "0"
 # gradient in block b's own edge_cam_pbwd (it holds dRes = dP' and relu(LN_b(P_b))), dSv / dP0 in
 # block b+1's (the kernel that produces dP').  0: edge_epilogue_bwd as before.
 EPI_FOLD = os.environ.get("GASFM_EPI_FOLD", "1") != "0"
+# round 4: the point half of XL's gradient in point-segment order (the layout of XLp itself): the
+# point attention's backward writes it streaming (no perm scatter) and edge_cam_pbwd reads edge e's
+# row at pos[e] (GatAttentionFn(dxl_sorted) + the camera Functions' dxl_pos).  0: edge order.
+DXL_PT = os.environ.get("GASFM_DXL_PT", "0") != "0"
+
+
+def dxl_pos_of(pos):
+    """The dxl_pos the camera Functions' backward gets for a forward with XLp written through pos
+    (None: dXLp arrives in edge order)."""
+    return pos if (DXL_PT and pos is not None) else None
+
 # Block 0's prologue writes XL0 row by row through the point plan's permutation (one 32-B store
 # per row, gasfm_edge0_prologue_fwd_rows) instead of scattering the point halves through pos.
 E0_ROWS = os.environ.get("GASFM_E0_ROWS", "1") != "0"
@@ -158,6 +169,7 @@ class EdgeCamFn(torch.autograd.Function):
         ctx.att_shape = att.shape
         ctx.has_ln = ln_w is not None
         ctx.dwp = bool(dwp)
+        ctx.dxl_pos = dxl_pos_of(pos)
         ctx.defer = _native.defer_token(ln_w, ln_b, Wpt, bpt, Wc, bc, att, bias, Wp if dwp else None)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum, P0)
@@ -187,6 +199,7 @@ def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None):
     P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum, P0 = saved
     plan = ctx.plan
     E, dev = P.shape[0], P.device
+    dxl_pos = getattr(ctx, "dxl_pos", None) if dXLp is not None else None  # dXLp in point order (DXL_PT)
     dXLp = torch.zeros((E, 32), dtype=torch.float32, device=dev) if dXLp is None else dXLp.contiguous()
     g_c = torch.zeros_like(out) if g_c is None else (g_c if g_c.stride(1) == 1 else g_c.contiguous())
     dwp = ctx.dwp and dRes is not None and ln_w is not None
@@ -205,7 +218,7 @@ def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None):
                               Wp.contiguous() if dRes is not None else None, PROJ_SCALE, XR, attf, bias, ctx.slope,
                               out, smax, ssum, g_c, plan.items, plan.n_items, dXLp, dRes, dP, dXR, part_dxr, part,
                               epi=epi if use_epi else None,
-                              dwp=(P0 if P0 is not None else True) if dwp else None)
+                              dwp=(P0 if P0 is not None else True) if dwp else None, dxl_pos=dxl_pos)
         ctx.epi_done = use_epi
         bwd_combine(plan, part_dxr, 32, dXR)
         tot = _native.param_colsum(part, ctx.defer)
@@ -214,6 +227,8 @@ def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None):
         if dwp:
             dWp = tot[o + 192:o + 192 + 32 * wcols].view(32, wcols)
     else:
+        if dxl_pos is not None:  # the separate kernels take dXLp in edge order
+            dXLp = dXLp.index_select(0, dxl_pos.long())
         # camera attention backward (XLc recomputed from P): dXLc, dXR, [datt | dbias] partials
         dXLc = torch.empty((E, 32), dtype=torch.float32, device=dev)
         dXR = torch.empty((plan.num_targets, 32), dtype=torch.float32, device=dev)
@@ -394,6 +409,7 @@ class SeamFn(torch.autograd.Function):
         ctx.att_shape = att.shape
         ctx.has_ln = ln_w is not None
         ctx.dwp = bool(dwp_n)
+        ctx.dxl_pos = dxl_pos_of(pos)
         ctx.defer = _native.defer_token(ln_w, ln_b, Wpt, bpt, Wc, bc, att, bias, Wp_n if dwp_n else None)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(P, P0, Wp_c, lnw_b, lnb_b, Pn, ln_w, ln_b, Wpt, Wc, bc, Wp_n, XR, attf, bias, out, smax,
@@ -567,6 +583,7 @@ class Seam0Fn(torch.autograd.Function):
         ctx.att_shape = att.shape
         ctx.has_ln = True
         ctx.dwp = bool(dwp_n)
+        ctx.dxl_pos = dxl_pos_of(pos)
         ctx.defer = _native.defer_token(ln_w, ln_b, Wpt, bpt, Wc, bc, att, bias, Wp_n if dwp_n else None)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(Pc, lna_w, lna_b, lnb_w, lnb_b, Wp_c, Wsk_c, Pn, ln_w, ln_b, Wpt, Wc, bc, Wp_n, XR,

@@ -525,8 +525,10 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
                 XLp, agg_c, token = EdgeCamFn.apply(Pe, *cam_args)
                 holder["P"] = Pe
             holder["token"] = token
+            # dxl_sorted: XLp's gradient in XLp's own (point) order, read by the camera Function's
+            # backward through pos (edge_block.DXL_PT)
             agg_p = GatAttentionFn.apply(XLp, XRp, cp.att, cp.bias, pp, cp.heads, cp.negative_slope, pos is not None,
-                                         sec)[0]
+                                         sec, edge_block.dxl_pos_of(pos) is not None)[0]
             return agg_p, agg_c
         return attend
 

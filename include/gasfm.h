@@ -207,7 +207,9 @@ int gasfm_edge_cam_pbwd(const float* P, const float* ln_w, const float* ln_b, fl
  *   ldWpo > 0 (DWP): THIS block's lin_proj gradient scale sum_e dRes[e]^T [relu(LN(P[e])) | P0[e]]
  *     as a [32 x ldWpo] block after the gasfm_edge_cam_pbwd_part_cols() floats of each part row
  *     (ldWpo = 34 with P0 [E, 2], 32 without); requires ln_w and dRes.
- * part rows have stride ldPart (>= part_cols + 32 ldWpo). */
+ * part rows have stride ldPart (>= part_cols + 32 ldWpo).
+ * dxl_pos (round 4, may be null): dXLp is in point-segment order, edge e's row at dxl_pos[e] (the
+ * point plan's pos: the layout gasfm_gat_attn_bwd writes without perm); null: edge order. */
 int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
                            const float* Wc, const float* bc, const float* Wp, int32_t ldWp, float scale,
                            const float* XR, int64_t ldXR, const float* att, const float* bias, float slope,
@@ -216,7 +218,7 @@ int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const float* ln_b,
                            int32_t n_items, const float* dXLp, int64_t ldXp, const float* dRes, float* dP,
                            float* dXR, int64_t ldDXR, float* part_dxr, float* part, int64_t ldPart,
                            const float* We, int32_t ldWe, float scale_e, float* dSv_e, float* part_dsv_e,
-                           float* dP0_e, const float* P0, int32_t ldWpo, void* stream);
+                           float* dP0_e, const float* P0, int32_t ldWpo, const int32_t* dxl_pos, void* stream);
 
 /* ---- fused GATv2 edge-softmax + aggregation (device) ------------------- */
 

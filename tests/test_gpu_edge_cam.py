@@ -224,3 +224,42 @@ def test_block0_seam_vs_separate(device, monkeypatch):
         err = float((res[True][2][k] - g0).norm())
         own = float((g0 - torch.from_numpy(g64[k])).norm())
         assert err <= max(1e-3 * float(g0.norm()), 10 * own) + 1e-9, (k, err, own, float(g0.norm()))
+
+
+@pytest.mark.parametrize("pbwd", [True, False])
+def test_dxl_point_order_bitwise(device, monkeypatch, pbwd):
+    """XLp's gradient in point order (edge_block.DXL_PT: the point attention's backward writes dXL
+    without the perm scatter, edge_cam_pbwd reads edge e's row at pos[e]; with CAM_PBWD off the
+    separate kernels get it back in edge order) against edge order: the same values reach the same
+    products, so every parameter gradient is bitwise identical.  4 blocks: block 0 -> 1 seam,
+    folded 32-wide seams, the final update; items that split cameras (max_piece 64)."""
+    from gasfm_amd import edge_block
+    from oracle.weights import deterministic_state_dict
+    sc = synthetic.scaled_config4(0.05, seed=17)
+    data = gasfm_amd.SceneData.from_synthetic(sc, max_piece=64).to(device)
+    assert data.graph_wrappers["proj2scenepoint"].plan.pos is not None
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=4))
+    sd = deterministic_state_dict(net.state_dict(), torch.float64)
+    net.load_state_dict({k: v.float() for k, v in sd.items()})
+    net = net.to(device)
+    gen = torch.Generator().manual_seed(7)
+    cP = torch.randn((sc.m, 3, 4), generator=gen).to(device)
+    cX = torch.randn((4, sc.n), generator=gen).to(device)
+    monkeypatch.setattr(edge_block, "CAM_PBWD", pbwd)
+    seen = []
+    orig = _native.edge_cam_pbwd
+    monkeypatch.setattr(_native, "edge_cam_pbwd",
+                        lambda *a, **k: (seen.append(k.get("dxl_pos") is not None), orig(*a, **k))[1])
+    res = {}
+    for pt in (False, True):
+        monkeypatch.setattr(edge_block, "DXL_PT", pt)
+        seen.clear()
+        net.zero_grad(set_to_none=True)
+        pred = net(data)
+        ((pred["Ps_norm"] * cP).sum() + (pred["pts3D"] * cX).sum()).backward()
+        torch.cuda.synchronize()
+        res[pt] = {k: p.grad.detach().clone() for k, p in net.named_parameters()}
+        if pbwd:
+            assert seen and all(s == pt for s in seen), seen
+    for k, g0 in res[False].items():
+        assert torch.equal(res[True][k], g0), k
