@@ -28,6 +28,8 @@
 // sums gout over every segment (once, at its first item).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "common.hpp"
 #include "tile.hpp"
 
@@ -1048,7 +1050,7 @@ __device__ __forceinline__ gasfm_work_item uniform_item(const gasfm_work_item& w
   return gasfm_work_item{__builtin_amdgcn_readfirstlane(w.seg), __builtin_amdgcn_readfirstlane(w.begin),
                          __builtin_amdgcn_readfirstlane(w.end), __builtin_amdgcn_readfirstlane(w.slot)};
 }
-template <bool LN, bool RES, bool EPI, bool DWP>
+template <bool LN, bool RES, bool EPI, bool DWP, bool XP = false>
 __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kernel(
     const float* __restrict__ P, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
     const float* __restrict__ Wpt, const float* __restrict__ Wc, const float* __restrict__ bc,
@@ -1130,28 +1132,30 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   f32x4 nPT[2], nXT[2], nRT[2];
   float2 nP0 = make_float2(0.f, 0.f);  // (DWP) P0 of edge c (a dummy read of P without P0)
   const float* p0p = (DWP && ep.P0) ? ep.P0 : P;
-  // dxl_pos (round 4): dXLp in point-segment order, edge e's row at dxl_pos[e] (the point attention's
-  // backward then writes it streaming instead of scattering it).  The next tile's position is the
-  // first load of issue(); its dXLp row is requested by issue_x() half a tile later, once the
-  // position has arrived (waiting for it there does not wait for the loads issued after it).
-  // Without dxl_pos the row is edge row0 + c; the "position" load then reads P as a dummy.
-  const int32_t* posp = dxl_pos ? dxl_pos : reinterpret_cast<const int32_t*>(P);
+  // XP (round 4, dxl_pos): dXLp in point-segment order, edge e's row at dxl_pos[e] (the point
+  // attention's backward then writes it streaming instead of scattering it).  The next tile's
+  // position is the first load of issue(); its dXLp row is requested by issue_x() half a tile later,
+  // once the position has arrived (waiting for it there does not wait for the loads issued after
+  // it).  Without XP the dXLp row (edge row0 + c) is requested in issue() with the others.
   int npos = 0;
-  int64_t xrow = 0;  // the next tile's edge row of lane c (clamped)
-  auto issue = [&](int64_t row0, int nrows) {
-    xrow = row0 + (c < nrows ? c : 0);
-    npos = posp[xrow];
-    load_slabs32(P, row0, nrows, nPT, lane);
-    if (RES) load_slabs32(dRes, row0, nrows, nRT, lane);
-    if (DWP) nP0 = *reinterpret_cast<const float2*>(p0p + xrow * 2);
-  };
-  auto issue_x = [&]() {
-    const float* p = dXLp + (dxl_pos ? int64_t(npos) : xrow) * ldXp + 4 * g;
+  auto load_x = [&](int64_t r) {
+    const float* p = dXLp + r * ldXp + 4 * g;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const float4 t = *reinterpret_cast<const float4*>(p + 16 * u);
       nXT[u] = f32x4{t.x, t.y, t.z, t.w};
     }
+  };
+  auto issue = [&](int64_t row0, int nrows) {
+    const int64_t xrow = row0 + (c < nrows ? c : 0);
+    if (XP) npos = dxl_pos[xrow];
+    load_slabs32(P, row0, nrows, nPT, lane);
+    if (!XP) load_x(xrow);
+    if (RES) load_slabs32(dRes, row0, nrows, nRT, lane);
+    if (DWP) nP0 = *reinterpret_cast<const float2*>(p0p + xrow * 2);
+  };
+  auto issue_x = [&]() {
+    if (XP) load_x(npos);
   };
   auto rows_at = [](const gasfm_work_item& w, int64_t row0) { return int(w.end - row0 < TR ? w.end - row0 : TR); };
   gasfm_work_item w{0, 0, 0, -1};
@@ -1676,24 +1680,31 @@ extern "C" int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const f
                        ldXR, att, bias, slope, out, ldOut, seg_max, seg_sum, ldStat, gout, ldG, items, n_items, dXLp,
                        ldXp, dRes, dP, dXR, ldDXR, part_dxr, part, ldPart, ep, dxl_pos);
   };
-  if (ln_w && dRes) {
-    if (epi && dwp)
-      launch(&edge_cam_pbwd_kernel<true, true, true, true>);
-    else if (epi)
-      launch(&edge_cam_pbwd_kernel<true, true, true, false>);
-    else if (dwp)
-      launch(&edge_cam_pbwd_kernel<true, true, false, true>);
-    else
-      launch(&edge_cam_pbwd_kernel<true, true, false, false>);
-  } else if (ln_w) {
-    launch(&edge_cam_pbwd_kernel<true, false, false, false>);
-  } else if (dRes) {
-    launch(&edge_cam_pbwd_kernel<false, true, false, false>);
-  } else if (epi) {
-    launch(&edge_cam_pbwd_kernel<false, false, true, false>);
-  } else {
-    launch(&edge_cam_pbwd_kernel<false, false, false, false>);
-  }
+  auto pick = [&](auto xp) {
+    constexpr bool X = decltype(xp)::value;
+    if (ln_w && dRes) {
+      if (epi && dwp)
+        launch(&edge_cam_pbwd_kernel<true, true, true, true, X>);
+      else if (epi)
+        launch(&edge_cam_pbwd_kernel<true, true, true, false, X>);
+      else if (dwp)
+        launch(&edge_cam_pbwd_kernel<true, true, false, true, X>);
+      else
+        launch(&edge_cam_pbwd_kernel<true, true, false, false, X>);
+    } else if (ln_w) {
+      launch(&edge_cam_pbwd_kernel<true, false, false, false, X>);
+    } else if (dRes) {
+      launch(&edge_cam_pbwd_kernel<false, true, false, false, X>);
+    } else if (epi) {
+      launch(&edge_cam_pbwd_kernel<false, false, true, false, X>);
+    } else {
+      launch(&edge_cam_pbwd_kernel<false, false, false, false, X>);
+    }
+  };
+  if (dxl_pos)
+    pick(std::true_type{});
+  else
+    pick(std::false_type{});
   return launch_status("gasfm_edge_cam_pbwd");
 }
 

@@ -1259,6 +1259,9 @@ extern "C" int gasfm_gat_attn_fwd(const float* XL, int64_t ldXL, const float* XR
   return launch_status("gasfm_gat_attn_fwd");
 }
 
+#ifndef GASFM_COMBINE_SMALL
+#define GASFM_COMBINE_SMALL 0
+#endif
 extern "C" int gasfm_gat_attn_combine(const gasfm_combine_item* combine, int32_t n_combine, int32_t H,
                                       int32_t C, const float* part, const float* bias, int32_t finalize, float* out,
                                       int64_t ldOut, float* seg_max, float* seg_sum, int64_t ldStat, void* stream) {
@@ -1271,7 +1274,10 @@ extern "C" int gasfm_gat_attn_combine(const gasfm_combine_item* combine, int32_t
   if (vec_ok) {
     done = dispatch_shape(H, C, [&](auto g) {
       using G = decltype(g);
-      const int threads = 1024;
+      // GASFM_COMBINE_SMALL (round 4): 256 threads for the narrow rows (HC <= 64: 32 to 256 slot
+      // rows per pass, while a combine entry holds <= ~64 slots after the two-level split) instead
+      // of 1024 threads whose 16-wave LDS merge and launch cost dominate a few-slot merge
+      const int threads = (GASFM_COMBINE_SMALL && G::HC <= 64) ? 256 : 1024;
       const size_t lds = size_t(threads / kWave) * G::LPE * (G::VEC + 2 * G::HPL) * sizeof(float);
       note_dispatch(GASFM_K_ATTN_COMBINE_VEC);
       hipLaunchKernelGGL((attn_combine_kernel<G>), dim3(n_combine), dim3(threads), lds, st, combine, part, bias,
