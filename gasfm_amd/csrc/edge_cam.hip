@@ -56,6 +56,12 @@ __device__ __forceinline__ float row_max16(float v) {
   return v;
 }
 
+// a work item in scalar registers (its fields are wave-uniform)
+__device__ __forceinline__ gasfm_work_item uniform_item(const gasfm_work_item& w) {
+  return gasfm_work_item{__builtin_amdgcn_readfirstlane(w.seg), __builtin_amdgcn_readfirstlane(w.begin),
+                         __builtin_amdgcn_readfirstlane(w.end), __builtin_amdgcn_readfirstlane(w.slot)};
+}
+
 // Rows of a 16 x 32 tile in row layout: lane l holds row (l >> 3) + 8u (u = 0, 1), columns
 // 4 (l & 7) .. + 3.  Rows >= nrows re-read row 0 (always valid); phat_to_lds writes zeros for
 // them.  No select on the loaded registers here: these loads are the next tile's prefetch, and
@@ -751,6 +757,389 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
 }
 
 // =============================================================================================
+// the forward seam with its inputs staged through LDS, two tiles ahead (round 4, GASFM_SEAM_LDS /
+// gasfm_tuning_set(GASFM_TUNE_SEAM_LDS);
+// blocks 1-11, not block 0's EP0 form).  edge_seam_fwd_kernel holds the next tile's P slabs and
+// Sp rows in registers, one tile ahead: ~4 KB in flight per wave at 2 waves / SIMD, about what a
+// CU needs for half the HBM rate at the loaded latency, and its memory and MFMA/VALU phases
+// add up (453 us for 1.6 GB + 48 MFMA per tile).  Here the loads are direct-to-LDS
+// (global_load_lds: no VGPRs held while they fly) in a per-wave ring, in three stages per tile t:
+//   I(t+3)  edge indices: pt, pos, P0 pairs (one 4-B load per lane), the item's XR / Sv rows (one)
+//   B(t+2)  the Sp[pt] rows of tile t+2 (pt from its I slot, loaded an iteration earlier)
+//   A(t+2)  the P rows of tile t+2
+// so a tile's P and Sp rows are requested two iterations before use (~8 KB in flight per wave).
+// P / Sp rows sit row-major in the slot with their 16-B chunks swizzled (chunk k of row r at
+// position k ^ (r & 7)), so the T-layout reads (lane (g, c): row c, chunk 4 u + g) spread over the
+// banks.  Every stage issues a fixed number of requests (clamped re-reads past the wave's last
+// tile), and the only vector-memory requests in the loop are these and the tile's 4 stores, so
+// one s_waitcnt vmcnt(8) at the top of a tile (vmcnt(4) for the first) covers the tile's slots
+// and the I slot the B stage reads next; the work items are scalar loads (lgkmcnt).
+// The arithmetic is edge_seam_fwd_kernel's, line for line (outputs bitwise equal).
+// =============================================================================================
+constexpr int SL_PS = 3;                    // P / Sp ring slots per wave
+constexpr int SL_IX = 4;                    // index ring slots per wave
+constexpr int SL_PSF = 2 * TR * F;          // floats per P / Sp slot (P rows, then Sp rows)
+constexpr int SL_IXF = 128;                 // dwords per index slot
+constexpr int SL_WAVE = SL_PS * SL_PSF + SL_IX * SL_IXF;  // floats per wave
+constexpr size_t SL_DYN = size_t(kWaves) * SL_WAVE * sizeof(float);
+
+__device__ __forceinline__ gasfm_work_item item_s(const gasfm_work_item* __restrict__ items, int it) {
+  // wave-uniform index -> scalar loads
+  const gasfm_work_item w = items[__builtin_amdgcn_readfirstlane(it)];
+  return uniform_item(w);
+}
+
+// LDS reads of the seam's DMA ring through inline asm: the compiler waits for every LDS-DMA
+// request before a read it sees of the same LDS object (it cannot tell the ring's slots apart),
+// which would drain the two-tile prefetch each tile; these reads are ordered by the kernel's own
+// s_waitcnt vmcnt instead, and wait for themselves (lgkmcnt(0)) before their results are used
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) char*)p));
+}
+__device__ __forceinline__ void lds_tile_reads(const float* pa, const float* pb, const float* sa, const float* sb,
+                                               const float* q, const float* ps, f32x4& P0, f32x4& P1, f32x4& S0,
+                                               f32x4& S1, f32x2v& Q, int& pos) {
+  asm volatile(
+      "ds_read_b128 %0, %6\n"
+      "ds_read_b128 %1, %7\n"
+      "ds_read_b128 %2, %8\n"
+      "ds_read_b128 %3, %9\n"
+      "ds_read_b64 %4, %10\n"
+      "ds_read_b32 %5, %11\n"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(P0), "=&v"(P1), "=&v"(S0), "=&v"(S1), "=&v"(Q), "=&v"(pos)
+      : "v"(lds_off(pa)), "v"(lds_off(pb)), "v"(lds_off(sa)), "v"(lds_off(sb)), "v"(lds_off(q)), "v"(lds_off(ps))
+      : "memory");
+}
+__device__ __forceinline__ void lds_read4x4(const float* a, const float* b, const float* c2, const float* d,
+                                            f32x4& A, f32x4& B, f32x4& C, f32x4& D) {
+  asm volatile(
+      "ds_read_b128 %0, %4\n"
+      "ds_read_b128 %1, %5\n"
+      "ds_read_b128 %2, %6\n"
+      "ds_read_b128 %3, %7\n"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(A), "=&v"(B), "=&v"(C), "=&v"(D)
+      : "v"(lds_off(a)), "v"(lds_off(b)), "v"(lds_off(c2)), "v"(lds_off(d))
+      : "memory");
+}
+__device__ __forceinline__ void lds_read2i(const int32_t* a, const int32_t* b, int& A, int& B) {
+  asm volatile(
+      "ds_read_b32 %0, %2\n"
+      "ds_read_b32 %1, %3\n"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(A), "=&v"(B)
+      : "v"(lds_off(a)), "v"(lds_off(b))
+      : "memory");
+}
+
+template <bool LN>
+__global__ __launch_bounds__(kThreads, 2) void edge_seam_lds_kernel(
+    SeamEpi ep, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
+    const float* __restrict__ Wpt, const float* __restrict__ bpt, const float* __restrict__ Wc,
+    const float* __restrict__ bc, float* __restrict__ XLp, int64_t ldXLp, const int32_t* __restrict__ pos,
+    const float* __restrict__ XR, int64_t ldXR, const float* __restrict__ att, const float* __restrict__ bias,
+    float slope, const gasfm_work_item* __restrict__ items, int n_items, int finalize, float* __restrict__ out,
+    int64_t ldOut, float* __restrict__ seg_max, float* __restrict__ seg_sum, int64_t ldStat,
+    float* __restrict__ part) {
+  typedef __attribute__((address_space(3))) void* lds_vp;
+  typedef const __attribute__((address_space(1))) void* glb_vp;
+  __shared__ __attribute__((aligned(16))) float Wl[NX * F];
+  __shared__ __attribute__((aligned(16))) float WpQ[F * F];
+  __shared__ __attribute__((aligned(16))) float V[12 * F];
+  extern __shared__ __attribute__((aligned(16))) float dyn[];
+  stage_slabs32<NX, kThreads>([&](int q) { return q < F * F ? Wpt[q] : Wc[q - F * F]; }, Wl);
+  stage_slabs32<F, kThreads>([&](int q) { return ep.Wp[(q / F) * ep.ldWp + q % F]; }, WpQ);
+  if (threadIdx.x < F) {
+    const int f = threadIdx.x;
+    V[f] = ep.gam[f];
+    V[F + f] = ep.bet[f];
+    V[2 * F + f] = ep.bp[f] + ep.Sg[f];
+    V[3 * F + f] = ep.P0 ? ep.Wp[f * ep.ldWp + 32] : 0.f;
+    V[4 * F + f] = ep.P0 ? ep.Wp[f * ep.ldWp + 33] : 0.f;
+    V[5 * F + f] = LN ? gam[f] : 1.f;
+    V[6 * F + f] = LN ? bet[f] : 0.f;
+    V[7 * F + f] = bpt[f];
+    V[8 * F + f] = bc[f];
+    V[9 * F + f] = att[f];
+    V[10 * F + f] = finalize ? bias[f] : 0.f;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
+  const int c = lane & 15, g = lane >> 4;
+  auto vec = [&](int which, int q) {
+    const float4 t = *reinterpret_cast<const float4*>(V + which * F + 16 * q + 4 * g);
+    return f32x4{t.x, t.y, t.z, t.w};
+  };
+  float* ring = dyn + wave * SL_WAVE;         // P / Sp slots
+  float* ixr = ring + SL_PS * SL_PSF;         // index slots
+  const int gw = blockIdx.x * kWaves + wave, nw = gridDim.x * kWaves;
+  const float* p0src = ep.P0 ? ep.P0 : ep.P;  // a dummy (finite) read of P without P0
+  const int32_t* possrc = pos ? pos : ep.pt;
+
+  // a walker over this wave's tiles (items gw, gw + nw, ...; empty items have none); past the last
+  // tile it stays on it (its stages then re-read that tile)
+  struct Walk {
+    int it;
+    gasfm_work_item w;
+    int64_t row0;
+  };
+  auto walk_init = [&](Walk& k) {
+    k.it = gw;
+    k.row0 = 0;
+    k.w = gasfm_work_item{0, 0, 0, -1};
+    while (k.it < n_items) {
+      k.w = item_s(items, k.it);
+      if (k.w.begin < k.w.end) {
+        k.row0 = k.w.begin;
+        return;
+      }
+      k.it += nw;
+    }
+  };
+  auto walk_next = [&](Walk& k) {
+    if (k.it >= n_items) return;
+    if (k.row0 + TR < k.w.end) {
+      k.row0 += TR;
+      return;
+    }
+    int it2 = k.it + nw;
+    while (it2 < n_items) {
+      const gasfm_work_item w2 = item_s(items, it2);
+      if (w2.begin < w2.end) {
+        k.it = it2;
+        k.w = w2;
+        k.row0 = w2.begin;
+        return;
+      }
+      it2 += nw;
+    }
+  };
+  auto walk_rows = [](const Walk& k) { return int(k.w.end - k.row0 < TR ? k.w.end - k.row0 : TR); };
+  // I stage of the walker's tile into index slot s (2 requests)
+  auto stage_i = [&](const Walk& k, int s) {
+    float* ix = ixr + s * SL_IXF;
+    const int nr = walk_rows(k);
+    const int rr = (lane & 15) < nr ? (lane & 15) : 0;
+    const int64_t e = k.row0 + rr;
+    const void* src;
+    if (lane < 16)
+      src = ep.pt + e;
+    else if (lane < 32)
+      src = possrc + e;
+    else
+      src = p0src + (k.row0 + ((lane - 32) >> 1 < nr ? (lane - 32) >> 1 : 0)) * 2 + (lane & 1);
+    __builtin_amdgcn_global_load_lds((glb_vp)src, (lds_vp)ix, 4, 0, 0);
+    const int64_t seg = k.w.seg;
+    const float* src2 = lane < 32 ? XR + seg * ldXR + lane : ep.Sv + seg * ep.ldSv + (lane - 32);
+    __builtin_amdgcn_global_load_lds((glb_vp)src2, (lds_vp)(ix + 64), 4, 0, 0);
+  };
+  // A / B stages of the walker's tile into P / Sp slot s (2 + 2 requests); pt from index slot si
+  auto stage_ab = [&](const Walk& k, int s, int si) {
+    float* ps = ring + s * SL_PSF;
+    const int32_t* ix = reinterpret_cast<const int32_t*>(ixr + si * SL_IXF);
+    const int nr = walk_rows(k);
+    int pts[2];  // the rows' points (clamped at their I stage)
+    lds_read2i(ix + (lane >> 3), ix + 8 + (lane >> 3), pts[0], pts[1]);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int row = 8 * u + (lane >> 3);
+      const int ck = (lane & 7) ^ (row & 7);
+      __builtin_amdgcn_global_load_lds((glb_vp)(ep.Sp + int64_t(pts[u]) * F + 4 * ck),
+                                       (lds_vp)(ps + TR * F + u * 256), 16, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int row = 8 * u + (lane >> 3);
+      const int ck = (lane & 7) ^ (row & 7);
+      const int64_t e = k.row0 + (row < nr ? row : 0);
+      __builtin_amdgcn_global_load_lds((glb_vp)(ep.P + e * F + 4 * ck), (lds_vp)(ps + u * 256), 16, 0, 0);
+    }
+  };
+  auto wait_vm = [](auto n) {
+    if constexpr (decltype(n)::value == 4)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (decltype(n)::value == 8)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  Walk kI, kA;  // the I stage's walker (3 tiles ahead), the A / B stages' (2 ahead)
+  walk_init(kI);
+  kA = kI;
+  // prologue: I(0), I(1), I(2); wait; B(0) A(0), B(1) A(1)
+  stage_i(kI, 0);
+  walk_next(kI);
+  stage_i(kI, 1);
+  walk_next(kI);
+  stage_i(kI, 2);
+  walk_next(kI);
+  wait_vm(std::integral_constant<int, 0>{});
+  __builtin_amdgcn_wave_barrier();
+  stage_ab(kA, 0, 0);
+  walk_next(kA);
+  stage_ab(kA, 1, 1);
+  walk_next(kA);
+  int t = 0;  // this wave's tile counter
+  for (int it = gw; it < n_items; it += nw) {
+    const gasfm_work_item w = item_s(items, it);
+    const int64_t seg = w.seg;
+    float m[2] = {-INFINITY, -INFINITY}, s[2] = {0.f, 0.f};
+    f32x4 a[2] = {zero4(), zero4()};
+    f32x4 xr[2], sv[2];
+    for (int64_t row0 = w.begin; row0 < w.end; row0 += TR, ++t) {
+      const int nrows = int(w.end - row0 < TR ? w.end - row0 : TR);
+      if (t == 0)
+        wait_vm(std::integral_constant<int, 4>{});
+      else
+        wait_vm(std::integral_constant<int, 8>{});
+      __builtin_amdgcn_wave_barrier();
+      const float* ps = ring + (t % SL_PS) * SL_PSF;
+      const float* ix = ixr + (t % SL_IX) * SL_IXF;
+      f32x4 pb[2], sp[2];
+      f32x2v q0v;
+      int npos;
+      {
+        const int k0 = g ^ (c & 7), k1 = (4 + g) ^ (c & 7);
+        lds_tile_reads(ps + c * F + 4 * k0, ps + c * F + 4 * k1, ps + TR * F + c * F + 4 * k0,
+                       ps + TR * F + c * F + 4 * k1, ix + 32 + 2 * c, ix + 16 + c, pb[0], pb[1], sp[0], sp[1], q0v,
+                       npos);
+      }
+      const float2 q0 = make_float2(q0v[0], q0v[1]);
+      if (row0 == w.begin)
+        lds_read4x4(ix + 64 + 4 * g, ix + 64 + 16 + 4 * g, ix + 96 + 4 * g, ix + 96 + 16 + 4 * g, xr[0], xr[1], sv[0],
+                    sv[1]);
+      const int64_t dst = pos ? int64_t(npos) : row0 + (c < nrows ? c : 0);
+      // the stages of the tiles ahead (their slots were consumed an iteration ago)
+      stage_i(kI, (t + 3) % SL_IX);
+      walk_next(kI);
+      stage_ab(kA, (t + 2) % SL_PS, (t + 2) % SL_IX);
+      walk_next(kA);
+      const bool valid = c < nrows;
+      // ---- epilogue of block b (T layout): edge_seam_fwd_kernel's
+      f32x4 pn[2];
+      {
+        f32x4 ph[2] = {pb[0], pb[1]};
+        float gs[2][4], bs[2][4];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const f32x4 ga = vec(0, q), be = vec(1, q);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            gs[q][r] = ga[r];
+            bs[q][r] = be[r];
+          }
+        }
+        phat_slabs<true>(ph, gs, bs, ep.eps);
+        f32x4 y[2] = {zero4(), zero4()};
+        xl_slabs<2>(reinterpret_cast<const float4*>(WpQ), ph, y, lane);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const f32x4 cs = vec(2, q), w32 = vec(3, q), w33 = vec(4, q);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float d = y[q][r] + cs[r];
+            d = fmaf(w32[r], q0.x, fmaf(w33[r], q0.y, d));
+            d = (d + sv[q][r]) + sp[q][r];
+            pn[q][r] = fmaf(d, ep.scale, pb[q][r]);
+          }
+        }
+      }
+      {
+        const int64_t prow = row0 + (valid ? c : 0);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          *reinterpret_cast<float4*>(ep.Pout + prow * F + 16 * q + 4 * g) =
+              make_float4(pn[q][0], pn[q][1], pn[q][2], pn[q][3]);
+      }
+      // ---- prologue + camera attention of block b+1 on P'
+      {
+        float gs[2][4], bs[2][4];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const f32x4 ga = vec(5, q), be = vec(6, q);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            gs[q][r] = ga[r];
+            bs[q][r] = be[r];
+          }
+        }
+        phat_slabs<LN>(pn, gs, bs, eps);
+      }
+      f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
+      xl_slabs<4>(reinterpret_cast<const float4*>(Wl), pn, acc, lane);
+      {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int ot = 0; ot < 2; ++ot) {
+          const f32x4 b = vec(7, ot);
+          __builtin_nontemporal_store(v4f{acc[ot][0] + b[0], acc[ot][1] + b[1], acc[ot][2] + b[2], acc[ot][3] + b[3]},
+                                      reinterpret_cast<v4f*>(XLp + dst * ldXLp + 16 * ot + 4 * g));
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const f32x4 bcq = vec(8, q), atq = vec(9, q);
+        float xl[4], p = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          xl[r] = acc[2 + q][r] + bcq[r];
+          p = fmaf(leaky(xl[r] + xr[q][r], slope), atq[r], p);
+        }
+        p += __shfl_xor(p, 16);
+        if (valid) {
+          const float mn = fmaxf(m[q], p);
+          const float sc = __expf(m[q] - mn), wt = __expf(p - mn);
+          s[q] = fmaf(s[q], sc, wt);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) a[q][r] = fmaf(a[q][r], sc, wt * xl[r]);
+          m[q] = mn;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();  // this tile's slot reads before a later stage rewrites it
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float M = row_max16(m[q]);
+      const float f = (m[q] > -INFINITY) ? __expf(m[q] - M) : 0.f;
+      const float S = group_sum<16>(s[q] * f);
+      float A[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) A[r] = group_sum<16>(a[q][r] * f);
+      if (c == 0) {
+        const int f0 = 16 * q + 4 * g, h = 2 * q + (g >> 1);
+        if (w.slot < 0) {
+          const float inv = 1.f / (S + 1e-16f);
+          float4 o;
+          if (finalize) {
+            const f32x4 bq = vec(10, q);
+            o = make_float4(fmaf(A[0], inv, bq[0]), fmaf(A[1], inv, bq[1]), fmaf(A[2], inv, bq[2]),
+                            fmaf(A[3], inv, bq[3]));
+          } else {
+            o = make_float4(A[0], A[1], A[2], A[3]);
+          }
+          *reinterpret_cast<float4*>(out + seg * ldOut + f0) = o;
+          if ((g & 1) == 0) {
+            seg_max[seg * ldStat + h] = M;
+            seg_sum[seg * ldStat + h] = S;
+          }
+        } else {
+          float* pr = part + int64_t(w.slot) * PART;
+          *reinterpret_cast<float4*>(pr + f0) = make_float4(A[0], A[1], A[2], A[3]);
+          if ((g & 1) == 0) {
+            pr[F + h] = M;
+            pr[F + H + h] = S;
+          }
+        }
+      }
+    }
+  }
+  wait_vm(std::integral_constant<int, 0>{});  // no LDS-DMA outstanding at the end of the wave
+}
+
+// =============================================================================================
 // backward of the camera attention, XLc recomputed from P
 // =============================================================================================
 // per workgroup partial row: [32 datt | 32 dbias]
@@ -1046,10 +1435,7 @@ __device__ __forceinline__ void prod_c2(const float4* __restrict__ Q, const f32x
 #ifndef GASFM_PBWD_BF
 #define GASFM_PBWD_BF 0
 #endif
-__device__ __forceinline__ gasfm_work_item uniform_item(const gasfm_work_item& w) {
-  return gasfm_work_item{__builtin_amdgcn_readfirstlane(w.seg), __builtin_amdgcn_readfirstlane(w.begin),
-                         __builtin_amdgcn_readfirstlane(w.end), __builtin_amdgcn_readfirstlane(w.slot)};
-}
+
 template <bool LN, bool RES, bool EPI, bool DWP, bool XP = false>
 __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kernel(
     const float* __restrict__ P, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
@@ -1750,6 +2136,27 @@ extern "C" int gasfm_edge_seam_fwd(const float* Pb, const float* P0, const int32
                        pos, XR, ldXR, att, bias, slope, items, n_items, finalize, out, ldOut, seg_max, seg_sum,
                        ldStat, part);
   };
+  if (tune(GASFM_TUNE_SEAM_LDS) != 0) {
+    note_dispatch(GASFM_K_SEAM_LDS);
+    auto launch_lds = [&](auto kern) {
+      static bool attr = false;  // > 64 KB of LDS per workgroup (static + dynamic)
+      if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  int(SL_DYN));
+        attr = true;
+      }
+      const int grid = resident_grid(reinterpret_cast<const void*>(kern), kThreads, SL_DYN, n_items, kWaves);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), SL_DYN, st, ep, ln_w, ln_b, eps, Wpt, bpt, Wc, bc, XLp,
+                         ldXLp, pos, XR, ldXR, att, bias, slope, items, n_items, finalize, out, ldOut, seg_max,
+                         seg_sum, ldStat, part);
+    };
+    if (ln_w)
+      launch_lds(&edge_seam_lds_kernel<true>);
+    else
+      launch_lds(&edge_seam_lds_kernel<false>);
+    return launch_status("gasfm_edge_seam_fwd");
+  }
+  note_dispatch(GASFM_K_SEAM_REG);
   if (ln_w)
     launch(&edge_seam_fwd_kernel<true, false>);
   else

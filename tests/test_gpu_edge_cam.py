@@ -263,3 +263,36 @@ def test_dxl_point_order_bitwise(device, monkeypatch, pbwd):
             assert seen and all(s == pt for s in seen), seen
     for k, g0 in res[False].items():
         assert torch.equal(res[True][k], g0), k
+
+
+@pytest.mark.parametrize("max_piece", [None, 48])
+def test_seam_lds_bitwise(device, max_piece):
+    """The forward seam with its inputs staged through LDS two tiles ahead (gasfm_tuning_set
+    seam_lds, csrc/edge_cam.hip edge_seam_lds_kernel) against the register-prefetch seam: the same
+    arithmetic, so the forward outputs and every parameter gradient are bitwise identical.  5 blocks
+    (seams into blocks 2-4 and the final update's LayerNorm-free seam); max_piece 48: items of 3
+    tiles, the last one ragged, split cameras with partial rows."""
+    from oracle.weights import deterministic_state_dict
+    sc = synthetic.scaled_config4(0.05, seed=19)
+    data = gasfm_amd.SceneData.from_synthetic(sc, max_piece=max_piece).to(device)
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=5))
+    sd = deterministic_state_dict(net.state_dict(), torch.float64)
+    net.load_state_dict({k: v.float() for k, v in sd.items()})
+    net = net.to(device)
+    gen = torch.Generator().manual_seed(9)
+    cP = torch.randn((sc.m, 3, 4), generator=gen).to(device)
+    cX = torch.randn((4, sc.n), generator=gen).to(device)
+    res = {}
+    for lds in (0, 1):
+        with _native.tuned(seam_lds=lds), _native.dispatch_record() as rec:
+            net.zero_grad(set_to_none=True)
+            pred = net(data)
+            ((pred["Ps_norm"] * cP).sum() + (pred["pts3D"] * cX).sum()).backward()
+            torch.cuda.synchronize()
+        assert rec.counts["seam_lds" if lds else "seam_reg"] >= 4 and rec.counts["seam_reg" if lds else "seam_lds"] == 0, \
+            rec.counts
+        res[lds] = (pred["Ps_norm"].detach().clone(), pred["pts3D"].detach().clone(),
+                    {k: p.grad.detach().clone() for k, p in net.named_parameters()})
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    for k, g0 in res[0][2].items():
+        assert torch.equal(res[1][2][k], g0), k

@@ -1,7 +1,7 @@
 # round 4: parity of the fused global convs and of the point-ordered dXL path (+ the branch-free
 # pbwd build), then same-box A/Bs on config 4 (20 replayed steps, 2 alternations) and the
-# rank-0-of-8 proxy, then a kernel trace of the proxy.  Libraries: libgasfm_base.so = the tree
-# before the dXL change, libgasfm.so = this tree, libgasfm_bf.so = this tree with GASFM_PBWD_BF=1.
+# rank-0-of-8 proxy, then a kernel trace of the proxy.  Libraries: libgasfm.so = this tree,
+# libgasfm_bf.so = this tree with GASFM_PBWD_BF=1; GASFM_SEAM_LDS=1: the LDS-staged forward seam.
 set -o pipefail
 mkdir -p gpurun_out
 T="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
@@ -16,12 +16,13 @@ run() {  # label, env..., -- bench args
 }
 for rep in 1 2; do
   EXTRA=""
-  run base GASFM_LIB=$PWD/gasfm_amd/libgasfm_base.so
+  run seam_lds GASFM_SEAM_LDS=1
   run new GASFM_DXL_PT=0
   run new+dxl GASFM_DXL_PT=1
   run bf+dxl GASFM_DXL_PT=1 GASFM_LIB=$PWD/gasfm_amd/libgasfm_bf.so
   run bf GASFM_DXL_PT=0 GASFM_LIB=$PWD/gasfm_amd/libgasfm_bf.so
   run new+dxl,gatt0 GASFM_DXL_PT=1 GASFM_GLOBAL_ATTN=0
+  run seam_lds+dxl GASFM_SEAM_LDS=1 GASFM_DXL_PT=1
 done
 for rep in 1 2; do
   EXTRA="--emulate-world 8"
