@@ -918,7 +918,9 @@ __global__ __launch_bounds__(kThreads, 2) void edge_seam_lds_kernel(
   };
   auto walk_rows = [](const Walk& k) { return int(k.w.end - k.row0 < TR ? k.w.end - k.row0 : TR); };
   // I stage of the walker's tile into index slot s (2 requests)
+  // (a wave without any tile issues nothing: its walkers never had a tile to stay on)
   auto stage_i = [&](const Walk& k, int s) {
+    if (k.w.begin >= k.w.end) return;
     float* ix = ixr + s * SL_IXF;
     const int nr = walk_rows(k);
     const int rr = (lane & 15) < nr ? (lane & 15) : 0;
@@ -937,6 +939,7 @@ __global__ __launch_bounds__(kThreads, 2) void edge_seam_lds_kernel(
   };
   // A / B stages of the walker's tile into P / Sp slot s (2 + 2 requests); pt from index slot si
   auto stage_ab = [&](const Walk& k, int s, int si) {
+    if (k.w.begin >= k.w.end) return;
     float* ps = ring + s * SL_PSF;
     const int32_t* ix = reinterpret_cast<const int32_t*>(ixr + si * SL_IXF);
     const int nr = walk_rows(k);
