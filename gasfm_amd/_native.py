@@ -245,9 +245,10 @@ KERNELS = {
     "attn_fwd_grp": 0, "attn_fwd_glds": 1, "attn_fwd_vec": 2, "attn_fwd_generic": 3, "attn_fwd_lanes": 4,
     "attn_bwd_glds": 5, "attn_bwd_vec": 6, "attn_bwd_generic": 7, "attn_bwd_lanes": 8,
     "attn_combine_vec": 9, "attn_combine_generic": 10, "attn_bwd_grp": 11, "seam_lds": 12, "seam_reg": 13,
+    "rowsum_grp": 14,
 }
 TUNING = {"attn_grp_rows": 0, "attn_grp_min_fill": 1, "attn_glds": 2, "attn_wave_cap": 3, "attn_grp_bwd": 4,
-          "seam_lds": 5}
+          "seam_lds": 5, "rowsum_grp": 6}
 
 
 def dispatch_counts():

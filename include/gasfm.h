@@ -78,6 +78,7 @@ enum {
   GASFM_K_ATTN_BWD_GRP = 11,     /* grouped items backward (32-wide, streamed XL) */
   GASFM_K_SEAM_LDS = 12,         /* forward seam with its inputs staged through LDS (round 4) */
   GASFM_K_SEAM_REG = 13,         /* forward seam with its inputs prefetched into registers */
+  GASFM_K_ROWSUM_GRP = 14,       /* segment row sums, 8 segments per wave task */
   GASFM_K_COUNT = 16
 };
 
@@ -94,6 +95,7 @@ enum {
   GASFM_TUNE_ATTN_WAVE_CAP = 3,      /* GASFM_ATTN_WAVES: cap on item-loop waves, 0 = occupancy */
   GASFM_TUNE_ATTN_GRP_BWD = 4,       /* grouped backward on (1) / off (0) */
   GASFM_TUNE_SEAM_LDS = 5,           /* GASFM_SEAM_LDS: forward seam (blocks 1-11) LDS-staged (1) / registers (0) */
+  GASFM_TUNE_ROWSUM_GRP = 6,         /* GASFM_ROWSUM_GRP: gasfm_segment_rowsum grouped (1) / one item per wave (0) */
   GASFM_TUNE_COUNT = 8
 };
 int gasfm_tuning_set(int32_t key, double value);
