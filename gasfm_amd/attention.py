@@ -50,9 +50,13 @@ LANES_MAX_AVG = 32  # 4-wide convs with <= this many edges per item on average: 
 # general kernel.
 BWD_LANES = os.environ.get("GASFM_ATTN_BWD_LANES", "1") != "0"
 # The two convs onto the global node as ONE forward and ONE backward launch (global_attn.hip, round
-# 4) instead of an attention kernel + ordered combines per conv (~6 launches each way per block);
-# GASFM_GLOBAL_ATTN=0 restores the general plan kernels (the A/B knob).
-GLOBAL_ATTN = os.environ.get("GASFM_GLOBAL_ATTN", "1") != "0"
+# 4) instead of an attention kernel + ordered combines per conv (~6 launches each way per block).
+# Measured slower, so off by default (GASFM_GLOBAL_ATTN=1 turns it on): its workgroups walk 64 views
+# / 2048 points one source step at a time (15 workgroups on a rank of 8, 114 at one GPU) and the
+# last arriver merges the slots serially; gatt_fwd 53 us + gatt_bwd 81 us per block on the
+# rank-0-of-8 proxy, where the plan kernels + combines take ~65 us: config 4 29.58-29.60 ms without
+# vs 30.27-30.43 with, the proxy 8.03 vs 8.91 ms (same box, tools/gpu_r4_ab3.sh, profiles/r4_ab3.txt).
+GLOBAL_ATTN = os.environ.get("GASFM_GLOBAL_ATTN", "0") != "0"
 
 
 def gatt_ok(plan, heads, XL, XR, att):

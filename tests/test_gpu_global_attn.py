@@ -15,6 +15,13 @@ from gasfm_amd.attention import AttnPlan, GlobalPairFn
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _fused_global_convs(monkeypatch):
+    """The fused kernels are an option (attention.GLOBAL_ATTN, off by default): on for these tests."""
+    from gasfm_amd import attention
+    monkeypatch.setattr(attention, "GLOBAL_ATTN", True)
+
 H = 4
 SLOPE = 0.2
 
