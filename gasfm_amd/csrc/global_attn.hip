@@ -5,7 +5,7 @@
 // Round 3 ran each conv as a work-item attention kernel plus one or two ordered combine launches
 // (points -> global: ~4k short pieces, a two-level combine) and, backward, a kernel plus a colsum:
 // ~6 launches each way per block, each a few us of latency.  Here a workgroup takes a chunk of
-// sources (64 views, 2048 points), keeps an online softmax state (max, sum, acc) per head and
+// sources (8 views, 256 points; round 4), keeps an online softmax state (max, sum, acc) per head and
 // writes it to a slot; the problem's LAST-arriving workgroup (write-through stores, one relaxed
 // agent-scope ticket: reduce.hip's hand-off) merges the slots -- max, then the rescaled sums,
 // parallel over slots with a fixed association order -- and writes the output + statistics, or
@@ -27,8 +27,17 @@ namespace {
 
 constexpr int kT = 256;
 constexpr int H = 4;
-constexpr int kChunkV = 64;    // sources per workgroup, C = 256
-constexpr int kChunkP = 2048;  // sources per workgroup, C = 16
+// sources per workgroup (round 4 retune: 64 / 2048 left 15 workgroups on a rank of 8 walking their
+// chunks one step at a time, 53 + 81 us per block; the slots are now read back by plain batched
+// loads, so more, shorter chunks cost little at the merge)
+#ifndef GASFM_GATT_CHUNK_V
+#define GASFM_GATT_CHUNK_V 8
+#endif
+#ifndef GASFM_GATT_CHUNK_P
+#define GASFM_GATT_CHUNK_P 256
+#endif
+constexpr int kChunkV = GASFM_GATT_CHUNK_V;  // sources per workgroup, C = 256
+constexpr int kChunkP = GASFM_GATT_CHUNK_P;  // sources per workgroup, C = 16
 constexpr int kMaxProb = 2;
 
 struct GaProb {
@@ -80,9 +89,6 @@ __device__ __forceinline__ int src_row(const GaProb& p, int j) { return p.src ? 
 __device__ __forceinline__ void st_sc1(float* q, float v) {
   __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ float ld_sc1(const float* q) {
-  return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // true for the problem's last-arriving workgroup (after its slot was stored write-through)
 __device__ __forceinline__ bool last_arrival(uint32_t* cnt, int n, uint32_t* flag) {
@@ -94,7 +100,9 @@ __device__ __forceinline__ bool last_arrival(uint32_t* cnt, int n, uint32_t* fla
   }
   __syncthreads();
   if (*flag == 0u) return false;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // agent-scope acquire: this CU's L1 holds no stale slot lines, so the merges read the slots with
+  // plain (batched, vector) loads instead of one relaxed atomic load per value
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   return true;
 }
 
@@ -110,7 +118,7 @@ __device__ void merge_fwd(const GaProb& p, float* sc) {
   {
     const int h = threadIdx.x & 3;
     float m = -INFINITY;
-    for (int k = threadIdx.x >> 2; k < n; k += kT / 4) m = fmaxf(m, ld_sc1(p.slots + int64_t(k) * L + p.HC + h));
+    for (int k = threadIdx.x >> 2; k < n; k += kT / 4) m = fmaxf(m, p.slots[int64_t(k) * L + p.HC + h]);
 #pragma unroll
     for (int o = 32; o >= 4; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     __syncthreads();
@@ -127,7 +135,7 @@ __device__ void merge_fwd(const GaProb& p, float* sc) {
     float s = 0.f;
     for (int k = threadIdx.x >> 2; k < n; k += kT / 4) {
       const float* q = p.slots + int64_t(k) * L + p.HC;
-      const float mk = ld_sc1(q + h), sk = ld_sc1(q + H + h);
+      const float mk = q[h], sk = q[H + h];
       s += mk == -INFINITY ? 0.f : sk * __expf(mk - M);
     }
 #pragma unroll
@@ -160,14 +168,16 @@ __device__ void merge_fwd(const GaProb& p, float* sc) {
   if (p.C == 256) {
     const int f0 = 4 * threadIdx.x, h = f0 / 256;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
     for (int k = 0; k < n; ++k) {
       const float* q = p.slots + int64_t(k) * L;
-      const float mk = ld_sc1(q + p.HC + h);
+      const float mk = q[p.HC + h];
       const float w = mk == -INFINITY ? 0.f : __expf(mk - MH[h]);
-      a.x = fmaf(ld_sc1(q + f0), w, a.x);
-      a.y = fmaf(ld_sc1(q + f0 + 1), w, a.y);
-      a.z = fmaf(ld_sc1(q + f0 + 2), w, a.z);
-      a.w = fmaf(ld_sc1(q + f0 + 3), w, a.w);
+      const float4 v = *reinterpret_cast<const float4*>(q + f0);  // L % 4 == 0
+      a.x = fmaf(v.x, w, a.x);
+      a.y = fmaf(v.y, w, a.y);
+      a.z = fmaf(v.z, w, a.z);
+      a.w = fmaf(v.w, w, a.w);
     }
     finish(f0, a.x);
     finish(f0 + 1, a.y);
@@ -177,10 +187,11 @@ __device__ void merge_fwd(const GaProb& p, float* sc) {
     const int f = threadIdx.x & 63, grp = threadIdx.x >> 6, h = f / p.C;
     float a = 0.f;
     if (f < p.HC)
+#pragma unroll 8
       for (int k = grp; k < n; k += 4) {
         const float* q = p.slots + int64_t(k) * L;
-        const float mk = ld_sc1(q + p.HC + h);
-        a = fmaf(ld_sc1(q + f), mk == -INFINITY ? 0.f : __expf(mk - MH[h]), a);
+        const float mk = q[p.HC + h];
+        a = fmaf(q[f], mk == -INFINITY ? 0.f : __expf(mk - MH[h]), a);
       }
     accg[grp][f] = a;
     __syncthreads();
@@ -323,12 +334,13 @@ __device__ void merge_bwd(const GaProb& p) {
     for (int half = 0; half < 2; ++half) {
       const int f0 = 4 * threadIdx.x;
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
       for (int k = 0; k < n; ++k) {
-        const float* q = p.slots + int64_t(k) * L + half * p.HC + f0;
-        a.x += ld_sc1(q);
-        a.y += ld_sc1(q + 1);
-        a.z += ld_sc1(q + 2);
-        a.w += ld_sc1(q + 3);
+        const float4 v = *reinterpret_cast<const float4*>(p.slots + int64_t(k) * L + half * p.HC + f0);
+        a.x += v.x;
+        a.y += v.y;
+        a.z += v.z;
+        a.w += v.w;
       }
       float* d = half ? p.datt : p.dXR;
       d[f0] = a.x;
@@ -345,7 +357,8 @@ __device__ void merge_bwd(const GaProb& p) {
       const int v = (threadIdx.x & 63) + 64 * r;
       float a = 0.f;
       if (v < L)
-        for (int k = grp; k < n; k += 4) a += ld_sc1(p.slots + int64_t(k) * L + v);
+#pragma unroll 8
+        for (int k = grp; k < n; k += 4) a += p.slots[int64_t(k) * L + v];
       acc4[grp][v] = a;
     }
     __syncthreads();
