@@ -51,18 +51,22 @@ LANES_MAX_AVG = 32  # 4-wide convs with <= this many edges per item on average: 
 BWD_LANES = os.environ.get("GASFM_ATTN_BWD_LANES", "1") != "0"
 # The two convs onto the global node as ONE forward and ONE backward launch (global_attn.hip, round
 # 4) instead of an attention kernel + ordered combines per conv (~6 launches each way per block).
-# Measured slower, so off by default (GASFM_GLOBAL_ATTN=1 turns it on): its workgroups walk 64 views
-# / 2048 points one source step at a time (15 workgroups on a rank of 8, 114 at one GPU) and the
-# last arriver merges the slots serially; gatt_fwd 53 us + gatt_bwd 81 us per block on the
-# rank-0-of-8 proxy, where the plan kernels + combines take ~65 us: config 4 29.58-29.60 ms without
-# vs 30.27-30.43 with, the proxy 8.03 vs 8.91 ms (same box, tools/gpu_r4_ab3.sh, profiles/r4_ab3.txt).
-GLOBAL_ATTN = os.environ.get("GASFM_GLOBAL_ATTN", "0") != "0"
+# Taken for point sets of at most GATT_MAX_SRC sources (a rank's shard), where it measured faster:
+# rank-0-of-8 proxy 8.00-8.02 -> 7.71 ms; for a whole config-4 scene (200k points: 782 chunks
+# merged by one workgroup) it is slower (29.56-29.75 -> 30.03-30.10 ms), profiles/r4_ab5.txt.
+# (The first version, 64-view / 2048-point chunks merged through atomic loads: 8.03 -> 8.91 and
+# 29.59 -> 30.35 ms, profiles/r4_ab3.txt.)  GASFM_GLOBAL_ATTN=0 / 1 forces it off / on.
+_GATT_ENV = os.environ.get("GASFM_GLOBAL_ATTN", "auto")
+GLOBAL_ATTN = _GATT_ENV != "0"
+GATT_MAX_SRC = int(os.environ.get("GASFM_GATT_MAX_SRC", "65536")) if _GATT_ENV == "auto" else 1 << 62
 
 
 def gatt_ok(plan, heads, XL, XR, att):
     """Whether the fused global-conv kernels take this single-target conv (H = 4, C in {16, 256})."""
     HC = att.numel()
     if not GLOBAL_ATTN or plan.num_targets != 1 or heads != 4 or HC not in (64, 1024):
+        return False
+    if plan.num_edges > GATT_MAX_SRC:
         return False
     if XL.dim() != 2 or XL.shape[1] != HC or XL.stride(1) != 1 or XL.stride(0) % 4 or XL.data_ptr() % 16:
         return False

@@ -1259,8 +1259,10 @@ extern "C" int gasfm_gat_attn_fwd(const float* XL, int64_t ldXL, const float* XR
   return launch_status("gasfm_gat_attn_fwd");
 }
 
+// 1 (default since round 4): rank-0-of-8 proxy 8.00-8.02 -> 7.88 ms, config 4 unchanged (29.56-29.75
+// vs 29.60-29.71), profiles/r4_ab5.txt
 #ifndef GASFM_COMBINE_SMALL
-#define GASFM_COMBINE_SMALL 0
+#define GASFM_COMBINE_SMALL 1
 #endif
 extern "C" int gasfm_gat_attn_combine(const gasfm_combine_item* combine, int32_t n_combine, int32_t H,
                                       int32_t C, const float* part, const float* bias, int32_t finalize, float* out,

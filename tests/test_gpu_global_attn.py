@@ -18,9 +18,11 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(autouse=True)
 def _fused_global_convs(monkeypatch):
-    """The fused kernels are an option (attention.GLOBAL_ATTN, off by default): on for these tests."""
+    """The fused kernels are taken for shard-size point sets only (attention.GATT_MAX_SRC): on for
+    every size in these tests."""
     from gasfm_amd import attention
     monkeypatch.setattr(attention, "GLOBAL_ATTN", True)
+    monkeypatch.setattr(attention, "GATT_MAX_SRC", 1 << 62)
 
 H = 4
 SLOPE = 0.2
