@@ -119,6 +119,7 @@ _SIGS = {
     "gasfm_gchain_counters": (_i32, [_vp]),
     "gasfm_gchain_bwd": (_i32, [_vp] * 16),
     "gasfm_gatt_scratch_floats": (_i64, [_i32, _vp]),
+    "gasfm_gatt_counters": (_i32, [_i32, _vp]),
     "gasfm_gatt_fwd": (_i32, [_i32, _vp, _f32, _vp, _vp, _vp]),
     "gasfm_gatt_bwd": (_i32, [_i32, _vp, _f32, _vp, _vp, _vp]),
     "gasfm_gatt_merge": (_i32, [_i32, _vp, _i32, _i64, _vp]),
@@ -1254,7 +1255,7 @@ def gatt_fwd(probs, slope):
     L = lib()
     dev = probs[0]["XL"].device
     ws = torch.empty(int(L.gasfm_gatt_scratch_floats(len(probs), ctypes.addressof(arr))), dtype=torch.float32, device=dev)
-    cnt = _counters(dev, len(probs))
+    cnt = _counters(dev, int(L.gasfm_gatt_counters(len(probs), ctypes.addressof(arr))))
     check(L.gasfm_gatt_fwd(len(probs), ctypes.addressof(arr), float(slope), _p(ws), _p(cnt), _stream(probs[0]["XL"])),
           "gasfm_gatt_fwd")
 
@@ -1265,7 +1266,7 @@ def gatt_bwd(probs, slope):
     L = lib()
     dev = probs[0]["XL"].device
     ws = torch.empty(int(L.gasfm_gatt_scratch_floats(len(probs), ctypes.addressof(arr))), dtype=torch.float32, device=dev)
-    cnt = _counters(dev, len(probs))
+    cnt = _counters(dev, int(L.gasfm_gatt_counters(len(probs), ctypes.addressof(arr))))
     check(L.gasfm_gatt_bwd(len(probs), ctypes.addressof(arr), float(slope), _p(ws), _p(cnt), _stream(probs[0]["XL"])),
           "gasfm_gatt_bwd")
 

@@ -39,6 +39,9 @@ constexpr int H = 4;
 constexpr int kChunkV = GASFM_GATT_CHUNK_V;  // sources per workgroup, C = 256
 constexpr int kChunkP = GASFM_GATT_CHUNK_P;  // sources per workgroup, C = 16
 constexpr int kMaxProb = 2;
+// slots per first-level group: a whole config-4 scene's 200k points are 782 chunks, which one
+// workgroup merged in ~25 us; 25 groups of 32 merge in parallel, then 25 group rows
+constexpr int kGroup = 32;
 
 struct GaProb {
   const float* XL;
@@ -60,6 +63,11 @@ struct GaProb {
   uint32_t* cnt;   // the problem's ticket
   int64_t sl;      // forward slot stride
   int S, HC, C, blk0, nblk;
+  // two-level merge (nblk > kGroup): groups of kGroup consecutive slots are merged by their own
+  // last arriver into group rows (same layout), and the last group merges the group rows
+  float* gslots;   // [ngroups, slot floats]
+  uint32_t* gcnt;  // [ngroups] tickets
+  int ngroups;
 };
 struct GaArgs {
   GaProb p[kMaxProb];
@@ -151,11 +159,11 @@ __device__ void merge_fwd(const GaProb& p, float* sc) {
   // 4 slot groups (k = grp, grp + 4, ..), the groups added in order
   auto finish = [&](int f, float a) {
     const int h = f / p.C;
-    if (p.part) {
-      p.part[f] = a;
+    if (p.part) {  // write-through: a group row is merged by another workgroup in this launch
+      st_sc1(p.part + f, a);
       if (f < H) {
-        p.part[p.HC + f] = MH[f];
-        p.part[p.HC + H + f] = SH[f];
+        st_sc1(p.part + p.HC + f, MH[f]);
+        st_sc1(p.part + p.HC + H + f, SH[f]);
       }
     } else {
       p.out[f] = a / (SH[h] + 1e-16f) + p.bias[f];
@@ -199,6 +207,34 @@ __device__ void merge_fwd(const GaProb& p, float* sc) {
   }
 }
 
+// after a workgroup's slot is stored: the merge, by the problem's last arriver (one level), or by
+// the group's last arriver into the group row and then the last group's into the output
+__device__ void done_fwd(const GaProb& p, int blk, uint32_t* flag, float* sc) {
+  if (p.ngroups <= 1) {
+    if (last_arrival(p.cnt, p.nblk, flag)) {
+      merge_fwd(p, sc);
+      if (threadIdx.x == 0) __hip_atomic_store(p.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  const int g = blk / kGroup, n0 = g * kGroup;
+  const int ng = p.nblk - n0 < kGroup ? p.nblk - n0 : kGroup;
+  if (!last_arrival(p.gcnt + g, ng, flag)) return;
+  GaProb q = p;  // the group's slots -> its raw (packed) group row
+  q.slots = p.slots + int64_t(n0) * p.sl;
+  q.nblk = ng;
+  q.part = p.gslots + int64_t(g) * p.sl;
+  merge_fwd(q, sc);
+  if (threadIdx.x == 0) __hip_atomic_store(p.gcnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (!last_arrival(p.cnt, p.ngroups, flag)) return;
+  GaProb r = p;  // the group rows -> the output (or the exchange's packed row)
+  r.slots = p.gslots;
+  r.nblk = p.ngroups;
+  merge_fwd(r, sc);
+  if (threadIdx.x == 0) __hip_atomic_store(p.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // --------------------------------------------------------------------------------- forward
 __device__ void fwd_views(const GaProb& p, int blk, float slope, uint32_t* flag, float* sc) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -233,10 +269,7 @@ __device__ void fwd_views(const GaProb& p, int blk, float slope, uint32_t* flag,
     st_sc1(slot + p.HC + wave, m);
     st_sc1(slot + p.HC + H + wave, s);
   }
-  if (last_arrival(p.cnt, p.nblk, flag)) {
-    merge_fwd(p, sc);
-    if (threadIdx.x == 0) __hip_atomic_store(p.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  done_fwd(p, blk, flag, sc);
 }
 
 // C = 16: thread (ql = tid >> 4: source lane, fq = tid & 15: features 4 fq.., head fq >> 2)
@@ -307,10 +340,7 @@ __device__ void fwd_points(const GaProb& p, int blk, float slope, uint32_t* flag
       st_sc1(slot + p.HC + H + hh, S);
     }
   }
-  if (last_arrival(p.cnt, p.nblk, flag)) {
-    merge_fwd(p, sc);
-    if (threadIdx.x == 0) __hip_atomic_store(p.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  done_fwd(p, blk, flag, sc);
 }
 
 __global__ __launch_bounds__(kT) void gatt_fwd_kernel(GaArgs a) {
@@ -327,7 +357,8 @@ __global__ __launch_bounds__(kT) void gatt_fwd_kernel(GaArgs a) {
 
 // -------------------------------------------------------------------------------- backward
 // slots [nblk][2 HC] (dXR | datt); the last arriver sums them in slot order
-__device__ void merge_bwd(const GaProb& p) {
+// final == false (first level of a two-level merge): the raw sums go to grow [2 HC] (write-through)
+__device__ void merge_bwd(const GaProb& p, bool final = true, float* grow = nullptr) {
   __shared__ float acc4[4][2 * 64];
   const int L = 2 * p.HC, n = p.nblk;
   if (p.C == 256) {  // thread t: features 4t..4t+3 of both halves
@@ -342,14 +373,23 @@ __device__ void merge_bwd(const GaProb& p) {
         a.z += v.z;
         a.w += v.w;
       }
+      if (!final) {
+        float* d = grow + half * p.HC + f0;
+        st_sc1(d, a.x);
+        st_sc1(d + 1, a.y);
+        st_sc1(d + 2, a.z);
+        st_sc1(d + 3, a.w);
+        continue;
+      }
       float* d = half ? p.datt : p.dXR;
       d[f0] = a.x;
       d[f0 + 1] = a.y;
       d[f0 + 2] = a.z;
       d[f0 + 3] = a.w;
     }
-    *reinterpret_cast<float4*>(p.datt + p.HC + 4 * threadIdx.x) =
-        *reinterpret_cast<const float4*>(p.gout + 4 * threadIdx.x);
+    if (final)
+      *reinterpret_cast<float4*>(p.datt + p.HC + 4 * threadIdx.x) =
+          *reinterpret_cast<const float4*>(p.gout + 4 * threadIdx.x);
   } else {  // 2 HC = 128 values x 4 slot groups (256 threads: value v = tid & 63 (+ 64), group tid >> 6)
     const int grp = threadIdx.x >> 6;
 #pragma unroll
@@ -364,13 +404,41 @@ __device__ void merge_bwd(const GaProb& p) {
     __syncthreads();
     if (threadIdx.x < L) {
       const float a = (acc4[0][threadIdx.x] + acc4[1][threadIdx.x]) + (acc4[2][threadIdx.x] + acc4[3][threadIdx.x]);
-      if (threadIdx.x < p.HC)
+      if (!final)
+        st_sc1(grow + threadIdx.x, a);
+      else if (threadIdx.x < p.HC)
         p.dXR[threadIdx.x] = a;
       else
         p.datt[threadIdx.x - p.HC] = a;
     }
-    if (threadIdx.x < p.HC) p.datt[p.HC + threadIdx.x] = p.gout[threadIdx.x];
+    if (final && threadIdx.x < p.HC) p.datt[p.HC + threadIdx.x] = p.gout[threadIdx.x];
   }
+}
+
+__device__ void done_bwd(const GaProb& p, int blk, uint32_t* flag) {
+  if (p.ngroups <= 1) {
+    if (last_arrival(p.cnt, p.nblk, flag)) {
+      merge_bwd(p);
+      if (threadIdx.x == 0) __hip_atomic_store(p.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  const int g = blk / kGroup, n0 = g * kGroup;
+  const int ng = p.nblk - n0 < kGroup ? p.nblk - n0 : kGroup;
+  if (!last_arrival(p.gcnt + g, ng, flag)) return;
+  const int64_t L = 2 * int64_t(p.HC);
+  GaProb q = p;
+  q.slots = p.slots + int64_t(n0) * L;
+  q.nblk = ng;
+  merge_bwd(q, false, p.gslots + int64_t(g) * L);
+  if (threadIdx.x == 0) __hip_atomic_store(p.gcnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (!last_arrival(p.cnt, p.ngroups, flag)) return;
+  GaProb r = p;
+  r.slots = p.gslots;
+  r.nblk = p.ngroups;
+  merge_bwd(r);
+  if (threadIdx.x == 0) __hip_atomic_store(p.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ void bwd_views(const GaProb& p, int blk, float slope, uint32_t* flag) {
@@ -433,10 +501,7 @@ __device__ void bwd_views(const GaProb& p, int blk, float slope, uint32_t* flag)
   st_sc1(slot + p.HC + f0 + 2, dat.z);
   st_sc1(slot + p.HC + f0 + 3, dat.w);
   (void)lane;
-  if (last_arrival(p.cnt, p.nblk, flag)) {
-    merge_bwd(p);
-    if (threadIdx.x == 0) __hip_atomic_store(p.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  done_bwd(p, blk, flag);
 }
 
 __device__ void bwd_points(const GaProb& p, int blk, float slope, uint32_t* flag) {
@@ -516,10 +581,7 @@ __device__ void bwd_points(const GaProb& p, int blk, float slope, uint32_t* flag
     st_sc1(d + 2, sum.z);
     st_sc1(d + 3, sum.w);
   }
-  if (last_arrival(p.cnt, p.nblk, flag)) {
-    merge_bwd(p);
-    if (threadIdx.x == 0) __hip_atomic_store(p.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  done_bwd(p, blk, flag);
 }
 
 __global__ __launch_bounds__(kT) void gatt_bwd_kernel(GaArgs a) {
@@ -541,10 +603,13 @@ __global__ __launch_bounds__(kT) void gatt_merge_kernel(GaArgs a) {
 
 int chunk_of(int C) { return C == 256 ? kChunkV : kChunkP; }
 
+int groups_of(int nblk) { return nblk > kGroup ? (nblk + kGroup - 1) / kGroup : 1; }
+
 int setup(const gasfm_gatt_prob* in, int nprob, float* scratch, uint32_t* counters, bool bwd, GaArgs& a) {
   a.nprob = nprob;
   int blocks = 0;
   float* ws = scratch;
+  uint32_t* cn = counters;
   for (int q = 0; q < nprob; ++q) {
     const gasfm_gatt_prob& s = in[q];
     GaProb& p = a.p[q];
@@ -557,8 +622,14 @@ int setup(const gasfm_gatt_prob* in, int nprob, float* scratch, uint32_t* counte
     p.blk0 = blocks;
     p.slots = ws;
     p.sl = p.HC + 2 * H;
-    p.cnt = counters + q;
-    ws += int64_t(p.nblk) * (bwd ? 2 * p.HC : p.HC + 2 * H);
+    const int64_t slot = bwd ? 2 * p.HC : p.HC + 2 * H;
+    ws += int64_t(p.nblk) * slot;
+    p.ngroups = groups_of(p.nblk);
+    p.gslots = ws;
+    if (p.ngroups > 1) ws += int64_t(p.ngroups) * slot;
+    p.cnt = cn++;
+    p.gcnt = cn;
+    if (p.ngroups > 1) cn += p.ngroups;
     blocks += p.nblk;
   }
   for (int q = nprob; q < kMaxProb; ++q) a.p[q].blk0 = blocks;
@@ -590,14 +661,28 @@ static int gatt_check(int32_t nprob, const gasfm_gatt_prob* probs, bool bwd) {
   return GASFM_OK;
 }
 
+static int64_t nblk_of(const gasfm_gatt_prob& p) {
+  const int C = p.HC / H;
+  const int64_t nblk = (p.S + chunk_of(C) - 1) / chunk_of(C);
+  return nblk < 1 ? 1 : nblk;
+}
+
 extern "C" int64_t gasfm_gatt_scratch_floats(int32_t nprob, const gasfm_gatt_prob* probs) {
   int64_t n = 0;
   for (int q = 0; q < nprob; ++q) {
-    const int C = probs[q].HC / H;
-    const int64_t nblk = (probs[q].S + chunk_of(C) - 1) / chunk_of(C);
-    n += (nblk < 1 ? 1 : nblk) * (2 * int64_t(probs[q].HC) + 2 * H);
+    const int64_t nblk = nblk_of(probs[q]), ng = groups_of(int(nblk));
+    n += (nblk + (ng > 1 ? ng : 0)) * (2 * int64_t(probs[q].HC) + 2 * H);
   }
   return n + 16;
+}
+
+extern "C" int32_t gasfm_gatt_counters(int32_t nprob, const gasfm_gatt_prob* probs) {
+  int32_t n = 0;
+  for (int q = 0; q < nprob; ++q) {
+    const int ng = groups_of(int(nblk_of(probs[q])));
+    n += 1 + (ng > 1 ? ng : 0);
+  }
+  return n;
 }
 
 extern "C" int gasfm_gatt_fwd(int32_t nprob, const gasfm_gatt_prob* probs, float slope, float* scratch,
@@ -629,6 +714,7 @@ extern "C" int gasfm_gatt_merge(int32_t nprob, const gasfm_gatt_prob* probs, int
     p.slots = const_cast<float*>(s.part);
     p.sl = stride;
     p.nblk = nrows;
+    p.ngroups = 1;
   }
   hipLaunchKernelGGL(gatt_merge_kernel, dim3(nprob), dim3(kT), 0, reinterpret_cast<hipStream_t>(stream), a);
   return launch_status("gasfm_gatt_merge");

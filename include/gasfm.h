@@ -732,7 +732,9 @@ typedef struct gasfm_gatt_prob {
   float *dXR, *datt;
 } gasfm_gatt_prob;
 int64_t gasfm_gatt_scratch_floats(int32_t nprob, const gasfm_gatt_prob* probs);
-/* counters: nprob zeroed self-resetting tickets. */
+/* counters: gasfm_gatt_counters(nprob, probs) zeroed self-resetting tickets (one per problem, plus
+ * one per group of 32 source chunks when a problem has more than 32 chunks: two-level merge). */
+int32_t gasfm_gatt_counters(int32_t nprob, const gasfm_gatt_prob* probs);
 int gasfm_gatt_fwd(int32_t nprob, const gasfm_gatt_prob* probs, float slope, float* scratch, uint32_t* counters,
                    void* stream);
 int gasfm_gatt_bwd(int32_t nprob, const gasfm_gatt_prob* probs, float slope, float* scratch, uint32_t* counters,
