@@ -1428,8 +1428,9 @@ __device__ __forceinline__ void prod_c2(const float4* __restrict__ Q, const f32x
 #ifndef GASFM_PBWD_LW4
 #define GASFM_PBWD_LW4 0
 #endif
-// 1: no exec-mask branches inside the tile loop (round 4).  The work item is made wave-uniform
-// (scalar registers), so the next-tile choice is a scalar select; the dead-row masks of the
+// 3: no exec-mask branches inside the tile loop (round 4).  Bit 2: the work item is made
+// wave-uniform (scalar registers), so the next-tile choice is a scalar select; bit 1: the dead-row
+// masks of the
 // attention weights, the LayerNorm backward input, the dW / dWp operands and the dSv sums are
 // multiplications by a 0 / 1 factor (every masked value is finite: dead rows are clamped copies of
 // a live row) instead of selects the compiler turned into branches around LDS reads and v_exp,
@@ -1550,7 +1551,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   gasfm_work_item w{0, 0, 0, -1};
   if (gw < n_items) {
     w = items[gw];
-    if (GASFM_PBWD_BF) w = uniform_item(w);
+    if (GASFM_PBWD_BF & 2) w = uniform_item(w);
     if (w.begin < w.end) {
       issue(w.begin, rows_at(w, w.begin));
       issue_x();
@@ -1595,7 +1596,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
     gasfm_work_item wn{0, 0, 0, -1};
     const bool more = it + nw < n_items;
     if (more) wn = items[it + nw];
-    if (GASFM_PBWD_BF) wn = uniform_item(wn);
+    if (GASFM_PBWD_BF & 2) wn = uniform_item(wn);
     if (w.begin >= w.end && more && wn.begin < wn.end) {
       issue(wn.begin, rows_at(wn, wn.begin));
       issue_x();
@@ -1608,7 +1609,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
         RT[1] = nRT[1];
       }
       const float2 p0t = nP0;
-      if (GASFM_PBWD_BF) {  // the same choice as scalar selects (w, wn are wave-uniform)
+      if (GASFM_PBWD_BF & 2) {  // the same choice as scalar selects (w, wn are wave-uniform)
         const bool in_item = row0 + TR < w.end, nx = more && wn.begin < wn.end;
         const int64_t r1 = in_item ? row0 + TR : (nx ? int64_t(wn.begin) : row0);
         const int64_t e1 = in_item ? int64_t(w.end) : (nx ? int64_t(wn.end) : int64_t(w.end));
@@ -1679,7 +1680,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
         }
         p += __shfl_xor(p, 16);
         da += __shfl_xor(da, 16);
-        const float alpha = GASFM_PBWD_BF ? __expf(p - M[q]) * inv[q] * vmask : (valid ? __expf(p - M[q]) * inv[q] : 0.f);
+        const float alpha = (GASFM_PBWD_BF & 1) ? __expf(p - M[q]) * inv[q] * vmask : (valid ? __expf(p - M[q]) * inv[q] : 0.f);
         const float de = alpha * (da - delta[q]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1717,7 +1718,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
         for (int nt = 0; nt < 2; ++nt) {
           xh[nt] = LN ? (PC[nt][r] - mean) * rstd : PC[nt][r];
           ph[nt][r] = LN ? fmaxf(fmaf(xh[nt], gC[nt], bC[nt]), 0.f) : xh[nt];
-          float dy = GASFM_PBWD_BF ? dph[nt][r] * lm[r] : (live ? dph[nt][r] : 0.f);
+          float dy = (GASFM_PBWD_BF & 1) ? dph[nt][r] * lm[r] : (live ? dph[nt][r] : 0.f);
           if (LN) {
             dy = (fmaf(xh[nt], gC[nt], bC[nt]) > 0.f) ? dy : 0.f;
             dg[nt] = fmaf(dy, xh[nt], dg[nt]);
@@ -1762,8 +1763,8 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
         for (int r = 0; r < 4; ++r) {
           const bool live = 4 * g + r < nrows;
           // the item's column sums of dP (dSv) live in LDS: no registers held across tiles
-          Ls[0] += GASFM_PBWD_BF ? dv[r][0] * lm[r] : (live ? dv[r][0] : 0.f);
-          Ls[1] += GASFM_PBWD_BF ? dv[r][1] * lm[r] : (live ? dv[r][1] : 0.f);
+          Ls[0] += (GASFM_PBWD_BF & 1) ? dv[r][0] * lm[r] : (live ? dv[r][0] : 0.f);
+          Ls[1] += (GASFM_PBWD_BF & 1) ? dv[r][1] * lm[r] : (live ? dv[r][1] : 0.f);
           if (!GASFM_PBWD_EPI_T) {  // A/B: 16-lane sums per row (DPP), lanes c = 0, 1 store
             const float s0 = sum16(fmaf(dv[r][0], V[4 * F + c], dv[r][1] * V[4 * F + 16 + c]));
             const float s1 = sum16(fmaf(dv[r][0], V[5 * F + c], dv[r][1] * V[5 * F + 16 + c]));
@@ -1797,7 +1798,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
 #pragma unroll
       for (int ft = 0; ft < 2; ++ft)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) XC[ft][r] = GASFM_PBWD_BF ? XC[ft][r] * lm[r] : (4 * g + r < nrows ? XC[ft][r] : 0.f);
+        for (int r = 0; r < 4; ++r) XC[ft][r] = (GASFM_PBWD_BF & 1) ? XC[ft][r] * lm[r] : (4 * g + r < nrows ? XC[ft][r] : 0.f);
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2) {
 #pragma unroll
@@ -1818,7 +1819,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
           float rr[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            rr[r] = GASFM_PBWD_BF ? T2[(4 * g + r) * LDT + 16 * ft + c] * lm[r]
+            rr[r] = (GASFM_PBWD_BF & 1) ? T2[(4 * g + r) * LDT + 16 * ft + c] * lm[r]
                                   : (4 * g + r < nrows ? T2[(4 * g + r) * LDT + 16 * ft + c] : 0.f);
           f32x4 ap[2] = {zero4(), zero4()};
 #pragma unroll
