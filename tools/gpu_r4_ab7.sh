@@ -1,9 +1,12 @@
 # round 4: the fused global convs with the two-level merge: parity, then forced on (GASFM_GLOBAL_ATTN=1)
-# against the default (on for <= 64k point sources only) on config 4 and the proxy
+# against the default (on for <= 64k point sources only) on config 4 and the proxy; the mask-only
+# branch-free pbwd (libgasfm_bf1.so, GASFM_PBWD_BF=1)
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_global_attn.py tests/test_gpu_global.py -x -q --timeout 300 --timeout-method thread > gpurun_out/ab7_tests.log 2>&1 || { grep -B2 -A30 "^E \|FAILED" gpurun_out/ab7_tests.log | head -60; exit 1; }
 tail -1 gpurun_out/ab7_tests.log
+GASFM_LIB=$PWD/gasfm_amd/libgasfm_bf1.so timeout -k 10 300 python -u -m pytest tests/test_gpu_edge_cam.py -x -q --timeout 300 --timeout-method thread > gpurun_out/ab7_tests_bf1.log 2>&1 || { grep -B2 -A30 "^E \|FAILED" gpurun_out/ab7_tests_bf1.log | head -60; exit 1; }
+tail -1 gpurun_out/ab7_tests_bf1.log
 run() {
   local label=$1; shift
   env "$@" timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline $EXTRA > gpurun_out/ab7.json 2> gpurun_out/ab7.err || { tail -20 gpurun_out/ab7.err; exit 1; }
@@ -14,6 +17,7 @@ for rep in 1 2; do
   run default
   run gatt_on GASFM_GLOBAL_ATTN=1
   run gatt_off GASFM_GLOBAL_ATTN=0
+  run pbwd_bf1 GASFM_LIB=$PWD/gasfm_amd/libgasfm_bf1.so
   EXTRA="--emulate-world 8"
   run default
   run gatt_off GASFM_GLOBAL_ATTN=0
