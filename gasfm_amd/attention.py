@@ -51,14 +51,14 @@ LANES_MAX_AVG = 32  # 4-wide convs with <= this many edges per item on average: 
 BWD_LANES = os.environ.get("GASFM_ATTN_BWD_LANES", "1") != "0"
 # The two convs onto the global node as ONE forward and ONE backward launch (global_attn.hip, round
 # 4) instead of an attention kernel + ordered combines per conv (~6 launches each way per block).
-# Taken for point sets of at most GATT_MAX_SRC sources (a rank's shard), where it measured faster:
-# rank-0-of-8 proxy 8.00-8.02 -> 7.71 ms; for a whole config-4 scene (200k points: 782 chunks
-# merged by one workgroup) it is slower (29.56-29.75 -> 30.03-30.10 ms), profiles/r4_ab5.txt.
-# (The first version, 64-view / 2048-point chunks merged through atomic loads: 8.03 -> 8.91 and
-# 29.59 -> 30.35 ms, profiles/r4_ab3.txt.)  GASFM_GLOBAL_ATTN=0 / 1 forces it off / on.
-_GATT_ENV = os.environ.get("GASFM_GLOBAL_ATTN", "auto")
-GLOBAL_ATTN = _GATT_ENV != "0"
-GATT_MAX_SRC = int(os.environ.get("GASFM_GATT_MAX_SRC", "65536")) if _GATT_ENV == "auto" else 1 << 62
+# Measured in three versions on one box each: 64-view / 2048-point chunks with
+# atomic-load merges slower everywhere (profiles/r4_ab3.txt); 8 / 256 chunks with plain batched
+# merges faster on a rank's shard only (r4_ab5.txt); with the two-level merge faster at both sizes:
+# config 4 29.81-29.85 -> 29.51-29.60 ms, the rank-0-of-8 proxy 7.87-7.88 -> 7.61-7.62 ms
+# (r4_ab7.txt).  GASFM_GLOBAL_ATTN=0 restores the plan kernels; GASFM_GATT_MAX_SRC caps the point
+# sources it takes (default: no cap).
+GLOBAL_ATTN = os.environ.get("GASFM_GLOBAL_ATTN", "1") != "0"
+GATT_MAX_SRC = int(os.environ.get("GASFM_GATT_MAX_SRC", str(1 << 62)))
 
 
 def gatt_ok(plan, heads, XL, XR, att):
