@@ -244,17 +244,12 @@ __device__ void fwd_views(const GaProb& p, int blk, float slope, uint32_t* flag,
   const float4 at = *reinterpret_cast<const float4*>(p.att + f0);
   float m = -INFINITY, s = 0.f;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  // every row of the chunk requested at once (clamped to the chunk's last source; one latency)
-  float4 xs[kChunkV];
-  const int jl = j1 > j0 ? j1 - 1 : j0;
-#pragma unroll
-  for (int u = 0; u < kChunkV; ++u)
-    xs[u] = j0 < j1 ? *reinterpret_cast<const float4*>(p.XL + int64_t(src_row(p, j0 + u < j1 ? j0 + u : jl)) * p.ldXL + f0)
-                    : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-  for (int u = 0; u < kChunkV; ++u) {
-    if (j0 + u >= j1) break;
-    const float4 x = xs[u];
+  float4 nx = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (j0 < j1) nx = *reinterpret_cast<const float4*>(p.XL + int64_t(src_row(p, j0)) * p.ldXL + f0);
+  for (int j = j0; j < j1; ++j) {
+    const float4 x = nx;
+    const int jn = j + 1 < j1 ? j + 1 : j;
+    nx = *reinterpret_cast<const float4*>(p.XL + int64_t(src_row(p, jn)) * p.ldXL + f0);
     float e = leaky(x.x + xr.x, slope) * at.x + leaky(x.y + xr.y, slope) * at.y + leaky(x.z + xr.z, slope) * at.z +
               leaky(x.w + xr.w, slope) * at.w;
     e = wave_sum(e);
@@ -288,7 +283,7 @@ __device__ void fwd_points(const GaProb& p, int blk, float slope, uint32_t* flag
   const float4 at = *reinterpret_cast<const float4*>(p.att + f0);
   float m = -INFINITY, s = 0.f;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  constexpr int U = kChunkP / 16;  // a source lane's whole share of the chunk in flight together
+  constexpr int U = 4;  // sources per step per lane, loads in flight together
   for (int jb = j0 + ql; jb < j1; jb += 16 * U) {
     float4 x[U];
 #pragma unroll
@@ -459,20 +454,18 @@ __device__ void bwd_views(const GaProb& p, int blk, float slope, uint32_t* flag)
   const float delta =
       wave_sum(go.x * (o4.x - b4.x) + go.y * (o4.y - b4.y) + go.z * (o4.z - b4.z) + go.w * (o4.w - b4.w));
   float4 dxr = make_float4(0.f, 0.f, 0.f, 0.f), dat = dxr;
-  // every row of the chunk requested at once (clamped to the chunk's last source)
-  float4 xs[kChunkV];
-  int rs[kChunkV];
-  const int jl = j1 > j0 ? j1 - 1 : j0;
-#pragma unroll
-  for (int u = 0; u < kChunkV; ++u) rs[u] = j0 < j1 ? src_row(p, j0 + u < j1 ? j0 + u : jl) : 0;
-#pragma unroll
-  for (int u = 0; u < kChunkV; ++u)
-    xs[u] = j0 < j1 ? *reinterpret_cast<const float4*>(p.XL + int64_t(rs[u]) * p.ldXL + f0) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-  for (int u = 0; u < kChunkV; ++u) {
-    if (j0 + u >= j1) break;
-    const float4 x = xs[u];
-    const int row = rs[u];
+  int jr = 0;
+  float4 nx = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (j0 < j1) {
+    jr = src_row(p, j0);
+    nx = *reinterpret_cast<const float4*>(p.XL + int64_t(jr) * p.ldXL + f0);
+  }
+  for (int j = j0; j < j1; ++j) {
+    const float4 x = nx;
+    const int row = jr;
+    const int jn = j + 1 < j1 ? j + 1 : j;
+    jr = src_row(p, jn);
+    nx = *reinterpret_cast<const float4*>(p.XL + int64_t(jr) * p.ldXL + f0);
     const float z[4] = {x.x + xr.x, x.y + xr.y, x.z + xr.z, x.w + xr.w};
     const float a4[4] = {at.x, at.y, at.z, at.w};
     const float g4[4] = {go.x, go.y, go.z, go.w};
@@ -528,7 +521,7 @@ __device__ void bwd_points(const GaProb& p, int blk, float slope, uint32_t* flag
   const float a4[4] = {at.x, at.y, at.z, at.w};
   const float g4[4] = {go.x, go.y, go.z, go.w};
   float4 dxr = make_float4(0.f, 0.f, 0.f, 0.f), dat = dxr;
-  constexpr int U = kChunkP / 16;  // a source lane's whole share of the chunk in flight together
+  constexpr int U = 4;
   for (int jb = j0 + ql; jb < j1; jb += 16 * U) {
     float4 x[U];
     int rows[U];
