@@ -93,7 +93,7 @@ enum {
   GASFM_TUNE_ATTN_GRP_MIN_FILL = 1,  /* GASFM_ATTN_GRP_MIN_FILL: grouped when tasks >= fill x resident waves */
   GASFM_TUNE_ATTN_GLDS = 2,          /* GASFM_ATTN_GLDS: direct-to-LDS kernels on (1) / off (0) */
   GASFM_TUNE_ATTN_WAVE_CAP = 3,      /* GASFM_ATTN_WAVES: cap on item-loop waves, 0 = occupancy */
-  GASFM_TUNE_ATTN_GRP_BWD = 4,       /* grouped backward on (1) / off (0) */
+  GASFM_TUNE_ATTN_GRP_BWD = 4,       /* GASFM_ATTN_GRP_BWD: grouped backward (32-wide, streamed XL) on (1) / off (0) */
   GASFM_TUNE_SEAM_LDS = 5,           /* GASFM_SEAM_LDS: forward seam (blocks 1-11) LDS-staged (1) / registers (0) */
   GASFM_TUNE_ROWSUM_GRP = 6,         /* GASFM_ROWSUM_GRP: gasfm_segment_rowsum grouped (1) / one item per wave (0) */
   GASFM_TUNE_COUNT = 8
