@@ -44,7 +44,10 @@ PBWD_BYTES_PER_EDGE = 512  # P, dXL point half, dRes read, dP written (camera ro
 # (32 x 34: 2,176) + dP0 (2 x 32 dots: 128) FLOP, + P0 read 8 + dP0 written 8 bytes per edge
 PBWD_FOLD_FLOP_PER_EDGE = PBWD_FLOP_PER_EDGE + 2176 + 128
 PBWD_FOLD_BYTES_PER_EDGE = PBWD_BYTES_PER_EDGE + 16
-PMC_KERNELS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r3_pmc_kernels.txt")
+_PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
+# the newest committed per-kernel PMC table (tools/pmc_kernels.sh)
+PMC_KERNELS = next((os.path.join(_PROFILES, f) for f in ("r4_pmc_kernels.txt", "r3_pmc_kernels.txt")
+                    if os.path.exists(os.path.join(_PROFILES, f))), os.path.join(_PROFILES, "r3_pmc_kernels.txt"))
 
 
 def log(*a):
@@ -74,9 +77,10 @@ def pmc_kernel_traffic(name, E):
     if E != 4001638:
         return None
     try:
+        key = name.rstrip(">")  # the table truncates names (and round 4 added a template argument)
         with open(PMC_KERNELS) as f:
             for line in f:
-                if line.startswith(name):
+                if line.startswith(key):
                     return float(line.split()[-3]) * 1e6  # total MB column
     except (OSError, ValueError, IndexError):
         return None
@@ -350,7 +354,7 @@ def main():
                          "bound": "mfma", "achieved": pbwd_tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                          "frac": (pbwd_tfs / MFMA_F32_PEAK_TFS) if pbwd_tfs else None,
                          "traffic": pbwd_traffic,
-                         "traffic_source": "profiles/r3_pmc_kernels.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                         "traffic_source": f"profiles/{os.path.basename(PMC_KERNELS)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                                            "passes of this bench, per launch"
                                            + (f"; {pbwd_traffic / (bytes_e * e_cam):.2f}x the algorithmic bytes)"
                                               if pbwd_traffic else "; not taken on this workload)"),
