@@ -27,6 +27,9 @@ ALGO_MB = {  # config 4 algorithmic bytes per launch, DESIGN.md §5
     "edge_cam_pbwd_kernel<true, true, false, true>": 2081,
     # the seam kernel's two modes (32-wide epilogue / block 0's 2-wide one: P 8 + P' 128 + XL 128 + pt, pos 8)
     "edge_seam_fwd_kernel<true, false>": 1601, "edge_seam_fwd_kernel<true, true>": 1088,
+    # round 4: the pbwd kernels carry a fifth template argument (XP: dXLp gathered through pos)
+    "edge_cam_pbwd_kernel<true, true, true, true, false>": 2113,
+    "edge_cam_pbwd_kernel<true, true, false, true, false>": 2081,
 }
 
 
