@@ -65,6 +65,10 @@ _SIGS = {
     "gasfm_edge_cam_pbwd_ex": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _f32, _vp, _i64, _vp, _vp, _f32,
                                       _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _vp, _i64,
                                       _vp, _vp, _i64, _vp, _i32, _f32, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
+    "gasfm_edge_cam_pbwd_e0_cols": (_i32, []),
+    "gasfm_edge_cam_pbwd_e0": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _f32, _vp, _i64, _vp, _vp, _f32,
+                                      _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _vp, _i64,
+                                      _vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_edge_cam_fwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32,
                                   _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
     "gasfm_edge_cam_bwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _vp, _i64,
@@ -669,15 +673,22 @@ def edge0_seam_fwd(P, pt, lna_w, lna_b, lnb_w, lnb_b, eps0, Wp, bp, Wsk, bsk, Sp
     check(st, "gasfm_edge0_seam_fwd")
 
 
-def edge_cam_pbwd_part_shape(n_items, dwp_cols=0):
-    """(rows, cols) of edge_cam_pbwd's part buffer; dwp_cols = 32 or 34 with the dWp block (dwp)."""
+def edge_cam_pbwd_part_shape(n_items, dwp_cols=0, e0=False):
+    """(rows, cols) of edge_cam_pbwd's part buffer; dwp_cols = 32 or 34 with the dWp block (dwp);
+    e0: block 0's epilogue part after it (edge_cam_pbwd epi0)."""
     L = lib()
-    return int(L.gasfm_edge_cam_pbwd_part_rows(n_items)), int(L.gasfm_edge_cam_pbwd_part_cols()) + 32 * dwp_cols
+    return (int(L.gasfm_edge_cam_pbwd_part_rows(n_items)),
+            int(L.gasfm_edge_cam_pbwd_part_cols()) + 32 * dwp_cols + (int(L.gasfm_edge_cam_pbwd_e0_cols()) if e0 else 0))
+
+
+def edge_cam_pbwd_e0_offset(dwp_cols=34):
+    """First column of block 0's epilogue part in an edge_cam_pbwd part row (epi0)."""
+    return int(lib().gasfm_edge_cam_pbwd_part_cols()) + 32 * dwp_cols
 
 
 def edge_cam_pbwd(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, scale, XR, att, bias, slope, out, seg_max, seg_sum, gout,
                   plan_items, n_items, dXLp, dRes, dP, dXR, part_dxr, part, ldStat=4, epi=None, dwp=None,
-                  dxl_pos=None):
+                  dxl_pos=None, epi0=None):
     """The camera attention's backward and the block's edge prologue backward in one pass
     (csrc/edge_cam.hip edge_cam_pbwd): dP, dXR (+ split partials), part rows
     [dW 64x32 | db 64 | dgamma 32 | dbeta 32 | datt 32 | dbias 32] per workgroup.
@@ -686,7 +697,10 @@ def edge_cam_pbwd(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, scale, XR, att, bias, slo
     gradients from this dP (dSv rows / split-camera partial rows of the same plan, dP0).
     dwp = P0 or None (requires ln_w and dRes): also this block's lin_proj weight gradient,
     [32 x (32 | 34)] appended to each part row (part has edge_cam_pbwd_part_shape(n, dwp=...) columns).
-    dxl_pos (int32 [E] or None): dXLp rows in point-segment order, edge e's at dxl_pos[e]."""
+    dxl_pos (int32 [E] or None): dXLp rows in point-segment order, edge e's at dxl_pos[e].
+    epi0 = (Wp0, Wsk0, ln0, eps0, scale0, dSv0, part_dsv0, aux0) (round 4, block 1's launch; requires
+    dwp = P0, block 0's input): block 0's 2-wide epilogue backward from this dP
+    (gasfm_edge_cam_pbwd_e0; part has edge_cam_pbwd_part_shape(n, 34, e0=True) columns)."""
     _req(P, "P", 32)
     ldXR = _rows32(XR, "XR")
     We = dSv = part_dsv = dP0 = None
@@ -703,6 +717,26 @@ def edge_cam_pbwd(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, scale, XR, att, bias, slo
         ldWpo = 34 if P0 is not None else 32
     if P0 is not None:
         _req(P0, "P0", 2)
+    if epi0 is not None:
+        if epi is not None or P0 is None:
+            raise ValueError("edge_cam_pbwd: epi0 needs dwp = P0 (block 0's input) and no epi")
+        Wp0, Wsk0, ln0, eps0, scale0, dSv0, part_dsv0, aux0 = epi0
+        _req(dSv0, "dSv0", 32)
+        _req(aux0, "aux0", 4)
+        for t, nm in ((Wp0, "Wp0"), (Wsk0, "Wsk0")):
+            if not (t.is_contiguous() and tuple(t.shape) == (32, 2)):
+                raise ValueError(f"edge_cam_pbwd: {nm} must be a contiguous [32, 2] tensor")
+        if not (ln0.is_contiguous() and ln0.numel() == 8):
+            raise ValueError("edge_cam_pbwd: ln0 must be the 8 contiguous LayerNorm affines")
+        st = lib().gasfm_edge_cam_pbwd_e0(_p(P), _p(ln_w), _p(ln_b), eps, _p(Wpt), _p(Wc), _p(bc), _p(Wp),
+                                          Wp.stride(0), scale, _p(XR), ldXR, _p(att), _p(bias), slope, _p(out),
+                                          out.stride(0), _p(seg_max), _p(seg_sum), ldStat, _p(gout), gout.stride(0),
+                                          _p(plan_items), n_items, _p(dXLp), dXLp.stride(0), _p(dRes), _p(dP),
+                                          _p(dXR), dXR.stride(0), _p(part_dxr), _p(part), part.stride(0), _p(P0),
+                                          _p(Wp0), _p(Wsk0), _p(ln0), eps0, scale0, _p(dSv0), _p(part_dsv0), _p(aux0),
+                                          _p(dxl_pos), _stream(P))
+        check(st, "gasfm_edge_cam_pbwd_e0")
+        return
     st = lib().gasfm_edge_cam_pbwd_ex(_p(P), _p(ln_w), _p(ln_b), eps, _p(Wpt), _p(Wc), _p(bc), _p(Wp),
                                       Wp.stride(0) if Wp is not None else 0, scale, _p(XR), ldXR, _p(att), _p(bias),
                                       slope, _p(out), out.stride(0), _p(seg_max), _p(seg_sum), ldStat, _p(gout),

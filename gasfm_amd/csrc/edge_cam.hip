@@ -1355,6 +1355,7 @@ constexpr int PB2_PRO = NX * F + NX + 2 * F;  // the prologue_bwd part row
 constexpr int PB2_PART = PB2_PRO + BP_PART;
 constexpr int LDT = F + 4;                    // transpose tile row stride
 constexpr int PB_NDW = 20;                    // (DWP) per-lane dWp sums: 16 MFMA values + 4 P0 terms
+constexpr int PB_E0 = 164;                    // (EPI == 2) block 0's epilogue part: dWp 64 | dWsk 64 | dbsk 32 | 4
 
 // The edge epilogues' backward folded into edge_cam_pbwd (round 3).  With SeamFn, the kernel that
 // produces block b+1's dP is the one place where block b's epilogue gradient dP' (= that dP) is in
@@ -1373,6 +1374,13 @@ struct PbwdEpi {
   float* dP0;         // EPI: [E, 2] or null (no P0 skip input)
   const float* P0;    // DWP: [E, 2] or null
   int ldWpo;          // DWP: dWp row width in the part row (34 with P0, 32 without)
+  // EPI == 2 (block 0's epilogue, round 4): its 2-wide weights Wp0 / Wsk0 [32 x 2] (We = Wp0), the
+  // two 2-feature LayerNorms' affines [ga | ba | gb | bb] (2 each), their eps, the per-edge output
+  // aux [E, 4] = (dP_hat_a (2), dP through the skip branch (2)) that edge0_prologue_bwd consumes
+  const float* Wsk0;
+  const float* ln0;
+  float eps0;
+  float* aux;
 };
 
 // C-layout rows of a [*, 32] tensor: v[ft][r] = X[row0 + 4 g + r][16 ft + c] (rows clamped, not masked)
@@ -1440,7 +1448,14 @@ __device__ __forceinline__ void prod_c2(const float4* __restrict__ Q, const f32x
 #define GASFM_PBWD_BF 0
 #endif
 
-template <bool LN, bool RES, bool EPI, bool DWP, bool XP = false>
+// EPI == 2 (round 4): the previous block is block 0, whose epilogue is 2-wide
+// (P' = Wsk relu(LN_b(P0)) + bsk + scale (Wp relu(LN_a(P0)) + bp + Sp + Sv + Sg), edge_block0.hip),
+// folded like the 32-wide one: dSv from the same column sums, per edge the four dots
+// (scale Wp, Wsk)^T dP and the LN_b backward on P0 (this launch's DWP P0 rows, i.e. block 0's
+// input) to aux, and the weight sums [dWp dWsk | dbsk] = dP^T [relu(LN_a P0) relu(LN_b P0) | 1]
+// as 8 MFMA per tile (B operand: the five edge values in tile 1's padding columns).  Replaces
+// edge0_epilogue_bwd's pass over dP' (128 B per edge read back).
+template <bool LN, bool RES, int EPI, bool DWP, bool XP = false>
 __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kernel(
     const float* __restrict__ P, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
     const float* __restrict__ Wpt, const float* __restrict__ Wc, const float* __restrict__ bc,
@@ -1452,15 +1467,21 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
     float* __restrict__ dXR, int64_t ldDXR, float* __restrict__ part_dxr, float* __restrict__ part, int64_t ldPart,
     PbwdEpi ep, const int32_t* __restrict__ dxl_pos) {
   static_assert(!DWP || (LN && RES), "edge_cam_pbwd: the epilogue weight gradient needs relu(LN(P)) and dRes");
+  static_assert(EPI != 2 || DWP, "edge_cam_pbwd: block 0's epilogue fold reads block 0's input as the DWP P0 rows");
   // LDS: weight slabs (Wc for XLc; Wpt^T, Wc^T, (scale Wp)^T for dP_hat), the per-feature vectors,
   // per wave four 16 x 32 transpose tiles (T -> C layout of P, dXLp, dRes, dXLc), and (DWP) per
   // wave the lanes' running dWp sums
   constexpr int QW = F * F;  // floats per 32 x 32 slab set
-  constexpr int OV = 4 * QW, OT = OV + (EPI ? 6 : 4) * F, WT = 4 * TR * LDT;
+  constexpr int OV = 4 * QW, OT = OV + (EPI == 2 ? 8 * F + 8 : EPI ? 6 * F : 4 * F), WT = 4 * TR * LDT;
   constexpr int OD = OT + kWaves * WT;
   constexpr int NLS = (DWP ? PB_NDW : 0) + (EPI ? 2 : 0);  // per-lane LDS sums
   constexpr int OX = OD + kWaves * NLS * kW;                 // per wave: the item's [XR | gout] rows
-  constexpr int NL = OX + (GASFM_PBWD_ITEM_LDS ? kWaves * 2 * F : 0);
+  // (EPI == 2) per wave 17 x 4 floats: the LN_b affine sums [dgb | dbb] of lanes c (group 0), then
+  // one slot the other groups' (duplicate) values land in; per wave 21 x 8 floats: the weight sums
+  // of the 20 lanes c < 5 (C layout), then a dummy slot (registers held across tiles spill here)
+  constexpr int OG = OX + (GASFM_PBWD_ITEM_LDS ? kWaves * 2 * F : 0);
+  constexpr int OA = OG + (EPI == 2 ? kWaves * 17 * 4 : 0);
+  constexpr int NL = OA + (EPI == 2 ? kWaves * 21 * 8 : 0);
   __shared__ __attribute__((aligned(16))) float lds[NL];
   float* WcQ = lds;
   float* WptTQ = lds + QW;
@@ -1476,9 +1497,16 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
     V[F + threadIdx.x] = LN ? bet[threadIdx.x] : 0.f;
     V[2 * F + threadIdx.x] = bc[threadIdx.x];
     V[3 * F + threadIdx.x] = att[threadIdx.x];
-    if (EPI) {
+    if (EPI == 1) {
       V[4 * F + threadIdx.x] = ep.dP0 ? ep.scale * ep.We[threadIdx.x * ep.ldWe + 32] : 0.f;
       V[5 * F + threadIdx.x] = ep.dP0 ? ep.scale * ep.We[threadIdx.x * ep.ldWe + 33] : 0.f;
+    }
+    if (EPI == 2) {  // [scale Wp0[:, 0] | scale Wp0[:, 1] | Wsk0[:, 0] | Wsk0[:, 1] | ga ba gb bb]
+      V[4 * F + threadIdx.x] = ep.scale * ep.We[threadIdx.x * 2];
+      V[5 * F + threadIdx.x] = ep.scale * ep.We[threadIdx.x * 2 + 1];
+      V[6 * F + threadIdx.x] = ep.Wsk0[threadIdx.x * 2];
+      V[7 * F + threadIdx.x] = ep.Wsk0[threadIdx.x * 2 + 1];
+      if (threadIdx.x < 8) V[8 * F + threadIdx.x] = ep.ln0[threadIdx.x];
     }
   }
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
@@ -1488,8 +1516,16 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   float* Lw = lds + OD + (wave * kW + lane) * NLS;
   float* Ls = Lw + (DWP ? PB_NDW : 0);
   float* Xi = lds + OX + wave * 2 * F;  // (GASFM_PBWD_ITEM_LDS) [XR | gout] of the wave's camera item
+  float* Lg = lds + OG + wave * 17 * 4 + (g == 0 ? c : 16) * 4;  // (EPI == 2) this lane's affine sums
+  float* La = lds + OA + wave * 21 * 8 + (c < 5 ? 5 * g + c : 20) * 8;  // (EPI == 2) its weight sums
 #pragma unroll
   for (int k = 0; k < NLS; ++k) Lw[k] = 0.f;
+  if (EPI == 2) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Lg[k] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) La[k] = 0.f;
+  }
   const float gC[2] = {LN ? gam[c] : 1.f, LN ? gam[16 + c] : 1.f}, bC[2] = {LN ? bet[c] : 0.f, LN ? bet[16 + c] : 0.f};
   __syncthreads();
   // T-layout vector at this lane's features 16 q + 4 g .. + 3
@@ -1564,8 +1600,10 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
     const int ilen = __builtin_amdgcn_readfirstlane(int(w.end - w.begin));
     const auto dPrs = __builtin_amdgcn_make_buffer_rsrc(dP + ibeg * F, 0, ilen * F * 4, 0x00020000);
     // (EPI) dP0 rows of this item; without dP0 an empty range (every store dropped)
-    const auto dP0rs = __builtin_amdgcn_make_buffer_rsrc(EPI && ep.dP0 ? ep.dP0 + ibeg * 2 : dP, 0,
-                                                         EPI && ep.dP0 ? ilen * 8 : 0, 0x00020000);
+    // (EPI == 2) aux rows of this item instead
+    const auto dP0rs = EPI == 2 ? __builtin_amdgcn_make_buffer_rsrc(ep.aux + ibeg * 4, 0, ilen * 16, 0x00020000)
+                                : __builtin_amdgcn_make_buffer_rsrc(EPI && ep.dP0 ? ep.dP0 + ibeg * 2 : dP, 0,
+                                                                    EPI && ep.dP0 ? ilen * 8 : 0, 0x00020000);
     // per-camera constants of the attention backward (edge_cam_bwd_kernel)
     f32x4 xr[2], gv[2];
     float M[2], inv[2], delta[2];
@@ -1765,7 +1803,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
           // the item's column sums of dP (dSv) live in LDS: no registers held across tiles
           Ls[0] += (GASFM_PBWD_BF & 1) ? dv[r][0] * lm[r] : (live ? dv[r][0] : 0.f);
           Ls[1] += (GASFM_PBWD_BF & 1) ? dv[r][1] * lm[r] : (live ? dv[r][1] : 0.f);
-          if (!GASFM_PBWD_EPI_T) {  // A/B: 16-lane sums per row (DPP), lanes c = 0, 1 store
+          if (!GASFM_PBWD_EPI_T && EPI == 1) {  // A/B: 16-lane sums per row (DPP), lanes c = 0, 1 store
             const float s0 = sum16(fmaf(dv[r][0], V[4 * F + c], dv[r][1] * V[4 * F + 16 + c]));
             const float s1 = sum16(fmaf(dv[r][0], V[5 * F + c], dv[r][1] * V[5 * F + 16 + c]));
             const int off = c < 2 ? int(((row0 - ibeg + 4 * g + r) * 2 + c) * 4) : 0x7ffffff0;
@@ -1776,7 +1814,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
           }
         }
       }
-      if (EPI && GASFM_PBWD_EPI_T) {
+      if (EPI == 1 && GASFM_PBWD_EPI_T) {
         float* T0 = Tt;
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
@@ -1793,6 +1831,69 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
         const int off = g == 0 ? int((row0 - ibeg + c) * 8) : 0x7ffffff0;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s0), dP0rs, off, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s1), dP0rs, off + 4, 0, 0);
+      }
+      if (EPI == 2) {
+        // block 0's epilogue backward for edge c (T layout; the four lane groups hold the same values)
+        float* T0 = Tt;
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        float q[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const float4 d4 = *reinterpret_cast<const float4*>(T0 + c * LDT + 16 * u + 4 * g);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x4 a = vecT(4 + j, u);
+            q[j] = fmaf(d4.x, a[0], fmaf(d4.y, a[1], fmaf(d4.z, a[2], fmaf(d4.w, a[3], q[j]))));
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = sum_groups(q[j]);
+        const float4 la = *reinterpret_cast<const float4*>(V + 8 * F);      // ga0 ga1 ba0 ba1
+        const float4 lb = *reinterpret_cast<const float4*>(V + 8 * F + 4);  // gb0 gb1 bb0 bb1
+        const float mean = 0.5f * (p0t.x + p0t.y), e0 = p0t.x - mean, e1 = p0t.y - mean;
+        const float rs = rsqrtf(0.5f * (e0 * e0 + e1 * e1) + ep.eps0);
+        const float xh0 = e0 * rs, xh1 = e1 * rs;
+        const float yb0 = fmaf(xh0, lb.x, lb.z), yb1 = fmaf(xh1, lb.y, lb.w);
+        // LN_b / ReLU backward of the skip branch
+        const float db0 = yb0 > 0.f ? q[2] : 0.f, db1 = yb1 > 0.f ? q[3] : 0.f;
+        const float g0 = db0 * lb.x, g1 = db1 * lb.y;
+        const float mg = 0.5f * (g0 + g1), mgx = 0.5f * (g0 * xh0 + g1 * xh1);
+        const float dx0 = rs * (g0 - mg - xh0 * mgx), dx1 = rs * (g1 - mg - xh1 * mgx);
+        // aux[edge c] = (qa0, qa1, dx0, dx1): lane group g stores component g (rows past the item's
+        // end fall outside the descriptor's range)
+        const float av = g == 0 ? q[0] : g == 1 ? q[1] : g == 2 ? dx0 : dx1;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(av), dP0rs, int(((row0 - ibeg + c) * 4 + g) * 4), 0, 0);
+        const float f = vmask;  // group 0's slots count each live edge once (the others: the dummy slot)
+        Lg[0] = fmaf(f * db0, xh0, Lg[0]);
+        Lg[1] = fmaf(f * db1, xh1, Lg[1]);
+        Lg[2] = fmaf(f, db0, Lg[2]);
+        Lg[3] = fmaf(f, db1, Lg[3]);
+        // [relu(LN_a P0) | relu(LN_b P0)] of edge c into tile 1's padding columns (tile 1's rows were
+        // read back before the attention)
+        if (g == 0)
+          *reinterpret_cast<float4*>(Tt + TR * LDT + c * LDT + 32) =
+              make_float4(fmaxf(fmaf(xh0, la.x, la.z), 0.f), fmaxf(fmaf(xh1, la.y, la.w), 0.f), fmaxf(yb0, 0.f),
+                          fmaxf(yb1, 0.f));
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        // [dWp0 dWsk0 | dbsk0] += dP^T [h | 1] (dead rows zeroed in the B operand; dP re-read from tile 0
+        // in the C layout rather than held in registers since the LayerNorm backward)
+        const float* T1 = Tt + TR * LDT;
+        f32x4 acc0[2] = {zero4(), zero4()};
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const float hv = T1[(4 * g + s2) * LDT + 32 + (c & 3)];
+          const float b = (c < 4 ? hv : (c == 4 ? 1.f : 0.f)) * lm[s2];
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) acc0[nt] = mfma16(T0[(4 * g + s2) * LDT + 16 * nt + c], b, acc0[nt]);
+        }
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const float4 o = *reinterpret_cast<const float4*>(La + 4 * nt);
+          *reinterpret_cast<float4*>(La + 4 * nt) =
+              make_float4(o.x + acc0[nt][0], o.y + acc0[nt][1], o.z + acc0[nt][2], o.w + acc0[nt][3]);
+        }
       }
       // ---- dW += [dXLp | dXLc]^T relu(LN(P)), db (C layout, row 4 g + s at step s)
 #pragma unroll
@@ -1878,8 +1979,17 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   }
   // workgroup reduction: 32 accW + 4 db + 2 dg + 2 dbt (C layout) + 16 (datt, dbias summed over
   // the 16 edge columns first) (+ DWP: the lanes' 20 dWp sums, read before the scratch is reused)
-  constexpr int NV = 56 + (DWP ? PB_NDW : 0);
+  constexpr int NB2 = 56 + (DWP ? PB_NDW : 0);  // (EPI == 2) v[NB2 ..]: acc0 (8), then Lg (4)
+  constexpr int NV = NB2 + (EPI == 2 ? 12 : 0);
   float v[NV];
+  if (EPI == 2) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[NB2 + nt * 4 + r] = c < 5 ? La[nt * 4 + r] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[NB2 + 8 + k] = g == 0 ? Lg[k] : 0.f;
+  }
   if (DWP) {  // v[56 + (ft * 2 + nt) * 4 + r] = the MFMA sums, v[72 + ft * 2 + j] = the P0 terms
 #pragma unroll
     for (int ft = 0; ft < 2; ++ft) {
@@ -1911,6 +2021,29 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   wg_reduce_ordered<NV, kWaves, NL>(v, lds, wave, lane);
   if (wave == 0) {
     float* o = part + int64_t(blockIdx.x) * ldPart;
+    if (EPI == 2) {  // [dWp0 64 | dWsk0 64 | dbsk0 32 | dgb 2 | dbb 2] after the dWp block (edge0_epilogue_bwd's row)
+      float* o2 = o + PB2_PART + F * ep.ldWpo;
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int f = 16 * nt + 4 * g + r;
+          const float x = v[NB2 + nt * 4 + r];
+          if (c < 2)
+            o2[2 * f + c] = x * ep.scale;
+          else if (c < 4)
+            o2[64 + 2 * f + c - 2] = x;
+          else if (c == 4)
+            o2[128 + f] = x;
+        }
+      float t2[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t2[k] = sum_groups(group_sum<16>(v[NB2 + 8 + k]));
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o2[160 + k] = t2[k];
+      }
+    }
     if (DWP) {  // [32 x ldWpo] after the prologue/attention part, scaled as the epilogue's
       float* od = o + PB2_PART;
 #pragma unroll
@@ -2037,16 +2170,19 @@ extern "C" int gasfm_edge_cam_bwd(const float* P, const float* ln_w, const float
 extern "C" int32_t gasfm_edge_cam_pbwd_part_rows(int32_t n_items) { return grid_cam_pbwd(n_items > 0 ? n_items : 1); }
 extern "C" int32_t gasfm_edge_cam_pbwd_part_cols(void) { return PB2_PART; }
 
-extern "C" int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const float* ln_b, float eps,
-                                      const float* Wpt, const float* Wc, const float* bc, const float* Wp, int32_t ldWp,
-                                      float scale, const float* XR, int64_t ldXR, const float* att, const float* bias,
-                                      float slope, const float* out, int64_t ldOut, const float* seg_max,
-                                      const float* seg_sum, int64_t ldStat, const float* gout, int64_t ldG,
-                                      const gasfm_work_item* items, int32_t n_items, const float* dXLp, int64_t ldXp,
-                                      const float* dRes, float* dP, float* dXR, int64_t ldDXR, float* part_dxr,
-                                      float* part, int64_t ldPart, const float* We, int32_t ldWe, float scale_e,
-                                      float* dSv_e, float* part_dsv_e, float* dP0_e, const float* P0, int32_t ldWpo,
-                                      const int32_t* dxl_pos, void* stream) {
+namespace {
+// the launcher behind gasfm_edge_cam_pbwd_ex and gasfm_edge_cam_pbwd_e0 (ep.aux set: block 0's fold)
+int pbwd_launch(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wpt, const float* Wc,
+                const float* bc, const float* Wp, int32_t ldWp, float scale, const float* XR, int64_t ldXR,
+                const float* att, const float* bias, float slope, const float* out, int64_t ldOut,
+                const float* seg_max, const float* seg_sum, int64_t ldStat, const float* gout, int64_t ldG,
+                const gasfm_work_item* items, int32_t n_items, const float* dXLp, int64_t ldXp, const float* dRes,
+                float* dP, float* dXR, int64_t ldDXR, float* part_dxr, float* part, int64_t ldPart,
+                const PbwdEpi& ep, const int32_t* dxl_pos, void* stream) {
+  const float *We = ep.We, *P0 = ep.P0;
+  const int32_t ldWe = ep.ldWe, ldWpo = ep.ldWpo;
+  float *dSv_e = ep.dSv, *dP0_e = ep.dP0;
+  const bool e0 = ep.aux != nullptr;
   GASFM_REQUIRE(n_items >= 0 && P && Wpt && Wc && bc && XR && att && bias && out && seg_max && seg_sum && gout &&
                     items && dXLp && dP && dXR && part && (!dRes || (Wp && ldWp >= F)),
                 "gasfm_edge_cam_pbwd: null pointer");
@@ -2056,15 +2192,18 @@ extern "C" int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const f
                     (!part_dxr || aligned16(part_dxr)) && (!ln_w || (aligned16(ln_w) && aligned16(ln_b))),
                 "gasfm_edge_cam_pbwd: 16-byte rows required");
   const bool epi = dSv_e != nullptr, dwp = ldWpo > 0;
-  GASFM_REQUIRE(!epi || (We && ldWe >= F + (dP0_e ? 2 : 0) && (ln_w != nullptr) == (dRes != nullptr)),
+  GASFM_REQUIRE(!epi || (We && (e0 || ldWe >= F + (dP0_e ? 2 : 0)) && (ln_w != nullptr) == (dRes != nullptr)),
                 "gasfm_edge_cam_pbwd: the previous epilogue's outputs need its lin_proj weight (and LN == RES)");
   GASFM_REQUIRE(!dwp || (ln_w && dRes && ldWpo == (P0 ? F + 2 : F)),
                 "gasfm_edge_cam_pbwd: the epilogue weight gradient needs LN, dRes and ldWpo = 32 (+2 with P0)");
-  GASFM_REQUIRE(ldPart >= PB2_PART + (dwp ? int64_t(F) * ldWpo : 0), "gasfm_edge_cam_pbwd: part row too narrow");
+  GASFM_REQUIRE(!e0 || (epi && dwp && P0 && ep.Wsk0 && ep.ln0 && !dP0_e && aligned16(ep.aux)),
+                "gasfm_edge_cam_pbwd_e0: block 0's fold needs dSv, the DWP P0 rows (block 0's input), Wsk0, "
+                "the LayerNorm affines and a 16-byte aligned aux");
+  GASFM_REQUIRE(ldPart >= PB2_PART + (dwp ? int64_t(F) * ldWpo : 0) + (e0 ? PB_E0 : 0),
+                "gasfm_edge_cam_pbwd: part row too narrow");
   if (n_items == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int grid = grid_cam_pbwd(n_items);
-  const PbwdEpi ep{We, ldWe, scale_e, dSv_e, part_dsv_e, dP0_e, P0, ldWpo};
   auto launch = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, st, P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, ldWp, scale, XR,
                        ldXR, att, bias, slope, out, ldOut, seg_max, seg_sum, ldStat, gout, ldG, items, n_items, dXLp,
@@ -2073,7 +2212,9 @@ extern "C" int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const f
   auto pick = [&](auto xp) {
     constexpr bool X = decltype(xp)::value;
     if (ln_w && dRes) {
-      if (epi && dwp)
+      if (e0)
+        launch(&edge_cam_pbwd_kernel<true, true, 2, true, X>);
+      else if (epi && dwp)
         launch(&edge_cam_pbwd_kernel<true, true, true, true, X>);
       else if (epi)
         launch(&edge_cam_pbwd_kernel<true, true, true, false, X>);
@@ -2096,6 +2237,42 @@ extern "C" int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const f
   else
     pick(std::false_type{});
   return launch_status("gasfm_edge_cam_pbwd");
+}
+}  // namespace
+
+extern "C" int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const float* ln_b, float eps,
+                                      const float* Wpt, const float* Wc, const float* bc, const float* Wp, int32_t ldWp,
+                                      float scale, const float* XR, int64_t ldXR, const float* att, const float* bias,
+                                      float slope, const float* out, int64_t ldOut, const float* seg_max,
+                                      const float* seg_sum, int64_t ldStat, const float* gout, int64_t ldG,
+                                      const gasfm_work_item* items, int32_t n_items, const float* dXLp, int64_t ldXp,
+                                      const float* dRes, float* dP, float* dXR, int64_t ldDXR, float* part_dxr,
+                                      float* part, int64_t ldPart, const float* We, int32_t ldWe, float scale_e,
+                                      float* dSv_e, float* part_dsv_e, float* dP0_e, const float* P0, int32_t ldWpo,
+                                      const int32_t* dxl_pos, void* stream) {
+  const PbwdEpi ep{We, ldWe, scale_e, dSv_e, part_dsv_e, dP0_e, P0, ldWpo, nullptr, nullptr, 0.f, nullptr};
+  return pbwd_launch(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, ldWp, scale, XR, ldXR, att, bias, slope, out, ldOut,
+                     seg_max, seg_sum, ldStat, gout, ldG, items, n_items, dXLp, ldXp, dRes, dP, dXR, ldDXR, part_dxr,
+                     part, ldPart, ep, dxl_pos, stream);
+}
+
+extern "C" int32_t gasfm_edge_cam_pbwd_e0_cols(void) { return PB_E0; }
+
+extern "C" int gasfm_edge_cam_pbwd_e0(const float* P, const float* ln_w, const float* ln_b, float eps,
+                                      const float* Wpt, const float* Wc, const float* bc, const float* Wp, int32_t ldWp,
+                                      float scale, const float* XR, int64_t ldXR, const float* att, const float* bias,
+                                      float slope, const float* out, int64_t ldOut, const float* seg_max,
+                                      const float* seg_sum, int64_t ldStat, const float* gout, int64_t ldG,
+                                      const gasfm_work_item* items, int32_t n_items, const float* dXLp, int64_t ldXp,
+                                      const float* dRes, float* dP, float* dXR, int64_t ldDXR, float* part_dxr,
+                                      float* part, int64_t ldPart, const float* P0, const float* Wp0,
+                                      const float* Wsk0, const float* ln0, float eps0, float scale0, float* dSv0,
+                                      float* part_dsv0, float* aux0, const int32_t* dxl_pos, void* stream) {
+  GASFM_REQUIRE(Wp0 && Wsk0 && ln0 && dSv0 && aux0 && P0, "gasfm_edge_cam_pbwd_e0: null pointer");
+  const PbwdEpi ep{Wp0, 2, scale0, dSv0, part_dsv0, nullptr, P0, F + 2, Wsk0, ln0, eps0, aux0};
+  return pbwd_launch(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, ldWp, scale, XR, ldXR, att, bias, slope, out, ldOut,
+                     seg_max, seg_sum, ldStat, gout, ldG, items, n_items, dXLp, ldXp, dRes, dP, dXR, ldDXR, part_dxr,
+                     part, ldPart, ep, dxl_pos, stream);
 }
 
 extern "C" int gasfm_edge_cam_pbwd(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wpt,

@@ -46,6 +46,11 @@ def dxl_pos_of(pos):
     (None: dXLp arrives in edge order)."""
     return pos if (DXL_PT and pos is not None) else None
 
+# round 4: block 0's 2-wide epilogue backward folded into block 1's edge_cam_pbwd the same way
+# (gasfm_edge_cam_pbwd_e0: dSv, aux and the block-0 weight sums from the dP' that launch produces,
+# block 0's input read as the launch's DWP P0 rows).  0: edge0_epilogue_bwd as before.
+E0_FOLD = os.environ.get("GASFM_E0_FOLD", "1") != "0"
+
 # Block 0's prologue writes XL0 row by row through the point plan's permutation (one 32-B store
 # per row, gasfm_edge0_prologue_fwd_rows) instead of scattering the point halves through pos.
 E0_ROWS = os.environ.get("GASFM_E0_ROWS", "1") != "0"
@@ -191,11 +196,12 @@ def _dwp_torch(P, ln_w, ln_b, eps, dRes, P0):
     return PROJ_SCALE * (dRes.t() @ ph)
 
 
-def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None):
+def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None, epi0=None):
     """EdgeCamFn's backward from its saved state (ctx attributes eps, heads, slope, plan, att_shape,
     has_ln, dwp, defer): the 20 input gradients of EdgeCamFn.forward.  epi: the previous block's
     epilogue outputs to fill from dP (edge_cam_pbwd's EPI), or None; ctx.epi_done tells whether
-    they were filled."""
+    they were filled.  epi0: the same for block 0's epilogue (edge_cam_pbwd's epi0, block 1 only);
+    when filled, ctx.epi0_part holds the block-0 weight partial rows (a column slice of part)."""
     P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum, P0 = saved
     plan = ctx.plan
     E, dev = P.shape[0], P.device
@@ -204,22 +210,28 @@ def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None):
     g_c = torch.zeros_like(out) if g_c is None else (g_c if g_c.stride(1) == 1 else g_c.contiguous())
     dwp = ctx.dwp and dRes is not None and ln_w is not None
     ctx.epi_done = False
+    ctx.epi0_part = None
     dWp = None
     if CAM_PBWD and plan.n_items:
         # camera attention backward + prologue backward in one kernel (gasfm_edge_cam_pbwd)
         dXR = torch.empty((plan.num_targets, 32), dtype=torch.float32, device=dev)
         part_dxr = torch.empty((plan.n_part_rows, 32), dtype=torch.float32, device=dev) if plan.n_slots else None
         wcols = (34 if P0 is not None else 32) if dwp else 0
-        rows, cols = _native.edge_cam_pbwd_part_shape(plan.n_items, wcols)
+        use_e0 = epi0 is not None and dwp and P0 is not None
+        rows, cols = _native.edge_cam_pbwd_part_shape(plan.n_items, wcols, e0=use_e0)
         part = torch.empty((rows, cols), dtype=torch.float32, device=dev)
         dP = torch.empty_like(P)
-        use_epi = epi is not None and (ln_w is None) == (dRes is None)
+        use_epi = epi is not None and (ln_w is None) == (dRes is None) and not use_e0
         _native.edge_cam_pbwd(P, ln_w, ln_b, ctx.eps, Wpt.contiguous(), Wc.contiguous(), bc.contiguous(),
                               Wp.contiguous() if dRes is not None else None, PROJ_SCALE, XR, attf, bias, ctx.slope,
                               out, smax, ssum, g_c, plan.items, plan.n_items, dXLp, dRes, dP, dXR, part_dxr, part,
                               epi=epi if use_epi else None,
-                              dwp=(P0 if P0 is not None else True) if dwp else None, dxl_pos=dxl_pos)
+                              dwp=(P0 if P0 is not None else True) if dwp else None, dxl_pos=dxl_pos,
+                              epi0=epi0 if use_e0 else None)
         ctx.epi_done = use_epi
+        if use_e0:
+            off = _native.edge_cam_pbwd_e0_offset(wcols)
+            ctx.epi0_part = part[:, off:off + 164]
         bwd_combine(plan, part_dxr, 32, dXR)
         tot = _native.param_colsum(part, ctx.defer)
         o = 64 * 32
@@ -522,22 +534,26 @@ class Block0EpilogueFn(torch.autograd.Function):
         return _epilogue0_backward(ctx, ctx.saved_tensors, dPo)
 
 
-def _epilogue0_backward(ctx, saved, dPo):
+def _epilogue0_backward(ctx, saved, dPo, folded=None):
     """Block0EpilogueFn's backward from its saved state (ctx attributes eps, edges, sg_shape): its 15
-    input gradients."""
+    input gradients.  folded: (dSv, part_dsv, aux, part rows) already filled by block 1's
+    edge_cam_pbwd (epi0), so edge0_epilogue_bwd does not run."""
     P, lna_w, lna_b, lnb_w, lnb_b, Wp, Wsk = saved
     edges = ctx.edges
     dPo = dPo.contiguous()
     dev = P.device
     E = P.shape[0]
     pc, pp = edges.plans["proj2view"], edges.plans["proj2scenepoint"]
-    dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
-    part_dsv = torch.empty((max(pc.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
-    aux = torch.empty((E, 4), dtype=torch.float32, device=dev)
-    rows = _native.edge0_part_rows(1, E, pc.n_items)
-    part = torch.empty((rows, 164), dtype=torch.float32, device=dev)
-    _native.edge0_epilogue_bwd(pc.items, pc.n_items, dPo, P, lna_w, lna_b, lnb_w, lnb_b, ctx.eps,
-                               Wp.contiguous(), Wsk.contiguous(), PROJ_SCALE, dSv, part_dsv, aux, part)
+    if folded is not None:
+        dSv, part_dsv, aux, part = folded
+    else:
+        dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
+        part_dsv = torch.empty((max(pc.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
+        aux = torch.empty((E, 4), dtype=torch.float32, device=dev)
+        rows = _native.edge0_part_rows(1, E, pc.n_items)
+        part = torch.empty((rows, 164), dtype=torch.float32, device=dev)
+        _native.edge0_epilogue_bwd(pc.items, pc.n_items, dPo, P, lna_w, lna_b, lnb_w, lnb_b, ctx.eps,
+                                   Wp.contiguous(), Wsk.contiguous(), PROJ_SCALE, dSv, part_dsv, aux, part)
     bwd_combine(pc, part_dsv, 32, dSv)
     tot = _native.colsum(part)
     dSg = _native.colsum(dSv)
@@ -596,7 +612,23 @@ class Seam0Fn(torch.autograd.Function):
         saved = ctx.saved_tensors
         epi, cam = saved[:7], saved[7:]
         dRes = dtoken.contiguous() if (dtoken is not None and dtoken.stride(0) != 0) else None
-        gc = _cam_backward(ctx, cam, dXLp, g_c, dRes)
+        edges = ctx.edges
+        P, lna_w, lna_b, lnb_w, lnb_b, Wp, Wsk = epi
+        P0_n = cam[-1]
+        epi0 = None
+        if (E0_FOLD and gPn is None and dRes is not None and ctx.dwp and ctx.plan is edges.plans["proj2view"]
+                and P0_n is not None and P0_n.data_ptr() == P.data_ptr() and P0_n.stride() == P.stride()
+                and P0_n.shape == P.shape and tuple(Wp.shape) == (32, 2) and tuple(Wsk.shape) == (32, 2)):
+            # block 0's epilogue backward from the dP' block 1's launch produces (its P0 rows are
+            # block 0's input: the same embedded projections)
+            dev = P.device
+            dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
+            part_dsv = torch.empty((max(ctx.plan.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
+            aux = torch.empty((P.shape[0], 4), dtype=torch.float32, device=dev)
+            ln0 = torch.cat([lna_w, lna_b, lnb_w, lnb_b]).contiguous()
+            epi0 = (Wp, Wsk, ln0, ctx.e_eps, PROJ_SCALE, dSv, part_dsv, aux)
+        gc = _cam_backward(ctx, cam, dXLp, g_c, dRes, epi0=epi0)
+        folded = None if ctx.epi0_part is None else (epi0[5], epi0[6], epi0[7], ctx.epi0_part)
         dPn = gc[0] if gPn is None else gc[0] + gPn
-        ectx = _EpiState(ctx.e_eps, ctx.edges, ctx.sg_shape, None)
-        return _epilogue0_backward(ectx, epi, dPn) + gc[1:]
+        ectx = _EpiState(ctx.e_eps, edges, ctx.sg_shape, None)
+        return _epilogue0_backward(ectx, epi, dPn, folded) + gc[1:]

@@ -224,6 +224,26 @@ int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const float* ln_b,
                            float* dXR, int64_t ldDXR, float* part_dxr, float* part, int64_t ldPart,
                            const float* We, int32_t ldWe, float scale_e, float* dSv_e, float* part_dsv_e,
                            float* dP0_e, const float* P0, int32_t ldWpo, const int32_t* dxl_pos, void* stream);
+/* Block 1's gasfm_edge_cam_pbwd_ex (LN, dRes, DWP with P0) with BLOCK 0's 2-wide epilogue backward
+ * folded in (round 4; replaces gasfm_edge0_epilogue_bwd, reference: the autograd of
+ * residual_skipconn_proj_norm_layer + skip_projection + lin_proj of block 0, layers.py:214-220,
+ * 256-261, 959-969).  P0 [E, 2] is block 0's input (the embedded projections, also block 1's skip
+ * input); Wp0 / Wsk0 [32 x 2]; ln0 = [ga0 ga1 ba0 ba1 gb0 gb1 bb0 bb1] (LN_a, LN_b affines), eps0;
+ * scale0 the epilogue scale.  Outputs, as gasfm_edge0_epilogue_bwd's: dSv0 (+ part_dsv0 split rows),
+ * aux0 [E, 4] = (dP_hat_a (2), dP of the skip branch (2)) and, after the 32 x 34 dWp block of each
+ * part row, gasfm_edge_cam_pbwd_e0_cols() floats [dWp0 64 | dWsk0 64 | dbsk0 32 | dgb 2 | dbb 2]
+ * (ldPart >= part_cols + 32 x 34 + e0_cols). */
+int32_t gasfm_edge_cam_pbwd_e0_cols(void);
+int gasfm_edge_cam_pbwd_e0(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
+                           const float* Wc, const float* bc, const float* Wp, int32_t ldWp, float scale,
+                           const float* XR, int64_t ldXR, const float* att, const float* bias, float slope,
+                           const float* out, int64_t ldOut, const float* seg_max, const float* seg_sum,
+                           int64_t ldStat, const float* gout, int64_t ldG, const gasfm_work_item* items,
+                           int32_t n_items, const float* dXLp, int64_t ldXp, const float* dRes, float* dP,
+                           float* dXR, int64_t ldDXR, float* part_dxr, float* part, int64_t ldPart,
+                           const float* P0, const float* Wp0, const float* Wsk0, const float* ln0, float eps0,
+                           float scale0, float* dSv0, float* part_dsv0, float* aux0, const int32_t* dxl_pos,
+                           void* stream);
 
 /* ---- fused GATv2 edge-softmax + aggregation (device) ------------------- */
 

@@ -186,6 +186,54 @@ def test_epilogue_fold_vs_unfolded(device, monkeypatch):
         assert err <= max(1e-3 * float(g0.norm()), 10 * own) + 1e-9, (k, err, own, float(g0.norm()))
 
 
+@pytest.mark.parametrize("max_piece", [None, 64])
+def test_block0_fold_vs_unfolded(device, monkeypatch, max_piece):
+    """Block 0's 2-wide epilogue backward folded into block 1's edge_cam_pbwd (edge_block.E0_FOLD,
+    gasfm_edge_cam_pbwd_e0) against edge0_epilogue_bwd: identical forward, no edge0_epilogue_bwd
+    launch left, block 0's epilogue weights (lin_proj, the skip projection, LN_b) within 1e-4
+    normwise of the unfolded gradients, and every parameter gradient within 1e-3 normwise or within
+    10x the unfolded one's own distance from the fp64 oracle (as test_epilogue_fold_vs_unfolded).
+    max_piece 64 splits cameras over several items (dSv through the partial rows)."""
+    from conftest import oracle_grads
+    from gasfm_amd import edge_block
+    from oracle.weights import deterministic_state_dict
+    sc = synthetic.scaled_config4(0.05, seed=19)
+    data = gasfm_amd.SceneData.from_synthetic(sc, max_piece=max_piece).to(device)
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=3))
+    sd = deterministic_state_dict(net.state_dict(), torch.float64)
+    net.load_state_dict({k: v.float() for k, v in sd.items()})
+    net = net.to(device)
+    gen = torch.Generator().manual_seed(9)
+    cP = torch.randn((sc.m, 3, 4), generator=gen, dtype=torch.float64)
+    cX = torch.randn((4, sc.n), generator=gen, dtype=torch.float64)
+    calls = []
+    orig = _native.edge0_epilogue_bwd
+    monkeypatch.setattr(_native, "edge0_epilogue_bwd", lambda *a, **k: (calls.append(1), orig(*a, **k))[1])
+    res = {}
+    for fold in (False, True):
+        monkeypatch.setattr(edge_block, "E0_FOLD", fold)
+        calls.clear()
+        net.zero_grad(set_to_none=True)
+        pred = net(data)
+        ((pred["Ps_norm"] * cP.float().to(device)).sum() + (pred["pts3D"] * cX.float().to(device)).sum()).backward()
+        torch.cuda.synchronize()
+        res[fold] = (pred["Ps_norm"].detach().clone(), {k: p.grad.detach().double().cpu() for k, p in net.named_parameters()},
+                     len(calls))
+    assert torch.equal(res[True][0], res[False][0])
+    assert res[False][2] == 1 and res[True][2] == 0, (res[False][2], res[True][2])
+    (g64, _), _ = oracle_grads(sd, sc, cP, cX)
+    b0 = [k for k in res[False][1] if k.startswith("equivariant_blocks.0.") and
+          ("projection_feature_update.lin_proj" in k or "skip" in k)]
+    assert len(b0) == 6, b0
+    for k, g0 in res[False][1].items():
+        g1 = res[True][1][k]
+        err = float((g1 - g0).norm())
+        if k in b0:
+            assert err <= 1e-4 * float(g0.norm()) + 1e-9, (k, err, float(g0.norm()))
+        own = float((g0 - torch.from_numpy(g64[k])).norm())
+        assert err <= max(1e-3 * float(g0.norm()), 10 * own) + 1e-9, (k, err, own, float(g0.norm()))
+
+
 def test_block0_seam_vs_separate(device, monkeypatch):
     """Block 0's epilogue run inside block 1's prologue + camera attention kernel (Seam0Fn,
     gasfm_edge0_seam_fwd) against the separate launches (EDGE_SEAM off: Block0EpilogueFn +
