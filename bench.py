@@ -71,15 +71,18 @@ def pmc_traffic(E, N):
     return r["point"]["traffic_bytes"]
 
 
-def pmc_kernel_traffic(name, E):
-    """HBM bytes per launch of ``name`` from the committed per-kernel PMC table (tools/pmc_kernels.sh
-    on this bench: 2 x FETCH_SIZE + WRITE_SIZE), when it was taken on the config-4 workload."""
+def pmc_kernel_traffic(names, E):
+    """HBM bytes per launch of the first of ``names`` in the committed per-kernel PMC table
+    (tools/pmc_kernels.sh on this bench: 2 x FETCH_SIZE + WRITE_SIZE), when it was taken on the
+    config-4 workload."""
     if E != 4001638:
         return None
     try:
-        key = name.rstrip(">")  # the table truncates names (and round 4 added a template argument)
         with open(PMC_KERNELS) as f:
-            for line in f:
+            lines = f.readlines()
+        for name in ((names,) if isinstance(names, str) else names):
+            key = name.rstrip(">")  # the table truncates names (and round 4 added a template argument)
+            for line in lines:
                 if line.startswith(key):
                     return float(line.split()[-3]) * 1e6  # total MB column
     except (OSError, ValueError, IndexError):
@@ -301,7 +304,10 @@ def main():
                        and (not fold or (k.get("epi") is not None and k.get("dwp") is not None)))
     flop_e = PBWD_FOLD_FLOP_PER_EDGE if fold else PBWD_FLOP_PER_EDGE
     bytes_e = PBWD_FOLD_BYTES_PER_EDGE if fold else PBWD_BYTES_PER_EDGE
-    pbwd_name = "edge_cam_pbwd_kernel<true, true, true, true>" if fold else "edge_cam_pbwd_kernel<true, true, false, false>"
+    # (round 4: the EPI template argument is an int -- 1 the 32-wide fold, 2 block 0's -- so newer
+    # tables print it as a number)
+    pbwd_name = (("edge_cam_pbwd_kernel<true, true, 1, true>", "edge_cam_pbwd_kernel<true, true, true, true>") if fold
+                 else ("edge_cam_pbwd_kernel<true, true, 0, false>", "edge_cam_pbwd_kernel<true, true, false, false>"))
     for _ in range(2):
         fwd_bwd()
     timer.enabled = False
@@ -348,7 +354,7 @@ def main():
                                        if emul else
                                        f"{'point+camera' if data.shard.cams is not None else 'point'}-sharded x{world}"
                                        if dist_on else "single GPU")},
-            "roofline": {"kernel": pbwd_name + ": camera-attention + edge-prologue backward"
+            "roofline": {"kernel": pbwd_name[0] + ": camera-attention + edge-prologue backward"
                                    + (" + the edge epilogue's backward (dSv, dP0 of the previous block, dWp of this "
                                       "one)" if fold else "") + " (the step's largest kernel), per launch",
                          "bound": "mfma", "achieved": pbwd_tfs, "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",

@@ -48,8 +48,12 @@ def dxl_pos_of(pos):
 
 # round 4: block 0's 2-wide epilogue backward folded into block 1's edge_cam_pbwd the same way
 # (gasfm_edge_cam_pbwd_e0: dSv, aux and the block-0 weight sums from the dP' that launch produces,
-# block 0's input read as the launch's DWP P0 rows).  0: edge0_epilogue_bwd as before.
-E0_FOLD = os.environ.get("GASFM_E0_FOLD", "1") != "0"
+# block 0's input read as the launch's DWP P0 rows).  Off by default: measured on MI355X
+# (tools/gpu_r4_e0fold.sh, profiles/r4_e0fold.txt) the folded launch takes 883 us against 726 for
+# block 1's unfolded one, more than the 137 us edge0_epilogue_bwd it replaces (config 4 29.32-29.33
+# vs 29.28-29.42 ms): the four dots, the 2-wide LayerNorm backward and the weight sums add VALU and
+# LDS work to an issue-bound kernel and raise its spills (14 -> 30 VGPRs).  1: the fold.
+E0_FOLD = os.environ.get("GASFM_E0_FOLD", "0") != "0"
 
 # Block 0's prologue writes XL0 row by row through the point plan's permutation (one 32-B store
 # per row, gasfm_edge0_prologue_fwd_rows) instead of scattering the point halves through pos.

@@ -30,6 +30,10 @@ ALGO_MB = {  # config 4 algorithmic bytes per launch, DESIGN.md §5
     # round 4: the pbwd kernels carry a fifth template argument (XP: dXLp gathered through pos)
     "edge_cam_pbwd_kernel<true, true, true, true, false>": 2113,
     "edge_cam_pbwd_kernel<true, true, false, true, false>": 2081,
+    # round 4: EPI became an int template argument (1: the 32-wide fold; 2: block 0's, + aux 16 B per edge)
+    "edge_cam_pbwd_kernel<true, true, 1, true, false>": 2113,
+    "edge_cam_pbwd_kernel<true, true, 0, true, false>": 2081,
+    "edge_cam_pbwd_kernel<true, true, 2, true, false>": 2145,
 }
 
 
