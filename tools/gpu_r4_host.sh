@@ -1,0 +1,5 @@
+# round 4: host-side profile of the eager config-3 union step (tools/host_profile.py)
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u tools/host_profile.py --steps 10 > gpurun_out/host_prof.txt 2> gpurun_out/host_prof.err || { tail -30 gpurun_out/host_prof.err; exit 1; }
+head -5 gpurun_out/host_prof.txt
