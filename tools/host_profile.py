@@ -33,7 +33,12 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--top", type=int, default=45)
     ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--same-thread", action="store_true",
+                    help="run the backward on this thread (autograd multithreading off) so cProfile sees it")
+    ap.add_argument("--callers", default="", help="also print the callers of functions matching this name")
     args = ap.parse_args()
+    if args.same_thread:
+        torch.autograd.set_multithreading_enabled(False)
     dev = torch.device("cuda", 0)
     np.random.seed(0)
     torch.manual_seed(0)
@@ -79,6 +84,8 @@ def main():
     st = pstats.Stats(pr)
     st.sort_stats("tottime").print_stats(args.top)
     st.sort_stats("cumulative").print_stats(args.top)
+    if args.callers:
+        st.print_callers(args.callers)
 
 
 if __name__ == "__main__":
