@@ -1447,6 +1447,12 @@ __device__ __forceinline__ void prod_c2(const float4* __restrict__ Q, const f32x
 #ifndef GASFM_PBWD_BF
 #define GASFM_PBWD_BF 0
 #endif
+// 1: the camera bias gradient's sums (added once per camera, by lanes c = 0) live in LDS, 8 floats
+// per lane group, instead of 8 VGPRs held across every tile of the kernel (round 4); 2: also the
+// LayerNorm affine of the lane's two C-layout columns re-read from LDS in each tile (4 VGPRs)
+#ifndef GASFM_PBWD_DB_LDS
+#define GASFM_PBWD_DB_LDS 0
+#endif
 
 // EPI == 2 (round 4): the previous block is block 0, whose epilogue is 2-wide
 // (P' = Wsk relu(LN_b(P0)) + bsk + scale (Wp relu(LN_a(P0)) + bp + Sp + Sv + Sg), edge_block0.hip),
@@ -1481,7 +1487,8 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   // of the 20 lanes c < 5 (C layout), then a dummy slot (registers held across tiles spill here)
   constexpr int OG = OX + (GASFM_PBWD_ITEM_LDS ? kWaves * 2 * F : 0);
   constexpr int OA = OG + (EPI == 2 ? kWaves * 17 * 4 : 0);
-  constexpr int NL = OA + (EPI == 2 ? kWaves * 21 * 8 : 0);
+  constexpr int OB = OA + (EPI == 2 ? kWaves * 21 * 8 : 0);
+  constexpr int NL = OB + (GASFM_PBWD_DB_LDS ? kWaves * 4 * 8 : 0);
   __shared__ __attribute__((aligned(16))) float lds[NL];
   float* WcQ = lds;
   float* WptTQ = lds + QW;
@@ -1518,6 +1525,11 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   float* Xi = lds + OX + wave * 2 * F;  // (GASFM_PBWD_ITEM_LDS) [XR | gout] of the wave's camera item
   float* Lg = lds + OG + wave * 17 * 4 + (g == 0 ? c : 16) * 4;  // (EPI == 2) this lane's affine sums
   float* La = lds + OA + wave * 21 * 8 + (c < 5 ? 5 * g + c : 20) * 8;  // (EPI == 2) its weight sums
+  float* Ldb = lds + OB + (wave * 4 + g) * 8;  // (GASFM_PBWD_DB_LDS) the lane group's dbias sums (lane c = 0)
+  if (GASFM_PBWD_DB_LDS && c == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) Ldb[k] = 0.f;
+  }
 #pragma unroll
   for (int k = 0; k < NLS; ++k) Lw[k] = 0.f;
   if (EPI == 2) {
@@ -1526,7 +1538,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
 #pragma unroll
     for (int k = 0; k < 8; ++k) La[k] = 0.f;
   }
-  const float gC[2] = {LN ? gam[c] : 1.f, LN ? gam[16 + c] : 1.f}, bC[2] = {LN ? bet[c] : 0.f, LN ? bet[16 + c] : 0.f};
+  const float gC0[2] = {LN ? gam[c] : 1.f, LN ? gam[16 + c] : 1.f}, bC0[2] = {LN ? bet[c] : 0.f, LN ? bet[16 + c] : 0.f};
   __syncthreads();
   // T-layout vector at this lane's features 16 q + 4 g .. + 3
   auto vecT = [&](int which, int q) {
@@ -1628,7 +1640,15 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
     const bool first = it == 0 || items[it - 1].seg != w.seg;
     if (first && c == 0) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q) dbias[q] += gv[q];
+      for (int q = 0; q < 2; ++q) {
+        if (GASFM_PBWD_DB_LDS) {
+          const float4 o = *reinterpret_cast<const float4*>(Ldb + 4 * q);
+          *reinterpret_cast<float4*>(Ldb + 4 * q) = make_float4(o.x + gv[q][0], o.y + gv[q][1], o.z + gv[q][2],
+                                                                 o.w + gv[q][3]);
+        } else {
+          dbias[q] += gv[q];
+        }
+      }
     }
     f32x4 dxr[2] = {zero4(), zero4()};
     gasfm_work_item wn{0, 0, 0, -1};
@@ -1737,6 +1757,12 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
       f32x4 XcC[2];
       to_c(3, dXc, XcC);
       // ---- LayerNorm statistics of the C-layout rows, LN backward, dP
+      float gC[2], bC[2];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        gC[nt] = GASFM_PBWD_DB_LDS >= 2 ? (LN ? V[16 * nt + c] : 1.f) : gC0[nt];
+        bC[nt] = GASFM_PBWD_DB_LDS >= 2 ? (LN ? V[F + 16 * nt + c] : 0.f) : bC0[nt];
+      }
       f32x4 ph[2];  // relu(LN(P)) (C layout) for the weight gradient
       float dv[4][2];  // dP (C layout) for the branch-free stores (GASFM_PBWD_V2)
 #pragma unroll
@@ -2016,7 +2042,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       v[40 + q * 4 + r] = group_sum<16>(datt[q][r]);
-      v[48 + q * 4 + r] = group_sum<16>(dbias[q][r]);
+      v[48 + q * 4 + r] = group_sum<16>(GASFM_PBWD_DB_LDS ? (c == 0 ? Ldb[4 * q + r] : 0.f) : dbias[q][r]);
     }
   wg_reduce_ordered<NV, kWaves, NL>(v, lds, wave, lane);
   if (wave == 0) {
