@@ -1449,7 +1449,8 @@ __device__ __forceinline__ void prod_c2(const float4* __restrict__ Q, const f32x
 #endif
 // 1: the camera bias gradient's sums (added once per camera, by lanes c = 0) live in LDS, 8 floats
 // per lane group, instead of 8 VGPRs held across every tile of the kernel (round 4); 2: also the
-// LayerNorm affine of the lane's two C-layout columns re-read from LDS in each tile (4 VGPRs)
+// LayerNorm affine of the lane's two C-layout columns re-read from LDS in each tile (4 VGPRs); 3: also
+// the camera's softmax constants (max, 1 / sum, delta: 6 VGPRs) parked per lane group in LDS
 #ifndef GASFM_PBWD_DB_LDS
 #define GASFM_PBWD_DB_LDS 0
 #endif
@@ -1488,7 +1489,8 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   constexpr int OG = OX + (GASFM_PBWD_ITEM_LDS ? kWaves * 2 * F : 0);
   constexpr int OA = OG + (EPI == 2 ? kWaves * 17 * 4 : 0);
   constexpr int OB = OA + (EPI == 2 ? kWaves * 21 * 8 : 0);
-  constexpr int NL = OB + (GASFM_PBWD_DB_LDS ? kWaves * 4 * 8 : 0);
+  constexpr int OC = OB + (GASFM_PBWD_DB_LDS ? kWaves * 4 * 8 : 0);
+  constexpr int NL = OC + (GASFM_PBWD_DB_LDS >= 3 ? kWaves * 4 * 8 : 0);
   __shared__ __attribute__((aligned(16))) float lds[NL];
   float* WcQ = lds;
   float* WptTQ = lds + QW;
@@ -1526,6 +1528,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   float* Lg = lds + OG + wave * 17 * 4 + (g == 0 ? c : 16) * 4;  // (EPI == 2) this lane's affine sums
   float* La = lds + OA + wave * 21 * 8 + (c < 5 ? 5 * g + c : 20) * 8;  // (EPI == 2) its weight sums
   float* Ldb = lds + OB + (wave * 4 + g) * 8;  // (GASFM_PBWD_DB_LDS) the lane group's dbias sums (lane c = 0)
+  float* Lsm = lds + OC + (wave * 4 + g) * 8;  // (GASFM_PBWD_DB_LDS >= 3) [M | inv | delta] of the item
   if (GASFM_PBWD_DB_LDS && c == 0) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) Ldb[k] = 0.f;
@@ -1636,6 +1639,11 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
       delta[q] = d + __shfl_xor(d, 16);
       M[q] = seg_max[seg * ldStat + h];
       inv[q] = 1.f / (seg_sum[seg * ldStat + h] + 1e-16f);
+      if (GASFM_PBWD_DB_LDS >= 3 && c == 0) {
+        Lsm[q] = M[q];
+        Lsm[2 + q] = inv[q];
+        Lsm[4 + q] = delta[q];
+      }
     }
     const bool first = it == 0 || items[it - 1].seg != w.seg;
     if (first && c == 0) {
@@ -1738,8 +1746,10 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
         }
         p += __shfl_xor(p, 16);
         da += __shfl_xor(da, 16);
-        const float alpha = (GASFM_PBWD_BF & 1) ? __expf(p - M[q]) * inv[q] * vmask : (valid ? __expf(p - M[q]) * inv[q] : 0.f);
-        const float de = alpha * (da - delta[q]);
+        const float Mq = GASFM_PBWD_DB_LDS >= 3 ? Lsm[q] : M[q], iq = GASFM_PBWD_DB_LDS >= 3 ? Lsm[2 + q] : inv[q];
+        const float dq = GASFM_PBWD_DB_LDS >= 3 ? Lsm[4 + q] : delta[q];
+        const float alpha = (GASFM_PBWD_BF & 1) ? __expf(p - Mq) * iq * vmask : (valid ? __expf(p - Mq) * iq : 0.f);
+        const float de = alpha * (da - dq);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float dz = de * at[r] * (z[r] > 0.f ? 1.f : slope);

@@ -1,9 +1,9 @@
 # round 4: edge_cam_pbwd with fewer registers held across tiles (GASFM_PBWD_DB_LDS=1: the camera bias
-# sums in LDS; =2: also the LayerNorm affine re-read per tile) vs the default, same box
+# sums in LDS; =2: also the LayerNorm affine re-read per tile; =3: also the softmax constants) vs the default, same box
 set -o pipefail
 mkdir -p gpurun_out
 T="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
-GASFM_LIB=$PWD/gasfm_amd/libgasfm_db2.so timeout -k 10 400 $T tests/test_gpu_edge_cam.py > gpurun_out/ab12_tests.log 2>&1 || { grep -B2 -A30 "^E \|FAILED" gpurun_out/ab12_tests.log | head -60; exit 1; }
+GASFM_LIB=$PWD/gasfm_amd/libgasfm_db3.so timeout -k 10 400 $T tests/test_gpu_edge_cam.py > gpurun_out/ab12_tests.log 2>&1 || { grep -B2 -A30 "^E \|FAILED" gpurun_out/ab12_tests.log | head -60; exit 1; }
 tail -1 gpurun_out/ab12_tests.log
 run() {
   local label=$1; shift
@@ -15,7 +15,9 @@ for rep in 1 2; do
   run default
   run db1 GASFM_LIB=$PWD/gasfm_amd/libgasfm_db1.so
   run db2 GASFM_LIB=$PWD/gasfm_amd/libgasfm_db2.so
+  run db3 GASFM_LIB=$PWD/gasfm_amd/libgasfm_db3.so
   EXTRA="--emulate-world 8"
   run default
   run db2 GASFM_LIB=$PWD/gasfm_amd/libgasfm_db2.so
+  run db3 GASFM_LIB=$PWD/gasfm_amd/libgasfm_db3.so
 done
