@@ -219,9 +219,16 @@ def _p(t):
 _LAUNCH_STREAM = None   # set by launching_on(): libgasfm launches go there instead of torch's stream
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream(t):
     s = _LAUNCH_STREAM
     if s is None:
+        if _RAW_STREAM is not None and t.device.index is not None:
+            # the current stream's handle without building a torch.cuda.Stream object (~2 us per
+            # launch on the host: ~4,700 launches per eager training step)
+            return ctypes.c_void_p(_RAW_STREAM(t.device.index))
         s = torch.cuda.current_stream(t.device)
     return ctypes.c_void_p(s.cuda_stream)
 
