@@ -467,6 +467,14 @@ struct SeamEpi {
 // EP0: block 0's epilogue (edge0_epilogue_fwd, 2-wide P) as the seam's first half:
 //   P' = Wsk relu(LN_b(P)) + bsk + scale (Wp relu(LN_a(P)) + bp + Sg + Sp[pt] + Sv[cam])
 // computed per lane on its 8 features (2-wide products: no MFMA), in edge0_epilogue_fwd's order.
+// 1: the seam's work items dealt so that the workgroups of one XCD (blocks b = x mod 8) take
+// contiguous item ranges: at any time an XCD's resident waves cover ~16 consecutive cameras, so its
+// L2 holds their point windows' Sp rows instead of those of ~130 cameras spread over all 8 XCDs
+// (round 4; the Sp[pt] gathers in camera order are the seam's 1.15x traffic).  The items and their
+// outputs are the same either way.
+#ifndef GASFM_SEAM_XCD
+#define GASFM_SEAM_XCD 0
+#endif
 template <bool LN, bool EP0>
 __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kernel(
     SeamEpi ep, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
@@ -509,7 +517,9 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
     const float4 t = *reinterpret_cast<const float4*>(V + which * F + 16 * q + 4 * g);
     return f32x4{t.x, t.y, t.z, t.w};
   };
-  const int gw = blockIdx.x * kWaves + wave, nw = gridDim.x * kWaves;
+  const int bx = (GASFM_SEAM_XCD && gridDim.x % 8 == 0)
+                     ? int(blockIdx.x % 8) * int(gridDim.x / 8) + int(blockIdx.x / 8) : int(blockIdx.x);
+  const int gw = bx * kWaves + wave, nw = gridDim.x * kWaves;
   // next tile: P_b slabs, the edge's point and P0 pair, its point-order row (all branch-free)
   f32x4 ns[2];
   int32_t npos = 0, npt = 0;
