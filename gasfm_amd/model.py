@@ -1043,6 +1043,13 @@ class GraphAttnSfMNet(Module):
     # takes the immediate path.  False disables the batching.
     batch_weight_grads = True
 
+    def _apply(self, *args, **kwargs):
+        # .to() / .cuda() / .float() may replace Parameter objects without a registration hook
+        # (torch.__future__.set_overwrite_module_params_on_conversion): re-list them afterwards
+        out = super()._apply(*args, **kwargs)
+        _bump_tree_version()
+        return out
+
     def _param_list(self):
         """The parameters as a list, rebuilt only after a parameter or module was registered anywhere
         (torch's global registration hooks bump _TREE_VERSION): self.parameters() walks ~180 modules

@@ -205,3 +205,23 @@ def test_binding_arity_matches_header():
         if n != len(_native._SIGS[name][1]):
             bad.append((name, n, len(_native._SIGS[name][1])))
     assert not bad, bad
+
+
+def test_param_list_cache_follows_the_module_tree():
+    """GraphAttnSfMNet._param_list (the forward's deferred-gradient check) is a cached list: it must
+    follow a parameter replaced deep in the tree and a dtype / device conversion that creates new
+    Parameter objects (torch's overwrite-on-conversion mode)."""
+    import gasfm_amd
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=2))
+    same = lambda: len(net._param_list()) == len(list(net.parameters())) and all(
+        p is q for p, q in zip(net._param_list(), net.parameters()))
+    assert same()
+    net.equivariant_blocks[0].skip_projection.lin_proj.weight = torch.nn.Parameter(torch.zeros(32, 2))
+    assert same()
+    prev = torch.__future__.get_overwrite_module_params_on_conversion()
+    torch.__future__.set_overwrite_module_params_on_conversion(True)
+    try:
+        net.double()
+        assert same()
+    finally:
+        torch.__future__.set_overwrite_module_params_on_conversion(prev)
