@@ -475,6 +475,9 @@ struct SeamEpi {
 #ifndef GASFM_SEAM_XCD
 #define GASFM_SEAM_XCD 0
 #endif
+#ifndef GASFM_SEAM_PRIO
+#define GASFM_SEAM_PRIO 0
+#endif
 template <bool LN, bool EP0>
 __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kernel(
     SeamEpi ep, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
@@ -520,6 +523,7 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
   const int bx = (GASFM_SEAM_XCD && gridDim.x % 8 == 0)
                      ? int(blockIdx.x % 8) * int(gridDim.x / 8) + int(blockIdx.x / 8) : int(blockIdx.x);
   const int gw = bx * kWaves + wave, nw = gridDim.x * kWaves;
+  if (GASFM_SEAM_PRIO && blockIdx.x >= gridDim.x / 2) __builtin_amdgcn_s_setprio(1);  // as GASFM_PBWD_PRIO
   // next tile: P_b slabs, the edge's point and P0 pair, its point-order row (all branch-free)
   f32x4 ns[2];
   int32_t npos = 0, npt = 0;
@@ -1464,6 +1468,9 @@ __device__ __forceinline__ void prod_c2(const float4* __restrict__ Q, const f32x
 #ifndef GASFM_PBWD_DB_LDS
 #define GASFM_PBWD_DB_LDS 0
 #endif
+#ifndef GASFM_PBWD_PRIO
+#define GASFM_PBWD_PRIO 0
+#endif
 
 // EPI == 2 (round 4): the previous block is block 0, whose epilogue is 2-wide
 // (P' = Wsk relu(LN_b(P0)) + bsk + scale (Wp relu(LN_a(P0)) + bp + Sp + Sv + Sg), edge_block0.hip),
@@ -1578,6 +1585,10 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   float db[4] = {0.f, 0.f, 0.f, 0.f}, dg[2] = {0.f, 0.f}, dbt[2] = {0.f, 0.f};
   f32x4 datt[2] = {zero4(), zero4()}, dbias[2] = {zero4(), zero4()};
   const int gw = blockIdx.x * kWaves + wave, nw = gridDim.x * kWaves;
+  // (GASFM_PBWD_PRIO) the second-dispatched half of the resident grid -- a CU's second workgroup,
+  // whose waves share each SIMD with the first's -- issues at priority 1 (MI355X_MICROARCH.md
+  // "Static priority for the younger half")
+  if (GASFM_PBWD_PRIO && blockIdx.x >= gridDim.x / 2) __builtin_amdgcn_s_setprio(1);
 
   // next tile's rows of P, dXLp, dRes in T layout, one tile ahead (clamped, masked where consumed)
   f32x4 nPT[2], nXT[2], nRT[2];
