@@ -17,4 +17,3 @@ cat gpurun_out/r4f_pmc.txt
 timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --emulate-world 8 > gpurun_out/r4f_em8.json 2> gpurun_out/r4f_em8.err || { tail -20 gpurun_out/r4f_em8.err; exit 1; }
 tail -1 gpurun_out/r4f_em8.json | cut -c1-200
 bash tools/prof_emul.sh r4f8 --emulate-world 8
-bash tools/gpu_r4_ab14.sh
