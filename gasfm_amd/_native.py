@@ -54,6 +54,12 @@ _SIGS = {
     "gasfm_edge_seam_fwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _f32, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _f32, _vp, _vp,
                                    _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _i32,
                                    _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
+    "gasfm_edge_seam_fwd_x": (_i32, [_vp, _vp, _vp, _vp, _vp, _f32, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _f32, _vp, _vp,
+                                     _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _i32,
+                                     _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp]),
+    "gasfm_edge_cam_pbwd_xlc": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _f32, _vp, _i64, _vp, _vp, _f32,
+                                       _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _vp, _i64,
+                                       _vp, _vp, _i64, _vp, _i32, _f32, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
     "gasfm_edge_cam_pbwd_part_rows": (_i32, [_i32]),
     "gasfm_edge_cam_pbwd_part_cols": (_i32, []),
     "gasfm_edge_cam_pbwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _f32, _vp, _i64, _vp, _vp, _f32, _vp,
@@ -647,12 +653,23 @@ def edge_cam_bwd(P, ln_w, ln_b, eps, Wc, bc, XR, att, bias, slope, out, seg_max,
 
 def edge_seam_fwd(Pb, P0, pt, lnw_b, lnb_b, eps_b, Wp, bp, Sp, Sv, Sg, scale, Pout, ln_w, ln_b, eps, Wpt, bpt, Wc, bc,
                   XLp, pos, XR, att, bias, slope, plan_items, n_items, finalize, out, seg_max, seg_sum, part,
-                  ldStat=4):
+                  ldStat=4, XLc=None):
     """Block b's edge epilogue (P' = Pout) + block b+1's prologue and camera attention forward in one
-    pass (csrc/edge_cam.hip edge_seam_fwd); outputs as edge_cam_fwd's plus Pout."""
+    pass (csrc/edge_cam.hip edge_seam_fwd); outputs as edge_cam_fwd's plus Pout (and XLc, block b+1's
+    camera half, when given: gasfm_edge_seam_fwd_x)."""
     _req(Pb, "Pb", 32)
     ldXR = _rows32(XR, "XR")
     ldSv = _rows32(Sv, "Sv")
+    if XLc is not None:
+        _req(XLc, "XLc", 32)
+        st = lib().gasfm_edge_seam_fwd_x(_p(Pb), _p(P0), _p(pt), _p(lnw_b), _p(lnb_b), eps_b, _p(Wp), Wp.stride(0),
+                                         _p(bp), _p(Sp), _p(Sv), ldSv, _p(Sg), scale, _p(Pout), _p(ln_w), _p(ln_b),
+                                         eps, _p(Wpt), _p(bpt), _p(Wc), _p(bc), _p(XLp), XLp.stride(0), _p(pos),
+                                         _p(XR), ldXR, _p(att), _p(bias), slope, _p(plan_items), n_items,
+                                         int(finalize), _p(out), out.stride(0) if out is not None else 0,
+                                         _p(seg_max), _p(seg_sum), ldStat, _p(part), _p(XLc), _stream(Pb))
+        check(st, "gasfm_edge_seam_fwd_x")
+        return
     st = lib().gasfm_edge_seam_fwd(_p(Pb), _p(P0), _p(pt), _p(lnw_b), _p(lnb_b), eps_b, _p(Wp), Wp.stride(0), _p(bp),
                                    _p(Sp), _p(Sv), ldSv, _p(Sg), scale, _p(Pout), _p(ln_w), _p(ln_b), eps, _p(Wpt),
                                    _p(bpt), _p(Wc), _p(bc), _p(XLp), XLp.stride(0), _p(pos), _p(XR), ldXR, _p(att),
@@ -695,7 +712,7 @@ def edge_cam_pbwd_e0_offset(dwp_cols=34):
 
 def edge_cam_pbwd(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, scale, XR, att, bias, slope, out, seg_max, seg_sum, gout,
                   plan_items, n_items, dXLp, dRes, dP, dXR, part_dxr, part, ldStat=4, epi=None, dwp=None,
-                  dxl_pos=None, epi0=None):
+                  dxl_pos=None, epi0=None, XLc=None):
     """The camera attention's backward and the block's edge prologue backward in one pass
     (csrc/edge_cam.hip edge_cam_pbwd): dP, dXR (+ split partials), part rows
     [dW 64x32 | db 64 | dgamma 32 | dbeta 32 | datt 32 | dbias 32] per workgroup.
@@ -743,6 +760,17 @@ def edge_cam_pbwd(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, scale, XR, att, bias, slo
                                           _p(Wp0), _p(Wsk0), _p(ln0), eps0, scale0, _p(dSv0), _p(part_dsv0), _p(aux0),
                                           _p(dxl_pos), _stream(P))
         check(st, "gasfm_edge_cam_pbwd_e0")
+        return
+    if XLc is not None and epi is not None and ldWpo:  # the kernel keeps XLc only with EPI and DWP
+        _req(XLc, "XLc", 32)
+        st = lib().gasfm_edge_cam_pbwd_xlc(_p(P), _p(ln_w), _p(ln_b), eps, _p(Wpt), _p(Wc), _p(bc), _p(Wp),
+                                           Wp.stride(0) if Wp is not None else 0, scale, _p(XR), ldXR, _p(att),
+                                           _p(bias), slope, _p(out), out.stride(0), _p(seg_max), _p(seg_sum), ldStat,
+                                           _p(gout), gout.stride(0), _p(plan_items), n_items, _p(dXLp),
+                                           dXLp.stride(0), _p(dRes), _p(dP), _p(dXR), dXR.stride(0), _p(part_dxr),
+                                           _p(part), part.stride(0), _p(We), ldWe, scale_e, _p(dSv), _p(part_dsv),
+                                           _p(dP0), _p(P0), ldWpo, _p(dxl_pos), _p(XLc), _stream(P))
+        check(st, "gasfm_edge_cam_pbwd_xlc")
         return
     st = lib().gasfm_edge_cam_pbwd_ex(_p(P), _p(ln_w), _p(ln_b), eps, _p(Wpt), _p(Wc), _p(bc), _p(Wp),
                                       Wp.stride(0) if Wp is not None else 0, scale, _p(XR), ldXR, _p(att), _p(bias),

@@ -438,6 +438,7 @@ struct SeamEpi {
   const float* bb;
   const float* Wsk;   // skip projection [32 x 2]
   const float* bsk;   // [32]
+  float* XLc;         // (XS, round 4 experiment) block b+1's XLc [E, 32] in edge order, or null
 };
 
 #ifndef GASFM_SEAM_MINW
@@ -478,7 +479,7 @@ struct SeamEpi {
 #ifndef GASFM_SEAM_PRIO
 #define GASFM_SEAM_PRIO 0
 #endif
-template <bool LN, bool EP0>
+template <bool LN, bool EP0, bool XS = false>
 __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kernel(
     SeamEpi ep, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
     const float* __restrict__ Wpt, const float* __restrict__ bpt, const float* __restrict__ Wc,
@@ -711,6 +712,10 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
         for (int r = 0; r < 4; ++r) {
           xl[r] = acc[2 + q][r] + bcq[r];
           p = fmaf(leaky(xl[r] + xr[q][r], slope), atq[r], p);
+        }
+        if (XS) {  // XLc kept for edge_cam_pbwd (lanes past the item's end rewrite row0's own values)
+          const int64_t xrow = row0 + (valid ? c : 0);
+          *reinterpret_cast<float4*>(ep.XLc + xrow * F + 16 * q + 4 * g) = make_float4(xl[0], xl[1], xl[2], xl[3]);
         }
         p += __shfl_xor(p, 16);  // the head's other 4 features
         if (GASFM_SEAM_V2) {
@@ -1395,6 +1400,7 @@ struct PbwdEpi {
   const float* ln0;
   float eps0;
   float* aux;
+  const float* XLc;   // (XS, round 4 experiment) XLc [E, 32] kept by the forward seam, or null
 };
 
 // C-layout rows of a [*, 32] tensor: v[ft][r] = X[row0 + 4 g + r][16 ft + c] (rows clamped, not masked)
@@ -1479,7 +1485,7 @@ __device__ __forceinline__ void prod_c2(const float4* __restrict__ Q, const f32x
 // input) to aux, and the weight sums [dWp dWsk | dbsk] = dP^T [relu(LN_a P0) relu(LN_b P0) | 1]
 // as 8 MFMA per tile (B operand: the five edge values in tile 1's padding columns).  Replaces
 // edge0_epilogue_bwd's pass over dP' (128 B per edge read back).
-template <bool LN, bool RES, int EPI, bool DWP, bool XP = false>
+template <bool LN, bool RES, int EPI, bool DWP, bool XP = false, bool XS = false>
 __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kernel(
     const float* __restrict__ P, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
     const float* __restrict__ Wpt, const float* __restrict__ Wc, const float* __restrict__ bc,
@@ -1591,7 +1597,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
   if (GASFM_PBWD_PRIO && blockIdx.x >= gridDim.x / 2) __builtin_amdgcn_s_setprio(1);
 
   // next tile's rows of P, dXLp, dRes in T layout, one tile ahead (clamped, masked where consumed)
-  f32x4 nPT[2], nXT[2], nRT[2];
+  f32x4 nPT[2], nXT[2], nRT[2], nXc[2];
   float2 nP0 = make_float2(0.f, 0.f);  // (DWP) P0 of edge c (a dummy read of P without P0)
   const float* p0p = (DWP && ep.P0) ? ep.P0 : P;
   // XP (round 4, dxl_pos): dXLp in point-segment order, edge e's row at dxl_pos[e] (the point
@@ -1613,6 +1619,14 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
     if (XP) npos = dxl_pos[xrow];
     load_slabs32(P, row0, nrows, nPT, lane);
     if (!XP) load_x(xrow);
+    if (XS) {  // XLc of edge c (T layout), kept by the forward seam
+      const float* p = ep.XLc + xrow * F + 4 * g;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float4 t = *reinterpret_cast<const float4*>(p + 16 * u);
+        nXc[u] = f32x4{t.x, t.y, t.z, t.w};
+      }
+    }
     if (RES) load_slabs32(dRes, row0, nrows, nRT, lane);
     if (DWP) nP0 = *reinterpret_cast<const float2*>(p0p + xrow * 2);
   };
@@ -1690,7 +1704,11 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
     }
     for (int64_t row0 = w.begin; row0 < w.end; row0 += TR) {
       const int nrows = rows_at(w, row0);
-      f32x4 PT[2] = {nPT[0], nPT[1]}, XT[2] = {nXT[0], nXT[1]}, RT[2];
+      f32x4 PT[2] = {nPT[0], nPT[1]}, XT[2] = {nXT[0], nXT[1]}, RT[2], XcT[2];
+      if (XS) {
+        XcT[0] = nXc[0];
+        XcT[1] = nXc[1];
+      }
       if (RES) {
         RT[0] = nRT[0];
         RT[1] = nRT[1];
@@ -1744,8 +1762,13 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
         }
         phat_slabs_st<LN>(PT, gs, bs, eps, tmean, trstd);
       }
-      f32x4 xc[2] = {vecT(2, 0), vecT(2, 1)};  // b_c, then + Wc P_hat^T
-      xl_slabs<2>(reinterpret_cast<const float4*>(WcQ), PT, xc, lane);
+      f32x4 xc[2] = {vecT(2, 0), vecT(2, 1)};  // b_c, then + Wc P_hat^T (XS: the forward's rows)
+      if (XS) {
+        xc[0] = XcT[0];
+        xc[1] = XcT[1];
+      } else {
+        xl_slabs<2>(reinterpret_cast<const float4*>(WcQ), PT, xc, lane);
+      }
       f32x4 dXc[2];
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
@@ -2271,6 +2294,8 @@ int pbwd_launch(const float* P, const float* ln_w, const float* ln_b, float eps,
     if (ln_w && dRes) {
       if (e0)
         launch(&edge_cam_pbwd_kernel<true, true, 2, true, X>);
+      else if (epi && dwp && ep.XLc)
+        launch(&edge_cam_pbwd_kernel<true, true, 1, true, X, true>);
       else if (epi && dwp)
         launch(&edge_cam_pbwd_kernel<true, true, true, true, X>);
       else if (epi)
@@ -2313,6 +2338,23 @@ extern "C" int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const f
                      part, ldPart, ep, dxl_pos, stream);
 }
 
+extern "C" int gasfm_edge_cam_pbwd_xlc(const float* P, const float* ln_w, const float* ln_b, float eps,
+                                       const float* Wpt, const float* Wc, const float* bc, const float* Wp,
+                                       int32_t ldWp, float scale, const float* XR, int64_t ldXR, const float* att,
+                                       const float* bias, float slope, const float* out, int64_t ldOut,
+                                       const float* seg_max, const float* seg_sum, int64_t ldStat, const float* gout,
+                                       int64_t ldG, const gasfm_work_item* items, int32_t n_items, const float* dXLp,
+                                       int64_t ldXp, const float* dRes, float* dP, float* dXR, int64_t ldDXR,
+                                       float* part_dxr, float* part, int64_t ldPart, const float* We, int32_t ldWe,
+                                       float scale_e, float* dSv_e, float* part_dsv_e, float* dP0_e, const float* P0,
+                                       int32_t ldWpo, const int32_t* dxl_pos, const float* XLc, void* stream) {
+  GASFM_REQUIRE(XLc && aligned16(XLc), "gasfm_edge_cam_pbwd_xlc: XLc must be a 16-byte aligned [E, 32] array");
+  const PbwdEpi ep{We, ldWe, scale_e, dSv_e, part_dsv_e, dP0_e, P0, ldWpo, nullptr, nullptr, 0.f, nullptr, XLc};
+  return pbwd_launch(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, ldWp, scale, XR, ldXR, att, bias, slope, out, ldOut,
+                     seg_max, seg_sum, ldStat, gout, ldG, items, n_items, dXLp, ldXp, dRes, dP, dXR, ldDXR, part_dxr,
+                     part, ldPart, ep, dxl_pos, stream);
+}
+
 extern "C" int32_t gasfm_edge_cam_pbwd_e0_cols(void) { return PB_E0; }
 
 extern "C" int gasfm_edge_cam_pbwd_e0(const float* P, const float* ln_w, const float* ln_b, float eps,
@@ -2345,15 +2387,17 @@ extern "C" int gasfm_edge_cam_pbwd(const float* P, const float* ln_w, const floa
                                 nullptr, stream);
 }
 
-extern "C" int gasfm_edge_seam_fwd(const float* Pb, const float* P0, const int32_t* pt, const float* ln_wb,
-                                   const float* ln_bb, float eps_b, const float* Wp, int32_t ldWp, const float* bp,
-                                   const float* Sp, const float* Sv, int64_t ldSv, const float* Sg, float scale,
-                                   float* Pout, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
-                                   const float* bpt, const float* Wc, const float* bc, float* XLp, int64_t ldXLp,
-                                   const int32_t* pos, const float* XR, int64_t ldXR, const float* att,
-                                   const float* bias, float slope, const gasfm_work_item* items, int32_t n_items,
-                                   int32_t finalize, float* out, int64_t ldOut, float* seg_max, float* seg_sum,
-                                   int64_t ldStat, float* part, void* stream) {
+extern "C" int gasfm_edge_seam_fwd_x(const float* Pb, const float* P0, const int32_t* pt, const float* ln_wb,
+                                     const float* ln_bb, float eps_b, const float* Wp, int32_t ldWp, const float* bp,
+                                     const float* Sp, const float* Sv, int64_t ldSv, const float* Sg, float scale,
+                                     float* Pout, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
+                                     const float* bpt, const float* Wc, const float* bc, float* XLp, int64_t ldXLp,
+                                     const int32_t* pos, const float* XR, int64_t ldXR, const float* att,
+                                     const float* bias, float slope, const gasfm_work_item* items, int32_t n_items,
+                                     int32_t finalize, float* out, int64_t ldOut, float* seg_max, float* seg_sum,
+                                     int64_t ldStat, float* part, float* XLc, void* stream) {
+  GASFM_REQUIRE(!XLc || (aligned16(XLc) && ln_w && tune(GASFM_TUNE_SEAM_LDS) == 0),
+                "gasfm_edge_seam_fwd_x: XLc needs 16-byte rows, the LayerNorm and the register seam");
   GASFM_REQUIRE(n_items >= 0 && Pb && pt && ln_wb && ln_bb && Wp && bp && Sp && Sv && Sg && Pout && Wpt && bpt &&
                     Wc && bc && XLp && XR && att && items,
                 "gasfm_edge_seam_fwd: null pointer");
@@ -2367,7 +2411,7 @@ extern "C" int gasfm_edge_seam_fwd(const float* Pb, const float* P0, const int32
   if (n_items == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const SeamEpi ep{Pb, P0, pt, ln_wb, ln_bb, eps_b, Wp, ldWp, bp, Sp, Sv, ldSv, Sg, scale, Pout,
-                   nullptr, nullptr, nullptr, nullptr};
+                   nullptr, nullptr, nullptr, nullptr, XLc};
   auto launch = [&](auto kern) {
     const int grid = resident_grid(reinterpret_cast<const void*>(kern), kThreads, 0, n_items, kWaves);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, st, ep, ln_w, ln_b, eps, Wpt, bpt, Wc, bc, XLp, ldXLp,
@@ -2395,11 +2439,27 @@ extern "C" int gasfm_edge_seam_fwd(const float* Pb, const float* P0, const int32
     return launch_status("gasfm_edge_seam_fwd");
   }
   note_dispatch(GASFM_K_SEAM_REG);
-  if (ln_w)
+  if (ln_w && XLc)
+    launch(&edge_seam_fwd_kernel<true, false, true>);
+  else if (ln_w)
     launch(&edge_seam_fwd_kernel<true, false>);
   else
     launch(&edge_seam_fwd_kernel<false, false>);
   return launch_status("gasfm_edge_seam_fwd");
+}
+
+extern "C" int gasfm_edge_seam_fwd(const float* Pb, const float* P0, const int32_t* pt, const float* ln_wb,
+                                   const float* ln_bb, float eps_b, const float* Wp, int32_t ldWp, const float* bp,
+                                   const float* Sp, const float* Sv, int64_t ldSv, const float* Sg, float scale,
+                                   float* Pout, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
+                                   const float* bpt, const float* Wc, const float* bc, float* XLp, int64_t ldXLp,
+                                   const int32_t* pos, const float* XR, int64_t ldXR, const float* att,
+                                   const float* bias, float slope, const gasfm_work_item* items, int32_t n_items,
+                                   int32_t finalize, float* out, int64_t ldOut, float* seg_max, float* seg_sum,
+                                   int64_t ldStat, float* part, void* stream) {
+  return gasfm_edge_seam_fwd_x(Pb, P0, pt, ln_wb, ln_bb, eps_b, Wp, ldWp, bp, Sp, Sv, ldSv, Sg, scale, Pout, ln_w,
+                               ln_b, eps, Wpt, bpt, Wc, bc, XLp, ldXLp, pos, XR, ldXR, att, bias, slope, items,
+                               n_items, finalize, out, ldOut, seg_max, seg_sum, ldStat, part, nullptr, stream);
 }
 
 extern "C" int gasfm_edge0_seam_fwd(const float* P, const int32_t* pt, const float* ln_a_w, const float* ln_a_b,

@@ -54,6 +54,9 @@ def dxl_pos_of(pos):
 # vs 29.28-29.42 ms): the four dots, the 2-wide LayerNorm backward and the weight sums add VALU and
 # LDS work to an issue-bound kernel and raise its spills (14 -> 30 VGPRs).  1: the fold.
 E0_FOLD = os.environ.get("GASFM_E0_FOLD", "0") != "0"
+# round 4 experiment: the forward seam keeps block b+1's camera-half XLc ([E, 32], edge order) and
+# that block's edge_cam_pbwd reads it instead of recomputing it from P.  0: recompute.
+XLC_STORE = os.environ.get("GASFM_XLC_STORE", "0") != "0"
 
 # Block 0's prologue writes XL0 row by row through the point plan's permutation (one 32-B store
 # per row, gasfm_edge0_prologue_fwd_rows) instead of scattering the point halves through pos.
@@ -200,7 +203,7 @@ def _dwp_torch(P, ln_w, ln_b, eps, dRes, P0):
     return PROJ_SCALE * (dRes.t() @ ph)
 
 
-def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None, epi0=None):
+def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None, epi0=None, xlc=None):
     """EdgeCamFn's backward from its saved state (ctx attributes eps, heads, slope, plan, att_shape,
     has_ln, dwp, defer): the 20 input gradients of EdgeCamFn.forward.  epi: the previous block's
     epilogue outputs to fill from dP (edge_cam_pbwd's EPI), or None; ctx.epi_done tells whether
@@ -231,7 +234,7 @@ def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None, epi0=None):
                               out, smax, ssum, g_c, plan.items, plan.n_items, dXLp, dRes, dP, dXR, part_dxr, part,
                               epi=epi if use_epi else None,
                               dwp=(P0 if P0 is not None else True) if dwp else None, dxl_pos=dxl_pos,
-                              epi0=epi0 if use_e0 else None)
+                              epi0=epi0 if use_e0 else None, XLc=xlc if (use_epi and dwp) else None)
         ctx.epi_done = use_epi
         if use_e0:
             off = _native.edge_cam_pbwd_e0_offset(wcols)
@@ -410,11 +413,13 @@ class SeamFn(torch.autograd.Function):
         Pn = torch.empty_like(P)
         Wp_c, Sp_c, Sv_r, Sg_f = Wp.contiguous(), Sp.contiguous(), _rows(Sv), Sg.reshape(-1).contiguous()
         bp_c = bp.contiguous()
+        xlc = (torch.empty((E, 32), dtype=torch.float32, device=dev)
+               if XLC_STORE and ln_w is not None and dwp_n else None)
 
         def launch(items, n_items, finalize, out, smax, ssum, part):
             _native.edge_seam_fwd(P, P0, edges.pt, lnw_b, lnb_b, eps_b, Wp_c, bp_c, Sp_c, Sv_r, Sg_f, PROJ_SCALE, Pn,
                                   ln_w, ln_b, eps, Wpt, bpt, Wc, bc, XLp, pos, XR, attf, bias if finalize else None,
-                                  slope, items, n_items, finalize, out, smax, ssum, part)
+                                  slope, items, n_items, finalize, out, smax, ssum, part, XLc=xlc)
         out, smax, ssum = _cam_attention_fwd(launch, bias, plan, heads, HC, plan_partial, shard, dev)
         # EdgeEpilogueFn's state
         ctx.e_eps, ctx.edges, ctx.sg_shape = eps_b, edges, Sg.shape
@@ -431,6 +436,7 @@ class SeamFn(torch.autograd.Function):
         ctx.save_for_backward(P, P0, Wp_c, lnw_b, lnb_b, Pn, ln_w, ln_b, Wpt, Wc, bc, Wp_n, XR, attf, bias, out, smax,
                               ssum, P0_n)
         ctx.n_epi = 5
+        ctx.xlc = xlc
         token_n = P.new_empty((1, 1)).expand(E, P.shape[1])
         return Pn, XLp, out, token_n
 
@@ -450,7 +456,8 @@ class SeamFn(torch.autograd.Function):
             dP0 = torch.empty((P_b.shape[0], 2), dtype=torch.float32, device=dev) if P0_b is not None else None
             folded = (dSv, part_dsv, dP0)
         gc = _cam_backward(ctx, cam, dXLp, g_c, dRes,
-                           epi=None if folded is None else (Wp_b, PROJ_SCALE) + folded)
+                           epi=None if folded is None else (Wp_b, PROJ_SCALE) + folded, xlc=ctx.xlc)
+        ctx.xlc = None
         if not ctx.epi_done:
             folded = None
         dPn = gc[0] if gPn is None else gc[0] + gPn

@@ -168,6 +168,17 @@ int gasfm_edge_seam_fwd(const float* Pb, const float* P0, const int32_t* pt, con
                         int64_t ldXR, const float* att, const float* bias, float slope,
                         const gasfm_work_item* items, int32_t n_items, int32_t finalize, float* out, int64_t ldOut,
                         float* seg_max, float* seg_sum, int64_t ldStat, float* part, void* stream);
+/* gasfm_edge_seam_fwd that also writes block b+1's camera-half XLc [E, 32] (edge order, bias
+ * included) for gasfm_edge_cam_pbwd_xlc (round 4 experiment: XLc kept instead of recomputed in the
+ * backward; XLc null: gasfm_edge_seam_fwd).  Requires ln_w. */
+int gasfm_edge_seam_fwd_x(const float* Pb, const float* P0, const int32_t* pt, const float* ln_wb, const float* ln_bb,
+                          float eps_b, const float* Wp, int32_t ldWp, const float* bp, const float* Sp, const float* Sv,
+                          int64_t ldSv, const float* Sg, float scale, float* Pout, const float* ln_w,
+                          const float* ln_b, float eps, const float* Wpt, const float* bpt, const float* Wc,
+                          const float* bc, float* XLp, int64_t ldXLp, const int32_t* pos, const float* XR,
+                          int64_t ldXR, const float* att, const float* bias, float slope,
+                          const gasfm_work_item* items, int32_t n_items, int32_t finalize, float* out, int64_t ldOut,
+                          float* seg_max, float* seg_sum, int64_t ldStat, float* part, float* XLc, void* stream);
 
 /* Block 0's edge epilogue (2-wide P: P' = Wsk relu(LN_b(P)) + bsk + scale (Wp relu(LN_a(P)) + bp +
  * Sg + Sp[pt] + Sv[cam]), gasfm_edge0_epilogue_fwd) and block 1's prologue + camera attention
@@ -233,6 +244,18 @@ int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const float* ln_b,
  * aux0 [E, 4] = (dP_hat_a (2), dP of the skip branch (2)) and, after the 32 x 34 dWp block of each
  * part row, gasfm_edge_cam_pbwd_e0_cols() floats [dWp0 64 | dWsk0 64 | dbsk0 32 | dgb 2 | dbb 2]
  * (ldPart >= part_cols + 32 x 34 + e0_cols). */
+/* gasfm_edge_cam_pbwd_ex (LN, dRes, EPI and DWP) reading XLc [E, 32] as written by
+ * gasfm_edge_seam_fwd_x instead of recomputing it from P (round 4 experiment). */
+int gasfm_edge_cam_pbwd_xlc(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
+                            const float* Wc, const float* bc, const float* Wp, int32_t ldWp, float scale,
+                            const float* XR, int64_t ldXR, const float* att, const float* bias, float slope,
+                            const float* out, int64_t ldOut, const float* seg_max, const float* seg_sum,
+                            int64_t ldStat, const float* gout, int64_t ldG, const gasfm_work_item* items,
+                            int32_t n_items, const float* dXLp, int64_t ldXp, const float* dRes, float* dP,
+                            float* dXR, int64_t ldDXR, float* part_dxr, float* part, int64_t ldPart,
+                            const float* We, int32_t ldWe, float scale_e, float* dSv_e, float* part_dsv_e,
+                            float* dP0_e, const float* P0, int32_t ldWpo, const int32_t* dxl_pos, const float* XLc,
+                            void* stream);
 int32_t gasfm_edge_cam_pbwd_e0_cols(void);
 int gasfm_edge_cam_pbwd_e0(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
                            const float* Wc, const float* bc, const float* Wp, int32_t ldWp, float scale,

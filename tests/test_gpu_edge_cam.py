@@ -186,6 +186,46 @@ def test_epilogue_fold_vs_unfolded(device, monkeypatch):
         assert err <= max(1e-3 * float(g0.norm()), 10 * own) + 1e-9, (k, err, own, float(g0.norm()))
 
 
+def test_xlc_store_vs_recompute(device, monkeypatch):
+    """XLc kept by the forward seam and read by edge_cam_pbwd (edge_block.XLC_STORE) against the
+    recompute from P: identical forward, the kept rows used by the folded launches (blocks 2-3 of a
+    4-block net), every parameter gradient within 1e-4 normwise of the recomputing path or within
+    10x its own distance from the fp64 oracle."""
+    from conftest import oracle_grads
+    from gasfm_amd import edge_block
+    from oracle.weights import deterministic_state_dict
+    sc = synthetic.scaled_config4(0.05, seed=23)
+    data = gasfm_amd.SceneData.from_synthetic(sc, max_piece=64).to(device)
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=4))
+    sd = deterministic_state_dict(net.state_dict(), torch.float64)
+    net.load_state_dict({k: v.float() for k, v in sd.items()})
+    net = net.to(device)
+    gen = torch.Generator().manual_seed(13)
+    cP = torch.randn((sc.m, 3, 4), generator=gen, dtype=torch.float64)
+    cX = torch.randn((4, sc.n), generator=gen, dtype=torch.float64)
+    used = []
+    orig = _native.edge_cam_pbwd
+    monkeypatch.setattr(_native, "edge_cam_pbwd",
+                        lambda *a, **k: (used.append(k.get("XLc") is not None), orig(*a, **k))[1])
+    res = {}
+    for keep in (False, True):
+        monkeypatch.setattr(edge_block, "XLC_STORE", keep)
+        used.clear()
+        net.zero_grad(set_to_none=True)
+        pred = net(data)
+        ((pred["Ps_norm"] * cP.float().to(device)).sum() + (pred["pts3D"] * cX.float().to(device)).sum()).backward()
+        torch.cuda.synchronize()
+        res[keep] = (pred["Ps_norm"].detach().clone(), {k: p.grad.detach().double().cpu() for k, p in net.named_parameters()},
+                     sum(used))
+    assert torch.equal(res[True][0], res[False][0])
+    assert res[False][2] == 0 and res[True][2] == 2, (res[False][2], res[True][2])
+    (g64, _), _ = oracle_grads(sd, sc, cP, cX)
+    for k, g0 in res[False][1].items():
+        err = float((res[True][1][k] - g0).norm())
+        own = float((g0 - torch.from_numpy(g64[k])).norm())
+        assert err <= max(1e-4 * float(g0.norm()), 10 * own) + 1e-9, (k, err, own, float(g0.norm()))
+
+
 @pytest.mark.parametrize("max_piece", [None, 64])
 def test_block0_fold_vs_unfolded(device, monkeypatch, max_piece):
     """Block 0's 2-wide epilogue backward folded into block 1's edge_cam_pbwd (edge_block.E0_FOLD,
