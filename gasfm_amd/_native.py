@@ -54,12 +54,6 @@ _SIGS = {
     "gasfm_edge_seam_fwd": (_i32, [_vp, _vp, _vp, _vp, _vp, _f32, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _f32, _vp, _vp,
                                    _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _i32,
                                    _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
-    "gasfm_edge_seam_fwd_x": (_i32, [_vp, _vp, _vp, _vp, _vp, _f32, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _f32, _vp, _vp,
-                                     _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _i32,
-                                     _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp]),
-    "gasfm_edge_cam_pbwd_xlc": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _f32, _vp, _i64, _vp, _vp, _f32,
-                                       _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _vp, _i64,
-                                       _vp, _vp, _i64, _vp, _i32, _f32, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
     "gasfm_edge_cam_pbwd_part_rows": (_i32, [_i32]),
     "gasfm_edge_cam_pbwd_part_cols": (_i32, []),
     "gasfm_edge_cam_pbwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _f32, _vp, _i64, _vp, _vp, _f32, _vp,
@@ -70,11 +64,7 @@ _SIGS = {
                                     _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
     "gasfm_edge_cam_pbwd_ex": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _f32, _vp, _i64, _vp, _vp, _f32,
                                       _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _vp, _i64,
-                                      _vp, _vp, _i64, _vp, _i32, _f32, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
-    "gasfm_edge_cam_pbwd_e0_cols": (_i32, []),
-    "gasfm_edge_cam_pbwd_e0": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _i32, _f32, _vp, _i64, _vp, _vp, _f32,
-                                      _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _vp, _i64,
-                                      _vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp, _vp, _vp]),
+                                      _vp, _vp, _i64, _vp, _i32, _f32, _vp, _vp, _vp, _vp, _i32, _vp]),
     "gasfm_edge_cam_fwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _f32,
                                   _vp, _i32, _i32, _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
     "gasfm_edge_cam_bwd": (_i32, [_vp, _vp, _vp, _f32, _vp, _vp, _vp, _i64, _vp, _vp, _f32, _vp, _i64, _vp, _vp, _i64,
@@ -222,39 +212,15 @@ def _p(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
-_LAUNCH_STREAM = None   # set by launching_on(): libgasfm launches go there instead of torch's stream
-
-
 _RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
 def _stream(t):
-    s = _LAUNCH_STREAM
-    if s is None:
-        if _RAW_STREAM is not None and t.device.index is not None:
-            # the current stream's handle without building a torch.cuda.Stream object (~2 us per
-            # launch on the host: ~4,700 launches per eager training step)
-            return ctypes.c_void_p(_RAW_STREAM(t.device.index))
-        s = torch.cuda.current_stream(t.device)
-    return ctypes.c_void_p(s.cuda_stream)
-
-
-class launching_on:
-    """Route libgasfm launches (only those: torch ops and allocations stay on torch's current
-    stream) to ``stream`` inside the block; see gasfm_amd/streams.py."""
-
-    def __init__(self, stream):
-        self.stream = stream
-
-    def __enter__(self):
-        global _LAUNCH_STREAM
-        self.prev, _LAUNCH_STREAM = _LAUNCH_STREAM, self.stream
-        return self
-
-    def __exit__(self, *exc):
-        global _LAUNCH_STREAM
-        _LAUNCH_STREAM = self.prev
-        return False
+    if _RAW_STREAM is not None and t.device.index is not None:
+        # the current stream's handle without building a torch.cuda.Stream object (~2 us per
+        # launch on the host: ~4,700 launches per eager training step)
+        return ctypes.c_void_p(_RAW_STREAM(t.device.index))
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 
 # ---------------------------------------------------------------- kernel-choice record, tuning
@@ -262,11 +228,9 @@ class launching_on:
 KERNELS = {
     "attn_fwd_grp": 0, "attn_fwd_glds": 1, "attn_fwd_vec": 2, "attn_fwd_generic": 3, "attn_fwd_lanes": 4,
     "attn_bwd_glds": 5, "attn_bwd_vec": 6, "attn_bwd_generic": 7, "attn_bwd_lanes": 8,
-    "attn_combine_vec": 9, "attn_combine_generic": 10, "attn_bwd_grp": 11, "seam_lds": 12, "seam_reg": 13,
-    "rowsum_grp": 14,
+    "attn_combine_vec": 9, "attn_combine_generic": 10, "seam_reg": 13,
 }
-TUNING = {"attn_grp_rows": 0, "attn_grp_min_fill": 1, "attn_glds": 2, "attn_wave_cap": 3, "attn_grp_bwd": 4,
-          "seam_lds": 5, "rowsum_grp": 6}
+TUNING = {"attn_grp_rows": 0, "attn_grp_min_fill": 1, "attn_glds": 2, "attn_wave_cap": 3}
 
 
 def dispatch_counts():
@@ -653,23 +617,12 @@ def edge_cam_bwd(P, ln_w, ln_b, eps, Wc, bc, XR, att, bias, slope, out, seg_max,
 
 def edge_seam_fwd(Pb, P0, pt, lnw_b, lnb_b, eps_b, Wp, bp, Sp, Sv, Sg, scale, Pout, ln_w, ln_b, eps, Wpt, bpt, Wc, bc,
                   XLp, pos, XR, att, bias, slope, plan_items, n_items, finalize, out, seg_max, seg_sum, part,
-                  ldStat=4, XLc=None):
+                  ldStat=4):
     """Block b's edge epilogue (P' = Pout) + block b+1's prologue and camera attention forward in one
-    pass (csrc/edge_cam.hip edge_seam_fwd); outputs as edge_cam_fwd's plus Pout (and XLc, block b+1's
-    camera half, when given: gasfm_edge_seam_fwd_x)."""
+    pass (csrc/edge_cam.hip edge_seam_fwd); outputs as edge_cam_fwd's plus Pout."""
     _req(Pb, "Pb", 32)
     ldXR = _rows32(XR, "XR")
     ldSv = _rows32(Sv, "Sv")
-    if XLc is not None:
-        _req(XLc, "XLc", 32)
-        st = lib().gasfm_edge_seam_fwd_x(_p(Pb), _p(P0), _p(pt), _p(lnw_b), _p(lnb_b), eps_b, _p(Wp), Wp.stride(0),
-                                         _p(bp), _p(Sp), _p(Sv), ldSv, _p(Sg), scale, _p(Pout), _p(ln_w), _p(ln_b),
-                                         eps, _p(Wpt), _p(bpt), _p(Wc), _p(bc), _p(XLp), XLp.stride(0), _p(pos),
-                                         _p(XR), ldXR, _p(att), _p(bias), slope, _p(plan_items), n_items,
-                                         int(finalize), _p(out), out.stride(0) if out is not None else 0,
-                                         _p(seg_max), _p(seg_sum), ldStat, _p(part), _p(XLc), _stream(Pb))
-        check(st, "gasfm_edge_seam_fwd_x")
-        return
     st = lib().gasfm_edge_seam_fwd(_p(Pb), _p(P0), _p(pt), _p(lnw_b), _p(lnb_b), eps_b, _p(Wp), Wp.stride(0), _p(bp),
                                    _p(Sp), _p(Sv), ldSv, _p(Sg), scale, _p(Pout), _p(ln_w), _p(ln_b), eps, _p(Wpt),
                                    _p(bpt), _p(Wc), _p(bc), _p(XLp), XLp.stride(0), _p(pos), _p(XR), ldXR, _p(att),
@@ -697,22 +650,14 @@ def edge0_seam_fwd(P, pt, lna_w, lna_b, lnb_w, lnb_b, eps0, Wp, bp, Wsk, bsk, Sp
     check(st, "gasfm_edge0_seam_fwd")
 
 
-def edge_cam_pbwd_part_shape(n_items, dwp_cols=0, e0=False):
-    """(rows, cols) of edge_cam_pbwd's part buffer; dwp_cols = 32 or 34 with the dWp block (dwp);
-    e0: block 0's epilogue part after it (edge_cam_pbwd epi0)."""
+def edge_cam_pbwd_part_shape(n_items, dwp_cols=0):
+    """(rows, cols) of edge_cam_pbwd's part buffer; dwp_cols = 32 or 34 with the dWp block (dwp)."""
     L = lib()
-    return (int(L.gasfm_edge_cam_pbwd_part_rows(n_items)),
-            int(L.gasfm_edge_cam_pbwd_part_cols()) + 32 * dwp_cols + (int(L.gasfm_edge_cam_pbwd_e0_cols()) if e0 else 0))
-
-
-def edge_cam_pbwd_e0_offset(dwp_cols=34):
-    """First column of block 0's epilogue part in an edge_cam_pbwd part row (epi0)."""
-    return int(lib().gasfm_edge_cam_pbwd_part_cols()) + 32 * dwp_cols
+    return int(L.gasfm_edge_cam_pbwd_part_rows(n_items)), int(L.gasfm_edge_cam_pbwd_part_cols()) + 32 * dwp_cols
 
 
 def edge_cam_pbwd(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, scale, XR, att, bias, slope, out, seg_max, seg_sum, gout,
-                  plan_items, n_items, dXLp, dRes, dP, dXR, part_dxr, part, ldStat=4, epi=None, dwp=None,
-                  dxl_pos=None, epi0=None, XLc=None):
+                  plan_items, n_items, dXLp, dRes, dP, dXR, part_dxr, part, ldStat=4, epi=None, dwp=None):
     """The camera attention's backward and the block's edge prologue backward in one pass
     (csrc/edge_cam.hip edge_cam_pbwd): dP, dXR (+ split partials), part rows
     [dW 64x32 | db 64 | dgamma 32 | dbeta 32 | datt 32 | dbias 32] per workgroup.
@@ -720,11 +665,7 @@ def edge_cam_pbwd(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, scale, XR, att, bias, slo
     epi = (We, scale_e, dSv, part_dsv, dP0 or None): also the previous block's edge-epilogue
     gradients from this dP (dSv rows / split-camera partial rows of the same plan, dP0).
     dwp = P0 or None (requires ln_w and dRes): also this block's lin_proj weight gradient,
-    [32 x (32 | 34)] appended to each part row (part has edge_cam_pbwd_part_shape(n, dwp=...) columns).
-    dxl_pos (int32 [E] or None): dXLp rows in point-segment order, edge e's at dxl_pos[e].
-    epi0 = (Wp0, Wsk0, ln0, eps0, scale0, dSv0, part_dsv0, aux0) (round 4, block 1's launch; requires
-    dwp = P0, block 0's input): block 0's 2-wide epilogue backward from this dP
-    (gasfm_edge_cam_pbwd_e0; part has edge_cam_pbwd_part_shape(n, 34, e0=True) columns)."""
+    [32 x (32 | 34)] appended to each part row (part has edge_cam_pbwd_part_shape(n, dwp=...) columns)."""
     _req(P, "P", 32)
     ldXR = _rows32(XR, "XR")
     We = dSv = part_dsv = dP0 = None
@@ -741,44 +682,12 @@ def edge_cam_pbwd(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, scale, XR, att, bias, slo
         ldWpo = 34 if P0 is not None else 32
     if P0 is not None:
         _req(P0, "P0", 2)
-    if epi0 is not None:
-        if epi is not None or P0 is None:
-            raise ValueError("edge_cam_pbwd: epi0 needs dwp = P0 (block 0's input) and no epi")
-        Wp0, Wsk0, ln0, eps0, scale0, dSv0, part_dsv0, aux0 = epi0
-        _req(dSv0, "dSv0", 32)
-        _req(aux0, "aux0", 4)
-        for t, nm in ((Wp0, "Wp0"), (Wsk0, "Wsk0")):
-            if not (t.is_contiguous() and tuple(t.shape) == (32, 2)):
-                raise ValueError(f"edge_cam_pbwd: {nm} must be a contiguous [32, 2] tensor")
-        if not (ln0.is_contiguous() and ln0.numel() == 8):
-            raise ValueError("edge_cam_pbwd: ln0 must be the 8 contiguous LayerNorm affines")
-        st = lib().gasfm_edge_cam_pbwd_e0(_p(P), _p(ln_w), _p(ln_b), eps, _p(Wpt), _p(Wc), _p(bc), _p(Wp),
-                                          Wp.stride(0), scale, _p(XR), ldXR, _p(att), _p(bias), slope, _p(out),
-                                          out.stride(0), _p(seg_max), _p(seg_sum), ldStat, _p(gout), gout.stride(0),
-                                          _p(plan_items), n_items, _p(dXLp), dXLp.stride(0), _p(dRes), _p(dP),
-                                          _p(dXR), dXR.stride(0), _p(part_dxr), _p(part), part.stride(0), _p(P0),
-                                          _p(Wp0), _p(Wsk0), _p(ln0), eps0, scale0, _p(dSv0), _p(part_dsv0), _p(aux0),
-                                          _p(dxl_pos), _stream(P))
-        check(st, "gasfm_edge_cam_pbwd_e0")
-        return
-    if XLc is not None and epi is not None and ldWpo:  # the kernel keeps XLc only with EPI and DWP
-        _req(XLc, "XLc", 32)
-        st = lib().gasfm_edge_cam_pbwd_xlc(_p(P), _p(ln_w), _p(ln_b), eps, _p(Wpt), _p(Wc), _p(bc), _p(Wp),
-                                           Wp.stride(0) if Wp is not None else 0, scale, _p(XR), ldXR, _p(att),
-                                           _p(bias), slope, _p(out), out.stride(0), _p(seg_max), _p(seg_sum), ldStat,
-                                           _p(gout), gout.stride(0), _p(plan_items), n_items, _p(dXLp),
-                                           dXLp.stride(0), _p(dRes), _p(dP), _p(dXR), dXR.stride(0), _p(part_dxr),
-                                           _p(part), part.stride(0), _p(We), ldWe, scale_e, _p(dSv), _p(part_dsv),
-                                           _p(dP0), _p(P0), ldWpo, _p(dxl_pos), _p(XLc), _stream(P))
-        check(st, "gasfm_edge_cam_pbwd_xlc")
-        return
     st = lib().gasfm_edge_cam_pbwd_ex(_p(P), _p(ln_w), _p(ln_b), eps, _p(Wpt), _p(Wc), _p(bc), _p(Wp),
                                       Wp.stride(0) if Wp is not None else 0, scale, _p(XR), ldXR, _p(att), _p(bias),
                                       slope, _p(out), out.stride(0), _p(seg_max), _p(seg_sum), ldStat, _p(gout),
                                       gout.stride(0), _p(plan_items), n_items, _p(dXLp), dXLp.stride(0), _p(dRes),
                                       _p(dP), _p(dXR), dXR.stride(0), _p(part_dxr), _p(part), part.stride(0), _p(We),
-                                      ldWe, scale_e, _p(dSv), _p(part_dsv), _p(dP0), _p(P0), ldWpo, _p(dxl_pos),
-                                      _stream(P))
+                                      ldWe, scale_e, _p(dSv), _p(part_dsv), _p(dP0), _p(P0), ldWpo, _stream(P))
     check(st, "gasfm_edge_cam_pbwd")
 
 

@@ -61,8 +61,9 @@ GLOBAL_ATTN = os.environ.get("GASFM_GLOBAL_ATTN", "1") != "0"
 GATT_MAX_SRC = int(os.environ.get("GASFM_GATT_MAX_SRC", str(1 << 62)))
 
 
-def gatt_ok(plan, heads, XL, XR, att):
-    """Whether the fused global-conv kernels take this single-target conv (H = 4, C in {16, 256})."""
+def gatt_ok(plan, heads, XL, XR, att, bias=None):
+    """Whether the fused global-conv kernels take this single-target conv (H = 4, C in {16, 256}).
+    Inputs the kernels cannot read (dtype, alignment) take the plan kernels instead."""
     HC = att.numel()
     if not GLOBAL_ATTN or plan.num_targets != 1 or heads != 4 or HC not in (64, 1024):
         return False
@@ -71,6 +72,13 @@ def gatt_ok(plan, heads, XL, XR, att):
     if XL.dim() != 2 or XL.shape[1] != HC or XL.stride(1) != 1 or XL.stride(0) % 4 or XL.data_ptr() % 16:
         return False
     if XL.shape[0] < plan.src_rows or (plan.perm is not None and plan.perm.dtype != torch.int32):
+        return False
+    if any(t.dtype != torch.float32 for t in (XL, XR, att)):
+        return False
+    # att / bias are read as float4 columns (global_attn.hip): 16-byte aligned, unit stride
+    if not att.is_contiguous() or att.data_ptr() % 16:
+        return False
+    if bias is not None and (bias.dtype != torch.float32 or not bias.is_contiguous() or bias.data_ptr() % 16):
         return False
     return XR.numel() == HC and XR.is_contiguous() and XR.data_ptr() % 16 == 0
 
@@ -387,12 +395,10 @@ def combine_partials(gathered, world, N, heads, bias, combine_items):
 
 
 def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, gout, dXL=None, xl_sorted=False,
-                      defer=False, dXR=None, dxl_sorted=False):
+                      defer=False, dXR=None):
     """Launch the backward kernels; returns (dXL, dXR, datt[HC], dbias[HC]).
 
-    dXL is in source-row (edge) order; xl_sorted says XL itself is in segment order.  dxl_sorted
-    (with xl_sorted, round 4): dXL in segment order too, the layout of XL (row j = source row
-    plan.perm[j]): written streaming instead of scattered through perm.
+    dXL is in source-row (edge) order; xl_sorted says XL itself is in segment order.
     dXR: optional [num_targets, HC] row view (unit column stride) to write the target-row
     gradient into."""
     HC = att.numel()
@@ -410,8 +416,7 @@ def attn_backward_raw(XL, XR, att, bias, plan, heads, slope, out, smax, ssum, go
     datt_part = torch.empty((max(n_waves, 1), 2 * HC), dtype=torch.float32, device=dev)
     attf = att.reshape(-1).contiguous()
     if plan.n_items:
-        perm = None if (dxl_sorted and xl_sorted) else plan.perm
-        _native.attn_bwd(XL, XR, attf, bias, perm, plan.items, plan.n_items, heads, C, slope, out, smax,
+        _native.attn_bwd(XL, XR, attf, bias, plan.perm, plan.items, plan.n_items, heads, C, slope, out, smax,
                          ssum, gout, dXL, dXR, part, datt_part, xl_by_position=xl_sorted,
                          lanes=BWD_LANES and _lanes(plan, heads, HC))
         bwd_combine(plan, part, HC, dXR)
@@ -428,15 +433,12 @@ class GatAttentionFn(torch.autograd.Function):
     """out[i] = sum_{j->i} softmax_j(att . leaky_relu(XL[j] + XR[i])) XL[j] + bias."""
 
     @staticmethod
-    def forward(ctx, XL, XR, att, bias, plan, heads, slope, xl_sorted=False, sec=None, dxl_sorted=False):
+    def forward(ctx, XL, XR, att, bias, plan, heads, slope, xl_sorted=False):
         """xl_sorted: XL rows in segment order (written through plan.pos); the XL gradient is
-        returned in source-row (edge) order, or with dxl_sorted in XL's own (segment) order, for a
-        producer whose backward reads it through plan.pos (edge_cam_pbwd's dxl_pos).
-        sec: streams.SideSection joined before backward."""
+        returned in source-row (edge) order."""
         out, smax, ssum = attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True, xl_sorted=xl_sorted)
         ctx.plan, ctx.heads, ctx.slope = plan, heads, slope
-        ctx.xl_sorted, ctx.sec = xl_sorted, sec
-        ctx.dxl_sorted = bool(dxl_sorted) and bool(xl_sorted)
+        ctx.xl_sorted = xl_sorted
         ctx.defer = _native.defer_token(att, bias)
         ctx.save_for_backward(XL, XR, att, bias, out, smax, ssum)
         ctx.mark_non_differentiable(smax, ssum)
@@ -447,13 +449,10 @@ class GatAttentionFn(torch.autograd.Function):
     def backward(ctx, gout, _gm, _gs):
         XL, XR, att, bias, out, smax, ssum = ctx.saved_tensors
         if gout is None:
-            return None, None, None, None, None, None, None, None, None, None
-        if ctx.sec is not None:
-            ctx.sec.join()
+            return None, None, None, None, None, None, None, None
         dXL, dXR, datt, dbias = attn_backward_raw(XL, XR, att, bias, ctx.plan, ctx.heads, ctx.slope, out, smax,
-                                                  ssum, gout, xl_sorted=ctx.xl_sorted, defer=ctx.defer,
-                                                  dxl_sorted=ctx.dxl_sorted)
-        return dXL, dXR, datt.view_as(att), dbias, None, None, None, None, None, None
+                                                  ssum, gout, xl_sorted=ctx.xl_sorted, defer=ctx.defer)
+        return dXL, dXR, datt.view_as(att), dbias, None, None, None, None
 
 
 class GlobalPairFn(torch.autograd.Function):
@@ -464,7 +463,7 @@ class GlobalPairFn(torch.autograd.Function):
     def forward(ctx, XLv, XRv, att_v, bias_v, XLp, XRp, att_p, bias_p, plan_v, plan_p, heads, slope):
         HCv, HCp = att_v.numel(), att_p.numel()
         x = torch.empty((1, HCv + HCp), dtype=torch.float32, device=XLv.device)
-        ctx.fused = gatt_ok(plan_v, heads, XLv, XRv, att_v) and gatt_ok(plan_p, heads, XLp, XRp, att_p)
+        ctx.fused = gatt_ok(plan_v, heads, XLv, XRv, att_v, bias_v) and gatt_ok(plan_p, heads, XLp, XRp, att_p, bias_p)
         if ctx.fused:
             st = torch.empty((4, heads), dtype=torch.float32, device=XLv.device)
             mv, sv, mp, sp = st[0:1], st[1:2], st[2:3], st[3:4]

@@ -28,9 +28,6 @@ struct Tuning {
     v[GASFM_TUNE_ATTN_GRP_MIN_FILL] = env("GASFM_ATTN_GRP_MIN_FILL", 0.5);
     v[GASFM_TUNE_ATTN_GLDS] = env("GASFM_ATTN_GLDS", 1);
     v[GASFM_TUNE_ATTN_WAVE_CAP] = env("GASFM_ATTN_WAVES", 0);
-    v[GASFM_TUNE_ATTN_GRP_BWD] = env("GASFM_ATTN_GRP_BWD", 0);
-    v[GASFM_TUNE_SEAM_LDS] = env("GASFM_SEAM_LDS", 0);
-    v[GASFM_TUNE_ROWSUM_GRP] = env("GASFM_ROWSUM_GRP", 0);
   }
 };
 

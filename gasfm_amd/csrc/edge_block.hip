@@ -822,63 +822,6 @@ __global__ __launch_bounds__(kThreads) void segment_rowsum_kernel(const gasfm_wo
   }
 }
 
-// segment_rowsum, grouped (round 4, tuning option rowsum_grp / GASFM_ROWSUM_GRP): a wave task is
-// 8 consecutive items (point segments of ~20 edges), one per group of 8 lanes; lane (j, k) adds
-// features 4 k .. 4 k + 3 of item j's rows one edge per step, so the item's sum needs no cross-lane
-// reduction and no lanes idle past a short segment's last 8-row chunk.  Per step of 4 edges the
-// perm entries are loaded first, then the 4 gathered rows (clamped to the item's last edge and
-// masked at the add: no load under a branch); the next step's perm entries are requested before
-// this step's rows are summed.  Summation order: edge order within an item (deterministic).
-__global__ __launch_bounds__(kThreads) void segment_rowsum_grp_kernel(const gasfm_work_item* __restrict__ items,
-                                                                     int n_items, const int32_t* __restrict__ perm,
-                                                                     const float* __restrict__ X, int64_t ldX,
-                                                                     float scale, float* __restrict__ out,
-                                                                     float* __restrict__ part) {
-  constexpr int U = 4;
-  const int lane = threadIdx.x & (kW - 1);
-  const int j = lane >> 3, k4 = (lane & 7) * 4;
-  const int n_tasks = (n_items + 7) / 8;
-  const int nw = gridDim.x * kWaves;
-  for (int t = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + threadIdx.x / kW); t < n_tasks; t += nw) {
-    const int it = 8 * t + j;
-    const bool live = it < n_items;
-    const gasfm_work_item w = items[live ? it : n_items - 1];
-    const int b = w.begin, len = live ? w.end - w.begin : 0;
-    const int last = len > 0 ? w.end - 1 : 0;  // clamp target (a valid edge index)
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    int src[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {  // (an empty item reads nothing: E may be 0)
-      const int e = b + u < last ? b + u : last;
-      src[u] = (perm && len > 0) ? perm[e] : e;
-    }
-    for (int s0 = 0; s0 < len; s0 += U) {
-      float4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const float4*>(X + int64_t(src[u]) * ldX + k4);
-      const int n_ok = len - s0;  // edges s0 .. s0 + U - 1 of which n_ok (if < U) are live
-#pragma unroll
-      for (int u = 0; u < U; ++u) {  // the next step's perm entries before this step's adds
-        const int e = b + s0 + U + u < last ? b + s0 + U + u : last;
-        src[u] = perm ? perm[e] : e;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const float m = u < n_ok ? 1.f : 0.f;
-        acc.x = fmaf(v[u].x, m, acc.x);
-        acc.y = fmaf(v[u].y, m, acc.y);
-        acc.z = fmaf(v[u].z, m, acc.z);
-        acc.w = fmaf(v[u].w, m, acc.w);
-      }
-    }
-    if (live) {
-      const float4 r = make_float4(acc.x * scale, acc.y * scale, acc.z * scale, acc.w * scale);
-      float* dst = (w.slot < 0) ? out + int64_t(w.seg) * F : part + int64_t(w.slot) * F;
-      *reinterpret_cast<float4*>(dst + k4) = r;
-    }
-  }
-}
-
 // Grids: at most the workgroups resident at once (a grid-stride loop covers the rest); the
 // backward partial buffers have one row per workgroup, so their size follows the same grid.
 int64_t tiles_of(int64_t E) { return (E + TR - 1) / TR; }
@@ -994,14 +937,6 @@ extern "C" int gasfm_segment_rowsum(const gasfm_work_item* items, int32_t n_item
   GASFM_REQUIRE(aligned16(X) && ldX % 4 == 0 && aligned16(out), "gasfm_segment_rowsum: alignment");
   if (n_items <= 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (tune(GASFM_TUNE_ROWSUM_GRP) != 0) {
-    note_dispatch(GASFM_K_ROWSUM_GRP);
-    const int g = resident_grid(reinterpret_cast<const void*>(&segment_rowsum_grp_kernel), kThreads, 0,
-                                (int64_t(n_items) + 7) / 8, kWaves);
-    hipLaunchKernelGGL(segment_rowsum_grp_kernel, dim3(g), dim3(kThreads), 0, st, items, n_items, perm, X, ldX, scale,
-                       out, part);
-    return launch_status("gasfm_segment_rowsum");
-  }
   const int g = resident_grid(reinterpret_cast<const void*>(&segment_rowsum_kernel), kThreads, 0, n_items, kWaves);
   hipLaunchKernelGGL(segment_rowsum_kernel, dim3(g), dim3(kThreads), 0, st, items,
                      n_items, perm, X, ldX, scale, out, part);

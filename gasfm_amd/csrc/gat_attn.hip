@@ -949,149 +949,6 @@ __global__ __launch_bounds__(kBlock, GASFM_GLDS_BWD_MINWAVES) void attn_bwd_glds
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// backward, grouped items (round 4; Geom<32,8>, XL streamed in segment order): the layout of
-// attn_fwd_grp_kernel -- a wave task is 8 consecutive work items, lane group g (8 lanes = one
-// 128-B row) owns item g and walks its edges U rows per iteration, the next iteration's rows (and
-// their dXL destinations) requested before this one's are used.  Per edge: alpha from the saved
-// statistics, dXL row stored (through perm: edge order; perm == NULL: segment order), dz summed
-// into the item's dXR in the group's lanes (no cross-row reduction per item), datt / dbias per
-// wave.  The d bias of a segment is added once, at its first item.  Same per-wave partial rows as
-// the other backward kernels (grid = bwd_grid).
-// ------------------------------------------------------------------------------------------
-template <int U, int MINW>
-__global__ __launch_bounds__(kBlock, MINW) void attn_bwd_grp_kernel(
-    const float* __restrict__ XL, int64_t ldXL, const float* __restrict__ XR, int64_t ldXR,
-    const float* __restrict__ att, const float* __restrict__ bias, const int32_t* __restrict__ perm,
-    const gasfm_work_item* __restrict__ items, int n_items, float slope, const float* __restrict__ out,
-    int64_t ldOut, const float* __restrict__ seg_max, const float* __restrict__ seg_sum,
-    const float* __restrict__ gout, int64_t ldG, float* __restrict__ dXL, int64_t ldDXL,
-    float* __restrict__ dXR, int64_t ldDXR, float* __restrict__ part_dxr, float* __restrict__ datt_part) {
-  constexpr int HC = 32, H = 4, C = 8, GR = 8;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int g = lane >> 3, li = lane & 7, f0 = li * 4, h = f0 / C;
-  const int wave = wave_id_uniform();
-  const int nwaves = gridDim.x * (blockDim.x / kWave);
-  const int ntasks = (n_items + GR - 1) / GR;
-  float attv[4], bv[4], datt[4] = {0.f, 0.f, 0.f, 0.f}, dbias[4] = {0.f, 0.f, 0.f, 0.f};
-  load_vec<4>(attv, att + f0);
-  load_vec<4>(bv, bias + f0);
-  auto item_of = [&](int t) {
-    const int i = t * GR + g;
-    gasfm_work_item w{-1, 0, 0, -1};
-    if (t < ntasks && i < n_items) w = items[i];
-    return w;
-  };
-  auto wave_max_len = [&](const gasfm_work_item& w) {
-    int l = w.seg >= 0 ? w.end - w.begin : 0;
-    l = max(l, __shfl_xor(l, 8));
-    l = max(l, __shfl_xor(l, 16));
-    l = max(l, __shfl_xor(l, 32));
-    return __builtin_amdgcn_readfirstlane(l);
-  };
-  // rows k .. k + U - 1 of item w (clamped to its first row; an empty item reads row 0)
-  auto issue = [&](const gasfm_work_item& w, int k, float (&x)[U][4], int64_t (&d)[U]) {
-    const int64_t base = w.begin < w.end ? w.begin : 0;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t r = int64_t(w.begin) + k + u;
-      const int64_t rc = r < w.end ? r : base;
-      d[u] = perm ? int64_t(perm[rc]) : rc;
-      load_vec<4>(x[u], XL + rc * ldXL + f0);
-    }
-  };
-  int t = wave;
-  gasfm_work_item w = item_of(t);
-  int L = t < ntasks ? wave_max_len(w) : 0;
-  float nx[U][4];
-  int64_t nd[U];
-  if (L > 0) issue(w, 0, nx, nd);
-  for (; t < ntasks; t += nwaves) {
-    const gasfm_work_item wn = item_of(t + nwaves);  // started at this task's last iteration
-    int Ln = 0;
-    const int len = w.seg >= 0 ? w.end - w.begin : 0;
-    // the item's segment data (all lanes of the group; an empty group reads row 0, unused)
-    const int64_t sg = w.seg >= 0 ? w.seg : 0;
-    float xr[4], go[4], o[4];
-    load_vec<4>(xr, XR + sg * ldXR + f0);
-    load_vec<4>(go, gout + sg * ldG + f0);
-    load_vec<4>(o, out + sg * ldOut + f0);
-    const float M = seg_max[sg * H + h], inv = 1.f / (seg_sum[sg * H + h] + 1e-16f);
-    float dl = 0.f;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) dl = fmaf(go[v], o[v] - bv[v], dl);
-    const float delta = dl + xor_lane<1>(dl);  // the 2 lanes of a head
-    const int i = t * GR + g;
-    const bool first = w.seg >= 0 && (i == 0 || items[i - 1].seg != w.seg);
-    if (first) {
-#pragma unroll
-      for (int v = 0; v < 4; ++v) dbias[v] += go[v];
-    }
-    float dxr[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < L; k += U) {
-      float xl[U][4];
-      int64_t dst[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        dst[u] = nd[u];
-#pragma unroll
-        for (int v = 0; v < 4; ++v) xl[u][v] = nx[u][v];
-      }
-      if (k + U < L) {
-        issue(w, k + U, nx, nd);
-      } else {  // last iteration of this task: start the next one
-        Ln = wave_max_len(wn);
-        if (Ln > 0) issue(wn, 0, nx, nd);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        float z[4], p = 0.f, da = 0.f;
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          z[v] = xl[u][v] + xr[v];
-          p = fmaf(leaky(z[v], slope), attv[v], p);
-          da = fmaf(go[v], xl[u][v], da);
-        }
-        p += xor_lane<1>(p);
-        da += xor_lane<1>(da);
-        const bool valid = k + u < len;
-        const float alpha = valid ? __expf(p - M) * inv : 0.f;
-        const float de = alpha * (da - delta);
-        float dx[4];
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const float dz = de * attv[v] * (z[v] > 0.f ? 1.f : slope);
-          dx[v] = fmaf(alpha, go[v], dz);
-          dxr[v] += dz;
-          datt[v] = fmaf(de, leaky(z[v], slope), datt[v]);
-        }
-        if (valid) store_vec<4>(dXL + dst[u] * ldDXL + f0, dx);
-      }
-    }
-    if (L == 0) {  // every item of the task empty: the next task was not started above
-      Ln = t + nwaves < ntasks ? wave_max_len(wn) : 0;
-      if (Ln > 0) issue(wn, 0, nx, nd);
-    }
-    if (w.seg >= 0) {
-      if (w.slot < 0)
-        store_vec<4>(dXR + int64_t(w.seg) * ldDXR + f0, dxr);
-      else
-        store_vec<4>(part_dxr + int64_t(w.slot) * HC + f0, dxr);
-    }
-    w = wn;
-    L = Ln;
-  }
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    datt[v] = xor_sum_from<8>(datt[v]);
-    dbias[v] = xor_sum_from<8>(dbias[v]);
-  }
-  if (g == 0) {
-    store_vec<4>(datt_part + int64_t(wave) * 2 * HC + f0, datt);
-    store_vec<4>(datt_part + int64_t(wave) * 2 * HC + HC + f0, dbias);
-  }
-}
-
 // dXR[seg] = ordered sum of its partial slots.
 // grid = (combine entries, column blocks of CB = min(HC, 64)): R = kBlock / CB row groups take
 // slots k = grp, grp + R, ... and are added in group order (deterministic for a given HC).
@@ -1477,13 +1334,6 @@ extern "C" int gasfm_gat_attn_bwd(const float* XL, int64_t ldXL, const float* XR
                       aligned16(gout) && aligned16(dXL) && aligned16(dXR) && aligned16(att) &&
                       aligned16(bias) && aligned16(datt_part) && (!part_dxr || aligned16(part_dxr));
   bool done = false;
-  if (vec_ok && H * C == 32 && C == 8 && (perm == nullptr || xl_by_position) && tune(GASFM_TUNE_ATTN_GRP_BWD) != 0) {
-    note_dispatch(GASFM_K_ATTN_BWD_GRP);
-    hipLaunchKernelGGL((attn_bwd_grp_kernel<4, 1>), dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att, bias,
-                       perm, items, n_items, slope, out, ldOut, seg_max, seg_sum, gout, ldG, dXL, ldDXL, dXR, ldDXR,
-                       part_dxr, datt_part);
-    done = true;
-  }
   if (!done && vec_ok && H * C == 32 && C == 8 && (perm == nullptr || xl_by_position) && glds_enabled() &&
       aligned16(seg_max) && aligned16(seg_sum)) {
     note_dispatch(GASFM_K_ATTN_BWD_GLDS);

@@ -385,7 +385,7 @@ class ShardedGlobalAttentionFn(torch.autograd.Function):
         # per rank, so that in the gathered [W*B] buffer rank r's rows are slots r*B/Lv (v) and
         # (r*B + ov)/Lp (p) of row width Lv / Lp: the combines read them in place
         pack = torch.empty(B, **f32)
-        ctx.fused = gatt_ok(plan_v, heads, XLv, XRv, att_v) and gatt_ok(plan_p, heads, XLp, XRp, att_p)
+        ctx.fused = gatt_ok(plan_v, heads, XLv, XRv, att_v, bias_v) and gatt_ok(plan_p, heads, XLp, XRp, att_p, bias_p)
         if ctx.fused:  # both partial rows from one launch (global_attn.hip)
             _native.gatt_fwd([gatt_prob(plan_v, XLv, XRv, att_v, bias_v, part=pack[:Lv]),
                               gatt_prob(plan_p, XLp, XRp, att_p, bias_p, part=pack[ov:ov + Lp])], slope)
@@ -465,17 +465,23 @@ def partition_points(pt, n, world):
     return np.maximum.accumulate(np.asarray(bounds))
 
 
-def shard_scene(scene, rank, world, max_piece=None, cameras=False, emulate=False):
+def shard_scene(scene, rank, world, max_piece=None, cameras=False, emulate=False, point_bounds=None):
     """Rank-local SceneData of a synthetic (or any cam-major) scene.
 
     scene: object with m, n, cam, pt (cam-major sorted) and normalized_values().
     cameras: shard the camera (view) rows too (module docstring).  emulate: a ShardContext
-    without a process group (see ShardContext).
+    without a process group (see ShardContext).  point_bounds: explicit contiguous point ranges
+    [world + 1] (default: partition_points' edge-balanced split).
     """
     cam = np.asarray(scene.cam)
     pt = np.asarray(scene.pt)
     m, n = scene.m, scene.n
-    bounds = partition_points(pt, n, world)
+    if point_bounds is None:
+        bounds = partition_points(pt, n, world)
+    else:
+        bounds = np.asarray(point_bounds, dtype=np.int64)
+        if bounds.shape != (world + 1,) or bounds[0] != 0 or bounds[-1] != n or np.any(np.diff(bounds) < 0):
+            raise ValueError(f"point_bounds must be {world + 1} non-decreasing boundaries from 0 to {n}")
     p0, p1 = int(bounds[rank]), int(bounds[rank + 1])
     sel = (pt >= p0) & (pt < p1)
     vals = scene.normalized_values()[sel]

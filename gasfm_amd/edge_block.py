@@ -35,28 +35,9 @@ CAM_PBWD = os.environ.get("GASFM_CAM_PBWD", "1") != "0"
 # gradient in block b's own edge_cam_pbwd (it holds dRes = dP' and relu(LN_b(P_b))), dSv / dP0 in
 # block b+1's (the kernel that produces dP').  0: edge_epilogue_bwd as before.
 EPI_FOLD = os.environ.get("GASFM_EPI_FOLD", "1") != "0"
-# round 4: the point half of XL's gradient in point-segment order (the layout of XLp itself): the
-# point attention's backward writes it streaming (no perm scatter) and edge_cam_pbwd reads edge e's
-# row at pos[e] (GatAttentionFn(dxl_sorted) + the camera Functions' dxl_pos).  0: edge order.
-DXL_PT = os.environ.get("GASFM_DXL_PT", "0") != "0"
-
-
-def dxl_pos_of(pos):
-    """The dxl_pos the camera Functions' backward gets for a forward with XLp written through pos
-    (None: dXLp arrives in edge order)."""
-    return pos if (DXL_PT and pos is not None) else None
-
-# round 4: block 0's 2-wide epilogue backward folded into block 1's edge_cam_pbwd the same way
-# (gasfm_edge_cam_pbwd_e0: dSv, aux and the block-0 weight sums from the dP' that launch produces,
-# block 0's input read as the launch's DWP P0 rows).  Off by default: measured on MI355X
-# (tools/gpu_r4_e0fold.sh, profiles/r4_e0fold.txt) the folded launch takes 883 us against 726 for
-# block 1's unfolded one, more than the 137 us edge0_epilogue_bwd it replaces (config 4 29.32-29.33
-# vs 29.28-29.42 ms): the four dots, the 2-wide LayerNorm backward and the weight sums add VALU and
-# LDS work to an issue-bound kernel and raise its spills (14 -> 30 VGPRs).  1: the fold.
-E0_FOLD = os.environ.get("GASFM_E0_FOLD", "0") != "0"
-# round 4 experiment: the forward seam keeps block b+1's camera-half XLc ([E, 32], edge order) and
-# that block's edge_cam_pbwd reads it instead of recomputing it from P (VERDICT r3 #4).  0: recompute.
-XLC_STORE = os.environ.get("GASFM_XLC_STORE", "0") != "0"
+# Measured and removed in round 5 (kept in git history): dXLp in point-segment order
+# (GASFM_DXL_PT), block 0's epilogue backward folded into block 1's edge_cam_pbwd (GASFM_E0_FOLD),
+# XLc kept by the forward seam instead of recomputed (GASFM_XLC_STORE).
 
 # Block 0's prologue writes XL0 row by row through the point plan's permutation (one 32-B store
 # per row, gasfm_edge0_prologue_fwd_rows) instead of scattering the point halves through pos.
@@ -181,7 +162,6 @@ class EdgeCamFn(torch.autograd.Function):
         ctx.att_shape = att.shape
         ctx.has_ln = ln_w is not None
         ctx.dwp = bool(dwp)
-        ctx.dxl_pos = dxl_pos_of(pos)
         ctx.defer = _native.defer_token(ln_w, ln_b, Wpt, bpt, Wc, bc, att, bias, Wp if dwp else None)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum, P0)
@@ -203,42 +183,34 @@ def _dwp_torch(P, ln_w, ln_b, eps, dRes, P0):
     return PROJ_SCALE * (dRes.t() @ ph)
 
 
-def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None, epi0=None, xlc=None):
+def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None):
     """EdgeCamFn's backward from its saved state (ctx attributes eps, heads, slope, plan, att_shape,
     has_ln, dwp, defer): the 20 input gradients of EdgeCamFn.forward.  epi: the previous block's
     epilogue outputs to fill from dP (edge_cam_pbwd's EPI), or None; ctx.epi_done tells whether
-    they were filled.  epi0: the same for block 0's epilogue (edge_cam_pbwd's epi0, block 1 only);
-    when filled, ctx.epi0_part holds the block-0 weight partial rows (a column slice of part)."""
+    they were filled."""
     P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum, P0 = saved
     plan = ctx.plan
     E, dev = P.shape[0], P.device
-    dxl_pos = getattr(ctx, "dxl_pos", None) if dXLp is not None else None  # dXLp in point order (DXL_PT)
     dXLp = torch.zeros((E, 32), dtype=torch.float32, device=dev) if dXLp is None else dXLp.contiguous()
     g_c = torch.zeros_like(out) if g_c is None else (g_c if g_c.stride(1) == 1 else g_c.contiguous())
     dwp = ctx.dwp and dRes is not None and ln_w is not None
     ctx.epi_done = False
-    ctx.epi0_part = None
     dWp = None
     if CAM_PBWD and plan.n_items:
         # camera attention backward + prologue backward in one kernel (gasfm_edge_cam_pbwd)
         dXR = torch.empty((plan.num_targets, 32), dtype=torch.float32, device=dev)
         part_dxr = torch.empty((plan.n_part_rows, 32), dtype=torch.float32, device=dev) if plan.n_slots else None
         wcols = (34 if P0 is not None else 32) if dwp else 0
-        use_e0 = epi0 is not None and dwp and P0 is not None
-        rows, cols = _native.edge_cam_pbwd_part_shape(plan.n_items, wcols, e0=use_e0)
+        rows, cols = _native.edge_cam_pbwd_part_shape(plan.n_items, wcols)
         part = torch.empty((rows, cols), dtype=torch.float32, device=dev)
         dP = torch.empty_like(P)
-        use_epi = epi is not None and (ln_w is None) == (dRes is None) and not use_e0
+        use_epi = epi is not None and (ln_w is None) == (dRes is None)
         _native.edge_cam_pbwd(P, ln_w, ln_b, ctx.eps, Wpt.contiguous(), Wc.contiguous(), bc.contiguous(),
                               Wp.contiguous() if dRes is not None else None, PROJ_SCALE, XR, attf, bias, ctx.slope,
                               out, smax, ssum, g_c, plan.items, plan.n_items, dXLp, dRes, dP, dXR, part_dxr, part,
                               epi=epi if use_epi else None,
-                              dwp=(P0 if P0 is not None else True) if dwp else None, dxl_pos=dxl_pos,
-                              epi0=epi0 if use_e0 else None, XLc=xlc if (use_epi and dwp) else None)
+                              dwp=(P0 if P0 is not None else True) if dwp else None)
         ctx.epi_done = use_epi
-        if use_e0:
-            off = _native.edge_cam_pbwd_e0_offset(wcols)
-            ctx.epi0_part = part[:, off:off + 164]
         bwd_combine(plan, part_dxr, 32, dXR)
         tot = _native.param_colsum(part, ctx.defer)
         o = 64 * 32
@@ -246,8 +218,6 @@ def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None, epi0=None, xlc=None):
         if dwp:
             dWp = tot[o + 192:o + 192 + 32 * wcols].view(32, wcols)
     else:
-        if dxl_pos is not None:  # the separate kernels take dXLp in edge order
-            dXLp = dXLp.index_select(0, dxl_pos.long())
         # camera attention backward (XLc recomputed from P): dXLc, dXR, [datt | dbias] partials
         dXLc = torch.empty((E, 32), dtype=torch.float32, device=dev)
         dXR = torch.empty((plan.num_targets, 32), dtype=torch.float32, device=dev)
@@ -290,7 +260,7 @@ class DualAttentionFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, XL, XR_pt, XR_cam, att_pt, att_cam, bias_pt, bias_cam, plan_pt, plan_cam, heads, slope,
-                plan_cam_partial=None, shard=None, xl_sorted=False, sec=None):
+                plan_cam_partial=None, shard=None, xl_sorted=False):
         h = XL.shape[1] // 2
         XLp, XLc = XL[:, :h], XL[:, h:]
         out_p, mp, sp = attn_forward_raw(XLp, XR_pt, att_pt, bias_pt, plan_pt, heads, slope, xl_sorted=xl_sorted)
@@ -304,7 +274,6 @@ class DualAttentionFn(torch.autograd.Function):
                                              shard.combine_items(N, XL.device))
         ctx.plans = (plan_pt, plan_cam)
         ctx.heads, ctx.slope, ctx.xl_sorted = heads, slope, xl_sorted
-        ctx.sec = sec  # streams.SideSection of this block: joined before the point-side gradient is read
         ctx.defer = _native.defer_token(att_pt, att_cam, bias_pt, bias_cam)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(XL, XR_pt, XR_cam, att_pt, att_cam, bias_pt, bias_cam, out_p, mp, sp, out_c, mc, sc)
@@ -314,8 +283,6 @@ class DualAttentionFn(torch.autograd.Function):
     def backward(ctx, g_p, g_c):
         XL, XR_pt, XR_cam, att_pt, att_cam, bias_pt, bias_cam, out_p, mp, sp, out_c, mc, sc = ctx.saved_tensors
         plan_pt, plan_cam = ctx.plans
-        if ctx.sec is not None:
-            ctx.sec.join()
         h = XL.shape[1] // 2
         if g_p is None:
             g_p = torch.zeros_like(out_p)
@@ -328,7 +295,7 @@ class DualAttentionFn(torch.autograd.Function):
         _, dXRc, dattc, dbc = attn_backward_raw(XL[:, h:], XR_cam, att_cam, bias_cam, plan_cam, ctx.heads, ctx.slope,
                                                 out_c, mc, sc, g_c, dXL=dXL[:, h:], defer=ctx.defer)
         return (dXL, dXRp, dXRc, dattp.view_as(att_pt), dattc.view_as(att_cam), dbp, dbc, None, None, None, None,
-                None, None, None, None)
+                None, None, None)
 
 
 class EdgeEpilogueFn(torch.autograd.Function):
@@ -413,13 +380,11 @@ class SeamFn(torch.autograd.Function):
         Pn = torch.empty_like(P)
         Wp_c, Sp_c, Sv_r, Sg_f = Wp.contiguous(), Sp.contiguous(), _rows(Sv), Sg.reshape(-1).contiguous()
         bp_c = bp.contiguous()
-        xlc = (torch.empty((E, 32), dtype=torch.float32, device=dev)
-               if XLC_STORE and ln_w is not None and dwp_n else None)
 
         def launch(items, n_items, finalize, out, smax, ssum, part):
             _native.edge_seam_fwd(P, P0, edges.pt, lnw_b, lnb_b, eps_b, Wp_c, bp_c, Sp_c, Sv_r, Sg_f, PROJ_SCALE, Pn,
                                   ln_w, ln_b, eps, Wpt, bpt, Wc, bc, XLp, pos, XR, attf, bias if finalize else None,
-                                  slope, items, n_items, finalize, out, smax, ssum, part, XLc=xlc)
+                                  slope, items, n_items, finalize, out, smax, ssum, part)
         out, smax, ssum = _cam_attention_fwd(launch, bias, plan, heads, HC, plan_partial, shard, dev)
         # EdgeEpilogueFn's state
         ctx.e_eps, ctx.edges, ctx.sg_shape = eps_b, edges, Sg.shape
@@ -430,13 +395,11 @@ class SeamFn(torch.autograd.Function):
         ctx.att_shape = att.shape
         ctx.has_ln = ln_w is not None
         ctx.dwp = bool(dwp_n)
-        ctx.dxl_pos = dxl_pos_of(pos)
         ctx.defer = _native.defer_token(ln_w, ln_b, Wpt, bpt, Wc, bc, att, bias, Wp_n if dwp_n else None)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(P, P0, Wp_c, lnw_b, lnb_b, Pn, ln_w, ln_b, Wpt, Wc, bc, Wp_n, XR, attf, bias, out, smax,
                               ssum, P0_n)
         ctx.n_epi = 5
-        ctx.xlc = xlc
         token_n = P.new_empty((1, 1)).expand(E, P.shape[1])
         return Pn, XLp, out, token_n
 
@@ -455,9 +418,7 @@ class SeamFn(torch.autograd.Function):
             part_dsv = torch.empty((max(ctx.plan.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
             dP0 = torch.empty((P_b.shape[0], 2), dtype=torch.float32, device=dev) if P0_b is not None else None
             folded = (dSv, part_dsv, dP0)
-        gc = _cam_backward(ctx, cam, dXLp, g_c, dRes,
-                           epi=None if folded is None else (Wp_b, PROJ_SCALE) + folded, xlc=ctx.xlc)
-        ctx.xlc = None
+        gc = _cam_backward(ctx, cam, dXLp, g_c, dRes, epi=None if folded is None else (Wp_b, PROJ_SCALE) + folded)
         if not ctx.epi_done:
             folded = None
         dPn = gc[0] if gPn is None else gc[0] + gPn
@@ -545,26 +506,22 @@ class Block0EpilogueFn(torch.autograd.Function):
         return _epilogue0_backward(ctx, ctx.saved_tensors, dPo)
 
 
-def _epilogue0_backward(ctx, saved, dPo, folded=None):
+def _epilogue0_backward(ctx, saved, dPo):
     """Block0EpilogueFn's backward from its saved state (ctx attributes eps, edges, sg_shape): its 15
-    input gradients.  folded: (dSv, part_dsv, aux, part rows) already filled by block 1's
-    edge_cam_pbwd (epi0), so edge0_epilogue_bwd does not run."""
+    input gradients."""
     P, lna_w, lna_b, lnb_w, lnb_b, Wp, Wsk = saved
     edges = ctx.edges
     dPo = dPo.contiguous()
     dev = P.device
     E = P.shape[0]
     pc, pp = edges.plans["proj2view"], edges.plans["proj2scenepoint"]
-    if folded is not None:
-        dSv, part_dsv, aux, part = folded
-    else:
-        dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
-        part_dsv = torch.empty((max(pc.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
-        aux = torch.empty((E, 4), dtype=torch.float32, device=dev)
-        rows = _native.edge0_part_rows(1, E, pc.n_items)
-        part = torch.empty((rows, 164), dtype=torch.float32, device=dev)
-        _native.edge0_epilogue_bwd(pc.items, pc.n_items, dPo, P, lna_w, lna_b, lnb_w, lnb_b, ctx.eps,
-                                   Wp.contiguous(), Wsk.contiguous(), PROJ_SCALE, dSv, part_dsv, aux, part)
+    dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
+    part_dsv = torch.empty((max(pc.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
+    aux = torch.empty((E, 4), dtype=torch.float32, device=dev)
+    rows = _native.edge0_part_rows(1, E, pc.n_items)
+    part = torch.empty((rows, 164), dtype=torch.float32, device=dev)
+    _native.edge0_epilogue_bwd(pc.items, pc.n_items, dPo, P, lna_w, lna_b, lnb_w, lnb_b, ctx.eps,
+                               Wp.contiguous(), Wsk.contiguous(), PROJ_SCALE, dSv, part_dsv, aux, part)
     bwd_combine(pc, part_dsv, 32, dSv)
     tot = _native.colsum(part)
     dSg = _native.colsum(dSv)
@@ -610,7 +567,6 @@ class Seam0Fn(torch.autograd.Function):
         ctx.att_shape = att.shape
         ctx.has_ln = True
         ctx.dwp = bool(dwp_n)
-        ctx.dxl_pos = dxl_pos_of(pos)
         ctx.defer = _native.defer_token(ln_w, ln_b, Wpt, bpt, Wc, bc, att, bias, Wp_n if dwp_n else None)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(Pc, lna_w, lna_b, lnb_w, lnb_b, Wp_c, Wsk_c, Pn, ln_w, ln_b, Wpt, Wc, bc, Wp_n, XR,
@@ -624,22 +580,7 @@ class Seam0Fn(torch.autograd.Function):
         epi, cam = saved[:7], saved[7:]
         dRes = dtoken.contiguous() if (dtoken is not None and dtoken.stride(0) != 0) else None
         edges = ctx.edges
-        P, lna_w, lna_b, lnb_w, lnb_b, Wp, Wsk = epi
-        P0_n = cam[-1]
-        epi0 = None
-        if (E0_FOLD and gPn is None and dRes is not None and ctx.dwp and ctx.plan is edges.plans["proj2view"]
-                and P0_n is not None and P0_n.data_ptr() == P.data_ptr() and P0_n.stride() == P.stride()
-                and P0_n.shape == P.shape and tuple(Wp.shape) == (32, 2) and tuple(Wsk.shape) == (32, 2)):
-            # block 0's epilogue backward from the dP' block 1's launch produces (its P0 rows are
-            # block 0's input: the same embedded projections)
-            dev = P.device
-            dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
-            part_dsv = torch.empty((max(ctx.plan.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
-            aux = torch.empty((P.shape[0], 4), dtype=torch.float32, device=dev)
-            ln0 = torch.cat([lna_w, lna_b, lnb_w, lnb_b]).contiguous()
-            epi0 = (Wp, Wsk, ln0, ctx.e_eps, PROJ_SCALE, dSv, part_dsv, aux)
-        gc = _cam_backward(ctx, cam, dXLp, g_c, dRes, epi0=epi0)
-        folded = None if ctx.epi0_part is None else (epi0[5], epi0[6], epi0[7], ctx.epi0_part)
+        gc = _cam_backward(ctx, cam, dXLp, g_c, dRes)
         dPn = gc[0] if gPn is None else gc[0] + gPn
         ectx = _EpiState(ctx.e_eps, edges, ctx.sg_shape, None)
-        return _epilogue0_backward(ectx, epi, dPn, folded) + gc[1:]
+        return _epilogue0_backward(ectx, epi, dPn) + gc[1:]

@@ -44,14 +44,38 @@ def retire_collectives():
     dist = torch.distributed
     if not (dist.is_available() and dist.is_initialized()):
         return
-    from torch.distributed import distributed_c10d as c10d
-    for pg in list(c10d._world.pg_map.keys()):
+    for pg in _process_groups():
         try:
             nccl = dist.get_backend(pg) == "nccl"
         except (RuntimeError, ValueError):
             nccl = False
         if nccl:
-            pg._wait_for_pending_works()
+            wait = getattr(pg, "_wait_for_pending_works", None)
+            if wait is None:
+                raise RuntimeError(
+                    f"torch {torch.__version__}: ProcessGroup._wait_for_pending_works is missing; without it "
+                    "a capture can race ProcessGroupNCCL's watchdog (graph_step.retire_collectives)")
+            wait()
+
+
+def _process_groups():
+    """Every process group torch.distributed has created (private c10d state: checked here, so a
+    torch upgrade that renames it fails loudly instead of skipping the retire step)."""
+    from torch.distributed import distributed_c10d as c10d
+    world = getattr(c10d, "_world", None)
+    pg_map = getattr(world, "pg_map", None)
+    if pg_map is None:
+        raise RuntimeError(f"torch {torch.__version__}: distributed_c10d._world.pg_map is missing "
+                           "(graph_step.retire_collectives needs the process-group list)")
+    return list(pg_map.keys())
+
+
+def private_api_ok():
+    """The private torch.distributed symbols retire_collectives relies on exist in this torch."""
+    from torch.distributed import distributed_c10d as c10d
+    pg_cls = getattr(torch._C._distributed_c10d, "ProcessGroup", None)
+    return (getattr(getattr(c10d, "_world", None), "pg_map", None) is not None and pg_cls is not None
+            and hasattr(pg_cls, "_wait_for_pending_works"))
 
 
 def _grad_mismatch(params, ref_grads, rtol):

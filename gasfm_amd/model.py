@@ -26,7 +26,7 @@ import torch
 import torch.nn.functional as F
 from torch.nn import Identity, LayerNorm, Linear, Module, ModuleList, ReLU, Sequential
 
-from . import _native, dense, edge_block, edge_ops, point_block, streams, view_block
+from . import _native, dense, edge_block, edge_ops, point_block, view_block
 from .attention import AttnPlan, GatAttentionFn, gat_attention
 from .edge_block import (Block0EpilogueFn, Block0PrologueFn, DualAttentionFn, EdgeCamFn, EdgeEpilogueFn,
                          EdgePrologueFn, PendingEpilogue, SeamFn, materialize)
@@ -168,12 +168,10 @@ class _NodeAggregation(Module):
             return conv.lin_r(zero).expand(num_targets, -1)
         return dense.linear(dense.sequential(getattr(self, self._state_key), prev), conv.lin_r)
 
-    def tail(self, x, prev, sec=None):
-        """Everything after the GATv2 aggregation: proj, state skip, LN+ReLU, MLP, skip.
-        sec: streams.SideSection the fused point tail runs in (None: torch's stream)."""
+    def tail(self, x, prev):
+        """Everything after the GATv2 aggregation: proj, state skip, LN+ReLU, MLP, skip."""
         if point_block.tail_fusable(self, x, prev):
-            return point_block.tail(self, x, prev, sec)
-        assert sec is None
+            return point_block.tail(self, x, prev)
         if view_block.tail_fusable(self, x, prev):
             return view_block.tail(self, x, prev)
         if self.n_feat_agg != self.n_feat_out:
@@ -427,7 +425,7 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
     def forward_fused(self, XL, plans, prev_pt=None, prev_view=None, prev_glob=None, xl_sorted=False, carry=None,
                       pfu=None, nxt=None, attend=None):
         """Node side of the update given XL = [lin_l_point(P_hat) | lin_l_camera(P_hat)] [E, 64]
-        (point half in point-segment order when xl_sorted), or attend(XRp, XRc, sec) -> (point
+        (point half in point-segment order when xl_sorted), or attend(XRp, XRc) -> (point
         aggregates, camera aggregates) (the fused prologue + camera attention, edge_cam_attend).
 
         carry: per-forward dict through which PointHubFn / ViewHubFn hand the next block its
@@ -457,24 +455,15 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         hubs = carry is not None and self.output_global and nxt is not None
         vsg = self.view_and_scenepoint2global if hubs else None
         hp = point_block.hub_params(pfu, vsg.graph_conv_scenepoint2global, nxt.proj2scenepoint) if hubs else None
-        # point tail + hub on a side stream, concurrent with the camera tail + hub (streams.py)
-        sec = None
-        if hp is not None and point_block.tail_fusable(sp, XRp.new_empty((0, cp.heads * cp.out_channels)), prev_pt):
-            sec = streams.section_for(XRp.device, _native.defer_token())
         if attend is not None:
-            agg_p, agg_c = attend(XRp, XRc, sec)
+            agg_p, agg_c = attend(XRp, XRc)
         else:
             agg_p, agg_c = DualAttentionFn.apply(XL, XRp, XRc, cp.att, cc.att, cp.bias, cc.bias, pp, pc, cp.heads,
                                                  cp.negative_slope, plans.get("_partial", {}).get("proj2view"), shard,
-                                                 xl_sorted, sec)
-        if sec is not None:
-            point_block.forward_buffers(sec, agg_p.shape[0], agg_p)
-            sec.fork()
+                                                 xl_sorted)
         if cams:  # this rank's camera rows only from here on (distributed.py, camera sharding)
             from .distributed import own_rows
             agg_c = own_rows(agg_c, shard)
-        # created in this order so that the backward runs the point hub (which forks the side
-        # stream) before the camera hub, and the point tail on the side stream after it
         view = sv.tail(agg_c, prev_view)
         if hubs:
             hv = view_block.hub_params(pfu, vsg.graph_conv_view2global, nxt.proj2view)
@@ -486,12 +475,10 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
                 carry.update(XRc=XRn, view_skip=skip, SV=SV, XLv2g=XLv)
             elif cams:
                 raise RuntimeError("camera-sharded execution needs the fused view hub shapes")
-        pts = sp.tail(agg_p, prev_pt, sec=sec)
+        pts = sp.tail(agg_p, prev_pt)
         if hp is not None and point_block._rows_ok(pts, point_block.P_W):
-            skip, SA, XLs, XRn = point_block.hub(pts, hp, sec)
+            skip, SA, XLs, XRn = point_block.hub(pts, hp)
             carry.update(XRp=XRn, pts_skip=skip, SA=SA, XLs2g=XLs)
-        if sec is not None:
-            sec.join()
         return self._finish(pts, view, plans, prev_glob, carry, pfu, nxt)
 
     def cam_fusable(self, plans):
@@ -511,7 +498,7 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
         cp, cc = self.proj2scenepoint.graph_conv, self.proj2view.graph_conv
         pos = pp.pos
 
-        def attend(XRp, XRc, sec):
+        def attend(XRp, XRc):
             cam_args = (ln_w, ln_b, W, b, W2, b2, Wp, eps, pos, XRc, cc.att, cc.bias, pc, cc.heads, cc.negative_slope,
                         plans.get("_partial", {}).get("proj2view"), plans.get("_shard"), P0, dwp)
             Pe = P
@@ -525,10 +512,8 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
                 XLp, agg_c, token = EdgeCamFn.apply(Pe, *cam_args)
                 holder["P"] = Pe
             holder["token"] = token
-            # dxl_sorted: XLp's gradient in XLp's own (point) order, read by the camera Function's
-            # backward through pos (edge_block.DXL_PT)
-            agg_p = GatAttentionFn.apply(XLp, XRp, cp.att, cp.bias, pp, cp.heads, cp.negative_slope, pos is not None,
-                                         sec, edge_block.dxl_pos_of(pos) is not None)[0]
+            agg_p = GatAttentionFn.apply(XLp, XRp, cp.att, cp.bias, pp, cp.heads, cp.negative_slope,
+                                         pos is not None)[0]
             return agg_p, agg_c
         return attend
 

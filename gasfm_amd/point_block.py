@@ -14,8 +14,6 @@ block).  Routing every consumer through PointHubFn makes its backward the only p
 dp: the C pass adds the next block's target-row gradient to the incoming skip gradient, the
 A+B pass adds lin_l and lin_scenepoint terms in place, and no add kernel runs.
 """
-import contextlib
-
 import torch
 
 from . import _native
@@ -30,20 +28,15 @@ def _f32(*shape, like):
 
 class PointTailFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, prev, agg, Wp, bp, ln_w, ln_b, Wm, bm, eps, sec=None):
-        ins = (prev, agg, Wp, Wm)
+    def forward(ctx, prev, agg, Wp, bp, ln_w, ln_b, Wm, bm, eps):
         agg = agg.contiguous()
         prev = prev.contiguous() if prev is not None else None
         Wp, Wm = Wp.contiguous(), Wm.contiguous()
         N = agg.shape[0]
-        out = _take(sec, "tail_out", (N, P_W), agg)
-        with _on_side(sec, ins, (prev, agg, Wp, Wm), (prev, agg, Wp, bp, ln_w, ln_b, Wm, bm, out)):
-            _native.point_tail_fwd(prev, agg, Wp, bp, ln_w, ln_b, eps, Wm, bm, out)
+        out = _f32(N, P_W, like=agg)
+        _native.point_tail_fwd(prev, agg, Wp, bp, ln_w, ln_b, eps, Wm, bm, out)
         ctx.save_for_backward(prev, agg, Wp, bp, ln_w, ln_b, Wm)
         ctx.eps = eps
-        ctx.sec = sec
-        if sec is not None:
-            sec.tail_has_prev = prev is not None
         ctx.defer = _native.defer_token(Wp, bp, ln_w, ln_b, Wm, bm)
         return out
 
@@ -51,54 +44,37 @@ class PointTailFn(torch.autograd.Function):
     def backward(ctx, dout):
         prev, agg, Wp, bp, ln_w, ln_b, Wm = ctx.saved_tensors
         N = agg.shape[0]
-        sec = ctx.sec
-        # continues on the side stream after PointHubFn.backward, whose dp is the only gradient
-        # of the tail output and which allocated this pass's buffers before forking; anything
-        # else (a copy, an accumulated gradient) is a torch-stream result: allocate, then fork
-        dp = getattr(sec, "dp", None)
-        cont = (sec is not None and sec.forked and dp is not None and dout.data_ptr() == dp.data_ptr()
-                and dout.shape == dp.shape and dout.stride() == dp.stride())
-        if sec is not None and not cont:
-            sec.bufs.clear()
         dout = dout.contiguous()
         rows, cols = _native.point_tail_part_shape(N, prev is not None)
-        dx = _take(sec, "tail_dx", (N, P_W), agg)
-        dagg = _take(sec, "tail_dagg", (N, A_W), agg)
+        dx = _f32(N, P_W, like=agg)
+        dagg = _f32(N, A_W, like=agg)
         if rows == 0:
             tot = torch.zeros(cols, dtype=torch.float32, device=agg.device)
         else:
-            part = _take(sec, "tail_part", (rows, cols), agg)
-            with _on_side(sec, (), (), (dout, prev, agg, Wp, bp, ln_w, ln_b, Wm, dx, dagg, part)):
-                _native.point_tail_bwd(dout, prev, agg, Wp, bp, ln_w, ln_b, ctx.eps, Wm, dx, dagg, part)
+            part = _f32(rows, cols, like=agg)
+            _native.point_tail_bwd(dout, prev, agg, Wp, bp, ln_w, ln_b, ctx.eps, Wm, dx, dagg, part)
             tot = _native.param_colsum(part, ctx.defer)
-        if sec is not None:
-            sec.dp = None
         o = 0
         dWm = tot[o:o + P_W * P_W].view(P_W, P_W)
         o += P_W * P_W
         dWp = tot[o:o + P_W * A_W].view(P_W, A_W)
         o += P_W * A_W
         dbm, dbp, dg, dbt = (tot[o + k * P_W:o + (k + 1) * P_W] for k in range(4))
-        return (dx if prev is not None else None), dagg, dWp, dbp, dg, dbt, dWm, dbm, None, None
+        return (dx if prev is not None else None), dagg, dWp, dbp, dg, dbt, dWm, dbm, None
 
 
 class PointHubFn(torch.autograd.Function):
     """p -> (skip, SA, XL, XR); see the module docstring for the four consumers."""
 
     @staticmethod
-    def forward(ctx, p, gA, bA, WA, WB, bB, gC, bC, WC, bWC, WD, bD, eps, sec=None):
-        ins = (p, WA, WB, WC, WD)
+    def forward(ctx, p, gA, bA, WA, WB, bB, gC, bC, WC, bWC, WD, bD, eps):
         p = p.contiguous()
         WA, WB, WC, WD = (w.contiguous() for w in (WA, WB, WC, WD))
         N = p.shape[0]
-        SA, XL, XR = _take(sec, "hub_SA", (N, A_W), p), _take(sec, "hub_XL", (N, P_W), p), \
-            _take(sec, "hub_XR", (N, A_W), p)
-        with _on_side(sec, ins, (p, WA, WB, WC, WD),
-                      (p, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR)):
-            _native.point_hub_fwd(p, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR)
+        SA, XL, XR = _f32(N, A_W, like=p), _f32(N, P_W, like=p), _f32(N, A_W, like=p)
+        _native.point_hub_fwd(p, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR)
         ctx.save_for_backward(p, gA, bA, WA, WB, gC, bC, WC, bWC, WD)
         ctx.eps = eps
-        ctx.sec = sec
         ctx.defer = _native.defer_token(gA, bA, WA, WB, bB, gC, bC, WC, bWC, WD, bD)
         ctx.set_materialize_grads(False)
         return p.view_as(p), SA, XL, XR
@@ -114,33 +90,14 @@ class PointHubFn(torch.autograd.Function):
         dskip = dskip.contiguous() if dskip is not None else None
         rc, cc = _native.point_hub_part_shape(N, 1, dskip is not None)
         ra, ca = _native.point_hub_part_shape(N, 0, True)
-        sec = ctx.sec
-        if sec is not None:
-            # this pass's buffers and the tail's (which continues on the side stream) are
-            # allocated before the fork: torch-stream kernels enqueued after it (the camera
-            # side) can not have used their memory
-            sec.bufs.clear()
-            sec.alloc("hub_dp", (N, P_W), p)
-            sec.alloc("hub_part_c", (rc, cc), p)
-            sec.alloc("hub_part_a", (ra, ca), p)
-            rt, ct = _native.point_tail_part_shape(N, getattr(sec, "tail_has_prev", True))
-            sec.alloc("tail_dx", (N, P_W), p)
-            sec.alloc("tail_dagg", (N, A_W), p)
-            sec.alloc("tail_part", (rt, ct), p)
-            sec.fork()
-        dp = _take(sec, "hub_dp", (N, P_W), p)
-        if sec is not None:
-            sec.dp = dp
-        keep = (p, gA, bA, WA, WB, gC, bC, WC, bWC, WD, dSA, dXL, dXR, dskip, dp)
+        dp = _f32(N, P_W, like=p)
         if N == 0:
             tc = torch.zeros(cc, dtype=torch.float32, device=p.device)
             ta = torch.zeros(ca, dtype=torch.float32, device=p.device)
         else:
-            part_c = _take(sec, "hub_part_c", (rc, cc), p)
-            part_a = _take(sec, "hub_part_a", (ra, ca), p)
-            with _on_side(sec, (), (), keep + (part_c, part_a)):
-                _native.point_hub_bwd(p, ctx.eps, gA, bA, WA, WB, gC, bC, WC, bWC, WD, dSA, dXL, dXR, dskip, dp,
-                                      part_a, part_c)
+            part_c, part_a = _f32(rc, cc, like=p), _f32(ra, ca, like=p)
+            _native.point_hub_bwd(p, ctx.eps, gA, bA, WA, WB, gC, bC, WC, bWC, WD, dSA, dXL, dXR, dskip, dp,
+                                  part_a, part_c)
             tc, ta = _native.param_colsum(part_c, ctx.defer), _native.param_colsum(part_a, ctx.defer)
         o = 0
         dWC = tc[o:o + A_W * P_W].view(A_W, P_W)
@@ -156,39 +113,7 @@ class PointHubFn(torch.autograd.Function):
         dWB = ta[o:o + P_W * P_W].view(P_W, P_W)
         o += P_W * P_W
         dbB, dgA, dbA = (ta[o + k * P_W:o + (k + 1) * P_W] for k in range(3))
-        return dp, dgA, dbA, dWA, dWB, dbB, dgC, dbC, dWC, dbWC, dWD, dbD, None, None
-
-
-def forward_buffers(sec, N, like):
-    """Outputs of this block's PointTailFn / PointHubFn forward, allocated before the fork."""
-    sec.bufs.clear()
-    sec.alloc("tail_out", (N, P_W), like)
-    sec.alloc("hub_SA", (N, A_W), like)
-    sec.alloc("hub_XL", (N, P_W), like)
-    sec.alloc("hub_XR", (N, A_W), like)
-
-
-def _take(sec, key, shape, like):
-    """A buffer for a side-stream launch: the one allocated before the fork, or a new one
-    followed by a fork (new memory may have been freed by torch-stream work enqueued since)."""
-    if sec is None:
-        return _f32(*shape, like=like)
-    t = sec.bufs.pop(key, None)
-    if t is None or tuple(t.shape) != tuple(shape):
-        t = _f32(*shape, like=like)
-        sec.fork()
-    return t
-
-
-def _on_side(sec, before, after, used):
-    """Launch context of a Function that may run on sec's side stream.  before/after: its
-    inputs before and after .contiguous(); a copy was made on torch's stream after the fork,
-    so the side stream waits again."""
-    if sec is None:
-        return contextlib.nullcontext()
-    if any(a is not b for a, b in zip(before, after)):
-        sec.fork()
-    return sec.launches(*used)
+        return dp, dgA, dbA, dWA, dWB, dbB, dgC, dbC, dWC, dbWC, dWD, dbD, None
 
 
 def _is_ln(m, w):
@@ -214,10 +139,10 @@ def tail_fusable(agg_mod, x, prev):
             and _is_ln(agg_mod.norm_pre_mlp, P_W) and len(agg_mod.mlp) == 1 and _is_lin(agg_mod.mlp[0], P_W, P_W, True))
 
 
-def tail(agg_mod, x, prev, sec=None):
+def tail(agg_mod, x, prev):
     proj = getattr(agg_mod, agg_mod._proj_key)
     ln, lin = agg_mod.norm_pre_mlp, agg_mod.mlp[0]
-    return PointTailFn.apply(prev, x, proj.weight, proj.bias, ln.weight, ln.bias, lin.weight, lin.bias, ln.eps, sec)
+    return PointTailFn.apply(prev, x, proj.weight, proj.bias, ln.weight, ln.bias, lin.weight, lin.bias, ln.eps)
 
 
 def hub_params(pfu, s2g_conv, nxt):
@@ -241,8 +166,8 @@ def hub_params(pfu, s2g_conv, nxt):
             linC.bias, linD.weight, linD.bias, lnA.eps)
 
 
-def hub(p, params, sec=None):
-    return PointHubFn.apply(p, *params, sec)
+def hub(p, params):
+    return PointHubFn.apply(p, *params)
 
 
 class PointHeadFn(torch.autograd.Function):

@@ -40,32 +40,6 @@ FP32_GEMM = os.environ.get("GASFM_VIEW_GEMM", "torch")
 # batch's ~60) go to csrc/gemm_smallm.hip (1,024 waves of 16 x 32 tiles x K-quarters) instead of
 # hipBLASLt, whose 125 x 1024 x 1024 tiles take ~11.5 us; 0 disables
 SMALLM_ROWS = int(os.environ.get("GASFM_SMALLM_ROWS", "256"))
-# round 4: in the backward of the 1000-row camera side (hipBLASLt path), the weight-gradient GEMM
-# (dW = dY^T X) runs on a second stream beside dX = dY W and the view kernel that consumes it (each
-# GEMM fills 256 workgroups, one per CU); joined before the Function returns.
-SIDE_GEMM = os.environ.get("GASFM_SIDE_GEMM", "0") != "0"
-
-
-class _SideMM:
-    """dW = a @ b on streams.side_stream beside the caller's stream: out is allocated on the caller's
-    stream before the fork, the operands stay referenced by the caller until join()."""
-
-    def __init__(self, a, b, like):
-        from . import streams
-        self.out = torch.empty((a.shape[0], b.shape[1]), dtype=torch.float32, device=like.device)
-        self.cur = torch.cuda.current_stream(like.device)
-        self.side = streams.side_stream(like.device)
-        self.side.wait_stream(self.cur)
-        with torch.cuda.stream(self.side):
-            torch.mm(a, b, out=self.out)
-
-    def join(self):
-        self.cur.wait_stream(self.side)
-        return self.out
-
-
-def _side_ok(m, bf16):
-    return SIDE_GEMM and not bf16 and FP32_GEMM != "hip" and m > SMALLM_ROWS
 # fp32 camera sides of at most 256 rows (view_chain_ok) run as csrc/view_chain.hip: the D x D GEMMs
 # with the view kernels as their prologues / epilogues, 2 launches forward and 4 backward per block
 # (round 3: 7 and 10); GASFM_VIEW_CHAIN=0 keeps the separate view kernels + GEMMs
@@ -134,9 +108,8 @@ class ViewTailFn(torch.autograd.Function):
             dWp = tot[:D * A_W].view(D, A_W)
             dbp, dg, dbt, dbm = (tot[D * A_W + k * D:D * A_W + (k + 1) * D] for k in range(4))
             return (dx if ctx.has_prev else None), dagg, dWp, dbp, dg, dbt, dWm, dbm, None, None
-        side = _SideMM(dview.t(), h, like=x) if _side_ok(m, ctx.bf16) else None
         dh = _mm(dview, Wm, bf16=ctx.bf16)
-        dWm = _mm(dview.t(), h, bf16=ctx.bf16) if side is None else None
+        dWm = _mm(dview.t(), h, bf16=ctx.bf16)
         dx, dagg = _f32(m, D, like=x), _f32(m, A_W, like=x)
         cols = _native.view_tail_part_cols(D)
         if m == 0:
@@ -146,8 +119,6 @@ class ViewTailFn(torch.autograd.Function):
             _native.view_tail_bwd(dview, dh, x, rs, agg, Wp, ln_w, ln_b, dx, dagg, part,
                                   _native.view_scratch(m, D, x.device))
             tot = _native.param_colsum(part, ctx.defer)
-        if side is not None:
-            dWm = side.join()
         dWp = tot[:D * A_W].view(D, A_W)
         dbp, dg, dbt, dbm = (tot[D * A_W + k * D:D * A_W + (k + 1) * D] for k in range(4))
         return (dx if ctx.has_prev else None), dagg, dWp, dbp, dg, dbt, dWm, dbm, None, None
@@ -193,7 +164,6 @@ class ViewHubFn(torch.autograd.Function):
         dXR = dXR.contiguous() if dXR is not None else zeros(A_W)
         dXL = dXL.contiguous() if dXL is not None else zeros(D)
         dres = None
-        side = _SideMM(dXL.t(), v, like=v) if (not ctx.chain and _side_ok(m, ctx.bf16)) else None
         if ctx.chain:
             dacc, dWl = _f32(m, D, like=v), torch.empty_like(Wl)
             part = _f32((m + TR - 1) // TR, _native.view_hub_part_cols(D), like=v)
@@ -206,7 +176,7 @@ class ViewHubFn(torch.autograd.Function):
             dacc = _mm(dXL, Wl)
             dres = dskip.contiguous() if dskip is not None else None
         if not ctx.chain:
-            dWl = _mm(dXL.t(), v, bf16=ctx.bf16) if side is None else None
+            dWl = _mm(dXL.t(), v, bf16=ctx.bf16)
             cols = _native.view_hub_part_cols(D)
             if m == 0:
                 tot = torch.zeros(cols, dtype=torch.float32, device=v.device)
@@ -215,8 +185,6 @@ class ViewHubFn(torch.autograd.Function):
                 _native.view_hub_bwd(v, rs, gC, bC, Wv, gA, bA, Wa, t, Wr, dSV, dXR, dXL, dacc, part,
                                      _native.view_scratch(m, D, v.device), dres=dres)
                 tot = _native.param_colsum(part, ctx.defer)
-            if side is not None:
-                dWl = side.join()
         o = 0
         dWv = tot[o:o + A_W * D].view(A_W, D)
         o += A_W * D

@@ -75,10 +75,9 @@ enum {
   GASFM_K_ATTN_BWD_LANES = 8,
   GASFM_K_ATTN_COMBINE_VEC = 9,
   GASFM_K_ATTN_COMBINE_GENERIC = 10,
-  GASFM_K_ATTN_BWD_GRP = 11,     /* grouped items backward (32-wide, streamed XL) */
-  GASFM_K_SEAM_LDS = 12,         /* forward seam with its inputs staged through LDS (round 4) */
-  GASFM_K_SEAM_REG = 13,         /* forward seam with its inputs prefetched into registers */
-  GASFM_K_ROWSUM_GRP = 14,       /* segment row sums, 8 segments per wave task */
+  /* 11, 12, 14: reserved (round-4 variants measured and removed: grouped attention backward,
+   * LDS-staged forward seam, grouped segment row sums) */
+  GASFM_K_SEAM_REG = 13,         /* forward seam (blocks 1-11) */
   GASFM_K_COUNT = 16
 };
 
@@ -93,9 +92,7 @@ enum {
   GASFM_TUNE_ATTN_GRP_MIN_FILL = 1,  /* GASFM_ATTN_GRP_MIN_FILL: grouped when tasks >= fill x resident waves */
   GASFM_TUNE_ATTN_GLDS = 2,          /* GASFM_ATTN_GLDS: direct-to-LDS kernels on (1) / off (0) */
   GASFM_TUNE_ATTN_WAVE_CAP = 3,      /* GASFM_ATTN_WAVES: cap on item-loop waves, 0 = occupancy */
-  GASFM_TUNE_ATTN_GRP_BWD = 4,       /* GASFM_ATTN_GRP_BWD: grouped backward (32-wide, streamed XL) on (1) / off (0) */
-  GASFM_TUNE_SEAM_LDS = 5,           /* GASFM_SEAM_LDS: forward seam (blocks 1-11) LDS-staged (1) / registers (0) */
-  GASFM_TUNE_ROWSUM_GRP = 6,         /* GASFM_ROWSUM_GRP: gasfm_segment_rowsum grouped (1) / one item per wave (0) */
+  /* 4, 5, 6: reserved (removed round-4 variants) */
   GASFM_TUNE_COUNT = 8
 };
 int gasfm_tuning_set(int32_t key, double value);
@@ -168,18 +165,6 @@ int gasfm_edge_seam_fwd(const float* Pb, const float* P0, const int32_t* pt, con
                         int64_t ldXR, const float* att, const float* bias, float slope,
                         const gasfm_work_item* items, int32_t n_items, int32_t finalize, float* out, int64_t ldOut,
                         float* seg_max, float* seg_sum, int64_t ldStat, float* part, void* stream);
-/* gasfm_edge_seam_fwd that also writes block b+1's camera-half XLc [E, 32] (edge order, bias
- * included) for gasfm_edge_cam_pbwd_xlc (round 4 experiment: XLc kept instead of recomputed in the
- * backward; XLc null: gasfm_edge_seam_fwd).  Requires ln_w. */
-int gasfm_edge_seam_fwd_x(const float* Pb, const float* P0, const int32_t* pt, const float* ln_wb, const float* ln_bb,
-                          float eps_b, const float* Wp, int32_t ldWp, const float* bp, const float* Sp, const float* Sv,
-                          int64_t ldSv, const float* Sg, float scale, float* Pout, const float* ln_w,
-                          const float* ln_b, float eps, const float* Wpt, const float* bpt, const float* Wc,
-                          const float* bc, float* XLp, int64_t ldXLp, const int32_t* pos, const float* XR,
-                          int64_t ldXR, const float* att, const float* bias, float slope,
-                          const gasfm_work_item* items, int32_t n_items, int32_t finalize, float* out, int64_t ldOut,
-                          float* seg_max, float* seg_sum, int64_t ldStat, float* part, float* XLc, void* stream);
-
 /* Block 0's edge epilogue (2-wide P: P' = Wsk relu(LN_b(P)) + bsk + scale (Wp relu(LN_a(P)) + bp +
  * Sg + Sp[pt] + Sv[cam]), gasfm_edge0_epilogue_fwd) and block 1's prologue + camera attention
  * (gasfm_edge_cam_fwd) in ONE pass, as gasfm_edge_seam_fwd for the 32-wide blocks (round 3).
@@ -223,9 +208,7 @@ int gasfm_edge_cam_pbwd(const float* P, const float* ln_w, const float* ln_b, fl
  *   ldWpo > 0 (DWP): THIS block's lin_proj gradient scale sum_e dRes[e]^T [relu(LN(P[e])) | P0[e]]
  *     as a [32 x ldWpo] block after the gasfm_edge_cam_pbwd_part_cols() floats of each part row
  *     (ldWpo = 34 with P0 [E, 2], 32 without); requires ln_w and dRes.
- * part rows have stride ldPart (>= part_cols + 32 ldWpo).
- * dxl_pos (round 4, may be null): dXLp is in point-segment order, edge e's row at dxl_pos[e] (the
- * point plan's pos: the layout gasfm_gat_attn_bwd writes without perm); null: edge order. */
+ * part rows have stride ldPart (>= part_cols + 32 ldWpo). */
 int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
                            const float* Wc, const float* bc, const float* Wp, int32_t ldWp, float scale,
                            const float* XR, int64_t ldXR, const float* att, const float* bias, float slope,
@@ -234,39 +217,7 @@ int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const float* ln_b,
                            int32_t n_items, const float* dXLp, int64_t ldXp, const float* dRes, float* dP,
                            float* dXR, int64_t ldDXR, float* part_dxr, float* part, int64_t ldPart,
                            const float* We, int32_t ldWe, float scale_e, float* dSv_e, float* part_dsv_e,
-                           float* dP0_e, const float* P0, int32_t ldWpo, const int32_t* dxl_pos, void* stream);
-/* Block 1's gasfm_edge_cam_pbwd_ex (LN, dRes, DWP with P0) with BLOCK 0's 2-wide epilogue backward
- * folded in (round 4; replaces gasfm_edge0_epilogue_bwd, reference: the autograd of
- * residual_skipconn_proj_norm_layer + skip_projection + lin_proj of block 0, layers.py:214-220,
- * 256-261, 959-969).  P0 [E, 2] is block 0's input (the embedded projections, also block 1's skip
- * input); Wp0 / Wsk0 [32 x 2]; ln0 = [ga0 ga1 ba0 ba1 gb0 gb1 bb0 bb1] (LN_a, LN_b affines), eps0;
- * scale0 the epilogue scale.  Outputs, as gasfm_edge0_epilogue_bwd's: dSv0 (+ part_dsv0 split rows),
- * aux0 [E, 4] = (dP_hat_a (2), dP of the skip branch (2)) and, after the 32 x 34 dWp block of each
- * part row, gasfm_edge_cam_pbwd_e0_cols() floats [dWp0 64 | dWsk0 64 | dbsk0 32 | dgb 2 | dbb 2]
- * (ldPart >= part_cols + 32 x 34 + e0_cols). */
-/* gasfm_edge_cam_pbwd_ex (LN, dRes, EPI and DWP) reading XLc [E, 32] as written by
- * gasfm_edge_seam_fwd_x instead of recomputing it from P (round 4 experiment). */
-int gasfm_edge_cam_pbwd_xlc(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
-                            const float* Wc, const float* bc, const float* Wp, int32_t ldWp, float scale,
-                            const float* XR, int64_t ldXR, const float* att, const float* bias, float slope,
-                            const float* out, int64_t ldOut, const float* seg_max, const float* seg_sum,
-                            int64_t ldStat, const float* gout, int64_t ldG, const gasfm_work_item* items,
-                            int32_t n_items, const float* dXLp, int64_t ldXp, const float* dRes, float* dP,
-                            float* dXR, int64_t ldDXR, float* part_dxr, float* part, int64_t ldPart,
-                            const float* We, int32_t ldWe, float scale_e, float* dSv_e, float* part_dsv_e,
-                            float* dP0_e, const float* P0, int32_t ldWpo, const int32_t* dxl_pos, const float* XLc,
-                            void* stream);
-int32_t gasfm_edge_cam_pbwd_e0_cols(void);
-int gasfm_edge_cam_pbwd_e0(const float* P, const float* ln_w, const float* ln_b, float eps, const float* Wpt,
-                           const float* Wc, const float* bc, const float* Wp, int32_t ldWp, float scale,
-                           const float* XR, int64_t ldXR, const float* att, const float* bias, float slope,
-                           const float* out, int64_t ldOut, const float* seg_max, const float* seg_sum,
-                           int64_t ldStat, const float* gout, int64_t ldG, const gasfm_work_item* items,
-                           int32_t n_items, const float* dXLp, int64_t ldXp, const float* dRes, float* dP,
-                           float* dXR, int64_t ldDXR, float* part_dxr, float* part, int64_t ldPart,
-                           const float* P0, const float* Wp0, const float* Wsk0, const float* ln0, float eps0,
-                           float scale0, float* dSv0, float* part_dsv0, float* aux0, const int32_t* dxl_pos,
-                           void* stream);
+                           float* dP0_e, const float* P0, int32_t ldWpo, void* stream);
 
 /* ---- fused GATv2 edge-softmax + aggregation (device) ------------------- */
 

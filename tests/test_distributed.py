@@ -97,6 +97,24 @@ def test_camera_rows_and_cam_param_classification():
     assert {k for k in names if gd.is_local_param(k)} <= part
 
 
+def test_watchdog_retire_private_api_present():
+    """graph_step.retire_collectives rests on two private torch.distributed symbols
+    (c10d._world.pg_map, ProcessGroup._wait_for_pending_works): pinned on this torch, and a process
+    group without the method makes it raise instead of silently skipping the retire step."""
+    from gasfm_amd import graph_step
+    assert graph_step.private_api_ok(), torch.__version__
+
+    class _NoWait:  # a stand-in process group that lacks the private method
+        pass
+
+    import unittest.mock as um
+    with um.patch.object(graph_step, "_process_groups", lambda: [_NoWait()]), \
+            um.patch.object(dist, "is_initialized", lambda: True), \
+            um.patch.object(dist, "get_backend", lambda pg: "nccl"):
+        with pytest.raises(RuntimeError, match="_wait_for_pending_works"):
+            graph_step.retire_collectives()
+
+
 def _partial_state(logits, vals):
     m = logits.max(0).values
     e = torch.exp(logits - m)
@@ -164,7 +182,7 @@ def test_collective_wrappers_gloo_world2():
         assert ga == [[3.0] * 3] * 2 and gb == [10.0] * 5  # AllReduceGradN: one all-reduce, None -> 0
 
 
-def _worker_sharded_model(rank, world, port, q, cameras=False):
+def _worker_sharded_model(rank, world, port, q, cameras=False, bounds=None, max_piece=64):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -176,7 +194,7 @@ def _worker_sharded_model(rank, world, port, q, cameras=False):
         net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=3))
         net.load_state_dict(deterministic_state_dict(net.state_dict()))
         model = gd.ShardedGraphAttnSfMNet(net.to(dev), cameras=cameras)
-        data = gd.shard_scene(sc, rank, world, max_piece=64, cameras=cameras).to(dev)
+        data = gd.shard_scene(sc, rank, world, max_piece=max_piece, cameras=cameras, point_bounds=bounds).to(dev)
         g = torch.Generator().manual_seed(1)
         cP = torch.randn((sc.m, 3, 4), generator=g).to(dev)
         cX = torch.randn((4, sc.n), generator=g).to(dev)
@@ -192,11 +210,9 @@ def _worker_sharded_model(rank, world, port, q, cameras=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("cameras", [False, True], ids=["points", "points+cameras"])
-def test_sharded_model_matches_single_gpu(device, cameras):
-    """2 ranks (gloo staging, one GPU) vs the single-GPU forward, and both vs the fp64 oracle's grads;
-    points sharded, and points + camera rows sharded (the view chain split over the ranks)."""
+def _run_sharded_vs_oracle(device, world, cameras, bounds=None, max_piece=64):
+    """``world`` ranks (gloo staging, all on one GPU) vs the single-GPU forward, and both vs the fp64
+    oracle's gradients; every parameter gradient bitwise identical across the ranks."""
     import gasfm_amd
     from conftest import check_grad, oracle_grads
     from oracle.weights import deterministic_state_dict
@@ -216,7 +232,8 @@ def test_sharded_model_matches_single_gpu(device, cameras):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_sharded_model, args=(r, 2, port, q, cameras)) for r in range(2)]
+    procs = [ctx.Process(target=_worker_sharded_model, args=(r, world, port, q, cameras, bounds, max_piece))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=600) for _ in procs]
@@ -224,6 +241,8 @@ def test_sharded_model_matches_single_gpu(device, cameras):
         p.join(timeout=120)
         assert p.exitcode == 0
     res.sort(key=lambda t: t[0])
+    assert [r[3] for r in res] == [(int(a), int(b)) for a, b in zip(res_bounds(sc, world, bounds)[:-1],
+                                                                     res_bounds(sc, world, bounds)[1:])]
     for rank, ps, pts, (a, b), grads in res:
         np.testing.assert_allclose(ps, pred["Ps_norm"].detach().cpu().numpy(), atol=1e-5, rtol=1e-4)
         np.testing.assert_allclose(pts, pred["pts3D"][:, a:b].detach().cpu().numpy(), atol=1e-5, rtol=1e-4)
@@ -231,9 +250,43 @@ def test_sharded_model_matches_single_gpu(device, cameras):
             check_grad(grads[k], g64[k], f"rank {rank} {k}", g32[k])
     for k, p in net.named_parameters():
         check_grad(p.grad, g64[k], f"single-GPU {k}", g32[k])
-    # every parameter gradient ends bitwise identical on both ranks (replicated optimizer steps stay in sync)
-    for k in g64:
-        assert np.array_equal(res[0][4][k], res[1][4][k]), k
+    # every parameter gradient ends bitwise identical on every rank (replicated optimizer steps stay in sync)
+    for rank in range(1, world):
+        for k in g64:
+            assert np.array_equal(res[0][4][k], res[rank][4][k]), (rank, k)
+
+
+def res_bounds(sc, world, bounds):
+    return gd.partition_points(sc.pt, sc.n, world) if bounds is None else np.asarray(bounds)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cameras", [False, True], ids=["points", "points+cameras"])
+def test_sharded_model_matches_single_gpu(device, cameras):
+    """2 ranks (gloo staging, one GPU) vs the single-GPU forward, and both vs the fp64 oracle's grads;
+    points sharded, and points + camera rows sharded (the view chain split over the ranks)."""
+    _run_sharded_vs_oracle(device, 2, cameras)
+
+
+def _bounds_with_small_shard(world):
+    """Edge-balanced point ranges except that rank 3 keeps only 5 points (a shard far smaller than a
+    camera work item, next to ranks holding the rest)."""
+    sc = synthetic.scaled_config4(0.02, seed=5)
+    b = gd.partition_points(sc.pt, sc.n, world).copy()
+    b[4] = b[3] + 5
+    return b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cameras,small", [(False, False), (True, False), (True, True)],
+                         ids=["points", "points+cameras", "points+cameras-small-shard"])
+def test_sharded_model_world8_matches_oracle(device, cameras, small):
+    """The 8-way decomposition bench.py's N = 8 path takes: 8 gloo ranks on one GPU,
+    scaled config 4 (m = 20, n = 4000), 3 blocks.  camera_rows(20, 8) gives ranks of 3, 2 and 0
+    camera rows; eight partial rows per camera merge; the camera plans use the shard-sized piece
+    length (camera_max_piece); small: one rank holds only 5 points."""
+    bounds = _bounds_with_small_shard(8) if small else None
+    _run_sharded_vs_oracle(device, 8, cameras, bounds=bounds, max_piece=None)
 
 
 def _worker_capture_agree(rank, world, port, q):

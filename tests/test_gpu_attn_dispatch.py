@@ -204,13 +204,12 @@ def test_forced_forward_variants_vs_oracle(device, tuning, kernel, max_piece):
     compare(got, ref, nonempty, f"{kernel} {tuning}")
 
 
-@pytest.mark.parametrize("tuning,kernel", [(dict(attn_glds=1, attn_grp_bwd=0), "attn_bwd_glds"),
-                                           (dict(attn_glds=0, attn_grp_bwd=0), "attn_bwd_vec"),
-                                           (dict(attn_grp_bwd=1), "attn_bwd_grp")])
+@pytest.mark.parametrize("tuning,kernel", [(dict(attn_glds=1), "attn_bwd_glds"),
+                                           (dict(attn_glds=0), "attn_bwd_vec")])
 @pytest.mark.parametrize("max_piece", [64, 7])
 def test_forced_backward_variants_vs_oracle(device, tuning, kernel, max_piece):
-    """Backward kernels of the 32-wide conv: direct-to-LDS, register and grouped (8 items per wave
-    task), streamed and by position; max_piece 7: most items partial (dXR partial slots)."""
+    """Backward kernels of the 32-wide conv: direct-to-LDS and register, streamed and by position;
+    max_piece 7: most items partial (dXR partial slots)."""
     N, E, H, C = 2000, 40000, 4, 8
     plan = random_sorted_plan(device, N, E, max_piece, seed=9)
     XLs, XR, att, bias, gout = inputs(device, E, N, H, C, seed=4)
@@ -220,22 +219,6 @@ def test_forced_backward_variants_vs_oracle(device, tuning, kernel, max_piece):
     ref = oracle_sorted(XLs, XR, att, bias, plan, gout, H)
     nonempty = (plan.seg_ptr[1:] > plan.seg_ptr[:-1]).to(device)
     compare(got, ref, nonempty, f"bwd {kernel} max_piece={max_piece}")
-
-
-@pytest.mark.parametrize("scale", [0.1, 1.0])
-def test_point_direction_grouped_backward_vs_oracle(device, scene_plans, scale):
-    """The model's point-direction conv (xl_sorted, dXL scattered through perm to edge order) with
-    the grouped backward (attn_grp_bwd) at scaled_config4(0.1) and full config 4."""
-    sc, plans = scene_plans(scale)
-    plan = plans["proj2scenepoint"]
-    H, C = 4, 8
-    XLs, XR, att, bias, gout = inputs(device, plan.num_edges, plan.num_targets, H, C, seed=21 + int(scale * 100))
-    with _native.tuned(attn_grp_bwd=1):
-        got, fwd, bwd = run_case(device, plan, XLs, XR, att, bias, H, gout, xl_sorted=True)
-    assert bwd["attn_bwd_grp"] == 1 and bwd["attn_bwd_glds"] == 0, bwd
-    ref = oracle_sorted(XLs, XR, att, bias, plan, gout, H)
-    nonempty = (plan.seg_ptr[1:] > plan.seg_ptr[:-1]).to(device)
-    compare(got, ref, nonempty, f"point grouped bwd scale {scale}")
 
 
 def test_lanes_rule_block0_point_direction(device, scene_plans):

@@ -93,11 +93,9 @@ def test_prologue_without_ln(device):
     normwise(bd.grad, br.grad, msg="b")
 
 
-@pytest.mark.parametrize("grp", [0, 1])
 @pytest.mark.parametrize("n,E,max_piece", [(500, 20000, 16), (5003, 20000, 256), (37, 40, 16)])
-def test_segment_rowsum_matches_index_add(device, grp, n, E, max_piece):
-    """One item per wave (grp 0) and 8 items per wave task (grp 1, tuning option rowsum_grp):
-    ragged item counts (not a multiple of 8), empty segments, split segments, vs fp64 index_add."""
+def test_segment_rowsum_matches_index_add(device, n, E, max_piece):
+    """Ragged item counts, empty segments, split segments, vs fp64 index_add."""
     from gasfm_amd import _native
     from gasfm_amd.attention import AttnPlan, bwd_combine
     rng = np.random.default_rng(2)
@@ -106,9 +104,7 @@ def test_segment_rowsum_matches_index_add(device, grp, n, E, max_piece):
     X = torch.randn(E, 32, device=device)
     out = torch.empty(n, 32, device=device)
     part = torch.empty(max(plan.n_part_rows, 1), 32, device=device)
-    with _native.tuned(rowsum_grp=grp), _native.dispatch_record() as rec:
-        _native.segment_rowsum(plan.items, plan.n_items, plan.perm, X, 0.25, out, part)
-    assert rec.counts["rowsum_grp"] == grp
+    _native.segment_rowsum(plan.items, plan.n_items, plan.perm, X, 0.25, out, part)
     bwd_combine(plan, part, 32, out)
     ref = torch.zeros(n, 32, dtype=torch.float64).index_add(0, dst, X.double().cpu()) * 0.25
     np.testing.assert_allclose(out.cpu().numpy(), ref.numpy(), atol=1e-5, rtol=1e-4)

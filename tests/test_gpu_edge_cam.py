@@ -186,94 +186,6 @@ def test_epilogue_fold_vs_unfolded(device, monkeypatch):
         assert err <= max(1e-3 * float(g0.norm()), 10 * own) + 1e-9, (k, err, own, float(g0.norm()))
 
 
-def test_xlc_store_vs_recompute(device, monkeypatch):
-    """XLc kept by the forward seam and read by edge_cam_pbwd (edge_block.XLC_STORE) against the
-    recompute from P: identical forward, the kept rows used by the folded launches (blocks 2-3 of a
-    4-block net), every parameter gradient within 1e-4 normwise of the recomputing path or within
-    10x its own distance from the fp64 oracle."""
-    from conftest import oracle_grads
-    from gasfm_amd import edge_block
-    from oracle.weights import deterministic_state_dict
-    sc = synthetic.scaled_config4(0.05, seed=23)
-    data = gasfm_amd.SceneData.from_synthetic(sc, max_piece=64).to(device)
-    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=4))
-    sd = deterministic_state_dict(net.state_dict(), torch.float64)
-    net.load_state_dict({k: v.float() for k, v in sd.items()})
-    net = net.to(device)
-    gen = torch.Generator().manual_seed(13)
-    cP = torch.randn((sc.m, 3, 4), generator=gen, dtype=torch.float64)
-    cX = torch.randn((4, sc.n), generator=gen, dtype=torch.float64)
-    used = []
-    orig = _native.edge_cam_pbwd
-    monkeypatch.setattr(_native, "edge_cam_pbwd",
-                        lambda *a, **k: (used.append(k.get("XLc") is not None), orig(*a, **k))[1])
-    res = {}
-    for keep in (False, True):
-        monkeypatch.setattr(edge_block, "XLC_STORE", keep)
-        used.clear()
-        net.zero_grad(set_to_none=True)
-        pred = net(data)
-        ((pred["Ps_norm"] * cP.float().to(device)).sum() + (pred["pts3D"] * cX.float().to(device)).sum()).backward()
-        torch.cuda.synchronize()
-        res[keep] = (pred["Ps_norm"].detach().clone(), {k: p.grad.detach().double().cpu() for k, p in net.named_parameters()},
-                     sum(used))
-    assert torch.equal(res[True][0], res[False][0])
-    assert res[False][2] == 0 and res[True][2] == 2, (res[False][2], res[True][2])
-    (g64, _), _ = oracle_grads(sd, sc, cP, cX)
-    for k, g0 in res[False][1].items():
-        err = float((res[True][1][k] - g0).norm())
-        own = float((g0 - torch.from_numpy(g64[k])).norm())
-        assert err <= max(1e-4 * float(g0.norm()), 10 * own) + 1e-9, (k, err, own, float(g0.norm()))
-
-
-@pytest.mark.parametrize("max_piece", [None, 64])
-def test_block0_fold_vs_unfolded(device, monkeypatch, max_piece):
-    """Block 0's 2-wide epilogue backward folded into block 1's edge_cam_pbwd (edge_block.E0_FOLD,
-    gasfm_edge_cam_pbwd_e0) against edge0_epilogue_bwd: identical forward, no edge0_epilogue_bwd
-    launch left, block 0's epilogue weights (lin_proj, the skip projection, LN_b) within 1e-4
-    normwise of the unfolded gradients, and every parameter gradient within 1e-3 normwise or within
-    10x the unfolded one's own distance from the fp64 oracle (as test_epilogue_fold_vs_unfolded).
-    max_piece 64 splits cameras over several items (dSv through the partial rows)."""
-    from conftest import oracle_grads
-    from gasfm_amd import edge_block
-    from oracle.weights import deterministic_state_dict
-    sc = synthetic.scaled_config4(0.05, seed=19)
-    data = gasfm_amd.SceneData.from_synthetic(sc, max_piece=max_piece).to(device)
-    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=3))
-    sd = deterministic_state_dict(net.state_dict(), torch.float64)
-    net.load_state_dict({k: v.float() for k, v in sd.items()})
-    net = net.to(device)
-    gen = torch.Generator().manual_seed(9)
-    cP = torch.randn((sc.m, 3, 4), generator=gen, dtype=torch.float64)
-    cX = torch.randn((4, sc.n), generator=gen, dtype=torch.float64)
-    calls = []
-    orig = _native.edge0_epilogue_bwd
-    monkeypatch.setattr(_native, "edge0_epilogue_bwd", lambda *a, **k: (calls.append(1), orig(*a, **k))[1])
-    res = {}
-    for fold in (False, True):
-        monkeypatch.setattr(edge_block, "E0_FOLD", fold)
-        calls.clear()
-        net.zero_grad(set_to_none=True)
-        pred = net(data)
-        ((pred["Ps_norm"] * cP.float().to(device)).sum() + (pred["pts3D"] * cX.float().to(device)).sum()).backward()
-        torch.cuda.synchronize()
-        res[fold] = (pred["Ps_norm"].detach().clone(), {k: p.grad.detach().double().cpu() for k, p in net.named_parameters()},
-                     len(calls))
-    assert torch.equal(res[True][0], res[False][0])
-    assert res[False][2] == 1 and res[True][2] == 0, (res[False][2], res[True][2])
-    (g64, _), _ = oracle_grads(sd, sc, cP, cX)
-    b0 = [k for k in res[False][1] if k.startswith("equivariant_blocks.0.") and
-          ("projection_feature_update.lin_proj" in k or "skip" in k)]
-    assert len(b0) == 6, b0
-    for k, g0 in res[False][1].items():
-        g1 = res[True][1][k]
-        err = float((g1 - g0).norm())
-        if k in b0:
-            assert err <= 1e-4 * float(g0.norm()) + 1e-9, (k, err, float(g0.norm()))
-        own = float((g0 - torch.from_numpy(g64[k])).norm())
-        assert err <= max(1e-3 * float(g0.norm()), 10 * own) + 1e-9, (k, err, own, float(g0.norm()))
-
-
 def test_block0_seam_vs_separate(device, monkeypatch):
     """Block 0's epilogue run inside block 1's prologue + camera attention kernel (Seam0Fn,
     gasfm_edge0_seam_fwd) against the separate launches (EDGE_SEAM off: Block0EpilogueFn +
@@ -312,75 +224,3 @@ def test_block0_seam_vs_separate(device, monkeypatch):
         err = float((res[True][2][k] - g0).norm())
         own = float((g0 - torch.from_numpy(g64[k])).norm())
         assert err <= max(1e-3 * float(g0.norm()), 10 * own) + 1e-9, (k, err, own, float(g0.norm()))
-
-
-@pytest.mark.parametrize("pbwd", [True, False])
-def test_dxl_point_order_bitwise(device, monkeypatch, pbwd):
-    """XLp's gradient in point order (edge_block.DXL_PT: the point attention's backward writes dXL
-    without the perm scatter, edge_cam_pbwd reads edge e's row at pos[e]; with CAM_PBWD off the
-    separate kernels get it back in edge order) against edge order: the same values reach the same
-    products, so every parameter gradient is bitwise identical.  4 blocks: block 0 -> 1 seam,
-    folded 32-wide seams, the final update; items that split cameras (max_piece 64)."""
-    from gasfm_amd import edge_block
-    from oracle.weights import deterministic_state_dict
-    sc = synthetic.scaled_config4(0.05, seed=17)
-    data = gasfm_amd.SceneData.from_synthetic(sc, max_piece=64).to(device)
-    assert data.graph_wrappers["proj2scenepoint"].plan.pos is not None
-    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=4))
-    sd = deterministic_state_dict(net.state_dict(), torch.float64)
-    net.load_state_dict({k: v.float() for k, v in sd.items()})
-    net = net.to(device)
-    gen = torch.Generator().manual_seed(7)
-    cP = torch.randn((sc.m, 3, 4), generator=gen).to(device)
-    cX = torch.randn((4, sc.n), generator=gen).to(device)
-    monkeypatch.setattr(edge_block, "CAM_PBWD", pbwd)
-    seen = []
-    orig = _native.edge_cam_pbwd
-    monkeypatch.setattr(_native, "edge_cam_pbwd",
-                        lambda *a, **k: (seen.append(k.get("dxl_pos") is not None), orig(*a, **k))[1])
-    res = {}
-    for pt in (False, True):
-        monkeypatch.setattr(edge_block, "DXL_PT", pt)
-        seen.clear()
-        net.zero_grad(set_to_none=True)
-        pred = net(data)
-        ((pred["Ps_norm"] * cP).sum() + (pred["pts3D"] * cX).sum()).backward()
-        torch.cuda.synchronize()
-        res[pt] = {k: p.grad.detach().clone() for k, p in net.named_parameters()}
-        if pbwd:
-            assert seen and all(s == pt for s in seen), seen
-    for k, g0 in res[False].items():
-        assert torch.equal(res[True][k], g0), k
-
-
-@pytest.mark.parametrize("max_piece", [None, 48])
-def test_seam_lds_bitwise(device, max_piece):
-    """The forward seam with its inputs staged through LDS two tiles ahead (gasfm_tuning_set
-    seam_lds, csrc/edge_cam.hip edge_seam_lds_kernel) against the register-prefetch seam: the same
-    arithmetic, so the forward outputs and every parameter gradient are bitwise identical.  5 blocks
-    (seams into blocks 2-4 and the final update's LayerNorm-free seam); max_piece 48: items of 3
-    tiles, the last one ragged, split cameras with partial rows."""
-    from oracle.weights import deterministic_state_dict
-    sc = synthetic.scaled_config4(0.05, seed=19)
-    data = gasfm_amd.SceneData.from_synthetic(sc, max_piece=max_piece).to(device)
-    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=5))
-    sd = deterministic_state_dict(net.state_dict(), torch.float64)
-    net.load_state_dict({k: v.float() for k, v in sd.items()})
-    net = net.to(device)
-    gen = torch.Generator().manual_seed(9)
-    cP = torch.randn((sc.m, 3, 4), generator=gen).to(device)
-    cX = torch.randn((4, sc.n), generator=gen).to(device)
-    res = {}
-    for lds in (0, 1):
-        with _native.tuned(seam_lds=lds), _native.dispatch_record() as rec:
-            net.zero_grad(set_to_none=True)
-            pred = net(data)
-            ((pred["Ps_norm"] * cP).sum() + (pred["pts3D"] * cX).sum()).backward()
-            torch.cuda.synchronize()
-        assert rec.counts["seam_lds" if lds else "seam_reg"] >= 4 and rec.counts["seam_reg" if lds else "seam_lds"] == 0, \
-            rec.counts
-        res[lds] = (pred["Ps_norm"].detach().clone(), pred["pts3D"].detach().clone(),
-                    {k: p.grad.detach().clone() for k, p in net.named_parameters()})
-    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
-    for k, g0 in res[0][2].items():
-        assert torch.equal(res[1][2][k], g0), k

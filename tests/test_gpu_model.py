@@ -122,54 +122,10 @@ def test_oom_maps_to_torch_oom(device):
         _native.check(_native.GASFM_ERR_OOM, "probe")
 
 
-@pytest.mark.parametrize("capture", [False, True])
-def test_side_gemm_bitwise(device, capture):
-    """The camera side's weight-gradient GEMMs on a second stream (view_block.SIDE_GEMM, rows above
-    the small-M path) give bitwise the gradients of the one-stream order, eagerly and replayed."""
-    from gasfm_amd import graph_step, synthetic, view_block
-    sc = synthetic.windowed_scene(320, 8000, seed=7)
-    data = gasfm_amd.SceneData.from_synthetic(sc).to(device)
-    assert sc.m > view_block.SMALLM_ROWS
-    torch.manual_seed(0)
-    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=3)).to(device)
-    gen = torch.Generator().manual_seed(3)
-    cP = torch.randn((sc.m, 3, 4), generator=gen).to(device)
-    cX = torch.randn((4, sc.n), generator=gen).to(device)
-
-    def fwd_bwd():
-        pred = net(data)
-        loss = (pred["Ps_norm"] * cP).sum() + (pred["pts3D"] * cX).sum()
-        loss.backward()
-        return loss
-
-    def run(side):
-        prev, view_block.SIDE_GEMM = view_block.SIDE_GEMM, side
-        try:
-            for p in net.parameters():
-                p.grad = None
-            if capture:
-                step = graph_step.CapturedStep(fwd_bwd, net.parameters())
-                assert step.captured, step.fallback_reason
-                loss = step()
-            else:
-                loss = fwd_bwd()
-            torch.cuda.synchronize()
-            return float(loss), {k: p.grad.detach().clone() for k, p in net.named_parameters()}
-        finally:
-            view_block.SIDE_GEMM = prev
-
-    l1, g1 = run(False)
-    l2, g2 = run(True)
-    assert l1 == l2
-    bad = [k for k in g1 if not torch.equal(g1[k], g2[k])]
-    assert not bad, f"{len(bad)} of {len(g1)} gradients differ: {bad[:12]}"
-
-
-@pytest.mark.parametrize("capture", [False, True])
-def test_side_stream_bitwise(device, capture):
-    """Point side on the second stream (streams.py) gives bitwise the outputs and gradients of the
-    one-stream order, eagerly and replayed from a captured hipGraph."""
-    from gasfm_amd import graph_step, streams, synthetic
+def test_captured_step_bitwise_vs_eager(device):
+    """The whole step replayed from a captured hipGraph (graph_step.CapturedStep) gives bitwise the
+    loss and gradients of the eager step (every reduction is ordered: no float atomics)."""
+    from gasfm_amd import graph_step, synthetic
     sc = synthetic.scaled_config4(0.02, seed=7)
     data = gasfm_amd.SceneData.from_synthetic(sc).to(device)
     torch.manual_seed(0)
@@ -184,21 +140,17 @@ def test_side_stream_bitwise(device, capture):
         loss.backward()
         return loss
 
-    def run(side):
-        prev, streams.enabled = streams.enabled, side
-        try:
-            for p in net.parameters():
-                p.grad = None
-            if capture:
-                step = graph_step.CapturedStep(fwd_bwd, net.parameters())
-                assert step.captured, step.fallback_reason
-                loss = step()
-            else:
-                loss = fwd_bwd()
-            torch.cuda.synchronize()
-            return float(loss), {k: p.grad.detach().clone() for k, p in net.named_parameters()}
-        finally:
-            streams.enabled = prev
+    def run(capture):
+        for p in net.parameters():
+            p.grad = None
+        if capture:
+            step = graph_step.CapturedStep(fwd_bwd, net.parameters())
+            assert step.captured, step.fallback_reason
+            loss = step()
+        else:
+            loss = fwd_bwd()
+        torch.cuda.synchronize()
+        return float(loss), {k: p.grad.detach().clone() for k, p in net.named_parameters()}
 
     l1, g1 = run(False)
     l2, g2 = run(True)
