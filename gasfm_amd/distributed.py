@@ -290,6 +290,11 @@ def _packed_block(xs):
     return xs[0].as_strided((rows, tot), (tot, 1))
 
 
+def _as_rows(x):
+    """[rows, prod(other dims)] (reshape(rows, -1) is ambiguous for 0 rows)."""
+    return x.reshape(x.shape[0], int(np.prod(x.shape[1:])))
+
+
 class GatherRowsFn(torch.autograd.Function):
     """Own camera rows of several [own, w_k] tensors -> the full [m, w_k] tensors, with ONE
     all-gather of their concatenation (no concatenation when they already are one row block:
@@ -303,8 +308,8 @@ class GatherRowsFn(torch.autograd.Function):
         _, _, chunk, m = shard.cams
         flat = _packed_block(xs)
         if flat is None:
-            flat = torch.cat([x.reshape(x.shape[0], -1) for x in xs], 1) if len(xs) > 1 else xs[0].reshape(
-                xs[0].shape[0], -1)
+            # explicit widths: a rank without camera rows (camera_rows past m) has 0-row blocks
+            flat = torch.cat([_as_rows(x) for x in xs], 1) if len(xs) > 1 else _as_rows(xs[0])
         full = shard.all_gather(_pad_rows(flat, chunk))[:m]
         out, at = [], 0
         for x in xs:
@@ -362,6 +367,9 @@ class ShardedAttentionFn(torch.autograd.Function):
         XL, XR, att, bias, out, smax, ssum = ctx.saved_tensors
         dXL, dXR, datt, dbias = attn_backward_raw(XL, XR, att, bias, ctx.plan, ctx.heads, ctx.slope, out, smax,
                                                   ssum, g, defer=ctx.defer)
+        if ctx.plan.num_targets > 1:  # replicated targets: the rank-independent sum (edge_block.replicated_dbias)
+            from .edge_block import replicated_dbias
+            dbias = replicated_dbias(g, ctx.defer)
         return dXL, dXR, datt.view_as(att), dbias, None, None, None, None, None
 
 

@@ -162,6 +162,7 @@ class EdgeCamFn(torch.autograd.Function):
         ctx.att_shape = att.shape
         ctx.has_ln = ln_w is not None
         ctx.dwp = bool(dwp)
+        ctx.sharded = shard is not None
         ctx.defer = _native.defer_token(ln_w, ln_b, Wpt, bpt, Wc, bc, att, bias, Wp if dwp else None)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum, P0)
@@ -248,8 +249,25 @@ def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None):
     dW, db = tot[:o].view(64, 32), tot[o:o + 64]
     dgam = tot[o + 64:o + 96] if ctx.has_ln else None
     dbet = tot[o + 96:o + 128] if ctx.has_ln else None
+    dbias = ta[32:]
+    if getattr(ctx, "sharded", False):
+        dbias = replicated_dbias(g_c, ctx.defer)
     return (dP, dgam, dbet, dW[:32], db[:32], dW[32:], db[32:], dWp, None, None, dXR,
-            ta[:32].view(ctx.att_shape), ta[32:], None, None, None, None, None, None, None)
+            ta[:32].view(ctx.att_shape), dbias, None, None, None, None, None, None, None)
+
+
+def replicated_dbias(gout, defer):
+    """The attention bias gradient of a conv whose targets are replicated over point shards (the
+    camera direction): the column sum of the replicated output gradient over ALL targets, so every
+    rank gets the same bits.  The kernels' own d bias sums gout over the rank's local work items
+    (first item of each segment), whose split and order differ between ranks (round 5: caught by
+    the world-8 test, tests/test_distributed.py).  Deferred into the end-of-backward batched sums."""
+    g = gout.reshape(gout.shape[0], int(gout[0].numel()) if gout.shape[0] else gout.shape[-1])
+    if not (g.stride(1) == 1 and g.stride(0) >= g.shape[1]):  # e.g. an expanded (stride-0) gradient
+        g = g.contiguous()
+    # a view, as every other deferred sum reaches AccumulateGrad: the sum tensor itself is also held
+    # by the pending job list, so AccumulateGrad would copy it (unfilled) instead of adopting it
+    return _native.param_colsum(g, defer)[:]
 
 
 class DualAttentionFn(torch.autograd.Function):
@@ -274,6 +292,7 @@ class DualAttentionFn(torch.autograd.Function):
                                              shard.combine_items(N, XL.device))
         ctx.plans = (plan_pt, plan_cam)
         ctx.heads, ctx.slope, ctx.xl_sorted = heads, slope, xl_sorted
+        ctx.sharded = shard is not None
         ctx.defer = _native.defer_token(att_pt, att_cam, bias_pt, bias_cam)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(XL, XR_pt, XR_cam, att_pt, att_cam, bias_pt, bias_cam, out_p, mp, sp, out_c, mc, sc)
@@ -294,6 +313,8 @@ class DualAttentionFn(torch.autograd.Function):
                                                 defer=ctx.defer)
         _, dXRc, dattc, dbc = attn_backward_raw(XL[:, h:], XR_cam, att_cam, bias_cam, plan_cam, ctx.heads, ctx.slope,
                                                 out_c, mc, sc, g_c, dXL=dXL[:, h:], defer=ctx.defer)
+        if ctx.sharded:
+            dbc = replicated_dbias(g_c, ctx.defer)
         return (dXL, dXRp, dXRc, dattp.view_as(att_pt), dattc.view_as(att_cam), dbp, dbc, None, None, None, None,
                 None, None, None)
 
@@ -395,6 +416,7 @@ class SeamFn(torch.autograd.Function):
         ctx.att_shape = att.shape
         ctx.has_ln = ln_w is not None
         ctx.dwp = bool(dwp_n)
+        ctx.sharded = shard is not None
         ctx.defer = _native.defer_token(ln_w, ln_b, Wpt, bpt, Wc, bc, att, bias, Wp_n if dwp_n else None)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(P, P0, Wp_c, lnw_b, lnb_b, Pn, ln_w, ln_b, Wpt, Wc, bc, Wp_n, XR, attf, bias, out, smax,
@@ -567,6 +589,7 @@ class Seam0Fn(torch.autograd.Function):
         ctx.att_shape = att.shape
         ctx.has_ln = True
         ctx.dwp = bool(dwp_n)
+        ctx.sharded = shard is not None
         ctx.defer = _native.defer_token(ln_w, ln_b, Wpt, bpt, Wc, bc, att, bias, Wp_n if dwp_n else None)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(Pc, lna_w, lna_b, lnb_w, lnb_b, Wp_c, Wsk_c, Pn, ln_w, ln_b, Wpt, Wc, bc, Wp_n, XR,

@@ -236,10 +236,7 @@ def _run_sharded_vs_oracle(device, world, cameras, bounds=None, max_piece=64):
              for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=600) for _ in procs]
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    res = _collect(q, procs)
     res.sort(key=lambda t: t[0])
     assert [r[3] for r in res] == [(int(a), int(b)) for a, b in zip(res_bounds(sc, world, bounds)[:-1],
                                                                      res_bounds(sc, world, bounds)[1:])]
@@ -254,6 +251,32 @@ def _run_sharded_vs_oracle(device, world, cameras, bounds=None, max_piece=64):
     for rank in range(1, world):
         for k in g64:
             assert np.array_equal(res[0][4][k], res[rank][4][k]), (rank, k)
+
+
+def _collect(q, procs, timeout=600):
+    """One result per process; fails at once when a rank dies (its peers would wait forever in a
+    collective), terminating the rest."""
+    import queue
+    import time
+    res, t0 = [], time.time()
+    try:
+        while len(res) < len(procs):
+            try:
+                res.append(q.get(timeout=2))
+                continue
+            except queue.Empty:
+                pass
+            dead = [i for i, p in enumerate(procs) if p.exitcode not in (None, 0)]
+            assert not dead, f"rank(s) {dead} exited with {[procs[i].exitcode for i in dead]}"
+            assert time.time() - t0 < timeout, "sharded ranks timed out"
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
+    return res
 
 
 def res_bounds(sc, world, bounds):
