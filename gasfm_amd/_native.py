@@ -123,6 +123,9 @@ _SIGS = {
     "gasfm_gatt_fwd": (_i32, [_i32, _vp, _f32, _vp, _vp, _vp]),
     "gasfm_gatt_bwd": (_i32, [_i32, _vp, _f32, _vp, _vp, _vp]),
     "gasfm_gatt_merge": (_i32, [_i32, _vp, _i32, _i64, _vp]),
+    "gasfm_exchange_unpack": (_i32, [_vp, _i32, _i64, _i64, _i32, _i32, _i32, _vp, _i64, _i64, _i32, _vp, _vp]),
+    "gasfm_gatt_merge_unpack": (_i32, [_i32, _vp, _i32, _i64, _vp, _i32, _i64, _i64, _i32, _i32, _i32, _vp, _i64,
+                                       _vp]),
     "gasfm_pose_fwd": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "gasfm_pose_bwd": (_i32, [_vp, _i64, _i64, _vp, _vp, _i64, _vp]),
     "gasfm_esfm_part_rows": (_i32, [_i64]),
@@ -1249,17 +1252,48 @@ def gatt_bwd(probs, slope):
           "gasfm_gatt_bwd")
 
 
-def gatt_merge(probs, nrows, stride):
+def gatt_merge(probs, nrows, stride, unpack=None):
     """One launch: merge the nrows gathered partial rows of each problem (probs[q]["part"]: the first
-    row; rank r's at + r * stride floats) into its out / smax / ssum (gasfm_gatt_merge)."""
+    row; rank r's at + r * stride floats) into its out / smax / ssum (gasfm_gatt_merge).  unpack =
+    (G, blk, roff, chunk, dst [m, width]): the same launch also copies every rank's own rows out of
+    the gathered send blocks G (gasfm_gatt_merge_unpack)."""
     arr = (_GattProb * len(probs))()
     for q, d in enumerate(probs):
         a = arr[q]
         a.HC = int(d["bias"].numel())
         for k in ("bias", "out", "smax", "ssum", "part"):
             setattr(a, k, _p(d[k]))
-    check(lib().gasfm_gatt_merge(len(probs), ctypes.addressof(arr), int(nrows), int(stride), _stream(d["bias"])),
-          "gasfm_gatt_merge")
+    if unpack is None:
+        check(lib().gasfm_gatt_merge(len(probs), ctypes.addressof(arr), int(nrows), int(stride), _stream(d["bias"])),
+              "gasfm_gatt_merge")
+        return
+    G, blk, roff, chunk, dst = unpack
+    _exchange_args(G, dst, None)
+    check(lib().gasfm_gatt_merge_unpack(len(probs), ctypes.addressof(arr), int(nrows), int(stride), _p(G), int(nrows),
+                                        int(blk), int(roff), int(chunk), int(dst.shape[1]), int(dst.shape[0]), _p(dst),
+                                        dst.stride(0) if dst.shape[0] > 1 else dst.shape[1], _stream(G)),
+          "gasfm_gatt_merge_unpack")
+
+
+def _exchange_args(G, rows_dst, sum_dst):
+    for t, nm in ((G, "G"), (rows_dst, "rows_dst"), (sum_dst, "sum_dst")):
+        if t is not None and (not t.is_cuda or t.dtype != torch.float32 or t.stride(-1) != 1):
+            raise TypeError(f"exchange_unpack: {nm} must be float32 CUDA with unit column stride")
+
+
+def exchange_unpack(G, W, blk, rows=None, sums=None):
+    """Unpack W gathered send blocks of blk floats (gasfm_exchange_unpack): rows = (roff, chunk, dst
+    [m, width]) copies every rank's own rows into dst, sums = (soff, dst [sn]) the rank-order sum of
+    the W partial vectors."""
+    roff, chunk, rdst = rows if rows is not None else (0, 1, None)
+    soff, sdst = sums if sums is not None else (0, None)
+    _exchange_args(G, rdst, sdst)
+    width = int(rdst.shape[1]) if rdst is not None else 4
+    m = int(rdst.shape[0]) if rdst is not None else 0
+    ld = (rdst.stride(0) if m > 1 else width) if rdst is not None else 4
+    check(lib().gasfm_exchange_unpack(_p(G), int(W), int(blk), int(roff), int(chunk), width, m, _p(rdst), ld,
+                                      int(soff), int(sdst.numel()) if sdst is not None else 0, _p(sdst), _stream(G)),
+          "gasfm_exchange_unpack")
 
 
 # ---------------------------------------------------------------- device scene builder (scene_build.hip)

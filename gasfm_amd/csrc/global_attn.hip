@@ -595,10 +595,55 @@ __global__ __launch_bounds__(kT) void gatt_bwd_kernel(GaArgs a) {
     bwd_points(p, blk, a.slope, &flag);
 }
 
-// the sharded forward's second half: problem blockIdx.x's W gathered partial rows -> out / stats
-__global__ __launch_bounds__(kT) void gatt_merge_kernel(GaArgs a) {
+// ---- the camera-sharded block exchange (round 5): ONE all-gather of per-rank send blocks carries
+// several payloads; these unpack it.  Rank r's block (blk floats) holds at roff its chunk own rows of
+// width floats (rows past the scene's m are padding) and, at soff, a partial vector of sn floats.
+struct Unpack {
+  const float* G;    // [W, blk] gathered send blocks
+  int64_t blk, roff, soff, ld_dst;
+  float* rows_dst;   // [m, width] (row stride ld_dst) or null
+  float* sum_dst;    // [sn] or null: the W partial vectors summed in rank order
+  int W, chunk, width, m, sn;
+};
+
+__device__ __forceinline__ int unpack_units(const Unpack& u) {
+  return (u.rows_dst ? u.m * (u.width / 4) : 0) + (u.sum_dst ? u.sn / 4 : 0);
+}
+
+// float4 unit k of the unpack: a row piece, then a piece of the rank-order sum
+__device__ __forceinline__ void unpack_unit(const Unpack& u, int k) {
+  const int nr = u.rows_dst ? u.m * (u.width / 4) : 0;
+  if (k < nr) {
+    const int w4 = u.width / 4, c = k / w4, q = k % w4;
+    const float4 v = *reinterpret_cast<const float4*>(u.G + int64_t(c / u.chunk) * u.blk + u.roff +
+                                                      int64_t(c % u.chunk) * u.width + 4 * q);
+    *reinterpret_cast<float4*>(u.rows_dst + int64_t(c) * u.ld_dst + 4 * q) = v;
+    return;
+  }
+  const int j = k - nr;
+  float4 acc = *reinterpret_cast<const float4*>(u.G + u.soff + 4 * j);
+  for (int r = 1; r < u.W; ++r) {
+    const float4 v = *reinterpret_cast<const float4*>(u.G + int64_t(r) * u.blk + u.soff + 4 * j);
+    acc = make_float4(acc.x + v.x, acc.y + v.y, acc.z + v.z, acc.w + v.w);
+  }
+  *reinterpret_cast<float4*>(u.sum_dst + 4 * j) = acc;
+}
+
+__global__ __launch_bounds__(kT) void exchange_unpack_kernel(Unpack u) {
+  const int k = int(blockIdx.x) * kT + int(threadIdx.x);
+  if (k < unpack_units(u)) unpack_unit(u, k);
+}
+
+// the sharded forward's second half: problem blockIdx.x's W gathered partial rows -> out / stats;
+// blocks past nprob unpack the exchange's row payload (the view hub's SV | XR rows)
+__global__ __launch_bounds__(kT) void gatt_merge_kernel(GaArgs a, Unpack u) {
   __shared__ float sc[16];
-  merge_fwd(a.p[blockIdx.x], sc);
+  if (int(blockIdx.x) < a.nprob) {
+    merge_fwd(a.p[blockIdx.x], sc);
+    return;
+  }
+  const int k = (int(blockIdx.x) - a.nprob) * kT + int(threadIdx.x);
+  if (k < unpack_units(u)) unpack_unit(u, k);
 }
 
 int chunk_of(int C) { return C == 256 ? kChunkV : kChunkP; }
@@ -697,8 +742,60 @@ extern "C" int gasfm_gatt_fwd(int32_t nprob, const gasfm_gatt_prob* probs, float
   return launch_status("gasfm_gatt_fwd");
 }
 
+static int unpack_check(const Unpack& u, const char* who) {
+  GASFM_REQUIRE(u.G && u.W >= 1 && u.blk % 4 == 0 && u.roff % 4 == 0 && u.soff % 4 == 0 && u.width % 4 == 0 &&
+                    u.ld_dst % 4 == 0 && u.sn % 4 == 0 && u.m >= 0 && u.chunk >= 1 && u.m <= int64_t(u.W) * u.chunk &&
+                    aligned16(u.G) && aligned16(u.rows_dst) && aligned16(u.sum_dst) &&
+                    (!u.rows_dst || (u.roff + int64_t(u.chunk) * u.width <= u.blk && u.ld_dst >= u.width)) &&
+                    (!u.sum_dst || u.soff + u.sn <= u.blk),
+                "%s: W=%d blk=%lld roff=%lld chunk=%d width=%d m=%d soff=%lld sn=%d (layout / alignment)", who, u.W,
+                (long long)u.blk, (long long)u.roff, u.chunk, u.width, u.m, (long long)u.soff, u.sn);
+  return GASFM_OK;
+}
+
+static Unpack make_unpack(const float* G, int32_t W, int64_t blk, int64_t roff, int32_t chunk, int32_t width, int32_t m,
+                          float* rows_dst, int64_t ld_dst, int64_t soff, int32_t sn, float* sum_dst) {
+  Unpack u;
+  u.G = G, u.blk = blk, u.roff = roff, u.soff = soff, u.ld_dst = ld_dst;
+  u.rows_dst = rows_dst, u.sum_dst = sum_dst;
+  u.W = W, u.chunk = chunk, u.width = width, u.m = m, u.sn = sn;
+  return u;
+}
+
+extern "C" int gasfm_exchange_unpack(const float* G, int32_t W, int64_t blk, int64_t roff, int32_t chunk,
+                                     int32_t width, int32_t m, float* rows_dst, int64_t ld_dst, int64_t soff,
+                                     int32_t sn, float* sum_dst, void* stream) {
+  const Unpack u = make_unpack(G, W, blk, roff, chunk, width, m, rows_dst, ld_dst, soff, sn, sum_dst);
+  const int s0 = unpack_check(u, "gasfm_exchange_unpack");
+  if (s0 != GASFM_OK) return s0;
+  const int units = (rows_dst ? m * (width / 4) : 0) + (sum_dst ? sn / 4 : 0);
+  if (units == 0) return GASFM_OK;
+  hipLaunchKernelGGL(exchange_unpack_kernel, dim3((units + kT - 1) / kT), dim3(kT), 0,
+                     reinterpret_cast<hipStream_t>(stream), u);
+  return launch_status("gasfm_exchange_unpack");
+}
+
+static int merge_launch(int32_t nprob, const gasfm_gatt_prob* probs, int32_t nrows, int64_t stride, const Unpack& u,
+                        void* stream);
+
 extern "C" int gasfm_gatt_merge(int32_t nprob, const gasfm_gatt_prob* probs, int32_t nrows, int64_t stride,
                                 void* stream) {
+  Unpack u{};
+  return merge_launch(nprob, probs, nrows, stride, u, stream);
+}
+
+extern "C" int gasfm_gatt_merge_unpack(int32_t nprob, const gasfm_gatt_prob* probs, int32_t nrows, int64_t stride,
+                                       const float* G, int32_t W, int64_t blk, int64_t roff, int32_t chunk,
+                                       int32_t width, int32_t m, float* rows_dst, int64_t ld_dst, void* stream) {
+  GASFM_REQUIRE(rows_dst, "gasfm_gatt_merge_unpack: rows_dst");
+  const Unpack u = make_unpack(G, W, blk, roff, chunk, width, m, rows_dst, ld_dst, 0, 0, nullptr);
+  const int s0 = unpack_check(u, "gasfm_gatt_merge_unpack");
+  if (s0 != GASFM_OK) return s0;
+  return merge_launch(nprob, probs, nrows, stride, u, stream);
+}
+
+static int merge_launch(int32_t nprob, const gasfm_gatt_prob* probs, int32_t nrows, int64_t stride, const Unpack& u,
+                        void* stream) {
   GASFM_REQUIRE(nprob >= 1 && nprob <= kMaxProb && probs && nrows >= 1, "gasfm_gatt_merge: nprob=%d nrows=%d", nprob,
                 nrows);
   GaArgs a{};
@@ -716,7 +813,9 @@ extern "C" int gasfm_gatt_merge(int32_t nprob, const gasfm_gatt_prob* probs, int
     p.nblk = nrows;
     p.ngroups = 1;
   }
-  hipLaunchKernelGGL(gatt_merge_kernel, dim3(nprob), dim3(kT), 0, reinterpret_cast<hipStream_t>(stream), a);
+  const int units = u.G ? (u.rows_dst ? u.m * (u.width / 4) : 0) + (u.sum_dst ? u.sn / 4 : 0) : 0;
+  hipLaunchKernelGGL(gatt_merge_kernel, dim3(nprob + (units + kT - 1) / kT), dim3(kT), 0,
+                     reinterpret_cast<hipStream_t>(stream), a, u);
   return launch_status("gasfm_gatt_merge");
 }
 

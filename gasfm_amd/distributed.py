@@ -241,8 +241,10 @@ class AllReduceGradN(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *gs):
         dev, dt = ctx.devdtype
-        flat = torch.cat([(g if g is not None else torch.zeros(sh, device=dev, dtype=dt)).reshape(-1)
-                          for g, sh in zip(gs, ctx.shapes)])
+        flat = _adjacent_flat(gs, ctx.shapes)
+        if flat is None:
+            flat = torch.cat([(g if g is not None else torch.zeros(sh, device=dev, dtype=dt)).reshape(-1)
+                              for g, sh in zip(gs, ctx.shapes)])
         ctx.shard.all_reduce_(flat)
         out, at = [], 0
         for sh in ctx.shapes:
@@ -252,27 +254,102 @@ class AllReduceGradN(torch.autograd.Function):
         return (None,) + tuple(out)
 
 
+def _adjacent_flat(gs, shapes):
+    """The one flat buffer the gradients gs already are consecutive contiguous views of, in order
+    (the edge backward writes the boundary's dSv | dSg | dXR that way: edge_block._boundary_buffers),
+    else None (then they are concatenated)."""
+    if any(g is None or not g.is_contiguous() or g.shape != sh for g, sh in zip(gs, shapes)):
+        return None
+    at = gs[0].data_ptr()
+    for g in gs:
+        if g.data_ptr() != at or g.untyped_storage().data_ptr() != gs[0].untyped_storage().data_ptr():
+            return None
+        at += g.numel() * g.element_size()
+    total = sum(g.numel() for g in gs)
+    base = gs[0]
+    return base.as_strided((total,), (1,), base.storage_offset())
+
+
 def _pad_rows(x, rows):
     if x.shape[0] == rows:
         return x.contiguous()
     return torch.cat([x, x.new_zeros((rows - x.shape[0],) + tuple(x.shape[1:]))])
 
 
+def _c4(n):
+    return -(-n // 4) * 4
+
+
+class BlockExchange:
+    """A camera-sharded block's collectives, two per block instead of four (round 5):
+
+    forward   ONE all-gather of [own SV | XR rows (chunk x 64) | view->global partial row |
+              points->global partial row] per rank (view hub -> send block <- global convs'
+              partial rows), then ONE launch merges the global partials and unpacks every rank's
+              rows (gasfm_gatt_merge_unpack): ShardedGlobalExchangeFn.
+    backward  ONE all-gather of [own camera-aggregate gradient rows (chunk x 32) | this rank's
+              partial gradient of the two global target rows] (OwnRowsFn), then ONE launch unpacks
+              the rows and sums the W partial target-row gradients in rank order into ``red``
+              (gasfm_exchange_unpack).  The global convs' backward (which runs first) writes its
+              partial into the send block and hands ``red`` to autograd before it is filled: its
+              consumer, the previous block's GlobalChainFn, runs only after this block's camera
+              attention backward (which needs OwnRowsFn's output), see ShardedGlobalExchangeFn."""
+
+    def __init__(self, shard, HCv, HCp, heads, dev):
+        c0, c1, chunk, m = shard.cams
+        self.shard, self.chunk, self.m, self.own = shard, chunk, m, c1 - c0
+        self.HCv, self.HCp, self.dev = HCv, HCp, dev
+        self.Lv, self.Lp = HCv + 2 * heads, HCp + 2 * heads
+        self.f_ov = chunk * 64
+        self.f_op = _c4(self.f_ov + self.Lv)
+        self.f_blk = _c4(self.f_op + self.Lp)
+        self.b_rows = chunk * 32
+        self.b_blk = _c4(self.b_rows + HCv + HCp)
+        self.send_f = torch.empty(self.f_blk, dtype=torch.float32, device=dev)
+        self.send_b = None
+        self.red = None  # [HCv + HCp]: the reduced target-row gradient (filled by OwnRowsFn.backward)
+
+    def rows_out(self):
+        """The view hub's [own, 64] SV | XR destination inside the forward send block."""
+        return self.send_f[:self.own * 64].view(self.own, 64)
+
+    def backward_block(self):
+        if self.send_b is None:
+            self.send_b = torch.empty(self.b_blk, dtype=torch.float32, device=self.dev)
+        return self.send_b
+
+    def dagg_out(self):
+        """The view tail's own-row camera-aggregate gradient [own, 32] inside the backward send block."""
+        return self.backward_block()[:self.own * 32].view(self.own, 32)
+
+
 class OwnRowsFn(torch.autograd.Function):
     """Replicated camera rows [m, ...] -> this rank's rows [c0, c1); the backward all-gathers the
-    own-row gradients (each rank's slice is the full gradient of its rows)."""
+    own-row gradients (each rank's slice is the full gradient of its rows).  exch (BlockExchange):
+    the gather also carries the global target rows' partial gradients (and sums them)."""
 
     @staticmethod
-    def forward(ctx, x, shard):
-        ctx.shard = shard
+    def forward(ctx, x, shard, exch=None):
+        ctx.shard, ctx.exch = shard, exch
         c0, c1, _, _ = shard.cams
         return x[c0:c1]
 
     @staticmethod
     def backward(ctx, g):
-        shard = ctx.shard
+        shard, ex = ctx.shard, ctx.exch
         _, _, chunk, m = shard.cams
-        return shard.all_gather(_pad_rows(g, chunk))[:m], None
+        if ex is None or g.dim() != 2 or g.shape[1] != 32:
+            return shard.all_gather(_pad_rows(g, chunk))[:m], None, None
+        send = ex.backward_block()
+        head = ex.dagg_out()
+        if g.data_ptr() != head.data_ptr() or not g.is_contiguous():  # the view tail wrote elsewhere
+            head.copy_(g)
+        G = shard.all_gather(send.view(1, -1)).view(-1)
+        full = torch.empty((m, 32), dtype=torch.float32, device=g.device)
+        sums = (ex.b_rows, ex.red) if ex.red is not None else None
+        _native.exchange_unpack(G, shard.world, ex.b_blk, rows=(0, chunk, full), sums=sums)
+        ctx.exch = None
+        return full, None, None
 
 
 def _packed_block(xs):
@@ -325,8 +402,8 @@ class GatherRowsFn(torch.autograd.Function):
         return (None,) + tuple(None if g is None else g[c0:c1].contiguous() for g in gs)
 
 
-def own_rows(x, shard):
-    return x if shard is None or shard.cams is None else OwnRowsFn.apply(x, shard)
+def own_rows(x, shard, exch=None):
+    return x if shard is None or shard.cams is None else OwnRowsFn.apply(x, shard, exch)
 
 
 def gather_rows(shard, *xs):
@@ -450,6 +527,82 @@ class ShardedGlobalAttentionFn(torch.autograd.Function):
         ctx.shard.all_reduce_(flat)
         return (dXLv, flat[:, :HCv], dattv.view_as(att_v), dbv, dXLp, flat[:, HCv:], dattp.view_as(att_p), dbp,
                 None, None, None, None)
+
+
+class ShardedGlobalExchangeFn(torch.autograd.Function):
+    """ShardedGlobalAttentionFn and GatherRowsFn(SV, XR) of a camera-sharded block with ONE
+    all-gather (BlockExchange): the view hub wrote this rank's [own, 64] SV | XR rows into the
+    forward send block, the global convs write their two partial rows after them; one launch merges
+    the partials and unpacks every rank's rows.  -> (xcat [1, HCv + HCp], SV [m, 32], XR [m, 32]).
+
+    Backward: the global convs against the merged statistics; their target-row gradients (partial
+    per rank) go into the backward send block and are summed by the NEXT collective of this block,
+    OwnRowsFn's (defer_xr; the returned gradients are views of exch.red, filled there: their
+    consumer is the previous block's GlobalChainFn, whose backward also needs this block's boundary
+    all-reduce, which comes after OwnRowsFn's).  Without defer_xr (block 0: the target rows are
+    lin_r(0), consumed at once) they are all-reduced here.  SV / XR: own-row slices of the
+    (already summed) gradients, as GatherRowsFn."""
+
+    @staticmethod
+    def forward(ctx, XLv, XRv, att_v, bias_v, XLp, XRp, att_p, bias_p, SV_own, XR_own, plans, heads, slope, shard,
+                exch, defer_xr):
+        plan_v, plan_p = plans
+        HCv, HCp = att_v.numel(), att_p.numel()
+        dev = XLv.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        ex = exch
+        rows = ex.rows_out()
+        if ex.own and (SV_own.data_ptr() != rows.data_ptr() or XR_own.data_ptr() != rows[:, 32:].data_ptr()):
+            rows[:, :32].copy_(SV_own)
+            rows[:, 32:].copy_(XR_own)
+        send = ex.send_f
+        _native.gatt_fwd([gatt_prob(plan_v, XLv, XRv, att_v, bias_v, part=send[ex.f_ov:ex.f_ov + ex.Lv]),
+                          gatt_prob(plan_p, XLp, XRp, att_p, bias_p, part=send[ex.f_op:ex.f_op + ex.Lp])], slope)
+        G = shard.all_gather(send.view(1, -1)).view(-1)
+        xcat = torch.empty((1, HCv + HCp), **f32)
+        stats = torch.empty((4, heads), **f32)
+        full = torch.empty((ex.m, 64), **f32)
+        _native.gatt_merge([dict(part=G[ex.f_ov:], bias=bias_v, out=xcat[:, :HCv], smax=stats[0], ssum=stats[1]),
+                            dict(part=G[ex.f_op:], bias=bias_p, out=xcat[:, HCv:], smax=stats[2], ssum=stats[3])],
+                           shard.world, ex.f_blk, unpack=(G, ex.f_blk, 0, ex.chunk, full))
+        ctx.plans, ctx.heads, ctx.slope, ctx.shard, ctx.HCv = (plan_v, plan_p), heads, slope, shard, HCv
+        ctx.exch, ctx.defer_xr = ex, bool(defer_xr)
+        ctx.defer = _native.defer_token(att_v, bias_v, att_p, bias_p)
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(XLv, XRv, att_v, bias_v, XLp, XRp, att_p, bias_p, xcat, stats)
+        return xcat, full[:, :32], full[:, 32:]
+
+    @staticmethod
+    def backward(ctx, g, gSV, gXR):
+        XLv, XRv, att_v, bias_v, XLp, XRp, att_p, bias_p, xcat, stats = ctx.saved_tensors
+        plan_v, plan_p = ctx.plans
+        HCv = ctx.HCv
+        HCp = xcat.shape[1] - HCv
+        ex, shard = ctx.exch, ctx.shard
+        c0, c1, _, _ = shard.cams
+        dev = xcat.device
+        g = g.contiguous() if g is not None else torch.zeros_like(xcat)
+        if ctx.defer_xr:  # the partial into the backward send block, summed by OwnRowsFn's gather
+            send = ex.backward_block()
+            flat = send[ex.b_rows:ex.b_rows + HCv + HCp].view(1, HCv + HCp)
+            ex.red = torch.empty(HCv + HCp, dtype=torch.float32, device=dev)
+            red = ex.red.view(1, HCv + HCp)
+        else:
+            flat = torch.empty_like(xcat)
+            red = flat
+        dXLv, dXLp = gatt_dxl(plan_v, XLv, HCv), gatt_dxl(plan_p, XLp, HCp)
+        dab = torch.empty(2 * (HCv + HCp), dtype=torch.float32, device=dev)
+        _native.gatt_bwd([gatt_prob(plan_v, XLv, XRv, att_v, bias_v, out=xcat[:, :HCv], smax=stats[0], ssum=stats[1],
+                                    gout=g[:, :HCv], dXL=dXLv, dXR=flat[:, :HCv], datt=dab[:2 * HCv]),
+                          gatt_prob(plan_p, XLp, XRp, att_p, bias_p, out=xcat[:, HCv:], smax=stats[2], ssum=stats[3],
+                                    gout=g[:, HCv:], dXL=dXLp, dXR=flat[:, HCv:], datt=dab[2 * HCv:])], ctx.slope)
+        if not ctx.defer_xr:
+            shard.all_reduce_(flat)
+        o = 2 * HCv
+        own = lambda t: None if t is None else t[c0:c1].contiguous()  # noqa: E731
+        return (dXLv, red[:, :HCv].view_as(XRv), dab[:HCv].view_as(att_v), dab[HCv:o].view_as(bias_v), dXLp,
+                red[:, HCv:].view_as(XRp), dab[o:o + HCp].view_as(att_p), dab[o + HCp:].view_as(bias_p),
+                own(gSV), own(gXR), None, None, None, None, None, None)
 
 
 def _pack_layout(a, b):

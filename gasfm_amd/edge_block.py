@@ -184,11 +184,12 @@ def _dwp_torch(P, ln_w, ln_b, eps, dRes, P0):
     return PROJ_SCALE * (dRes.t() @ ph)
 
 
-def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None):
+def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None, dXR=None):
     """EdgeCamFn's backward from its saved state (ctx attributes eps, heads, slope, plan, att_shape,
     has_ln, dwp, defer): the 20 input gradients of EdgeCamFn.forward.  epi: the previous block's
     epilogue outputs to fill from dP (edge_cam_pbwd's EPI), or None; ctx.epi_done tells whether
-    they were filled."""
+    they were filled.  dXR: the [num_targets, 32] buffer for the camera target rows' gradient (a
+    view of the boundary all-reduce's payload, _boundary_buffers), or None."""
     P, ln_w, ln_b, Wpt, Wc, bc, Wp, XR, attf, bias, out, smax, ssum, P0 = saved
     plan = ctx.plan
     E, dev = P.shape[0], P.device
@@ -199,7 +200,8 @@ def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None):
     dWp = None
     if CAM_PBWD and plan.n_items:
         # camera attention backward + prologue backward in one kernel (gasfm_edge_cam_pbwd)
-        dXR = torch.empty((plan.num_targets, 32), dtype=torch.float32, device=dev)
+        if dXR is None:
+            dXR = torch.empty((plan.num_targets, 32), dtype=torch.float32, device=dev)
         part_dxr = torch.empty((plan.n_part_rows, 32), dtype=torch.float32, device=dev) if plan.n_slots else None
         wcols = (34 if P0 is not None else 32) if dwp else 0
         rows, cols = _native.edge_cam_pbwd_part_shape(plan.n_items, wcols)
@@ -221,7 +223,8 @@ def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None):
     else:
         # camera attention backward (XLc recomputed from P): dXLc, dXR, [datt | dbias] partials
         dXLc = torch.empty((E, 32), dtype=torch.float32, device=dev)
-        dXR = torch.empty((plan.num_targets, 32), dtype=torch.float32, device=dev)
+        if dXR is None:
+            dXR = torch.empty((plan.num_targets, 32), dtype=torch.float32, device=dev)
         part_dxr = torch.empty((plan.n_part_rows, 32), dtype=torch.float32, device=dev) if plan.n_slots else None
         rows, cols = _native.edge_cam_bwd_part_shape(plan.n_items)
         part_a = (torch.empty if plan.n_items else torch.zeros)((rows, cols), dtype=torch.float32, device=dev)
@@ -332,6 +335,7 @@ class EdgeEpilogueFn(torch.autograd.Function):
         ctx.sg_shape = Sg.shape
         ctx.wp_by_cam = bool(wp_by_cam)
         ctx.defer = _native.defer_token(Wp)
+        ctx.defer_b = _native.defer_token(bp)
         ctx.save_for_backward(P, P0, Wp_c, ln_w, ln_b)
         return out
 
@@ -340,11 +344,12 @@ class EdgeEpilogueFn(torch.autograd.Function):
         return _epilogue_backward(ctx, ctx.saved_tensors, dPo)
 
 
-def _epilogue_backward(ctx, saved, dPo, folded=None):
+def _epilogue_backward(ctx, saved, dPo, folded=None, dSg=None):
     """EdgeEpilogueFn's backward from its saved state (ctx attributes eps, edges, sg_shape,
-    wp_by_cam, defer): the 13 input gradients of EdgeEpilogueFn.forward (the block input's through
-    the token).  folded: (dSv, part_dsv, dP0) already filled by the next block's edge_cam_pbwd
-    (SeamFn), so edge_epilogue_bwd does not run (Wp's gradient is then the block's EdgeCamFn's)."""
+    wp_by_cam, defer, defer_b): the 13 input gradients of EdgeEpilogueFn.forward (the block input's
+    through the token).  folded: (dSv, part_dsv, dP0) already filled by the next block's
+    edge_cam_pbwd (SeamFn), so edge_epilogue_bwd does not run (Wp's gradient is then the block's
+    EdgeCamFn's).  dSg: its [32] destination (a view of the boundary all-reduce's payload) or None."""
     P, P0, Wp, ln_w, ln_b = saved
     edges = ctx.edges
     dPo = dPo.contiguous()
@@ -366,13 +371,25 @@ def _epilogue_backward(ctx, saved, dPo, folded=None):
         if not ctx.wp_by_cam:
             dWp = _native.param_colsum(part_w, ctx.defer).view(32, Wp.shape[1])
     bwd_combine(pc, part_dsv, 32, dSv)
-    dSg = _native.colsum(dSv)          # == d bias_proj: every edge belongs to one camera
+    dSg_shared = dSg is not None
+    dSg = _native.colsum(dSv, out=dSg)  # == d bias_proj: every edge belongs to one camera
     # point side: dSp = per-point sum of dP'/4 through the point permutation
     dSp = torch.empty((edges.n, 32), dtype=torch.float32, device=dev)
     part_dsp = torch.empty((max(pp.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
     _native.segment_rowsum(pp.items, pp.n_items, pp.perm, dPo, PROJ_SCALE, dSp, part_dsp)
     bwd_combine(pp, part_dsp, 32, dSp)
-    return (None, dP0, dPo, dSp, dSv, dSg.view(ctx.sg_shape), dWp, dSg.clone(), None, None, None, None, None)
+    return (None, dP0, dPo, dSp, dSv, dSg.view(ctx.sg_shape), dWp,
+            _bias_grad(dSv, dSg, getattr(ctx, "defer_b", False), shared=dSg_shared), None, None, None, None, None)
+
+
+def _bias_grad(dSv, dSg, defer, shared=False):
+    """lin_proj's bias gradient: the same column sum as dSg (every edge belongs to one camera), as
+    its own tensor -- a deferred sum in the end-of-backward batch (no clone launch), or a clone of
+    dSg.  shared: dSv / dSg are views of the boundary all-reduce's payload (_boundary_buffers),
+    summed over the ranks IN PLACE before the pass ends, so the rank-local sum is taken now."""
+    if defer and not shared:
+        return _native.param_colsum(dSv, defer)[:]
+    return dSg.clone()
 
 
 class SeamFn(torch.autograd.Function):
@@ -411,6 +428,7 @@ class SeamFn(torch.autograd.Function):
         ctx.e_eps, ctx.edges, ctx.sg_shape = eps_b, edges, Sg.shape
         ctx.e_wp_by_cam = bool(wp_by_cam)
         ctx.e_defer = _native.defer_token(Wp)
+        ctx.e_defer_b = _native.defer_token(bp)
         # EdgeCamFn's state
         ctx.eps, ctx.heads, ctx.slope, ctx.plan = eps, heads, slope, plan
         ctx.att_shape = att.shape
@@ -431,28 +449,42 @@ class SeamFn(torch.autograd.Function):
         epi, cam = saved[:ctx.n_epi], saved[ctx.n_epi:]
         dRes = dtoken.contiguous() if (dtoken is not None and dtoken.stride(0) != 0) else None
         edges = ctx.edges
+        dev = epi[0].device
+        # sharded: block b's dSv / dSg and block b+1's camera target-row gradient, all partial per
+        # rank, side by side in the one buffer the boundary all-reduce sums (AllReduceGradN: no cat)
+        bnd = _boundary_buffers(edges.m, ctx.plan.num_targets, dev) if ctx.sharded else None
         folded = None
         if EPI_FOLD and ctx.e_wp_by_cam and gPn is None and ctx.plan is edges.plans["proj2view"]:
             # block b's dSv / dP0 from the dP' this launch produces (edge_cam_pbwd EPI)
             P_b, P0_b, Wp_b = epi[0], epi[1], epi[2]
-            dev = P_b.device
-            dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
+            dSv = bnd[0] if bnd is not None else torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
             part_dsv = torch.empty((max(ctx.plan.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
             dP0 = torch.empty((P_b.shape[0], 2), dtype=torch.float32, device=dev) if P0_b is not None else None
             folded = (dSv, part_dsv, dP0)
-        gc = _cam_backward(ctx, cam, dXLp, g_c, dRes, epi=None if folded is None else (Wp_b, PROJ_SCALE) + folded)
+        gc = _cam_backward(ctx, cam, dXLp, g_c, dRes, epi=None if folded is None else (Wp_b, PROJ_SCALE) + folded,
+                           dXR=bnd[2] if bnd is not None else None)
         if not ctx.epi_done:
             folded = None
         dPn = gc[0] if gPn is None else gc[0] + gPn
-        ectx = _EpiState(ctx.e_eps, edges, ctx.sg_shape, ctx.e_defer, ctx.e_wp_by_cam)
-        ge = _epilogue_backward(ectx, epi, dPn, folded)
+        ectx = _EpiState(ctx.e_eps, edges, ctx.sg_shape, ctx.e_defer, ctx.e_wp_by_cam, ctx.e_defer_b)
+        ge = _epilogue_backward(ectx, epi, dPn, folded,
+                                dSg=bnd[1] if (bnd is not None and folded is not None) else None)
         return ge + gc[1:]
 
 
+def _boundary_buffers(m, n_xr, dev):
+    """(dSv [m, 32], dSg [32], dXR [n_xr, 32]) as consecutive views of ONE buffer: the payload of the
+    point-sharded block boundary's all-reduce (distributed.AllReduceGradN sums it in place when its
+    gradients arrive as these views, in this order)."""
+    flat = torch.empty(m * 32 + 32 + n_xr * 32, dtype=torch.float32, device=dev)
+    return flat[:m * 32].view(m, 32), flat[m * 32:m * 32 + 32], flat[m * 32 + 32:].view(n_xr, 32)
+
+
 class _EpiState:
-    def __init__(self, eps, edges, sg_shape, defer, wp_by_cam=False):
+    def __init__(self, eps, edges, sg_shape, defer, wp_by_cam=False, defer_b=False):
         self.eps, self.edges, self.sg_shape, self.defer = eps, edges, sg_shape, defer
         self.wp_by_cam = wp_by_cam
+        self.defer_b = defer_b
 
 
 class PendingEpilogue:
@@ -520,6 +552,7 @@ class Block0EpilogueFn(torch.autograd.Function):
                                    bp.contiguous(), Wsk.contiguous(), bsk.contiguous(), Sp.contiguous(),
                                    _rows(Sv), Sg.reshape(-1).contiguous(), PROJ_SCALE, out)
         ctx.eps, ctx.edges, ctx.sg_shape = eps, edges, Sg.shape
+        ctx.defer_b = _native.defer_token(bp)
         ctx.save_for_backward(P, lna_w, lna_b, lnb_w, lnb_b, Wp, Wsk)
         return out
 
@@ -528,16 +561,17 @@ class Block0EpilogueFn(torch.autograd.Function):
         return _epilogue0_backward(ctx, ctx.saved_tensors, dPo)
 
 
-def _epilogue0_backward(ctx, saved, dPo):
-    """Block0EpilogueFn's backward from its saved state (ctx attributes eps, edges, sg_shape): its 15
-    input gradients."""
+def _epilogue0_backward(ctx, saved, dPo, bnd=None):
+    """Block0EpilogueFn's backward from its saved state (ctx attributes eps, edges, sg_shape,
+    defer_b): its 15 input gradients.  bnd: the boundary all-reduce's (dSv, dSg, ...) views
+    (_boundary_buffers) or None."""
     P, lna_w, lna_b, lnb_w, lnb_b, Wp, Wsk = saved
     edges = ctx.edges
     dPo = dPo.contiguous()
     dev = P.device
     E = P.shape[0]
     pc, pp = edges.plans["proj2view"], edges.plans["proj2scenepoint"]
-    dSv = torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
+    dSv = bnd[0] if bnd is not None else torch.empty((edges.m, 32), dtype=torch.float32, device=dev)
     part_dsv = torch.empty((max(pc.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
     aux = torch.empty((E, 4), dtype=torch.float32, device=dev)
     rows = _native.edge0_part_rows(1, E, pc.n_items)
@@ -546,12 +580,13 @@ def _epilogue0_backward(ctx, saved, dPo):
                                Wp.contiguous(), Wsk.contiguous(), PROJ_SCALE, dSv, part_dsv, aux, part)
     bwd_combine(pc, part_dsv, 32, dSv)
     tot = _native.colsum(part)
-    dSg = _native.colsum(dSv)
+    dSg = _native.colsum(dSv, out=bnd[1] if bnd is not None else None)
     dSp = torch.empty((edges.n, 32), dtype=torch.float32, device=dev)
     part_dsp = torch.empty((max(pp.n_part_rows, 1), 32), dtype=torch.float32, device=dev)
     _native.segment_rowsum(pp.items, pp.n_items, pp.perm, dPo, PROJ_SCALE, dSp, part_dsp)
     bwd_combine(pp, part_dsp, 32, dSp)
-    return (None, aux, dSp, dSv, dSg.view(ctx.sg_shape), tot[:64].view(32, 2), dSg.clone(), None, None,
+    return (None, aux, dSp, dSv, dSg.view(ctx.sg_shape), tot[:64].view(32, 2),
+            _bias_grad(dSv, dSg, getattr(ctx, "defer_b", False), shared=bnd is not None), None, None,
             tot[160:162], tot[162:164], tot[64:128].view(32, 2), tot[128:160], None, None)
 
 
@@ -584,6 +619,7 @@ class Seam0Fn(torch.autograd.Function):
         out, smax, ssum = _cam_attention_fwd(launch, bias, plan, heads, HC, plan_partial, shard, dev)
         # Block0EpilogueFn's state
         ctx.e_eps, ctx.edges, ctx.sg_shape = eps0, edges, Sg.shape
+        ctx.e_defer_b = _native.defer_token(bp)
         # EdgeCamFn's state
         ctx.eps, ctx.heads, ctx.slope, ctx.plan = eps, heads, slope, plan
         ctx.att_shape = att.shape
@@ -603,7 +639,8 @@ class Seam0Fn(torch.autograd.Function):
         epi, cam = saved[:7], saved[7:]
         dRes = dtoken.contiguous() if (dtoken is not None and dtoken.stride(0) != 0) else None
         edges = ctx.edges
-        gc = _cam_backward(ctx, cam, dXLp, g_c, dRes)
+        bnd = _boundary_buffers(edges.m, ctx.plan.num_targets, epi[0].device) if ctx.sharded else None
+        gc = _cam_backward(ctx, cam, dXLp, g_c, dRes, dXR=bnd[2] if bnd is not None else None)
         dPn = gc[0] if gPn is None else gc[0] + gPn
-        ectx = _EpiState(ctx.e_eps, edges, ctx.sg_shape, None)
-        return _epilogue0_backward(ectx, epi, dPn) + gc[1:]
+        ectx = _EpiState(ctx.e_eps, edges, ctx.sg_shape, None, defer_b=ctx.e_defer_b)
+        return _epilogue0_backward(ectx, epi, dPn, bnd) + gc[1:]

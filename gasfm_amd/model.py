@@ -168,12 +168,13 @@ class _NodeAggregation(Module):
             return conv.lin_r(zero).expand(num_targets, -1)
         return dense.linear(dense.sequential(getattr(self, self._state_key), prev), conv.lin_r)
 
-    def tail(self, x, prev):
-        """Everything after the GATv2 aggregation: proj, state skip, LN+ReLU, MLP, skip."""
+    def tail(self, x, prev, exch=None):
+        """Everything after the GATv2 aggregation: proj, state skip, LN+ReLU, MLP, skip.  exch: the
+        camera-sharded block exchange (the view tail's backward writes into its send block)."""
         if point_block.tail_fusable(self, x, prev):
             return point_block.tail(self, x, prev)
         if view_block.tail_fusable(self, x, prev):
-            return view_block.tail(self, x, prev)
+            return view_block.tail(self, x, prev, exch)
         if self.n_feat_agg != self.n_feat_out:
             x = dense.linear(x, getattr(self, self._proj_key))
         if prev is not None:
@@ -233,13 +234,16 @@ class ViewAndScenePoint2Global(Module):
         self.mlp = get_linear_layers((2 + n_hidden_layers_global_update) * [n_feat_global_out], norm=False)
 
     def forward_plan(self, view, pts, plan_v2g, plan_s2g, prev, plan_s2g_partial=None, shard=None, xl_pts=None,
-                     xl_view=None, pre_glob=None, plan_v2g_partial=None, chain=None):
+                     xl_view=None, pre_glob=None, plan_v2g_partial=None, chain=None, exch=None, rows=None):
         """xl_pts / xl_view: the convs' lin_l(pts) / lin_l(view) when already computed (hubs);
         pre_glob: (XR_view2global, XR_scenepoint2global, skip of prev) from GlobalHubFn.
         Camera-sharded (shard.cams): view holds this rank's camera rows and both attentions
         exchange partial states in one all-gather (distributed.ShardedGlobalAttentionFn).
         chain: dense.chain_params of this update and the consumers of its output; the tail then runs
-        as one GlobalChainFn and forward_plan returns its (g, SG[, XRv, XRp]) tuple."""
+        as one GlobalChainFn and forward_plan returns its (g, SG[, XRv, XRp]) tuple.
+        exch / rows: the camera-sharded block exchange (distributed.BlockExchange) and the view hub's
+        own (SV, XR) rows: both convs' partial rows and those rows leave in ONE all-gather
+        (ShardedGlobalExchangeFn); rows["SV"], rows["XRc"] are set to the gathered [m, 32] rows."""
         assert self.stateful == (prev is not None)
         cv, c = self.graph_conv_view2global, self.graph_conv_scenepoint2global
         if pre_glob is not None:
@@ -250,6 +254,13 @@ class ViewAndScenePoint2Global(Module):
             XRv, XRp = _target_row(cv, xv, view, plan_v2g.num_targets), _target_row(c, xp, pts, plan_s2g.num_targets)
         XLv = xl_view if xl_view is not None else dense.linear(view, cv.lin_l)
         XLp = xl_pts if xl_pts is not None else dense.linear(pts, c.lin_l)
+        if _cam_sharded(shard) and exch is not None:
+            from .distributed import ShardedGlobalExchangeFn
+            x, SVf, XRf = ShardedGlobalExchangeFn.apply(
+                XLv, XRv, cv.att, cv._bias(XLv), XLp, XRp, c.att, c.bias, rows["own"][0], rows["own"][1],
+                (plan_v2g, plan_s2g), c.heads, c.negative_slope, shard, exch, pre_glob is not None)
+            rows.update(SV=SVf, XRc=XRf)
+            return self._global_tail(x, prev, chain)
         if _cam_sharded(shard):
             from .distributed import ShardedGlobalAttentionFn
             x = ShardedGlobalAttentionFn.apply(
@@ -461,18 +472,27 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
             agg_p, agg_c = DualAttentionFn.apply(XL, XRp, XRc, cp.att, cc.att, cp.bias, cc.bias, pp, pc, cp.heads,
                                                  cp.negative_slope, plans.get("_partial", {}).get("proj2view"), shard,
                                                  xl_sorted)
+        exch = None
         if cams:  # this rank's camera rows only from here on (distributed.py, camera sharding)
-            from .distributed import own_rows
-            agg_c = own_rows(agg_c, shard)
-        view = sv.tail(agg_c, prev_view)
+            from .distributed import BlockExchange, own_rows
+            if hubs and self._exchange_ok(vsg):
+                cvg, csg = vsg.graph_conv_view2global, vsg.graph_conv_scenepoint2global
+                exch = BlockExchange(shard, cvg.att.numel(), csg.att.numel(), csg.heads, agg_c.device)
+            agg_c = own_rows(agg_c, shard, exch)
+        view = sv.tail(agg_c, prev_view, exch=exch)
         if hubs:
             hv = view_block.hub_params(pfu, vsg.graph_conv_view2global, nxt.proj2view)
             if hv is not None and view_block._rows_ok(view, view.shape[1]):
-                skip, SV, XLv, XRn = view_block.hub(view, hv, getattr(self, "_proj_bf16", False), packed=cams)
-                if cams:  # every rank's edges read all cameras' SV and XR: one all-gather
+                skip, SV, XLv, XRn = view_block.hub(view, hv, getattr(self, "_proj_bf16", False), packed=cams,
+                                                    out=exch.rows_out() if exch is not None else None)
+                if exch is not None:  # SV and XR of every rank travel with the global convs' partial rows
+                    carry.update(exch=exch, rows_own=(SV, XRn))
+                elif cams:  # every rank's edges read all cameras' SV and XR: one all-gather
                     from .distributed import gather_rows
                     SV, XRn = gather_rows(shard, SV, XRn)
-                carry.update(XRc=XRn, view_skip=skip, SV=SV, XLv2g=XLv)
+                if exch is None:
+                    carry.update(XRc=XRn, SV=SV)
+                carry.update(view_skip=skip, XLv2g=XLv)
             elif cams:
                 raise RuntimeError("camera-sharded execution needs the fused view hub shapes")
         pts = sp.tail(agg_p, prev_pt)
@@ -480,6 +500,15 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
             skip, SA, XLs, XRn = point_block.hub(pts, hp)
             carry.update(XRp=XRn, pts_skip=skip, SA=SA, XLs2g=XLs)
         return self._finish(pts, view, plans, prev_glob, carry, pfu, nxt)
+
+    def _exchange_ok(self, vsg):
+        """The merged block exchange applies: both global convs on the fused kernels' shapes (H = 4,
+        C in {256, 16}, global_attn.hip) and the fused view hub's 32-wide SV / XR."""
+        if vsg is None:
+            return False
+        cvg, csg = vsg.graph_conv_view2global, vsg.graph_conv_scenepoint2global
+        return (cvg.heads == 4 and csg.heads == 4 and cvg.att.numel() in (64, 1024) and csg.att.numel() in (64, 1024)
+                and cvg.negative_slope == csg.negative_slope and cvg.bias is not None and csg.bias is not None)
 
     def cam_fusable(self, plans):
         """The fused prologue + camera attention (EdgeCamFn) applies: both convs H = 4, C = 8, and
@@ -533,12 +562,16 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
                 nv = nxt.view_and_scenepoint2global if nxt is not None and getattr(nxt, "output_global", False) \
                     else None
                 chain = dense.chain_params(self.view_and_scenepoint2global, pfu, nv)
+            exch = carry.pop("exch", None) if carry is not None else None
+            rows = {"own": carry.pop("rows_own")} if exch is not None else None
             glob = self.view_and_scenepoint2global.forward_plan(
                 view, pts, plans["view2global"], plans["scenepoint2global"], prev_glob,
                 plans.get("_partial", {}).get("scenepoint2global"), plans.get("_shard"),
                 xl_pts=carry.pop("XLs2g", None) if carry is not None else None,
                 xl_view=carry.pop("XLv2g", None) if carry is not None else None, pre_glob=pre_glob,
-                plan_v2g_partial=plans.get("_partial", {}).get("view2global"), chain=chain)
+                plan_v2g_partial=plans.get("_partial", {}).get("view2global"), chain=chain, exch=exch, rows=rows)
+            if rows is not None:
+                carry.update(SV=rows["SV"], XRc=rows["XRc"])
             if isinstance(glob, tuple):  # GlobalChainFn: g with its consumers' rows
                 if len(glob) == 4:
                     glob, SG, XRv, XRp = glob

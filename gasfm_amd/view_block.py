@@ -72,7 +72,9 @@ def _mm(a, b, cin=None, bias=None, bf16=False, out=None):
 
 class ViewTailFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, prev, agg, Wp, bp, ln_w, ln_b, Wm, bm, eps, bf16=False):
+    def forward(ctx, prev, agg, Wp, bp, ln_w, ln_b, Wm, bm, eps, bf16=False, exch=None):
+        """exch (distributed.BlockExchange): the backward writes d agg straight into the block's
+        backward send block (the camera-sharded own-row gather)."""
         agg = agg.contiguous()
         prev = prev.contiguous() if prev is not None else None
         Wp, Wm = Wp.contiguous(), Wm.contiguous()
@@ -91,6 +93,7 @@ class ViewTailFn(torch.autograd.Function):
             view = _mm(h, Wm.t(), cin=xb, bf16=bf16, out=xb)
         ctx.save_for_backward(agg, x, rs, h, Wp, ln_w, ln_b, Wm)
         ctx.eps, ctx.has_prev, ctx.bf16 = eps, prev is not None, bf16
+        ctx.exch = exch
         ctx.defer = _native.defer_token(Wp, bp, ln_w, ln_b, bm)
         return view
 
@@ -99,18 +102,21 @@ class ViewTailFn(torch.autograd.Function):
         agg, x, rs, h, Wp, ln_w, ln_b, Wm = ctx.saved_tensors
         m, D = x.shape
         dview = dview.contiguous()
+        ex, ctx.exch = ctx.exch, None
         if ctx.chain:
-            dh, dx, dagg = _f32(m, D, like=x), _f32(m, D, like=x), _f32(m, A_W, like=x)
+            dh, dx = _f32(m, D, like=x), _f32(m, D, like=x)
+            dagg = ex.dagg_out() if (ex is not None and ex.own == m) else _f32(m, A_W, like=x)
             dWm = torch.empty_like(Wm)
             part = _f32((m + TR - 1) // TR, _native.view_tail_part_cols(D), like=x)
             _native.view_chain_tail_bwd(dview, x, h, rs, agg, Wp, ln_w, ln_b, Wm, dh, dWm, dx, dagg, part)
             tot = _native.param_colsum(part, ctx.defer)
             dWp = tot[:D * A_W].view(D, A_W)
             dbp, dg, dbt, dbm = (tot[D * A_W + k * D:D * A_W + (k + 1) * D] for k in range(4))
-            return (dx if ctx.has_prev else None), dagg, dWp, dbp, dg, dbt, dWm, dbm, None, None
+            return (dx if ctx.has_prev else None), dagg, dWp, dbp, dg, dbt, dWm, dbm, None, None, None
         dh = _mm(dview, Wm, bf16=ctx.bf16)
         dWm = _mm(dview.t(), h, bf16=ctx.bf16)
-        dx, dagg = _f32(m, D, like=x), _f32(m, A_W, like=x)
+        dx = _f32(m, D, like=x)
+        dagg = ex.dagg_out() if (ex is not None and ex.own == m) else _f32(m, A_W, like=x)
         cols = _native.view_tail_part_cols(D)
         if m == 0:
             tot = torch.zeros(cols, dtype=torch.float32, device=x.device)
@@ -121,22 +127,23 @@ class ViewTailFn(torch.autograd.Function):
             tot = _native.param_colsum(part, ctx.defer)
         dWp = tot[:D * A_W].view(D, A_W)
         dbp, dg, dbt, dbm = (tot[D * A_W + k * D:D * A_W + (k + 1) * D] for k in range(4))
-        return (dx if ctx.has_prev else None), dagg, dWp, dbp, dg, dbt, dWm, dbm, None, None
+        return (dx if ctx.has_prev else None), dagg, dWp, dbp, dg, dbt, dWm, dbm, None, None, None
 
 
 class ViewHubFn(torch.autograd.Function):
     """v -> (skip, SV, XL, XR)."""
 
     @staticmethod
-    def forward(ctx, v, gC, bC, Wv, Wl, bl, gA, bA, Wa, ba, Wr, br, eps, bf16=False, packed=False):
+    def forward(ctx, v, gC, bC, Wv, Wl, bl, gA, bA, Wa, ba, Wr, br, eps, bf16=False, packed=False, out=None):
         """packed: SV and XR are the two column halves of one [m, 64] block (the camera-sharded
-        path all-gathers that block as it is: distributed.GatherRowsFn)."""
+        path all-gathers that block as it is); out: that block's [m, 64] destination (the block
+        exchange's send block, distributed.BlockExchange)."""
         v = v.contiguous()
         Wv, Wl, Wa, Wr = (w.contiguous() for w in (Wv, Wl, Wa, Wr))
         m = v.shape[0]
         t = _f32(m, A_W, like=v)
         if packed:
-            blk = _f32(m, 2 * A_W, like=v)
+            blk = out if out is not None else _f32(m, 2 * A_W, like=v)
             SV, XR = blk[:, :A_W], blk[:, A_W:]
         else:
             SV, XR = _f32(m, A_W, like=v), _f32(m, A_W, like=v)
@@ -195,7 +202,7 @@ class ViewHubFn(torch.autograd.Function):
         dWr = tot[o:o + A_W * A_W].view(A_W, A_W)
         o += A_W * A_W
         dba, dbr = tot[o:o + A_W], tot[o + A_W:o + 2 * A_W]
-        return dacc, dgC, dbC, dWv, dWl, dbl, dgA, dbA, dWa, dba, dWr, dbr, None, None, None
+        return dacc, dgC, dbC, dWv, dWl, dbl, dgA, dbA, dWa, dba, dWr, dbr, None, None, None, None
 
 
 def _is_ln(mod, w):
@@ -223,11 +230,11 @@ def tail_fusable(agg_mod, x, prev):
             and _is_ln(agg_mod.norm_pre_mlp, D) and len(agg_mod.mlp) == 1 and _is_lin(agg_mod.mlp[0], D, D, True))
 
 
-def tail(agg_mod, x, prev):
+def tail(agg_mod, x, prev, exch=None):
     proj = getattr(agg_mod, agg_mod._proj_key)
     ln, lin = agg_mod.norm_pre_mlp, agg_mod.mlp[0]
     return ViewTailFn.apply(prev, x, proj.weight, proj.bias, ln.weight, ln.bias, lin.weight, lin.bias, ln.eps,
-                            getattr(agg_mod, "_proj_bf16", False))
+                            getattr(agg_mod, "_proj_bf16", False), exch)
 
 
 def hub_params(pfu, v2g_conv, nxt):
@@ -250,5 +257,5 @@ def hub_params(pfu, v2g_conv, nxt):
             linR.weight, linR.bias, lnC.eps)
 
 
-def hub(v, params, bf16=False, packed=False):
-    return ViewHubFn.apply(v, *params, bf16, packed)
+def hub(v, params, bf16=False, packed=False, out=None):
+    return ViewHubFn.apply(v, *params, bf16, packed, out)

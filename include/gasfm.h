@@ -738,6 +738,24 @@ int gasfm_gatt_bwd(int32_t nprob, const gasfm_gatt_prob* probs, float slope, flo
  * (+ bias), the same on every rank.  One workgroup per problem, one launch. */
 int gasfm_gatt_merge(int32_t nprob, const gasfm_gatt_prob* probs, int32_t nrows, int64_t stride, void* stream);
 
+/* The camera-sharded block exchange (round 5): one all-gather of per-rank send blocks carries
+ * several payloads.  G holds W send blocks of blk floats; rank r's block carries at float offset
+ * roff its chunk own rows of width floats (rows past the scene's m are padding) and at soff a
+ * partial vector of sn floats.  rows_dst [m, width] (row stride ld_dst; may be null) receives camera
+ * row c = G[(c / chunk) blk + roff + (c % chunk) width ..]; sum_dst [sn] (may be null) the W
+ * partial vectors summed in rank order (the same bits on every rank).  blk, roff, soff, width,
+ * ld_dst, sn multiples of 4; 16-byte aligned pointers.  Replaces (reference: none, the reference
+ * is single-device) a second collective per block: the forward's view-row gather rides with the
+ * global convs' partial rows, the backward's camera-aggregate gradient gather with the global
+ * target rows' gradient sum. */
+int gasfm_exchange_unpack(const float* G, int32_t W, int64_t blk, int64_t roff, int32_t chunk, int32_t width,
+                          int32_t m, float* rows_dst, int64_t ld_dst, int64_t soff, int32_t sn, float* sum_dst,
+                          void* stream);
+/* gasfm_gatt_merge and gasfm_exchange_unpack's row copy (no sum) in ONE launch. */
+int gasfm_gatt_merge_unpack(int32_t nprob, const gasfm_gatt_prob* probs, int32_t nrows, int64_t stride,
+                            const float* G, int32_t W, int64_t blk, int64_t roff, int32_t chunk, int32_t width,
+                            int32_t m, float* rows_dst, int64_t ld_dst, void* stream);
+
 /* Reprojection error of compute_core_errors' "our_repro" (code/evaluation.py:8-31 ->
  * geo_utils.reprojection_error_with_points, geo_utils.py:371-391) over the E visibility edges:
  * err_e = || xy_e - (P_c X)_xy / (P_c X)_z ||, X = pflat(pts3D[:, p]), P = Ps_pix [m x 12]
