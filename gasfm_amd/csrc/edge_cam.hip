@@ -163,16 +163,14 @@ __device__ __forceinline__ void phat_slabs(f32x4 (&v)[2], const float (&g8)[2][4
                                            float eps) {
   if (!LN) return;
   float sm = (v[0][0] + v[0][1]) + (v[0][2] + v[0][3]) + ((v[1][0] + v[1][1]) + (v[1][2] + v[1][3]));
-  sm += __shfl_xor(sm, 16);
-  sm += __shfl_xor(sm, 32);
+  sm = xsum32(xsum16(sm));
   const float mean = sm * (1.f / F);
   float q = 0.f;
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int j = 0; j < 4; ++j) q = fmaf(v[u][j] - mean, v[u][j] - mean, q);
-  q += __shfl_xor(q, 16);
-  q += __shfl_xor(q, 32);
+  q = xsum32(xsum16(q));
   const float rstd = rsqrtf(q * (1.f / F) + eps);
 #pragma unroll
   for (int u = 0; u < 2; ++u)
@@ -188,16 +186,14 @@ __device__ __forceinline__ void phat_slabs_st(f32x4 (&v)[2], const float (&g8)[2
   rstd = 1.f;
   if (!LN) return;
   float sm = (v[0][0] + v[0][1]) + (v[0][2] + v[0][3]) + ((v[1][0] + v[1][1]) + (v[1][2] + v[1][3]));
-  sm += __shfl_xor(sm, 16);
-  sm += __shfl_xor(sm, 32);
+  sm = xsum32(xsum16(sm));
   mean = sm * (1.f / F);
   float q = 0.f;
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int j = 0; j < 4; ++j) q = fmaf(v[u][j] - mean, v[u][j] - mean, q);
-  q += __shfl_xor(q, 16);
-  q += __shfl_xor(q, 32);
+  q = xsum32(xsum16(q));
   rstd = rsqrtf(q * (1.f / F) + eps);
 #pragma unroll
   for (int u = 0; u < 2; ++u)
@@ -357,7 +353,7 @@ __global__ __launch_bounds__(kThreads, GASFM_CAM_MINW) void edge_cam_fwd_kernel(
           xl[r] = acc[2 + q][r] + bcv[q][r];
           p = fmaf(leaky(xl[r] + xr[q][r], slope), attv[q][r], p);
         }
-        p += __shfl_xor(p, 16);  // the head's other 4 features
+        p = xsum16(p);  // the head's other 4 features
         if (valid) {
           const float mn = fmaxf(m[q], p);
           const float sc = __expf(m[q] - mn), wt = __expf(p - mn);
@@ -669,7 +665,7 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
           xl[r] = acc[2 + q][r] + bcq[r];
           p = fmaf(leaky(xl[r] + xr[q][r], slope), atq[r], p);
         }
-        p += __shfl_xor(p, 16);  // the head's other 4 features
+        p = xsum16(p);  // the head's other 4 features
         if (valid) {
           const float mn = fmaxf(m[q], p);
           const float sc = __expf(m[q] - mn), wt = __expf(p - mn);
@@ -805,7 +801,7 @@ __global__ __launch_bounds__(kThreads, GASFM_CAM_MINW) void edge_cam_bwd_kernel(
       float d = 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) d = fmaf(gv[q][r], o[r] - biasv[q][r], d);
-      delta[q] = d + __shfl_xor(d, 16);
+      delta[q] = xsum16(d);
       M[q] = seg_max[seg * ldStat + h];
       inv[q] = 1.f / (seg_sum[seg * ldStat + h] + 1e-16f);
     }
@@ -857,8 +853,8 @@ __global__ __launch_bounds__(kThreads, GASFM_CAM_MINW) void edge_cam_bwd_kernel(
           p = fmaf(lz[r], attv[q][r], p);
           da = fmaf(gv[q][r], xl[r], da);
         }
-        p += __shfl_xor(p, 16);
-        da += __shfl_xor(da, 16);
+        p = xsum16(p);
+        da = xsum16(da);
         const float alpha = valid ? __expf(p - M[q]) * inv[q] : 0.f;
         const float de = alpha * (da - delta[q]);
         float dx[4];
@@ -1111,7 +1107,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
       xr[q] = f32x4{x4.x, x4.y, x4.z, x4.w};
       gv[q] = f32x4{g4v.x, g4v.y, g4v.z, g4v.w};
       float d = fmaf(g4v.x, o4.x - b4.x, fmaf(g4v.y, o4.y - b4.y, fmaf(g4v.z, o4.z - b4.z, g4v.w * (o4.w - b4.w))));
-      delta[q] = d + __shfl_xor(d, 16);
+      delta[q] = xsum16(d);
       M[q] = seg_max[seg * ldStat + h];
       inv[q] = 1.f / (seg_sum[seg * ldStat + h] + 1e-16f);
     }
@@ -1170,6 +1166,9 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
           }
         }
         phat_slabs_st<LN>(PT, gs, bs, eps, tmean, trstd);
+        // edge c's statistics next to tile 3's row c (every lane group: same values), read back by the
+        // C-layout rows (one ds_write_b64, four ds_read_b64 per tile; no lane shuffles)
+        *reinterpret_cast<float2*>(Tt + 3 * TR * LDT + c * LDT + 32) = make_float2(tmean, trstd);
       }
       f32x4 xc[2] = {vecT(2, 0), vecT(2, 1)};  // b_c, then + Wc P_hat^T
       xl_slabs<2>(reinterpret_cast<const float4*>(WcQ), PT, xc, lane);
@@ -1185,8 +1184,8 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
           p = fmaf(lz[r], at[r], p);
           da = fmaf(gv[q][r], xc[q][r], da);
         }
-        p += __shfl_xor(p, 16);
-        da += __shfl_xor(da, 16);
+        p = xsum16(p);
+        da = xsum16(da);
         const float alpha = valid ? __expf(p - M[q]) * inv[q] : 0.f;
         const float de = alpha * (da - delta[q]);
 #pragma unroll
@@ -1212,8 +1211,9 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
         const bool live = 4 * g + r < nrows;
         float mean = 0.f, rstd = 1.f;
         if (LN) {
-          mean = __shfl(tmean, 4 * g + r);
-          rstd = __shfl(trstd, 4 * g + r);
+          const float2 st = *reinterpret_cast<const float2*>(Tt + 3 * TR * LDT + (4 * g + r) * LDT + 32);
+          mean = st.x;
+          rstd = st.y;
         }
         float xh[2], gvv[2], s1 = 0.f, s2 = 0.f;
 #pragma unroll

@@ -1208,6 +1208,16 @@ __global__ __launch_bounds__(kThreadsT, GASFM_PT_FWD_T_MINW) void point_hub_fwd_
 #ifndef GASFM_PT_BWD_R
 #define GASFM_PT_BWD_R 1
 #endif
+// 1: scheduling barriers between the phases of a tile (each phase's MFMAs and VALU work stay
+// together); 0: none (the compiler may interleave a phase's VALU with the next phase's MFMAs)
+#ifndef GASFM_PT_SCHED
+#define GASFM_PT_SCHED 1
+#endif
+#if GASFM_PT_SCHED
+#define PT_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define PT_SCHED_BARRIER() ((void)0)
+#endif
 // 1 wave per SIMD (~210 VGPRs + 116 AGPRs) with the next tile's rows requested one tile ahead;
 // 2 waves per SIMD spills (256 VGPRs, 52 spilled): 110 vs 86 us at n = 200k without the prefetch
 #ifndef GASFM_PT_BWD_R_MINW
@@ -1407,11 +1417,11 @@ __global__ __launch_bounds__(kThreadsR, GASFM_PT_BWD_R_MINW) void point_tail_bwd
     for (int ot = 0; ot < 4; ++ot)
 #pragma unroll
       for (int r = 0; r < 4; ++r) x[ot][r] = (x[ot][r] - mean[r]) * rstd[r];  // x_hat from here on
-    __builtin_amdgcn_sched_barrier(0);
+    PT_SCHED_BARRIER();
     // phase 2: dh = dout W_m (C layout)
     f32x4 dh[4] = {zero4(), zero4(), zero4(), zero4()};
     layer_c<4, 4>(WmTQ, dT, dh, lane);
-    __builtin_amdgcn_sched_barrier(0);
+    PT_SCHED_BARRIER();
     // phase 3: LayerNorm backward -> dx (C layout), bias sums
     f32x4 dxc[4];
     cl_ln_relu_bwd(x, dh, gmC, btC, rstd, nrows, g, dg, dbt, dxc);
@@ -1421,7 +1431,7 @@ __global__ __launch_bounds__(kThreadsR, GASFM_PT_BWD_R_MINW) void point_tail_bwd
       dbm[ot] += (dC[ot][0] + dC[ot][1]) + (dC[ot][2] + dC[ot][3]);
       dbp[ot] += (dxc[ot][0] + dxc[ot][1]) + (dxc[ot][2] + dxc[ot][3]);
     }
-    __builtin_amdgcn_sched_barrier(0);
+    PT_SCHED_BARRIER();
     // phase 4: weight gradients over the tile's rows (step s: row 4 g + s; rows past nrows: dout,
     // dx are 0); h = relu(x_hat g + b) recomputed here (not live through phases 2-3)
 #pragma unroll
@@ -1437,7 +1447,7 @@ __global__ __launch_bounds__(kThreadsR, GASFM_PT_BWD_R_MINW) void point_tail_bwd
         for (int nt = 0; nt < 2; ++nt) dWp[mt][nt] = mfma16(dxc[mt][s], agC[nt][s], dWp[mt][nt]);
       }
     }
-    __builtin_amdgcn_sched_barrier(0);
+    PT_SCHED_BARRIER();
     f32x4 dxT[4];
     c_to_t64(dxc, X, dxT, lane);
     slabs_store<FP>(dx, row0, nrows, dxT, lane);
@@ -1631,13 +1641,19 @@ __global__ __launch_bounds__(kThreadsR, GASFM_PT_HUB_BWD_R_MINW) void point_hub_
       for (int ft = 0; ft < 2; ++ft) tC[ft] += V[4 * FP + 16 * ft + c];
       layer_c<2, 4>(WCQ, pc, tC, lane);
     }
-    float meanC[4], rstdC[4];  // row 4 g + r lives on lane c = 4 g + r
+    // row 4 g + r's statistics, computed on lane c = 4 g + r: through the padding columns 64, 65 of
+    // the wave's p tile (row c; every lane group writes the same values), not 8 lane shuffles
+    *reinterpret_cast<float2*>(Tp + c * LDX + FP) = make_float2(mean, rstd);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    float meanC[4], rstdC[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      meanC[r] = __shfl(mean, 4 * g + r);
-      rstdC[r] = __shfl(rstd, 4 * g + r);
+      const float2 st = *reinterpret_cast<const float2*>(Tp + (4 * g + r) * LDX + FP);
+      meanC[r] = st.x;
+      rstdC[r] = st.y;
     }
-    __builtin_amdgcn_sched_barrier(0);
+    PT_SCHED_BARRIER();
     // phase 2: dt (C and T layouts), dt W_C, LN_C backward onto dRes
     f32x4 dtC[2] = {zero4(), zero4()};
     f32x4 xh[4];
@@ -1649,7 +1665,7 @@ __global__ __launch_bounds__(kThreadsR, GASFM_PT_HUB_BWD_R_MINW) void point_hub_
       f32x4 dtT[2] = {zero4(), zero4()}, dp[4] = {zero4(), zero4(), zero4(), zero4()}, dq[4];
       layer_c<2, 2>(WDTQ, rT, dtC, lane);
       layer_t<2, 2>(WDTQ, rT, dtT, lane);
-      __builtin_amdgcn_sched_barrier(0);
+      PT_SCHED_BARRIER();
       layer_c<4, 2>(WCTQ, dtT, dp, lane);
       float gm[4], bt[4];
 #pragma unroll
@@ -1661,7 +1677,7 @@ __global__ __launch_bounds__(kThreadsR, GASFM_PT_HUB_BWD_R_MINW) void point_hub_
 #pragma unroll
       for (int ot = 0; ot < 4; ++ot) acc[ot] = HR ? dq[ot] + acc[ot] : dq[ot];
     }
-    __builtin_amdgcn_sched_barrier(0);
+    PT_SCHED_BARRIER();
     // phase 3: dSA W_A, LN_A backward; dXL W_B accumulated on top; dp stored
     {
       f32x4 dp[4] = {zero4(), zero4(), zero4(), zero4()}, da[4];
@@ -1676,10 +1692,10 @@ __global__ __launch_bounds__(kThreadsR, GASFM_PT_HUB_BWD_R_MINW) void point_hub_
 #pragma unroll
       for (int ot = 0; ot < 4; ++ot) acc[ot] = da[ot] + acc[ot];
     }
-    __builtin_amdgcn_sched_barrier(0);
+    PT_SCHED_BARRIER();
     layer_c<4, 4>(WBTQ, lT, acc, lane);
     cl_store<FP>(dX, row0, nrows, acc, lane);
-    __builtin_amdgcn_sched_barrier(0);
+    PT_SCHED_BARRIER();
     // phase 4: weight gradients over the tile's rows (step s: row 4 g + s, C-layout operands read
     // from the LDS copies; dead rows: the A operands are masked to 0), bias sums
     cl_mask(dtC, nrows, g);

@@ -34,11 +34,7 @@ __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 // Sum over the 16 lanes of a lane group (same l>>4).
 __device__ __forceinline__ float sum16(float v) { return group_sum<16>(v); }
 // Sum over the 4 lane groups (l>>4).
-__device__ __forceinline__ float sum_groups(float v) {
-  v += __shfl_xor(v, 16);
-  v += __shfl_xor(v, 32);
-  return v;
-}
+__device__ __forceinline__ float sum_groups(float v) { return xsum32(xsum16(v)); }
 
 // Weight staging (once per workgroup): every thread issues ALL of its N / NT global loads before
 // the first LDS store.  The plain `for (q = threadIdx.x; q < N; q += NT) L[f(q)] = W[q]` form

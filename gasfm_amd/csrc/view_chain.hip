@@ -28,6 +28,7 @@
 #include <cstdint>
 
 #include "common.hpp"
+#include "lanes.hpp"
 
 namespace gasfm {
 namespace {
@@ -676,12 +677,9 @@ __global__ __launch_bounds__(NT) void vc_hub_bwd1_kernel(
 #pragma unroll
   for (int tt = 0; tt < 2; ++tt) {
     float a = dgp[tt], bsum = dbp[tt], l = dlp[tt];
-    a += __shfl_xor(a, 16);
-    a += __shfl_xor(a, 32);
-    bsum += __shfl_xor(bsum, 16);
-    bsum += __shfl_xor(bsum, 32);
-    l += __shfl_xor(l, 16);
-    l += __shfl_xor(l, 32);
+    a = xsum32(xsum16(a));
+    bsum = xsum32(xsum16(bsum));
+    l = xsum32(xsum16(l));
     if (g == 0) {
       const int col = t.col0 + 16 * tt + c;
       out[(ba_ ? P.GA : P.GC) + col] = a;
@@ -844,12 +842,9 @@ __global__ __launch_bounds__(NT) void vc_tail_bwd1_kernel(const float* __restric
       s1[r] = fmaf(dy, gv, s1[r]);
       s2[r] = fmaf(dy * gv, xh, s2[r]);
     }
-    dgp += __shfl_xor(dgp, 16);
-    dgp += __shfl_xor(dgp, 32);
-    dbp += __shfl_xor(dbp, 16);
-    dbp += __shfl_xor(dbp, 32);
-    dmp += __shfl_xor(dmp, 16);
-    dmp += __shfl_xor(dmp, 32);
+    dgp = xsum32(xsum16(dgp));
+    dbp = xsum32(xsum16(dbp));
+    dmp = xsum32(xsum16(dmp));
     if (g == 0) {
       out[int64_t(D) * VA + D + col] = dgp;
       out[int64_t(D) * VA + 2 * D + col] = dbp;
@@ -967,8 +962,7 @@ __global__ __launch_bounds__(TB2_T) void vc_tail_bwd2_kernel(const float* __rest
       DX[wave][rr][cl] = o;
       dbp += o;
     }
-    dbp += __shfl_xor(dbp, 16);
-    dbp += __shfl_xor(dbp, 32);
+    dbp = xsum32(xsum16(dbp));
     if (g == 0) out[int64_t(D) * VA + col] = dbp;
   }
   __builtin_amdgcn_wave_barrier();
