@@ -984,7 +984,12 @@ __device__ __forceinline__ void prod_c2(const float4* __restrict__ Q, const f32x
 #ifndef GASFM_PBWD_MINW
 #define GASFM_PBWD_MINW 2
 #endif
+// 1: the LayerNorm backward in the T layout (round 5); 0: in the C layout (round 4)
+#ifndef GASFM_PBWD_T
+#define GASFM_PBWD_T 1
+#endif
 
+#if !GASFM_PBWD_T
 template <bool LN, bool RES, bool EPI, bool DWP>
 __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kernel(
     const float* __restrict__ P, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
@@ -1432,6 +1437,485 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
     }
   }
 }
+
+#endif  // !GASFM_PBWD_T
+
+#if GASFM_PBWD_T
+// T-layout backward (round 5).  The LayerNorm backward runs where the forward's statistics are --
+// lane (g, c) holds 8 features of edge c -- instead of in the C layout (4 edges x 2 features per
+// lane): dP_hat comes out of the transposed products (A = the same weight slabs, B = the T-layout
+// rows; acc[ot][r] = feature 16 ot + 4 g + r of edge c), so each row sum is 8 local adds and two
+// cross-group swaps instead of a 16-lane DPP sum per edge, dP leaves as two 16-byte stores per lane,
+// EPI's dP0 dot needs no transpose back and no statistics cross lanes.  The item's rows are read
+// through bounds-checked buffer descriptors: rows past the item's end load as zeros, which zeroes
+// every dead-edge quantity at its source (dXLp, dRes, P0; dXLc through alpha = 0), so no per-row
+// masks remain.  Two transpose tiles per wave (was four): P_hat, dXLp and dXLc pass through tile A
+// in turn (each read back at once), dRes and P0 sit in tile B for the dWp sums.  The attention bias
+// gradient is not summed here: the host takes the column sum of gout over all targets
+// (edge_block.replicated_dbias), which is also PyG's semantics for a target without edges.
+// Why VALU: fp32 MFMA and VALU issue do not overlap on gfx950 (profiles/r5_mfma_valu_overlap.txt).
+__device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t rs, int off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+  return f32x4{__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3])};
+}
+__device__ __forceinline__ void bstore4(const f32x4& x, __amdgpu_buffer_rsrc_t rs, int off) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = {__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2]), __float_as_uint(x[3])};
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
+}
+// descriptor over rows [begin, begin + len) of a row-major [*, ld] float tensor; its fields are
+// wave-uniform and made provably so (a descriptor the compiler places in vector registers costs a
+// waterfall loop around every load through it)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* X, int64_t ld, int begin, int len) {
+  const uint64_t a = reinterpret_cast<uint64_t>(X + int64_t(begin) * ld);
+  const uint64_t lo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(a))));
+  const uint64_t hi = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(a >> 32))));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<float*>(lo | (hi << 32)), 0,
+                                           __builtin_amdgcn_readfirstlane(int(len * ld * 4)), 0x00020000);
+}
+
+template <bool LN, bool RES, bool EPI, bool DWP>
+__global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kernel(
+    const float* __restrict__ P, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
+    const float* __restrict__ Wpt, const float* __restrict__ Wc, const float* __restrict__ bc,
+    const float* __restrict__ Wp, int ldWp, float scale, const float* __restrict__ XR, int64_t ldXR,
+    const float* __restrict__ att, const float* __restrict__ bias, float slope, const float* __restrict__ out,
+    int64_t ldOut, const float* __restrict__ seg_max, const float* __restrict__ seg_sum, int64_t ldStat,
+    const float* __restrict__ gout, int64_t ldG, const gasfm_work_item* __restrict__ items, int n_items,
+    const float* __restrict__ dXLp, int64_t ldXp, const float* __restrict__ dRes, float* __restrict__ dP,
+    float* __restrict__ dXR, int64_t ldDXR, float* __restrict__ part_dxr, float* __restrict__ part, int64_t ldPart,
+    PbwdEpi ep) {
+  static_assert(!DWP || (LN && RES), "edge_cam_pbwd: the epilogue weight gradient needs relu(LN(P)) and dRes");
+  // LDS: weight slabs (Wc for XLc; Wpt^T, Wc^T, (scale Wp)^T for dP_hat), the per-feature vectors,
+  // per wave two 16 x 36 transpose tiles, per lane the running sums (DWP: dWp; EPI: dSv) at a lane
+  // stride of an odd number of 16-byte quads (a 16-lane b128 access touches 16 distinct bank quads)
+  constexpr int QW = F * F;  // floats per 32 x 32 slab set
+  constexpr int OV = 4 * QW, OT = OV + (EPI ? 6 * F : 4 * F), WT = 2 * TR * LDT;
+  constexpr int OD = OT + kWaves * WT;
+  constexpr int NLS = DWP ? (PB_NDW + (EPI ? 8 : 0)) : (EPI ? 12 : 0);
+  constexpr int NL = OD + kWaves * NLS * kW;
+  __shared__ __attribute__((aligned(16))) float lds[NL];
+  float* WcQ = lds;
+  float* WptTQ = lds + QW;
+  float* WcTQ = lds + 2 * QW;
+  float* WqTQ = lds + 3 * QW;
+  float* V = lds + OV;  // [gamma | beta | bc | att] (32 each), (EPI) [scale_e We[:, 32] | scale_e We[:, 33]]
+  stage_slabs32<F, kThreads>([&](int q) { return Wc[q]; }, WcQ);
+  stage_slabs32<F, kThreads>([&](int q) { return Wpt[(q % F) * F + q / F]; }, WptTQ);
+  stage_slabs32<F, kThreads>([&](int q) { return Wc[(q % F) * F + q / F]; }, WcTQ);
+  if (RES) stage_slabs32<F, kThreads>([&](int q) { return scale * Wp[(q % F) * ldWp + q / F]; }, WqTQ);
+  if (threadIdx.x < F) {
+    V[threadIdx.x] = LN ? gam[threadIdx.x] : 1.f;
+    V[F + threadIdx.x] = LN ? bet[threadIdx.x] : 0.f;
+    V[2 * F + threadIdx.x] = bc[threadIdx.x];
+    V[3 * F + threadIdx.x] = att[threadIdx.x];
+    if (EPI) {
+      V[4 * F + threadIdx.x] = ep.dP0 ? ep.scale * ep.We[threadIdx.x * ep.ldWe + 32] : 0.f;
+      V[5 * F + threadIdx.x] = ep.dP0 ? ep.scale * ep.We[threadIdx.x * ep.ldWe + 33] : 0.f;
+    }
+  }
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
+  const int c = lane & 15, g = lane >> 4;
+  float* Ta = lds + OT + wave * WT;  // P_hat, dXLp, dXLc in turn (each read back at once)
+  float* Tb = Ta + TR * LDT;         // (DWP) dRes rows, P0 in columns 32, 33: read by the dWp sums
+  float* Lw = lds + OD + (wave * kW + lane) * NLS;  // (DWP) this lane's dWp sums at Lw[0, 20)
+  float* Ls = Lw + (DWP ? PB_NDW : 0);              // (EPI) the item's dSv column sums (T layout, 8)
+#pragma unroll
+  for (int k = 0; k < NLS; ++k) Lw[k] = 0.f;
+  __syncthreads();
+  // T-layout vector at this lane's features 16 q + 4 g .. + 3
+  auto vecT = [&](int which, int q) {
+    const float4 t = *reinterpret_cast<const float4*>(V + which * F + 16 * q + 4 * g);
+    return f32x4{t.x, t.y, t.z, t.w};
+  };
+  // T -> C layout through tile T: writes the two slabs, returns the C-layout rows
+  auto to_c = [&](float* T, const f32x4 (&t)[2], f32x4 (&o)[2]) {
+    asm volatile("" ::: "memory");  // after the previous transpose's reads of the same tile
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      *reinterpret_cast<float4*>(T + c * LDT + 16 * u + 4 * g) = make_float4(t[u][0], t[u][1], t[u][2], t[u][3]);
+    // one wave's LDS instructions execute in order: a compiler barrier suffices
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[ft][r] = T[(4 * g + r) * LDT + 16 * ft + c];
+  };
+  f32x4 accW[4][2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) accW[mt][0] = accW[mt][1] = zero4();
+  float db[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x4 dg[2] = {zero4(), zero4()}, dbt[2] = {zero4(), zero4()}, datt[2] = {zero4(), zero4()};
+  // the wave's first item (provably wave-uniform: the item loop, its branches and the descriptors
+  // built from the items stay scalar -- no waterfall loops around the buffer loads)
+  const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wave), nw = gridDim.x * kWaves;
+
+  // next tile's rows of P, dXLp, dRes (T layout) and P0, one tile ahead; rows past the item's end
+  // read as zeros (the descriptor's range check)
+  f32x4 nPT[2], nXT[2], nRT[2];
+  float2 nP0 = make_float2(0.f, 0.f);
+  auto issue = [&](const gasfm_work_item& wi, int row0) {
+    const int b = __builtin_amdgcn_readfirstlane(wi.begin), n = __builtin_amdgcn_readfirstlane(wi.end - wi.begin);
+    const int r = row0 - b + c;  // edge c's row within the item
+    const auto Prs = rows_rsrc(P, F, b, n);
+    const auto Xrs = rows_rsrc(dXLp, ldXp, b, n);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) nPT[u] = bload4(Prs, (r * F + 16 * u + 4 * g) * 4);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) nXT[u] = bload4(Xrs, int((r * ldXp + 16 * u + 4 * g) * 4));
+    if (RES) {
+      const auto Rrs = rows_rsrc(dRes, F, b, n);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) nRT[u] = bload4(Rrs, (r * F + 16 * u + 4 * g) * 4);
+    }
+    if (DWP && ep.P0) {  // (a global load: the compiler tail-merges a descriptor here into vector registers)
+      const float2 t = *reinterpret_cast<const float2*>(ep.P0 + (int64_t(b) + (r < n ? r : 0)) * 2);
+      nP0 = r < n ? t : make_float2(0.f, 0.f);
+    }
+  };
+  gasfm_work_item w{0, 0, 0, -1};
+  if (gw < n_items) {
+    w = uniform_item(items[gw]);
+    if (w.begin < w.end) issue(w, w.begin);
+  }
+  for (int it = gw; it < n_items; it += nw) {
+    const int64_t seg = w.seg;
+    const int ibeg = w.begin, ilen = w.end - w.begin;
+    const auto dPrs = rows_rsrc(dP, F, ibeg, ilen);
+    // (EPI) dP0 rows of this item; without dP0 an empty range (every store dropped)
+    const auto dP0rs = (EPI && ep.dP0) ? rows_rsrc(ep.dP0, 2, ibeg, ilen) : rows_rsrc(dP, F, ibeg, 0);
+    // per-camera constants of the attention backward (edge_cam_bwd_kernel)
+    f32x4 xr[2], gv[2];
+    float M[2], inv[2], delta[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int f0 = 16 * q + 4 * g, h = 2 * q + (g >> 1);
+      const float4 x4 = *reinterpret_cast<const float4*>(XR + seg * ldXR + f0);
+      const float4 g4v = *reinterpret_cast<const float4*>(gout + seg * ldG + f0);
+      const float4 o4 = *reinterpret_cast<const float4*>(out + seg * ldOut + f0);
+      const float4 b4 = *reinterpret_cast<const float4*>(bias + f0);
+      xr[q] = f32x4{x4.x, x4.y, x4.z, x4.w};
+      gv[q] = f32x4{g4v.x, g4v.y, g4v.z, g4v.w};
+      float d = fmaf(g4v.x, o4.x - b4.x, fmaf(g4v.y, o4.y - b4.y, fmaf(g4v.z, o4.z - b4.z, g4v.w * (o4.w - b4.w))));
+      delta[q] = xsum16(d);
+      M[q] = seg_max[seg * ldStat + h];
+      inv[q] = 1.f / (seg_sum[seg * ldStat + h] + 1e-16f);
+    }
+    f32x4 dxr[2] = {zero4(), zero4()};
+    gasfm_work_item wn{0, 0, 0, -1};
+    const bool more = it + nw < n_items;
+    if (more) wn = uniform_item(items[it + nw]);
+    if (w.begin >= w.end && more && wn.begin < wn.end) issue(wn, wn.begin);
+    for (int row0 = w.begin; row0 < w.end; row0 += TR) {
+      const int nrows = w.end - row0 < TR ? w.end - row0 : TR;
+      f32x4 PT[2] = {nPT[0], nPT[1]}, XT[2] = {nXT[0], nXT[1]}, RT[2];
+      if (RES) {
+        RT[0] = nRT[0];
+        RT[1] = nRT[1];
+      }
+      const float2 p0t = nP0;
+      // the next tile: this item's, else the next item's first
+      if (row0 + TR < w.end)
+        issue(w, row0 + TR);
+      else if (more && wn.begin < wn.end)
+        issue(wn, wn.begin);
+      const bool valid = c < nrows;
+      // ---- LayerNorm of edge c (T layout): PT becomes xh, ph = relu(LN(P))
+      f32x4 ph[2];
+      float rstd = 1.f;
+      if (LN) {
+        const float sm = (PT[0][0] + PT[0][1]) + (PT[0][2] + PT[0][3]) + ((PT[1][0] + PT[1][1]) + (PT[1][2] + PT[1][3]));
+        const float mean = xsum32(xsum16(sm)) * (1.f / F);
+        float q = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            PT[u][j] -= mean;
+            q = fmaf(PT[u][j], PT[u][j], q);
+          }
+        rstd = rsqrtf(xsum32(xsum16(q)) * (1.f / F) + eps);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const f32x4 a = vecT(0, u), b = vecT(1, u);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            PT[u][j] *= rstd;
+            ph[u][j] = fmaxf(fmaf(PT[u][j], a[j], b[j]), 0.f);
+          }
+        }
+      } else {
+        ph[0] = PT[0];
+        ph[1] = PT[1];
+      }
+      // ---- C layout of P_hat (the weight gradients' B operand); dRes and P0 into tile B
+      f32x4 phC[2];
+      to_c(Ta, ph, phC);
+      if (DWP) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          *reinterpret_cast<float4*>(Tb + c * LDT + 16 * u + 4 * g) = make_float4(RT[u][0], RT[u][1], RT[u][2], RT[u][3]);
+        if (g == 0) *reinterpret_cast<float2*>(Tb + c * LDT + 32) = p0t;
+      }
+      // ---- camera attention backward (T layout: edge c, features 16 q + 4 g + r)
+      f32x4 xc[2] = {vecT(2, 0), vecT(2, 1)};  // b_c, then + Wc P_hat^T
+      xl_slabs<2>(reinterpret_cast<const float4*>(WcQ), ph, xc, lane);
+      f32x4 dXc[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const f32x4 at = vecT(3, q);
+        float z[4], lz[4], p = 0.f, da = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          z[r] = xc[q][r] + xr[q][r];
+          lz[r] = leaky(z[r], slope);
+          p = fmaf(lz[r], at[r], p);
+          da = fmaf(gv[q][r], xc[q][r], da);
+        }
+        p = xsum16(p);
+        da = xsum16(da);
+        const float alpha = valid ? __expf(p - M[q]) * inv[q] : 0.f;
+        const float de = alpha * (da - delta[q]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float dz = de * at[r] * (z[r] > 0.f ? 1.f : slope);
+          dXc[q][r] = fmaf(alpha, gv[q][r], dz);  // 0 for dead edges
+          dxr[q][r] += dz;
+          datt[q][r] = fmaf(de, lz[r], datt[q][r]);
+        }
+      }
+      // ---- dP_hat (T layout) = dXLp Wpt + dXLc Wc (+ dRes scale Wp[:, :32])
+      f32x4 dph[2] = {zero4(), zero4()};
+      xl_slabs<2>(reinterpret_cast<const float4*>(WptTQ), XT, dph, lane);
+      xl_slabs<2>(reinterpret_cast<const float4*>(WcTQ), dXc, dph, lane);
+      if (RES) xl_slabs<2>(reinterpret_cast<const float4*>(WqTQ), RT, dph, lane);
+      f32x4 XC[2], XcC[2];  // C layouts of dXLp, dXLc (the weight gradients' A operand)
+      to_c(Ta, XT, XC);
+      to_c(Ta, dXc, XcC);
+      // ---- LayerNorm backward of edge c, dP (T layout)
+      f32x4 dv[2];
+      if (LN) {
+        f32x4 gvv[2];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const f32x4 a = vecT(0, u);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float dy = ph[u][j] > 0.f ? dph[u][j] : 0.f;
+            dg[u][j] = fmaf(dy, PT[u][j], dg[u][j]);
+            dbt[u][j] += dy;
+            gvv[u][j] = dy * a[j];
+            s1 += gvv[u][j];
+            s2 = fmaf(gvv[u][j], PT[u][j], s2);
+          }
+        }
+        s1 = xsum32(xsum16(s1)) * (1.f / F);
+        s2 = xsum32(xsum16(s2)) * (1.f / F);
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float v = rstd * (gvv[u][j] - s1 - PT[u][j] * s2);
+            if (RES) v += RT[u][j];
+            dv[u][j] = v;
+          }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dv[u][j] = dph[u][j] + (RES ? RT[u][j] : 0.f);
+      }
+      // rows past the item's end fall outside the descriptor's range: the hardware drops them
+#pragma unroll
+      for (int u = 0; u < 2; ++u) bstore4(dv[u], dPrs, ((row0 - ibeg + c) * F + 16 * u + 4 * g) * 4);
+      if (EPI) {
+        // the previous block's epilogue: the item's column sums of dP (dSv; dead edges hold 0), and
+        // dP0 = scale_e We[:, 32:34]^T dP per edge (a dot per lane, the 4 lane groups summed; group
+        // 0 stores the pair, the other groups an out-of-range offset)
+        float4* L4 = reinterpret_cast<float4*>(Ls);
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          float4 t = L4[u];
+          t.x += dv[u][0];
+          t.y += dv[u][1];
+          t.z += dv[u][2];
+          t.w += dv[u][3];
+          L4[u] = t;
+          const f32x4 a = vecT(4, u), b = vecT(5, u);
+          s0 = fmaf(dv[u][0], a[0], fmaf(dv[u][1], a[1], fmaf(dv[u][2], a[2], fmaf(dv[u][3], a[3], s0))));
+          s1 = fmaf(dv[u][0], b[0], fmaf(dv[u][1], b[1], fmaf(dv[u][2], b[2], fmaf(dv[u][3], b[3], s1))));
+        }
+        s0 = sum_groups(s0);
+        s1 = sum_groups(s1);
+        const int off = g == 0 ? (row0 - ibeg + c) * 8 : 0x7ffffff0;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s0), dP0rs, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s1), dP0rs, off + 4, 0, 0);
+      }
+      // ---- dW += [dXLp | dXLc]^T relu(LN(P)), db (C layout, row 4 g + s at step s; dead rows 0)
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const float a = mt < 2 ? XC[mt][s2] : XcC[mt - 2][s2];
+          db[mt] += a;
+          accW[mt][0] = mfma16(a, phC[0][s2], accW[mt][0]);
+          accW[mt][1] = mfma16(a, phC[1][s2], accW[mt][1]);
+        }
+      }
+      if (DWP) {
+        // this block's epilogue: dWp += dRes^T [relu(LN(P)) | P0] (dead rows are zeros), one
+        // 16-feature half of dRes at a time, its rows and P0 read from tile B, the products added
+        // into the lanes' LDS sums
+#pragma unroll
+        for (int ft = 0; ft < 2; ++ft) {
+          float rr[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) rr[r] = Tb[(4 * g + r) * LDT + 16 * ft + c];
+          f32x4 ap[2] = {zero4(), zero4()};
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) ap[nt] = mfma16(rr[s2], phC[nt][s2], ap[nt]);
+          float a0[2] = {0.f, 0.f};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            a0[0] = fmaf(rr[r], Tb[(4 * g + r) * LDT + 32], a0[0]);
+            a0[1] = fmaf(rr[r], Tb[(4 * g + r) * LDT + 33], a0[1]);
+          }
+          float* q = Lw + 10 * ft;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) q[k] += ap[k / 4][k % 4];
+          q[8] += a0[0];
+          q[9] += a0[1];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();  // this tile's LDS reads before the next tile's writes
+      asm volatile("" ::: "memory");
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = group_sum<16>(dxr[q][r]);
+      if (c == 0) {
+        float* d = (w.slot < 0) ? dXR + seg * ldDXR : part_dxr + int64_t(w.slot) * F;
+        *reinterpret_cast<float4*>(d + 16 * q + 4 * g) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+    if (EPI) {  // the item's dSv row: the 16 edge lanes of each group summed
+      float4* L4 = reinterpret_cast<float4*>(Ls);
+      float sv[2][4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float4 t = L4[u];
+        L4[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        sv[u][0] = group_sum<16>(t.x) * ep.scale;
+        sv[u][1] = group_sum<16>(t.y) * ep.scale;
+        sv[u][2] = group_sum<16>(t.z) * ep.scale;
+        sv[u][3] = group_sum<16>(t.w) * ep.scale;
+      }
+      if (c == 0) {
+        float* d = (w.slot < 0) ? ep.dSv + seg * F : ep.part_dsv + int64_t(w.slot) * F;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          *reinterpret_cast<float4*>(d + 16 * u + 4 * g) = make_float4(sv[u][0], sv[u][1], sv[u][2], sv[u][3]);
+      }
+    }
+    w = wn;
+  }
+  // workgroup reduction: 32 accW + 4 db (C layout) + 1 (dgamma / dbeta: the 16 edge lanes summed,
+  // lane c keeps value c of its group) + 3 spare + 8 datt (edge lanes summed) + 8 spare (the bias
+  // gradient is the host's) (+ DWP: the lanes' 20 dWp sums, read before the scratch is reused)
+  constexpr int NV = 56 + (DWP ? PB_NDW : 0);
+  float v[NV];
+  if (DWP) {  // v[56 + (ft * 2 + nt) * 4 + r] = the MFMA sums, v[72 + ft * 2 + j] = the P0 terms
+#pragma unroll
+    for (int ft = 0; ft < 2; ++ft) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[56 + ft * 8 + k] = Lw[10 * ft + k];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) v[72 + ft * 2 + j] = Lw[10 * ft + 8 + j];
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[(mt * 2 + nt) * 4 + r] = accW[mt][nt][r];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) v[32 + mt] = db[mt];
+  {
+    float sel = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float t = group_sum<16>(k < 8 ? dg[k / 4][k % 4] : dbt[(k - 8) / 4][k % 4]);
+      sel = c == k ? t : sel;
+    }
+    v[36] = sel;
+  }
+  v[37] = v[38] = v[39] = 0.f;
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[40 + q * 4 + r] = group_sum<16>(datt[q][r]);
+      v[48 + q * 4 + r] = 0.f;
+    }
+  wg_reduce_ordered<NV, kWaves, NL>(v, lds, wave, lane);
+  if (wave == 0) {
+    float* o = part + int64_t(blockIdx.x) * ldPart;
+    if (DWP) {  // [32 x ldWpo] after the prologue/attention part, scaled as the epilogue's
+      float* od = o + PB2_PART;
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            od[(16 * ft + 4 * g + r) * ep.ldWpo + 16 * nt + c] = v[56 + (ft * 2 + nt) * 4 + r] * scale;
+      float t0[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t0[k] = sum_groups(v[72 + k]);
+      if (ep.P0 && g == 0) {
+#pragma unroll
+        for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) od[(16 * ft + c) * ep.ldWpo + 32 + j] = t0[ft * 2 + j] * scale;
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[(mt * 16 + 4 * g + r) * F + nt * 16 + c] = v[(mt * 2 + nt) * 4 + r];
+    float tt[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tt[k] = sum_groups(v[32 + k]);
+    if (g == 0) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) o[NX * F + mt * 16 + c] = tt[mt];
+    }
+    {  // dgamma / dbeta: lane (g, c) holds value c of group g: feature 16 (c / 4 % 2) + 4 g + c % 4
+      const int k = c & 7;
+      o[NX * F + NX + (c < 8 ? 0 : F) + 16 * (k >> 2) + 4 * g + (k & 3)] = v[36];
+    }
+    if (c == 0) {
+      float* oa = o + PB2_PRO;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        *reinterpret_cast<float4*>(oa + 16 * q + 4 * g) =
+            make_float4(v[40 + q * 4], v[40 + q * 4 + 1], v[40 + q * 4 + 2], v[40 + q * 4 + 3]);
+        *reinterpret_cast<float4*>(oa + F + 16 * q + 4 * g) = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  }
+}
+#endif  // GASFM_PBWD_T
 
 int grid_cam_pbwd(int n_items) {
   return resident_grid(reinterpret_cast<const void*>(&edge_cam_pbwd_kernel<true, true, false, false>), kThreads, 0,

@@ -253,7 +253,8 @@ def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None, dXR=None):
     dgam = tot[o + 64:o + 96] if ctx.has_ln else None
     dbet = tot[o + 96:o + 128] if ctx.has_ln else None
     dbias = ta[32:]
-    if getattr(ctx, "sharded", False):
+    if getattr(ctx, "sharded", False) or (CAM_PBWD and plan.n_items):
+        # edge_cam_pbwd leaves the bias gradient to this column sum of gout over all targets
         dbias = replicated_dbias(g_c, ctx.defer)
     return (dP, dgam, dbet, dW[:32], db[:32], dW[32:], db[32:], dWp, None, None, dXR,
             ta[:32].view(ctx.att_shape), dbias, None, None, None, None, None, None, None)
