@@ -905,25 +905,22 @@ __global__ __launch_bounds__(kThreads, GASFM_CAM_MINW) void edge_cam_bwd_kernel(
 
 // =============================================================================================
 // backward, fused: camera attention + edge prologue of the block in ONE pass over the camera
-// plan's items (gasfm_edge_cam_pbwd).  Per 16-edge tile:
-//   XLc = Wc relu(LN(P)) + bc recomputed (T layout, as edge_cam_bwd), the camera attention's
-//   backward -> dXLc in registers (T layout: the A operand of the next products as it stands);
-//   dP_hat = dXLp Wpt + dXLc Wc + dRes (scale Wp[:, :32])  (C layout, A = T-layout rows);
-//   dP = LN_bwd(mask * dP_hat) + dRes  (C layout, stored), dgamma, dbeta;
-//   dW += [dXLp | dXLc]^T relu(LN(P)), db  (C-layout operands; dXLc through a per-wave LDS
-//   transpose, dXLp / P / dRes re-read in C layout from L1).
+// plan's items (gasfm_edge_cam_pbwd).  Per 16-edge tile, all in the T layout (lane (g, c): edge c,
+// features 16 u + 4 g + j) except the weight-gradient operands:
+//   P_hat = relu(LN(P)); XLc = Wc P_hat + bc recomputed; the camera attention's backward -> dXLc;
+//   dP_hat = dXLp Wpt + dXLc Wc + dRes (scale Wp[:, :32])  (transposed products: B = T-layout rows);
+//   dP = LN_bwd(mask * dP_hat) + dRes (stored), dgamma, dbeta;
+//   dW += [dXLp | dXLc]^T P_hat, db  (C-layout operands through a per-wave LDS transpose).
 // Replaces edge_cam_bwd + edge_prologue_bwd: dXLc (128 B per edge) is neither written nor read
-// back, and P is read once.  Semantics: exactly those two kernels' (same partial-row layouts,
-// concatenated: [dW 64x32 | db 64 | dgamma 32 | dbeta 32 | datt 32 | dbias 32] per workgroup).
+// back, and P is read once.  Partial rows per workgroup: [dW 64x32 | db 64 | dgamma 32 | dbeta 32 |
+// datt 32 | 0 (32: the bias gradient is the host's column sum of gout)].
 // =============================================================================================
-// Measured choices (tools/edge_bench.py, tools/gpu_pbwd_ab.sh): the C-layout
-// LayerNorm statistics are the T-layout ones (computed for XLc) moved across by lane shuffles, and
-// dP is stored through a bounds-checked buffer descriptor per work item (rows past the item's end are
-// dropped by the range check), so no per-row branch splits the tile's code (683-692 -> 645-649 us);
-// EPI's dP0 goes back to the T layout through the free transpose tile 0 (a dot per lane, two
-// cross-group sums) rather than eight 16-lane DPP sums; DWP's sums are scalar LDS read-modify-writes.
-// Rejected in round 4: exec-mask-free tile loops, fewer registers held across tiles (spills 23 -> 6,
-// no faster), dXLp in point order, block 0's epilogue folded in, XLc kept by the forward seam, static
+// Measured choices (tools/edge_bench.py, tools/gpu_ab_libs.sh): round 5's T-layout
+// LayerNorm backward (below) replaced round 4's C-layout one (757 -> 675 us at config 4); dP is
+// stored through a bounds-checked buffer descriptor per work item (rows past the item's end are
+// dropped by the range check), so no per-row branch splits the tile's code; DWP's sums are LDS
+// read-modify-writes.  Rejected in round 4: exec-mask-free tile loops, fewer registers held across
+// tiles, dXLp in point order, block 0's epilogue folded in, XLc kept by the forward seam, static
 // wave priority.
 constexpr int PB2_PRO = NX * F + NX + 2 * F;  // the prologue_bwd part row
 constexpr int PB2_PART = PB2_PRO + BP_PART;
@@ -949,498 +946,10 @@ struct PbwdEpi {
   int ldWpo;          // DWP: dWp row width in the part row (34 with P0, 32 without)
 };
 
-// C-layout rows of a [*, 32] tensor: v[ft][r] = X[row0 + 4 g + r][16 ft + c] (rows clamped, not masked)
-__device__ __forceinline__ void cl_load32(const float* __restrict__ X, int64_t ld, int64_t row0, int nrows,
-                                          f32x4 (&v)[2], int lane) {
-  const int c = lane & 15, g = lane >> 4;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int rr = 4 * g + r;
-    const float* p = X + (row0 + (rr < nrows ? rr : 0)) * ld + c;
-    v[0][r] = p[0];
-    v[1][r] = p[16];
-  }
-}
-
-// acc[nt] += X M^T, X (T-layout slabs, K = 32) as the A operand: acc[nt][r] = Y[row 4 g + r][16 nt + c]
-__device__ __forceinline__ void prod_c2(const float4* __restrict__ Q, const f32x4 (&x)[2], f32x4 (&acc)[2],
-                                        int lane) {
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    float4 w[2];
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) w[nt] = Q[(nt * 2 + u) * 64 + lane];
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma16(x[u][0], w[nt].x, acc[nt]);
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma16(x[u][1], w[nt].y, acc[nt]);
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma16(x[u][2], w[nt].z, acc[nt]);
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) acc[nt] = mfma16(x[u][3], w[nt].w, acc[nt]);
-  }
-}
-
 #ifndef GASFM_PBWD_MINW
 #define GASFM_PBWD_MINW 2
 #endif
-// 1: the LayerNorm backward in the T layout (round 5); 0: in the C layout (round 4)
-#ifndef GASFM_PBWD_T
-#define GASFM_PBWD_T 1
-#endif
 
-#if !GASFM_PBWD_T
-template <bool LN, bool RES, bool EPI, bool DWP>
-__global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kernel(
-    const float* __restrict__ P, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
-    const float* __restrict__ Wpt, const float* __restrict__ Wc, const float* __restrict__ bc,
-    const float* __restrict__ Wp, int ldWp, float scale, const float* __restrict__ XR, int64_t ldXR,
-    const float* __restrict__ att, const float* __restrict__ bias, float slope, const float* __restrict__ out,
-    int64_t ldOut, const float* __restrict__ seg_max, const float* __restrict__ seg_sum, int64_t ldStat,
-    const float* __restrict__ gout, int64_t ldG, const gasfm_work_item* __restrict__ items, int n_items,
-    const float* __restrict__ dXLp, int64_t ldXp, const float* __restrict__ dRes, float* __restrict__ dP,
-    float* __restrict__ dXR, int64_t ldDXR, float* __restrict__ part_dxr, float* __restrict__ part, int64_t ldPart,
-    PbwdEpi ep) {
-  static_assert(!DWP || (LN && RES), "edge_cam_pbwd: the epilogue weight gradient needs relu(LN(P)) and dRes");
-  // LDS: weight slabs (Wc for XLc; Wpt^T, Wc^T, (scale Wp)^T for dP_hat), the per-feature vectors,
-  // per wave four 16 x 32 transpose tiles (T -> C layout of P, dXLp, dRes, dXLc), and (DWP) per
-  // wave the lanes' running dWp sums
-  constexpr int QW = F * F;  // floats per 32 x 32 slab set
-  constexpr int OV = 4 * QW, OT = OV + (EPI ? 6 * F : 4 * F), WT = 4 * TR * LDT;
-  constexpr int OD = OT + kWaves * WT;
-  constexpr int NLS = (DWP ? PB_NDW : 0) + (EPI ? 2 : 0);  // per-lane LDS sums
-  constexpr int NL = OD + kWaves * NLS * kW;
-  __shared__ __attribute__((aligned(16))) float lds[NL];
-  float* WcQ = lds;
-  float* WptTQ = lds + QW;
-  float* WcTQ = lds + 2 * QW;
-  float* WqTQ = lds + 3 * QW;
-  float* V = lds + OV;  // [gamma | beta | bc | att] (32 each), (EPI) [scale_e We[:, 32] | scale_e We[:, 33]]
-  stage_slabs32<F, kThreads>([&](int q) { return Wc[q]; }, WcQ);
-  stage_slabs32<F, kThreads>([&](int q) { return Wpt[(q % F) * F + q / F]; }, WptTQ);
-  stage_slabs32<F, kThreads>([&](int q) { return Wc[(q % F) * F + q / F]; }, WcTQ);
-  if (RES) stage_slabs32<F, kThreads>([&](int q) { return scale * Wp[(q % F) * ldWp + q / F]; }, WqTQ);
-  if (threadIdx.x < F) {
-    V[threadIdx.x] = LN ? gam[threadIdx.x] : 1.f;
-    V[F + threadIdx.x] = LN ? bet[threadIdx.x] : 0.f;
-    V[2 * F + threadIdx.x] = bc[threadIdx.x];
-    V[3 * F + threadIdx.x] = att[threadIdx.x];
-    if (EPI) {
-      V[4 * F + threadIdx.x] = ep.dP0 ? ep.scale * ep.We[threadIdx.x * ep.ldWe + 32] : 0.f;
-      V[5 * F + threadIdx.x] = ep.dP0 ? ep.scale * ep.We[threadIdx.x * ep.ldWe + 33] : 0.f;
-    }
-  }
-  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
-  const int c = lane & 15, g = lane >> 4;
-  float* Tt = lds + OT + wave * WT;  // tiles 0: P, 1: dXLp, 2: dRes, 3: dXLc
-  // (DWP) value k of this lane's dWp sums at Lw[k]; (EPI) the item's dSv column sums at Ls[0, 1]
-  float* Lw = lds + OD + (wave * kW + lane) * NLS;
-  float* Ls = Lw + (DWP ? PB_NDW : 0);
-#pragma unroll
-  for (int k = 0; k < NLS; ++k) Lw[k] = 0.f;
-  const float gC[2] = {LN ? gam[c] : 1.f, LN ? gam[16 + c] : 1.f}, bC[2] = {LN ? bet[c] : 0.f, LN ? bet[16 + c] : 0.f};
-  __syncthreads();
-  // T-layout vector at this lane's features 16 q + 4 g .. + 3
-  auto vecT = [&](int which, int q) {
-    const float4 t = *reinterpret_cast<const float4*>(V + which * F + 16 * q + 4 * g);
-    return f32x4{t.x, t.y, t.z, t.w};
-  };
-  // T -> C layout through tile k of this wave: writes the two slabs, returns the C-layout rows
-  auto to_c = [&](int k, const f32x4 (&t)[2], f32x4 (&o)[2]) {
-    float* T = Tt + k * TR * LDT;
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-      *reinterpret_cast<float4*>(T + c * LDT + 16 * u + 4 * g) = make_float4(t[u][0], t[u][1], t[u][2], t[u][3]);
-    // one wave's LDS instructions execute in order: a compiler barrier suffices
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int ft = 0; ft < 2; ++ft)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[ft][r] = T[(4 * g + r) * LDT + 16 * ft + c];
-  };
-  f32x4 accW[4][2];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) accW[mt][0] = accW[mt][1] = zero4();
-  float db[4] = {0.f, 0.f, 0.f, 0.f}, dg[2] = {0.f, 0.f}, dbt[2] = {0.f, 0.f};
-  f32x4 datt[2] = {zero4(), zero4()}, dbias[2] = {zero4(), zero4()};
-  const int gw = blockIdx.x * kWaves + wave, nw = gridDim.x * kWaves;
-
-  // next tile's rows of P, dXLp, dRes in T layout, one tile ahead (clamped, masked where consumed)
-  f32x4 nPT[2], nXT[2], nRT[2];
-  float2 nP0 = make_float2(0.f, 0.f);  // (DWP) P0 of edge c (a dummy read of P without P0)
-  const float* p0p = (DWP && ep.P0) ? ep.P0 : P;
-  auto issue = [&](int64_t row0, int nrows) {
-    const int64_t xrow = row0 + (c < nrows ? c : 0);
-    load_slabs32(P, row0, nrows, nPT, lane);
-    {
-      const float* p = dXLp + xrow * ldXp + 4 * g;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const float4 t = *reinterpret_cast<const float4*>(p + 16 * u);
-        nXT[u] = f32x4{t.x, t.y, t.z, t.w};
-      }
-    }
-    if (RES) load_slabs32(dRes, row0, nrows, nRT, lane);
-    if (DWP) nP0 = *reinterpret_cast<const float2*>(p0p + xrow * 2);
-  };
-  auto rows_at = [](const gasfm_work_item& w, int64_t row0) { return int(w.end - row0 < TR ? w.end - row0 : TR); };
-  gasfm_work_item w{0, 0, 0, -1};
-  if (gw < n_items) {
-    w = items[gw];
-    if (w.begin < w.end) issue(w.begin, rows_at(w, w.begin));
-  }
-  for (int it = gw; it < n_items; it += nw) {
-    const int64_t seg = w.seg;
-    // dP's descriptor for this item's rows (wave-uniform inputs made provably uniform)
-    const int64_t ibeg = __builtin_amdgcn_readfirstlane(int(w.begin));
-    const int ilen = __builtin_amdgcn_readfirstlane(int(w.end - w.begin));
-    const auto dPrs = __builtin_amdgcn_make_buffer_rsrc(dP + ibeg * F, 0, ilen * F * 4, 0x00020000);
-    // (EPI) dP0 rows of this item; without dP0 an empty range (every store dropped)
-    const auto dP0rs = __builtin_amdgcn_make_buffer_rsrc(EPI && ep.dP0 ? ep.dP0 + ibeg * 2 : dP, 0,
-                                                         EPI && ep.dP0 ? ilen * 8 : 0, 0x00020000);
-    // per-camera constants of the attention backward (edge_cam_bwd_kernel)
-    f32x4 xr[2], gv[2];
-    float M[2], inv[2], delta[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int f0 = 16 * q + 4 * g, h = 2 * q + (g >> 1);
-      const float4 x4 = *reinterpret_cast<const float4*>(XR + seg * ldXR + f0);
-      const float4 g4v = *reinterpret_cast<const float4*>(gout + seg * ldG + f0);
-      const float4 o4 = *reinterpret_cast<const float4*>(out + seg * ldOut + f0);
-      const float4 b4 = *reinterpret_cast<const float4*>(bias + f0);
-      xr[q] = f32x4{x4.x, x4.y, x4.z, x4.w};
-      gv[q] = f32x4{g4v.x, g4v.y, g4v.z, g4v.w};
-      float d = fmaf(g4v.x, o4.x - b4.x, fmaf(g4v.y, o4.y - b4.y, fmaf(g4v.z, o4.z - b4.z, g4v.w * (o4.w - b4.w))));
-      delta[q] = xsum16(d);
-      M[q] = seg_max[seg * ldStat + h];
-      inv[q] = 1.f / (seg_sum[seg * ldStat + h] + 1e-16f);
-    }
-    const bool first = it == 0 || items[it - 1].seg != w.seg;
-    if (first && c == 0) {
-#pragma unroll
-      for (int q = 0; q < 2; ++q) dbias[q] += gv[q];
-    }
-    f32x4 dxr[2] = {zero4(), zero4()};
-    gasfm_work_item wn{0, 0, 0, -1};
-    const bool more = it + nw < n_items;
-    if (more) wn = items[it + nw];
-    if (w.begin >= w.end && more && wn.begin < wn.end) issue(wn.begin, rows_at(wn, wn.begin));
-    for (int64_t row0 = w.begin; row0 < w.end; row0 += TR) {
-      const int nrows = rows_at(w, row0);
-      f32x4 PT[2] = {nPT[0], nPT[1]}, XT[2] = {nXT[0], nXT[1]}, RT[2];
-      if (RES) {
-        RT[0] = nRT[0];
-        RT[1] = nRT[1];
-      }
-      const float2 p0t = nP0;
-      {  // the next tile (this item's, else the next item's first; the last one re-reads itself)
-        int64_t r1 = row0;
-        int n1 = nrows;
-        if (row0 + TR < w.end) {
-          r1 = row0 + TR;
-          n1 = rows_at(w, r1);
-        } else if (more && wn.begin < wn.end) {
-          r1 = wn.begin;
-          n1 = rows_at(wn, r1);
-        }
-        issue(r1, n1);
-      }
-      const bool valid = c < nrows;
-      // C layouts of P, dXLp, dRes (raw) through LDS, before P's slabs are normalised in place
-      f32x4 PC[2], XC[2], RC[2];
-      to_c(0, PT, PC);
-      to_c(1, XT, XC);
-      if (RES) to_c(2, RT, RC);
-      if (DWP) {  // edge c's P0 in tile 2's padding columns 32, 33 (read back in C layout by the dWp sums)
-        float* T2 = Tt + 2 * TR * LDT + c * LDT + 32;
-        T2[0] = p0t.x;
-        T2[1] = p0t.y;
-      }
-      // ---- camera attention backward (T layout: edge c, features 16 q + 4 g + r)
-      float tmean = 0.f, trstd = 1.f;  // LayerNorm statistics of edge c (T layout)
-      if (LN) {
-        float gs[2][4], bs[2][4];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const f32x4 a = vecT(0, q), b = vecT(1, q);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            gs[q][r] = a[r];
-            bs[q][r] = b[r];
-          }
-        }
-        phat_slabs_st<LN>(PT, gs, bs, eps, tmean, trstd);
-        // edge c's statistics next to tile 3's row c (every lane group: same values), read back by the
-        // C-layout rows (one ds_write_b64, four ds_read_b64 per tile; no lane shuffles)
-        *reinterpret_cast<float2*>(Tt + 3 * TR * LDT + c * LDT + 32) = make_float2(tmean, trstd);
-      }
-      f32x4 xc[2] = {vecT(2, 0), vecT(2, 1)};  // b_c, then + Wc P_hat^T
-      xl_slabs<2>(reinterpret_cast<const float4*>(WcQ), PT, xc, lane);
-      f32x4 dXc[2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const f32x4 at = vecT(3, q);
-        float z[4], lz[4], p = 0.f, da = 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          z[r] = xc[q][r] + xr[q][r];
-          lz[r] = leaky(z[r], slope);
-          p = fmaf(lz[r], at[r], p);
-          da = fmaf(gv[q][r], xc[q][r], da);
-        }
-        p = xsum16(p);
-        da = xsum16(da);
-        const float alpha = valid ? __expf(p - M[q]) * inv[q] : 0.f;
-        const float de = alpha * (da - delta[q]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float dz = de * at[r] * (z[r] > 0.f ? 1.f : slope);
-          dXc[q][r] = fmaf(alpha, gv[q][r], dz);  // 0 for invalid edges
-          dxr[q][r] += dz;
-          datt[q][r] = fmaf(de, lz[r], datt[q][r]);
-        }
-      }
-      // ---- dP_hat (C layout) = dXLp Wpt + dXLc Wc (+ dRes scale Wp)
-      f32x4 dph[2] = {zero4(), zero4()};
-      prod_c2(reinterpret_cast<const float4*>(WptTQ), XT, dph, lane);
-      prod_c2(reinterpret_cast<const float4*>(WcTQ), dXc, dph, lane);
-      if (RES) prod_c2(reinterpret_cast<const float4*>(WqTQ), RT, dph, lane);
-      f32x4 XcC[2];
-      to_c(3, dXc, XcC);
-      // ---- LayerNorm backward (statistics of edge 4 g + r live on lane c = 4 g + r), dP
-      f32x4 ph[2];     // relu(LN(P)) (C layout) for the weight gradient
-      float dv[4][2];  // dP (C layout)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool live = 4 * g + r < nrows;
-        float mean = 0.f, rstd = 1.f;
-        if (LN) {
-          const float2 st = *reinterpret_cast<const float2*>(Tt + 3 * TR * LDT + (4 * g + r) * LDT + 32);
-          mean = st.x;
-          rstd = st.y;
-        }
-        float xh[2], gvv[2], s1 = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          xh[nt] = LN ? (PC[nt][r] - mean) * rstd : PC[nt][r];
-          ph[nt][r] = LN ? fmaxf(fmaf(xh[nt], gC[nt], bC[nt]), 0.f) : xh[nt];
-          float dy = live ? dph[nt][r] : 0.f;
-          if (LN) {
-            dy = (fmaf(xh[nt], gC[nt], bC[nt]) > 0.f) ? dy : 0.f;
-            dg[nt] = fmaf(dy, xh[nt], dg[nt]);
-            dbt[nt] += dy;
-          }
-          gvv[nt] = LN ? dy * gC[nt] : dy;
-          s1 += gvv[nt];
-          s2 = fmaf(gvv[nt], xh[nt], s2);
-        }
-        if (LN) {
-          s1 = sum16(s1) * (1.f / F);
-          s2 = sum16(s2) * (1.f / F);
-        }
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          float v = LN ? rstd * (gvv[nt] - s1 - xh[nt] * s2) : gvv[nt];
-          if (RES) v += RC[nt][r];
-          dv[r][nt] = v;
-        }
-      }
-      // rows past the item's end fall outside the descriptor's range: the hardware drops them
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-          __builtin_amdgcn_raw_buffer_store_b32(  // (the builtin's data operand is a 32-bit integer)
-              __float_as_uint(dv[r][nt]), dPrs, int(((row0 - ibeg + 4 * g + r) * F + 16 * nt + c) * 4), 0, 0);
-      if (EPI) {
-        // the previous block's epilogue: column sums of dP (dSv), and dP0 = scale_e We[:, 32:34]^T dP
-        // per row: dP through tile 0 (free since P's transpose) back to the T layout, lane (g, c)
-        // dots row c's features 16 u + 4 g .. + 3, the 4 lane groups summed; group 0 stores the
-        // row's pair (the other groups an out-of-range offset)
-        float* T0 = Tt;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool live = 4 * g + r < nrows;
-          // the item's column sums of dP (dSv) live in LDS: no registers held across tiles
-          Ls[0] += live ? dv[r][0] : 0.f;
-          Ls[1] += live ? dv[r][1] : 0.f;
-          T0[(4 * g + r) * LDT + c] = dv[r][0];
-          T0[(4 * g + r) * LDT + 16 + c] = dv[r][1];
-        }
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-        float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const float4 d4 = *reinterpret_cast<const float4*>(T0 + c * LDT + 16 * u + 4 * g);
-          const f32x4 a = vecT(4, u), b = vecT(5, u);
-          s0 = fmaf(d4.x, a[0], fmaf(d4.y, a[1], fmaf(d4.z, a[2], fmaf(d4.w, a[3], s0))));
-          s1 = fmaf(d4.x, b[0], fmaf(d4.y, b[1], fmaf(d4.z, b[2], fmaf(d4.w, b[3], s1))));
-        }
-        s0 = sum_groups(s0);
-        s1 = sum_groups(s1);
-        const int off = g == 0 ? int((row0 - ibeg + c) * 8) : 0x7ffffff0;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s0), dP0rs, off, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s1), dP0rs, off + 4, 0, 0);
-      }
-      // ---- dW += [dXLp | dXLc]^T relu(LN(P)), db (C layout, row 4 g + s at step s)
-#pragma unroll
-      for (int ft = 0; ft < 2; ++ft)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) XC[ft][r] = 4 * g + r < nrows ? XC[ft][r] : 0.f;
-#pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) {
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const float a = mt < 2 ? XC[mt][s2] : XcC[mt - 2][s2];
-          db[mt] += a;
-          accW[mt][0] = mfma16(a, ph[0][s2], accW[mt][0]);
-          accW[mt][1] = mfma16(a, ph[1][s2], accW[mt][1]);
-        }
-      }
-      if (DWP) {
-        // this block's epilogue: dWp += dRes^T [relu(LN(P)) | P0] (dead rows zeroed), one 16-feature
-        // half of dRes at a time, its rows and P0 re-read from tile 2 (no registers held across the
-        // tile), the products added into the lanes' LDS sums
-        const float* T2 = Tt + 2 * TR * LDT;
-#pragma unroll
-        for (int ft = 0; ft < 2; ++ft) {
-          float rr[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) rr[r] = 4 * g + r < nrows ? T2[(4 * g + r) * LDT + 16 * ft + c] : 0.f;
-          f32x4 ap[2] = {zero4(), zero4()};
-#pragma unroll
-          for (int s2 = 0; s2 < 4; ++s2)
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt) ap[nt] = mfma16(rr[s2], ph[nt][s2], ap[nt]);
-          float a0[2] = {0.f, 0.f};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            a0[0] = fmaf(rr[r], T2[(4 * g + r) * LDT + 32], a0[0]);
-            a0[1] = fmaf(rr[r], T2[(4 * g + r) * LDT + 33], a0[1]);
-          }
-          // this half's 10 sums: [ap[0] | ap[1] | a0] at Lw[lane * 20 + 10 ft ..] (lane stride 20
-          // floats: a 16-lane b128 access touches 16 distinct bank quads)
-          float* q = Lw + 10 * ft;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) q[k] += ap[k / 4][k % 4];
-          q[8] += a0[0];
-          q[9] += a0[1];
-        }
-      }
-      __builtin_amdgcn_wave_barrier();  // this tile's transpose reads before the next tile's writes
-      asm volatile("" ::: "memory");
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = group_sum<16>(dxr[q][r]);
-      if (c == 0) {
-        float* d = (w.slot < 0) ? dXR + seg * ldDXR : part_dxr + int64_t(w.slot) * F;
-        *reinterpret_cast<float4*>(d + 16 * q + 4 * g) = make_float4(v[0], v[1], v[2], v[3]);
-      }
-    }
-    if (EPI) {
-      const float s0 = sum_groups(Ls[0]) * ep.scale, s1 = sum_groups(Ls[1]) * ep.scale;
-      Ls[0] = Ls[1] = 0.f;
-      if (g == 0) {
-        float* d = (w.slot < 0) ? ep.dSv + seg * F : ep.part_dsv + int64_t(w.slot) * F;
-        d[c] = s0;
-        d[16 + c] = s1;
-      }
-    }
-    w = wn;
-  }
-  // workgroup reduction: 32 accW + 4 db + 2 dg + 2 dbt (C layout) + 16 (datt, dbias summed over
-  // the 16 edge columns first) (+ DWP: the lanes' 20 dWp sums, read before the scratch is reused)
-  constexpr int NV = 56 + (DWP ? PB_NDW : 0);
-  float v[NV];
-  if (DWP) {  // v[56 + (ft * 2 + nt) * 4 + r] = the MFMA sums, v[72 + ft * 2 + j] = the P0 terms
-#pragma unroll
-    for (int ft = 0; ft < 2; ++ft) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[56 + ft * 8 + k] = Lw[10 * ft + k];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) v[72 + ft * 2 + j] = Lw[10 * ft + 8 + j];
-    }
-  }
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[(mt * 2 + nt) * 4 + r] = accW[mt][nt][r];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) v[32 + mt] = db[mt];
-  v[36] = dg[0];
-  v[37] = dg[1];
-  v[38] = dbt[0];
-  v[39] = dbt[1];
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      v[40 + q * 4 + r] = group_sum<16>(datt[q][r]);
-      v[48 + q * 4 + r] = group_sum<16>(dbias[q][r]);
-    }
-  wg_reduce_ordered<NV, kWaves, NL>(v, lds, wave, lane);
-  if (wave == 0) {
-    float* o = part + int64_t(blockIdx.x) * ldPart;
-    if (DWP) {  // [32 x ldWpo] after the prologue/attention part, scaled as the epilogue's
-      float* od = o + PB2_PART;
-#pragma unroll
-      for (int ft = 0; ft < 2; ++ft)
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            od[(16 * ft + 4 * g + r) * ep.ldWpo + 16 * nt + c] = v[56 + (ft * 2 + nt) * 4 + r] * scale;
-      float t0[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) t0[k] = sum_groups(v[72 + k]);
-      if (ep.P0 && g == 0) {
-#pragma unroll
-        for (int ft = 0; ft < 2; ++ft)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) od[(16 * ft + c) * ep.ldWpo + 32 + j] = t0[ft * 2 + j] * scale;
-      }
-    }
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[(mt * 16 + 4 * g + r) * F + nt * 16 + c] = v[(mt * 2 + nt) * 4 + r];
-    float tt[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) tt[k] = sum_groups(v[32 + k]);
-    if (g == 0) {
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) o[NX * F + mt * 16 + c] = tt[mt];
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        o[NX * F + NX + nt * 16 + c] = tt[4 + nt];
-        o[NX * F + NX + F + nt * 16 + c] = tt[6 + nt];
-      }
-    }
-    if (c == 0) {
-      float* oa = o + PB2_PRO;
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        *reinterpret_cast<float4*>(oa + 16 * q + 4 * g) =
-            make_float4(v[40 + q * 4], v[40 + q * 4 + 1], v[40 + q * 4 + 2], v[40 + q * 4 + 3]);
-        *reinterpret_cast<float4*>(oa + F + 16 * q + 4 * g) =
-            make_float4(v[48 + q * 4], v[48 + q * 4 + 1], v[48 + q * 4 + 2], v[48 + q * 4 + 3]);
-      }
-    }
-  }
-}
-
-#endif  // !GASFM_PBWD_T
-
-#if GASFM_PBWD_T
 // T-layout backward (round 5).  The LayerNorm backward runs where the forward's statistics are --
 // lane (g, c) holds 8 features of edge c -- instead of in the C layout (4 edges x 2 features per
 // lane): dP_hat comes out of the transposed products (A = the same weight slabs, B = the T-layout
@@ -1915,7 +1424,6 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
     }
   }
 }
-#endif  // GASFM_PBWD_T
 
 int grid_cam_pbwd(int n_items) {
   return resident_grid(reinterpret_cast<const void*>(&edge_cam_pbwd_kernel<true, true, false, false>), kThreads, 0,
