@@ -618,9 +618,14 @@ def edge_cam_bwd(P, ln_w, ln_b, eps, Wc, bc, XR, att, bias, slope, out, seg_max,
     check(st, "gasfm_edge_cam_bwd")
 
 
+def _ld_stat(seg_max):
+    """row stride of the [N, heads] statistics (4 for their own tensors; the partial-row stride when
+    they are columns of a packed partial buffer)"""
+    return seg_max.stride(0) if seg_max is not None else 4
+
+
 def edge_seam_fwd(Pb, P0, pt, lnw_b, lnb_b, eps_b, Wp, bp, Sp, Sv, Sg, scale, Pout, ln_w, ln_b, eps, Wpt, bpt, Wc, bc,
-                  XLp, pos, XR, att, bias, slope, plan_items, n_items, finalize, out, seg_max, seg_sum, part,
-                  ldStat=4):
+                  XLp, pos, XR, att, bias, slope, plan_items, n_items, finalize, out, seg_max, seg_sum, part):
     """Block b's edge epilogue (P' = Pout) + block b+1's prologue and camera attention forward in one
     pass (csrc/edge_cam.hip edge_seam_fwd); outputs as edge_cam_fwd's plus Pout."""
     _req(Pb, "Pb", 32)
@@ -630,14 +635,14 @@ def edge_seam_fwd(Pb, P0, pt, lnw_b, lnb_b, eps_b, Wp, bp, Sp, Sv, Sg, scale, Po
                                    _p(Sp), _p(Sv), ldSv, _p(Sg), scale, _p(Pout), _p(ln_w), _p(ln_b), eps, _p(Wpt),
                                    _p(bpt), _p(Wc), _p(bc), _p(XLp), XLp.stride(0), _p(pos), _p(XR), ldXR, _p(att),
                                    _p(bias), slope, _p(plan_items), n_items, int(finalize), _p(out),
-                                   out.stride(0) if out is not None else 0, _p(seg_max), _p(seg_sum), ldStat, _p(part),
-                                   _stream(Pb))
+                                   out.stride(0) if out is not None else 0, _p(seg_max), _p(seg_sum), _ld_stat(seg_max),
+                                   _p(part), _stream(Pb))
     check(st, "gasfm_edge_seam_fwd")
 
 
 def edge0_seam_fwd(P, pt, lna_w, lna_b, lnb_w, lnb_b, eps0, Wp, bp, Wsk, bsk, Sp, Sv, Sg, scale, Pout, ln_w, ln_b, eps,
                    Wpt, bpt, Wc, bc, XLp, pos, XR, att, bias, slope, plan_items, n_items, finalize, out, seg_max,
-                   seg_sum, part, ldStat=4):
+                   seg_sum, part):
     """Block 0's edge epilogue (2-wide P, edge0_epilogue_fwd) + block 1's prologue and camera
     attention forward in one pass (csrc/edge_cam.hip edge_seam_fwd, EP0); outputs as
     edge_seam_fwd's."""
@@ -648,8 +653,8 @@ def edge0_seam_fwd(P, pt, lna_w, lna_b, lnb_w, lnb_b, eps0, Wp, bp, Wsk, bsk, Sp
                                     _p(Wsk), _p(bsk), _p(Sp), _p(Sv), ldSv, _p(Sg), scale, _p(Pout), _p(ln_w), _p(ln_b),
                                     eps, _p(Wpt), _p(bpt), _p(Wc), _p(bc), _p(XLp), XLp.stride(0), _p(pos), _p(XR),
                                     ldXR, _p(att), _p(bias), slope, _p(plan_items), n_items, int(finalize), _p(out),
-                                    out.stride(0) if out is not None else 0, _p(seg_max), _p(seg_sum), ldStat,
-                                    _p(part), _stream(P))
+                                    out.stride(0) if out is not None else 0, _p(seg_max), _p(seg_sum),
+                                    _ld_stat(seg_max), _p(part), _stream(P))
     check(st, "gasfm_edge0_seam_fwd")
 
 
@@ -663,7 +668,8 @@ def edge_cam_pbwd(P, ln_w, ln_b, eps, Wpt, Wc, bc, Wp, scale, XR, att, bias, slo
                   plan_items, n_items, dXLp, dRes, dP, dXR, part_dxr, part, ldStat=4, epi=None, dwp=None):
     """The camera attention's backward and the block's edge prologue backward in one pass
     (csrc/edge_cam.hip edge_cam_pbwd): dP, dXR (+ split partials), part rows
-    [dW 64x32 | db 64 | dgamma 32 | dbeta 32 | datt 32 | dbias 32] per workgroup.
+    [dW 64x32 | db 64 | dgamma 32 | dbeta 32 | datt 32 | 0 (32)] per workgroup (the attention bias
+    gradient is the caller's column sum of gout).
 
     epi = (We, scale_e, dSv, part_dsv, dP0 or None): also the previous block's edge-epilogue
     gradients from this dP (dSv rows / split-camera partial rows of the same plan, dP0).
@@ -1151,16 +1157,21 @@ _GC_W = ("W1", "b1", "gM", "bM", "W2", "b2", "gA", "bA", "WA", "gB", "bB", "WB",
 _GC_D = tuple("d" + k for k in _GC_W)
 
 
+_GC_SHADOW = ("W1", "W2", "WA", "WB", "WC", "WD", "WE")  # the weights with an optional bf16 shadow
+
+
 class _GChain(ctypes.Structure):
-    _fields_ = [(k, _i32) for k in _GC_DIMS] + [("eps_m", _f32), ("eps_h", _f32)] + [(k, _vp) for k in _GC_W]
+    _fields_ = ([(k, _i32) for k in _GC_DIMS] + [("eps_m", _f32), ("eps_h", _f32)] + [(k, _vp) for k in _GC_W]
+                + [(k + "h", _vp) for k in _GC_SHADOW])
 
 
 class _GChainGrads(ctypes.Structure):
     _fields_ = [(k, _vp) for k in _GC_D]
 
 
-def gchain_struct(w, eps_m, eps_h):
-    """gasfm_gchain of the weights dict w (keys _GC_W; the hub's B..E absent for the last block)."""
+def gchain_struct(w, eps_m, eps_h, shadows=None):
+    """gasfm_gchain of the weights dict w (keys _GC_W; the hub's B..E absent for the last block);
+    shadows: dict weight key -> its bf16 shadow (BASELINE config 5) or None."""
     c = _GChain()
     W1, WA = w["W1"], w["WA"]
     hub = w.get("WB") is not None
@@ -1175,6 +1186,11 @@ def gchain_struct(w, eps_m, eps_h):
         if t is not None:
             _req(t, k)
             setattr(c, k, t.data_ptr())
+    for k, t in (shadows or {}).items():
+        if t is not None:
+            if t.dtype != torch.bfloat16 or not t.is_contiguous() or t.shape != w[k].shape:
+                raise ValueError(f"gchain: the bf16 shadow of {k} must be a contiguous bf16 tensor of its shape")
+            setattr(c, k + "h", t.data_ptr())
     return c
 
 

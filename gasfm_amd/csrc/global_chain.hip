@@ -8,7 +8,9 @@
 //       xv  = WB relu(LN_B(g)) + bWB             next block's norm_and_proj_global2view   :497-505
 //       xp  = WC relu(LN_C(g)) + bWC             next block's norm_and_proj_global2scenepoint :512-520
 //   F4  XRv = WD xv + bD,  XRp = WE xp + bE      the next block's two GATv2 lin_r rows (PyG)
-// (the last block's chain ends at F3 with SG only).  Round 3 ran this as gvec launches with a
+// (the last block's chain ends at F3 with SG only).  BASELINE config 5 (round 5): with bf16 weight
+// shadows (gasfm_gchain.W*h) every GEMV streams half the weight bytes (fp32 accumulation; the
+// weight gradients stay fp32: dW = dy x h reads no weight).  Round 3 ran this as gvec launches with a
 // one-workgroup "finish" kernel after every backward GEMV (12 launches per block, ~100 us); here:
 //
 //   gnode_fwd   one wave per output row; the wave's W row is requested FIRST, into registers,
@@ -70,6 +72,17 @@ __device__ __forceinline__ void block_sums(float (&v)[NV], float* scratch) {
   for (int k = 0; k < NV; ++k) v[k] = scratch[k] + scratch[NV + k] + scratch[2 * NV + k] + scratch[3 * NV + k];
 }
 
+// 4 consecutive weights from the bf16 shadow (8-byte load) or the fp32 row (16-byte load)
+template <bool BF>
+__device__ __forceinline__ float4 w4(const float* W, const uint16_t* Wh, int64_t off) {
+  if (BF) {
+    const uint2 t = *reinterpret_cast<const uint2*>(Wh + off);
+    return make_float4(__uint_as_float(t.x << 16), __uint_as_float(t.x & 0xffff0000u), __uint_as_float(t.y << 16),
+                       __uint_as_float(t.y & 0xffff0000u));
+  }
+  return *reinterpret_cast<const float4*>(W + off);
+}
+
 // mean / rstd of a row held as kPer strided values per thread (j = tid + 256 u; 0 past K)
 __device__ __forceinline__ void row_stats(const float (&xv)[kPer], int K, float eps, float* scratch, float& mean,
                                           float& rstd) {
@@ -115,13 +128,14 @@ struct GnFwdProb {
   float* y;          // [N]
   int K, N, blk0;
   float eps;
+  const uint16_t* Wh;  // bf16 shadow of W (null: W)
 };
 struct GnFwdArgs {
   GnFwdProb p[kMaxProb];
   int nprob;
 };
 
-template <int KI>  // float4 per lane of a W row: K <= 256 KI
+template <int KI, bool BF>  // float4 per lane of a W row: K <= 256 KI; BF: the bf16 shadows (every problem's)
 __global__ __launch_bounds__(kFT) void gnode_fwd_kernel(GnFwdArgs a) {
   __shared__ __attribute__((aligned(16))) float h[kMaxK];
   __shared__ float scratch[8];
@@ -136,11 +150,10 @@ __global__ __launch_bounds__(kFT) void gnode_fwd_kernel(GnFwdArgs a) {
   // every load of the kernel first: the wave's W row, the input row and its LayerNorm affine
   // (clamped in-range addresses; values past K are zeroed where consumed)
   float4 w[KI];
-  const float* wr = p.W + int64_t(ic) * K;
 #pragma unroll
   for (int u = 0; u < KI; ++u) {
     const int j = 4 * lane + 256 * u;
-    w[u] = *reinterpret_cast<const float4*>(wr + (j < K ? j : 0));
+    w[u] = w4<BF>(p.W, p.Wh, int64_t(ic) * K + (j < K ? j : 0));
   }
   const bool ln = p.gam != nullptr;
   const float* gp = ln ? p.gam : p.x;
@@ -190,14 +203,20 @@ int launch_fwd(GnFwdArgs& a, hipStream_t st) {
     kmax = a.p[q].K > kmax ? a.p[q].K : kmax;
   }
   for (int q = a.nprob; q < kMaxProb; ++q) a.p[q].blk0 = blocks;
+  bool bf = true;  // the bf16 kernels when every problem has its shadow (no per-load branch)
+  for (int q = 0; q < a.nprob; ++q) bf = bf && a.p[q].Wh != nullptr;
+  auto go = [&](auto k32, auto k16) {
+    const auto kern = bf ? k16 : k32;
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(kFT), 0, st, a);
+  };
   if (kmax <= 256)
-    hipLaunchKernelGGL(gnode_fwd_kernel<1>, dim3(blocks), dim3(kFT), 0, st, a);
+    go(&gnode_fwd_kernel<1, false>, &gnode_fwd_kernel<1, true>);
   else if (kmax <= 1024)
-    hipLaunchKernelGGL(gnode_fwd_kernel<4>, dim3(blocks), dim3(kFT), 0, st, a);
+    go(&gnode_fwd_kernel<4, false>, &gnode_fwd_kernel<4, true>);
   else if (kmax <= 1280)
-    hipLaunchKernelGGL(gnode_fwd_kernel<5>, dim3(blocks), dim3(kFT), 0, st, a);
+    go(&gnode_fwd_kernel<5, false>, &gnode_fwd_kernel<5, true>);
   else
-    hipLaunchKernelGGL(gnode_fwd_kernel<8>, dim3(blocks), dim3(kFT), 0, st, a);
+    go(&gnode_fwd_kernel<8, false>, &gnode_fwd_kernel<8, true>);
   return launch_status("gasfm_gchain_fwd");
 }
 
@@ -222,6 +241,7 @@ struct GnBwdProb {
   float* lnp;        // [slabs][2]
   float* stats;      // (mean, rstd) of x, written by slab 0 (null: not needed)
   int lnfin;
+  const uint16_t* Wh;  // bf16 shadow of W (null: W)
 };
 // The launch's prologue (the previous level's LayerNorm backward, finished per row here):
 //   dy[n] = dres[n] + sum_q rstd (gv_q[n] - S1_q / F - xh[n] S2_q / F),  xh = (x - mean) rstd,
@@ -252,7 +272,7 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int RPT>  // rows per thread: a chunk is 32 RPT rows
+template <int RPT, bool BF>  // rows per thread: a chunk is 32 RPT rows; BF: the bf16 shadows
 __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
   static_assert(32 * RPT == kBT, "one dy row per thread");
   __shared__ float dys[32 * RPT];
@@ -296,7 +316,7 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
 #pragma unroll
   for (int r = 0; r < RPT; ++r) {
     const int n = row0 + rl + 32 * r;
-    w[r] = *reinterpret_cast<const float4*>(p.W + int64_t(n < N ? n : N - 1) * K + col);
+    w[r] = w4<BF>(p.W, p.Wh, int64_t(n < N ? n : N - 1) * K + col);
   }
   const float4 x4 = *reinterpret_cast<const float4*>(p.x + col);
   const bool ln = p.gam != nullptr;
@@ -470,7 +490,10 @@ int launch_bwd(GnBwdArgs& a, float*& ws, uint32_t*& cnt, hipStream_t st, const c
     blocks += p.slabs * p.chunks;
   }
   for (int q = a.nprob; q < kMaxProb; ++q) a.p[q].blk0 = blocks;
-  hipLaunchKernelGGL(gnode_bwd_kernel<kRPT>, dim3(blocks), dim3(kBT), 0, st, a);
+  bool bf = true;
+  for (int q = 0; q < a.nprob; ++q) bf = bf && a.p[q].Wh != nullptr;
+  const auto kern = bf ? &gnode_bwd_kernel<kRPT, true> : &gnode_bwd_kernel<kRPT, false>;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBT), 0, st, a);
   return launch_status(where);
 }
 
@@ -498,6 +521,9 @@ static int gchain_check(const gasfm_gchain* c) {
   }
   const void* ws[] = {c->W1, c->W2, c->WA, c->WB, c->WC, c->WD, c->WE};
   for (const void* p : ws) GASFM_REQUIRE(!p || aligned16(p), "gasfm_gchain: weights must be 16-byte aligned");
+  const void* wh[] = {c->W1h, c->W2h, c->WAh, c->WBh, c->WCh, c->WDh, c->WEh};
+  for (const void* p : wh)
+    GASFM_REQUIRE(!p || reinterpret_cast<uintptr_t>(p) % 8 == 0, "gasfm_gchain: bf16 shadows must be 8-byte aligned");
   return GASFM_OK;
 }
 
@@ -527,23 +553,23 @@ extern "C" int gasfm_gchain_fwd(const gasfm_gchain* c, const float* xcat, const 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   GnFwdArgs a{};
   a.nprob = 1;
-  a.p[0] = GnFwdProb{xcat, nullptr, nullptr, c->W1, c->b1, prev, x1, c->Kc, c->G, 0, 0.f};
+  a.p[0] = GnFwdProb{xcat, nullptr, nullptr, c->W1, c->b1, prev, x1, c->Kc, c->G, 0, 0.f, c->W1h};
   int s = launch_fwd(a, st);
   if (s != GASFM_OK) return s;
-  a.p[0] = GnFwdProb{x1, c->gM, c->bM, c->W2, c->b2, x1, g, c->G, c->G, 0, c->eps_m};
+  a.p[0] = GnFwdProb{x1, c->gM, c->bM, c->W2, c->b2, x1, g, c->G, c->G, 0, c->eps_m, c->W2h};
   s = launch_fwd(a, st);
   if (s != GASFM_OK) return s;
-  a.p[0] = GnFwdProb{g, c->gA, c->bA, c->WA, nullptr, nullptr, sg, c->G, c->NA, 0, c->eps_h};
+  a.p[0] = GnFwdProb{g, c->gA, c->bA, c->WA, nullptr, nullptr, sg, c->G, c->NA, 0, c->eps_h, c->WAh};
   if (hub_on(c)) {
     a.nprob = 3;
-    a.p[1] = GnFwdProb{g, c->gB, c->bB, c->WB, c->bWB, nullptr, xv, c->G, c->NB, 0, c->eps_h};
-    a.p[2] = GnFwdProb{g, c->gC, c->bC, c->WC, c->bWC, nullptr, xp, c->G, c->NC, 0, c->eps_h};
+    a.p[1] = GnFwdProb{g, c->gB, c->bB, c->WB, c->bWB, nullptr, xv, c->G, c->NB, 0, c->eps_h, c->WBh};
+    a.p[2] = GnFwdProb{g, c->gC, c->bC, c->WC, c->bWC, nullptr, xp, c->G, c->NC, 0, c->eps_h, c->WCh};
   }
   s = launch_fwd(a, st);
   if (s != GASFM_OK || !hub_on(c)) return s;
   a.nprob = 2;
-  a.p[0] = GnFwdProb{xv, nullptr, nullptr, c->WD, c->bD, nullptr, xrv, c->NB, c->ND, 0, 0.f};
-  a.p[1] = GnFwdProb{xp, nullptr, nullptr, c->WE, c->bE, nullptr, xrp, c->NC, c->NE, 0, 0.f};
+  a.p[0] = GnFwdProb{xv, nullptr, nullptr, c->WD, c->bD, nullptr, xrv, c->NB, c->ND, 0, 0.f, c->WDh};
+  a.p[1] = GnFwdProb{xp, nullptr, nullptr, c->WE, c->bE, nullptr, xrp, c->NC, c->NE, 0, 0.f, c->WEh};
   return launch_fwd(a, st);
 }
 
@@ -582,9 +608,9 @@ extern "C" int gasfm_gchain_bwd(const gasfm_gchain* c, const float* xcat, const 
     GnBwdArgs a{};
     a.nprob = 2;
     a.p[0] = GnBwdProb{dxrv, xv, nullptr, nullptr, c->WD, d->dWD, d->dbD, dhD};
-    a.p[0].K = c->NB, a.p[0].N = c->ND;
+    a.p[0].K = c->NB, a.p[0].N = c->ND, a.p[0].Wh = c->WDh;
     a.p[1] = GnBwdProb{dxrp, xp, nullptr, nullptr, c->WE, d->dWE, d->dbE, dhE};
-    a.p[1].K = c->NC, a.p[1].N = c->NE;
+    a.p[1].K = c->NC, a.p[1].N = c->NE, a.p[1].Wh = c->WEh;
     s = launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(lin_r)");
     if (s != GASFM_OK) return s;
   }
@@ -592,17 +618,17 @@ extern "C" int gasfm_gchain_bwd(const gasfm_gchain* c, const float* xcat, const 
      // their LayerNorm backwards (gv, gamma / beta gradients, row-sum partials)
     GnBwdArgs a{};
     a.nprob = hub ? 3 : 1;
-    auto lnprob = [&](const float* dy, const float* gam, const float* bet, const float* W, float* dW, float* db,
-                      int N, float* gv, float* dgam, float* dbet, float* lnp, float* stats) {
+    auto lnprob = [&](const float* dy, const float* gam, const float* bet, const float* W, const uint16_t* Wh,
+                      float* dW, float* db, int N, float* gv, float* dgam, float* dbet, float* lnp, float* stats) {
       GnBwdProb p{dy, g, gam, bet, W, dW, db, gv};
-      p.K = c->G, p.N = N, p.eps = c->eps_h;
+      p.K = c->G, p.N = N, p.eps = c->eps_h, p.Wh = Wh;
       p.dgam = dgam, p.dbet = dbet, p.lnp = lnp, p.stats = stats, p.lnfin = 1;
       return p;
     };
-    a.p[0] = lnprob(dsg, c->gA, c->bA, c->WA, d->dWA, nullptr, c->NA, gvA, d->dgA, d->dbA, lnA, stg);
+    a.p[0] = lnprob(dsg, c->gA, c->bA, c->WA, c->WAh, d->dWA, nullptr, c->NA, gvA, d->dgA, d->dbA, lnA, stg);
     if (hub) {
-      a.p[1] = lnprob(dhD, c->gB, c->bB, c->WB, d->dWB, d->dbWB, c->NB, gvB, d->dgB, d->dbB, lnB, nullptr);
-      a.p[2] = lnprob(dhE, c->gC, c->bC, c->WC, d->dWC, d->dbWC, c->NC, gvC, d->dgC, d->dbC, lnC, nullptr);
+      a.p[1] = lnprob(dhD, c->gB, c->bB, c->WB, c->WBh, d->dWB, d->dbWB, c->NB, gvB, d->dgB, d->dbB, lnB, nullptr);
+      a.p[2] = lnprob(dhE, c->gC, c->bC, c->WC, c->WCh, d->dWC, d->dbWC, c->NC, gvC, d->dgC, d->dbC, lnC, nullptr);
     }
     s = launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(hub)");
     if (s != GASFM_OK) return s;
@@ -613,7 +639,7 @@ extern "C" int gasfm_gchain_bwd(const gasfm_gchain* c, const float* xcat, const 
     a.nprob = 1;
     GnBwdProb& p = a.p[0];
     p = GnBwdProb{nullptr, x1, c->gM, c->bM, c->W2, d->dW2, d->db2, gv2};
-    p.K = c->G, p.N = c->G, p.eps = c->eps_m;
+    p.K = c->G, p.N = c->G, p.eps = c->eps_m, p.Wh = c->W2h;
     p.dgam = d->dgM, p.dbet = d->dbM, p.lnp = ln2, p.stats = st1, p.lnfin = 1;
     GnPro& pr = a.pro;
     pr.nq = hub ? 3 : 1;
@@ -628,7 +654,7 @@ extern "C" int gasfm_gchain_bwd(const gasfm_gchain* c, const float* xcat, const 
   GnBwdArgs a{};
   a.nprob = 1;
   a.p[0] = GnBwdProb{nullptr, xcat, nullptr, nullptr, c->W1, d->dW1, d->db1, dxcat};
-  a.p[0].K = c->Kc, a.p[0].N = c->G;
+  a.p[0].K = c->Kc, a.p[0].N = c->G, a.p[0].Wh = c->W1h;
   GnPro& pr = a.pro;
   pr.nq = 1;
   pr.gv[0] = gv2, pr.lnp[0] = ln2;

@@ -10,6 +10,8 @@ gradient as a batched GEMM over row chunks followed by a sum (split-K), which fi
 the chip.
 The single global row goes through csrc/global_vec.hip (GlobalLinearFn).
 """
+import weakref
+
 import torch
 import torch.nn.functional as F
 from torch.nn import LayerNorm, Linear, ReLU, Sequential
@@ -193,6 +195,39 @@ _GC_W = ("W1", "b1", "gM", "bM", "W2", "b2", "gA", "bA", "WA", "gB", "bB", "WB",
 GCHAIN_MAX = 2048
 
 
+_SHADOWS = {}  # id(weight) -> (weakref(weight), bf16 shadow, weight version, weight storage)
+
+
+def weight_shadow(w):
+    """w's bf16 shadow (BASELINE config 5: the global chain's GEMVs stream bf16 weights): re-rounded
+    when w changed since its last use (version counter or storage).  A captured step's replays skip
+    that check: call refresh_weight_shadows() after each optimizer step (GraphAttnSfMNet's
+    refresh_weight_shadows)."""
+    e = _SHADOWS.get(id(w))
+    if e is not None and e[0]() is w:
+        _, sh, ver, ptr = e
+        if ver == w._version and ptr == w.data_ptr():
+            return sh
+    else:
+        sh = torch.empty(w.shape, dtype=torch.bfloat16, device=w.device)
+    with torch.no_grad():
+        sh.copy_(w)
+    _SHADOWS[id(w)] = (weakref.ref(w), sh, w._version, w.data_ptr())
+    return sh
+
+
+def refresh_weight_shadows():
+    """Re-round every live bf16 shadow from its weight (after an optimizer step)."""
+    with torch.no_grad():
+        for k, (ref, sh, _, _) in list(_SHADOWS.items()):
+            w = ref()
+            if w is None:
+                del _SHADOWS[k]
+                continue
+            sh.copy_(w)
+            _SHADOWS[k] = (ref, sh, w._version, w.data_ptr())
+
+
 class GlobalChainFn(torch.autograd.Function):
     """A block's whole global-node chain on ONE row (csrc/global_chain.hip), four launches each way:
     ViewAndScenePoint2Global's tail (layers.py:527-528, 590-603) and every consumer of its output g
@@ -202,14 +237,16 @@ class GlobalChainFn(torch.autograd.Function):
     and GlobalHubFn (12 backward launches per block, each GEMV followed by a one-workgroup finish).
 
     apply(xcat [1, Kc], prev [1, G] or None, *weights (_GC_W order; the hub's B..E None for the last
-    block), eps_m, eps_h) -> (g, SG, XRv, XRp), or (g, SG) without the hub."""
+    block), eps_m, eps_h, bf16) -> (g, SG, XRv, XRp), or (g, SG) without the hub.  bf16: the GEMVs read
+    the weights' bf16 shadows (weight_shadow; BASELINE config 5), fp32 accumulation and gradients."""
 
     @staticmethod
     def forward(ctx, xcat, prev, *args):
         from . import _native
-        ws, eps_m, eps_h = args[:-2], args[-2], args[-1]
+        ws, eps_m, eps_h, bf16 = args[:-3], args[-3], args[-2], args[-1]
         w = {k: (t.contiguous() if t is not None else None) for k, t in zip(_GC_W, ws)}
-        c = _native.gchain_struct(w, eps_m, eps_h)
+        sh = {k: weight_shadow(w[k]) for k in _native._GC_SHADOW if w[k] is not None} if bf16 else None
+        c = _native.gchain_struct(w, eps_m, eps_h, sh)
         hub = w["WB"] is not None
         f = dict(dtype=torch.float32, device=xcat.device)
         x1c = xcat.reshape(-1).contiguous()
@@ -222,6 +259,7 @@ class GlobalChainFn(torch.autograd.Function):
         _native.gchain_fwd(c, x1c, pv, x1, g, sg, xv, xp, xrv, xrp)
         ctx.save_for_backward(x1c, x1, g, xv, xp, *(w[k] for k in _GC_W))
         ctx.eps = (eps_m, eps_h)
+        ctx.shadows = sh
         ctx.hub, ctx.has_prev = hub, prev is not None
         ctx.shapes = (xcat.shape, prev.shape if prev is not None else None)
         ctx.set_materialize_grads(False)
@@ -234,7 +272,7 @@ class GlobalChainFn(torch.autograd.Function):
         from . import _native
         x1c, x1, g, xv, xp, *wl = ctx.saved_tensors
         w = dict(zip(_GC_W, wl))
-        c = _native.gchain_struct(w, *ctx.eps)
+        c = _native.gchain_struct(w, *ctx.eps, ctx.shadows)
         f = dict(dtype=torch.float32, device=g.device)
         row = lambda t, n: t.reshape(-1).contiguous() if t is not None else torch.zeros(n, **f)  # noqa: E731
         dskip = grads[0].reshape(-1).contiguous() if grads[0] is not None else None
@@ -248,7 +286,7 @@ class GlobalChainFn(torch.autograd.Function):
         _native.gchain_bwd(c, x1c, x1, g, xv, xp, dskip, dsg, dxrv, dxrp, dxcat, dprev, d)
         xs, ps = ctx.shapes
         return (dxcat.view(xs), dprev.view(ps) if dprev is not None else None,
-                *(d["d" + k] for k in _GC_W), None, None)
+                *(d["d" + k] for k in _GC_W), None, None, None)
 
 
 def _ln_of(ln, G):
@@ -286,14 +324,14 @@ def chain_params(vsg, pfu, nvsg):
     return tuple(w.get(k) for k in _GC_W), lnM.eps, lnA.eps
 
 
-def global_chain(x, prev, params):
+def global_chain(x, prev, params, bf16=False):
     """GlobalChainFn on a single row x [1, Kc] (prev [1, G] or None) when it fits, else None."""
     if not (x.is_cuda and x.dim() == 2 and x.shape[0] == 1 and x.dtype == torch.float32):
         return None
     if prev is not None and not (prev.numel() == params[0][0].shape[0] and prev.is_cuda):
         return None
     ws, eps_m, eps_h = params
-    return GlobalChainFn.apply(x, prev, *ws, eps_m, eps_h)
+    return GlobalChainFn.apply(x, prev, *ws, eps_m, eps_h, bool(bf16))
 
 
 def _gvec_ok(x, k):

@@ -283,7 +283,7 @@ class ViewAndScenePoint2Global(Module):
 
     def _global_tail(self, x, prev, chain=None):
         if chain is not None:
-            out = dense.global_chain(x, prev, chain)
+            out = dense.global_chain(x, prev, chain, getattr(self, "_proj_bf16", False))
             if out is not None:
                 return out
         if hasattr(self, "proj_view_and_scenepoint2global"):
@@ -982,13 +982,22 @@ class GraphAttnSfMNet(Module):
     def set_projection_precision(self, precision):
         """"fp32" (default: the reference's precision) or "bf16": the camera-side D x D products
         (Proj2View's MLP, graph_conv_view2global.lin_l; layers.py:292-320, 352-358, 506-511) in
-        bf16 on MFMA with fp32 accumulation, forward and backward (BASELINE config 5)."""
+        bf16 on MFMA with fp32 accumulation, forward and backward, and the global node's chain
+        (layers.py:497-533, 594-603, 928-935) on bf16 weight shadows (BASELINE config 5; call
+        refresh_weight_shadows() after each optimizer step when the step is a captured graph)."""
         if precision not in ("fp32", "bf16"):
             raise ValueError(f"projection precision {precision!r}: expected 'fp32' or 'bf16'")
         self._projection_precision = precision
         for mod in self.modules():
             mod._proj_bf16 = precision == "bf16"
         return self
+
+    @staticmethod
+    def refresh_weight_shadows():
+        """Re-round the bf16 weight shadows (set_projection_precision("bf16")) from their weights:
+        after an optimizer step whose forward/backward is replayed from a captured graph (an eager
+        forward re-rounds a changed weight by itself)."""
+        dense.refresh_weight_shadows()
 
     # ------------------------------------------------------------------ forward
     def edge_index_for(self, data, device):

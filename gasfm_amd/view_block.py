@@ -47,7 +47,11 @@ VIEW_CHAIN = os.environ.get("GASFM_VIEW_CHAIN", "1") != "0"
 
 
 def _chain_ok(m, D, bf16):
-    return VIEW_CHAIN and not bf16 and FP32_GEMM == "torch" and m > 0 and _native.view_chain_ok(m, D)
+    """The fused small-m view chain (vc_* kernels, fp32 products) runs whenever it fits, in the bf16
+    projection mode too: at its row counts (a camera-sharded rank's ~125 rows, a training batch's
+    ~60) the separate bf16 GEMM launches are latency-bound and slower (rank-0-of-8: 8.67 vs 7.66 ms,
+    round 5), so bf16 applies to the large-m GEMM path only."""
+    return VIEW_CHAIN and FP32_GEMM == "torch" and m > 0 and _native.view_chain_ok(m, D)
 
 
 def _mm(a, b, cin=None, bias=None, bf16=False, out=None):

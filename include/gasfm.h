@@ -183,7 +183,8 @@ int gasfm_edge0_seam_fwd(const float* P, const int32_t* pt, const float* ln_a_w,
  * camera plan's items (gasfm_edge_cam_bwd followed by gasfm_edge_prologue_bwd with dXLc, without
  * storing dXLc): dP [E, 32], dXR per camera (split items: part_dxr rows for
  * gasfm_gat_attn_bwd_combine), and per workgroup the partial row
- * [dW 64x32 | db 64 | dgamma 32 | dbeta 32 | datt 32 | dbias 32]
+ * [dW 64x32 | db 64 | dgamma 32 | dbeta 32 | datt 32 | 0 (32)]; the attention bias gradient is the
+ * column sum of gout over all targets (every target's output carries the bias), taken by the caller
  * (part[gasfm_edge_cam_pbwd_part_rows(n_items), gasfm_edge_cam_pbwd_part_cols()]).
  * dXLp: the point half of dXL in edge order (row stride ldXp); dRes / Wp (row stride ldWp) / scale:
  * the block output's residual gradient and lin_proj, as in gasfm_edge_prologue_bwd (dRes may be null).
@@ -680,6 +681,10 @@ typedef struct gasfm_gchain {
   const float *gA, *bA, *WA;
   const float *gB, *bB, *WB, *bWB, *gC, *bC, *WC, *bWC;
   const float *WD, *bD, *WE, *bE;
+  /* optional bf16 shadows (round 5, BASELINE config 5: the weights rounded to bf16, refreshed by the
+   * caller once per optimizer step; NULL: read the fp32 weight).  The GEMVs stream half the weight
+   * bytes and accumulate in fp32; every gradient stays fp32 (dW = dy x h does not read W). */
+  const uint16_t *W1h, *W2h, *WAh, *WBh, *WCh, *WDh, *WEh;
 } gasfm_gchain;
 typedef struct gasfm_gchain_grads {
   float *dW1, *db1, *dgM, *dbM, *dW2, *db2;

@@ -2,9 +2,11 @@
 set_projection_precision("bf16") against the fp64 oracle (reference code/models/ forward,
 oracle/gasfm_ref.py).
 
-Only the camera-side D x D products (Proj2View's MLP and graph_conv_view2global.lin_l,
-layers.py:292-320, 352-358, 506-511; forward and both backward products) change: their operands
-are rounded to bf16 (2^-9 relative) and accumulated in fp32.  Stated tolerance of this mode,
+What changes: the camera-side D x D products (Proj2View's MLP and graph_conv_view2global.lin_l,
+layers.py:292-320, 352-358, 506-511; forward and both backward products) on the large-m GEMM path
+(operands rounded to bf16, 2^-9 relative, fp32 accumulation; the small-m fused view chain stays
+fp32: view_block._chain_ok), and the global node's chain (layers.py:497-533, 594-603, 928-935) on
+bf16 weight shadows (round 5; fp32 accumulation, fp32 gradients).  Stated tolerance of this mode,
 against the fp64 reference on the 12-block learning conf (scaled config 4):
     outputs    ||got - ref|| <= 2e-2 ||ref||        (Ps_norm, pts3D; normwise)
     gradient   ||G - G_ref|| <= 0.1 ||G_ref||       (all parameter gradients flattened into one
@@ -39,9 +41,11 @@ def rel(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
 
 
-@pytest.mark.parametrize("scale,layers", [(0.02, 12), (0.05, 3)])
-def test_bf16_projections_vs_oracle(device, scale, layers):
-    from gasfm_amd import synthetic
+@pytest.mark.parametrize("scale,layers,chain", [(0.02, 12, True), (0.05, 3, True), (0.05, 3, False)])
+def test_bf16_projections_vs_oracle(device, scale, layers, chain, monkeypatch):
+    """chain False: the view side through the bf16 GEMM kernel (the large-m path) at this small m."""
+    from gasfm_amd import synthetic, view_block
+    monkeypatch.setattr(view_block, "VIEW_CHAIN", chain)
     sc = synthetic.scaled_config4(scale, seed=11)
     vals = sc.normalized_values()
     data = gasfm_amd.SceneData.from_synthetic(sc).to(device)
@@ -122,3 +126,37 @@ def test_bf16_training_tracks_fp32(device):
     assert np.all(np.abs(traj["bf16"] - traj["fp32"]) <= 0.05 * np.abs(traj["fp32"]))
     # the first Adam step from this init overshoots (0.049 -> 0.487, both modes); descent after it
     assert traj["fp32"][-1] < traj["fp32"][1] and traj["bf16"][-1] < traj["bf16"][1]
+
+
+def test_gchain_bf16_shadows(device):
+    """The global node's chain on bf16 weight shadows (dense.weight_shadow, set_projection_precision
+    "bf16"): the shadows are the weights rounded to bf16, re-rounded by the next forward after an
+    in-place weight update, and the chain's outputs move from the fp32 mode's by a bf16-sized amount
+    (> 0: the shadows were read; <= 2e-2 normwise on the global features)."""
+    from gasfm_amd import dense, synthetic
+    sc = synthetic.scaled_config4(0.02, seed=5)
+    data = gasfm_amd.SceneData.from_synthetic(sc).to(device)
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=3))
+    sd = deterministic_state_dict(net.state_dict(), torch.float64)
+    net.load_state_dict({k: v.float() for k, v in sd.items()})
+    net = net.to(device)
+    with torch.no_grad():
+        ref = net(data)["Ps_norm"].clone()
+        net.set_projection_precision("bf16")
+        dense._SHADOWS.clear()
+        got = net(data)["Ps_norm"].clone()
+    live = [(r(), sh) for r, sh, _, _ in dense._SHADOWS.values() if r() is not None]
+    assert len(live) >= 7, len(live)  # W1, W2, WA and the hub's WB..WE of at least one block
+    for w, sh in live:
+        assert torch.equal(sh, w.detach().to(torch.bfloat16))
+    d = rel(got.cpu().numpy(), ref.cpu().numpy())
+    assert 0 < d <= 2e-2, d
+    name, p = next((k, v) for k, v in net.named_parameters()
+                   if k.endswith("view_and_scenepoint2global.mlp.0.weight"))
+    with torch.no_grad():
+        p.mul_(1.25)
+        net(data)
+    sh = next(s for r, s, _, _ in dense._SHADOWS.values() if r() is p)
+    assert torch.equal(sh, p.detach().to(torch.bfloat16)), name
+    net.refresh_weight_shadows()
+    assert torch.equal(sh, p.detach().to(torch.bfloat16))

@@ -1,5 +1,6 @@
-# Library A/B (round 5): parity tests of the edge kernels on the default library, then per library
-# (default + the given variants, gasfm_amd/<name>.so) the edge kernels alone at config-4 size
+# Library / knob A/B (round 5): parity tests of the edge kernels on the default library, then per
+# variant -- the default, then each argument: a library gasfm_amd/<name>.so or an environment
+# assignment VAR=value (default library) -- the edge kernels alone at config-4 size
 # (tools/edge_bench.py: seam, pbwd EPI+DWP) and the config-4 and rank-0-of-8 benches, two rounds.
 set -o pipefail
 mkdir -p gpurun_out
@@ -8,9 +9,11 @@ timeout -k 10 600 $T tests/test_gpu_edge_cam.py tests/test_gpu_model.py tests/te
 tail -1 gpurun_out/ab_tests.log
 for rep in 1 2; do
 for lib in libgasfm.so "$@"; do
-  GASFM_LIB=$PWD/gasfm_amd/$lib timeout -k 10 300 python tools/edge_bench.py --reps 10 > gpurun_out/ab_eb.log 2>/dev/null
-  GASFM_LIB=$PWD/gasfm_amd/$lib timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/ab_c4.json 2>/dev/null || { echo "bench failed $lib"; exit 1; }
-  GASFM_LIB=$PWD/gasfm_amd/$lib timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --emulate-world 8 > gpurun_out/ab_em8.json 2>/dev/null || { echo "em8 failed $lib"; exit 1; }
+  envs=(GASFM_LIB=$PWD/gasfm_amd/$lib)
+  case "$lib" in *=*) envs=(GASFM_LIB=$PWD/gasfm_amd/libgasfm.so "$lib");; esac
+  env "${envs[@]}" timeout -k 10 300 python tools/edge_bench.py --reps 10 > gpurun_out/ab_eb.log 2>/dev/null
+  env "${envs[@]}" timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/ab_c4.json 2>/dev/null || { echo "bench failed $lib"; exit 1; }
+  env "${envs[@]}" timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --emulate-world 8 > gpurun_out/ab_em8.json 2>/dev/null || { echo "em8 failed $lib"; exit 1; }
   python - "$lib" <<'PY'
 import json, sys
 eb = [json.loads(l) for l in open("gpurun_out/ab_eb.log") if l.startswith("{")]
