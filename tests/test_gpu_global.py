@@ -138,7 +138,7 @@ def test_global_chain_matches_fp64(device, G, Kc, V, S, hub, with_prev):
     torch.autograd.backward(outs64, douts)
     got = {k: v.detach().float().to(device).requires_grad_(True) for k, v in ref.items()}
     ws = [got.get(k) for k in names[2:]]
-    outs = dense.GlobalChainFn.apply(got["xcat"], got.get("prev"), *ws, 1e-5, 1e-5)
+    outs = dense.GlobalChainFn.apply(got["xcat"], got.get("prev"), *ws, 1e-5, 1e-5, False)
     assert len(outs) == len(outs64)
     for name, o, r64 in zip(("g", "SG", "XRv", "XRp"), outs, outs64):
         torch.testing.assert_close(o.double().cpu(), r64.detach(), rtol=0, atol=2e-5 * r64.abs().max().item() + 1e-5,
@@ -152,7 +152,7 @@ def test_global_chain_matches_fp64(device, G, Kc, V, S, hub, with_prev):
     first = {k: a.grad.clone() for k, a in got.items()}
     for a in got.values():
         a.grad = None
-    outs = dense.GlobalChainFn.apply(got["xcat"], got.get("prev"), *ws, 1e-5, 1e-5)
+    outs = dense.GlobalChainFn.apply(got["xcat"], got.get("prev"), *ws, 1e-5, 1e-5, False)
     torch.autograd.backward(list(outs), [d.float().to(device) for d in douts])
     for k, a in got.items():
         assert torch.equal(a.grad, first[k]), k
