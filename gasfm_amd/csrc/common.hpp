@@ -28,6 +28,11 @@ inline int launch_status(const char* where) { return hip_status(hipGetLastError(
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// 1 / sqrt(x) for x in the normal range -- a LayerNorm's variance + eps: the bare v_rsq_f32.
+// rsqrtf's expansion only adds a denormal-input rescale around it (a compare, two multiplies and
+// two selects per call) that cannot trigger here, so the result is bitwise the same (round 5).
+__device__ __forceinline__ float rsq_normal(float x) { return __builtin_amdgcn_rsqf(x); }
+
 // Workgroups of `fn` (block threads, dynamic LDS bytes) resident on the current device at once
 // (occupancy x CU count; occupancy.cpp, cached).
 int resident_blocks(const void* fn, int block, size_t lds);

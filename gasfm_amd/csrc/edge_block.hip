@@ -126,7 +126,7 @@ __device__ __forceinline__ void norm_rows32(const float4 (&v)[2], int nrows, con
 #pragma unroll
       for (int k = 0; k < 4; ++k) q = fmaf(x[k] - mean, x[k] - mean, q);
       q = group_sum<8>(q);
-      rstd = rsqrtf(q * (1.f / F) + eps);
+      rstd = rsq_normal(q * (1.f / F) + eps);
     }
     const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
@@ -630,7 +630,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINWAVES) void edge_prologue_b
 #pragma unroll
           for (int k = 0; k < 4; ++k) q = fmaf(x[k] - mean, x[k] - mean, q);
           q = group_sum<8>(q);
-          rstd = rsqrtf(q * (1.f / F) + eps);
+          rstd = rsq_normal(q * (1.f / F) + eps);
         }
         const bool live = r < nrows;
         float* d = T2 + r * LD34 + (lane & 7) * 4;

@@ -37,7 +37,7 @@ struct LN2 {
 __device__ __forceinline__ LN2 ln2(float a, float b, float eps) {
   const float mean = 0.5f * (a + b);
   const float d0 = a - mean, d1 = b - mean;
-  const float rstd = rsqrtf(0.5f * (d0 * d0 + d1 * d1) + eps);
+  const float rstd = rsq_normal(0.5f * (d0 * d0 + d1 * d1) + eps);
   return {d0 * rstd, d1 * rstd, rstd};
 }
 

@@ -45,7 +45,9 @@ constexpr int LD34 = 34;    // LDS row stride of the P_hat tile
 constexpr int LDA = 36;     // LDS row stride of staged weights W[out][in] (A operand, 2-way banks)
 constexpr int PART = F + 2 * H;  // packed partial row
 
-__device__ __forceinline__ float leaky(float z, float slope) { return z > 0.f ? z : z * slope; }
+// leaky_relu for 0 <= slope <= 1 (the launchers require it; GATv2's 0.2): max(z, slope z) is
+// two VALU instead of a compare, a multiply and a select
+__device__ __forceinline__ float leaky(float z, float slope) { return fmaxf(z, z * slope); }
 
 // max over the 16 lanes of a row (DPP, as lanes.hpp's sums)
 __device__ __forceinline__ float row_max16(float v) {
@@ -92,7 +94,7 @@ __device__ __forceinline__ void phat_to_lds(const float4 (&v)[2], int nrows, flo
       float q = 0.f;
 #pragma unroll
       for (int k = 0; k < 4; ++k) q = fmaf(x[k] - mean, x[k] - mean, q);
-      rstd = rsqrtf(group_sum<8>(q) * (1.f / F) + eps);
+      rstd = rsq_normal(group_sum<8>(q) * (1.f / F) + eps);
     }
     float ph[4];
 #pragma unroll
@@ -171,7 +173,7 @@ __device__ __forceinline__ void phat_slabs(f32x4 (&v)[2], const float (&g8)[2][4
 #pragma unroll
     for (int j = 0; j < 4; ++j) q = fmaf(v[u][j] - mean, v[u][j] - mean, q);
   q = xsum32(xsum16(q));
-  const float rstd = rsqrtf(q * (1.f / F) + eps);
+  const float rstd = rsq_normal(q * (1.f / F) + eps);
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -194,7 +196,7 @@ __device__ __forceinline__ void phat_slabs_st(f32x4 (&v)[2], const float (&g8)[2
 #pragma unroll
     for (int j = 0; j < 4; ++j) q = fmaf(v[u][j] - mean, v[u][j] - mean, q);
   q = xsum32(xsum16(q));
-  rstd = rsqrtf(q * (1.f / F) + eps);
+  rstd = rsq_normal(q * (1.f / F) + eps);
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -577,7 +579,7 @@ __global__ __launch_bounds__(kThreads, GASFM_SEAM_MINW) void edge_seam_fwd_kerne
         // block 0: 2-wide P (q0), LN_a / LN_b over its 2 features (edge0_epilogue_fwd's order)
         const float mean = 0.5f * (q0.x + q0.y);
         const float d0 = q0.x - mean, d1 = q0.y - mean;
-        const float rs = rsqrtf(0.5f * (d0 * d0 + d1 * d1) + ep.eps);
+        const float rs = rsq_normal(0.5f * (d0 * d0 + d1 * d1) + ep.eps);
         const float xh0 = d0 * rs, xh1 = d1 * rs;
         const float ha0 = fmaxf(fmaf(xh0, ga0, ba0), 0.f), ha1 = fmaxf(fmaf(xh1, ga1, ba1), 0.f);
         const float hb0 = fmaxf(fmaf(xh0, gb0, bb0), 0.f), hb1 = fmaxf(fmaf(xh1, gb1, bb1), 0.f);
@@ -1144,7 +1146,7 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
             PT[u][j] -= mean;
             q = fmaf(PT[u][j], PT[u][j], q);
           }
-        rstd = rsqrtf(xsum32(xsum16(q)) * (1.f / F) + eps);
+        rstd = rsq_normal(xsum32(xsum16(q)) * (1.f / F) + eps);
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const f32x4 a = vecT(0, u), b = vecT(1, u);
@@ -1455,6 +1457,7 @@ extern "C" int gasfm_edge_cam_fwd(const float* P, const float* ln_w, const float
                     aligned16(P) && aligned16(XLp) && aligned16(XR) && (!out || aligned16(out)) &&
                     (!part || aligned16(part)) && (!ln_w || (aligned16(ln_w) && aligned16(ln_b))),
                 "gasfm_edge_cam_fwd: 16-byte rows required");
+  GASFM_REQUIRE(slope >= 0.f && slope <= 1.f, "gasfm_edge_cam_fwd: negative_slope %g outside [0, 1]", double(slope));
   if (n_items == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   auto launch = [&](auto kern) {
@@ -1483,6 +1486,7 @@ extern "C" int gasfm_edge_cam_bwd(const float* P, const float* ln_w, const float
                     aligned16(XR) && aligned16(out) && aligned16(gout) && aligned16(dXLc) && aligned16(dXR) &&
                     (!part_dxr || aligned16(part_dxr)) && (!ln_w || (aligned16(ln_w) && aligned16(ln_b))),
                 "gasfm_edge_cam_bwd: 16-byte rows required");
+  GASFM_REQUIRE(slope >= 0.f && slope <= 1.f, "gasfm_edge_cam_bwd: negative_slope %g outside [0, 1]", double(slope));
   if (n_items == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int grid = grid_cam_bwd(n_items);
@@ -1525,6 +1529,7 @@ extern "C" int gasfm_edge_cam_pbwd_ex(const float* P, const float* ln_w, const f
   GASFM_REQUIRE(!dwp || (ln_w && dRes && ldWpo == (P0 ? F + 2 : F)),
                 "gasfm_edge_cam_pbwd: the epilogue weight gradient needs LN, dRes and ldWpo = 32 (+2 with P0)");
   GASFM_REQUIRE(ldPart >= PB2_PART + (dwp ? int64_t(F) * ldWpo : 0), "gasfm_edge_cam_pbwd: part row too narrow");
+  GASFM_REQUIRE(slope >= 0.f && slope <= 1.f, "gasfm_edge_cam_pbwd: negative_slope %g outside [0, 1]", double(slope));
   if (n_items == 0) return GASFM_OK;
   const PbwdEpi ep{We, ldWe, scale_e, dSv_e, part_dsv_e, dP0_e, P0, ldWpo};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -1587,6 +1592,7 @@ extern "C" int gasfm_edge_seam_fwd(const float* Pb, const float* P0, const int32
                     aligned16(Sv) && aligned16(XLp) && aligned16(XR) && (!out || aligned16(out)) &&
                     (!part || aligned16(part)) && (!P0 || (reinterpret_cast<uintptr_t>(P0) % 8 == 0)),
                 "gasfm_edge_seam_fwd: aligned rows required");
+  GASFM_REQUIRE(slope >= 0.f && slope <= 1.f, "gasfm_edge_seam_fwd: negative_slope %g outside [0, 1]", double(slope));
   if (n_items == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const SeamEpi ep{Pb, P0, pt, ln_wb, ln_bb, eps_b, Wp, ldWp, bp, Sp, Sv, ldSv, Sg, scale, Pout,
@@ -1624,6 +1630,7 @@ extern "C" int gasfm_edge0_seam_fwd(const float* P, const int32_t* pt, const flo
                     aligned16(Pout) && aligned16(Sp) && aligned16(Sv) && aligned16(XLp) && aligned16(XR) &&
                     (!out || aligned16(out)) && (!part || aligned16(part)),
                 "gasfm_edge0_seam_fwd: aligned rows required");
+  GASFM_REQUIRE(slope >= 0.f && slope <= 1.f, "gasfm_edge0_seam_fwd: negative_slope %g outside [0, 1]", double(slope));
   if (n_items == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const SeamEpi ep{P, nullptr, pt, ln_a_w, ln_a_b, eps0, Wp, 2, bp, Sp, Sv, ldSv, Sg, scale, Pout,

@@ -99,7 +99,7 @@ __device__ __forceinline__ void row_stats(const float (&xv)[kPer], int K, float 
     q[0] = fmaf(d, d, q[0]);
   }
   block_sums<1>(q, scratch);
-  rstd = rsqrtf(q[0] / K + eps);
+  rstd = rsq_normal(q[0] / K + eps);
 }
 
 __device__ __forceinline__ void load_row(const float* __restrict__ x, int K, float (&xv)[kPer]) {

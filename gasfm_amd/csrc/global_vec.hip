@@ -63,7 +63,7 @@ __device__ __forceinline__ void row_stats(const float* __restrict__ x, int K, fl
     const float d = x[j] - mean;
     q = fmaf(d, d, q);
   }
-  rstd = rsqrtf(block_sum<nT>(q, scratch) / K + eps);
+  rstd = rsq_normal(block_sum<nT>(q, scratch) / K + eps);
 }
 
 // y[i] = W[i,:] . h + b[i] (+ res[i]);  h = relu(LN(x)) if gam else x
@@ -253,7 +253,7 @@ __device__ __forceinline__ void row_stats_reg(const float (&xv)[PER], int K, flo
     q[0] = fmaf(d, d, q[0]);
   }
   block_sums<kFinT, 1>(q, scratch);
-  rstd = rsqrtf(q[0] / K + eps);
+  rstd = rsq_normal(q[0] / K + eps);
 }
 
 // dh = sum_c part[c, :];  dx = LN_bwd(mask * dh) (+ dy if resid); dgamma, dbeta.  Every global

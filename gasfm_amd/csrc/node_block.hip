@@ -65,7 +65,7 @@ __device__ __forceinline__ void load_ln64(const float* __restrict__ X, int64_t r
     float q = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) q = fmaf(x[k] - mean, x[k] - mean, q);
-    const float rstd = rsqrtf(sum16(q) * (1.f / FI) + eps);
+    const float rstd = rsq_normal(sum16(q) * (1.f / FI) + eps);
     const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
     const bool live = r < nrows;
 #pragma unroll

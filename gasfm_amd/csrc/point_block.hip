@@ -66,7 +66,7 @@ __device__ __forceinline__ void row_stats64(const float4 (&v)[4], float eps, flo
     float q = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) q = fmaf(x[k] - mean, x[k] - mean, q);
-    const float rstd = rsqrtf(sum16(q) * (1.f / FP) + eps);
+    const float rstd = rsq_normal(sum16(q) * (1.f / FP) + eps);
     if ((lane & 15) == 0) {
       MS[r] = mean;
       RS[r] = rstd;
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(kThreads) void point_tail_fwd_kernel(
       float q = 0.f;
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) q = fmaf(xv[nt][r] - mean, xv[nt][r] - mean, q);
-      const float rstd = rsqrtf(sum16(q) * (1.f / FP) + eps);
+      const float rstd = rsq_normal(sum16(q) * (1.f / FP) + eps);
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
         Ph[e * L66 + nt * 16 + c] = fmaxf(fmaf((xv[nt][r] - mean) * rstd, gv[nt], bv[nt]), 0.f);
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(kThreads8) void point_tail_bwd_kernel(
       float q = 0.f;
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) q = fmaf(xr[nt] - mean, xr[nt] - mean, q);
-      const float rstd = rsqrtf(sum16(q) * (1.f / FP) + eps);
+      const float rstd = rsq_normal(sum16(q) * (1.f / FP) + eps);
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) XH[e * L66 + nt * 16 + c] = (xr[nt] - mean) * rstd;
       if (c == 0) RSt[e] = rstd;
@@ -1047,7 +1047,7 @@ __device__ __forceinline__ void slab_stats(const f32x4 (&x)[4], float eps, float
   for (int u = 0; u < 4; ++u)
 #pragma unroll
     for (int j = 0; j < 4; ++j) q = fmaf(x[u][j] - mean, x[u][j] - mean, q);
-  rstd = rsqrtf(sum_groups(q) * (1.f / FP) + eps);
+  rstd = rsq_normal(sum_groups(q) * (1.f / FP) + eps);
 }
 
 template <bool PREV>
@@ -1307,7 +1307,7 @@ __device__ __forceinline__ void cl_stats(const f32x4 (&x)[4], float eps, float (
     float q = 0.f;
 #pragma unroll
     for (int ot = 0; ot < 4; ++ot) q = fmaf(x[ot][r] - mean[r], x[ot][r] - mean[r], q);
-    rstd[r] = rsqrtf(sum16(q) * (1.f / FP) + eps);
+    rstd[r] = rsq_normal(sum16(q) * (1.f / FP) + eps);
   }
 }
 

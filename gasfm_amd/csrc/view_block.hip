@@ -121,7 +121,7 @@ __device__ __forceinline__ void merge_stats(const float2* __restrict__ SP, const
         const float d = p[b].x - mean;
         m2 += p[b].y + CB * d * d;
       }
-      rstd = rsqrtf(m2 / (s.ncb * CB) + eps);
+      rstd = rsq_normal(m2 / (s.ncb * CB) + eps);
     }
     MS[lane] = mean;
     RS[lane] = rstd;

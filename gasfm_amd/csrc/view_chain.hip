@@ -143,7 +143,7 @@ __device__ __forceinline__ void tile_stats(const float* X, float eps, float (&xs
     const float d = xs[i] - mean;
     q = fmaf(d, d, q);
   }
-  rstd = rsqrtf(half_sum(q) / D + eps);
+  rstd = rsq_normal(half_sum(q) / D + eps);
 }
 
 // this wave's share (K range [kw KU 16, +KU 16)) of the 16 x 32 product A (LDS tile, rows of
