@@ -158,49 +158,56 @@ __device__ __forceinline__ void load_slabs32(const float* __restrict__ X, int64_
   }
 }
 
+// ---- the LayerNorm of a row held as slabs (lane (g, c): 8 features of row c), in packed fp32 math
+// (round 5): v_pk_add / v_pk_mul / v_pk_fma handle two features per instruction (the compiler does
+// not pair these on its own), so the statistics and the affine take about half the VALU.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pair(const f32x4& v, int h) { return h ? f32x2{v[2], v[3]} : f32x2{v[0], v[1]}; }
+__device__ __forceinline__ void set_pair(f32x4& v, int h, f32x2 x) {
+  v[2 * h] = x.x;
+  v[2 * h + 1] = x.y;
+}
+// centres v in place (v - mean over the row's 32 features) and returns rstd
+__device__ __forceinline__ float ln_center(f32x4 (&v)[2], float eps) {
+  const f32x2 s2 = (pair(v[0], 0) + pair(v[0], 1)) + (pair(v[1], 0) + pair(v[1], 1));
+  const float mean = xsum32(xsum16(s2.x + s2.y)) * (1.f / F);
+  const f32x2 m2 = {mean, mean};
+  f32x2 q2 = {0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x2 d = pair(v[u], h) - m2;
+      q2 = __builtin_elementwise_fma(d, d, q2);
+      set_pair(v[u], h, d);
+    }
+  return rsq_normal(xsum32(xsum16(q2.x + q2.y)) * (1.f / F) + eps);
+}
+// out = relu(d rstd gamma + beta) for the centred slabs d (xh = d rstd also returned when asked)
+__device__ __forceinline__ void ln_affine(const f32x4 (&d)[2], float rstd, const float (&g8)[2][4],
+                                          const float (&b8)[2][4], f32x4 (&out)[2], f32x4* xh = nullptr) {
+  const f32x2 r2 = {rstd, rstd};
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x2 x = pair(d[u], h) * r2;
+      const f32x2 y = __builtin_elementwise_fma(x, f32x2{g8[u][2 * h], g8[u][2 * h + 1]},
+                                                f32x2{b8[u][2 * h], b8[u][2 * h + 1]});
+      if (xh) set_pair(xh[u], h, x);
+      out[u][2 * h] = fmaxf(y.x, 0.f);
+      out[u][2 * h + 1] = fmaxf(y.y, 0.f);
+    }
+}
+
 // relu(LN(P)) (LN) or P (the final update) in place on the slabs; g8 / b8: gamma / beta at this
 // lane's features 16 u + 4 g + j
 template <bool LN>
 __device__ __forceinline__ void phat_slabs(f32x4 (&v)[2], const float (&g8)[2][4], const float (&b8)[2][4],
                                            float eps) {
   if (!LN) return;
-  float sm = (v[0][0] + v[0][1]) + (v[0][2] + v[0][3]) + ((v[1][0] + v[1][1]) + (v[1][2] + v[1][3]));
-  sm = xsum32(xsum16(sm));
-  const float mean = sm * (1.f / F);
-  float q = 0.f;
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) q = fmaf(v[u][j] - mean, v[u][j] - mean, q);
-  q = xsum32(xsum16(q));
-  const float rstd = rsq_normal(q * (1.f / F) + eps);
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[u][j] = fmaxf(fmaf((v[u][j] - mean) * rstd, g8[u][j], b8[u][j]), 0.f);
-}
-
-// phat_slabs that also returns the row statistics (mean, rstd of edge c; 0 / 1 without LN)
-template <bool LN>
-__device__ __forceinline__ void phat_slabs_st(f32x4 (&v)[2], const float (&g8)[2][4], const float (&b8)[2][4],
-                                              float eps, float& mean, float& rstd) {
-  mean = 0.f;
-  rstd = 1.f;
-  if (!LN) return;
-  float sm = (v[0][0] + v[0][1]) + (v[0][2] + v[0][3]) + ((v[1][0] + v[1][1]) + (v[1][2] + v[1][3]));
-  sm = xsum32(xsum16(sm));
-  mean = sm * (1.f / F);
-  float q = 0.f;
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) q = fmaf(v[u][j] - mean, v[u][j] - mean, q);
-  q = xsum32(xsum16(q));
-  rstd = rsq_normal(q * (1.f / F) + eps);
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[u][j] = fmaxf(fmaf((v[u][j] - mean) * rstd, g8[u][j], b8[u][j]), 0.f);
+  const float rstd = ln_center(v, eps);
+  ln_affine(v, rstd, g8, b8, v);
 }
 
 // acc[ot] += W P_hat^T (A = W slabs, B = P_hat slabs): acc[ot][r] = feature 16 ot + 4 g + r of edge c
@@ -1135,27 +1142,22 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
       // ---- LayerNorm of edge c (T layout): PT becomes xh, ph = relu(LN(P))
       f32x4 ph[2];
       float rstd = 1.f;
-      if (LN) {
-        const float sm = (PT[0][0] + PT[0][1]) + (PT[0][2] + PT[0][3]) + ((PT[1][0] + PT[1][1]) + (PT[1][2] + PT[1][3]));
-        const float mean = xsum32(xsum16(sm)) * (1.f / F);
-        float q = 0.f;
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            PT[u][j] -= mean;
-            q = fmaf(PT[u][j], PT[u][j], q);
-          }
-        rstd = rsq_normal(xsum32(xsum16(q)) * (1.f / F) + eps);
+      if (LN) {  // packed math (ln_center / ln_affine, as the forward kernels)
+        rstd = ln_center(PT, eps);
+        float gs[2][4], bs[2][4];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const f32x4 a = vecT(0, u), b = vecT(1, u);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            PT[u][j] *= rstd;
-            ph[u][j] = fmaxf(fmaf(PT[u][j], a[j], b[j]), 0.f);
+            gs[u][j] = a[j];
+            bs[u][j] = b[j];
           }
         }
+        f32x4 xh[2];
+        ln_affine(PT, rstd, gs, bs, ph, xh);
+        PT[0] = xh[0];
+        PT[1] = xh[1];
       } else {
         ph[0] = PT[0];
         ph[1] = PT[1];
@@ -1206,31 +1208,34 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINW) void edge_cam_pbwd_kerne
       to_c(Ta, dXc, XcC);
       // ---- LayerNorm backward of edge c, dP (T layout)
       f32x4 dv[2];
-      if (LN) {
-        f32x4 gvv[2];
-        float s1 = 0.f, s2 = 0.f;
+      if (LN) {  // packed math: two features per v_pk_* instruction
+        f32x2 gvv[2][2], s1p = {0.f, 0.f}, s2p = {0.f, 0.f};
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const f32x4 a = vecT(0, u);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float dy = ph[u][j] > 0.f ? dph[u][j] : 0.f;
-            dg[u][j] = fmaf(dy, PT[u][j], dg[u][j]);
-            dbt[u][j] += dy;
-            gvv[u][j] = dy * a[j];
-            s1 += gvv[u][j];
-            s2 = fmaf(gvv[u][j], PT[u][j], s2);
+          for (int h = 0; h < 2; ++h) {
+            const f32x2 dy = {ph[u][2 * h] > 0.f ? dph[u][2 * h] : 0.f,
+                              ph[u][2 * h + 1] > 0.f ? dph[u][2 * h + 1] : 0.f};
+            const f32x2 xh = pair(PT[u], h);
+            set_pair(dg[u], h, __builtin_elementwise_fma(dy, xh, pair(dg[u], h)));
+            set_pair(dbt[u], h, pair(dbt[u], h) + dy);
+            const f32x2 gv = dy * pair(a, h);
+            gvv[u][h] = gv;
+            s1p += gv;
+            s2p = __builtin_elementwise_fma(gv, xh, s2p);
           }
         }
-        s1 = xsum32(xsum16(s1)) * (1.f / F);
-        s2 = xsum32(xsum16(s2)) * (1.f / F);
+        const float s1 = xsum32(xsum16(s1p.x + s1p.y)) * (1.f / F);
+        const float s2 = xsum32(xsum16(s2p.x + s2p.y)) * (1.f / F);
+        const f32x2 s1v = {s1, s1}, ms2 = {-s2, -s2}, r2 = {rstd, rstd};
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float v = rstd * (gvv[u][j] - s1 - PT[u][j] * s2);
-            if (RES) v += RT[u][j];
-            dv[u][j] = v;
+          for (int h = 0; h < 2; ++h) {
+            // rstd ((gvv - s1) - xh s2) (+ dRes)
+            const f32x2 t = __builtin_elementwise_fma(pair(PT[u], h), ms2, gvv[u][h] - s1v);
+            set_pair(dv[u], h, RES ? __builtin_elementwise_fma(t, r2, pair(RT[u], h)) : t * r2);
           }
       } else {
 #pragma unroll
