@@ -1312,28 +1312,41 @@ __device__ __forceinline__ void cl_stats(const f32x4 (&x)[4], float eps, float (
 }
 
 // LayerNorm + ReLU backward of the C-layout rows (xh: normalised x, dh: gradient of relu(xh g + b));
-// rows >= nrows give 0.  Accumulates dgamma / dbeta per lane feature 16 ot + c.
+// rows >= nrows give 0.  Accumulates dgamma / dbeta per lane feature 16 ot + c.  Packed fp32 math
+// (round 5): features (16 ot + c, 16 (ot + 1) + c) of a row as one pair per v_pk_* instruction.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void cl_ln_relu_bwd(const f32x4 (&xh)[4], const f32x4 (&dh)[4], const float (&gm)[4],
                                                const float (&bt)[4], const float (&rstd)[4], int nrows, int g,
                                                float (&dg)[4], float (&db)[4], f32x4 (&dx)[4]) {
+  f32x2 dg2[2] = {{dg[0], dg[1]}, {dg[2], dg[3]}}, db2[2] = {{db[0], db[1]}, {db[2], db[3]}};
+  const f32x2 gm2[2] = {{gm[0], gm[1]}, {gm[2], gm[3]}}, bt2[2] = {{bt[0], bt[1]}, {bt[2], bt[3]}};
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const bool live = 4 * g + r < nrows;
-    float s1 = 0.f, s2 = 0.f, gv[4];
+    f32x2 s1p = {0.f, 0.f}, s2p = {0.f, 0.f}, gv[2], x2[2];
 #pragma unroll
-    for (int ot = 0; ot < 4; ++ot) {
-      const float dy = (live && fmaf(xh[ot][r], gm[ot], bt[ot]) > 0.f) ? dh[ot][r] : 0.f;
-      dg[ot] = fmaf(dy, xh[ot][r], dg[ot]);
-      db[ot] += dy;
-      gv[ot] = dy * gm[ot];
-      s1 += gv[ot];
-      s2 = fmaf(gv[ot], xh[ot][r], s2);
+    for (int h = 0; h < 2; ++h) {
+      x2[h] = f32x2{xh[2 * h][r], xh[2 * h + 1][r]};
+      const f32x2 pre = __builtin_elementwise_fma(x2[h], gm2[h], bt2[h]);
+      const f32x2 dy = {(live && pre.x > 0.f) ? dh[2 * h][r] : 0.f, (live && pre.y > 0.f) ? dh[2 * h + 1][r] : 0.f};
+      dg2[h] = __builtin_elementwise_fma(dy, x2[h], dg2[h]);
+      db2[h] += dy;
+      gv[h] = dy * gm2[h];
+      s1p += gv[h];
+      s2p = __builtin_elementwise_fma(gv[h], x2[h], s2p);
     }
-    s1 = sum16(s1) * (1.f / FP);
-    s2 = sum16(s2) * (1.f / FP);
+    const float s1 = sum16(s1p.x + s1p.y) * (1.f / FP);
+    const float s2 = sum16(s2p.x + s2p.y) * (1.f / FP);
+    const f32x2 s1v = {s1, s1}, ms2 = {-s2, -s2}, r2 = {rstd[r], rstd[r]};
 #pragma unroll
-    for (int ot = 0; ot < 4; ++ot) dx[ot][r] = rstd[r] * (gv[ot] - s1 - xh[ot][r] * s2);
+    for (int h = 0; h < 2; ++h) {
+      const f32x2 t = __builtin_elementwise_fma(x2[h], ms2, gv[h] - s1v) * r2;  // rstd ((gv - s1) - xh s2)
+      dx[2 * h][r] = t.x;
+      dx[2 * h + 1][r] = t.y;
+    }
   }
+  dg[0] = dg2[0].x, dg[1] = dg2[0].y, dg[2] = dg2[1].x, dg[3] = dg2[1].y;
+  db[0] = db2[0].x, db[1] = db2[0].y, db[2] = db2[1].x, db[3] = db2[1].y;
 }
 
 // dx = dout + LN_bwd(mask * (dout W_m)) (== d prev), dagg = dx W_p; partial row per workgroup in the
@@ -1555,7 +1568,7 @@ __global__ __launch_bounds__(kThreadsR, GASFM_PT_HUB_BWD_R_MINW) void point_hub_
     float* __restrict__ part_c) {
   constexpr int OC = 0, ODT = OC + FA * FP, OCT = ODT + FA * FA, OAT = OCT + FA * FP, OBT = OAT + FA * FP,
                 OV = OBT + FP * FP, OT = OV + 6 * FP;
-  constexpr int TW = TR * (2 * LDX + 2 * LDA);  // per wave: p, dXL (64 wide), dSA, dXR (32 wide)
+  constexpr int TW = TR * (2 * LDX + 3 * LDA);  // per wave: p, dXL (64 wide), dSA, dXR, dt (32 wide)
   constexpr int NLDS = OT + kWavesR * TW;
   constexpr int NRED = 144 + 24;
   __shared__ __attribute__((aligned(16))) float lds[NLDS];
@@ -1571,6 +1584,7 @@ __global__ __launch_bounds__(kThreadsR, GASFM_PT_HUB_BWD_R_MINW) void point_hub_
   float* Tl = Tp + TR * LDX;
   float* Ts = Tl + TR * LDX;
   float* Tr = Ts + TR * LDA;
+  float* Td = Tr + TR * LDA;  // dt's C -> T transpose
   const int64_t ntiles = (N + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWavesR + wave, nw = int64_t(gridDim.x) * kWavesR;
   f32x4 n_pT[4], n_rT[2], n_sT[2], n_lT[4];  // the next tile's T-layout rows
@@ -1664,7 +1678,19 @@ __global__ __launch_bounds__(kThreadsR, GASFM_PT_HUB_BWD_R_MINW) void point_hub_
     {
       f32x4 dtT[2] = {zero4(), zero4()}, dp[4] = {zero4(), zero4(), zero4(), zero4()}, dq[4];
       layer_c<2, 2>(WDTQ, rT, dtC, lane);
-      layer_t<2, 2>(WDTQ, rT, dtT, lane);
+      // dt's T layout through the wave's LDS tile, not a second product (16 MFMA): the same
+      // products summed in the same k order, so bitwise the layer_t result (round 5)
+#pragma unroll
+      for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Td[(4 * g + r) * LDA + 16 * ft + c] = dtC[ft][r];
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float4 t4 = *reinterpret_cast<const float4*>(Td + c * LDA + 16 * u + 4 * g);
+        dtT[u] = f32x4{t4.x, t4.y, t4.z, t4.w};
+      }
       PT_SCHED_BARRIER();
       layer_c<4, 2>(WCTQ, dtT, dp, lane);
       float gm[4], bt[4];
