@@ -42,6 +42,7 @@ _SIGS = {
     "gasfm_gat_attn_fwd_lanes": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _f32, _i32,
                                   _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
     "gasfm_gat_attn_bwd_combine": (_i32, [_vp, _i32, _i32, _vp, _vp, _i64, _vp]),
+    "gasfm_gat_attn_bwd_combine2": (_i32, [_vp, _i32, _i32, _vp, _vp, _i64, _vp, _vp, _i64, _vp]),
     "gasfm_colsum_ws_floats": (_i64, [_i64, _i32]),
     "gasfm_edge_part_floats": (_i32, [_i32, _i64, _i32]),
     "gasfm_edge_prologue_fwd": (_i32, [_vp, _i64, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
@@ -359,6 +360,13 @@ def attn_bwd_combine(combine, n_combine, HC, part_dxr, dXR):
     st = lib().gasfm_gat_attn_bwd_combine(_p(combine), n_combine, HC, _p(part_dxr), _p(dXR), dXR.stride(0),
                                           _stream(dXR))
     check(st, "gasfm_gat_attn_bwd_combine")
+
+
+def attn_bwd_combine2(combine, n_combine, HC, part_a, out_a, part_b, out_b):
+    """attn_bwd_combine of two partial-row arrays over the same entries, one launch."""
+    st = lib().gasfm_gat_attn_bwd_combine2(_p(combine), n_combine, HC, _p(part_a), _p(out_a), out_a.stride(0),
+                                           _p(part_b), _p(out_b), out_b.stride(0), _stream(out_a))
+    check(st, "gasfm_gat_attn_bwd_combine2")
 
 
 _COUNTERS = {}

@@ -307,6 +307,19 @@ def _check(t, name, rows=None, cols=None):
         raise ValueError(f"{name}: has {t.shape[1]} columns, expected {cols}")
 
 
+def bwd_combine2(plan, part_a, out_a, part_b, out_b, HC):
+    """bwd_combine of two partial-row arrays over the same plan's slots (the camera plan's dXR and
+    the folded epilogue's dSv rows), one launch per level instead of two."""
+    if plan.num_targets == 1:
+        bwd_combine(plan, part_a, HC, out_a)
+        bwd_combine(plan, part_b, HC, out_b)
+        return
+    if plan.n_l1:
+        _native.attn_bwd_combine2(plan.combine_l1, plan.n_l1, HC, part_a, part_a, part_b, part_b)
+    if plan.n_combine:
+        _native.attn_bwd_combine2(plan.combine, plan.n_combine, HC, part_a, out_a, part_b, out_b)
+
+
 def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True, xl_sorted=False, out=None):
     """Launch the forward kernels; returns (out, seg_max, seg_sum) for all plan targets.
 

@@ -952,11 +952,20 @@ __global__ __launch_bounds__(kBlock, GASFM_GLDS_BWD_MINWAVES) void attn_bwd_glds
 // dXR[seg] = ordered sum of its partial slots.
 // grid = (combine entries, column blocks of CB = min(HC, 64)): R = kBlock / CB row groups take
 // slots k = grp, grp + R, ... and are added in group order (deterministic for a given HC).
+// One or two (part, out) pairs over the same combine entries (blockIdx.z selects the pair): the
+// camera plan's dXR and the folded epilogue's dSv partial rows share their slots (round 5: one
+// launch for both).
+struct CombPair {
+  const float* part[2];
+  float* out[2];
+  int64_t ld[2];
+};
 __global__ __launch_bounds__(kBlock) void attn_bwd_combine_kernel(const gasfm_combine_item* __restrict__ comb,
-                                                             int n_comb, int HC,
-                                                             const float* __restrict__ part,
-                                                             float* __restrict__ dXR, int64_t ld) {
+                                                             int n_comb, int HC, CombPair pr) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
+  const float* __restrict__ part = pr.part[blockIdx.z];
+  float* __restrict__ dXR = pr.out[blockIdx.z];
+  const int64_t ld = pr.ld[blockIdx.z];
   const gasfm_combine_item ci = comb[blockIdx.x];
   const int CB = HC < 64 ? HC : 64;
   const int R = kBlock / CB;
@@ -1366,8 +1375,22 @@ extern "C" int gasfm_gat_attn_bwd_combine(const gasfm_combine_item* combine, int
   if (n_combine == 0) return GASFM_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int cb = HC < 64 ? HC : 64;
-  hipLaunchKernelGGL(attn_bwd_combine_kernel, dim3(n_combine, (HC + cb - 1) / cb), dim3(kBlock),
-                     kBlock * sizeof(float), st, combine,
-                     n_combine, HC, part_dxr, dXR, ldDXR);
+  const CombPair pr{{part_dxr, part_dxr}, {dXR, dXR}, {ldDXR, ldDXR}};
+  hipLaunchKernelGGL(attn_bwd_combine_kernel, dim3(n_combine, (HC + cb - 1) / cb, 1), dim3(kBlock),
+                     kBlock * sizeof(float), st, combine, n_combine, HC, pr);
   return launch_status("gasfm_gat_attn_bwd_combine");
+}
+
+extern "C" int gasfm_gat_attn_bwd_combine2(const gasfm_combine_item* combine, int32_t n_combine, int32_t HC,
+                                           const float* part_a, float* out_a, int64_t ld_a, const float* part_b,
+                                           float* out_b, int64_t ld_b, void* stream) {
+  GASFM_REQUIRE(HC > 0 && n_combine >= 0 && part_a && out_a && part_b && out_b,
+                "gasfm_gat_attn_bwd_combine2: bad args");
+  if (n_combine == 0) return GASFM_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int cb = HC < 64 ? HC : 64;
+  const CombPair pr{{part_a, part_b}, {out_a, out_b}, {ld_a, ld_b}};
+  hipLaunchKernelGGL(attn_bwd_combine_kernel, dim3(n_combine, (HC + cb - 1) / cb, 2), dim3(kBlock),
+                     kBlock * sizeof(float), st, combine, n_combine, HC, pr);
+  return launch_status("gasfm_gat_attn_bwd_combine2");
 }

@@ -24,8 +24,8 @@ import os
 import torch
 
 from . import _native
-from .attention import (attn_backward_raw, attn_forward_partial, attn_forward_raw, bwd_combine, combine_fwd_l1,
-                        combine_partials)
+from .attention import (attn_backward_raw, attn_forward_partial, attn_forward_raw, bwd_combine, bwd_combine2,
+                        combine_fwd_l1, combine_partials)
 
 PROJ_SCALE = 0.25  # the "/ 4" of layers.py:945
 # EdgeCamFn's backward as ONE kernel (gasfm_edge_cam_pbwd: camera attention backward + edge
@@ -214,7 +214,13 @@ def _cam_backward(ctx, saved, dXLp, g_c, dRes, epi=None, dXR=None):
                               epi=epi if use_epi else None,
                               dwp=(P0 if P0 is not None else True) if dwp else None)
         ctx.epi_done = use_epi
-        bwd_combine(plan, part_dxr, 32, dXR)
+        ctx.epi_combined = False
+        if use_epi and part_dxr is not None and epi[3] is not None:
+            # the split cameras' dXR and (EPI) dSv rows share their slots: one combine launch
+            bwd_combine2(plan, part_dxr, dXR, epi[3], epi[2], 32)
+            ctx.epi_combined = True
+        else:
+            bwd_combine(plan, part_dxr, 32, dXR)
         tot = _native.param_colsum(part, ctx.defer)
         o = 64 * 32
         ta = tot[o + 128:o + 192]
@@ -358,7 +364,7 @@ def _epilogue_backward(ctx, saved, dPo, folded=None, dSg=None):
     pc = edges.plans["proj2view"]
     pp = edges.plans["proj2scenepoint"]
     dWp = None
-    if folded is not None:
+    if folded is not None:  # part_dsv None: merged together with the camera plan's dXR (edge_cam_pbwd)
         dSv, part_dsv, dP0 = folded
     else:
         # camera side: dSv (+ dWp, dP0) in one pass over the camera work items
@@ -371,7 +377,8 @@ def _epilogue_backward(ctx, saved, dPo, folded=None, dSg=None):
                                   part_dsv, dP0, part_w)
         if not ctx.wp_by_cam:
             dWp = _native.param_colsum(part_w, ctx.defer).view(32, Wp.shape[1])
-    bwd_combine(pc, part_dsv, 32, dSv)
+    if part_dsv is not None:
+        bwd_combine(pc, part_dsv, 32, dSv)
     dSg_shared = dSg is not None
     dSg = _native.colsum(dSv, out=dSg)  # == d bias_proj: every edge belongs to one camera
     # point side: dSp = per-point sum of dP'/4 through the point permutation
@@ -466,6 +473,8 @@ class SeamFn(torch.autograd.Function):
                            dXR=bnd[2] if bnd is not None else None)
         if not ctx.epi_done:
             folded = None
+        elif ctx.epi_combined:
+            folded = (folded[0], None, folded[2])
         dPn = gc[0] if gPn is None else gc[0] + gPn
         ectx = _EpiState(ctx.e_eps, edges, ctx.sg_shape, ctx.e_defer, ctx.e_wp_by_cam, ctx.e_defer_b)
         ge = _epilogue_backward(ectx, epi, dPn, folded,

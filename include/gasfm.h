@@ -296,6 +296,11 @@ int gasfm_gat_attn_bwd(const float* XL, int64_t ldXL,
 int gasfm_gat_attn_bwd_combine(const gasfm_combine_item* combine, int32_t n_combine,
                                int32_t HC, const float* part_dxr,
                                float* dXR, int64_t ldDXR, void* stream);
+/* gasfm_gat_attn_bwd_combine for two partial-row arrays over the same combine entries in ONE launch
+ * (round 5: the camera plan's dXR and the folded epilogue's dSv rows, gasfm_edge_cam_pbwd_ex). */
+int gasfm_gat_attn_bwd_combine2(const gasfm_combine_item* combine, int32_t n_combine, int32_t HC,
+                                const float* part_a, float* out_a, int64_t ld_a, const float* part_b,
+                                float* out_b, int64_t ld_b, void* stream);
 
 /* out[c] = sum_r A[r*ld + c] for c < cols: ONE launch, deterministic (per-block partial slabs
  * in ws, summed in block order by the last block of each column chunk).  ws must hold
