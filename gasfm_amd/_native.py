@@ -157,6 +157,12 @@ _SIGS = {
     "gasfm_esfm_fwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _vp, _vp]),
     "gasfm_esfm_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i64, _f32, _f32, _i32, _i32,
                               _i32, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_esfm_seg_part_rows": (_i32, [_i32]),
+    "gasfm_esfm_seg_fwd": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i64, _f32, _f32, _i32, _vp, _vp, _vp,
+                                  _vp]),
+    "gasfm_esfm_seg_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _f32,
+                                  _f32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "gasfm_reproj_error_seg": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _i64, _vp, _vp, _vp]),
     "gasfm_point_tail_part_shape": (_i32, [_i64, _i32, _vp]),
     "gasfm_point_hub_part_shape": (_i32, [_i64, _i32, _i32, _vp]),
     "gasfm_point_tail_fwd": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
@@ -1123,6 +1129,55 @@ def reproj_error(cam, pt, xy, P, X, err=None):
     st = lib().gasfm_reproj_error(_p(cam), _p(pt), _p(xy), E, _p(P), _p(X), n, _p(err), _p(part), _stream(X))
     check(st, "gasfm_reproj_error")
     return part
+
+
+def _seg_args(eoff, S, name):
+    if eoff.dtype != torch.int32 or not eoff.is_contiguous() or eoff.numel() != S + 1:
+        raise TypeError(f"{name}: eoff must be a contiguous int32 [S + 1] tensor")
+
+
+def esfm_seg_fwd(cam, pt, vals, eoff, weight, P, X, margin, hinge_w, hinge):
+    """Union-batch ESFMLoss forward (gasfm_esfm_seg_fwd): (loss [1], tot [S, 2])."""
+    S = int(weight.numel())
+    _seg_args(eoff, S, "esfm_seg_fwd")
+    n = X.shape[1]
+    if X.shape[0] != 4 or cam.shape != pt.shape or vals.shape != (cam.shape[0], 2):
+        raise ValueError("esfm_seg_fwd: expected pts3D [4, n] and E-long cam / pt / values")
+    dev = X.device
+    part = torch.empty((lib().gasfm_esfm_seg_part_rows(S), 2), dtype=torch.float32, device=dev)
+    tot = torch.empty((S, 2), dtype=torch.float32, device=dev)
+    loss = torch.empty(1, dtype=torch.float32, device=dev)
+    st = lib().gasfm_esfm_seg_fwd(_p(cam), _p(pt), _p(vals), _p(eoff), S, _p(weight), _p(P), _p(X), n, margin, hinge_w,
+                                  int(hinge), _p(part), _p(tot), _p(loss), _stream(X))
+    check(st, "gasfm_esfm_seg_fwd")
+    return loss, tot
+
+
+def esfm_seg_bwd(cptr, pptr, perm, cam, pt, vals, eoff, scene_of_cam, scene_of_pt, weight, P, X, margin, hinge_w,
+                 hinge, equalize, valid_only, dloss, tot, dP, dX):
+    """Union-batch ESFMLoss backward (gasfm_esfm_seg_bwd) into dP [m, 12] and dX [4, n]."""
+    S = int(weight.numel())
+    _seg_args(eoff, S, "esfm_seg_bwd")
+    m, n = P.shape[0], X.shape[1]
+    if cptr.numel() != m + 1 or pptr.numel() != n + 1 or scene_of_cam.numel() != m or scene_of_pt.numel() != n:
+        raise ValueError("esfm_seg_bwd: CSR / scene map shapes do not match m / n")
+    st = lib().gasfm_esfm_seg_bwd(_p(cptr), m, _p(pptr), _p(perm), _p(cam), _p(pt), _p(vals), _p(eoff), S,
+                                  _p(scene_of_cam), _p(scene_of_pt), _p(weight), _p(P), _p(X), n, margin, hinge_w,
+                                  int(hinge), int(equalize), int(valid_only), _p(dloss), _p(tot), _p(dP), _p(dX),
+                                  _stream(X))
+    check(st, "gasfm_esfm_seg_bwd")
+
+
+def reproj_error_seg(cam, pt, xy, eoff, S, P, X):
+    """Per scene of a union batch: tot [S, 2] = (sum of the non-NaN reprojection errors, count)."""
+    _seg_args(eoff, S, "reproj_error_seg")
+    dev = X.device
+    part = torch.empty((lib().gasfm_esfm_seg_part_rows(S), 2), dtype=torch.float32, device=dev)
+    tot = torch.empty((S, 2), dtype=torch.float32, device=dev)
+    st = lib().gasfm_reproj_error_seg(_p(cam), _p(pt), _p(xy), _p(eoff), S, _p(P), _p(X), X.shape[1], _p(part),
+                                      _p(tot), _stream(X))
+    check(st, "gasfm_reproj_error_seg")
+    return tot
 
 
 # ---------------------------------------------------------------- batched single-row problems (global hub)

@@ -114,17 +114,12 @@ __global__ __launch_bounds__(kT) void esfm_fwd_kernel(const int32_t* __restrict_
   }
 }
 
-// dP_c: one workgroup per camera over its contiguous edge range [cptr[c], cptr[c+1])
-__global__ __launch_bounds__(kT) void esfm_bwd_cam_kernel(const int32_t* __restrict__ cptr,
-                                                          const int32_t* __restrict__ cam,
-                                                          const int32_t* __restrict__ pt,
-                                                          const float* __restrict__ vals, int64_t E_norm,
-                                                          const float* __restrict__ P, const float* __restrict__ X,
-                                                          int64_t n, EsfmConf k, const float* __restrict__ dloss,
-                                                          const float* __restrict__ tot, float* __restrict__ dP) {
+// dP_c over camera c's contiguous edge range [cptr[c], cptr[c+1]) by the workgroup
+__device__ __forceinline__ void cam_grad(const int32_t* __restrict__ cptr, const int32_t* __restrict__ pt,
+                                         const float* __restrict__ vals, const float* __restrict__ P,
+                                         const float* __restrict__ X, int64_t n, const EsfmConf& k, int c,
+                                         float scale, float inv_pos, float inv_e, float* __restrict__ dP) {
   __shared__ float sh[kT / 64 * 12];
-  const int c = blockIdx.x;
-  const float inv_e = 1.f / float(E_norm), scale = dloss[0] * inv_e, inv_pos = 1.f / fmaxf(1.f, tot[1]);
   float acc[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) acc[i] = 0.f;
@@ -154,17 +149,12 @@ __global__ __launch_bounds__(kT) void esfm_bwd_cam_kernel(const int32_t* __restr
   }
 }
 
-// d pts3D[:, p]: one thread per point over its edges in CSR order (perm: edge ids)
-__global__ __launch_bounds__(kT) void esfm_bwd_pt_kernel(const int32_t* __restrict__ pptr,
-                                                         const int32_t* __restrict__ perm,
-                                                         const int32_t* __restrict__ cam,
-                                                         const float* __restrict__ vals, int64_t E_norm,
-                                                         const float* __restrict__ P, const float* __restrict__ X,
-                                                         int64_t n, EsfmConf k, const float* __restrict__ dloss,
-                                                         const float* __restrict__ tot, float* __restrict__ dX) {
-  const int64_t p = int64_t(blockIdx.x) * kT + threadIdx.x;
-  if (p >= n) return;
-  const float inv_e = 1.f / float(E_norm), scale = dloss[0] * inv_e, inv_pos = 1.f / fmaxf(1.f, tot[1]);
+// d pts3D[:, p] over point p's edges in CSR order (perm: edge ids)
+__device__ __forceinline__ void pt_grad(const int32_t* __restrict__ pptr, const int32_t* __restrict__ perm,
+                                        const int32_t* __restrict__ cam, const float* __restrict__ vals,
+                                        const float* __restrict__ P, const float* __restrict__ X, int64_t n,
+                                        const EsfmConf& k, int64_t p, float scale, float inv_pos, float inv_e,
+                                        float* __restrict__ dX) {
   float a[4] = {0.f, 0.f, 0.f, 0.f};
   for (int q = pptr[p]; q < pptr[p + 1]; ++q) {
     const int e = perm ? perm[q] : q;
@@ -181,12 +171,160 @@ __global__ __launch_bounds__(kT) void esfm_bwd_pt_kernel(const int32_t* __restri
   for (int j = 0; j < 4; ++j) dX[j * n + p] = a[j];
 }
 
+// dP_c: one workgroup per camera
+__global__ __launch_bounds__(kT) void esfm_bwd_cam_kernel(const int32_t* __restrict__ cptr,
+                                                          const int32_t* __restrict__ pt,
+                                                          const float* __restrict__ vals, int64_t E_norm,
+                                                          const float* __restrict__ P, const float* __restrict__ X,
+                                                          int64_t n, EsfmConf k, const float* __restrict__ dloss,
+                                                          const float* __restrict__ tot, float* __restrict__ dP) {
+  const float inv_e = 1.f / float(E_norm), scale = dloss[0] * inv_e, inv_pos = 1.f / fmaxf(1.f, tot[1]);
+  cam_grad(cptr, pt, vals, P, X, n, k, blockIdx.x, scale, inv_pos, inv_e, dP);
+}
+
+// d pts3D[:, p]: one thread per point
+__global__ __launch_bounds__(kT) void esfm_bwd_pt_kernel(const int32_t* __restrict__ pptr,
+                                                         const int32_t* __restrict__ perm,
+                                                         const int32_t* __restrict__ cam,
+                                                         const float* __restrict__ vals, int64_t E_norm,
+                                                         const float* __restrict__ P, const float* __restrict__ X,
+                                                         int64_t n, EsfmConf k, const float* __restrict__ dloss,
+                                                         const float* __restrict__ tot, float* __restrict__ dX) {
+  const int64_t p = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (p >= n) return;
+  const float inv_e = 1.f / float(E_norm), scale = dloss[0] * inv_e, inv_pos = 1.f / fmaxf(1.f, tot[1]);
+  pt_grad(pptr, perm, cam, vals, P, X, n, k, p, scale, inv_pos, inv_e, dX);
+}
+
+// ---- several scenes in one edge list (a union batch): scene s owns edges [eoff[s], eoff[s+1]),
+// its cameras / points are the ones scene_of_cam / scene_of_pt map to s.  The batch loss is
+// sum_s weight[s] * loss_s; a scene of weight 0 (padding) contributes nothing, and its cameras'
+// and points' gradients are written as zeros without reading its projections.
+constexpr int kSegG = 32;  // workgroups per scene in the segmented sums
+
+// part[(s * kSegG + g)] = (sum of l_e, count of pos_e) over scene s's edges, slice g
+__global__ __launch_bounds__(kT) void esfm_fwd_seg_kernel(const int32_t* __restrict__ cam,
+                                                          const int32_t* __restrict__ pt,
+                                                          const float* __restrict__ vals,
+                                                          const int32_t* __restrict__ eoff,
+                                                          const float* __restrict__ P, const float* __restrict__ X,
+                                                          int64_t n, EsfmConf k, float* __restrict__ part) {
+  __shared__ float sh[kT / 64];
+  const int s = blockIdx.y;
+  const int64_t e1 = eoff[s + 1];
+  float sum = 0.f, cnt = 0.f;
+  for (int64_t e = eoff[s] + int64_t(blockIdx.x) * kT + threadIdx.x; e < e1; e += int64_t(kSegG) * kT) {
+    const float2 m = reinterpret_cast<const float2*>(vals)[e];
+    const Proj r = project(P, X, n, cam[e], pt[e], k);
+    sum += edge_value(r, m.x, m.y, k);
+    cnt += r.pos ? 1.f : 0.f;
+  }
+  sum = block_sum(sum, sh);
+  cnt = block_sum(cnt, sh);
+  if (threadIdx.x == 0) {
+    const int64_t row = int64_t(s) * kSegG + blockIdx.x;
+    part[2 * row] = sum;
+    part[2 * row + 1] = cnt;
+  }
+}
+
+// tot[s] = ordered sum of scene s's kSegG partials; loss (optional) = sum over the scenes of
+// weight nonzero of weight[s] * tot[s][0] / E_s, in scene order.  One workgroup, S <= kT.
+__global__ __launch_bounds__(kT) void seg_total_kernel(const float* __restrict__ part, int S,
+                                                       const int32_t* __restrict__ eoff,
+                                                       const float* __restrict__ weight, float* __restrict__ tot,
+                                                       float* __restrict__ loss) {
+  __shared__ float sh[kT];
+  const int s = threadIdx.x;
+  if (s < S) {
+    float a = 0.f, b = 0.f;
+    for (int g = 0; g < kSegG; ++g) {
+      a += part[2 * (int64_t(s) * kSegG + g)];
+      b += part[2 * (int64_t(s) * kSegG + g) + 1];
+    }
+    tot[2 * s] = a;
+    tot[2 * s + 1] = b;
+    sh[s] = a;
+  }
+  __syncthreads();
+  if (loss && threadIdx.x == 0) {
+    float L = 0.f;
+    for (int q = 0; q < S; ++q) {
+      const float w = weight[q];
+      if (w != 0.f) L += w * (sh[q] / float(eoff[q + 1] - eoff[q]));
+    }
+    loss[0] = L;
+  }
+}
+
+struct SegScale {
+  bool skip;
+  float scale, inv_pos, inv_e;
+};
+
+__device__ __forceinline__ SegScale seg_scale(int s, const int32_t* __restrict__ eoff,
+                                              const float* __restrict__ weight, const float* __restrict__ dloss,
+                                              const float* __restrict__ tot) {
+  SegScale r;
+  const float w = weight[s];
+  r.skip = w == 0.f;
+  r.inv_e = 1.f / float(eoff[s + 1] - eoff[s]);
+  r.scale = dloss[0] * w * r.inv_e;
+  r.inv_pos = 1.f / fmaxf(1.f, tot[2 * s + 1]);
+  return r;
+}
+
+__global__ __launch_bounds__(kT) void esfm_bwd_cam_seg_kernel(
+    const int32_t* __restrict__ cptr, const int32_t* __restrict__ pt, const float* __restrict__ vals,
+    const int32_t* __restrict__ eoff, const int32_t* __restrict__ scene_of_cam, const float* __restrict__ weight,
+    const float* __restrict__ P, const float* __restrict__ X, int64_t n, EsfmConf k,
+    const float* __restrict__ dloss, const float* __restrict__ tot, float* __restrict__ dP) {
+  const int c = blockIdx.x;
+  const SegScale sc = seg_scale(scene_of_cam[c], eoff, weight, dloss, tot);
+  if (sc.skip) {
+    if (threadIdx.x < 12) dP[int64_t(c) * 12 + threadIdx.x] = 0.f;
+    return;
+  }
+  cam_grad(cptr, pt, vals, P, X, n, k, c, sc.scale, sc.inv_pos, sc.inv_e, dP);
+}
+
+__global__ __launch_bounds__(kT) void esfm_bwd_pt_seg_kernel(
+    const int32_t* __restrict__ pptr, const int32_t* __restrict__ perm, const int32_t* __restrict__ cam,
+    const float* __restrict__ vals, const int32_t* __restrict__ eoff, const int32_t* __restrict__ scene_of_pt,
+    const float* __restrict__ weight, const float* __restrict__ P, const float* __restrict__ X, int64_t n,
+    EsfmConf k, const float* __restrict__ dloss, const float* __restrict__ tot, float* __restrict__ dX) {
+  const int64_t p = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (p >= n) return;
+  const SegScale sc = seg_scale(scene_of_pt[p], eoff, weight, dloss, tot);
+  if (sc.skip) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dX[j * n + p] = 0.f;
+    return;
+  }
+  pt_grad(pptr, perm, cam, vals, P, X, n, k, p, sc.scale, sc.inv_pos, sc.inv_e, dX);
+}
+
 // compute_core_errors' "our_repro" (code/evaluation.py:8-31; geo_utils.py:371-391): per edge
 //   X = pts3D[:, p] / pts3D[3, p]   (pflat)      y = Ps_pix[c] X      err = ||xy - y_xy / y_z||
 // with Ps_pix = Ns^-1 Ps_norm (pixel-space cameras, caller-supplied) and xy the PIXEL
 // measurement of the edge.  err[e] is written when err != NULL; the workgroup partial is
 // (sum of the non-NaN errors, their count): np.nanmean's operands.  An inf error (y_z == 0,
 // y_xy != 0) is summed like numpy does.
+__device__ __forceinline__ float reproj_edge(const int32_t* __restrict__ cam, const int32_t* __restrict__ pt,
+                                             const float* __restrict__ xy, const float* __restrict__ P,
+                                             const float* __restrict__ X, int64_t n, int64_t e) {
+  const float2 m = reinterpret_cast<const float2*>(xy)[e];
+  const int c = cam[e], p = pt[e];
+  const float w = X[3 * n + p];
+  const float x0 = X[p] / w, x1 = X[n + p] / w, x2 = X[2 * n + p] / w;
+  const float* pc = P + int64_t(c) * 12;
+  float y[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) y[i] = fmaf(pc[4 * i], x0, fmaf(pc[4 * i + 1], x1, fmaf(pc[4 * i + 2], x2, pc[4 * i + 3])));
+  const float u = m.x - y[0] / y[2], v = m.y - y[1] / y[2];
+  return sqrtf(u * u + v * v);
+}
+
 __global__ __launch_bounds__(kT) void reproj_kernel(const int32_t* __restrict__ cam, const int32_t* __restrict__ pt,
                                                     const float* __restrict__ xy, int64_t E,
                                                     const float* __restrict__ P, const float* __restrict__ X,
@@ -194,16 +332,7 @@ __global__ __launch_bounds__(kT) void reproj_kernel(const int32_t* __restrict__ 
   __shared__ float sh[kT / 64];
   float s = 0.f, cnt = 0.f;
   for (int64_t e = int64_t(blockIdx.x) * kT + threadIdx.x; e < E; e += int64_t(gridDim.x) * kT) {
-    const float2 m = reinterpret_cast<const float2*>(xy)[e];
-    const int c = cam[e], p = pt[e];
-    const float w = X[3 * n + p];
-    const float x0 = X[p] / w, x1 = X[n + p] / w, x2 = X[2 * n + p] / w;
-    const float* pc = P + int64_t(c) * 12;
-    float y[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) y[i] = fmaf(pc[4 * i], x0, fmaf(pc[4 * i + 1], x1, fmaf(pc[4 * i + 2], x2, pc[4 * i + 3])));
-    const float u = m.x - y[0] / y[2], v = m.y - y[1] / y[2];
-    const float r = sqrtf(u * u + v * v);
+    const float r = reproj_edge(cam, pt, xy, P, X, n, e);
     if (err) err[e] = r;
     if (!isnan(r)) {
       s += r;
@@ -215,6 +344,33 @@ __global__ __launch_bounds__(kT) void reproj_kernel(const int32_t* __restrict__ 
   if (threadIdx.x == 0) {
     part[2 * blockIdx.x] = s;
     part[2 * blockIdx.x + 1] = cnt;
+  }
+}
+
+// the same per scene of a union batch: part[(s * kSegG + g)] over scene s's edges, slice g
+__global__ __launch_bounds__(kT) void reproj_seg_kernel(const int32_t* __restrict__ cam,
+                                                        const int32_t* __restrict__ pt,
+                                                        const float* __restrict__ xy,
+                                                        const int32_t* __restrict__ eoff,
+                                                        const float* __restrict__ P, const float* __restrict__ X,
+                                                        int64_t n, float* __restrict__ part) {
+  __shared__ float sh[kT / 64];
+  const int s = blockIdx.y;
+  const int64_t e1 = eoff[s + 1];
+  float sum = 0.f, cnt = 0.f;
+  for (int64_t e = eoff[s] + int64_t(blockIdx.x) * kT + threadIdx.x; e < e1; e += int64_t(kSegG) * kT) {
+    const float r = reproj_edge(cam, pt, xy, P, X, n, e);
+    if (!isnan(r)) {
+      sum += r;
+      cnt += 1.f;
+    }
+  }
+  sum = block_sum(sum, sh);
+  cnt = block_sum(cnt, sh);
+  if (threadIdx.x == 0) {
+    const int64_t row = int64_t(s) * kSegG + blockIdx.x;
+    part[2 * row] = sum;
+    part[2 * row + 1] = cnt;
   }
 }
 
@@ -250,8 +406,8 @@ extern "C" int gasfm_esfm_bwd(const int32_t* cptr, int32_t m, const int32_t* ppt
   GASFM_REQUIRE(cptr && pptr && cam && pt && vals && P && X && dloss && tot && dP && dX, "gasfm_esfm_bwd: null pointer");
   const EsfmConf k{margin, hinge_w, hinge, equalize, valid_only};
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(esfm_bwd_cam_kernel, dim3(m), dim3(kT), 0, st, cptr, cam, pt, vals, E_norm, P, X, n, k, dloss,
-                     tot, dP);
+  hipLaunchKernelGGL(esfm_bwd_cam_kernel, dim3(m), dim3(kT), 0, st, cptr, pt, vals, E_norm, P, X, n, k, dloss, tot,
+                     dP);
   hipLaunchKernelGGL(esfm_bwd_pt_kernel, dim3(unsigned((n + kT - 1) / kT)), dim3(kT), 0, st, pptr, perm, cam, vals,
                      E_norm, P, X, n, k, dloss, tot, dX);
   return launch_status("gasfm_esfm_bwd");
@@ -264,4 +420,50 @@ extern "C" int gasfm_reproj_error(const int32_t* cam, const int32_t* pt, const f
   hipLaunchKernelGGL(reproj_kernel, dim3(gasfm_esfm_part_rows(E)), dim3(kT), 0, (hipStream_t)stream, cam, pt, xy, E,
                      P, pts3D, n, err, part);
   return launch_status("gasfm_reproj_error");
+}
+
+extern "C" int32_t gasfm_esfm_seg_part_rows(int32_t S) { return S * kSegG; }
+
+extern "C" int gasfm_esfm_seg_fwd(const int32_t* cam, const int32_t* pt, const float* vals, const int32_t* eoff,
+                                  int32_t S, const float* weight, const float* P, const float* X, int64_t n,
+                                  float margin, float hinge_w, int32_t hinge, float* part, float* tot, float* loss,
+                                  void* stream) {
+  GASFM_REQUIRE(S > 0 && S <= kT && n > 0, "gasfm_esfm_seg_fwd: S=%d n=%lld", S, (long long)n);
+  GASFM_REQUIRE(cam && pt && vals && eoff && weight && P && X && part && tot && loss, "gasfm_esfm_seg_fwd: null pointer");
+  GASFM_REQUIRE((reinterpret_cast<uintptr_t>(vals) & 7) == 0, "gasfm_esfm_seg_fwd: vals must be 8-byte aligned");
+  const EsfmConf k{margin, hinge_w, hinge, 0, 0};
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(esfm_fwd_seg_kernel, dim3(kSegG, S), dim3(kT), 0, st, cam, pt, vals, eoff, P, X, n, k, part);
+  hipLaunchKernelGGL(seg_total_kernel, dim3(1), dim3(kT), 0, st, part, S, eoff, weight, tot, loss);
+  return launch_status("gasfm_esfm_seg_fwd");
+}
+
+extern "C" int gasfm_esfm_seg_bwd(const int32_t* cam_ptr, int32_t m, const int32_t* pt_ptr, const int32_t* perm,
+                                  const int32_t* cam, const int32_t* pt, const float* vals, const int32_t* eoff,
+                                  int32_t S, const int32_t* scene_of_cam, const int32_t* scene_of_pt,
+                                  const float* weight, const float* P, const float* X, int64_t n, float margin,
+                                  float hinge_w, int32_t hinge, int32_t equalize, int32_t valid_only,
+                                  const float* dloss, const float* tot, float* dP, float* dX, void* stream) {
+  GASFM_REQUIRE(S > 0 && m > 0 && n > 0, "gasfm_esfm_seg_bwd: S=%d m=%d n=%lld", S, m, (long long)n);
+  GASFM_REQUIRE(cam_ptr && pt_ptr && cam && pt && vals && eoff && scene_of_cam && scene_of_pt && weight && P && X &&
+                    dloss && tot && dP && dX,
+                "gasfm_esfm_seg_bwd: null pointer");
+  const EsfmConf k{margin, hinge_w, hinge, equalize, valid_only};
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(esfm_bwd_cam_seg_kernel, dim3(m), dim3(kT), 0, st, cam_ptr, pt, vals, eoff, scene_of_cam, weight,
+                     P, X, n, k, dloss, tot, dP);
+  hipLaunchKernelGGL(esfm_bwd_pt_seg_kernel, dim3(unsigned((n + kT - 1) / kT)), dim3(kT), 0, st, pt_ptr, perm, cam,
+                     vals, eoff, scene_of_pt, weight, P, X, n, k, dloss, tot, dX);
+  return launch_status("gasfm_esfm_seg_bwd");
+}
+
+extern "C" int gasfm_reproj_error_seg(const int32_t* cam, const int32_t* pt, const float* xy, const int32_t* eoff,
+                                      int32_t S, const float* P, const float* pts3D, int64_t n, float* part,
+                                      float* tot, void* stream) {
+  GASFM_REQUIRE(S > 0 && S <= kT && n > 0 && cam && pt && xy && eoff && P && pts3D && part && tot,
+                "gasfm_reproj_error_seg: bad args");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(reproj_seg_kernel, dim3(kSegG, S), dim3(kT), 0, st, cam, pt, xy, eoff, P, pts3D, n, part);
+  hipLaunchKernelGGL(seg_total_kernel, dim3(1), dim3(kT), 0, st, part, S, eoff, nullptr, tot, nullptr);
+  return launch_status("gasfm_reproj_error_seg");
 }

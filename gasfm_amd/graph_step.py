@@ -102,8 +102,11 @@ class CapturedStep:
     collective sequences.
     """
 
-    def __init__(self, fn, params, warmup=3, check=True, rtol=1e-5, agree=None):
+    def __init__(self, fn, params, warmup=3, check=True, rtol=1e-5, agree=None, pool=None):
+        """pool: a torch.cuda.graph_pool_handle() shared with other CapturedSteps that are never
+        replayed concurrently (static_batch.StaticTrainer: one graph per bucket)."""
         self.fn = fn
+        self.pool = pool
         self.params = list(params)
         self.graph = None
         self.static_out = None
@@ -135,7 +138,7 @@ class CapturedStep:
             # while it captures.  ProcessGroupNCCL's watchdog thread queries nothing during the
             # capture: every warm-up collective was retired from its list above, and collectives
             # issued while capturing are never put on it (they belong to the graph).
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):  # records only
+            with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):  # records only
                 out = self.fn()
         except RuntimeError as e:  # capture unsupported for some op
             self.fallback_reason = f"capture failed: {e}"

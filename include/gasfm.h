@@ -648,6 +648,25 @@ int gasfm_esfm_bwd(const int32_t* cam_ptr, int32_t m, const int32_t* pt_ptr, con
                    const float* pts3D, int64_t n, float margin, float hinge_w, int32_t hinge, int32_t equalize,
                    int32_t valid_only, const float* dloss, const float* tot, float* dP, float* dpts3D, void* stream);
 
+/* Union batch of S scenes in one edge list (the captured training step, gasfm_amd/static_batch.py):
+ * scene s owns edges [eoff[s], eoff[s+1]) and the cameras / points scene_of_cam / scene_of_pt map
+ * to s.  Forward: tot[s] = (sum of loss terms, #pos) of scene s, loss[0] = sum over the scenes with
+ * weight[s] != 0 of weight[s] * tot[s][0] / E_s (train.py:76-96 sums the per-scene ESFMLoss of a
+ * batch); part: gasfm_esfm_seg_part_rows(S) x 2 floats of workspace.  Backward: each camera's /
+ * point's gradient as gasfm_esfm_bwd with that scene's E_s and tot[s], scaled by weight[s]; a
+ * scene of weight 0 (padding) gets exact zeros.  S <= 256.  Fixed launch geometry for a given S,
+ * so the calls replay inside a captured graph while the edge counts in eoff change. */
+int32_t gasfm_esfm_seg_part_rows(int32_t S);
+int gasfm_esfm_seg_fwd(const int32_t* cam, const int32_t* pt, const float* vals, const int32_t* eoff, int32_t S,
+                       const float* weight, const float* P, const float* pts3D, int64_t n, float margin,
+                       float hinge_w, int32_t hinge, float* part, float* tot, float* loss, void* stream);
+int gasfm_esfm_seg_bwd(const int32_t* cam_ptr, int32_t m, const int32_t* pt_ptr, const int32_t* perm,
+                       const int32_t* cam, const int32_t* pt, const float* vals, const int32_t* eoff, int32_t S,
+                       const int32_t* scene_of_cam, const int32_t* scene_of_pt, const float* weight, const float* P,
+                       const float* pts3D, int64_t n, float margin, float hinge_w, int32_t hinge, int32_t equalize,
+                       int32_t valid_only, const float* dloss, const float* tot, float* dP, float* dpts3D,
+                       void* stream);
+
 /* ---- global node (ONE row): LayerNorm -> ReLU -> Linear (+ residual) ----
  * Replaces the M = 1 aten chains on the global feature vector: norm_and_proj_global2view /
  * _global2scenepoint (layers.py:497-520), both convs' lin_r on those rows (PyG),
@@ -774,6 +793,10 @@ int gasfm_gatt_merge_unpack(int32_t nprob, const gasfm_gatt_prob* probs, int32_t
  * operands of np.nanmean (finish with gasfm_colsum). */
 int gasfm_reproj_error(const int32_t* cam, const int32_t* pt, const float* xy, int64_t E, const float* P,
                        const float* pts3D, int64_t n, float* err, float* part, void* stream);
+/* The same per scene of a union batch (eoff, S as gasfm_esfm_seg_fwd): tot[s] = (sum of the
+ * non-NaN errors of scene s, their count); part: gasfm_esfm_seg_part_rows(S) x 2 floats. */
+int gasfm_reproj_error_seg(const int32_t* cam, const int32_t* pt, const float* xy, const int32_t* eoff, int32_t S,
+                           const float* P, const float* pts3D, int64_t n, float* part, float* tot, void* stream);
 
 /* ---- device-side scene graph builder (scene_build.hip) ------------------
  * For a dense measurement matrix M [2m x n] (row stride ldM floats) already in HBM, builds on

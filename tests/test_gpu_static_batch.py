@@ -1,0 +1,125 @@
+"""The shape-stable union batch (gasfm_amd/static_batch.py) against the eager union batch (batch.py).
+
+The padded bucket runs the real scenes' computation of the eager union with a disjoint, zero-weight
+pad scene, every camera through a partial slot, other global-graph pieces and per-scene loss partials:
+fp32 summation order only.  Bars (as tests/test_gpu_batch.py): outputs |d| <= 1e-5 + 1e-4 |ref|, the
+loss and the per-scene reprojection errors rtol 1e-5, parameter gradients elementwise rtol 1e-4,
+atol 1e-6.  The trainer test replays a bucket captured on one batch with ANOTHER batch's data
+filled into its static buffers -- the captured graph must read everything it depends on from them.
+12-block learning conf, training-step-sized scenes sampled and augmented on the device.
+"""
+import numpy as np
+import pytest
+import torch
+
+import gasfm_amd
+from gasfm_amd import evaluation, static_batch, synthetic
+from gasfm_amd.batch import forward_batch
+from gasfm_amd.loss import ESFMLoss
+from gasfm_amd.scene_device import apply_rotational_homography_aug_device, sample_data_device, scene_from_dense_device
+
+from test_gpu_batch import _conf, _grads
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def s2g_pieces(monkeypatch):
+    monkeypatch.setattr(static_batch, "S2G_PIECES", 128)  # the test scenes have ~1-2k valid points
+
+
+def _scenes(device, views, seed=0, n=3000):
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    out = []
+    for i, v in enumerate(views):
+        sc = synthetic.windowed_scene(40, n, mean_extra=6, seed=20 + i + 7 * seed)
+        full = scene_from_dense_device(torch.from_numpy(sc.dense_M()).to(device), torch.from_numpy(sc.Ns()).to(device),
+                                       torch.from_numpy(sc.Ps_gt()).to(device), f"s{i}")
+        out.append(apply_rotational_homography_aug_device(sample_data_device(full, v), 15, 20))
+    return out
+
+
+def _eager(net, lossf, datas):
+    net.zero_grad(set_to_none=True)
+    pred = forward_batch(net, datas)
+    loss = sum(lossf(p, d) for p, d in zip(pred, datas))
+    loss.backward()
+    errs = [float(evaluation.reprojection_error_mean(d, p)) for p, d in zip(pred, datas)]
+    return pred, float(loss), _grads(net), errs
+
+
+def _check_grads(net, g, g_ref):
+    for (n, _), a, b in zip(net.named_parameters(), g, g_ref):
+        assert (a is None) == (b is None), n
+        if a is not None:
+            torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6, msg=n)
+
+
+def test_static_batch_matches_eager_union(device):
+    torch.manual_seed(1)
+    conf = _conf()
+    net = gasfm_amd.GraphAttnSfMNet(conf).to(device)
+    lossf = ESFMLoss(conf)
+    datas = _scenes(device, (12, 15, 18))
+    pred_ref, loss_ref, g_ref, err_ref = _eager(net, lossf, datas)
+    st = static_batch.BatchStats(datas)
+    assert st.expressible() is None
+    sb = static_batch.StaticBatch(static_batch.Caps.for_batch(st), device)
+    sb.fill(datas, st)
+    net.zero_grad(set_to_none=True)
+    pred = net(sb)
+    loss = static_batch.batch_loss(pred, sb, lossf)
+    tot = static_batch.batch_repro_errors(pred, sb)
+    loss.backward()
+    for a, b in zip(sb.split(pred), pred_ref):
+        for k in ("Ps_norm", "pts3D"):
+            np.testing.assert_allclose(a[k].detach().cpu().numpy(), b[k].detach().cpu().numpy(), rtol=1e-4, atol=1e-5)
+    assert torch.isfinite(pred["Ps_norm"]).all() and torch.isfinite(pred["pts3D"]).all()  # the pad scene too
+    assert abs(float(loss) - loss_ref) <= 1e-5 * abs(loss_ref)
+    t = tot.tolist()
+    np.testing.assert_allclose([a / b for a, b in t[:st.B]], err_ref, rtol=1e-5)
+    _check_grads(net, _grads(net), g_ref)
+
+
+def test_static_trainer_replays_another_batch(device, monkeypatch):
+    monkeypatch.setattr(static_batch, "MAX_WASTE", 10.0)  # the second batch reuses the first one's bucket
+    torch.manual_seed(2)
+    conf = _conf()
+    net = gasfm_amd.GraphAttnSfMNet(conf).to(device)
+    lossf = ESFMLoss(conf)
+    trainer = static_batch.StaticTrainer(net, lossf)
+    batches = [_scenes(device, (14, 16, 18), seed=0), _scenes(device, (10, 12, 13), seed=1)]
+    for k, datas in enumerate(batches):
+        loss, errs = trainer.step(datas)
+        g = _grads(net)
+        assert trainer.fallbacks == [] and trainer.eager_steps == 0
+        assert len(trainer.buckets) == 1 and trainer.captures == 1
+        assert next(iter(trainer.buckets.values()))[1].captured
+        _, loss_ref, g_ref, err_ref = _eager(net, lossf, datas)
+        assert abs(float(loss) - loss_ref) <= 1e-5 * abs(loss_ref), k
+        np.testing.assert_allclose(errs, err_ref, rtol=1e-5)
+        _check_grads(net, g, g_ref)
+
+
+def test_static_trainer_outlier_inputs(device):
+    """Config 5: the network sees the outlier-injected scenes, the loss and errors the clean ones."""
+    from gasfm_amd.outliers import inject_outliers
+    torch.manual_seed(3)
+    conf = _conf()
+    net = gasfm_amd.GraphAttnSfMNet(conf).to(device)
+    lossf = ESFMLoss(conf)
+    datas = _scenes(device, (14, 16, 18), seed=2)
+    inputs = [inject_outliers(d, 0.1, log=lambda s: None) for d in datas]
+    assert all(x is not None for x in inputs)
+    trainer = static_batch.StaticTrainer(net, lossf)
+    loss, errs = trainer.step(datas, inputs)
+    g = _grads(net)
+    net.zero_grad(set_to_none=True)
+    pred = forward_batch(net, inputs)
+    loss_ref = sum(lossf(p, d) for p, d in zip(pred, datas))
+    loss_ref.backward()
+    err_ref = [float(evaluation.reprojection_error_mean(d, p)) for p, d in zip(pred, datas)]
+    assert abs(float(loss) - float(loss_ref)) <= 1e-5 * abs(float(loss_ref))
+    np.testing.assert_allclose(errs, err_ref, rtol=1e-5)
+    _check_grads(net, g, _grads(net))

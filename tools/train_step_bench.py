@@ -58,6 +58,11 @@ def main():
                     help="outlier injection rate (config 5: rhaug-15-20 + 0.1 outliers), 0 = off")
     ap.add_argument("--per-scene", action="store_true",
                     help="also time one forward per scene (train.py's loop) beside the batched union forward")
+    ap.add_argument("--captured", action="store_true",
+                    help="also time the captured step (static_batch.StaticTrainer: the batch padded to a bucket, "
+                         "forward + loss + errors + backward replayed as one hipGraph per bucket)")
+    ap.add_argument("--prime", type=int, default=40,
+                    help="--captured: batches run before the timed steps (they create and capture the buckets)")
     ap.add_argument("--capture-floor", action="store_true",
                     help="also time one FIXED batch's forward + loss + backward captured as a hipGraph and "
                          "replayed (the GPU-side floor of the union step, without the host's launch cost)")
@@ -135,11 +140,65 @@ def main():
                 "ms_adam": 1e3 * t_opt / steps, "first_repro_px": float(repro[0]),
                 "last_repro_px": float(repro[-1])}
 
+    def run_captured(prep, steps, prime):
+        from gasfm_amd.static_batch import StaticTrainer
+        trainer = StaticTrainer(net, lossf)
+        t_prep = t_fb = t_opt = 0.0
+        n_done = 0
+        repro = []
+        caps_before = 0
+        t_prime = time.perf_counter()
+        for it in range(prime + steps):
+            if it == prime:
+                torch.cuda.synchronize()
+                t_prime = time.perf_counter() - t_prime
+                caps_before = trainer.captures
+            if it % 10 == 0:
+                print(f"captured: batch {it}/{prime + steps}, buckets {len(trainer.buckets)}", file=sys.stderr,
+                      flush=True)
+            batch = [scenes[int(i)] for i in np.random.choice(len(scenes), args.batch, replace=False)]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            datas = [prep(s) for s in batch]
+            inputs = datas if not args.outliers else [inject_outliers(d, args.outliers, log=lambda s: None)
+                                                      for d in datas]
+            keep = [k for k, d in enumerate(inputs) if d is not None]
+            datas, inputs = [datas[k] for k in keep], [inputs[k] for k in keep]
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            opt.zero_grad()
+            loss, errs = trainer.step(datas, inputs)  # reads the per-scene errors: a host sync
+            repro.extend(errs)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            opt.step()
+            torch.cuda.synchronize()
+            t3 = time.perf_counter()
+            if it >= prime:
+                t_prep += t1 - t0
+                t_fb += t2 - t1
+                t_opt += t3 - t2
+                n_done += len(datas)
+        tot = t_prep + t_fb + t_opt
+        return {"scenes_per_s": n_done / tot, "ms_per_step": 1e3 * tot / steps,
+                "ms_data_prep": 1e3 * t_prep / steps, "ms_fill_replay_errors": 1e3 * t_fb / steps,
+                "ms_adam": 1e3 * t_opt / steps, "prime_batches": prime, "s_prime": t_prime,
+                "buckets": len(trainer.buckets), "captures_in_prime": caps_before,
+                "captures_in_timed": trainer.captures - caps_before, "eager_steps": trainer.eager_steps,
+                "fallbacks": sorted(set(map(str, trainer.fallbacks))), "first_repro_px": float(repro[0]),
+                "last_repro_px": float(repro[-1])}
+
     res = run(prep_device, args.steps, args.warmup)
     tag = f" + {args.outliers:g} outlier injection" if args.outliers else ""
     print(json.dumps({"mode": "device data path (sample + rhaug" + tag + " + graph build on GPU), batch as one union forward",
                       "batch": args.batch, "scene": f"m={args.views} n={args.points}, 10-20 sampled views", **res}),
           flush=True)
+    if args.captured:
+        res = run_captured(prep_device, args.steps, args.prime)
+        print(json.dumps({"mode": "captured: device data path" + tag + ", the batch padded to a bucket and filled into "
+                                  "its static buffers, forward + ESFMLoss + errors + backward replayed as one hipGraph",
+                          "batch": args.batch, "scene": f"m={args.views} n={args.points}, 10-20 sampled views", **res}),
+              flush=True)
     if args.capture_floor:
         from gasfm_amd.batch import SceneBatch
         from gasfm_amd.graph_step import CapturedStep
