@@ -42,6 +42,7 @@ a point seen by > 256 views, a scene with < S2G_PIECES valid points) run eagerly
 batch.SceneBatch, counted in ``StaticTrainer.eager_steps``.
 """
 import math
+import time
 
 import torch
 
@@ -404,10 +405,17 @@ class StaticTrainer:
     ``step(datas, inputs=None)`` leaves this batch's gradients in ``p.grad`` (as zero_grad + the eager
     union's loss.backward()) and returns (loss 0-d tensor, per-scene our_repro errors list).
     Config 5: ``inputs`` = the outlier-injected scenes the network sees, ``datas`` the clean ones the
-    loss and the errors use (train.py:73-90)."""
+    loss and the errors use (train.py:73-90).
 
-    def __init__(self, net, lossf, warmup=2):
+    optimizer: stepped after the gradients (train.py:97-100).  With ``capturable=True`` (torch's
+    Adam / AdamW) its step is captured too, one graph per bucket over that bucket's gradient
+    tensors, once its state exists (the first step of a run is eager); a Python-float learning rate
+    is then fixed at capture (pass a tensor lr to schedule it)."""
+
+    def __init__(self, net, lossf, warmup=2, optimizer=None):
         self.net, self.lossf = net, lossf
+        self.optimizer = optimizer
+        self.opt_graphs = 0
         self.params = [p for p in net.parameters() if p.requires_grad]
         self.buckets = {}
         self.pool = torch.cuda.graph_pool_handle()
@@ -415,6 +423,7 @@ class StaticTrainer:
         self.captures = 0
         self.eager_steps = 0
         self.fallbacks = []
+        self.profile = None  # a dict: per-phase host seconds (stats, fill, replay, optimizer), synchronised
 
     def _bucket(self, st, dev):
         best = None
@@ -444,18 +453,49 @@ class StaticTrainer:
         errs = [float(evaluation.reprojection_error_mean(d, p)) for p, d in zip(preds, datas)]
         return loss.detach(), errs
 
+    def _optimizer_step(self, b):
+        opt = self.optimizer
+        if len(b) > 3:
+            b[3].replay()
+        elif b[1].captured and opt.defaults.get("capturable") and all(p in opt.state for p in self.params):
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
+                opt.step()
+            g.replay()
+            b.append(g)
+            self.opt_graphs += 1
+        else:
+            opt.step()
+        if getattr(self.net, "_projection_precision", "fp32") == "bf16":
+            self.net.refresh_weight_shadows()
+
+    def _tick(self, phase):
+        if self.profile is not None:
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            if phase is not None:
+                self.profile[phase] = self.profile.get(phase, 0.0) + t - self._t
+            self._t = t
+
     def step(self, datas, inputs=None):
         from .graph_step import CapturedStep
         inputs = datas if inputs is None else inputs
+        self._tick(None)
         st = BatchStats(inputs)
         why = st.expressible()
         if why is not None:
             self.fallbacks.append(why)
-            return self._eager(datas, inputs)
+            loss, errs = self._eager(datas, inputs)
+            if self.optimizer is not None:
+                self.optimizer.step()
+            return loss, errs
         dev = inputs[0].x.values.device
         b, _ = self._bucket(st, dev)
         sb = b[0]
+        self._tick("stats")
         sb.fill(datas, st, inputs)
+        self._tick("fill")
         out = {}
 
         def fwd_bwd():
@@ -473,6 +513,10 @@ class StaticTrainer:
             if not b[1].captured:
                 self.fallbacks.append(b[1].fallback_reason)
         loss = b[1]()
+        self._tick("replay" if b[1].captured else "eager")
+        if self.optimizer is not None:
+            self._optimizer_step(b)
+            self._tick("optimizer")
         err = b[2]["err"]
         tot = err[:st.B].tolist()
         return loss, [t[0] / t[1] if t[1] else float("nan") for t in tot]

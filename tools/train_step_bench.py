@@ -63,6 +63,8 @@ def main():
                          "forward + loss + errors + backward replayed as one hipGraph per bucket)")
     ap.add_argument("--prime", type=int, default=40,
                     help="--captured: batches run before the timed steps (they create and capture the buckets)")
+    ap.add_argument("--phases", action="store_true",
+                    help="--captured: also time the trainer's phases with a synchronize between them (slower)")
     ap.add_argument("--capture-floor", action="store_true",
                     help="also time one FIXED batch's forward + loss + backward captured as a hipGraph and "
                          "replayed (the GPU-side floor of the union step, without the host's launch cost)")
@@ -142,7 +144,9 @@ def main():
 
     def run_captured(prep, steps, prime):
         from gasfm_amd.static_batch import StaticTrainer
-        trainer = StaticTrainer(net, lossf)
+        # Adam as above, with its step captured into each bucket's graph pair (capturable=True)
+        copt = torch.optim.Adam(net.parameters(), lr=1e-4, fused=True, capturable=True)
+        trainer = StaticTrainer(net, lossf, optimizer=copt)
         t_prep = t_fb = t_opt = 0.0
         n_done = 0
         repro = []
@@ -153,6 +157,7 @@ def main():
                 torch.cuda.synchronize()
                 t_prime = time.perf_counter() - t_prime
                 caps_before = trainer.captures
+                trainer.profile = {} if args.phases else None
             if it % 10 == 0:
                 print(f"captured: batch {it}/{prime + steps}, buckets {len(trainer.buckets)}", file=sys.stderr,
                       flush=True)
@@ -166,14 +171,11 @@ def main():
             datas, inputs = [datas[k] for k in keep], [inputs[k] for k in keep]
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            opt.zero_grad()
-            loss, errs = trainer.step(datas, inputs)  # reads the per-scene errors: a host sync
+            copt.zero_grad()
+            loss, errs = trainer.step(datas, inputs)  # + Adam; reads the per-scene errors (a host sync)
             repro.extend(errs)
             torch.cuda.synchronize()
-            t2 = time.perf_counter()
-            opt.step()
-            torch.cuda.synchronize()
-            t3 = time.perf_counter()
+            t2 = t3 = time.perf_counter()
             if it >= prime:
                 t_prep += t1 - t0
                 t_fb += t2 - t1
@@ -181,11 +183,13 @@ def main():
                 n_done += len(datas)
         tot = t_prep + t_fb + t_opt
         return {"scenes_per_s": n_done / tot, "ms_per_step": 1e3 * tot / steps,
-                "ms_data_prep": 1e3 * t_prep / steps, "ms_fill_replay_errors": 1e3 * t_fb / steps,
-                "ms_adam": 1e3 * t_opt / steps, "prime_batches": prime, "s_prime": t_prime,
+                "ms_data_prep": 1e3 * t_prep / steps, "ms_fill_replay_errors_adam": 1e3 * t_fb / steps,
+                "prime_batches": prime, "s_prime": t_prime, "optimizer_graphs": trainer.opt_graphs,
                 "buckets": len(trainer.buckets), "captures_in_prime": caps_before,
                 "captures_in_timed": trainer.captures - caps_before, "eager_steps": trainer.eager_steps,
-                "fallbacks": sorted(set(map(str, trainer.fallbacks))), "first_repro_px": float(repro[0]),
+                "fallbacks": sorted(set(map(str, trainer.fallbacks))),
+                "ms_phases_synced": {k: 1e3 * v / steps for k, v in (trainer.profile or {}).items()},
+                "first_repro_px": float(repro[0]),
                 "last_repro_px": float(repro[-1])}
 
     res = run(prep_device, args.steps, args.warmup)
