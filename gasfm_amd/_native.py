@@ -163,6 +163,8 @@ _SIGS = {
     "gasfm_esfm_seg_bwd": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _f32,
                                   _f32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_reproj_error_seg": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _i64, _vp, _vp, _vp]),
+    "gasfm_union_fill_scene": (_i32, [_vp, _vp, _vp]),
+    "gasfm_union_fill_pad": (_i32, [_vp, _vp, _vp]),
     "gasfm_point_tail_part_shape": (_i32, [_i64, _i32, _vp]),
     "gasfm_point_hub_part_shape": (_i32, [_i64, _i32, _i32, _vp]),
     "gasfm_point_tail_fwd": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
@@ -1178,6 +1180,31 @@ def reproj_error_seg(cam, pt, xy, eoff, S, P, X):
                                       _p(tot), _stream(X))
     check(st, "gasfm_reproj_error_seg")
     return tot
+
+
+class UnionScene(ctypes.Structure):
+    _fields_ = ([("idx", _vp), ("ld_idx", _i64)] + [(k, _vp) for k in (
+        "vals", "vals_loss", "cptr", "pptr", "perm", "pos", "cam_per_pts", "pts_per_cam", "M")] + [("ldM", _i64),
+        ("Ns", _vp)] + [(k, _i64) for k in ("E", "m", "n", "e0", "c0", "p0", "item0")] + [("scene", _i32)])
+
+
+class UnionOut(ctypes.Structure):
+    _fields_ = ([("indices", _vp), ("ld_indices", _i64)] + [(k, _vp) for k in (
+        "cam32", "pt32", "values", "values_loss", "xy", "perm", "pos", "cam_ptr", "pt_ptr", "cam_per_pts",
+        "pts_per_cam", "soc", "soc32", "sop32", "Ns_inv", "items_c", "comb_c", "items_p")] + [("piece", _i32)])
+
+
+class UnionPad(ctypes.Structure):
+    _fields_ = [(k, _i64) for k in ("M", "N", "E", "mp", "npd", "ep", "dI", "item0")] + [("scene", _i32)]
+
+
+def union_fill_scene(sc, out, stream_of):
+    check(lib().gasfm_union_fill_scene(ctypes.byref(sc), ctypes.byref(out), _stream(stream_of)),
+          "gasfm_union_fill_scene")
+
+
+def union_fill_pad(pd, out, stream_of):
+    check(lib().gasfm_union_fill_pad(ctypes.byref(pd), ctypes.byref(out), _stream(stream_of)), "gasfm_union_fill_pad")
 
 
 # ---------------------------------------------------------------- batched single-row problems (global hub)

@@ -44,6 +44,7 @@ batch.SceneBatch, counted in ``StaticTrainer.eager_steps``.
 import math
 import time
 
+import numpy as np
 import torch
 
 from . import _native
@@ -76,7 +77,8 @@ class BatchStats:
             rows.append(torch.stack([pieces.sum(), deg.min(), (ppc >= MIN_N_POINTS_PER_VIEW).sum(),
                                      (cpp >= MIN_N_VIEWS_PER_POINT).sum(), cpp.max()]))
         v = torch.stack(rows).tolist()
-        self.pieces = sum(r[0] for r in v)
+        self.pieces_s = [r[0] for r in v]
+        self.pieces = sum(self.pieces_s)
         self.min_cam_deg = min(r[1] for r in v)
         self.kv = [r[2] for r in v]
         self.kp = [r[3] for r in v]
@@ -176,7 +178,17 @@ class StaticBatch:
         self.cam_per_pts, self.pts_per_cam = z(N, 1, **i64), z(M, 1, **i64)
         self.scene_of_cam = z(M, **i64)
         self.soc32, self.sop32 = z(M, **i32), z(N, **i32)
-        self.eoff = z(S + 1, **i32)
+        # one int32 buffer fed from the host per step: the global graphs' items / segments and the
+        # loss's edge offsets (views below; items first, so their rows stay 16-byte aligned)
+        nh = S * c.P * 4 + S * 4 + 3 * (S + 1)
+        self.hostfed = z(nh, **i32)
+        o = 0
+        views = {}
+        for name, n, shape in (("items_s", S * c.P * 4, (S * c.P, 4)), ("items_v", S * 4, (S, 4)),
+                               ("seg_v", S + 1, (S + 1,)), ("seg_p", S + 1, (S + 1,)), ("eoff", S + 1, (S + 1,))):
+            views[name] = self.hostfed[o:o + n].view(shape)
+            o += n
+        self.eoff = views["eoff"]
         self.weight = torch.tensor([1.0] * c.B + [0.0], **f32)
         self.Ns_inv = torch.eye(3, **f32).repeat(M, 1, 1)
         # camera plan: I items, every camera through partial slots, one combine entry per camera
@@ -186,10 +198,11 @@ class StaticBatch:
         self.items_p = z(N, 4, **i32)
         # global graphs: sources = valid views / points (scene-major), one segment per scene
         self.kv_cap, self.kp_cap = M - c.inv_v, N - c.inv_p
-        self.src_v, self.src_p = z(self.kv_cap, **i32), z(self.kp_cap, **i32)
-        self.seg_v, self.seg_p = z(S + 1, **i32), z(S + 1, **i32)
-        self.items_v = z(S, 4, **i32)
-        self.items_s = z(S * c.P, 4, **i32)
+        # (all views valid / all points valid -- the usual case -- makes the sources the identity)
+        self.src_v = torch.arange(M, **i32) if c.inv_v == 0 else z(self.kv_cap, **i32)
+        self.src_p = torch.arange(N, **i32) if c.inv_p == 0 else z(self.kp_cap, **i32)
+        self.seg_v, self.seg_p = views["seg_v"], views["seg_p"]
+        self.items_v, self.items_s = views["items_v"], views["items_s"]
         self.pos_v = torch.arange(M, **i32) if self.kv_cap == M else None
         self.pos_p = torch.arange(N, **i32) if self.kp_cap == N else None
         n_slots = S * c.P
@@ -229,12 +242,101 @@ class StaticBatch:
         self.x.__dict__["_gasfm_edges"] = {
             (str(dev), self.indices.data_ptr()): EdgeIndex(self.cam32, self.pt32, M, N, plans)}
         self.offsets = None
+        self._out = None
+        if dev.type == "cuda":
+            o = _native.UnionOut()
+            for k in ("indices", "cam32", "pt32", "values", "values_loss", "xy", "perm", "pos", "cam_ptr", "pt_ptr",
+                      "cam_per_pts", "pts_per_cam", "soc32", "sop32", "Ns_inv", "items_c", "comb_c", "items_p"):
+                setattr(o, k, getattr(self, k).data_ptr())
+            o.soc = self.scene_of_cam.data_ptr()
+            o.ld_indices = E
+            o.piece = PIECE
+            self._out = o
+
+    def _host_plans(self, st, npd):
+        """The global graphs' segments / items and the edge offsets from host counts (all views and all
+        points valid): int32 array laid out as self.hostfed."""
+        c = self.caps
+        S, P = c.S, c.P
+        seg_v = np.concatenate([[0], np.cumsum(st.ms + [c.M - st.M])]).astype(np.int64)
+        seg_p = np.concatenate([[0], np.cumsum(st.ns + [npd])]).astype(np.int64)
+        k = np.arange(S * P)
+        ks, kq = k // P, k % P
+        cnt = (seg_p[1:] - seg_p[:-1])[ks]
+        b2, r2 = cnt // P, cnt % P
+        begin = seg_p[:-1][ks] + kq * b2 + np.minimum(kq, r2)
+        items_s = np.stack([ks, begin, begin + b2 + (kq < r2), k], 1)
+        items_v = np.stack([np.arange(S), seg_v[:-1], seg_v[1:], np.full(S, -1)], 1)
+        eo = np.concatenate([[0], np.cumsum(st.Es), [c.E]])
+        return np.concatenate([items_s.ravel(), items_v.ravel(), seg_v, seg_p, eo]).astype(np.int32)
 
     # ------------------------------------------------------------------ per-step fill
     def fill(self, datas, st, inputs=None):
         """Write the batch (device-built scenes; ``inputs``: the network's inputs when they differ from
         the loss's scenes, e.g. outlier-injected copies with the same edges) and this bucket's pad scene
-        into the static buffers.  Device work only."""
+        into the static buffers: one gasfm_union_fill_scene launch per scene, one gasfm_union_fill_pad,
+        one host-to-device copy of the global graphs' items.  fill_torch is the same in torch ops (the
+        CPU path, and the GPU test's check of this one)."""
+        c = self.caps
+        if self._out is None:
+            return self.fill_torch(datas, st, inputs)
+        pad = c.pad(st)
+        if pad is None:
+            raise ValueError("StaticBatch.fill: the batch does not fit this bucket")
+        mp, npd, ep, dI = pad
+        inputs = datas if inputs is None else inputs
+        dev = self.device
+        mo = [sum(st.ms[:i]) for i in range(st.B + 1)]
+        no = [sum(st.ns[:i]) for i in range(st.B + 1)]
+        eo = [sum(st.Es[:i]) for i in range(st.B + 1)]
+        keep = []  # operands made contiguous here stay referenced until the launches are queued
+        item0 = 0
+        for s, (d, din, a) in enumerate(zip(datas, inputs, st.arrays)):
+            if int(din.x.indices.shape[1]) != st.Es[s]:
+                raise ValueError("StaticBatch.fill: the network's input scene has other edges than the loss's")
+            sc = _native.UnionScene()
+            idx = d.x.indices
+            if idx.dtype != torch.int64 or idx.stride(1) != 1:
+                idx = idx.to(torch.int64).contiguous()
+            sc.idx, sc.ld_idx = idx.data_ptr(), idx.stride(0)
+            t = {"vals": din.x.values, "vals_loss": d.x.values}
+            for k, v in t.items():
+                t[k] = v.to(torch.float32).contiguous()
+            t["cptr"], t["pptr"] = a[0].to(torch.int32).contiguous(), a[1].to(torch.int32).contiguous()
+            t["perm"] = None if a[2] is None else a[2].to(torch.int32).contiguous()
+            t["pos"] = None if a[3] is None else a[3].to(torch.int32).contiguous()
+            t["cam_per_pts"] = d.x.cam_per_pts.to(torch.int64).contiguous()
+            t["pts_per_cam"] = d.x.pts_per_cam.to(torch.int64).contiguous()
+            t["Ns"] = d.Ns.to(dev, torch.float32).contiguous()
+            Md = getattr(d, "_M", None)
+            if Md is None:
+                Md = getattr(d, "M", None)
+            if Md is not None:
+                Md = Md.to(dev, torch.float32)
+                if Md.stride(1) != 1:
+                    Md = Md.contiguous()
+                sc.ldM = Md.stride(0)
+            t["M"] = Md
+            for k, v in t.items():
+                setattr(sc, k, None if v is None else v.data_ptr())
+            keep.append((idx, t))
+            sc.E, sc.m, sc.n = st.Es[s], st.ms[s], st.ns[s]
+            sc.e0, sc.c0, sc.p0, sc.item0, sc.scene = eo[s], mo[s], no[s], item0, s
+            item0 += st.pieces_s[s]
+            _native.union_fill_scene(sc, self._out, self.values)
+        pd = _native.UnionPad()
+        pd.M, pd.N, pd.E, pd.mp, pd.npd, pd.ep, pd.dI, pd.item0, pd.scene = st.M, st.N, st.E, mp, npd, ep, dI, item0, st.B
+        _native.union_fill_pad(pd, self._out, self.values)
+        self.offsets = (mo, no, eo)
+        if c.inv_v == 0 and c.inv_p == 0:
+            # a fresh pinned block per step: the caching host allocator keeps it until the copy ran
+            self.hostfed.copy_(torch.from_numpy(self._host_plans(st, npd)).pin_memory(), non_blocking=True)
+        else:
+            self.eoff.copy_(torch.tensor(eo + [c.E], dtype=torch.int32).to(dev))
+            self._global_plans_torch()
+
+    def fill_torch(self, datas, st, inputs=None):
+        """``fill`` in torch ops."""
         c = self.caps
         pad = c.pad(st)
         if pad is None:
@@ -281,7 +383,7 @@ class StaticBatch:
                 Md = Md.to(dev)
                 self.xy[e0:e1, 0].copy_(Md[2 * idx[0], idx[1]])
                 self.xy[e0:e1, 1].copy_(Md[2 * idx[0] + 1, idx[1]])
-            self.Ns_inv[c0:c1].copy_(_inv3(d.Ns.to(dev, torch.float32)))
+        self.Ns_inv[:M].copy_(_inv3(torch.cat([d.Ns.to(dev, torch.float32) for d in datas])))
         # the pad scene: mp cameras, npd points, ep edges, cam-major and point-sorted
         ar = lambda n: torch.arange(n, **i64)
         degc = ep // mp + (ar(mp) < ep % mp).to(torch.int64)
@@ -331,6 +433,14 @@ class StaticBatch:
         # point plan
         pptr = self.pt_ptr.to(torch.int64)
         self.items_p.copy_(torch.stack([ar(c.N), pptr[:-1], pptr[1:], torch.full((c.N,), -1, **i64)], 1))
+        self._global_plans_torch()
+
+    def _global_plans_torch(self):
+        """view2global / scenepoint2global segments and items from the filled counts (torch ops)."""
+        c = self.caps
+        i64 = dict(dtype=torch.int64, device=self.device)
+        ar = lambda n: torch.arange(n, **i64)
+        sop = self.sop32.to(torch.int64)
         # view2global: one item per scene over its valid views
         valid_v = self.pts_per_cam.view(-1) >= MIN_N_POINTS_PER_VIEW
         self.src_v.copy_(torch.nonzero_static(valid_v, size=self.kv_cap).view(-1))

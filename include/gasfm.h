@@ -793,6 +793,58 @@ int gasfm_gatt_merge_unpack(int32_t nprob, const gasfm_gatt_prob* probs, int32_t
  * operands of np.nanmean (finish with gasfm_colsum). */
 int gasfm_reproj_error(const int32_t* cam, const int32_t* pt, const float* xy, int64_t E, const float* P,
                        const float* pts3D, int64_t n, float* err, float* part, void* stream);
+/* ---- shape-stable union batch fill (static_batch.hip; gasfm_amd/static_batch.py) ----
+ * The captured config-3 / config-5 training step (train.py:60-152) replays one graph per bucket of
+ * fixed cameras / points / edges / camera items; each step writes the sampled scenes and a pad
+ * scene into the bucket's static buffers.  gasfm_union_fill_scene writes scene s at union offsets
+ * (e0, c0, p0): indices [2 x E_cap] (row stride ld_indices) and their int32 copies, the network's
+ * and the loss's measurements, pixel measurements gathered from the scene's dense M [2m x n] (row
+ * stride ldM; NULL: zeros), perm / pos (point-order edge ids and their inverse; NULL: identity) and
+ * both CSRs offset by e0, cam_per_pts / pts_per_cam, the scene maps, Ns^-1 per camera (fp64
+ * inverse, fp32 out), one point work item per point (slot -1) and ceil(deg / piece) camera work
+ * items per camera from item0 on, every camera through partial slots (slot = item index) with one
+ * combine entry (c, first, pieces, 1).  m <= GASFM_UNION_MAX_CAMS.  gasfm_union_fill_pad writes
+ * the pad scene after the real ones: mp cameras / npd points / ep edges from (M, N, E), degrees
+ * spread evenly, edge k joining the k-th entries of the two degree expansions, zero measurements,
+ * identity Ns^-1, the remaining dI camera items from item0 on, and the closing CSR entries. */
+#define GASFM_UNION_MAX_CAMS 4096
+typedef struct gasfm_union_scene {
+  const int64_t* idx; /* [2 x E] (cam, pt), row stride ld_idx */
+  int64_t ld_idx;
+  const float* vals;      /* [E x 2] the network's measurements */
+  const float* vals_loss; /* [E x 2] the loss's (the clean scene under outlier injection) */
+  const int32_t* cptr;    /* [m + 1] */
+  const int32_t* pptr;    /* [n + 1] */
+  const int32_t* perm;    /* [E] or NULL */
+  const int32_t* pos;     /* [E] or NULL */
+  const int64_t* cam_per_pts; /* [n] */
+  const int64_t* pts_per_cam; /* [m] */
+  const float* M;             /* [2m x n] or NULL */
+  int64_t ldM;
+  const float* Ns; /* [m x 3 x 3] */
+  int64_t E, m, n;
+  int64_t e0, c0, p0, item0;
+  int32_t scene;
+} gasfm_union_scene;
+typedef struct gasfm_union_out {
+  int64_t* indices;
+  int64_t ld_indices;
+  int32_t *cam32, *pt32;
+  float *values, *values_loss, *xy;
+  int32_t *perm, *pos, *cam_ptr, *pt_ptr;
+  int64_t *cam_per_pts, *pts_per_cam, *soc;
+  int32_t *soc32, *sop32;
+  float* Ns_inv;
+  int32_t *items_c, *comb_c, *items_p;
+  int32_t piece;
+} gasfm_union_out;
+typedef struct gasfm_union_pad {
+  int64_t M, N, E, mp, npd, ep, dI, item0;
+  int32_t scene;
+} gasfm_union_pad;
+int gasfm_union_fill_scene(const gasfm_union_scene* scene, const gasfm_union_out* out, void* stream);
+int gasfm_union_fill_pad(const gasfm_union_pad* pad, const gasfm_union_out* out, void* stream);
+
 /* The same per scene of a union batch (eoff, S as gasfm_esfm_seg_fwd): tot[s] = (sum of the
  * non-NaN errors of scene s, their count); part: gasfm_esfm_seg_part_rows(S) x 2 floats. */
 int gasfm_reproj_error_seg(const int32_t* cam, const int32_t* pt, const float* xy, const int32_t* eoff, int32_t S,

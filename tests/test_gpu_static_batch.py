@@ -89,6 +89,24 @@ def test_static_batch_matches_eager_union(device):
     _check_grads(net, _grads(net), g_ref)
 
 
+def test_native_fill_matches_torch_fill(device):
+    """gasfm_union_fill_scene / _pad + the host-fed global plans write exactly what fill_torch writes
+    (Ns^-1: fp64 inverse vs the fp32 closed form, rtol 1e-5)."""
+    from gasfm_amd.outliers import inject_outliers
+    datas = _scenes(device, (12, 15, 18), seed=4)
+    inputs = [inject_outliers(d, 0.1, log=lambda s: None) for d in datas]
+    st = static_batch.BatchStats(inputs)
+    caps = static_batch.Caps.for_batch(st)
+    a, b = static_batch.StaticBatch(caps, device), static_batch.StaticBatch(caps, device)
+    a.fill(datas, st, inputs)
+    b.fill_torch(datas, st, inputs)
+    for k in ("values", "values_loss", "xy", "indices", "cam32", "pt32", "cam_ptr", "pt_ptr", "perm", "pos",
+              "cam_per_pts", "pts_per_cam", "scene_of_cam", "soc32", "sop32", "items_c", "comb_c", "items_p",
+              "hostfed", "src_v", "src_p"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    torch.testing.assert_close(a.Ns_inv, b.Ns_inv, rtol=1e-5, atol=1e-6)
+
+
 def test_static_trainer_replays_another_batch(device, monkeypatch):
     monkeypatch.setattr(static_batch, "MAX_WASTE", 10.0)  # the second batch reuses the first one's bucket
     torch.manual_seed(2)

@@ -117,6 +117,8 @@ def test_static_batch_structure(small_pieces):
         assert rows[0, 1] == s * P and (rows[1:, 1] == rows[:-1, 1] + rows[:-1, 2]).all()
         assert rows[:, 2].sum() == P
         assert tuple(cs[s]) == (s, S * P + s * caps.NG, caps.NG, 1)
+    # the host-side restatement of the global plans the GPU fill copies in (all views / points valid)
+    assert (sb._host_plans(st, npd) == sb.hostfed.numpy()).all()
     plans = {n: w.plan for n, w in sb.graph_wrappers.items()}
     assert plans["proj2view"].n_slots == caps.I and plans["proj2view"].n_combine == M
     assert plans["scenepoint2global"].n_part_rows == S * P + S * caps.NG
