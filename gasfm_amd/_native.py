@@ -1252,14 +1252,17 @@ _GC_SHADOW = ("W1", "W2", "WA", "WB", "WC", "WD", "WE")  # the weights with an o
 
 class _GChain(ctypes.Structure):
     _fields_ = ([(k, _i32) for k in _GC_DIMS] + [("eps_m", _f32), ("eps_h", _f32)] + [(k, _vp) for k in _GC_W]
-                + [(k + "h", _vp) for k in _GC_SHADOW])
+                + [(k + "h", _vp) for k in _GC_SHADOW] + [("rows", _i32)])
+
+
+GCHAIN_MAX_ROWS = 8  # GASFM_GCHAIN_MAX_ROWS
 
 
 class _GChainGrads(ctypes.Structure):
     _fields_ = [(k, _vp) for k in _GC_D]
 
 
-def gchain_struct(w, eps_m, eps_h, shadows=None):
+def gchain_struct(w, eps_m, eps_h, shadows=None, rows=1):
     """gasfm_gchain of the weights dict w (keys _GC_W; the hub's B..E absent for the last block);
     shadows: dict weight key -> its bf16 shadow (BASELINE config 5) or None."""
     c = _GChain()
@@ -1281,6 +1284,9 @@ def gchain_struct(w, eps_m, eps_h, shadows=None):
             if t.dtype != torch.bfloat16 or not t.is_contiguous() or t.shape != w[k].shape:
                 raise ValueError(f"gchain: the bf16 shadow of {k} must be a contiguous bf16 tensor of its shape")
             setattr(c, k + "h", t.data_ptr())
+    if not 1 <= rows <= GCHAIN_MAX_ROWS:
+        raise ValueError(f"gchain: {rows} rows (1..{GCHAIN_MAX_ROWS})")
+    c.rows = int(rows)
     return c
 
 

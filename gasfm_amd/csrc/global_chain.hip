@@ -49,6 +49,7 @@ constexpr int kMaxK = 2048;           // widest row (G)
 constexpr int kPer = kMaxK / 256;     // row values per thread in the full-row prologues
 constexpr int kMaxProb = 3;
 constexpr int kMaxRaw = 3;
+constexpr int kMaxRows = GASFM_GCHAIN_MAX_ROWS;  // global rows of a union batch per launch
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -129,13 +130,16 @@ struct GnFwdProb {
   int K, N, blk0;
   float eps;
   const uint16_t* Wh;  // bf16 shadow of W (null: W)
+  int rows;            // rows of x / res / y ([rows, K], [rows, N], [rows, N]); 1 for the one-scene chain
 };
 struct GnFwdArgs {
   GnFwdProb p[kMaxProb];
   int nprob;
 };
 
-template <int KI, bool BF>  // float4 per lane of a W row: K <= 256 KI; BF: the bf16 shadows (every problem's)
+// R: the rows of a union batch's global nodes (one per scene, batch.SceneBatch / static_batch), up
+// to R per launch (p.rows of them); each workgroup streams its W rows once for all of them.
+template <int KI, bool BF, int R>  // float4 per lane of a W row: K <= 256 KI; BF: the bf16 shadows (every problem's)
 __global__ __launch_bounds__(kFT) void gnode_fwd_kernel(GnFwdArgs a) {
   __shared__ __attribute__((aligned(16))) float h[kMaxK];
   __shared__ float scratch[8];
@@ -145,6 +149,7 @@ __global__ __launch_bounds__(kFT) void gnode_fwd_kernel(GnFwdArgs a) {
   const GnFwdProb& p = a.p[find_prob(blk0, a.nprob)];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int K = p.K;
+  const int rows = R == 1 ? 1 : p.rows;
   const int i = (int(blockIdx.x) - p.blk0) * (kFT / 64) + wave;
   const int ic = i < p.N ? i : p.N - 1;
   // every load of the kernel first: the wave's W row, the input row and its LayerNorm affine
@@ -166,33 +171,51 @@ __global__ __launch_bounds__(kFT) void gnode_fwd_kernel(GnFwdArgs a) {
     gv[u] = gp[jc];
     bv[u] = bp[jc];
   }
+  float acc[R];
 #pragma unroll
-  for (int u = 0; u < kPer; ++u)
-    if (int(threadIdx.x) + 256 * u >= K) xv[u] = 0.f;
-  if (ln) {
-    float mean, rstd;
-    row_stats(xv, K, p.eps, scratch, mean, rstd);
+  for (int r = 0; r < R; ++r) {
+    acc[r] = 0.f;
+    if (r >= rows) continue;  // uniform
+    if (r > 0) {
+      __syncthreads();  // row r - 1's h consumed
 #pragma unroll
-    for (int u = 0; u < kPer; ++u) {
-      const int j = int(threadIdx.x) + 256 * u;
-      h[j] = j < K ? fmaxf(fmaf((xv[u] - mean) * rstd, gv[u], bv[u]), 0.f) : 0.f;
+      for (int u = 0; u < kPer; ++u) {
+        const int j = int(threadIdx.x) + 256 * u;
+        xv[u] = p.x[int64_t(r) * K + (j < K ? j : 0)];
+      }
     }
-  } else {
 #pragma unroll
-    for (int u = 0; u < kPer; ++u) h[int(threadIdx.x) + 256 * u] = xv[u];
-  }
-  __syncthreads();
-  float acc = 0.f;
+    for (int u = 0; u < kPer; ++u)
+      if (int(threadIdx.x) + 256 * u >= K) xv[u] = 0.f;
+    if (ln) {
+      float mean, rstd;
+      row_stats(xv, K, p.eps, scratch, mean, rstd);
 #pragma unroll
-  for (int u = 0; u < KI; ++u) {
-    const int j = 4 * lane + 256 * u;
-    if (j < kMaxK) {
-      const float4 hv = *reinterpret_cast<const float4*>(h + j);  // 0 past K
-      acc = fmaf(w[u].x, hv.x, fmaf(w[u].y, hv.y, fmaf(w[u].z, hv.z, fmaf(w[u].w, hv.w, acc))));
+      for (int u = 0; u < kPer; ++u) {
+        const int j = int(threadIdx.x) + 256 * u;
+        h[j] = j < K ? fmaxf(fmaf((xv[u] - mean) * rstd, gv[u], bv[u]), 0.f) : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) h[int(threadIdx.x) + 256 * u] = xv[u];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < KI; ++u) {
+      const int j = 4 * lane + 256 * u;
+      if (j < kMaxK) {
+        const float4 hv = *reinterpret_cast<const float4*>(h + j);  // 0 past K
+        acc[r] = fmaf(w[u].x, hv.x, fmaf(w[u].y, hv.y, fmaf(w[u].z, hv.z, fmaf(w[u].w, hv.w, acc[r]))));
+      }
     }
   }
-  acc = wave_sum(acc);
-  if (lane == 0 && i < p.N) p.y[i] = acc + (p.b ? p.b[i] : 0.f) + (p.res ? p.res[i] : 0.f);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (r >= rows) continue;
+    const float v = wave_sum(acc[r]);
+    if (lane == 0 && i < p.N)
+      p.y[int64_t(r) * p.N + i] = v + (p.b ? p.b[i] : 0.f) + (p.res ? p.res[int64_t(r) * p.N + i] : 0.f);
+  }
 }
 
 int launch_fwd(GnFwdArgs& a, hipStream_t st) {
@@ -205,18 +228,24 @@ int launch_fwd(GnFwdArgs& a, hipStream_t st) {
   for (int q = a.nprob; q < kMaxProb; ++q) a.p[q].blk0 = blocks;
   bool bf = true;  // the bf16 kernels when every problem has its shadow (no per-load branch)
   for (int q = 0; q < a.nprob; ++q) bf = bf && a.p[q].Wh != nullptr;
-  auto go = [&](auto k32, auto k16) {
-    const auto kern = bf ? k16 : k32;
+  const int rows = a.p[0].rows;
+  auto go = [&](auto k32, auto k16, auto m32, auto m16) {
+    const auto kern = rows > 1 ? (bf ? m16 : m32) : (bf ? k16 : k32);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(kFT), 0, st, a);
   };
+  constexpr int RM = kMaxRows;
   if (kmax <= 256)
-    go(&gnode_fwd_kernel<1, false>, &gnode_fwd_kernel<1, true>);
+    go(&gnode_fwd_kernel<1, false, 1>, &gnode_fwd_kernel<1, true, 1>, &gnode_fwd_kernel<1, false, RM>,
+       &gnode_fwd_kernel<1, true, RM>);
   else if (kmax <= 1024)
-    go(&gnode_fwd_kernel<4, false>, &gnode_fwd_kernel<4, true>);
+    go(&gnode_fwd_kernel<4, false, 1>, &gnode_fwd_kernel<4, true, 1>, &gnode_fwd_kernel<4, false, RM>,
+       &gnode_fwd_kernel<4, true, RM>);
   else if (kmax <= 1280)
-    go(&gnode_fwd_kernel<5, false>, &gnode_fwd_kernel<5, true>);
+    go(&gnode_fwd_kernel<5, false, 1>, &gnode_fwd_kernel<5, true, 1>, &gnode_fwd_kernel<5, false, RM>,
+       &gnode_fwd_kernel<5, true, RM>);
   else
-    go(&gnode_fwd_kernel<8, false>, &gnode_fwd_kernel<8, true>);
+    go(&gnode_fwd_kernel<8, false, 1>, &gnode_fwd_kernel<8, true, 1>, &gnode_fwd_kernel<8, false, RM>,
+       &gnode_fwd_kernel<8, true, RM>);
   return launch_status("gasfm_gchain_fwd");
 }
 
@@ -242,6 +271,9 @@ struct GnBwdProb {
   float* stats;      // (mean, rstd) of x, written by slab 0 (null: not needed)
   int lnfin;
   const uint16_t* Wh;  // bf16 shadow of W (null: W)
+  // rows > 1 (a union batch's global nodes): dy / x / dh are [rows, N] / [rows, K] / [rows, K],
+  // ws [chunks, rows, K], lnp [rows, slabs, 2], stats [rows, 2]; dW, db, dgam, dbet sum the rows
+  int rows;
 };
 // The launch's prologue (the previous level's LayerNorm backward, finished per row here):
 //   dy[n] = dres[n] + sum_q rstd (gv_q[n] - S1_q / F - xh[n] S2_q / F),  xh = (x - mean) rstd,
@@ -253,7 +285,7 @@ struct GnPro {
   const float* x;
   const float* dres;   // or null
   float* out;          // or null: dy rows written by the slab-0 workgroups (d prev)
-  int nq, F, slabs;
+  int nq, F, slabs;     // rows > 1: gv / x / dres / out are [rows, F], lnp [rows, slabs, 2], stats [rows, 2]
 };
 struct GnBwdArgs {
   GnBwdProb p[kMaxProb];
@@ -272,18 +304,20 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int RPT, bool BF>  // rows per thread: a chunk is 32 RPT rows; BF: the bf16 shadows
+template <int RPT, bool BF, int R>  // rows per thread: a chunk is 32 RPT rows; BF: the bf16 shadows;
+                                     // R: global rows per launch (p.rows of them)
 __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
   static_assert(32 * RPT == kBT, "one dy row per thread");
-  __shared__ float dys[32 * RPT];
+  __shared__ float dys[R][32 * RPT];
   __shared__ float4 red[kBT];
-  __shared__ float scratch[4 * 2 * kMaxRaw + 8];
+  __shared__ float scratch[4 * 2 * kMaxRaw * R + 8];
   __shared__ uint32_t flag;
   int blk0[kMaxProb];
 #pragma unroll
   for (int q = 0; q < kMaxProb; ++q) blk0[q] = a.p[q].blk0;
   const int pi = find_prob(blk0, a.nprob);
   const GnBwdProb& p = a.p[pi];
+  const int rows = R == 1 ? 1 : p.rows;
   const int local = int(blockIdx.x) - p.blk0;
   const int slab = local % p.slabs, chunk = local / p.slabs;
   const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
@@ -294,33 +328,47 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
   const GnPro& pr = a.pro;
   const bool pro = pr.nq > 0;
   // 1. every load first: the prologue's operands (they gate dy), the workgroup's W slab rows, the
-  // input row (+ affine)
-  float dres = 0.f, xr = 0.f, gvr[kMaxRaw], lp[2 * kMaxRaw], st0 = 0.f, st1 = 0.f, dyv = 0.f;
-  if (pro) {
-    dres = pr.dres ? pr.dres[nrc] : 0.f;
-    xr = pr.x[nrc];
-    st0 = pr.stats[0];
-    st1 = pr.stats[1];
-    const int tc = int(threadIdx.x) < pr.slabs ? int(threadIdx.x) : 0;
+  // input rows (+ affine)
+  float dres[R], xr[R], gvr[R][kMaxRaw], lp[R * 2 * kMaxRaw], st0[R], st1[R], dyv[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    dres[r] = xr[r] = st0[r] = st1[r] = dyv[r] = 0.f;
 #pragma unroll
     for (int q = 0; q < kMaxRaw; ++q) {
-      const bool on = q < pr.nq;
-      gvr[q] = on ? pr.gv[q][nrc] : 0.f;
-      lp[2 * q] = on ? pr.lnp[q][2 * tc] : 0.f;
-      lp[2 * q + 1] = on ? pr.lnp[q][2 * tc + 1] : 0.f;
+      gvr[r][q] = 0.f;
+      lp[(r * kMaxRaw + q) * 2] = lp[(r * kMaxRaw + q) * 2 + 1] = 0.f;
     }
-  } else {
-    dyv = p.dy[nrc];
+    if (r >= rows) continue;
+    if (pro) {
+      const int64_t ro = int64_t(r) * pr.F;
+      dres[r] = pr.dres ? pr.dres[ro + nrc] : 0.f;
+      xr[r] = pr.x[ro + nrc];
+      st0[r] = pr.stats[2 * r];
+      st1[r] = pr.stats[2 * r + 1];
+      const int tc = int(threadIdx.x) < pr.slabs ? int(threadIdx.x) : 0;
+#pragma unroll
+      for (int q = 0; q < kMaxRaw; ++q) {
+        const bool on = q < pr.nq;
+        gvr[r][q] = on ? pr.gv[q][ro + nrc] : 0.f;
+        const int64_t lo = (int64_t(r) * pr.slabs + tc) * 2;
+        lp[(r * kMaxRaw + q) * 2] = on ? pr.lnp[q][lo] : 0.f;
+        lp[(r * kMaxRaw + q) * 2 + 1] = on ? pr.lnp[q][lo + 1] : 0.f;
+      }
+    } else {
+      dyv[r] = p.dy[int64_t(r) * N + nrc];
+    }
   }
   float4 w[RPT];
 #pragma unroll
-  for (int r = 0; r < RPT; ++r) {
-    const int n = row0 + rl + 32 * r;
-    w[r] = w4<BF>(p.W, p.Wh, int64_t(n < N ? n : N - 1) * K + col);
+  for (int k = 0; k < RPT; ++k) {
+    const int n = row0 + rl + 32 * k;
+    w[k] = w4<BF>(p.W, p.Wh, int64_t(n < N ? n : N - 1) * K + col);
   }
-  const float4 x4 = *reinterpret_cast<const float4*>(p.x + col);
+  float4 x4[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) x4[r] = *reinterpret_cast<const float4*>(p.x + int64_t(r < rows ? r : 0) * K + col);
   const bool ln = p.gam != nullptr;
-  float4 g4 = x4, b4 = x4;
+  float4 g4 = x4[0], b4 = x4[0];
   float xv[kPer];
   if (ln) {
     g4 = *reinterpret_cast<const float4*>(p.gam + col);
@@ -338,69 +386,111 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
   if (pro) {
     if (int(threadIdx.x) >= pr.slabs) {
 #pragma unroll
-      for (int k = 0; k < 2 * kMaxRaw; ++k) lp[k] = 0.f;
+      for (int k = 0; k < R * 2 * kMaxRaw; ++k) lp[k] = 0.f;
     }
-    block_sums<2 * kMaxRaw>(lp, scratch);
-    const float xh = (xr - st0) * st1, invF = 1.f / pr.F;
-    float d = dres;
+    block_sums<R * 2 * kMaxRaw>(lp, scratch);
+    const float invF = 1.f / pr.F;
 #pragma unroll
-    for (int q = 0; q < kMaxRaw; ++q)
-      if (q < pr.nq) d += st1 * (gvr[q] - lp[2 * q] * invF - xh * lp[2 * q + 1] * invF);
-    dyv = d;
-    if (slab == 0 && pr.out && nrow < N) pr.out[nrow] = d;
+    for (int r = 0; r < R; ++r) {
+      if (r >= rows) continue;
+      const float xh = (xr[r] - st0[r]) * st1[r];
+      float d = dres[r];
+#pragma unroll
+      for (int q = 0; q < kMaxRaw; ++q)
+        if (q < pr.nq)
+          d += st1[r] * (gvr[r][q] - lp[(r * kMaxRaw + q) * 2] * invF - xh * lp[(r * kMaxRaw + q) * 2 + 1] * invF);
+      dyv[r] = d;
+      if (slab == 0 && pr.out && nrow < N) pr.out[int64_t(r) * pr.F + nrow] = d;
+    }
   }
-  dys[threadIdx.x] = nrow < N ? dyv : 0.f;
-  // 3. h over the thread's 4 slab columns
-  float4 h4 = x4, xh4 = x4;
-  float mean = 0.f, rstd = 0.f;
-  if (ln) {
-    __syncthreads();  // the prologue's block_sums scratch before row_stats reuses it
-    row_stats(xv, K, p.eps, scratch, mean, rstd);
-    xh4 = make_float4((x4.x - mean) * rstd, (x4.y - mean) * rstd, (x4.z - mean) * rstd, (x4.w - mean) * rstd);
-    h4 = make_float4(fmaxf(fmaf(xh4.x, g4.x, b4.x), 0.f), fmaxf(fmaf(xh4.y, g4.y, b4.y), 0.f),
-                     fmaxf(fmaf(xh4.z, g4.z, b4.z), 0.f), fmaxf(fmaf(xh4.w, g4.w, b4.w), 0.f));
+#pragma unroll
+  for (int r = 0; r < R; ++r) dys[r][threadIdx.x] = (nrow < N && r < rows) ? dyv[r] : 0.f;
+  // 3. h over the thread's 4 slab columns, per row
+  float4 h4[R], xh4[R];
+  float mean[R], rstd[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    h4[r] = xh4[r] = x4[r];
+    mean[r] = rstd[r] = 0.f;
+    if (ln && r < rows) {
+      if (r > 0) {
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+          const int j = int(threadIdx.x) + 256 * u;
+          xv[u] = j < K ? p.x[int64_t(r) * K + j] : 0.f;
+        }
+      }
+      __syncthreads();  // the prologue's / the previous row's block_sums scratch before row_stats reuses it
+      row_stats(xv, K, p.eps, scratch, mean[r], rstd[r]);
+      const float4 xx = x4[r];
+      xh4[r] = make_float4((xx.x - mean[r]) * rstd[r], (xx.y - mean[r]) * rstd[r], (xx.z - mean[r]) * rstd[r],
+                           (xx.w - mean[r]) * rstd[r]);
+      h4[r] = make_float4(fmaxf(fmaf(xh4[r].x, g4.x, b4.x), 0.f), fmaxf(fmaf(xh4[r].y, g4.y, b4.y), 0.f),
+                          fmaxf(fmaf(xh4[r].z, g4.z, b4.z), 0.f), fmaxf(fmaf(xh4[r].w, g4.w, b4.w), 0.f));
+    }
   }
   __syncthreads();  // dys
-  // 4. this thread's share of dh (the dW rows are stored last: a ticket's s_waitcnt vmcnt(0)
-  // would otherwise wait for them too)
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  float dr[RPT];
-#pragma unroll
-  for (int r = 0; r < RPT; ++r) {
-    const float d = dys[rl + 32 * r];  // 0 past N
-    dr[r] = d;
-    s.x = fmaf(d, w[r].x, s.x);
-    s.y = fmaf(d, w[r].y, s.y);
-    s.z = fmaf(d, w[r].z, s.z);
-    s.w = fmaf(d, w[r].w, s.w);
-  }
   auto store_dw = [&]() {
 #pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-      const int n = row0 + rl + 32 * r;
-      const float d = dr[r];
-      if (n < N)
-        *reinterpret_cast<float4*>(p.dW + int64_t(n) * K + col) = make_float4(d * h4.x, d * h4.y, d * h4.z, d * h4.w);
+    for (int k = 0; k < RPT; ++k) {
+      const int n = row0 + rl + 32 * k;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r >= rows) continue;
+        const float d = dys[r][rl + 32 * k];
+        v.x = fmaf(d, h4[r].x, v.x);
+        v.y = fmaf(d, h4[r].y, v.y);
+        v.z = fmaf(d, h4[r].z, v.z);
+        v.w = fmaf(d, h4[r].w, v.w);
+      }
+      if (n < N) *reinterpret_cast<float4*>(p.dW + int64_t(n) * K + col) = v;
     }
-    if (p.db && slab == 0 && nrow < N) p.db[nrow] = dys[threadIdx.x];
+    if (p.db && slab == 0 && nrow < N) {
+      float v = 0.f;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (r < rows) v += dys[r][threadIdx.x];
+      p.db[nrow] = v;
+    }
   };
-  // 5. the 32 row lanes summed in lane order
-  red[threadIdx.x] = s;
-  __syncthreads();
-  float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (threadIdx.x < 8) {
+  // 4. + 5. this thread's share of dh per row (the dW rows are stored last: a ticket's s_waitcnt
+  // vmcnt(0) would otherwise wait for them too), the 32 row lanes summed in lane order
+  float4 tot[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    tot[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r >= rows) continue;
+    float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const float d = dys[r][rl + 32 * k];  // 0 past N
+      sv.x = fmaf(d, w[k].x, sv.x);
+      sv.y = fmaf(d, w[k].y, sv.y);
+      sv.z = fmaf(d, w[k].z, sv.z);
+      sv.w = fmaf(d, w[k].w, sv.w);
+    }
+    if (r > 0) __syncthreads();  // red of row r - 1 read
+    red[threadIdx.x] = sv;
+    __syncthreads();
+    if (threadIdx.x < 8) {
 #pragma unroll 8
-    for (int l = 0; l < 32; ++l) {
-      const float4 v = red[l * 8 + threadIdx.x];
-      tot.x += v.x;
-      tot.y += v.y;
-      tot.z += v.z;
-      tot.w += v.w;
+      for (int l = 0; l < 32; ++l) {
+        const float4 v = red[l * 8 + threadIdx.x];
+        tot[r].x += v.x;
+        tot[r].y += v.y;
+        tot[r].z += v.z;
+        tot[r].w += v.w;
+      }
     }
   }
   if (p.chunks > 1) {
-    // 6. the chunk partial to the slab's last arriver (write-through stores, one ticket)
-    if (threadIdx.x < 8) st_sc1(p.ws + int64_t(chunk) * K + col, tot);
+    // 6. the chunk partials to the slab's last arriver (write-through stores, one ticket)
+    if (threadIdx.x < 8) {
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (r < rows) st_sc1(p.ws + (int64_t(chunk) * rows + r) * K + col, tot[r]);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -415,57 +505,70 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (threadIdx.x < 8) {
       constexpr int MAXC = 16;
-      float4 v[MAXC];
 #pragma unroll
-      for (int ch = 0; ch < MAXC; ++ch) {
-        const float* q = p.ws + int64_t(ch < p.chunks ? ch : 0) * K + col;
-        v[ch] = make_float4(ld_sc1(q), ld_sc1(q + 1), ld_sc1(q + 2), ld_sc1(q + 3));
-      }
-      tot = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int r = 0; r < R; ++r) {
+        if (r >= rows) continue;
+        float4 v[MAXC];
 #pragma unroll
-      for (int ch = 0; ch < MAXC; ++ch)
-        if (ch < p.chunks) {
-          tot.x += v[ch].x;
-          tot.y += v[ch].y;
-          tot.z += v[ch].z;
-          tot.w += v[ch].w;
+        for (int ch = 0; ch < MAXC; ++ch) {
+          const float* q = p.ws + (int64_t(ch < p.chunks ? ch : 0) * rows + r) * K + col;
+          v[ch] = make_float4(ld_sc1(q), ld_sc1(q + 1), ld_sc1(q + 2), ld_sc1(q + 3));
         }
+        tot[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int ch = 0; ch < MAXC; ++ch)
+          if (ch < p.chunks) {
+            tot[r].x += v[ch].x;
+            tot[r].y += v[ch].y;
+            tot[r].z += v[ch].z;
+            tot[r].w += v[ch].w;
+          }
+      }
     }
     if (threadIdx.x == 0) __hip_atomic_store(p.cnt + slab, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // 7. the slab's final dh, or its columns of the LayerNorm backward of x
   if (threadIdx.x < 8) {
     if (p.lnfin) {
-      const float t4[4] = {tot.x, tot.y, tot.z, tot.w};
-      const float xh[4] = {xh4.x, xh4.y, xh4.z, xh4.w};
       const float gg[4] = {g4.x, g4.y, g4.z, g4.w};
       const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
-      float d[4], gv[4], s1 = 0.f, s2 = 0.f;
+      float dg[4] = {0.f, 0.f, 0.f, 0.f}, db[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        d[k] = fmaf(xh[k], gg[k], bb[k]) > 0.f ? t4[k] : 0.f;
-        gv[k] = d[k] * gg[k];
-        s1 += gv[k];
-        s2 = fmaf(gv[k], xh[k], s2);
-      }
-      *reinterpret_cast<float4*>(p.dh + col) = make_float4(gv[0], gv[1], gv[2], gv[3]);
-      *reinterpret_cast<float4*>(p.dgam + col) = make_float4(d[0] * xh[0], d[1] * xh[1], d[2] * xh[2], d[3] * xh[3]);
-      *reinterpret_cast<float4*>(p.dbet + col) = make_float4(d[0], d[1], d[2], d[3]);
+      for (int r = 0; r < R; ++r) {
+        if (r >= rows) continue;
+        const float t4[4] = {tot[r].x, tot[r].y, tot[r].z, tot[r].w};
+        const float xh[4] = {xh4[r].x, xh4[r].y, xh4[r].z, xh4[r].w};
+        float d[4], gv[4], s1 = 0.f, s2 = 0.f;
 #pragma unroll
-      for (int o = 1; o < 8; o <<= 1) {
-        s1 += __shfl_xor(s1, o);
-        s2 += __shfl_xor(s2, o);
-      }
-      if (threadIdx.x == 0) {
-        p.lnp[2 * slab] = s1;
-        p.lnp[2 * slab + 1] = s2;
-        if (slab == 0 && p.stats) {
-          p.stats[0] = mean;
-          p.stats[1] = rstd;
+        for (int k = 0; k < 4; ++k) {
+          d[k] = fmaf(xh[k], gg[k], bb[k]) > 0.f ? t4[k] : 0.f;
+          gv[k] = d[k] * gg[k];
+          s1 += gv[k];
+          s2 = fmaf(gv[k], xh[k], s2);
+          dg[k] = fmaf(d[k], xh[k], dg[k]);
+          db[k] += d[k];
+        }
+        *reinterpret_cast<float4*>(p.dh + int64_t(r) * K + col) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+          s1 += __shfl_xor(s1, o);
+          s2 += __shfl_xor(s2, o);
+        }
+        if (threadIdx.x == 0) {
+          p.lnp[(int64_t(r) * p.slabs + slab) * 2] = s1;
+          p.lnp[(int64_t(r) * p.slabs + slab) * 2 + 1] = s2;
+          if (slab == 0 && p.stats) {
+            p.stats[2 * r] = mean[r];
+            p.stats[2 * r + 1] = rstd[r];
+          }
         }
       }
+      *reinterpret_cast<float4*>(p.dgam + col) = make_float4(dg[0], dg[1], dg[2], dg[3]);
+      *reinterpret_cast<float4*>(p.dbet + col) = make_float4(db[0], db[1], db[2], db[3]);
     } else {
-      *reinterpret_cast<float4*>(p.dh + col) = tot;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (r < rows) *reinterpret_cast<float4*>(p.dh + int64_t(r) * K + col) = tot[r];
     }
   }
   store_dw();
@@ -475,8 +578,8 @@ constexpr int kRPT = 8;  // 256 rows per chunk
 
 int chunks_of(int N) { return (N + 32 * kRPT - 1) / (32 * kRPT); }
 
-// fills blk0 / slabs / chunks / ws / cnt of the level's problems; ws and cnt advance
-int launch_bwd(GnBwdArgs& a, float*& ws, uint32_t*& cnt, hipStream_t st, const char* where) {
+// fills blk0 / slabs / chunks / ws / cnt / rows of the level's problems; ws and cnt advance
+int launch_bwd(GnBwdArgs& a, int rows, float*& ws, uint32_t*& cnt, hipStream_t st, const char* where) {
   int blocks = 0;
   for (int q = 0; q < a.nprob; ++q) {
     GnBwdProb& p = a.p[q];
@@ -485,17 +588,21 @@ int launch_bwd(GnBwdArgs& a, float*& ws, uint32_t*& cnt, hipStream_t st, const c
     p.chunks = chunks_of(p.N);
     p.ws = ws;
     p.cnt = cnt;
-    ws += int64_t(p.chunks) * p.K;
+    p.rows = rows;
+    ws += int64_t(p.chunks) * rows * p.K;
     cnt += p.slabs;
     blocks += p.slabs * p.chunks;
   }
   for (int q = a.nprob; q < kMaxProb; ++q) a.p[q].blk0 = blocks;
   bool bf = true;
   for (int q = 0; q < a.nprob; ++q) bf = bf && a.p[q].Wh != nullptr;
-  const auto kern = bf ? &gnode_bwd_kernel<kRPT, true> : &gnode_bwd_kernel<kRPT, false>;
+  const auto kern = rows > 1 ? (bf ? &gnode_bwd_kernel<kRPT, true, kMaxRows> : &gnode_bwd_kernel<kRPT, false, kMaxRows>)
+                             : (bf ? &gnode_bwd_kernel<kRPT, true, 1> : &gnode_bwd_kernel<kRPT, false, 1>);
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBT), 0, st, a);
   return launch_status(where);
 }
+
+int rows_of(const gasfm_gchain* c) { return c->rows > 1 ? c->rows : 1; }
 
 bool hub_on(const gasfm_gchain* c) { return c->NB > 0; }
 
@@ -519,6 +626,7 @@ static int gchain_check(const gasfm_gchain* c) {
                       c->bE,
                   "gasfm_gchain: null hub weight");
   }
+  GASFM_REQUIRE(c->rows >= 0 && c->rows <= kMaxRows, "gasfm_gchain: rows=%d (<= %d)", c->rows, kMaxRows);
   const void* ws[] = {c->W1, c->W2, c->WA, c->WB, c->WC, c->WD, c->WE};
   for (const void* p : ws) GASFM_REQUIRE(!p || aligned16(p), "gasfm_gchain: weights must be 16-byte aligned");
   const void* wh[] = {c->W1h, c->W2h, c->WAh, c->WBh, c->WCh, c->WDh, c->WEh};
@@ -531,13 +639,14 @@ extern "C" int64_t gasfm_gchain_scratch_floats(const gasfm_gchain* c) {
   if (!c) return 0;
   // vectors: dh_D, dh_E, gv_A, gv_B, gv_C, gv_2; LayerNorm row-sum partials and statistics; chunk
   // partials of every level (each level its own range)
+  const int64_t R = rows_of(c);
   const int64_t vec = int64_t(c->NB) + c->NC + 4 * int64_t(c->G);
   const int64_t lnp = 4 * 2 * int64_t(c->G / kSW) + 8;
   const int64_t l1 = int64_t(chunks_of(c->ND)) * c->NB + int64_t(chunks_of(c->NE)) * c->NC;
   const int64_t l2 = int64_t(chunks_of(c->NA) + chunks_of(c->NB) + chunks_of(c->NC)) * c->G;
   const int64_t l3 = int64_t(chunks_of(c->G)) * c->G;
   const int64_t l4 = int64_t(chunks_of(c->G)) * c->Kc;
-  return vec + lnp + l1 + l2 + l3 + l4 + 64;
+  return R * (vec + lnp + l1 + l2 + l3 + l4 + c->G) + 64;
 }
 
 extern "C" int32_t gasfm_gchain_counters(const gasfm_gchain* c) {
@@ -551,25 +660,26 @@ extern "C" int gasfm_gchain_fwd(const gasfm_gchain* c, const float* xcat, const 
   if (s0 != GASFM_OK) return s0;
   GASFM_REQUIRE(xcat && x1 && g && sg && (!hub_on(c) || (xv && xp && xrv && xrp)), "gasfm_gchain_fwd: null output");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int R = rows_of(c);
   GnFwdArgs a{};
   a.nprob = 1;
-  a.p[0] = GnFwdProb{xcat, nullptr, nullptr, c->W1, c->b1, prev, x1, c->Kc, c->G, 0, 0.f, c->W1h};
+  a.p[0] = GnFwdProb{xcat, nullptr, nullptr, c->W1, c->b1, prev, x1, c->Kc, c->G, 0, 0.f, c->W1h, R};
   int s = launch_fwd(a, st);
   if (s != GASFM_OK) return s;
-  a.p[0] = GnFwdProb{x1, c->gM, c->bM, c->W2, c->b2, x1, g, c->G, c->G, 0, c->eps_m, c->W2h};
+  a.p[0] = GnFwdProb{x1, c->gM, c->bM, c->W2, c->b2, x1, g, c->G, c->G, 0, c->eps_m, c->W2h, R};
   s = launch_fwd(a, st);
   if (s != GASFM_OK) return s;
-  a.p[0] = GnFwdProb{g, c->gA, c->bA, c->WA, nullptr, nullptr, sg, c->G, c->NA, 0, c->eps_h, c->WAh};
+  a.p[0] = GnFwdProb{g, c->gA, c->bA, c->WA, nullptr, nullptr, sg, c->G, c->NA, 0, c->eps_h, c->WAh, R};
   if (hub_on(c)) {
     a.nprob = 3;
-    a.p[1] = GnFwdProb{g, c->gB, c->bB, c->WB, c->bWB, nullptr, xv, c->G, c->NB, 0, c->eps_h, c->WBh};
-    a.p[2] = GnFwdProb{g, c->gC, c->bC, c->WC, c->bWC, nullptr, xp, c->G, c->NC, 0, c->eps_h, c->WCh};
+    a.p[1] = GnFwdProb{g, c->gB, c->bB, c->WB, c->bWB, nullptr, xv, c->G, c->NB, 0, c->eps_h, c->WBh, R};
+    a.p[2] = GnFwdProb{g, c->gC, c->bC, c->WC, c->bWC, nullptr, xp, c->G, c->NC, 0, c->eps_h, c->WCh, R};
   }
   s = launch_fwd(a, st);
   if (s != GASFM_OK || !hub_on(c)) return s;
   a.nprob = 2;
-  a.p[0] = GnFwdProb{xv, nullptr, nullptr, c->WD, c->bD, nullptr, xrv, c->NB, c->ND, 0, 0.f, c->WDh};
-  a.p[1] = GnFwdProb{xp, nullptr, nullptr, c->WE, c->bE, nullptr, xrp, c->NC, c->NE, 0, 0.f, c->WEh};
+  a.p[0] = GnFwdProb{xv, nullptr, nullptr, c->WD, c->bD, nullptr, xrv, c->NB, c->ND, 0, 0.f, c->WDh, R};
+  a.p[1] = GnFwdProb{xp, nullptr, nullptr, c->WE, c->bE, nullptr, xrp, c->NC, c->NE, 0, 0.f, c->WEh, R};
   return launch_fwd(a, st);
 }
 
@@ -589,19 +699,21 @@ extern "C" int gasfm_gchain_bwd(const gasfm_gchain* c, const float* xcat, const 
                   "gasfm_gchain_bwd: null hub pointer");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int slabsG = c->G / kSW;
+  const int R = rows_of(c);  // every vector below is [R, len]
   float* dhD = scratch;
-  float* dhE = dhD + c->NB;
-  float* gvA = dhE + c->NC;
-  float* gvB = gvA + c->G;
-  float* gvC = gvB + c->G;
-  float* gv2 = gvC + c->G;
-  float* lnA = gv2 + c->G;  // [slabsG][2] each
-  float* lnB = lnA + 2 * slabsG;
-  float* lnC = lnB + 2 * slabsG;
-  float* ln2 = lnC + 2 * slabsG;
-  float* stg = ln2 + 2 * slabsG;  // (mean, rstd) of g, then of x1
-  float* st1 = stg + 2;
-  float* ws = stg + 8;
+  float* dhE = dhD + int64_t(R) * c->NB;
+  float* gvA = dhE + int64_t(R) * c->NC;
+  float* gvB = gvA + int64_t(R) * c->G;
+  float* gvC = gvB + int64_t(R) * c->G;
+  float* gv2 = gvC + int64_t(R) * c->G;
+  float* lnA = gv2 + int64_t(R) * c->G;  // [R][slabsG][2] each
+  float* lnB = lnA + 2 * R * slabsG;
+  float* lnC = lnB + 2 * R * slabsG;
+  float* ln2 = lnC + 2 * R * slabsG;
+  float* stg = ln2 + 2 * R * slabsG;  // [R][2] (mean, rstd) of g, then of x1
+  float* st1 = stg + 2 * R;
+  float* dgr = st1 + 2 * R + 4;  // [R][G] dg per row (B3's dy; with one row it equals db2)
+  float* ws = dgr + int64_t(R) * c->G;
   uint32_t* cnt = counters;
   int s;
   if (hub) {  // B1: the two lin_r rows
@@ -611,7 +723,7 @@ extern "C" int gasfm_gchain_bwd(const gasfm_gchain* c, const float* xcat, const 
     a.p[0].K = c->NB, a.p[0].N = c->ND, a.p[0].Wh = c->WDh;
     a.p[1] = GnBwdProb{dxrp, xp, nullptr, nullptr, c->WE, d->dWE, d->dbE, dhE};
     a.p[1].K = c->NC, a.p[1].N = c->NE, a.p[1].Wh = c->WEh;
-    s = launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(lin_r)");
+    s = launch_bwd(a, R, ws, cnt, st, "gasfm_gchain_bwd(lin_r)");
     if (s != GASFM_OK) return s;
   }
   {  // B2: the LayerNorm -> Linear consumers of g; each slab's last arriver runs its columns of
@@ -630,7 +742,7 @@ extern "C" int gasfm_gchain_bwd(const gasfm_gchain* c, const float* xcat, const 
       a.p[1] = lnprob(dhD, c->gB, c->bB, c->WB, c->WBh, d->dWB, d->dbWB, c->NB, gvB, d->dgB, d->dbB, lnB, nullptr);
       a.p[2] = lnprob(dhE, c->gC, c->bC, c->WC, c->WCh, d->dWC, d->dbWC, c->NC, gvC, d->dgC, d->dbC, lnC, nullptr);
     }
-    s = launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(hub)");
+    s = launch_bwd(a, R, ws, cnt, st, "gasfm_gchain_bwd(hub)");
     if (s != GASFM_OK) return s;
   }
   {  // B3: the MLP Linear on dg (= dskip + the hub LayerNorms' backward, finished per row in the
@@ -646,8 +758,8 @@ extern "C" int gasfm_gchain_bwd(const gasfm_gchain* c, const float* xcat, const 
     pr.gv[0] = gvA, pr.lnp[0] = lnA;
     pr.gv[1] = gvB, pr.lnp[1] = lnB;
     pr.gv[2] = gvC, pr.lnp[2] = lnC;
-    pr.stats = stg, pr.x = g, pr.dres = dskip, pr.out = nullptr, pr.F = c->G, pr.slabs = slabsG;
-    s = launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(mlp)");
+    pr.stats = stg, pr.x = g, pr.dres = dskip, pr.out = R > 1 ? dgr : nullptr, pr.F = c->G, pr.slabs = slabsG;
+    s = launch_bwd(a, R, ws, cnt, st, "gasfm_gchain_bwd(mlp)");
     if (s != GASFM_OK) return s;
   }
   // B4: proj_view_and_scenepoint2global on dx1 = dg + LN_M backward (prologue; = d b1 = d prev)
@@ -658,6 +770,6 @@ extern "C" int gasfm_gchain_bwd(const gasfm_gchain* c, const float* xcat, const 
   GnPro& pr = a.pro;
   pr.nq = 1;
   pr.gv[0] = gv2, pr.lnp[0] = ln2;
-  pr.stats = st1, pr.x = x1, pr.dres = d->db2, pr.out = dprev, pr.F = c->G, pr.slabs = slabsG;
-  return launch_bwd(a, ws, cnt, st, "gasfm_gchain_bwd(proj)");
+  pr.stats = st1, pr.x = x1, pr.dres = R > 1 ? dgr : d->db2, pr.out = dprev, pr.F = c->G, pr.slabs = slabsG;
+  return launch_bwd(a, R, ws, cnt, st, "gasfm_gchain_bwd(proj)");
 }

@@ -236,9 +236,11 @@ class GlobalChainFn(torch.autograd.Function):
     two lin_r rows of its global convs.  Replaces the linear_res / ln_relu_linear GlobalLinearFns
     and GlobalHubFn (12 backward launches per block, each GEMV followed by a one-workgroup finish).
 
-    apply(xcat [1, Kc], prev [1, G] or None, *weights (_GC_W order; the hub's B..E None for the last
-    block), eps_m, eps_h, bf16) -> (g, SG, XRv, XRp), or (g, SG) without the hub.  bf16: the GEMVs read
-    the weights' bf16 shadows (weight_shadow; BASELINE config 5), fp32 accumulation and gradients."""
+    apply(xcat [R, Kc], prev [R, G] or None, *weights (_GC_W order; the hub's B..E None for the last
+    block), eps_m, eps_h, bf16) -> (g, SG, XRv, XRp), or (g, SG) without the hub, each [R, .].  R <= 8
+    rows: a union batch's global nodes (one per scene), every weight streamed once for all of them.
+    bf16: the GEMVs read the weights' bf16 shadows (weight_shadow; BASELINE config 5), fp32
+    accumulation and gradients."""
 
     @staticmethod
     def forward(ctx, xcat, prev, *args):
@@ -246,16 +248,17 @@ class GlobalChainFn(torch.autograd.Function):
         ws, eps_m, eps_h, bf16 = args[:-3], args[-3], args[-2], args[-1]
         w = {k: (t.contiguous() if t is not None else None) for k, t in zip(_GC_W, ws)}
         sh = {k: weight_shadow(w[k]) for k in _native._GC_SHADOW if w[k] is not None} if bf16 else None
-        c = _native.gchain_struct(w, eps_m, eps_h, sh)
+        R = xcat.shape[0]
+        c = _native.gchain_struct(w, eps_m, eps_h, sh, rows=R)
         hub = w["WB"] is not None
         f = dict(dtype=torch.float32, device=xcat.device)
-        x1c = xcat.reshape(-1).contiguous()
-        pv = prev.reshape(-1).contiguous() if prev is not None else None
+        x1c = xcat.contiguous()
+        pv = prev.reshape(R, -1).contiguous() if prev is not None else None
         G = c.G
-        x1, g, sg = torch.empty(G, **f), torch.empty(G, **f), torch.empty(c.NA, **f)
+        x1, g, sg = torch.empty(R, G, **f), torch.empty(R, G, **f), torch.empty(R, c.NA, **f)
         xv = xp = xrv = xrp = None
         if hub:
-            xv, xp, xrv, xrp = (torch.empty(n, **f) for n in (c.NB, c.NC, c.ND, c.NE))
+            xv, xp, xrv, xrp = (torch.empty(R, n, **f) for n in (c.NB, c.NC, c.ND, c.NE))
         _native.gchain_fwd(c, x1c, pv, x1, g, sg, xv, xp, xrv, xrp)
         ctx.save_for_backward(x1c, x1, g, xv, xp, *(w[k] for k in _GC_W))
         ctx.eps = (eps_m, eps_h)
@@ -264,25 +267,26 @@ class GlobalChainFn(torch.autograd.Function):
         ctx.shapes = (xcat.shape, prev.shape if prev is not None else None)
         ctx.set_materialize_grads(False)
         if hub:
-            return g.view(1, G), sg.view(1, -1), xrv.view(1, -1), xrp.view(1, -1)
-        return g.view(1, G), sg.view(1, -1)
+            return g, sg, xrv, xrp
+        return g, sg
 
     @staticmethod
     def backward(ctx, *grads):
         from . import _native
         x1c, x1, g, xv, xp, *wl = ctx.saved_tensors
         w = dict(zip(_GC_W, wl))
-        c = _native.gchain_struct(w, *ctx.eps, ctx.shadows)
+        R = g.shape[0]
+        c = _native.gchain_struct(w, *ctx.eps, ctx.shadows, rows=R)
         f = dict(dtype=torch.float32, device=g.device)
-        row = lambda t, n: t.reshape(-1).contiguous() if t is not None else torch.zeros(n, **f)  # noqa: E731
-        dskip = grads[0].reshape(-1).contiguous() if grads[0] is not None else None
+        row = lambda t, n: t.reshape(R, n).contiguous() if t is not None else torch.zeros(R, n, **f)  # noqa: E731
+        dskip = grads[0].reshape(R, -1).contiguous() if grads[0] is not None else None
         dsg = row(grads[1], c.NA)
         dxrv = dxrp = None
         if ctx.hub:
             dxrv, dxrp = row(grads[2], c.ND), row(grads[3], c.NE)
         d = {"d" + k: (torch.empty_like(t) if t is not None else None) for k, t in w.items()}
-        dxcat = torch.empty(c.Kc, **f)
-        dprev = torch.empty(c.G, **f) if ctx.has_prev else None
+        dxcat = torch.empty(R, c.Kc, **f)
+        dprev = torch.empty(R, c.G, **f) if ctx.has_prev else None
         _native.gchain_bwd(c, x1c, x1, g, xv, xp, dskip, dsg, dxrv, dxrp, dxcat, dprev, d)
         xs, ps = ctx.shapes
         return (dxcat.view(xs), dprev.view(ps) if dprev is not None else None,
@@ -325,10 +329,12 @@ def chain_params(vsg, pfu, nvsg):
 
 
 def global_chain(x, prev, params, bf16=False):
-    """GlobalChainFn on a single row x [1, Kc] (prev [1, G] or None) when it fits, else None."""
-    if not (x.is_cuda and x.dim() == 2 and x.shape[0] == 1 and x.dtype == torch.float32):
+    """GlobalChainFn on the rows x [R, Kc] (prev [R, G] or None; R <= 8: one per scene of a union batch)
+    when they fit, else None."""
+    from . import _native
+    if not (x.is_cuda and x.dim() == 2 and 1 <= x.shape[0] <= _native.GCHAIN_MAX_ROWS and x.dtype == torch.float32):
         return None
-    if prev is not None and not (prev.numel() == params[0][0].shape[0] and prev.is_cuda):
+    if prev is not None and not (prev.numel() == x.shape[0] * params[0][0].shape[0] and prev.is_cuda):
         return None
     ws, eps_m, eps_h = params
     return GlobalChainFn.apply(x, prev, *ws, eps_m, eps_h, bool(bf16))

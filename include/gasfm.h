@@ -709,7 +709,14 @@ typedef struct gasfm_gchain {
    * caller once per optimizer step; NULL: read the fp32 weight).  The GEMVs stream half the weight
    * bytes and accumulate in fp32; every gradient stays fp32 (dW = dy x h does not read W). */
   const uint16_t *W1h, *W2h, *WAh, *WBh, *WCh, *WDh, *WEh;
+  /* rows (round 5): the chain on `rows` global rows at once -- a union batch's one global node per
+   * scene (train.py's batch as one forward; gasfm_amd/static_batch.py), every weight streamed once
+   * for all of them.  0 or 1: one row.  Every activation / gradient vector argument of
+   * gasfm_gchain_fwd / _bwd is then [rows, len] row-major; the parameter gradients sum the rows.
+   * rows <= GASFM_GCHAIN_MAX_ROWS. */
+  int32_t rows;
 } gasfm_gchain;
+#define GASFM_GCHAIN_MAX_ROWS 8
 typedef struct gasfm_gchain_grads {
   float *dW1, *db1, *dgM, *dbM, *dW2, *db2;
   float *dgA, *dbA, *dWA;

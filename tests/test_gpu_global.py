@@ -111,16 +111,18 @@ def test_global_hub_matches_fp64(device, G, V, S, with_skip):
 @pytest.mark.parametrize("G,Kc,V,S", [(2048, 1088, 1024, 64), (128, 128, 64, 64)])
 @pytest.mark.parametrize("hub", [True, False], ids=["hub", "last_block"])
 @pytest.mark.parametrize("with_prev", [True, False], ids=["prev", "no_prev"])
-def test_global_chain_matches_fp64(device, G, Kc, V, S, hub, with_prev):
+@pytest.mark.parametrize("rows", [1, 5], ids=["row", "rows5"])
+def test_global_chain_matches_fp64(device, G, Kc, V, S, hub, with_prev, rows):
     """GlobalChainFn (csrc/global_chain.hip: the block's global tail + every consumer of g, four
     launches each way) vs the fp64 composition of layers.py:527-603 and its consumers (:497-520,
-    :928-935, the next convs' lin_r).  Tolerances as the gvec tests: outputs 2e-5 * max|ref|,
-    gradients normwise 1e-4."""
-    gen = torch.Generator().manual_seed(G + Kc + 2 * hub + with_prev)
+    :928-935, the next convs' lin_r), on one row or on 5 (a 4-scene union batch + its pad scene:
+    one global node per scene, the parameter gradients summed over them).  Tolerances as the gvec
+    tests: outputs 2e-5 * max|ref|, gradients normwise 1e-4."""
+    gen = torch.Generator().manual_seed(G + Kc + 2 * hub + with_prev + 7 * rows)
     r = lambda *s, sc=1.0, sh=0.0: torch.randn(*s, generator=gen, dtype=torch.float64) * sc + sh  # noqa: E731
     names = ["xcat", "prev", "W1", "b1", "gM", "bM", "W2", "b2", "gA", "bA", "WA",
              "gB", "bB", "WB", "bWB", "gC", "bC", "WC", "bWC", "WD", "bD", "WE", "bE"]
-    vals = [r(1, Kc, sc=1.5, sh=0.1), r(1, G, sc=2), r(G, Kc, sc=Kc ** -0.5), r(G, sc=0.1), r(G, sc=0.3, sh=1),
+    vals = [r(rows, Kc, sc=1.5, sh=0.1), r(rows, G, sc=2), r(G, Kc, sc=Kc ** -0.5), r(G, sc=0.1), r(G, sc=0.3, sh=1),
             r(G, sc=0.2), r(G, G, sc=G ** -0.5), r(G, sc=0.1), r(G, sc=0.3, sh=1), r(G, sc=0.2), r(32, G, sc=G ** -0.5),
             r(G, sc=0.3, sh=1), r(G, sc=0.2), r(V, G, sc=G ** -0.5), r(V, sc=0.1),
             r(G, sc=0.3, sh=1), r(G, sc=0.2), r(S, G, sc=G ** -0.5), r(S, sc=0.1),

@@ -4,10 +4,12 @@ The padded bucket runs the real scenes' computation of the eager union with a di
 pad scene, every camera through a partial slot, other global-graph pieces and per-scene loss partials:
 fp32 summation order only.  Bars (as tests/test_gpu_batch.py): outputs |d| <= 1e-5 + 1e-4 |ref|, the
 loss and the per-scene reprojection errors rtol 1e-5, parameter gradients elementwise rtol 1e-4,
-atol 1e-6.  With config 5's outlier-injected inputs a few cancellation-limited weight-gradient
-entries differ by up to ~4e-6 (~7e-4 relative: the global graphs' other piece lengths change the
-order of their softmax sums, and the outliers' large loss gradients cancel in the column sums), so
-there a gradient tensor passes elementwise as above OR norm-wise, ||diff|| <= 1e-4 ||ref||.  The trainer test replays a bucket captured on one batch with ANOTHER batch's data
+atol 1e-6.  In the trainer tests a few cancellation-limited weight-gradient entries differ by up to
+~4e-6 (up to ~7e-4 relative with config 5's outliers: the global graphs' other piece lengths change
+the order of their softmax sums, and large loss gradients cancel in the column sums), so there a
+gradient tensor passes elementwise as above OR norm-wise, ||diff|| <= 1e-3 ||ref||; the replay
+itself is checked against the same padded computation run eagerly: loss rtol 1e-6, gradients
+rtol 1e-4 / atol 1e-7 (not bitwise: a library GEMM may pick another algorithm inside a capture).  The trainer test replays a bucket captured on one batch with ANOTHER batch's data
 filled into its static buffers -- the captured graph must read everything it depends on from them.
 12-block learning conf, training-step-sized scenes sampled and augmented on the device.
 """
@@ -53,12 +55,12 @@ def _eager(net, lossf, datas):
 
 
 def _check_grads(net, g, g_ref, normwise=False):
-    """Elementwise rtol 1e-4, atol 1e-6; normwise: a tensor also passes when ||a - b|| <= 1e-4 ||b||."""
+    """Elementwise rtol 1e-4, atol 1e-6; normwise: a tensor also passes when ||a - b|| <= 1e-3 ||b||."""
     for (n, _), a, b in zip(net.named_parameters(), g, g_ref):
         assert (a is None) == (b is None), n
         if a is None:
             continue
-        if normwise and float((a.double() - b.double()).norm()) <= 1e-4 * float(b.double().norm()):
+        if normwise and float((a.double() - b.double()).norm()) <= 1e-3 * float(b.double().norm()):
             continue
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6, msg=lambda m: f"{n}: {m}")
 
@@ -120,11 +122,21 @@ def test_static_trainer_replays_another_batch(device, monkeypatch):
         g = _grads(net)
         assert trainer.fallbacks == [] and trainer.eager_steps == 0
         assert len(trainer.buckets) == 1 and trainer.captures == 1
-        assert next(iter(trainer.buckets.values()))[1].captured
+        sb, step = next(iter(trainer.buckets.values()))[:2]
+        assert step.captured
+        # the replay equals the same padded computation run eagerly on the buffers fill() wrote
+        # (a stale input in the graph would show here at O(1))
+        net.zero_grad(set_to_none=True)
+        pred = net(sb)
+        loss_st = static_batch.batch_loss(pred, sb, lossf)
+        loss_st.backward()
+        assert abs(float(loss) - float(loss_st)) <= 1e-6 * abs(float(loss_st)), k
+        for (n, _), a, b in zip(net.named_parameters(), g, _grads(net)):
+            torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-7, msg=lambda m: f"{n}: {m}")
         _, loss_ref, g_ref, err_ref = _eager(net, lossf, datas)
         assert abs(float(loss) - loss_ref) <= 1e-5 * abs(loss_ref), k
         np.testing.assert_allclose(errs, err_ref, rtol=1e-5)
-        _check_grads(net, g, g_ref)
+        _check_grads(net, g, g_ref, normwise=True)
 
 
 def test_static_trainer_outlier_inputs(device):
