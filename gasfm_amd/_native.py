@@ -164,6 +164,8 @@ _SIGS = {
                                   _f32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_reproj_error_seg": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _i64, _vp, _vp, _vp]),
     "gasfm_union_fill_scene": (_i32, [_vp, _vp, _vp]),
+    "gasfm_adam_step": (_i32, [_vp, _vp, _i32, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                               ctypes.c_double, _i64, _vp]),
     "gasfm_union_fill_pad": (_i32, [_vp, _vp, _vp]),
     "gasfm_point_tail_part_shape": (_i32, [_i64, _i32, _vp]),
     "gasfm_point_hub_part_shape": (_i32, [_i64, _i32, _i32, _vp]),
@@ -1201,6 +1203,15 @@ class UnionPad(ctypes.Structure):
 def union_fill_scene(sc, out, stream_of):
     check(lib().gasfm_union_fill_scene(ctypes.byref(sc), ctypes.byref(out), _stream(stream_of)),
           "gasfm_union_fill_scene")
+
+
+ADAM_CHUNK = 4096  # GASFM_ADAM_CHUNK
+
+
+def adam_step(tensors, chunks, n_chunks, lr, beta1, beta2, eps, weight_decay, step, stream_of):
+    """gasfm_adam_step over device tables (uint8 tensors holding gasfm_adam_tensor / _chunk rows)."""
+    check(lib().gasfm_adam_step(_p(tensors), _p(chunks), int(n_chunks), float(lr), float(beta1), float(beta2),
+                                float(eps), float(weight_decay), int(step), _stream(stream_of)), "gasfm_adam_step")
 
 
 def union_fill_pad(pd, out, stream_of):

@@ -800,6 +800,28 @@ int gasfm_gatt_merge_unpack(int32_t nprob, const gasfm_gatt_prob* probs, int32_t
  * operands of np.nanmean (finish with gasfm_colsum). */
 int gasfm_reproj_error(const int32_t* cam, const int32_t* pt, const float* xy, int64_t E, const float* P,
                        const float* pts3D, int64_t n, float* err, float* part, void* stream);
+/* ---- Adam over all parameter tensors in one launch (adam.hip; gasfm_amd/optim.py) ----
+ * torch.optim.Adam's update (amsgrad off, maximize off; torch/optim/adam.py) for every tensor of
+ * the table at optimizer step `step` (>= 1): g' = g + weight_decay p, m += (1 - beta1)(g' - m),
+ * v = beta2 v + (1 - beta2) g'^2, p -= lr / (1 - beta1^step) m / (sqrt(v) / sqrt(1 - beta2^step)
+ * + eps).  chunks: one entry per GASFM_ADAM_CHUNK values of a tensor (tensor index, first value),
+ * one workgroup each.  p / m / v are updated in place; g is read. */
+#define GASFM_ADAM_CHUNK 4096
+typedef struct gasfm_adam_tensor {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  int64_t numel;
+} gasfm_adam_tensor;
+typedef struct gasfm_adam_chunk {
+  int32_t tensor;
+  int32_t reserved;
+  int64_t begin;
+} gasfm_adam_chunk;
+int gasfm_adam_step(const gasfm_adam_tensor* tensors, const gasfm_adam_chunk* chunks, int32_t n_chunks, double lr,
+                    double beta1, double beta2, double eps, double weight_decay, int64_t step, void* stream);
+
 /* ---- shape-stable union batch fill (static_batch.hip; gasfm_amd/static_batch.py) ----
  * The captured config-3 / config-5 training step (train.py:60-152) replays one graph per bucket of
  * fixed cameras / points / edges / camera items; each step writes the sampled scenes and a pad

@@ -63,6 +63,9 @@ def main():
                          "forward + loss + errors + backward replayed as one hipGraph per bucket)")
     ap.add_argument("--prime", type=int, default=40,
                     help="--captured: batches run before the timed steps (they create and capture the buckets)")
+    ap.add_argument("--gasfm-adam", action="store_true",
+                    help="--captured: gasfm_amd.optim.Adam (one HIP launch) instead of torch's captured fused Adam")
+    ap.add_argument("--no-eager", action="store_true", help="skip the eager union mode (e.g. to profile --captured)")
     ap.add_argument("--phases", action="store_true",
                     help="--captured: also time the trainer's phases with a synchronize between them (slower)")
     ap.add_argument("--capture-floor", action="store_true",
@@ -144,8 +147,13 @@ def main():
 
     def run_captured(prep, steps, prime):
         from gasfm_amd.static_batch import StaticTrainer
-        # Adam as above, with its step captured into each bucket's graph pair (capturable=True)
-        copt = torch.optim.Adam(net.parameters(), lr=1e-4, fused=True, capturable=True)
+        # Adam (lr as above): torch's fused Adam with its step captured into each bucket's graph pair
+        # (capturable=True), or --gasfm-adam: gasfm_amd.optim.Adam, one launch per step
+        if args.gasfm_adam:
+            from gasfm_amd.optim import Adam
+            copt = Adam(net.parameters(), lr=1e-4)
+        else:
+            copt = torch.optim.Adam(net.parameters(), lr=1e-4, fused=True, capturable=True)
         trainer = StaticTrainer(net, lossf, optimizer=copt)
         t_prep = t_fb = t_opt = 0.0
         n_done = 0
@@ -192,11 +200,12 @@ def main():
                 "first_repro_px": float(repro[0]),
                 "last_repro_px": float(repro[-1])}
 
-    res = run(prep_device, args.steps, args.warmup)
     tag = f" + {args.outliers:g} outlier injection" if args.outliers else ""
-    print(json.dumps({"mode": "device data path (sample + rhaug" + tag + " + graph build on GPU), batch as one union forward",
-                      "batch": args.batch, "scene": f"m={args.views} n={args.points}, 10-20 sampled views", **res}),
-          flush=True)
+    if not args.no_eager:
+        res = run(prep_device, args.steps, args.warmup)
+        print(json.dumps({"mode": "device data path (sample + rhaug" + tag + " + graph build on GPU), batch as one union forward",
+                          "batch": args.batch, "scene": f"m={args.views} n={args.points}, 10-20 sampled views", **res}),
+              flush=True)
     if args.captured:
         res = run_captured(prep_device, args.steps, args.prime)
         print(json.dumps({"mode": "captured: device data path" + tag + ", the batch padded to a bucket and filled into "
