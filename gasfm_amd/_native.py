@@ -1266,7 +1266,7 @@ class _GChain(ctypes.Structure):
                 + [(k + "h", _vp) for k in _GC_SHADOW] + [("rows", _i32)])
 
 
-GCHAIN_MAX_ROWS = 8  # GASFM_GCHAIN_MAX_ROWS
+GCHAIN_MAX_ROWS = 7  # GASFM_GCHAIN_MAX_ROWS
 
 
 class _GChainGrads(ctypes.Structure):

@@ -574,6 +574,263 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_kernel(GnBwdArgs a) {
   store_dw();
 }
 
+// The same level on rows > 1 global rows (a union batch's global nodes), arranged for register
+// pressure: the per-row dy go to LDS as soon as they are formed, the previous level's row-sum
+// partials are summed by every wave for itself (lane l holds slab l: slabs <= 64; the same lanes
+// and order as block_sums' wave 0, so bitwise the one-row result), the LayerNorm statistics of all
+// rows take two workgroup sum rounds, and h / xh are recomputed where they are used.
+template <int RPT, bool BF, int R>
+__global__ __launch_bounds__(kBT) void gnode_bwd_rows_kernel(GnBwdArgs a) {
+  static_assert(32 * RPT == kBT, "one dy row per thread");
+  __shared__ float dys[R][32 * RPT];
+  __shared__ float4 red[kBT];
+  __shared__ float4 tots[R][8];
+  __shared__ float scratch[4 * R + 8];
+  __shared__ uint32_t flag;
+  int blk0[kMaxProb];
+#pragma unroll
+  for (int q = 0; q < kMaxProb; ++q) blk0[q] = a.p[q].blk0;
+  const int pi = find_prob(blk0, a.nprob);
+  const GnBwdProb& p = a.p[pi];
+  const int rows = p.rows;
+  const int local = int(blockIdx.x) - p.blk0;
+  const int slab = local % p.slabs, chunk = local / p.slabs;
+  const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3, lane = threadIdx.x & 63;
+  const int K = p.K, N = p.N;
+  const int col = slab * kSW + 4 * cl;
+  const int row0 = chunk * 32 * RPT;
+  const int nrow = row0 + int(threadIdx.x), nrc = nrow < N ? nrow : N - 1;  // this thread's dy row
+  const GnPro& pr = a.pro;
+  const bool pro = pr.nq > 0;
+  // 1. the workgroup's W slab rows first (the longest loads), then dy of every row into LDS
+  float4 w[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int n = row0 + rl + 32 * k;
+    w[k] = w4<BF>(p.W, p.Wh, int64_t(n < N ? n : N - 1) * K + col);
+  }
+  const float invF = pro ? 1.f / pr.F : 0.f;
+  for (int r = 0; r < rows; ++r) {
+    float d;
+    if (pro) {
+      const int64_t ro = int64_t(r) * pr.F;
+      const int tl = lane < pr.slabs ? lane : 0;
+      float gq[kMaxRaw], l1[kMaxRaw], l2[kMaxRaw];
+#pragma unroll
+      for (int q = 0; q < kMaxRaw; ++q) {
+        const bool on = q < pr.nq;
+        gq[q] = on ? pr.gv[q][ro + nrc] : 0.f;
+        const int64_t lo = (int64_t(r) * pr.slabs + tl) * 2;
+        l1[q] = on && lane < pr.slabs ? pr.lnp[q][lo] : 0.f;
+        l2[q] = on && lane < pr.slabs ? pr.lnp[q][lo + 1] : 0.f;
+      }
+      d = pr.dres ? pr.dres[ro + nrc] : 0.f;
+      const float m0 = pr.stats[2 * r], r0 = pr.stats[2 * r + 1];
+      const float xh = (pr.x[ro + nrc] - m0) * r0;
+#pragma unroll
+      for (int q = 0; q < kMaxRaw; ++q) {
+        const float s1 = wave_sum(l1[q]), s2 = wave_sum(l2[q]);
+        if (q < pr.nq) d += r0 * (gq[q] - s1 * invF - xh * s2 * invF);
+      }
+      if (slab == 0 && pr.out && nrow < N) pr.out[ro + nrow] = d;
+    } else {
+      d = p.dy[int64_t(r) * N + nrc];
+    }
+    dys[r][threadIdx.x] = nrow < N ? d : 0.f;
+  }
+  // 2. the LayerNorm statistics of the input rows (two workgroup sum rounds for all of them)
+  const bool ln = p.gam != nullptr;
+  float4 g4 = make_float4(0.f, 0.f, 0.f, 0.f), b4 = g4;
+  float mean[R], rstd[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) mean[r] = rstd[r] = 0.f;
+  if (ln) {
+    g4 = *reinterpret_cast<const float4*>(p.gam + col);
+    b4 = *reinterpret_cast<const float4*>(p.bet + col);
+    float sx[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      sx[r] = 0.f;
+      if (r < rows)
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+          const int j = int(threadIdx.x) + 256 * u;
+          sx[r] += j < K ? p.x[int64_t(r) * K + j] : 0.f;
+        }
+    }
+    block_sums<R>(sx, scratch);
+#pragma unroll
+    for (int r = 0; r < R; ++r) mean[r] = sx[r] / K;
+    float sq[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      sq[r] = 0.f;
+      if (r < rows)
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+          const int j = int(threadIdx.x) + 256 * u;
+          const float dd = j < K ? p.x[int64_t(r) * K + j] - mean[r] : 0.f;
+          sq[r] = fmaf(dd, dd, sq[r]);
+        }
+    }
+    block_sums<R>(sq, scratch);
+#pragma unroll
+    for (int r = 0; r < R; ++r) rstd[r] = rsq_normal(sq[r] / K + p.eps);
+  }
+  __syncthreads();  // dys
+  // 3. per row: this thread's share of dh, the 32 row lanes summed in lane order (into tots)
+  for (int r = 0; r < rows; ++r) {
+    float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const float d = dys[r][rl + 32 * k];  // 0 past N
+      sv.x = fmaf(d, w[k].x, sv.x);
+      sv.y = fmaf(d, w[k].y, sv.y);
+      sv.z = fmaf(d, w[k].z, sv.z);
+      sv.w = fmaf(d, w[k].w, sv.w);
+    }
+    if (r > 0) __syncthreads();  // red of row r - 1 read
+    red[threadIdx.x] = sv;
+    __syncthreads();
+    if (threadIdx.x < 8) {
+      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+      for (int l = 0; l < 32; ++l) {
+        const float4 v = red[l * 8 + threadIdx.x];
+        t.x += v.x;
+        t.y += v.y;
+        t.z += v.z;
+        t.w += v.w;
+      }
+      tots[r][threadIdx.x] = t;
+    }
+  }
+  auto hrow = [&](int r, float4& xh, float4& h) {
+    const float4 x4 = *reinterpret_cast<const float4*>(p.x + int64_t(r) * K + col);
+    if (!ln) {
+      xh = h = x4;
+      return;
+    }
+    xh = make_float4((x4.x - mean[r]) * rstd[r], (x4.y - mean[r]) * rstd[r], (x4.z - mean[r]) * rstd[r],
+                     (x4.w - mean[r]) * rstd[r]);
+    h = make_float4(fmaxf(fmaf(xh.x, g4.x, b4.x), 0.f), fmaxf(fmaf(xh.y, g4.y, b4.y), 0.f),
+                    fmaxf(fmaf(xh.z, g4.z, b4.z), 0.f), fmaxf(fmaf(xh.w, g4.w, b4.w), 0.f));
+  };
+  auto store_dw = [&]() {
+    float4 hs[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float4 xh;
+      hs[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < rows) hrow(r, xh, hs[r]);
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int n = row0 + rl + 32 * k;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (r >= rows) continue;
+        const float d = dys[r][rl + 32 * k];
+        v.x = fmaf(d, hs[r].x, v.x);
+        v.y = fmaf(d, hs[r].y, v.y);
+        v.z = fmaf(d, hs[r].z, v.z);
+        v.w = fmaf(d, hs[r].w, v.w);
+      }
+      if (n < N) *reinterpret_cast<float4*>(p.dW + int64_t(n) * K + col) = v;
+    }
+    if (p.db && slab == 0 && nrow < N) {
+      float v = 0.f;
+      for (int r = 0; r < rows; ++r) v += dys[r][threadIdx.x];
+      p.db[nrow] = v;
+    }
+  };
+  if (p.chunks > 1) {
+    // 4. the chunk partials to the slab's last arriver (write-through stores, one ticket)
+    if (threadIdx.x < 8)
+      for (int r = 0; r < rows; ++r) st_sc1(p.ws + (int64_t(chunk) * rows + r) * K + col, tots[r][threadIdx.x]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t t = __hip_atomic_fetch_add(p.cnt + slab, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag = t == uint32_t(p.chunks - 1) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (flag == 0u) {
+      store_dw();
+      return;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (threadIdx.x < 8) {
+      constexpr int MAXC = 16;
+      for (int r = 0; r < rows; ++r) {
+        float4 v[MAXC];
+#pragma unroll
+        for (int ch = 0; ch < MAXC; ++ch) {
+          const float* q = p.ws + (int64_t(ch < p.chunks ? ch : 0) * rows + r) * K + col;
+          v[ch] = make_float4(ld_sc1(q), ld_sc1(q + 1), ld_sc1(q + 2), ld_sc1(q + 3));
+        }
+        float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int ch = 0; ch < MAXC; ++ch)
+          if (ch < p.chunks) {
+            t.x += v[ch].x;
+            t.y += v[ch].y;
+            t.z += v[ch].z;
+            t.w += v[ch].w;
+          }
+        tots[r][threadIdx.x] = t;
+      }
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(p.cnt + slab, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // 5. the slab's final dh, or its columns of the LayerNorm backward of x
+  if (threadIdx.x < 8) {
+    if (p.lnfin) {
+      const float gg[4] = {g4.x, g4.y, g4.z, g4.w};
+      const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
+      float dg[4] = {0.f, 0.f, 0.f, 0.f}, db[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < rows; ++r) {
+        float4 xh4, h4;
+        hrow(r, xh4, h4);
+        const float4 tt = tots[r][threadIdx.x];
+        const float t4[4] = {tt.x, tt.y, tt.z, tt.w};
+        const float xh[4] = {xh4.x, xh4.y, xh4.z, xh4.w};
+        float d[4], gv[4], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          d[k] = fmaf(xh[k], gg[k], bb[k]) > 0.f ? t4[k] : 0.f;
+          gv[k] = d[k] * gg[k];
+          s1 += gv[k];
+          s2 = fmaf(gv[k], xh[k], s2);
+          dg[k] = fmaf(d[k], xh[k], dg[k]);
+          db[k] += d[k];
+        }
+        *reinterpret_cast<float4*>(p.dh + int64_t(r) * K + col) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+          s1 += __shfl_xor(s1, o);
+          s2 += __shfl_xor(s2, o);
+        }
+        if (threadIdx.x == 0) {
+          p.lnp[(int64_t(r) * p.slabs + slab) * 2] = s1;
+          p.lnp[(int64_t(r) * p.slabs + slab) * 2 + 1] = s2;
+          if (slab == 0 && p.stats) {
+            p.stats[2 * r] = mean[r];
+            p.stats[2 * r + 1] = rstd[r];
+          }
+        }
+      }
+      *reinterpret_cast<float4*>(p.dgam + col) = make_float4(dg[0], dg[1], dg[2], dg[3]);
+      *reinterpret_cast<float4*>(p.dbet + col) = make_float4(db[0], db[1], db[2], db[3]);
+    } else {
+      for (int r = 0; r < rows; ++r)
+        *reinterpret_cast<float4*>(p.dh + int64_t(r) * K + col) = tots[r][threadIdx.x];
+    }
+  }
+  store_dw();
+}
+
 constexpr int kRPT = 8;  // 256 rows per chunk
 
 int chunks_of(int N) { return (N + 32 * kRPT - 1) / (32 * kRPT); }
@@ -596,7 +853,8 @@ int launch_bwd(GnBwdArgs& a, int rows, float*& ws, uint32_t*& cnt, hipStream_t s
   for (int q = a.nprob; q < kMaxProb; ++q) a.p[q].blk0 = blocks;
   bool bf = true;
   for (int q = 0; q < a.nprob; ++q) bf = bf && a.p[q].Wh != nullptr;
-  const auto kern = rows > 1 ? (bf ? &gnode_bwd_kernel<kRPT, true, kMaxRows> : &gnode_bwd_kernel<kRPT, false, kMaxRows>)
+  const auto kern = rows > 1 ? (bf ? &gnode_bwd_rows_kernel<kRPT, true, kMaxRows>
+                                    : &gnode_bwd_rows_kernel<kRPT, false, kMaxRows>)
                              : (bf ? &gnode_bwd_kernel<kRPT, true, 1> : &gnode_bwd_kernel<kRPT, false, 1>);
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBT), 0, st, a);
   return launch_status(where);

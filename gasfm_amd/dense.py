@@ -237,7 +237,7 @@ class GlobalChainFn(torch.autograd.Function):
     and GlobalHubFn (12 backward launches per block, each GEMV followed by a one-workgroup finish).
 
     apply(xcat [R, Kc], prev [R, G] or None, *weights (_GC_W order; the hub's B..E None for the last
-    block), eps_m, eps_h, bf16) -> (g, SG, XRv, XRp), or (g, SG) without the hub, each [R, .].  R <= 8
+    block), eps_m, eps_h, bf16) -> (g, SG, XRv, XRp), or (g, SG) without the hub, each [R, .].  R <= 7
     rows: a union batch's global nodes (one per scene), every weight streamed once for all of them.
     bf16: the GEMVs read the weights' bf16 shadows (weight_shadow; BASELINE config 5), fp32
     accumulation and gradients."""
@@ -329,7 +329,7 @@ def chain_params(vsg, pfu, nvsg):
 
 
 def global_chain(x, prev, params, bf16=False):
-    """GlobalChainFn on the rows x [R, Kc] (prev [R, G] or None; R <= 8: one per scene of a union batch)
+    """GlobalChainFn on the rows x [R, Kc] (prev [R, G] or None; R <= 7: one per scene of a union batch)
     when they fit, else None."""
     from . import _native
     if not (x.is_cuda and x.dim() == 2 and 1 <= x.shape[0] <= _native.GCHAIN_MAX_ROWS and x.dtype == torch.float32):

@@ -716,7 +716,7 @@ typedef struct gasfm_gchain {
    * rows <= GASFM_GCHAIN_MAX_ROWS. */
   int32_t rows;
 } gasfm_gchain;
-#define GASFM_GCHAIN_MAX_ROWS 8
+#define GASFM_GCHAIN_MAX_ROWS 7
 typedef struct gasfm_gchain_grads {
   float *dW1, *db1, *dgM, *dbM, *dW2, *db2;
   float *dgA, *dbA, *dWA;
