@@ -583,7 +583,7 @@ template <int RPT, bool BF, int R>
 __global__ __launch_bounds__(kBT) void gnode_bwd_rows_kernel(GnBwdArgs a) {
   static_assert(32 * RPT == kBT, "one dy row per thread");
   __shared__ float dys[R][32 * RPT];
-  __shared__ float4 red[kBT];
+  __shared__ float4 red[R][kBT];
   __shared__ float4 tots[R][8];
   __shared__ float scratch[4 * R + 8];
   __shared__ uint32_t flag;
@@ -678,8 +678,11 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_rows_kernel(GnBwdArgs a) {
     for (int r = 0; r < R; ++r) rstd[r] = rsq_normal(sq[r] / K + p.eps);
   }
   __syncthreads();  // dys
-  // 3. per row: this thread's share of dh, the 32 row lanes summed in lane order (into tots)
-  for (int r = 0; r < rows; ++r) {
+  // 3. per row: this thread's share of dh; then 8 threads per row sum that row's 32 row lanes in
+  // lane order (all rows at once: one barrier)
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (r >= rows) continue;
     float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
@@ -689,21 +692,22 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_rows_kernel(GnBwdArgs a) {
       sv.z = fmaf(d, w[k].z, sv.z);
       sv.w = fmaf(d, w[k].w, sv.w);
     }
-    if (r > 0) __syncthreads();  // red of row r - 1 read
-    red[threadIdx.x] = sv;
-    __syncthreads();
-    if (threadIdx.x < 8) {
-      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    red[r][threadIdx.x] = sv;
+  }
+  __syncthreads();
+  const int tr = threadIdx.x >> 3;  // the row (r, column lane cl) of the threads < 8 rows
+  const bool rowlane = int(threadIdx.x) < 8 * rows;
+  if (rowlane) {
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 8
-      for (int l = 0; l < 32; ++l) {
-        const float4 v = red[l * 8 + threadIdx.x];
-        t.x += v.x;
-        t.y += v.y;
-        t.z += v.z;
-        t.w += v.w;
-      }
-      tots[r][threadIdx.x] = t;
+    for (int l = 0; l < 32; ++l) {
+      const float4 v = red[tr][l * 8 + cl];
+      t.x += v.x;
+      t.y += v.y;
+      t.z += v.z;
+      t.w += v.w;
     }
+    tots[tr][cl] = t;
   }
   auto hrow = [&](int r, float4& xh, float4& h) {
     const float4 x4 = *reinterpret_cast<const float4*>(p.x + int64_t(r) * K + col);
@@ -747,8 +751,7 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_rows_kernel(GnBwdArgs a) {
   };
   if (p.chunks > 1) {
     // 4. the chunk partials to the slab's last arriver (write-through stores, one ticket)
-    if (threadIdx.x < 8)
-      for (int r = 0; r < rows; ++r) st_sc1(p.ws + (int64_t(chunk) * rows + r) * K + col, tots[r][threadIdx.x]);
+    if (rowlane) st_sc1(p.ws + (int64_t(chunk) * rows + tr) * K + col, tots[tr][cl]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -761,72 +764,88 @@ __global__ __launch_bounds__(kBT) void gnode_bwd_rows_kernel(GnBwdArgs a) {
       return;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (threadIdx.x < 8) {
+    if (rowlane) {
       constexpr int MAXC = 16;
-      for (int r = 0; r < rows; ++r) {
-        float4 v[MAXC];
+      float4 v[MAXC];
 #pragma unroll
-        for (int ch = 0; ch < MAXC; ++ch) {
-          const float* q = p.ws + (int64_t(ch < p.chunks ? ch : 0) * rows + r) * K + col;
-          v[ch] = make_float4(ld_sc1(q), ld_sc1(q + 1), ld_sc1(q + 2), ld_sc1(q + 3));
-        }
-        float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int ch = 0; ch < MAXC; ++ch)
-          if (ch < p.chunks) {
-            t.x += v[ch].x;
-            t.y += v[ch].y;
-            t.z += v[ch].z;
-            t.w += v[ch].w;
-          }
-        tots[r][threadIdx.x] = t;
+      for (int ch = 0; ch < MAXC; ++ch) {
+        const float* q = p.ws + (int64_t(ch < p.chunks ? ch : 0) * rows + tr) * K + col;
+        v[ch] = make_float4(ld_sc1(q), ld_sc1(q + 1), ld_sc1(q + 2), ld_sc1(q + 3));
       }
+      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int ch = 0; ch < MAXC; ++ch)
+        if (ch < p.chunks) {
+          t.x += v[ch].x;
+          t.y += v[ch].y;
+          t.z += v[ch].z;
+          t.w += v[ch].w;
+        }
+      tots[tr][cl] = t;
     }
     if (threadIdx.x == 0) __hip_atomic_store(p.cnt + slab, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // 5. the slab's final dh, or its columns of the LayerNorm backward of x
-  if (threadIdx.x < 8) {
-    if (p.lnfin) {
+  // 5. the slab's final dh, or its columns of the LayerNorm backward of x: 8 threads per row
+  if (p.lnfin) {
+    float4 dgr = make_float4(0.f, 0.f, 0.f, 0.f), dbr = dgr;
+    if (rowlane) {
+      float4 xh4, h4;
+      hrow(tr, xh4, h4);
+      const float4 tt = tots[tr][cl];
+      const float t4[4] = {tt.x, tt.y, tt.z, tt.w};
+      const float xh[4] = {xh4.x, xh4.y, xh4.z, xh4.w};
       const float gg[4] = {g4.x, g4.y, g4.z, g4.w};
       const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
-      float dg[4] = {0.f, 0.f, 0.f, 0.f}, db[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int r = 0; r < rows; ++r) {
-        float4 xh4, h4;
-        hrow(r, xh4, h4);
-        const float4 tt = tots[r][threadIdx.x];
-        const float t4[4] = {tt.x, tt.y, tt.z, tt.w};
-        const float xh[4] = {xh4.x, xh4.y, xh4.z, xh4.w};
-        float d[4], gv[4], s1 = 0.f, s2 = 0.f;
+      float d[4], gv[4], s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          d[k] = fmaf(xh[k], gg[k], bb[k]) > 0.f ? t4[k] : 0.f;
-          gv[k] = d[k] * gg[k];
-          s1 += gv[k];
-          s2 = fmaf(gv[k], xh[k], s2);
-          dg[k] = fmaf(d[k], xh[k], dg[k]);
-          db[k] += d[k];
-        }
-        *reinterpret_cast<float4*>(p.dh + int64_t(r) * K + col) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+      for (int k = 0; k < 4; ++k) {
+        d[k] = fmaf(xh[k], gg[k], bb[k]) > 0.f ? t4[k] : 0.f;
+        gv[k] = d[k] * gg[k];
+        s1 += gv[k];
+        s2 = fmaf(gv[k], xh[k], s2);
+      }
+      dgr = make_float4(d[0] * xh[0], d[1] * xh[1], d[2] * xh[2], d[3] * xh[3]);
+      dbr = make_float4(d[0], d[1], d[2], d[3]);
+      *reinterpret_cast<float4*>(p.dh + int64_t(tr) * K + col) = make_float4(gv[0], gv[1], gv[2], gv[3]);
 #pragma unroll
-        for (int o = 1; o < 8; o <<= 1) {
-          s1 += __shfl_xor(s1, o);
-          s2 += __shfl_xor(s2, o);
-        }
-        if (threadIdx.x == 0) {
-          p.lnp[(int64_t(r) * p.slabs + slab) * 2] = s1;
-          p.lnp[(int64_t(r) * p.slabs + slab) * 2 + 1] = s2;
-          if (slab == 0 && p.stats) {
-            p.stats[2 * r] = mean[r];
-            p.stats[2 * r + 1] = rstd[r];
-          }
+      for (int o = 1; o < 8; o <<= 1) {  // the row's 8 column lanes (consecutive lanes of one wave)
+        s1 += __shfl_xor(s1, o);
+        s2 += __shfl_xor(s2, o);
+      }
+      if (cl == 0) {
+        p.lnp[(int64_t(tr) * p.slabs + slab) * 2] = s1;
+        p.lnp[(int64_t(tr) * p.slabs + slab) * 2 + 1] = s2;
+        if (slab == 0 && p.stats) {
+          p.stats[2 * tr] = mean[tr];
+          p.stats[2 * tr + 1] = rstd[tr];
         }
       }
-      *reinterpret_cast<float4*>(p.dgam + col) = make_float4(dg[0], dg[1], dg[2], dg[3]);
-      *reinterpret_cast<float4*>(p.dbet + col) = make_float4(db[0], db[1], db[2], db[3]);
-    } else {
-      for (int r = 0; r < rows; ++r)
-        *reinterpret_cast<float4*>(p.dh + int64_t(r) * K + col) = tots[r][threadIdx.x];
     }
+    // gamma / beta gradients: the rows' column partials summed in row order
+    __syncthreads();  // red's dh partials consumed (step 3)
+    if (rowlane) {
+      red[tr][cl] = dgr;
+      red[tr][8 + cl] = dbr;
+    }
+    __syncthreads();
+    if (threadIdx.x < 8) {
+      float4 dg = make_float4(0.f, 0.f, 0.f, 0.f), db = dg;
+      for (int r = 0; r < rows; ++r) {
+        const float4 a4 = red[r][threadIdx.x], b4v = red[r][8 + threadIdx.x];
+        dg.x += a4.x;
+        dg.y += a4.y;
+        dg.z += a4.z;
+        dg.w += a4.w;
+        db.x += b4v.x;
+        db.y += b4v.y;
+        db.z += b4v.z;
+        db.w += b4v.w;
+      }
+      *reinterpret_cast<float4*>(p.dgam + col) = dg;
+      *reinterpret_cast<float4*>(p.dbet + col) = db;
+    }
+  } else if (rowlane) {
+    *reinterpret_cast<float4*>(p.dh + int64_t(tr) * K + col) = tots[tr][cl];
   }
   store_dw();
 }
