@@ -522,8 +522,10 @@ class StaticTrainer:
     tensors, once its state exists (the first step of a run is eager); a Python-float learning rate
     is then fixed at capture (pass a tensor lr to schedule it)."""
 
-    def __init__(self, net, lossf, warmup=2, optimizer=None):
+    def __init__(self, net, lossf, warmup=2, optimizer=None, max_buckets=32):
+        """max_buckets: the least recently used bucket (its graphs and buffers) is dropped beyond it."""
         self.net, self.lossf = net, lossf
+        self.max_buckets = max_buckets
         self.optimizer = optimizer
         self.opt_graphs = 0
         self.params = [p for p in net.parameters() if p.requires_grad]
@@ -542,12 +544,16 @@ class StaticTrainer:
             if c.pad(st) is not None and c.waste_ok(st) and (best is None or c.E < best[0].caps.E):
                 best = b
         if best is not None:
+            key = best[0].caps.key()
+            self.buckets[key] = self.buckets.pop(key)  # most recently used last
             return best, False
         caps = Caps.for_batch(st)
-        best = self.buckets.get(caps.key())
+        best = self.buckets.pop(caps.key(), None)
         if best is None:
             best = [StaticBatch(caps, dev), None]
-            self.buckets[caps.key()] = best
+            while len(self.buckets) >= self.max_buckets:  # drop the least recently used
+                self.buckets.pop(next(iter(self.buckets)))
+        self.buckets[caps.key()] = best
         return best, True
 
     def _eager(self, datas, inputs):

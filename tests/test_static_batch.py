@@ -144,3 +144,19 @@ def test_bucket_reuse_and_fit(small_pieces):
 def test_inv3():
     A = torch.randn(5, 3, 3, dtype=torch.float64) + 3 * torch.eye(3, dtype=torch.float64)
     torch.testing.assert_close(static_batch._inv3(A), torch.linalg.inv(A))
+
+
+def test_trainer_bucket_lru(small_pieces, monkeypatch):
+    """StaticTrainer keeps at most max_buckets buckets, dropping the least recently used."""
+    trainer = static_batch.StaticTrainer.__new__(static_batch.StaticTrainer)
+    trainer.buckets, trainer.max_buckets = {}, 2
+    monkeypatch.setattr(static_batch, "StaticBatch", lambda caps, dev: type("SB", (), {"caps": caps})())
+    sts = [static_batch.BatchStats(_scenes(m0=m, n=n)) for m, n in ((8, 900), (12, 1500), (16, 2100))]
+    keys = []
+    for st in sts:
+        b, new = trainer._bucket(st, torch.device("cpu"))
+        assert new
+        keys.append(b[0].caps.key())
+    assert list(trainer.buckets) == keys[1:]  # the first (least recently used) was dropped
+    b, new = trainer._bucket(sts[1], torch.device("cpu"))  # reuse moves it to the end
+    assert not new and list(trainer.buckets) == [keys[2], keys[1]]
