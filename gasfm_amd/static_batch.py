@@ -594,17 +594,28 @@ class StaticTrainer:
                 self.profile[phase] = self.profile.get(phase, 0.0) + t - self._t
             self._t = t
 
-    def step(self, datas, inputs=None):
+    @staticmethod
+    def errors(tot):
+        """Per-scene our_repro from the [B, 2] (sum, count) device tensor step(read_errors=False) returns."""
+        return [a / b if b else float("nan") for a, b in tot.tolist()]
+
+    def step(self, datas, inputs=None, stats=None, read_errors=True):
+        """stats: the inputs' BatchStats when already taken (e.g. on the stream that prepared the batch);
+        read_errors=False: return the per-scene (sum, count) error tensor instead of reading it (no host
+        synchronisation: the caller can prepare the next batch while this one replays; ``errors``
+        converts it)."""
         from .graph_step import CapturedStep
         inputs = datas if inputs is None else inputs
         self._tick(None)
-        st = BatchStats(inputs)
+        st = BatchStats(inputs) if stats is None else stats
         why = st.expressible()
         if why is not None:
             self.fallbacks.append(why)
             loss, errs = self._eager(datas, inputs)
             if self.optimizer is not None:
                 self.optimizer.step()
+            if not read_errors:
+                errs = torch.tensor([[e, 1.0] for e in errs], dtype=torch.float32)
             return loss, errs
         dev = inputs[0].x.values.device
         b, _ = self._bucket(st, dev)
@@ -633,6 +644,7 @@ class StaticTrainer:
         if self.optimizer is not None:
             self._optimizer_step(b)
             self._tick("optimizer")
-        err = b[2]["err"]
-        tot = err[:st.B].tolist()
-        return loss, [t[0] / t[1] if t[1] else float("nan") for t in tot]
+        err = b[2]["err"][:st.B]
+        if not read_errors:
+            return loss, err.clone()  # the static buffer is overwritten by the next replay
+        return loss, self.errors(err)

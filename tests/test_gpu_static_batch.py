@@ -160,3 +160,28 @@ def test_static_trainer_outlier_inputs(device):
     assert abs(float(loss) - float(loss_ref)) <= 1e-5 * abs(float(loss_ref))
     np.testing.assert_allclose(errs, err_ref, rtol=1e-5)
     _check_grads(net, g, _grads(net), normwise=True)
+
+
+def test_static_trainer_prefetch_stream(device):
+    """The pipelined use (tools/train_step_bench.py --pipeline): the batch and its BatchStats made on a
+    second stream, the step on the main stream with read_errors=False; same loss, errors and
+    gradients as the eager union."""
+    torch.manual_seed(4)
+    conf = _conf()
+    net = gasfm_amd.GraphAttnSfMNet(conf).to(device)
+    lossf = ESFMLoss(conf)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        datas = _scenes(device, (11, 14, 17), seed=5)
+        st = static_batch.BatchStats(datas)
+    torch.cuda.current_stream().wait_stream(side)
+    trainer = static_batch.StaticTrainer(net, lossf)
+    loss, err = trainer.step(datas, stats=st, read_errors=False)
+    assert torch.is_tensor(err) and tuple(err.shape) == (3, 2)
+    errs = trainer.errors(err)
+    g = _grads(net)
+    _, loss_ref, g_ref, err_ref = _eager(net, lossf, datas)
+    assert abs(float(loss) - loss_ref) <= 1e-5 * abs(loss_ref)
+    np.testing.assert_allclose(errs, err_ref, rtol=1e-5)
+    _check_grads(net, g, g_ref, normwise=True)

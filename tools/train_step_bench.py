@@ -63,6 +63,8 @@ def main():
                          "forward + loss + errors + backward replayed as one hipGraph per bucket)")
     ap.add_argument("--prime", type=int, default=40,
                     help="--captured: batches run before the timed steps (they create and capture the buckets)")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="also time the captured step with the next batch prepared on a second stream (prefetch)")
     ap.add_argument("--gasfm-adam", action="store_true",
                     help="--captured: gasfm_amd.optim.Adam (one HIP launch) instead of torch's captured fused Adam")
     ap.add_argument("--no-eager", action="store_true", help="skip the eager union mode (e.g. to profile --captured)")
@@ -145,6 +147,60 @@ def main():
                 "ms_adam": 1e3 * t_opt / steps, "first_repro_px": float(repro[0]),
                 "last_repro_px": float(repro[-1])}
 
+    def run_pipelined(prep, steps, prime):
+        """The captured step with the next batch's data path (sampling, augmentation, scene build,
+        outlier injection, batch statistics) prepared on a second stream while this batch replays --
+        the reference's DataLoader prefetch, on the device.  Wall time per step."""
+        from gasfm_amd.optim import Adam
+        from gasfm_amd.static_batch import BatchStats, StaticTrainer
+        trainer = StaticTrainer(net, lossf, optimizer=Adam(net.parameters(), lr=1e-4))
+        side = torch.cuda.Stream()
+        main = torch.cuda.current_stream()
+
+        def prepare(first=False):
+            batch = [scenes[int(i)] for i in np.random.choice(len(scenes), args.batch, replace=False)]
+            if first:  # the scenes were made on the main stream; later batches read only them (no wait)
+                side.wait_stream(main)
+            with torch.cuda.stream(side):
+                datas = [prep(s) for s in batch]
+                inputs = datas if not args.outliers else [inject_outliers(d, args.outliers, log=lambda s: None)
+                                                          for d in datas]
+                keep = [k for k, d in enumerate(inputs) if d is not None]
+                datas, inputs = [datas[k] for k in keep], [inputs[k] for k in keep]
+                st = BatchStats(inputs)  # its one host read waits for this stream only
+            return datas, inputs, st
+
+        repro = []
+        nxt = prepare(first=True)
+        t_start = None
+        per_step = []  # (wall seconds, captured a new bucket)
+        for it in range(prime + steps):
+            if it == prime:
+                torch.cuda.synchronize()
+                t_start = time.perf_counter()
+                caps_before = trainer.captures
+            if it % 10 == 0:
+                print(f"pipelined: batch {it}/{prime + steps}, buckets {len(trainer.buckets)}", file=sys.stderr,
+                      flush=True)
+            t0, c0 = time.perf_counter(), trainer.captures
+            datas, inputs, st = nxt
+            main.wait_stream(side)
+            loss, err = trainer.step(datas, inputs, stats=st, read_errors=False)
+            nxt = prepare()  # the host prepares the next batch while the GPU replays this one
+            repro.extend(trainer.errors(err))  # host sync on this step (the batch tensors stay alive until here)
+            if it >= prime:
+                per_step.append((time.perf_counter() - t0, trainer.captures != c0))
+        torch.cuda.synchronize()
+        tot = time.perf_counter() - t_start
+        steady = [t for t, cap in per_step if not cap]
+        return {"scenes_per_s": steps * args.batch / tot, "ms_per_step": 1e3 * tot / steps,
+                "ms_per_step_without_capture_steps": 1e3 * sum(steady) / max(1, len(steady)),
+                "scenes_per_s_without_capture_steps": args.batch * len(steady) / max(1e-9, sum(steady)),
+                "ms_per_step_median": 1e3 * float(np.median([t for t, _ in per_step])), "prime_batches": prime,
+                "buckets": len(trainer.buckets), "captures_in_timed": trainer.captures - caps_before,
+                "eager_steps": trainer.eager_steps, "fallbacks": sorted(set(map(str, trainer.fallbacks))),
+                "first_repro_px": float(repro[0]), "last_repro_px": float(repro[-1])}
+
     def run_captured(prep, steps, prime):
         from gasfm_amd.static_batch import StaticTrainer
         # Adam (lr as above): torch's fused Adam with its step captured into each bucket's graph pair
@@ -212,6 +268,12 @@ def main():
                                   "its static buffers, forward + ESFMLoss + errors + backward replayed as one hipGraph",
                           "batch": args.batch, "scene": f"m={args.views} n={args.points}, 10-20 sampled views", **res}),
               flush=True)
+    if args.pipeline:
+        res = run_pipelined(prep_device, args.steps, args.prime)
+        print(json.dumps({"mode": "captured + pipelined: the next batch's device data path" + tag + " (and its batch "
+                                  "statistics) on a second stream while this batch's graph replays; gasfm_amd.optim."
+                                  "Adam", "batch": args.batch,
+                          "scene": f"m={args.views} n={args.points}, 10-20 sampled views", **res}), flush=True)
     if args.capture_floor:
         from gasfm_amd.batch import SceneBatch
         from gasfm_amd.graph_step import CapturedStep
