@@ -5,8 +5,9 @@ batch.  torch's multi-tensor Adam walks the ~880 parameter tensors (145 M values
 conf) in ~34 kernel launches and reaches ~2.9 TB/s: 1.39 ms of a 13.7 ms captured training step
 (profiles/r5_train_step_breakdown_*.txt).  ``Adam`` keeps torch.optim.Adam's update, state names
 (``exp_avg``, ``exp_avg_sq``, ``step``) and param-group options, and runs every tensor of a group
-in ONE launch from a cached table of (p, grad, exp_avg, exp_avg_sq) pointers, rebuilt only when a
-parameter's gradient tensor changes (e.g. static_batch.StaticTrainer's per-bucket gradients).
+in ONE launch from a cached table of (p, grad, exp_avg, exp_avg_sq) pointers; when the gradient tensors
+are new ones (zero_grad(set_to_none=True) between steps, or StaticTrainer's per-bucket gradients) only
+their pointer column is rewritten (one small host-to-device copy).
 Supported: fp32 CUDA parameters, amsgrad=False, maximize=False; anything else raises (no fallback).
 """
 import ctypes
@@ -16,19 +17,19 @@ import torch
 from . import _native
 
 
-class _Tensor(ctypes.Structure):
-    _fields_ = [("p", ctypes.c_void_p), ("g", ctypes.c_void_p), ("m", ctypes.c_void_p), ("v", ctypes.c_void_p),
-                ("numel", ctypes.c_int64)]
-
-
 class _Chunk(ctypes.Structure):
     _fields_ = [("tensor", ctypes.c_int32), ("reserved", ctypes.c_int32), ("begin", ctypes.c_int64)]
 
 
-def _device_table(rows, ctype, device):
-    arr = (ctype * len(rows))(*rows)
-    host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
-    return host.to(device)
+def _chunk_table(sizes, device):
+    """gasfm_adam_chunk rows (tensor index, first value) for tensors of these sizes, on the device."""
+    import numpy as np
+    t = np.concatenate([np.stack([np.full(-(-n // _native.ADAM_CHUNK), i, np.int64),
+                                  np.arange(0, n, _native.ADAM_CHUNK, dtype=np.int64)], 1) for i, n in enumerate(sizes)])
+    rows = np.zeros((t.shape[0], 2), dtype=np.int64)  # (int32 tensor | int32 reserved), int64 begin
+    rows[:, 0] = t[:, 0]
+    rows[:, 1] = t[:, 1]
+    return torch.from_numpy(rows).to(device)
 
 
 class Adam(torch.optim.Optimizer):
@@ -42,33 +43,46 @@ class Adam(torch.optim.Optimizer):
         self._tables = {}
 
     def _build(self, ps, grads):
-        """Validate the group, create missing state, build the device pointer tables."""
+        """Validate the group, create missing state, build the device tables: gasfm_adam_tensor rows as
+        int64 [n, 5] (p, g, m, v, numel) and the chunk table.  A later step whose gradient tensors are
+        other tensors (p.grad = None between steps) only rewrites column 1 (``_regrad``)."""
         for p, g in zip(ps, grads):
             if g is None:
                 raise RuntimeError("gasfm_amd.optim.Adam: every parameter of a group needs a gradient "
                                    "(or none of them)")
-            if not p.is_cuda or p.dtype != torch.float32 or g.dtype != torch.float32 or g.is_sparse:
-                raise TypeError("gasfm_amd.optim.Adam: fp32 dense CUDA parameters and gradients only")
-            if not (p.is_contiguous() and g.is_contiguous()):
-                raise TypeError("gasfm_amd.optim.Adam: contiguous parameters and gradients only")
+            if not p.is_cuda or p.dtype != torch.float32 or p.is_sparse:
+                raise TypeError("gasfm_amd.optim.Adam: fp32 dense CUDA parameters only")
+            if not p.is_contiguous():
+                raise TypeError("gasfm_amd.optim.Adam: contiguous parameters only")
         steps = {int(self.state[p]["step"]) for p in ps if self.state[p]}
         if len(steps) > 1:
             raise RuntimeError("gasfm_amd.optim.Adam: the parameters of a group are at different steps")
         step = torch.tensor(float(steps.pop() if steps else 0))  # ONE step counter shared by the group
-        tensors, chunks = [], []
-        for i, (p, g) in enumerate(zip(ps, grads)):
+        rows = []
+        for p, g in zip(ps, grads):
             st = self.state[p]
             if "exp_avg" not in st:
                 st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                 st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
             st["step"] = step
-            tensors.append(_Tensor(p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
-                                   p.numel()))
-            chunks.extend(_Chunk(i, 0, b) for b in range(0, p.numel(), _native.ADAM_CHUNK))
+            rows.append([p.data_ptr(), 0, st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), p.numel()])
         dev = ps[0].device
-        # the entry holds the tensors whose pointers it stores, so the key's ids stay theirs
-        keep = (list(ps), list(grads), [self.state[p]["exp_avg"] for p in ps], [self.state[p]["exp_avg_sq"] for p in ps])
-        return (_device_table(tensors, _Tensor, dev), _device_table(chunks, _Chunk, dev), len(chunks), step, keep)
+        tensors = torch.tensor(rows, dtype=torch.int64).to(dev)
+        chunks = _chunk_table([p.numel() for p in ps], dev)
+        # the entry holds the tensors whose pointers it stores, so their ids stay theirs
+        keep = (list(ps), [self.state[p]["exp_avg"] for p in ps], [self.state[p]["exp_avg_sq"] for p in ps])
+        return {"tensors": tensors, "chunks": chunks, "n": chunks.shape[0], "step": step, "keep": keep,
+                "grads": None}
+
+    @staticmethod
+    def _regrad(t, grads):
+        """Point the table at this step's gradient tensors (one host-to-device copy of n pointers)."""
+        for g in grads:
+            if g is None or g.dtype != torch.float32 or g.is_sparse or not g.is_contiguous():
+                raise TypeError("gasfm_amd.optim.Adam: dense contiguous fp32 gradients for every parameter")
+        ptrs = torch.tensor([g.data_ptr() for g in grads], dtype=torch.int64)
+        t["tensors"][:, 1].copy_(ptrs.pin_memory().to(t["tensors"].device, non_blocking=True))
+        t["grads"] = list(grads)  # keeps them alive, and their ids for the next comparison
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
@@ -85,17 +99,17 @@ class Adam(torch.optim.Optimizer):
             grads = [p.grad for p in ps]
             if all(g is None for g in grads):
                 continue
-            # one dict lookup per step: the table of this exact set of (param, grad, moment) tensors
-            key = (gi, tuple(map(id, ps)), tuple(map(id, grads)))
+            key = (gi, tuple(map(id, ps)))
             t = self._tables.get(key)
             if t is None:
                 t = self._build(ps, grads)
-                if len(self._tables) > 64:
+                if len(self._tables) > 16:
                     self._tables.clear()
                 self._tables[key] = t
-            tensors, chunks, n, step, _ = t
-            step += 1  # in place: every parameter's state["step"]
+            if t["grads"] is None or any(a is not b for a, b in zip(grads, t["grads"])):
+                self._regrad(t, grads)
+            t["step"] += 1  # in place: every parameter's state["step"]
             b1, b2 = group["betas"]
-            _native.adam_step(tensors, chunks, n, group["lr"], b1, b2, group["eps"], group["weight_decay"],
-                              int(step), ps[0])
+            _native.adam_step(t["tensors"], t["chunks"], t["n"], group["lr"], b1, b2, group["eps"],
+                              group["weight_decay"], int(t["step"]), ps[0])
         return loss

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--eager-only", action="store_true")
+    ap.add_argument("--gasfm-adam", action="store_true", help="gasfm_amd.optim.Adam instead of torch's fused Adam")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -45,7 +46,12 @@ def main():
     net = gasfm_amd.GraphAttnSfMNet(conf).to(dev)
     data = gasfm_amd.SceneData.from_synthetic(sc).to(dev)
     lossf = ESFMLoss(conf)
-    opt = torch.optim.Adam(net.parameters(), lr=1e-4, fused=True)
+    if args.gasfm_adam:  # gasfm_amd.optim.Adam: torch.optim.Adam's update in one HIP launch
+        from gasfm_amd.optim import Adam
+        opt = Adam(net.parameters(), lr=1e-4)
+    else:
+        opt = torch.optim.Adam(net.parameters(), lr=1e-4, fused=True)
+    adam_name = "one-launch Adam (gasfm_amd.optim)" if args.gasfm_adam else "fused Adam step"
 
     def fwd_bwd():
         loss = lossf(net(data), data)
@@ -56,7 +62,7 @@ def main():
     for mode in modes:
         if mode == "captured":
             step_fn = CapturedStep(fwd_bwd, net.parameters(), warmup=args.warmup)
-            execution = ("hipGraph replay of forward+loss+backward, fused Adam step" if step_fn.captured
+            execution = (f"hipGraph replay of forward+loss+backward, {adam_name}" if step_fn.captured
                          else f"eager fallback ({step_fn.fallback_reason})")
         else:
             def step_fn():
@@ -66,7 +72,7 @@ def main():
             for _ in range(args.warmup):
                 step_fn()
                 opt.step()
-            execution = "eager forward+loss+backward (one launch per kernel), fused Adam step"
+            execution = f"eager forward+loss+backward (one launch per kernel), {adam_name}"
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
