@@ -13,7 +13,9 @@ from .model import GraphAttnSfMNet  # noqa: F401
 from .ba import euc_ba, proj_ba  # noqa: F401
 from .outliers import OutlierInjector, inject_outliers  # noqa: F401
 from .scene import AxialAggregationGraphWrapper, SceneData, SparseMat, M2sparse  # noqa: F401
+from .optim import Adam  # noqa: F401
+from .static_batch import StaticTrainer  # noqa: F401
 
 __all__ = ["AttnPlan", "gat_attention", "Conf", "learning_conf", "optim_conf", "GATv2Conv", "ESFMLoss", "GraphAttnSfMNet",
            "AxialAggregationGraphWrapper", "SceneData", "SparseMat", "M2sparse",
-           "OutlierInjector", "inject_outliers", "euc_ba", "proj_ba"]
+           "OutlierInjector", "inject_outliers", "euc_ba", "proj_ba", "Adam", "StaticTrainer"]

@@ -10,20 +10,14 @@ are new ones (zero_grad(set_to_none=True) between steps, or StaticTrainer's per-
 their pointer column is rewritten (one small host-to-device copy).
 Supported: fp32 CUDA parameters, amsgrad=False, maximize=False; anything else raises (no fallback).
 """
-import ctypes
-
+import numpy as np
 import torch
 
 from . import _native
 
 
-class _Chunk(ctypes.Structure):
-    _fields_ = [("tensor", ctypes.c_int32), ("reserved", ctypes.c_int32), ("begin", ctypes.c_int64)]
-
-
 def _chunk_table(sizes, device):
     """gasfm_adam_chunk rows (tensor index, first value) for tensors of these sizes, on the device."""
-    import numpy as np
     t = np.concatenate([np.stack([np.full(-(-n // _native.ADAM_CHUNK), i, np.int64),
                                   np.arange(0, n, _native.ADAM_CHUNK, dtype=np.int64)], 1) for i, n in enumerate(sizes)])
     rows = np.zeros((t.shape[0], 2), dtype=np.int64)  # (int32 tensor | int32 reserved), int64 begin
