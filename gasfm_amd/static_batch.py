@@ -18,8 +18,8 @@ quantity that sizes a launch is a function of the bucket alone:
                                    + one combine entry per camera
                                    (I_cap items, M_cap combines)
   point plan (proj2scenepoint)     one item per point (deg <= 256)      one item per pad point
-  view2global                      one item per scene over its valid    all pad cameras valid
-                                   views (S = B + 1 items)              (>= 8 edges each)
+  view2global                      V2G_PIECES pieces per scene, every   all pad cameras valid
+                                   scene split, one-level combine       (>= 8 edges each)
   scenepoint2global                S2G_PIECES pieces per scene, every   all pad points valid
                                    scene split, fixed two-level combine (2..256 edges each)
 
@@ -55,6 +55,7 @@ from .scene import MIN_N_POINTS_PER_VIEW, MIN_N_VIEWS_PER_POINT, AxialAggregatio
 
 PIECE = DEFAULT_MAX_PIECE  # camera pieces: ceil(deg / PIECE) per real camera, as the eager plans
 S2G_PIECES = 512  # pieces per scene of the points -> global graph (read when a bucket is made)
+V2G_PIECES = 4  # pieces per scene of the views -> global graph (one-level combine)
 HEADROOM = 1.04  # a new bucket's sizes over the batch's
 MAX_WASTE = 1.12  # a batch reuses a bucket up to this much larger than itself (+ the fixed pads)
 
@@ -93,8 +94,8 @@ class BatchStats:
             return "a camera without edges"
         if self.max_pt_deg > PIECE:
             return f"a point seen by {self.max_pt_deg} > {PIECE} views"
-        if min(self.kv) < 1:
-            return "a scene without valid views"
+        if min(self.kv) < V2G_PIECES:
+            return f"a scene with {min(self.kv)} < V2G_PIECES = {V2G_PIECES} valid views"
         if min(self.kp) < S2G_PIECES:
             return f"a scene with {min(self.kp)} < S2G_PIECES = {S2G_PIECES} valid points"
         return None
@@ -109,6 +110,7 @@ class Caps:
         self.S = B + 1
         self.I = -(-E // PIECE) + M  # >= sum of ceil(deg / PIECE) over any M cameras with E edges
         self.P = S2G_PIECES
+        self.PV = V2G_PIECES
         self.G = math.ceil(math.sqrt(self.P))  # level-1 group size of its combine (attention._two_level)
         self.NG = -(-self.P // self.G)  # level-1 rows per scene
 
@@ -117,10 +119,11 @@ class Caps:
 
     def pad(self, st):
         """(M_pad, N_pad, E_pad, pad camera pieces) for a batch, or None when the batch does not fit."""
-        if (st.B, st.inv_v, st.inv_p) != (self.B, self.inv_v, self.inv_p) or min(st.kp) < self.P:
+        if (st.B, st.inv_v, st.inv_p) != (self.B, self.inv_v, self.inv_p) or min(st.kp) < self.P \
+                or min(st.kv) < self.PV:
             return None
         mp, npd, ep, dI = self.M - st.M, self.N - st.N, self.E - st.E, self.I - st.pieces
-        if mp < 1 or npd < self.P or ep < 2 * npd or ep > PIECE * npd or ep < MIN_N_POINTS_PER_VIEW * mp:
+        if mp < self.PV or npd < self.P or ep < 2 * npd or ep > PIECE * npd or ep < MIN_N_POINTS_PER_VIEW * mp:
             return None
         if dI < mp or ep // mp < -(-dI // mp):  # every pad camera: >= 1 piece, >= 1 edge per piece
             return None
@@ -180,11 +183,11 @@ class StaticBatch:
         self.soc32, self.sop32 = z(M, **i32), z(N, **i32)
         # one int32 buffer fed from the host per step: the global graphs' items / segments and the
         # loss's edge offsets (views below; items first, so their rows stay 16-byte aligned)
-        nh = S * c.P * 4 + S * 4 + 3 * (S + 1)
+        nh = S * c.P * 4 + S * c.PV * 4 + 3 * (S + 1)
         self.hostfed = z(nh, **i32)
         o = 0
         views = {}
-        for name, n, shape in (("items_s", S * c.P * 4, (S * c.P, 4)), ("items_v", S * 4, (S, 4)),
+        for name, n, shape in (("items_s", S * c.P * 4, (S * c.P, 4)), ("items_v", S * c.PV * 4, (S * c.PV, 4)),
                                ("seg_v", S + 1, (S + 1,)), ("seg_p", S + 1, (S + 1,)), ("eoff", S + 1, (S + 1,))):
             views[name] = self.hostfed[o:o + n].view(shape)
             o += n
@@ -217,7 +220,10 @@ class StaticBatch:
         pv = AttnPlan(self.cam_ptr, None, self.items_c, self.comb_c, I, M, E, E, max_piece=PIECE, combine_l1=None)
         pp = AttnPlan(self.pt_ptr, self.perm, self.items_p, empty, 0, N, E, E, max_piece=PIECE, pos=self.pos,
                       combine_l1=None)
-        pg = AttnPlan(self.seg_v, self.src_v, self.items_v, empty, 0, S, self.kv_cap, M, max_piece=1 << 30,
+        sv = torch.arange(S, **i64)
+        self.comb_v = torch.stack([sv, sv * c.PV, torch.full_like(sv, c.PV), torch.ones_like(sv)], 1).to(
+            torch.int32).contiguous()
+        pg = AttnPlan(self.seg_v, self.src_v, self.items_v, self.comb_v, S * c.PV, S, self.kv_cap, M, max_piece=1 << 30,
                       pos=self.pos_v, combine_l1=None)
         ps = AttnPlan(self.seg_p, self.src_p, self.items_s, self.comb_s, n_slots, S, self.kp_cap, N,
                       max_piece=1 << 30, pos=self.pos_p, combine_l1=self.l1_s)
@@ -253,6 +259,18 @@ class StaticBatch:
             o.piece = PIECE
             self._out = o
 
+    @staticmethod
+    def _pieces_np(seg, P):
+        """P pieces per segment of seg (lengths differing by at most one, the first len % P longer),
+        slot = item index: the items of an all-split plan (numpy)."""
+        S = seg.shape[0] - 1
+        k = np.arange(S * P)
+        ks, kq = k // P, k % P
+        cnt = (seg[1:] - seg[:-1])[ks]
+        b2, r2 = cnt // P, cnt % P
+        begin = seg[:-1][ks] + kq * b2 + np.minimum(kq, r2)
+        return np.stack([ks, begin, begin + b2 + (kq < r2), k], 1)
+
     def _host_plans(self, st, npd):
         """The global graphs' segments / items and the edge offsets from host counts (all views and all
         points valid): int32 array laid out as self.hostfed."""
@@ -260,13 +278,8 @@ class StaticBatch:
         S, P = c.S, c.P
         seg_v = np.concatenate([[0], np.cumsum(st.ms + [c.M - st.M])]).astype(np.int64)
         seg_p = np.concatenate([[0], np.cumsum(st.ns + [npd])]).astype(np.int64)
-        k = np.arange(S * P)
-        ks, kq = k // P, k % P
-        cnt = (seg_p[1:] - seg_p[:-1])[ks]
-        b2, r2 = cnt // P, cnt % P
-        begin = seg_p[:-1][ks] + kq * b2 + np.minimum(kq, r2)
-        items_s = np.stack([ks, begin, begin + b2 + (kq < r2), k], 1)
-        items_v = np.stack([np.arange(S), seg_v[:-1], seg_v[1:], np.full(S, -1)], 1)
+        items_s = self._pieces_np(seg_p, P)
+        items_v = self._pieces_np(seg_v, c.PV)
         eo = np.concatenate([[0], np.cumsum(st.Es), [c.E]])
         return np.concatenate([items_s.ravel(), items_v.ravel(), seg_v, seg_p, eo]).astype(np.int32)
 
@@ -439,27 +452,30 @@ class StaticBatch:
         """view2global / scenepoint2global segments and items from the filled counts (torch ops)."""
         c = self.caps
         i64 = dict(dtype=torch.int64, device=self.device)
-        ar = lambda n: torch.arange(n, **i64)
         sop = self.sop32.to(torch.int64)
-        # view2global: one item per scene over its valid views
+        # view2global: V2G_PIECES pieces per scene over its valid views, every scene split
         valid_v = self.pts_per_cam.view(-1) >= MIN_N_POINTS_PER_VIEW
         self.src_v.copy_(torch.nonzero_static(valid_v, size=self.kv_cap).view(-1))
         cv = torch.zeros(c.S, **i64).index_add_(0, self.scene_of_cam, valid_v.to(torch.int64))
         self.seg_v[1:].copy_(torch.cumsum(cv, 0))
-        sv = self.seg_v.to(torch.int64)
-        self.items_v.copy_(torch.stack([ar(c.S), sv[:-1], sv[1:], torch.full((c.S,), -1, **i64)], 1))
+        self.items_v.copy_(self._pieces_torch(self.seg_v.to(torch.int64), c.PV))
         # scenepoint2global: S2G_PIECES pieces per scene, every scene split
         valid_p = self.cam_per_pts.view(-1) >= MIN_N_VIEWS_PER_POINT
         self.src_p.copy_(torch.nonzero_static(valid_p, size=self.kp_cap).view(-1))
         cp = torch.zeros(c.S, **i64).index_add_(0, sop, valid_p.to(torch.int64))
         self.seg_p[1:].copy_(torch.cumsum(cp, 0))
-        sp = self.seg_p.to(torch.int64)
-        k = ar(c.S * c.P)
-        ks, kq = k // c.P, k % c.P
-        cnt = (sp[1:] - sp[:-1])[ks]
-        b2, r2 = cnt // c.P, cnt % c.P
-        begin = sp[:-1][ks] + kq * b2 + torch.minimum(kq, r2)
-        self.items_s.copy_(torch.stack([ks, begin, begin + b2 + (kq < r2).to(torch.int64), k], 1))
+        self.items_s.copy_(self._pieces_torch(self.seg_p.to(torch.int64), c.P))
+
+    @staticmethod
+    def _pieces_torch(seg, P):
+        """_pieces_np in torch ops on seg's device."""
+        S = seg.shape[0] - 1
+        k = torch.arange(S * P, dtype=torch.int64, device=seg.device)
+        ks, kq = k // P, k % P
+        cnt = (seg[1:] - seg[:-1])[ks]
+        b2, r2 = cnt // P, cnt % P
+        begin = seg[:-1][ks] + kq * b2 + torch.minimum(kq, r2)
+        return torch.stack([ks, begin, begin + b2 + (kq < r2).to(torch.int64), k], 1)
 
     def split(self, pred):
         """Per-scene prediction dicts (views into the union outputs) of the last fill."""

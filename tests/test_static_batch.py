@@ -92,13 +92,17 @@ def test_static_batch_structure(small_pieces):
     assert (sb.eoff.numpy() == np.array(eo + [E])).all()
     assert sb.weight.tolist() == [1.0] * B + [0.0]
     assert (soc[cam] == np.repeat(np.arange(S), np.diff(sb.eoff.numpy()))).all()
-    # view2global: one item per scene over its valid views
+    # view2global: PV pieces per scene over its valid views, every scene split, one combine entry each
     src_v, seg_v = sb.src_v.numpy(), sb.seg_v.numpy()
     valid_v = np.diff(cptr) >= 8
     assert (src_v == np.nonzero(valid_v)[0]).all()
     assert (np.diff(seg_v) == np.bincount(soc[valid_v], minlength=S)).all()
-    iv = sb.items_v.numpy()
-    assert (iv[:, 0] == np.arange(S)).all() and (iv[:, 1] == seg_v[:-1]).all() and (iv[:, 2] == seg_v[1:]).all()
+    iv, PV = sb.items_v.numpy(), caps.PV
+    assert iv.shape == (S * PV, 4) and (iv[:, 3] == np.arange(S * PV)).all()
+    _tiles(iv, 0, seg_v[-1])
+    for s in range(S):
+        assert (iv[s * PV:(s + 1) * PV, 0] == s).all() and iv[s * PV, 1] == seg_v[s]
+        assert tuple(sb.comb_v.numpy()[s]) == (s, s * PV, PV, 1)
     # scenepoint2global: P pieces per scene, all split, fixed two-level combine
     src_p, seg_p = sb.src_p.numpy(), sb.seg_p.numpy()
     valid_p = np.diff(pptr) >= 2
