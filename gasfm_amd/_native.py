@@ -164,6 +164,8 @@ _SIGS = {
                                   _f32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_reproj_error_seg": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _i64, _vp, _vp, _vp]),
     "gasfm_union_fill_scene": (_i32, [_vp, _vp, _vp]),
+    "gasfm_fold_scene_rows_fwd": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _vp]),
+    "gasfm_fold_scene_rows_bwd": (_i32, [_vp, _i64, _vp, _i64, _i32, _i32, _vp, _i64, _vp]),
     "gasfm_adam_step": (_i32, [_vp, _vp, _i32, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                ctypes.c_double, _i64, _vp]),
     "gasfm_union_fill_pad": (_i32, [_vp, _vp, _vp]),
@@ -1203,6 +1205,22 @@ class UnionPad(ctypes.Structure):
 def union_fill_scene(sc, out, stream_of):
     check(lib().gasfm_union_fill_scene(ctypes.byref(sc), ctypes.byref(out), _stream(stream_of)),
           "gasfm_union_fill_scene")
+
+
+def fold_scene_rows_fwd(sv, sg, soc):
+    """sv [m, w] + sg[soc] (gasfm_fold_scene_rows_fwd); unit column strides."""
+    out = torch.empty((sv.shape[0], sv.shape[1]), dtype=torch.float32, device=sv.device)
+    check(lib().gasfm_fold_scene_rows_fwd(_p(sv), sv.stride(0), _p(sg), sg.stride(0), _p(soc), sv.shape[0],
+                                          sv.shape[1], _p(out), out.stride(0), _stream(sv)), "gasfm_fold_scene_rows_fwd")
+    return out
+
+
+def fold_scene_rows_bwd(dout, soc, S):
+    """[S, w] per-scene sums of dout's rows in camera order (gasfm_fold_scene_rows_bwd)."""
+    dsg = torch.empty((S, dout.shape[1]), dtype=torch.float32, device=dout.device)
+    check(lib().gasfm_fold_scene_rows_bwd(_p(dout), dout.stride(0), _p(soc), dout.shape[0], S, dout.shape[1], _p(dsg),
+                                          dsg.stride(0), _stream(dout)), "gasfm_fold_scene_rows_bwd")
+    return dsg
 
 
 ADAM_CHUNK = 4096  # GASFM_ADAM_CHUNK

@@ -212,3 +212,54 @@ extern "C" int gasfm_union_fill_pad(const gasfm_union_pad* pd, const gasfm_union
                      *pd, *out);
   return launch_status("gasfm_union_fill_pad");
 }
+
+// ---- the per-scene global term of a union batch folded into the per-camera term (model._fold_global):
+//   forward   out[c] = sv[c] + sg[soc[c]]                       (one thread per value)
+//   backward  dsg[s] = sum over the cameras c of scene s of dout[c], in camera order (one workgroup per
+//             scene, one thread per column: deterministic, no atomics)
+namespace gasfm {
+namespace {
+
+__global__ __launch_bounds__(kT) void fold_rows_fwd_kernel(const float* __restrict__ sv, int64_t ldsv,
+                                                           const float* __restrict__ sg, int64_t ldsg,
+                                                           const int64_t* __restrict__ soc, int64_t m, int width,
+                                                           float* __restrict__ out, int64_t ldo) {
+  const int64_t i = int64_t(blockIdx.x) * kT + threadIdx.x;
+  if (i >= m * width) return;
+  const int64_t c = i / width, j = i % width;
+  out[c * ldo + j] = sv[c * ldsv + j] + sg[soc[c] * ldsg + j];
+}
+
+__global__ __launch_bounds__(kT) void fold_rows_bwd_kernel(const float* __restrict__ dout, int64_t ld,
+                                                           const int64_t* __restrict__ soc, int64_t m, int width,
+                                                           float* __restrict__ dsg, int64_t ldsg) {
+  const int s = blockIdx.x;
+  for (int j = threadIdx.x; j < width; j += kT) {
+    float acc = 0.f;
+    for (int64_t c = 0; c < m; ++c)
+      if (soc[c] == s) acc += dout[c * ld + j];
+    dsg[int64_t(s) * ldsg + j] = acc;
+  }
+}
+
+}  // namespace
+}  // namespace gasfm
+
+extern "C" int gasfm_fold_scene_rows_fwd(const float* sv, int64_t ldsv, const float* sg, int64_t ldsg,
+                                         const int64_t* soc, int64_t m, int32_t width, float* out, int64_t ldo,
+                                         void* stream) {
+  GASFM_REQUIRE(sv && sg && soc && out && m >= 0 && width > 0, "gasfm_fold_scene_rows_fwd: bad arguments");
+  if (m == 0) return GASFM_OK;
+  const int64_t n = m * width;
+  hipLaunchKernelGGL(fold_rows_fwd_kernel, dim3(unsigned((n + kT - 1) / kT)), dim3(kT), 0,
+                     reinterpret_cast<hipStream_t>(stream), sv, ldsv, sg, ldsg, soc, m, width, out, ldo);
+  return launch_status("gasfm_fold_scene_rows_fwd");
+}
+
+extern "C" int gasfm_fold_scene_rows_bwd(const float* dout, int64_t ld, const int64_t* soc, int64_t m, int32_t S,
+                                         int32_t width, float* dsg, int64_t ldsg, void* stream) {
+  GASFM_REQUIRE(dout && soc && dsg && m >= 0 && S > 0 && width > 0, "gasfm_fold_scene_rows_bwd: bad arguments");
+  hipLaunchKernelGGL(fold_rows_bwd_kernel, dim3(S), dim3(kT), 0, reinterpret_cast<hipStream_t>(stream), dout, ld,
+                     soc, m, width, dsg, ldsg);
+  return launch_status("gasfm_fold_scene_rows_bwd");
+}

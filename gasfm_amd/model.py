@@ -324,6 +324,36 @@ def _seam0_ok(args):
             and sp.shape[1] == 32 and sv.shape[1] == 32)
 
 
+class FoldGlobalFn(torch.autograd.Function):
+    """Sv'[c] = Sv[c] + Sg[scene(c)] in one kernel each way (csrc/static_batch.hip): the backward's
+    per-scene sums run in camera order without atomics (torch's index_select backward is an
+    atomic index_add after a fill)."""
+
+    @staticmethod
+    def forward(ctx, sv, sg, soc):
+        ctx.save_for_backward(soc)
+        ctx.S = sg.shape[0]
+        return _native.fold_scene_rows_fwd(sv, sg, soc)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (soc,) = ctx.saved_tensors
+        dout = dout if dout.stride(1) == 1 else dout.contiguous()
+        return dout, _native.fold_scene_rows_bwd(dout, soc, ctx.S), None
+
+
+_ZERO_ROWS = {}
+
+
+def _zero_row(width, device):
+    """A cached [1, width] zero row (read-only): the folded global term Sg' without a fill launch."""
+    key = (width, str(device))
+    z = _ZERO_ROWS.get(key)
+    if z is None:
+        z = _ZERO_ROWS[key] = torch.zeros((1, width), dtype=torch.float32, device=device)
+    return z
+
+
 def _fold_global(sv, sg, plans):
     """SceneBatch (batch.py): the per-edge global term of scene s, Sg[s], added to the per-camera
     term of its cameras (every camera belongs to one scene), so the edge kernels see one scene:
@@ -331,6 +361,9 @@ def _fold_global(sv, sg, plans):
     soc = plans.get("_scene_of_cam")
     if soc is None or sg is None or sg.shape[0] == 1:
         return sv, sg
+    if (sv.is_cuda and sv.dtype == torch.float32 and sg.dtype == torch.float32 and sv.dim() == 2
+            and sv.stride(1) == 1 and sg.stride(1) == 1 and sg.shape[1] == sv.shape[1] and soc.dtype == torch.int64):
+        return FoldGlobalFn.apply(sv, sg, soc), _zero_row(sg.shape[1], sg.device)
     return sv + sg.index_select(0, soc), torch.zeros((1, sg.shape[1]), dtype=sg.dtype, device=sg.device)
 
 

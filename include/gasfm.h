@@ -822,6 +822,15 @@ typedef struct gasfm_adam_chunk {
 int gasfm_adam_step(const gasfm_adam_tensor* tensors, const gasfm_adam_chunk* chunks, int32_t n_chunks, double lr,
                     double beta1, double beta2, double eps, double weight_decay, int64_t step, void* stream);
 
+/* ---- a union batch's per-scene global term folded into its cameras' rows (static_batch.hip) ----
+ * model._fold_global (batch.py's union of scenes, one global node per scene): forward
+ * out[c] = sv[c] + sg[soc[c]] ([m x width] rows, row strides given); backward dsg[s] = the sum over
+ * the cameras of scene s of dout[c], in camera order (one workgroup per scene, no atomics). */
+int gasfm_fold_scene_rows_fwd(const float* sv, int64_t ldsv, const float* sg, int64_t ldsg, const int64_t* soc,
+                              int64_t m, int32_t width, float* out, int64_t ldo, void* stream);
+int gasfm_fold_scene_rows_bwd(const float* dout, int64_t ld, const int64_t* soc, int64_t m, int32_t S,
+                              int32_t width, float* dsg, int64_t ldsg, void* stream);
+
 /* ---- shape-stable union batch fill (static_batch.hip; gasfm_amd/static_batch.py) ----
  * The captured config-3 / config-5 training step (train.py:60-152) replays one graph per bucket of
  * fixed cameras / points / edges / camera items; each step writes the sampled scenes and a pad
