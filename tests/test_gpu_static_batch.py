@@ -185,3 +185,24 @@ def test_static_trainer_prefetch_stream(device):
     assert abs(float(loss) - loss_ref) <= 1e-5 * abs(loss_ref)
     np.testing.assert_allclose(errs, err_ref, rtol=1e-5)
     _check_grads(net, g, g_ref, normwise=True)
+
+
+def test_static_trainer_eager_fallback(device, monkeypatch):
+    """A batch the padding cannot express runs through the eager union (counted, reason kept), with
+    the same loss / errors / gradients, and the optimizer still steps."""
+    from gasfm_amd.optim import Adam
+    monkeypatch.setattr(static_batch, "S2G_PIECES", 10 ** 6)  # no scene has that many valid points
+    torch.manual_seed(6)
+    conf = _conf()
+    net = gasfm_amd.GraphAttnSfMNet(conf).to(device)
+    lossf = ESFMLoss(conf)
+    datas = _scenes(device, (12, 15), seed=7)
+    _, loss_ref, g_ref, err_ref = _eager(net, lossf, datas)
+    before = [p.detach().clone() for p in net.parameters()]
+    trainer = static_batch.StaticTrainer(net, lossf, optimizer=Adam(net.parameters(), lr=1e-3))
+    loss, errs = trainer.step(datas)
+    assert trainer.eager_steps == 1 and trainer.captures == 0 and "valid points" in trainer.fallbacks[0]
+    assert abs(float(loss) - loss_ref) <= 1e-6 * abs(loss_ref)
+    np.testing.assert_allclose(errs, err_ref, rtol=1e-6)
+    _check_grads(net, _grads(net), g_ref)
+    assert any(not torch.equal(p, b) for p, b in zip(net.parameters(), before))  # Adam stepped
