@@ -106,4 +106,7 @@ class Adam(torch.optim.Optimizer):
             b1, b2 = group["betas"]
             _native.adam_step(t["tensors"], t["chunks"], t["n"], group["lr"], b1, b2, group["eps"],
                               group["weight_decay"], int(t["step"]), ps[0])
+            # the kernel wrote p in place behind autograd's back: bump the version counters, as an in-place
+            # torch op would (version-keyed caches -- e.g. dense.weight_shadow's bf16 shadows -- see it)
+            torch.autograd.graph.increment_version(ps)
         return loss

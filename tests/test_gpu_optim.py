@@ -73,3 +73,13 @@ def test_adam_state_dict_roundtrip(device):
     ob.step()
     for t, s in zip(b, a):
         torch.testing.assert_close(t, s, rtol=0, atol=0)
+
+
+def test_adam_bumps_versions(device):
+    """The kernel updates parameters in place: their version counters move as with an in-place torch op
+    (version-keyed caches such as dense.weight_shadow's bf16 shadows rely on it)."""
+    p = torch.ones(10, device=device, requires_grad=True)
+    p.grad = torch.ones_like(p)
+    v0 = p._version
+    Adam([p], lr=0.1).step()
+    assert p._version > v0 and float(p.detach()[0]) < 1.0

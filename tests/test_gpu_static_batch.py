@@ -206,3 +206,44 @@ def test_static_trainer_eager_fallback(device, monkeypatch):
     np.testing.assert_allclose(errs, err_ref, rtol=1e-6)
     _check_grads(net, _grads(net), g_ref)
     assert any(not torch.equal(p, b) for p, b in zip(net.parameters(), before))  # Adam stepped
+
+
+def test_static_trainer_bf16_shadows_follow_the_optimizer(device, monkeypatch):
+    """Config-5 bf16 mode under capture: after an optimizer step the replayed graph must read the new
+    weights' bf16 shadows (StaticTrainer re-rounds them after the step).  A replay on the updated
+    weights equals the eager union on them (rtol 1e-4); with stale shadows the lr = 1e-2 step would
+    show at the percent level."""
+    from gasfm_amd.optim import Adam
+    monkeypatch.setattr(static_batch, "MAX_WASTE", 10.0)  # both batches in one bucket
+    torch.manual_seed(8)
+    conf = _conf()
+    net = gasfm_amd.GraphAttnSfMNet(conf).to(device)
+    net.set_projection_precision("bf16")
+    lossf = ESFMLoss(conf)
+    trainer = static_batch.StaticTrainer(net, lossf, optimizer=Adam(net.parameters(), lr=1e-2))
+    a, b = _scenes(device, (14, 16, 18), seed=9), _scenes(device, (12, 13, 15), seed=10)
+    trainer.step(a)  # capture, then Adam + shadow refresh
+    trainer.optimizer = None  # the next replay leaves the weights as they are
+    loss, _ = trainer.step(b)
+    assert trainer.captures == 1 and trainer.eager_steps == 0
+    net.zero_grad(set_to_none=True)
+    ref = sum(lossf(p, d) for p, d in zip(forward_batch(net, b), b))
+    assert abs(float(loss) - float(ref)) <= 1e-4 * abs(float(ref)), (float(loss), float(ref))
+    # every live shadow equals its weight rounded to bf16 after the trainer's step (the refresh), and
+    # a step without the refresh leaves them behind the weights (the check above is then needed)
+    from gasfm_amd import dense
+
+    def shadows_current():
+        live = [(r(), sh) for r, sh, _, _ in dense._SHADOWS.values() if r() is not None]
+        assert live
+        return all(torch.equal(sh, w.detach().to(torch.bfloat16)) for w, sh in live)
+
+    trainer.optimizer = Adam(net.parameters(), lr=1e-2)
+    trainer.step(a)
+    assert shadows_current()
+    monkeypatch.setattr(net, "refresh_weight_shadows", lambda: None)
+    trainer.step(a)
+    assert not shadows_current()
+    # an eager forward re-rounds the changed weights by itself (gasfm Adam bumps their versions)
+    forward_batch(net, b)
+    assert shadows_current()
