@@ -777,8 +777,21 @@ __global__ __launch_bounds__(kThreads, GASFM_PBWD_MINWAVES) void edge_prologue_b
 
 // =====================================================================================
 // segment_rowsum: out[seg] = scale * sum_{e in item} X[src_e]   (32-wide rows, optional perm)
-// 8 lanes x float4 per row, 8 rows per wave, 4 row groups in flight.
+// 8 lanes x float4 per row, 8 rows per wave, 4 row groups in flight.  Items are pipelined two
+// deep across a wave's grid-stride loop (round 5): while item i's rows are in flight, item i+1's
+// first 32 source indices and item i+2's descriptor are requested, so an item costs one memory
+// round trip (its rows) instead of three (descriptor -> indices -> rows).  The per-lane summation
+// order is unchanged: the outputs are bitwise those of the unpipelined loop.
 // =====================================================================================
+__device__ __forceinline__ void rowsum_idx(const int32_t* __restrict__ perm, const gasfm_work_item& w, int row,
+                                           int (&src)[4]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = w.begin + 8 * u + row;
+    src[u] = e < w.end ? (perm ? perm[e] : e) : -1;
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void segment_rowsum_kernel(const gasfm_work_item* __restrict__ items,
                                                                  int n_items, const int32_t* __restrict__ perm,
                                                                  const float* __restrict__ X, int64_t ldX,
@@ -787,27 +800,43 @@ __global__ __launch_bounds__(kThreads) void segment_rowsum_kernel(const gasfm_wo
   const int lane = threadIdx.x & (kW - 1);
   const int row = lane >> 3, c = (lane & 7) * 4;
   const int nw = gridDim.x * kWaves;
-  for (int it = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + threadIdx.x / kW); it < n_items; it += nw) {
-    const gasfm_work_item w = items[it];
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int e0 = w.begin; e0 < w.end; e0 += 32) {
-      float4 v[4];
+  const gasfm_work_item none{0, 0, 0, 0};
+  int it = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + threadIdx.x / kW);
+  gasfm_work_item w = it < n_items ? items[it] : none;
+  gasfm_work_item wn = it + nw < n_items ? items[it + nw] : none;
+  int src[4];
+  rowsum_idx(perm, w, row, src);
+  for (; it < n_items; it += nw) {
+    // item it's first 32 rows
+    float4 v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = e0 + 8 * u + row;
-        if (e < w.end) {
-          const int64_t src = perm ? perm[e] : e;
-          v[u] = *reinterpret_cast<const float4*>(X + src * ldX + c);
-        } else {
-          v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-      }
+    for (int u = 0; u < 4; ++u)
+      v[u] = src[u] >= 0 ? *reinterpret_cast<const float4*>(X + int64_t(src[u]) * ldX + c)
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+    // the next item's first indices and the one after it's descriptor, behind them
+    int srcn[4];
+    rowsum_idx(perm, wn, row, srcn);
+    const gasfm_work_item wnn = it + 2 * nw < n_items ? items[it + 2 * nw] : none;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int e0 = w.begin;;) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         acc.x += v[u].x;
         acc.y += v[u].y;
         acc.z += v[u].z;
         acc.w += v[u].w;
+      }
+      e0 += 32;
+      if (e0 >= w.end) break;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // long items: the remaining rows, 32 at a time
+        const int e = e0 + 8 * u + row;
+        if (e < w.end) {
+          const int64_t s2 = perm ? perm[e] : e;
+          v[u] = *reinterpret_cast<const float4*>(X + s2 * ldX + c);
+        } else {
+          v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
       }
     }
     acc.x = xor_sum_from<8>(acc.x);
@@ -819,6 +848,10 @@ __global__ __launch_bounds__(kThreads) void segment_rowsum_kernel(const gasfm_wo
       float* dst = (w.slot < 0) ? out + int64_t(w.seg) * F : part + int64_t(w.slot) * F;
       *reinterpret_cast<float4*>(dst + c) = r;
     }
+    w = wn;
+    wn = wnn;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) src[u] = srcn[u];
   }
 }
 
