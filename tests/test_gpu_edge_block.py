@@ -93,13 +93,22 @@ def test_prologue_without_ln(device):
     normwise(bd.grad, br.grad, msg="b")
 
 
-@pytest.mark.parametrize("n,E,max_piece", [(500, 20000, 16), (5003, 20000, 256), (37, 40, 16)])
+@pytest.mark.parametrize("n,E,max_piece", [(500, 20000, 16), (5003, 20000, 256), (37, 40, 16), (7, 5000, 4096),
+                                             ("lens", 0, 4096)])
 def test_segment_rowsum_matches_index_add(device, n, E, max_piece):
-    """Ragged item counts, empty segments, split segments, vs fp64 index_add."""
+    """Ragged item counts, empty segments, split segments, items of several 32-row passes (the
+    kernel's long-item loop; "lens": segments of exactly 0, 1, 31, 32, 33, 64, 65 and 200 rows),
+    vs fp64 index_add."""
     from gasfm_amd import _native
     from gasfm_amd.attention import AttnPlan, bwd_combine
     rng = np.random.default_rng(2)
-    dst = torch.from_numpy(rng.integers(0, n, E))
+    if n == "lens":
+        lens = [0, 1, 31, 32, 33, 64, 65, 200, 0, 3]
+        n = len(lens)
+        dst = torch.from_numpy(rng.permutation(np.repeat(np.arange(n), lens)))
+        E = dst.numel()
+    else:
+        dst = torch.from_numpy(rng.integers(0, n, E))
     plan = AttnPlan.from_targets(dst, n, max_piece=max_piece).to(device)
     X = torch.randn(E, 32, device=device)
     out = torch.empty(n, 32, device=device)
