@@ -905,6 +905,8 @@ class FanOutFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, n):
+        # a consumer that sends no gradient stays None (not a zero-filled [E, 2] tensor summed in)
+        ctx.set_materialize_grads(False)
         return tuple(x.view_as(x) for _ in range(n))
 
     @staticmethod
