@@ -361,7 +361,48 @@ def linear_res(x, lin, res):
     return y if res is None else res + y
 
 
+# Row counts up to which a device LayerNorm over [rows, D] takes SmallLayerNormFn: there torch's
+# backward reduces gamma / beta with a few-workgroup kernel (GammaBetaBackwardSimple: 41 us for
+# 125 x 1024 on the rank-0-of-8 proxy's camera shard; 5-6 us per pass at 1000 rows)
+SMALL_LN_ROWS = 512
+
+
+class SmallLayerNormFn(torch.autograd.Function):
+    """F.layer_norm whose backward takes dx from aten's row kernel and reduces gamma / beta as
+    one [rows, 2D] partial matrix [dy xhat | dy] through param_colsum (batched with the step's
+    other parameter sums at the end of the backward pass)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        D = x.shape[-1]
+        y, mean, rstd = torch.native_layer_norm(x, [D], w, b, eps)
+        ctx.save_for_backward(x, mean, rstd, w, b)
+        from . import _native
+        ctx.defer = _native.defer_token(w, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _native
+        x, mean, rstd, w, b = ctx.saved_tensors
+        D = x.shape[-1]
+        dy = dy.contiguous()
+        dx = torch.ops.aten.native_layer_norm_backward(dy, x, [D], mean, rstd, w, b, [True, False, False])[0]
+        part = torch.empty((x.shape[0], 2 * D), dtype=dy.dtype, device=dy.device)
+        torch.sub(x, mean, out=part[:, :D])
+        part[:, :D].mul_(rstd).mul_(dy)
+        part[:, D:].copy_(dy)
+        tot = _native.param_colsum(part, ctx.defer)
+        # views of the (possibly deferred) sum: AccumulateGrad adopts a view, it would copy the
+        # pending sum tensor itself before it is filled
+        return dx, tot[:D], tot[D:], None
+
+
 def layer_norm(x, ln):
+    if (x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and 0 < x.shape[0] <= SMALL_LN_ROWS
+            and ln.weight is not None and ln.bias is not None and torch.is_grad_enabled()
+            and x.stride(1) == 1 and (x.requires_grad or ln.weight.requires_grad)):
+        return SmallLayerNormFn.apply(x, ln.weight, ln.bias, ln.eps)
     return F.layer_norm(x, ln.normalized_shape, ln.weight, ln.bias, ln.eps)
 
 

@@ -73,3 +73,32 @@ def test_node_dispatch_uses_kernel_for_point_rows(device):
     y = dense.sequential(seq, x)
     assert type(y.grad_fn).__name__ == "NodeLnLinearFnBackward"
     torch.testing.assert_close(y, seq(x), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("N,D", [(1, 1024), (125, 1024), (512, 64), (300, 4)])
+def test_small_layer_norm_matches_fp64(device, N, D):
+    """dense.layer_norm on few rows (SmallLayerNormFn: aten's dx, gamma / beta through
+    param_colsum) vs fp64 F.layer_norm; the same tolerances as above."""
+    g = torch.Generator().manual_seed(N + D)
+    x = torch.randn(N, D, generator=g, dtype=torch.float64) * 2 + 0.5
+    ln = torch.nn.LayerNorm(D).double()
+    with torch.no_grad():
+        ln.weight.copy_(1 + 0.3 * torch.randn(D, generator=g, dtype=torch.float64))
+        ln.bias.copy_(0.2 * torch.randn(D, generator=g, dtype=torch.float64))
+    dy = torch.randn(N, D, generator=g, dtype=torch.float64)
+    x64 = x.clone().requires_grad_(True)
+    y64 = F.layer_norm(x64, (D,), ln.weight, ln.bias, ln.eps)
+    y64.backward(dy)
+    ln32 = torch.nn.LayerNorm(D).to(device)
+    with torch.no_grad():
+        ln32.weight.copy_(ln.weight.float())
+        ln32.bias.copy_(ln.bias.float())
+    x32 = x.float().to(device).requires_grad_(True)
+    y = dense.layer_norm(x32, ln32)
+    assert "SmallLayerNorm" in type(y.grad_fn).__name__
+    y.backward(dy.float().to(device))
+    torch.testing.assert_close(y.double().cpu(), y64.detach(), rtol=0, atol=2e-5 * y64.abs().max().item() + 1e-5)
+    for got, ref, nm in ((x32.grad, x64.grad, "dx"), (ln32.weight.grad, ln.weight.grad, "dgamma"),
+                         (ln32.bias.grad, ln.bias.grad, "dbeta")):
+        err = (got.double().cpu() - ref).norm().item()
+        assert err <= 1e-4 * ref.norm().item() + 1e-6, f"{nm}: {err:.3e} vs |ref| {ref.norm().item():.3e}"
