@@ -42,6 +42,8 @@ def splitk_wgrad(dy, x):
     if R < 16384 and M * N > 262144:
         return dy.T @ x  # camera 1024x1024 weights: already 256 output tiles, no split
     B = max(1, min(_MAX_SLICES, R // _MIN_CHUNK))
+    if B == 1:
+        return dy.T @ x
     R0 = (R // B) * B
     dW = _colsum(torch.bmm(dy[:R0].reshape(B, R0 // B, M).transpose(1, 2), x[:R0].reshape(B, R0 // B, N))
                  .reshape(B, M * N)).view(M, N)
@@ -51,19 +53,29 @@ def splitk_wgrad(dy, x):
 
 
 class RowLinearFn(torch.autograd.Function):
+    """y = x W^T + b on device rows: the weight gradient split-K over tall inputs, the bias
+    gradient a column sum deferred into the end-of-backward batch (_native.param_colsum; aten's
+    addmm backward runs a reduce plus a memset launch per Linear)."""
+
     @staticmethod
     def forward(ctx, x, W, b):
+        from . import _native
         ctx.save_for_backward(x, W)
         ctx.has_b = b is not None
+        ctx.defer = _native.defer_token(b) if b is not None else False
         return F.linear(x, W, b)
 
     @staticmethod
     def backward(ctx, dy):
+        from . import _native
         x, W = ctx.saved_tensors
         dy = dy.contiguous()
         dx = dy @ W if ctx.needs_input_grad[0] else None
         dW = splitk_wgrad(dy, x.contiguous()) if ctx.needs_input_grad[1] else None
-        db = _colsum(dy) if ctx.has_b and ctx.needs_input_grad[2] else None
+        db = None
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            # a view of the (possibly deferred) sum: AccumulateGrad adopts it (edge_block.replicated_dbias)
+            db = (_native.param_colsum(dy, ctx.defer) if dy.shape[0] <= 4096 else _colsum(dy))[:]
         return dx, dW, db
 
 
@@ -348,7 +360,7 @@ def _gvec_ok(x, k):
 def linear(x, lin):
     if _gvec_ok(x, lin.in_features):
         return GlobalLinearFn.apply(x, None, None, lin.weight, lin.bias, None, 0.0, False)
-    if x.is_cuda and x.dim() == 2 and x.shape[0] >= SPLITK_MIN_ROWS and torch.is_grad_enabled():
+    if x.is_cuda and x.dim() == 2 and x.shape[0] > 0 and torch.is_grad_enabled():
         return RowLinearFn.apply(x, lin.weight, lin.bias)
     return F.linear(x, lin.weight, lin.bias)
 

@@ -1144,7 +1144,7 @@ class GraphAttnSfMNet(Module):
             pred["depths"] = SparseMat(self.depth_head(P), x.indices, x.cam_per_pts, x.pts_per_cam,
                                        [x.shape[0], x.shape[1], 1])
         if self.view_head_enabled:
-            out = self.extract_view_outputs(self.view_head(F.relu(view)))
+            out = self.extract_view_outputs(dense.sequential(self.view_head, F.relu(view)))
             shard = edges.plans.get("_shard")
             if _cam_sharded(shard):  # this rank's camera rows -> all cameras (one all-gather)
                 from .distributed import gather_rows
