@@ -30,6 +30,39 @@ def _glorot_(t):
         t.uniform_(-a, a)
 
 
+
+class ZeroTargetRowsFn(torch.autograd.Function):
+    """lin_r applied to the reference's zero target features (dataset_utils.py:569-571), broadcast
+    over n targets: lin_r(0) == lin_r.bias exactly.  Backward: the bias gradient is the column sum
+    of the targets' gradient, deferred into the end-of-backward batched parameter sums (aten ran a
+    one-workgroup reduce over the n rows, 21 us for a 25k-point shard, plus a GEMM and a reduce for
+    the zero row); the weight gets its zero gradient, as in the reference."""
+
+    @staticmethod
+    def forward(ctx, W, b, n):
+        from . import _native
+        ctx.w_shape = W.shape
+        ctx.defer = _native.defer_token(b)
+        return b.view(1, -1).expand(n, -1)
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import _native
+        g = g.contiguous()
+        if g.shape[0] <= 4096:
+            db = _native.param_colsum(g, ctx.defer)[:]  # a view: AccumulateGrad adopts it
+        else:
+            db = dense._colsum(g)
+        return torch.zeros(ctx.w_shape, dtype=g.dtype, device=g.device), db, None
+
+
+def zero_target_rows(lin_r, n, like):
+    """XR of n targets whose features are the reference's zeros: lin_r(0) broadcast."""
+    if like.is_cuda and lin_r.bias is not None and torch.is_grad_enabled() and n > 0:
+        return ZeroTargetRowsFn.apply(lin_r.weight, lin_r.bias, n)
+    zero = torch.zeros((1, lin_r.in_features), dtype=like.dtype, device=like.device)
+    return lin_r(zero).expand(n, -1)
+
 class GATv2Conv(torch.nn.Module):
     def __init__(self, in_channels, out_channels, heads=1, concat=True, negative_slope=0.2, dropout=0.0,
                  add_self_loops=True, edge_dim=None, fill_value="mean", bias=True, share_weights=False,
@@ -82,8 +115,7 @@ class GATv2Conv(torch.nn.Module):
             # one zero row through lin_r (== its bias) broadcast over the targets: lin_r.weight
             # still receives its (zero) gradient, as in the reference, so train.py:137's
             # torch.cat over every p.grad keeps working.
-            zero = torch.zeros((1, self.in_channels), dtype=x_src.dtype, device=x_src.device)
-            XR = self.lin_r(zero).expand(plan.num_targets, -1)
+            XR = zero_target_rows(self.lin_r, plan.num_targets, x_src)
         else:
             XR = dense.linear(x_tgt, self.lin_r)
         return gat_attention(XL, XR, self.att, self._bias(XL), plan, self.heads, self.negative_slope)

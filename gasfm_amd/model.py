@@ -30,7 +30,7 @@ from . import _native, dense, edge_block, edge_ops, point_block, view_block
 from .attention import AttnPlan, GatAttentionFn, gat_attention
 from .edge_block import (Block0EpilogueFn, Block0PrologueFn, DualAttentionFn, EdgeCamFn, EdgeEpilogueFn,
                          EdgePrologueFn, PendingEpilogue, SeamFn, materialize)
-from .gatv2 import GATv2Conv
+from .gatv2 import GATv2Conv, zero_target_rows
 
 
 # Edge prologue with the camera attention fused in (edge_block.EdgeCamFn, csrc/edge_cam.hip) for the
@@ -164,8 +164,7 @@ class _NodeAggregation(Module):
         """XR = lin_r(x_agg) of the destination nodes (lin_r(0) broadcast when stateless)."""
         conv = self.graph_conv
         if prev is None:
-            zero = torch.zeros((1, conv.in_channels), device=conv.lin_r.weight.device)
-            return conv.lin_r(zero).expand(num_targets, -1)
+            return zero_target_rows(conv.lin_r, num_targets, conv.lin_r.weight)
         return dense.linear(dense.sequential(getattr(self, self._state_key), prev), conv.lin_r)
 
     def tail(self, x, prev, exch=None):
@@ -302,7 +301,7 @@ def _target_row(conv, x_tgt, ref, n=1):
     """XR of a one-target GATv2 conv (n targets for a SceneBatch): lin_r(x_tgt), or lin_r(0) (== its
     bias) for the reference's zero target features when stateless (dataset_utils.py:569-571)."""
     if x_tgt is None:
-        return conv.lin_r(torch.zeros((1, conv.in_channels), device=ref.device)).expand(n, -1)
+        return zero_target_rows(conv.lin_r, n, ref)
     return dense.linear(x_tgt, conv.lin_r)
 
 
