@@ -36,6 +36,15 @@ def _colsum(a):
     return _native.colsum(a)
 
 
+def bias_colsum(dy, defer):
+    """A bias gradient (column sum of dy [rows, n]) as a VIEW of its sum tensor: deferred into the
+    end-of-backward batched parameter sums (_native.param_colsum) for camera-sized inputs, at once
+    through _colsum's tall kernel for edge / point-sized ones.  AccumulateGrad adopts a view; it
+    would copy a pending (not yet filled) sum tensor itself (edge_block.replicated_dbias)."""
+    from . import _native
+    return (_native.param_colsum(dy, defer) if dy.shape[0] <= 4096 else _colsum(dy))[:]
+
+
 def splitk_wgrad(dy, x):
     R, M = dy.shape
     N = x.shape[1]
@@ -67,15 +76,11 @@ class RowLinearFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        from . import _native
         x, W = ctx.saved_tensors
         dy = dy.contiguous()
         dx = dy @ W if ctx.needs_input_grad[0] else None
         dW = splitk_wgrad(dy, x.contiguous()) if ctx.needs_input_grad[1] else None
-        db = None
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            # a view of the (possibly deferred) sum: AccumulateGrad adopts it (edge_block.replicated_dbias)
-            db = (_native.param_colsum(dy, ctx.defer) if dy.shape[0] <= 4096 else _colsum(dy))[:]
+        db = bias_colsum(dy, ctx.defer) if ctx.has_b and ctx.needs_input_grad[2] else None
         return dx, dW, db
 
 

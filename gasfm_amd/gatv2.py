@@ -47,13 +47,8 @@ class ZeroTargetRowsFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        from . import _native
         g = g.contiguous()
-        if g.shape[0] <= 4096:
-            db = _native.param_colsum(g, ctx.defer)[:]  # a view: AccumulateGrad adopts it
-        else:
-            db = dense._colsum(g)
-        return torch.zeros(ctx.w_shape, dtype=g.dtype, device=g.device), db, None
+        return torch.zeros(ctx.w_shape, dtype=g.dtype, device=g.device), dense.bias_colsum(g, ctx.defer), None
 
 
 def zero_target_rows(lin_r, n, like):
