@@ -365,7 +365,8 @@ def _gvec_ok(x, k):
 def linear(x, lin):
     if _gvec_ok(x, lin.in_features):
         return GlobalLinearFn.apply(x, None, None, lin.weight, lin.bias, None, 0.0, False)
-    if x.is_cuda and x.dim() == 2 and x.shape[0] > 0 and torch.is_grad_enabled():
+    if (x.is_cuda and x.dim() == 2 and x.shape[0] > 0 and x.dtype == torch.float32 and lin.weight.dtype == x.dtype
+            and torch.is_grad_enabled()):
         return RowLinearFn.apply(x, lin.weight, lin.bias)
     return F.linear(x, lin.weight, lin.bias)
 
