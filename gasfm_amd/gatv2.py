@@ -53,7 +53,8 @@ class ZeroTargetRowsFn(torch.autograd.Function):
 
 def zero_target_rows(lin_r, n, like):
     """XR of n targets whose features are the reference's zeros: lin_r(0) broadcast."""
-    if like.is_cuda and lin_r.bias is not None and torch.is_grad_enabled() and n > 0:
+    if (like.is_cuda and lin_r.bias is not None and lin_r.bias.dtype == torch.float32 and torch.is_grad_enabled()
+            and n > 0):
         return ZeroTargetRowsFn.apply(lin_r.weight, lin_r.bias, n)
     zero = torch.zeros((1, lin_r.in_features), dtype=like.dtype, device=like.device)
     return lin_r(zero).expand(n, -1)
