@@ -176,6 +176,41 @@ def cpu_baseline(sample_scale, threads):
                       f"stands for config 4 (linear in E: profiles/r2_cpu_baseline_scaling.json)"}
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launcher_argv(gpus, argv, port):
+    """The torchrun command that starts ``gpus`` ranks of this bench on one node (one process per
+    GPU, RCCL), with the caller's own arguments passed through unchanged."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(gpus, argv, run=None):
+    """``bench.py --gpus N`` (N > 1) started without a launcher: run torchrun with N ranks as a CHILD
+    process (never exec: nothing here has touched the GPU yet, and the ranks initialise it
+    themselves), its stdout / stderr inherited, and return its exit code."""
+    import subprocess
+    run = run or subprocess.call
+    return run(rank_launcher_argv(gpus, argv, _free_port()))
+
+
+def world_from_env(gpus):
+    """(rank, world, local_rank) from the launcher's environment.  Under a launcher, --gpus must
+    equal WORLD_SIZE: a mismatch is an error (exit 2), never a silent 1-GPU run."""
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    if world != gpus:
+        log(f"error: --gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+        sys.exit(2)
+    return rank, world, local_rank
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -201,11 +236,9 @@ def main():
                          "local copies (timing of the per-rank compute; numerically meaningless)")
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local_rank = int(os.environ.get("LOCAL_RANK", 0))
-    if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    rank, world, local_rank = world_from_env(args.gpus)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist_on = world > 1 or args.dist
@@ -213,6 +246,9 @@ def main():
     cams = not args.no_cam_shard
     if dist_on:
         torch.distributed.init_process_group("nccl", device_id=dev)
+        if torch.distributed.get_world_size() != world:  # n_gpus is the rank count RCCL reports
+            log(f"error: RCCL reports {torch.distributed.get_world_size()} ranks, WORLD_SIZE {world}")
+            sys.exit(2)
         log(f"[rank {rank}] process group up (world {world})")
 
     import gasfm_amd

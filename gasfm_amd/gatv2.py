@@ -43,7 +43,9 @@ class ZeroTargetRowsFn(torch.autograd.Function):
         from . import _native
         ctx.w_shape = W.shape
         ctx.defer = _native.defer_token(b)
-        return b.view(1, -1).expand(n, -1)
+        # a fresh row, broadcast: the output must not alias the bias parameter (a later in-place
+        # optimizer step would trip the saved-tensor version checks of its consumers)
+        return b.detach().view(1, -1).clone().expand(n, -1)
 
     @staticmethod
     def backward(ctx, g):

@@ -8,7 +8,9 @@ conf) in ~34 kernel launches and reaches ~2.9 TB/s: 1.39 ms of a 13.7 ms capture
 in ONE launch from a cached table of (p, grad, exp_avg, exp_avg_sq) pointers; when the gradient tensors
 are new ones (zero_grad(set_to_none=True) between steps, or StaticTrainer's per-bucket gradients) only
 their pointer column is rewritten (one small host-to-device copy).
-Supported: fp32 CUDA parameters, amsgrad=False, maximize=False; anything else raises (no fallback).
+Supported: fp32 CUDA parameters, amsgrad=False, maximize=False, a float lr (a Tensor lr raises: it
+would need a host read per step); anything else raises (no fallback).  Parameters whose .grad is None
+are skipped, as torch.optim.Adam skips them (frozen or unused parameters keep their state).
 """
 import numpy as np
 import torch
@@ -31,8 +33,12 @@ class Adam(torch.optim.Optimizer):
                  maximize=False):
         if amsgrad or maximize:
             raise NotImplementedError("gasfm_amd.optim.Adam: amsgrad / maximize are not supported")
+        if torch.is_tensor(lr):
+            raise TypeError("gasfm_amd.optim.Adam: a Tensor lr is not supported (pass a float)")
         if not 0.0 <= lr or not 0.0 <= eps or not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0:
             raise ValueError(f"gasfm_amd.optim.Adam: lr={lr}, betas={betas}, eps={eps}")
+        if not 0.0 <= weight_decay:
+            raise ValueError(f"gasfm_amd.optim.Adam: invalid weight_decay value: {weight_decay}")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self._tables = {}
 
@@ -41,9 +47,6 @@ class Adam(torch.optim.Optimizer):
         int64 [n, 5] (p, g, m, v, numel) and the chunk table.  A later step whose gradient tensors are
         other tensors (p.grad = None between steps) only rewrites column 1 (``_regrad``)."""
         for p, g in zip(ps, grads):
-            if g is None:
-                raise RuntimeError("gasfm_amd.optim.Adam: every parameter of a group needs a gradient "
-                                   "(or none of them)")
             if not p.is_cuda or p.dtype != torch.float32 or p.is_sparse:
                 raise TypeError("gasfm_amd.optim.Adam: fp32 dense CUDA parameters only")
             if not p.is_contiguous():
@@ -89,24 +92,35 @@ class Adam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         for gi, group in enumerate(self.param_groups):
-            ps = group["params"]
-            grads = [p.grad for p in ps]
-            if all(g is None for g in grads):
+            if torch.is_tensor(group["lr"]):
+                raise TypeError("gasfm_amd.optim.Adam: a Tensor lr is not supported (pass a float)")
+            live = [p for p in group["params"] if p.grad is not None]  # torch skips grad-less params
+            if not live:
                 continue
-            key = (gi, tuple(map(id, ps)))
-            t = self._tables.get(key)
-            if t is None:
-                t = self._build(ps, grads)
-                if len(self._tables) > 16:
-                    self._tables.clear()
-                self._tables[key] = t
-            if t["grads"] is None or any(a is not b for a, b in zip(grads, t["grads"])):
-                self._regrad(t, grads)
-            t["step"] += 1  # in place: every parameter's state["step"]
-            b1, b2 = group["betas"]
-            _native.adam_step(t["tensors"], t["chunks"], t["n"], group["lr"], b1, b2, group["eps"],
-                              group["weight_decay"], int(t["step"]), ps[0])
-            # the kernel wrote p in place behind autograd's back: bump the version counters, as an in-place
-            # torch op would (version-keyed caches -- e.g. dense.weight_shadow's bf16 shadows -- see it)
-            torch.autograd.graph.increment_version(ps)
+            key = (gi, tuple(map(id, live)))
+            tabs = self._tables.get(key)
+            if tabs is None:
+                # another subset of this group has gradients now: its cached tables' shared step
+                # counters no longer describe every member, so they go; torch keeps one counter per
+                # parameter, so the parameters are split by their current step (one launch each)
+                for k in [k for k in self._tables if k[0] == gi]:
+                    del self._tables[k]
+                by_step = {}
+                for p in live:
+                    by_step.setdefault(int(self.state[p]["step"]) if self.state[p] else 0, []).append(p)
+                tabs = [self._build(ps, [p.grad for p in ps]) for ps in by_step.values()]
+                self._tables[key] = tabs
+            for t in tabs:
+                ps = t["keep"][0]
+                grads = [p.grad for p in ps]
+                if t["grads"] is None or any(a is not b for a, b in zip(grads, t["grads"])):
+                    self._regrad(t, grads)
+                t["step"] += 1  # in place: every parameter's state["step"]
+                b1, b2 = group["betas"]
+                _native.adam_step(t["tensors"], t["chunks"], t["n"], group["lr"], b1, b2, group["eps"],
+                                  group["weight_decay"], int(t["step"]), ps[0])
+                # the kernel wrote p in place behind autograd's back: bump the version counters, as an
+                # in-place torch op would (version-keyed caches -- e.g. dense.weight_shadow's bf16
+                # shadows -- see it)
+                torch.autograd.graph.increment_version(ps)
         return loss

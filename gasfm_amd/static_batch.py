@@ -599,6 +599,11 @@ class StaticTrainer:
             self.opt_graphs += 1
         else:
             opt.step()
+        self._refresh_if_bf16()
+
+    def _refresh_if_bf16(self):
+        """Re-round the bf16 weight shadows after every optimizer step, captured or eager: a replayed
+        graph reads dense._SHADOWS without a version check."""
         if getattr(self.net, "_projection_precision", "fp32") == "bf16":
             self.net.refresh_weight_shadows()
 
@@ -630,6 +635,7 @@ class StaticTrainer:
             loss, errs = self._eager(datas, inputs)
             if self.optimizer is not None:
                 self.optimizer.step()
+                self._refresh_if_bf16()
             if not read_errors:
                 errs = torch.tensor([[e, 1.0] for e in errs], dtype=torch.float32)
             return loss, errs

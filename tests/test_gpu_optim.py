@@ -83,3 +83,28 @@ def test_adam_bumps_versions(device):
     v0 = p._version
     Adam([p], lr=0.1).step()
     assert p._version > v0 and float(p.detach()[0]) < 1.0
+
+
+def test_adam_skips_params_without_grad(device):
+    """parameters whose .grad is None are skipped as torch.optim.Adam skips them (their
+    state stays empty / at its step), and a parameter that gets a gradient later starts its own step
+    count; against torch.optim.Adam over 4 steps with a changing subset of gradients."""
+    gen = torch.Generator().manual_seed(11)
+    shapes = [(64, 33), (17,), (5, 5), (4097,)]
+    ref = [torch.randn(s, generator=gen).to(device).requires_grad_(True) for s in shapes]
+    got = [r.detach().clone().requires_grad_(True) for r in ref]
+    o_ref = torch.optim.Adam(ref, lr=1e-2, weight_decay=0.01)
+    o_got = Adam(got, lr=1e-2, weight_decay=0.01)
+    subsets = [(0, 1), (0, 1), (0, 1, 2, 3), (1, 3)]
+    for sub in subsets:
+        for i, (a, b) in enumerate(zip(ref, got)):
+            if i in sub:
+                g = torch.randn(a.shape, generator=gen).to(device)
+                a.grad, b.grad = g.clone(), g.clone()
+            else:
+                a.grad = b.grad = None
+        o_ref.step()
+        o_got.step()
+    for a, b in zip(ref, got):
+        torch.testing.assert_close(b, a, rtol=2e-6, atol=1e-7)
+        assert int(o_got.state[b]["step"]) == int(o_ref.state[a]["step"])

@@ -247,3 +247,39 @@ def test_static_trainer_bf16_shadows_follow_the_optimizer(device, monkeypatch):
     # an eager forward re-rounds the changed weights by itself (gasfm Adam bumps their versions)
     forward_batch(net, b)
     assert shadows_current()
+
+
+def test_static_trainer_bf16_shadows_after_eager_fallback(device, monkeypatch):
+    """the eager-fallback optimizer step re-rounds the bf16 shadows too.  Expressible batch
+    (captured), then a batch that falls back to the eager union, then the captured bucket again: after
+    each step every live shadow equals its weight in bf16, and the last replay equals the eager union
+    on the updated weights."""
+    from gasfm_amd import dense
+    from gasfm_amd.optim import Adam
+    monkeypatch.setattr(static_batch, "MAX_WASTE", 10.0)
+    torch.manual_seed(12)
+    conf = _conf()
+    net = gasfm_amd.GraphAttnSfMNet(conf).to(device)
+    net.set_projection_precision("bf16")
+    lossf = ESFMLoss(conf)
+    trainer = static_batch.StaticTrainer(net, lossf, optimizer=Adam(net.parameters(), lr=1e-2))
+    a, b = _scenes(device, (14, 16, 18), seed=13), _scenes(device, (12, 13, 15), seed=14)
+
+    def shadows_current():
+        live = [(r(), sh) for r, sh, _, _ in dense._SHADOWS.values() if r() is not None]
+        assert live
+        return all(torch.equal(sh, w.detach().to(torch.bfloat16)) for w, sh in live)
+
+    trainer.step(a)
+    assert trainer.captures == 1 and shadows_current()
+    monkeypatch.setattr(static_batch, "S2G_PIECES", 10 ** 6)
+    trainer.step(b)  # the eager fallback, then Adam
+    assert trainer.eager_steps == 1
+    assert shadows_current()
+    monkeypatch.setattr(static_batch, "S2G_PIECES", 128)
+    trainer.optimizer = None
+    loss, _ = trainer.step(a)  # the bucket captured on step 1, replayed on the new weights
+    assert trainer.captures == 1
+    net.zero_grad(set_to_none=True)
+    ref = sum(lossf(p, d) for p, d in zip(forward_batch(net, a), a))
+    assert abs(float(loss) - float(ref)) <= 1e-4 * abs(float(ref)), (float(loss), float(ref))

@@ -38,3 +38,7 @@ def test_adam_rejects_options():
         Adam([p], amsgrad=True)
     with pytest.raises(ValueError):
         Adam([p], betas=(1.0, 0.999))
+    with pytest.raises(ValueError):
+        Adam([p], weight_decay=-1e-4)  # torch.optim.Adam rejects it too
+    with pytest.raises(TypeError):
+        Adam([p], lr=torch.tensor(1e-3))  # a Tensor lr would need a host read per step
