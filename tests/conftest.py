@@ -18,7 +18,7 @@ def pytest_configure(config):
 
 # multi-process and subprocess tests (spawned ranks, torchrun children) run last: under -x a
 # failure there must not keep the single-process kernel / model / config parity suites from running
-_RUN_LAST = ("test_distributed.py",)
+_RUN_LAST = ("test_distributed.py", "test_dist_train.py")
 
 
 def pytest_collection_modifyitems(config, items):
