@@ -147,7 +147,7 @@ def cpu_model():
 # 0.05 .. 1.0 (profiles/r2_cpu_baseline_scaling.json): the full config-4 workload runs within
 # 16 % of the 10 % sample's edges/s (51.3k vs 59.4k edges/s, 78 s per full step on 16 EPYC 9575F
 # threads), so the bench times the sample (a ~16 % optimistic CPU number) and reports its edges/s.
-def cpu_baseline(sample_scale, threads):
+def cpu_baseline(sample_scale, threads, reps=4):
     """Oracle (reference + PyG op sequence, torch CPU fp32) fwd+bwd edges/s on a sample scene."""
     import gasfm_amd
     from gasfm_amd import synthetic
@@ -160,7 +160,7 @@ def cpu_baseline(sample_scale, threads):
     sd = {k: v.detach().clone().requires_grad_(True) for k, v in net.state_dict().items()}
     gasfm_ref.PYG_FAITHFUL = True
     times = []
-    for it in range(4):  # 1 warm-up + median of 3
+    for it in range(1 + reps):  # 1 warm-up + median of reps
         t0 = time.perf_counter()
         out = gasfm_ref.forward(sd, vals, g, dtype=torch.float32)
         (out["Ps_norm"].sum() + out["pts3D"].sum()).backward()
@@ -169,9 +169,12 @@ def cpu_baseline(sample_scale, threads):
             v.grad = None
     gasfm_ref.PYG_FAITHFUL = False
     t = float(np.median(times[1:]))
+    lo, hi = sc.num_edges / max(times[1:]), sc.num_edges / min(times[1:])
     return {"value": sc.num_edges / t, "unit": "edges/s", "cores": threads, "kind": "port",
+            "range": [lo, hi],
             "sample": f"scaled config 4 (m={sc.m}, n={sc.n}, E={sc.num_edges}), 12 blocks, fp32, fwd+bwd, "
-                      f"median of 3 after 1 warm-up, {t:.2f} s/step, "
+                      f"median of {reps} after 1 warm-up ({lo / 1e3:.1f}k-{hi / 1e3:.1f}k edges/s over the {reps}), "
+                      f"{t:.2f} s/step, "
                       f"torch {torch.__version__} CPU threads={threads} on {cpu_model()}; edges/s of the sample "
                       f"stands for config 4 (linear in E: profiles/r2_cpu_baseline_scaling.json)"}
 

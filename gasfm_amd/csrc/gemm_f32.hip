@@ -13,10 +13,14 @@
 //     64 distinct banks), a register ring of kStages K tiles in flight per thread;
 //   - exact fp32 products on v_mfma_f32_16x16x4_f32 (same rounding as a k-ordered fma chain per
 //     4-step), fp32 sums in a fixed order: deterministic;
-//   - two tile shapes: 64 x 64 per workgroup (2 x 2 waves of 32 x 32) for large M; for M <= 256,
-//     32 x 32 per workgroup with the K steps dealt round-robin to its 4 waves and their four
-//     32 x 32 partials summed in wave order through LDS at the end (4x the workgroups of the
-//     large tile at the same per-wave work);
+//   - M x N <= 256k: 32 x 32 per workgroup with the K steps dealt round-robin to its 4 waves and
+//     their four 32 x 32 partials summed in wave order through LDS at the end;
+//   - larger (round 6, gemm_f32_d_kernel below): 64 x 64 per workgroup of 8 waves, operand tiles
+//     global -> LDS directly (global_load_lds, XOR-swizzled images), 64-wide K chunks in a 3-deep
+//     ring, one ds_read_b128 per four MFMA operands.  tools/gemm_bench.py at m = 1000 (MI355X,
+//     back-to-back launches): 27.3 / 27.4 / 26.9 us for x W^T / dy W / dy^T x against the round-3
+//     register-staged 64 x 64 kernel's 34.0 / 39.3 / 42.5 us and hipBLASLt's 25.9 / 25.2 / 27.9 us
+//     (profiles/r6_gemm_f32.txt); hipBLASLt stays the model's default at m = 1000 (view_block.py);
 //   - XCD-aware tile order as in gemm_bf16.hip.
 #include <hip/hip_runtime.h>
 
@@ -207,6 +211,201 @@ __global__ __launch_bounds__(kThreadsF) void gemm_f32_kernel(int M, int N, int K
     }
 }
 
+// The large-tile path (M x N > 256k: the m = 1000 camera products; round 6).  64 x 64 per
+// workgroup of NWV = 8 waves: wave w owns the 32 x 32 quadrant w % 4 and the k split w / 4 of every
+// chunk (the two waves of a quadrant share a SIMD); the splits are summed through LDS at the end.
+// The operand tiles go global -> LDS with global_load_lds
+// (16 B per lane, no VGPR staging, no ds_write), in a ring of DS stages (DS - 1 K chunks in flight),
+// one barrier per chunk.  The lanes' load order is the LDS image, so the layouts are chosen by
+// which global 16-byte chunk each lane fetches:
+//   k-contiguous operand (x, W of x W^T): [64 rows][8 chunks of 4 k], chunk kc of row r at slot
+//     kc ^ (r & 7) (8 consecutive rows' b128 reads of one kc hit 8 distinct bank quads); a lane's
+//     four k of a 16x16x4 quad step are ONE ds_read_b128 (k = 8 fq + 4 kh + t as in the q kernel);
+//   row-contiguous operand (W of dy W, dy^T of dy^T x): [32 k][16 chunks of 4 rows], chunk c of
+//     k row kr at slot c ^ (((kr >> 3) & 1) << 2) (the two k rows 8 apart that lanes 0-15 and
+//     16-31 read in one pass land 16 banks apart); one ds_read_b32 per MFMA operand.
+template <bool AM, bool BNC, int DS, int KB, int NWV>
+__global__ __launch_bounds__(64 * NWV) void gemm_f32_d_kernel(int M, int N, int K, const float* A, int64_t sAm,
+                                                         int64_t sAk, const float* B, int64_t sBk, int64_t sBn,
+                                                         const float* Cin, int64_t ldCin,
+                                                         const float* __restrict__ bias, float* C, int64_t ldC) {
+  typedef __attribute__((address_space(3))) void* lds_vp;
+  typedef const __attribute__((address_space(1))) void* glb_vp;
+  constexpr int BM = 64, BN = 64, TILE = 64 * KB;  // floats per operand tile
+  constexpr int CPR = KB / 4, NL = KB * 16 / (NWV * 64);  // 16-B chunks per k row; loads per operand per wave
+  constexpr int KS = NWV / 4, NH = KB / (16 * KS);  // k splits (waves per quadrant); 16-wide k groups per wave
+  constexpr int SW = KB / 4;  // k distance between the lanes fq and fq + 1 (row-contiguous swizzle bit)
+  __shared__ __attribute__((aligned(16))) float lds[DS * 2 * TILE];
+  const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN, nt = ntm * ntn;
+  int lt = blockIdx.x;
+  if (nt % kXcdF == 0) lt = (lt % kXcdF) * (nt / kXcdF) + lt / kXcdF;
+  const int gsz = kGroupMF * ntn, g = lt / gsz, gm0 = g * kGroupMF;
+  const int gm = ntm - gm0 < kGroupMF ? ntm - gm0 : kGroupMF;
+  const int tm = gm0 + (lt % gsz) % gm, tn = (lt % gsz) / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kh = wave >> 2, q = wave & 3;  // k split, quadrant
+  const int wm = (q >> 1) * 32, wn = (q & 1) * 32;
+  // this lane's fetch: (tile row, k offset within the chunk) of the 16 bytes it loads, per operand
+  // load l (0 .. NL - 1) of this lane: (tile row, k offset within the chunk) of its 16 bytes
+  auto coords = [&](bool rowc, int l, int& r, int& k) {
+    if (!rowc) {  // k-contiguous: [64 rows][CPR slots], slot holds chunk slot ^ (row & 7)
+      const int idx = (wave * NL + l) * 64 + lane;
+      r = idx / CPR;
+      k = 4 * ((idx % CPR) ^ (r & 7));
+    } else {      // row-contiguous: [KB k rows][16 slots of 4 rows], slot holds chunk slot ^ swz(k)
+      const int idx = (wave * NL + l) * 64 + lane;
+      k = idx / 16;
+      r = 4 * ((idx % 16) ^ (((k / SW) & 1) << 2));
+    }
+  };
+  int ra[NL], ka[NL], rb[NL], kb[NL];
+  int64_t aoff[NL], boff[NL];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    coords(AM, l, ra[l], ka[l]);
+    coords(BNC, l, rb[l], kb[l]);
+    // out-of-range rows / k read a clamped in-range address: their products only reach C entries
+    // that are never stored (rows >= M, cols >= N) or multiply a zeroed partner (k >= K, below)
+    aoff[l] = int64_t(m0 + ra[l] < M ? m0 + ra[l] : M - (AM ? 4 : 1)) * sAm;
+    boff[l] = int64_t(n0 + rb[l] < N ? n0 + rb[l] : N - (BNC ? 4 : 1)) * sBn;
+  }
+  const int kmaxA = AM ? K - 1 : K - 4, kmaxB = BNC ? K - 1 : K - 4;
+  const int nk = (K + KB - 1) / KB;
+  auto issue = [&](int t) {
+    const int tt = t < nk ? t : nk - 1;  // past the end: re-read the last chunk (never consumed)
+    const int k0 = tt * KB;
+    float* sa = lds + (t % DS) * 2 * TILE;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int kA = k0 + ka[l] < kmaxA ? k0 + ka[l] : kmaxA, kB = k0 + kb[l] < kmaxB ? k0 + kb[l] : kmaxB;
+      __builtin_amdgcn_global_load_lds((glb_vp)(A + (aoff[l] + int64_t(kA) * sAk)),
+                                       (lds_vp)(sa + (wave * NL + l) * 256), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_vp)(B + (boff[l] + int64_t(kB) * sBk)),
+                                       (lds_vp)(sa + TILE + (wave * NL + l) * 256), 16, 0, 0);
+    }
+  };
+  f32x4f acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < DS - 1; ++s) issue(s);
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int t = 0; t < nk; ++t) {
+    // chunk t landed for this wave (DS - 2 younger chunks may still fly), then for every wave
+    // (a bare s_barrier: __syncthreads' release fence would add vmcnt(0), draining the ring)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NL * (DS - 2)) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(t + DS - 1);  // into the slot chunk t - 1 used: every wave is past it (the barrier)
+    const float* sa = lds + (t % DS) * 2 * TILE;
+    const float* sb = sa + TILE;
+    const bool kdead = (t + 1) * KB > K;  // the last chunk of a K that is not a multiple of KB
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      const int kc = NH * (KS * fq + kh) + h;  // this lane's k chunk
+      f32x4f af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = wm + 16 * i + fr;
+        if constexpr (!AM) {
+          af[i] = *reinterpret_cast<const f32x4f*>(sa + r * KB + 4 * (kc ^ (r & 7)));
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int kr = 4 * kc + u;
+            af[i][u] = sa[kr * 64 + 4 * ((r >> 2) ^ (((kr / SW) & 1) << 2)) + (r & 3)];
+          }
+        }
+        const int c = wn + 16 * i + fr;
+        if constexpr (!BNC) {
+          bf[i] = *reinterpret_cast<const f32x4f*>(sb + c * KB + 4 * (kc ^ (c & 7)));
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int kr = 4 * kc + u;
+            bf[i][u] = sb[kr * 64 + 4 * ((c >> 2) ^ (((kr / SW) & 1) << 2)) + (c & 3)];
+          }
+        }
+      }
+      if (kdead) {  // zero A's k >= K (clamped reads hold real values)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool ok = t * KB + 4 * kc + u < K;
+#pragma unroll
+          for (int i = 0; i < 2; ++i) af[i][u] = ok ? af[i][u] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][u], bf[j][u], acc[i][j], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the re-read chunks past the end
+  __syncthreads();
+  // the KS k splits of each quadrant, summed in split order through LDS (free after the loop)
+  if (kh > 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lds[(((kh - 1) * 4 + q) * 16 + (i * 2 + j) * 4 + r) * 64 + lane] = acc[i][j][r];
+  }
+  __syncthreads();
+  if (kh > 0) return;
+#pragma unroll
+  for (int x = 1; x < KS; ++x)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += lds[(((x - 1) * 4 + q) * 16 + (i * 2 + j) * 4 + r) * 64 + lane];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn + 16 * j + (lane & 15);
+      if (col >= N) continue;
+      const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + 16 * i + (lane >> 4) * 4 + r;
+        if (row < M) {
+          float v = acc[i][j][r] + bv;
+          if (Cin) v += Cin[int64_t(row) * ldCin + col];
+          C[int64_t(row) * ldC + col] = v;
+        }
+      }
+    }
+}
+
+template <int DS, int KB, int NWV>
+void launch_f32_d(bool am, bool bn, int M, int N, int K, const float* A, int64_t sAm, int64_t sAk, const float* B,
+                  int64_t sBk, int64_t sBn, const float* Cin, int64_t ldCin, const float* bias, float* C,
+                  int64_t ldC, hipStream_t st) {
+  const dim3 grid(((N + 63) / 64) * ((M + 63) / 64));
+  if (am && bn)
+    hipLaunchKernelGGL((gemm_f32_d_kernel<true, true, DS, KB, NWV>), grid, dim3(64 * NWV), 0, st, M, N, K, A, sAm, sAk, B, sBk,
+                       sBn, Cin, ldCin, bias, C, ldC);
+  else if (am)
+    hipLaunchKernelGGL((gemm_f32_d_kernel<true, false, DS, KB, NWV>), grid, dim3(64 * NWV), 0, st, M, N, K, A, sAm, sAk, B, sBk,
+                       sBn, Cin, ldCin, bias, C, ldC);
+  else if (bn)
+    hipLaunchKernelGGL((gemm_f32_d_kernel<false, true, DS, KB, NWV>), grid, dim3(64 * NWV), 0, st, M, N, K, A, sAm, sAk, B, sBk,
+                       sBn, Cin, ldCin, bias, C, ldC);
+  else
+    hipLaunchKernelGGL((gemm_f32_d_kernel<false, false, DS, KB, NWV>), grid, dim3(64 * NWV), 0, st, M, N, K, A, sAm, sAk, B,
+                       sBk, sBn, Cin, ldCin, bias, C, ldC);
+}
+
 template <int BM, int BN, int KW>
 void launch_f32(bool am, bool bn, int M, int N, int K, const float* A, int64_t sAm, int64_t sAk, const float* B,
                 int64_t sBk, int64_t sBn, const float* Cin, int64_t ldCin, const float* bias, float* C, int64_t ldC,
@@ -255,6 +454,6 @@ extern "C" int gasfm_gemm_f32(int32_t M, int32_t N, int32_t K, const float* A, i
   if (int64_t(M) * N <= 256 * 1024)  // e.g. a camera shard's 125 x 1024: the 32 x 32, K-split tile
     launch_f32<32, 32, 4>(am, bn, M, N, K, A, sAm, sAk, B, sBk, sBn, Cin, ldCin, bias, C, ldC, st);
   else
-    launch_f32<64, 64, 1>(am, bn, M, N, K, A, sAm, sAk, B, sBk, sBn, Cin, ldCin, bias, C, ldC, st);
+    launch_f32_d<3, 64, 8>(am, bn, M, N, K, A, sAm, sAk, B, sBk, sBn, Cin, ldCin, bias, C, ldC, st);
   return launch_status("gasfm_gemm_f32");
 }

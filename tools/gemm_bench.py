@@ -1,8 +1,12 @@
 """gasfm_gemm_f32 and gasfm_gemm_f32_smallm vs torch (hipBLASLt) on the camera-side shapes: y = x W^T, dx = dy W, dW = dy^T x
 at m = 1000 and m = 125 (HIP events, 50 back-to-back launches each)."""
+import os
+import sys
+
 import torch
 
-from gasfm_amd import _native
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gasfm_amd import _native  # noqa: E402
 
 
 def t(fn, reps=50):

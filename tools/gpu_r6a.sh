@@ -19,3 +19,7 @@ timeout -k 10 400 python tools/train_step_bench.py --batch 1 --outliers 0.1 --ca
 cat gpurun_out/r6a_ts_b1_c5.jsonl
 timeout -k 10 300 python tools/dist_train_bench.py --emulate-world 8 --steps 20 > gpurun_out/r6a_dt_em8.json 2> gpurun_out/r6a_dt_em8.err || { tail -30 gpurun_out/r6a_dt_em8.err; exit 1; }
 cat gpurun_out/r6a_dt_em8.json
+GASFM_WGRAD_GEMM=torch timeout -k 10 300 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/r6a_bench_wgrad_torch.json 2> gpurun_out/r6a_bench_wgrad_torch.err || { tail -30 gpurun_out/r6a_bench_wgrad_torch.err; exit 1; }
+tail -1 gpurun_out/r6a_bench_wgrad_torch.json
+timeout -k 10 300 python bench.py --no-cpu-baseline --steps 20 > gpurun_out/r6a_bench_wgrad_hip.json 2> gpurun_out/r6a_bench_wgrad_hip.err || { tail -30 gpurun_out/r6a_bench_wgrad_hip.err; exit 1; }
+tail -1 gpurun_out/r6a_bench_wgrad_hip.json
