@@ -135,14 +135,18 @@ class Caps:
 
     @classmethod
     def for_batch(cls, st):
-        M = -(-(st.M + 1 + st.M // 8) // 8) * 8
+        # >= V2G_PIECES pad cameras (the pad scene's view->global graph is split like every scene's:
+        # a one-scene batch of 13 views would otherwise get 3 and no edge count could fix it)
+        M = -(-max(st.M + 1 + st.M // 8, st.M + V2G_PIECES) // 8) * 8
         N = -(-(int(st.N * HEADROOM) + S2G_PIECES + 64) // 256) * 256
         E = max(int(st.E * HEADROOM), st.E + 2 * (N - st.N) + MIN_N_POINTS_PER_VIEW * (M - st.M) + 256)
         E = -(-E // 2048) * 2048
         caps = cls(st.B, M, N, E, st.inv_v, st.inv_p)
-        while caps.pad(st) is None:  # grow the edges until the pads are expressible
+        for _ in range(1 << 16):  # grow the edges until the pads are expressible
+            if caps.pad(st) is not None:
+                return caps
             caps = cls(st.B, M, N, caps.E + 2048, st.inv_v, st.inv_p)
-        return caps
+        raise RuntimeError(f"StaticBatch: no bucket found for a batch of M={st.M} N={st.N} E={st.E}")
 
 
 def _inv3(Ns):

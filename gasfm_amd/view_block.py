@@ -44,9 +44,10 @@ SMALLM_ROWS = int(os.environ.get("GASFM_SMALLM_ROWS", "256"))
 # with the view kernels as their prologues / epilogues, 2 launches forward and 4 backward per block
 # (round 3: 7 and 10); GASFM_VIEW_CHAIN=0 keeps the separate view kernels + GEMMs
 VIEW_CHAIN = os.environ.get("GASFM_VIEW_CHAIN", "1") != "0"
-# the camera-side weight gradients dW = dy^T x above SMALLM_ROWS rows on csrc/gemm_f32.hip (round 6);
-# GASFM_WGRAD_GEMM=torch keeps hipBLASLt
-WGRAD_HIP = os.environ.get("GASFM_WGRAD_GEMM", "hip") != "torch"
+# GASFM_WGRAD_GEMM=hip: the camera-side weight gradients dW = dy^T x above SMALLM_ROWS rows on
+# csrc/gemm_f32.hip's direct-to-LDS kernel (round 6: 26.9 vs 27.9 us standalone at m = 1000, but the
+# config-4 step 28.22-28.29 vs 28.18-28.20 ms with hipBLASLt on the same box, profiles/r6_gemm_f32.txt)
+WGRAD_HIP = os.environ.get("GASFM_WGRAD_GEMM", "torch") == "hip"
 
 
 def _chain_ok(m, D, bf16):
@@ -71,8 +72,7 @@ def _mm(a, b, cin=None, bias=None, bf16=False, out=None):
         if y is not None:
             return y
     elif WGRAD_HIP and a.stride(0) == 1 and cin is None and bias is None:
-        # dW = dy^T x over >= 512 camera rows: csrc/gemm_f32.hip's direct-to-LDS kernel (26.9 us vs
-        # hipBLASLt's 27.9 at m = 1000, profiles/r6_gemm_f32.txt)
+        # dW = dy^T x over > SMALLM_ROWS camera rows on csrc/gemm_f32.hip (opt-in, above)
         return _native.gemm_f32(a, b, out=out)
     if cin is not None:
         if out is cin and bias is None:

@@ -164,3 +164,21 @@ def test_trainer_bucket_lru(small_pieces, monkeypatch):
     assert list(trainer.buckets) == keys[1:]  # the first (least recently used) was dropped
     b, new = trainer._bucket(sts[1], torch.device("cpu"))  # reuse moves it to the end
     assert not new and list(trainer.buckets) == [keys[2], keys[1]]
+
+
+@pytest.mark.parametrize("m", [8, 10, 13, 16, 20])
+def test_one_scene_batch_gets_a_bucket(small_pieces, m):
+    """B = 1 (the GASFM learning confs' batch_size): a batch of one 8-20 view scene gets a bucket with
+    >= V2G_PIECES pad cameras (round 6: 13 views gave 3 pad cameras and Caps.for_batch never
+    returned), and the padded structure holds (test_static_batch_structure's invariants on B = 1)."""
+    sc = synthetic.windowed_scene(m, 1500, mean_extra=4, seed=40 + m)
+    datas = [SceneData(torch.from_numpy(sc.dense_M()), torch.from_numpy(sc.Ns()), torch.from_numpy(sc.Ps_gt()), "s")]
+    st = static_batch.BatchStats(datas)
+    assert st.expressible() is None
+    caps = static_batch.Caps.for_batch(st)
+    pad = caps.pad(st)
+    assert pad is not None and pad[0] >= static_batch.V2G_PIECES and caps.waste_ok(st)
+    sb = static_batch.StaticBatch(caps, torch.device("cpu"))
+    sb.fill(datas, st)
+    _tiles(sb.items_c[:, :3].numpy(), 0, caps.E)
+    assert int(sb.cam_ptr[-1]) == caps.E and int(sb.pt_ptr[-1]) == caps.E

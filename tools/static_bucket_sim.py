@@ -31,7 +31,7 @@ buckets = []
 wastes = []
 t0 = time.time()
 for it in range(int(sys.argv[1]) if len(sys.argv) > 1 else 60):
-    datas = [prep(scenes[int(i)]) for i in np.random.choice(12, 4, replace=False)]
+    datas = [prep(scenes[int(i)]) for i in np.random.choice(12, int(__import__("os").environ.get("SIM_BATCH", "4")), replace=False)]
     st = static_batch.BatchStats(datas)
     why = st.expressible()
     if why:

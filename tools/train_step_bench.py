@@ -68,6 +68,7 @@ def main():
     ap.add_argument("--gasfm-adam", action="store_true",
                     help="--captured: gasfm_amd.optim.Adam (one HIP launch) instead of torch's captured fused Adam")
     ap.add_argument("--no-eager", action="store_true", help="skip the eager union mode (e.g. to profile --captured)")
+    ap.add_argument("--progress", type=int, default=10, help="a progress line every this many batches")
     ap.add_argument("--phases", action="store_true",
                     help="--captured: also time the trainer's phases with a synchronize between them (slower)")
     ap.add_argument("--capture-floor", action="store_true",
@@ -179,7 +180,7 @@ def main():
                 torch.cuda.synchronize()
                 t_start = time.perf_counter()
                 caps_before = trainer.captures
-            if it % 10 == 0:
+            if it % args.progress == 0:
                 print(f"pipelined: batch {it}/{prime + steps}, buckets {len(trainer.buckets)}", file=sys.stderr,
                       flush=True)
             t0, c0 = time.perf_counter(), trainer.captures
@@ -215,16 +216,16 @@ def main():
         n_done = 0
         repro = []
         caps_before = 0
-        t_prime = time.perf_counter()
+        t_prime = t_prime_0 = time.perf_counter()
         for it in range(prime + steps):
             if it == prime:
                 torch.cuda.synchronize()
                 t_prime = time.perf_counter() - t_prime
                 caps_before = trainer.captures
                 trainer.profile = {} if args.phases else None
-            if it % 10 == 0:
-                print(f"captured: batch {it}/{prime + steps}, buckets {len(trainer.buckets)}", file=sys.stderr,
-                      flush=True)
+            if it % args.progress == 0:
+                print(f"captured: batch {it}/{prime + steps}, buckets {len(trainer.buckets)}, captures {trainer.captures}, "
+                      f"{time.perf_counter() - t_prime_0:.1f} s", file=sys.stderr, flush=True)
             batch = [scenes[int(i)] for i in np.random.choice(len(scenes), args.batch, replace=False)]
             torch.cuda.synchronize()
             t0 = time.perf_counter()
