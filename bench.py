@@ -234,6 +234,11 @@ def main():
                     help="N > 1: shard the points only (the view chain replicated on every rank)")
     ap.add_argument("--cam-shard-1", action="store_true",
                     help="with --dist at one rank: run the camera-sharded code path anyway (RCCL capture test)")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="process-group backend at N > 1: nccl (= RCCL, the measured path); gloo stages the "
+                         "collectives through the host (a functional test of the N-rank launch, not a measurement)")
+    ap.add_argument("--one-gpu", action="store_true",
+                    help="with --backend gloo: every rank on cuda:0 (tests the N-rank path on a one-GPU box)")
     ap.add_argument("--emulate-world", type=int, default=0, metavar="W",
                     help="per-rank proxy: rank 0's shard of a W-GPU step on this one GPU, collectives replaced by "
                          "local copies (timing of the per-rank compute; numerically meaningless)")
@@ -242,13 +247,20 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     rank, world, local_rank = world_from_env(args.gpus)
+    if args.one_gpu and args.backend != "gloo":
+        log("error: --one-gpu needs --backend gloo (RCCL does not run two ranks on one GPU)")
+        sys.exit(2)
+    local_rank = 0 if args.one_gpu else local_rank
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist_on = world > 1 or args.dist
     emul = args.emulate_world > 1 and not dist_on
     cams = not args.no_cam_shard
     if dist_on:
-        torch.distributed.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=dev)
+        else:
+            torch.distributed.init_process_group("gloo")
         if torch.distributed.get_world_size() != world:  # n_gpus is the rank count RCCL reports
             log(f"error: RCCL reports {torch.distributed.get_world_size()} ranks, WORLD_SIZE {world}")
             sys.exit(2)
@@ -307,7 +319,7 @@ def main():
         agree = None
         if dist_on:
             def agree(ok):  # AND over ranks, one collective outside the graph
-                t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+                t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev if args.backend == "nccl" else "cpu")
                 torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
                 return bool(t.item())
         captured = CapturedStep(fwd_bwd, model.parameters(), warmup=args.warmup, agree=agree)
@@ -326,7 +338,7 @@ def main():
         torch.distributed.barrier()
     dt = time.perf_counter() - t0
     if dist_on:
-        t = torch.tensor([dt], device=dev)
+        t = torch.tensor([dt], device=dev if args.backend == "nccl" else "cpu")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
     # roofline kernel: the point-direction attention forward, in eager steps right after the
@@ -393,6 +405,8 @@ def main():
                                        " sharded; collectives replaced by local copies: per-rank compute only)"
                                        if emul else
                                        f"{'point+camera' if data.shard.cams is not None else 'point'}-sharded x{world}"
+                                       + ("" if args.backend == "nccl" else
+                                          " (gloo on one GPU: a functional test of the N-rank path, not a measurement)")
                                        if dist_on else "single GPU")},
             "roofline": {"kernel": pbwd_name[0] + ": camera-attention + edge-prologue backward"
                                    + (" + the edge epilogue's backward (dSv, dP0 of the previous block, dWp of this "

@@ -480,3 +480,25 @@ def test_sharded_esfm_loss_matches_single_gpu(device, valid_only):
             assert np.linalg.norm(g - r) <= 1e-3 * nr + 1e-7, f"rank {rank} {k}: {np.linalg.norm(g - r):.3e} / {nr:.3e}"
     for k in ref:
         assert np.array_equal(res[0][2][k], res[1][2][k]), k
+
+
+@pytest.mark.gpu
+def test_bench_self_launches_n_ranks(tmp_path):
+    """VERDICT r5 #1 end to end: ``python bench.py --gpus 2`` with no launcher in the environment starts
+    two torchrun ranks itself (a child process), they run the sharded step and rank 0 prints ONE JSON
+    line with n_gpus 2.  gloo on one GPU (RCCL cannot put two ranks on one device): the N-rank launch,
+    rank logic and max-over-ranks timing, not the wire."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--backend", "gloo", "--one-gpu",
+           "--cameras", "100", "--points", "10000", "--layers", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=repo, env=env, capture_output=True, text=True, timeout=240)
+    (tmp_path / "bench_stderr.log").write_text(r.stderr)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # only rank 0 prints
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["value"] > 0 and "x2" in res["config"]["parallelism"]
