@@ -20,6 +20,15 @@ def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
 
+def file_flags(src):
+    """Extra hipcc flags a source asks for on its first line (``// hipcc-flags: ...``), e.g. the
+    machine scheduler of csrc/edge_seam.hip."""
+    with open(src) as f:
+        first = f.readline()
+    tag = "// hipcc-flags:"
+    return first[len(tag):].split() if first.startswith(tag) else []
+
+
 def _stale():
     if not os.path.exists(LIB):
         return True
@@ -44,7 +53,7 @@ def build(force=False, verbose=False, defines=(), out=None):
     procs = []
     for src in sources():
         obj = os.path.join(build_dir, os.path.basename(src) + ".o")
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-c", src, "-o", obj]
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-c", src, "-o", obj] + file_flags(src)
         cmd += [f"-D{d}" for d in defines]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
