@@ -1,3 +1,6 @@
+// hipcc-flags: -mllvm --amdgpu-sched-strategy=max-ilp
+// (round 6: the rank-0-of-8 proxy 7.19-7.20 -> 7.16 ms on one box, profiles/r6_ab_sched_files.txt; the
+// other kernel files measured within noise or slower under max-ilp)
 // The global node's chain of one GASFM block -- a single row of G = 2048 features -- forward and
 // backward in four launches each way, gfx950.
 //
