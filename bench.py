@@ -46,7 +46,7 @@ PBWD_FOLD_FLOP_PER_EDGE = PBWD_FLOP_PER_EDGE + 2176 + 128
 PBWD_FOLD_BYTES_PER_EDGE = PBWD_BYTES_PER_EDGE + 16
 _PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
 # the newest committed per-kernel PMC table (tools/pmc_kernels.sh)
-PMC_KERNELS = next((os.path.join(_PROFILES, f) for f in ("r5_pmc_kernels.txt", "r4_pmc_kernels.txt",
+PMC_KERNELS = next((os.path.join(_PROFILES, f) for f in ("r6_pmc_kernels.txt", "r5_pmc_kernels.txt", "r4_pmc_kernels.txt",
                                                           "r3_pmc_kernels.txt")
                     if os.path.exists(os.path.join(_PROFILES, f))), os.path.join(_PROFILES, "r3_pmc_kernels.txt"))
 
