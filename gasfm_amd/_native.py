@@ -174,10 +174,10 @@ _SIGS = {
     "gasfm_point_tail_fwd": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp]),
     "gasfm_point_tail_bwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_point_hub_fwd": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                   _vp, _vp, _vp, _vp]),
+                                   _vp, _vp, _vp]),
     "gasfm_point_hub_bwd_c": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_point_hub_bwd_ab": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "gasfm_point_hub_bwd": (_i32, [_vp, _i64, _f32] + [_vp] * 18),
+    "gasfm_point_hub_bwd": (_i32, [_vp, _i64, _f32] + [_vp] * 17),
     "gasfm_point_head_part_shape": (_i32, [_i64, _i32, _vp]),
     "gasfm_point_head_fwd": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_point_head_bwd": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -848,15 +848,10 @@ def point_tail_bwd(dout, prev, agg, Wp, bp, ln_w, ln_b, eps, Wm, dx, dagg, part)
     check(st, "gasfm_point_tail_bwd")
 
 
-def point_hub_fwd(X, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR, T=None):
-    """T: optional [N, 32] output for the rows t = WC relu(LN_C(X)) + bWC (the split backward's input)."""
+def point_hub_fwd(X, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR):
     _req(X, "X", 64)
-    if T is not None:
-        _req(T, "T", 32)
-        if T.shape[0] != X.shape[0]:
-            raise ValueError(f"T: expected {X.shape[0]} rows, got {T.shape[0]}")
     st = lib().gasfm_point_hub_fwd(_p(X), X.shape[0], eps, _p(gA), _p(bA), _p(WA), _p(SA), _p(WB), _p(bB), _p(XL),
-                                   _p(gC), _p(bC), _p(WC), _p(bWC), _p(WD), _p(bD), _p(XR), _p(T), _stream(X))
+                                   _p(gC), _p(bC), _p(WC), _p(bWC), _p(WD), _p(bD), _p(XR), _stream(X))
     check(st, "gasfm_point_hub_fwd")
 
 
@@ -881,22 +876,17 @@ def point_hub_bwd_ab(X, eps, gA, bA, WA, WB, dSA, dXL, dRes, dX, part):
     check(st, "gasfm_point_hub_bwd_ab")
 
 
-def point_hub_bwd(X, eps, gA, bA, WA, WB, gC, bC, WC, bWC, WD, dSA, dXL, dXR, dRes, dX, part_a, part_c, T=None):
-    """The whole point-hub backward (gasfm_point_hub_bwd): the split data + weight-gradient kernels
-    when T (point_hub_fwd's t rows) is given, the one-pass kernel otherwise."""
+def point_hub_bwd(X, eps, gA, bA, WA, WB, gC, bC, WC, bWC, WD, dSA, dXL, dXR, dRes, dX, part_a, part_c):
+    """The whole point-hub backward in one pass (gasfm_point_hub_bwd)."""
     _req(X, "X", 64)
     _req(dSA, "dSA", 32)
     _req(dXL, "dXL", 64)
     _req(dXR, "dXR", 32)
     if dRes is not None:
         _req(dRes, "dRes", 64)
-    if T is not None:
-        _req(T, "T", 32)
-        if T.shape[0] != X.shape[0]:
-            raise ValueError(f"T: expected {X.shape[0]} rows, got {T.shape[0]}")
     st = lib().gasfm_point_hub_bwd(_p(X), X.shape[0], eps, _p(gA), _p(bA), _p(WA), _p(WB), _p(gC), _p(bC), _p(WC),
-                                   _p(bWC), _p(WD), _p(dSA), _p(dXL), _p(dXR), _p(dRes), _p(T), _p(dX),
-                                   _p(part_a), _p(part_c), _stream(X))
+                                   _p(bWC), _p(WD), _p(dSA), _p(dXL), _p(dXR), _p(dRes), _p(dX), _p(part_a),
+                                   _p(part_c), _stream(X))
     check(st, "gasfm_point_hub_bwd")
 
 

@@ -1118,7 +1118,7 @@ __global__ __launch_bounds__(kThreadsT, GASFM_PT_FWD_T_MINW) void point_hub_fwd_
     const float* __restrict__ WA, float* __restrict__ SA, const float* __restrict__ WB,
     const float* __restrict__ bB, float* __restrict__ XL, const float* __restrict__ gC,
     const float* __restrict__ bC, const float* __restrict__ WC, const float* __restrict__ bWC,
-    const float* __restrict__ WD, const float* __restrict__ bD, float* __restrict__ XR, float* __restrict__ T) {
+    const float* __restrict__ WD, const float* __restrict__ bD, float* __restrict__ XR) {
   __shared__ float4 WAQ[FA * FP / 4], WBQ[FP * FP / 4], WCQ[HC ? FA * FP / 4 : 1], WDQ[HC ? FA * FA / 4 : 1];
   __shared__ float V[5 * FP + 2 * FA];  // gamma_A beta_A gamma_C beta_C b_B | b_C b_D
   const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW, g = lane >> 4;
@@ -1184,7 +1184,6 @@ __global__ __launch_bounds__(kThreadsT, GASFM_PT_FWD_T_MINW) void point_hub_fwd_
       }
       f32x4 tq[2] = {vec_at(V + 5 * FP, 0, g), vec_at(V + 5 * FP, 1, g)};  // b_C, then + W_C h
       layer_t<2, 4>(WCQ, h, tq, lane);
-      if (T) slabs_store<FA>(T, row0, nrows, tq, lane);  // t rows for the split backward's dW_D
       f32x4 xr[2] = {vec_at(V + 5 * FP + FA, 0, g), vec_at(V + 5 * FP + FA, 1, g)};  // b_D, then + W_D t
       layer_t<2, 2>(WDQ, tq, xr, lane);
       slabs_store<FA>(XR, row0, nrows, xr, lane);
@@ -1848,384 +1847,6 @@ __global__ __launch_bounds__(kThreadsR, GASFM_PT_HUB_BWD_R_MINW) void point_hub_
   }
 }
 
-// ----------------------------------------------------------------------------- hub backward, split (round 6)
-// The one-pass kernel above keeps 144 weight-gradient accumulators beside the data path.  That
-// holds it at one wave per SIMD: 115 us at n = 200k, i.e. 320 MFMA per tile at 0.45 of the fp32
-// MFMA peak.  The split form runs as two kernels, with the same partial layouts:
-//   point_hub_bwd_d_kernel  the data path.  It computes dp and the four LayerNorm gamma / beta
-//                           gradients: 144 MFMA per tile and no weight accumulators, so it runs
-//                           at 2 waves per SIMD.  The ops and their order are the one-pass
-//                           kernel's, so dp is bitwise that kernel's.
-//   point_hub_wgrad_kernel  dW_A, dW_B, dW_C, dW_D and the row sums for b_B, b_C, b_D: 160 MFMA per
-//                           tile.  The 144 weight-gradient MFMAs take every operand in the K layout
-//                           (below), loaded straight from global memory, with no LDS tile.  It recomputes
-//                           dt = dXR W_D (16 MFMA) and reads t = W_C relu(LN_C p) + b_C from rows
-//                           the forward stored (gasfm_point_hub_fwd's T).
-// Algorithmic bytes per row: d 1,280 (as the one-pass kernel), wgrad p 256 + dSA 128 + dXL 256 +
-// dXR 128 + t 128 = 896; forward +128 (t).
-#ifndef GASFM_PT_HUB_D_MINW
-#define GASFM_PT_HUB_D_MINW 2
-#endif
-#ifndef GASFM_PT_HUB_W_MINW
-#define GASFM_PT_HUB_W_MINW 1
-#endif
-#ifndef GASFM_PT_HUB_W_PREFETCH
-#define GASFM_PT_HUB_W_PREFETCH 1
-#endif
-
-template <bool HR>
-__global__ __launch_bounds__(kThreadsR, GASFM_PT_HUB_D_MINW) void point_hub_bwd_d_kernel(
-    const float* __restrict__ X, int64_t N, float eps, const float* __restrict__ gA, const float* __restrict__ bA,
-    const float* __restrict__ WA, const float* __restrict__ WB, const float* __restrict__ gC,
-    const float* __restrict__ bC, const float* __restrict__ WC, const float* __restrict__ WD,
-    const float* __restrict__ dSA, const float* __restrict__ dXL, const float* __restrict__ dXR, const float* dRes,
-    float* dX, float* __restrict__ part_a, float* __restrict__ part_c) {
-  constexpr int ODT = 0, OCT = ODT + FA * FA, OAT = OCT + FA * FP, OBT = OAT + FA * FP, OV = OBT + FP * FP,
-                OT = OV + 4 * FP;
-  constexpr int TW = TR * (LDX + LDA);  // per wave: p (64 wide), dt (32 wide)
-  constexpr int NLDS = OT + kWavesR * TW;
-  constexpr int NRED = 16;
-  __shared__ __attribute__((aligned(16))) float lds[NLDS];
-  const float4* WDTQ = reinterpret_cast<const float4*>(lds + ODT);   // slabs of W_D^T (out t,  k xr)
-  const float4* WCTQ = reinterpret_cast<const float4*>(lds + OCT);   // slabs of W_C^T (out p,  k t)
-  const float4* WATQ = reinterpret_cast<const float4*>(lds + OAT);   // slabs of W_A^T (out p,  k sa)
-  const float4* WBTQ = reinterpret_cast<const float4*>(lds + OBT);   // slabs of W_B^T (out p,  k xl)
-  const float* V = lds + OV;  // gamma_C beta_C gamma_A beta_A
-  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
-  const int c = lane & 15, g = lane >> 4;
-  float* Tp = lds + OT + wave * TW;
-  float* Td = Tp + TR * LDX;  // dt's C -> T transpose
-  const int64_t ntiles = (N + TR - 1) / TR;
-  const int64_t gw = int64_t(blockIdx.x) * kWavesR + wave, nw = int64_t(gridDim.x) * kWavesR;
-  f32x4 n_pT[4], n_rT[2], n_sT[2], n_lT[4];  // the next tile's T-layout rows
-  auto fetch = [&](int64_t tt) {
-    const int64_t r0 = tt * TR;
-    const int nr = int(N - r0 < TR ? N - r0 : TR);
-    slabs_load<FP>(X, r0, nr, n_pT, lane);
-    slabs_load<FA>(dXR, r0, nr, n_rT, lane);
-    slabs_load<FA>(dSA, r0, nr, n_sT, lane);
-    slabs_load<FP>(dXL, r0, nr, n_lT, lane);
-  };
-  if (gw < ntiles) fetch(gw);  // the first tile's rows fly while the weights are staged
-  stage_slabs_tr<FA, FA, kThreadsR>(WD, lds + ODT);
-  stage_slabs_tr<FA, FP, kThreadsR>(WC, lds + OCT);
-  stage_slabs_tr<FA, FP, kThreadsR>(WA, lds + OAT);
-  stage_slabs_tr<FP, FP, kThreadsR>(WB, lds + OBT);
-  if (threadIdx.x < FP) {
-    lds[OV + threadIdx.x] = gC[threadIdx.x];
-    lds[OV + FP + threadIdx.x] = bC[threadIdx.x];
-    lds[OV + 2 * FP + threadIdx.x] = gA[threadIdx.x];
-    lds[OV + 3 * FP + threadIdx.x] = bA[threadIdx.x];
-  }
-  __syncthreads();
-  float dgA[4] = {0.f, 0.f, 0.f, 0.f}, dbA[4] = {0.f, 0.f, 0.f, 0.f};
-  float dgC[4] = {0.f, 0.f, 0.f, 0.f}, dbCl[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t t = gw; t < ntiles; t += nw) {
-    const int64_t row0 = t * TR;
-    const int nrows = int(N - row0 < TR ? N - row0 : TR);
-    asm volatile("" ::: "memory");  // weight slabs re-read from LDS per tile (not hoisted into VGPRs)
-    f32x4 pT[4], rT[2] = {n_rT[0], n_rT[1]}, sT[2] = {n_sT[0], n_sT[1]}, lT[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      pT[u] = n_pT[u];
-      lT[u] = n_lT[u];
-    }
-    f32x4 acc[4];
-    if (HR) cl_load<FP>(dRes, row0, nrows, acc, lane);
-    fetch(t + nw < ntiles ? t + nw : t);  // unconditional: see point_hub_bwd_r_kernel
-    t_to_lds<FP, LDX>(pT, Tp, lane);
-    float mean, rstd;
-    slab_stats(pT, eps, mean, rstd);
-    *reinterpret_cast<float2*>(Tp + c * LDX + FP) = make_float2(mean, rstd);
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-    float meanC[4], rstdC[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float2 st = *reinterpret_cast<const float2*>(Tp + (4 * g + r) * LDX + FP);
-      meanC[r] = st.x;
-      rstdC[r] = st.y;
-    }
-    PT_SCHED_BARRIER();
-    f32x4 xh[4];
-#pragma unroll
-    for (int ot = 0; ot < 4; ++ot)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) xh[ot][r] = (Tp[(4 * g + r) * LDX + 16 * ot + c] - meanC[r]) * rstdC[r];
-    {
-      f32x4 dtC[2] = {zero4(), zero4()}, dtT[2], dp[4] = {zero4(), zero4(), zero4(), zero4()}, dq[4];
-      layer_c<2, 2>(WDTQ, rT, dtC, lane);
-#pragma unroll
-      for (int ft = 0; ft < 2; ++ft)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Td[(4 * g + r) * LDA + 16 * ft + c] = dtC[ft][r];
-      __builtin_amdgcn_wave_barrier();
-      asm volatile("" ::: "memory");
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const float4 t4 = *reinterpret_cast<const float4*>(Td + c * LDA + 16 * u + 4 * g);
-        dtT[u] = f32x4{t4.x, t4.y, t4.z, t4.w};
-      }
-      PT_SCHED_BARRIER();
-      layer_c<4, 2>(WCTQ, dtT, dp, lane);
-      float gm[4], bt[4];
-#pragma unroll
-      for (int ot = 0; ot < 4; ++ot) {
-        gm[ot] = V[16 * ot + c];
-        bt[ot] = V[FP + 16 * ot + c];
-      }
-      cl_ln_relu_bwd(xh, dp, gm, bt, rstdC, nrows, g, dgC, dbCl, dq);
-#pragma unroll
-      for (int ot = 0; ot < 4; ++ot) acc[ot] = HR ? dq[ot] + acc[ot] : dq[ot];
-    }
-    PT_SCHED_BARRIER();
-    {
-      f32x4 dp[4] = {zero4(), zero4(), zero4(), zero4()}, da[4];
-      layer_c<4, 2>(WATQ, sT, dp, lane);
-      float gm[4], bt[4];
-#pragma unroll
-      for (int ot = 0; ot < 4; ++ot) {
-        gm[ot] = V[2 * FP + 16 * ot + c];
-        bt[ot] = V[3 * FP + 16 * ot + c];
-      }
-      cl_ln_relu_bwd(xh, dp, gm, bt, rstdC, nrows, g, dgA, dbA, da);
-#pragma unroll
-      for (int ot = 0; ot < 4; ++ot) acc[ot] = da[ot] + acc[ot];
-    }
-    PT_SCHED_BARRIER();
-    layer_c<4, 4>(WBTQ, lT, acc, lane);
-    cl_store<FP>(dX, row0, nrows, acc, lane);
-    __builtin_amdgcn_wave_barrier();  // this tile's LDS reads before the next tile's writes
-    asm volatile("" ::: "memory");
-  }
-  float v[NRED];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    v[k] = dgA[k];
-    v[4 + k] = dbA[k];
-    v[8 + k] = dgC[k];
-    v[12 + k] = dbCl[k];
-  }
-  wg_reduce_ordered<NRED, kWavesR, NLDS>(v, lds, wave, lane);
-  if (wave == 0) {
-    float tt[NRED];
-#pragma unroll
-    for (int k = 0; k < NRED; ++k) tt[k] = sum_groups(v[k]);
-    if (g == 0) {
-      float* oa = part_a + int64_t(blockIdx.x) * HA_PART;
-      float* oc = part_c + int64_t(blockIdx.x) * HC_PART;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        oa[HA_GA + k * 16 + c] = tt[k];
-        oa[HA_BA + k * 16 + c] = tt[4 + k];
-        oc[HC_GC + k * 16 + c] = tt[8 + k];
-        oc[HC_BCL + k * 16 + c] = tt[12 + k];
-      }
-    }
-  }
-}
-
-// K layout (the weight gradients' operands): lane (g, c) holds, for s < 4, the Q = W / 16 consecutive
-// features Q c + q (q < Q) of row 4 g + s as v[q][s] -- one 16-byte (W = 64) or 8-byte (W = 32) load
-// per row per lane, the 16 lanes of a group reading the whole row.  As MFMA operands (k = row 4 g + s
-// at step s) block q of a product holds feature Q i + q at operand index i, so a weight-gradient tile
-// comes out with its features interleaved, which the partial-row writer undoes.  Rows >= nrows read
-// row 0 (cl_mask zeroes them where it matters).
-template <int W>
-__device__ __forceinline__ void kl_load(const float* __restrict__ X, int64_t row0, int nrows, f32x4 (&v)[W / 16],
-                                        int lane) {
-  constexpr int Q = W / 16;
-  const int c = lane & 15, g = lane >> 4;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int rr = 4 * g + s;
-    const float* p = X + (row0 + (rr < nrows ? rr : 0)) * W + Q * c;
-    if constexpr (Q == 4) {
-      const float4 t = *reinterpret_cast<const float4*>(p);
-      v[0][s] = t.x;
-      v[1][s] = t.y;
-      v[2][s] = t.z;
-      v[3][s] = t.w;
-    } else {
-      const float2 t = *reinterpret_cast<const float2*>(p);
-      v[0][s] = t.x;
-      v[1][s] = t.y;
-    }
-  }
-}
-
-__global__ __launch_bounds__(kThreadsR, GASFM_PT_HUB_W_MINW) void point_hub_wgrad_kernel(
-    const float* __restrict__ X, int64_t N, float eps, const float* __restrict__ gA, const float* __restrict__ bA,
-    const float* __restrict__ gC, const float* __restrict__ bC, const float* __restrict__ WD,
-    const float* __restrict__ T, const float* __restrict__ dSA, const float* __restrict__ dXL,
-    const float* __restrict__ dXR, float* __restrict__ part_a, float* __restrict__ part_c) {
-  constexpr int ODT = 0, ORED = ODT + FA * FA;
-  constexpr int NRED = 144 + 8;
-  constexpr int NLDS = ORED + 32 * kWavesR * kW;  // reduction scratch: 32 values per chunk
-  __shared__ __attribute__((aligned(16))) float lds[NLDS];
-  // W_D slabs for dt = dXR W_D in the K layout: Q[(ot * 2 + u) * 64 + 16 g + c][j] = W_D[16 u + 4 g + j][2 c + ot]
-  // (layer_c: input feature 16 u + 4 g + j, output feature 2 c + ot)
-  const float4* WDQ = reinterpret_cast<const float4*>(lds + ODT);
-  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
-  const int c = lane & 15, g = lane >> 4;
-  const int64_t ntiles = (N + TR - 1) / TR;
-  const int64_t gw = int64_t(blockIdx.x) * kWavesR + wave, nw = int64_t(gridDim.x) * kWavesR;
-  // the next tile's rows in the K layout, dXR also in the T layout (dt's A operand)
-  f32x4 n_p[4], n_l[4], n_s[2], n_r[2], n_t[2], n_rT[2];
-  auto fetch = [&](int64_t tt) {
-    const int64_t r0 = tt * TR;
-    const int nr = int(N - r0 < TR ? N - r0 : TR);
-    kl_load<FP>(X, r0, nr, n_p, lane);
-    kl_load<FP>(dXL, r0, nr, n_l, lane);
-    kl_load<FA>(dSA, r0, nr, n_s, lane);
-    kl_load<FA>(dXR, r0, nr, n_r, lane);
-    kl_load<FA>(T, r0, nr, n_t, lane);
-    slabs_load<FA>(dXR, r0, nr, n_rT, lane);
-  };
-  if (GASFM_PT_HUB_W_PREFETCH && gw < ntiles) fetch(gw);
-  {
-    Stage<FA * FA, kThreadsR> st;
-    st.load([&](int q) { return WD[q]; });
-    st.store([&](int q, float v) {
-      const int a = q / FA, b = q % FA;  // W_D[a = xr][b = t]
-      lds[ODT + (((b % 2) * 2 + a / 16) * 64 + ((a % 16) / 4) * 16 + b / 2) * 4 + a % 4] = v;
-    });
-  }
-  float gAv[4], bAv[4], gCv[4], bCv[4];  // features 4 c + q
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    gAv[q] = gA[4 * c + q];
-    bAv[q] = bA[4 * c + q];
-    gCv[q] = gC[4 * c + q];
-    bCv[q] = bC[4 * c + q];
-  }
-  __syncthreads();
-  f32x4 dWA[2][4], dWB[4][4], dWC[2][4], dWD[2][2];
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    dWA[0][nt] = dWA[1][nt] = dWC[0][nt] = dWC[1][nt] = zero4();
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) dWB[mt][nt] = zero4();
-  }
-  dWD[0][0] = dWD[0][1] = dWD[1][0] = dWD[1][1] = zero4();
-  float dbB[4] = {0.f, 0.f, 0.f, 0.f}, dbC[2] = {0.f, 0.f}, dbD[2] = {0.f, 0.f};
-  for (int64_t t = gw; t < ntiles; t += nw) {
-    const int nrows = int(N - t * TR < TR ? N - t * TR : TR);
-    asm volatile("" ::: "memory");  // W_D's slabs re-read from LDS per tile
-    if (!GASFM_PT_HUB_W_PREFETCH) fetch(t);
-    f32x4 pK[4], lK[4], sK[2] = {n_s[0], n_s[1]}, rK[2] = {n_r[0], n_r[1]}, tK[2] = {n_t[0], n_t[1]};
-    f32x4 rT[2] = {n_rT[0], n_rT[1]};
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      pK[u] = n_p[u];
-      lK[u] = n_l[u];
-    }
-    if (GASFM_PT_HUB_W_PREFETCH) fetch(t + nw < ntiles ? t + nw : t);  // unconditional: see point_hub_bwd_r_kernel
-    f32x4 dtK[2] = {zero4(), zero4()};
-    layer_c<2, 2>(WDQ, rT, dtK, lane);
-    // dead rows: the A operands and the bias sums read 0
-    cl_mask(lK, nrows, g);
-    cl_mask(sK, nrows, g);
-    cl_mask(rK, nrows, g);
-    cl_mask(dtK, nrows, g);
-    float mean[4], rstd[4];
-    cl_stats(pK, eps, mean, rstd);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      dbC[q] += (dtK[q][0] + dtK[q][1]) + (dtK[q][2] + dtK[q][3]);
-      dbD[q] += (rK[q][0] + rK[q][1]) + (rK[q][2] + rK[q][3]);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) dbB[q] += (lK[q][0] + lK[q][1]) + (lK[q][2] + lK[q][3]);
-    PT_SCHED_BARRIER();
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      float pa[4], pc[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const float xh = (pK[nt][s] - mean[s]) * rstd[s];
-        pa[nt] = fmaxf(fmaf(xh, gAv[nt], bAv[nt]), 0.f);
-        pc[nt] = fmaxf(fmaf(xh, gCv[nt], bCv[nt]), 0.f);
-      }
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          dWA[mt][nt] = mfma16(sK[mt][s], pa[nt], dWA[mt][nt]);
-          dWC[mt][nt] = mfma16(dtK[mt][s], pc[nt], dWC[mt][nt]);
-        }
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) dWD[mt][nt] = mfma16(rK[mt][s], tK[nt][s], dWD[mt][nt]);
-      }
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) dWB[mt][nt] = mfma16(lK[mt][s], pK[nt][s], dWB[mt][nt]);
-    }
-  }
-  float v[NRED];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        v[(mt * 4 + nt) * 4 + r] = dWA[mt][nt][r];
-        v[96 + (mt * 4 + nt) * 4 + r] = dWC[mt][nt][r];
-      }
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) v[32 + (mt * 4 + nt) * 4 + r] = dWB[mt][nt][r];
-    }
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) v[128 + (mt * 2 + nt) * 4 + r] = dWD[mt][nt][r];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) v[144 + k] = dbB[k];
-  v[148] = dbC[0];
-  v[149] = dbC[1];
-  v[150] = dbD[0];
-  v[151] = dbD[1];
-  wg_reduce_ordered<NRED, kWavesR, NLDS - ORED>(v, lds + ORED, wave, lane);
-  if (wave == 0) {
-    // tile element (i = 4 g + r, j = c) of block (mt, nt): features (Q_out i + mt, Q_in j + nt)
-    float* oa = part_a + int64_t(blockIdx.x) * HA_PART;
-    float* oc = part_c + int64_t(blockIdx.x) * HC_PART;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = 4 * g + r;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          oa[HA_WA + (2 * i + mt) * FP + 4 * c + nt] = v[(mt * 4 + nt) * 4 + r];
-          oc[HC_WC + (2 * i + mt) * FP + 4 * c + nt] = v[96 + (mt * 4 + nt) * 4 + r];
-        }
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) oa[HA_WB + (4 * i + mt) * FP + 4 * c + nt] = v[32 + (mt * 4 + nt) * 4 + r];
-      }
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) oc[HC_WD + (2 * i + mt) * FA + 2 * c + nt] = v[128 + (mt * 2 + nt) * 4 + r];
-    }
-    float tt[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) tt[k] = sum_groups(v[144 + k]);
-    if (g == 0) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) oa[HA_BB + 4 * c + q] = tt[q];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        oc[HC_BC + 2 * c + q] = tt[4 + q];
-        oc[HC_BD + 2 * c + q] = tt[6 + q];
-      }
-    }
-  }
-}
-
 int64_t tiles_of(int64_t N) { return (N + TR - 1) / TR; }
 
 template <class K>
@@ -2260,20 +1881,6 @@ int hub_c_grid(int64_t N, bool hr) {
 // and the two-pass entry points launch that many workgroups too while it is the default (their
 // partial buffers come from gasfm_point_hub_part_shape)
 int hub_r_grid(int64_t N) { return gridR(&point_hub_bwd_r_kernel<true>, N); }
-// rows of the hub's partial buffers = the grid every hub backward form launches: the split data
-// kernel's resident grid (2 waves per SIMD; the one-pass and wgrad kernels, resident at one wave per
-// SIMD, run their workgroups in two rounds), but at least GASFM_PT_HUB_TILES_PER_WG tiles per
-// workgroup (small N: the per-workgroup weight staging and partial-row reduction cost more than the
-// extra workgroups save)
-#ifndef GASFM_PT_HUB_TILES_PER_WG
-#define GASFM_PT_HUB_TILES_PER_WG 8
-#endif
-int hub_rows(int64_t N) {
-  const int d = gridR(&point_hub_bwd_d_kernel<true>, N), r = hub_r_grid(N);
-  const int64_t by_tiles = (tiles_of(N) + GASFM_PT_HUB_TILES_PER_WG - 1) / GASFM_PT_HUB_TILES_PER_WG;
-  const int res = d > r ? d : r;
-  return int(by_tiles < res ? (by_tiles > 1 ? by_tiles : 1) : res);
-}
 
 }  // namespace
 }  // namespace gasfm
@@ -2288,7 +1895,7 @@ extern "C" int32_t gasfm_point_tail_part_shape(int64_t N, int32_t has_prev, int3
 extern "C" int32_t gasfm_point_hub_part_shape(int64_t N, int32_t which, int32_t has_res, int32_t* cols) {
   if (cols) *cols = which ? HC_PART : HA_PART;
   if (N <= 0) return 0;
-  if (GASFM_PT_HUB_BWD_R) return hub_rows(N);
+  if (GASFM_PT_HUB_BWD_R) return hub_r_grid(N);
   return which ? hub_c_grid(N, has_res != 0) : hub_ab_grid(N, has_res != 0);
 }
 extern "C" int gasfm_point_tail_fwd(const float* prev, const float* agg, int64_t N, const float* Wp, const float* bp,
@@ -2348,23 +1955,21 @@ extern "C" int gasfm_point_tail_bwd(const float* dout, const float* prev, const 
 extern "C" int gasfm_point_hub_fwd(const float* X, int64_t N, float eps, const float* gA, const float* bA,
                                    const float* WA, float* SA, const float* WB, const float* bB, float* XL,
                                    const float* gC, const float* bC, const float* WC, const float* bWC,
-                                   const float* WD, const float* bD, float* XR, float* T, void* stream) {
+                                   const float* WD, const float* bD, float* XR, void* stream) {
   GASFM_REQUIRE(N >= 0, "gasfm_point_hub_fwd: N < 0");
   const bool hc = gC != nullptr;
   if (N == 0) return GASFM_OK;
   GASFM_REQUIRE(X && gA && bA && WA && SA && WB && bB && XL, "gasfm_point_hub_fwd: null pointer");
   GASFM_REQUIRE(!hc || (bC && WC && bWC && WD && bD && XR), "gasfm_point_hub_fwd: null pointer (C part)");
-  GASFM_REQUIRE(!T || (hc && GASFM_PT_FWD_T), "gasfm_point_hub_fwd: T needs the C part (and the T-layout kernel)");
-  GASFM_REQUIRE(aligned16(X) && (!T || aligned16(T)), "gasfm_point_hub_fwd: alignment");
+  GASFM_REQUIRE(aligned16(X), "gasfm_point_hub_fwd: alignment");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (GASFM_PT_FWD_T) {
     if (hc)
       hipLaunchKernelGGL(point_hub_fwd_t_kernel<true>, dim3(gridT(&point_hub_fwd_t_kernel<true>, N)), dim3(kThreadsT),
-                         0, st, X, N, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR, T);
+                         0, st, X, N, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR);
     else
       hipLaunchKernelGGL(point_hub_fwd_t_kernel<false>, dim3(gridT(&point_hub_fwd_t_kernel<false>, N)),
-                         dim3(kThreadsT), 0, st, X, N, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR,
-                         nullptr);
+                         dim3(kThreadsT), 0, st, X, N, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR);
     return launch_status("gasfm_point_hub_fwd");
   }
   if (hc)
@@ -2386,10 +1991,10 @@ extern "C" int gasfm_point_hub_bwd_c(const float* X, int64_t N, float eps, const
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const bool hr = dRes != nullptr;
   if (hr)
-    hipLaunchKernelGGL(point_hub_bwd_c_kernel<true>, dim3((GASFM_PT_HUB_BWD_R ? hub_rows(N) : hub_c_grid(N, true))), dim3(kThreads8), 0, st, X, N, eps,
+    hipLaunchKernelGGL(point_hub_bwd_c_kernel<true>, dim3((GASFM_PT_HUB_BWD_R ? hub_r_grid(N) : hub_c_grid(N, true))), dim3(kThreads8), 0, st, X, N, eps,
                        gC, bC, WC, bWC, WD, dXR, dRes, dX, part);
   else
-    hipLaunchKernelGGL(point_hub_bwd_c_kernel<false>, dim3((GASFM_PT_HUB_BWD_R ? hub_rows(N) : hub_c_grid(N, false))), dim3(kThreads8), 0, st, X, N,
+    hipLaunchKernelGGL(point_hub_bwd_c_kernel<false>, dim3((GASFM_PT_HUB_BWD_R ? hub_r_grid(N) : hub_c_grid(N, false))), dim3(kThreads8), 0, st, X, N,
                        eps, gC, bC, WC, bWC, WD, dXR, dRes, dX, part);
   return launch_status("gasfm_point_hub_bwd_c");
 }
@@ -2404,10 +2009,10 @@ extern "C" int gasfm_point_hub_bwd_ab(const float* X, int64_t N, float eps, cons
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const bool hr = dRes != nullptr;
   if (hr)
-    hipLaunchKernelGGL(point_hub_bwd_ab_kernel<true>, dim3((GASFM_PT_HUB_BWD_R ? hub_rows(N) : hub_ab_grid(N, true))), dim3(kThreads8), 0, st, X, N,
+    hipLaunchKernelGGL(point_hub_bwd_ab_kernel<true>, dim3((GASFM_PT_HUB_BWD_R ? hub_r_grid(N) : hub_ab_grid(N, true))), dim3(kThreads8), 0, st, X, N,
                        eps, gA, bA, WA, WB, dSA, dXL, dRes, dX, part);
   else
-    hipLaunchKernelGGL(point_hub_bwd_ab_kernel<false>, dim3((GASFM_PT_HUB_BWD_R ? hub_rows(N) : hub_ab_grid(N, false))), dim3(kThreads8), 0, st, X, N,
+    hipLaunchKernelGGL(point_hub_bwd_ab_kernel<false>, dim3((GASFM_PT_HUB_BWD_R ? hub_r_grid(N) : hub_ab_grid(N, false))), dim3(kThreads8), 0, st, X, N,
                        eps, gA, bA, WA, WB, dSA, dXL, dRes, dX, part);
   return launch_status("gasfm_point_hub_bwd_ab");
 }
@@ -2415,8 +2020,8 @@ extern "C" int gasfm_point_hub_bwd_ab(const float* X, int64_t N, float eps, cons
 extern "C" int gasfm_point_hub_bwd(const float* X, int64_t N, float eps, const float* gA, const float* bA,
                                    const float* WA, const float* WB, const float* gC, const float* bC,
                                    const float* WC, const float* bWC, const float* WD, const float* dSA,
-                                   const float* dXL, const float* dXR, const float* dRes, const float* T, float* dX,
-                                   float* part_a, float* part_c, void* stream) {
+                                   const float* dXL, const float* dXR, const float* dRes, float* dX, float* part_a,
+                                   float* part_c, void* stream) {
   GASFM_REQUIRE(N >= 0, "gasfm_point_hub_bwd: N < 0");
   if (N == 0) return GASFM_OK;
   GASFM_REQUIRE(X && gA && bA && WA && WB && gC && bC && WC && bWC && WD && dSA && dXL && dXR && dX && part_a &&
@@ -2430,22 +2035,8 @@ extern "C" int gasfm_point_hub_bwd(const float* X, int64_t N, float eps, const f
     if (st != GASFM_OK) return st;
     return gasfm_point_hub_bwd_ab(X, N, eps, gA, bA, WA, WB, dSA, dXL, dX, dX, part_a, stream);
   }
-  GASFM_REQUIRE(!T || (aligned16(T) && dX != T), "gasfm_point_hub_bwd: T alignment / aliasing");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int gsz = hub_rows(N);
-  if (T) {  // the split form: data path, then the weight gradients
-    if (dRes)
-      hipLaunchKernelGGL(point_hub_bwd_d_kernel<true>, dim3(gsz), dim3(kThreadsR), 0, st, X, N, eps, gA, bA, WA, WB,
-                         gC, bC, WC, WD, dSA, dXL, dXR, dRes, dX, part_a, part_c);
-    else
-      hipLaunchKernelGGL(point_hub_bwd_d_kernel<false>, dim3(gsz), dim3(kThreadsR), 0, st, X, N, eps, gA, bA, WA, WB,
-                         gC, bC, WC, WD, dSA, dXL, dXR, dRes, dX, part_a, part_c);
-    const int s1 = launch_status("gasfm_point_hub_bwd");
-    if (s1 != GASFM_OK) return s1;
-    hipLaunchKernelGGL(point_hub_wgrad_kernel, dim3(gsz), dim3(kThreadsR), 0, st, X, N, eps, gA, bA, gC, bC, WD, T,
-                       dSA, dXL, dXR, part_a, part_c);
-    return launch_status("gasfm_point_hub_bwd");
-  }
+  const int gsz = hub_r_grid(N);
   if (dRes)
     hipLaunchKernelGGL(point_hub_bwd_r_kernel<true>, dim3(gsz), dim3(kThreadsR), 0, st, X, N, eps, gA, bA, WA, WB,
                        gC, bC, WC, bWC, WD, dSA, dXL, dXR, dRes, dX, part_a, part_c);

@@ -2,8 +2,7 @@
 
 PointTailFn  -- the end of Proj2ScenePoint.forward (reference code/models/layers.py:438-454):
                 x = prev + proj_proj2scenepoint(agg);  p = x + mlp(relu(norm_pre_mlp(x)))
-PointHubFn   -- every consumer of the block output p, in one kernel forward and one backward
-                (two kernels: the data path, then the weight gradients):
+PointHubFn   -- every consumer of the block output p, in one kernel forward and two backward:
                 skip = p                                          next block's state skip (:442)
                 SA   = lin_scenepoint(relu(scenepoint_norm_layer(p)))            (:928-935)
                 XL   = graph_conv_scenepoint2global.lin_l(p)                     (:560-575, PyG)
@@ -15,17 +14,12 @@ block).  Routing every consumer through PointHubFn makes its backward the only p
 dp: the C pass adds the next block's target-row gradient to the incoming skip gradient, the
 A+B pass adds lin_l and lin_scenepoint terms in place, and no add kernel runs.
 """
-import os
-
 import torch
 
 from . import _native
 
 P_W = 64   # n_feat_scenepoint
 A_W = 32   # n_feat_proj
-# the hub backward as a data-path kernel + a weight-gradient kernel (round 6; the forward stores the
-# rows t = W_C relu(LN_C p) + b_C for it, 128 B per point); 0: the one-pass kernel
-HUB_SPLIT = os.environ.get("GASFM_PT_HUB_SPLIT", "0") != "0"
 
 
 def _f32(*shape, like):
@@ -78,9 +72,8 @@ class PointHubFn(torch.autograd.Function):
         WA, WB, WC, WD = (w.contiguous() for w in (WA, WB, WC, WD))
         N = p.shape[0]
         SA, XL, XR = _f32(N, A_W, like=p), _f32(N, P_W, like=p), _f32(N, A_W, like=p)
-        T = _f32(N, A_W, like=p) if HUB_SPLIT and N > 0 else None
-        _native.point_hub_fwd(p, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR, T)
-        ctx.save_for_backward(p, gA, bA, WA, WB, gC, bC, WC, bWC, WD, T)
+        _native.point_hub_fwd(p, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR)
+        ctx.save_for_backward(p, gA, bA, WA, WB, gC, bC, WC, bWC, WD)
         ctx.eps = eps
         ctx.defer = _native.defer_token(gA, bA, WA, WB, bB, gC, bC, WC, bWC, WD, bD)
         ctx.set_materialize_grads(False)
@@ -88,7 +81,7 @@ class PointHubFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dskip, dSA, dXL, dXR):
-        p, gA, bA, WA, WB, gC, bC, WC, bWC, WD, T = ctx.saved_tensors
+        p, gA, bA, WA, WB, gC, bC, WC, bWC, WD = ctx.saved_tensors
         N = p.shape[0]
         zeros = lambda w: torch.zeros((N, w), dtype=torch.float32, device=p.device)  # noqa: E731
         dSA = dSA.contiguous() if dSA is not None else zeros(A_W)
@@ -104,7 +97,7 @@ class PointHubFn(torch.autograd.Function):
         else:
             part_c, part_a = _f32(rc, cc, like=p), _f32(ra, ca, like=p)
             _native.point_hub_bwd(p, ctx.eps, gA, bA, WA, WB, gC, bC, WC, bWC, WD, dSA, dXL, dXR, dskip, dp,
-                                  part_a, part_c, T)
+                                  part_a, part_c)
             tc, ta = _native.param_colsum(part_c, ctx.defer), _native.param_colsum(part_a, ctx.defer)
         o = 0
         dWC = tc[o:o + A_W * P_W].view(A_W, P_W)

@@ -478,7 +478,7 @@ int gasfm_point_tail_bwd(const float* dout, const float* prev, const float* agg,
 int gasfm_point_hub_fwd(const float* X, int64_t N, float eps, const float* gA, const float* bA, const float* WA,
                         float* SA, const float* WB, const float* bB, float* XL, const float* gC, const float* bC,
                         const float* WC, const float* bWC, const float* WD, const float* bD, float* XR,
-                        float* T, void* stream);
+                        void* stream);
 
 /* dX = dRes + LN_C_bwd(mask (dXR WD WC)) (dRes may be null), partials. */
 int gasfm_point_hub_bwd_c(const float* X, int64_t N, float eps, const float* gC, const float* bC, const float* WC,
@@ -490,16 +490,14 @@ int gasfm_point_hub_bwd_ab(const float* X, int64_t N, float eps, const float* gA
                            const float* WA, const float* WB, const float* dSA, const float* dXL,
                            const float* dRes, float* dX, float* part, void* stream);
 
-/* The whole hub backward (both of the above): dX = dRes + dXL WB + LN_A_bwd(mask (dSA WA))
+/* The whole hub backward in one pass (both of the above; the two-pass form when the library is
+ * built with GASFM_PT_HUB_BWD_R=0): dX = dRes + dXL WB + LN_A_bwd(mask (dSA WA))
  * + LN_C_bwd(mask (dXR WD WC)); dRes may be null or alias dX, dX must not alias the other inputs.
- * T: the [N x 32] rows t = WC relu(LN_C(X)) + bWC that gasfm_point_hub_fwd stored (its T argument)
- * selects the split form (a data-path kernel, then a weight-gradient kernel, round 6); null selects
- * the one-pass kernel (the two-pass form when the library is built with GASFM_PT_HUB_BWD_R=0).
  * part_a / part_c: the which = 0 / which = 1 partial layouts above, gasfm_point_hub_part_shape rows. */
 int gasfm_point_hub_bwd(const float* X, int64_t N, float eps, const float* gA, const float* bA, const float* WA,
                         const float* WB, const float* gC, const float* bC, const float* WC, const float* bWC,
                         const float* WD, const float* dSA, const float* dXL, const float* dXR, const float* dRes,
-                        const float* T, float* dX, float* part_a, float* part_c, void* stream);
+                        float* dX, float* part_a, float* part_c, void* stream);
 
 /* ---- input embedding (embed.hip): P = values W^T + b, the Linear(2, 2) of EmbeddingLayer
  * (layers.py:992-1015, graph_attn_sfm.py:53); values, P [E x 2] row-major, W [2 x 2], b [2]. */

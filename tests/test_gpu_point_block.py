@@ -100,40 +100,3 @@ def test_point_hub_deterministic(device):
         res.append([t.grad.clone() for t in ins])
     for a, b in zip(*res):
         assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("N", [1, 17, 1000, 70_001])
-@pytest.mark.parametrize("with_skip", [True, False])
-def test_point_hub_split_matches_one_pass(device, N, with_skip):
-    """The split hub backward (data kernel + weight-gradient kernel, fed the forward's stored t rows)
-    against the one-pass kernel on the same inputs: dp bitwise (the data kernel runs the one-pass
-    kernel's ops in its order), the partial column sums to 1e-5 of their norm (another grouping of
-    the rows), and the stored t rows against the fp64 composition."""
-    from gasfm_amd import _native
-    g = torch.Generator().manual_seed(7 * N + with_skip)
-    ins = [_rnd(g, N, 64, scale=1.5, shift=-0.2), _rnd(g, 64, scale=0.3, shift=1), _rnd(g, 64, scale=0.2),
-           _rnd(g, 32, 64, scale=0.125), _rnd(g, 64, 64, scale=0.125), _rnd(g, 64, scale=0.1),
-           _rnd(g, 64, scale=0.3, shift=1), _rnd(g, 64, scale=0.2), _rnd(g, 32, 64, scale=0.125),
-           _rnd(g, 32, scale=0.1), _rnd(g, 32, 32, scale=0.18), _rnd(g, 32, scale=0.1)]
-    p, gA, bA, WA, WB, bB, gC, bC, WC, bWC, WD, bD = (t.float().to(device).contiguous() for t in ins)
-    dsk = _rnd(g, N, 64).float().to(device) if with_skip else None
-    dSA, dXL, dXR = (_rnd(g, N, w).float().to(device) for w in (32, 64, 32))
-    SA, XL, XR, T = (torch.empty(N, w, device=device) for w in (32, 64, 32, 32))
-    _native.point_hub_fwd(p, EPS, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR, T)
-    t64 = F.linear(F.relu(F.layer_norm(ins[0], (64,), ins[6], ins[7], EPS)), ins[8], ins[9])
-    torch.testing.assert_close(T.double().cpu(), t64, rtol=0, atol=2e-5 * t64.abs().max().item() + 1e-5)
-    out = {}
-    for split in (False, True):
-        rc, cc = _native.point_hub_part_shape(N, 1, with_skip)
-        ra, ca = _native.point_hub_part_shape(N, 0, True)
-        part_c = torch.full((rc, cc), float("nan"), device=device)
-        part_a = torch.full((ra, ca), float("nan"), device=device)
-        dp = torch.empty(N, 64, device=device)
-        _native.point_hub_bwd(p, EPS, gA, bA, WA, WB, gC, bC, WC, bWC, WD, dSA, dXL, dXR, dsk, dp, part_a, part_c,
-                              T if split else None)
-        out[split] = (dp, part_a.sum(0), part_c.sum(0))
-    assert torch.equal(out[False][0], out[True][0])
-    for k in (1, 2):
-        a, b = out[True][k], out[False][k]
-        assert torch.isfinite(a).all()
-        assert (a - b).norm().item() <= 1e-5 * b.norm().item() + 1e-6

@@ -50,13 +50,8 @@ def main():
         dp2 = r(N, 64)
         t_h1 = timeit(lambda: _native.point_hub_bwd(X, 1e-5, gA, bA, WA, WB, gC, bC, WC, bWC, WD, dSA, dXL, dXR,
                                                     dskip, dp2, pa, pc))
-        T = r(N, 32)
-        t_hfT = timeit(lambda: _native.point_hub_fwd(X, 1e-5, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR,
-                                                     T))
-        t_hs = timeit(lambda: _native.point_hub_bwd(X, 1e-5, gA, bA, WA, WB, gC, bC, WC, bWC, WD, dSA, dXL, dXR,
-                                                    dskip, dp2, pa, pc, T))
-        print(f"kernel us N={N}: tail_fwd {t_tf:.1f} tail_bwd {t_tb:.1f} hub_fwd {t_hf:.1f} (+T {t_hfT:.1f}) "
-              f"hub_bwd_c {t_hc:.1f} hub_bwd_ab {t_ha:.1f} hub_bwd (one pass) {t_h1:.1f} (split) {t_hs:.1f} "
+        print(f"kernel us N={N}: tail_fwd {t_tf:.1f} tail_bwd {t_tb:.1f} hub_fwd {t_hf:.1f} "
+              f"hub_bwd_c {t_hc:.1f} hub_bwd_ab {t_ha:.1f} hub_bwd (one pass) {t_h1:.1f} "
               f"(part rows tail {rows}, hub {rc}/{ra})", flush=True)
 
 
