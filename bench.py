@@ -91,9 +91,16 @@ def pmc_kernel_traffic(names, E):
     return None
 
 
+# spin-kernel length (torch.cuda._sleep cycles) issued before each timed launch: the start event, the
+# launch and the end event are then all enqueued while the GPU spins, so the events bracket the
+# kernel's execution and not the host's enqueue latency (rocprof's in-step durations agree)
+HOLD_CYCLES = 2_000_000
+
+
 class LaunchTimer:
     """HIP events around every call of a gasfm_amd._native launcher (module attribute swapped in place,
-    restored by close()) whose arguments ``select`` accepts, on the stream the launch goes to."""
+    restored by close()) whose arguments ``select`` accepts, on the stream the launch goes to; the
+    stream is held by a spin kernel (HOLD_CYCLES) while the three are enqueued."""
 
     def __init__(self, name, select):
         from gasfm_amd import _native
@@ -104,6 +111,7 @@ class LaunchTimer:
             if not select(*a, **k):
                 return self.orig(*a, **k)
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            torch.cuda._sleep(HOLD_CYCLES)
             ev[0].record()
             r = self.orig(*a, **k)
             ev[1].record()
@@ -345,7 +353,7 @@ def main():
     # timed region (events cannot be read out of a replayed graph): events around each of its
     # launches (mean_us: matches rocprof's in-step durations), plus 20 back-to-back re-launches
     # on the inputs of its last launch (mean_us_back_to_back: cache-warm, informational)
-    timer = attention.KernelTimer(lambda tag, HC: tag == "proj2scenepoint" and HC == 32)
+    timer = attention.KernelTimer(lambda tag, HC: tag == "proj2scenepoint" and HC == 32, hold_cycles=HOLD_CYCLES)
     attention.KERNEL_TIMER = timer
     timer.enabled = True
     # the dominant kernel: edge_cam_pbwd with LayerNorm and the residual term (blocks 1..11); with the
@@ -424,8 +432,9 @@ def main():
                          "hbm_frac": (pbwd_gbs / HBM_PEAK_GBS) if pbwd_gbs else None,
                          "mean_us": pbwd_ms * 1e3 if pbwd_ms else None, "launches_timed": pbwd_launches,
                          "timing": "HIP events on the launch stream around each of its launches in 2 eager steps "
-                                   "after the timed region (agrees with the rocprof durations inside the replayed "
-                                   "step)"},
+                                   "after the timed region, the stream held by a spin kernel while the events and "
+                                   "the launch are enqueued (the host's enqueue latency is not timed; agrees with "
+                                   "the rocprof durations inside the replayed step)"},
             "roofline_attention": {"kernel": "attn_fwd_grp_kernel<4,1> point direction (proj2scenepoint), per launch",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
@@ -436,7 +445,8 @@ def main():
                          "mean_us_back_to_back": b2b_ms * 1e3 if b2b_ms else None,
                          "launches_timed": len(timer.events),
                          "timing": "HIP events on the launch stream around each of its launches in 2 eager steps "
-                                   "after the timed region (mean_us; agrees with the rocprof durations inside the "
+                                   "after the timed region, the stream held by a spin kernel while the events and "
+                                   "the launch are enqueued (mean_us; agrees with the rocprof durations inside the "
                                    "replayed step); mean_us_back_to_back: 20 re-launches on the inputs of its last "
                                    "launch between two events (cache-warm, not used for achieved)"},
             "execution": execution,

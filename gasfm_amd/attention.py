@@ -107,15 +107,24 @@ KERNEL_TIMER = None
 class KernelTimer:
     """Records (start, end) torch.cuda.Events around selected kernel launches."""
 
-    def __init__(self, select):
+    def __init__(self, select, hold_cycles=0):
         self.select = select
         self.events = []
         self.enabled = False
+        self.hold_cycles = int(hold_cycles)  # hold(): spin-kernel length
         self.gathered = None  # whether the timed launches read XL through perm
         self.launch = None    # closure re-issuing the last timed launch (same inputs / outputs)
 
     def __call__(self, tag, HC):
         return self.enabled and self.select(tag, HC)
+
+    def hold(self):
+        """Before a timed launch: a spin kernel on the stream, so the start event, the kernel and the
+        end event are all enqueued before the GPU reaches them -- the events then bracket the
+        kernel's execution, not the host's enqueue latency (eager launches at a rank's shard size
+        are host-bound: the GPU would otherwise sit idle between the start event and the kernel)."""
+        if self.hold_cycles > 0:
+            torch.cuda._sleep(self.hold_cycles)
 
     def mean_ms(self):
         torch.cuda.synchronize()
@@ -344,6 +353,7 @@ def attn_forward_raw(XL, XR, att, bias, plan, heads, slope, finalize=True, xl_so
     timed = KERNEL_TIMER is not None and KERNEL_TIMER(plan.tag, HC)
     if timed:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        KERNEL_TIMER.hold()
         ev[0].record()
     def launch():
         _native.attn_fwd(XL, XR, attf, bias, None if xl_sorted else plan.perm, plan.items, plan.n_items, heads, C,
