@@ -25,7 +25,27 @@ After each replay every parameter's ``.grad`` is (re)set to the tensor the graph
 ``optimizer.zero_grad()`` between steps is harmless; a replay does not accumulate into an
 existing gradient (each replay's gradients are that step's alone, as after zero_grad + backward).
 """
+import contextlib
+import gc
+
 import torch
+
+
+@contextlib.contextmanager
+def gc_paused():
+    """Python's cyclic garbage collector off for the duration (a stream capture).  A collection
+    that runs mid-capture finalises whatever cyclic garbage is pending, e.g. an earlier step's
+    CUDAGraph, whose hipGraphExecDestroy on the capturing thread is refused under
+    capture_error_mode="thread_local" and aborts the process from the destructor (seen once in
+    the GPU suite, round 6).  torch.cuda.graph collects before it begins capturing; this keeps
+    the collector from running again until the capture has ended."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def retire_collectives():
@@ -138,7 +158,7 @@ class CapturedStep:
             # while it captures.  ProcessGroupNCCL's watchdog thread queries nothing during the
             # capture: every warm-up collective was retired from its list above, and collectives
             # issued while capturing are never put on it (they belong to the graph).
-            with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):  # records only
+            with gc_paused(), torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):  # records only
                 out = self.fn()
         except RuntimeError as e:  # capture unsupported for some op
             self.fallback_reason = f"capture failed: {e}"

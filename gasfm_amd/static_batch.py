@@ -50,6 +50,7 @@ import torch
 from . import _native
 from .attention import DEFAULT_MAX_PIECE, AttnPlan
 from .batch import _scene_arrays
+from .graph_step import gc_paused
 from .model import EdgeIndex
 from .scene import MIN_N_POINTS_PER_VIEW, MIN_N_VIEWS_PER_POINT, AxialAggregationGraphWrapper, SparseMat
 
@@ -596,7 +597,7 @@ class StaticTrainer:
         elif b[1].captured and opt.defaults.get("capturable") and all(p in opt.state for p in self.params):
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize()
-            with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
+            with gc_paused(), torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
                 opt.step()
             g.replay()
             b.append(g)
