@@ -112,8 +112,9 @@ def test_colsum_tall_in_captured_graph(device):
     with torch.cuda.stream(s):
         _native.colsum_tall(A)
     torch.cuda.current_stream().wait_stream(s)
+    from gasfm_amd.graph_step import gc_paused
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with gc_paused(), torch.cuda.graph(g):
         out = _native.colsum_tall(A)
     for _ in range(3):
         g.replay()
