@@ -29,17 +29,21 @@ def camera_max_piece(num_edges):
     (distributed.shard_scene; whole scenes and training batches keep DEFAULT_MAX_PIECE: a training
     batch is host-bound and measured 6 ms per step slower with the extra split pieces' launches).
 
-    256 (DEFAULT_MAX_PIECE), halved down to 64 while the plan would hold fewer than ~4 items per
-    resident wave of the camera-item edge kernels (512 workgroups x 4 waves): a 1/8-points shard
-    (~500 edges per camera) otherwise runs edge_cam_pbwd / edge_seam_fwd / edge_epilogue_bwd at
-    about one 16-tile item per wave.  Rank 0 of 8 (bench.py --emulate-world 8): 9.92 ms at 256,
-    9.33 at 128, 9.26 at 64; the whole config-4 scene stays at 256 (31.94 vs 32.15 ms at 128).
+    256 (DEFAULT_MAX_PIECE), stepped down through 128, 64 and 48 while the plan would hold fewer than
+    ~4 items per resident wave of the camera-item edge kernels (512 workgroups x 4 waves): a
+    1/8-points shard (~500 edges per camera) otherwise runs edge_cam_pbwd / edge_seam_fwd /
+    edge_epilogue_bwd at about one 16-tile item per wave.  Rank 0 of 8 (bench.py --emulate-world 8):
+    9.92 ms at 256, 9.33 at 128, 9.26 at 64 (round 3); the whole config-4 scene stays at 256 (31.94 vs
+    32.15 ms at 128).  Round 6, the 48 step: at 64 the shard's 8,277 pieces are 4.04 per resident wave,
+    so the 85 waves that take a fifth 4-tile piece set the launch's length (the grid-stride maximum is
+    20 tiles per wave against a mean of 16.2); 3-tile pieces spread the tail: edge_cam_pbwd 118.3 ->
+    113.4 us, the proxy 7.13-7.14 -> 7.04-7.05 ms (32: 7.11-7.12, 96: 7.13; profiles/r6_ab_cam_piece.txt).
     """
     if _MAX_PIECE_ENV:
         return int(_MAX_PIECE_ENV)
     mp = DEFAULT_MAX_PIECE
-    while mp > 64 and num_edges < 8192 * mp:
-        mp //= 2
+    while mp > 48 and num_edges < 8192 * mp:
+        mp = mp // 2 if mp > 64 else 48
     return mp
 LANES_MAX_AVG = 32  # 4-wide convs with <= this many edges per item on average: one lane per item
 # The lane-per-item forward replaced a 226 us launch by a 43 us one at config 4.  The backward with
