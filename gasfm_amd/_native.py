@@ -244,9 +244,9 @@ def _stream(t):
 KERNELS = {
     "attn_fwd_grp": 0, "attn_fwd_glds": 1, "attn_fwd_vec": 2, "attn_fwd_generic": 3, "attn_fwd_lanes": 4,
     "attn_bwd_glds": 5, "attn_bwd_vec": 6, "attn_bwd_generic": 7, "attn_bwd_lanes": 8,
-    "attn_combine_vec": 9, "attn_combine_generic": 10, "seam_reg": 13,
+    "attn_combine_vec": 9, "attn_combine_generic": 10, "seam_reg": 13, "attn_fwd_grp_s2": 14, "attn_fwd_grp_s4": 15,
 }
-TUNING = {"attn_grp_rows": 0, "attn_grp_min_fill": 1, "attn_glds": 2, "attn_wave_cap": 3}
+TUNING = {"attn_grp_rows": 0, "attn_grp_min_fill": 1, "attn_glds": 2, "attn_wave_cap": 3, "attn_grp_split": 4}
 
 
 def dispatch_counts():

@@ -28,6 +28,7 @@ struct Tuning {
     v[GASFM_TUNE_ATTN_GRP_MIN_FILL] = env("GASFM_ATTN_GRP_MIN_FILL", 0.5);
     v[GASFM_TUNE_ATTN_GLDS] = env("GASFM_ATTN_GLDS", 1);
     v[GASFM_TUNE_ATTN_WAVE_CAP] = env("GASFM_ATTN_WAVES", 0);
+    v[GASFM_TUNE_ATTN_GRP_SPLIT] = env("GASFM_ATTN_SPLIT", 0);
   }
 };
 

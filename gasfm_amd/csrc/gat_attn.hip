@@ -455,16 +455,23 @@ __global__ __launch_bounds__(kBlock) void attn_fwd_glds_kernel(
 // ~(mean / padded max) lane occupancy instead of 20/32, with no per-item tail.
 // Pipelining: every iteration waits for its rows, issues the NEXT iteration's U rows (or, at
 // the last iteration of a task, the next task's first rows and XR rows), then computes.
+// S > 1 (round 6, small shards): S lane groups share an item -- group s of the item takes rows
+// k + s U .. k + s U + U - 1 of each S U-row step -- so a task holds 8 / S items, the grid S times
+// the waves, and a wave's dependent chain of row round trips is S times shorter; the S online
+// softmax states merge by an xor butterfly over the groups at the item's end (group 0 stores).
+// A rank-of-8 point shard (25k points) is ~3k tasks at S = 1: 12 waves per CU, each walking ~8
+// round trips, i.e. latency-bound.
 // ------------------------------------------------------------------------------------------
-template <int U, int MINW>
+template <int U, int MINW, int S>
 __global__ __launch_bounds__(kBlock, MINW) void attn_fwd_grp_kernel(
     const float* __restrict__ XL, int64_t ldXL, const float* __restrict__ XR, int64_t ldXR,
     const float* __restrict__ att, const float* __restrict__ bias, const gasfm_work_item* __restrict__ items,
     int n_items, float slope, int finalize, float* __restrict__ out, int64_t ldOut, float* __restrict__ seg_max,
     float* __restrict__ seg_sum, int64_t ldStat, float* __restrict__ part) {
-  constexpr int HC = 32, H = 4, C = 8, LDP = HC + 2 * H, GR = 8;
+  static_assert(S == 1 || S == 2 || S == 4, "lane groups per item");
+  constexpr int HC = 32, H = 4, C = 8, LDP = HC + 2 * H, GR = 8 / S, STEP = U * S;
   const int lane = threadIdx.x & (kWave - 1);
-  const int g = lane >> 3, li = lane & 7, f0 = li * 4, h = f0 / C;
+  const int g = (lane >> 3) / S, sub = (lane >> 3) % S, li = lane & 7, f0 = li * 4, h = f0 / C;
   const int nwaves = gridDim.x * (blockDim.x / kWave);
   const int ntasks = (n_items + GR - 1) / GR;
   float attv[4], bv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -488,7 +495,7 @@ __global__ __launch_bounds__(kBlock, MINW) void attn_fwd_grp_kernel(
     const int64_t base = w.begin < w.end ? w.begin : 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t r = int64_t(w.begin) + k + u;
+      const int64_t r = int64_t(w.begin) + k + sub * U + u;
       load_vec<4>(x[u], XL + (r < w.end ? r : base) * ldXL + f0);
     }
   };
@@ -506,14 +513,14 @@ __global__ __launch_bounds__(kBlock, MINW) void attn_fwd_grp_kernel(
     float xrn[4] = {0.f, 0.f, 0.f, 0.f};
     float m = -INFINITY, ssum = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
     const int len = w.end - w.begin;
-    for (int k = 0; k < L; k += U) {
+    for (int k = 0; k < L; k += STEP) {
       float xl[U][4];
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int v = 0; v < 4; ++v) xl[u][v] = nx[u][v];
-      if (k + U < L) {
-        issue(w, k + U, nx);
+      if (k + STEP < L) {
+        issue(w, k + STEP, nx);
       } else {  // last iteration of this task: start the next one
         Ln = wave_max_len(wn);
         if (wn.seg >= 0) load_vec<4>(xrn, XR + int64_t(wn.seg) * ldXR + f0);
@@ -526,7 +533,7 @@ __global__ __launch_bounds__(kBlock, MINW) void attn_fwd_grp_kernel(
 #pragma unroll
         for (int v = 0; v < 4; ++v) p = fmaf(leaky(xl[u][v] + xr[v], slope), attv[v], p);
         p += xor_lane<1>(p);  // the 2 lanes of a head
-        lg[u] = (k + u < len) ? p : -INFINITY;
+        lg[u] = (k + sub * U + u < len) ? p : -INFINITY;
       }
       float cm = lg[0];
 #pragma unroll
@@ -550,7 +557,22 @@ __global__ __launch_bounds__(kBlock, MINW) void attn_fwd_grp_kernel(
       if (wn.seg >= 0) load_vec<4>(xrn, XR + int64_t(wn.seg) * ldXR + f0);
       if (Ln > 0) issue(wn, 0, nx);
     }
-    if (w.seg >= 0) {
+    if constexpr (S > 1) {  // the item's S group states, butterfly over the group bits of the lane id
+#pragma unroll
+      for (int o = 8; o < 8 * S; o *= 2) {
+        const float m2 = __shfl_xor(m, o), s2 = __shfl_xor(ssum, o);
+        float a2[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) a2[v] = __shfl_xor(acc[v], o);
+        const float mn = fmaxf(m, m2);
+        const float f1 = safe_scale(m, mn), f2 = safe_scale(m2, mn);
+        ssum = ssum * f1 + s2 * f2;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[v] = acc[v] * f1 + a2[v] * f2;
+        m = mn;
+      }
+    }
+    if (w.seg >= 0 && sub == 0) {
       const bool head_leader = (li & 1) == 0;
       if (w.slot < 0) {
         float o[4];
@@ -1165,6 +1187,17 @@ static int grp_rows() {
   return (v == 8 || v == 4 || v == 46 || v == 48) ? v : 0;
 }
 
+// Lane groups per item of the U = 4 grouped forward (GASFM_ATTN_SPLIT: 1 / 2 / 4 forced; 0 = by
+// size: S = 2 when the S = 1 tasks fit in one round of the resident waves, i.e. every wave would
+// walk a single task's chain of row round trips; else S = 1).  Measured (profiles/r6_ab_attn_split.txt,
+// events): a rank-of-8 shard's 25k points 23.6-24.2 -> 21.7-21.9 us at S = 2 (22.4-22.5 at S = 4);
+// config 4's 200k points (25k tasks, 6x the resident waves) 114.0 at S = 1 vs 114.7 / 120.1.
+static int grp_split(int n_items, int resident_waves) {
+  const int v = int(tune(GASFM_TUNE_ATTN_GRP_SPLIT));
+  if (v == 1 || v == 2 || v == 4) return v;
+  return int64_t(n_items) <= int64_t(8) * resident_waves ? 2 : 1;
+}
+
 // Minimum fill (wave tasks / resident waves) for the grouped-item forward (A/B knob
 // GASFM_ATTN_GRP_MIN_FILL; 0 = always grouped when enabled).
 static double grp_min_fill() { return tune(GASFM_TUNE_ATTN_GRP_MIN_FILL); }
@@ -1217,26 +1250,39 @@ extern "C" int gasfm_gat_attn_fwd(const float* XL, int64_t ldXL, const float* XR
   const bool grp_fills = [&] {
     if (grp <= 0) return false;
     const int tasks = (n_items + 7) / 8;
-    const int res = resident_blocks(reinterpret_cast<const void*>(&attn_fwd_grp_kernel<4, 1>), kBlock, 0) *
+    const int res = resident_blocks(reinterpret_cast<const void*>(&attn_fwd_grp_kernel<4, 1, 1>), kBlock, 0) *
                     (kBlock / kWave);
     return double(tasks) >= grp_min_fill() * double(res);
   }();
   if (vec_ok && perm == nullptr && H * C == 32 && C == 8 && grp_fills) {
-    auto launch = [&](auto kern) {
-      const int tasks = (n_items + 7) / 8;
+    auto launch = [&](auto kern, int S) {
+      const int per = 8 / S;
+      const int tasks = (n_items + per - 1) / per;
       const int grid = grid_for(tasks, resident_blocks(reinterpret_cast<const void*>(kern), kBlock, 0));
       hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, XL, ldXL, XR, ldXR, att, bias, items, n_items,
                          slope, finalize, out, ldOut, seg_max, seg_sum, ldStat, part);
     };
     note_dispatch(GASFM_K_ATTN_FWD_GRP);
-    if (grp == 8)
-      launch(&attn_fwd_grp_kernel<8, 1>);
-    else if (grp == 46)
-      launch(&attn_fwd_grp_kernel<4, 6>);
-    else if (grp == 48)
-      launch(&attn_fwd_grp_kernel<4, 8>);
-    else
-      launch(&attn_fwd_grp_kernel<4, 1>);
+    if (grp == 8) {
+      launch(&attn_fwd_grp_kernel<8, 1, 1>, 1);
+    } else if (grp == 46) {
+      launch(&attn_fwd_grp_kernel<4, 6, 1>, 1);
+    } else if (grp == 48) {
+      launch(&attn_fwd_grp_kernel<4, 8, 1>, 1);
+    } else {
+      const int res =
+          resident_blocks(reinterpret_cast<const void*>(&attn_fwd_grp_kernel<4, 1, 2>), kBlock, 0) * (kBlock / kWave);
+      const int S = grp_split(n_items, env_wave_cap() ? env_wave_cap() : res);
+      if (S == 4) {
+        note_dispatch(GASFM_K_ATTN_FWD_GRP_S4);
+        launch(&attn_fwd_grp_kernel<4, 1, 4>, 4);
+      } else if (S == 2) {
+        note_dispatch(GASFM_K_ATTN_FWD_GRP_S2);
+        launch(&attn_fwd_grp_kernel<4, 1, 2>, 2);
+      } else {
+        launch(&attn_fwd_grp_kernel<4, 1, 1>, 1);
+      }
+    }
     done = true;
   }
   if (!done && vec_ok && perm == nullptr && H * C == 32 && C == 8 && glds_enabled()) {

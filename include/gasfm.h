@@ -75,9 +75,11 @@ enum {
   GASFM_K_ATTN_BWD_LANES = 8,
   GASFM_K_ATTN_COMBINE_VEC = 9,
   GASFM_K_ATTN_COMBINE_GENERIC = 10,
-  /* 11, 12, 14: reserved (round-4 variants measured and removed: grouped attention backward,
-   * LDS-staged forward seam, grouped segment row sums) */
+  /* 11, 12: reserved (round-4 variants measured and removed: grouped attention backward,
+   * LDS-staged forward seam); 14 was the grouped segment row sums */
   GASFM_K_SEAM_REG = 13,         /* forward seam (blocks 1-11) */
+  GASFM_K_ATTN_FWD_GRP_S2 = 14,  /* grouped items, 2 lane groups per item (also counted as _GRP) */
+  GASFM_K_ATTN_FWD_GRP_S4 = 15,  /* grouped items, 4 lane groups per item (also counted as _GRP) */
   GASFM_K_COUNT = 16
 };
 
@@ -92,7 +94,9 @@ enum {
   GASFM_TUNE_ATTN_GRP_MIN_FILL = 1,  /* GASFM_ATTN_GRP_MIN_FILL: grouped when tasks >= fill x resident waves */
   GASFM_TUNE_ATTN_GLDS = 2,          /* GASFM_ATTN_GLDS: direct-to-LDS kernels on (1) / off (0) */
   GASFM_TUNE_ATTN_WAVE_CAP = 3,      /* GASFM_ATTN_WAVES: cap on item-loop waves, 0 = occupancy */
-  /* 4, 5, 6: reserved (removed round-4 variants) */
+  GASFM_TUNE_ATTN_GRP_SPLIT = 4,     /* GASFM_ATTN_SPLIT: lane groups per item of the grouped forward, 1 / 2 / 4;
+                                        0 = by size: 2 when the 1-group tasks fit in the resident waves */
+  /* 5, 6: reserved (removed round-4 variants) */
   GASFM_TUNE_COUNT = 8
 };
 int gasfm_tuning_set(int32_t key, double value);

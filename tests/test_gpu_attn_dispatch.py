@@ -121,14 +121,17 @@ def scene_plans(device):
 def test_point_direction_grouped_forward_vs_oracle(device, scene_plans, scale):
     """The model's point-direction conv exactly as the bench runs it (xl_sorted, no perm): the
     grouped-item forward must be the kernel that ran, at scaled_config4(0.1) (20k points, 2.5k wave
-    tasks) and at full config 4 (200k points, 4,001,638 edges)."""
+    tasks: the 2-groups-per-item form) and at full config 4 (200k points, 4,001,638 edges)."""
     sc, plans = scene_plans(scale)
     plan = plans["proj2scenepoint"]
     assert plan.perm is not None and plan.pos is not None
     H, C = 4, 8
     XLs, XR, att, bias, gout = inputs(device, plan.num_edges, plan.num_targets, H, C, seed=int(scale * 100))
     got, fwd, bwd = run_case(device, plan, XLs, XR, att, bias, H, gout, xl_sorted=True)
-    assert fwd["attn_fwd_grp"] == 1 and sum(fwd.values()) == 1, fwd
+    assert fwd["attn_fwd_grp"] == 1 and sum(v for k, v in fwd.items() if not k.startswith("attn_fwd_grp_s")) == 1, fwd
+    # 20k points (2.5k tasks of 8 items, under one round of resident waves): 2 lane groups per item;
+    # config 4's 25k tasks: one group per item
+    assert fwd["attn_fwd_grp_s2"] == (1 if scale < 1.0 else 0) and fwd["attn_fwd_grp_s4"] == 0, fwd
     assert bwd["attn_bwd_glds"] == 1, bwd
     ref = oracle_sorted(XLs, XR, att, bias, plan, gout, H)
     nonempty = (plan.seg_ptr[1:] > plan.seg_ptr[:-1]).to(device)
@@ -178,7 +181,10 @@ def random_sorted_plan(device, N, E, max_piece, seed, empty_frac=0.15):
 
 # every variant of the forward dispatch, forced at a small size: (tuning, expected kernel)
 VARIANTS = [
-    (dict(attn_grp_rows=4, attn_grp_min_fill=0), "attn_fwd_grp"),
+    (dict(attn_grp_rows=4, attn_grp_min_fill=0, attn_grp_split=1), "attn_fwd_grp"),
+    # round 6: 2 / 4 lane groups per item (the small-shard form), states merged at the item's end
+    (dict(attn_grp_rows=4, attn_grp_min_fill=0, attn_grp_split=2), "attn_fwd_grp_s2"),
+    (dict(attn_grp_rows=4, attn_grp_min_fill=0, attn_grp_split=4), "attn_fwd_grp_s4"),
     (dict(attn_grp_rows=8, attn_grp_min_fill=0), "attn_fwd_grp"),
     (dict(attn_grp_rows=46, attn_grp_min_fill=0), "attn_fwd_grp"),
     (dict(attn_grp_rows=48, attn_grp_min_fill=0), "attn_fwd_grp"),
@@ -198,7 +204,12 @@ def test_forced_forward_variants_vs_oracle(device, tuning, kernel, max_piece):
     XLs, XR, att, bias, gout = inputs(device, E, N, H, C, seed=3)
     with _native.tuned(**tuning):
         got, fwd, bwd = run_case(device, plan, XLs, XR, att, bias, H, gout, xl_sorted=False)
-    assert fwd[kernel] == 1 and sum(v for k, v in fwd.items() if k.startswith("attn_fwd")) == 1, fwd
+    # the split forms also count as attn_fwd_grp (one kernel launched)
+    launched = sum(v for k, v in fwd.items() if k.startswith("attn_fwd") and not k.startswith("attn_fwd_grp_s"))
+    assert fwd[kernel] == 1 and launched == 1, fwd
+    if kernel.startswith("attn_fwd_grp"):
+        assert fwd["attn_fwd_grp"] == 1 and fwd["attn_fwd_grp_s2"] == (kernel == "attn_fwd_grp_s2") \
+            and fwd["attn_fwd_grp_s4"] == (kernel == "attn_fwd_grp_s4"), fwd
     ref = oracle_sorted(XLs, XR, att, bias, plan, gout, H)
     nonempty = (plan.seg_ptr[1:] > plan.seg_ptr[:-1]).to(device)
     compare(got, ref, nonempty, f"{kernel} {tuning}")

@@ -1,6 +1,7 @@
 """Time the edge-softmax + aggregate kernels alone on the config-4 plans (GPU box).
 
-usage: python tools/attn_bench.py [--reps R]
+usage: python tools/attn_bench.py [--reps R] [--points N]
+(--points 25000: a rank-of-8 point shard's size, all 1000 cameras; default config 4's 200k)
 Prints one JSON line per direction with the forward / backward mean launch time (HIP events
 on the launch stream) and the achieved GB/s from the algorithmic byte formulas of
 BASELINE.md (forward: E*4*HC + E*4*perm + 2*N*4*HC + N*8*H + (N+1)*4).
@@ -34,9 +35,10 @@ def _time(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--points", type=int, default=200_000)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    sc = synthetic.config4()
+    sc = synthetic.config4(n=args.points)
     data = SceneData.from_synthetic(sc).to(dev)
     E = sc.num_edges
     H, HC = 4, 32
