@@ -175,6 +175,7 @@ _SIGS = {
     "gasfm_point_tail_bwd": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_point_hub_fwd": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp, _vp, _vp]),
+    "gasfm_point_tail_hub_fwd": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _f32] + [_vp] * 15),
     "gasfm_point_hub_bwd_c": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_point_hub_bwd_ab": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gasfm_point_hub_bwd": (_i32, [_vp, _i64, _f32] + [_vp] * 17),
@@ -853,6 +854,19 @@ def point_hub_fwd(X, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, X
     st = lib().gasfm_point_hub_fwd(_p(X), X.shape[0], eps, _p(gA), _p(bA), _p(WA), _p(SA), _p(WB), _p(bB), _p(XL),
                                    _p(gC), _p(bC), _p(WC), _p(bWC), _p(WD), _p(bD), _p(XR), _stream(X))
     check(st, "gasfm_point_hub_fwd")
+
+
+def point_tail_hub_fwd(prev, agg, Wp, bp, ln_w, ln_b, eps, Wm, bm, out, eps_h, gA, bA, WA, SA, WB, bB, XL, gC, bC,
+                       WC, bWC, WD, bD, XR):
+    """point_tail_fwd + point_hub_fwd on its output in one launch (out = p)."""
+    _req(agg, "agg", 32)
+    _req(out, "out", 64)
+    if prev is not None:
+        _req(prev, "prev", 64)
+    st = lib().gasfm_point_tail_hub_fwd(_p(prev), _p(agg), agg.shape[0], _p(Wp), _p(bp), _p(ln_w), _p(ln_b), eps,
+                                        _p(Wm), _p(bm), _p(out), eps_h, _p(gA), _p(bA), _p(WA), _p(SA), _p(WB), _p(bB),
+                                        _p(XL), _p(gC), _p(bC), _p(WC), _p(bWC), _p(WD), _p(bD), _p(XR), _stream(agg))
+    check(st, "gasfm_point_tail_hub_fwd")
 
 
 def point_hub_bwd_c(X, eps, gC, bC, WC, bWC, WD, dXR, dRes, dX, part):

@@ -1050,6 +1050,111 @@ __device__ __forceinline__ void slab_stats(const f32x4 (&x)[4], float eps, float
   rstd = rsq_normal(sum_groups(q) * (1.f / FP) + eps);
 }
 
+// One 16-row tile of the tail in registers (T layout in, T layout out): y = x + W_m relu(LN(x)) + b_m,
+// x = prev + W_p agg + b_p; V = [b_p | gamma | beta | b_m] in LDS.  Shared by the tail kernel and the
+// fused tail + hub kernel (the same instruction sequence: bitwise the same p).
+__device__ __forceinline__ void tail_tile_t(const float4* __restrict__ WpQ, const float4* __restrict__ WmQ,
+                                            const float* V, const f32x4 (&ag)[2], const f32x4 (&pv)[4], float eps,
+                                            int lane, f32x4 (&y)[4]) {
+  const int g = lane >> 4;
+  f32x4 x[4];
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot) x[ot] = vec_at(V, ot, g) + pv[ot];  // b_p + prev, then + W_p agg
+  layer_t<4, 2>(WpQ, ag, x, lane);
+  f32x4 gm[4], bt[4];
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot) {
+    gm[ot] = vec_at(V + FP, ot, g);
+    bt[ot] = vec_at(V + 2 * FP, ot, g);
+  }
+  float mean, rstd;
+  slab_stats(x, eps, mean, rstd);
+  f32x4 h[4];
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) h[ot][j] = fmaxf(fmaf((x[ot][j] - mean) * rstd, gm[ot][j], bt[ot][j]), 0.f);
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot) y[ot] = vec_at(V + 3 * FP, ot, g);  // b_m, then + W_m h
+  layer_t<4, 4>(WmQ, h, y, lane);
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot) y[ot] = x[ot] + y[ot];
+}
+
+// One 16-row tile of the hub on p in registers (T layout): XL = W_B p + b_B, SA = W_A relu(LN_A p),
+// (HC) XR = W_D (W_C relu(LN_C p) + b_C) + b_D, stored as rows row0 .. row0 + nrows - 1.
+// V = [gamma_A | beta_A | gamma_C | beta_C | b_B | b_C (32) | b_D (32)] in LDS.
+template <bool HC>
+__device__ __forceinline__ void hub_tile_t(const f32x4 (&p)[4], float eps, const float4* __restrict__ WAQ,
+                                           const float4* __restrict__ WBQ, const float4* __restrict__ WCQ,
+                                           const float4* __restrict__ WDQ, const float* V, int lane, int64_t row0,
+                                           int nrows, float* __restrict__ SA, float* __restrict__ XL,
+                                           float* __restrict__ XR) {
+  const int g = lane >> 4;
+  float mean, rstd;
+  slab_stats(p, eps, mean, rstd);
+  {
+    f32x4 xl[4];
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot) xl[ot] = vec_at(V + 4 * FP, ot, g);  // b_B, then + W_B p
+    layer_t<4, 4>(WBQ, p, xl, lane);
+    slabs_store<FP>(XL, row0, nrows, xl, lane);
+  }
+  f32x4 h[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const f32x4 gm = vec_at(V, u, g), bt = vec_at(V + FP, u, g);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) h[u][j] = fmaxf(fmaf((p[u][j] - mean) * rstd, gm[j], bt[j]), 0.f);
+  }
+  {
+    f32x4 sa[2] = {zero4(), zero4()};
+    layer_t<2, 4>(WAQ, h, sa, lane);
+    slabs_store<FA>(SA, row0, nrows, sa, lane);
+  }
+  if (HC) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f32x4 gm = vec_at(V + 2 * FP, u, g), bt = vec_at(V + 3 * FP, u, g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) h[u][j] = fmaxf(fmaf((p[u][j] - mean) * rstd, gm[j], bt[j]), 0.f);
+    }
+    f32x4 tq[2] = {vec_at(V + 5 * FP, 0, g), vec_at(V + 5 * FP, 1, g)};  // b_C, then + W_C h
+    layer_t<2, 4>(WCQ, h, tq, lane);
+    f32x4 xr[2] = {vec_at(V + 5 * FP + FA, 0, g), vec_at(V + 5 * FP + FA, 1, g)};  // b_D, then + W_D t
+    layer_t<2, 2>(WDQ, tq, xr, lane);
+    slabs_store<FA>(XR, row0, nrows, xr, lane);
+  }
+}
+
+// weights and vectors of the hub in LDS (every thread of the workgroup takes part)
+template <bool HC, int NT>
+__device__ __forceinline__ void hub_stage_t(const float* __restrict__ gA, const float* __restrict__ bA,
+                                            const float* __restrict__ WA, const float* __restrict__ WB,
+                                            const float* __restrict__ bB, const float* __restrict__ gC,
+                                            const float* __restrict__ bC, const float* __restrict__ WC,
+                                            const float* __restrict__ bWC, const float* __restrict__ WD,
+                                            const float* __restrict__ bD, float4* WAQ, float4* WBQ, float4* WCQ,
+                                            float4* WDQ, float* V) {
+  stage_slabs<FA, FP, NT>(WA, reinterpret_cast<float*>(WAQ));
+  stage_slabs<FP, FP, NT>(WB, reinterpret_cast<float*>(WBQ));
+  if (HC) {
+    stage_slabs<FA, FP, NT>(WC, reinterpret_cast<float*>(WCQ));
+    stage_slabs<FA, FA, NT>(WD, reinterpret_cast<float*>(WDQ));
+  }
+  if (threadIdx.x < FP) {
+    V[threadIdx.x] = gA[threadIdx.x];
+    V[FP + threadIdx.x] = bA[threadIdx.x];
+    V[2 * FP + threadIdx.x] = HC ? gC[threadIdx.x] : 0.f;
+    V[3 * FP + threadIdx.x] = HC ? bC[threadIdx.x] : 0.f;
+    V[4 * FP + threadIdx.x] = bB[threadIdx.x];
+    if (threadIdx.x < FA) {
+      V[5 * FP + threadIdx.x] = HC ? bWC[threadIdx.x] : 0.f;
+      V[5 * FP + FA + threadIdx.x] = HC ? bD[threadIdx.x] : 0.f;
+    }
+  }
+}
+
 template <bool PREV>
 __global__ __launch_bounds__(kThreadsT, GASFM_PT_FWD_T_MINW) void point_tail_fwd_t_kernel(
     const float* __restrict__ prev, const float* __restrict__ agg, int64_t N, const float* __restrict__ Wp,
@@ -1057,7 +1162,7 @@ __global__ __launch_bounds__(kThreadsT, GASFM_PT_FWD_T_MINW) void point_tail_fwd
     const float* __restrict__ Wm, const float* __restrict__ bm, float* __restrict__ out) {
   __shared__ float4 WpQ[FP * FA / 4], WmQ[FP * FP / 4];
   __shared__ float V[4 * FP];  // b_p gamma beta b_m
-  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW, g = lane >> 4;
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int64_t ntiles = (N + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWavesT + wave, nw = int64_t(gridDim.x) * kWavesT;
   f32x4 na[2], np[4];  // next tile's rows, requested before this tile's MFMA work
@@ -1085,29 +1190,8 @@ __global__ __launch_bounds__(kThreadsT, GASFM_PT_FWD_T_MINW) void point_tail_fwd
 #pragma unroll
     for (int u = 0; u < 4; ++u) pv[u] = PREV ? np[u] : zero4();
     if (t + nw < ntiles) fetch(t + nw);
-    f32x4 x[4];
-#pragma unroll
-    for (int ot = 0; ot < 4; ++ot) x[ot] = vec_at(V, ot, g) + pv[ot];  // b_p + prev, then + W_p agg
-    layer_t<4, 2>(WpQ, ag, x, lane);
-    f32x4 gm[4], bt[4];
-#pragma unroll
-    for (int ot = 0; ot < 4; ++ot) {
-      gm[ot] = vec_at(V + FP, ot, g);
-      bt[ot] = vec_at(V + 2 * FP, ot, g);
-    }
-    float mean, rstd;
-    slab_stats(x, eps, mean, rstd);
-    f32x4 h[4];
-#pragma unroll
-    for (int ot = 0; ot < 4; ++ot)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) h[ot][j] = fmaxf(fmaf((x[ot][j] - mean) * rstd, gm[ot][j], bt[ot][j]), 0.f);
     f32x4 y[4];
-#pragma unroll
-    for (int ot = 0; ot < 4; ++ot) y[ot] = vec_at(V + 3 * FP, ot, g);  // b_m, then + W_m h
-    layer_t<4, 4>(WmQ, h, y, lane);
-#pragma unroll
-    for (int ot = 0; ot < 4; ++ot) y[ot] = x[ot] + y[ot];
+    tail_tile_t(WpQ, WmQ, V, ag, pv, eps, lane, y);
     slabs_store<FP>(out, row0, nrows, y, lane);
   }
 }
@@ -1121,7 +1205,7 @@ __global__ __launch_bounds__(kThreadsT, GASFM_PT_FWD_T_MINW) void point_hub_fwd_
     const float* __restrict__ WD, const float* __restrict__ bD, float* __restrict__ XR) {
   __shared__ float4 WAQ[FA * FP / 4], WBQ[FP * FP / 4], WCQ[HC ? FA * FP / 4 : 1], WDQ[HC ? FA * FA / 4 : 1];
   __shared__ float V[5 * FP + 2 * FA];  // gamma_A beta_A gamma_C beta_C b_B | b_C b_D
-  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW, g = lane >> 4;
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
   const int64_t ntiles = (N + TR - 1) / TR;
   const int64_t gw = int64_t(blockIdx.x) * kWavesT + wave, nw = int64_t(gridDim.x) * kWavesT;
   f32x4 nx[4];
@@ -1130,23 +1214,7 @@ __global__ __launch_bounds__(kThreadsT, GASFM_PT_FWD_T_MINW) void point_hub_fwd_
     slabs_load<FP>(X, r0, int(N - r0 < TR ? N - r0 : TR), nx, lane);
   };
   if (gw < ntiles) fetch(gw);  // the first tile's rows fly while the weights are staged
-  stage_slabs<FA, FP, kThreadsT>(WA, reinterpret_cast<float*>(WAQ));
-  stage_slabs<FP, FP, kThreadsT>(WB, reinterpret_cast<float*>(WBQ));
-  if (HC) {
-    stage_slabs<FA, FP, kThreadsT>(WC, reinterpret_cast<float*>(WCQ));
-    stage_slabs<FA, FA, kThreadsT>(WD, reinterpret_cast<float*>(WDQ));
-  }
-  if (threadIdx.x < FP) {
-    V[threadIdx.x] = gA[threadIdx.x];
-    V[FP + threadIdx.x] = bA[threadIdx.x];
-    V[2 * FP + threadIdx.x] = HC ? gC[threadIdx.x] : 0.f;
-    V[3 * FP + threadIdx.x] = HC ? bC[threadIdx.x] : 0.f;
-    V[4 * FP + threadIdx.x] = bB[threadIdx.x];
-    if (threadIdx.x < FA) {
-      V[5 * FP + threadIdx.x] = HC ? bWC[threadIdx.x] : 0.f;
-      V[5 * FP + FA + threadIdx.x] = HC ? bD[threadIdx.x] : 0.f;
-    }
-  }
+  hub_stage_t<HC, kThreadsT>(gA, bA, WA, WB, bB, gC, bC, WC, bWC, WD, bD, WAQ, WBQ, WCQ, WDQ, V);
   __syncthreads();
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row0 = t * TR;
@@ -1154,40 +1222,61 @@ __global__ __launch_bounds__(kThreadsT, GASFM_PT_FWD_T_MINW) void point_hub_fwd_
     if (GASFM_PT_FWD_T_LDSW) asm volatile("" ::: "memory");
     f32x4 p[4] = {nx[0], nx[1], nx[2], nx[3]};
     if (t + nw < ntiles) fetch(t + nw);
-    float mean, rstd;
-    slab_stats(p, eps, mean, rstd);
-    {
-      f32x4 xl[4];
+    hub_tile_t<HC>(p, eps, WAQ, WBQ, WCQ, WDQ, V, lane, row0, nrows, SA, XL, XR);
+  }
+}
+
+// The tail and the hub in ONE pass (round 6): p = tail(prev, agg) stays in registers between the two
+// bodies (the tail's T-layout output is the hub's T-layout input), is stored once as the block's
+// point features, and feeds the hub's consumers directly: no re-read of p, one launch and one weight
+// staging fewer per block.  Same tile bodies as the two kernels: bitwise the same outputs.
+template <bool PREV, bool HC, int NWV>
+__global__ __launch_bounds__(NWV * kW) void point_tail_hub_fwd_t_kernel(
+    const float* __restrict__ prev, const float* __restrict__ agg, int64_t N, const float* __restrict__ Wp,
+    const float* __restrict__ bp, const float* __restrict__ gam, const float* __restrict__ bet, float eps,
+    const float* __restrict__ Wm, const float* __restrict__ bm, float* __restrict__ out, float eps_h,
+    const float* __restrict__ gA, const float* __restrict__ bA, const float* __restrict__ WA, float* __restrict__ SA,
+    const float* __restrict__ WB, const float* __restrict__ bB, float* __restrict__ XL,
+    const float* __restrict__ gC, const float* __restrict__ bC, const float* __restrict__ WC,
+    const float* __restrict__ bWC, const float* __restrict__ WD, const float* __restrict__ bD,
+    float* __restrict__ XR) {
+  __shared__ float4 WpQ[FP * FA / 4], WmQ[FP * FP / 4];
+  __shared__ float4 WAQ[FA * FP / 4], WBQ[FP * FP / 4], WCQ[HC ? FA * FP / 4 : 1], WDQ[HC ? FA * FA / 4 : 1];
+  __shared__ float VT[4 * FP];               // b_p gamma beta b_m
+  __shared__ float VH[5 * FP + 2 * FA];      // the hub's vectors (hub_stage_t)
+  const int lane = threadIdx.x & (kW - 1), wave = threadIdx.x / kW;
+  const int64_t ntiles = (N + TR - 1) / TR;
+  const int64_t gw = int64_t(blockIdx.x) * NWV + wave, nw = int64_t(gridDim.x) * NWV;
+  f32x4 na[2], np[4];
+  auto fetch = [&](int64_t tt) {
+    const int64_t r0 = tt * TR;
+    const int nr = int(N - r0 < TR ? N - r0 : TR);
+    slabs_load<FA>(agg, r0, nr, na, lane);
+    if (PREV) slabs_load<FP>(prev, r0, nr, np, lane);
+  };
+  if (gw < ntiles) fetch(gw);
+  stage_slabs<FP, FA, NWV * kW>(Wp, reinterpret_cast<float*>(WpQ));
+  stage_slabs<FP, FP, NWV * kW>(Wm, reinterpret_cast<float*>(WmQ));
+  if (threadIdx.x < FP) {
+    VT[threadIdx.x] = bp[threadIdx.x];
+    VT[FP + threadIdx.x] = gam[threadIdx.x];
+    VT[2 * FP + threadIdx.x] = bet[threadIdx.x];
+    VT[3 * FP + threadIdx.x] = bm[threadIdx.x];
+  }
+  hub_stage_t<HC, NWV * kW>(gA, bA, WA, WB, bB, gC, bC, WC, bWC, WD, bD, WAQ, WBQ, WCQ, WDQ, VH);
+  __syncthreads();
+  for (int64_t t = gw; t < ntiles; t += nw) {
+    const int64_t row0 = t * TR;
+    const int nrows = int(N - row0 < TR ? N - row0 : TR);
+    if (GASFM_PT_FWD_T_LDSW) asm volatile("" ::: "memory");
+    f32x4 ag[2] = {na[0], na[1]}, pv[4];
 #pragma unroll
-      for (int ot = 0; ot < 4; ++ot) xl[ot] = vec_at(V + 4 * FP, ot, g);  // b_B, then + W_B p
-      layer_t<4, 4>(WBQ, p, xl, lane);
-      slabs_store<FP>(XL, row0, nrows, xl, lane);
-    }
-    f32x4 h[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const f32x4 gm = vec_at(V, u, g), bt = vec_at(V + FP, u, g);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) h[u][j] = fmaxf(fmaf((p[u][j] - mean) * rstd, gm[j], bt[j]), 0.f);
-    }
-    {
-      f32x4 sa[2] = {zero4(), zero4()};
-      layer_t<2, 4>(WAQ, h, sa, lane);
-      slabs_store<FA>(SA, row0, nrows, sa, lane);
-    }
-    if (HC) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const f32x4 gm = vec_at(V + 2 * FP, u, g), bt = vec_at(V + 3 * FP, u, g);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) h[u][j] = fmaxf(fmaf((p[u][j] - mean) * rstd, gm[j], bt[j]), 0.f);
-      }
-      f32x4 tq[2] = {vec_at(V + 5 * FP, 0, g), vec_at(V + 5 * FP, 1, g)};  // b_C, then + W_C h
-      layer_t<2, 4>(WCQ, h, tq, lane);
-      f32x4 xr[2] = {vec_at(V + 5 * FP + FA, 0, g), vec_at(V + 5 * FP + FA, 1, g)};  // b_D, then + W_D t
-      layer_t<2, 2>(WDQ, tq, xr, lane);
-      slabs_store<FA>(XR, row0, nrows, xr, lane);
-    }
+    for (int u = 0; u < 4; ++u) pv[u] = PREV ? np[u] : zero4();
+    if (t + nw < ntiles) fetch(t + nw);
+    f32x4 p[4];
+    tail_tile_t(WpQ, WmQ, VT, ag, pv, eps, lane, p);
+    slabs_store<FP>(out, row0, nrows, p, lane);
+    hub_tile_t<HC>(p, eps_h, WAQ, WBQ, WCQ, WDQ, VH, lane, row0, nrows, SA, XL, XR);
   }
 }
 
@@ -1979,6 +2068,44 @@ extern "C" int gasfm_point_hub_fwd(const float* X, int64_t N, float eps, const f
     hipLaunchKernelGGL(point_hub_fwd_kernel<false>, dim3(grid4(&point_hub_fwd_kernel<false>, N)), dim3(kThreads), 0,
                        st, X, N, eps, gA, bA, WA, SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR);
   return launch_status("gasfm_point_hub_fwd");
+}
+
+extern "C" int gasfm_point_tail_hub_fwd(const float* prev, const float* agg, int64_t N, const float* Wp,
+                                        const float* bp, const float* ln_w, const float* ln_b, float eps,
+                                        const float* Wm, const float* bm, float* out, float eps_h, const float* gA,
+                                        const float* bA, const float* WA, float* SA, const float* WB,
+                                        const float* bB, float* XL, const float* gC, const float* bC,
+                                        const float* WC, const float* bWC, const float* WD, const float* bD,
+                                        float* XR, void* stream) {
+  GASFM_REQUIRE(N >= 0, "gasfm_point_tail_hub_fwd: N < 0");
+  const bool hc = gC != nullptr;
+  if (N == 0) return GASFM_OK;
+  GASFM_REQUIRE(agg && Wp && bp && ln_w && ln_b && Wm && bm && out && gA && bA && WA && SA && WB && bB && XL,
+                "gasfm_point_tail_hub_fwd: null pointer");
+  GASFM_REQUIRE(!hc || (bC && WC && bWC && WD && bD && XR), "gasfm_point_tail_hub_fwd: null pointer (C part)");
+  GASFM_REQUIRE(aligned16(agg) && (!prev || aligned16(prev)) && aligned16(out) && aligned16(SA) && aligned16(XL) &&
+                    (!hc || aligned16(XR)),
+                "gasfm_point_tail_hub_fwd: alignment");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // 4-wave workgroups (two per CU by the 64 KB of staged weights: 2 waves per SIMD); 6-wave ones
+  // (3 per SIMD at 156 VGPRs) measured 31.5 vs 18.3 us per rank-of-8 launch, 94.9 vs 72.5 at config 4
+  // (profiles/r6_ab_tail_hub.txt)
+#define GASFM_LAUNCH(PV, HCV)                                                                                  \
+  hipLaunchKernelGGL((point_tail_hub_fwd_t_kernel<PV, HCV, 4>),                                                \
+                     dim3(resident_grid(reinterpret_cast<const void*>(&point_tail_hub_fwd_t_kernel<PV, HCV, 4>), \
+                                        4 * kW, 0, tiles_of(N), 4)),                                           \
+                     dim3(4 * kW), 0, st, prev, agg, N, Wp, bp, ln_w, ln_b, eps, Wm, bm, out, eps_h, gA, bA, WA, \
+                     SA, WB, bB, XL, gC, bC, WC, bWC, WD, bD, XR)
+  if (prev && hc)
+    GASFM_LAUNCH(true, true);
+  else if (prev)
+    GASFM_LAUNCH(true, false);
+  else if (hc)
+    GASFM_LAUNCH(false, true);
+  else
+    GASFM_LAUNCH(false, false);
+#undef GASFM_LAUNCH
+  return launch_status("gasfm_point_tail_hub_fwd");
 }
 
 extern "C" int gasfm_point_hub_bwd_c(const float* X, int64_t N, float eps, const float* gC, const float* bC,

@@ -527,10 +527,15 @@ class GraphAttnSfMGlobalFeatureUpdate(Module):
                 carry.update(view_skip=skip, XLv2g=XLv)
             elif cams:
                 raise RuntimeError("camera-sharded execution needs the fused view hub shapes")
-        pts = sp.tail(agg_p, prev_pt)
-        if hp is not None and point_block._rows_ok(pts, point_block.P_W):
-            skip, SA, XLs, XRn = point_block.hub(pts, hp)
+        if hp is not None and point_block.FUSED_TAIL_HUB and point_block.tail_fusable(sp, agg_p, prev_pt):
+            # the point tail and hub as one forward launch (round 6, PointTailHubFn)
+            pts, skip, SA, XLs, XRn = point_block.tail_hub(sp, agg_p, prev_pt, hp)
             carry.update(XRp=XRn, pts_skip=skip, SA=SA, XLs2g=XLs)
+        else:
+            pts = sp.tail(agg_p, prev_pt)
+            if hp is not None and point_block._rows_ok(pts, point_block.P_W):
+                skip, SA, XLs, XRn = point_block.hub(pts, hp)
+                carry.update(XRp=XRn, pts_skip=skip, SA=SA, XLs2g=XLs)
         return self._finish(pts, view, plans, prev_glob, carry, pfu, nxt)
 
     def _exchange_ok(self, vsg):

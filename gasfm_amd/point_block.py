@@ -14,6 +14,8 @@ block).  Routing every consumer through PointHubFn makes its backward the only p
 dp: the C pass adds the next block's target-row gradient to the incoming skip gradient, the
 A+B pass adds lin_l and lin_scenepoint terms in place, and no add kernel runs.
 """
+import os
+
 import torch
 
 from . import _native
@@ -42,25 +44,30 @@ class PointTailFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        prev, agg, Wp, bp, ln_w, ln_b, Wm = ctx.saved_tensors
-        N = agg.shape[0]
-        dout = dout.contiguous()
-        rows, cols = _native.point_tail_part_shape(N, prev is not None)
-        dx = _f32(N, P_W, like=agg)
-        dagg = _f32(N, A_W, like=agg)
-        if rows == 0:
-            tot = torch.zeros(cols, dtype=torch.float32, device=agg.device)
-        else:
-            part = _f32(rows, cols, like=agg)
-            _native.point_tail_bwd(dout, prev, agg, Wp, bp, ln_w, ln_b, ctx.eps, Wm, dx, dagg, part)
-            tot = _native.param_colsum(part, ctx.defer)
-        o = 0
-        dWm = tot[o:o + P_W * P_W].view(P_W, P_W)
-        o += P_W * P_W
-        dWp = tot[o:o + P_W * A_W].view(P_W, A_W)
-        o += P_W * A_W
-        dbm, dbp, dg, dbt = (tot[o + k * P_W:o + (k + 1) * P_W] for k in range(4))
-        return (dx if prev is not None else None), dagg, dWp, dbp, dg, dbt, dWm, dbm, None
+        return _tail_backward(ctx.saved_tensors, ctx.eps, ctx.defer, dout) + (None,)
+
+
+def _tail_backward(saved, eps, defer, dout):
+    """PointTailFn's backward: (d prev, d agg, dWp, dbp, dgamma, dbeta, dWm, dbm)."""
+    prev, agg, Wp, bp, ln_w, ln_b, Wm = saved
+    N = agg.shape[0]
+    dout = dout.contiguous()
+    rows, cols = _native.point_tail_part_shape(N, prev is not None)
+    dx = _f32(N, P_W, like=agg)
+    dagg = _f32(N, A_W, like=agg)
+    if rows == 0:
+        tot = torch.zeros(cols, dtype=torch.float32, device=agg.device)
+    else:
+        part = _f32(rows, cols, like=agg)
+        _native.point_tail_bwd(dout, prev, agg, Wp, bp, ln_w, ln_b, eps, Wm, dx, dagg, part)
+        tot = _native.param_colsum(part, defer)
+    o = 0
+    dWm = tot[o:o + P_W * P_W].view(P_W, P_W)
+    o += P_W * P_W
+    dWp = tot[o:o + P_W * A_W].view(P_W, A_W)
+    o += P_W * A_W
+    dbm, dbp, dg, dbt = (tot[o + k * P_W:o + (k + 1) * P_W] for k in range(4))
+    return (dx if prev is not None else None), dagg, dWp, dbp, dg, dbt, dWm, dbm
 
 
 class PointHubFn(torch.autograd.Function):
@@ -81,39 +88,76 @@ class PointHubFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dskip, dSA, dXL, dXR):
-        p, gA, bA, WA, WB, gC, bC, WC, bWC, WD = ctx.saved_tensors
-        N = p.shape[0]
-        zeros = lambda w: torch.zeros((N, w), dtype=torch.float32, device=p.device)  # noqa: E731
-        dSA = dSA.contiguous() if dSA is not None else zeros(A_W)
-        dXL = dXL.contiguous() if dXL is not None else zeros(P_W)
-        dXR = dXR.contiguous() if dXR is not None else zeros(A_W)
-        dskip = dskip.contiguous() if dskip is not None else None
-        rc, cc = _native.point_hub_part_shape(N, 1, dskip is not None)
-        ra, ca = _native.point_hub_part_shape(N, 0, True)
-        dp = _f32(N, P_W, like=p)
-        if N == 0:
-            tc = torch.zeros(cc, dtype=torch.float32, device=p.device)
-            ta = torch.zeros(ca, dtype=torch.float32, device=p.device)
-        else:
-            part_c, part_a = _f32(rc, cc, like=p), _f32(ra, ca, like=p)
-            _native.point_hub_bwd(p, ctx.eps, gA, bA, WA, WB, gC, bC, WC, bWC, WD, dSA, dXL, dXR, dskip, dp,
-                                  part_a, part_c)
-            tc, ta = _native.param_colsum(part_c, ctx.defer), _native.param_colsum(part_a, ctx.defer)
-        o = 0
-        dWC = tc[o:o + A_W * P_W].view(A_W, P_W)
-        o += A_W * P_W
-        dWD = tc[o:o + A_W * A_W].view(A_W, A_W)
-        o += A_W * A_W
-        dbWC, dbD = tc[o:o + A_W], tc[o + A_W:o + 2 * A_W]
-        o += 2 * A_W
-        dgC, dbC = tc[o:o + P_W], tc[o + P_W:o + 2 * P_W]
-        o = 0
-        dWA = ta[o:o + A_W * P_W].view(A_W, P_W)
-        o += A_W * P_W
-        dWB = ta[o:o + P_W * P_W].view(P_W, P_W)
-        o += P_W * P_W
-        dbB, dgA, dbA = (ta[o + k * P_W:o + (k + 1) * P_W] for k in range(3))
-        return dp, dgA, dbA, dWA, dWB, dbB, dgC, dbC, dWC, dbWC, dWD, dbD, None
+        return _hub_backward(ctx.saved_tensors, ctx.eps, ctx.defer, dskip, dSA, dXL, dXR) + (None,)
+
+
+def _hub_backward(saved, eps, defer, dskip, dSA, dXL, dXR):
+    """PointHubFn's backward: (dp, dgA, dbA, dWA, dWB, dbB, dgC, dbC, dWC, dbWC, dWD, dbD); dp includes dskip."""
+    p, gA, bA, WA, WB, gC, bC, WC, bWC, WD = saved
+    N = p.shape[0]
+    zeros = lambda w: torch.zeros((N, w), dtype=torch.float32, device=p.device)  # noqa: E731
+    dSA = dSA.contiguous() if dSA is not None else zeros(A_W)
+    dXL = dXL.contiguous() if dXL is not None else zeros(P_W)
+    dXR = dXR.contiguous() if dXR is not None else zeros(A_W)
+    dskip = dskip.contiguous() if dskip is not None else None
+    rc, cc = _native.point_hub_part_shape(N, 1, dskip is not None)
+    ra, ca = _native.point_hub_part_shape(N, 0, True)
+    dp = _f32(N, P_W, like=p)
+    if N == 0:
+        tc = torch.zeros(cc, dtype=torch.float32, device=p.device)
+        ta = torch.zeros(ca, dtype=torch.float32, device=p.device)
+    else:
+        part_c, part_a = _f32(rc, cc, like=p), _f32(ra, ca, like=p)
+        _native.point_hub_bwd(p, eps, gA, bA, WA, WB, gC, bC, WC, bWC, WD, dSA, dXL, dXR, dskip, dp,
+                              part_a, part_c)
+        tc, ta = _native.param_colsum(part_c, defer), _native.param_colsum(part_a, defer)
+    o = 0
+    dWC = tc[o:o + A_W * P_W].view(A_W, P_W)
+    o += A_W * P_W
+    dWD = tc[o:o + A_W * A_W].view(A_W, A_W)
+    o += A_W * A_W
+    dbWC, dbD = tc[o:o + A_W], tc[o + A_W:o + 2 * A_W]
+    o += 2 * A_W
+    dgC, dbC = tc[o:o + P_W], tc[o + P_W:o + 2 * P_W]
+    o = 0
+    dWA = ta[o:o + A_W * P_W].view(A_W, P_W)
+    o += A_W * P_W
+    dWB = ta[o:o + P_W * P_W].view(P_W, P_W)
+    o += P_W * P_W
+    dbB, dgA, dbA = (ta[o + k * P_W:o + (k + 1) * P_W] for k in range(3))
+    return dp, dgA, dbA, dWA, dWB, dbB, dgC, dbC, dWC, dbWC, dWD, dbD
+
+
+class PointTailHubFn(torch.autograd.Function):
+    """PointTailFn then PointHubFn on its output as ONE forward kernel (gasfm_point_tail_hub_fwd,
+    round 6): p never re-read, one launch fewer per block.  Outputs (p, SA, XL, XR): p is the block's
+    point features AND the next block's state skip (the hub's identity output), so its gradient --
+    whatever consumes it -- enters the hub's backward as dRes.  The backward is the two Functions'
+    own kernels in autograd's order (hub, then tail on the hub's dp)."""
+
+    @staticmethod
+    def forward(ctx, prev, agg, Wp, bp, ln_w, ln_b, Wm, bm, eps, gA, bA, WA, WB, bB, gC, bC, WC, bWC, WD, bD, eps_h):
+        agg = agg.contiguous()
+        prev = prev.contiguous() if prev is not None else None
+        Wp, Wm, WA, WB, WC, WD = (w.contiguous() for w in (Wp, Wm, WA, WB, WC, WD))
+        N = agg.shape[0]
+        p = _f32(N, P_W, like=agg)
+        SA, XL, XR = _f32(N, A_W, like=agg), _f32(N, P_W, like=agg), _f32(N, A_W, like=agg)
+        _native.point_tail_hub_fwd(prev, agg, Wp, bp, ln_w, ln_b, eps, Wm, bm, p, eps_h, gA, bA, WA, SA, WB, bB, XL,
+                                   gC, bC, WC, bWC, WD, bD, XR)
+        ctx.save_for_backward(prev, agg, Wp, bp, ln_w, ln_b, Wm, p, gA, bA, WA, WB, gC, bC, WC, bWC, WD)
+        ctx.eps, ctx.eps_h = eps, eps_h
+        ctx.defer_t = _native.defer_token(Wp, bp, ln_w, ln_b, Wm, bm)
+        ctx.defer_h = _native.defer_token(gA, bA, WA, WB, bB, gC, bC, WC, bWC, WD, bD)
+        ctx.set_materialize_grads(False)
+        return p, SA, XL, XR
+
+    @staticmethod
+    def backward(ctx, dp, dSA, dXL, dXR):
+        saved = ctx.saved_tensors
+        gh = _hub_backward(saved[7:], ctx.eps_h, ctx.defer_h, dp, dSA, dXL, dXR)
+        gt = _tail_backward(saved[:7], ctx.eps, ctx.defer_t, gh[0])
+        return gt[:8] + (None,) + gh[1:] + (None,)
 
 
 def _is_ln(m, w):
@@ -168,6 +212,21 @@ def hub_params(pfu, s2g_conv, nxt):
 
 def hub(p, params):
     return PointHubFn.apply(p, *params)
+
+
+# round 6: the tail and the hub as one forward launch (PointTailHubFn); GASFM_TAIL_HUB=0 runs the two
+# Functions (A/B knob)
+FUSED_TAIL_HUB = os.environ.get("GASFM_TAIL_HUB", "1") != "0"
+
+
+def tail_hub(agg_mod, x, prev, params):
+    """(p, skip, SA, XL, XR) of tail() then hub() -- one forward kernel; skip IS p (see PointTailHubFn)."""
+    proj = getattr(agg_mod, agg_mod._proj_key)
+    ln, lin = agg_mod.norm_pre_mlp, agg_mod.mlp[0]
+    gA, bA, WA, WB, bB, gC, bC, WC, bWC, WD, bD, eps_h = params
+    p, SA, XL, XR = PointTailHubFn.apply(prev, x, proj.weight, proj.bias, ln.weight, ln.bias, lin.weight, lin.bias,
+                                         ln.eps, gA, bA, WA, WB, bB, gC, bC, WC, bWC, WD, bD, eps_h)
+    return p, p, SA, XL, XR
 
 
 class PointHeadFn(torch.autograd.Function):

@@ -484,6 +484,17 @@ int gasfm_point_hub_fwd(const float* X, int64_t N, float eps, const float* gA, c
                         const float* WC, const float* bWC, const float* WD, const float* bD, float* XR,
                         void* stream);
 
+/* gasfm_point_tail_fwd then gasfm_point_hub_fwd on its output in ONE launch (round 6): out = p, and
+ * SA / XL / (gC non-null) XR of p, bitwise as the two calls; eps_h: the hub's LayerNorm epsilon.
+ * Replaces the pair the reference runs as Proj2ScenePoint's tail (code/models/layers.py:438-454) and
+ * the consumers of its output (:429, :560-575, :924-935). */
+int gasfm_point_tail_hub_fwd(const float* prev, const float* agg, int64_t N, const float* Wp, const float* bp,
+                             const float* ln_w, const float* ln_b, float eps, const float* Wm, const float* bm,
+                             float* out, float eps_h, const float* gA, const float* bA, const float* WA, float* SA,
+                             const float* WB, const float* bB, float* XL, const float* gC, const float* bC,
+                             const float* WC, const float* bWC, const float* WD, const float* bD, float* XR,
+                             void* stream);
+
 /* dX = dRes + LN_C_bwd(mask (dXR WD WC)) (dRes may be null), partials. */
 int gasfm_point_hub_bwd_c(const float* X, int64_t N, float eps, const float* gC, const float* bC, const float* WC,
                           const float* bWC, const float* WD, const float* dXR, const float* dRes, float* dX,

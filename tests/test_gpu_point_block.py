@@ -100,3 +100,47 @@ def test_point_hub_deterministic(device):
         res.append([t.grad.clone() for t in ins])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("N", [1, 17, 1000, 70_001])
+@pytest.mark.parametrize("with_prev", [True, False])
+def test_point_tail_hub_fused_bitwise(device, N, with_prev):
+    """PointTailHubFn (one forward kernel, round 6) against PointTailFn then PointHubFn: the same tile
+    bodies, so p / SA / XL / XR are bitwise equal, and the gradients -- the same backward kernels in the
+    same order, the skip gradient entering the hub as dRes -- bitwise too; plus the fp64 composition."""
+    g = torch.Generator().manual_seed(7 * N + with_prev)
+    tail_in = [_rnd(g, N, 64, scale=2, shift=0.3) if with_prev else None, _rnd(g, N, 32),
+               _rnd(g, 64, 32, scale=0.2), _rnd(g, 64, scale=0.1), _rnd(g, 64, scale=0.3, shift=1),
+               _rnd(g, 64, scale=0.2), _rnd(g, 64, 64, scale=0.125), _rnd(g, 64, scale=0.1)]
+    hub_in = [_rnd(g, 64, scale=0.3, shift=1), _rnd(g, 64, scale=0.2), _rnd(g, 32, 64, scale=0.125),
+              _rnd(g, 64, 64, scale=0.125), _rnd(g, 64, scale=0.1), _rnd(g, 64, scale=0.3, shift=1),
+              _rnd(g, 64, scale=0.2), _rnd(g, 32, 64, scale=0.125), _rnd(g, 32, scale=0.1),
+              _rnd(g, 32, 32, scale=0.18), _rnd(g, 32, scale=0.1)]
+    dp, dSA, dXL, dXR = _rnd(g, N, 64), _rnd(g, N, 32), _rnd(g, N, 64), _rnd(g, N, 32)
+    dev = lambda ts: [t.float().to(device).requires_grad_(True) if t is not None else None for t in ts]  # noqa: E731
+    # the two Functions
+    t2, h2 = dev(tail_in), dev(hub_in)
+    p2 = point_block.PointTailFn.apply(*t2, EPS)
+    outs2 = point_block.PointHubFn.apply(p2, *h2, EPS)
+    torch.autograd.backward(outs2, [d.float().to(device) for d in (dp, dSA, dXL, dXR)])
+    # one kernel
+    t1, h1 = dev(tail_in), dev(hub_in)
+    outs1 = point_block.PointTailHubFn.apply(*t1, EPS, *h1, EPS)
+    for name, a, b in zip(("p", "SA", "XL", "XR"), outs1, outs2):
+        assert torch.equal(a, b), name
+    torch.autograd.backward(outs1, [d.float().to(device) for d in (dp, dSA, dXL, dXR)])
+    for name, a, b in zip(("prev", "agg", "Wp", "bp", "gamma", "beta", "Wm", "bm", "gA", "bA", "WA", "WB", "bB",
+                           "gC", "bC", "WC", "bWC", "WD", "bD"), t1 + h1, t2 + h2):
+        if a is None:
+            continue
+        assert torch.equal(a.grad, b.grad), name
+    # and against the fp64 composition
+    r_t = [t.clone().requires_grad_(True) if t is not None else None for t in tail_in]
+    r_h = [t.clone().requires_grad_(True) for t in hub_in]
+    outs64 = _hub_ref(_tail_ref(*r_t), *r_h)
+    for name, o, r in zip(("p", "SA", "XL", "XR"), outs1, outs64):
+        torch.testing.assert_close(o.double().cpu(), r.detach(), rtol=0, atol=5e-5 * r.abs().max().item() + 1e-5,
+                                   msg=name)
+    torch.autograd.backward(list(outs64), [dp, dSA, dXL, dXR])
+    _close_grads(("prev", "agg", "Wp", "bp", "gamma", "beta", "Wm", "bm", "gA", "bA", "WA", "WB", "bB", "gC", "bC",
+                  "WC", "bWC", "WD", "bD"), t1 + h1, r_t + r_h)
