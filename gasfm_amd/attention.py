@@ -20,7 +20,7 @@ import torch
 
 from . import _native
 
-DEFAULT_MAX_PIECE = 256  # edges per work item
+DEFAULT_MAX_PIECE = int(os.environ.get("GASFM_DEFAULT_PIECE", "256"))  # edges per work item (env: A/B knob)
 _MAX_PIECE_ENV = os.environ.get("GASFM_MAX_PIECE")  # A/B knob: a fixed camera-direction piece length
 
 
