@@ -1,6 +1,6 @@
 # Round 6: the point tail + hub forward as one kernel (GASFM_TAIL_HUB) -- parity tests, then config 4 and the
-# (its kernel-trace step looked for a stats csv the default output format does not write; tools/gpu_tail_hub_prof.sh took the per-kernel times)
 # rank-0-of-8 proxy alternating with / without, then kernel traces of both
+# (its kernel-trace step looked for a stats csv the default output format does not write; tools/gpu_tail_hub_prof.sh took the per-kernel times)
 mkdir -p gpurun_out
 timeout -k 10 500 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_point_block.py tests/test_gpu_model.py tests/test_gpu_train_step.py > gpurun_out/th_tests.log 2>&1 || { tail -30 gpurun_out/th_tests.log; exit 1; }
 tail -1 gpurun_out/th_tests.log

@@ -1,6 +1,6 @@
 # Round 6: the fused point tail + hub forward at 4- vs 6-wave workgroups (GASFM_TAIL_HUB_WAVES): parity,
-# (the GASFM_TAIL_HUB_WAVES knob was removed after this A/B: 4-wave workgroups kept, profiles/r6_ab_tail_hub.txt)
 # per-kernel times (proxy, config 4), proxy steps alternating
+# (the GASFM_TAIL_HUB_WAVES knob was removed after this A/B: 4-wave workgroups kept, profiles/r6_ab_tail_hub.txt)
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_point_block.py -k fused > gpurun_out/thw_tests.log 2>&1 || { tail -30 gpurun_out/thw_tests.log; exit 1; }
 tail -1 gpurun_out/thw_tests.log
