@@ -199,3 +199,40 @@ def test_several_forwards_one_backward(device):
             assert torch.isfinite(g[k]).all(), k
             torch.testing.assert_close(g[k], ref[k], rtol=1e-4, atol=1e-5, msg=f"{k} batched={batched} defer={defer}")
     net.batch_weight_grads = True
+
+
+def test_fused_point_tail_hub_bitwise_in_model(device, monkeypatch):
+    """The model with the point tail + hub forward as one kernel (point_block.FUSED_TAIL_HUB, round 6)
+    against the two-kernel path: bitwise the same outputs, loss and every parameter gradient (the fused
+    kernel runs the same tile bodies, and the backward the same kernels in the same order), with the
+    fused Function recorded as taken in every block that has a next block."""
+    from gasfm_amd import point_block, synthetic
+    sc = synthetic.scaled_config4(0.02, seed=5)
+    data = gasfm_amd.SceneData.from_synthetic(sc).to(device)
+    torch.manual_seed(0)
+    net = gasfm_amd.GraphAttnSfMNet(gasfm_amd.learning_conf(num_layers=4)).to(device)
+    gen = torch.Generator().manual_seed(4)
+    cP = torch.randn((sc.m, 3, 4), generator=gen).to(device)
+    cX = torch.randn((4, sc.n), generator=gen).to(device)
+    calls = []
+    orig = point_block.PointTailHubFn.apply
+    monkeypatch.setattr(point_block.PointTailHubFn, "apply", lambda *a: calls.append(1) or orig(*a))
+
+    def run(fused):
+        monkeypatch.setattr(point_block, "FUSED_TAIL_HUB", fused)
+        for p in net.parameters():
+            p.grad = None
+        pred = net(data)
+        loss = (pred["Ps_norm"] * cP).sum() + (pred["pts3D"] * cX).sum()
+        loss.backward()
+        torch.cuda.synchronize()
+        return pred, float(loss), {k: p.grad.detach().clone() for k, p in net.named_parameters()}
+
+    p2, l2, g2 = run(False)
+    assert not calls
+    p1, l1, g1 = run(True)
+    assert len(calls) == 3, calls  # blocks 1..3 each have a next consumer; block 0 / the final update do not
+    assert torch.equal(p1["Ps_norm"], p2["Ps_norm"]) and torch.equal(p1["pts3D"], p2["pts3D"])
+    assert l1 == l2
+    bad = [k for k in g1 if not torch.equal(g1[k], g2[k])]
+    assert not bad, f"{len(bad)} of {len(g1)} gradients differ: {bad[:12]}"
